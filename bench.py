@@ -1,0 +1,153 @@
+#!/usr/bin/env python
+"""Headline benchmark: fit time & speedup vs Spark-ML CPU on the reference's workload suite.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 launched with
+``torch.distributed.run --nproc-per-node N`` (one rank per MI355X, RCCL over xGMI).
+
+What is measured (BASELINE.json metric "fit time (s) & speedup vs Spark-ML CPU at fixed
+rows x features"): the reference's 8 headline workloads — KMeans (k=1000, 30 iters, random
+init), PCA (k=3), LinearRegression OLS / ElasticNet / Ridge, LogisticRegression (L2, 200
+iters), RandomForestClassifier (50 trees, depth 13, 128 bins), RandomForestRegressor (30 trees,
+depth 6) — on 1,000,000 x 3000 float32 synthetic data of the same families, split row-wise
+over N ranks (strong scaling: total rows fixed). A "step" = one full fit of every workload
+through the public estimator API, starting from host-resident (pinned) Arrow-backed
+DataFrames, so the timed region includes host->device ingest, every kernel, every RCCL
+collective and model construction. ``value`` = geometric-mean speedup of our fit time over
+the Spark-ML CPU fit time; ``vs_baseline`` = value / the reference GPU's own
+geometric-mean speedup on the same table (20.1x).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+import traceback
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--rows", type=int, default=1_000_000)
+    ap.add_argument("--cols", type=int, default=3000)
+    ap.add_argument("--algos", type=str, default="all")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    use_gpu = torch.cuda.is_available()
+    device = torch.device("cuda", local_rank) if use_gpu else torch.device("cpu")
+    if use_gpu:
+        torch.cuda.set_device(device)
+    if world > 1:
+        from datetime import timedelta
+
+        dist.init_process_group("nccl" if use_gpu else "gloo", timeout=timedelta(minutes=30),
+                                **({"device_id": device} if use_gpu else {}))
+
+    from spark_rapids_ml_nai_amd import DataFrame
+    from spark_rapids_ml_nai_amd.bench.suite import REF_GEOMEAN_SPEEDUP, REF_GPU_S, SPARK_CPU_S, geomean, make_shard, registry
+    from spark_rapids_ml_nai_amd.ops import native
+
+    if use_gpu:
+        native.lib()  # fail loudly if the HIP kernels are not available
+
+    def barrier_sync() -> None:
+        if use_gpu:
+            torch.cuda.synchronize(device)
+        if world > 1:
+            dist.barrier()
+        if use_gpu:
+            torch.cuda.synchronize(device)
+
+    reg = registry()
+    names = list(SPARK_CPU_S.keys()) if args.algos == "all" else args.algos.split(",")
+    m_total = args.rows
+    bounds = np.linspace(0, m_total, world + 1).astype(np.int64)
+    m_local = int(bounds[rank + 1] - bounds[rank])
+
+    results = {}
+    errors = {}
+    for name in names:
+        wl = reg.get(name)
+        if wl is None:
+            errors[name] = "not implemented"
+            continue
+        try:
+            Xh, yh = make_shard(wl.data, m_local, args.cols, device, rank, m_total)
+            df = DataFrame.from_numpy(Xh, yh if wl.label else None)
+            est = wl.make_estimator()
+            est.num_workers = world
+            for _ in range(args.warmup):
+                est.fit(df)
+            barrier_sync()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                model = est.fit(df)
+            barrier_sync()
+            dt = time.perf_counter() - t0
+            if world > 1:
+                t = torch.tensor([dt], dtype=torch.float64, device=device)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                dt = float(t.item())
+            per_fit = dt / args.steps
+            results[name] = {
+                "fit_s": round(per_fit, 4),
+                "speedup_vs_spark_cpu": round(SPARK_CPU_S[name] / per_fit, 1),
+                "ref_gpu_fit_s": REF_GPU_S[name],
+                "vs_ref_gpu": round(REF_GPU_S[name] / per_fit, 1),
+                "phases": {k: round(v, 4) for k, v in getattr(model, "_fit_timings", {}).items()},
+            }
+            del df, Xh, yh, model
+        except Exception as e:  # noqa: BLE001
+            errors[name] = repr(e)[:400]
+            if rank == 0:
+                traceback.print_exc(file=sys.stderr)
+        if use_gpu:
+            torch.cuda.empty_cache()
+
+    speedups = [SPARK_CPU_S[k] / r["fit_s"] for k, r in results.items()]
+    value = geomean(speedups) if speedups else 0.0
+    step_s = sum(r["fit_s"] for r in results.values())
+    line = {
+        "metric": "fit-time speedup vs Spark-ML CPU (geomean over reference headline workloads, 1Mx3000 fp32)",
+        "value": round(value, 2),
+        "unit": "x",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(step_s * 1000.0, 2),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": round(value / REF_GEOMEAN_SPEEDUP, 3) if speedups else None,
+        "dtype": "fp32",
+        "data": "synthetic (device-generated, pinned host Arrow-backed DataFrames; H2D ingest inside timed fit)",
+        "config": {
+            "model": "spark-rapids-ml headline suite: " + ",".join(results.keys()),
+            "global_batch": m_total,
+            "seq_len": args.cols,
+            "rows": m_total,
+            "features": args.cols,
+            "parallelism": "dp%d" % world,
+            "workloads": results,
+            "missing_or_failed": errors,
+            "ref_geomean_speedup": round(REF_GEOMEAN_SPEEDUP, 2),
+        },
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,96 @@
+"""Synthetic benchmark data generated directly on the device (one shard per rank).
+
+Same distribution families as the reference generators (``python/benchmark/gen_data.py``,
+``gen_data_distributed.py`` — SURVEY Appendix D): ``low_rank_matrix`` (bell + tail singular
+profile, effective_rank 10, tail_strength 0.5), ``regression`` (N(0,1) features, sparse
+informative ground truth ~100·U(0,1), Gaussian noise), ``classification`` (hypercube-vertex
+class clusters over informative features + linear redundant features + noise), ``uniform``
+(``RandomRDDs.uniformVectorRDD``) and ``blobs``. Generating on the GPU keeps 1M x 3000 shards
+to a second instead of minutes of host RNG; the result is copied once into pinned host memory
+(``to_pinned_numpy``) so that the timed fit starts from host-resident "Arrow" data like a
+Spark executor's batches.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+
+
+def _gen(device: torch.device, seed: int) -> torch.Generator:
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    return g
+
+
+def low_rank_matrix(m: int, n: int, device: torch.device, seed: int = 0, effective_rank: int = 10,
+                    tail_strength: float = 0.5, rank_cap: int = 256, m_total: Optional[int] = None) -> torch.Tensor:
+    g = _gen(device, seed)
+    r = min(n, rank_cap)
+    i = torch.arange(r, device=device, dtype=torch.float32)
+    low = (1 - tail_strength) * torch.exp(-1.0 * (i / effective_rank) ** 2)
+    tail = tail_strength * torch.exp(-0.1 * i / effective_rank)
+    s = low + tail
+    # V: orthonormal rows shared by every rank (seeded identically)
+    gv = _gen(device, 12345)
+    V, _ = torch.linalg.qr(torch.randn(n, r, device=device, generator=gv, dtype=torch.float32))
+    U = torch.randn(m, r, device=device, generator=g, dtype=torch.float32) / float(np.sqrt(m_total or m))
+    return (U * s) @ V.T
+
+
+def regression(m: int, n: int, device: torch.device, seed: int = 0, n_informative: Optional[int] = None,
+               noise: float = 1.0, bias: float = 0.0) -> Tuple[torch.Tensor, torch.Tensor]:
+    g = _gen(device, seed)
+    X = torch.randn(m, n, device=device, generator=g, dtype=torch.float32)
+    gw = _gen(device, 777)
+    k = n_informative or max(1, n // 10)
+    w = torch.zeros(n, device=device)
+    idx = torch.randperm(n, device=device, generator=gw)[:k]
+    w[idx] = 100.0 * torch.rand(k, device=device, generator=gw)
+    y = X @ w + bias + noise * torch.randn(m, device=device, generator=g)
+    return X, y
+
+
+def classification(m: int, n: int, device: torch.device, seed: int = 0, n_classes: int = 2,
+                   n_informative: Optional[int] = None, n_redundant: Optional[int] = None,
+                   class_sep: float = 1.0, flip_y: float = 0.01) -> Tuple[torch.Tensor, torch.Tensor]:
+    g = _gen(device, seed)
+    ni = n_informative if n_informative is not None else max(1, n // 3)
+    nr = n_redundant if n_redundant is not None else max(0, n // 3)
+    ni = min(ni, n)
+    nr = min(nr, n - ni)
+    y = torch.randint(0, n_classes, (m,), device=device, generator=g)
+    gc = _gen(device, 999)
+    centroids = (torch.randint(0, 2, (n_classes, ni), device=device, generator=gc).float() * 2 - 1) * class_sep
+    X = torch.empty(m, n, device=device, dtype=torch.float32)
+    X[:, :ni] = torch.randn(m, ni, device=device, generator=g) + centroids[y]
+    if nr > 0:
+        B = 2 * torch.rand(ni, nr, device=device, generator=gc) - 1
+        X[:, ni: ni + nr] = (X[:, :ni] @ B) / float(np.sqrt(ni))
+    if ni + nr < n:
+        X[:, ni + nr:] = torch.randn(m, n - ni - nr, device=device, generator=g)
+    flip = torch.rand(m, device=device, generator=g) < flip_y
+    y = torch.where(flip, torch.randint(0, n_classes, (m,), device=device, generator=g), y)
+    return X, y.float()
+
+
+def uniform(m: int, n: int, device: torch.device, seed: int = 0) -> torch.Tensor:
+    return torch.rand(m, n, device=device, generator=_gen(device, seed), dtype=torch.float32)
+
+
+def blobs(m: int, n: int, device: torch.device, seed: int = 0, centers: int = 20,
+          cluster_std: float = 1.0) -> Tuple[torch.Tensor, torch.Tensor]:
+    g = _gen(device, seed)
+    gc = _gen(device, 4242)
+    C = (torch.rand(centers, n, device=device, generator=gc) * 20 - 10)
+    lab = torch.randint(0, centers, (m,), device=device, generator=g)
+    X = C[lab] + cluster_std * torch.randn(m, n, device=device, generator=g)
+    return X, lab.float()
+
+
+def to_pinned_numpy(t: torch.Tensor) -> np.ndarray:
+    """Device tensor -> numpy array backed by pinned host memory (fast H2D path in ingest)."""
+    h = torch.empty(t.shape, dtype=t.dtype, pin_memory=torch.cuda.is_available())
+    h.copy_(t)
+    return h.numpy()

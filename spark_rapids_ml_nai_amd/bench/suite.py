@@ -1,0 +1,141 @@
+"""The reference's headline benchmark suite, re-run on MI355X.
+
+Reference: Databricks, 1M rows x 3000 float32 features, Spark-ML CPU (2x m5.2xlarge) vs
+Spark-RAPIDS-ML (2x A10G); fit times in seconds (``python/benchmark/databricks/run_benchmark.sh:45-133``,
+``results/running_times.png``). Each workload here uses the same algorithm
+parameters, the same row x feature shape and the same data family, generated on the device.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Any, Callable, Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import datagen
+
+# fit seconds from BASELINE.md (Spark ML CPU, spark-rapids-ml GPU)
+SPARK_CPU_S = {
+    "kmeans": 9526.0,
+    "pca": 661.0,
+    "linear_regression": 594.0,
+    "linear_regression_elasticnet": 551.0,
+    "linear_regression_ridge": 558.0,
+    "logistic_regression": 406.0,
+    "random_forest_classifier": 2364.0,
+    "random_forest_regressor": 1572.0,
+}
+REF_GPU_S = {
+    "kmeans": 82.0,
+    "pca": 37.0,
+    "linear_regression": 41.0,
+    "linear_regression_elasticnet": 79.0,
+    "linear_regression_ridge": 32.0,
+    "logistic_regression": 69.0,
+    "random_forest_classifier": 59.0,
+    "random_forest_regressor": 52.0,
+}
+
+
+def geomean(xs: List[float]) -> float:
+    return float(math.exp(sum(math.log(x) for x in xs) / len(xs))) if xs else float("nan")
+
+
+REF_GEOMEAN_SPEEDUP = geomean([SPARK_CPU_S[k] / REF_GPU_S[k] for k in SPARK_CPU_S])
+
+
+@dataclass
+class Workload:
+    name: str
+    data: str  # generator family
+    make_estimator: Callable[[], Any]
+    label: bool = False
+
+
+def _pca() -> Any:
+    from ..feature import PCA
+
+    return PCA(k=3, inputCol="features")
+
+
+def _registry() -> Dict[str, Workload]:
+    reg: Dict[str, Workload] = {
+        "pca": Workload("pca", "low_rank_matrix", _pca),
+    }
+    try:
+        from ..clustering import KMeans
+
+        reg["kmeans"] = Workload(
+            "kmeans", "uniform",
+            lambda: KMeans(k=1000, maxIter=30, tol=1e-20, initMode="random", featuresCol="features", seed=1),
+        )
+    except ImportError:
+        pass
+    try:
+        from ..regression import LinearRegression
+
+        reg["linear_regression"] = Workload(
+            "linear_regression", "regression",
+            lambda: LinearRegression(regParam=0.0, elasticNetParam=0.0, standardization=False,
+                                     featuresCol="features", labelCol="label"), label=True)
+        reg["linear_regression_elasticnet"] = Workload(
+            "linear_regression_elasticnet", "regression",
+            lambda: LinearRegression(regParam=1e-5, elasticNetParam=0.5, tol=1e-30, maxIter=10, standardization=False,
+                                     featuresCol="features", labelCol="label"), label=True)
+        reg["linear_regression_ridge"] = Workload(
+            "linear_regression_ridge", "regression",
+            lambda: LinearRegression(regParam=1e-5, elasticNetParam=0.0, tol=1e-30, maxIter=10, standardization=False,
+                                     featuresCol="features", labelCol="label"), label=True)
+    except ImportError:
+        pass
+    try:
+        from ..classification import LogisticRegression
+
+        reg["logistic_regression"] = Workload(
+            "logistic_regression", "classification",
+            lambda: LogisticRegression(standardization=False, maxIter=200, tol=1e-30, regParam=1e-5,
+                                       featuresCol="features", labelCol="label"), label=True)
+    except ImportError:
+        pass
+    try:
+        from ..classification import RandomForestClassifier
+        from ..regression import RandomForestRegressor
+
+        reg["random_forest_classifier"] = Workload(
+            "random_forest_classifier", "classification",
+            lambda: RandomForestClassifier(numTrees=50, maxBins=128, maxDepth=13, featuresCol="features",
+                                           labelCol="label", seed=1), label=True)
+        reg["random_forest_regressor"] = Workload(
+            "random_forest_regressor", "regression",
+            lambda: RandomForestRegressor(numTrees=30, maxBins=128, maxDepth=6, featuresCol="features",
+                                          labelCol="label", seed=1), label=True)
+    except ImportError:
+        pass
+    return reg
+
+
+def registry() -> Dict[str, Workload]:
+    return _registry()
+
+
+def make_shard(family: str, m_local: int, n: int, device: torch.device, rank: int, m_total: int) -> Tuple[np.ndarray, Optional[np.ndarray]]:
+    seed = 1000 + rank
+    if family == "low_rank_matrix":
+        X = datagen.low_rank_matrix(m_local, n, device, seed=seed, m_total=m_total)
+        y = None
+    elif family == "uniform":
+        X = datagen.uniform(m_local, n, device, seed=seed)
+        y = None
+    elif family == "regression":
+        X, y = datagen.regression(m_local, n, device, seed=seed)
+    elif family == "classification":
+        X, y = datagen.classification(m_local, n, device, seed=seed, n_informative=n // 3, n_redundant=n // 3)
+    else:
+        raise ValueError(family)
+    Xh = datagen.to_pinned_numpy(X)
+    yh = y.cpu().numpy() if y is not None else None
+    del X
+    torch.cuda.empty_cache() if device.type == "cuda" else None
+    return Xh, yh

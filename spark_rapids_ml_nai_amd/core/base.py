@@ -1,0 +1,551 @@
+"""Estimator / Model base classes and the fit & transform drivers.
+
+Re-design of the reference's framework core (``core.py:426-1647``):
+
+* ``_Estimator._fit_internal`` = ``_CumlCaller._call_cuml_fit_func`` + ``_CumlEstimator._fit_internal``:
+  validate params, select/cast feature columns (array, VectorUDT dense/sparse, multi-column),
+  split the data into ``num_workers`` row partitions, run the algorithm's worker closure on
+  every rank, build one model per param map (``fitMultiple`` single pass).
+* Three execution backends for the same worker closure (``parallel/``):
+  SPMD (caller already runs one process per GPU under torchrun: no data movement, RCCL
+  group reused), LocalBarrierRunner (N spawned ranks, the Spark-free barrier stage) and
+  in-process for ``num_workers == 1``; the Spark barrier path lives in ``parallel/spark.py``.
+* The worker closure receives a ``FitInput`` with the partition already on the device
+  (zero-copy Arrow view -> pinned staging -> async H2D) and a ``WorkerContext`` holding the
+  rank's communicator — the analogue of the raft ``Handle`` the reference passes to cuML.
+* ``_Model._transform`` runs the model's device predict function per partition and appends
+  the output columns (prediction / probability / rawPrediction / outputCol).
+"""
+from __future__ import annotations
+
+import logging
+import threading
+from abc import abstractmethod
+from dataclasses import dataclass, field
+from typing import Any, Callable, Dict, Iterator, List, Optional, Sequence, Tuple, Type, Union
+
+import numpy as np
+import torch
+
+from ..parallel.context import (
+    PartitionDescriptor,
+    WorkerContext,
+    current_context,
+    gpu_available,
+    spmd_active,
+    use_context,
+)
+from ..utils.log import get_logger
+from ..utils.timer import PhaseTimer
+from .dataframe import (
+    DataFrame,
+    as_dataframe,
+    is_array_field,
+    is_vector_field,
+    restore_kind,
+    vector_column_is_sparse,
+    vector_column_to_csr,
+    vector_column_to_dense,
+    array_column_to_dense,
+)
+from .params import Param, _BackendParams
+from .persistence import (
+    EstimatorReader,
+    EstimatorWriter,
+    MLReadable,
+    MLWritable,
+    ModelReader,
+    ModelWriter,
+)
+
+
+# --------------------------------------------------------------------------------------
+# Column aliases (reference core.py:122-156)
+# --------------------------------------------------------------------------------------
+class alias:
+    data = "srml_values_c3BhcmtjdW1s"
+    label = "srml_label_c3BhcmtjdW1s"
+    row_number = "srml_row_number_c3BhcmtjdW1s"
+
+
+class pred:
+    prediction = "prediction"
+    probability = "probability"
+    model_index = "model_index"
+    raw_prediction = "raw_prediction"
+
+
+class param_alias:
+    cuml_init = "cuml_init"
+    handle = "handle"
+    num_cols = "num_cols"
+    part_sizes = "part_sizes"
+    loop = "loop"
+    fit_multiple_params = "fit_multiple_params"
+
+
+# --------------------------------------------------------------------------------------
+# Data carried to a worker and onto its device
+# --------------------------------------------------------------------------------------
+@dataclass
+class CSR:
+    """Device CSR matrix (row offsets int64, column indices int32, values)."""
+
+    indptr: torch.Tensor
+    indices: torch.Tensor
+    data: torch.Tensor
+    shape: Tuple[int, int]
+
+    @property
+    def device(self) -> torch.device:
+        return self.data.device
+
+    @property
+    def dtype(self) -> torch.dtype:
+        return self.data.dtype
+
+    def to_dense(self) -> torch.Tensor:
+        return torch.sparse_csr_tensor(self.indptr, self.indices.long(), self.data, self.shape).to_dense()
+
+
+@dataclass
+class HostPartition:
+    X: Any  # np.ndarray (rows, n) | scipy.sparse.csr_matrix | None
+    y: Optional[np.ndarray] = None
+    cols: Dict[str, np.ndarray] = field(default_factory=dict)
+    n_cols: int = 0
+
+    @property
+    def rows(self) -> int:
+        if self.X is not None:
+            return int(self.X.shape[0])
+        if self.y is not None:
+            return int(self.y.shape[0])
+        return int(next(iter(self.cols.values())).shape[0]) if self.cols else 0
+
+
+@dataclass
+class FitInput:
+    X: Union[torch.Tensor, CSR, None]
+    y: Optional[torch.Tensor]
+    cols: Dict[str, np.ndarray]
+    desc: PartitionDescriptor
+    host: HostPartition
+
+
+def to_device(X: Any, device: torch.device, dtype: Optional[torch.dtype] = None) -> Any:
+    """Host array -> device tensor through pinned staging (chunked, async H2D)."""
+    from ..ops.ingest import host_to_device
+
+    return host_to_device(X, device, dtype)
+
+
+def _dense_from_df(df: DataFrame, col: Optional[str], cols: Optional[List[str]], np_dtype: Any) -> Any:
+    if cols:
+        mats = [df.to_numpy(c).reshape(-1, 1) for c in cols]
+        return np.ascontiguousarray(np.hstack(mats).astype(np_dtype))
+    f = df.schema.field(col)
+    if is_vector_field(f):
+        return vector_column_to_dense(df.column(col), np_dtype)
+    if is_array_field(f):
+        return array_column_to_dense(df.column(col), np_dtype)
+    return df.to_numpy(col).astype(np_dtype).reshape(-1, 1)
+
+
+# --------------------------------------------------------------------------------------
+# Shared base
+# --------------------------------------------------------------------------------------
+class _CommonBase(_BackendParams, MLWritable, MLReadable):
+    def __init__(self) -> None:
+        super().__init__()
+        self.logger = get_logger(self.__class__)
+
+    @classmethod
+    def _pyspark_class(cls) -> Optional[str]:
+        """Fully-qualified pyspark.ml class this one mirrors (for ``cpu()``)."""
+        return None
+
+    def _verbose(self) -> Any:
+        return self._backend_params.get("verbose", False)
+
+
+def _split_rows(n: int, parts: int) -> List[Tuple[int, int]]:
+    b = np.linspace(0, n, parts + 1).astype(np.int64)
+    return [(int(b[i]), int(b[i + 1])) for i in range(parts)]
+
+
+class _Estimator(_CommonBase):
+    """Base of every estimator (reference ``_CumlEstimator`` + ``_CumlCaller``)."""
+
+    def __init__(self) -> None:
+        super().__init__()
+        self._initialize_backend_params()
+
+    # ---- hooks ------------------------------------------------------------------
+    @abstractmethod
+    def _get_fit_func(
+        self, dataset: DataFrame, extra_params: Optional[List[Dict[str, Any]]] = None
+    ) -> Callable[[FitInput, WorkerContext, Dict[str, Any]], Union[Dict[str, Any], List[Dict[str, Any]]]]:
+        """Return the worker closure ``fit(inp, ctx, params) -> attributes (or list for fitMultiple)``."""
+
+    @abstractmethod
+    def _create_model(self, result: Dict[str, Any]) -> "_Model":
+        ...
+
+    def _enable_fit_multiple_in_single_pass(self) -> bool:
+        return False
+
+    def _require_comm(self) -> bool:
+        """Whether the fit needs a live communicator (False -> ranks never talk, e.g. RF ensemble)."""
+        return True
+
+    def _fit_uses_label(self) -> bool:
+        return False
+
+    def _fit_extra_cols(self) -> List[str]:
+        return []
+
+    def _fit_array_order(self) -> str:
+        return "C"
+
+    def _supports_sparse(self) -> bool:
+        return False
+
+    def _validate_parameters(self) -> None:
+        pass
+
+    def _label_dtype(self, float32: bool) -> Any:
+        return np.float32 if float32 else np.float64
+
+    def _supportsTransformEvaluate(self, evaluator: Any) -> bool:
+        return False
+
+    # ---- data preparation ----------------------------------------------------------
+    def _use_sparse(self, df: DataFrame, col: Optional[str]) -> bool:
+        if col is None or not df.is_vector(col) or not self._supports_sparse():
+            return False
+        flag = None
+        if self.hasParam("enable_sparse_data_optim"):
+            flag = self.getOrDefault("enable_sparse_data_optim")
+        if flag is None:
+            return vector_column_is_sparse(df.column(col))
+        return bool(flag)
+
+    def _host_partition(self, df: DataFrame) -> HostPartition:
+        col, cols = self._get_input_columns()
+        np_dtype = np.float32 if self._float32_inputs else np.float64
+        if self._use_sparse(df, col):
+            X = vector_column_to_csr(df.column(col), np_dtype)
+        else:
+            X = _dense_from_df(df, col, cols, np_dtype)
+        y = None
+        if self._fit_uses_label():
+            lc = self.getOrDefault("labelCol")
+            y = df.to_numpy(lc).astype(self._label_dtype(self._float32_inputs))
+        extra = {c: df.to_numpy(c) for c in self._fit_extra_cols() if c in df.columns}
+        return HostPartition(X=X, y=y, cols=extra, n_cols=int(X.shape[1]) if X is not None else 0)
+
+    def _backend_param_maps(self, paramMaps: Optional[Sequence[Dict[Param, Any]]]) -> List[Dict[str, Any]]:
+        out = []
+        for pm in paramMaps or []:
+            d = {}
+            for k, v in pm.items():
+                name = self._get_backend_param(k.name, False)
+                if name is not None:
+                    d[name] = self._get_backend_mapping_value(name, v)
+            out.append(d)
+        return out
+
+    # ---- fit ----------------------------------------------------------------------
+    def fit(self, dataset: Any, params: Any = None) -> Any:
+        if params is None:
+            return self._fit(dataset)
+        if isinstance(params, dict):
+            return self.copy(params)._fit(dataset)
+        if isinstance(params, (list, tuple)):
+            models: List[Any] = [None] * len(params)
+            for idx, model in self.fitMultiple(dataset, params):
+                models[idx] = model
+            return models
+        raise TypeError("Params must be either a param map or a list/tuple of param maps")
+
+    def _fit(self, dataset: Any) -> "_Model":
+        return self._fit_internal(dataset, None)[0]
+
+    def fitMultiple(self, dataset: Any, paramMaps: Sequence[Dict[Param, Any]]) -> Iterator[Tuple[int, "_Model"]]:
+        if self._enable_fit_multiple_in_single_pass():
+            for pm in paramMaps:
+                for p in pm:
+                    self._get_backend_param(p.name, silent=False)
+            return _FitMultipleIterator(lambda: self._fit_internal(dataset, paramMaps), len(paramMaps))
+
+        est = self.copy()
+
+        def _gen() -> Iterator[Tuple[int, "_Model"]]:
+            for i, pm in enumerate(paramMaps):
+                yield i, est.copy(pm)._fit(dataset)
+
+        return _ThreadSafeIter(_gen())
+
+    def _fit_internal(self, dataset: Any, paramMaps: Optional[Sequence[Dict[Param, Any]]]) -> List["_Model"]:
+        self._validate_parameters()
+        timer = PhaseTimer()
+        df, _ = as_dataframe(dataset)
+        fit_multiple = self._backend_param_maps(paramMaps)
+        params = {
+            param_alias.cuml_init: dict(self._backend_params),
+            param_alias.fit_multiple_params: fit_multiple,
+        }
+        fit_fn = self._get_fit_func(df, fit_multiple or None)
+        results = run_fit_job(self, df, fit_fn, params, timer)
+        if not isinstance(results, list):
+            results = [results]
+        models = []
+        for i, r in enumerate(results):
+            model = self._create_model(r)
+            model._num_workers = self._num_workers
+            model._float32_inputs = self._float32_inputs
+            self._copyValues(model)
+            self._copy_backend_params(model)
+            if paramMaps is not None:
+                est_i = self.copy(paramMaps[i])
+                est_i._copyValues(model)
+                est_i._copy_backend_params(model)
+            model._fit_timings = dict(timer.times)
+            models.append(model)
+        return models
+
+    def write(self) -> EstimatorWriter:
+        return EstimatorWriter(self)
+
+    @classmethod
+    def read(cls) -> EstimatorReader:
+        return EstimatorReader(cls)
+
+
+class _EstimatorSupervised(_Estimator):
+    def _fit_uses_label(self) -> bool:
+        return True
+
+
+def _fit_worker(ctx: WorkerContext, payload: Tuple[HostPartition, Callable, Dict[str, Any], bool]) -> Any:
+    """Body of one barrier task: ingest to device, describe partitions, run the fit closure."""
+    hp, fit_fn, params, float32 = payload
+    if hp.rows == 0:
+        raise RuntimeError("A worker received no data. Please increase amount of data or use fewer workers.")
+    dtype = torch.float32 if float32 else torch.float64
+    X = to_device(hp.X, ctx.device, dtype) if hp.X is not None else None
+    y = to_device(hp.y, ctx.device) if hp.y is not None else None
+    desc = PartitionDescriptor.build(ctx, hp.rows, hp.n_cols)
+    inp = FitInput(X=X, y=y, cols=hp.cols, desc=desc, host=hp)
+    return fit_fn(inp, ctx, params)
+
+
+def run_fit_job(est: _Estimator, df: DataFrame, fit_fn: Callable, params: Dict[str, Any],
+                timer: Optional[PhaseTimer] = None) -> Any:
+    """Dispatch the worker closure to SPMD / in-process / LocalBarrierRunner (or Spark)."""
+    timer = timer or PhaseTimer()
+    float32 = est._float32_inputs
+    if spmd_active():
+        ctx = current_context() or WorkerContext.from_process_group()
+        with timer.phase("ingest"):
+            hp = est._host_partition(df)
+        with use_context(ctx), timer.phase("fit"):
+            res = _fit_worker(ctx, (hp, fit_fn, params, float32))
+        return res
+    nw = est.num_workers
+    if nw <= 1:
+        ctx = current_context() or WorkerContext.single()
+        with timer.phase("ingest"):
+            hp = est._host_partition(df)
+        with use_context(ctx), timer.phase("fit"):
+            return _fit_worker(ctx, (hp, fit_fn, params, float32))
+    from ..parallel.launcher import run_barrier_job
+
+    with timer.phase("ingest"):
+        if df.getNumPartitions() != nw:
+            df = df.repartition(nw)
+        hps = [est._host_partition(DataFrame([p])) for p in df.partitions]
+    with timer.phase("fit"):
+        results = run_barrier_job(_fit_worker, [(hp, fit_fn, params, float32) for hp in hps])
+    return results[0]
+
+
+class _FitMultipleIterator:
+    """Thread-safe iterator that fits every param map in ONE job on first ``next()``."""
+
+    def __init__(self, fitMultipleModels: Callable[[], List["_Model"]], numModels: int) -> None:
+        self.fitMultipleModels = fitMultipleModels
+        self.numModels = numModels
+        self.counter = 0
+        self.lock = threading.Lock()
+        self.models: Optional[List["_Model"]] = None
+
+    def __iter__(self) -> Iterator[Tuple[int, "_Model"]]:
+        return self
+
+    def __next__(self) -> Tuple[int, "_Model"]:
+        with self.lock:
+            index = self.counter
+            if index >= self.numModels:
+                raise StopIteration("No models remaining.")
+            if index == 0:
+                self.models = self.fitMultipleModels()
+                assert len(self.models) == self.numModels
+            self.counter += 1
+        assert self.models is not None
+        return index, self.models[index]
+
+    next = __next__
+
+
+class _ThreadSafeIter:
+    def __init__(self, it: Iterator) -> None:
+        self.it = it
+        self.lock = threading.Lock()
+
+    def __iter__(self) -> "_ThreadSafeIter":
+        return self
+
+    def __next__(self) -> Any:
+        with self.lock:
+            return next(self.it)
+
+
+# --------------------------------------------------------------------------------------
+# Models
+# --------------------------------------------------------------------------------------
+TransformFn = Callable[[Any, Any, WorkerContext], Dict[str, np.ndarray]]
+
+
+class _Model(_CommonBase):
+    """Base of every fitted model (reference ``_CumlModel``)."""
+
+    def __init__(self, **model_attributes: Any) -> None:
+        super().__init__()
+        self._model_attributes = model_attributes
+        self._fit_timings: Dict[str, float] = {}
+        self._device_state_cache: Dict[Any, Any] = {}
+        self._initialize_backend_params()
+
+    def _get_backend_params_default(self) -> Dict[str, Any]:
+        return {}
+
+    def _get_model_attributes(self) -> Dict[str, Any]:
+        return self._model_attributes
+
+    @classmethod
+    def _from_row(cls, model_attributes: Any) -> "_Model":
+        d = model_attributes.asDict() if hasattr(model_attributes, "asDict") else dict(model_attributes)
+        return cls(**d)
+
+    def cpu(self) -> Any:
+        raise NotImplementedError("cpu() needs pyspark; it is not installed" if not _have_pyspark() else "")
+
+    # ---- transform hooks -------------------------------------------------------------
+    @abstractmethod
+    def _get_transform_func(self, dataset: DataFrame) -> Tuple[Callable[[WorkerContext], Any], TransformFn]:
+        """Return (construct(ctx) -> device state, predict(state, X, ctx) -> {col: ndarray})."""
+
+    def _transform_input_cols(self) -> Tuple[Optional[str], Optional[List[str]]]:
+        return self._get_input_columns()
+
+    def _transform_supports_sparse(self) -> bool:
+        return False
+
+    def _transform_dtype(self) -> Any:
+        return np.float32 if self._float32_inputs else np.float64
+
+    def _transform_features(self, part: DataFrame) -> Any:
+        col, cols = self._transform_input_cols()
+        dt = self._transform_dtype()
+        if col is not None and part.is_vector(col) and self._transform_supports_sparse() and vector_column_is_sparse(part.column(col)):
+            return vector_column_to_csr(part.column(col), dt)
+        return _dense_from_df(part, col, cols, dt)
+
+    def _output_is_vector(self, df: DataFrame, out_col: str) -> bool:
+        """probability/rawPrediction are vectors; array outputs mirror a vector input column."""
+        return out_col in self._vector_output_cols()
+
+    def _vector_output_cols(self) -> List[str]:
+        return []
+
+    def _device(self) -> torch.device:
+        ctx = current_context()
+        if ctx is not None:
+            return ctx.device
+        from ..parallel.context import local_device
+
+        return local_device()
+
+    def transform(self, dataset: Any, params: Optional[Dict[Param, Any]] = None) -> Any:
+        if params:
+            return self.copy(params)._transform(dataset)
+        return self._transform(dataset)
+
+    def _transform(self, dataset: Any) -> Any:
+        df, kind = as_dataframe(dataset)
+        out = self._transform_df(df)
+        return restore_kind(out, kind)
+
+    def _transform_df(self, df: DataFrame) -> DataFrame:
+        construct, predict = self._get_transform_func(df)
+        ctx = current_context() or WorkerContext.single(self._device())
+        state = construct(ctx)
+        results: List[Dict[str, np.ndarray]] = []
+        for p in df.partitions:
+            part = DataFrame([p])
+            if p.num_rows == 0:
+                results.append({})
+                continue
+            X = self._transform_features(part)
+            results.append(predict(state, X, ctx))
+        names = [k for r in results for k in r.keys()]
+        names = list(dict.fromkeys(names))
+        out_parts = []
+        vec_cols = set(self._vector_output_cols())
+        for p, r in zip(df.partitions, results):
+            part = DataFrame([p])
+            for name in names:
+                v = r.get(name)
+                if v is None:
+                    v = np.zeros((0,), dtype=np.float64)
+                if isinstance(v, np.ndarray) and v.ndim == 2 and name in vec_cols:
+                    from .dataframe import dense_to_vector_array
+
+                    part = part.withColumn(name, dense_to_vector_array(v), vector=True)
+                else:
+                    part = part.withColumn(name, v)
+            out_parts.append(part.partitions[0])
+        return DataFrame(out_parts)
+
+    # ---- evaluation in the transform pass (CrossValidator fast path) ----------------------
+    def _transformEvaluate(self, dataset: Any, evaluator: Any, num_models: int = 1, params: Any = None) -> List[float]:
+        raise NotImplementedError()
+
+    @classmethod
+    def _combine(cls, models: List["_Model"]) -> "_Model":
+        raise NotImplementedError()
+
+    def write(self) -> ModelWriter:
+        return ModelWriter(self)
+
+    @classmethod
+    def read(cls) -> ModelReader:
+        return ModelReader(cls)
+
+
+class _ModelWithPredictionCol(_Model):
+    @property
+    def numFeatures(self) -> int:
+        n = self._model_attributes.get("n_cols")
+        return int(n) if n else -1
+
+
+def _have_pyspark() -> bool:
+    try:
+        import pyspark  # noqa: F401
+
+        return True
+    except Exception:  # noqa: BLE001
+        return False

@@ -1,0 +1,699 @@
+"""Spark-ML-compatible Param system plus the Spark<->backend parameter mapping layer.
+
+The reference builds on ``pyspark.ml.param`` (``python/src/spark_rapids_ml/params.py:131-554``).
+pyspark is an optional dependency here, so this module provides an API-compatible
+``Param``/``Params``/``TypeConverters``/``keyword_only`` implementation (same method names and
+semantics: defaults vs. user-set values, ``copy(extra)``, ``extractParamMap``, ``explainParams``)
+and, on top of it, ``_BackendParams`` — the Spark-param <-> device-solver kwarg mapping:
+
+* a Spark Param mapped to ``None`` raises when it is set (unsupported),
+* mapped to ``""`` warns and is ignored,
+* value mappers translate enum-like values (``params.py:137-212`` of the reference),
+* ``_set_params`` accepts Spark names, backend names, ``num_workers`` and ``float32_inputs``.
+
+The backend kwargs are exposed as ``backend_params`` with the reference's ``cuml_params`` kept
+as an alias so user code written against the reference keeps working.
+"""
+from __future__ import annotations
+
+import copy as _copy
+import functools
+import uuid
+import warnings
+from typing import Any, Callable, Dict, Iterable, List, Optional, Tuple, TypeVar, Union
+
+import numpy as np
+
+__all__ = [
+    "Param",
+    "Params",
+    "TypeConverters",
+    "keyword_only",
+    "_BackendParams",
+]
+
+
+# --------------------------------------------------------------------------------------
+# TypeConverters
+# --------------------------------------------------------------------------------------
+class TypeConverters:
+    """Same converters (and error behaviour) as ``pyspark.ml.param.TypeConverters``."""
+
+    @staticmethod
+    def _is_numeric(value: Any) -> bool:
+        return isinstance(value, (int, float, np.integer, np.floating)) and not isinstance(
+            value, bool
+        )
+
+    @staticmethod
+    def _is_integer(value: Any) -> bool:
+        return TypeConverters._is_numeric(value) and float(value).is_integer()
+
+    @staticmethod
+    def _can_convert_to_list(value: Any) -> bool:
+        return isinstance(value, (list, tuple, np.ndarray, range)) or hasattr(value, "toArray")
+
+    @staticmethod
+    def identity(value: Any) -> Any:
+        return value
+
+    @staticmethod
+    def toList(value: Any) -> List:
+        if type(value) == list:
+            return value
+        if TypeConverters._can_convert_to_list(value):
+            if hasattr(value, "toArray"):
+                return list(value.toArray())
+            return list(value)
+        raise TypeError("Could not convert %s to list" % value)
+
+    @staticmethod
+    def toListFloat(value: Any) -> List[float]:
+        v = TypeConverters.toList(value)
+        if all(TypeConverters._is_numeric(x) for x in v):
+            return [float(x) for x in v]
+        raise TypeError("Could not convert %s to list of floats" % value)
+
+    @staticmethod
+    def toListListFloat(value: Any) -> List[List[float]]:
+        return [TypeConverters.toListFloat(x) for x in TypeConverters.toList(value)]
+
+    @staticmethod
+    def toListInt(value: Any) -> List[int]:
+        v = TypeConverters.toList(value)
+        if all(TypeConverters._is_integer(x) for x in v):
+            return [int(x) for x in v]
+        raise TypeError("Could not convert %s to list of ints" % value)
+
+    @staticmethod
+    def toListString(value: Any) -> List[str]:
+        v = TypeConverters.toList(value)
+        if all(isinstance(x, str) for x in v):
+            return [str(x) for x in v]
+        raise TypeError("Could not convert %s to list of strings" % value)
+
+    @staticmethod
+    def toVector(value: Any) -> Any:
+        from .linalg import DenseVector, Vectors
+
+        if hasattr(value, "toArray") and hasattr(value, "size"):
+            return value
+        if TypeConverters._can_convert_to_list(value):
+            v = TypeConverters.toList(value)
+            if all(TypeConverters._is_numeric(x) for x in v):
+                return Vectors.dense(v)
+        raise TypeError("Could not convert %s to vector" % value)
+
+    @staticmethod
+    def toMatrix(value: Any) -> Any:
+        if hasattr(value, "toArray") and hasattr(value, "numRows"):
+            return value
+        raise TypeError("Could not convert %s to matrix" % value)
+
+    @staticmethod
+    def toFloat(value: Any) -> float:
+        if TypeConverters._is_numeric(value):
+            return float(value)
+        raise TypeError("Could not convert %s to float" % value)
+
+    @staticmethod
+    def toInt(value: Any) -> int:
+        if TypeConverters._is_integer(value):
+            return int(value)
+        raise TypeError("Could not convert %s to int" % value)
+
+    @staticmethod
+    def toString(value: Any) -> str:
+        if isinstance(value, str):
+            return value
+        if isinstance(value, np.str_):
+            return str(value)
+        raise TypeError("Could not convert %s to string type" % type(value))
+
+    @staticmethod
+    def toBoolean(value: Any) -> bool:
+        if type(value) == bool or isinstance(value, np.bool_):
+            return bool(value)
+        raise TypeError("Boolean Param requires value of type bool. Found %s." % type(value))
+
+
+# --------------------------------------------------------------------------------------
+# Param / Params
+# --------------------------------------------------------------------------------------
+class _Dummy:
+    uid = "undefined"
+
+
+class Param:
+    """A param with self-contained documentation (pyspark.ml.param.Param equivalent)."""
+
+    def __init__(
+        self,
+        parent: Any,
+        name: str,
+        doc: str,
+        typeConverter: Optional[Callable[[Any], Any]] = None,
+    ) -> None:
+        if not isinstance(parent, _Dummy) and not hasattr(parent, "uid"):
+            raise TypeError("Parent must be a Params object but got %s" % type(parent))
+        self.parent = parent.uid
+        self.name = str(name)
+        self.doc = str(doc)
+        self.typeConverter = TypeConverters.identity if typeConverter is None else typeConverter
+
+    def _copy_new_parent(self, parent: Any) -> "Param":
+        if self.parent == "undefined":
+            param = _copy.copy(self)
+            param.parent = parent.uid
+            return param
+        raise ValueError("Cannot copy from non-dummy parent %s." % parent)
+
+    def __str__(self) -> str:
+        return str(self.parent) + "__" + self.name
+
+    def __repr__(self) -> str:
+        return "Param(parent=%r, name=%r, doc=%r)" % (self.parent, self.name, self.doc)
+
+    def __hash__(self) -> int:
+        return hash(str(self))
+
+    def __eq__(self, other: Any) -> bool:
+        if isinstance(other, Param):
+            return self.parent == other.parent and self.name == other.name
+        return False
+
+
+def keyword_only(func: Callable) -> Callable:
+    """Only allow keyword arguments; stores them in ``self._input_kwargs`` (pyspark semantics)."""
+
+    @functools.wraps(func)
+    def wrapper(self: Any, *args: Any, **kwargs: Any) -> Any:
+        if len(args) > 0:
+            raise TypeError("Method %s forces keyword arguments." % func.__name__)
+        self._input_kwargs = kwargs
+        return func(self, **kwargs)
+
+    return wrapper
+
+
+class Params:
+    """Components that take parameters (pyspark.ml.param.Params equivalent)."""
+
+    @staticmethod
+    def _dummy() -> _Dummy:
+        return _Dummy()
+
+    def __init__(self) -> None:
+        self.uid = self._randomUID()
+        self._paramMap: Dict[Param, Any] = {}
+        self._defaultParamMap: Dict[Param, Any] = {}
+        self._params: Optional[List[Param]] = None
+        self._copy_params()
+
+    @classmethod
+    def _randomUID(cls) -> str:
+        return cls.__name__ + "_" + uuid.uuid4().hex[-12:]
+
+    def _copy_params(self) -> None:
+        cls = type(self)
+        src_name_attrs = [(x, getattr(cls, x)) for x in dir(cls)]
+        src_params = [(n, a) for n, a in src_name_attrs if isinstance(a, Param)]
+        for name, param in src_params:
+            setattr(self, name, param._copy_new_parent(self))
+
+    @property
+    def params(self) -> List[Param]:
+        if self._params is None:
+            self._params = [
+                getattr(self, x)
+                for x in dir(self)
+                if x != "params" and not isinstance(getattr(type(self), x, None), property)
+                and isinstance(getattr(self, x), Param)
+            ]
+        return self._params
+
+    def explainParam(self, param: Union[str, Param]) -> str:
+        param = self._resolveParam(param)
+        values = []
+        if self.isDefined(param):
+            if param in self._defaultParamMap:
+                values.append("default: %s" % self._defaultParamMap[param])
+            if param in self._paramMap:
+                values.append("current: %s" % self._paramMap[param])
+        else:
+            values.append("undefined")
+        return "%s: %s (%s)" % (param.name, param.doc, ", ".join(values))
+
+    def explainParams(self) -> str:
+        return "\n".join([self.explainParam(p) for p in self.params])
+
+    def getParam(self, paramName: str) -> Param:
+        param = getattr(self, paramName, None)
+        if isinstance(param, Param):
+            return param
+        raise ValueError("Cannot find param with name %s." % paramName)
+
+    def hasParam(self, paramName: str) -> bool:
+        if isinstance(paramName, str):
+            p = getattr(self, paramName, None)
+            return isinstance(p, Param)
+        raise TypeError("hasParam(): paramName must be a string")
+
+    def isSet(self, param: Union[str, Param]) -> bool:
+        return self._resolveParam(param) in self._paramMap
+
+    def hasDefault(self, param: Union[str, Param]) -> bool:
+        return self._resolveParam(param) in self._defaultParamMap
+
+    def isDefined(self, param: Union[str, Param]) -> bool:
+        return self.isSet(param) or self.hasDefault(param)
+
+    def getOrDefault(self, param: Union[str, Param]) -> Any:
+        param = self._resolveParam(param)
+        if param in self._paramMap:
+            return self._paramMap[param]
+        if param in self._defaultParamMap:
+            return self._defaultParamMap[param]
+        raise KeyError("Param %s is not set and has no default." % param.name)
+
+    def extractParamMap(self, extra: Optional[Dict[Param, Any]] = None) -> Dict[Param, Any]:
+        if extra is None:
+            extra = dict()
+        paramMap = self._defaultParamMap.copy()
+        paramMap.update(self._paramMap)
+        paramMap.update(extra)
+        return paramMap
+
+    def copy(self: "P_", extra: Optional[Dict[Param, Any]] = None) -> "P_":
+        if extra is None:
+            extra = dict()
+        that = _copy.copy(self)
+        that._paramMap = {}
+        that._defaultParamMap = {}
+        return self._copyValues(that, extra)
+
+    def set(self, param: Param, value: Any) -> None:
+        self._shouldOwn(param)
+        try:
+            value = param.typeConverter(value)
+        except ValueError as e:
+            raise ValueError('Invalid param value given for param "%s". %s' % (param.name, e))
+        self._paramMap[param] = value
+
+    def _shouldOwn(self, param: Param) -> None:
+        if not (self.uid == param.parent and self.hasParam(param.name)):
+            raise ValueError("Param %r does not belong to %r." % (param, self))
+
+    def _resolveParam(self, param: Union[str, Param]) -> Param:
+        if isinstance(param, Param):
+            self._shouldOwn(param)
+            return param
+        if isinstance(param, str):
+            return self.getParam(param)
+        raise TypeError("Cannot resolve %r as a param." % param)
+
+    def clear(self, param: Param) -> None:
+        if self.isSet(param):
+            del self._paramMap[self._resolveParam(param)]
+
+    def _set(self: "P_", **kwargs: Any) -> "P_":
+        for param, value in kwargs.items():
+            p = getattr(self, param)
+            if value is not None:
+                try:
+                    value = p.typeConverter(value)
+                except TypeError as e:
+                    raise TypeError('Invalid param value given for param "%s". %s' % (p.name, e))
+            self._paramMap[p] = value
+        return self
+
+    def _clear(self, param: Param) -> None:
+        self.clear(param)
+
+    def _setDefault(self: "P_", **kwargs: Any) -> "P_":
+        for param, value in kwargs.items():
+            p = getattr(self, param)
+            if value is not None and not isinstance(value, dict):
+                try:
+                    value = p.typeConverter(value)
+                except TypeError as e:
+                    raise TypeError(
+                        'Invalid default param value given for param "%s". %s' % (p.name, e)
+                    )
+            self._defaultParamMap[p] = value
+        return self
+
+    def _copyValues(self, to: "P_", extra: Optional[Dict[Param, Any]] = None) -> "P_":
+        paramMap = self._paramMap.copy()
+        if isinstance(extra, dict):
+            for param, value in extra.items():
+                if isinstance(param, Param):
+                    paramMap[param] = value
+                else:
+                    raise TypeError("Expecting a valid instance of Param, but received: %s" % param)
+        elif extra is not None:
+            raise TypeError("Expecting a dict, but received an object of type %s." % type(extra))
+        for param in self.params:
+            if param in self._defaultParamMap and to.hasParam(param.name):
+                to._defaultParamMap[to.getParam(param.name)] = self._defaultParamMap[param]
+            if param in paramMap and to.hasParam(param.name):
+                to._set(**{param.name: paramMap[param]})
+        return to
+
+    def _resetUid(self: "P_", newUid: Any) -> "P_":
+        newUid = str(newUid)
+        self.uid = newUid
+        newDefaultParamMap = dict()
+        newParamMap = dict()
+        for param in self.params:
+            newParam = _copy.copy(param)
+            newParam.parent = newUid
+            if param in self._defaultParamMap:
+                newDefaultParamMap[newParam] = self._defaultParamMap[param]
+            if param in self._paramMap:
+                newParamMap[newParam] = self._paramMap[param]
+            param.parent = newUid
+        self._defaultParamMap = newDefaultParamMap
+        self._paramMap = newParamMap
+        return self
+
+
+P_ = TypeVar("P_", bound=Params)
+
+
+# --------------------------------------------------------------------------------------
+# Shared Spark params (pyspark.ml.param.shared equivalents that the API needs)
+# --------------------------------------------------------------------------------------
+def _shared(name: str, doc: str, conv: Callable, getter: str) -> type:
+    def _init(self: Any) -> None:
+        super(cls, self).__init__()  # type: ignore[misc]
+
+    def _get(self: Any) -> Any:
+        return self.getOrDefault(getattr(self, name))
+
+    cls = type(
+        "Has" + name[0].upper() + name[1:],
+        (Params,),
+        {name: Param(Params._dummy(), name, doc, typeConverter=conv), getter: _get},
+    )
+    return cls
+
+
+HasFeaturesCol = _shared("featuresCol", "features column name.", TypeConverters.toString, "getFeaturesCol")
+HasFeaturesCols = _shared(
+    "featuresCols", "features column names for multi-column input.", TypeConverters.toListString, "getFeaturesCols"
+)
+HasInputCol = _shared("inputCol", "input column name.", TypeConverters.toString, "getInputCol")
+HasInputCols = _shared("inputCols", "input column names.", TypeConverters.toListString, "getInputCols")
+HasOutputCol = _shared("outputCol", "output column name.", TypeConverters.toString, "getOutputCol")
+HasLabelCol = _shared("labelCol", "label column name.", TypeConverters.toString, "getLabelCol")
+HasPredictionCol = _shared("predictionCol", "prediction column name.", TypeConverters.toString, "getPredictionCol")
+HasProbabilityCol = _shared(
+    "probabilityCol",
+    "Column name for predicted class conditional probabilities.",
+    TypeConverters.toString,
+    "getProbabilityCol",
+)
+HasRawPredictionCol = _shared(
+    "rawPredictionCol", "raw prediction (a.k.a. confidence) column name.", TypeConverters.toString, "getRawPredictionCol"
+)
+HasMaxIter = _shared("maxIter", "max number of iterations (>= 0).", TypeConverters.toInt, "getMaxIter")
+HasTol = _shared("tol", "the convergence tolerance for iterative algorithms (>= 0).", TypeConverters.toFloat, "getTol")
+HasSeed = _shared("seed", "random seed.", TypeConverters.toInt, "getSeed")
+HasRegParam = _shared("regParam", "regularization parameter (>= 0).", TypeConverters.toFloat, "getRegParam")
+HasElasticNetParam = _shared(
+    "elasticNetParam",
+    "the ElasticNet mixing parameter, in range [0, 1]. For alpha = 0, the penalty is an L2 penalty. "
+    "For alpha = 1, it is an L1 penalty.",
+    TypeConverters.toFloat,
+    "getElasticNetParam",
+)
+HasFitIntercept = _shared("fitIntercept", "whether to fit an intercept term.", TypeConverters.toBoolean, "getFitIntercept")
+HasStandardization = _shared(
+    "standardization",
+    "whether to standardize the training features before fitting the model.",
+    TypeConverters.toBoolean,
+    "getStandardization",
+)
+HasWeightCol = _shared(
+    "weightCol",
+    "weight column name. If this is not set or empty, we treat all instance weights as 1.0.",
+    TypeConverters.toString,
+    "getWeightCol",
+)
+HasAggregationDepth = _shared(
+    "aggregationDepth", "suggested depth for treeAggregate (>= 2).", TypeConverters.toInt, "getAggregationDepth"
+)
+HasMaxBlockSizeInMB = _shared(
+    "maxBlockSizeInMB",
+    "maximum memory in MB for stacking input data into blocks.",
+    TypeConverters.toFloat,
+    "getMaxBlockSizeInMB",
+)
+HasSolver = _shared("solver", "the solver algorithm for optimization.", TypeConverters.toString, "getSolver")
+HasLoss = _shared("loss", "the loss function to be optimized.", TypeConverters.toString, "getLoss")
+HasThreshold = _shared(
+    "threshold", "threshold in binary classification prediction, in range [0, 1].", TypeConverters.toFloat, "getThreshold"
+)
+HasThresholds = _shared(
+    "thresholds", "Thresholds in multi-class classification.", TypeConverters.toListFloat, "getThresholds"
+)
+HasDistanceMeasure = _shared(
+    "distanceMeasure",
+    "the distance measure. Supported options: 'euclidean' and 'cosine'.",
+    TypeConverters.toString,
+    "getDistanceMeasure",
+)
+HasCheckpointInterval = _shared(
+    "checkpointInterval", "set checkpoint interval (>= 1) or disable checkpoint (-1).", TypeConverters.toInt,
+    "getCheckpointInterval",
+)
+HasLeafCol = _shared("leafCol", "Leaf indices column name.", TypeConverters.toString, "getLeafCol")
+
+
+class HasIDCol(Params):
+    """Mixin for param idCol (reference ``params.py:90-128``)."""
+
+    idCol = Param(Params._dummy(), "idCol", "id column name.", typeConverter=TypeConverters.toString)
+
+    def getIdCol(self) -> str:
+        return self.getOrDefault("idCol")
+
+    def _ensureIdCol(self, df: Any) -> Any:
+        """Add a monotonically increasing id column unless the user set one that exists."""
+        if not self.isSet("idCol"):
+            while self.getIdCol() in df.columns:
+                self._set(**{"idCol": self.getIdCol() + "_dedup"})
+            return df.with_row_id(self.getIdCol())
+        if self.getIdCol() not in df.columns:
+            return df.with_row_id(self.getIdCol())
+        return df
+
+
+class HasEnableSparseDataOptim(Params):
+    """enable_sparse_data_optim: None=auto (first row decides), True=CSR, False=dense."""
+
+    enable_sparse_data_optim = Param(
+        Params._dummy(),
+        "enable_sparse_data_optim",
+        "If None, use sparse arrays when the first vector of the features column is sparse; "
+        "if True always build CSR; if False always densify.",
+        typeConverter=TypeConverters.toBoolean,
+    )
+
+    def __init__(self) -> None:
+        super().__init__()
+        self._setDefault(enable_sparse_data_optim=None)
+
+
+# --------------------------------------------------------------------------------------
+# Spark <-> backend parameter mapping
+# --------------------------------------------------------------------------------------
+class _BackendClass:
+    """Helper hooks for mapping Spark ML Params to device-solver kwargs."""
+
+    @classmethod
+    def _param_mapping(cls) -> Dict[str, Optional[str]]:
+        """Spark Param name -> backend kwarg name ('' = ignore with warning, None = unsupported)."""
+        return {}
+
+    @classmethod
+    def _param_value_mapping(cls) -> Dict[str, Callable[[Any], Union[None, str, float, int]]]:
+        """backend kwarg name -> function mapping a Spark value to a backend value (None = unsupported)."""
+        return {}
+
+    def _get_backend_params_default(self) -> Dict[str, Any]:
+        raise NotImplementedError()
+
+
+class _BackendParams(_BackendClass, Params):
+    """Common param handling for every estimator and model (reference ``params.py:215-554``)."""
+
+    _backend_params: Dict[str, Any] = {}
+    _num_workers: Optional[int] = None
+    _float32_inputs: bool = True
+
+    # --- backend kwargs ------------------------------------------------------------
+    @property
+    def backend_params(self) -> Dict[str, Any]:
+        return self._backend_params
+
+    @property
+    def cuml_params(self) -> Dict[str, Any]:
+        """Alias kept for source compatibility with spark-rapids-ml user code."""
+        return self._backend_params
+
+    @property
+    def num_workers(self) -> int:
+        """Number of device workers (one rank per GPU)."""
+        from ..parallel.context import infer_num_workers
+
+        inferred = infer_num_workers()
+        if self._num_workers is not None:
+            if self._num_workers < 1:
+                raise ValueError("num_workers must be >= 1")
+            return self._num_workers
+        return inferred
+
+    @num_workers.setter
+    def num_workers(self, value: int) -> None:
+        self._num_workers = value
+
+    def copy(self: "BP", extra: Optional[Dict[Param, Any]] = None) -> "BP":
+        instance: BP = super().copy(extra)  # type: ignore[assignment]
+        backend_params = instance._backend_params.copy()
+        if isinstance(extra, dict):
+            for param, value in extra.items():
+                if isinstance(param, Param):
+                    name = instance._get_backend_param(param.name, silent=False)
+                    if name is not None:
+                        backend_params[name] = instance._get_backend_mapping_value(name, value)
+                else:
+                    raise TypeError("Expecting a valid instance of Param, but received: {}".format(param))
+        instance._backend_params = backend_params
+        return instance
+
+    def _initialize_backend_params(self) -> None:
+        self._backend_params = self._get_backend_params_default()
+        for spark_param in self._param_mapping().keys():
+            if self.hasParam(spark_param) and self.hasDefault(spark_param):
+                self._set_backend_param(spark_param, self.getOrDefault(spark_param))
+
+    # reference-compatible name
+    _initialize_cuml_params = _initialize_backend_params
+
+    def _set_params(self: "BP", **kwargs: Any) -> "BP":
+        param_map = self._param_mapping()
+        for spark_param, be_param in param_map.items():
+            if spark_param != be_param and spark_param in kwargs and be_param in kwargs:
+                raise ValueError(f"'{be_param}' is an alias of '{spark_param}', set one or the other.")
+
+        for k, v in kwargs.items():
+            if k == "inputCol":
+                if isinstance(v, str):
+                    self._set(**{"inputCol": v})
+                elif isinstance(v, (list, tuple)):
+                    self._set(**{"inputCols": list(v)})
+            elif k == "featuresCol":
+                if isinstance(v, str):
+                    self._set(**{"featuresCol": v})
+                elif isinstance(v, (list, tuple)):
+                    self._set(**{"featuresCols": list(v)})
+            elif self.hasParam(k):
+                self._set(**{str(k): v})
+                self._set_backend_param(k, v, silent=False)
+            elif k in self._backend_params:
+                self._backend_params[k] = v
+                for spark_param, be_param in param_map.items():
+                    if k == be_param and self.hasParam(spark_param):
+                        try:
+                            self._set(**{str(spark_param): v})
+                        except TypeError:
+                            pass
+            elif k == "num_workers":
+                self._num_workers = v
+            elif k == "float32_inputs":
+                self._float32_inputs = v
+            else:
+                raise ValueError(f"Unsupported param '{k}'.")
+        return self
+
+    def clear(self, param: Param) -> None:
+        super().clear(param)
+        be = self._param_mapping().get(param.name)
+        if be:
+            self._backend_params[be] = self._get_backend_mapping_value(be, self.getOrDefault(param.name))
+
+    def _copy_backend_params(self, to: "BP") -> "BP":
+        for k, v in self._backend_params.items():
+            if k in to._backend_params:
+                to._backend_params[k] = v
+        return to
+
+    _copy_cuml_params = _copy_backend_params
+
+    def _get_input_columns(self) -> Tuple[Optional[str], Optional[List[str]]]:
+        if self.hasParam("inputCols") and self.isDefined("inputCols"):
+            return None, self.getOrDefault("inputCols")
+        if self.hasParam("inputCol") and self.isDefined("inputCol"):
+            return self.getOrDefault("inputCol"), None
+        if self.hasParam("featuresCols") and self.isDefined("featuresCols"):
+            return None, self.getOrDefault("featuresCols")
+        if self.hasParam("featuresCol") and self.isDefined("featuresCol"):
+            return self.getOrDefault("featuresCol"), None
+        raise ValueError("Please set inputCol(s) or featuresCol(s)")
+
+    def _get_backend_param(self, spark_param: str, silent: bool = True) -> Optional[str]:
+        param_map = self._param_mapping()
+        if spark_param not in param_map:
+            return None
+        be = param_map[spark_param]
+        if be is None:
+            if not silent:
+                raise ValueError(f"Spark Param '{spark_param}' is not supported on the device backend.")
+            return None
+        if be == "":
+            if not silent:
+                warnings.warn(f"Spark Param '{spark_param}' is not used by the device backend.")
+            return None
+        return be
+
+    _get_cuml_param = _get_backend_param
+
+    def _set_backend_param(self, spark_param: str, spark_value: Any, silent: bool = True) -> None:
+        be = self._get_backend_param(spark_param, silent)
+        if be is not None:
+            try:
+                self._backend_params[be] = self._get_backend_mapping_value(be, spark_value)
+            except ValueError:
+                ref = be + " or " + spark_param if be != spark_param else spark_param
+                raise ValueError(f"{ref} given invalid value {spark_value}")
+
+    _set_cuml_param = _set_backend_param
+
+    def _get_backend_mapping_value(self, k: str, v: Any) -> Any:
+        vm = self._param_value_mapping()
+        if k not in vm:
+            return v
+        mapped = vm[k](v)
+        if mapped is None:
+            raise ValueError(f"Value '{v}' for '{k}' param is unsupported")
+        return mapped
+
+    _get_cuml_mapping_value = _get_backend_mapping_value
+
+
+BP = TypeVar("BP", bound=_BackendParams)
+
+
+def _params_getters_setters(cls: type, names: Iterable[str]) -> None:
+    """Attach ``getX``/``setX`` methods for Params declared on ``cls`` (keeps API surface uniform)."""
+    for n in names:
+        cap = n[0].upper() + n[1:]
+        if not hasattr(cls, "get" + cap):
+            setattr(cls, "get" + cap, lambda self, _n=n: self.getOrDefault(_n))
+        if not hasattr(cls, "set" + cap):
+            def _setter(self: Any, value: Any, _n: str = n) -> Any:
+                return self._set_params(**{_n: value})
+
+            setattr(cls, "set" + cap, _setter)

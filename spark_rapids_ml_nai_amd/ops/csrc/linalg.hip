@@ -1,0 +1,222 @@
+// Dense linear-algebra building blocks for the solvers.
+//
+//  * srml_xw_f32     — skinny GEMM  out = X W + bias  (X: m x n row-major, W: n x k, k <= 32).
+//                      Bandwidth-bound: ONE pass over X, W staged in LDS, each wave owns a row
+//                      at a time with 16-B vector loads, per-lane k partial sums reduced with
+//                      wave64 shuffles. PCA transform (X·pcᵀ), GLM / linear predictions, and the
+//                      reference's JNI `dgemm` on a cudf list column (rapidsml_jni.cu:75-107).
+//  * srml_dgemm      — fp64 C = alpha op(A) op(B) + beta C on the f64 MFMA
+//                      (`v_mfma_f64_16x16x4_f64`), LDS-tiled 64x64 per 256-thread block.
+//                      Krylov products with the fp64 covariance (PCA eigensolver), normal-
+//                      equation solves, and the C-ABI `srml_dgemm` (reference JNI dgemm,
+//                      rapidsml_jni.cu:131-212).
+//  * srml_sign_flip_f64 — deterministic eigenvector signs: one wave per column finds the
+//                      max-|x| entry with a wave64 arg-max and negates the column if that entry
+//                      is negative (reference N1 `signFlip`, rapidsml_jni.cu:35-61, which used
+//                      one thread per column).
+#include "common.h"
+
+// ------------------------------------------------------------------------------------------
+// skinny GEMM
+// ------------------------------------------------------------------------------------------
+template <int K, bool VEC>
+__global__ __launch_bounds__(256) void xw_kernel(const float* __restrict__ X, long m, int n, long ld,
+                                                 const float* __restrict__ W, const float* __restrict__ bias,
+                                                 float* __restrict__ out, long ldo, int wlds_rows) {
+  extern __shared__ __attribute__((aligned(16))) float Ws[];  // [wlds_rows][K]
+  for (int i = threadIdx.x; i < wlds_rows * K; i += blockDim.x) Ws[i] = W[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const long nwaves = (long)gridDim.x * 4;
+  for (long r = wave; r < m; r += nwaves) {
+    const float* row = X + r * ld;
+    float acc[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) acc[c] = 0.f;
+    if (VEC) {
+      for (int d = lane * 4; d < n; d += 256) {
+        floatx4 v = *reinterpret_cast<const floatx4*>(row + d);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float* w = (d + q < wlds_rows) ? &Ws[(d + q) * K] : &W[(long)(d + q) * K];
+#pragma unroll
+          for (int c = 0; c < K; ++c) acc[c] = fmaf(v[q], w[c], acc[c]);
+        }
+      }
+    } else {
+      for (int d = lane; d < n; d += 64) {
+        const float v = row[d];
+        const float* w = (d < wlds_rows) ? &Ws[d * K] : &W[(long)d * K];
+#pragma unroll
+        for (int c = 0; c < K; ++c) acc[c] = fmaf(v, w[c], acc[c]);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < K; ++c) acc[c] = wave_sum(acc[c]);
+    if (lane < K) {
+      float v = 0.f;
+#pragma unroll
+      for (int c = 0; c < K; ++c)
+        if (c == lane) v = acc[c];
+      out[r * ldo + lane] = v + (bias ? bias[lane] : 0.f);
+    }
+  }
+}
+
+template <int K>
+static int launch_xw(const float* X, long m, int n, long ld, const float* W, const float* bias, float* out, long ldo,
+                     hipStream_t stream) {
+  const int max_rows = (48 * 1024) / (4 * K);
+  const int wrows = n < max_rows ? n : max_rows;
+  const bool vec = ((ld & 3) == 0) && ((n & 3) == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
+  long blocks = (m + 3) / 4;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  size_t lds = (size_t)wrows * K * sizeof(float);
+  if (vec)
+    hipLaunchKernelGGL((xw_kernel<K, true>), dim3((unsigned)blocks), dim3(256), lds, stream, X, m, n, ld, W, bias, out,
+                       ldo, wrows);
+  else
+    hipLaunchKernelGGL((xw_kernel<K, false>), dim3((unsigned)blocks), dim3(256), lds, stream, X, m, n, ld, W, bias, out,
+                       ldo, wrows);
+  return srml_status();
+}
+
+SRML_API int srml_xw_f32(const float* X, long m, int n, long ld, const float* W, int k, const float* bias, float* out,
+                         long ldo, hipStream_t stream) {
+  if (m <= 0) return 0;
+  switch (k) {
+    case 1: return launch_xw<1>(X, m, n, ld, W, bias, out, ldo, stream);
+    case 2: return launch_xw<2>(X, m, n, ld, W, bias, out, ldo, stream);
+    case 3: return launch_xw<3>(X, m, n, ld, W, bias, out, ldo, stream);
+    case 4: return launch_xw<4>(X, m, n, ld, W, bias, out, ldo, stream);
+    case 8: return launch_xw<8>(X, m, n, ld, W, bias, out, ldo, stream);
+    case 16: return launch_xw<16>(X, m, n, ld, W, bias, out, ldo, stream);
+    case 32: return launch_xw<32>(X, m, n, ld, W, bias, out, ldo, stream);
+    default: return -1;  // caller pads k up to a supported width
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// fp64 GEMM on f64 MFMA (16x16x4): block tile 64x64, 4 waves each 32x32 (2x2 MFMA tiles), BK=16
+// ------------------------------------------------------------------------------------------
+namespace {
+constexpr int DT = 64;
+constexpr int DK = 16;
+}
+
+// v_mfma_f64_16x16x4_f64: A[i=l&15][k=l>>4], B[k=l>>4][j=l&15]; D: col=l&15, row=(l>>4)+4*r
+__global__ __launch_bounds__(256) void dgemm_kernel(int M, int N, int K, double alpha, const double* __restrict__ A,
+                                                    long lda, int ta, const double* __restrict__ B, long ldb, int tb,
+                                                    double beta, double* __restrict__ C, long ldc) {
+  __shared__ double As[DK][DT + 1];  // As[k][i]
+  __shared__ double Bs[DK][DT + 1];  // Bs[k][j]
+  const int i0 = blockIdx.y * DT, j0 = blockIdx.x * DT;
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int wi = wid >> 1, wj = wid & 1;
+  doublex4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = doublex4{0, 0, 0, 0};
+
+  for (int k0 = 0; k0 < K; k0 += DK) {
+    // stage 64x16 of op(A) and 16x64 of op(B): 1024 elements each, 4 per thread
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      int e = t + 256 * p;
+      int kk = e / DT, ii = e % DT;  // natural for ta (A^T: row k contiguous in i)
+      int gi = i0 + ii, gk = k0 + kk;
+      double va = 0.0;
+      if (ta) {
+        if (gi < M && gk < K) va = A[(long)gk * lda + gi];
+      } else {
+        int kk2 = e % DK, ii2 = e / DK;  // A row-major: k contiguous
+        gi = i0 + ii2; gk = k0 + kk2;
+        if (gi < M && gk < K) va = A[(long)gi * lda + gk];
+        kk = kk2; ii = ii2;
+      }
+      As[kk][ii] = va;
+      int jj = e % DT, kb = e / DT;
+      int gj = j0 + jj, gkb = k0 + kb;
+      double vb = 0.0;
+      if (!tb) {
+        if (gj < N && gkb < K) vb = B[(long)gkb * ldb + gj];
+      } else {
+        int kb2 = e % DK, jj2 = e / DK;  // B^T: B stored N x K row-major
+        gj = j0 + jj2; gkb = k0 + kb2;
+        if (gj < N && gkb < K) vb = B[(long)gj * ldb + gkb];
+        kb = kb2; jj = jj2;
+      }
+      Bs[kb][jj] = vb;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < DK / 4; ++ks) {
+      const int k = ks * 4 + (lane >> 4);
+      double a0 = As[k][wi * 32 + (lane & 15)];
+      double a1 = As[k][wi * 32 + 16 + (lane & 15)];
+      double b0 = Bs[k][wj * 32 + (lane & 15)];
+      double b1 = Bs[k][wj * 32 + 16 + (lane & 15)];
+      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int gi = i0 + wi * 32 + mt * 16 + (lane >> 4) + 4 * r;
+        int gj = j0 + wj * 32 + nt * 16 + (lane & 15);
+        if (gi < M && gj < N) {
+          double* c = &C[(long)gi * ldc + gj];
+          *c = alpha * acc[mt][nt][r] + (beta != 0.0 ? beta * *c : 0.0);
+        }
+      }
+}
+
+SRML_API int srml_dgemm(int ta, int tb, int M, int N, int K, double alpha, const double* A, long lda, const double* B,
+                        long ldb, double beta, double* C, long ldc, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  dim3 grid(ceil_div(N, DT), ceil_div(M, DT));
+  hipLaunchKernelGGL(dgemm_kernel, grid, dim3(256), 0, stream, M, N, K, alpha, A, lda, ta, B, ldb, tb, beta, C, ldc);
+  return srml_status();
+}
+
+// ------------------------------------------------------------------------------------------
+// sign flip (one wave per column)
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sign_flip_kernel(double* __restrict__ U, int rows, int cols, long ld) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= cols) return;
+  double best = -1.0, bval = 0.0;
+  int bidx = 0x7fffffff;
+  for (int r = lane; r < rows; r += 64) {
+    double v = U[(long)r * ld + c];
+    double a = fabs(v);
+    if (a > best) { best = a; bval = v; bidx = r; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    double ob = __shfl_xor(best, o, 64);
+    double ov = __shfl_xor(bval, o, 64);
+    int oi = __shfl_xor(bidx, o, 64);
+    if (ob > best || (ob == best && oi < bidx)) { best = ob; bval = ov; bidx = oi; }
+  }
+  if (bval < 0.0) {
+    for (int r = lane; r < rows; r += 64) U[(long)r * ld + c] = -U[(long)r * ld + c];
+  }
+}
+
+SRML_API int srml_sign_flip_f64(double* U, int rows, int cols, long ld, hipStream_t stream) {
+  if (cols <= 0) return 0;
+  hipLaunchKernelGGL(sign_flip_kernel, dim3(ceil_div(cols, 4)), dim3(256), 0, stream, U, rows, cols, ld);
+  return srml_status();
+}

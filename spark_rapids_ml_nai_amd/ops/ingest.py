@@ -1,0 +1,90 @@
+"""Host -> device ingest with pinned staging and overlapped H2D.
+
+The reference converts each Arrow batch through a per-row Python list and (optionally) copies
+to the GPU (``core.py:724-748``) — the dominant host cost at 1M x 3000. Here the numpy view of
+the Arrow values buffer is copied into a small ring of pinned staging buffers and DMA'd to a
+pre-allocated device tensor with ``non_blocking`` copies: while chunk i is in flight over PCIe
+the host fills chunk i+1 (two buffers, event-guarded reuse). Small arrays take the direct path.
+"""
+from __future__ import annotations
+
+from typing import Any, Optional
+
+import numpy as np
+import torch
+
+_CHUNK_BYTES = 64 << 20
+_DIRECT_BYTES = 8 << 20
+_staging: dict = {}
+
+
+def _pinned(device: torch.device, slot: int, nbytes: int) -> torch.Tensor:
+    key = (device.index, slot)
+    buf = _staging.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(nbytes, _CHUNK_BYTES), dtype=torch.uint8, pin_memory=True)
+        _staging[key] = buf
+    return buf
+
+
+def _dense_to_device(a: np.ndarray, device: torch.device, dtype: Optional[torch.dtype]) -> torch.Tensor:
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if dtype is not None and t.dtype != dtype and not t.dtype.is_floating_point:
+        t = t.to(dtype)
+    elif dtype is not None and t.dtype != dtype:
+        t = t.to(dtype)
+    if device.type != "cuda":
+        return t.to(device)
+    if t.is_pinned():
+        # Arrow batch already in page-locked memory: one DMA straight into HBM
+        return t.to(device, non_blocking=True)
+    nbytes = t.numel() * t.element_size()
+    if nbytes <= _DIRECT_BYTES or t.dim() == 0:
+        return t.to(device, non_blocking=False)
+    out = torch.empty(t.shape, dtype=t.dtype, device=device)
+    flat_src = t.reshape(-1).view(torch.uint8)
+    flat_dst = out.reshape(-1).view(torch.uint8)
+    stream = torch.cuda.current_stream(device)
+    events = [None, None]
+    off = 0
+    slot = 0
+    while off < nbytes:
+        n = min(_CHUNK_BYTES, nbytes - off)
+        if events[slot] is not None:
+            events[slot].synchronize()
+        buf = _pinned(device, slot, _CHUNK_BYTES)
+        buf[:n].copy_(flat_src[off: off + n])
+        flat_dst[off: off + n].copy_(buf[:n], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        events[slot] = ev
+        off += n
+        slot ^= 1
+    for ev in events:
+        if ev is not None:
+            ev.synchronize()
+    return out
+
+
+def host_to_device(X: Any, device: torch.device, dtype: Optional[torch.dtype] = None) -> Any:
+    """numpy dense / scipy CSR / torch tensor -> device tensor (or ``core.base.CSR``)."""
+    import scipy.sparse as sp
+
+    if isinstance(X, torch.Tensor):
+        X = X.to(device)
+        return X.to(dtype) if dtype is not None and X.is_floating_point() else X
+    if sp.issparse(X):
+        from ..core.base import CSR
+
+        csr = sp.csr_matrix(X)
+        vals = csr.data
+        return CSR(
+            indptr=_dense_to_device(csr.indptr.astype(np.int64), device, None),
+            indices=_dense_to_device(csr.indices.astype(np.int32), device, None),
+            data=_dense_to_device(vals, device, dtype),
+            shape=(int(csr.shape[0]), int(csr.shape[1])),
+        )
+    a = np.asarray(X)
+    if a.dtype.kind in "iub" and dtype is not None and dtype.is_floating_point:
+        a = a.astype(np.float32 if dtype == torch.float32 else np.float64)
+    return _dense_to_device(a, device, dtype if a.dtype.kind == "f" else None)

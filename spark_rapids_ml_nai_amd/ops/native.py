@@ -1,0 +1,100 @@
+"""ctypes binding of ``libsrml_ops.so`` (the hand-written gfx950 kernels).
+
+Every kernel entry point is ``extern "C"`` and takes raw device pointers plus the HIP stream
+torch is currently using, so launches are ordered with torch's own work and can be captured
+into a HIP graph by ``torch.cuda.graph``. A non-zero return is a launch error and raises.
+
+Policy: when a tensor lives on a GPU the native kernel MUST run — if the library is missing
+or fails to load the op raises (no silent fallback to a PyTorch implementation). CPU tensors
+(GPU-less CI) use the reference PyTorch implementations in ``ops/__init__.py``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Any, Dict, Optional, Tuple
+
+import torch
+
+from . import build as _build
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_L = ctypes.c_long
+_D = ctypes.c_double
+_F = ctypes.c_float
+
+# name -> argtypes (restype is always int status)
+SIGNATURES: Dict[str, Tuple[Any, ...]] = {
+    "srml_col_moments_f32": (_P, _L, _I, _L, _P, _P, _P),
+    "srml_col_moments_f64": (_P, _L, _I, _L, _P, _P, _P),
+    "srml_standardize_f32": (_P, _L, _I, _L, _P, _P, _P),
+    "srml_gram_f32": (_P, _L, _I, _L, _P, _P, _P),
+    "srml_mirror_upper_f64": (_P, _I, _P),
+    "srml_xw_f32": (_P, _L, _I, _L, _P, _I, _P, _P, _L, _P),
+    "srml_dgemm": (_I, _I, _I, _I, _I, _D, _P, _L, _P, _L, _D, _P, _L, _P),
+    "srml_sign_flip_f64": (_P, _I, _I, _L, _P),
+}
+
+_lock = threading.Lock()
+_lib: Optional[ctypes.CDLL] = None
+_load_error: Optional[str] = None
+
+
+def _load() -> ctypes.CDLL:
+    global _lib, _load_error
+    with _lock:
+        if _lib is not None:
+            return _lib
+        path = _build.lib_path()
+        if (not os.path.exists(path) or _build.needs_build()) and os.environ.get("SRML_NO_AUTOBUILD", "0") != "1":
+            try:
+                _build.build()
+            except Exception as e:  # noqa: BLE001
+                if not os.path.exists(path):
+                    _load_error = "build failed: %s" % e
+                    raise RuntimeError(_load_error)
+        # make sure torch's HIP runtime is the one our library binds to
+        import torch.cuda  # noqa: F401
+
+        lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
+        for name, argt in SIGNATURES.items():
+            try:
+                fn = getattr(lib, name)
+            except AttributeError:
+                continue
+            fn.argtypes = list(argt)
+            fn.restype = ctypes.c_int
+        _lib = lib
+        return lib
+
+
+def lib() -> ctypes.CDLL:
+    """The loaded native library; raises RuntimeError if it cannot be built/loaded."""
+    return _load()
+
+
+def available() -> bool:
+    try:
+        _load()
+        return True
+    except Exception:  # noqa: BLE001
+        return False
+
+
+def ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def call(name: str, *args: Any) -> None:
+    fn = getattr(lib(), name)
+    rc = fn(*args)
+    if rc != 0:
+        raise RuntimeError("%s launch failed with HIP status %d" % (name, rc))

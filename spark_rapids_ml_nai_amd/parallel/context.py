@@ -1,0 +1,132 @@
+"""Per-rank worker context: rank, world size, pinned device and communicator.
+
+Equivalent of the reference's ``_CumlCommon._set_gpu_device`` + ``CumlContext``
+(``core.py:343-388``, ``common/cuml_context.py:35-193``) and ``PartitionDescriptor``
+(``utils.py:173-210``), re-designed for one process per MI355X:
+
+* device pinning: ``cuda:<local_rank>`` (HIP device) from ``LOCAL_RANK`` / the Spark task's
+  ``gpu`` resource / ``HIP_VISIBLE_DEVICES``; CPU when no GPU is visible (tests).
+* communicator: ``torch.distributed`` group on RCCL (GPU) or gloo (CPU); bootstrap via
+  env rendezvous (torchrun / LocalBarrierRunner) or Spark barrier ``allGather`` of the rank-0
+  TCPStore address (see ``parallel/spark.py``).
+* ``PartitionDescriptor``: global ``m``, ``n`` and per-rank row counts obtained with ONE
+  device all-gather, not a JSON list through the Spark driver.
+"""
+from __future__ import annotations
+
+import os
+import threading
+from dataclasses import dataclass, field
+from typing import Any, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from .comm import Communicator
+
+_tls = threading.local()
+
+
+def gpu_available() -> bool:
+    if os.environ.get("SRML_FORCE_CPU", "0") == "1":
+        return False
+    try:
+        return torch.cuda.is_available() and torch.cuda.device_count() > 0
+    except Exception:  # noqa: BLE001
+        return False
+
+
+def local_device(local_rank: Optional[int] = None) -> torch.device:
+    """Device this rank computes on."""
+    if not gpu_available():
+        return torch.device("cpu")
+    n = torch.cuda.device_count()
+    if local_rank is None:
+        local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    return torch.device("cuda", local_rank % n)
+
+
+def spmd_active() -> bool:
+    """True when the caller already runs one process per GPU inside a torch.distributed world."""
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+def infer_num_workers() -> int:
+    if spmd_active():
+        return dist.get_world_size()
+    env = os.environ.get("SRML_NUM_WORKERS")
+    if env:
+        return int(env)
+    if gpu_available():
+        return torch.cuda.device_count()
+    return 1
+
+
+@dataclass
+class WorkerContext:
+    rank: int = 0
+    world_size: int = 1
+    device: torch.device = field(default_factory=lambda: torch.device("cpu"))
+    comm: Communicator = field(default_factory=Communicator)
+    partition_id: int = 0
+    timers: dict = field(default_factory=dict)
+
+    @property
+    def is_gpu(self) -> bool:
+        return self.device.type == "cuda"
+
+    def sync(self) -> None:
+        if self.is_gpu:
+            torch.cuda.synchronize(self.device)
+
+    @staticmethod
+    def single(device: Optional[torch.device] = None) -> "WorkerContext":
+        dev = device if device is not None else local_device()
+        return WorkerContext(0, 1, dev, Communicator(0, 1, dev))
+
+    @staticmethod
+    def from_process_group(device: Optional[torch.device] = None) -> "WorkerContext":
+        rank, size = dist.get_rank(), dist.get_world_size()
+        dev = device if device is not None else local_device()
+        if dev.type == "cuda":
+            torch.cuda.set_device(dev)
+        return WorkerContext(rank, size, dev, Communicator(rank, size, dev), partition_id=rank)
+
+
+def current_context() -> Optional[WorkerContext]:
+    return getattr(_tls, "ctx", None)
+
+
+class use_context:
+    def __init__(self, ctx: WorkerContext) -> None:
+        self.ctx = ctx
+        self.prev: Optional[WorkerContext] = None
+
+    def __enter__(self) -> WorkerContext:
+        self.prev = current_context()
+        _tls.ctx = self.ctx
+        return self.ctx
+
+    def __exit__(self, *exc: Any) -> None:
+        _tls.ctx = self.prev
+
+
+@dataclass
+class PartitionDescriptor:
+    """Global layout of the row-partitioned input (reference ``utils.py:173-210``)."""
+
+    m: int
+    n: int
+    rank: int
+    parts_rank_size: List[tuple]
+
+    @classmethod
+    def build(cls, ctx: WorkerContext, local_rows: int, n_cols: int) -> "PartitionDescriptor":
+        t = torch.tensor([local_rows, n_cols], dtype=torch.int64, device=ctx.device)
+        g = ctx.comm.allgather(t.view(1, 2)).view(-1, 2).cpu().tolist()
+        ns = {int(r[1]) for r in g if r[0] > 0}
+        if len(ns) > 1:
+            raise ValueError("ranks disagree on the number of columns: %s" % ns)
+        n = ns.pop() if ns else n_cols
+        parts = [(r, int(g[r][0])) for r in range(ctx.world_size)]
+        return cls(sum(p[1] for p in parts), n, ctx.rank, parts)

@@ -1,0 +1,78 @@
+"""Kernel numerics: every HIP kernel vs a plain PyTorch fp32/fp64 reference of the same op."""
+import numpy as np
+import pytest
+import torch
+
+from spark_rapids_ml_nai_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _rand(m, n, dev, seed=0, dtype=torch.float32, shift=0.0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(m, n, generator=g, dtype=torch.float64) + shift).to(dtype).to(dev)
+
+
+@pytest.mark.parametrize("m,n", [(1, 5), (1000, 3), (4097, 130), (20000, 257), (3000, 1000)])
+def test_col_moments(gpu_device, m, n):
+    X = _rand(m, n, gpu_device, shift=3.0)
+    s, q = ops.col_moments(X)
+    Xd = X.double().cpu()
+    torch.testing.assert_close(s.cpu(), Xd.sum(0), rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(q.cpu(), (Xd * Xd).sum(0), rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("m,n,center", [(100, 3, False), (1000, 128, True), (5000, 130, True), (777, 301, False),
+                                        (20000, 513, True)])
+def test_gram(gpu_device, m, n, center):
+    X = _rand(m, n, gpu_device, seed=1, shift=1.0)
+    mu = X.double().mean(0) if center else None
+    G = ops.gram(X, mu)
+    Xc = X.double().cpu() - (mu.cpu() if center else 0.0)
+    ref = Xc.T @ Xc
+    err = (G.cpu() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-6, err
+    assert torch.allclose(G, G.T)
+
+
+def test_gram_asymmetric_columns(gpu_device):
+    # asymmetric operand pattern: catches row/col swaps in the MFMA C-write
+    m, n = 64, 200
+    X = torch.zeros(m, n, dtype=torch.float32)
+    for r in range(m):
+        X[r, (r * 7) % n] = 1.0 + r
+        X[r, (r * 13 + 5) % n] = -2.0
+    G = ops.gram(X.to(gpu_device)).cpu()
+    ref = X.double().T @ X.double()
+    torch.testing.assert_close(G, ref)
+
+
+@pytest.mark.parametrize("m,n,k", [(1000, 3000, 3), (12345, 128, 1), (999, 37, 5), (4000, 256, 16), (300, 64, 32)])
+def test_xw(gpu_device, m, n, k):
+    X = _rand(m, n, gpu_device, seed=2)
+    W = _rand(n, k, gpu_device, seed=3)
+    b = _rand(1, k, gpu_device, seed=4).view(-1)
+    out = ops.xw(X, W, b).cpu().double()
+    ref = X.double().cpu() @ W.double().cpu() + b.double().cpu()
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("ta,tb", [(False, False), (True, False), (False, True), (True, True)])
+def test_dgemm(gpu_device, ta, tb):
+    M, N, K = 130, 67, 301
+    A = _rand(K if ta else M, M if ta else K, gpu_device, seed=5, dtype=torch.float64)
+    B = _rand(N if tb else K, K if tb else N, gpu_device, seed=6, dtype=torch.float64)
+    C = _rand(M, N, gpu_device, seed=7, dtype=torch.float64)
+    ref = 0.5 * ((A.T if ta else A) @ (B.T if tb else B)) + 2.0 * C
+    out = ops.dgemm(A, B, ta, tb, alpha=0.5, beta=2.0, out=C.clone())
+    torch.testing.assert_close(out, ref, rtol=1e-12, atol=1e-10)
+
+
+def test_sign_flip(gpu_device):
+    U = _rand(500, 7, gpu_device, seed=8, dtype=torch.float64)
+    ref = U.clone().cpu()
+    ops.sign_flip(ref)  # CPU reference path
+    out = ops.sign_flip(U.clone()).cpu()
+    torch.testing.assert_close(out, ref)
+    idx = out.abs().argmax(0)
+    assert torch.all(out[idx, torch.arange(7)] > 0)
