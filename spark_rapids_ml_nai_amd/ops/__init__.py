@@ -10,7 +10,8 @@ import torch
 
 from . import native
 
-__all__ = ["col_moments", "gram", "xw", "dgemm", "sign_flip", "is_native"]
+__all__ = ["col_moments", "gram", "xw", "dgemm", "sign_flip", "is_native", "xtv", "row_sqnorm",
+           "logreg_binary_loss_grad", "nearest_centroid", "cluster_sums"]
 
 
 def is_native(t: torch.Tensor) -> bool:
@@ -129,3 +130,118 @@ def sign_flip(U: torch.Tensor) -> torch.Tensor:
         return U
     native.call("srml_sign_flip_f64", U.data_ptr(), rows, cols, U.stride(0), native.stream(U.device))
     return U
+
+
+# ------------------------------------------------------------------------------------------
+# GLM / KMeans primitives
+# ------------------------------------------------------------------------------------------
+def xtv(X: torch.Tensor, V: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out (n, k) fp64 += X^T V for X (m, n) fp32 and V (m, k) (k <= 4 native; wider -> chunks)."""
+    m, n = X.shape
+    V2 = V.reshape(m, -1)
+    k = V2.shape[1]
+    if out is None:
+        out = torch.zeros((n, k), dtype=torch.float64, device=X.device)
+    if not X.is_cuda:
+        out += X.double().T @ V2.double()
+        return out
+    if X.dtype != torch.float32:
+        out += (X.T @ V2.to(X.dtype)).double()
+        return out
+    X = _c(X)
+    for c0 in range(0, k, 4):
+        kk = min(4, k - c0)
+        Vc = _c(V2[:, c0: c0 + kk].to(torch.float32))
+        tmp = torch.zeros((n, kk), dtype=torch.float64, device=X.device)
+        native.call("srml_xtv_f32", X.data_ptr(), m, n, X.stride(0), Vc.data_ptr(), kk, Vc.stride(0), tmp.data_ptr(),
+                    native.stream(X.device))
+        out[:, c0: c0 + kk] += tmp
+    return out
+
+
+def row_sqnorm(X: torch.Tensor) -> torch.Tensor:
+    m, n = X.shape
+    if not X.is_cuda or X.dtype != torch.float32:
+        return (X.float() * X.float()).sum(1)
+    X = _c(X)
+    out = torch.empty(m, dtype=torch.float32, device=X.device)
+    native.call("srml_row_sqnorm_f32", X.data_ptr(), m, n, X.stride(0), out.data_ptr(), native.stream(X.device))
+    return out
+
+
+def logreg_binary_loss_grad(X: torch.Tensor, y: torch.Tensor, w: torch.Tensor, b: float) -> torch.Tensor:
+    """fp64 [grad_w (n), grad_b, loss_sum] of sum_r softplus(z_r) - y_r z_r, z = X w + b (one pass)."""
+    m, n = X.shape
+    if not X.is_cuda or X.dtype != torch.float32 or n > 4096:
+        Xd = X.double()
+        z = Xd @ w.double().to(X.device) + b
+        yd = y.double()
+        p = torch.sigmoid(z)
+        r = p - yd
+        loss = torch.nn.functional.softplus(z).sum() - (yd * z).sum()
+        return torch.cat([Xd.T @ r, r.sum().view(1), loss.view(1)])
+    X = _c(X)
+    out = torch.zeros(n + 2, dtype=torch.float64, device=X.device)
+    wf = _c(w.to(device=X.device, dtype=torch.float64))
+    yf = _c(y.to(torch.float32))
+    native.call("srml_logreg_binary_f32", X.data_ptr(), m, n, X.stride(0), yf.data_ptr(), wf.data_ptr(), float(b),
+                out.data_ptr(), native.stream(X.device))
+    return out
+
+
+def nearest_centroid(X: torch.Tensor, C: torch.Tensor, xnorm: Optional[torch.Tensor] = None,
+                     cnorm: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(labels int32 [m], squared distance fp32 [m]) of each row's nearest centroid (fused, no m x k matrix)."""
+    m, n = X.shape
+    k = C.shape[0]
+    if cnorm is None:
+        cnorm = (C.float() * C.float()).sum(1)
+    if not X.is_cuda or X.dtype != torch.float32:
+        labels = torch.empty(m, dtype=torch.int32, device=X.device)
+        dist = torch.empty(m, dtype=torch.float32, device=X.device)
+        bs = max(1, (1 << 24) // max(k, 1))
+        for s in range(0, m, bs):
+            xb = X[s: s + bs].float()
+            d = cnorm.view(1, -1) - 2.0 * (xb @ C.float().T)
+            v, i = d.min(1)
+            xn = (xb * xb).sum(1) if xnorm is None else xnorm[s: s + bs]
+            labels[s: s + bs] = i.int()
+            dist[s: s + bs] = (v + xn).clamp_min(0)
+        return labels, dist
+    X = _c(X)
+    C = _c(C.to(torch.float32))
+    cn = _c(cnorm.to(torch.float32))
+    best = torch.full((m,), -1, dtype=torch.int64, device=X.device)  # 0xFFFF... as uint64
+    st = native.stream(X.device)
+    native.call("srml_nearest_centroid_f32", X.data_ptr(), m, n, X.stride(0), C.data_ptr(), k, C.stride(0),
+                cn.data_ptr(), best.data_ptr(), st)
+    if xnorm is None:
+        xnorm = row_sqnorm(X)
+    labels = torch.empty(m, dtype=torch.int32, device=X.device)
+    dist = torch.empty(m, dtype=torch.float32, device=X.device)
+    native.call("srml_nn_finalize", best.data_ptr(), m, xnorm.data_ptr(), labels.data_ptr(), dist.data_ptr(), st)
+    return labels, dist
+
+
+def cluster_sums(X: torch.Tensor, labels: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(sums fp64 [k, n], counts int64 [k]) of rows grouped by label."""
+    m, n = X.shape
+    if not X.is_cuda or X.dtype != torch.float32:
+        sums = torch.zeros((k, n), dtype=torch.float64, device=X.device)
+        sums.index_add_(0, labels.long(), X.double())
+        counts = torch.bincount(labels.long(), minlength=k)
+        return sums, counts
+    X = _c(X)
+    lab = _c(labels.to(torch.int32))
+    counts = torch.zeros(k, dtype=torch.int32, device=X.device)
+    st = native.stream(X.device)
+    if k * n * 4 + k * 4 <= 64 * 1024:
+        sums = torch.zeros((k, n), dtype=torch.float64, device=X.device)
+        native.call("srml_kmeans_accumulate_f32", X.data_ptr(), m, n, X.stride(0), lab.data_ptr(), k, sums.data_ptr(),
+                    None, counts.data_ptr(), st)
+    else:
+        s32 = torch.zeros((k, n), dtype=torch.float32, device=X.device)
+        native.call("srml_kmeans_accumulate_f32", X.data_ptr(), m, n, X.stride(0), lab.data_ptr(), k, None,
+                    s32.data_ptr(), counts.data_ptr(), st)
+        sums = s32.double()
+    return sums, counts.long()

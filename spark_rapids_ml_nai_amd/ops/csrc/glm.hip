@@ -1,0 +1,337 @@
+// GLM primitives: transposed skinny products and the fused logistic loss/gradient.
+//
+//  * srml_xtv_f32    — out (n x k, fp64) += X^T V  with V (m x k), k <= 4. One streaming pass over
+//                      X: lanes own 4 adjacent columns (16-B loads), V rows are broadcast, fp32
+//                      partial chains folded to fp64 every 256 rows, one fp64 atomic per column
+//                      per block. Normal-equation right-hand side X^T y (LinearRegression),
+//                      multinomial LogReg gradient X^T (P - Y).
+//  * srml_row_sqnorm_f32 — ||x_r||^2 per row (KMeans inertia, kNN/DBSCAN distances).
+//  * srml_logreg_binary_f32 — ONE pass over X per L-BFGS function evaluation:
+//        z_r = x_r · w + b ;  loss += softplus(z_r) - y_r z_r ;  g += (sigmoid(z_r) - y_r) x_r
+//    wave-per-row: the row (up to 256*V floats) is held in registers while its dot product is
+//    reduced with wave64 shuffles, then reused for the gradient update, so X is read exactly
+//    once (the reference's cuML QN path reads it twice: forward GEMV then X^T residual).
+//    w lives in LDS, each wave keeps a private gradient accumulator in registers, waves fold
+//    into LDS and blocks fold into the fp64 output with atomics.
+#include "common.h"
+#include <stdlib.h>
+
+// ------------------------------------------------------------------------------------------
+template <int K>
+__global__ __launch_bounds__(256) void xtv_kernel(const float* __restrict__ X, long m, int n, long ld,
+                                                  const float* __restrict__ V, long ldv, double* __restrict__ out,
+                                                  long rows_per_block) {
+  const int c0 = (blockIdx.x * 256 + threadIdx.x) * 4;
+  const long r0 = (long)blockIdx.y * rows_per_block;
+  const long r1 = min(m, r0 + rows_per_block);
+  if (c0 >= n) return;
+  double acc[K][4];
+  float facc[K][4];
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { acc[k][j] = 0.0; facc[k][j] = 0.f; }
+  const bool full = (c0 + 3 < n) && ((ld & 3) == 0);
+  int cnt = 0;
+  for (long r = r0; r < r1; ++r) {
+    floatx4 x;
+    if (full) {
+      x = *reinterpret_cast<const floatx4*>(X + r * ld + c0);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) x[j] = (c0 + j < n) ? X[r * ld + c0 + j] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const float v = V[r * ldv + k];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) facc[k][j] = fmaf(x[j], v, facc[k][j]);
+    }
+    if (++cnt == 256) {
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { acc[k][j] += facc[k][j]; facc[k][j] = 0.f; }
+      cnt = 0;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc[k][j] += facc[k][j];
+      if (c0 + j < n) atomicAdd(&out[(long)(c0 + j) * K + k], acc[k][j]);
+    }
+}
+
+SRML_API int srml_xtv_f32(const float* X, long m, int n, long ld, const float* V, int k, long ldv, double* out,
+                          hipStream_t stream) {
+  if (m <= 0 || n <= 0) return 0;
+  unsigned gx = ceil_div(n, 1024);
+  long gy = (2048 + gx - 1) / gx;
+  long rpb = (m + gy - 1) / gy;
+  if (rpb < 64) rpb = 64;
+  gy = (m + rpb - 1) / rpb;
+  dim3 grid(gx, (unsigned)gy);
+  switch (k) {
+    case 1: hipLaunchKernelGGL(xtv_kernel<1>, grid, dim3(256), 0, stream, X, m, n, ld, V, ldv, out, rpb); break;
+    case 2: hipLaunchKernelGGL(xtv_kernel<2>, grid, dim3(256), 0, stream, X, m, n, ld, V, ldv, out, rpb); break;
+    case 3: hipLaunchKernelGGL(xtv_kernel<3>, grid, dim3(256), 0, stream, X, m, n, ld, V, ldv, out, rpb); break;
+    case 4: hipLaunchKernelGGL(xtv_kernel<4>, grid, dim3(256), 0, stream, X, m, n, ld, V, ldv, out, rpb); break;
+    default: return -1;
+  }
+  return srml_status();
+}
+
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void row_sqnorm_kernel(const float* __restrict__ X, long m, int n, long ld,
+                                                         float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const long nw = (long)gridDim.x * 4;
+  const bool vec = ((ld & 3) == 0) && ((n & 3) == 0);
+  for (long r = wave; r < m; r += nw) {
+    const float* row = X + r * ld;
+    float s = 0.f;
+    if (vec) {
+      for (int d = lane * 4; d < n; d += 256) {
+        floatx4 v = *reinterpret_cast<const floatx4*>(row + d);
+        s = fmaf(v[0], v[0], fmaf(v[1], v[1], fmaf(v[2], v[2], fmaf(v[3], v[3], s))));
+      }
+    } else {
+      for (int d = lane; d < n; d += 64) s = fmaf(row[d], row[d], s);
+    }
+    s = wave_sum(s);
+    if (lane == 0) out[r] = s;
+  }
+}
+
+SRML_API int srml_row_sqnorm_f32(const float* X, long m, int n, long ld, float* out, hipStream_t stream) {
+  if (m <= 0) return 0;
+  long blocks = (m + 3) / 4;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(row_sqnorm_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, X, m, n, ld, out);
+  return srml_status();
+}
+
+// ------------------------------------------------------------------------------------------
+// fused binary logistic loss + gradient
+// out layout (fp64): [0..n) gradient wrt w, [n] gradient wrt b, [n+1] loss sum
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ float softplus_f(float z) {
+  // log(1 + exp(z)) without overflow
+  return z > 0.f ? z + log1pf(__expf(-z)) : log1pf(__expf(z));
+}
+
+template <int V, bool REREAD>
+__global__ __launch_bounds__(256) void logreg_binary_kernel(const float* __restrict__ X, long m, int n, long ld,
+                                                            const float* __restrict__ y, const double* __restrict__ w,
+                                                            double b, double* __restrict__ out, long rows_per_block) {
+  // w is kept in fp64 (LDS) and margins / losses are evaluated in fp64 so that the objective the
+  // quasi-Newton line search sees is smooth to ~1e-15; X stays fp32 and the kernel stays
+  // HBM-bound (fp64 FMA rate is far above the 1 FMA per 4 streamed bytes needed here).
+  extern __shared__ __attribute__((aligned(16))) double ldsd[];  // w[256*V] (fp64) then gsum[256*V] (fp32)
+  double* ws = ldsd;
+  float* gs = reinterpret_cast<float*>(ldsd + 256 * V);
+  const int NV = 256 * V;
+  for (int i = threadIdx.x; i < NV; i += 256) {
+    ws[i] = (i < n) ? w[i] : 0.0;
+    gs[i] = 0.f;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const long r0 = (long)blockIdx.x * rows_per_block;
+  const long r1 = min(m, r0 + rows_per_block);
+
+  floatx4 g[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) g[v] = floatx4{0.f, 0.f, 0.f, 0.f};
+  double gb = 0.0, loss = 0.0;
+  const bool vec = ((ld & 3) == 0);
+  for (long r = r0 + wid; r < r1; r += 4) {
+    const float* row = X + r * ld;
+    floatx4 x[REREAD ? 1 : V];
+    double dot = 0.0;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const int c = (v * 64 + lane) * 4;
+      floatx4& xv = x[REREAD ? 0 : v];
+      if (vec && c + 3 < n) {
+        xv = *reinterpret_cast<const floatx4*>(row + c);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) xv[q] = (c + q < n) ? row[c + q] : 0.f;
+      }
+      const double2 w01 = *reinterpret_cast<const double2*>(&ws[c]);
+      const double2 w23 = *reinterpret_cast<const double2*>(&ws[c + 2]);
+      dot = fma((double)xv[0], w01.x, fma((double)xv[1], w01.y, fma((double)xv[2], w23.x,
+                fma((double)xv[3], w23.y, dot))));
+    }
+    dot = wave_sum(dot);
+    const double z = dot + b;
+    const double yr = (double)y[r];
+    const double p = 1.0 / (1.0 + exp(-z));
+    const double res = p - yr;
+    if (lane == 0) {
+      loss += (z > 0.0 ? z + log1p(exp(-z)) : log1p(exp(z))) - yr * z;
+      gb += res;
+    }
+    const float rf = (float)res;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      floatx4 xv;
+      if (REREAD) {  // second touch of the row hits L1/L2; HBM traffic is unchanged
+        const int c = (v * 64 + lane) * 4;
+        if (vec && c + 3 < n) {
+          xv = *reinterpret_cast<const floatx4*>(row + c);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) xv[q] = (c + q < n) ? row[c + q] : 0.f;
+        }
+      } else {
+        xv = x[v];
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) g[v][q] = fmaf(rf, xv[q], g[v][q]);
+    }
+  }
+  // fold the 4 waves' gradients in LDS, then one fp64 atomic per column per block
+#pragma unroll
+  for (int v = 0; v < V; ++v)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) atomicAdd(&gs[(v * 64 + lane) * 4 + q], g[v][q]);
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += 256) atomicAdd(&out[i], (double)gs[i]);
+  if (lane == 0) {
+    atomicAdd(&out[n], gb);
+    atomicAdd(&out[n + 1], loss);
+  }
+}
+
+
+// Column-split variant for 1024 < n <= 4096: each of the 4 waves owns a 256*V-column slice of
+// every row (x and its gradient slice stay in registers), the block processes R rows per step;
+// per-row partial margins are exchanged through LDS (double-buffered, one barrier per step).
+template <int V, int R>
+__global__ __launch_bounds__(256, 2) void logreg_binary_split_kernel(const float* __restrict__ X, long m, int n,
+                                                                     long ld, const float* __restrict__ y,
+                                                                     const double* __restrict__ w, double b,
+                                                                     double* __restrict__ out, long rows_per_block) {
+  __shared__ double part[2][R][4];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int cbase = wid * 256 * V;
+  double wreg[V][4];
+#pragma unroll
+  for (int v = 0; v < V; ++v)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = cbase + (v * 64 + lane) * 4 + q;
+      wreg[v][q] = c < n ? w[c] : 0.0;
+    }
+  floatx4 g[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) g[v] = floatx4{0.f, 0.f, 0.f, 0.f};
+  double gb = 0.0, loss = 0.0;
+  const long r0 = (long)blockIdx.x * rows_per_block;
+  const long r1 = min(m, r0 + rows_per_block);
+  const bool vec = ((ld & 3) == 0);
+  int buf = 0;
+  for (long rb = r0; rb < r1; rb += R) {
+    floatx4 x[R][V];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const long r = rb + i;
+      double dot = 0.0;
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const int c = cbase + (v * 64 + lane) * 4;
+        floatx4 xv = {0.f, 0.f, 0.f, 0.f};
+        if (r < r1) {
+          const float* row = X + r * ld;
+          if (vec && c + 3 < n) {
+            xv = *reinterpret_cast<const floatx4*>(row + c);
+          } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) xv[q] = (c + q < n) ? row[c + q] : 0.f;
+          }
+        }
+        x[i][v] = xv;
+        dot = fma((double)xv[0], wreg[v][0], fma((double)xv[1], wreg[v][1],
+              fma((double)xv[2], wreg[v][2], fma((double)xv[3], wreg[v][3], dot))));
+      }
+      dot = wave_sum(dot);
+      if (lane == 0) part[buf][i][wid] = dot;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const long r = rb + i;
+      if (r >= r1) break;
+      const double z = part[buf][i][0] + part[buf][i][1] + part[buf][i][2] + part[buf][i][3] + b;
+      const double yr = (double)y[r];
+      const double p = 1.0 / (1.0 + exp(-z));
+      const double res = p - yr;
+      if (wid == 0 && lane == 0) {
+        loss += (z > 0.0 ? z + log1p(exp(-z)) : log1p(exp(z))) - yr * z;
+        gb += res;
+      }
+      const float rf = (float)res;
+#pragma unroll
+      for (int v = 0; v < V; ++v)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) g[v][q] = fmaf(rf, x[i][v][q], g[v][q]);
+    }
+    buf ^= 1;
+  }
+#pragma unroll
+  for (int v = 0; v < V; ++v)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = cbase + (v * 64 + lane) * 4 + q;
+      if (c < n) atomicAdd(&out[c], (double)g[v][q]);
+    }
+  if (wid == 0 && lane == 0) {
+    atomicAdd(&out[n], gb);
+    atomicAdd(&out[n + 1], loss);
+  }
+}
+
+SRML_API int srml_logreg_binary_f32(const float* X, long m, int n, long ld, const float* y, const double* w, double b,
+                                    double* out, hipStream_t stream) {
+  if (m <= 0) return 0;
+  long blocks = 2048;
+  long rpb = (m + blocks - 1) / blocks;
+  if (rpb < 16) rpb = 16;
+  blocks = (m + rpb - 1) / rpb;
+  int V = (n + 255) / 256;
+  size_t lds = 256 * (size_t)(V <= 1 ? 1 : V <= 2 ? 2 : V <= 4 ? 4 : V <= 8 ? 8 : V <= 12 ? 12 : 16) * (sizeof(double) + sizeof(float));
+  dim3 grid((unsigned)blocks), blk(256);
+  static const int split = getenv("SRML_LOGREG_SPLIT") ? atoi(getenv("SRML_LOGREG_SPLIT")) : 1;
+  if (split && n > 1024 && n <= 4096) {
+    constexpr int R = 4;
+    const int VS = (n + 1023) / 1024;
+    if (VS == 1) hipLaunchKernelGGL((logreg_binary_split_kernel<1, R>), grid, blk, 0, stream, X, m, n, ld, y, w, b, out, rpb);
+    else if (VS == 2) hipLaunchKernelGGL((logreg_binary_split_kernel<2, R>), grid, blk, 0, stream, X, m, n, ld, y, w, b, out, rpb);
+    else if (VS == 3) hipLaunchKernelGGL((logreg_binary_split_kernel<3, R>), grid, blk, 0, stream, X, m, n, ld, y, w, b, out, rpb);
+    else hipLaunchKernelGGL((logreg_binary_split_kernel<4, R>), grid, blk, 0, stream, X, m, n, ld, y, w, b, out, rpb);
+    return srml_status();
+  }
+  const int reread = 0;
+#define SRML_LR_LAUNCH(VV)                                                                                       \
+  do {                                                                                                           \
+    if (reread)                                                                                                  \
+      hipLaunchKernelGGL((logreg_binary_kernel<VV, true>), grid, blk, lds, stream, X, m, n, ld, y, w, b, out, rpb);  \
+    else                                                                                                         \
+      hipLaunchKernelGGL((logreg_binary_kernel<VV, false>), grid, blk, lds, stream, X, m, n, ld, y, w, b, out, rpb); \
+  } while (0)
+  if (V <= 1) SRML_LR_LAUNCH(1);
+  else if (V <= 2) SRML_LR_LAUNCH(2);
+  else if (V <= 4) SRML_LR_LAUNCH(4);
+  else if (V <= 8) SRML_LR_LAUNCH(8);
+  else if (V <= 12) SRML_LR_LAUNCH(12);
+  else if (V <= 16) SRML_LR_LAUNCH(16);
+  else return -2;  // n > 4096: caller uses the two-pass GEMV path
+  return srml_status();
+}

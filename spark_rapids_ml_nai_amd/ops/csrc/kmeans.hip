@@ -1,0 +1,271 @@
+// KMeans (and nearest-centroid) kernels.
+//
+// srml_nearest_centroid_f32: fused distance GEMM + arg-min. For every row x and centroid c the
+//   MFMA tile computes x·c (exact f32 `v_mfma_f32_32x32x2_f32`); the epilogue turns it into the
+//   partial squared distance ||c||^2 - 2 x·c and reduces the arg-min over the tile's columns with
+//   wave64 shuffles; per-row results from different centroid tiles are merged with ONE 64-bit
+//   atomicMin on a packed (orderable-dist << 32 | index) key. The m x k distance matrix is never
+//   materialised (reference: cuML KMeansMG / RAFT fusedL2NN).
+//   Grid: (row tiles) x (centroid tiles), centroid tile fastest and XCD-remapped, so the blocks
+//   that share one X row tile run on the same XCD and read it from that L2 (HBM traffic for X
+//   ~1x instead of k/BN x). Two tile shapes: 128x128 (large k) and 256x32 (small k, e.g. the
+//   k=20 north-star config, where a 128-wide centroid tile would idle 84% of the MFMAs).
+// srml_nn_finalize: unpack keys -> int32 labels and full squared distances (+||x||^2, >= 0).
+// srml_kmeans_accumulate_f32: per-cluster sums / counts for the Lloyd update.
+//   small k*n: block-private sums in LDS (ds_add_f32), flushed with fp64 global atomics;
+//   large k*n: wave-per-row fp32 global atomics, 256 contiguous bytes per atomic instruction
+//   (the full-rate atomic shape on MI355X).
+#include "common.h"
+
+namespace {
+constexpr int BK = 32;
+constexpr int PADK = BK + 1;
+
+__device__ __forceinline__ unsigned orderable(float f) {
+  unsigned u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float unorderable(unsigned u) {
+  return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+
+template <int ROWS, bool VEC>
+__device__ __forceinline__ void stage_tile(const float* __restrict__ A, long lda, long nrows_total, int ncols,
+                                           long row0, int k0, float (*dst)[PADK]) {
+  // ROWS x 32 tile, row-major source; thread t loads float4 (row t/8 + 32p, cols (t%8)*4)
+  const int t = threadIdx.x;
+  constexpr int PASSES = (ROWS * 8 + 255) / 256;
+#pragma unroll
+  for (int p = 0; p < PASSES; ++p) {
+    const int idx = t + 256 * p;
+    if (idx < ROWS * 8) {
+      const int rr = idx >> 3;
+      const int c4 = (idx & 7) * 4;
+      const long r = row0 + rr;
+      floatx4 v = {0.f, 0.f, 0.f, 0.f};
+      if (r < nrows_total) {
+        const float* src = A + r * lda + k0 + c4;
+        if (VEC && k0 + c4 + 3 < ncols) {
+          v = *reinterpret_cast<const floatx4*>(src);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = (k0 + c4 + q < ncols) ? src[q] : 0.f;
+        }
+      }
+      dst[rr][c4 + 0] = v[0];
+      dst[rr][c4 + 1] = v[1];
+      dst[rr][c4 + 2] = v[2];
+      dst[rr][c4 + 3] = v[3];
+    }
+  }
+}
+
+// BM x BN block tile, WM x WN waves (WM*WN = 4), each wave MT x NT tiles of 32x32
+template <int BM, int BN, int WM, int MT, int NT, bool VEC>
+__global__ __launch_bounds__(256, 2) void nearest_centroid_kernel(const float* __restrict__ X, long m, int n, long ldx,
+                                                                  const float* __restrict__ C, int k, long ldc,
+                                                                  const float* __restrict__ cnorm,
+                                                                  unsigned long long* __restrict__ best,
+                                                                  int n_ctiles) {
+  constexpr int WN = 4 / WM;
+  __shared__ float Xs[2][BM][PADK];
+  __shared__ float Cs[2][BN][PADK];
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const long rtile = bid / n_ctiles;
+  const int ctile = bid % n_ctiles;
+  const long row0 = rtile * BM;
+  const int col0 = ctile * BN;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int li = lane & 31, lk = lane >> 5;
+
+  floatx16 acc[MT][NT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  const int nk = (n + BK - 1) / BK;
+  stage_tile<BM, VEC>(X, ldx, m, n, row0, 0, Xs[0]);
+  stage_tile<BN, VEC>(C, ldc, k, n, col0, 0, Cs[0]);
+  __syncthreads();
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) {
+      stage_tile<BM, VEC>(X, ldx, m, n, row0, (kt + 1) * BK, Xs[cur ^ 1]);
+      stage_tile<BN, VEC>(C, ldc, k, n, col0, (kt + 1) * BK, Cs[cur ^ 1]);
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK / 2; ++kk) {
+      const int kx = 2 * kk + lk;
+      float a[MT], b[NT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) a[mt] = Xs[cur][wm * MT * 32 + mt * 32 + li][kx];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) b[nt] = Cs[cur][wn * NT * 32 + nt * 32 + li][kx];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // epilogue: per-row arg-min over this wave's columns, then one packed atomicMin per row
+  float cn[NT];
+  int cj[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    cj[nt] = col0 + wn * NT * 32 + nt * 32 + li;
+    cn[nt] = (cj[nt] < k) ? cnorm[cj[nt]] : 0.f;
+  }
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float bv = __builtin_huge_valf();
+      int bi = 0x7fffffff;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        if (cj[nt] < k) {
+          const float d = fmaf(-2.f, acc[mt][nt][r], cn[nt]);
+          if (d < bv) { bv = d; bi = cj[nt]; }
+        }
+      }
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) {
+        const float ov = __shfl_xor(bv, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ov < bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+      }
+      if (li == 0 && bi != 0x7fffffff) {
+        const long row = row0 + wm * MT * 32 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        if (row < m) {
+          const unsigned long long key = ((unsigned long long)orderable(bv) << 32) | (unsigned)bi;
+          atomicMin(&best[row], key);
+        }
+      }
+    }
+  }
+}
+
+__global__ void nn_finalize_kernel(const unsigned long long* __restrict__ best, long m, const float* __restrict__ xnorm,
+                                   int* __restrict__ labels, float* __restrict__ dist) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const unsigned long long key = best[i];
+  labels[i] = (int)(key & 0xffffffffu);
+  float d = unorderable((unsigned)(key >> 32)) + (xnorm ? xnorm[i] : 0.f);
+  dist[i] = d > 0.f ? d : 0.f;
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void accumulate_lds_kernel(const float* __restrict__ X, long m, int n, long ld,
+                                                             const int* __restrict__ labels, int k,
+                                                             double* __restrict__ sums, int* __restrict__ counts,
+                                                             long rows_per_block) {
+  extern __shared__ __attribute__((aligned(16))) float s_sum[];  // k*n floats then k ints
+  int* s_cnt = reinterpret_cast<int*>(s_sum + (long)k * n);
+  for (int i = threadIdx.x; i < k * n; i += 256) s_sum[i] = 0.f;
+  for (int i = threadIdx.x; i < k; i += 256) s_cnt[i] = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const long r0 = (long)blockIdx.x * rows_per_block;
+  const long r1 = min(m, r0 + rows_per_block);
+  for (long r = r0 + wid; r < r1; r += 4) {
+    const int l = labels[r];
+    if (lane == 0) atomicAdd(&s_cnt[l], 1);
+    float* dst = s_sum + (long)l * n;
+    const float* row = X + r * ld;
+    for (int d = lane; d < n; d += 64) atomicAdd(&dst[d], row[d]);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < k * n; i += 256) {
+    const float v = s_sum[i];
+    if (v != 0.f) atomicAdd(&sums[i], (double)v);
+  }
+  for (int i = threadIdx.x; i < k; i += 256)
+    if (s_cnt[i]) atomicAdd(&counts[i], s_cnt[i]);
+}
+
+__global__ __launch_bounds__(256) void accumulate_global_kernel(const float* __restrict__ X, long m, int n, long ld,
+                                                                const int* __restrict__ labels,
+                                                                float* __restrict__ sums, int* __restrict__ counts) {
+  const int lane = threadIdx.x & 63;
+  const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const long nw = (long)gridDim.x * 4;
+  for (long r = wave; r < m; r += nw) {
+    const int l = labels[r];
+    if (lane == 0) atomicAdd(&counts[l], 1);
+    float* dst = sums + (long)l * n;
+    const float* row = X + r * ld;
+    for (int d = lane; d < n; d += 64) atomicAdd(&dst[d], row[d]);
+  }
+}
+}  // namespace
+
+SRML_API int srml_nearest_centroid_f32(const float* X, long m, int n, long ldx, const float* C, int k, long ldc,
+                                       const float* cnorm, unsigned long long* best, hipStream_t stream) {
+  if (m <= 0 || k <= 0) return 0;
+  const bool vec = ((ldx & 3) == 0) && ((ldc & 3) == 0) && ((n & 3) == 0) &&
+                   ((reinterpret_cast<uintptr_t>(X) & 15) == 0) && ((reinterpret_cast<uintptr_t>(C) & 15) == 0);
+  if (k > 64) {
+    constexpr int BM = 128, BN = 128;
+    const long rt = (m + BM - 1) / BM;
+    const int ct = (k + BN - 1) / BN;
+    const long nb = rt * ct;
+    if (nb > 0x7fffffffL) return -3;
+    if (vec)
+      hipLaunchKernelGGL((nearest_centroid_kernel<BM, BN, 2, 2, 2, true>), dim3((unsigned)nb), dim3(256), 0, stream, X,
+                         m, n, ldx, C, k, ldc, cnorm, best, ct);
+    else
+      hipLaunchKernelGGL((nearest_centroid_kernel<BM, BN, 2, 2, 2, false>), dim3((unsigned)nb), dim3(256), 0, stream, X,
+                         m, n, ldx, C, k, ldc, cnorm, best, ct);
+  } else {
+    constexpr int BM = 256, BN = 64;
+    const long rt = (m + BM - 1) / BM;
+    const int ct = (k + BN - 1) / BN;
+    const long nb = rt * ct;
+    if (vec)
+      hipLaunchKernelGGL((nearest_centroid_kernel<BM, BN, 4, 2, 2, true>), dim3((unsigned)nb), dim3(256), 0, stream, X,
+                         m, n, ldx, C, k, ldc, cnorm, best, ct);
+    else
+      hipLaunchKernelGGL((nearest_centroid_kernel<BM, BN, 4, 2, 2, false>), dim3((unsigned)nb), dim3(256), 0, stream, X,
+                         m, n, ldx, C, k, ldc, cnorm, best, ct);
+  }
+  return srml_status();
+}
+
+SRML_API int srml_nn_finalize(const unsigned long long* best, long m, const float* xnorm, int* labels, float* dist,
+                              hipStream_t stream) {
+  if (m <= 0) return 0;
+  hipLaunchKernelGGL(nn_finalize_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream, best, m, xnorm, labels,
+                     dist);
+  return srml_status();
+}
+
+// sums: fp64 (k*n) when use_lds, fp32 otherwise (sums_f32); counts int32 (k)
+SRML_API int srml_kmeans_accumulate_f32(const float* X, long m, int n, long ld, const int* labels, int k,
+                                        double* sums_f64, float* sums_f32, int* counts, hipStream_t stream) {
+  if (m <= 0) return 0;
+  const size_t lds = (size_t)k * n * sizeof(float) + (size_t)k * sizeof(int);
+  if (sums_f64 && lds <= 64 * 1024) {
+    long blocks = 1024;
+    long rpb = (m + blocks - 1) / blocks;
+    if (rpb < 256) rpb = 256;
+    blocks = (m + rpb - 1) / rpb;
+    hipLaunchKernelGGL(accumulate_lds_kernel<true>, dim3((unsigned)blocks), dim3(256), lds, stream, X, m, n, ld, labels, k,
+                       sums_f64, counts, rpb);
+  } else {
+    if (!sums_f32) return -4;
+    long blocks = (m + 3) / 4;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(accumulate_global_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, X, m, n, ld, labels,
+                       sums_f32, counts);
+  }
+  return srml_status();
+}

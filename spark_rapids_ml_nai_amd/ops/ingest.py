@@ -8,6 +8,7 @@ the host fills chunk i+1 (two buffers, event-guarded reuse). Small arrays take t
 """
 from __future__ import annotations
 
+import warnings
 from typing import Any, Optional
 
 import numpy as np
@@ -28,7 +29,10 @@ def _pinned(device: torch.device, slot: int, nbytes: int) -> torch.Tensor:
 
 
 def _dense_to_device(a: np.ndarray, device: torch.device, dtype: Optional[torch.dtype]) -> torch.Tensor:
-    t = torch.from_numpy(np.ascontiguousarray(a))
+    with warnings.catch_warnings():
+        # Arrow buffers are read-only; we only ever read them
+        warnings.simplefilter("ignore", UserWarning)
+        t = torch.from_numpy(np.ascontiguousarray(a))
     if dtype is not None and t.dtype != dtype and not t.dtype.is_floating_point:
         t = t.to(dtype)
     elif dtype is not None and t.dtype != dtype:

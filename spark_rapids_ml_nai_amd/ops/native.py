@@ -35,6 +35,12 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_xw_f32": (_P, _L, _I, _L, _P, _I, _P, _P, _L, _P),
     "srml_dgemm": (_I, _I, _I, _I, _I, _D, _P, _L, _P, _L, _D, _P, _L, _P),
     "srml_sign_flip_f64": (_P, _I, _I, _L, _P),
+    "srml_xtv_f32": (_P, _L, _I, _L, _P, _I, _L, _P, _P),
+    "srml_row_sqnorm_f32": (_P, _L, _I, _L, _P, _P),
+    "srml_logreg_binary_f32": (_P, _L, _I, _L, _P, _P, _D, _P, _P),
+    "srml_nearest_centroid_f32": (_P, _L, _I, _L, _P, _I, _L, _P, _P, _P),
+    "srml_nn_finalize": (_P, _L, _P, _P, _P, _P),
+    "srml_kmeans_accumulate_f32": (_P, _L, _I, _L, _P, _I, _P, _P, _P, _P),
 }
 
 _lock = threading.Lock()

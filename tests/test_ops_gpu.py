@@ -76,3 +76,59 @@ def test_sign_flip(gpu_device):
     torch.testing.assert_close(out, ref)
     idx = out.abs().argmax(0)
     assert torch.all(out[idx, torch.arange(7)] > 0)
+
+
+@pytest.mark.parametrize("m,n,k", [(1000, 3, 1), (5000, 300, 2), (20000, 3000, 1), (777, 129, 4), (100, 10, 7)])
+def test_xtv(gpu_device, m, n, k):
+    X = _rand(m, n, gpu_device, seed=11)
+    V = _rand(m, k, gpu_device, seed=12)
+    out = ops.xtv(X, V).cpu()
+    ref = X.double().cpu().T @ V.double().cpu()
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-3)
+
+
+def test_row_sqnorm(gpu_device):
+    X = _rand(3001, 131, gpu_device, seed=13)
+    torch.testing.assert_close(ops.row_sqnorm(X).cpu().double(), (X.double() ** 2).sum(1).cpu(), rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("m,n", [(500, 7), (4000, 256), (3000, 1000), (5000, 3000), (2000, 4096), (1000, 1500)])
+def test_logreg_binary_loss_grad(gpu_device, m, n):
+    X = _rand(m, n, gpu_device, seed=14) * 0.1
+    y = (torch.rand(m, generator=torch.Generator().manual_seed(1)) > 0.5).float().to(gpu_device)
+    w = torch.randn(n, generator=torch.Generator().manual_seed(2), dtype=torch.float64).to(gpu_device) * 0.3
+    b = 0.25
+    out = ops.logreg_binary_loss_grad(X, y, w, b).cpu()
+    Xd = X.double().cpu()
+    z = Xd @ w.cpu() + b
+    p = torch.sigmoid(z)
+    r = p - y.double().cpu()
+    loss = torch.nn.functional.softplus(z).sum() - (y.double().cpu() * z).sum()
+    torch.testing.assert_close(out[:n], Xd.T @ r, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(out[n], r.sum(), rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(out[n + 1], loss, rtol=1e-10, atol=1e-8)
+
+
+@pytest.mark.parametrize("m,n,k", [(1000, 16, 20), (3000, 64, 5), (2000, 300, 130), (1024, 3000, 257), (777, 33, 1)])
+def test_nearest_centroid(gpu_device, m, n, k):
+    g = torch.Generator().manual_seed(3)
+    C = torch.randn(k, n, generator=g) * 3
+    lab = torch.randint(0, k, (m,), generator=g)
+    X = (C[lab] + 0.5 * torch.randn(m, n, generator=g)).float()
+    labels, dist = ops.nearest_centroid(X.to(gpu_device), C.float().to(gpu_device))
+    D = torch.cdist(X.double(), C.double()) ** 2
+    ref_d, ref_l = D.min(1)
+    got = D[torch.arange(m), labels.long().cpu()]
+    # chosen centroid is (numerically) optimal; distances match
+    assert torch.all(got <= ref_d + 1e-3 * (1 + ref_d))
+    torch.testing.assert_close(dist.double().cpu(), ref_d, rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("m,n,k", [(5000, 16, 20), (20000, 3000, 50), (3000, 64, 200)])
+def test_cluster_sums(gpu_device, m, n, k):
+    X = _rand(m, n, gpu_device, seed=15)
+    labels = torch.randint(0, k, (m,), generator=torch.Generator().manual_seed(4)).int()
+    sums, counts = ops.cluster_sums(X, labels.to(gpu_device), k)
+    ref = torch.zeros(k, n, dtype=torch.float64).index_add_(0, labels.long(), X.double().cpu())
+    torch.testing.assert_close(sums.cpu(), ref, rtol=1e-4, atol=1e-3)
+    assert torch.equal(counts.cpu(), torch.bincount(labels.long(), minlength=k))
