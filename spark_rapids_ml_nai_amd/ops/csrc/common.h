@@ -18,16 +18,44 @@ typedef double doublex4 __attribute__((ext_vector_type(4)));
 
 static constexpr int kWave = 64;
 
+// Wave64 all-reduce on DPP (no LDS): quad_perm swaps and row mirrors reduce within each 16-lane
+// row, row_bcast:15 / row_bcast:31 fold the four rows into lane 63, readlane broadcasts the
+// result as a wave-uniform value. __shfl_xor lowers to ds_bpermute (an LDS round trip per step),
+// which made per-row reductions the bottleneck of the row-streaming kernels.
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW_MASK, 0xf, false));
+}
+
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ double dpp_d(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffLL), CTRL, ROW_MASK, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROW_MASK, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dpp_f<0xb1>(v);        // quad_perm [1,0,3,2]
+  v += dpp_f<0x4e>(v);        // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);       // row_half_mirror
+  v += dpp_f<0x140>(v);       // row_mirror   -> every lane holds its 16-lane row sum
+  v += dpp_f<0x142, 0xa>(v);  // row_bcast:15 into rows 1,3
+  v += dpp_f<0x143, 0xc>(v);  // row_bcast:31 into rows 2,3 -> lane 63 holds the total
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dpp_d<0xb1>(v);
+  v += dpp_d<0x4e>(v);
+  v += dpp_d<0x141>(v);
+  v += dpp_d<0x140>(v);
+  v += dpp_d<0x142, 0xa>(v);
+  v += dpp_d<0x143, 0xc>(v);
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffLL), 63);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
 __device__ __forceinline__ float wave_max(float v) {

@@ -123,6 +123,18 @@ __device__ __forceinline__ float softplus_f(float z) {
   return z > 0.f ? z + log1pf(__expf(-z)) : log1pf(__expf(z));
 }
 
+// Per-row logistic terms. The piecewise-linear parts of the loss (max(z,0) - y z) stay in fp64 so
+// the objective is smooth for the line search; the bounded transcendental part log1p(exp(-|z|))
+// and the sigmoid use the fp32 hardware exp/log (v_exp_f32 / v_log_f32): fp64 exp/log1p are long
+// software sequences that made the kernel VALU-bound.
+__device__ __forceinline__ void logistic_terms(double z, double y, double& res, double& loss) {
+  const float zf = (float)z;
+  const float e = __expf(-fabsf(zf));             // in (0, 1]
+  const float p = zf >= 0.f ? 1.f / (1.f + e) : e / (1.f + e);
+  res = (double)p - y;
+  loss = (z > 0.0 ? z : 0.0) - y * z + (double)log1pf(e);
+}
+
 template <int V, bool REREAD>
 __global__ __launch_bounds__(256) void logreg_binary_kernel(const float* __restrict__ X, long m, int n, long ld,
                                                             const float* __restrict__ y, const double* __restrict__ w,
@@ -171,10 +183,10 @@ __global__ __launch_bounds__(256) void logreg_binary_kernel(const float* __restr
     dot = wave_sum(dot);
     const double z = dot + b;
     const double yr = (double)y[r];
-    const double p = 1.0 / (1.0 + exp(-z));
-    const double res = p - yr;
+    double res, lt;
+    logistic_terms(z, yr, res, lt);
     if (lane == 0) {
-      loss += (z > 0.0 ? z + log1p(exp(-z)) : log1p(exp(z))) - yr * z;
+      loss += lt;
       gb += res;
     }
     const float rf = (float)res;
@@ -247,15 +259,16 @@ __global__ __launch_bounds__(256, 2) void logreg_binary_split_kernel(const float
 #pragma unroll
       for (int v = 0; v < V; ++v) {
         const int c = cbase + (v * 64 + lane) * 4;
-        floatx4 xv = {0.f, 0.f, 0.f, 0.f};
-        if (r < r1) {
-          const float* row = X + r * ld;
-          if (vec && c + 3 < n) {
-            xv = *reinterpret_cast<const floatx4*>(row + c);
-          } else {
+        // branch-free: clamped row / column, out-of-range lanes multiply by zero weights
+        // (wreg is 0 beyond n) and rows past r1 are dropped after the reduction
+        const float* row = X + (r < r1 ? r : r1 - 1) * ld;
+        floatx4 xv;
+        if (vec) {
+          xv = *reinterpret_cast<const floatx4*>(row + (c + 3 < n ? c : 0));
+          if (c + 3 >= n) xv = floatx4{0.f, 0.f, 0.f, 0.f};
+        } else {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) xv[q] = (c + q < n) ? row[c + q] : 0.f;
-          }
+          for (int q = 0; q < 4; ++q) xv[q] = row[c + q < n ? c + q : 0] * (c + q < n ? 1.f : 0.f);
         }
         x[i][v] = xv;
         dot = fma((double)xv[0], wreg[v][0], fma((double)xv[1], wreg[v][1],
@@ -271,10 +284,10 @@ __global__ __launch_bounds__(256, 2) void logreg_binary_split_kernel(const float
       if (r >= r1) break;
       const double z = part[buf][i][0] + part[buf][i][1] + part[buf][i][2] + part[buf][i][3] + b;
       const double yr = (double)y[r];
-      const double p = 1.0 / (1.0 + exp(-z));
-      const double res = p - yr;
+      double res, lt;
+      logistic_terms(z, yr, res, lt);
       if (wid == 0 && lane == 0) {
-        loss += (z > 0.0 ? z + log1p(exp(-z)) : log1p(exp(z))) - yr * z;
+        loss += lt;
         gb += res;
       }
       const float rf = (float)res;
@@ -308,14 +321,22 @@ SRML_API int srml_logreg_binary_f32(const float* X, long m, int n, long ld, cons
   int V = (n + 255) / 256;
   size_t lds = 256 * (size_t)(V <= 1 ? 1 : V <= 2 ? 2 : V <= 4 ? 4 : V <= 8 ? 8 : V <= 12 ? 12 : 16) * (sizeof(double) + sizeof(float));
   dim3 grid((unsigned)blocks), blk(256);
-  static const int split = getenv("SRML_LOGREG_SPLIT") ? atoi(getenv("SRML_LOGREG_SPLIT")) : 1;
+  static const int split = getenv("SRML_LOGREG_SPLIT") ? atoi(getenv("SRML_LOGREG_SPLIT")) : 0;
   if (split && n > 1024 && n <= 4096) {
-    constexpr int R = 4;
+    static const int rsel = getenv("SRML_LOGREG_R") ? atoi(getenv("SRML_LOGREG_R")) : 4;
     const int VS = (n + 1023) / 1024;
-    if (VS == 1) hipLaunchKernelGGL((logreg_binary_split_kernel<1, R>), grid, blk, 0, stream, X, m, n, ld, y, w, b, out, rpb);
-    else if (VS == 2) hipLaunchKernelGGL((logreg_binary_split_kernel<2, R>), grid, blk, 0, stream, X, m, n, ld, y, w, b, out, rpb);
-    else if (VS == 3) hipLaunchKernelGGL((logreg_binary_split_kernel<3, R>), grid, blk, 0, stream, X, m, n, ld, y, w, b, out, rpb);
-    else hipLaunchKernelGGL((logreg_binary_split_kernel<4, R>), grid, blk, 0, stream, X, m, n, ld, y, w, b, out, rpb);
+#define SRML_LR_SPLIT(VV, RR) \
+    hipLaunchKernelGGL((logreg_binary_split_kernel<VV, RR>), grid, blk, 0, stream, X, m, n, ld, y, w, b, out, rpb)
+    if (rsel == 8) {
+      if (VS == 1) SRML_LR_SPLIT(1, 8); else if (VS == 2) SRML_LR_SPLIT(2, 8);
+      else if (VS == 3) SRML_LR_SPLIT(3, 8); else SRML_LR_SPLIT(4, 8);
+    } else if (rsel == 2) {
+      if (VS == 1) SRML_LR_SPLIT(1, 2); else if (VS == 2) SRML_LR_SPLIT(2, 2);
+      else if (VS == 3) SRML_LR_SPLIT(3, 2); else SRML_LR_SPLIT(4, 2);
+    } else {
+      if (VS == 1) SRML_LR_SPLIT(1, 4); else if (VS == 2) SRML_LR_SPLIT(2, 4);
+      else if (VS == 3) SRML_LR_SPLIT(3, 4); else SRML_LR_SPLIT(4, 4);
+    }
     return srml_status();
   }
   const int reread = 0;

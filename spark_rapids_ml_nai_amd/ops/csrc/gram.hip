@@ -24,53 +24,74 @@ constexpr int NTHREADS = 256;
 struct TileStage {
   floatx4 a[4];
   floatx4 b[4];
+  floatx4 mua, mub;
+  unsigned okmask;  // bits 0..15: A elements valid, 16..31: B elements valid
 };
 
+// Branch-free staging: every lane always issues its loads from a clamped, valid address; masking
+// and mean-centring are applied in store_stage() (after the MFMAs of the current tile), so hipcc
+// emits no per-load branch or early vmcnt wait and the next tile's loads stay in flight.
 template <bool CENTER, bool VEC>
 __device__ __forceinline__ void load_stage(const float* __restrict__ X, long ld, int n, long r_base, long r_end,
-                                           int i0, int j0, bool diag, const float* __restrict__ mu,
-                                           TileStage& st) {
+                                           int i0, int j0, const float* __restrict__ mu, TileStage& st) {
   const int t = threadIdx.x;
   const int c4 = (t & 31) * 4;
+  const int ca = i0 + c4, cb = j0 + c4;
+  const bool oka = ca < n, okb = cb < n;  // n % 4 == 0 on the VEC path
+  const int cac = oka ? ca : 0, cbc = okb ? cb : 0;
+  unsigned mask = 0u;
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     const int rr = (t >> 5) + 8 * p;
     const long r = r_base + rr;
-    floatx4 va = {0.f, 0.f, 0.f, 0.f};
-    floatx4 vb = {0.f, 0.f, 0.f, 0.f};
-    if (r < r_end) {
-      const float* row = X + r * ld;
-      if (VEC) {
-        if (i0 + c4 < n) va = *reinterpret_cast<const floatx4*>(row + i0 + c4);
-        if (!diag && j0 + c4 < n) vb = *reinterpret_cast<const floatx4*>(row + j0 + c4);
-      } else {
+    const bool okr = r < r_end;
+    const float* row = X + (okr ? r : r_end - 1) * ld;
+    if (VEC) {
+      st.a[p] = *reinterpret_cast<const floatx4*>(row + cac);
+      st.b[p] = *reinterpret_cast<const floatx4*>(row + cbc);
+    } else {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          if (i0 + c4 + q < n) va[q] = row[i0 + c4 + q];
-          if (!diag && j0 + c4 + q < n) vb[q] = row[j0 + c4 + q];
-        }
-      }
-      if (CENTER) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          if (i0 + c4 + q < n) va[q] -= mu[i0 + c4 + q];
-          if (!diag && j0 + c4 + q < n) vb[q] -= mu[j0 + c4 + q];
-        }
+      for (int q = 0; q < 4; ++q) {
+        st.a[p][q] = row[min(ca + q, n - 1)];
+        st.b[p][q] = row[min(cb + q, n - 1)];
       }
     }
-    st.a[p] = va;
-    st.b[p] = vb;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const bool ina = okr && (VEC ? oka : (ca + q < n));
+      const bool inb = okr && (VEC ? okb : (cb + q < n));
+      mask |= (ina ? 1u : 0u) << (4 * p + q);
+      mask |= (inb ? 1u : 0u) << (16 + 4 * p + q);
+    }
+  }
+  st.okmask = mask;
+}
+
+template <bool CENTER>
+__device__ __forceinline__ void load_mean(const float* __restrict__ mu, int n, int i0, int j0, TileStage& st) {
+  const int c4 = (threadIdx.x & 31) * 4;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    st.mua[q] = CENTER ? mu[min(i0 + c4 + q, n - 1)] : 0.f;
+    st.mub[q] = CENTER ? mu[min(j0 + c4 + q, n - 1)] : 0.f;
   }
 }
 
+template <bool CENTER>
 __device__ __forceinline__ void store_stage(float (*As)[BT], float (*Bs)[BT], bool diag, const TileStage& st) {
   const int t = threadIdx.x;
   const int c4 = (t & 31) * 4;
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     const int rr = (t >> 5) + 8 * p;
-    *reinterpret_cast<floatx4*>(&As[rr][c4]) = st.a[p];
-    if (!diag) *reinterpret_cast<floatx4*>(&Bs[rr][c4]) = st.b[p];
+    floatx4 a, b;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      a[q] = ((st.okmask >> (4 * p + q)) & 1u) ? (CENTER ? st.a[p][q] - st.mua[q] : st.a[p][q]) : 0.f;
+      b[q] = ((st.okmask >> (16 + 4 * p + q)) & 1u) ? (CENTER ? st.b[p][q] - st.mub[q] : st.b[p][q]) : 0.f;
+    }
+    *reinterpret_cast<floatx4*>(&As[rr][c4]) = a;
+    if (!diag) *reinterpret_cast<floatx4*>(&Bs[rr][c4]) = b;
   }
 }
 
@@ -111,14 +132,15 @@ __global__ __launch_bounds__(NTHREADS, 2) void gram_f32_kernel(const float* __re
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 
   TileStage st;
-  load_stage<CENTER, VEC>(X, ld, n, r_begin, r_end, i0, j0, diag, mu, st);
-  store_stage(As[0], Bs[0], diag, st);
+  load_mean<CENTER>(mu, n, i0, j0, st);
+  load_stage<CENTER, VEC>(X, ld, n, r_begin, r_end, i0, j0, mu, st);
+  store_stage<CENTER>(As[0], Bs[0], diag, st);
   __syncthreads();
 
   int cur = 0;
   for (int kt = 0; kt < nk; ++kt) {
     const bool more = (kt + 1 < nk);
-    if (more) load_stage<CENTER, VEC>(X, ld, n, r_begin + (long)(kt + 1) * BK, r_end, i0, j0, diag, mu, st);
+    if (more) load_stage<CENTER, VEC>(X, ld, n, r_begin + (long)(kt + 1) * BK, r_end, i0, j0, mu, st);
 
     const float(*A)[BT] = As[cur];
     const float(*B)[BT] = diag ? As[cur] : Bs[cur];
@@ -134,7 +156,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gram_f32_kernel(const float* __re
       acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
       acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
     }
-    if (more) store_stage(As[cur ^ 1], Bs[cur ^ 1], diag, st);
+    if (more) store_stage<CENTER>(As[cur ^ 1], Bs[cur ^ 1], diag, st);
     __syncthreads();
     cur ^= 1;
   }

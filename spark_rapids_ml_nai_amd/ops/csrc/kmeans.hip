@@ -29,36 +29,58 @@ __device__ __forceinline__ float unorderable(unsigned u) {
   return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
 }
 
+// ROWS x 32 tile of a row-major matrix, staged through registers. load(): branch-free (clamped
+// addresses + select after the load) so the next k-tile's loads stay in flight under the MFMAs;
+// store(): scalar ds_writes into the padded [row][33] LDS image (conflict-free operand reads).
 template <int ROWS, bool VEC>
-__device__ __forceinline__ void stage_tile(const float* __restrict__ A, long lda, long nrows_total, int ncols,
-                                           long row0, int k0, float (*dst)[PADK]) {
-  // ROWS x 32 tile, row-major source; thread t loads float4 (row t/8 + 32p, cols (t%8)*4)
-  const int t = threadIdx.x;
-  constexpr int PASSES = (ROWS * 8 + 255) / 256;
+struct RowTile {
+  static constexpr int PER = (ROWS * 8 + 255) / 256;
+  floatx4 v[PER];
+  unsigned okmask;  // bit 4p+q: element valid (row and column in range)
+
+  // issue the loads only; masking happens in store() so no wait is emitted before the MFMAs
+  __device__ __forceinline__ void load(const float* __restrict__ A, long lda, long nrows, int ncols, long row0,
+                                       int k0) {
+    const int t = threadIdx.x;
+    okmask = 0u;
 #pragma unroll
-  for (int p = 0; p < PASSES; ++p) {
-    const int idx = t + 256 * p;
-    if (idx < ROWS * 8) {
-      const int rr = idx >> 3;
+    for (int p = 0; p < PER; ++p) {
+      const int idx = t + 256 * p;
+      const int rr = (idx >> 3) % ROWS;
       const int c4 = (idx & 7) * 4;
       const long r = row0 + rr;
-      floatx4 v = {0.f, 0.f, 0.f, 0.f};
-      if (r < nrows_total) {
-        const float* src = A + r * lda + k0 + c4;
-        if (VEC && k0 + c4 + 3 < ncols) {
-          v = *reinterpret_cast<const floatx4*>(src);
-        } else {
+      const bool okr = (idx < ROWS * 8) && (r < nrows);
+      const float* row = A + (okr ? r : 0) * lda;
+      const int kc = k0 + c4;
+      if (VEC) {
+        const bool okk = kc < ncols;  // ncols % 4 == 0 on the VEC path
+        v[p] = *reinterpret_cast<const floatx4*>(row + (okk ? kc : 0));
+        okmask |= (okr && okk) ? (0xFu << (4 * p)) : 0u;
+      } else {
 #pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] = (k0 + c4 + q < ncols) ? src[q] : 0.f;
+        for (int q = 0; q < 4; ++q) {
+          const bool okk = kc + q < ncols;
+          v[p][q] = row[okk ? kc + q : 0];
+          okmask |= (okr && okk) ? (1u << (4 * p + q)) : 0u;
         }
       }
-      dst[rr][c4 + 0] = v[0];
-      dst[rr][c4 + 1] = v[1];
-      dst[rr][c4 + 2] = v[2];
-      dst[rr][c4 + 3] = v[3];
     }
   }
-}
+
+  __device__ __forceinline__ void store(float (*dst)[PADK]) const {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int p = 0; p < PER; ++p) {
+      const int idx = t + 256 * p;
+      if (PER * 256 == ROWS * 8 || idx < ROWS * 8) {
+        const int rr = idx >> 3;
+        const int c4 = (idx & 7) * 4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dst[rr][c4 + q] = ((okmask >> (4 * p + q)) & 1u) ? v[p][q] : 0.f;
+      }
+    }
+  }
+};
 
 // BM x BN block tile, WM x WN waves (WM*WN = 4), each wave MT x NT tiles of 32x32
 template <int BM, int BN, int WM, int MT, int NT, bool VEC>
@@ -88,14 +110,19 @@ __global__ __launch_bounds__(256, 2) void nearest_centroid_kernel(const float* _
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 
   const int nk = (n + BK - 1) / BK;
-  stage_tile<BM, VEC>(X, ldx, m, n, row0, 0, Xs[0]);
-  stage_tile<BN, VEC>(C, ldc, k, n, col0, 0, Cs[0]);
+  RowTile<BM, VEC> xt;
+  RowTile<BN, VEC> ct;
+  xt.load(X, ldx, m, n, row0, 0);
+  ct.load(C, ldc, k, n, col0, 0);
+  xt.store(Xs[0]);
+  ct.store(Cs[0]);
   __syncthreads();
   int cur = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) {
-      stage_tile<BM, VEC>(X, ldx, m, n, row0, (kt + 1) * BK, Xs[cur ^ 1]);
-      stage_tile<BN, VEC>(C, ldc, k, n, col0, (kt + 1) * BK, Cs[cur ^ 1]);
+    const bool more = kt + 1 < nk;
+    if (more) {  // issue next tile's global loads; they land while this tile's MFMAs run
+      xt.load(X, ldx, m, n, row0, (kt + 1) * BK);
+      ct.load(C, ldc, k, n, col0, (kt + 1) * BK);
     }
 #pragma unroll
     for (int kk = 0; kk < BK / 2; ++kk) {
@@ -110,6 +137,10 @@ __global__ __launch_bounds__(256, 2) void nearest_centroid_kernel(const float* _
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
+    }
+    if (more) {
+      xt.store(Xs[cur ^ 1]);
+      ct.store(Cs[cur ^ 1]);
     }
     __syncthreads();
     cur ^= 1;

@@ -19,6 +19,60 @@
 // ------------------------------------------------------------------------------------------
 // skinny GEMM
 // ------------------------------------------------------------------------------------------
+// Two-row-per-wave variant for n <= 256*V: every lane issues all of its 16-B loads for two rows
+// before the first FMA (2*V loads in flight per lane, no per-iteration vmcnt(0) round trip),
+// then reduces the K partial sums of each row with wave64 shuffles.
+template <int K, int V>
+__global__ __launch_bounds__(256) void xw_rows_kernel(const float* __restrict__ X, long m, int n, long ld,
+                                                      const float* __restrict__ W, const float* __restrict__ bias,
+                                                      float* __restrict__ out, long ldo) {
+  extern __shared__ __attribute__((aligned(16))) float Ws[];  // [256*V][K], zero-padded
+  for (int i = threadIdx.x; i < 256 * V * K; i += blockDim.x) Ws[i] = (i / K < n) ? W[i] : 0.f;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const long nwaves = (long)gridDim.x * 4;
+  for (long r0 = 2 * wave; r0 < m; r0 += 2 * nwaves) {
+    const long ra = r0, rb = (r0 + 1 < m) ? r0 + 1 : r0;
+    floatx4 xa[V], xb[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const int c = (v * 64 + lane) * 4;
+      const int cc = c < n ? c : 0;  // n % 4 == 0 on this path; padded W rows are zero
+      xa[v] = *reinterpret_cast<const floatx4*>(X + ra * ld + cc);
+      xb[v] = *reinterpret_cast<const floatx4*>(X + rb * ld + cc);
+    }
+    float acca[K], accb[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) { acca[c] = 0.f; accb[c] = 0.f; }
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const int c = (v * 64 + lane) * 4;
+      const float sel = c < n ? 1.f : 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float* w = &Ws[(c + q) * K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          acca[j] = fmaf(xa[v][q] * sel, w[j], acca[j]);
+          accb[j] = fmaf(xb[v][q] * sel, w[j], accb[j]);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j) { acca[j] = wave_sum(acca[j]); accb[j] = wave_sum(accb[j]); }
+    if (lane < K) {
+      float va = 0.f, vb = 0.f;
+#pragma unroll
+      for (int j = 0; j < K; ++j)
+        if (j == lane) { va = acca[j]; vb = accb[j]; }
+      const float bb = bias ? bias[lane] : 0.f;
+      out[ra * ldo + lane] = va + bb;
+      if (rb != ra) out[rb * ldo + lane] = vb + bb;
+    }
+  }
+}
+
 template <int K, bool VEC>
 __global__ __launch_bounds__(256) void xw_kernel(const float* __restrict__ X, long m, int n, long ld,
                                                  const float* __restrict__ W, const float* __restrict__ bias,
@@ -73,6 +127,22 @@ static int launch_xw(const float* X, long m, int n, long ld, const float* W, con
   long blocks = (m + 3) / 4;
   if (blocks > 4096) blocks = 4096;
   if (blocks < 1) blocks = 1;
+  if (vec && K <= 4 && n <= 4096) {
+    const int V = (n + 255) / 256;
+    long b2 = (m + 7) / 8;
+    if (b2 > 8192) b2 = 8192;
+    if (b2 < 1) b2 = 1;
+#define SRML_XW_ROWS(VV)                                                                                          \
+    hipLaunchKernelGGL((xw_rows_kernel<K, VV>), dim3((unsigned)b2), dim3(256), (size_t)256 * VV * K * sizeof(float), \
+                       stream, X, m, n, ld, W, bias, out, ldo)
+    if (V <= 1) SRML_XW_ROWS(1);
+    else if (V <= 2) SRML_XW_ROWS(2);
+    else if (V <= 4) SRML_XW_ROWS(4);
+    else if (V <= 8) SRML_XW_ROWS(8);
+    else if (V <= 12) SRML_XW_ROWS(12);
+    else SRML_XW_ROWS(16);
+    return srml_status();
+  }
   size_t lds = (size_t)wrows * K * sizeof(float);
   if (vec)
     hipLaunchKernelGGL((xw_kernel<K, true>), dim3((unsigned)blocks), dim3(256), lds, stream, X, m, n, ld, W, bias, out,

@@ -106,7 +106,7 @@ def test_logreg_binary_loss_grad(gpu_device, m, n):
     loss = torch.nn.functional.softplus(z).sum() - (y.double().cpu() * z).sum()
     torch.testing.assert_close(out[:n], Xd.T @ r, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(out[n], r.sum(), rtol=1e-6, atol=1e-6)
-    torch.testing.assert_close(out[n + 1], loss, rtol=1e-10, atol=1e-8)
+    torch.testing.assert_close(out[n + 1], loss, rtol=1e-7, atol=1e-6)
 
 
 @pytest.mark.parametrize("m,n,k", [(1000, 16, 20), (3000, 64, 5), (2000, 300, 130), (1024, 3000, 257), (777, 33, 1)])
@@ -121,7 +121,8 @@ def test_nearest_centroid(gpu_device, m, n, k):
     got = D[torch.arange(m), labels.long().cpu()]
     # chosen centroid is (numerically) optimal; distances match
     assert torch.all(got <= ref_d + 1e-3 * (1 + ref_d))
-    torch.testing.assert_close(dist.double().cpu(), ref_d, rtol=1e-4, atol=1e-2)
+    scale = (X.double() ** 2).sum(1) + (C.double() ** 2).sum(1).max()
+    assert torch.all((dist.double().cpu() - ref_d).abs() <= 1e-5 * scale + 1e-3)
 
 
 @pytest.mark.parametrize("m,n,k", [(5000, 16, 20), (20000, 3000, 50), (3000, 64, 200)])

@@ -1,0 +1,84 @@
+"""Micro-benchmark of the hot HIP kernels at the headline shapes (1M x 3000 fp32)."""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch
+
+from spark_rapids_ml_nai_amd import ops
+
+
+def timeit(fn, reps=5):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--m", type=int, default=1_000_000)
+    ap.add_argument("--n", type=int, default=3000)
+    ap.add_argument("--k", type=int, default=1000)
+    ap.add_argument("--only", type=str, default="")
+    a = ap.parse_args()
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(0)
+    X = torch.randn(a.m, a.n, device=dev, generator=g)
+    res = {}
+    gb = a.m * a.n * 4 / 1e9
+    sel = set(a.only.split(",")) if a.only else None
+
+    def want(name):
+        return sel is None or name in sel
+
+    if want("col_moments"):
+        t = timeit(lambda: ops.col_moments(X))
+        res["col_moments"] = {"ms": t, "TB/s": gb / t}
+    if want("gram"):
+        mu = X.mean(0).double()
+        t = timeit(lambda: ops.gram(X, mu), 3)
+        res["gram"] = {"ms": t, "TFLOP/s(sym)": a.m * a.n * a.n / t / 1e9}
+    if want("xtv"):
+        y = torch.randn(a.m, device=dev)
+        t = timeit(lambda: ops.xtv(X, y))
+        res["xtv"] = {"ms": t, "TB/s": gb / t}
+    if want("logreg"):
+        y = (torch.rand(a.m, device=dev) > 0.5).float()
+        w = torch.randn(a.n, device=dev, dtype=torch.float64) * 0.01
+        t = timeit(lambda: ops.logreg_binary_loss_grad(X, y, w, 0.1))
+        res["logreg"] = {"ms": t, "TB/s": gb / t}
+    if want("xw"):
+        W = torch.randn(a.n, 3, device=dev)
+        t = timeit(lambda: ops.xw(X, W))
+        res["xw_k3"] = {"ms": t, "TB/s": gb / t}
+    if want("nearest"):
+        C = torch.randn(a.k, a.n, device=dev, generator=g)
+        xn = ops.row_sqnorm(X)
+        t = timeit(lambda: ops.nearest_centroid(X, C, xn), 3)
+        res["nearest_centroid"] = {"ms": t, "TFLOP/s": 2 * a.m * a.k * a.n / t / 1e9}
+    if want("sums"):
+        lab = torch.randint(0, a.k, (a.m,), device=dev, dtype=torch.int32)
+        t = timeit(lambda: ops.cluster_sums(X, lab, a.k), 3)
+        res["cluster_sums"] = {"ms": t, "TB/s": gb / t}
+    if want("rowsq"):
+        t = timeit(lambda: ops.row_sqnorm(X))
+        res["row_sqnorm"] = {"ms": t, "TB/s": gb / t}
+    if want("h2d"):
+        h = torch.empty(a.m, a.n, pin_memory=True)
+        t = timeit(lambda: h.to(dev, non_blocking=True), 3)
+        res["h2d_pinned"] = {"ms": t, "GB/s": gb / t * 1000}
+    print(json.dumps({k: {kk: round(vv, 3) for kk, vv in v.items()} for k, v in res.items()}))
+
+
+if __name__ == "__main__":
+    main()
