@@ -45,7 +45,7 @@ from .core.params import (
     keyword_only,
 )
 from .parallel.context import WorkerContext
-from .regression import _FeaturesColMixin
+from .core.params import _FeaturesColMixin
 
 
 class _ClassifierColsMixin(_FeaturesColMixin):
@@ -326,3 +326,97 @@ class LogisticRegressionModel(LogisticRegressionClass, _ModelWithPredictionCol, 
         first._copy_backend_params(out)
         out._combined_models = list(models)
         return out
+
+
+# ======================================================================================
+# RandomForestClassifier
+# ======================================================================================
+from .tree import _RandomForestEstimator, _RandomForestModel  # noqa: E402
+
+
+class _RFClassifierParams:
+    def setProbabilityCol(self, value: str) -> Any:
+        return self._set_params(probabilityCol=value)
+
+    def setRawPredictionCol(self, value: str) -> Any:
+        return self._set(rawPredictionCol=value)
+
+
+class RandomForestClassifier(_RandomForestEstimator, HasProbabilityCol, HasRawPredictionCol, _RFClassifierParams):
+    """Random forest classifier grown level-wise on MI355X (LDS histograms, device split search).
+
+    Defaults follow Spark (numTrees=20, maxDepth=5, maxBins=32, impurity="gini"); each rank grows
+    its share of the trees on its local rows (reference parity) unless ``split_mode="data_parallel"``.
+    """
+
+    _is_classification = True
+
+    @keyword_only
+    def __init__(self, *, featuresCol: Union[str, List[str]] = "features", labelCol: str = "label",
+                 predictionCol: str = "prediction", probabilityCol: str = "probability",
+                 rawPredictionCol: str = "rawPrediction", maxDepth: int = 5, maxBins: int = 32,
+                 minInstancesPerNode: int = 1, minInfoGain: float = 0.0, maxMemoryInMB: int = 256,
+                 cacheNodeIds: bool = False, checkpointInterval: int = 10, impurity: str = "gini",
+                 numTrees: int = 20, featureSubsetStrategy: str = "auto", seed: Optional[int] = None,
+                 subsamplingRate: float = 1.0, leafCol: str = "", minWeightFractionPerNode: float = 0.0,
+                 weightCol: Optional[str] = None, bootstrap: Optional[bool] = True,
+                 num_workers: Optional[int] = None, verbose: Union[int, bool] = False, **kwargs: Any) -> None:
+        super().__init__()
+        self._setDefault(impurity="gini", probabilityCol="probability", rawPredictionCol="rawPrediction")
+        self._initialize_backend_params()
+        self._set_params(**self._input_kwargs)
+
+    def _supportsTransformEvaluate(self, evaluator: Any) -> bool:
+        return type(evaluator).__name__ == "MulticlassClassificationEvaluator"
+
+    def _create_model(self, result: Dict[str, Any]) -> "RandomForestClassificationModel":
+        return RandomForestClassificationModel._from_row(result)
+
+
+class RandomForestClassificationModel(_RandomForestModel, HasProbabilityCol, HasRawPredictionCol,
+                                      _RFClassifierParams):
+    _is_classification = True
+
+    def __init__(self, trees: List[Dict[str, Any]], n_cols: int, dtype: str = "float32", num_classes: int = 2) -> None:
+        super().__init__(trees=trees, n_cols=n_cols, dtype=dtype, num_classes=num_classes)
+        self._setDefault(probabilityCol="probability", rawPredictionCol="rawPrediction")
+
+    @property
+    def numClasses(self) -> int:
+        return self._num_classes
+
+    def _raw_np(self, value: Any) -> np.ndarray:
+        return self._raw_sum(np.asarray(as_dense_array(value), dtype=np.float32).reshape(1, -1),
+                             torch.device("cpu")).numpy()[0]
+
+    def predictRaw(self, value: Any) -> Any:
+        return Vectors.dense(self._raw_np(value))
+
+    def predictProbability(self, value: Any) -> Any:
+        r = self._raw_np(value)
+        return Vectors.dense(r / r.sum() if r.sum() > 0 else r)
+
+    def predict(self, value: Any) -> float:
+        return float(np.argmax(self._raw_np(value)))
+
+    def _vector_output_cols(self) -> List[str]:
+        return [self.getOrDefault("probabilityCol"), self.getOrDefault("rawPredictionCol")]
+
+    def _get_transform_func(self, dataset: DataFrame) -> Tuple[Callable, Callable]:
+        pc, prc, rc = self.getPredictionCol(), self.getOrDefault("probabilityCol"), self.getOrDefault("rawPredictionCol")
+
+        def construct(ctx: WorkerContext) -> Any:
+            self._pack(ctx.device)
+            return ctx.device
+
+        def predict(device: Any, X: Any, ctx: WorkerContext) -> Dict[str, np.ndarray]:
+            raw = self._raw_sum(X, ctx.device)  # Spark rawPrediction: sum of per-tree class distributions
+            tot = raw.sum(1, keepdim=True)
+            prob = torch.where(tot > 0, raw / tot.clamp_min(1e-300), raw)
+            lab = raw.argmax(1).double()
+            return {pc: lab.cpu().numpy(), prc: prob.cpu().numpy(), rc: raw.cpu().numpy()}
+
+        return construct, predict
+
+    def evaluate(self, dataset: Any) -> Any:
+        raise NotImplementedError("use an Evaluator on transform()")

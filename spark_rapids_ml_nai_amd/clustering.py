@@ -38,7 +38,7 @@ from .core.params import (
     keyword_only,
 )
 from .parallel.context import WorkerContext
-from .regression import _FeaturesColMixin
+from .core.params import _FeaturesColMixin
 
 
 def _stable_seed(name: str) -> int:

@@ -697,3 +697,28 @@ def _params_getters_setters(cls: type, names: Iterable[str]) -> None:
                 return self._set_params(**{_n: value})
 
             setattr(cls, "set" + cap, _setter)
+
+
+class _FeaturesColMixin:
+    """featuresCol / featuresCols (single vector/array column or multiple numeric columns)."""
+
+    def getFeaturesCol(self) -> Union[str, List[str]]:  # type: ignore[override]
+        if self.isDefined("featuresCols"):
+            return self.getOrDefault("featuresCols")
+        if self.isDefined("featuresCol"):
+            return self.getOrDefault("featuresCol")
+        raise RuntimeError("featuresCol is not set")
+
+    def setFeaturesCol(self, value: Union[str, List[str]]) -> Any:
+        if isinstance(value, str):
+            return self._set_params(featuresCol=value)
+        return self._set_params(featuresCols=value)
+
+    def setFeaturesCols(self, value: List[str]) -> Any:
+        return self._set_params(featuresCols=value)
+
+    def setLabelCol(self, value: str) -> Any:
+        return self._set_params(labelCol=value)
+
+    def setPredictionCol(self, value: str) -> Any:
+        return self._set_params(predictionCol=value)

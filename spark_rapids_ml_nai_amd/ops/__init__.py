@@ -245,3 +245,174 @@ def cluster_sums(X: torch.Tensor, labels: torch.Tensor, k: int) -> Tuple[torch.T
                     s32.data_ptr(), counts.data_ptr(), st)
         sums = s32.double()
     return sums, counts.long()
+
+
+# ------------------------------------------------------------------------------------------
+# Random forest primitives
+# ------------------------------------------------------------------------------------------
+def rf_quantize(X: torch.Tensor, edges: torch.Tensor) -> torch.Tensor:
+    """Feature-major uint8 bins (n, m): bin(x) = #edges[f] strictly below x. edges: (n, B-1) fp32."""
+    m, n = X.shape
+    ne = edges.shape[1]
+    if not X.is_cuda or X.dtype != torch.float32:
+        out = torch.empty((n, m), dtype=torch.uint8, device=X.device)
+        for f in range(n):
+            out[f] = torch.searchsorted(edges[f].contiguous().to(X.dtype), X[:, f].contiguous(), right=False).to(torch.uint8)
+        return out
+    X = _c(X)
+    e = _c(edges.to(torch.float32))
+    out = torch.empty((n, m), dtype=torch.uint8, device=X.device)
+    native.call("srml_rf_quantize_u8", X.data_ptr(), m, n, X.stride(0), e.data_ptr(), ne, out.data_ptr(),
+                native.stream(X.device))
+    return out
+
+
+def rf_hist(bins: torch.Tensor, idx: torch.Tensor, label: torch.Tensor, wcnt: Optional[torch.Tensor],
+            items: torch.Tensor, node_feats: torch.Tensor, nodes: int, B: int, S: int,
+            regression: bool) -> torch.Tensor:
+    """Per-(node, feature slot, bin) statistics: uint32 class counts or fp64 (count, sum, sumsq)."""
+    n, m = bins.shape
+    nf = node_feats.shape[1]
+    dev = bins.device
+    if regression:
+        hist = torch.zeros((nodes, nf, B, S), dtype=torch.float64, device=dev)
+    else:
+        hist = torch.zeros((nodes, nf, B, S), dtype=torch.int32, device=dev)
+    if items.shape[0] == 0:
+        return hist
+    if not bins.is_cuda:
+        it = items.cpu().numpy()
+        for node, rb, re, fc in it:
+            rows = idx[rb:re].long()
+            w = wcnt[rows].double() if wcnt is not None else torch.ones(len(rows), dtype=torch.float64)
+            y = label[rows]
+            for j in range(fc * 8, min(nf, fc * 8 + 8)):
+                f = int(node_feats[node, j])
+                b = bins[f, rows].long()
+                if regression:
+                    hist[node, j, :, 0].index_add_(0, b, w)
+                    hist[node, j, :, 1].index_add_(0, b, w * y.double())
+                    hist[node, j, :, 2].index_add_(0, b, w * y.double() ** 2)
+                else:
+                    flat = b * S + y.long()
+                    hist[node, j].view(-1).index_add_(0, flat, w.to(torch.int32))
+        return hist
+    lab = _c(label.to(torch.float32))
+    st = native.stream(dev)
+    native.call("srml_rf_hist", bins.data_ptr(), m, idx.data_ptr(), lab.data_ptr(),
+                wcnt.data_ptr() if wcnt is not None else None, _c(items).data_ptr(), int(items.shape[0]),
+                _c(node_feats).data_ptr(), nf, B, S, int(regression),
+                hist.data_ptr() if not regression else None, hist.data_ptr() if regression else None, st)
+    return hist
+
+
+def rf_best_split(hist: torch.Tensor, B: int, S: int, regression: bool, crit: int, min_leaf: float,
+                  min_gain: float) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Per node: out (nodes, 6) = {gain, feature_slot, bin, n_left, n_right, impurity}; totals (nodes, S)."""
+    nodes, nf = hist.shape[0], hist.shape[1]
+    dev = hist.device
+    if not hist.is_cuda:
+        return _rf_best_split_ref(hist.double(), S, regression, crit, min_leaf, min_gain)
+    out = torch.empty((nodes, 6), dtype=torch.float64, device=dev)
+    tot = torch.empty((nodes, S), dtype=torch.float64, device=dev)
+    native.call("srml_rf_best_split", hist.data_ptr() if not regression else None,
+                hist.data_ptr() if regression else None, nodes, nf, B, S, int(regression), int(crit),
+                float(min_leaf), float(min_gain), out.data_ptr(), tot.data_ptr(), native.stream(dev))
+    return out, tot
+
+
+def _impurity_ref(s: torch.Tensor, crit: int) -> torch.Tensor:
+    if crit == 2:
+        n = s[..., 0]
+        mean = s[..., 1] / n.clamp_min(1e-300)
+        return torch.where(n > 0, (s[..., 2] / n.clamp_min(1e-300) - mean * mean).clamp_min(0), torch.zeros_like(n))
+    n = s.sum(-1)
+    p = s / n.clamp_min(1e-300).unsqueeze(-1)
+    if crit == 0:
+        return torch.where(n > 0, 1 - (p * p).sum(-1), torch.zeros_like(n))
+    ent = -(torch.where(p > 0, p * torch.log2(p.clamp_min(1e-300)), torch.zeros_like(p))).sum(-1)
+    return torch.where(n > 0, ent, torch.zeros_like(n))
+
+
+def _rf_best_split_ref(hist: torch.Tensor, S: int, regression: bool, crit: int, min_leaf: float,
+                       min_gain: float) -> Tuple[torch.Tensor, torch.Tensor]:
+    nodes, nf, B, _ = hist.shape
+    tot = hist[:, 0].sum(1)  # (nodes, S)
+    ntot = tot[:, 0] if regression else tot.sum(-1)
+    pimp = _impurity_ref(tot, crit)
+    left = hist.cumsum(2)[:, :, : B - 1]  # (nodes, nf, B-1, S)
+    right = tot[:, None, None, :] - left
+    nl = left[..., 0] if regression else left.sum(-1)
+    nr = ntot[:, None, None] - nl
+    gain = pimp[:, None, None] - nl / ntot[:, None, None].clamp_min(1e-300) * _impurity_ref(left, crit) \
+        - nr / ntot[:, None, None].clamp_min(1e-300) * _impurity_ref(right, crit)
+    valid = (nl >= min_leaf) & (nr >= min_leaf) & (nl > 0) & (nr > 0)
+    gain = torch.where(valid, gain, torch.full_like(gain, -1.0))
+    out = torch.empty((nodes, 6), dtype=torch.float64)
+    flat = gain.reshape(nodes, -1)
+    best, arg = flat.max(1)  # first max -> lowest (feature, bin)
+    f = arg // (B - 1)
+    b = arg % (B - 1)
+    ok = (best > 1e-15) & ((best > min_gain) | (min_gain < 0))
+    out[:, 0] = torch.where(ok, best, torch.full_like(best, -1.0))
+    out[:, 1] = torch.where(ok, f.double(), torch.full_like(best, -1.0))
+    out[:, 2] = torch.where(ok, b.double(), torch.full_like(best, -1.0))
+    nlw = nl.reshape(nodes, -1).gather(1, arg.view(-1, 1)).view(-1)
+    out[:, 3] = torch.where(ok, nlw, torch.zeros_like(nlw))
+    out[:, 4] = torch.where(ok, ntot - nlw, torch.zeros_like(nlw))
+    out[:, 5] = pimp
+    return out, tot
+
+
+def rf_route(bins: torch.Tensor, idx: torch.Tensor, seg_node: torch.Tensor, node_feature: torch.Tensor,
+             node_bin: torch.Tensor, child_base: torch.Tensor) -> torch.Tensor:
+    n, m = bins.shape
+    total = idx.shape[0]
+    if not bins.is_cuda:
+        f = node_feature[seg_node.long()]
+        leaf = f < 0
+        fb = bins[f.clamp_min(0).long(), idx.long()].int()
+        right = (fb > node_bin[seg_node.long()]).int()
+        keys = child_base[seg_node.long()] + right
+        return torch.where(leaf, torch.full_like(keys, 2**31 - 1), keys)
+    keys = torch.empty(total, dtype=torch.int32, device=bins.device)
+    native.call("srml_rf_route", bins.data_ptr(), m, idx.data_ptr(), seg_node.data_ptr(), total,
+                node_feature.data_ptr(), node_bin.data_ptr(), child_base.data_ptr(), keys.data_ptr(),
+                native.stream(bins.device))
+    return keys
+
+
+def rf_predict(X: torch.Tensor, roots: torch.Tensor, feature: torch.Tensor, threshold: torch.Tensor,
+               left: torch.Tensor, right: torch.Tensor, value_off: torch.Tensor, values: torch.Tensor, S: int,
+               want_leaves: bool = False) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """Sum over trees of leaf value vectors (rows, S) (+ per-tree leaf ids)."""
+    m = X.shape[0]
+    T = roots.shape[0]
+    if not X.is_cuda or X.dtype != torch.float32 or S > 32:
+        Xf = X.float()
+        out = torch.zeros((m, S), dtype=torch.float32, device=X.device)
+        leaves = torch.empty((m, T), dtype=torch.int32, device=X.device) if want_leaves else None
+        rows = torch.arange(m, device=X.device)
+        for t in range(T):
+            node = torch.full((m,), int(roots[t]), dtype=torch.long, device=X.device)
+            while True:
+                f = feature[node]
+                active = f >= 0
+                if not bool(active.any()):
+                    break
+                xv = Xf[rows, f.clamp_min(0).long()]
+                go_left = xv <= threshold[node]
+                nxt = torch.where(go_left, left[node].long(), right[node].long())
+                node = torch.where(active, nxt, node)
+            if leaves is not None:
+                leaves[:, t] = (node - int(roots[t])).int()
+            off = value_off[node].long()
+            out += values[off.view(-1, 1) + torch.arange(S, device=X.device).view(1, -1)]
+        return out, leaves
+    X = _c(X)
+    out = torch.empty((m, S), dtype=torch.float32, device=X.device)
+    leaves = torch.empty((m, T), dtype=torch.int32, device=X.device) if want_leaves else None
+    native.call("srml_rf_predict", X.data_ptr(), m, X.stride(0), roots.data_ptr(), T, feature.data_ptr(),
+                threshold.data_ptr(), left.data_ptr(), right.data_ptr(), value_off.data_ptr(), values.data_ptr(), S,
+                out.data_ptr(), leaves.data_ptr() if leaves is not None else None, native.stream(X.device))
+    return out, leaves

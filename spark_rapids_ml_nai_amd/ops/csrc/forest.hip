@@ -1,0 +1,387 @@
+// Random-forest kernels: quantisation, level-wise histogram build, split search, row routing
+// and forest inference (reference: cuML RandomForest{Classifier,Regressor} / FIL called from
+// tree.py:309-414 and 571-613; SURVEY §2.4(c) RF rows).
+//
+// Data layout: the fp32 row-major feature block is quantised ONCE per fit into a FEATURE-MAJOR
+// uint8 matrix (n x m): a histogram pass for feature f streams bins[f][row] for the node's rows,
+// which are kept in ascending row order inside each node's segment of a row-index array (stable
+// partitions), so reads are monotone and mostly coalesced at the top of the tree.
+//
+//  * srml_rf_quantize_u8 — 256-row x 32-feature tiles: coalesced fp32 row reads, per-feature
+//    binary search in the (L1/L2-resident) edge table, LDS transpose, 256-byte feature rows out.
+//  * srml_rf_hist — one block per work item (node, 8-feature chunk, row chunk): histograms are
+//    privatised in LDS (ds_add) and flushed with one global atomic per non-empty cell.
+//    Classification cells are per-class weighted counts (uint32); regression cells are
+//    (count, sum y, sum y^2) in fp32 (fp64 fold on flush).
+//  * srml_rf_best_split — one block per node: every thread sweeps the bins of one candidate
+//    feature with running left statistics (Gini / entropy / variance gain, min-instances per
+//    child), then a block arg-max (ties -> lowest feature slot, lowest bin).
+//  * srml_rf_route — child key per row (2*slot + goes_right; dropped rows -> sentinel) for the
+//    stable re-partition of the row-index array.
+//  * srml_rf_predict — FIL-equivalent inference on raw fp32 rows: one thread per row walks every
+//    tree (nodes in breadth-first flat arrays) and accumulates leaf vectors.
+#include "common.h"
+
+namespace {
+constexpr int FB = 8;  // features per histogram work item
+}
+
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void rf_quantize_kernel(const float* __restrict__ X, long m, int n, long ld,
+                                                          const float* __restrict__ edges, int nedges,
+                                                          unsigned char* __restrict__ out) {
+  __shared__ unsigned char tile[32][256 + 4];
+  const long r0 = (long)blockIdx.x * 256;
+  const int f0 = blockIdx.y * 32;
+  const int t = threadIdx.x;
+  const int fl = t & 31;
+  const int f = f0 + fl;
+  const float* e = edges + (long)min(f, n - 1) * nedges;
+#pragma unroll 4
+  for (int p = 0; p < 32; ++p) {
+    const int rl = (t >> 5) + 8 * p;
+    const long r = r0 + rl;
+    unsigned char b = 0;
+    if (r < m && f < n) {
+      const float x = X[r * ld + f];
+      // number of edges strictly below x  (x <= e[b]  <=>  bin(x) <= b)
+      int lo = 0, hi = nedges;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (e[mid] < x) lo = mid + 1; else hi = mid;
+      }
+      b = (unsigned char)lo;
+    }
+    tile[fl][rl] = b;
+  }
+  __syncthreads();
+  // 32 features x 256 rows: each thread writes 4 consecutive bytes of one feature row
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int idx = t + 256 * p;  // 0..2047
+    const int fl2 = idx >> 6;     // 64 x 4-byte words per feature row
+    const int w = idx & 63;
+    const int ff = f0 + fl2;
+    const long rr = r0 + w * 4;
+    if (ff < n) {
+      unsigned char* dst = out + (long)ff * m + rr;
+      if (rr + 3 < m && ((reinterpret_cast<uintptr_t>(dst) & 3) == 0)) {
+        *reinterpret_cast<unsigned*>(dst) = *reinterpret_cast<const unsigned*>(&tile[fl2][w * 4]);
+      } else {
+        for (int q = 0; q < 4; ++q)
+          if (rr + q < m) dst[q] = tile[fl2][w * 4 + q];
+      }
+    }
+  }
+}
+
+SRML_API int srml_rf_quantize_u8(const float* X, long m, int n, long ld, const float* edges, int nedges,
+                                 unsigned char* out, hipStream_t stream) {
+  if (m <= 0 || n <= 0) return 0;
+  dim3 grid(ceil_div(m, 256), ceil_div(n, 32));
+  hipLaunchKernelGGL(rf_quantize_kernel, grid, dim3(256), 0, stream, X, m, n, ld, edges, nedges, out);
+  return srml_status();
+}
+
+// ------------------------------------------------------------------------------------------
+// histogram build. items: int4 {node_slot, row_begin, row_end, feature_chunk}
+// node_feats: [nodes][nf] global feature ids. hist layout: [node][nf][B][S] with S = C (class
+// counts, uint32) or 3 (regression stats, fp32 folded into fp64 output as double[3])
+// ------------------------------------------------------------------------------------------
+template <bool REG>
+__global__ __launch_bounds__(256) void rf_hist_kernel(const unsigned char* __restrict__ bins, long m,
+                                                      const int* __restrict__ idx, const float* __restrict__ label,
+                                                      const unsigned char* __restrict__ wcnt,
+                                                      const int4* __restrict__ items, const int* __restrict__ node_feats,
+                                                      int nf, int B, int S, unsigned* __restrict__ hist_u,
+                                                      double* __restrict__ hist_d) {
+  extern __shared__ __attribute__((aligned(16))) unsigned lh_u[];  // FB*B*S cells (uint32 or float)
+  float* lh_f = reinterpret_cast<float*>(lh_u);
+  const int4 it = items[blockIdx.x];
+  const int node = it.x, rb = it.y, re = it.z, fc = it.w;
+  const int f_begin = fc * FB;
+  const int nfb = min(FB, nf - f_begin);
+  const int cells = FB * B * S;
+  for (int i = threadIdx.x; i < cells; i += 256) lh_u[i] = 0u;
+  int feats[FB];
+#pragma unroll
+  for (int j = 0; j < FB; ++j) feats[j] = (j < nfb) ? node_feats[(long)node * nf + f_begin + j] : 0;
+  __syncthreads();
+  for (int i = rb + threadIdx.x; i < re; i += 256) {
+    const int r = idx[i];
+    const unsigned w = wcnt ? wcnt[r] : 1u;
+    if (w == 0u) continue;
+    const float y = label[r];
+#pragma unroll
+    for (int j = 0; j < FB; ++j) {
+      if (j < nfb) {
+        const int b = bins[(long)feats[j] * m + r];
+        const int base = (j * B + b) * S;
+        if (REG) {
+          atomicAdd(&lh_f[base + 0], (float)w);
+          atomicAdd(&lh_f[base + 1], (float)w * y);
+          atomicAdd(&lh_f[base + 2], (float)w * y * y);
+        } else {
+          atomicAdd(&lh_u[base + (int)y], w);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const long out_base = ((long)node * nf + f_begin) * B * S;
+  const int valid_cells = nfb * B * S;
+  for (int i = threadIdx.x; i < valid_cells; i += 256) {
+    if (REG) {
+      const float v = lh_f[i];
+      if (v != 0.f) atomicAdd(&hist_d[out_base + i], (double)v);
+    } else {
+      const unsigned v = lh_u[i];
+      if (v) atomicAdd(&hist_u[out_base + i], v);
+    }
+  }
+}
+
+SRML_API int srml_rf_hist(const unsigned char* bins, long m, const int* idx, const float* label,
+                          const unsigned char* wcnt, const int* items, int n_items, const int* node_feats, int nf,
+                          int B, int S, int regression, unsigned* hist_u, double* hist_d, hipStream_t stream) {
+  if (n_items <= 0) return 0;
+  const size_t lds = (size_t)FB * B * S * sizeof(unsigned);
+  if (lds > 64 * 1024) return -5;
+  if (regression)
+    hipLaunchKernelGGL(rf_hist_kernel<true>, dim3(n_items), dim3(256), lds, stream, bins, m, idx, label, wcnt,
+                       reinterpret_cast<const int4*>(items), node_feats, nf, B, S, hist_u, hist_d);
+  else
+    hipLaunchKernelGGL(rf_hist_kernel<false>, dim3(n_items), dim3(256), lds, stream, bins, m, idx, label, wcnt,
+                       reinterpret_cast<const int4*>(items), node_feats, nf, B, S, hist_u, hist_d);
+  return srml_status();
+}
+
+// ------------------------------------------------------------------------------------------
+// split search. crit: 0 gini, 1 entropy, 2 variance.  out per node (double[6]):
+//   {gain, feature_slot, bin, n_left, n_right, parent_impurity}
+// totals per node (double[S]): class counts or (count, sum, sumsq)
+// ------------------------------------------------------------------------------------------
+template <int SMAX>
+__device__ __forceinline__ double impurity(const double* s, int S, int crit, double n) {
+  if (n <= 0.0) return 0.0;
+  if (crit == 2) {
+    const double mean = s[1] / n;
+    const double v = s[2] / n - mean * mean;
+    return v > 0.0 ? v : 0.0;
+  }
+  double acc = 0.0;
+  if (crit == 0) {
+#pragma unroll
+    for (int c = 0; c < SMAX; ++c)
+      if (c < S) { const double p = s[c] / n; acc += p * p; }
+    return 1.0 - acc;
+  }
+#pragma unroll
+  for (int c = 0; c < SMAX; ++c)
+    if (c < S && s[c] > 0.0) { const double p = s[c] / n; acc -= p * log2(p); }
+  return acc;
+}
+
+template <int SMAX, bool REG>
+__global__ __launch_bounds__(256) void rf_best_split_kernel(const unsigned* __restrict__ hist_u,
+                                                            const double* __restrict__ hist_d, int nf, int B, int S,
+                                                            int crit, double min_leaf, double min_gain,
+                                                            double* __restrict__ out, double* __restrict__ totals) {
+  __shared__ double s_gain[256];
+  __shared__ int s_key[256];
+  __shared__ double s_tot[SMAX];
+  const int node = blockIdx.x;
+  const long nbase = (long)node * nf * B * S;
+  // node totals from feature slot 0 (every feature's histogram sums to the node totals)
+  if (threadIdx.x < S) {
+    double acc = 0.0;
+    for (int b = 0; b < B; ++b) {
+      const long i = nbase + (long)b * S + threadIdx.x;
+      acc += REG ? hist_d[i] : (double)hist_u[i];
+    }
+    s_tot[threadIdx.x] = acc;
+  }
+  __syncthreads();
+  double tot[SMAX];
+#pragma unroll
+  for (int c = 0; c < SMAX; ++c) tot[c] = c < S ? s_tot[c] : 0.0;
+  double ntot = 0.0;
+  if (REG) {
+    ntot = tot[0];
+  } else {
+#pragma unroll
+    for (int c = 0; c < SMAX; ++c) ntot += tot[c];
+  }
+  const double pimp = impurity<SMAX>(tot, S, crit, ntot);
+  double best = -1.0;
+  int bkey = 0x7fffffff;
+  for (int f = threadIdx.x; f < nf; f += 256) {
+    double left[SMAX];
+#pragma unroll
+    for (int c = 0; c < SMAX; ++c) left[c] = 0.0;
+    const long fbase = nbase + (long)f * B * S;
+    for (int b = 0; b < B - 1; ++b) {
+      double nl = 0.0;
+#pragma unroll
+      for (int c = 0; c < SMAX; ++c) {
+        if (c < S) {
+          const long i = fbase + (long)b * S + c;
+          left[c] += REG ? hist_d[i] : (double)hist_u[i];
+        }
+      }
+      if (REG) {
+        nl = left[0];
+      } else {
+#pragma unroll
+        for (int c = 0; c < SMAX; ++c) nl += left[c];
+      }
+      const double nr = ntot - nl;
+      if (nl < min_leaf || nr < min_leaf || nl <= 0.0 || nr <= 0.0) continue;
+      double right[SMAX];
+#pragma unroll
+      for (int c = 0; c < SMAX; ++c) right[c] = tot[c] - left[c];
+      const double gain = pimp - (nl / ntot) * impurity<SMAX>(left, S, crit, nl) -
+                          (nr / ntot) * impurity<SMAX>(right, S, crit, nr);
+      const int key = f * 1024 + b;
+      if (gain > best || (gain == best && key < bkey)) { best = gain; bkey = key; }
+    }
+  }
+  s_gain[threadIdx.x] = best;
+  s_key[threadIdx.x] = bkey;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      const double og = s_gain[threadIdx.x + o];
+      const int ok = s_key[threadIdx.x + o];
+      if (og > s_gain[threadIdx.x] || (og == s_gain[threadIdx.x] && ok < s_key[threadIdx.x])) {
+        s_gain[threadIdx.x] = og;
+        s_key[threadIdx.x] = ok;
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double g = s_gain[0];
+    const int key = s_key[0];
+    double* o = out + (long)node * 6;
+    const bool ok = (g > min_gain || (g >= 0.0 && min_gain < 0.0)) && key != 0x7fffffff && g > 1e-15;
+    o[0] = ok ? g : -1.0;
+    o[1] = ok ? (double)(key / 1024) : -1.0;
+    o[2] = ok ? (double)(key % 1024) : -1.0;
+    o[3] = 0.0;
+    o[4] = 0.0;
+    o[5] = pimp;
+    if (ok) {  // left/right weighted counts of the winner
+      const int f = key / 1024, bb = key % 1024;
+      double nl = 0.0;
+      for (int b = 0; b <= bb; ++b) {
+        if (REG) {
+          nl += hist_d[nbase + ((long)f * B + b) * S];
+        } else {
+          for (int c = 0; c < S; ++c) nl += (double)hist_u[nbase + ((long)f * B + b) * S + c];
+        }
+      }
+      o[3] = nl;
+      o[4] = ntot - nl;
+    }
+  }
+  if (threadIdx.x < S) totals[(long)node * S + threadIdx.x] = s_tot[threadIdx.x];
+}
+
+SRML_API int srml_rf_best_split(const unsigned* hist_u, const double* hist_d, int nodes, int nf, int B, int S,
+                                int regression, int crit, double min_leaf, double min_gain, double* out,
+                                double* totals, hipStream_t stream) {
+  if (nodes <= 0) return 0;
+#define SRML_RF_SPLIT(SM)                                                                                          \
+  do {                                                                                                             \
+    if (regression)                                                                                                \
+      hipLaunchKernelGGL((rf_best_split_kernel<SM, true>), dim3(nodes), dim3(256), 0, stream, hist_u, hist_d, nf, B, \
+                         S, crit, min_leaf, min_gain, out, totals);                                               \
+    else                                                                                                           \
+      hipLaunchKernelGGL((rf_best_split_kernel<SM, false>), dim3(nodes), dim3(256), 0, stream, hist_u, hist_d, nf, \
+                         B, S, crit, min_leaf, min_gain, out, totals);                                            \
+  } while (0)
+  if (S <= 2) SRML_RF_SPLIT(2);
+  else if (S <= 4) SRML_RF_SPLIT(4);
+  else if (S <= 8) SRML_RF_SPLIT(8);
+  else if (S <= 16) SRML_RF_SPLIT(16);
+  else if (S <= 32) SRML_RF_SPLIT(32);
+  else return -6;
+  return srml_status();
+}
+
+// ------------------------------------------------------------------------------------------
+// routing: key[i] = 2*child_base[node]+right for split nodes, INT_MAX for rows leaving the tree.
+// seg_node: node slot of each position i (int32), node_feature/node_bin: split per node (-1: leaf)
+// ------------------------------------------------------------------------------------------
+__global__ void rf_route_kernel(const unsigned char* __restrict__ bins, long m, const int* __restrict__ idx,
+                                const int* __restrict__ seg_node, long total, const int* __restrict__ node_feature,
+                                const int* __restrict__ node_bin, const int* __restrict__ child_base,
+                                int* __restrict__ keys) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int node = seg_node[i];
+  const int f = node_feature[node];
+  if (f < 0) {
+    keys[i] = 0x7fffffff;
+    return;
+  }
+  const int r = idx[i];
+  const int right = bins[(long)f * m + r] > node_bin[node] ? 1 : 0;
+  keys[i] = child_base[node] + right;
+}
+
+SRML_API int srml_rf_route(const unsigned char* bins, long m, const int* idx, const int* seg_node, long total,
+                           const int* node_feature, const int* node_bin, const int* child_base, int* keys,
+                           hipStream_t stream) {
+  if (total <= 0) return 0;
+  hipLaunchKernelGGL(rf_route_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, bins, m, idx,
+                     seg_node, total, node_feature, node_bin, child_base, keys);
+  return srml_status();
+}
+
+// ------------------------------------------------------------------------------------------
+// inference: trees stored as flat node arrays; roots[t] = first node of tree t.
+// feature < 0 => leaf whose value vector (width S) starts at values[value_off[node]].
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void rf_predict_kernel(const float* __restrict__ X, long m, long ld,
+                                                         const int* __restrict__ roots, int ntrees,
+                                                         const int* __restrict__ feature,
+                                                         const float* __restrict__ threshold,
+                                                         const int* __restrict__ left, const int* __restrict__ right,
+                                                         const int* __restrict__ value_off,
+                                                         const float* __restrict__ values, int S,
+                                                         float* __restrict__ out, int* __restrict__ leaves) {
+  const long r = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= m) return;
+  const float* row = X + r * ld;
+  float acc[32];
+#pragma unroll
+  for (int c = 0; c < 32; ++c) acc[c] = 0.f;
+  for (int t = 0; t < ntrees; ++t) {
+    int node = roots[t];
+    int f = feature[node];
+    while (f >= 0) {
+      node = (row[f] <= threshold[node]) ? left[node] : right[node];
+      f = feature[node];
+    }
+    if (leaves) leaves[r * ntrees + t] = node - roots[t];
+    const float* v = values + value_off[node];
+#pragma unroll
+    for (int c = 0; c < 32; ++c)
+      if (c < S) acc[c] += v[c];
+  }
+#pragma unroll
+  for (int c = 0; c < 32; ++c)
+    if (c < S) out[r * S + c] = acc[c];
+}
+
+SRML_API int srml_rf_predict(const float* X, long m, long ld, const int* roots, int ntrees, const int* feature,
+                             const float* threshold, const int* left, const int* right, const int* value_off,
+                             const float* values, int S, float* out, int* leaves, hipStream_t stream) {
+  if (m <= 0) return 0;
+  if (S > 32) return -7;
+  hipLaunchKernelGGL(rf_predict_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream, X, m, ld, roots,
+                     ntrees, feature, threshold, left, right, value_off, values, S, out, leaves);
+  return srml_status();
+}

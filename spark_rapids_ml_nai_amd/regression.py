@@ -42,27 +42,7 @@ from .core.params import (
 from .parallel.context import WorkerContext
 
 
-class _FeaturesColMixin:
-    def getFeaturesCol(self) -> Union[str, List[str]]:  # type: ignore[override]
-        if self.isDefined("featuresCols"):
-            return self.getOrDefault("featuresCols")
-        if self.isDefined("featuresCol"):
-            return self.getOrDefault("featuresCol")
-        raise RuntimeError("featuresCol is not set")
-
-    def setFeaturesCol(self, value: Union[str, List[str]]) -> Any:
-        if isinstance(value, str):
-            return self._set_params(featuresCol=value)
-        return self._set_params(featuresCols=value)
-
-    def setFeaturesCols(self, value: List[str]) -> Any:
-        return self._set_params(featuresCols=value)
-
-    def setLabelCol(self, value: str) -> Any:
-        return self._set_params(labelCol=value)
-
-    def setPredictionCol(self, value: str) -> Any:
-        return self._set_params(predictionCol=value)
+from .core.params import _FeaturesColMixin  # noqa: E402  (re-exported for tree.py / clustering.py)
 
 
 # ======================================================================================
@@ -293,3 +273,73 @@ class LinearRegressionModel(LinearRegressionClass, _ModelWithPredictionCol, _Lin
         first._copy_backend_params(out)
         out._combined_models = list(models)
         return out
+
+
+# ======================================================================================
+# RandomForestRegressor
+# ======================================================================================
+from .tree import _RandomForestEstimator, _RandomForestModel  # noqa: E402
+
+
+class RandomForestRegressor(_RandomForestEstimator):
+    """Random forest regressor (variance impurity) grown level-wise on MI355X."""
+
+    _is_classification = False
+
+    @classmethod
+    def _param_value_mapping(cls) -> Dict[str, Callable[[Any], Any]]:
+        m = dict(super()._param_value_mapping())
+        m["split_criterion"] = lambda x: {"variance": "mse", "mse": "mse"}.get(x)
+        return m
+
+    @keyword_only
+    def __init__(self, *, featuresCol: Union[str, List[str]] = "features", labelCol: str = "label",
+                 predictionCol: str = "prediction", maxDepth: int = 5, maxBins: int = 32,
+                 minInstancesPerNode: int = 1, minInfoGain: float = 0.0, maxMemoryInMB: int = 256,
+                 cacheNodeIds: bool = False, checkpointInterval: int = 10, impurity: str = "variance",
+                 subsamplingRate: float = 1.0, seed: Optional[int] = None, numTrees: int = 20,
+                 featureSubsetStrategy: str = "auto", leafCol: str = "", minWeightFractionPerNode: float = 0.0,
+                 weightCol: Optional[str] = None, bootstrap: Optional[bool] = True,
+                 num_workers: Optional[int] = None, verbose: Union[int, bool] = False, **kwargs: Any) -> None:
+        super().__init__()
+        self._setDefault(impurity="variance")
+        self._initialize_backend_params()
+        self._set_params(**self._input_kwargs)
+
+    def _supportsTransformEvaluate(self, evaluator: Any) -> bool:
+        return type(evaluator).__name__ == "RegressionEvaluator"
+
+    def _create_model(self, result: Dict[str, Any]) -> "RandomForestRegressionModel":
+        return RandomForestRegressionModel._from_row(result)
+
+
+class RandomForestRegressionModel(_RandomForestModel):
+    _is_classification = False
+
+    def predict(self, value: Any) -> float:
+        x = np.asarray(as_dense_array(value), dtype=np.float32).reshape(1, -1)
+        return float(self._raw_sum(x, torch.device("cpu")).numpy()[0, 0] / max(len(self._trees), 1))
+
+    def _get_transform_func(self, dataset: DataFrame) -> Tuple[Callable, Callable]:
+        pc = self.getPredictionCol()
+        T = max(len(self._trees), 1)
+
+        def construct(ctx: WorkerContext) -> Any:
+            self._pack(ctx.device)
+            return ctx.device
+
+        def predict(device: Any, X: Any, ctx: WorkerContext) -> Dict[str, np.ndarray]:
+            raw = self._raw_sum(X, ctx.device)
+            return {pc: (raw[:, 0] / T).cpu().numpy()}
+
+        return construct, predict
+
+    def evaluate(self, dataset: Any) -> Any:
+        from .core.dataframe import as_dataframe
+        from .metrics import RegressionMetrics, RegressionSummary
+
+        out = self.transform(dataset)
+        df, _ = as_dataframe(out)
+        y = df.to_numpy(self.getLabelCol(), np.float64)
+        p = df.to_numpy(self.getPredictionCol(), np.float64)
+        return LinearRegressionSummary(RegressionMetrics(RegressionSummary.from_arrays(y, p)), out)

@@ -133,3 +133,78 @@ def test_cluster_sums(gpu_device, m, n, k):
     ref = torch.zeros(k, n, dtype=torch.float64).index_add_(0, labels.long(), X.double().cpu())
     torch.testing.assert_close(sums.cpu(), ref, rtol=1e-4, atol=1e-3)
     assert torch.equal(counts.cpu(), torch.bincount(labels.long(), minlength=k))
+
+
+def _rf_setup(dev, m=5000, n=40, B=32, C=3, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    X = torch.randn(m, n, generator=g)
+    edges = torch.sort(X[torch.randperm(m, generator=g)[:1000]], 0).values[torch.linspace(30, 970, B - 1).long()].T.contiguous()
+    y = torch.randint(0, C, (m,), generator=g).float()
+    return X, edges, y
+
+
+def test_rf_quantize(gpu_device):
+    X, edges, _ = _rf_setup(gpu_device)
+    ref = ops.rf_quantize(X, edges)
+    got = ops.rf_quantize(X.to(gpu_device), edges.to(gpu_device)).cpu()
+    assert torch.equal(ref, got)
+
+
+@pytest.mark.parametrize("regression", [False, True])
+def test_rf_hist_split_route(gpu_device, regression):
+    X, edges, y = _rf_setup(gpu_device)
+    if regression:
+        y = X[:, 0] * 2 + 0.1 * torch.randn(X.shape[0], generator=torch.Generator().manual_seed(5))
+    S = 3
+    B = edges.shape[1] + 1
+    bins = ops.rf_quantize(X, edges)
+    m = X.shape[0]
+    w = torch.randint(0, 3, (m,), generator=torch.Generator().manual_seed(1)).to(torch.uint8)
+    idx = torch.nonzero(w).view(-1).int()
+    # two nodes: first 60% / rest of the in-bag rows
+    cut = int(0.6 * idx.shape[0])
+    feats = torch.stack([torch.randperm(40, generator=torch.Generator().manual_seed(s))[:12] for s in (2, 3)]).int()
+    items = []
+    for node, (rb, re) in enumerate([(0, cut), (cut, idx.shape[0])]):
+        for r0 in range(rb, re, 1000):
+            for fc in range(2):
+                items.append((node, r0, min(re, r0 + 1000), fc))
+    items = torch.tensor(items, dtype=torch.int32)
+    ref = ops.rf_hist(bins, idx, y, w, items, feats, 2, B, S, regression)
+    got = ops.rf_hist(bins.to(gpu_device), idx.to(gpu_device), y.to(gpu_device), w.to(gpu_device),
+                      items.to(gpu_device), feats.to(gpu_device), 2, B, S, regression).cpu()
+    torch.testing.assert_close(got.double(), ref.double(), rtol=1e-5, atol=1e-3)
+    crit = 2 if regression else 0
+    o_ref, t_ref = ops.rf_best_split(ref, B, S, regression, crit, 1.0, 0.0)
+    o_got, t_got = ops.rf_best_split(got.to(gpu_device), B, S, regression, crit, 1.0, 0.0)
+    torch.testing.assert_close(t_got.cpu(), t_ref, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(o_got.cpu()[:, 0], o_ref[:, 0], rtol=1e-5, atol=1e-8)
+    assert torch.equal(o_got.cpu()[:, 1:3], o_ref[:, 1:3])
+    seg = torch.cat([torch.zeros(cut, dtype=torch.int32), torch.ones(idx.shape[0] - cut, dtype=torch.int32)])
+    nf = torch.tensor([int(feats[0, int(o_ref[0, 1])]), -1], dtype=torch.int32)
+    nb = torch.tensor([int(o_ref[0, 2]), 0], dtype=torch.int32)
+    cb = torch.tensor([0, 0], dtype=torch.int32)
+    k_ref = ops.rf_route(bins, idx, seg, nf, nb, cb)
+    k_got = ops.rf_route(bins.to(gpu_device), idx.to(gpu_device), seg.to(gpu_device), nf.to(gpu_device),
+                         nb.to(gpu_device), cb.to(gpu_device)).cpu()
+    assert torch.equal(k_ref, k_got)
+
+
+def test_rf_predict(gpu_device):
+    from spark_rapids_ml_nai_amd.models.forest import pack_forest
+
+    trees = [
+        {"feature": [0, -1, 1, -1, -1], "threshold": [0.0, 0, 0.5, 0, 0], "left": [1, -1, 3, -1, -1],
+         "right": [2, -1, 4, -1, -1], "value": [[0, 0], [1, 0], [0, 0], [0.2, 0.8], [0, 1]]},
+        {"feature": [1, -1, -1], "threshold": [-0.3, 0, 0], "left": [1, -1, -1], "right": [2, -1, -1],
+         "value": [[0, 0], [0.6, 0.4], [0.1, 0.9]]},
+    ]
+    X = torch.randn(1000, 3, generator=torch.Generator().manual_seed(0))
+    pc = pack_forest(trees, 2, torch.device("cpu"))
+    pg = pack_forest(trees, 2, gpu_device)
+    r_ref, l_ref = ops.rf_predict(X, pc["roots"], pc["feature"], pc["threshold"], pc["left"], pc["right"],
+                                  pc["value_off"], pc["values"], 2, True)
+    r_got, l_got = ops.rf_predict(X.to(gpu_device), pg["roots"], pg["feature"], pg["threshold"], pg["left"],
+                                  pg["right"], pg["value_off"], pg["values"], 2, True)
+    torch.testing.assert_close(r_got.cpu(), r_ref)
+    assert torch.equal(l_got.cpu(), l_ref)
