@@ -178,26 +178,22 @@ def grow_tree(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: Wor
     counts = np.array([int(idx.shape[0])], dtype=np.int64)
     depth = 0
     n_leaves = 1
+    # root totals (weighted class counts / regression moments); deeper levels inherit their
+    # totals from the parent's winning split (prefix of its histogram), no pass over the rows
+    wr = w[idx.long()].double()
+    if regression:
+        yr = yv[idx.long()].double()
+        tot = torch.stack([wr.sum(), (wr * yr).sum(), (wr * yr * yr).sum()]).view(1, 3)
+    else:
+        tot = torch.bincount(yv[idx.long()].long(), weights=wr, minlength=S)[:S].double().view(1, S)
+    if data_parallel:
+        ctx.comm.allreduce(tot)
+    nfc = (nf + 7) // 8
     while level_nodes:
         L = len(level_nodes)
         total = int(counts.sum())
-        # node totals for every node of the level (weighted class counts / regression moments)
         seg_node = torch.repeat_interleave(torch.arange(L, device=dev, dtype=torch.int32),
                                            torch.from_numpy(counts).to(dev))
-        rows = idx[:total].long()
-        wr = w[rows].double()
-        if regression:
-            yr = yv[rows].double()
-            tot = torch.zeros((L, 3), dtype=torch.float64, device=dev)
-            tot[:, 0].index_add_(0, seg_node.long(), wr)
-            tot[:, 1].index_add_(0, seg_node.long(), wr * yr)
-            tot[:, 2].index_add_(0, seg_node.long(), wr * yr * yr)
-        else:
-            tot = torch.zeros((L * S,), dtype=torch.float64, device=dev)
-            tot.index_add_(0, seg_node.long() * S + yv[rows].long(), wr)
-            tot = tot.view(L, S)
-        if data_parallel:
-            ctx.comm.allreduce(tot)
         tot_h = tot.cpu().numpy()
         wsum = tot_h[:, 0] if regression else tot_h.sum(1)
         for j, nid in enumerate(level_nodes):
@@ -216,16 +212,25 @@ def grow_tree(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: Wor
             feats = torch.arange(n, device=dev, dtype=torch.int32).repeat(C, 1)
         else:
             feats = torch.rand((C, n), generator=gen, device=dev).argsort(1)[:, :nf].to(torch.int32).contiguous()
-        # work items (node slot, row begin, row end, feature chunk)
-        items = []
-        nfc = (nf + 7) // 8
-        for ci, j in enumerate(cand):
-            s0, c0 = int(starts[j]), int(counts[j])
-            for rb in range(s0, s0 + c0, ROWS_PER_ITEM):
-                re = min(s0 + c0, rb + ROWS_PER_ITEM)
-                for fc in range(nfc):
-                    items.append((ci, rb, re, fc))
-        items_t = torch.tensor(items, dtype=torch.int32).view(-1, 4).to(dev) if items else torch.zeros((0, 4), dtype=torch.int32, device=dev)
+        # work items (node slot, row begin, row end, feature chunk), built vectorised
+        cand_a = np.asarray(cand, dtype=np.int64)
+        c_start, c_cnt = starts[cand_a], counts[cand_a]
+        nch = (c_cnt + ROWS_PER_ITEM - 1) // ROWS_PER_ITEM
+        tot_ch = int(nch.sum())
+        if tot_ch:
+            node_rep = np.repeat(np.arange(C), nch)
+            first = np.repeat(np.cumsum(nch) - nch, nch)
+            chunk = np.arange(tot_ch) - first
+            rb = c_start[node_rep] + chunk * ROWS_PER_ITEM
+            re = np.minimum(rb + ROWS_PER_ITEM, c_start[node_rep] + c_cnt[node_rep])
+            it = np.empty((tot_ch * nfc, 4), dtype=np.int32)
+            it[:, 0] = np.repeat(node_rep, nfc)
+            it[:, 1] = np.repeat(rb, nfc)
+            it[:, 2] = np.repeat(re, nfc)
+            it[:, 3] = np.tile(np.arange(nfc), tot_ch)
+            items_t = torch.from_numpy(it).to(dev)
+        else:
+            items_t = torch.zeros((0, 4), dtype=torch.int32, device=dev)
         hist = ops.rf_hist(bins, idx, yv, w, items_t, feats, C, B, S, regression)
         if data_parallel:
             ctx.comm.allreduce(hist)
@@ -243,9 +248,17 @@ def grow_tree(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: Wor
         child_base = np.zeros(L, dtype=np.int32)
         next_nodes: List[int] = []
         k = 0
+        split_ci: List[int] = []
+        split_slot: List[int] = []
+        split_bin: List[int] = []
+        split_j: List[int] = []
         for ci, j in enumerate(cand):
             if ci not in split_set:
                 continue
+            split_ci.append(ci)
+            split_slot.append(int(out_h[ci, 1]))
+            split_bin.append(int(out_h[ci, 2]))
+            split_j.append(j)
             nid = level_nodes[j]
             slot = int(out_h[ci, 1])
             b = int(out_h[ci, 2])
@@ -263,6 +276,12 @@ def grow_tree(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: Wor
             n_leaves += 1
         if k == 0:
             break
+        # children totals = prefix of the winning feature's histogram up to the split bin
+        ci_t = torch.tensor(split_ci, device=dev)
+        sel = hist[ci_t, torch.tensor(split_slot, device=dev)].double()  # (k, B, S)
+        left = sel.cumsum(1)[torch.arange(k, device=dev), torch.tensor(split_bin, device=dev)]
+        right = tot[torch.tensor(split_j, device=dev)] - left
+        tot = torch.stack([left, right], 1).reshape(2 * k, S)
         keys = ops.rf_route(bins, idx[:total].contiguous(), seg_node.contiguous(),
                             torch.from_numpy(node_feature).to(dev), torch.from_numpy(node_bin).to(dev),
                             torch.from_numpy(child_base).to(dev))

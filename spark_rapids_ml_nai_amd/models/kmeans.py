@@ -111,10 +111,20 @@ def init_kmeans_parallel(X: torch.Tensor, xnorm: torch.Tensor, desc: PartitionDe
     if C.shape[0] <= k:
         extra = init_random(X, desc, ctx, k - C.shape[0], seed + 1) if C.shape[0] < k else None
         return torch.cat([C, extra], 0) if extra is not None else C
+    # the candidate set is tiny (~ steps * oversampling * k points): run a few seeded k-means++
+    # + weighted Lloyd trials on it and keep the lowest weighted cost (deterministic per seed)
     g2 = torch.Generator(device=dev)
     g2.manual_seed(int(seed))
-    C0 = _weighted_kmeanspp(C, w, k, g2)
-    return _weighted_lloyd(C, w, C0)
+    Cf = C.float().contiguous()
+    cn = ops.row_sqnorm(Cf) if Cf.is_cuda else (Cf * Cf).sum(1)
+    best, best_cost = None, float("inf")
+    for _ in range(5):
+        Ct = _weighted_lloyd(C, w, _weighted_kmeanspp(C, w, k, g2))
+        _, d2 = ops.nearest_centroid(Cf, Ct.float(), cn)
+        cost = float((d2.double() * w).sum().item())
+        if cost < best_cost:
+            best, best_cost = Ct, cost
+    return best
 
 
 def kmeans_fit(X: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext, k: int, max_iter: int, tol: float,
