@@ -84,9 +84,9 @@ def run_barrier_job(
     world = len(per_rank_inputs)
     if use_gpu is None:
         use_gpu = gpu_available()
-    # fork is cheap and safe while this (driver) process has not touched the GPU; GPU ranks
-    # always spawn so each gets a clean HIP runtime.
-    method = "spawn" if use_gpu else "fork"
+    # always spawn: forking a process whose torch CPU thread pool (OpenMP) or HIP runtime is
+    # already initialised deadlocks the child inside its first parallel op
+    method = os.environ.get("SRML_MP_START", "spawn")
     mpctx = mp.get_context(method)
     q = mpctx.Queue()
     port = free_port()
@@ -101,12 +101,23 @@ def run_barrier_job(
     got = 0
     import queue as _queue
 
+    import time as _time
+
+    deadline = _time.monotonic() + timeout_s
     while got < world:
         try:
-            rank, status, body = q.get(timeout=timeout_s)
+            rank, status, body = q.get(timeout=1.0)
         except _queue.Empty:
-            errors.append("barrier job timed out after %.0fs" % timeout_s)
-            break
+            # watchdog: a rank that died without reporting fails the whole barrier stage
+            dead = [i for i, p in enumerate(procs) if not p.is_alive() and p.exitcode not in (0, None)]
+            if dead:
+                errors.append("rank(s) %s exited with code(s) %s before reporting"
+                              % (dead, [procs[i].exitcode for i in dead]))
+                break
+            if _time.monotonic() > deadline:
+                errors.append("barrier job timed out after %.0fs" % timeout_s)
+                break
+            continue
         got += 1
         if status == "ok":
             results[rank] = cloudpickle.loads(body)

@@ -1,0 +1,93 @@
+"""Multi-rank correctness on CPU ranks (gloo, world_size 2) through the LocalBarrierRunner —
+the same worker closures that run one-rank-per-MI355X over RCCL. Oracle: the single-rank fit on
+the same data (reference test strategy: multi-GPU vs single-GPU cuML, tests/test_pca.py:307-355,
+tests/test_kmeans.py:257-330, tests/test_random_forest.py:322-417)."""
+import os
+import warnings
+
+import numpy as np
+import pytest
+
+from spark_rapids_ml_nai_amd import DataFrame
+
+warnings.filterwarnings("ignore")
+pytestmark = pytest.mark.dist
+
+
+@pytest.fixture(autouse=True)
+def _cpu(monkeypatch):
+    monkeypatch.setenv("SRML_FORCE_CPU", "1")
+
+
+def _data(m=2000, n=12, seed=0):
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((m, n)).astype(np.float32) * rng.uniform(0.5, 3, n).astype(np.float32) + 2.0
+    return X
+
+
+def test_pca_two_ranks():
+    from spark_rapids_ml_nai_amd.feature import PCA
+
+    X = _data()
+    df = DataFrame.from_numpy(X, num_partitions=2)
+    m1 = PCA(k=3, inputCol="features", num_workers=1).fit(df)
+    m2 = PCA(k=3, inputCol="features", num_workers=2).fit(df)
+    assert np.allclose(m1.mean, m2.mean, atol=1e-5)
+    assert np.allclose(np.abs(m1.components_), np.abs(m2.components_), atol=1e-4)
+    assert np.allclose(m1.explained_variance_ratio_, m2.explained_variance_ratio_, atol=1e-6)
+    assert np.allclose(m1.singular_values_, m2.singular_values_, rtol=1e-5)
+
+
+def test_linear_regression_two_ranks():
+    from spark_rapids_ml_nai_amd.regression import LinearRegression
+
+    X = _data(seed=1)
+    y = X @ np.arange(1, 13, dtype=np.float32) + 0.5
+    df = DataFrame.from_numpy(X, y, num_partitions=2)
+    for kw in (dict(regParam=0.0), dict(regParam=0.1, elasticNetParam=0.0), dict(regParam=0.05, elasticNetParam=0.5)):
+        a = LinearRegression(num_workers=1, **kw).fit(df)
+        b = LinearRegression(num_workers=2, **kw).fit(df)
+        assert np.allclose(a.coefficients.toArray(), b.coefficients.toArray(), rtol=1e-5, atol=1e-5)
+        assert np.isclose(a.intercept, b.intercept, rtol=1e-5, atol=1e-4)
+
+
+def test_kmeans_two_ranks():
+    from spark_rapids_ml_nai_amd.clustering import KMeans
+
+    rng = np.random.default_rng(3)
+    C = rng.uniform(-20, 20, (5, 4))
+    X = (C[rng.integers(0, 5, 3000)] + rng.standard_normal((3000, 4))).astype(np.float32)
+    df = DataFrame.from_numpy(X, num_partitions=2)
+    a = KMeans(k=5, seed=1, maxIter=50, num_workers=1).fit(df)
+    b = KMeans(k=5, seed=1, maxIter=50, num_workers=2).fit(df)
+    ca = np.array(sorted(a.clusterCenters(), key=lambda c: tuple(c)))
+    cb = np.array(sorted(b.clusterCenters(), key=lambda c: tuple(c)))
+    assert np.allclose(ca, cb, atol=1e-3)
+
+
+def test_logistic_regression_two_ranks():
+    from spark_rapids_ml_nai_amd.classification import LogisticRegression
+
+    X = _data(seed=4)
+    y = (X[:, 0] - 2 + 0.5 * X[:, 1] > 1.0).astype(np.float64)
+    df = DataFrame.from_numpy(X, y, num_partitions=2)
+    a = LogisticRegression(regParam=0.01, num_workers=1).fit(df)
+    b = LogisticRegression(regParam=0.01, num_workers=2).fit(df)
+    assert np.allclose(a.coefficients.toArray(), b.coefficients.toArray(), atol=1e-4)
+    assert np.isclose(a.intercept, b.intercept, atol=1e-4)
+
+
+@pytest.mark.parametrize("mode", ["ensemble", "data_parallel"])
+def test_random_forest_two_ranks(mode):
+    from sklearn.datasets import make_classification
+
+    from spark_rapids_ml_nai_amd.classification import RandomForestClassifier
+
+    X, y = make_classification(n_samples=3000, n_features=10, n_informative=6, random_state=0)
+    df = DataFrame.from_numpy(X.astype(np.float32), y.astype(float), num_partitions=2)
+    a = RandomForestClassifier(numTrees=6, maxDepth=6, seed=7, num_workers=1).fit(df)
+    b = RandomForestClassifier(numTrees=6, maxDepth=6, seed=7, num_workers=2, split_mode=mode).fit(df)
+    assert b.getNumTrees == 6
+    acc = lambda m: (m.transform(df).to_numpy("prediction") == y).mean()
+    # reference gate: multi-worker accuracy within 0.07 of single worker
+    assert abs(acc(a) - acc(b)) < 0.07
