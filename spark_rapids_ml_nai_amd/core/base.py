@@ -371,6 +371,26 @@ def run_fit_job(est: _Estimator, df: DataFrame, fit_fn: Callable, params: Dict[s
     return results[0]
 
 
+def run_worker_job(fn: Callable[[WorkerContext, Any], Any], payloads: Sequence[Any]) -> List[Any]:
+    """Run ``fn(ctx, payload)`` once per worker and return every rank's result.
+
+    SPMD (torch.distributed already initialised): this process is one rank and ``payloads``
+    holds only its own entry. Otherwise one payload runs in-process and several run as a
+    LocalBarrierRunner stage (one process per GPU).
+    """
+    if spmd_active():
+        ctx = current_context() or WorkerContext.from_process_group()
+        with use_context(ctx):
+            return [fn(ctx, payloads[0])]
+    if len(payloads) <= 1:
+        ctx = current_context() or WorkerContext.single()
+        with use_context(ctx):
+            return [fn(ctx, payloads[0])]
+    from ..parallel.launcher import run_barrier_job
+
+    return run_barrier_job(fn, list(payloads))
+
+
 class _FitMultipleIterator:
     """Thread-safe iterator that fits every param map in ONE job on first ``next()``."""
 

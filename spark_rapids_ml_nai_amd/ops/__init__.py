@@ -416,3 +416,81 @@ def rf_predict(X: torch.Tensor, roots: torch.Tensor, feature: torch.Tensor, thre
                 threshold.data_ptr(), left.data_ptr(), right.data_ptr(), value_off.data_ptr(), values.data_ptr(), S,
                 out.data_ptr(), leaves.data_ptr() if leaves is not None else None, native.stream(X.device))
     return out, leaves
+
+
+# ------------------------------------------------------------------------------------------
+# Nearest-neighbour search
+# ------------------------------------------------------------------------------------------
+KNN_KMAX = 64
+
+
+def knn(Q: torch.Tensor, I: torch.Tensor, k: int, inorm: Optional[torch.Tensor] = None,
+        qnorm: Optional[torch.Tensor] = None, id_offset: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Exact k nearest items of every query: (squared L2 distances fp32 [mq, k], item ids int64 [mq, k])."""
+    mq, n = Q.shape
+    mi = I.shape[0]
+    kk = min(k, mi)
+    if inorm is None:
+        inorm = row_sqnorm(I)
+    if qnorm is None:
+        qnorm = row_sqnorm(Q)
+    if not Q.is_cuda or Q.dtype != torch.float32 or k > KNN_KMAX:
+        Qf, If = Q.float(), I.float()
+        outs_d, outs_i = [], []
+        bs = max(1, (1 << 25) // max(mi, 1))
+        for s in range(0, mq, bs):
+            d = (qnorm[s: s + bs].float().view(-1, 1) + inorm.float().view(1, -1) - 2.0 * (Qf[s: s + bs] @ If.T))
+            v, i = torch.topk(d, kk, dim=1, largest=False)
+            outs_d.append(v.clamp_min(0))
+            outs_i.append(i + id_offset)
+        return torch.cat(outs_d), torch.cat(outs_i)
+    Q = _c(Q)
+    I = _c(I.to(torch.float32))
+    inorm = _c(inorm.float())
+    # enough item slices that the grid covers the chip for small query sets
+    qblocks = (mq + 127) // 128
+    slices = max(1, min((mi + 4095) // 4096, (1024 + qblocks - 1) // qblocks))
+    od = torch.empty((mq, slices, kk), dtype=torch.float32, device=Q.device)
+    oi = torch.empty((mq, slices, kk), dtype=torch.int64, device=Q.device)
+    native.call("srml_knn_f32", Q.data_ptr(), mq, n, Q.stride(0), I.data_ptr(), mi, I.stride(0), inorm.data_ptr(), kk,
+                slices, od.data_ptr(), oi.data_ptr(), int(id_offset), native.stream(Q.device))
+    od = od.view(mq, slices * kk)
+    oi = oi.view(mq, slices * kk)
+    if slices > 1:
+        v, j = torch.topk(od, kk, dim=1, largest=False)
+        oi = oi.gather(1, j)
+        od = v
+    return (od + qnorm.float().view(-1, 1)).clamp_min(0), oi
+
+
+def ivf_search(Q: torch.Tensor, probes: torch.Tensor, list_off: torch.Tensor, items: torch.Tensor,
+               inorm: torch.Tensor, ids: torch.Tensor, k: int, qnorm: Optional[torch.Tensor] = None
+               ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """IVF-Flat scan of each query's probed lists: (squared L2 [nq, k], ids int64 [nq, k])."""
+    nq, n = Q.shape
+    if qnorm is None:
+        qnorm = row_sqnorm(Q)
+    if not Q.is_cuda or Q.dtype != torch.float32 or k > KNN_KMAX:
+        od = torch.full((nq, k), float("inf"), dtype=torch.float32, device=Q.device)
+        oi = torch.full((nq, k), -1, dtype=torch.int64, device=Q.device)
+        lo = list_off.cpu().numpy()
+        pr = probes.cpu().numpy()
+        for q in range(nq):
+            rows = [torch.arange(int(lo[l]), int(lo[l + 1]), device=Q.device) for l in pr[q] if l >= 0]
+            if not rows:
+                continue
+            r = torch.cat(rows)
+            d = inorm[r].float() - 2.0 * (items[r].float() @ Q[q].float())
+            kk = min(k, d.shape[0])
+            v, j = torch.topk(d, kk, largest=False)
+            od[q, :kk] = v
+            oi[q, :kk] = ids[r[j]]
+        return (od + qnorm.float().view(-1, 1)).clamp_min(0), oi
+    Q = _c(Q)
+    od = torch.empty((nq, k), dtype=torch.float32, device=Q.device)
+    oi = torch.empty((nq, k), dtype=torch.int64, device=Q.device)
+    native.call("srml_ivf_search_f32", Q.data_ptr(), nq, n, Q.stride(0), _c(probes.int()).data_ptr(),
+                int(probes.shape[1]), _c(list_off.long()).data_ptr(), _c(items).data_ptr(), items.stride(0),
+                _c(inorm.float()).data_ptr(), _c(ids.long()).data_ptr(), k, od.data_ptr(), oi.data_ptr(),
+                native.stream(Q.device))
+    return (od + qnorm.float().view(-1, 1)).clamp_min(0), oi

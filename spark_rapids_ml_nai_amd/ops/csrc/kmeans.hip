@@ -237,7 +237,247 @@ __global__ __launch_bounds__(256) void accumulate_global_kernel(const float* __r
     for (int d = lane; d < n; d += 64) atomicAdd(&dst[d], row[d]);
   }
 }
+// ------------------------------------------------------------------------------------------
+// Exact k-nearest-neighbours: fused MFMA distance tiles + per-query top-k in LDS.
+// Block = 128 queries x one slice of the item range; the query tile's top-k list lives in LDS
+// for the whole item sweep, so the q x items distance matrix is never materialised (reference:
+// cuML NearestNeighborsMG brute force, knn.py:638-749). After each 128x128 MFMA tile the
+// partial distances (||i||^2 - 2 q.i) go through the (reused) staging LDS and 128 threads each
+// merge one query row with a threshold test + insertion into a sorted list (most candidates are
+// rejected by the threshold after the first tiles). Item-range slices (grid.y) keep >= 512
+// blocks in flight for small query sets; slices are merged by the caller.
+// ------------------------------------------------------------------------------------------
+constexpr int KNN_KMAX = 64;
+
+template <bool VEC>
+__global__ __launch_bounds__(256, 1) void knn_kernel(const float* __restrict__ Q, long mq, int n, long ldq,
+                                                     const float* __restrict__ I, long mi, long ldi,
+                                                     const float* __restrict__ inorm, int k, long items_per_slice,
+                                                     float* __restrict__ out_d, long long* __restrict__ out_i,
+                                                     long long id_offset) {
+  constexpr int BM = 128, BN = 128, MT = 2, NT = 2;
+  union Smem {
+    struct {
+      float Xs[2][BM][PADK];
+      float Cs[2][BN][PADK];
+    } st;
+    float D[BM][BN + 1];
+  };
+  __shared__ Smem sm;
+  // +1 pad: thread t walks row t, so an unpadded 64-word stride would put every thread on one bank
+  __shared__ float topd[BM][KNN_KMAX + 1];
+  __shared__ int topi[BM][KNN_KMAX + 1];
+  const long q0 = (long)blockIdx.x * BM;
+  const long slice = blockIdx.y;
+  const long ibeg = slice * items_per_slice;
+  const long iend = min(mi, ibeg + items_per_slice);
+  const int t = threadIdx.x;
+  const int lane = t & 63, wid = t >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int li = lane & 31, lk = lane >> 5;
+  for (int i = t; i < BM * (KNN_KMAX + 1); i += 256) {
+    (&topd[0][0])[i] = __builtin_huge_valf();
+    (&topi[0][0])[i] = -1;
+  }
+  const int nk = (n + BK - 1) / BK;
+  for (long c0 = ibeg; c0 < iend; c0 += BN) {
+    floatx16 acc[MT][NT];
+#pragma unroll
+    for (int a = 0; a < MT; ++a)
+#pragma unroll
+      for (int b = 0; b < NT; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+    RowTile<BM, VEC> xt;
+    RowTile<BN, VEC> ct;
+    xt.load(Q, ldq, mq, n, q0, 0);
+    ct.load(I, ldi, iend, n, c0, 0);
+    __syncthreads();  // previous tile's top-k scan has finished with sm.D
+    xt.store(sm.st.Xs[0]);
+    ct.store(sm.st.Cs[0]);
+    __syncthreads();
+    int cur = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool more = kt + 1 < nk;
+      if (more) {
+        xt.load(Q, ldq, mq, n, q0, (kt + 1) * BK);
+        ct.load(I, ldi, iend, n, c0, (kt + 1) * BK);
+      }
+#pragma unroll
+      for (int kk = 0; kk < BK / 2; ++kk) {
+        const int kx = 2 * kk + lk;
+        float a[MT], b[NT];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) a[mt] = sm.st.Xs[cur][wm * MT * 32 + mt * 32 + li][kx];
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) b[nt] = sm.st.Cs[cur][wn * NT * 32 + nt * 32 + li][kx];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt)
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
+      }
+      if (more) {
+        xt.store(sm.st.Xs[cur ^ 1]);
+        ct.store(sm.st.Cs[cur ^ 1]);
+      }
+      __syncthreads();
+      cur ^= 1;
+    }
+    // partial distances -> LDS tile (staging buffers are dead now)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int cl = wn * NT * 32 + nt * 32 + li;
+      const long cg = c0 + cl;
+      const float in = cg < iend ? inorm[cg] : 0.f;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rl = wm * MT * 32 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+          sm.D[rl][cl] = cg < iend ? fmaf(-2.f, acc[mt][nt][r], in) : __builtin_huge_valf();
+        }
+    }
+    __syncthreads();
+    if (t < BM) {
+      float thr = topd[t][k - 1];
+      const int ncol = (int)min((long)BN, iend - c0);
+      for (int c = 0; c < ncol; ++c) {
+        const float d = sm.D[t][c];
+        if (d < thr) {
+          int p = k - 1;
+          while (p > 0 && topd[t][p - 1] > d) {
+            topd[t][p] = topd[t][p - 1];
+            topi[t][p] = topi[t][p - 1];
+            --p;
+          }
+          topd[t][p] = d;
+          topi[t][p] = (int)(c0 + c - ibeg);
+          thr = topd[t][k - 1];
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (t < BM && q0 + t < mq) {
+    const long base = ((q0 + t) * gridDim.y + slice) * (long)k;
+    for (int j = 0; j < k; ++j) {
+      out_d[base + j] = topd[t][j];
+      out_i[base + j] = topi[t][j] >= 0 ? (long long)topi[t][j] + ibeg + id_offset : -1;
+    }
+  }
+}
+
 }  // namespace
+
+// ------------------------------------------------------------------------------------------
+// IVF-Flat search: one block per query; the query's nprobe inverted lists (items pre-sorted by
+// list, contiguous) are swept by the 4 waves, one item per wave step: lanes split the feature
+// dimension (16-B loads), the dot product is a DPP wave reduction, and a wave-private sorted
+// top-k list in LDS takes the candidate when it beats the list's threshold. The four lists are
+// merged at the end (reference: cuML NearestNeighbors(algorithm="ivfflat"), knn.py:1295-1380).
+// ------------------------------------------------------------------------------------------
+namespace {
+__global__ __launch_bounds__(256) void ivf_search_kernel(const float* __restrict__ Q, long nq, int n, long ldq,
+                                                         const int* __restrict__ probes, int nprobe,
+                                                         const long long* __restrict__ list_off,
+                                                         const float* __restrict__ items, long ldi,
+                                                         const float* __restrict__ inorm,
+                                                         const long long* __restrict__ ids, int k,
+                                                         float* __restrict__ out_d, long long* __restrict__ out_i) {
+  extern __shared__ __attribute__((aligned(16))) float qs[];  // n floats (padded to 4)
+  __shared__ float wd[4][KNN_KMAX];
+  __shared__ long long wi[4][KNN_KMAX];
+  const long q = blockIdx.x;
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  for (int d = t; d < n; d += 256) qs[d] = Q[q * ldq + d];
+  for (int j = t; j < 4 * KNN_KMAX; j += 256) {
+    (&wd[0][0])[j] = __builtin_huge_valf();
+    (&wi[0][0])[j] = -1;
+  }
+  __syncthreads();
+  float thr = __builtin_huge_valf();
+  const bool vec = ((n & 3) == 0) && ((ldi & 3) == 0);
+  for (int p = 0; p < nprobe; ++p) {
+    const int l = probes[q * nprobe + p];
+    if (l < 0) continue;
+    const long s = list_off[l], e = list_off[l + 1];
+    for (long j = s + wid; j < e; j += 4) {
+      const float* row = items + j * ldi;
+      float acc = 0.f;
+      if (vec) {
+        for (int d = lane * 4; d < n; d += 256) {
+          const floatx4 x = *reinterpret_cast<const floatx4*>(row + d);
+          acc = fmaf(x[0], qs[d], fmaf(x[1], qs[d + 1], fmaf(x[2], qs[d + 2], fmaf(x[3], qs[d + 3], acc))));
+        }
+      } else {
+        for (int d = lane; d < n; d += 64) acc = fmaf(row[d], qs[d], acc);
+      }
+      const float dist = fmaf(-2.f, wave_sum(acc), inorm[j]);
+      if (dist < thr) {  // wave-uniform
+        if (lane == 0) {
+          int pos = k - 1;
+          while (pos > 0 && wd[wid][pos - 1] > dist) {
+            wd[wid][pos] = wd[wid][pos - 1];
+            wi[wid][pos] = wi[wid][pos - 1];
+            --pos;
+          }
+          wd[wid][pos] = dist;
+          wi[wid][pos] = ids[j];
+        }
+        __builtin_amdgcn_wave_barrier();
+        thr = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(wd[wid][k - 1])));
+      }
+    }
+  }
+  __syncthreads();
+  if (t == 0) {  // 4-way merge of the wave lists
+    int h[4] = {0, 0, 0, 0};
+    for (int j = 0; j < k; ++j) {
+      int bw = 0;
+      float bd = wd[0][h[0]];
+      for (int w = 1; w < 4; ++w)
+        if (wd[w][h[w]] < bd) { bd = wd[w][h[w]]; bw = w; }
+      out_d[q * k + j] = bd;
+      out_i[q * k + j] = wi[bw][h[bw]];
+      if (h[bw] < k - 1) ++h[bw]; else wd[bw][h[bw]] = __builtin_huge_valf();
+    }
+  }
+}
+}  // namespace
+
+SRML_API int srml_ivf_search_f32(const float* Q, long nq, int n, long ldq, const int* probes, int nprobe,
+                                 const long long* list_off, const float* items, long ldi, const float* inorm,
+                                 const long long* ids, int k, float* out_d, long long* out_i, hipStream_t stream) {
+  if (nq <= 0) return 0;
+  if (k < 1 || k > KNN_KMAX) return -8;
+  const size_t lds = (size_t)((n + 3) / 4) * 4 * sizeof(float);
+  hipLaunchKernelGGL(ivf_search_kernel, dim3((unsigned)nq), dim3(256), lds, stream, Q, nq, n, ldq, probes, nprobe,
+                     list_off, items, ldi, inorm, ids, k, out_d, out_i);
+  return srml_status();
+}
+
+// out_d / out_i: (mq, slices, k) partial top-k (distance WITHOUT the ||q||^2 term)
+SRML_API int srml_knn_f32(const float* Q, long mq, int n, long ldq, const float* I, long mi, long ldi,
+                          const float* inorm, int k, int slices, float* out_d, long long* out_i, long long id_offset,
+                          hipStream_t stream) {
+  if (mq <= 0) return 0;
+  if (k < 1 || k > KNN_KMAX) return -8;
+  const bool vec = ((ldq & 3) == 0) && ((ldi & 3) == 0) && ((n & 3) == 0) &&
+                   ((reinterpret_cast<uintptr_t>(Q) & 15) == 0) && ((reinterpret_cast<uintptr_t>(I) & 15) == 0);
+  if (slices < 1) slices = 1;
+  long per = (mi + slices - 1) / slices;
+  per = ((per + 127) / 128) * 128;
+  if (per < 128) per = 128;
+  dim3 grid(ceil_div(mq, 128), (unsigned)slices);
+  if (vec)
+    hipLaunchKernelGGL(knn_kernel<true>, grid, dim3(256), 0, stream, Q, mq, n, ldq, I, mi, ldi, inorm, k, per, out_d,
+                       out_i, id_offset);
+  else
+    hipLaunchKernelGGL(knn_kernel<false>, grid, dim3(256), 0, stream, Q, mq, n, ldq, I, mi, ldi, inorm, k, per,
+                       out_d, out_i, id_offset);
+  return srml_status();
+}
 
 SRML_API int srml_nearest_centroid_f32(const float* X, long m, int n, long ldx, const float* C, int k, long ldc,
                                        const float* cnorm, unsigned long long* best, hipStream_t stream) {

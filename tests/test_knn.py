@@ -1,0 +1,162 @@
+"""Exact kNN and IVF-Flat ANN (reference tests/test_nearest_neighbors.py,
+tests/test_approximate_nearest_neighbors.py). Oracle: sklearn brute-force NearestNeighbors."""
+import warnings
+
+import numpy as np
+import pytest
+from sklearn.neighbors import NearestNeighbors as SkNN
+
+from spark_rapids_ml_nai_amd import DataFrame
+from spark_rapids_ml_nai_amd.knn import (
+    ApproximateNearestNeighbors,
+    ApproximateNearestNeighborsModel,
+    NearestNeighbors,
+    NearestNeighborsModel,
+)
+
+warnings.filterwarnings("ignore")
+
+
+def _blobs(m=1500, n=16, centers=12, seed=0):
+    rng = np.random.default_rng(seed)
+    C = rng.uniform(-10, 10, (centers, n))
+    return (C[rng.integers(0, centers, m)] + rng.standard_normal((m, n))).astype(np.float32)
+
+
+def _knn_arrays(knn_df, id_name="unique_id"):
+    t = knn_df.toPandas()
+    return (t["query_" + id_name].to_numpy(), np.stack([np.asarray(v) for v in t["indices"]]),
+            np.stack([np.asarray(v) for v in t["distances"]]))
+
+
+def test_params_and_mapping():
+    nn = NearestNeighbors(k=7, inputCol="features")
+    assert nn.getK() == 7
+    assert nn.cuml_params["n_neighbors"] == 7
+    ann = ApproximateNearestNeighbors(k=3, algoParams={"nlist": 4, "nprobe": 2}, metric="sqeuclidean")
+    assert ann.getAlgorithm() == "ivfflat"
+    assert ann.cuml_params["algo_params"] == {"nlist": 4, "nprobe": 2}
+    assert ann.cuml_params["metric"] == "sqeuclidean"
+    with pytest.raises(NotImplementedError):
+        nn.write()
+    with pytest.raises(NotImplementedError):
+        NearestNeighborsModel.load("/tmp/x")
+
+
+def test_exact_knn_matches_sklearn():
+    X = _blobs()
+    Q = X[:200] + 0.01
+    items = DataFrame.from_numpy(X, num_partitions=3)
+    queries = DataFrame.from_numpy(Q, num_partitions=2)
+    model = NearestNeighbors(k=6, inputCol="features").fit(items)
+    item_df, query_df, knn_df = model.kneighbors(queries)
+    assert "unique_id" in item_df.columns and "unique_id" in query_df.columns
+    qid, ind, dist = _knn_arrays(knn_df)
+    assert np.all(np.diff(qid) > 0)
+    d_ref, i_ref = SkNN(n_neighbors=6, algorithm="brute").fit(X).kneighbors(Q)
+    assert np.allclose(dist, d_ref, rtol=1e-4, atol=1e-3)
+    # ids may differ only among exact ties
+    assert (ind == i_ref).mean() > 0.99
+
+
+def test_exact_knn_user_id_and_join():
+    X = _blobs(m=300, n=8, seed=2)
+    ids = np.arange(300) * 10 + 5
+    items = DataFrame.from_numpy(X, extra={"id": ids})
+    model = NearestNeighbors(k=3, inputCol="features", idCol="id").fit(items)
+    _, _, knn_df = model.kneighbors(items)
+    qid, ind, dist = _knn_arrays(knn_df, "id")
+    assert np.array_equal(ind[:, 0], qid)  # every item is its own nearest neighbour
+    assert np.allclose(dist[:, 0], 0, atol=1e-3)
+    join = model.exactNearestNeighborsJoin(items, distCol="dist")
+    assert join.columns == ["item_df", "query_df", "dist"]
+    assert join.count() == 300 * 3
+    rows = join.collect()
+    r = rows[0]
+    q = np.asarray(r["query_df"]["features"])
+    it = np.asarray(r["item_df"]["features"])
+    assert np.isclose(np.linalg.norm(q - it), r["dist"], atol=1e-3)
+
+
+def test_exact_knn_k_larger_than_items():
+    X = _blobs(m=4, n=3)
+    model = NearestNeighbors(k=6, inputCol="features").fit(DataFrame.from_numpy(X))
+    _, _, knn_df = model.kneighbors(DataFrame.from_numpy(X[:2]))
+    _, ind, _ = _knn_arrays(knn_df)
+    assert ind.shape == (2, 4)
+
+
+@pytest.mark.parametrize("metric", ["euclidean", "sqeuclidean", "inner_product"])
+def test_ann_ivfflat_recall(metric):
+    X = _blobs(m=3000, n=16, centers=20, seed=5)
+    items = DataFrame.from_numpy(X, num_partitions=2)
+    ann = ApproximateNearestNeighbors(k=10, algoParams={"nlist": 20, "nprobe": 6}, metric=metric, inputCol="features")
+    model = ann.fit(items)
+    assert isinstance(model, ApproximateNearestNeighborsModel)
+    _, _, knn_df = model.kneighbors(items)
+    qid, ind, dist = _knn_arrays(knn_df)
+    if metric == "inner_product":
+        exact = np.argsort(-(X @ X.T), axis=1, kind="stable")[:, :10]
+    else:
+        _, exact = SkNN(n_neighbors=10, algorithm="brute").fit(X).kneighbors(X)
+    recall = np.mean([len(set(a) & set(b)) / 10.0 for a, b in zip(ind, exact)])
+    assert recall >= 0.95, recall
+    # distances are consistent with the returned ids
+    j = ind[:, 0]
+    if metric == "euclidean":
+        ref = np.linalg.norm(X - X[j], axis=1)
+        assert np.allclose(dist[:, 0], ref, atol=1e-2)
+    elif metric == "sqeuclidean":
+        ref = ((X - X[j]) ** 2).sum(1)
+        assert np.allclose(dist[:, 0], ref, rtol=1e-3, atol=1e-2)
+    else:
+        ref = (X * X[j]).sum(1)
+        assert np.allclose(dist[:, 0], ref, rtol=1e-3, atol=1e-2)
+        assert np.all(np.diff(dist, axis=1) <= 1e-3)
+
+
+def test_ann_brute_is_exact_and_join():
+    X = _blobs(m=500, n=8, seed=7)
+    model = ApproximateNearestNeighbors(k=4, algorithm="brute", inputCol="features").fit(DataFrame.from_numpy(X))
+    _, _, knn_df = model.kneighbors(DataFrame.from_numpy(X[:50]))
+    _, ind, dist = _knn_arrays(knn_df)
+    d_ref, _ = SkNN(n_neighbors=4, algorithm="brute").fit(X).kneighbors(X[:50])
+    assert np.allclose(dist, d_ref, atol=1e-3)
+    join = model.approxSimilarityJoin(DataFrame.from_numpy(X[:50]))
+    assert join.count() == 200 and "distCol" in join.columns
+
+
+def test_ann_bad_algorithm():
+    with pytest.raises(ValueError):
+        ApproximateNearestNeighbors(algorithm="cagra_x", inputCol="features").fit(DataFrame.from_numpy(_blobs(m=10)))
+
+
+@pytest.mark.dist
+def test_exact_knn_two_ranks(monkeypatch):
+    monkeypatch.setenv("SRML_FORCE_CPU", "1")
+    X = _blobs(m=800, n=8, seed=11)
+    Q = X[::7] + 0.05
+    items = DataFrame.from_numpy(X, num_partitions=2)
+    a = NearestNeighbors(k=5, inputCol="features", num_workers=1).fit(items)
+    b = NearestNeighbors(k=5, inputCol="features", num_workers=2).fit(items)
+    _, _, ka = a.kneighbors(DataFrame.from_numpy(Q, num_partitions=2))
+    _, _, kb = b.kneighbors(DataFrame.from_numpy(Q, num_partitions=2))
+    qa, ia, da = _knn_arrays(ka)
+    qb, ib, db = _knn_arrays(kb)
+    assert np.array_equal(qa, qb)
+    assert np.allclose(da, db, atol=1e-4)
+    assert (ia == ib).mean() > 0.99
+
+
+@pytest.mark.dist
+def test_ann_two_ranks(monkeypatch):
+    monkeypatch.setenv("SRML_FORCE_CPU", "1")
+    X = _blobs(m=1200, n=8, centers=10, seed=13)
+    items = DataFrame.from_numpy(X, num_partitions=2)
+    model = ApproximateNearestNeighbors(k=5, algoParams={"nlist": 8, "nprobe": 4}, inputCol="features",
+                                        num_workers=2).fit(items)
+    _, _, knn_df = model.kneighbors(DataFrame.from_numpy(X[:300], num_partitions=2))
+    _, ind, _ = _knn_arrays(knn_df)
+    _, exact = SkNN(n_neighbors=5, algorithm="brute").fit(X).kneighbors(X[:300])
+    recall = np.mean([len(set(a) & set(b)) / 5.0 for a, b in zip(ind, exact)])
+    assert recall >= 0.95

@@ -208,3 +208,50 @@ def test_rf_predict(gpu_device):
                                   pg["right"], pg["value_off"], pg["values"], 2, True)
     torch.testing.assert_close(r_got.cpu(), r_ref)
     assert torch.equal(l_got.cpu(), l_ref)
+
+
+@pytest.mark.parametrize("mq,mi,n,k", [(1, 50, 3, 5), (300, 5000, 17, 10), (1000, 20000, 128, 64), (129, 300, 256, 1),
+                                       (64, 100, 130, 100)])
+def test_knn(gpu_device, mq, mi, n, k):
+    Q = _rand(mq, n, gpu_device, seed=11)
+    I = _rand(mi, n, gpu_device, seed=12)
+    d, i = ops.knn(Q, I, k)
+    kk = min(k, mi)
+    ref = torch.cdist(Q.double().cpu(), I.double().cpu()) ** 2
+    rv, _ = torch.topk(ref, kk, dim=1, largest=False)
+    assert d.shape == (mq, kk) and i.shape == (mq, kk)
+    scale = ref.max().item()
+    assert (d.cpu().double() - rv).abs().max().item() / scale < 1e-5
+    # the returned ids really are at the returned distances
+    got = ref.gather(1, i.cpu())
+    assert (got - rv).abs().max().item() / scale < 1e-5
+    assert torch.all(i.cpu().unique(dim=1).shape[1] == kk)
+
+
+def test_knn_id_offset(gpu_device):
+    Q = _rand(70, 8, gpu_device, seed=3)
+    I = _rand(900, 8, gpu_device, seed=4)
+    _, i0 = ops.knn(Q, I, 7)
+    _, i1 = ops.knn(Q, I, 7, id_offset=1000)
+    assert torch.equal(i0 + 1000, i1)
+
+
+@pytest.mark.parametrize("n,nlist,nprobe,k", [(16, 10, 3, 10), (130, 32, 8, 5), (3, 5, 5, 64)])
+def test_ivf_search(gpu_device, n, nlist, nprobe, k):
+    from spark_rapids_ml_nai_amd.models.knn import build_ivf
+
+    X = _rand(4000, n, gpu_device, seed=21)
+    ids = torch.arange(4000, device=gpu_device) * 3
+    index = build_ivf(X, ids, nlist, seed=1, iters=5)
+    Q = _rand(257, n, gpu_device, seed=22)
+    qn = ops.row_sqnorm(Q)
+    _, probes = ops.knn(Q, index.centroids, nprobe)
+    d, gi = ops.ivf_search(Q, probes.int(), index.list_off, index.items, index.inorm, index.ids, k, qnorm=qn)
+    # oracle: brute force over exactly the probed lists (CPU torch path)
+    dc, ic = ops.ivf_search(Q.cpu(), probes.cpu(), index.list_off.cpu(), index.items.cpu(), index.inorm.cpu(),
+                            index.ids.cpu(), k, qnorm=qn.cpu())
+    fin = torch.isfinite(dc)
+    assert torch.equal(fin, torch.isfinite(d.cpu()))
+    scale = dc[fin].abs().max().item()
+    assert (d.cpu()[fin] - dc[fin]).abs().max().item() / scale < 1e-5
+    assert (gi.cpu()[fin] == ic[fin]).float().mean().item() > 0.99
