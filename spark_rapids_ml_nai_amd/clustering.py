@@ -196,3 +196,172 @@ class KMeansModel(KMeansClass, _ModelWithPredictionCol, _KMeansParams):
             return {pred_col: kmeans_predict(Xd, Cd).cpu().numpy().astype(np.int32)}
 
         return construct, predict
+
+
+# ------------------------------------------------------------------------------------------
+# DBSCAN
+# ------------------------------------------------------------------------------------------
+class DBSCANClass(_BackendClass):
+    @classmethod
+    def _param_mapping(cls) -> Dict[str, Optional[str]]:
+        # Spark params carry the backend names (reference mapping is empty for the same reason)
+        return {k: k for k in ("eps", "min_samples", "metric", "algorithm", "max_mbytes_per_batch",
+                               "calc_core_sample_indices")}
+
+    def _get_backend_params_default(self) -> Dict[str, Any]:
+        return {
+            "eps": 0.5,
+            "min_samples": 5,
+            "metric": "euclidean",
+            "algorithm": "brute",
+            "verbose": False,
+            "max_mbytes_per_batch": None,
+            "calc_core_sample_indices": False,
+        }
+
+
+class _DBSCANParams(_FeaturesColMixin, _BackendParams, HasFeaturesCol, HasFeaturesCols, HasPredictionCol, HasIDCol):
+    eps = Param(Params._dummy(), "eps",
+                "The maximum distance between 2 points such they reside in the same neighborhood.",
+                typeConverter=TypeConverters.toFloat)
+    min_samples = Param(Params._dummy(), "min_samples",
+                        "The number of samples in a neighborhood such that this group can be considered as an "
+                        "important core point (including the point itself).", typeConverter=TypeConverters.toInt)
+    metric = Param(Params._dummy(), "metric", "The metric to use when calculating distances between points "
+                   "('euclidean' or 'cosine'; 'precomputed' is not supported).", typeConverter=TypeConverters.toString)
+    algorithm = Param(Params._dummy(), "algorithm", "The algorithm to be used by for nearest neighbor computations "
+                      "('brute' or 'rbc'; both run the fused brute-force tile sweep).",
+                      typeConverter=TypeConverters.toString)
+    max_mbytes_per_batch = Param(Params._dummy(), "max_mbytes_per_batch",
+                                 "Accepted for compatibility; the tiled kernels never materialise the N x N "
+                                 "distance matrix, so no batching is needed.", typeConverter=TypeConverters.toInt)
+    calc_core_sample_indices = Param(Params._dummy(), "calc_core_sample_indices",
+                                     "Indicates whether the indices of the core samples should be calculated.",
+                                     typeConverter=TypeConverters.toBoolean)
+
+    def __init__(self) -> None:
+        super().__init__()
+        self._setDefault(eps=0.5, min_samples=5, metric="euclidean", algorithm="brute", max_mbytes_per_batch=None,
+                         calc_core_sample_indices=True, idCol="unique_id", predictionCol="prediction",
+                         featuresCol="features")
+
+    def setEps(self, value: float) -> Any:
+        return self._set_params(eps=value)
+
+    def getEps(self) -> float:
+        return self.getOrDefault(self.eps)
+
+    def setMinSamples(self, value: int) -> Any:
+        return self._set_params(min_samples=value)
+
+    def getMinSamples(self) -> int:
+        return self.getOrDefault(self.min_samples)
+
+    def setMetric(self, value: str) -> Any:
+        return self._set_params(metric=value)
+
+    def getMetric(self) -> str:
+        return self.getOrDefault(self.metric)
+
+    def setAlgorithm(self, value: str) -> Any:
+        return self._set_params(algorithm=value)
+
+    def getAlgorithm(self) -> str:
+        return self.getOrDefault(self.algorithm)
+
+    def setMaxMbytesPerBatch(self, value: Optional[int]) -> Any:
+        return self._set_params(max_mbytes_per_batch=value)
+
+    def getMaxMbytesPerBatch(self) -> Optional[int]:
+        return self.getOrDefault(self.max_mbytes_per_batch)
+
+    def setCalcCoreSampleIndices(self, value: bool) -> Any:
+        return self._set_params(calc_core_sample_indices=value)
+
+    def getCalcCoreSampleIndices(self) -> bool:
+        return self.getOrDefault(self.calc_core_sample_indices)
+
+    def setIdCol(self, value: str) -> Any:
+        return self._set_params(idCol=value)
+
+
+def _dbscan_worker(ctx: WorkerContext, payload: Tuple[Any, ...]) -> Tuple[np.ndarray, np.ndarray]:
+    from .core.base import to_device
+    from .models.dbscan import dbscan_fit_predict
+
+    X, eps, min_samples, metric = payload
+    Xd = to_device(X, ctx.device, torch.float32)
+    return dbscan_fit_predict(Xd, ctx, eps, min_samples, metric)
+
+
+class DBSCAN(DBSCANClass, _Estimator, _DBSCANParams):
+    """Density-based clustering. Like the reference, ``fit`` does no work: it returns a
+    ``DBSCANModel`` whose ``transform`` clusters the dataset it is given (``clustering.py:820-833``).
+
+    >>> from spark_rapids_ml_nai_amd.clustering import DBSCAN
+    >>> df = DataFrame.createDataFrame([([0.0, 0.0],), ([1.0, 1.0],), ([9.0, 8.0],), ([8.0, 9.0],)], ["features"])
+    >>> model = DBSCAN(eps=2.0, min_samples=2).setFeaturesCol("features").fit(df)
+    >>> [r.prediction for r in model.transform(df).collect()]
+    [0, 0, 1, 1]
+    """
+
+    @keyword_only
+    def __init__(self, *, featuresCol: Union[str, List[str]] = "features", predictionCol: str = "prediction",
+                 eps: float = 0.5, min_samples: int = 5, metric: str = "euclidean", algorithm: str = "brute",
+                 max_mbytes_per_batch: Optional[int] = None, calc_core_sample_indices: bool = True,
+                 idCol: Optional[str] = None, num_workers: Optional[int] = None,
+                 verbose: Union[int, bool] = False, **kwargs: Any) -> None:
+        super().__init__()
+        self._set_params(**self._input_kwargs)
+
+    def _get_fit_func(self, dataset: DataFrame, extra_params: Optional[List[Dict[str, Any]]] = None) -> Callable:
+        raise NotImplementedError("DBSCAN does not fit and generate model")
+
+    def _create_model(self, result: Dict[str, Any]) -> "DBSCANModel":
+        raise NotImplementedError("DBSCAN does not support model creation from Row")
+
+    def _fit(self, dataset: Any) -> "DBSCANModel":
+        if self.getMetric() == "precomputed":
+            raise ValueError("The 'precomputed' metric of sklearn/cuML is not supported; use those libraries instead")
+        if self.getMetric() not in ("euclidean", "cosine", "l2"):
+            raise ValueError("Unsupported metric %r" % self.getMetric())
+        model = DBSCANModel(n_cols=0, dtype="", verbose=self._backend_params.get("verbose", False))
+        model._num_workers = self._num_workers
+        model._float32_inputs = self._float32_inputs
+        self._copyValues(model)
+        self._copy_backend_params(model)
+        return model
+
+
+class DBSCANModel(DBSCANClass, _ModelWithPredictionCol, _DBSCANParams):
+    def __init__(self, n_cols: int = 0, dtype: str = "", verbose: Union[int, bool] = False) -> None:
+        super().__init__(n_cols=n_cols, dtype=dtype, verbose=verbose)
+        self.n_cols = n_cols
+        self.dtype = dtype
+        self.verbose = verbose
+        self.core_sample_indices_: Optional[np.ndarray] = None
+
+    def _get_transform_func(self, dataset: DataFrame) -> Tuple[Callable, Callable]:
+        raise NotImplementedError("DBSCANModel clusters the whole dataset in transform()")
+
+    def _features_all(self, df: DataFrame) -> np.ndarray:
+        from .core.base import _dense_from_df
+
+        fc = self.getFeaturesCol()
+        col, cols = (fc, None) if isinstance(fc, str) else (None, list(fc))
+        return _dense_from_df(df, col, cols, np.float32)
+
+    def _transform_df(self, df: DataFrame) -> DataFrame:
+        from .core.base import run_worker_job
+
+        nw = max(1, self.num_workers)
+        parts = df.repartition(nw).partitions if df.getNumPartitions() != nw else df.partitions
+        payloads = [(self._features_all(DataFrame([p])), self.getEps(), self.getMinSamples(), self.getMetric())
+                    for p in parts]
+        res = run_worker_job(_dbscan_worker, payloads)
+        labels = np.concatenate([r[0] for r in res]).astype(np.int32)
+        core = np.concatenate([r[1] for r in res])
+        if self.getCalcCoreSampleIndices():
+            self.core_sample_indices_ = np.nonzero(core)[0]
+        out = DataFrame(parts) if len(parts) != df.getNumPartitions() else df
+        return out.withColumn(self.getPredictionCol(), labels)

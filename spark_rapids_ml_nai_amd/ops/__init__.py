@@ -6,6 +6,7 @@ from __future__ import annotations
 
 from typing import Optional, Tuple
 
+import numpy as np
 import torch
 
 from . import native
@@ -494,3 +495,133 @@ def ivf_search(Q: torch.Tensor, probes: torch.Tensor, list_off: torch.Tensor, it
                 _c(inorm.float()).data_ptr(), _c(ids.long()).data_ptr(), k, od.data_ptr(), oi.data_ptr(),
                 native.stream(Q.device))
     return (od + qnorm.float().view(-1, 1)).clamp_min(0), oi
+
+
+# ------------------------------------------------------------------------------------------
+# DBSCAN: eps-degree / core-core union-find over lower-triangle 128x128 tile pairs
+# ------------------------------------------------------------------------------------------
+DB_TILE = 128
+
+
+def dbscan_num_tiles(N: int) -> int:
+    nt = (N + DB_TILE - 1) // DB_TILE
+    return nt * (nt + 1) // 2
+
+
+def _tri_decode(t: int) -> Tuple[int, int]:
+    i = int((np.sqrt(8.0 * t + 1.0) - 1.0) * 0.5)
+    while i > 0 and i * (i + 1) // 2 > t:
+        i -= 1
+    while (i + 1) * (i + 2) // 2 <= t:
+        i += 1
+    return i, t - i * (i + 1) // 2
+
+
+def _db_tiles(X: torch.Tensor, xnorm: torch.Tensor, eps2: float, t0: int, t1: int):
+    """CPU reference: yields (r0, c0, masked squared distances) per tile pair of the range."""
+    N = X.shape[0]
+    for t in range(t0, t1):
+        bi, bj = _tri_decode(t)
+        r0, c0 = bi * DB_TILE, bj * DB_TILE
+        A, B = X[r0: r0 + DB_TILE].float(), X[c0: c0 + DB_TILE].float()
+        d = (xnorm[r0: r0 + DB_TILE].float().view(-1, 1) + xnorm[c0: c0 + DB_TILE].float().view(1, -1)
+             - 2.0 * (A @ B.T)).clamp_min(0)
+        yield bi == bj, r0, c0, torch.where(d <= eps2, d, torch.full_like(d, float("inf")))
+
+
+def dbscan_degree(X: torch.Tensor, xnorm: torch.Tensor, eps2: float, t0: int, t1: int,
+                  counts: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """eps-neighbourhood sizes (self included) accumulated over tile pairs [t0, t1) into int32 counts."""
+    N = X.shape[0]
+    if counts is None:
+        counts = torch.zeros(N, dtype=torch.int32, device=X.device)
+    if not X.is_cuda or X.dtype != torch.float32:
+        for diag, r0, c0, d in _db_tiles(X, xnorm, eps2, t0, t1):
+            adj = torch.isfinite(d)
+            counts[r0: r0 + d.shape[0]] += adj.sum(1).int()
+            if not diag:
+                counts[c0: c0 + d.shape[1]] += adj.sum(0).int()
+        return counts
+    X = _c(X)
+    native.call("srml_dbscan_degree_f32", X.data_ptr(), N, X.shape[1], X.stride(0), _c(xnorm.float()).data_ptr(),
+                float(eps2), int(t0), int(t1), counts.data_ptr(), native.stream(X.device))
+    return counts
+
+
+def _orderable_key(d: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    """int64 view of the kernel's packed u64 key (orderable(d) << 32 | idx) for d >= 0."""
+    bits = d.float().contiguous().view(torch.int32).long() & 0xFFFFFFFF
+    return (((bits | 0x80000000) - (1 << 32)) << 32) | (idx.long() & 0xFFFFFFFF)
+
+
+def _uf_cpu_merge(parent: torch.Tensor, src: np.ndarray, dst: np.ndarray) -> None:
+    from scipy.sparse import coo_matrix
+    from scipy.sparse.csgraph import connected_components
+
+    N = parent.shape[0]
+    p = parent.cpu().numpy().astype(np.int64)
+    s = np.concatenate([np.arange(N), src])
+    d = np.concatenate([p, dst])
+    g = coo_matrix((np.ones(len(s), dtype=np.int8), (s, d)), shape=(N, N))
+    _, comp = connected_components(g, directed=False)
+    mins = np.full(comp.max() + 1, N, dtype=np.int64)
+    np.minimum.at(mins, comp, np.arange(N))
+    parent.copy_(torch.from_numpy(mins[comp].astype(np.int32)))
+
+
+def dbscan_link(X: torch.Tensor, xnorm: torch.Tensor, eps2: float, t0: int, t1: int, core: torch.Tensor,
+                parent: torch.Tensor, best: torch.Tensor) -> None:
+    """Unite core-core eps edges of tile pairs [t0, t1) into ``parent`` (int32 union-find) and keep,
+    for every non-core point, the packed key of its nearest core neighbour in ``best`` (int64 MIN)."""
+    N = X.shape[0]
+    if not X.is_cuda or X.dtype != torch.float32:
+        corb = core.bool()
+        srcs, dsts = [], []
+        for diag, r0, c0, d in _db_tiles(X, xnorm, eps2, t0, t1):
+            adj = torch.isfinite(d)
+            rc = corb[r0: r0 + d.shape[0]].view(-1, 1)
+            cc = corb[c0: c0 + d.shape[1]].view(1, -1)
+            e = torch.nonzero(adj & rc & cc)
+            srcs.append((e[:, 0] + r0).numpy())
+            dsts.append((e[:, 1] + c0).numpy())
+            ridx = torch.arange(c0, c0 + d.shape[1]).view(1, -1).expand_as(d)
+            cidx = torch.arange(r0, r0 + d.shape[0]).view(-1, 1).expand_as(d)
+            inf = torch.full_like(d, float("inf"))
+            # border row <- core column
+            dr = torch.where(adj & ~rc & cc, d, inf)
+            kr = torch.where(torch.isfinite(dr), _orderable_key(dr, ridx), torch.full_like(ridx, -1))
+            best[r0: r0 + d.shape[0]] = torch.minimum(best[r0: r0 + d.shape[0]], _min_valid(kr, 1))
+            dc = torch.where(adj & rc & ~cc, d, inf)
+            kc = torch.where(torch.isfinite(dc), _orderable_key(dc, cidx), torch.full_like(cidx, -1))
+            best[c0: c0 + d.shape[1]] = torch.minimum(best[c0: c0 + d.shape[1]], _min_valid(kc, 0))
+        if srcs:
+            _uf_cpu_merge(parent, np.concatenate(srcs), np.concatenate(dsts))
+        return
+    X = _c(X)
+    native.call("srml_dbscan_link_f32", X.data_ptr(), N, X.shape[1], X.stride(0), _c(xnorm.float()).data_ptr(),
+                float(eps2), int(t0), int(t1), _c(core.to(torch.uint8)).data_ptr(), parent.data_ptr(), best.data_ptr(),
+                native.stream(X.device))
+
+
+def _min_valid(k: torch.Tensor, dim: int) -> torch.Tensor:
+    # keys of real candidates are negative int64 (top bit set); -1 means "none" and is the largest
+    return k.min(dim).values
+
+
+def uf_unite_pairs(parent: torch.Tensor, other: torch.Tensor) -> None:
+    """Merge another union-find forest (edges i -> other[i]) into ``parent``."""
+    if not parent.is_cuda:
+        N = parent.shape[0]
+        o = other.cpu().numpy().astype(np.int64)
+        _uf_cpu_merge(parent, np.arange(N), o)
+        return
+    native.call("srml_uf_unite_pairs", parent.data_ptr(), parent.shape[0], _c(other.int()).data_ptr(),
+                native.stream(parent.device))
+
+
+def uf_compress(parent: torch.Tensor) -> None:
+    """Point every node directly at its root (the smallest index of its component)."""
+    if not parent.is_cuda:
+        _uf_cpu_merge(parent, np.zeros(0, np.int64), np.zeros(0, np.int64))
+        return
+    native.call("srml_uf_compress", parent.data_ptr(), parent.shape[0], native.stream(parent.device))

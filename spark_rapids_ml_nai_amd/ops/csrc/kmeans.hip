@@ -17,70 +17,10 @@
 //   (the full-rate atomic shape on MI355X).
 #include "common.h"
 
+#include "tile.h"
+
 namespace {
-constexpr int BK = 32;
-constexpr int PADK = BK + 1;
-
-__device__ __forceinline__ unsigned orderable(float f) {
-  unsigned u = __float_as_uint(f);
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
-__device__ __forceinline__ float unorderable(unsigned u) {
-  return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
-}
-
-// ROWS x 32 tile of a row-major matrix, staged through registers. load(): branch-free (clamped
-// addresses + select after the load) so the next k-tile's loads stay in flight under the MFMAs;
-// store(): scalar ds_writes into the padded [row][33] LDS image (conflict-free operand reads).
-template <int ROWS, bool VEC>
-struct RowTile {
-  static constexpr int PER = (ROWS * 8 + 255) / 256;
-  floatx4 v[PER];
-  unsigned okmask;  // bit 4p+q: element valid (row and column in range)
-
-  // issue the loads only; masking happens in store() so no wait is emitted before the MFMAs
-  __device__ __forceinline__ void load(const float* __restrict__ A, long lda, long nrows, int ncols, long row0,
-                                       int k0) {
-    const int t = threadIdx.x;
-    okmask = 0u;
-#pragma unroll
-    for (int p = 0; p < PER; ++p) {
-      const int idx = t + 256 * p;
-      const int rr = (idx >> 3) % ROWS;
-      const int c4 = (idx & 7) * 4;
-      const long r = row0 + rr;
-      const bool okr = (idx < ROWS * 8) && (r < nrows);
-      const float* row = A + (okr ? r : 0) * lda;
-      const int kc = k0 + c4;
-      if (VEC) {
-        const bool okk = kc < ncols;  // ncols % 4 == 0 on the VEC path
-        v[p] = *reinterpret_cast<const floatx4*>(row + (okk ? kc : 0));
-        okmask |= (okr && okk) ? (0xFu << (4 * p)) : 0u;
-      } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const bool okk = kc + q < ncols;
-          v[p][q] = row[okk ? kc + q : 0];
-          okmask |= (okr && okk) ? (1u << (4 * p + q)) : 0u;
-        }
-      }
-    }
-  }
-
-  __device__ __forceinline__ void store(float (*dst)[PADK]) const {
-    const int t = threadIdx.x;
-#pragma unroll
-    for (int p = 0; p < PER; ++p) {
-      const int idx = t + 256 * p;
-      if (PER * 256 == ROWS * 8 || idx < ROWS * 8) {
-        const int rr = idx >> 3;
-        const int c4 = (idx & 7) * 4;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) dst[rr][c4 + q] = ((okmask >> (4 * p + q)) & 1u) ? v[p][q] : 0.f;
-      }
-    }
-  }
-};
+using namespace srml_tile;
 
 // BM x BN block tile, WM x WN waves (WM*WN = 4), each wave MT x NT tiles of 32x32
 template <int BM, int BN, int WM, int MT, int NT, bool VEC>

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--m", type=int, default=1_000_000)
     ap.add_argument("--n", type=int, default=3000)
     ap.add_argument("--k", type=int, default=1000)
+    ap.add_argument("--q", type=int, default=10000)
     ap.add_argument("--only", type=str, default="")
     a = ap.parse_args()
     dev = torch.device("cuda")
@@ -77,6 +78,44 @@ def main():
         h = torch.empty(a.m, a.n, pin_memory=True)
         t = timeit(lambda: h.to(dev, non_blocking=True), 3)
         res["h2d_pinned"] = {"ms": t, "GB/s": gb / t * 1000}
+    if want("knn"):
+        Q = X[: a.q].clone()
+        xn = ops.row_sqnorm(X)
+        t = timeit(lambda: ops.knn(Q, X, 10, inorm=xn), 3)
+        res["knn_k10"] = {"ms": t, "TFLOP/s": 2 * a.q * a.m * a.n / t / 1e9}
+    if want("ivf"):
+        from spark_rapids_ml_nai_amd.models.knn import build_ivf
+
+        ids = torch.arange(a.m, device=dev)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        index = build_ivf(X, ids, 1024, seed=1, iters=10)
+        torch.cuda.synchronize()
+        res["ivf_build_nlist1024"] = {"ms": (time.perf_counter() - t0) * 1e3}
+        Q = X[: a.q].clone()
+        qn = ops.row_sqnorm(Q)
+
+        def _search():
+            _, probes = ops.knn(Q, index.centroids, 20, inorm=index.cnorm, qnorm=qn)
+            return ops.ivf_search(Q, probes.int(), index.list_off, index.items, index.inorm, index.ids, 10, qnorm=qn)
+
+        t = timeit(_search, 3)
+        scanned = a.q * 20 * (a.m / 1024) * a.n * 4 / 1e9
+        res["ivf_search_nprobe20"] = {"ms": t, "scan_TB/s": scanned / t}
+    if want("dbscan"):
+        from spark_rapids_ml_nai_amd.models.dbscan import dbscan_fit_predict
+        from spark_rapids_ml_nai_amd.parallel.context import WorkerContext
+
+        Nd, nd = 200_000, 64
+        C = torch.randn(50, nd, device=dev, generator=g) * 8
+        Xd = C[torch.randint(0, 50, (Nd,), device=dev, generator=g)] + torch.randn(Nd, nd, device=dev, generator=g)
+        xn = ops.row_sqnorm(Xd)
+        T = ops.dbscan_num_tiles(Nd)
+        t = timeit(lambda: ops.dbscan_degree(Xd, xn, 100.0, 0, T), 2)
+        res["dbscan_degree_200k_x64"] = {"ms": t, "TFLOP/s(sym)": Nd * Nd * nd / t / 1e9}
+        ctx = WorkerContext.single(dev)
+        t = timeit(lambda: dbscan_fit_predict(Xd, ctx, 10.0, 5), 2)
+        res["dbscan_fit_200k_x64"] = {"ms": t}
     print(json.dumps({k: {kk: round(vv, 3) for kk, vv in v.items()} for k, v in res.items()}))
 
 
