@@ -1,0 +1,333 @@
+"""UMAP on MI355X: kNN graph -> fuzzy simplicial set -> spectral/random init -> SGD layout.
+
+Semantics follow umap-learn / cuML UMAP (what the reference calls on one GPU, ``umap.py:924-958``):
+* kNN graph: exact, from the fused MFMA distance + top-k kernel (``ops.knn``), self included;
+* ``smooth_knn_dist`` (per-row bisection for sigma, rho = nearest non-zero distance with
+  ``local_connectivity``) vectorised over all rows on device;
+* membership strengths exp(-(d - rho) / sigma) and the fuzzy union A + Aᵀ - A∘Aᵀ
+  (``set_op_mix_ratio`` blends with the intersection) via one device sort of edge keys;
+* optional supervised intersection with a categorical target (far_dist 5, unknown 1) followed
+  by ``reset_local_connectivity``;
+* spectral init: top eigenvectors of D^-1/2 A D^-1/2 by block subspace iteration with sparse
+  CSR products on device (host ``eigsh`` for small graphs), scaled like umap-learn;
+* SGD: ``srml_umap_epoch`` (edge-parallel HIP kernel, hash RNG negative sampling), alpha decays
+  linearly, edges below max_w / n_epochs dropped, epochs_per_sample = n_epochs / (n_epochs·w/max_w);
+* transform: kNN to the training data, local_connectivity - 1, l1-normalised weighted init
+  from neighbour embeddings, n_epochs/3 (default 100 / 30) epochs at alpha/4 with the training
+  embedding fixed.
+"""
+from __future__ import annotations
+
+import math
+from typing import Any, Dict, Optional, Tuple
+
+import numpy as np
+import torch
+
+from .. import ops
+
+SMOOTH_K_TOLERANCE = 1e-5
+MIN_K_DIST_SCALE = 1e-3
+
+
+def find_ab_params(spread: float, min_dist: float) -> Tuple[float, float]:
+    """Fit 1 / (1 + a x^(2b)) to the target membership curve (umap-learn ``find_ab_params``)."""
+    from scipy.optimize import curve_fit
+
+    def curve(x, a, b):
+        return 1.0 / (1.0 + a * x ** (2 * b))
+
+    xv = np.linspace(0, spread * 3, 300)
+    yv = np.zeros(xv.shape)
+    yv[xv < min_dist] = 1.0
+    yv[xv >= min_dist] = np.exp(-(xv[xv >= min_dist] - min_dist) / spread)
+    params, _ = curve_fit(curve, xv, yv)
+    return float(params[0]), float(params[1])
+
+
+def knn_graph(Q: torch.Tensor, I: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(euclidean distances [mq, k] fp32, indices [mq, k] int64)."""
+    inorm = ops.row_sqnorm(I)
+    d2, idx = ops.knn(Q, I, k, inorm=inorm)
+    # refine the selected distances directly to avoid expansion cancellation
+    step = max(1, (1 << 26) // max(1, k * Q.shape[1]))
+    out = torch.empty_like(d2)
+    for s in range(0, Q.shape[0], step):
+        rows = I.index_select(0, idx[s: s + step].reshape(-1)).view(-1, idx.shape[1], Q.shape[1])
+        out[s: s + step] = ((rows - Q[s: s + step].unsqueeze(1)) ** 2).sum(-1)
+    d2, j = torch.sort(out, dim=1)
+    idx = idx.gather(1, j)
+    return torch.sqrt(d2.clamp_min(0)), idx
+
+
+def smooth_knn_dist(dist: torch.Tensor, k: float, n_iter: int = 64, local_connectivity: float = 1.0,
+                    bandwidth: float = 1.0) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Vectorised umap-learn ``smooth_knn_dist``: (sigmas, rhos) for every row."""
+    d = dist.double()
+    m, kk = d.shape
+    target = math.log2(k) * bandwidth
+    nz = torch.where(d > 0, d, torch.full_like(d, float("inf")))
+    nz_sorted, _ = torch.sort(nz, dim=1)
+    n_nz = (d > 0).sum(1)
+    index = int(math.floor(local_connectivity))
+    interp = local_connectivity - index
+    rho = torch.zeros(m, dtype=torch.float64, device=d.device)
+    ok = n_nz >= local_connectivity
+    if index > 0:
+        base = nz_sorted[:, index - 1]
+        rho_i = base.clone()
+        if interp > 1e-5 and index < kk:
+            rho_i = base + interp * (nz_sorted[:, index] - base)
+        rho = torch.where(ok, rho_i, rho)
+    else:
+        rho = torch.where(ok, interp * nz_sorted[:, 0], rho)
+    anyz = n_nz > 0
+    rho = torch.where(~ok & anyz, nz_sorted.masked_fill(~torch.isfinite(nz_sorted), -1).max(1).values, rho)
+    rho = torch.where(torch.isfinite(rho), rho, torch.zeros_like(rho))
+    lo = torch.zeros(m, dtype=torch.float64, device=d.device)
+    hi = torch.full((m,), float("inf"), dtype=torch.float64, device=d.device)
+    mid = torch.ones(m, dtype=torch.float64, device=d.device)
+    done = torch.zeros(m, dtype=torch.bool, device=d.device)
+    dd = d[:, 1:] - rho.view(-1, 1)
+    for _ in range(n_iter):
+        psum = torch.where(dd > 0, torch.exp(-dd / mid.view(-1, 1)), torch.ones_like(dd)).sum(1)
+        done = done | ((psum - target).abs() < SMOOTH_K_TOLERANCE)
+        gt = psum > target
+        new_hi = torch.where(gt, mid, hi)
+        new_lo = torch.where(gt, lo, mid)
+        new_mid = torch.where(gt, (lo + mid) / 2.0,
+                              torch.where(torch.isinf(hi), mid * 2.0, (mid + hi) / 2.0))
+        lo = torch.where(done, lo, new_lo)
+        hi = torch.where(done, hi, new_hi)
+        mid = torch.where(done, mid, new_mid)
+        if bool(done.all()):
+            break
+    mean_row = d.mean(1)
+    mean_all = d.mean()
+    sigma = torch.where(rho > 0, torch.maximum(mid, MIN_K_DIST_SCALE * mean_row),
+                        torch.maximum(mid, MIN_K_DIST_SCALE * mean_all))
+    return sigma, rho
+
+
+def membership_strengths(idx: torch.Tensor, dist: torch.Tensor, sigma: torch.Tensor, rho: torch.Tensor,
+                         self_rows: Optional[torch.Tensor] = None) -> torch.Tensor:
+    d = dist.double() - rho.view(-1, 1)
+    w = torch.where(d <= 0, torch.ones_like(d), torch.exp(-d / sigma.view(-1, 1)))
+    w = torch.where(sigma.view(-1, 1) == 0, torch.ones_like(w), w)
+    if self_rows is not None:
+        w = torch.where(idx == self_rows.view(-1, 1), torch.zeros_like(w), w)
+    w = torch.where(idx < 0, torch.zeros_like(w), w)
+    return w.float()
+
+
+def _coalesce(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n: int):
+    key = rows.long() * n + cols.long()
+    uk, inv = torch.unique(key, return_inverse=True)
+    return uk // n, uk % n, inv, uk.numel()
+
+
+def fuzzy_union(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n: int,
+                set_op_mix_ratio: float = 1.0) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """P = mix·(A + Aᵀ - A∘Aᵀ) + (1 - mix)·(A∘Aᵀ) for an n x n COO matrix without duplicates."""
+    keep = vals > 0
+    rows, cols, vals = rows[keep], cols[keep], vals[keep]
+    r2 = torch.cat([rows, cols])
+    c2 = torch.cat([cols, rows])
+    v2 = torch.cat([vals, vals]).double()
+    ur, uc, inv, nu = _coalesce(r2, c2, v2, n)
+    s = torch.zeros(nu, dtype=torch.float64, device=vals.device).index_add_(0, inv, v2)
+    cnt = torch.zeros(nu, dtype=torch.int64, device=vals.device).index_add_(0, inv, torch.ones_like(inv))
+    lp = torch.zeros(nu, dtype=torch.float64, device=vals.device).index_add_(0, inv, torch.log(v2))
+    prod = torch.where(cnt >= 2, torch.exp(lp), torch.zeros_like(lp))
+    out = set_op_mix_ratio * (s - prod) + (1.0 - set_op_mix_ratio) * prod
+    keep = out > 0
+    return ur[keep], uc[keep], out[keep].float()
+
+
+def categorical_intersection(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, y: torch.Tensor,
+                             n: int, unknown_dist: float = 1.0, far_dist: float = 5.0):
+    yr, yc = y[rows], y[cols]
+    unknown = (yr == -1) | (yc == -1)
+    differ = (yr != yc) & ~unknown
+    v = vals.double()
+    v = torch.where(unknown, v * math.exp(-unknown_dist), v)
+    v = torch.where(differ, v * math.exp(-far_dist), v)
+    # reset_local_connectivity: normalise rows by their max, then fuzzy union again
+    rmax = torch.zeros(n, dtype=torch.float64, device=v.device).scatter_reduce_(0, rows.long(), v, "amax",
+                                                                               include_self=True)
+    v = v / rmax[rows.long()].clamp_min(1e-30)
+    return fuzzy_union(rows, cols, v.float(), n)
+
+
+def _spectral_host(rows: np.ndarray, cols: np.ndarray, vals: np.ndarray, n: int, dim: int, seed: int) -> np.ndarray:
+    import scipy.sparse as sp
+    from scipy.sparse.linalg import eigsh
+
+    A = sp.coo_matrix((vals.astype(np.float64), (rows, cols)), shape=(n, n)).tocsr()
+    deg = np.asarray(A.sum(axis=1)).ravel()
+    dinv = 1.0 / np.sqrt(np.maximum(deg, 1e-30))
+    D = sp.diags(dinv)
+    L = sp.identity(n) - D @ A @ D
+    k = dim + 1
+    if n <= 2000 or n < 4 * k:
+        w, v = np.linalg.eigh(L.toarray())
+    else:
+        num_lanczos = max(2 * k + 1, int(np.sqrt(n)))
+        rng = np.random.default_rng(seed)
+        w, v = eigsh(L, k, which="SM", ncv=num_lanczos, tol=1e-4, v0=np.ones(n) + 0.01 * rng.standard_normal(n),
+                     maxiter=n * 5)
+    order = np.argsort(w)[1:k]
+    return v[:, order]
+
+
+def _spectral_device(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n: int, dim: int, seed: int,
+                     iters: int = 300) -> torch.Tensor:
+    dev = vals.device
+    deg = torch.zeros(n, dtype=torch.float64, device=dev).index_add_(0, rows.long(), vals.double())
+    dinv = 1.0 / torch.sqrt(deg.clamp_min(1e-30))
+    mv = (dinv[rows.long()] * vals.double() * dinv[cols.long()]).float()
+    M = torch.sparse_coo_tensor(torch.stack([rows.long(), cols.long()]), mv, (n, n)).coalesce().to_sparse_csr()
+    p = min(n, dim + 1 + 8)
+    g = torch.Generator(device="cpu").manual_seed(int(seed))
+    Y = torch.randn(n, p, generator=g).to(dev)
+    Y[:, 0] = torch.sqrt(deg).float()
+    Y, _ = torch.linalg.qr(Y)
+    for it in range(iters):
+        Y = 0.5 * (torch.sparse.mm(M, Y) + Y)  # (M + I) / 2: eigenvalues in [0, 1], order kept
+        if it % 5 == 4 or it == iters - 1:
+            Y, _ = torch.linalg.qr(Y)
+    T = Y.T @ (0.5 * (torch.sparse.mm(M, Y) + Y))
+    w, V = torch.linalg.eigh(T.double())
+    order = torch.argsort(w, descending=True)[1: dim + 1]
+    return (Y.double() @ V[:, order]).float()
+
+
+def spectral_init(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n: int, dim: int, seed: int) -> torch.Tensor:
+    dev = vals.device
+    if dev.type != "cuda" or n <= 20000:
+        coords = torch.from_numpy(_spectral_host(rows.cpu().numpy(), cols.cpu().numpy(), vals.cpu().numpy(), n, dim,
+                                                 seed)).float().to(dev)
+    else:
+        coords = _spectral_device(rows, cols, vals, n, dim, seed)
+    expansion = 10.0 / coords.abs().max().clamp_min(1e-30)
+    g = torch.Generator(device="cpu").manual_seed(int(seed) + 1)
+    return coords * expansion + (torch.randn(coords.shape, generator=g) * 1e-4).to(dev)
+
+
+def make_epochs_per_sample(w: torch.Tensor, n_epochs: int) -> torch.Tensor:
+    n_samples = n_epochs * (w / w.max())
+    return torch.where(n_samples > 0, float(n_epochs) / n_samples.clamp_min(1e-30), torch.full_like(w, -1.0))
+
+
+def optimize_layout(emb_head: torch.Tensor, emb_tail: torch.Tensor, head: torch.Tensor, tail: torch.Tensor,
+                    w: torch.Tensor, n_epochs: int, a: float, b: float, gamma: float, initial_alpha: float,
+                    negative_sample_rate: float, move_other: bool, seed: int) -> torch.Tensor:
+    w = torch.where(w < w.max() / float(n_epochs), torch.zeros_like(w), w)
+    keep = w > 0
+    head, tail, w = head[keep].int().contiguous(), tail[keep].int().contiguous(), w[keep]
+    eps = make_epochs_per_sample(w, n_epochs).float().contiguous()
+    eps_neg = (eps / float(negative_sample_rate)).contiguous()
+    next_sample = eps.clone()
+    next_neg = eps_neg.clone()
+    for n in range(n_epochs):
+        alpha = initial_alpha * (1.0 - float(n) / float(n_epochs))
+        ops.umap_epoch(head, tail, eps, next_sample, next_neg, eps_neg, emb_head, emb_tail, a, b, gamma, alpha, n,
+                       move_other, seed)
+    return emb_head
+
+
+def _n_epochs_default(n: int) -> int:
+    return 500 if n <= 10000 else 200
+
+
+def umap_fit(X: torch.Tensor, params: Dict[str, Any], y: Optional[torch.Tensor] = None) -> np.ndarray:
+    """Embedding (N x n_components, float32) of the rows of X."""
+    N = X.shape[0]
+    k = int(min(params.get("n_neighbors", 15), N))
+    dim = int(params.get("n_components", 2))
+    metric = params.get("metric", "euclidean")
+    seed = params.get("random_state")
+    seed = int(seed) if seed is not None else int(np.random.randint(0, 2 ** 31 - 1))
+    a, b = params.get("a"), params.get("b")
+    if a is None or b is None:
+        a, b = find_ab_params(float(params.get("spread", 1.0)), float(params.get("min_dist", 0.1)))
+    Xf = X.float().contiguous()
+    if metric in ("cosine", "correlation"):
+        if metric == "correlation":
+            Xf = Xf - Xf.mean(1, keepdim=True)
+        Xf = Xf / Xf.norm(dim=1, keepdim=True).clamp_min(1e-30)
+    elif metric not in ("euclidean", "l2", "sqeuclidean"):
+        raise ValueError("Unsupported UMAP metric %r" % metric)
+    pre = params.get("precomputed_knn")
+    if pre is not None:
+        idx = torch.as_tensor(np.asarray(pre[0]), dtype=torch.int64, device=X.device)[:, :k]
+        dist = torch.as_tensor(np.asarray(pre[1]), dtype=torch.float32, device=X.device)[:, :k]
+    else:
+        dist, idx = knn_graph(Xf, Xf, k)
+        if metric in ("cosine", "correlation"):
+            dist = 0.5 * dist * dist  # 1 - cos for unit rows
+        elif metric == "sqeuclidean":
+            dist = dist * dist
+    sigma, rho = smooth_knn_dist(dist, float(k), local_connectivity=float(params.get("local_connectivity", 1.0)))
+    self_rows = torch.arange(N, device=X.device)
+    w = membership_strengths(idx, dist, sigma, rho, self_rows)
+    rows = self_rows.view(-1, 1).expand_as(idx).reshape(-1)
+    cols = idx.reshape(-1)
+    rows, cols, vals = fuzzy_union(rows, cols.clamp_min(0), w.reshape(-1), N,
+                                   float(params.get("set_op_mix_ratio", 1.0)))
+    if y is not None:
+        yy = y.to(X.device).long().view(-1)
+        rows, cols, vals = categorical_intersection(rows, cols, vals, yy, N)
+    n_epochs = params.get("n_epochs")
+    n_epochs = int(n_epochs) if n_epochs else _n_epochs_default(N)
+    init = params.get("init", "spectral")
+    if isinstance(init, str) and init == "spectral" and N > dim + 1:
+        emb = spectral_init(rows, cols, vals, N, dim, seed)
+    else:
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        emb = (torch.rand(N, dim, generator=g) * 20.0 - 10.0).to(X.device)
+    mn, mx = emb.min(0).values, emb.max(0).values
+    emb = (10.0 * (emb - mn) / (mx - mn).clamp_min(1e-30)).float().contiguous()
+    optimize_layout(emb, emb, rows, cols, vals, n_epochs, a, b, float(params.get("repulsion_strength", 1.0)),
+                    float(params.get("learning_rate", 1.0)), float(params.get("negative_sample_rate", 5)), True, seed)
+    return emb.cpu().numpy()
+
+
+def umap_transform(X: torch.Tensor, raw: torch.Tensor, embedding: torch.Tensor, params: Dict[str, Any]) -> np.ndarray:
+    Nn = X.shape[0]
+    Ntr = raw.shape[0]
+    k = int(min(params.get("n_neighbors", 15), Ntr))
+    metric = params.get("metric", "euclidean")
+    seed = params.get("random_state")
+    seed = int(seed) if seed is not None else 42
+    a, b = params.get("a"), params.get("b")
+    if a is None or b is None:
+        a, b = find_ab_params(float(params.get("spread", 1.0)), float(params.get("min_dist", 0.1)))
+    Xf, Rf = X.float().contiguous(), raw.float().contiguous()
+    if metric in ("cosine", "correlation"):
+        if metric == "correlation":
+            Xf, Rf = Xf - Xf.mean(1, keepdim=True), Rf - Rf.mean(1, keepdim=True)
+        Xf = Xf / Xf.norm(dim=1, keepdim=True).clamp_min(1e-30)
+        Rf = Rf / Rf.norm(dim=1, keepdim=True).clamp_min(1e-30)
+    dist, idx = knn_graph(Xf, Rf, k)
+    if metric in ("cosine", "correlation"):
+        dist = 0.5 * dist * dist
+    elif metric == "sqeuclidean":
+        dist = dist * dist
+    adj_lc = max(0.0, float(params.get("local_connectivity", 1.0)) - 1.0)
+    sigma, rho = smooth_knn_dist(dist, float(k), local_connectivity=adj_lc)
+    w = membership_strengths(idx, dist, sigma, rho)
+    wn = w / w.sum(1, keepdim=True).clamp_min(1e-30)
+    emb_tr = embedding.float().contiguous()
+    init = (wn.unsqueeze(-1) * emb_tr[idx.clamp_min(0)]).sum(1).contiguous()
+    n_epochs = params.get("n_epochs")
+    n_epochs = int(n_epochs) // 3 if n_epochs else (100 if Nn <= 10000 else 30)
+    if n_epochs <= 0:
+        return init.cpu().numpy()
+    rows = torch.arange(Nn, device=X.device).view(-1, 1).expand_as(idx).reshape(-1)
+    cols = idx.reshape(-1).clamp_min(0)
+    vals = w.reshape(-1)
+    emb = optimize_layout(init, emb_tr.clone(), rows, cols, vals, n_epochs, a, b,
+                          float(params.get("repulsion_strength", 1.0)), float(params.get("learning_rate", 1.0)) / 4.0,
+                          float(params.get("negative_sample_rate", 5)), False, seed)
+    return emb.cpu().numpy()

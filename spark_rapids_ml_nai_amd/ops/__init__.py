@@ -625,3 +625,54 @@ def uf_compress(parent: torch.Tensor) -> None:
         _uf_cpu_merge(parent, np.zeros(0, np.int64), np.zeros(0, np.int64))
         return
     native.call("srml_uf_compress", parent.data_ptr(), parent.shape[0], native.stream(parent.device))
+
+
+# ------------------------------------------------------------------------------------------
+# UMAP: one SGD epoch over the fuzzy-graph edges
+# ------------------------------------------------------------------------------------------
+def umap_epoch(head: torch.Tensor, tail: torch.Tensor, eps: torch.Tensor, next_sample: torch.Tensor,
+               next_neg: torch.Tensor, eps_neg: torch.Tensor, emb_head: torch.Tensor, emb_tail: torch.Tensor,
+               a: float, b: float, gamma: float, alpha: float, epoch: int, move_other: bool, seed: int) -> None:
+    """In-place epoch ``epoch`` of umap-learn's optimize_layout_euclidean (edge-parallel)."""
+    n_tail = emb_tail.shape[0]
+    dim = emb_head.shape[1]
+    if emb_head.is_cuda:
+        native.call("srml_umap_epoch", head.data_ptr(), tail.data_ptr(), head.shape[0], eps.data_ptr(),
+                    next_sample.data_ptr(), next_neg.data_ptr(), eps_neg.data_ptr(), emb_head.data_ptr(),
+                    emb_tail.data_ptr(), n_tail, dim, float(a), float(b), float(gamma), float(alpha), float(epoch),
+                    int(bool(move_other)), int(seed) & 0xFFFFFFFF, native.stream(emb_head.device))
+        return
+    # CPU reference: all due edges of the epoch update from one snapshot (synchronous Hogwild)
+    ep = float(epoch)
+    idx = torch.nonzero((eps > 0) & (next_sample <= ep)).view(-1)
+    if idx.numel() == 0:
+        return
+    j, k = head[idx].long(), tail[idx].long()
+    cur = emb_head[j]
+    diff = cur - emb_tail[k]
+    d2 = (diff * diff).sum(1, keepdim=True)
+    pb = d2.clamp_min(1e-30) ** b
+    coef = torch.where(d2 > 0, (-2.0 * a * b * pb / d2.clamp_min(1e-30)) / (a * pb + 1.0), torch.zeros_like(d2))
+    g = (coef * diff).clamp(-4, 4) * alpha
+    cur = cur + g
+    next_sample[idx] += eps[idx]
+    en = eps_neg[idx]
+    n_neg = torch.where(en > 0, torch.floor((ep - next_neg[idx]) / en.clamp_min(1e-30)), torch.zeros_like(en))
+    n_neg = n_neg.clamp_min(0).long()
+    rep = torch.repeat_interleave(torch.arange(idx.numel()), n_neg)
+    delta = g
+    if rep.numel():
+        gen = torch.Generator().manual_seed((int(seed) * 1000003 + int(epoch)) & 0x7FFFFFFF)
+        kk = torch.randint(0, n_tail, (rep.numel(),), generator=gen)
+        dn = cur[rep] - emb_tail[kk]
+        d2n = (dn * dn).sum(1, keepdim=True)
+        c = torch.where(d2n > 0, 2.0 * gamma * b / ((0.001 + d2n) * (a * d2n.clamp_min(1e-30) ** b + 1.0)),
+                        torch.zeros_like(d2n))
+        gn = torch.where(c > 0, (c * dn).clamp(-4, 4), torch.full_like(dn, 4.0))
+        skip = ((d2n <= 0) & (j[rep] == kk).view(-1, 1)).expand_as(gn)
+        gn = torch.where(skip, torch.zeros_like(gn), gn) * alpha
+        delta = delta + torch.zeros_like(g).index_add_(0, rep, gn)
+    next_neg[idx] += n_neg.float() * en
+    if move_other:
+        emb_tail.index_add_(0, k, -g)
+    emb_head.index_add_(0, j, delta)

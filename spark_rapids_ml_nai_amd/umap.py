@@ -1,0 +1,242 @@
+"""``umap.UMAP`` / ``UMAPModel`` (reference ``umap.py:90-1327``).
+
+Like the reference, the fit runs on ONE device over the whole (optionally ``sample_fraction``
+sampled) dataset and the model keeps ``embedding_`` (N x n_components) and ``raw_data_``
+(N x n_features); ``transform`` is data-parallel over partitions and outputs only the features
+and the embedding columns (``umap.py:1149-1241``). Persistence writes the two matrices as
+``.npy`` files next to the JSON metadata (``umap.py:1262-1327``).
+
+Supported: euclidean / l2 / sqeuclidean / cosine / correlation metrics, ``init`` spectral or
+random, supervised fits through ``labelCol`` (categorical target intersection), ``a``/``b``
+overrides, ``precomputed_knn`` (indices, distances), ``random_state``.
+"""
+from __future__ import annotations
+
+from typing import Any, Callable, Dict, List, Optional, Tuple, Union
+
+import numpy as np
+import torch
+
+from .core.base import _dense_from_df, _Estimator, _Model, run_worker_job
+from .core.dataframe import DataFrame, as_dataframe
+from .core.params import (
+    HasFeaturesCol,
+    HasFeaturesCols,
+    HasLabelCol,
+    HasOutputCol,
+    Param,
+    Params,
+    TypeConverters,
+    _BackendClass,
+    _BackendParams,
+    _FeaturesColMixin,
+    keyword_only,
+)
+from .parallel.context import WorkerContext
+
+_UMAP_KEYS = ("n_neighbors", "n_components", "metric", "n_epochs", "learning_rate", "init", "min_dist", "spread",
+              "set_op_mix_ratio", "local_connectivity", "repulsion_strength", "negative_sample_rate",
+              "transform_queue_size", "a", "b", "precomputed_knn", "random_state")
+
+
+class UMAPClass(_BackendClass):
+    @classmethod
+    def _param_mapping(cls) -> Dict[str, Optional[str]]:
+        return {k: k for k in _UMAP_KEYS}
+
+    def _get_backend_params_default(self) -> Dict[str, Any]:
+        return {
+            "n_neighbors": 15, "n_components": 2, "metric": "euclidean", "n_epochs": None, "learning_rate": 1.0,
+            "init": "spectral", "min_dist": 0.1, "spread": 1.0, "set_op_mix_ratio": 1.0, "local_connectivity": 1.0,
+            "repulsion_strength": 1.0, "negative_sample_rate": 5, "transform_queue_size": 4.0, "a": None, "b": None,
+            "precomputed_knn": None, "random_state": None, "verbose": False,
+        }
+
+
+def _p(name: str, doc: str, conv: Callable) -> Param:
+    return Param(Params._dummy(), name, doc, typeConverter=conv)
+
+
+class _UMAPParams(_FeaturesColMixin, _BackendParams, HasFeaturesCol, HasFeaturesCols, HasLabelCol, HasOutputCol):
+    n_neighbors = _p("n_neighbors", "The size of local neighborhood used for manifold approximation.",
+                     TypeConverters.toFloat)
+    n_components = _p("n_components", "The dimension of the space to embed into.", TypeConverters.toInt)
+    metric = _p("metric", "Distance metric (euclidean, l2, sqeuclidean, cosine, correlation).", TypeConverters.toString)
+    n_epochs = _p("n_epochs", "The number of training epochs (None: 500 for small, 200 for large datasets).",
+                  TypeConverters.identity)
+    learning_rate = _p("learning_rate", "The initial learning rate for the embedding optimization.",
+                       TypeConverters.toFloat)
+    init = _p("init", "How to initialize the low dimensional embedding: 'spectral' or 'random'.",
+              TypeConverters.toString)
+    min_dist = _p("min_dist", "The effective minimum distance between embedded points.", TypeConverters.toFloat)
+    spread = _p("spread", "The effective scale of embedded points.", TypeConverters.toFloat)
+    set_op_mix_ratio = _p("set_op_mix_ratio", "Interpolate between fuzzy union (1.0) and intersection (0.0).",
+                          TypeConverters.toFloat)
+    local_connectivity = _p("local_connectivity", "The local connectivity required.", TypeConverters.toFloat)
+    repulsion_strength = _p("repulsion_strength", "Weighting applied to negative samples.", TypeConverters.toFloat)
+    negative_sample_rate = _p("negative_sample_rate", "Negative samples per positive sample.", TypeConverters.toInt)
+    transform_queue_size = _p("transform_queue_size", "Accepted for compatibility (exact kNN is used).",
+                              TypeConverters.toFloat)
+    a = _p("a", "More specific parameters controlling the embedding.", TypeConverters.identity)
+    b = _p("b", "More specific parameters controlling the embedding.", TypeConverters.identity)
+    precomputed_knn = _p("precomputed_knn", "(indices, distances) of a precomputed kNN graph.",
+                         TypeConverters.identity)
+    random_state = _p("random_state", "Seed of the pseudo random number generator.", TypeConverters.identity)
+    sample_fraction = _p("sample_fraction", "Fraction of the dataset used for fitting.", TypeConverters.toFloat)
+
+    def __init__(self) -> None:
+        super().__init__()
+        self._setDefault(n_neighbors=15, n_components=2, metric="euclidean", n_epochs=None, learning_rate=1.0,
+                         init="spectral", min_dist=0.1, spread=1.0, set_op_mix_ratio=1.0, local_connectivity=1.0,
+                         repulsion_strength=1.0, negative_sample_rate=5, transform_queue_size=4.0, a=None, b=None,
+                         precomputed_knn=None, random_state=None, sample_fraction=1.0, outputCol="embedding",
+                         featuresCol="features")
+
+    def getSampleFraction(self) -> float:
+        return self.getOrDefault(self.sample_fraction)
+
+    def setSampleFraction(self, value: float) -> Any:
+        return self._set_params(sample_fraction=value)
+
+    def setOutputCol(self, value: str) -> Any:
+        return self._set_params(outputCol=value)
+
+    def _umap_params(self) -> Dict[str, Any]:
+        d = {k: self._backend_params.get(k) for k in _UMAP_KEYS}
+        d["n_neighbors"] = int(d["n_neighbors"]) if d["n_neighbors"] is not None else 15
+        return d
+
+    def _features(self, df: DataFrame) -> np.ndarray:
+        fc = self.getFeaturesCol()
+        col, cols = (fc, None) if isinstance(fc, str) else (None, list(fc))
+        return _dense_from_df(df, col, cols, np.float32)
+
+
+for _n in _UMAP_KEYS:
+    _cap = "".join(p.capitalize() for p in _n.split("_"))
+    _cap = _cap[0].lower() + _cap[1:]
+    if not hasattr(_UMAPParams, "get" + _cap[0].upper() + _cap[1:]):
+        setattr(_UMAPParams, "get" + _cap[0].upper() + _cap[1:], lambda self, _k=_n: self.getOrDefault(_k))
+    if not hasattr(_UMAPParams, "set" + _cap[0].upper() + _cap[1:]):
+        setattr(_UMAPParams, "set" + _cap[0].upper() + _cap[1:], lambda self, v, _k=_n: self._set_params(**{_k: v}))
+
+
+def _umap_fit_worker(ctx: WorkerContext, payload: Tuple[Any, ...]) -> Tuple[np.ndarray, np.ndarray]:
+    from .core.base import to_device
+    from .models.umap import umap_fit
+
+    X, y, params = payload
+    parts = ctx.comm.allgather_object((X, y)) if ctx.world_size > 1 else [(X, y)]
+    Xall = np.concatenate([p[0] for p in parts])
+    yall = None if parts[0][1] is None else np.concatenate([p[1] for p in parts])
+    emb = None
+    if ctx.rank == 0:
+        Xd = to_device(Xall, ctx.device, torch.float32)
+        yd = torch.as_tensor(yall) if yall is not None else None
+        emb = umap_fit(Xd, params, yd)
+    if ctx.world_size > 1:
+        emb = ctx.comm.broadcast_object(emb, 0)
+    return emb, Xall
+
+
+class UMAP(UMAPClass, _Estimator, _UMAPParams):
+    """Uniform Manifold Approximation and Projection.
+
+    >>> from spark_rapids_ml_nai_amd.umap import UMAP
+    >>> model = UMAP(n_neighbors=15, n_components=2, random_state=1).fit(df)  # doctest: +SKIP
+    >>> model.transform(df).select("embedding")  # doctest: +SKIP
+    """
+
+    @keyword_only
+    def __init__(self, *, n_neighbors: Optional[float] = 15, n_components: Optional[int] = 2,
+                 metric: str = "euclidean", n_epochs: Optional[int] = None, learning_rate: Optional[float] = 1.0,
+                 init: Optional[str] = "spectral", min_dist: Optional[float] = 0.1, spread: Optional[float] = 1.0,
+                 set_op_mix_ratio: Optional[float] = 1.0, local_connectivity: Optional[float] = 1.0,
+                 repulsion_strength: Optional[float] = 1.0, negative_sample_rate: Optional[int] = 5,
+                 transform_queue_size: Optional[float] = 4.0, a: Optional[float] = None, b: Optional[float] = None,
+                 precomputed_knn: Optional[Any] = None, random_state: Optional[int] = None,
+                 sample_fraction: Optional[float] = 1.0, featuresCol: Optional[Union[str, List[str]]] = None,
+                 labelCol: Optional[str] = None, outputCol: Optional[str] = None, num_workers: Optional[int] = None,
+                 verbose: Union[int, bool] = False, **kwargs: Any) -> None:
+        super().__init__()
+        self._set_params(**self._input_kwargs)
+
+    def _get_fit_func(self, dataset: DataFrame, extra_params: Optional[List[Dict[str, Any]]] = None) -> Callable:
+        raise NotImplementedError("UMAP fits through _fit")
+
+    def _create_model(self, result: Dict[str, Any]) -> "UMAPModel":
+        return UMAPModel._from_row(result)
+
+    def _fit(self, dataset: Any) -> "UMAPModel":
+        df, _ = as_dataframe(dataset)
+        frac = self.getSampleFraction()
+        if frac is not None and frac < 1.0:
+            seed = self._backend_params.get("random_state")
+            df = df.sample(frac, seed=seed)
+        y = None
+        if self.isDefined("labelCol") and self.getLabelCol() in df.columns:
+            y = df.to_numpy(self.getLabelCol()).astype(np.int64)
+        X = self._features(df)
+        params = self._umap_params()
+        # one fit task on one device, as in the reference (umap.py:840-850); under SPMD every rank
+        # contributes its rows, rank 0 fits and broadcasts the embedding
+        emb, Xall = run_worker_job(_umap_fit_worker, [(X, y, params)])[0]
+        model = UMAPModel(embedding_=emb, raw_data_=Xall, n_cols=int(Xall.shape[1]), dtype="float32")
+        model._num_workers = self._num_workers
+        model._float32_inputs = True
+        self._copyValues(model)
+        self._copy_backend_params(model)
+        return model
+
+
+class UMAPModel(UMAPClass, _Model, _UMAPParams):
+    def __init__(self, embedding_: Any, raw_data_: Any, n_cols: int, dtype: str) -> None:
+        emb = np.asarray(embedding_, dtype=np.float32)
+        raw = np.asarray(raw_data_, dtype=np.float32)
+        super().__init__(embedding_=emb, raw_data_=raw, n_cols=n_cols, dtype=dtype)
+        self.embedding_ = emb
+        self.raw_data_ = raw
+        self.n_cols = int(n_cols)
+        self.dtype = dtype
+
+    @property
+    def embedding(self) -> List[List[float]]:
+        return self.embedding_.tolist()
+
+    @property
+    def raw_data(self) -> List[List[float]]:
+        return self.raw_data_.tolist()
+
+    def _get_transform_func(self, dataset: DataFrame) -> Tuple[Callable, Callable]:
+        params = self._umap_params()
+        out_col = self.getOutputCol()
+        emb, raw = self.embedding_, self.raw_data_
+
+        def construct(ctx: WorkerContext) -> Tuple[torch.Tensor, torch.Tensor]:
+            return torch.from_numpy(raw).to(ctx.device), torch.from_numpy(emb).to(ctx.device)
+
+        def predict(state: Tuple[torch.Tensor, torch.Tensor], X: Any, ctx: WorkerContext) -> Dict[str, np.ndarray]:
+            from .core.base import to_device
+            from .models.umap import umap_transform
+
+            Rd, Ed = state
+            Xd = to_device(np.asarray(X, dtype=np.float32), ctx.device, torch.float32)
+            return {out_col: umap_transform(Xd, Rd, Ed, params)}
+
+        return construct, predict
+
+    def _transform_df(self, df: DataFrame) -> DataFrame:
+        out = super()._transform_df(df)
+        fc = self.getFeaturesCol()
+        if isinstance(fc, str):
+            return out.select(fc, self.getOutputCol())
+        # multi-column input: emit one "features" array column like the reference
+        from .core.dataframe import dense_to_list_array
+
+        parts = []
+        for p in out.partitions:
+            part = DataFrame([p])
+            X = _dense_from_df(part, None, list(fc), np.float32)
+            part = part.withColumn("features", dense_to_list_array(X))
+            parts.append(part.select("features", self.getOutputCol()).partitions[0])
+        return DataFrame(parts)

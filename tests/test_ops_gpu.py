@@ -309,3 +309,40 @@ def test_uf_unite_pairs(gpu_device):
     ops.uf_unite_pairs(p, other.to(gpu_device))
     ops.uf_compress(p)
     assert torch.equal(p.cpu(), p_ref)
+
+
+@pytest.mark.parametrize("dim", [2, 3, 5])
+def test_umap_epoch_attraction(gpu_device, dim):
+    # disjoint edges (2i -> 2i+1), no negative samples: the GPU update must equal the CPU reference
+    N = 2000
+    g = torch.Generator().manual_seed(dim)
+    emb = torch.rand(N, dim, generator=g) * 10
+    head = torch.arange(0, N, 2, dtype=torch.int32)
+    tail = head + 1
+    E = head.numel()
+    eps = torch.ones(E)
+    eps_neg = torch.zeros(E)
+    args = dict(a=1.577, b=0.895, gamma=1.0, alpha=0.7, epoch=1, move_other=True, seed=3)
+    e_cpu = emb.clone()
+    ops.umap_epoch(head, tail, eps, eps.clone(), torch.zeros(E), eps_neg, e_cpu, e_cpu, **args)
+    e_gpu = emb.clone().to(gpu_device)
+    ops.umap_epoch(head.to(gpu_device), tail.to(gpu_device), eps.to(gpu_device), eps.clone().to(gpu_device),
+                   torch.zeros(E, device=gpu_device), eps_neg.to(gpu_device), e_gpu, e_gpu, **args)
+    torch.testing.assert_close(e_gpu.cpu(), e_cpu, rtol=1e-4, atol=1e-4)
+    assert not torch.allclose(e_cpu, emb)
+
+
+def test_umap_epoch_negative_samples(gpu_device):
+    # repulsion only pushes points apart: mean pairwise spread must grow
+    N, dim = 3000, 2
+    g = torch.Generator().manual_seed(0)
+    emb = (torch.rand(N, dim, generator=g) * 0.5).to(gpu_device)
+    head = torch.arange(N, dtype=torch.int32, device=gpu_device)
+    tail = torch.roll(head, 1)
+    E = N
+    eps = torch.ones(E, device=gpu_device)
+    before = emb.std(0).sum().item()
+    ops.umap_epoch(head, tail, eps, eps.clone(), torch.zeros(E, device=gpu_device), eps / 5, emb, emb,
+                   a=1.577, b=0.895, gamma=1.0, alpha=1.0, epoch=1, move_other=True, seed=1)
+    assert torch.isfinite(emb).all()
+    assert emb.std(0).sum().item() > before

@@ -1,0 +1,88 @@
+"""UMAP (reference tests/test_umap.py): quality gate = trustworthiness (sklearn) — the reference
+allows a gap <= 0.15 vs single-GPU cuML; umap-learn reaches ~0.98 on digits, we require >= 0.9."""
+import warnings
+
+import numpy as np
+import pytest
+from sklearn.datasets import load_digits, make_blobs
+from sklearn.manifold import trustworthiness
+
+from spark_rapids_ml_nai_amd import DataFrame
+from spark_rapids_ml_nai_amd.umap import UMAP, UMAPModel
+
+warnings.filterwarnings("ignore")
+
+
+def _digits(n=1200):
+    X, y = load_digits(return_X_y=True)
+    return X[:n].astype(np.float32), y[:n]
+
+
+def test_params():
+    u = UMAP()
+    assert u.cuml_params["n_neighbors"] == 15 and u.cuml_params["n_components"] == 2
+    assert u.getOutputCol() == "embedding"
+    u2 = UMAP(n_neighbors=10, min_dist=0.2, random_state=3)
+    assert u2.cuml_params["n_neighbors"] == 10 and u2.cuml_params["min_dist"] == 0.2
+    assert u2.cuml_params["random_state"] == 3
+
+
+def test_find_ab_params():
+    from spark_rapids_ml_nai_amd.models.umap import find_ab_params
+
+    a, b = find_ab_params(1.0, 0.1)
+    assert abs(a - 1.577) < 0.01 and abs(b - 0.895) < 0.01
+
+
+@pytest.mark.parametrize("init", ["spectral", "random"])
+def test_umap_fit_transform_trustworthiness(init, tmp_path):
+    X, y = _digits()
+    df = DataFrame.from_numpy(X, num_partitions=2)
+    model = UMAP(n_neighbors=15, random_state=1, init=init).setFeaturesCol("features").fit(df)
+    emb = np.asarray(model.embedding)
+    assert emb.shape == (len(X), 2)
+    assert trustworthiness(X, emb, n_neighbors=15) > 0.9
+    out = model.transform(df)
+    assert out.columns == ["features", "embedding"]
+    e2 = out.to_numpy("embedding")
+    assert e2.shape == (len(X), 2) and np.isfinite(e2).all()
+    assert trustworthiness(X, e2, n_neighbors=15) > 0.85
+    # persistence (npy side files)
+    path = str(tmp_path / "umap")
+    model.write().overwrite().save(path)
+    m2 = UMAPModel.load(path)
+    assert np.allclose(m2.embedding_, model.embedding_)
+    assert np.allclose(m2.raw_data_, model.raw_data_)
+    assert m2.getOrDefault("n_neighbors") == 15
+
+
+def test_umap_supervised_separates_classes():
+    X, y = make_blobs(800, 10, centers=4, cluster_std=4.0, random_state=0)
+    X = X.astype(np.float32)
+    df = DataFrame.from_numpy(X, y.astype(np.float64))
+    model = UMAP(random_state=2, labelCol="label").fit(df)
+    emb = model.embedding_
+    cent = np.stack([emb[y == c].mean(0) for c in range(4)])
+    within = np.mean([np.linalg.norm(emb[y == c] - cent[c], axis=1).mean() for c in range(4)])
+    between = np.mean([np.linalg.norm(cent[i] - cent[j]) for i in range(4) for j in range(i + 1, 4)])
+    assert between > 2 * within
+
+
+def test_umap_sample_fraction_and_cosine():
+    X, _ = _digits(800)
+    df = DataFrame.from_numpy(X)
+    model = UMAP(sample_fraction=0.5, metric="cosine", random_state=4, n_components=3).fit(df)
+    assert 300 < model.embedding_.shape[0] < 500
+    assert model.embedding_.shape[1] == 3
+    out = model.transform(df).to_numpy("embedding")
+    assert out.shape == (800, 3)
+
+
+def test_umap_multi_column_input():
+    X, _ = make_blobs(300, 3, centers=3, random_state=5)
+    import pandas as pd
+
+    df = DataFrame.from_pandas(pd.DataFrame({"a": X[:, 0], "b": X[:, 1], "c": X[:, 2]}))
+    model = UMAP(random_state=0).setFeaturesCols(["a", "b", "c"]).fit(df)
+    out = model.transform(df)
+    assert out.columns == ["features", "embedding"]

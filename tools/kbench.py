@@ -116,6 +116,23 @@ def main():
         ctx = WorkerContext.single(dev)
         t = timeit(lambda: dbscan_fit_predict(Xd, ctx, 10.0, 5), 2)
         res["dbscan_fit_200k_x64"] = {"ms": t}
+    if want("umap"):
+        # reference notebook config: blobs 100k x 3000, fit on a 50% sample (GPU 24.94 s there)
+        from spark_rapids_ml_nai_amd.models.umap import umap_fit, umap_transform
+
+        Nu, nu = 100_000, 3000
+        C = torch.randn(10, nu, device=dev, generator=g) * 4
+        Xu = C[torch.randint(0, 10, (Nu,), device=dev, generator=g)] + torch.randn(Nu, nu, device=dev, generator=g)
+        Xs = Xu[torch.randperm(Nu, device=dev, generator=g)[: Nu // 2]].contiguous()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        emb = umap_fit(Xs, dict(n_neighbors=15, n_components=2, random_state=1))
+        torch.cuda.synchronize()
+        res["umap_fit_50k_x3000"] = {"ms": (time.perf_counter() - t0) * 1e3}
+        t0 = time.perf_counter()
+        umap_transform(Xu, Xs, torch.from_numpy(emb).to(dev), dict(n_neighbors=15, random_state=1))
+        torch.cuda.synchronize()
+        res["umap_transform_100k_x3000"] = {"ms": (time.perf_counter() - t0) * 1e3}
     print(json.dumps({k: {kk: round(vv, 3) for kk, vv in v.items()} for k, v in res.items()}))
 
 
