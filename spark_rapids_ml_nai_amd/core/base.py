@@ -541,7 +541,50 @@ class _Model(_CommonBase):
 
     # ---- evaluation in the transform pass (CrossValidator fast path) ----------------------
     def _transformEvaluate(self, dataset: Any, evaluator: Any, num_models: int = 1, params: Any = None) -> List[float]:
-        raise NotImplementedError()
+        """Transform + evaluate every combined model in ONE pass over ``dataset`` (reference
+        ``core.py:1318-1468``): each partition's features are moved to the device once and all
+        models predict from that copy; the evaluator then scores each model's predictions."""
+        models = getattr(self, "_combined_models", None) or [self]
+        if params:
+            models = [m.copy(params) for m in models]
+        df, _ = as_dataframe(dataset)
+        label_col = evaluator.getLabelCol()
+        if label_col not in df.columns:
+            raise RuntimeError("Label column is not existing.")
+        ctx = current_context() or WorkerContext.single(self._device())
+        fns = [m._get_transform_func(df) for m in models]
+        states = [c(ctx) for c, _ in fns]
+        outs: List[Dict[str, List[np.ndarray]]] = [dict() for _ in models]
+        dt = torch.float32 if self._transform_dtype() == np.float32 else torch.float64
+        for p in df.partitions:
+            if p.num_rows == 0:
+                continue
+            X = self._transform_features(DataFrame([p]))
+            Xd = to_device(X, ctx.device, dt)
+            for i, ((_, predict), st) in enumerate(zip(fns, states)):
+                for k, v in predict(st, Xd, ctx).items():
+                    outs[i].setdefault(k, []).append(np.asarray(v))
+        label = df.to_numpy(label_col)
+        metrics = []
+        for m, o in zip(models, outs):
+            cols: Dict[str, Any] = {label_col: label}
+            for k, parts in o.items():
+                cols[k] = np.concatenate(parts) if parts else np.zeros(0)
+            ev = evaluator.copy()
+            pc = m.getOrDefault("predictionCol") if m.hasParam("predictionCol") else "prediction"
+            if ev.hasParam("predictionCol") and pc in cols:
+                ev._set(predictionCol=pc)
+            for pname in ("probabilityCol", "rawPredictionCol"):
+                if ev.hasParam(pname) and m.hasParam(pname) and m.getOrDefault(pname) in cols:
+                    ev._set(**{pname: m.getOrDefault(pname)})
+            import pyarrow as pa
+
+            from .dataframe import dense_to_list_array
+
+            edf = DataFrame([pa.table({k: dense_to_list_array(v) if v.ndim == 2 else pa.array(v)
+                                       for k, v in cols.items()})])
+            metrics.append(float(ev.evaluate(edf)))
+        return metrics
 
     @classmethod
     def _combine(cls, models: List["_Model"]) -> "_Model":
