@@ -676,3 +676,22 @@ def umap_epoch(head: torch.Tensor, tail: torch.Tensor, eps: torch.Tensor, next_s
     if move_other:
         emb_tail.index_add_(0, k, -g)
     emb_head.index_add_(0, j, delta)
+
+
+# ------------------------------------------------------------------------------------------
+# Symmetric eigensolver (parallel Jacobi, fp64)
+# ------------------------------------------------------------------------------------------
+def syevj(A: torch.Tensor, max_sweeps: int = 30, tol: float = 1e-15) -> Tuple[torch.Tensor, torch.Tensor]:
+    """All eigenpairs of a symmetric matrix: (eigenvalues descending, eigenvectors as columns)."""
+    n = A.shape[0]
+    if not A.is_cuda:
+        w, V = torch.linalg.eigh(A.double())
+        return w.flip(0), V.flip(1)
+    A = _c(A.double())
+    W = torch.empty(n, dtype=torch.float64, device=A.device)
+    V = torch.empty((n, n), dtype=torch.float64, device=A.device)
+    fn = getattr(native.lib(), "srml_syevj_f64")
+    rc = fn(A.data_ptr(), n, W.data_ptr(), V.data_ptr(), int(max_sweeps), float(tol), native.stream(A.device))
+    if rc < 0:
+        raise RuntimeError("srml_syevj_f64 failed with status %d" % rc)
+    return W, V

@@ -78,4 +78,11 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
 
 static inline int srml_status() { return (int)hipGetLastError(); }
 
+// keep the first failing HIP runtime status of a multi-call host routine in `err`
+#define SRML_TRY(err, call)                                  \
+  do {                                                       \
+    hipError_t e_ = (call);                                  \
+    if (e_ != hipSuccess && (err) == hipSuccess) (err) = e_; \
+  } while (0)
+
 static inline unsigned ceil_div(long a, long b) { return (unsigned)((a + b - 1) / b); }
