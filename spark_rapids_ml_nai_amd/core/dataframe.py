@@ -365,6 +365,33 @@ class DataFrame:
         pdf = pd.DataFrame({n: pd.Series(v, dtype=object if _needs_object(v) else None) for n, v in cols.items()})
         return cls.from_pandas(pdf, num_partitions)
 
+    @classmethod
+    def read_parquet(cls, path: str, columns: Optional[List[str]] = None) -> "DataFrame":
+        """One partition per Parquet file (a directory of part files, or a single file)."""
+        import glob
+        import os
+
+        import pyarrow.parquet as pq
+
+        files = sorted(glob.glob(os.path.join(path, "*.parquet"))) if os.path.isdir(path) else [path]
+        if not files:
+            raise FileNotFoundError("no parquet files under %s" % path)
+        return cls([pq.read_table(f, columns=columns) for f in files])
+
+    def write_parquet(self, path: str, overwrite: bool = False) -> None:
+        import os
+        import shutil
+
+        import pyarrow.parquet as pq
+
+        if os.path.exists(path):
+            if not overwrite:
+                raise FileExistsError(path)
+            shutil.rmtree(path)
+        os.makedirs(path)
+        for i, p in enumerate(self._parts):
+            pq.write_table(p, os.path.join(path, "part-%05d.parquet" % i))
+
     # ---- schema -------------------------------------------------------------------
     @property
     def schema(self) -> pa.Schema:

@@ -1,0 +1,63 @@
+"""Benchmark tooling (reference python/benchmark/test_gen_data.py + benchmark runner smoke)."""
+import os
+import warnings
+
+import numpy as np
+import pytest
+
+from spark_rapids_ml_nai_amd import DataFrame
+from spark_rapids_ml_nai_amd.bench import gen_data, runner
+
+warnings.filterwarnings("ignore")
+
+
+@pytest.mark.parametrize("kind", gen_data.TYPES)
+@pytest.mark.parametrize("feature_type", ["array", "vector", "multi_cols"])
+def test_gen_data(tmp_path, kind, feature_type):
+    out = str(tmp_path / kind)
+    counts = gen_data.generate([kind, "--num_rows", "500", "--num_cols", "6", "--feature_type", feature_type,
+                                "--output_num_files", "3", "--output_dir", out, "--device", "cpu"])
+    assert counts[out] == 500
+    df = DataFrame.read_parquet(out)
+    assert df.getNumPartitions() == 3 and df.count() == 500
+    if kind == "sparse_regression" or feature_type == "vector":
+        assert df.is_vector("feature_array")
+    elif feature_type == "array":
+        assert df.to_numpy("feature_array").shape == (500, 6)
+    else:
+        assert [c for c in df.columns if c != "label"] == ["c%d" % i for i in range(6)]
+    if kind in ("blobs", "regression", "classification", "sparse_regression"):
+        assert "label" in df.columns
+
+
+def test_gen_data_train_fraction_and_determinism(tmp_path):
+    a = str(tmp_path / "a")
+    b = str(tmp_path / "b")
+    for o in (a, b):
+        gen_data.generate(["regression", "--num_rows", "400", "--num_cols", "4", "--feature_type", "array",
+                           "--output_num_files", "2", "--output_dir", o, "--train_fraction", "0.75", "--device", "cpu"])
+    ta = DataFrame.read_parquet(os.path.join(a, "train"))
+    tb = DataFrame.read_parquet(os.path.join(b, "train"))
+    ea = DataFrame.read_parquet(os.path.join(a, "eval"))
+    assert ta.count() + ea.count() == 400
+    assert np.array_equal(ta.to_numpy("feature_array"), tb.to_numpy("feature_array"))
+
+
+@pytest.mark.parametrize("algo,kind,extra", [
+    ("kmeans", "blobs", ["--k", "4", "--maxIter", "5"]),
+    ("linear_regression", "regression", ["--regParam", "0.0"]),
+    ("random_forest_classifier", "classification", ["--numTrees", "3", "--maxDepth", "4"]),
+    ("approximate_nearest_neighbors", "blobs", ["--k", "4", "--algoParams", "{'nlist': 4, 'nprobe': 4}"]),
+])
+def test_runner(tmp_path, algo, kind, extra):
+    out = str(tmp_path / kind)
+    gen_data.generate([kind, "--num_rows", "600", "--num_cols", "8", "--feature_type", "array",
+                       "--output_num_files", "2", "--output_dir", out, "--device", "cpu"])
+    rep = str(tmp_path / "report.csv")
+    rows = runner.run([algo, "--train_path", out, "--report_path", rep] + extra)
+    assert rows[0]["fit"] > 0 and rows[0]["total"] >= rows[0]["fit"]
+    assert os.path.exists(rep)
+    if algo == "kmeans":
+        assert rows[0]["inertia"] > 0
+    if algo == "approximate_nearest_neighbors":
+        assert rows[0]["avg_recall"] >= 0.95
