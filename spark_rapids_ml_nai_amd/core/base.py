@@ -290,14 +290,22 @@ class _Estimator(_CommonBase):
     def _fit_internal(self, dataset: Any, paramMaps: Optional[Sequence[Dict[Param, Any]]]) -> List["_Model"]:
         self._validate_parameters()
         timer = PhaseTimer()
-        df, _ = as_dataframe(dataset)
         fit_multiple = self._backend_param_maps(paramMaps)
         params = {
             param_alias.cuml_init: dict(self._backend_params),
             param_alias.fit_multiple_params: fit_multiple,
         }
-        fit_fn = self._get_fit_func(df, fit_multiple or None)
-        results = run_fit_job(self, df, fit_fn, params, timer)
+        from ..parallel.spark import is_spark_dataframe, run_spark_fit
+
+        if is_spark_dataframe(dataset):
+            # Spark barrier stage: one task per GPU, RCCL bootstrapped through allGather
+            fit_fn = self._get_fit_func(dataset, fit_multiple or None)
+            with timer.phase("fit"):
+                results = run_spark_fit(self, dataset, fit_fn, params)
+        else:
+            df, _ = as_dataframe(dataset)
+            fit_fn = self._get_fit_func(df, fit_multiple or None)
+            results = run_fit_job(self, df, fit_fn, params, timer)
         if not isinstance(results, list):
             results = [results]
         models = []
@@ -490,6 +498,17 @@ class _Model(_CommonBase):
     def _vector_output_cols(self) -> List[str]:
         return []
 
+    def _spark_output_fields(self, sdf: Any) -> List[Any]:
+        """Spark schema of the columns ``transform`` appends (prediction double, array outputs)."""
+        from pyspark.sql.types import ArrayType, DoubleType, StructField  # type: ignore
+
+        out = []
+        for pname, arr in (("predictionCol", False), ("probabilityCol", True), ("rawPredictionCol", True),
+                           ("outputCol", True)):
+            if self.hasParam(pname) and self.isDefined(pname) and self.getOrDefault(pname):
+                out.append(StructField(self.getOrDefault(pname), ArrayType(DoubleType()) if arr else DoubleType()))
+        return out
+
     def _device(self) -> torch.device:
         ctx = current_context()
         if ctx is not None:
@@ -504,6 +523,10 @@ class _Model(_CommonBase):
         return self._transform(dataset)
 
     def _transform(self, dataset: Any) -> Any:
+        from ..parallel.spark import is_spark_dataframe, spark_transform
+
+        if is_spark_dataframe(dataset):
+            return spark_transform(self, dataset)
         df, kind = as_dataframe(dataset)
         out = self._transform_df(df)
         return restore_kind(out, kind)

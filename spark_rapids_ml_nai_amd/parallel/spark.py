@@ -1,0 +1,285 @@
+"""Spark integration: barrier-mode fit stage, per-batch transform, stage-level scheduling.
+
+Reference: ``_CumlCaller._call_cuml_fit_func`` / ``_train_udf`` (``core.py:622-787``) runs the
+algorithm closure in ``mapInPandas(...).rdd.barrier().mapPartitions`` tasks, bootstraps NCCL by
+sending the unique id through ``BarrierTaskContext.allGather`` (``common/cuml_context.py:35-124``)
+and yields the model attributes from rank 0. Here the same stage runs our worker closure:
+
+* rendezvous: every task ``allGather``s ``host:port`` (rank 0 binds a free port); rank 0 hosts the
+  ``torch.distributed`` TCP store and the group comes up on RCCL (``"nccl"``) over xGMI / RoCE,
+  or gloo for CPU tasks. Only this tiny bootstrap blob goes through the driver — every numeric
+  exchange (partition sizes, moments, forests, kNN partials) is a device collective;
+* device: the task's ``gpu`` resource address (cluster) or ``partitionId % device_count`` (local);
+* the pandas batches of the partition become one Arrow table -> ``HostPartition`` -> device
+  (pinned staging) exactly like the Spark-free paths, so the same ``_fit_worker`` runs;
+* failure: an exception aborts the communicator (``ncclCommAbort``), the barrier stage fails and
+  Spark retries it as a whole (reference semantics);
+* stage-level scheduling (``core.py:901-1004``): training tasks ask for a whole GPU and more than
+  half the executor cores so that two training tasks never share an executor.
+
+pyspark is optional: importing this module never requires it; the worker entry point works with
+any object offering ``partitionId() / allGather(str) / barrier()`` (tests drive it with a
+multi-process stand-in for ``BarrierTaskContext``).
+"""
+from __future__ import annotations
+
+import os
+import socket
+from datetime import timedelta
+from typing import Any, Callable, Dict, Iterable, Iterator, List, Optional, Tuple
+
+import cloudpickle
+
+
+def spark_available() -> bool:
+    try:
+        import pyspark  # noqa: F401
+
+        return True
+    except Exception:  # noqa: BLE001
+        return False
+
+
+def is_spark_dataframe(obj: Any) -> bool:
+    mod = type(obj).__module__
+    return mod.startswith("pyspark.sql") and type(obj).__name__ in ("DataFrame",)
+
+
+# ------------------------------------------------------------------------------------------
+# stage-level scheduling (pure decision logic, reference core.py:901-1004)
+# ------------------------------------------------------------------------------------------
+def _ver(v: str) -> Tuple[int, ...]:
+    out = []
+    for p in v.split(".")[:3]:
+        digits = "".join(ch for ch in p if ch.isdigit())
+        out.append(int(digits) if digits else 0)
+    return tuple(out + [0] * (3 - len(out)))
+
+
+def stage_level_scheduling_plan(spark_version: str, conf: Dict[str, Optional[str]], master: str,
+                                spark_plugins: str = "", rapids_sql_enabled: str = "true"
+                                ) -> Optional[Tuple[int, float]]:
+    """(task_cores, task_gpus) for the training stage, or None to leave scheduling alone."""
+    if master.startswith("local[") or master == "local":
+        return None
+    if _ver(spark_version) < (3, 4, 0):
+        return None
+    standalone = master.startswith("spark://") or master.startswith("local-cluster")
+    if (3, 4, 0) <= _ver(spark_version) < (3, 5, 1) and not standalone:
+        return None
+    cores, gpus = conf.get("spark.executor.cores"), conf.get("spark.executor.resource.gpu.amount")
+    if cores is None or gpus is None or int(cores) == 1 or float(gpus) > 1:
+        return None
+    task_gpus = conf.get("spark.task.resource.gpu.amount")
+    if task_gpus is not None and float(task_gpus) == float(gpus):
+        return None
+    plugin_sql = "SQLPlugin" in (spark_plugins or "") and (rapids_sql_enabled or "true").lower() == "true"
+    task_cores = int(cores) if plugin_sql else int(cores) // 2 + 1
+    return task_cores, 1.0
+
+
+def _try_stage_level_scheduling(rdd: Any, spark: Any) -> Any:
+    sc = spark.sparkContext
+    conf = {k: sc.getConf().get(k) for k in ("spark.executor.cores", "spark.executor.resource.gpu.amount",
+                                             "spark.task.resource.gpu.amount")}
+    plan = stage_level_scheduling_plan(spark.version, conf, sc.master, spark.conf.get("spark.plugins", ""),
+                                       spark.conf.get("spark.rapids.sql.enabled", "true"))
+    if plan is None:
+        return rdd
+    from pyspark.resource.profile import ResourceProfileBuilder  # type: ignore
+    from pyspark.resource.requests import TaskResourceRequests  # type: ignore
+
+    treqs = TaskResourceRequests().cpus(plan[0]).resource("gpu", plan[1])
+    return rdd.withResources(ResourceProfileBuilder().require(treqs).build)
+
+
+# ------------------------------------------------------------------------------------------
+# worker side
+# ------------------------------------------------------------------------------------------
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("", 0))
+        return int(s.getsockname()[1])
+
+
+def _local_ip() -> str:
+    try:
+        with socket.socket(socket.AF_INET, socket.SOCK_DGRAM) as s:
+            s.connect(("10.255.255.255", 1))
+            return s.getsockname()[0]
+    except OSError:
+        return "127.0.0.1"
+
+
+def _task_device(task_ctx: Any, use_gpu: bool) -> Any:
+    import torch
+
+    if not use_gpu:
+        return torch.device("cpu")
+    addr = None
+    try:
+        res = task_ctx.resources()
+        if "gpu" in res and res["gpu"].addresses:
+            addr = int(res["gpu"].addresses[0])
+    except Exception:  # noqa: BLE001 - stand-in contexts / local mode
+        addr = None
+    n = torch.cuda.device_count()
+    if addr is None:
+        addr = task_ctx.partitionId() % max(n, 1)
+    return torch.device("cuda", addr % max(n, 1))
+
+
+def init_barrier_group(task_ctx: Any, use_gpu: bool, timeout_s: float = 1800.0) -> Any:
+    """torch.distributed bootstrap through the barrier allGather; returns a WorkerContext."""
+    import torch
+    import torch.distributed as dist
+
+    from .context import WorkerContext
+
+    rank = task_ctx.partitionId()
+    host = os.environ.get("SRML_RENDEZVOUS_HOST") or _local_ip()
+    port = _free_port() if rank == 0 else 0
+    infos = task_ctx.allGather("%s:%d" % (host, port))
+    world = len(infos)
+    master_host, master_port = infos[0].rsplit(":", 1)
+    device = _task_device(task_ctx, use_gpu)
+    if device.type == "cuda":
+        torch.cuda.set_device(device)
+    store = dist.TCPStore(master_host, int(master_port), world, is_master=(rank == 0),
+                          timeout=timedelta(seconds=timeout_s))
+    dist.init_process_group("nccl" if device.type == "cuda" else "gloo", store=store, rank=rank, world_size=world,
+                            timeout=timedelta(seconds=timeout_s),
+                            **({"device_id": device} if device.type == "cuda" else {}))
+    return WorkerContext.from_process_group(device)
+
+
+def batches_to_table(batches: Iterable[Any], vector_cols: List[str]) -> Any:
+    """pandas batches of one partition -> one Arrow table (vector structs tagged as VectorUDT)."""
+    import pyarrow as pa
+
+    from ..core.dataframe import vector_field
+
+    tables = [pa.Table.from_pandas(b, preserve_index=False) for b in batches]
+    tables = [t for t in tables if t.num_rows > 0] or tables[:1]
+    t = pa.concat_tables(tables) if len(tables) > 1 else tables[0]
+    fields = [vector_field(f.name) if f.name in vector_cols else f for f in t.schema]
+    return pa.Table.from_arrays(t.columns, schema=pa.schema(fields))
+
+
+def spark_worker_entry(task_ctx: Any, batches: Iterable[Any], payload: bytes) -> Iterator[Any]:
+    """Body of one barrier fit task (reference ``_train_udf``, core.py:694-779)."""
+    import pandas as pd
+
+    from ..core.base import _fit_worker
+    from ..core.dataframe import DataFrame
+    from .context import use_context
+
+    est, fit_fn, params, float32, vector_cols, use_gpu = cloudpickle.loads(payload)
+    ctx = init_barrier_group(task_ctx, use_gpu)
+    try:
+        table = batches_to_table(batches, vector_cols)
+        hp = est._host_partition(DataFrame([table]))
+        with use_context(ctx):
+            res = _fit_worker(ctx, (hp, fit_fn, params, float32))
+        ctx.comm.barrier()
+    except BaseException:
+        ctx.comm.abort()
+        raise
+    import torch.distributed as dist
+
+    dist.destroy_process_group()
+    if task_ctx.partitionId() == 0:
+        yield pd.DataFrame({"result": [cloudpickle.dumps(res)]})
+
+
+# ------------------------------------------------------------------------------------------
+# driver side
+# ------------------------------------------------------------------------------------------
+def _unwrap_vectors(sdf: Any) -> Tuple[Any, List[str]]:
+    from pyspark.ml.linalg import VectorUDT  # type: ignore
+    from pyspark.sql import functions as F  # type: ignore
+
+    vec = [f.name for f in sdf.schema.fields if isinstance(f.dataType, VectorUDT)]
+    for c in vec:
+        sdf = sdf.withColumn(c, F.unwrap_udt(F.col(c)))
+    return sdf, vec
+
+
+def run_spark_fit(est: Any, sdf: Any, fit_fn: Callable, params: Dict[str, Any]) -> Any:
+    from pyspark.sql import SparkSession  # type: ignore
+
+    from .context import gpu_available
+
+    spark = SparkSession.getActiveSession()
+    nw = est.num_workers
+    col, cols = est._get_input_columns()
+    keep = list(cols or [col])
+    if est._fit_uses_label():
+        keep.append(est.getOrDefault("labelCol"))
+    keep += [c for c in est._fit_extra_cols() if c in sdf.columns]
+    sdf = sdf.select(*keep)
+    if sdf.rdd.getNumPartitions() != nw:
+        sdf = sdf.repartition(nw)
+    sdf, vec = _unwrap_vectors(sdf)
+    use_gpu = os.environ.get("SRML_FORCE_CPU", "0") != "1" and (gpu_available() or _cluster_has_gpus(spark))
+    payload = cloudpickle.dumps((est, fit_fn, params, est._float32_inputs, vec, use_gpu))
+
+    def _train(it: Iterator[Any]) -> Iterator[Any]:
+        from pyspark import BarrierTaskContext  # type: ignore
+
+        return spark_worker_entry(BarrierTaskContext.get(), it, payload)
+
+    rdd = sdf.mapInPandas(_train, schema="result binary").rdd.barrier().mapPartitions(lambda x: x)
+    rdd = _try_stage_level_scheduling(rdd, spark)
+    rows = rdd.collect()
+    return cloudpickle.loads(rows[0]["result"])
+
+
+def _cluster_has_gpus(spark: Any) -> bool:
+    return spark.sparkContext.getConf().get("spark.executor.resource.gpu.amount") is not None
+
+
+def spark_transform(model: Any, sdf: Any) -> Any:
+    """Per-batch transform with the model's device predict function (reference ``_transform``,
+    core.py:1419-1435 / 1537-1557): one model construction per task, pinned device per task."""
+    import numpy as np
+    import pandas as pd
+    import pyarrow as pa
+
+    from ..core.dataframe import DataFrame
+
+    sdf_u, vec = _unwrap_vectors(sdf)
+    blob = cloudpickle.dumps((model, vec))
+    out_fields = model._spark_output_fields(sdf)
+
+    def _predict(it: Iterator[Any]) -> Iterator[Any]:
+        import torch
+
+        from pyspark import TaskContext  # type: ignore
+
+        from .context import WorkerContext, gpu_available
+
+        m, vcols = cloudpickle.loads(blob)
+        tc = TaskContext.get()
+        dev = _task_device(tc, gpu_available()) if tc is not None else torch.device("cpu")
+        ctx = WorkerContext.single(dev)
+        construct, predict = m._get_transform_func(None)
+        state = construct(ctx)
+        for pdf in it:
+            if len(pdf) == 0:
+                continue
+            table = batches_to_table([pdf], vcols)
+            part = DataFrame([table])
+            X = m._transform_features(part)
+            res = predict(state, X, ctx)
+            out = pdf.copy()
+            for k, v in res.items():
+                v = np.asarray(v)
+                out[k] = list(v) if v.ndim == 2 else v
+            yield out
+
+    schema = sdf_u.schema
+    from pyspark.sql.types import StructType  # type: ignore
+
+    out_schema = StructType(list(schema.fields) + out_fields)
+    return sdf_u.mapInPandas(_predict, schema=out_schema)
