@@ -339,6 +339,7 @@ class _EstimatorSupervised(_Estimator):
 def _fit_worker(ctx: WorkerContext, payload: Tuple[HostPartition, Callable, Dict[str, Any], bool]) -> Any:
     """Body of one barrier task: ingest to device, describe partitions, run the fit closure."""
     hp, fit_fn, params, float32 = payload
+    _maybe_inject_fault(ctx, "ingest")
     if hp.rows == 0:
         raise RuntimeError("A worker received no data. Please increase amount of data or use fewer workers.")
     dtype = torch.float32 if float32 else torch.float64
@@ -346,7 +347,28 @@ def _fit_worker(ctx: WorkerContext, payload: Tuple[HostPartition, Callable, Dict
     y = to_device(hp.y, ctx.device) if hp.y is not None else None
     desc = PartitionDescriptor.build(ctx, hp.rows, hp.n_cols)
     inp = FitInput(X=X, y=y, cols=hp.cols, desc=desc, host=hp)
+    _maybe_inject_fault(ctx, "fit")
     return fit_fn(inp, ctx, params)
+
+
+def _maybe_inject_fault(ctx: WorkerContext, stage: str) -> None:
+    """Fault injection for failure-path tests: ``SRML_FAULT_RANK=<r>`` (``all`` for every rank),
+    ``SRML_FAULT_STAGE=ingest|fit`` (default fit), ``SRML_FAULT_MODE=raise|exit|hang``."""
+    import os
+
+    who = os.environ.get("SRML_FAULT_RANK")
+    if who is None or os.environ.get("SRML_FAULT_STAGE", "fit") != stage:
+        return
+    if who != "all" and int(who) != ctx.rank:
+        return
+    mode = os.environ.get("SRML_FAULT_MODE", "raise")
+    if mode == "exit":
+        os._exit(17)
+    if mode == "hang":
+        import time
+
+        time.sleep(3600)
+    raise RuntimeError("injected fault on rank %d at %s" % (ctx.rank, stage))
 
 
 def run_fit_job(est: _Estimator, df: DataFrame, fit_fn: Callable, params: Dict[str, Any],

@@ -82,6 +82,7 @@ def run_barrier_job(
     from .context import gpu_available
 
     world = len(per_rank_inputs)
+    timeout_s = float(os.environ.get("SRML_BARRIER_TIMEOUT", timeout_s))
     if use_gpu is None:
         use_gpu = gpu_available()
     # always spawn: forking a process whose torch CPU thread pool (OpenMP) or HIP runtime is

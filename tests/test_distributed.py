@@ -91,3 +91,37 @@ def test_random_forest_two_ranks(mode):
     acc = lambda m: (m.transform(df).to_numpy("prediction") == y).mean()
     # reference gate: multi-worker accuracy within 0.07 of single worker
     assert abs(acc(a) - acc(b)) < 0.07
+
+
+@pytest.mark.parametrize("mode", ["raise", "exit"])
+def test_fault_injection_fails_whole_stage(monkeypatch, mode):
+    """Barrier semantics (reference core.py:750-753, cuml_context.py:155-159): a failing rank fails
+    the whole stage promptly with its error instead of leaving its peers hanging."""
+    import time
+
+    from spark_rapids_ml_nai_amd.regression import LinearRegression
+
+    X = _data(seed=5)
+    y = X[:, 0].astype(np.float64)
+    df = DataFrame.from_numpy(X, y, num_partitions=2)
+    monkeypatch.setenv("SRML_FAULT_RANK", "1")
+    monkeypatch.setenv("SRML_FAULT_MODE", mode)
+    monkeypatch.setenv("SRML_BARRIER_TIMEOUT", "120")
+    t0 = time.time()
+    with pytest.raises(RuntimeError) as ei:
+        LinearRegression(num_workers=2).fit(df)
+    assert time.time() - t0 < 100
+    msg = str(ei.value)
+    assert ("injected fault on rank 1" in msg) if mode == "raise" else ("exited with code" in msg)
+
+
+def test_hung_rank_hits_stage_timeout(monkeypatch):
+    from spark_rapids_ml_nai_amd.regression import LinearRegression
+
+    X = _data(seed=6)
+    df = DataFrame.from_numpy(X, X[:, 1].astype(np.float64), num_partitions=2)
+    monkeypatch.setenv("SRML_FAULT_RANK", "0")
+    monkeypatch.setenv("SRML_FAULT_MODE", "hang")
+    monkeypatch.setenv("SRML_BARRIER_TIMEOUT", "15")
+    with pytest.raises(RuntimeError, match="timed out"):
+        LinearRegression(num_workers=2).fit(df)
