@@ -19,6 +19,7 @@ Re-design of the reference's framework core (``core.py:426-1647``):
 from __future__ import annotations
 
 import logging
+import os
 import threading
 from abc import abstractmethod
 from dataclasses import dataclass, field
@@ -131,6 +132,9 @@ class FitInput:
     cols: Dict[str, np.ndarray]
     desc: PartitionDescriptor
     host: HostPartition
+    # set for estimators that opt into streaming ingest: X's H2D is still in flight and the
+    # first pass must consume ``stream.chunks()`` (or call ``stream.wait_all()``) before using X
+    stream: Any = None
 
 
 def to_device(X: Any, device: torch.device, dtype: Optional[torch.dtype] = None) -> Any:
@@ -343,10 +347,20 @@ def _fit_worker(ctx: WorkerContext, payload: Tuple[HostPartition, Callable, Dict
     if hp.rows == 0:
         raise RuntimeError("A worker received no data. Please increase amount of data or use fewer workers.")
     dtype = torch.float32 if float32 else torch.float64
-    X = to_device(hp.X, ctx.device, dtype) if hp.X is not None else None
+    streamed = None
+    from ..ops.ingest import StreamedRows, is_pinned
+
+    if (ctx.is_gpu and isinstance(hp.X, np.ndarray) and hp.X.ndim == 2 and hp.X.shape[0] > 0
+            and hp.X.dtype == (np.float32 if float32 else np.float64) and hp.X.flags.c_contiguous
+            and getattr(fit_fn, "streaming_ingest", False) and os.environ.get("SRML_STREAM_INGEST", "1") == "1"
+            and is_pinned(hp.X)):
+        streamed = StreamedRows(hp.X, ctx.device, dtype)
+        X = streamed.X
+    else:
+        X = to_device(hp.X, ctx.device, dtype) if hp.X is not None else None
     y = to_device(hp.y, ctx.device) if hp.y is not None else None
     desc = PartitionDescriptor.build(ctx, hp.rows, hp.n_cols)
-    inp = FitInput(X=X, y=y, cols=hp.cols, desc=desc, host=hp)
+    inp = FitInput(X=X, y=y, cols=hp.cols, desc=desc, host=hp, stream=streamed)
     _maybe_inject_fault(ctx, "fit")
     return fit_fn(inp, ctx, params)
 

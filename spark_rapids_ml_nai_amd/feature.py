@@ -83,8 +83,9 @@ class PCA(PCAClass, _Estimator, _PCAParams):
             from .models.pca import pca_fit
 
             init = params["cuml_init"]
-            return pca_fit(inp.X, inp.desc.m, ctx, init.get("n_components"))
+            return pca_fit(inp.X, inp.desc.m, ctx, init.get("n_components"), stream=inp.stream)
 
+        _fit.streaming_ingest = True  # type: ignore[attr-defined]
         return _fit
 
     def _create_model(self, result: Dict[str, Any]) -> "PCAModel":

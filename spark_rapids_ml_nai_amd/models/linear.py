@@ -12,15 +12,17 @@ moments, lam_eff = regParam / sigma_y, p = 1 with standardization else 1/sigma_j
 
 Device work per rank is two streaming passes over the resident shard — ``col_moments`` (sum,
 sum of squares) and the fused-centring MFMA ``gram`` + ``xtv`` (X^T y) — and ONE coalesced
-RCCL all-reduce of [X'X, X'y] (fp64). The n x n solve runs on the replicated statistics:
-Cholesky for OLS/Ridge, cyclic coordinate descent on the Gram matrix ("covariance updates",
-O(n^2) per epoch, independent of m) for ElasticNet/Lasso. All param maps of a fitMultiple
-share the statistics (one pass over the data for every model).
+RCCL all-reduce of [X'X, X'y] (fp64). The n x n solve runs on the replicated statistics, on
+the device: blocked Cholesky (``srml_potrf_f64``, MFMA trailing updates) for OLS/Ridge, with the
+Jacobi eigensolver's minimum-norm solution for singular systems; cyclic coordinate descent on
+the Gram matrix ("covariance updates", O(n^2) per epoch, independent of m, one kernel launch —
+``srml_cd_gram_f64``) for ElasticNet/Lasso. All param maps of a fitMultiple share the
+statistics (one pass over the data for every model).
 """
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import Any, Dict, List, Optional
+from typing import Any, Dict
 
 import numpy as np
 import torch
@@ -31,123 +33,84 @@ from ..parallel.context import WorkerContext
 
 @dataclass
 class LSQStats:
+    """Replicated second-order statistics (fp64 tensors on the rank's device)."""
+
     m: int
-    xbar: np.ndarray
-    xstd: np.ndarray
+    xbar: torch.Tensor
+    xstd: torch.Tensor
     ybar: float
     ystd: float
-    cov: np.ndarray  # centred scatter / m  (n x n)
-    raw2: np.ndarray  # uncentred second moment / m
-    xy_c: np.ndarray  # centred cross moment / m
-    xy_raw: np.ndarray  # uncentred cross moment / m
+    cov: torch.Tensor  # centred scatter / m  (n x n)
+    xy_c: torch.Tensor  # centred cross moment / m
+    xy_raw: torch.Tensor  # uncentred cross moment / m
     yy_raw: float
 
+    @property
+    def raw2(self) -> torch.Tensor:
+        """uncentred second moment / m"""
+        return self.cov + torch.outer(self.xbar, self.xbar)
 
-def lsq_stats(X: torch.Tensor, y: torch.Tensor, m_total: int, ctx: WorkerContext) -> LSQStats:
-    n = X.shape[1]
-    dev = X.device
-    s, q = ops.col_moments(X)
-    yd = y.double()
-    ys = torch.stack([yd.sum(), (yd * yd).sum()])
-    small = torch.cat([s, q, ys])
-    ctx.comm.allreduce(small)
-    s, q, ys = small[:n], small[n: 2 * n], small[2 * n:]
-    mean = s / m_total
-    G = ops.gram(X, mean)  # centred scatter (fp64)
-    xty = ops.xtv(X, y.view(-1, 1)).view(-1)  # raw X'y (fp64)
-    big = torch.cat([G.view(-1), xty])
-    ctx.comm.allreduce(big)
-    G = big[: n * n].view(n, n)
-    xty = big[n * n:]
-    meanh = mean.cpu().numpy()
+
+def lsq_stats(X: torch.Tensor, y: torch.Tensor, m_total: int, ctx: WorkerContext, stream: Any = None) -> LSQStats:
+    """One pass (overlapped with the H2D when ``stream`` is given) + two all-reduces."""
+    from .stats import scatter_stats
+
+    st = scatter_stats(X, ctx, m_total, stream=stream, y=y, need_sq=True)
     mt = float(m_total)
-    var = np.maximum(q.cpu().numpy() / mt - meanh * meanh, 0.0)
-    ybar = float(ys[0].item()) / mt
-    yvar = max(float(ys[1].item()) / mt - ybar * ybar, 0.0)
-    cov = G.cpu().numpy() / mt
-    xy_raw = xty.cpu().numpy() / mt
-    xy_c = xy_raw - meanh * ybar
-    raw2 = cov + np.outer(meanh, meanh)
-    return LSQStats(m_total, meanh, np.sqrt(var), ybar, float(np.sqrt(yvar)), cov, raw2, xy_c, xy_raw,
-                    float(ys[1].item()) / mt)
+    mean = st.mean
+    cov = st.scatter / mt
+    xy_raw = st.xty / mt
+    var = (st.sumsq / mt - mean * mean).clamp_min(0.0)
+    ybar = st.y_sum / mt
+    yvar = max(st.y_sumsq / mt - ybar * ybar, 0.0)
+    return LSQStats(m_total, mean, torch.sqrt(var), ybar, float(np.sqrt(yvar)), cov, xy_raw - mean * ybar, xy_raw,
+                    st.y_sumsq / mt)
 
 
-def _cholesky_solve(A: np.ndarray, b: np.ndarray) -> np.ndarray:
-    try:
-        L = np.linalg.cholesky(A)
-        z = np.linalg.solve(L, b)
-        return np.linalg.solve(L.T, z)
-    except np.linalg.LinAlgError:
-        # singular normal equations: minimum-norm least-squares solution (eigen-solver fallback)
-        w, V = np.linalg.eigh(A)
-        tol = max(w.max(), 0.0) * A.shape[0] * np.finfo(np.float64).eps
-        inv = np.where(w > tol, 1.0 / np.where(w > tol, w, 1.0), 0.0)
-        return V @ (inv * (V.T @ b))
-
-
-def coordinate_descent(A: np.ndarray, b: np.ndarray, l1: np.ndarray, l2: np.ndarray, max_iter: int, tol: float,
-                       w0: Optional[np.ndarray] = None) -> np.ndarray:
-    """min 1/2 w'Aw - b'w + sum l1_j |w_j| + 1/2 sum l2_j w_j^2  by cyclic CD on the Gram matrix."""
-    n = A.shape[0]
-    w = np.zeros(n) if w0 is None else w0.copy()
-    grad = A @ w  # maintained A w
-    diag = np.diag(A) + l2
-    for _ in range(max(1, max_iter)):
-        max_delta = 0.0
-        max_w = 0.0
-        for j in range(n):
-            if diag[j] <= 0:
-                continue
-            rho = b[j] - grad[j] + A[j, j] * w[j]
-            if rho > l1[j]:
-                nw = (rho - l1[j]) / diag[j]
-            elif rho < -l1[j]:
-                nw = (rho + l1[j]) / diag[j]
-            else:
-                nw = 0.0
-            d = nw - w[j]
-            if d != 0.0:
-                grad += d * A[:, j]
-                w[j] = nw
-                max_delta = max(max_delta, abs(d))
-            max_w = max(max_w, abs(nw))
-        if max_delta <= tol * max(max_w, 1e-300):
-            break
-    return w
+def _min_norm_solve(A: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """Singular normal equations: minimum-norm least-squares solution (eigen-solver fallback)."""
+    w, V = ops.syevj(A) if A.is_cuda and A.shape[0] <= 4096 else torch.linalg.eigh(A)
+    tol = max(float(w.max()), 0.0) * A.shape[0] * float(np.finfo(np.float64).eps)
+    inv = torch.where(w > tol, 1.0 / torch.where(w > tol, w, torch.ones_like(w)), torch.zeros_like(w))
+    return V @ (inv * (V.T @ b))
 
 
 def lsq_solve(st: LSQStats, reg: float, l1_ratio: float, fit_intercept: bool, standardization: bool,
               max_iter: int, tol: float) -> Dict[str, Any]:
     n = st.xbar.shape[0]
+    dev = st.xbar.device
     xstd = st.xstd
     nz = xstd > 0
-    safe = np.where(nz, xstd, 1.0)
+    safe = torch.where(nz, xstd, torch.ones_like(xstd))
     if st.ystd == 0.0 and fit_intercept:
         # constant label: Spark returns zero coefficients and intercept = label mean
         return {"coef_": [0.0] * n, "intercept_": st.ybar}
     ystd = st.ystd if st.ystd > 0 else 1.0
+    denom = torch.outer(safe, safe)
     if fit_intercept:
-        A = st.cov / np.outer(safe, safe)
+        A = st.cov / denom
         b = st.xy_c / (safe * ystd)
     else:
-        A = st.raw2 / np.outer(safe, safe)
+        A = st.raw2 / denom
         b = st.xy_raw / (safe * ystd)
-    A[~nz, :] = 0.0
-    A[:, ~nz] = 0.0
-    b[~nz] = 0.0
+    keep = nz.double()
+    A = A * torch.outer(keep, keep)
+    b = b * keep
     lam = reg / ystd
-    l1 = lam * l1_ratio * (np.ones(n) if standardization else 1.0 / safe)
-    l2 = lam * (1.0 - l1_ratio) * (np.ones(n) if standardization else 1.0 / (safe * safe))
+    ones = torch.ones(n, dtype=torch.float64, device=dev)
+    l1 = lam * l1_ratio * (ones if standardization else 1.0 / safe)
+    l2 = lam * (1.0 - l1_ratio) * (ones if standardization else 1.0 / (safe * safe))
     if reg == 0.0 or l1_ratio == 0.0:
-        Areg = A + np.diag(l2)
-        Areg[~nz, ~nz] = 1.0
-        wt = _cholesky_solve(Areg, b)
+        Areg = A + torch.diag(l2 + (1.0 - keep))  # constant columns: identity rows, zero rhs
+        wt, ok = ops.spd_solve(Areg, b)
+        if not ok:
+            wt = _min_norm_solve(Areg, b)
     else:
-        wt = coordinate_descent(A, b, l1, l2, max_iter, tol)
-    wt[~nz] = 0.0
+        wt, _ = ops.cd_gram(A, b, l1, l2, max_iter, tol)
+    wt = wt * keep
     w = wt * ystd / safe
-    intercept = float(st.ybar - st.xbar @ w) if fit_intercept else 0.0
-    return {"coef_": w.tolist(), "intercept_": intercept}
+    intercept = float(st.ybar - float(st.xbar @ w)) if fit_intercept else 0.0
+    return {"coef_": w.cpu().tolist(), "intercept_": intercept}
 
 
 def linear_predict(X: torch.Tensor, coef: torch.Tensor, intercept: float) -> torch.Tensor:

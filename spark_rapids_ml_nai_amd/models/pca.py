@@ -4,9 +4,9 @@ Reference behaviour: cuML ``PCAMG.fit`` called from ``feature.py:216-257`` — c
 covariance reduced over NCCL, eigendecomposition, sign flip, explained-variance ratio, singular
 values. MI355X pipeline per rank:
 
-1. ``col_moments`` HIP kernel -> column sums (fp64) ; RCCL all-reduce (n values)
-2. ``gram`` MFMA SYRK kernel on the resident fp32 shard with the global mean subtracted in
-   the LDS staging pass -> fp64 scatter matrix ; ONE RCCL all-reduce (n^2 fp64)
+1-2. one pass (``models/stats.py``; chunk by chunk while the shard's H2D is still in flight):
+   ``col_moments`` column sums + the ``gram`` MFMA SYRK about a shift estimated from the first
+   chunk, exactly re-centred in fp64 -> RCCL all-reduce of the sums (n) and of the scatter (n^2)
 3. top-k eigensolver on the replicated covariance (``models/eig.py``), sign-fixed on device
 4. attributes exactly as the reference persists them (mean_, components_ k x n,
    explained_variance_ratio_ = λ/trace, singular_values_ = sqrt((m-1) λ), n_cols, dtype)
@@ -23,16 +23,16 @@ from ..parallel.context import WorkerContext
 from .eig import topk_eigh
 
 
-def pca_fit(X: torch.Tensor, m_total: int, ctx: WorkerContext, n_components: Any, timer: Any = None) -> Dict[str, Any]:
+def pca_fit(X: torch.Tensor, m_total: int, ctx: WorkerContext, n_components: Any, timer: Any = None,
+            stream: Any = None) -> Dict[str, Any]:
+    from .stats import scatter_stats
+
     n = X.shape[1]
     k = n if n_components is None else int(n_components)
     if k > n:
         raise ValueError("k (%d) must be <= number of features (%d)" % (k, n))
-    s, _ = ops.col_moments(X, need_sq=False)
-    ctx.comm.allreduce(s)
-    mean = s / float(m_total)
-    G = ops.gram(X, mean)
-    ctx.comm.allreduce(G)
+    st = scatter_stats(X, ctx, m_total, stream=stream, need_sq=False)
+    mean, G = st.mean, st.scatter
     denom = float(max(m_total - 1, 1))
     cov = G / denom
     total_var = float(torch.trace(cov).item())

@@ -41,32 +41,48 @@ def col_moments(X: torch.Tensor, need_sq: bool = True) -> Tuple[torch.Tensor, Op
     return s, q
 
 
-def gram(X: torch.Tensor, mean: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """out (fp64 n x n) += (X - mean)^T (X - mean); returns out (full symmetric matrix)."""
+def gram(X: torch.Tensor, mean: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+         finalize: bool = True) -> torch.Tensor:
+    """out (fp64 n x n) += (X - mean)^T (X - mean); returns out (full symmetric matrix).
+
+    ``finalize=False`` (streaming, one call per row chunk): only the upper triangle of ``out``
+    is accumulated, in place; call ``gram_mirror(out)`` once after the last chunk."""
     m, n = X.shape
     if out is None:
         out = torch.zeros((n, n), dtype=torch.float64, device=X.device)
-    if not X.is_cuda:
-        Xc = X.double() - (mean.double() if mean is not None else 0.0)
-        out += Xc.T @ Xc
-        return out
-    if X.dtype != torch.float32:
-        # fp64 inputs: f64 path on the f64 MFMA dgemm (A^T A)
+    if not X.is_cuda or X.dtype != torch.float32:
         Xc = X - mean.to(X.dtype) if mean is not None else X
-        Xc = _c(Xc)
-        dgemm(Xc, Xc, ta=True, tb=False, alpha=1.0, beta=1.0, out=out)
+        if X.is_cuda:
+            # fp64 inputs: f64 path on the f64 MFMA dgemm (A^T A)
+            dgemm(_c(Xc), _c(Xc), ta=True, tb=False, alpha=1.0, beta=1.0, out=out)
+        else:
+            Xc = Xc.double()
+            out += Xc.T @ Xc
         return out
     X = _c(X)
     mu = _c(mean.to(torch.float32)) if mean is not None else None
-    tmp = out
-    if mu is not None or True:
-        # kernel accumulates only the upper triangle; mirror afterwards
-        up = torch.zeros_like(out)
+    st = native.stream(X.device)
+    if not finalize:
         native.call("srml_gram_f32", X.data_ptr(), m, n, X.stride(0), mu.data_ptr() if mu is not None else None,
-                    up.data_ptr(), native.stream(X.device))
-        native.call("srml_mirror_upper_f64", up.data_ptr(), n, native.stream(X.device))
-        tmp += up
-    return tmp
+                    out.data_ptr(), st)
+        return out
+    # the kernel accumulates only the upper triangle; mirror into a temporary, then add
+    up = torch.zeros_like(out)
+    native.call("srml_gram_f32", X.data_ptr(), m, n, X.stride(0), mu.data_ptr() if mu is not None else None,
+                up.data_ptr(), st)
+    native.call("srml_mirror_upper_f64", up.data_ptr(), n, st)
+    out += up
+    return out
+
+
+def gram_mirror(G: torch.Tensor) -> torch.Tensor:
+    """Complete a streaming (upper-triangle) Gram accumulation into the full symmetric matrix."""
+    if not G.is_cuda:
+        iu = torch.triu_indices(G.shape[0], G.shape[0], 1)
+        G[iu[1], iu[0]] = G[iu[0], iu[1]]
+        return G
+    native.call("srml_mirror_upper_f64", G.data_ptr(), G.shape[0], native.stream(G.device))
+    return G
 
 
 _XW_WIDTHS = (1, 2, 3, 4, 8, 16, 32)
@@ -695,3 +711,59 @@ def syevj(A: torch.Tensor, max_sweeps: int = 30, tol: float = 1e-15) -> Tuple[to
     if rc < 0:
         raise RuntimeError("srml_syevj_f64 failed with status %d" % rc)
     return W, V
+
+
+# ------------------------------------------------------------------------------------------
+# SPD solve and Gram-matrix coordinate descent (linear models)
+# ------------------------------------------------------------------------------------------
+def spd_solve(A: torch.Tensor, b: torch.Tensor) -> Tuple[torch.Tensor, bool]:
+    """x = A^-1 b for symmetric positive definite A (fp64) by Cholesky; returns (x, ok).
+    ok=False when a non-positive pivot shows A is (numerically) singular."""
+    n = A.shape[0]
+    if not A.is_cuda:
+        L, info = torch.linalg.cholesky_ex(A.double())
+        if int(info) != 0:
+            return torch.zeros(n, dtype=torch.float64), False
+        return torch.cholesky_solve(b.double().view(-1, 1), L).view(-1), True
+    L = A.double().contiguous().clone()
+    info = torch.zeros(1, dtype=torch.int32, device=A.device)
+    st = native.stream(A.device)
+    native.call("srml_potrf_f64", L.data_ptr(), n, L.stride(0), info.data_ptr(), st)
+    x = b.double().contiguous().clone()
+    native.call("srml_potrs_f64", L.data_ptr(), n, L.stride(0), x.data_ptr(), st)
+    return x, int(info.item()) == 0
+
+
+def cd_gram(A: torch.Tensor, b: torch.Tensor, l1: torch.Tensor, l2: torch.Tensor, max_iter: int, tol: float,
+            w0: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, int]:
+    """Cyclic coordinate descent: argmin 1/2 w'Aw - b'w + sum l1|w| + 1/2 sum l2 w^2 (fp64)."""
+    n = A.shape[0]
+    w = (torch.zeros(n, dtype=torch.float64, device=A.device) if w0 is None else w0.double().clone()).contiguous()
+    if not A.is_cuda or 2 * n * 8 > 150 * 1024:
+        Ah, bh, l1h, l2h = (t.double().cpu().numpy() for t in (A, b, l1, l2))
+        wh = w.cpu().numpy()
+        g = Ah @ wh
+        diag = np.diag(Ah) + l2h
+        it = 0
+        for it in range(1, max(1, max_iter) + 1):
+            max_delta = max_w = 0.0
+            for j in range(n):
+                if diag[j] <= 0:
+                    continue
+                rho = bh[j] - g[j] + Ah[j, j] * wh[j]
+                nw = (rho - l1h[j]) / diag[j] if rho > l1h[j] else ((rho + l1h[j]) / diag[j] if rho < -l1h[j] else 0.0)
+                d = nw - wh[j]
+                if d != 0.0:
+                    g += d * Ah[:, j]
+                    wh[j] = nw
+                    max_delta = max(max_delta, abs(d))
+                max_w = max(max_w, abs(nw))
+            if max_delta <= tol * max(max_w, 1e-300):
+                break
+        return torch.from_numpy(wh).to(A.device), it
+    A = A.double().contiguous()
+    iters = torch.zeros(1, dtype=torch.int32, device=A.device)
+    native.call("srml_cd_gram_f64", A.data_ptr(), n, A.stride(0), _c(b.double()).data_ptr(), _c(l1.double()).data_ptr(),
+                _c(l2.double()).data_ptr(), w.data_ptr(), int(max_iter), float(tol), iters.data_ptr(),
+                native.stream(A.device))
+    return w, int(iters.item())

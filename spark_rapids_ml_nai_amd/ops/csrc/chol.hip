@@ -1,0 +1,217 @@
+// Dense SPD solves and Gram-matrix coordinate descent for the linear models, on device.
+//
+//  * srml_potrf_f64: blocked right-looking Cholesky (lower, row-major), 64-wide panels:
+//      diag block factored in LDS by one workgroup -> panel TRSM (thread per row, L11 in LDS)
+//      -> trailing update A22 -= A21 A21^T on the f64 MFMA GEMM (srml_dgemm).
+//    A non-positive pivot sets *info = column + 1 (the caller falls back to an eigen solve).
+//  * srml_potrs_f64: L L^T x = b for one right-hand side (two single-workgroup sweeps with
+//    block-wide dot products; O(n^2), latency-bound but ~ms at n = 3000).
+//  * srml_cd_gram_f64: cyclic coordinate descent for 1/2 w'Aw - b'w + sum l1|w| + 1/2 sum l2 w^2
+//    (Spark/cuML elastic-net objective on the standardised Gram matrix, "covariance updates"):
+//    one 1024-thread workgroup keeps w and A·w in LDS, each coordinate update streams one row
+//    of A (L2-resident) — the whole solve is one kernel launch instead of a host loop.
+// Reference: cuML LinearRegressionMG / RidgeMG / CDMG solves (regression.py:498-613).
+#include "common.h"
+
+extern "C" int srml_dgemm(int ta, int tb, int M, int N, int K, double alpha, const double* A, long lda,
+                          const double* B, long ldb, double beta, double* C, long ldc, hipStream_t stream);
+
+namespace {
+constexpr int NB = 64;
+
+__global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A, long lda, int k0, int nb,
+                                                         int* __restrict__ info) {
+  __shared__ double S[NB][NB + 1];
+  const int t = threadIdx.x;
+  for (int idx = t; idx < nb * nb; idx += 256) {
+    const int i = idx / nb, j = idx % nb;
+    S[i][j] = A[(long)(k0 + i) * lda + k0 + j];
+  }
+  __syncthreads();
+  for (int j = 0; j < nb; ++j) {
+    if (t == 0) {
+      const double d = S[j][j];
+      if (!(d > 0.0)) {
+        if (*info == 0) *info = k0 + j + 1;
+        S[j][j] = 1.0;
+      } else {
+        S[j][j] = sqrt(d);
+      }
+    }
+    __syncthreads();
+    const double djj = S[j][j];
+    for (int i = j + 1 + t; i < nb; i += 256) S[i][j] /= djj;
+    __syncthreads();
+    const int r = nb - j - 1;
+    for (int idx = t; idx < r * r; idx += 256) {
+      const int i = j + 1 + idx / r, l = j + 1 + idx % r;
+      if (l <= i) S[i][l] -= S[i][j] * S[l][j];
+    }
+    __syncthreads();
+  }
+  for (int idx = t; idx < nb * nb; idx += 256) {
+    const int i = idx / nb, j = idx % nb;
+    A[(long)(k0 + i) * lda + k0 + j] = j <= i ? S[i][j] : 0.0;
+  }
+}
+
+// rows r >= k1: x (1 x NB) solves x L11^T = A[r, k0:k0+NB] (only full panels reach the TRSM: the
+// last, possibly narrower, diagonal block has no rows below it)
+__global__ __launch_bounds__(256) void potrf_trsm_kernel(double* __restrict__ A, long lda, int k0, int k1, int n) {
+  __shared__ double L[NB][NB + 1];
+  const int t = threadIdx.x;
+  for (int idx = t; idx < NB * NB; idx += 256) {
+    const int i = idx / NB, j = idx % NB;
+    L[i][j] = A[(long)(k0 + i) * lda + k0 + j];
+  }
+  __syncthreads();
+  const int r = k1 + blockIdx.x * 256 + t;
+  if (r >= n) return;
+  double x[NB];
+  double* row = A + (long)r * lda + k0;
+#pragma unroll
+  for (int j = 0; j < NB; ++j) x[j] = row[j];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    double s = x[j];
+#pragma unroll
+    for (int l = 0; l < j; ++l) s -= x[l] * L[j][l];
+    x[j] = s / L[j][j];
+  }
+#pragma unroll
+  for (int j = 0; j < NB; ++j) row[j] = x[j];
+}
+
+__device__ __forceinline__ double block_sum(double v, double* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int w = 0; w < nw; ++w) s += red[w];
+  return s;
+}
+
+__global__ __launch_bounds__(1024) void potrs_kernel(const double* __restrict__ L, int n, long lda,
+                                                     double* __restrict__ b) {
+  extern __shared__ double x[];  // the right-hand side lives in LDS: no cross-wave global RAW
+  __shared__ double red[16];
+  for (int i = threadIdx.x; i < n; i += blockDim.x) x[i] = b[i];
+  __syncthreads();
+  // forward: L z = b
+  for (int i = 0; i < n; ++i) {
+    double s = 0.0;
+    for (int j = threadIdx.x; j < i; j += blockDim.x) s += L[(long)i * lda + j] * x[j];
+    s = block_sum(s, red);
+    if (threadIdx.x == 0) x[i] = (x[i] - s) / L[(long)i * lda + i];
+    __syncthreads();
+  }
+  // backward: L^T x = z
+  for (int i = n - 1; i >= 0; --i) {
+    double s = 0.0;
+    for (int j = i + 1 + threadIdx.x; j < n; j += blockDim.x) s += L[(long)j * lda + i] * x[j];
+    s = block_sum(s, red);
+    if (threadIdx.x == 0) x[i] = (x[i] - s) / L[(long)i * lda + i];
+    __syncthreads();
+  }
+  for (int i = threadIdx.x; i < n; i += blockDim.x) b[i] = x[i];
+}
+
+// A: n x n (row-major, symmetric), b, l1, l2: n. w: in/out (initial guess). Result iterations in *iters.
+__global__ __launch_bounds__(1024) void cd_gram_kernel(const double* __restrict__ A, int n, long lda,
+                                                       const double* __restrict__ b, const double* __restrict__ l1,
+                                                       const double* __restrict__ l2, double* __restrict__ w_out,
+                                                       int max_iter, double tol, int* __restrict__ iters) {
+  extern __shared__ double sm[];  // w[n], g[n] (= A w)
+  double* w = sm;
+  double* g = sm + n;
+  __shared__ double bc[4];
+  const int t = threadIdx.x;
+  for (int i = t; i < n; i += blockDim.x) w[i] = w_out[i];
+  __syncthreads();
+  // g = A w
+  for (int i = t; i < n; i += blockDim.x) {
+    double s = 0.0;
+    for (int j = 0; j < n; ++j) s += A[(long)i * lda + j] * w[j];
+    g[i] = s;
+  }
+  __syncthreads();
+  int it = 0;
+  for (; it < max_iter; ++it) {
+    double max_delta = 0.0, max_w = 0.0;  // meaningful on thread 0
+    for (int j = 0; j < n; ++j) {
+      if (t == 0) {
+        const double ajj = A[(long)j * lda + j];
+        const double diag = ajj + l2[j];
+        double d = 0.0;
+        if (diag > 0.0) {
+          const double rho = b[j] - g[j] + ajj * w[j];
+          double nw = 0.0;
+          if (rho > l1[j]) nw = (rho - l1[j]) / diag;
+          else if (rho < -l1[j]) nw = (rho + l1[j]) / diag;
+          d = nw - w[j];
+          w[j] = nw;
+          max_w = fmax(max_w, fabs(nw));
+          max_delta = fmax(max_delta, fabs(d));
+        }
+        bc[0] = d;
+      }
+      __syncthreads();
+      const double d = bc[0];
+      if (d != 0.0) {
+        const double* row = A + (long)j * lda;  // symmetric: column j == row j
+        for (int i = t; i < n; i += blockDim.x) g[i] += d * row[i];
+      }
+      __syncthreads();
+    }
+    if (t == 0) bc[1] = (max_delta <= tol * fmax(max_w, 1e-300)) ? 1.0 : 0.0;
+    __syncthreads();
+    if (bc[1] != 0.0) {
+      ++it;
+      break;
+    }
+  }
+  for (int i = t; i < n; i += blockDim.x) w_out[i] = w[i];
+  if (t == 0) *iters = it;
+}
+}  // namespace
+
+SRML_API int srml_potrf_f64(double* A, int n, long lda, int* info, hipStream_t stream) {
+  if (n <= 0) return 0;
+  hipError_t err = hipSuccess;
+  SRML_TRY(err, hipMemsetAsync(info, 0, sizeof(int), stream));
+  for (int k0 = 0; k0 < n; k0 += NB) {
+    const int nb = n - k0 < NB ? n - k0 : NB;
+    const int k1 = k0 + nb;
+    hipLaunchKernelGGL(potrf_diag_kernel, dim3(1), dim3(256), 0, stream, A, lda, k0, nb, info);
+    if (k1 < n) {
+      const int m2 = n - k1;
+      hipLaunchKernelGGL(potrf_trsm_kernel, dim3((m2 + 255) / 256), dim3(256), 0, stream, A, lda, k0, k1, n);
+      const int rc = srml_dgemm(0, 1, m2, m2, nb, -1.0, A + (long)k1 * lda + k0, lda, A + (long)k1 * lda + k0, lda,
+                                1.0, A + (long)k1 * lda + k1, lda, stream);
+      if (rc) return rc;
+    }
+  }
+  const int st = srml_status();
+  return err != hipSuccess ? (int)err : st;
+}
+
+SRML_API int srml_potrs_f64(const double* L, int n, long lda, double* b, hipStream_t stream) {
+  if (n <= 0) return 0;
+  const size_t lds = (size_t)n * sizeof(double);
+  if (lds > 150 * 1024) return -9;
+  (void)hipFuncSetAttribute((const void*)potrs_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(potrs_kernel, dim3(1), dim3(1024), lds, stream, L, n, lda, b);
+  return srml_status();
+}
+
+SRML_API int srml_cd_gram_f64(const double* A, int n, long lda, const double* b, const double* l1, const double* l2,
+                              double* w, int max_iter, double tol, int* iters, hipStream_t stream) {
+  if (n <= 0) return 0;
+  const size_t lds = (size_t)2 * n * sizeof(double);
+  if (lds > 150 * 1024) return -9;  // n <= 9600
+  (void)hipFuncSetAttribute((const void*)cd_gram_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(cd_gram_kernel, dim3(1), dim3(1024), lds, stream, A, n, lda, b, l1, l2, w, max_iter, tol, iters);
+  return srml_status();
+}

@@ -160,7 +160,7 @@ class LinearRegression(LinearRegressionClass, _EstimatorSupervised, _LinearRegre
                 p = dict(init, **mp)
                 if n == 1 and (p["alpha"] == 0 or p["l1_ratio"] == 0):
                     raise RuntimeError("LinearRegression doesn't support training data with 1 column")
-            st = lsq_stats(inp.X, inp.y, inp.desc.m, ctx)
+            st = lsq_stats(inp.X, inp.y, inp.desc.m, ctx, stream=inp.stream)
             out = []
             for mp in maps:
                 p = dict(init, **mp)
@@ -170,6 +170,7 @@ class LinearRegression(LinearRegressionClass, _EstimatorSupervised, _LinearRegre
                 out.append(res)
             return out if params["fit_multiple_params"] else out[0]
 
+        _fit.streaming_ingest = True  # type: ignore[attr-defined]
         return _fit
 
     def _create_model(self, result: Dict[str, Any]) -> "LinearRegressionModel":

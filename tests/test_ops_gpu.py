@@ -346,3 +346,67 @@ def test_umap_epoch_negative_samples(gpu_device):
                    a=1.577, b=0.895, gamma=1.0, alpha=1.0, epoch=1, move_other=True, seed=1)
     assert torch.isfinite(emb).all()
     assert emb.std(0).sum().item() > before
+
+
+@pytest.mark.parametrize("n", [1, 5, 64, 65, 200, 1000])
+def test_spd_solve(gpu_device, n):
+    g = torch.Generator().manual_seed(n)
+    M = torch.randn(n, n + 3, generator=g, dtype=torch.float64)
+    A = M @ M.T / n + 0.1 * torch.eye(n, dtype=torch.float64)
+    b = torch.randn(n, generator=g, dtype=torch.float64)
+    x, ok = ops.spd_solve(A.to(gpu_device), b.to(gpu_device))
+    assert ok
+    ref = torch.linalg.solve(A, b)
+    torch.testing.assert_close(x.cpu(), ref, rtol=1e-9, atol=1e-9)
+
+
+def test_spd_solve_detects_singular(gpu_device):
+    n = 100
+    g = torch.Generator().manual_seed(0)
+    M = torch.randn(n, 10, generator=g, dtype=torch.float64)
+    _, ok = ops.spd_solve((M @ M.T).to(gpu_device), torch.ones(n, dtype=torch.float64, device=gpu_device))
+    assert not ok
+
+
+@pytest.mark.parametrize("n", [3, 50, 700])
+def test_cd_gram(gpu_device, n):
+    g = torch.Generator().manual_seed(n)
+    M = torch.randn(4 * n, n, generator=g, dtype=torch.float64)
+    A = M.T @ M / (4 * n)
+    b = torch.randn(n, generator=g, dtype=torch.float64) * 0.3
+    l1 = torch.full((n,), 0.05, dtype=torch.float64)
+    l2 = torch.full((n,), 0.02, dtype=torch.float64)
+    w_ref, it_ref = ops.cd_gram(A, b, l1, l2, 200, 1e-10)
+    w, it = ops.cd_gram(A.to(gpu_device), b.to(gpu_device), l1.to(gpu_device), l2.to(gpu_device), 200, 1e-10)
+    assert it == it_ref
+    torch.testing.assert_close(w.cpu(), w_ref, rtol=1e-9, atol=1e-12)
+    if n >= 50:
+        assert (w_ref == 0).any()  # the L1 term produced exact zeros
+
+
+def test_streamed_ingest_scatter_stats(gpu_device):
+    from spark_rapids_ml_nai_amd.models.stats import scatter_stats
+    from spark_rapids_ml_nai_amd.ops.ingest import StreamedRows, is_pinned
+    from spark_rapids_ml_nai_amd.parallel.context import WorkerContext
+
+    m, n = 50000, 96
+    h = torch.empty((m, n), dtype=torch.float32, pin_memory=True)
+    g = torch.Generator().manual_seed(0)
+    h.copy_(torch.randn(m, n, generator=g) * 3 + 7)
+    Xh = h.numpy()
+    assert is_pinned(Xh)
+    y = torch.randn(m, generator=g, dtype=torch.float64)
+    ctx = WorkerContext.single(gpu_device)
+    st_ref = scatter_stats(torch.from_numpy(Xh).to(gpu_device), ctx, m, y=y.to(gpu_device))
+    sr = StreamedRows(Xh, gpu_device, torch.float32, chunk_bytes=1 << 20)
+    assert len(sr.bounds) > 10
+    st = scatter_stats(sr.X, ctx, m, stream=sr, y=y.to(gpu_device))
+    Xd = torch.from_numpy(Xh).double()
+    Xc = Xd - Xd.mean(0)
+    ref = Xc.T @ Xc
+    scale = ref.abs().max().item()
+    for s in (st, st_ref):
+        assert (s.scatter.cpu() - ref).abs().max().item() / scale < 1e-6
+        torch.testing.assert_close(s.mean.cpu(), Xd.mean(0), rtol=1e-9, atol=1e-9)
+        torch.testing.assert_close(s.xty.cpu(), Xd.T @ y, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(sr.wait_all().cpu(), h)
