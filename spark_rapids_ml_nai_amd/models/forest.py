@@ -215,14 +215,18 @@ def grow_tree(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: Wor
         # work items (node slot, row begin, row end, feature chunk), built vectorised
         cand_a = np.asarray(cand, dtype=np.int64)
         c_start, c_cnt = starts[cand_a], counts[cand_a]
-        nch = (c_cnt + ROWS_PER_ITEM - 1) // ROWS_PER_ITEM
+        # rows per work item: enough blocks to fill the chip (~8K) but as few per (node, feature
+        # chunk) as possible — every block flushes its LDS histogram with global fp64 atomics
+        rpi = int(min(65536, max(ROWS_PER_ITEM, (int(c_cnt.sum()) * nfc) // 8192)))
+        rpi = (rpi + 511) // 512 * 512
+        nch = (c_cnt + rpi - 1) // rpi
         tot_ch = int(nch.sum())
         if tot_ch:
             node_rep = np.repeat(np.arange(C), nch)
             first = np.repeat(np.cumsum(nch) - nch, nch)
             chunk = np.arange(tot_ch) - first
-            rb = c_start[node_rep] + chunk * ROWS_PER_ITEM
-            re = np.minimum(rb + ROWS_PER_ITEM, c_start[node_rep] + c_cnt[node_rep])
+            rb = c_start[node_rep] + chunk * rpi
+            re = np.minimum(rb + rpi, c_start[node_rep] + c_cnt[node_rep])
             it = np.empty((tot_ch * nfc, 4), dtype=np.int32)
             it[:, 0] = np.repeat(node_rep, nfc)
             it[:, 1] = np.repeat(rb, nfc)
@@ -231,10 +235,11 @@ def grow_tree(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: Wor
             items_t = torch.from_numpy(it).to(dev)
         else:
             items_t = torch.zeros((0, 4), dtype=torch.int32, device=dev)
-        hist = ops.rf_hist(bins, idx, yv, w, items_t, feats, C, B, S, regression)
+        SH = 2 if regression else S  # regression histograms carry (count, sum) only
+        hist = ops.rf_hist(bins, idx, yv, w, items_t, feats, C, B, SH, regression)
         if data_parallel:
             ctx.comm.allreduce(hist)
-        out, _ = ops.rf_best_split(hist, B, S, regression, crit, min_leaf, min_gain)
+        out, _ = ops.rf_best_split(hist, B, SH, regression, crit, min_leaf, min_gain)
         out_h = out.cpu().numpy()
         feats_h = feats.cpu().numpy()
         # honour max_leaves: keep the best-gain splits that fit
@@ -276,19 +281,35 @@ def grow_tree(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: Wor
             n_leaves += 1
         if k == 0:
             break
-        # children totals = prefix of the winning feature's histogram up to the split bin
-        ci_t = torch.tensor(split_ci, device=dev)
-        sel = hist[ci_t, torch.tensor(split_slot, device=dev)].double()  # (k, B, S)
-        left = sel.cumsum(1)[torch.arange(k, device=dev), torch.tensor(split_bin, device=dev)]
-        right = tot[torch.tensor(split_j, device=dev)] - left
-        tot = torch.stack([left, right], 1).reshape(2 * k, S)
+        if not regression:
+            # children totals = prefix of the winning feature's histogram up to the split bin
+            ci_t = torch.tensor(split_ci, device=dev)
+            sel = hist[ci_t, torch.tensor(split_slot, device=dev)].double()  # (k, B, S)
+            left = sel.cumsum(1)[torch.arange(k, device=dev), torch.tensor(split_bin, device=dev)]
+            right = tot[torch.tensor(split_j, device=dev)] - left
+            tot = torch.stack([left, right], 1).reshape(2 * k, S)
         keys = ops.rf_route(bins, idx[:total].contiguous(), seg_node.contiguous(),
                             torch.from_numpy(node_feature).to(dev), torch.from_numpy(node_bin).to(dev),
                             torch.from_numpy(child_base).to(dev))
         keys_sorted, perm = torch.sort(keys, stable=True)
         kept = int((keys_sorted != INT_MAX).sum().item())
         idx = idx[:total][perm[:kept]].contiguous()
-        cnt = torch.bincount(keys_sorted[:kept].long(), minlength=2 * k).cpu().numpy().astype(np.int64)
+        # child segment boundaries in the sorted key order (no atomics: keys are sorted)
+        bounds = torch.searchsorted(keys_sorted[:kept].contiguous(),
+                                    torch.arange(2 * k + 1, device=dev, dtype=keys_sorted.dtype))
+        if regression:
+            # children (count, sum, sumsq) as segment sums over the routed rows (histograms hold no
+            # sum of squares): one cumsum + boundary gathers
+            rows = idx.long()
+            wr = w[rows].double()
+            yr = yv[rows].double()
+            # (3, N) row-contiguous scans: torch's outer-dim scan of an (N, 3) tensor is ~100x slower
+            v = torch.stack([wr, wr * yr, wr * yr * yr], 0)
+            cs = torch.cat([torch.zeros((3, 1), dtype=torch.float64, device=dev), v.cumsum(1)], 1)
+            tot = (cs[:, bounds[1:]] - cs[:, bounds[:-1]]).T.contiguous()
+            if data_parallel:
+                ctx.comm.allreduce(tot)
+        cnt = (bounds[1:] - bounds[:-1]).cpu().numpy().astype(np.int64)
         counts = cnt
         starts = np.concatenate([[0], np.cumsum(cnt)[:-1]]).astype(np.int64)
         level_nodes = next_nodes

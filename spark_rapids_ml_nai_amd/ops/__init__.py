@@ -309,16 +309,26 @@ def rf_hist(bins: torch.Tensor, idx: torch.Tensor, label: torch.Tensor, wcnt: Op
                 if regression:
                     hist[node, j, :, 0].index_add_(0, b, w)
                     hist[node, j, :, 1].index_add_(0, b, w * y.double())
-                    hist[node, j, :, 2].index_add_(0, b, w * y.double() ** 2)
+                    if S > 2:
+                        hist[node, j, :, 2].index_add_(0, b, w * y.double() ** 2)
                 else:
                     flat = b * S + y.long()
                     hist[node, j].view(-1).index_add_(0, flat, w.to(torch.int32))
         return hist
-    lab = _c(label.to(torch.float32))
+    # compact (weight, label) into idx order once: contiguous loads in the row stream
+    rows = idx.long()
+    wv = wcnt[rows].float() if wcnt is not None else torch.ones(rows.shape[0], dtype=torch.float32, device=dev)
+    wy = torch.stack([wv, label[rows].float()], 1).contiguous()
+    yscale = 1.0
+    if regression:
+        if S != 2:
+            raise ValueError("device regression histograms carry (count, sum): S must be 2")
+        # i64 fixed point for w*y: |block sum| <= 65536 rows * 255 * max|y| < 2^24 max|y|
+        ymax = float(wy[:, 1].abs().max().item()) if wy.shape[0] else 0.0
+        yscale = float(2.0 ** 38 / ymax) if ymax > 0 else 1.0
     st = native.stream(dev)
-    native.call("srml_rf_hist", bins.data_ptr(), m, idx.data_ptr(), lab.data_ptr(),
-                wcnt.data_ptr() if wcnt is not None else None, _c(items).data_ptr(), int(items.shape[0]),
-                _c(node_feats).data_ptr(), nf, B, S, int(regression),
+    native.call("srml_rf_hist", bins.data_ptr(), m, idx.data_ptr(), wy.data_ptr(), _c(items).data_ptr(),
+                int(items.shape[0]), _c(node_feats).data_ptr(), nf, B, S, int(regression), yscale,
                 hist.data_ptr() if not regression else None, hist.data_ptr() if regression else None, st)
     return hist
 
@@ -356,13 +366,22 @@ def _rf_best_split_ref(hist: torch.Tensor, S: int, regression: bool, crit: int, 
     nodes, nf, B, _ = hist.shape
     tot = hist[:, 0].sum(1)  # (nodes, S)
     ntot = tot[:, 0] if regression else tot.sum(-1)
-    pimp = _impurity_ref(tot, crit)
+    pimp = _impurity_ref(tot, crit) if (not regression or S > 2) else torch.zeros_like(ntot)
     left = hist.cumsum(2)[:, :, : B - 1]  # (nodes, nf, B-1, S)
     right = tot[:, None, None, :] - left
     nl = left[..., 0] if regression else left.sum(-1)
     nr = ntot[:, None, None] - nl
-    gain = pimp[:, None, None] - nl / ntot[:, None, None].clamp_min(1e-300) * _impurity_ref(left, crit) \
-        - nr / ntot[:, None, None].clamp_min(1e-300) * _impurity_ref(right, crit)
+    if regression:
+        # variance reduction from (count, sum) only: (sL^2/nL + sR^2/nR - s^2/n) / n
+        nt = ntot[:, None, None].clamp_min(1e-300)
+        sl, sr = left[..., 1], right[..., 1]
+        gain = (sl * sl / nl.clamp_min(1e-300) + sr * sr / nr.clamp_min(1e-300)
+                - (tot[:, 1] ** 2)[:, None, None] / nt) / nt
+        if S < 3:
+            pimp = torch.zeros_like(ntot)
+    else:
+        gain = pimp[:, None, None] - nl / ntot[:, None, None].clamp_min(1e-300) * _impurity_ref(left, crit) \
+            - nr / ntot[:, None, None].clamp_min(1e-300) * _impurity_ref(right, crit)
     valid = (nl >= min_leaf) & (nr >= min_leaf) & (nl > 0) & (nr > 0)
     gain = torch.where(valid, gain, torch.full_like(gain, -1.0))
     out = torch.empty((nodes, 6), dtype=torch.float64)

@@ -85,81 +85,113 @@ SRML_API int srml_rf_quantize_u8(const float* X, long m, int n, long ld, const f
 
 // ------------------------------------------------------------------------------------------
 // histogram build. items: int4 {node_slot, row_begin, row_end, feature_chunk}
-// node_feats: [nodes][nf] global feature ids. hist layout: [node][nf][B][S] with S = C (class
-// counts, uint32) or 3 (regression stats, fp32 folded into fp64 output as double[3])
+// node_feats: [nodes][nf] global feature ids. wy: (weight, label) per position of idx (compacted
+// once per level, so the row stream is two contiguous loads + 8 byte-gathers per row). hist
+// layout: [node][nf][B][S] with S = C (class counts, uint32) or 2 (regression weighted count and
+// sum, fp32 in LDS folded into the fp64 output). Two rows per thread per step: all 16 bin gathers are
+// issued before the first LDS atomic (ILP instead of a load->atomic chain per row).
 // ------------------------------------------------------------------------------------------
 template <bool REG>
 __global__ __launch_bounds__(256) void rf_hist_kernel(const unsigned char* __restrict__ bins, long m,
-                                                      const int* __restrict__ idx, const float* __restrict__ label,
-                                                      const unsigned char* __restrict__ wcnt,
+                                                      const int* __restrict__ idx, const float2* __restrict__ wy,
                                                       const int4* __restrict__ items, const int* __restrict__ node_feats,
-                                                      int nf, int B, int S, unsigned* __restrict__ hist_u,
+                                                      int nf, int B, int S, double yscale, unsigned* __restrict__ hist_u,
                                                       double* __restrict__ hist_d) {
-  extern __shared__ __attribute__((aligned(16))) unsigned lh_u[];  // FB*B*S cells (uint32 or float)
-  float* lh_f = reinterpret_cast<float*>(lh_u);
+  // LDS (classification): u32 counts [feature][class][bin].
+  // LDS (regression): u32 weighted counts [feature][bin] then i64 fixed-point sums of w*y
+  //   [feature][bin]. Integer LDS atomics: ds_add_f32 issues ~50x slower than ds_add_u32 on
+  //   gfx950 (SQ_WAIT_INST_LDS), and the 2^-38·max|y| fixed-point step is finer than fp32.
+  extern __shared__ __attribute__((aligned(16))) unsigned lh_u[];
+  unsigned long long* lh_s = reinterpret_cast<unsigned long long*>(lh_u + FB * B);
   const int4 it = items[blockIdx.x];
   const int node = it.x, rb = it.y, re = it.z, fc = it.w;
   const int f_begin = fc * FB;
   const int nfb = min(FB, nf - f_begin);
-  const int cells = FB * B * S;
-  for (int i = threadIdx.x; i < cells; i += 256) lh_u[i] = 0u;
-  int feats[FB];
+  const int words = REG ? FB * B * 3 : FB * B * S;
+  for (int i = threadIdx.x; i < words; i += 256) lh_u[i] = 0u;
+  const unsigned char* col[FB];
 #pragma unroll
-  for (int j = 0; j < FB; ++j) feats[j] = (j < nfb) ? node_feats[(long)node * nf + f_begin + j] : 0;
+  for (int j = 0; j < FB; ++j) col[j] = bins + (long)((j < nfb) ? node_feats[(long)node * nf + f_begin + j] : 0) * m;
   __syncthreads();
-  for (int i = rb + threadIdx.x; i < re; i += 256) {
-    const int r = idx[i];
-    const unsigned w = wcnt ? wcnt[r] : 1u;
-    if (w == 0u) continue;
-    const float y = label[r];
+  for (int i = rb + threadIdx.x; i < re; i += 512) {
+    const int i2 = i + 256;
+    const bool has2 = i2 < re;
+    const int r1 = idx[i];
+    const int r2 = has2 ? idx[i2] : r1;
+    const float2 a1 = wy[i];
+    const float2 a2 = has2 ? wy[i2] : make_float2(0.f, 0.f);
+    int b1[FB], b2[FB];
+#pragma unroll
+    for (int j = 0; j < FB; ++j) {
+      b1[j] = col[j][r1];
+      b2[j] = col[j][r2];
+    }
+    const unsigned w1 = (unsigned)a1.x, w2 = (unsigned)a2.x;
+    unsigned long long s1 = 0ull, s2 = 0ull;
+    if (REG) {
+      s1 = (unsigned long long)(long long)rint((double)a1.x * (double)a1.y * yscale);
+      s2 = (unsigned long long)(long long)rint((double)a2.x * (double)a2.y * yscale);
+    }
 #pragma unroll
     for (int j = 0; j < FB; ++j) {
       if (j < nfb) {
-        const int b = bins[(long)feats[j] * m + r];
-        const int base = (j * B + b) * S;
         if (REG) {
-          atomicAdd(&lh_f[base + 0], (float)w);
-          atomicAdd(&lh_f[base + 1], (float)w * y);
-          atomicAdd(&lh_f[base + 2], (float)w * y * y);
+          atomicAdd(&lh_u[j * B + b1[j]], w1);
+          atomicAdd(&lh_s[j * B + b1[j]], s1);
+          if (w2) {
+            atomicAdd(&lh_u[j * B + b2[j]], w2);
+            atomicAdd(&lh_s[j * B + b2[j]], s2);
+          }
         } else {
-          atomicAdd(&lh_u[base + (int)y], w);
+          atomicAdd(&lh_u[(j * S + (int)a1.y) * B + b1[j]], w1);
+          if (w2) atomicAdd(&lh_u[(j * S + (int)a2.y) * B + b2[j]], w2);
         }
       }
     }
   }
   __syncthreads();
+  // fold into the global [node][feature][bin][stat] layout
   const long out_base = ((long)node * nf + f_begin) * B * S;
   const int valid_cells = nfb * B * S;
+  const double inv = 1.0 / yscale;
   for (int i = threadIdx.x; i < valid_cells; i += 256) {
+    const int j = i / (B * S), rem = i % (B * S), b = rem / S, st = rem % S;
     if (REG) {
-      const float v = lh_f[i];
-      if (v != 0.f) atomicAdd(&hist_d[out_base + i], (double)v);
+      double v;
+      if (st == 0) v = (double)lh_u[j * B + b];
+      else v = (double)(long long)lh_s[j * B + b] * inv;
+      if (v != 0.0) atomicAdd(&hist_d[out_base + i], v);
     } else {
-      const unsigned v = lh_u[i];
+      const unsigned v = lh_u[(j * S + st) * B + b];
       if (v) atomicAdd(&hist_u[out_base + i], v);
     }
   }
 }
 
-SRML_API int srml_rf_hist(const unsigned char* bins, long m, const int* idx, const float* label,
-                          const unsigned char* wcnt, const int* items, int n_items, const int* node_feats, int nf,
-                          int B, int S, int regression, unsigned* hist_u, double* hist_d, hipStream_t stream) {
+// wy: (weight, label) float pairs aligned with idx
+// regression: S must be 2 (weighted count, weighted sum); yscale = fixed-point scale for w*y
+SRML_API int srml_rf_hist(const unsigned char* bins, long m, const int* idx, const float* wy, const int* items,
+                          int n_items, const int* node_feats, int nf, int B, int S, int regression, double yscale,
+                          unsigned* hist_u, double* hist_d, hipStream_t stream) {
   if (n_items <= 0) return 0;
-  const size_t lds = (size_t)FB * B * S * sizeof(unsigned);
+  if (regression && S != 2) return -6;
+  const size_t lds = (size_t)FB * B * (regression ? 3 : S) * sizeof(unsigned);
   if (lds > 64 * 1024) return -5;
+  const float2* w2 = reinterpret_cast<const float2*>(wy);
   if (regression)
-    hipLaunchKernelGGL(rf_hist_kernel<true>, dim3(n_items), dim3(256), lds, stream, bins, m, idx, label, wcnt,
-                       reinterpret_cast<const int4*>(items), node_feats, nf, B, S, hist_u, hist_d);
+    hipLaunchKernelGGL(rf_hist_kernel<true>, dim3(n_items), dim3(256), lds, stream, bins, m, idx, w2,
+                       reinterpret_cast<const int4*>(items), node_feats, nf, B, S, yscale, hist_u, hist_d);
   else
-    hipLaunchKernelGGL(rf_hist_kernel<false>, dim3(n_items), dim3(256), lds, stream, bins, m, idx, label, wcnt,
-                       reinterpret_cast<const int4*>(items), node_feats, nf, B, S, hist_u, hist_d);
+    hipLaunchKernelGGL(rf_hist_kernel<false>, dim3(n_items), dim3(256), lds, stream, bins, m, idx, w2,
+                       reinterpret_cast<const int4*>(items), node_feats, nf, B, S, 1.0, hist_u, hist_d);
   return srml_status();
 }
 
 // ------------------------------------------------------------------------------------------
 // split search. crit: 0 gini, 1 entropy, 2 variance.  out per node (double[6]):
 //   {gain, feature_slot, bin, n_left, n_right, parent_impurity}
-// totals per node (double[S]): class counts or (count, sum, sumsq)
+// totals per node (double[S]): class counts or (count, sum); the regression gain is the exact
+// variance reduction computed from (count, sum) alone, parent impurity is reported as 0 then
 // ------------------------------------------------------------------------------------------
 template <int SMAX>
 __device__ __forceinline__ double impurity(const double* s, int S, int crit, double n) {
@@ -212,7 +244,7 @@ __global__ __launch_bounds__(256) void rf_best_split_kernel(const unsigned* __re
 #pragma unroll
     for (int c = 0; c < SMAX; ++c) ntot += tot[c];
   }
-  const double pimp = impurity<SMAX>(tot, S, crit, ntot);
+  const double pimp = (REG && S < 3) ? 0.0 : impurity<SMAX>(tot, S, crit, ntot);
   double best = -1.0;
   int bkey = 0x7fffffff;
   for (int f = threadIdx.x; f < nf; f += 256) {
@@ -237,11 +269,17 @@ __global__ __launch_bounds__(256) void rf_best_split_kernel(const unsigned* __re
       }
       const double nr = ntot - nl;
       if (nl < min_leaf || nr < min_leaf || nl <= 0.0 || nr <= 0.0) continue;
-      double right[SMAX];
+      double gain;
+      if (REG) {
+        // variance reduction = (s_L^2/n_L + s_R^2/n_R - s^2/n) / n  (the sums of squares cancel)
+        const double sl = left[1], sr = tot[1] - left[1];
+        gain = (sl * sl / nl + sr * sr / nr - tot[1] * tot[1] / ntot) / ntot;
+      } else {
+        double right[SMAX];
 #pragma unroll
-      for (int c = 0; c < SMAX; ++c) right[c] = tot[c] - left[c];
-      const double gain = pimp - (nl / ntot) * impurity<SMAX>(left, S, crit, nl) -
-                          (nr / ntot) * impurity<SMAX>(right, S, crit, nr);
+        for (int c = 0; c < SMAX; ++c) right[c] = tot[c] - left[c];
+        gain = pimp - (nl / ntot) * impurity<SMAX>(left, S, crit, nl) - (nr / ntot) * impurity<SMAX>(right, S, crit, nr);
+      }
       const int key = f * 1024 + b;
       if (gain > best || (gain == best && key < bkey)) { best = gain; bkey = key; }
     }

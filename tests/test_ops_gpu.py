@@ -155,7 +155,7 @@ def test_rf_hist_split_route(gpu_device, regression):
     X, edges, y = _rf_setup(gpu_device)
     if regression:
         y = X[:, 0] * 2 + 0.1 * torch.randn(X.shape[0], generator=torch.Generator().manual_seed(5))
-    S = 3
+    S = 2 if regression else 3
     B = edges.shape[1] + 1
     bins = ops.rf_quantize(X, edges)
     m = X.shape[0]

@@ -133,6 +133,32 @@ def main():
         umap_transform(Xu, Xs, torch.from_numpy(emb).to(dev), dict(n_neighbors=15, random_state=1))
         torch.cuda.synchronize()
         res["umap_transform_100k_x3000"] = {"ms": (time.perf_counter() - t0) * 1e3}
+    if want("rfhist"):
+        # root level of a regression tree at the headline shape: in-bag rows x 1000 sampled features
+        import numpy as np
+
+        n_, m_ = a.n, a.m
+        del X
+        torch.cuda.empty_cache()
+        bins = torch.randint(0, 128, (n_, m_), device=dev, dtype=torch.uint8, generator=g)
+        w = torch.poisson(torch.ones(m_, device=dev), generator=g).clamp_max(255).to(torch.uint8)
+        idx = torch.nonzero(w).view(-1).int()
+        y = torch.randn(m_, device=dev, generator=g)
+        nf = max(1, n_ // 3)
+        feats = torch.randperm(n_, device=dev, generator=g)[:nf].int().view(1, -1).contiguous()
+        nfc = (nf + 7) // 8
+        rows = idx.shape[0]
+        rpi = int(min(65536, max(4096, rows * nfc // 8192)))
+        rpi = (rpi + 511) // 512 * 512
+        it = []
+        for r0 in range(0, rows, rpi):
+            for fc in range(nfc):
+                it.append((0, r0, min(rows, r0 + rpi), fc))
+        items = torch.tensor(np.array(it, dtype=np.int32), device=dev)
+        for reg, S, nm in ((True, 2, "rf_hist_reg_root"), (False, 3, "rf_hist_clf3_root")):
+            yy = y if reg else torch.randint(0, 3, (m_,), device=dev, generator=g).float()
+            t = timeit(lambda: ops.rf_hist(bins, idx, yy, w, items, feats, 1, 128, S, reg), 3)
+            res[nm] = {"ms": t, "Gpairs/s": rows * nf / t / 1e6}
     print(json.dumps({k: {kk: round(vv, 3) for kk, vv in v.items()} for k, v in res.items()}))
 
 
