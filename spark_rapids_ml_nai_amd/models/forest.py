@@ -149,12 +149,40 @@ def _impurity_np(tot: np.ndarray, crit: int) -> float:
     return float(-(nz * np.log2(nz)).sum())
 
 
-def grow_tree(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: WorkerContext, gen: torch.Generator,
-              p: Dict[str, Any], S: int, regression: bool, data_parallel: bool,
-              gen_boot: Optional[torch.Generator] = None) -> Tree:
+def _segment_sums(vals: torch.Tensor, bounds: torch.Tensor) -> torch.Tensor:
+    """vals (K, N) fp64, bounds (L+1,) sorted positions -> (L, K) sums over [bounds[i], bounds[i+1])
+    as one row-contiguous scan + boundary gathers (no atomics)."""
+    K = vals.shape[0]
+    cs = torch.cat([torch.zeros((K, 1), dtype=torch.float64, device=vals.device), vals.cumsum(1)], 1)
+    return (cs[:, bounds[1:]] - cs[:, bounds[:-1]]).T.contiguous()
+
+
+def _node_stats(yv: torch.Tensor, idx: torch.Tensor, wpos: torch.Tensor, bounds: torch.Tensor, S: int,
+                regression: bool) -> torch.Tensor:
+    wr = wpos.double()
+    yr = yv[idx.long()].double()
+    if regression:
+        vals = torch.stack([wr, wr * yr, wr * yr * yr], 0)
+    else:
+        yl = yr.long()
+        vals = torch.stack([wr * (yl == c) for c in range(S)], 0)
+    return _segment_sums(vals, bounds)
+
+
+HIST_BUDGET_BYTES = 1 << 30
+
+
+def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: WorkerContext,
+                gen: torch.Generator, p: Dict[str, Any], S: int, regression: bool, data_parallel: bool,
+                gen_boot: Optional[torch.Generator], n_trees: int) -> List[Tree]:
+    """Grow ``n_trees`` trees level-synchronously: every level of every tree is ONE histogram /
+    split / route / partition pass over the concatenated (tree, node) segments, so the per-level
+    launches and host round trips are amortised over the whole forest (cuML grows trees
+    concurrently on streams for the same reason; here they share one batched launch)."""
     dev = bins.device
     n, m = bins.shape
     B = edges_h.shape[1] + 1
+    SH = 2 if regression else S  # regression histograms carry (count, sum) only
     crit = {"gini": 0, "entropy": 1, "variance": 2, "mse": 2}[p["split_criterion"]]
     max_depth = int(p["max_depth"])
     min_leaf = float(p["min_samples_leaf"])
@@ -162,66 +190,73 @@ def grow_tree(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: Wor
     min_gain = float(p.get("min_impurity_decrease", 0.0))
     nf = int(p["_nf"])
     max_leaves = int(p.get("max_leaves", -1))
-    # bootstrap multiplicities (Spark: Poisson(subsamplingRate) bagging)
-    if p["bootstrap"]:
-        rate = float(p.get("max_samples", 1.0))
-        w = torch.poisson(torch.full((m,), rate, device=dev), generator=gen_boot or gen).clamp_max(255).to(torch.uint8)
-    else:
-        w = torch.ones(m, dtype=torch.uint8, device=dev)
-    idx = torch.nonzero(w, as_tuple=False).view(-1).to(torch.int32)
-    yv = y.float()
-    tree = Tree()
-    root = tree.add_node()
-    # level state: tree node ids, segment starts/counts (host)
-    level_nodes = [root]
-    starts = np.array([0], dtype=np.int64)
-    counts = np.array([int(idx.shape[0])], dtype=np.int64)
-    depth = 0
-    n_leaves = 1
-    # root totals (weighted class counts / regression moments); deeper levels inherit their
-    # totals from the parent's winning split (prefix of its histogram), no pass over the rows
-    wr = w[idx.long()].double()
-    if regression:
-        yr = yv[idx.long()].double()
-        tot = torch.stack([wr.sum(), (wr * yr).sum(), (wr * yr * yr).sum()]).view(1, 3)
-    else:
-        tot = torch.bincount(yv[idx.long()].long(), weights=wr, minlength=S)[:S].double().view(1, S)
+    yv = y.float().contiguous()
+    trees = [Tree() for _ in range(n_trees)]
+    # bootstrap multiplicities per tree (Spark: Poisson(subsamplingRate) bagging); positions of
+    # all trees are concatenated: segment = (tree, node), rows stay ascending inside a segment
+    idx_l, w_l, cnt0 = [], [], []
+    for _ in range(n_trees):
+        if p["bootstrap"]:
+            rate = float(p.get("max_samples", 1.0))
+            w = torch.poisson(torch.full((m,), rate, device=dev), generator=gen_boot or gen).clamp_max(255)
+        else:
+            w = torch.ones(m, device=dev)
+        ii = torch.nonzero(w, as_tuple=False).view(-1).to(torch.int32)
+        idx_l.append(ii)
+        w_l.append(w[ii.long()].float())
+        cnt0.append(int(ii.shape[0]))
+    idx = torch.cat(idx_l).contiguous()
+    wpos = torch.cat(w_l).contiguous()
+    del idx_l, w_l
+    seg_tree = np.arange(n_trees, dtype=np.int64)
+    seg_nid = np.array([t.add_node() for t in trees], dtype=np.int64)
+    counts = np.asarray(cnt0, dtype=np.int64)
+    bounds_h = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    bounds = torch.from_numpy(bounds_h).to(dev)
+    tot = _node_stats(yv, idx, wpos, bounds, S, regression)
     if data_parallel:
         ctx.comm.allreduce(tot)
+    n_leaves = np.ones(n_trees, dtype=np.int64)
     nfc = (nf + 7) // 8
-    while level_nodes:
-        L = len(level_nodes)
-        total = int(counts.sum())
-        seg_node = torch.repeat_interleave(torch.arange(L, device=dev, dtype=torch.int32),
-                                           torch.from_numpy(counts).to(dev))
+    hist_cell = (8 if regression else 4) * nf * B * SH
+    group = max(1, HIST_BUDGET_BYTES // max(hist_cell, 1))
+    depth = 0
+    while len(seg_tree):
+        L = len(seg_tree)
         tot_h = tot.cpu().numpy()
         wsum = tot_h[:, 0] if regression else tot_h.sum(1)
-        for j, nid in enumerate(level_nodes):
-            tree.value[nid] = _leaf_value(tot_h[j], regression)
-            tree.count[nid] = float(wsum[j])
-            tree.impurity[nid] = _impurity_np(tot_h[j], crit)
-        tree.depth = depth
+        imps = np.empty(L)
+        for j in range(L):
+            t = trees[seg_tree[j]]
+            nid = int(seg_nid[j])
+            t.value[nid] = _leaf_value(tot_h[j], regression)
+            t.count[nid] = float(wsum[j])
+            imps[j] = t.impurity[nid] = _impurity_np(tot_h[j], crit)
+        for t in trees:
+            t.depth = depth
         if depth >= max_depth:
             break
-        cand = [j for j in range(L) if wsum[j] >= max(min_split, 2 * min_leaf) and tree.impurity[level_nodes[j]] > 0.0]
-        if not cand:
+        cand = np.nonzero((wsum >= max(min_split, 2 * min_leaf)) & (imps > 0.0))[0]
+        if cand.size == 0:
             break
-        # feature subsets (device RNG; identical on all ranks in data-parallel mode)
-        C = len(cand)
-        if nf >= n:
-            feats = torch.arange(n, device=dev, dtype=torch.int32).repeat(C, 1)
-        else:
-            feats = torch.rand((C, n), generator=gen, device=dev).argsort(1)[:, :nf].to(torch.int32).contiguous()
-        # work items (node slot, row begin, row end, feature chunk), built vectorised
-        cand_a = np.asarray(cand, dtype=np.int64)
-        c_start, c_cnt = starts[cand_a], counts[cand_a]
-        # rows per work item: enough blocks to fill the chip (~8K) but as few per (node, feature
-        # chunk) as possible — every block flushes its LDS histogram with global fp64 atomics
-        rpi = int(min(65536, max(ROWS_PER_ITEM, (int(c_cnt.sum()) * nfc) // 8192)))
-        rpi = (rpi + 511) // 512 * 512
-        nch = (c_cnt + rpi - 1) // rpi
-        tot_ch = int(nch.sum())
-        if tot_ch:
+        total = int(bounds_h[-1])
+        # ---- histograms + split search, in groups of candidate segments bounded by memory ----
+        res_out: List[np.ndarray] = []
+        res_feat: List[np.ndarray] = []
+        res_sel: List[torch.Tensor] = []
+        for g0 in range(0, cand.size, group):
+            cg = cand[g0: g0 + group]
+            C = int(cg.size)
+            if nf >= n:
+                feats = torch.arange(n, device=dev, dtype=torch.int32).repeat(C, 1)
+            else:
+                feats = torch.rand((C, n), generator=gen, device=dev).argsort(1)[:, :nf].to(torch.int32).contiguous()
+            c_start, c_cnt = bounds_h[cg], counts[cg]
+            # rows per work item: ~8K blocks to fill the chip, few blocks per (node, feature chunk)
+            rpi = int(min(65536, max(ROWS_PER_ITEM, (int(c_cnt.sum()) * nfc) // 8192)))
+            rpi = (rpi + 511) // 512 * 512
+            nch = (c_cnt + rpi - 1) // rpi
+            tot_ch = int(nch.sum())
             node_rep = np.repeat(np.arange(C), nch)
             first = np.repeat(np.cumsum(nch) - nch, nch)
             chunk = np.arange(tot_ch) - first
@@ -232,89 +267,108 @@ def grow_tree(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: Wor
             it[:, 1] = np.repeat(rb, nfc)
             it[:, 2] = np.repeat(re, nfc)
             it[:, 3] = np.tile(np.arange(nfc), tot_ch)
-            items_t = torch.from_numpy(it).to(dev)
+            items_t = torch.from_numpy(it).to(dev, non_blocking=False)
+            hist = ops.rf_hist(bins, idx, yv, None, items_t, feats, C, B, SH, regression, pos_weight=wpos)
+            if data_parallel:
+                ctx.comm.allreduce(hist)
+            out, _ = ops.rf_best_split(hist, B, SH, regression, crit, min_leaf, min_gain)
+            out_h = out.cpu().numpy()
+            res_out.append(out_h)
+            feats_h = feats.cpu().numpy()
+            ok = out_h[:, 1] >= 0
+            res_feat.append(np.where(ok, feats_h[np.arange(C), np.where(ok, out_h[:, 1], 0).astype(np.int64)], -1))
+            if not regression:
+                okc = np.nonzero(ok)[0]
+                if okc.size:
+                    ci_t = torch.from_numpy(okc).to(dev)
+                    sl_t = torch.from_numpy(out_h[okc, 1].astype(np.int64)).to(dev)
+                    res_sel.append(hist[ci_t, sl_t].double())  # (k_g, B, S) winning histograms
+            del hist
+        out_all = np.concatenate(res_out, 0)
+        feat_all = np.concatenate(res_feat, 0)
+        # ---- decide splits (honour max_leaves per tree) ----
+        ok = out_all[:, 1] >= 0
+        order = np.nonzero(ok)[0]
+        if max_leaves > 0 and order.size:
+            keep = []
+            by_tree: Dict[int, List[int]] = {}
+            for ci in order:
+                by_tree.setdefault(int(seg_tree[cand[ci]]), []).append(int(ci))
+            for t_i, cis in by_tree.items():
+                cis.sort(key=lambda ci: -out_all[ci, 0])
+                keep += cis[: max(0, max_leaves - int(n_leaves[t_i]))]
+            keep_set = set(keep)
         else:
-            items_t = torch.zeros((0, 4), dtype=torch.int32, device=dev)
-        SH = 2 if regression else S  # regression histograms carry (count, sum) only
-        hist = ops.rf_hist(bins, idx, yv, w, items_t, feats, C, B, SH, regression)
-        if data_parallel:
-            ctx.comm.allreduce(hist)
-        out, _ = ops.rf_best_split(hist, B, SH, regression, crit, min_leaf, min_gain)
-        out_h = out.cpu().numpy()
-        feats_h = feats.cpu().numpy()
-        # honour max_leaves: keep the best-gain splits that fit
-        order = [ci for ci in range(C) if out_h[ci, 1] >= 0]
-        if max_leaves > 0:
-            order.sort(key=lambda ci: -out_h[ci, 0])
-            order = order[: max(0, max_leaves - n_leaves)]
-        split_set = set(order)
+            keep_set = None
         node_feature = np.full(L, -1, dtype=np.int32)
         node_bin = np.zeros(L, dtype=np.int32)
         child_base = np.zeros(L, dtype=np.int32)
-        next_nodes: List[int] = []
+        new_tree: List[int] = []
+        new_nid: List[int] = []
+        sel_rows: List[int] = []  # index into the concatenated winning histograms (classification)
         k = 0
-        split_ci: List[int] = []
-        split_slot: List[int] = []
-        split_bin: List[int] = []
-        split_j: List[int] = []
-        for ci, j in enumerate(cand):
-            if ci not in split_set:
+        sel_i = -1
+        for ci in order:
+            sel_i += 1
+            if keep_set is not None and int(ci) not in keep_set:
                 continue
-            split_ci.append(ci)
-            split_slot.append(int(out_h[ci, 1]))
-            split_bin.append(int(out_h[ci, 2]))
-            split_j.append(j)
-            nid = level_nodes[j]
-            slot = int(out_h[ci, 1])
-            b = int(out_h[ci, 2])
-            f = int(feats_h[ci, slot])
-            tree.feature[nid] = f
-            tree.threshold[nid] = float(edges_h[f, b])
-            tree.gain[nid] = float(out_h[ci, 0])
-            lnode, rnode = tree.add_node(), tree.add_node()
-            tree.left[nid], tree.right[nid] = lnode, rnode
-            next_nodes += [lnode, rnode]
+            j = int(cand[ci])
+            t_i = int(seg_tree[j])
+            t = trees[t_i]
+            nid = int(seg_nid[j])
+            b = int(out_all[ci, 2])
+            f = int(feat_all[ci])
+            t.feature[nid] = f
+            t.threshold[nid] = float(edges_h[f, b])
+            t.gain[nid] = float(out_all[ci, 0])
+            lnode, rnode = t.add_node(), t.add_node()
+            t.left[nid], t.right[nid] = lnode, rnode
+            new_tree += [t_i, t_i]
+            new_nid += [lnode, rnode]
             node_feature[j] = f
             node_bin[j] = b
             child_base[j] = 2 * k
+            sel_rows.append(sel_i)
             k += 1
-            n_leaves += 1
+            n_leaves[t_i] += 1
         if k == 0:
             break
-        if not regression:
-            # children totals = prefix of the winning feature's histogram up to the split bin
-            ci_t = torch.tensor(split_ci, device=dev)
-            sel = hist[ci_t, torch.tensor(split_slot, device=dev)].double()  # (k, B, S)
-            left = sel.cumsum(1)[torch.arange(k, device=dev), torch.tensor(split_bin, device=dev)]
-            right = tot[torch.tensor(split_j, device=dev)] - left
-            tot = torch.stack([left, right], 1).reshape(2 * k, S)
-        keys = ops.rf_route(bins, idx[:total].contiguous(), seg_node.contiguous(),
-                            torch.from_numpy(node_feature).to(dev), torch.from_numpy(node_bin).to(dev),
-                            torch.from_numpy(child_base).to(dev))
+        # ---- route + stable partition into child segments ----
+        meta = torch.from_numpy(np.stack([node_feature, node_bin, child_base])).to(dev)
+        keys = ops.rf_route_segments(bins, idx, bounds, meta[0].contiguous(), meta[1].contiguous(),
+                                     meta[2].contiguous())
         keys_sorted, perm = torch.sort(keys, stable=True)
-        kept = int((keys_sorted != INT_MAX).sum().item())
-        idx = idx[:total][perm[:kept]].contiguous()
-        # child segment boundaries in the sorted key order (no atomics: keys are sorted)
-        bounds = torch.searchsorted(keys_sorted[:kept].contiguous(),
-                                    torch.arange(2 * k + 1, device=dev, dtype=keys_sorted.dtype))
+        nb = torch.searchsorted(keys_sorted.contiguous(), torch.arange(2 * k + 1, device=dev, dtype=keys_sorted.dtype))
+        kept = int(nb[-1].item())
+        perm = perm[:kept]
+        idx = idx[perm].contiguous()
+        wpos = wpos[perm].contiguous()
+        bounds = nb.to(torch.int64)
         if regression:
-            # children (count, sum, sumsq) as segment sums over the routed rows (histograms hold no
-            # sum of squares): one cumsum + boundary gathers
-            rows = idx.long()
-            wr = w[rows].double()
-            yr = yv[rows].double()
-            # (3, N) row-contiguous scans: torch's outer-dim scan of an (N, 3) tensor is ~100x slower
-            v = torch.stack([wr, wr * yr, wr * yr * yr], 0)
-            cs = torch.cat([torch.zeros((3, 1), dtype=torch.float64, device=dev), v.cumsum(1)], 1)
-            tot = (cs[:, bounds[1:]] - cs[:, bounds[:-1]]).T.contiguous()
-            if data_parallel:
-                ctx.comm.allreduce(tot)
-        cnt = (bounds[1:] - bounds[:-1]).cpu().numpy().astype(np.int64)
-        counts = cnt
-        starts = np.concatenate([[0], np.cumsum(cnt)[:-1]]).astype(np.int64)
-        level_nodes = next_nodes
+            tot = _node_stats(yv, idx, wpos, bounds, S, regression)
+        else:
+            # children totals = prefix of each winning histogram up to its split bin
+            sel = torch.cat(res_sel, 0)[torch.tensor(sel_rows, device=dev)]  # (k, B, S)
+            split_bin = torch.from_numpy(node_bin[node_feature >= 0].astype(np.int64)).to(dev)
+            # node_feature >= 0 segments are in cand order == split order
+            left = sel.cumsum(1)[torch.arange(k, device=dev), split_bin]
+            split_seg = torch.from_numpy(np.nonzero(node_feature >= 0)[0]).to(dev)
+            right = tot[split_seg] - left
+            tot = torch.stack([left, right], 1).reshape(2 * k, S)
+        if data_parallel and regression:
+            ctx.comm.allreduce(tot)
+        bounds_h = bounds.cpu().numpy().astype(np.int64)
+        counts = np.diff(bounds_h)
+        seg_tree = np.asarray(new_tree, dtype=np.int64)
+        seg_nid = np.asarray(new_nid, dtype=np.int64)
         depth += 1
-    return tree
+    return trees
+
+
+def grow_tree(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: WorkerContext, gen: torch.Generator,
+              p: Dict[str, Any], S: int, regression: bool, data_parallel: bool,
+              gen_boot: Optional[torch.Generator] = None) -> Tree:
+    return grow_forest(bins, edges_h, y, ctx, gen, p, S, regression, data_parallel, gen_boot, 1)[0]
 
 
 def fit_forest(X: torch.Tensor, y: torch.Tensor, ctx: WorkerContext, m_total: int, p: Dict[str, Any],
@@ -335,10 +389,13 @@ def fit_forest(X: torch.Tensor, y: torch.Tensor, ctx: WorkerContext, m_total: in
     gen.manual_seed((int(seed) if data_parallel else int(rank_seed)) & 0x7FFFFFFFFFFF)
     gen_boot = torch.Generator(device=X.device)
     gen_boot.manual_seed((int(rank_seed) * 31 + 17) & 0x7FFFFFFFFFFF)
-    trees = []
-    for _ in range(n_trees_local):
-        t = grow_tree(bins, edges_h, y, ctx, gen, p, S, not classification, data_parallel, gen_boot)
-        trees.append(t.to_dict())
+    trees: List[Dict[str, Any]] = []
+    # trees per batch: positions + weights cost ~8 B per in-bag row and tree
+    per_batch = max(1, int((4 << 30) // max(8 * m, 1)))
+    for t0 in range(0, n_trees_local, per_batch):
+        nt = min(per_batch, n_trees_local - t0)
+        for t in grow_forest(bins, edges_h, y, ctx, gen, p, S, not classification, data_parallel, gen_boot, nt):
+            trees.append(t.to_dict())
     del bins
     return trees
 

@@ -286,8 +286,9 @@ def rf_quantize(X: torch.Tensor, edges: torch.Tensor) -> torch.Tensor:
 
 def rf_hist(bins: torch.Tensor, idx: torch.Tensor, label: torch.Tensor, wcnt: Optional[torch.Tensor],
             items: torch.Tensor, node_feats: torch.Tensor, nodes: int, B: int, S: int,
-            regression: bool) -> torch.Tensor:
-    """Per-(node, feature slot, bin) statistics: uint32 class counts or fp64 (count, sum, sumsq)."""
+            regression: bool, pos_weight: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Per-(node, feature slot, bin) statistics: uint32 class counts or fp64 (count, sum[, sumsq]).
+    Weights: per row (``wcnt``, indexed by row id) or per position of ``idx`` (``pos_weight``)."""
     n, m = bins.shape
     nf = node_feats.shape[1]
     dev = bins.device
@@ -301,7 +302,10 @@ def rf_hist(bins: torch.Tensor, idx: torch.Tensor, label: torch.Tensor, wcnt: Op
         it = items.cpu().numpy()
         for node, rb, re, fc in it:
             rows = idx[rb:re].long()
-            w = wcnt[rows].double() if wcnt is not None else torch.ones(len(rows), dtype=torch.float64)
+            if pos_weight is not None:
+                w = pos_weight[rb:re].double()
+            else:
+                w = wcnt[rows].double() if wcnt is not None else torch.ones(len(rows), dtype=torch.float64)
             y = label[rows]
             for j in range(fc * 8, min(nf, fc * 8 + 8)):
                 f = int(node_feats[node, j])
@@ -317,7 +321,10 @@ def rf_hist(bins: torch.Tensor, idx: torch.Tensor, label: torch.Tensor, wcnt: Op
         return hist
     # compact (weight, label) into idx order once: contiguous loads in the row stream
     rows = idx.long()
-    wv = wcnt[rows].float() if wcnt is not None else torch.ones(rows.shape[0], dtype=torch.float32, device=dev)
+    if pos_weight is not None:
+        wv = pos_weight.float()
+    else:
+        wv = wcnt[rows].float() if wcnt is not None else torch.ones(rows.shape[0], dtype=torch.float32, device=dev)
     wy = torch.stack([wv, label[rows].float()], 1).contiguous()
     yscale = 1.0
     if regression:
@@ -415,6 +422,23 @@ def rf_route(bins: torch.Tensor, idx: torch.Tensor, seg_node: torch.Tensor, node
     native.call("srml_rf_route", bins.data_ptr(), m, idx.data_ptr(), seg_node.data_ptr(), total,
                 node_feature.data_ptr(), node_bin.data_ptr(), child_base.data_ptr(), keys.data_ptr(),
                 native.stream(bins.device))
+    return keys
+
+
+def rf_route_segments(bins: torch.Tensor, idx: torch.Tensor, bounds: torch.Tensor, node_feature: torch.Tensor,
+                      node_bin: torch.Tensor, child_base: torch.Tensor) -> torch.Tensor:
+    """Child key of every position: segment s = [bounds[s], bounds[s+1]) found by binary search."""
+    n, m = bins.shape
+    total = idx.shape[0]
+    if not bins.is_cuda:
+        pos = torch.arange(total, device=bins.device)
+        seg = (torch.searchsorted(bounds.long(), pos, right=True) - 1).int()
+        return rf_route(bins, idx, seg, node_feature, node_bin, child_base)
+    keys = torch.empty(total, dtype=torch.int32, device=bins.device)
+    if total:
+        native.call("srml_rf_route_segments", bins.data_ptr(), m, idx.data_ptr(), total,
+                    _c(bounds.long()).data_ptr(), int(bounds.shape[0] - 1), node_feature.data_ptr(),
+                    node_bin.data_ptr(), child_base.data_ptr(), keys.data_ptr(), native.stream(bins.device))
     return keys
 
 

@@ -378,6 +378,38 @@ SRML_API int srml_rf_route(const unsigned char* bins, long m, const int* idx, co
   return srml_status();
 }
 
+// segment-bounds variant: the segment of position i is found by binary search over the sorted
+// bounds (no per-position segment-id array to materialise each level)
+__global__ void rf_route_segments_kernel(const unsigned char* __restrict__ bins, long m, const int* __restrict__ idx,
+                                         long total, const long long* __restrict__ bounds, int nseg,
+                                         const int* __restrict__ node_feature, const int* __restrict__ node_bin,
+                                         const int* __restrict__ child_base, int* __restrict__ keys) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  int lo = 0, hi = nseg - 1;  // largest s with bounds[s] <= i
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (bounds[mid] <= i) lo = mid; else hi = mid - 1;
+  }
+  const int node = lo;
+  const int f = node_feature[node];
+  if (f < 0) {
+    keys[i] = 0x7fffffff;
+    return;
+  }
+  const int r = idx[i];
+  keys[i] = child_base[node] + (bins[(long)f * m + r] > node_bin[node] ? 1 : 0);
+}
+
+SRML_API int srml_rf_route_segments(const unsigned char* bins, long m, const int* idx, long total,
+                                    const long long* bounds, int nseg, const int* node_feature, const int* node_bin,
+                                    const int* child_base, int* keys, hipStream_t stream) {
+  if (total <= 0 || nseg <= 0) return 0;
+  hipLaunchKernelGGL(rf_route_segments_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, bins, m,
+                     idx, total, bounds, nseg, node_feature, node_bin, child_base, keys);
+  return srml_status();
+}
+
 // ------------------------------------------------------------------------------------------
 // inference: trees stored as flat node arrays; roots[t] = first node of tree t.
 // feature < 0 => leaf whose value vector (width S) starts at values[value_off[node]].
