@@ -149,24 +149,9 @@ def _impurity_np(tot: np.ndarray, crit: int) -> float:
     return float(-(nz * np.log2(nz)).sum())
 
 
-def _segment_sums(vals: torch.Tensor, bounds: torch.Tensor) -> torch.Tensor:
-    """vals (K, N) fp64, bounds (L+1,) sorted positions -> (L, K) sums over [bounds[i], bounds[i+1])
-    as one row-contiguous scan + boundary gathers (no atomics)."""
-    K = vals.shape[0]
-    cs = torch.cat([torch.zeros((K, 1), dtype=torch.float64, device=vals.device), vals.cumsum(1)], 1)
-    return (cs[:, bounds[1:]] - cs[:, bounds[:-1]]).T.contiguous()
-
-
 def _node_stats(yv: torch.Tensor, idx: torch.Tensor, wpos: torch.Tensor, bounds: torch.Tensor, S: int,
                 regression: bool) -> torch.Tensor:
-    wr = wpos.double()
-    yr = yv[idx.long()].double()
-    if regression:
-        vals = torch.stack([wr, wr * yr, wr * yr * yr], 0)
-    else:
-        yl = yr.long()
-        vals = torch.stack([wr * (yl == c) for c in range(S)], 0)
-    return _segment_sums(vals, bounds)
+    return ops.rf_node_stats(idx, wpos, yv, bounds, S, regression)
 
 
 HIST_BUDGET_BYTES = 1 << 30

@@ -442,6 +442,30 @@ def rf_route_segments(bins: torch.Tensor, idx: torch.Tensor, bounds: torch.Tenso
     return keys
 
 
+def rf_node_stats(idx: torch.Tensor, wpos: torch.Tensor, label: torch.Tensor, bounds: torch.Tensor, S: int,
+                  regression: bool) -> torch.Tensor:
+    """Per segment [bounds[s], bounds[s+1]): regression (sum w, sum w y, sum w y^2) or per-class sum w
+    (nseg, 3 | S) fp64."""
+    nseg = bounds.shape[0] - 1
+    K = 3 if regression else S
+    dev = idx.device
+    if not idx.is_cuda:
+        wr = wpos.double()
+        yr = label[idx.long()].double()
+        if regression:
+            vals = torch.stack([wr, wr * yr, wr * yr * yr], 0)
+        else:
+            vals = torch.stack([wr * (yr.long() == c) for c in range(S)], 0)
+        cs = torch.cat([torch.zeros((K, 1), dtype=torch.float64), vals.cumsum(1)], 1)
+        b = bounds.long()
+        return (cs[:, b[1:]] - cs[:, b[:-1]]).T.contiguous()
+    out = torch.zeros((nseg, K), dtype=torch.float64, device=dev)
+    native.call("srml_rf_node_stats", idx.data_ptr(), _c(wpos.float()).data_ptr(), _c(label.float()).data_ptr(),
+                int(idx.shape[0]), _c(bounds.long()).data_ptr(), nseg, int(S), int(regression), out.data_ptr(),
+                native.stream(dev))
+    return out
+
+
 def rf_predict(X: torch.Tensor, roots: torch.Tensor, feature: torch.Tensor, threshold: torch.Tensor,
                left: torch.Tensor, right: torch.Tensor, value_off: torch.Tensor, values: torch.Tensor, S: int,
                want_leaves: bool = False) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:

@@ -411,6 +411,75 @@ SRML_API int srml_rf_route_segments(const unsigned char* bins, long m, const int
 }
 
 // ------------------------------------------------------------------------------------------
+// per-segment node statistics (replaces cumsum-based segment sums): each block reduces a
+// contiguous chunk of positions in registers and flushes one fp64 atomic per (segment, stat)
+// it touched; chunks are sorted so a block rarely spans more than a couple of segments.
+// regression: (sum w, sum w y, sum w y^2); classification: per-class sum w.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void rf_node_stats_kernel(const int* __restrict__ idx,
+                                                            const float* __restrict__ wpos,
+                                                            const float* __restrict__ label, long total,
+                                                            const long long* __restrict__ bounds, int nseg, int S,
+                                                            int regression, long chunk, double* __restrict__ out) {
+  __shared__ double red[4][32];
+  const long p0 = (long)blockIdx.x * chunk;
+  const long p1 = min(total, p0 + chunk);
+  if (p0 >= p1) return;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // first segment of the chunk
+  int lo = 0, hi = nseg - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (bounds[mid] <= p0) lo = mid; else hi = mid - 1;
+  }
+  const int NS = regression ? 3 : S;
+  for (int seg = lo; seg < nseg && bounds[seg] < p1; ++seg) {
+    const long a = max(p0, (long)bounds[seg]), b = min(p1, (long)bounds[seg + 1]);
+    if (a >= b) continue;
+    double acc[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) acc[k] = 0.0;
+    for (long i = a + threadIdx.x; i < b; i += 256) {
+      const double w = wpos[i];
+      const double y = label[idx[i]];
+      if (regression) {
+        acc[0] += w;
+        acc[1] += w * y;
+        acc[2] += w * y * y;
+      } else {
+        const int c = (int)y;
+#pragma unroll
+        for (int k = 0; k < 32; ++k)
+          if (k == c) acc[k] += w;
+      }
+    }
+    for (int k = 0; k < NS; ++k) {
+      const double v = wave_sum(acc[k]);
+      if (lane == 0) red[wid][k] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < NS) {
+      const double v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+      if (v != 0.0) atomicAdd(&out[(long)seg * NS + threadIdx.x], v);
+    }
+    __syncthreads();
+  }
+}
+
+SRML_API int srml_rf_node_stats(const int* idx, const float* wpos, const float* label, long total,
+                                const long long* bounds, int nseg, int S, int regression, double* out,
+                                hipStream_t stream) {
+  if (total <= 0 || nseg <= 0) return 0;
+  if (!regression && S > 32) return -7;
+  long chunk = (total + 4095) / 4096;
+  if (chunk < 2048) chunk = 2048;
+  const long blocks = (total + chunk - 1) / chunk;
+  hipLaunchKernelGGL(rf_node_stats_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, idx, wpos, label, total,
+                     bounds, nseg, S, regression, chunk, out);
+  return srml_status();
+}
+
+// ------------------------------------------------------------------------------------------
 // inference: trees stored as flat node arrays; roots[t] = first node of tree t.
 // feature < 0 => leaf whose value vector (width S) starts at values[value_off[node]].
 // ------------------------------------------------------------------------------------------

@@ -57,6 +57,7 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_rf_best_split": (_P, _P, _I, _I, _I, _I, _I, _I, _D, _D, _P, _P, _P),
     "srml_rf_route": (_P, _L, _P, _P, _L, _P, _P, _P, _P, _P),
     "srml_rf_route_segments": (_P, _L, _P, _L, _P, _I, _P, _P, _P, _P, _P),
+    "srml_rf_node_stats": (_P, _P, _P, _L, _P, _I, _I, _I, _P, _P),
     "srml_rf_predict": (_P, _L, _L, _P, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P),
 }
 

@@ -411,3 +411,18 @@ def test_streamed_ingest_scatter_stats(gpu_device):
         ref_xty = Xd.T @ y.float().double()  # labels reach the kernel as fp32 (feature dtype)
         assert (s.xty.cpu() - ref_xty).abs().max().item() / ref_xty.abs().max().item() < 1e-6
     torch.testing.assert_close(sr.wait_all().cpu(), h)
+
+
+@pytest.mark.parametrize("regression", [True, False])
+def test_rf_node_stats(gpu_device, regression):
+    g = torch.Generator().manual_seed(3)
+    m = 200000
+    idx = torch.sort(torch.randperm(m, generator=g)[:150000]).values.int()
+    wpos = torch.randint(1, 4, (idx.shape[0],), generator=g).float()
+    y = (torch.randn(m, generator=g) * 5) if regression else torch.randint(0, 5, (m,), generator=g).float()
+    bounds = torch.tensor([0, 10, 10, 5000, 70000, 149999, 150000], dtype=torch.int64)
+    S = 5
+    ref = ops.rf_node_stats(idx, wpos, y, bounds, S, regression)
+    got = ops.rf_node_stats(idx.to(gpu_device), wpos.to(gpu_device), y.to(gpu_device), bounds.to(gpu_device), S,
+                            regression).cpu()
+    torch.testing.assert_close(got, ref, rtol=1e-9, atol=1e-6)
