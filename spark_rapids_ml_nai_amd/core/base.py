@@ -348,12 +348,12 @@ def _fit_worker(ctx: WorkerContext, payload: Tuple[HostPartition, Callable, Dict
         raise RuntimeError("A worker received no data. Please increase amount of data or use fewer workers.")
     dtype = torch.float32 if float32 else torch.float64
     streamed = None
-    from ..ops.ingest import StreamedRows, is_pinned
+    from ..ops.ingest import StreamedRows, is_pinned, uvm_enabled
 
     if (ctx.is_gpu and isinstance(hp.X, np.ndarray) and hp.X.ndim == 2 and hp.X.shape[0] > 0
             and hp.X.dtype == (np.float32 if float32 else np.float64) and hp.X.flags.c_contiguous
             and getattr(fit_fn, "streaming_ingest", False) and os.environ.get("SRML_STREAM_INGEST", "1") == "1"
-            and is_pinned(hp.X)):
+            and not uvm_enabled() and is_pinned(hp.X)):
         streamed = StreamedRows(hp.X, ctx.device, dtype)
         X = streamed.X
     else:

@@ -39,6 +39,11 @@ def _dense_to_device(a: np.ndarray, device: torch.device, dtype: Optional[torch.
         t = t.to(dtype)
     if device.type != "cuda":
         return t.to(device)
+    if uvm_enabled() and t.dim() >= 1 and t.numel() * t.element_size() > _DIRECT_BYTES:
+        # UVM mode: the device copy lives in managed memory (pages migrate on demand)
+        out = managed_empty(t.shape, t.dtype, device)
+        out.copy_(t, non_blocking=t.is_pinned())
+        return out
     if t.is_pinned():
         # Arrow batch already in page-locked memory: one DMA straight into HBM
         return t.to(device, non_blocking=True)
@@ -158,3 +163,57 @@ def is_pinned(a: Any) -> bool:
             return bool(torch.from_numpy(a).is_pinned())
         except Exception:  # noqa: BLE001
             return False
+
+
+# ------------------------------------------------------------------------------------------
+# UVM (managed memory) mode: SRML_UVM=1 or Spark conf spark.rocm.ml.uvm.enabled=true
+# ------------------------------------------------------------------------------------------
+_TYPESTR = {torch.float32: "<f4", torch.float64: "<f8", torch.int32: "<i4", torch.int64: "<i8",
+            torch.uint8: "|u1", torch.int8: "|i1", torch.float16: "<f2"}
+
+
+def uvm_enabled() -> bool:
+    import os
+
+    return os.environ.get("SRML_UVM", "0").lower() in ("1", "true", "yes")
+
+
+class _ManagedBuffer:
+    """hipMallocManaged allocation (srml_managed_malloc) exposed through __cuda_array_interface__;
+    torch keeps this object alive for the tensor's lifetime and the allocation is freed with it."""
+
+    def __init__(self, shape: Any, dtype: torch.dtype, device: torch.device) -> None:
+        import ctypes
+
+        from . import native
+
+        lib = native.lib()
+        if not getattr(lib, "_srml_uvm_typed", False):
+            lib.srml_managed_malloc.restype = ctypes.c_void_p
+            lib.srml_managed_malloc.argtypes = [ctypes.c_ssize_t, ctypes.c_int, ctypes.c_void_p]
+            lib.srml_managed_free.restype = None
+            lib.srml_managed_free.argtypes = [ctypes.c_void_p, ctypes.c_ssize_t, ctypes.c_int, ctypes.c_void_p]
+            lib._srml_uvm_typed = True
+        self._lib = lib
+        self.shape = tuple(int(d) for d in shape)
+        n = 1
+        for d in self.shape:
+            n *= d
+        self.nbytes = max(1, n * torch.empty((), dtype=dtype).element_size())
+        self.device = device
+        self.ptr = lib.srml_managed_malloc(self.nbytes, device.index or 0, None)
+        if not self.ptr:
+            raise MemoryError("hipMallocManaged(%d) failed" % self.nbytes)
+        self.__cuda_array_interface__ = {"shape": self.shape, "typestr": _TYPESTR[dtype],
+                                         "data": (self.ptr, False), "version": 3, "strides": None}
+
+    def __del__(self) -> None:
+        if getattr(self, "ptr", None):
+            self._lib.srml_managed_free(self.ptr, self.nbytes, self.device.index or 0, None)
+            self.ptr = None
+
+
+def managed_empty(shape: Any, dtype: torch.dtype, device: torch.device) -> torch.Tensor:
+    """Uninitialised tensor in managed (UVM) memory: pages live where the GPU touches them and can
+    exceed HBM capacity (the reference's spark.rapids.ml.uvm.enabled)."""
+    return torch.as_tensor(_ManagedBuffer(shape, dtype, device), device=device)

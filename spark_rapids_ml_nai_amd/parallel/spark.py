@@ -174,7 +174,9 @@ def spark_worker_entry(task_ctx: Any, batches: Iterable[Any], payload: bytes) ->
     from ..core.dataframe import DataFrame
     from .context import use_context
 
-    est, fit_fn, params, float32, vector_cols, use_gpu = cloudpickle.loads(payload)
+    est, fit_fn, params, float32, vector_cols, use_gpu, *rest = cloudpickle.loads(payload)
+    if rest and rest[0]:
+        os.environ["SRML_UVM"] = "1"  # spark.rocm.ml.uvm.enabled: managed-memory ingest
     ctx = init_barrier_group(task_ctx, use_gpu)
     try:
         table = batches_to_table(batches, vector_cols)
@@ -222,7 +224,8 @@ def run_spark_fit(est: Any, sdf: Any, fit_fn: Callable, params: Dict[str, Any]) 
         sdf = sdf.repartition(nw)
     sdf, vec = _unwrap_vectors(sdf)
     use_gpu = os.environ.get("SRML_FORCE_CPU", "0") != "1" and (gpu_available() or _cluster_has_gpus(spark))
-    payload = cloudpickle.dumps((est, fit_fn, params, est._float32_inputs, vec, use_gpu))
+    uvm = str(spark.conf.get("spark.rocm.ml.uvm.enabled", "false")).lower() == "true"
+    payload = cloudpickle.dumps((est, fit_fn, params, est._float32_inputs, vec, use_gpu, uvm))
 
     def _train(it: Iterator[Any]) -> Iterator[Any]:
         from pyspark import BarrierTaskContext  # type: ignore

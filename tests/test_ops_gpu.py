@@ -426,3 +426,18 @@ def test_rf_node_stats(gpu_device, regression):
     got = ops.rf_node_stats(idx.to(gpu_device), wpos.to(gpu_device), y.to(gpu_device), bounds.to(gpu_device), S,
                             regression).cpu()
     torch.testing.assert_close(got, ref, rtol=1e-9, atol=1e-6)
+
+
+def test_uvm_managed_ingest(gpu_device, monkeypatch):
+    from spark_rapids_ml_nai_amd.ops.ingest import host_to_device, managed_empty
+
+    monkeypatch.setenv("SRML_UVM", "1")
+    X = np.random.default_rng(0).standard_normal((50000, 64)).astype(np.float32)
+    Xd = host_to_device(X, gpu_device, torch.float32)
+    assert Xd.is_cuda
+    torch.testing.assert_close(Xd.cpu(), torch.from_numpy(X))
+    s, _ = ops.col_moments(Xd)  # kernels run on managed memory
+    torch.testing.assert_close(s.cpu(), torch.from_numpy(X).double().sum(0), rtol=1e-5, atol=1e-3)
+    t = managed_empty((1000,), torch.float32, gpu_device)
+    t.fill_(2.0)
+    assert float(t.sum()) == 2000.0
