@@ -580,6 +580,50 @@ def ivf_search(Q: torch.Tensor, probes: torch.Tensor, list_off: torch.Tensor, it
     return (od + qnorm.float().view(-1, 1)).clamp_min(0), oi
 
 
+def knn_lists(X: torch.Tensor, xnorm: torch.Tensor, list_off: torch.Tensor, probes: torch.Tensor,
+              tile_q0: torch.Tensor, tile_list: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """All-points kNN over IVF lists (rows of ``X`` sorted by list, ``list_off`` nlist+1 offsets).
+
+    Every query tile (``tile_q0[i]``: first row of <= 128 rows of list ``tile_list[i]``) is
+    compared with the items of the lists ``probes[tile_list[i]]``. Returns (N x k partial
+    distances ||i||^2 - 2 q.i fp32, N x k item positions int32, ascending); rows outside the
+    given tiles are +inf / -1.
+    """
+    N, n = X.shape
+    nprobe = int(probes.shape[1])
+    ntiles = int(tile_q0.shape[0])
+    od = torch.full((N, k), float("inf"), dtype=torch.float32, device=X.device)
+    oi = torch.full((N, k), -1, dtype=torch.int32, device=X.device)
+    if ntiles == 0:
+        return od, oi
+    if tile_list.shape[0] != ntiles or list_off.shape[0] != probes.shape[0] + 1:
+        raise ValueError("knn_lists: inconsistent tile / list descriptors")
+    if not X.is_cuda or X.dtype != torch.float32 or k > KNN_KMAX:
+        lo = list_off.cpu().numpy()
+        pr = probes.cpu().numpy()
+        tq = tile_q0.cpu().numpy()
+        tl = tile_list.cpu().numpy()
+        for q0, c in zip(tq, tl):
+            q1 = min(int(q0) + 128, int(lo[c + 1]))
+            cand = [torch.arange(int(lo[l]), int(lo[l + 1]), device=X.device) for l in pr[c] if l >= 0]
+            if not cand:
+                continue
+            r = torch.cat(cand)
+            d = xnorm[r].float().view(1, -1) - 2.0 * (X[int(q0):q1].float() @ X[r].float().T)
+            kk = min(k, d.shape[1])
+            v, j = torch.topk(d, kk, dim=1, largest=False)
+            od[int(q0):q1, :kk] = v
+            oi[int(q0):q1, :kk] = r[j].int()
+        return od, oi
+    if int(list_off[-1]) != N:
+        raise ValueError("knn_lists: list offsets do not cover the %d rows" % N)
+    X = _c(X)
+    native.call("srml_knn_lists_f32", X.data_ptr(), n, X.stride(0), _c(xnorm.float()).data_ptr(),
+                _c(list_off.long()).data_ptr(), _c(probes.int()).data_ptr(), nprobe, _c(tile_q0.long()).data_ptr(),
+                _c(tile_list.int()).data_ptr(), ntiles, int(k), od.data_ptr(), oi.data_ptr(), native.stream(X.device))
+    return od, oi
+
+
 # ------------------------------------------------------------------------------------------
 # DBSCAN: eps-degree / core-core union-find over lower-triangle 128x128 tile pairs
 # ------------------------------------------------------------------------------------------

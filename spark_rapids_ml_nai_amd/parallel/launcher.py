@@ -126,6 +126,13 @@ def run_barrier_job(
             errors.append("rank %d failed:\n%s" % (rank, body))
             break
     if errors:
+        # a peer's error is often just the symptom (its collective saw the connection drop):
+        # name any rank that died first so the root cause is in the message
+        if not any("exited with code" in e for e in errors):
+            _time.sleep(0.5)
+            dead = [i for i, p in enumerate(procs) if not p.is_alive() and p.exitcode not in (0, None)]
+            if dead:
+                errors.insert(0, "rank(s) %s exited with code(s) %s" % (dead, [procs[i].exitcode for i in dead]))
         for p in procs:
             if p.is_alive():
                 p.terminate()

@@ -36,7 +36,7 @@ from .parallel.context import WorkerContext
 
 _UMAP_KEYS = ("n_neighbors", "n_components", "metric", "n_epochs", "learning_rate", "init", "min_dist", "spread",
               "set_op_mix_ratio", "local_connectivity", "repulsion_strength", "negative_sample_rate",
-              "transform_queue_size", "a", "b", "precomputed_knn", "random_state")
+              "transform_queue_size", "a", "b", "precomputed_knn", "random_state", "build_algo", "build_kwds")
 
 
 class UMAPClass(_BackendClass):
@@ -49,7 +49,8 @@ class UMAPClass(_BackendClass):
             "n_neighbors": 15, "n_components": 2, "metric": "euclidean", "n_epochs": None, "learning_rate": 1.0,
             "init": "spectral", "min_dist": 0.1, "spread": 1.0, "set_op_mix_ratio": 1.0, "local_connectivity": 1.0,
             "repulsion_strength": 1.0, "negative_sample_rate": 5, "transform_queue_size": 4.0, "a": None, "b": None,
-            "precomputed_knn": None, "random_state": None, "verbose": False,
+            "precomputed_knn": None, "random_state": None, "build_algo": "auto", "build_kwds": None,
+            "verbose": False,
         }
 
 
@@ -83,6 +84,10 @@ class _UMAPParams(_FeaturesColMixin, _BackendParams, HasFeaturesCol, HasFeatures
                          TypeConverters.identity)
     random_state = _p("random_state", "Seed of the pseudo random number generator.", TypeConverters.identity)
     sample_fraction = _p("sample_fraction", "Fraction of the dataset used for fitting.", TypeConverters.toFloat)
+    build_algo = _p("build_algo", "kNN graph construction: 'auto' (exact up to 100k rows, IVF lists beyond), "
+                    "'brute_force_knn' or 'ivf'.", TypeConverters.toString)
+    build_kwds = _p("build_kwds", "kNN graph options, e.g. {'nlist': ..., 'nprobe': ...} for build_algo='ivf'.",
+                    TypeConverters.identity)
 
     def __init__(self) -> None:
         super().__init__()
@@ -90,7 +95,7 @@ class _UMAPParams(_FeaturesColMixin, _BackendParams, HasFeaturesCol, HasFeatures
                          init="spectral", min_dist=0.1, spread=1.0, set_op_mix_ratio=1.0, local_connectivity=1.0,
                          repulsion_strength=1.0, negative_sample_rate=5, transform_queue_size=4.0, a=None, b=None,
                          precomputed_knn=None, random_state=None, sample_fraction=1.0, outputCol="embedding",
-                         featuresCol="features")
+                         featuresCol="features", build_algo="auto", build_kwds=None)
 
     def getSampleFraction(self) -> float:
         return self.getOrDefault(self.sample_fraction)
@@ -126,17 +131,17 @@ def _umap_fit_worker(ctx: WorkerContext, payload: Tuple[Any, ...]) -> Tuple[np.n
     from .models.umap import umap_fit
 
     X, y, params = payload
-    parts = ctx.comm.allgather_object((X, y)) if ctx.world_size > 1 else [(X, y)]
-    Xall = np.concatenate([p[0] for p in parts])
-    yall = None if parts[0][1] is None else np.concatenate([p[1] for p in parts])
-    emb = None
-    if ctx.rank == 0:
-        Xd = to_device(Xall, ctx.device, torch.float32)
-        yd = torch.as_tensor(yall) if yall is not None else None
-        emb = umap_fit(Xd, params, yd)
+    Xd = to_device(np.ascontiguousarray(X, dtype=np.float32), ctx.device, torch.float32)
+    yd = torch.as_tensor(np.asarray(y), device=ctx.device) if y is not None else None
     if ctx.world_size > 1:
-        emb = ctx.comm.broadcast_object(emb, 0)
-    return emb, Xall
+        # every rank holds the whole (sampled) training set: device all-gather over RCCL
+        Xd = torch.cat([p.to(ctx.device) for p in ctx.comm.allgatherv(Xd)], 0)
+        if yd is not None:
+            yd = torch.cat([p.to(ctx.device) for p in ctx.comm.allgatherv(yd)], 0)
+    emb = umap_fit(Xd, params, yd, ctx=ctx)
+    if ctx.rank != 0:  # the model is built from rank 0's result only
+        return None, None
+    return emb, Xd.cpu().numpy()
 
 
 class UMAP(UMAPClass, _Estimator, _UMAPParams):
@@ -176,11 +181,23 @@ class UMAP(UMAPClass, _Estimator, _UMAPParams):
         y = None
         if self.isDefined("labelCol") and self.getLabelCol() in df.columns:
             y = df.to_numpy(self.getLabelCol()).astype(np.int64)
-        X = self._features(df)
         params = self._umap_params()
-        # one fit task on one device, as in the reference (umap.py:840-850); under SPMD every rank
-        # contributes its rows, rank 0 fits and broadcasts the embedding
-        emb, Xall = run_worker_job(_umap_fit_worker, [(X, y, params)])[0]
+        # The reference fits on ONE device (umap.py:840-850). Here num_workers > 1 (or SPMD)
+        # fits on all ranks: replicated rows, distributed kNN graph, edge-parallel SGD.
+        from .core.base import spmd_active
+
+        nw = self.num_workers
+        if spmd_active() or nw <= 1:
+            payloads = [(self._features(df), y, params)]
+        else:
+            if df.getNumPartitions() != nw:
+                df = df.repartition(nw)
+            payloads = []
+            for p in df.partitions:
+                part = DataFrame([p])
+                yp = part.to_numpy(self.getLabelCol()).astype(np.int64) if y is not None else None
+                payloads.append((self._features(part), yp, params))
+        emb, Xall = run_worker_job(_umap_fit_worker, payloads)[0]
         model = UMAPModel(embedding_=emb, raw_data_=Xall, n_cols=int(Xall.shape[1]), dtype="float32")
         model._num_workers = self._num_workers
         model._float32_inputs = True

@@ -258,6 +258,44 @@ def test_ivf_search(gpu_device, n, nlist, nprobe, k):
     assert (gi.cpu()[fin] == ic[fin]).float().mean().item() > 0.99
 
 
+@pytest.mark.parametrize("N,n,nlist,nprobe,k", [(3000, 16, 12, 4, 15), (5000, 128, 20, 6, 10), (700, 7, 3, 3, 64),
+                                                (2000, 130, 9, 2, 5)])
+def test_knn_lists(gpu_device, N, n, nlist, nprobe, k):
+    """IVF-list all-points kNN tile kernel vs brute force over exactly the probed lists."""
+    from spark_rapids_ml_nai_amd.models.knn_graph import ivf_tiles
+
+    X = _rand(N, n, gpu_device, seed=31)
+    g = torch.Generator().manual_seed(N)
+    lab = torch.randint(0, nlist, (N,), generator=g).to(gpu_device)
+    order = torch.argsort(lab, stable=True)
+    counts = torch.bincount(lab, minlength=nlist)
+    off = torch.zeros(nlist + 1, dtype=torch.int64, device=gpu_device)
+    off[1:] = torch.cumsum(counts, 0)
+    Xs = X[order].contiguous()
+    xn = ops.row_sqnorm(Xs)
+    rows = []
+    for c in range(nlist):  # own list first, then distinct random others
+        others = [j for j in torch.randperm(nlist, generator=g).tolist() if j != c][: nprobe - 1]
+        rows.append([c] + others)
+    probes = torch.tensor(rows, dtype=torch.int32, device=gpu_device)
+    tq, tl = ivf_tiles(counts, off)
+    # a strict subset of the tiles, as one rank of a distributed build would launch
+    sel = slice(1, None) if tq.shape[0] > 1 else slice(0, None)
+    d, i = ops.knn_lists(Xs, xn, off, probes, tq[sel], tl[sel], k)
+    dc, ic = ops.knn_lists(Xs.cpu(), xn.cpu(), off.cpu(), probes.cpu(), tq[sel].cpu(), tl[sel].cpu(), k)
+    d, i = d.cpu(), i.cpu()
+    fin = torch.isfinite(dc)
+    assert torch.equal(fin, torch.isfinite(d))
+    assert torch.equal(ic[~fin], i[~fin])
+    scale = dc[fin].abs().max().item()
+    assert (d[fin] - dc[fin]).abs().max().item() / scale < 1e-5
+    assert (i[fin] == ic[fin]).float().mean().item() > 0.99
+    # untouched rows (the skipped first tile) stay +inf / -1
+    if tq.shape[0] > 1:
+        r1 = int(tq[1])
+        assert torch.isinf(d[:r1]).all() and (i[:r1] == -1).all()
+
+
 @pytest.mark.parametrize("N,n,eps", [(5, 2, 1.5), (700, 7, 2.5), (3000, 64, 9.0), (1000, 130, 14.0)])
 def test_dbscan_kernels(gpu_device, N, n, eps):
     g = torch.Generator().manual_seed(N)

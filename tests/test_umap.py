@@ -78,6 +78,48 @@ def test_umap_sample_fraction_and_cosine():
     assert out.shape == (800, 3)
 
 
+def test_ivf_knn_graph_recall():
+    """IVF-list all-points graph (UMAP build_algo='ivf') vs the exact graph: recall >= 0.9."""
+    import torch
+
+    from spark_rapids_ml_nai_amd.models.knn_graph import knn_graph_brute, knn_graph_ivf
+
+    X, _ = make_blobs(4000, 16, centers=12, cluster_std=3.0, random_state=3)
+    Xt = torch.from_numpy(X.astype(np.float32))
+    de, ie = knn_graph_brute(Xt, 10)
+    da, ia = knn_graph_ivf(Xt, 10, nlist=16, nprobe=6, seed=1)
+    assert ia.shape == (4000, 10) and (ia[:, 0] == torch.arange(4000)).float().mean() > 0.99
+    hit = np.mean([len(set(a) & set(b)) / 10.0 for a, b in zip(ia.numpy(), ie.numpy())])
+    assert hit >= 0.9
+    assert torch.all(da[:, 1:] >= da[:, :-1] - 1e-6)
+    # distances are exact for the selected neighbours
+    sel = Xt[ia.clamp_min(0)]
+    ref = ((sel - Xt.unsqueeze(1)) ** 2).sum(-1).sqrt()
+    assert torch.allclose(da, ref, atol=1e-3)
+
+
+def test_umap_ivf_graph_trustworthiness():
+    X, _ = _digits()
+    df = DataFrame.from_numpy(X)
+    model = UMAP(random_state=1, build_algo="ivf", build_kwds={"nlist": 8, "nprobe": 4}).fit(df)
+    assert model.getOrDefault("build_algo") == "ivf"
+    assert trustworthiness(X, model.embedding_, n_neighbors=15) > 0.9
+
+
+@pytest.mark.dist
+def test_umap_two_ranks(monkeypatch):
+    """Distributed fit (replicated rows, tile-parallel graph, edge-parallel SGD with a delta
+    all-reduce per epoch) on 2 gloo ranks reaches the single-rank quality."""
+    monkeypatch.setenv("SRML_FORCE_CPU", "1")
+    X, _ = _digits(900)
+    df = DataFrame.from_numpy(X, num_partitions=2)
+    for algo in ("brute_force_knn", "ivf"):
+        m2 = UMAP(random_state=5, num_workers=2, n_epochs=200, build_algo=algo,
+                  build_kwds={"nlist": 8, "nprobe": 4}).fit(df)
+        assert m2.embedding_.shape == (900, 2) and m2.raw_data_.shape == X.shape
+        assert trustworthiness(X, m2.embedding_, n_neighbors=15) > 0.88
+
+
 def test_umap_multi_column_input():
     X, _ = make_blobs(300, 3, centers=3, random_state=5)
     import pandas as pd

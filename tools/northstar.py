@@ -1,0 +1,164 @@
+"""North-star configurations of BASELINE.json, measured through the public estimator API.
+
+    python tools/northstar.py [--configs kmeans,logreg,rf,umap,pca] [--scale 1.0] [--out file.jsonl]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/northstar.py ...
+
+Configs (BASELINE.json "configs"): PCA k=3 on 10k x 128; KMeans k=20 on 100M x 64; binary L2
+LogisticRegression on 200M x 256; RandomForestClassifier 100 trees depth 16 on 50M x 64
+(data-parallel histogram all-reduce); UMAP n_neighbors=15 d=2 on 20M x 128 (IVF kNN graph,
+edge-parallel SGD). ``--scale`` multiplies every row count (a 1-GPU box cannot hold the
+200M x 256 shard in pinned host memory next to its device copy). Rows are split over the
+ranks (strong scaling); synthetic data generated on the device of each rank, handed to the
+estimator as pinned host Arrow-backed DataFrames, so each timed fit includes H2D ingest.
+One JSON line per config on rank 0 (fit seconds = max over ranks).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+import traceback
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+CONFIGS = {
+    # name: (rows, cols, generator)
+    "pca": (10_000, 128, "low_rank"),
+    "kmeans": (100_000_000, 64, "blobs"),
+    "logreg": (200_000_000, 256, "classification"),
+    "rf": (50_000_000, 64, "classification"),
+    "umap": (20_000_000, 128, "blobs"),
+}
+
+
+def _estimator(name: str, world: int):
+    if name == "pca":
+        from spark_rapids_ml_nai_amd.feature import PCA
+
+        return PCA(k=3, inputCol="features")
+    if name == "kmeans":
+        from spark_rapids_ml_nai_amd.clustering import KMeans
+
+        return KMeans(k=20, maxIter=20, tol=1e-4, seed=1, featuresCol="features")
+    if name == "logreg":
+        from spark_rapids_ml_nai_amd.classification import LogisticRegression
+
+        return LogisticRegression(regParam=1e-5, maxIter=100, tol=1e-6, standardization=False,
+                                  featuresCol="features", labelCol="label")
+    if name == "rf":
+        from spark_rapids_ml_nai_amd.classification import RandomForestClassifier
+
+        return RandomForestClassifier(numTrees=100, maxDepth=16, maxBins=128, seed=1, featuresCol="features",
+                                      labelCol="label", split_mode="data_parallel" if world > 1 else "ensemble")
+    if name == "umap":
+        from spark_rapids_ml_nai_amd.umap import UMAP
+
+        return UMAP(n_neighbors=15, n_components=2, random_state=1, featuresCol="features")
+    raise ValueError(name)
+
+
+def _shard(gen: str, m: int, n: int, device, rank: int):
+    from spark_rapids_ml_nai_amd.bench import datagen
+
+    seed = 7000 + rank
+    y = None
+    if gen == "low_rank":
+        X = datagen.low_rank_matrix(m, n, device, seed=seed)
+    elif gen == "blobs":
+        X, _ = datagen.blobs(m, n, device, seed=seed, centers=20)
+    elif gen == "classification":
+        X, y = datagen.classification(m, n, device, seed=seed, n_informative=n // 2, n_redundant=n // 4)
+    else:
+        raise ValueError(gen)
+    Xh = datagen.to_pinned_numpy(X)
+    yh = y.cpu().numpy().astype(np.float64) if y is not None else None
+    del X, y
+    if device.type == "cuda":
+        torch.cuda.empty_cache()
+    return Xh, yh
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="pca,kmeans,logreg,rf,umap")
+    ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--warmup", type=int, default=0)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    use_gpu = torch.cuda.is_available()
+    device = torch.device("cuda", local_rank) if use_gpu else torch.device("cpu")
+    if use_gpu:
+        torch.cuda.set_device(device)
+    if world > 1:
+        from datetime import timedelta
+
+        dist.init_process_group("nccl" if use_gpu else "gloo", timeout=timedelta(minutes=30),
+                                **({"device_id": device} if use_gpu else {}))
+    from spark_rapids_ml_nai_amd import DataFrame
+
+    for name in a.configs.split(","):
+        rows, cols, gen = CONFIGS[name]
+        rows = max(1000, int(rows * a.scale)) if name != "pca" else rows
+        b = np.linspace(0, rows, world + 1).astype(np.int64)
+        m_local = int(b[rank + 1] - b[rank])
+        rec = {"config": name, "rows": rows, "cols": cols, "n_gpus": world, "scale": a.scale}
+        try:
+            t0 = time.perf_counter()
+            Xh, yh = _shard(gen, m_local, cols, device, rank)
+            rec["gen_s"] = round(time.perf_counter() - t0, 3)
+            df = DataFrame.from_numpy(Xh, yh)
+            est = _estimator(name, world)
+            est.num_workers = world
+            for _ in range(a.warmup):
+                est.fit(df)
+            if use_gpu:
+                torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            t0 = time.perf_counter()
+            model = est.fit(df)
+            if use_gpu:
+                torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            if world > 1:
+                t = torch.tensor([dt], dtype=torch.float64, device=device)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                dt = float(t.item())
+            rec["fit_s"] = round(dt, 3)
+            rec["rows_per_s"] = round(rows / dt, 1)
+            if name == "kmeans":
+                rec["iters"] = int(getattr(model, "num_iters", -1) or -1)
+            if name == "logreg":
+                rec["iters"] = int(getattr(model, "num_iters", -1))
+            if name == "rf":
+                rec["total_nodes"] = int(model.totalNumNodes)
+            if name == "umap":
+                emb = np.asarray(model.embedding_)
+                rec["finite"] = bool(np.isfinite(emb).all())
+            del model, df, Xh, yh
+        except Exception as e:  # noqa: BLE001
+            rec["error"] = repr(e)[:500]
+            if rank == 0:
+                traceback.print_exc()
+        if use_gpu:
+            torch.cuda.empty_cache()
+        if rank == 0:
+            line = json.dumps(rec)
+            print(line, flush=True)
+            if a.out:
+                with open(a.out, "a") as f:
+                    f.write(line + "\n")
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
