@@ -127,6 +127,24 @@ def init_kmeans_parallel(X: torch.Tensor, xnorm: torch.Tensor, desc: PartitionDe
     return best
 
 
+def _use_split(X: torch.Tensor, k: int) -> bool:
+    """Split-bf16 distance GEMM (fp32-exact, 6 bf16 MFMA products = 6/16 of the fp32 MFMA cost)
+    when the Lloyd step is GEMM-bound (k and n large) and the 1.5x-of-X planes fit in HBM.
+    ``SRML_KMEANS_SPLIT=0/1`` forces it off/on."""
+    import os
+    env = os.environ.get("SRML_KMEANS_SPLIT")
+    if env is not None:
+        return env == "1"
+    if not X.is_cuda or X.dtype != torch.float32:
+        return False
+    m, n = X.shape
+    if k < 128 or n < 128:
+        return False
+    need = 3 * 2 * ((m + 127) // 128 * 128) * ((n + 15) // 16 * 16)
+    free, _ = torch.cuda.mem_get_info(X.device)
+    return need < 0.6 * free
+
+
 def kmeans_fit(X: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext, k: int, max_iter: int, tol: float,
                seed: int, init: str = "scalable-k-means++", oversampling: float = 2.0, init_steps: int = 2,
                timer: Any = None) -> Dict[str, Any]:
@@ -140,11 +158,15 @@ def kmeans_fit(X: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext, k
         raise ValueError("Unsupported init mode %s" % init)
     C = C.double()
     tol2 = float(tol) ** 2
+    XP = ops.split_bf16x3(X) if _use_split(X, k) else None
     n_iter = 0
     inertia = 0.0
     for it in range(max(0, max_iter)):
         n_iter = it + 1
-        labels, d2 = ops.nearest_centroid(X, C.float(), xnorm)
+        if XP is not None:
+            labels, d2 = ops.nearest_centroid_split(XP, X.shape[0], C.float(), xnorm)
+        else:
+            labels, d2 = ops.nearest_centroid(X, C.float(), xnorm)
         sums, counts = ops.cluster_sums(X, labels, k)
         buf = torch.cat([sums.view(-1), counts.double(), d2.double().sum().view(1)])
         ctx.comm.allreduce(buf)
@@ -156,6 +178,7 @@ def kmeans_fit(X: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext, k
         C = newC
         if shift <= tol2:
             break
+    del XP
     return {
         "cluster_centers_": C.cpu().numpy().tolist(),
         "n_cols": int(n),

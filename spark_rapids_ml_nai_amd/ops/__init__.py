@@ -240,6 +240,54 @@ def nearest_centroid(X: torch.Tensor, C: torch.Tensor, xnorm: Optional[torch.Ten
     return labels, dist
 
 
+def split_bf16x3(X: torch.Tensor, row_multiple: int = 128) -> torch.Tensor:
+    """Exact three-way bf16 split of a fp32 matrix: planes P[3][rows_pad][kp] (bf16) with
+    X = P[0] + P[1] + P[2] (each plane the round-to-nearest bf16 of the remaining residual),
+    rows padded to ``row_multiple`` and columns to a multiple of 16 with zeros."""
+    m, n = X.shape
+    kp = (n + 15) // 16 * 16
+    rows_pad = max(row_multiple, (m + row_multiple - 1) // row_multiple * row_multiple)
+    if not X.is_cuda or X.dtype != torch.float32:
+        P = torch.zeros((3, rows_pad, kp), dtype=torch.bfloat16, device=X.device)
+        r = X.float()
+        for p in range(3):
+            P[p, :m, :n] = r.to(torch.bfloat16)
+            r = r - P[p, :m, :n].float()
+        return P
+    X = X if X.stride(1) == 1 else X.contiguous()
+    P = torch.empty((3, rows_pad, kp), dtype=torch.bfloat16, device=X.device)
+    native.call("srml_split_bf16x3", X.data_ptr(), m, n, X.stride(0), kp, rows_pad, P.data_ptr(),
+                native.stream(X.device))
+    return P
+
+
+def nearest_centroid_split(XP: torch.Tensor, m: int, C: torch.Tensor, xnorm: torch.Tensor,
+                           cnorm: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """``nearest_centroid`` on pre-split X planes (``split_bf16x3``): the distance GEMM runs on
+    the bf16 matrix cores as six cross products of the planes (fp32-accurate; see splitmm.hip)."""
+    k = C.shape[0]
+    Cf = C.float()
+    if cnorm is None:
+        cnorm = (Cf * Cf).sum(1)
+    CP = split_bf16x3(_c(Cf).to(XP.device), 256 if k > 256 else 128)
+    if not XP.is_cuda:
+        Xh, Xm, Xl = (XP[p, :m].float() for p in range(3))
+        Ch, Cm, Cl = (CP[p, :k].float() for p in range(3))
+        dot = Xl @ Ch.T + Xm @ Cm.T + Xh @ Cl.T + Xm @ Ch.T + Xh @ Cm.T + Xh @ Ch.T
+        v, i = (cnorm.float().view(1, -1) - 2.0 * dot).min(1)
+        return i.int(), (v + xnorm.float()).clamp_min(0)
+    cn = _c(cnorm.to(torch.float32))
+    best = torch.full((m,), -1, dtype=torch.int64, device=XP.device)
+    st = native.stream(XP.device)
+    native.call("srml_nearest_centroid_split", XP.data_ptr(), m, XP.shape[1], XP.shape[2], CP.data_ptr(), k,
+                CP.shape[1], cn.data_ptr(), best.data_ptr(), st)
+    labels = torch.empty(m, dtype=torch.int32, device=XP.device)
+    dist = torch.empty(m, dtype=torch.float32, device=XP.device)
+    native.call("srml_nn_finalize", best.data_ptr(), m, _c(xnorm.float()).data_ptr(), labels.data_ptr(),
+                dist.data_ptr(), st)
+    return labels, dist
+
+
 def cluster_sums(X: torch.Tensor, labels: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
     """(sums fp64 [k, n], counts int64 [k]) of rows grouped by label."""
     m, n = X.shape
@@ -256,12 +304,15 @@ def cluster_sums(X: torch.Tensor, labels: torch.Tensor, k: int) -> Tuple[torch.T
         sums = torch.zeros((k, n), dtype=torch.float64, device=X.device)
         native.call("srml_kmeans_accumulate_f32", X.data_ptr(), m, n, X.stride(0), lab.data_ptr(), k, sums.data_ptr(),
                     None, counts.data_ptr(), st)
-    else:
-        s32 = torch.zeros((k, n), dtype=torch.float32, device=X.device)
-        native.call("srml_kmeans_accumulate_f32", X.data_ptr(), m, n, X.stride(0), lab.data_ptr(), k, None,
-                    s32.data_ptr(), counts.data_ptr(), st)
-        sums = s32.double()
-    return sums, counts.long()
+        return sums, counts.long()
+    # large k*n: visit rows in label-sorted order (segment sums, ~(m/256 + k) * n fp64 atomics)
+    slab, perm = torch.sort(lab)
+    slab = slab.to(torch.int32)
+    perm = perm.to(torch.int32)
+    sums = torch.zeros((k, n), dtype=torch.float64, device=X.device)
+    native.call("srml_kmeans_accumulate_sorted_f32", X.data_ptr(), m, n, X.stride(0), perm.data_ptr(),
+                slab.data_ptr(), sums.data_ptr(), st)
+    return sums, torch.bincount(lab, minlength=k).long()
 
 
 # ------------------------------------------------------------------------------------------

@@ -177,6 +177,73 @@ __global__ __launch_bounds__(256) void accumulate_global_kernel(const float* __r
     for (int d = lane; d < n; d += 64) atomicAdd(&dst[d], row[d]);
   }
 }
+// Sorted-segment cluster sums: rows visited in label-sorted order (perm / slab from a device
+// sort), so a chunk of RPB consecutive rows spans few clusters. Each thread owns VW consecutive
+// columns and accumulates in fp32 registers while the (block-uniform) label stays the same; at a
+// label change or the chunk end the partial goes out as fp64 atomics. Atomics per iteration:
+// ~(m / RPB + k) * n instead of the m * n of per-row scattering (accumulate_global_kernel).
+template <int VW>
+__global__ __launch_bounds__(256) void accumulate_sorted_kernel(const float* __restrict__ X, long m, int n, long ld,
+                                                                const int* __restrict__ perm,
+                                                                const int* __restrict__ slab,
+                                                                double* __restrict__ sums, int rpb) {
+  __shared__ int s_row[256];
+  __shared__ int s_lab[256];
+  const long r0 = (long)blockIdx.x * rpb;
+  const int cnt = (int)min((long)rpb, m - r0);
+  for (int i = threadIdx.x; i < cnt; i += 256) {
+    s_row[i] = perm[r0 + i];
+    s_lab[i] = slab[r0 + i];
+  }
+  __syncthreads();
+  const int c = (blockIdx.y * 256 + threadIdx.x) * VW;
+  if (c >= n) return;
+  float acc[VW];
+#pragma unroll
+  for (int j = 0; j < VW; ++j) acc[j] = 0.f;
+  int cur = s_lab[0];
+  auto flush = [&](int lab) {
+    double* dst = sums + (long)lab * n + c;
+#pragma unroll
+    for (int j = 0; j < VW; ++j)
+      if (VW == 1 || c + j < n) atomicAdd(dst + j, (double)acc[j]);
+  };
+  constexpr int U = 8;
+  for (int i0 = 0; i0 < cnt; i0 += U) {
+    float v[U][VW];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u;
+      if (i < cnt) {
+        const float* row = X + (long)s_row[i] * ld + c;
+        if constexpr (VW == 4) {
+          const float4 q = *reinterpret_cast<const float4*>(row);
+          v[u][0] = q.x; v[u][1] = q.y; v[u][2] = q.z; v[u][3] = q.w;
+        } else {
+#pragma unroll
+          for (int j = 0; j < VW; ++j) v[u][j] = row[j];
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u;
+      if (i < cnt) {
+        const int l = s_lab[i];
+        if (l != cur) {
+          flush(cur);
+#pragma unroll
+          for (int j = 0; j < VW; ++j) acc[j] = 0.f;
+          cur = l;
+        }
+#pragma unroll
+        for (int j = 0; j < VW; ++j) acc[j] += v[u][j];
+      }
+    }
+  }
+  flush(cur);
+}
+
 // ------------------------------------------------------------------------------------------
 // Exact k-nearest-neighbours: fused MFMA distance tiles + per-query top-k in LDS.
 // Block = 128 queries x one slice of the item range; the query tile's top-k list lives in LDS
@@ -477,6 +544,25 @@ SRML_API int srml_kmeans_accumulate_f32(const float* X, long m, int n, long ld, 
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(accumulate_global_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, X, m, n, ld, labels,
                        sums_f32, counts);
+  }
+  return srml_status();
+}
+
+// sums (k*n fp64, zeroed) += rows of X grouped by label, rows visited in label-sorted order.
+SRML_API int srml_kmeans_accumulate_sorted_f32(const float* X, long m, int n, long ld, const int* perm,
+                                               const int* sorted_labels, double* sums, hipStream_t stream) {
+  if (m <= 0) return 0;
+  const int rpb = 256;
+  const bool vec = ((ld & 3) == 0) && ((n & 3) == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
+  const long gx = (m + rpb - 1) / rpb;
+  if (vec) {
+    dim3 grid((unsigned)gx, (unsigned)((n / 4 + 255) / 256));
+    hipLaunchKernelGGL(accumulate_sorted_kernel<4>, grid, dim3(256), 0, stream, X, m, n, ld, perm, sorted_labels,
+                       sums, rpb);
+  } else {
+    dim3 grid((unsigned)gx, (unsigned)((n + 255) / 256));
+    hipLaunchKernelGGL(accumulate_sorted_kernel<1>, grid, dim3(256), 0, stream, X, m, n, ld, perm, sorted_labels,
+                       sums, rpb);
   }
   return srml_status();
 }

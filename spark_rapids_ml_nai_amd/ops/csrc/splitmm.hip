@@ -1,0 +1,253 @@
+// Split-bf16 ("bf16x6") fp32-exact distance GEMM for the large-k nearest-centroid search.
+//
+// gfx950 has no xf32 MFMA: fp32-input MFMA (`v_mfma_f32_32x32x2_f32`) runs at 1/16 of the bf16
+// rate (64 vs 1024 FLOP/clk/SIMD). The KMeans distance GEMM (m x n . n x k, e.g. the reference
+// headline 1M x 3000 x 1000 per Lloyd iteration, reference cuML KMeansMG / RAFT fusedL2NN) is
+// therefore re-expressed on the bf16 matrix cores without giving up fp32 accuracy:
+//
+//   x = x_h + x_m + x_l   (three bf16 pieces, each the round-to-nearest bf16 of the remaining
+//                          fp32 residual; 3 x 8 significant bits = the 24 of fp32, so the split
+//                          is exact for normal numbers)
+//   x.c ~= h.h + h.m + m.h + h.l + m.m + l.h     (every product of relative weight >= 2^-16)
+//
+// The dropped products (m.l, l.m, l.l) are <= 2^-24 relative, i.e. below fp32 rounding, and
+// each bf16 x bf16 product is exact in the fp32 MFMA accumulator: the result has the accuracy
+// of an fp32 FMA dot product at 6/16 of the fp32 MFMA cost.
+//
+//  * srml_split_bf16x3: X (m x n fp32, ld) -> planes P[3][rows_pad][kp] bf16 (kp = n rounded up
+//    to 16, zero padded; rows >= m zero). One pass, 16-B stores.
+//  * srml_nearest_centroid_split: packed (dist, index) arg-min of ||c||^2 - 2 x.c over the
+//    centroids, the same 64-bit atomicMin contract as srml_nearest_centroid_f32 (kmeans.hip).
+//    Block tile 128 rows x 128 centroids, 4 waves as 2 x 2, each wave 2 x 2 tiles of
+//    `v_mfma_f32_32x32x16_bf16`; per 16-wide k step the block stages 6 plane tiles (X and C,
+//    h/m/l) in LDS (rows padded to 48 B: the 16-B fragment reads of 16 consecutive lanes hit 16
+//    distinct 4-bank groups), double-buffered with register prefetch so the next k step's
+//    global loads are in flight under the current 24 MFMAs per wave. Grid is 1-D, centroid tile
+//    fastest and XCD-remapped so the blocks sharing one X row tile run on one XCD's L2.
+#include "common.h"
+
+#include "tile.h"
+
+namespace {
+using srml_tile::orderable;
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned uintx4 __attribute__((ext_vector_type(4)));
+typedef unsigned uintx2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ unsigned bf16_rn(float f) {  // round-to-nearest-even (finite inputs)
+  unsigned u = __float_as_uint(f);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return u >> 16;
+}
+__device__ __forceinline__ float bf16_f(unsigned b) { return __uint_as_float(b << 16); }
+
+// 4 consecutive elements per thread -> three 8-byte plane stores
+__global__ __launch_bounds__(256) void split_kernel(const float* __restrict__ X, long m, int n, long ld, int kp,
+                                                    long rows_pad, unsigned short* __restrict__ P) {
+  const int q4 = kp >> 2;
+  const long total = rows_pad * q4;
+  const long plane = rows_pad * (long)kp;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long r = i / q4;
+    const int c = (int)(i - r * q4) * 4;
+    unsigned h[4], md[4], lo[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float x = (r < m && c + j < n) ? X[r * ld + c + j] : 0.f;
+      h[j] = bf16_rn(x);
+      const float r1 = x - bf16_f(h[j]);
+      md[j] = bf16_rn(r1);
+      lo[j] = bf16_rn(r1 - bf16_f(md[j]));
+    }
+    const long o = r * kp + c;
+    *reinterpret_cast<uintx2*>(P + o) = uintx2{h[0] | (h[1] << 16), h[2] | (h[3] << 16)};
+    *reinterpret_cast<uintx2*>(P + plane + o) = uintx2{md[0] | (md[1] << 16), md[2] | (md[3] << 16)};
+    *reinterpret_cast<uintx2*>(P + 2 * plane + o) = uintx2{lo[0] | (lo[1] << 16), lo[2] | (lo[3] << 16)};
+  }
+}
+
+constexpr int SBK = 16;
+constexpr int ROWB = 24;  // padded LDS row: 16 bf16 + 8 pad = 48 B
+
+// BM x BN block tile, WM x WN waves, each wave (BM/WM) x (BN/WN) = TM x TN tiles of 32x32.
+// Staging: thread t owns row (t >> 1), 16-byte half (t & 1) of every plane tile, so
+// BM == BN == 2 * threads (both configs below).
+template <int BM, int BN, int WM, int WN>
+struct SplitCfg {
+  static constexpr int NT = WM * WN * 64;
+  static constexpr int TM = BM / WM / 32;
+  static constexpr int TN = BN / WN / 32;
+  static_assert(BM == NT / 2 && BN == NT / 2, "staging assumes one A row and one B row per thread pair");
+};
+
+template <int BM, int BN>
+struct SplitStage {
+  unsigned short A[3][BM][ROWB];
+  unsigned short B[3][BN][ROWB];
+};
+
+template <int BM, int BN, int WM, int WN, int MINB>
+__global__ __launch_bounds__(WM * WN * 64, MINB) void nearest_centroid_split_kernel(
+    const unsigned short* __restrict__ XP, long m, long xrows, int kp, const unsigned short* __restrict__ CP, int k,
+    long crows, const float* __restrict__ cnorm, unsigned long long* __restrict__ best, int n_ctiles) {
+  using Cfg = SplitCfg<BM, BN, WM, WN>;
+  constexpr int TM = Cfg::TM, TN = Cfg::TN;
+  __shared__ SplitStage<BM, BN> st[2];
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const long rtile = bid / n_ctiles;
+  const int ctile = bid % n_ctiles;
+  const long row0 = rtile * BM;
+  const int col0 = ctile * BN;
+  const int t = threadIdx.x;
+  const int lane = t & 63, wid = t >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int li = lane & 31, lk = lane >> 5;
+
+  const int sr = t >> 1, sh = (t & 1) * 8;
+  long xr = row0 + sr;
+  if (xr >= xrows) xr = xrows - 1;  // clamp: those rows are never reported
+  const long xplane = xrows * (long)kp, cplane = crows * (long)kp;
+  const unsigned short* xa = XP + xr * kp + sh;
+  const unsigned short* ca = CP + (long)(col0 + sr) * kp + sh;  // crows is a multiple of BN
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  uintx4 ra[3], rb[3];
+#pragma unroll
+  for (int p = 0; p < 3; ++p) {
+    ra[p] = *reinterpret_cast<const uintx4*>(xa + p * xplane);
+    rb[p] = *reinterpret_cast<const uintx4*>(ca + p * cplane);
+  }
+#pragma unroll
+  for (int p = 0; p < 3; ++p) {
+    *reinterpret_cast<uintx4*>(&st[0].A[p][sr][sh]) = ra[p];
+    *reinterpret_cast<uintx4*>(&st[0].B[p][sr][sh]) = rb[p];
+  }
+  __syncthreads();
+  const int nk = kp / SBK;
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    const bool more = kt + 1 < nk;
+    if (more) {
+      const long ko = (long)(kt + 1) * SBK;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        ra[p] = *reinterpret_cast<const uintx4*>(xa + p * xplane + ko);
+        rb[p] = *reinterpret_cast<const uintx4*>(ca + p * cplane + ko);
+      }
+    }
+    bf16x8 fb[3][TN];
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int nt = 0; nt < TN; ++nt)
+        fb[p][nt] = *reinterpret_cast<const bf16x8*>(&st[cur].B[p][wn * (BN / WN) + nt * 32 + li][8 * lk]);
+#pragma unroll
+    for (int mt = 0; mt < TM; ++mt) {
+      bf16x8 fa[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        fa[p] = *reinterpret_cast<const bf16x8*>(&st[cur].A[p][wm * (BM / WM) + mt * 32 + li][8 * lk]);
+      // smallest terms first: l.h, m.m, h.l, m.h, h.m, h.h
+#pragma unroll
+      for (int nt = 0; nt < TN; ++nt) {
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[0][nt], acc[mt][nt], 0, 0, 0);
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1][nt], acc[mt][nt], 0, 0, 0);
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[2][nt], acc[mt][nt], 0, 0, 0);
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[0][nt], acc[mt][nt], 0, 0, 0);
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[1][nt], acc[mt][nt], 0, 0, 0);
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0][nt], acc[mt][nt], 0, 0, 0);
+      }
+    }
+    if (more) {
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        *reinterpret_cast<uintx4*>(&st[cur ^ 1].A[p][sr][sh]) = ra[p];
+        *reinterpret_cast<uintx4*>(&st[cur ^ 1].B[p][sr][sh]) = rb[p];
+      }
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // epilogue (C/D layout of the 32x32 MFMA: col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5))
+  float cn[TN];
+  int cj[TN];
+#pragma unroll
+  for (int nt = 0; nt < TN; ++nt) {
+    cj[nt] = col0 + wn * (BN / WN) + nt * 32 + li;
+    cn[nt] = (cj[nt] < k) ? cnorm[cj[nt]] : 0.f;
+  }
+#pragma unroll
+  for (int mt = 0; mt < TM; ++mt) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float bv = __builtin_huge_valf();
+      int bi = 0x7fffffff;
+#pragma unroll
+      for (int nt = 0; nt < TN; ++nt) {
+        if (cj[nt] < k) {
+          const float d = fmaf(-2.f, acc[mt][nt][r], cn[nt]);
+          if (d < bv) { bv = d; bi = cj[nt]; }
+        }
+      }
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) {
+        const float ov = __shfl_xor(bv, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ov < bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+      }
+      if (li == 0 && bi != 0x7fffffff) {
+        const long row = row0 + wm * (BM / WM) + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        if (row < m) {
+          const unsigned long long key = ((unsigned long long)orderable(bv) << 32) | (unsigned)bi;
+          atomicMin(&best[row], key);
+        }
+      }
+    }
+  }
+}
+}  // namespace
+
+// P: [3][rows_pad][kp] bf16 (uint16), kp % 16 == 0, kp >= n, rows_pad >= m
+SRML_API int srml_split_bf16x3(const float* X, long m, int n, long ld, int kp, long rows_pad, unsigned short* P,
+                               hipStream_t stream) {
+  if (rows_pad <= 0) return 0;
+  if ((kp & 15) || kp < n || rows_pad < m) return -2;
+  if ((reinterpret_cast<uintptr_t>(P) & 15) != 0) return -5;
+  long total = rows_pad * (long)(kp / 4);
+  long blocks = (total + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(split_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, X, m, n, ld, kp, rows_pad, P);
+  return srml_status();
+}
+
+// XP: planes of X ([3][xrows][kp]), CP: planes of the centroids ([3][crows][kp], crows % 128 == 0
+// (% 256 when k > 256), crows >= k). best: m packed keys, initialised to ~0 by the caller.
+SRML_API int srml_nearest_centroid_split(const unsigned short* XP, long m, long xrows, int kp,
+                                         const unsigned short* CP, int k, long crows, const float* cnorm,
+                                         unsigned long long* best, hipStream_t stream) {
+  if (m <= 0 || k <= 0) return 0;
+  const bool big = k > 256;  // 256 x 256 tiles: 4x fewer L2 bytes per MFMA than 128 x 128
+  const int T = big ? 256 : 128;
+  if ((kp & 15) || xrows < m || crows < k || (crows % T) != 0) return -2;
+  if ((reinterpret_cast<uintptr_t>(XP) & 15) || (reinterpret_cast<uintptr_t>(CP) & 15)) return -5;
+  const long rt = (m + T - 1) / T;
+  const int ct = (k + T - 1) / T;
+  const long nb = rt * ct;
+  if (nb > 0x7fffffffL) return -3;
+  if (big)
+    hipLaunchKernelGGL((nearest_centroid_split_kernel<256, 256, 2, 4, 1>), dim3((unsigned)nb), dim3(512), 0, stream,
+                       XP, m, xrows, kp, CP, k, crows, cnorm, best, ct);
+  else
+    hipLaunchKernelGGL((nearest_centroid_split_kernel<128, 128, 2, 2, 2>), dim3((unsigned)nb), dim3(256), 0, stream,
+                       XP, m, xrows, kp, CP, k, crows, cnorm, best, ct);
+  return srml_status();
+}

@@ -40,7 +40,10 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_logreg_binary_f32": (_P, _L, _I, _L, _P, _P, _D, _P, _P),
     "srml_nearest_centroid_f32": (_P, _L, _I, _L, _P, _I, _L, _P, _P, _P),
     "srml_nn_finalize": (_P, _L, _P, _P, _P, _P),
+    "srml_split_bf16x3": (_P, _L, _I, _L, _I, _L, _P, _P),
+    "srml_nearest_centroid_split": (_P, _L, _L, _I, _P, _I, _L, _P, _P, _P),
     "srml_kmeans_accumulate_f32": (_P, _L, _I, _L, _P, _I, _P, _P, _P, _P),
+    "srml_kmeans_accumulate_sorted_f32": (_P, _L, _I, _L, _P, _P, _P, _P),
     "srml_knn_f32": (_P, _L, _I, _L, _P, _L, _L, _P, _I, _I, _P, _P, ctypes.c_longlong, _P),
     "srml_ivf_search_f32": (_P, _L, _I, _L, _P, _I, _P, _P, _L, _P, _P, _I, _P, _P, _P),
     "srml_knn_lists_f32": (_P, _I, _L, _P, _P, _P, _I, _P, _P, _I, _I, _P, _P, _P),

@@ -1,0 +1,22 @@
+"""CPU-side checks of the device-op reference math (the same formulas the HIP kernels implement)."""
+import torch
+
+from spark_rapids_ml_nai_amd import ops
+
+
+def test_split_bf16x3_exact_and_distance():
+    g = torch.Generator().manual_seed(0)
+    m, n, k = 300, 70, 40
+    C = torch.randn(k, n, generator=g) * 3
+    X = (C[torch.randint(0, k, (m,), generator=g)] + 0.3 * torch.randn(m, n, generator=g)).float()
+    P = ops.split_bf16x3(X)
+    assert P.dtype == torch.bfloat16 and P.shape == (3, 384, 80)
+    # three bf16 pieces carry all 24 significand bits of fp32
+    assert torch.equal(P.float().sum(0)[:m, :n], X)
+    xn = (X * X).sum(1)
+    lab_s, d_s = ops.nearest_centroid_split(P, m, C, xn)
+    lab, d = ops.nearest_centroid(X, C, xn)
+    D = torch.cdist(X.double(), C.double()) ** 2
+    ref_d = D.min(1).values
+    assert torch.all(D[torch.arange(m), lab_s.long()] <= ref_d + 1e-4 * (1 + ref_d))
+    torch.testing.assert_close(d_s.double(), ref_d, rtol=1e-4, atol=1e-3)

@@ -125,7 +125,27 @@ def test_nearest_centroid(gpu_device, m, n, k):
     assert torch.all((dist.double().cpu() - ref_d).abs() <= 1e-5 * scale + 1e-3)
 
 
-@pytest.mark.parametrize("m,n,k", [(5000, 16, 20), (20000, 3000, 50), (3000, 64, 200)])
+@pytest.mark.parametrize("m,n,k", [(1000, 16, 20), (2000, 300, 130), (1024, 3000, 257), (777, 33, 1), (4099, 130, 1000)])
+def test_nearest_centroid_split(gpu_device, m, n, k):
+    """Split-bf16 (6-product) MFMA distance GEMM vs the fp64 distance matrix."""
+    g = torch.Generator().manual_seed(5)
+    C = torch.randn(k, n, generator=g) * 3
+    lab = torch.randint(0, k, (m,), generator=g)
+    X = (C[lab] + 0.5 * torch.randn(m, n, generator=g)).float()
+    Xd = X.to(gpu_device)
+    P = ops.split_bf16x3(Xd)
+    assert P.shape[1] % 128 == 0 and P.shape[2] % 16 == 0
+    torch.testing.assert_close(P.float().sum(0)[:m, :n].cpu(), X, rtol=0, atol=0)
+    labels, dist = ops.nearest_centroid_split(P, m, C.float().to(gpu_device), ops.row_sqnorm(Xd))
+    D = torch.cdist(X.double(), C.double()) ** 2
+    ref_d, _ = D.min(1)
+    got = D[torch.arange(m), labels.long().cpu()]
+    assert torch.all(got <= ref_d + 1e-3 * (1 + ref_d))
+    scale = (X.double() ** 2).sum(1) + (C.double() ** 2).sum(1).max()
+    assert torch.all((dist.double().cpu() - ref_d).abs() <= 1e-5 * scale + 1e-3)
+
+
+@pytest.mark.parametrize("m,n,k", [(5000, 16, 20), (20000, 3000, 50), (3000, 64, 200), (5000, 301, 300), (70000, 1024, 1000)])
 def test_cluster_sums(gpu_device, m, n, k):
     X = _rand(m, n, gpu_device, seed=15)
     labels = torch.randint(0, k, (m,), generator=torch.Generator().manual_seed(4)).int()

@@ -67,6 +67,16 @@ def main():
         xn = ops.row_sqnorm(X)
         t = timeit(lambda: ops.nearest_centroid(X, C, xn), 3)
         res["nearest_centroid"] = {"ms": t, "TFLOP/s": 2 * a.m * a.k * a.n / t / 1e9}
+    if want("nearest_split"):
+        C = torch.randn(a.k, a.n, device=dev, generator=g)
+        xn = ops.row_sqnorm(X)
+        t0 = timeit(lambda: ops.split_bf16x3(X), 2)
+        P = ops.split_bf16x3(X)
+        t = timeit(lambda: ops.nearest_centroid_split(P, a.m, C, xn), 3)
+        res["nearest_centroid_split"] = {"ms": t, "split_X_ms": t0,
+                                         "TFLOP/s(fp32-equiv)": 2 * a.m * a.k * a.n / t / 1e9,
+                                         "TFLOP/s(bf16 issued)": 12 * a.m * a.k * a.n / t / 1e9}
+        del P
     if want("sums"):
         lab = torch.randint(0, a.k, (a.m,), device=dev, dtype=torch.int32)
         t = timeit(lambda: ops.cluster_sums(X, lab, a.k), 3)
