@@ -311,18 +311,138 @@ __global__ __launch_bounds__(256, 2) void logreg_binary_split_kernel(const float
   }
 }
 
+// Column-split + prefetch variant: like logreg_binary_split_kernel, but the next R-row batch is
+// loaded into a second register set while the current batch's margins are reduced / exchanged
+// through LDS and its gradient is accumulated, so each wave keeps 2 * R * V * 1 KiB of X in flight
+// across the per-batch barrier (the kernel is HBM-latency bound, not VALU bound).
+template <int V, int R, int D>
+__global__ __launch_bounds__(256, 2) void logreg_binary_pf_kernel(const float* __restrict__ X, long m, int n, long ld,
+                                                                  const float* __restrict__ y,
+                                                                  const double* __restrict__ w, double b,
+                                                                  double* __restrict__ out, long rows_per_block) {
+  __shared__ double part[2][R][4];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int cbase = wid * 256 * V;
+  double wreg[V][4];
+  int coff[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    const int c = cbase + (v * 64 + lane) * 4;
+    coff[v] = (c + 3 < n) ? c : 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) wreg[v][q] = (c + 3 < n) ? w[c + q] : 0.0;
+  }
+  // tail columns (n % 4 != 0 or ld unaligned) are handled by the generic kernel; see launcher
+  floatx4 g[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) g[v] = floatx4{0.f, 0.f, 0.f, 0.f};
+  double gb = 0.0, loss = 0.0;
+  const long r0 = (long)blockIdx.x * rows_per_block;
+  const long r1 = min(m, r0 + rows_per_block);
+  if (r0 >= r1) return;
+
+  auto load = [&](long rb, floatx4 (&x)[R][V]) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const long r = rb + i < r1 ? rb + i : r1 - 1;
+      const float* row = X + r * ld;
+#pragma unroll
+      for (int v = 0; v < V; ++v) x[i][v] = *reinterpret_cast<const floatx4*>(row + coff[v]);
+    }
+  };
+  int buf = 0;
+  auto process = [&](long rb, const floatx4 (&x)[R][V]) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      double dot = 0.0;
+#pragma unroll
+      for (int v = 0; v < V; ++v)
+        dot = fma((double)x[i][v][0], wreg[v][0], fma((double)x[i][v][1], wreg[v][1],
+              fma((double)x[i][v][2], wreg[v][2], fma((double)x[i][v][3], wreg[v][3], dot))));
+      dot = wave_sum(dot);
+      if (lane == 0) part[buf][i][wid] = dot;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const long r = rb + i;
+      if (r < r1) {
+        const double z = part[buf][i][0] + part[buf][i][1] + part[buf][i][2] + part[buf][i][3] + b;
+        double res, lt;
+        logistic_terms(z, (double)y[r], res, lt);
+        if (wid == 0 && lane == 0) {
+          loss += lt;
+          gb += res;
+        }
+        const float rf = (float)res;
+#pragma unroll
+        for (int v = 0; v < V; ++v)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) g[v][q] = fmaf(rf, x[i][v][q], g[v][q]);
+      }
+    }
+    buf ^= 1;
+  };
+  // ring of D + 1 register batches: batch j is loaded D batches ahead of its use
+  floatx4 x[D + 1][R][V];
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+    if (r0 + d * R < r1) load(r0 + d * R, x[d]);
+  for (long rb = r0; rb < r1; rb += (D + 1) * R) {
+#pragma unroll
+    for (int ph = 0; ph <= D; ++ph) {
+      const long cur = rb + ph * R;
+      if (cur < r1) {
+        const long nxt = cur + D * R;
+        if (nxt < r1) load(nxt, x[(ph + D) % (D + 1)]);
+        process(cur, x[ph]);
+      }
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < V; ++v)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = cbase + (v * 64 + lane) * 4 + q;
+      if (cbase + (v * 64 + lane) * 4 + 3 < n) atomicAdd(&out[c], (double)g[v][q]);
+    }
+  if (wid == 0 && lane == 0) {
+    atomicAdd(&out[n], gb);
+    atomicAdd(&out[n + 1], loss);
+  }
+}
+
 SRML_API int srml_logreg_binary_f32(const float* X, long m, int n, long ld, const float* y, const double* w, double b,
                                     double* out, hipStream_t stream) {
   if (m <= 0) return 0;
-  long blocks = 2048;
+  static const long blocks_env = getenv("SRML_LOGREG_BLOCKS") ? atol(getenv("SRML_LOGREG_BLOCKS")) : 2048;
+  long blocks = blocks_env;
   long rpb = (m + blocks - 1) / blocks;
   if (rpb < 16) rpb = 16;
   blocks = (m + rpb - 1) / rpb;
   int V = (n + 255) / 256;
   size_t lds = 256 * (size_t)(V <= 1 ? 1 : V <= 2 ? 2 : V <= 4 ? 4 : V <= 8 ? 8 : V <= 12 ? 12 : 16) * (sizeof(double) + sizeof(float));
   dim3 grid((unsigned)blocks), blk(256);
-  static const int split = getenv("SRML_LOGREG_SPLIT") ? atoi(getenv("SRML_LOGREG_SPLIT")) : 0;
-  if (split && n > 1024 && n <= 4096) {
+  static const int split = getenv("SRML_LOGREG_SPLIT") ? atoi(getenv("SRML_LOGREG_SPLIT")) : 2;
+  // prefetching column-split kernel: needs 16-B aligned rows and n % 4 == 0 (no tail columns)
+  if (split == 2 && n > 1024 && n <= 4096 && (n & 3) == 0 && (ld & 3) == 0 &&
+      (reinterpret_cast<uintptr_t>(X) & 15) == 0) {
+    static const int rsel = getenv("SRML_LOGREG_R") ? atoi(getenv("SRML_LOGREG_R")) : 1;
+    static const int dsel = getenv("SRML_LOGREG_D") ? atoi(getenv("SRML_LOGREG_D")) : 3;
+    const int VS = (n + 1023) / 1024;
+#define SRML_LR_PF(VV, RR, DD) \
+    hipLaunchKernelGGL((logreg_binary_pf_kernel<VV, RR, DD>), grid, blk, 0, stream, X, m, n, ld, y, w, b, out, rpb)
+#define SRML_LR_PF_V(RR, DD) \
+    do { if (VS == 2) SRML_LR_PF(2, RR, DD); else if (VS == 3) SRML_LR_PF(3, RR, DD); else SRML_LR_PF(4, RR, DD); } while (0)
+    if (rsel == 2 && dsel == 1) SRML_LR_PF_V(2, 1);
+    else if (rsel == 2) SRML_LR_PF_V(2, 2);
+    else if (dsel == 1) SRML_LR_PF_V(1, 1);
+    else if (dsel == 3) SRML_LR_PF_V(1, 3);
+    else SRML_LR_PF_V(1, 2);
+    return srml_status();
+  }
+  if (split == 1 && n > 1024 && n <= 4096) {
     static const int rsel = getenv("SRML_LOGREG_R") ? atoi(getenv("SRML_LOGREG_R")) : 4;
     const int VS = (n + 1023) / 1024;
 #define SRML_LR_SPLIT(VV, RR) \
