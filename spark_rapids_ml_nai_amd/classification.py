@@ -299,8 +299,9 @@ class LogisticRegressionModel(LogisticRegressionClass, _ModelWithPredictionCol, 
             Wd, bd = state
             Xd = to_device(X, ctx.device, Wd.dtype)
             if isinstance(Xd, CSR):
-                Xs = torch.sparse_csr_tensor(Xd.indptr, Xd.indices.long(), Xd.data, Xd.shape)
-                S = (Xs @ Wd.T.to(Xd.dtype)) + bd
+                from . import ops
+
+                S = ops.csr_spmm(Xd, Wd.T, bd)
             else:
                 S = logistic_scores(Xd, Wd, bd)
             S = S.double()

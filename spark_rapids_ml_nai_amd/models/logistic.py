@@ -50,14 +50,12 @@ class _Evaluator:
 
     def _margins(self, W: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
         if self.sparse:
-            Xs = torch.sparse_csr_tensor(self.X.indptr, self.X.indices.long(), self.X.data, self.X.shape)
-            return (Xs @ W.to(self.X.dtype)).float() + b
+            return ops.csr_spmm(self.X, W.float(), b.float())
         return ops.xw(self.X, W.float(), b.float())
 
     def _xt(self, R: torch.Tensor) -> torch.Tensor:
         if self.sparse:
-            Xs = torch.sparse_csr_tensor(self.X.indptr, self.X.indices.long(), self.X.data, self.X.shape)
-            return (Xs.t() @ R.to(self.X.dtype)).double()
+            return ops.csr_spmtm(self.X, R)
         return ops.xtv(self.X, R)
 
     def __call__(self, theta: np.ndarray) -> Tuple[float, np.ndarray]:
@@ -67,7 +65,11 @@ class _Evaluator:
         Wt = theta[: K * n].reshape(K, n)
         b = theta[K * n: K * n + K] if self.fit_intercept else np.zeros(K)
         W = (Wt * self.inv_sigma).T  # n x K, original-space coefficients
-        if K == 1 and not self.sparse and self.X.dtype == torch.float32 and n <= 4096:
+        if K == 1 and self.sparse:
+            w_dev = torch.from_numpy(np.ascontiguousarray(W[:, 0])).to(self.dev)
+            out = ops.csr_logreg_binary_loss_grad(self.X, self.y, w_dev, float(b[0]))
+            g_w, g_b, loss = out[:n].view(n, 1), out[n: n + 1], out[n + 1: n + 2]
+        elif K == 1 and self.X.dtype == torch.float32 and n <= 4096:
             w_dev = torch.from_numpy(np.ascontiguousarray(W[:, 0])).to(self.dev)
             out = ops.logreg_binary_loss_grad(self.X, self.y, w_dev, float(b[0]))
             g_w, g_b, loss = out[:n].view(n, 1), out[n: n + 1], out[n + 1: n + 2]
@@ -195,10 +197,7 @@ def logistic_stats(X: Any, y: torch.Tensor, m_total: int, ctx: WorkerContext, sp
     """Column std-devs (population, Spark's featuresStd) and label histogram, all-reduced once."""
     n = X.shape[1]
     if sparse:
-        d = X.data.double()
-        cols = X.indices.long()
-        s = torch.zeros(n, dtype=torch.float64, device=d.device).index_add_(0, cols, d)
-        q = torch.zeros(n, dtype=torch.float64, device=d.device).index_add_(0, cols, d * d)
+        s, q = ops.csr_col_moments(X)
     else:
         s, q = ops.col_moments(X)
     yl = y.long()

@@ -12,7 +12,8 @@ import torch
 from . import native
 
 __all__ = ["col_moments", "gram", "xw", "dgemm", "sign_flip", "is_native", "xtv", "row_sqnorm",
-           "logreg_binary_loss_grad", "nearest_centroid", "cluster_sums"]
+           "logreg_binary_loss_grad", "nearest_centroid", "cluster_sums", "csr_logreg_binary_loss_grad",
+           "csr_spmm", "csr_spmtm", "csr_col_moments"]
 
 
 def is_native(t: torch.Tensor) -> bool:
@@ -929,3 +930,106 @@ def cd_gram(A: torch.Tensor, b: torch.Tensor, l1: torch.Tensor, l2: torch.Tensor
                 _c(l2.double()).data_ptr(), w.data_ptr(), int(max_iter), float(tol), iters.data_ptr(),
                 native.stream(A.device))
     return w, int(iters.item())
+
+
+# ------------------------------------------------------------------------------------------
+# CSR (sparse features): ``A`` is any object with indptr (int64), indices (int32), data, shape
+def _csr_torch(A) -> torch.Tensor:
+    return torch.sparse_csr_tensor(A.indptr, A.indices.long(), A.data, tuple(A.shape))
+
+
+def _csr_check(A) -> None:
+    if A.indptr.dtype != torch.int64 or A.indices.dtype != torch.int32:
+        raise TypeError("CSR kernels need int64 row offsets and int32 column indices")
+    if A.data.dtype not in (torch.float32, torch.float64):
+        raise TypeError("CSR kernels support fp32/fp64 values")
+    if A.indptr.numel() != A.shape[0] + 1 or A.indices.numel() != A.data.numel():
+        raise ValueError("inconsistent CSR arrays")
+    if getattr(A, "_srml_checked", False):
+        return
+    # one-time host check (the kernels index through indptr/indices without bounds checks)
+    ip = A.indptr.cpu()
+    if ip.numel() and (int(ip[0]) != 0 or int(ip[-1]) != A.indices.numel() or bool((ip[1:] < ip[:-1]).any())):
+        raise ValueError("CSR row offsets are not a monotone 0..nnz sequence")
+    if A.indices.numel():
+        lo, hi = int(A.indices.min().item()), int(A.indices.max().item())
+        if lo < 0 or hi >= A.shape[1]:
+            raise ValueError(f"CSR column index out of range [0, {A.shape[1]})")
+    try:
+        A._srml_checked = True
+    except AttributeError:
+        pass
+
+
+def _sfx(A) -> str:
+    return "f32" if A.data.dtype == torch.float32 else "f64"
+
+
+def csr_logreg_binary_loss_grad(A, y: torch.Tensor, w: torch.Tensor, b: float) -> torch.Tensor:
+    """fp64 [grad_w (n), grad_b, loss_sum] for CSR features: one pass over the non-zeros."""
+    m, n = A.shape
+    if not A.data.is_cuda:
+        Xs = _csr_torch(A).to(torch.float64) if A.data.dtype != torch.float64 else _csr_torch(A)
+        z = (Xs @ w.double().view(-1, 1)).view(-1) + b
+        yd = y.double()
+        r = torch.sigmoid(z) - yd
+        loss = torch.nn.functional.softplus(z).sum() - (yd * z).sum()
+        g = (Xs.t() @ r.view(-1, 1)).view(-1)
+        return torch.cat([g, r.sum().view(1), loss.view(1)])
+    _csr_check(A)
+    out = torch.zeros(n + 2, dtype=torch.float64, device=A.data.device)
+    wf = _c(w.to(device=A.data.device, dtype=torch.float64))
+    yf = _c(y.to(torch.float32))
+    native.call("srml_csr_logreg_binary_" + _sfx(A), A.indptr.data_ptr(), A.indices.data_ptr(), A.data.data_ptr(),
+                m, n, A.data.numel(), yf.data_ptr(), wf.data_ptr(), float(b), out.data_ptr(),
+                native.stream(A.data.device))
+    return out
+
+
+def csr_spmm(A, W: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """fp32 Z (m, K) = A W + bias for W (n, K), K <= 16 (multinomial margins)."""
+    m, n = A.shape
+    K = W.shape[1]
+    if not A.data.is_cuda or K > 16:
+        Z = (_csr_torch(A) @ W.to(A.data.dtype)).float()
+        return Z + bias.float() if bias is not None else Z
+    _csr_check(A)
+    Wf = _c(W.to(torch.float32))
+    bf = _c(bias.to(torch.float32)) if bias is not None else None
+    Z = torch.empty(m, K, dtype=torch.float32, device=A.data.device)
+    native.call("srml_csr_spmm_" + _sfx(A), A.indptr.data_ptr(), A.indices.data_ptr(), A.data.data_ptr(), m,
+                A.data.numel(), Wf.data_ptr(), K, bf.data_ptr() if bf is not None else None, Z.data_ptr(),
+                native.stream(A.data.device))
+    return Z
+
+
+def csr_spmtm(A, R: torch.Tensor) -> torch.Tensor:
+    """fp64 (n, K) = A^T R for R (m, K), K <= 16 (multinomial gradient)."""
+    m, n = A.shape
+    K = R.shape[1]
+    if not A.data.is_cuda or K > 16:
+        return (_csr_torch(A).t() @ R.to(A.data.dtype)).double()
+    _csr_check(A)
+    Rf = _c(R.to(torch.float32))
+    out = torch.zeros(n, K, dtype=torch.float64, device=A.data.device)
+    native.call("srml_csr_spmtm_" + _sfx(A), A.indptr.data_ptr(), A.indices.data_ptr(), A.data.data_ptr(), m,
+                A.data.numel(), Rf.data_ptr(), K, out.data_ptr(), native.stream(A.data.device))
+    return out
+
+
+def csr_col_moments(A) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Per-column fp64 (sum, sum of squares) over the non-zeros of a CSR matrix."""
+    n = A.shape[1]
+    dev = A.data.device
+    if not A.data.is_cuda:
+        d = A.data.double()
+        cols = A.indices.long()
+        s = torch.zeros(n, dtype=torch.float64).index_add_(0, cols, d)
+        q = torch.zeros(n, dtype=torch.float64).index_add_(0, cols, d * d)
+        return s, q
+    _csr_check(A)
+    s = torch.zeros(n, dtype=torch.float64, device=dev)
+    q = torch.zeros(n, dtype=torch.float64, device=dev)
+    native.call("srml_csr_col_moments_" + _sfx(A), A.indices.data_ptr(), A.data.data_ptr(), A.data.numel(),
+                s.data_ptr(), q.data_ptr(), native.stream(dev))
+    return s, q

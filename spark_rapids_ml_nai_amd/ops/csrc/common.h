@@ -76,6 +76,18 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
   return base + bid / nxcd;
 }
 
+// Per-row logistic terms. The piecewise-linear parts of the loss (max(z,0) - y z) stay in fp64 so
+// the objective is smooth for the line search; the bounded transcendental part log1p(exp(-|z|))
+// and the sigmoid use the fp32 hardware exp/log (v_exp_f32 / v_log_f32): fp64 exp/log1p are long
+// software sequences that made the kernel VALU-bound.
+__device__ __forceinline__ void logistic_terms(double z, double y, double& res, double& loss) {
+  const float zf = (float)z;
+  const float e = __expf(-fabsf(zf));             // in (0, 1]
+  const float p = zf >= 0.f ? 1.f / (1.f + e) : e / (1.f + e);
+  res = (double)p - y;
+  loss = (z > 0.0 ? z : 0.0) - y * z + (double)log1pf(e);
+}
+
 static inline int srml_status() { return (int)hipGetLastError(); }
 
 // keep the first failing HIP runtime status of a multi-call host routine in `err`

@@ -1,0 +1,286 @@
+// CSR (sparse-feature) kernels: the device path of LogisticRegression's sparse input mode.
+//
+// Reference: the reference hands a cupyx CSR matrix to cuML's QN solver when
+// `enable_sparse_data_optim` is on (classification.py:957-1151, core.py:192-246); cuML then runs
+// one sparse SpMV for the margins and a second transposed SpMV for the gradient, i.e. two passes
+// over the non-zeros per function evaluation. Here:
+//
+//  * srml_csr_logreg_binary_{f32,f64} — ONE pass over the non-zeros per L-BFGS evaluation:
+//        z_r = x_r . w + b ; loss += softplus(z_r) - y_r z_r ; g[col] += (sigmoid(z_r) - y_r) x_rc
+//    A group of G lanes (G in {4,8,16,32,64}, picked from the mean row length) owns one row: the
+//    lanes stride the row's non-zeros, reduce the dot product with intra-group shuffles, then
+//    reuse the same (index, value) registers for the scatter of the gradient (fp64 atomics in
+//    L2; sparse columns rarely collide within a wave). Non-zeros beyond 4*G per row are re-read.
+//  * srml_csr_spmm_{f32,f64}   — Z (m x K fp32) = X W + bias, W (n x K fp32 row-major), K <= 16:
+//    multinomial margins for every class in one pass.
+//  * srml_csr_spmtm_{f32,f64}  — out (n x K fp64) += X^T R, R (m x K fp32): multinomial gradient.
+//  * srml_csr_col_moments_{f32,f64} — column sum and sum of squares (fp64) over the non-zeros
+//    (standardisation statistics; zeros contribute nothing to either moment).
+//
+// Row offsets are int64, column indices int32 (the layout the ingest path builds from Arrow
+// sparse VectorUDT columns, core/dataframe.py:vector_column_to_csr).
+#include "common.h"
+
+template <int G, typename V>
+__device__ __forceinline__ V group_sum(V v) {
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// fold one fp64 value per row group into a global accumulator (one atomic per block)
+template <int GPB>
+__device__ __forceinline__ void block_fold2(double a, double b, bool holder, int g, double* outa, double* outb) {
+  __shared__ double red[2][GPB];
+  if (holder) {
+    red[0][g] = a;
+    red[1][g] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    double s = 0.0;
+    for (int i = 0; i < GPB; ++i) s += red[threadIdx.x][i];
+    atomicAdd(threadIdx.x == 0 ? outa : outb, s);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+template <typename T, int G>
+__global__ __launch_bounds__(256) void csr_logreg_binary_kernel(const long* __restrict__ indptr,
+                                                                const int* __restrict__ indices,
+                                                                const T* __restrict__ data, long m,
+                                                                const float* __restrict__ y,
+                                                                const double* __restrict__ w, double b,
+                                                                double* __restrict__ grad,
+                                                                double* __restrict__ tail) {
+  constexpr int GPB = 256 / G;  // row groups per block
+  constexpr int CACHE = 4;      // non-zeros per lane kept in registers between the two phases
+  const int g = threadIdx.x / G;
+  const int l = threadIdx.x % G;
+  double gb = 0.0, loss = 0.0;
+  for (long r = (long)blockIdx.x * GPB + g; r < m; r += (long)gridDim.x * GPB) {
+    const long p0 = indptr[r], p1 = indptr[r + 1];
+    int ci[CACHE];
+    double cv[CACHE];
+    double dot = 0.0;
+#pragma unroll
+    for (int t = 0; t < CACHE; ++t) {
+      const long p = p0 + t * G + l;
+      ci[t] = -1;
+      cv[t] = 0.0;
+      if (p < p1) {
+        ci[t] = indices[p];
+        cv[t] = (double)data[p];
+        dot = fma(cv[t], w[ci[t]], dot);
+      }
+    }
+    for (long p = p0 + CACHE * G + l; p < p1; p += G) dot = fma((double)data[p], w[indices[p]], dot);
+    dot = group_sum<G>(dot);
+    double res, lt;
+    logistic_terms(dot + b, (double)y[r], res, lt);
+    if (l == 0) {
+      gb += res;
+      loss += lt;
+    }
+#pragma unroll
+    for (int t = 0; t < CACHE; ++t)
+      if (ci[t] >= 0) atomicAdd(&grad[ci[t]], res * cv[t]);
+    for (long p = p0 + CACHE * G + l; p < p1; p += G) atomicAdd(&grad[indices[p]], res * (double)data[p]);
+  }
+  block_fold2<GPB>(gb, loss, l == 0, g, tail, tail + 1);
+}
+
+// ------------------------------------------------------------------------------------------
+template <typename T, int G, int K>
+__global__ __launch_bounds__(256) void csr_spmm_kernel(const long* __restrict__ indptr, const int* __restrict__ indices,
+                                                       const T* __restrict__ data, long m,
+                                                       const float* __restrict__ W, int kk,
+                                                       const float* __restrict__ bias, float* __restrict__ Z) {
+  constexpr int GPB = 256 / G;
+  const int g = threadIdx.x / G;
+  const int l = threadIdx.x % G;
+  for (long r = (long)blockIdx.x * GPB + g; r < m; r += (long)gridDim.x * GPB) {
+    float acc[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = 0.f;
+    const long p1 = indptr[r + 1];
+    for (long p = indptr[r] + l; p < p1; p += G) {
+      const float v = (float)data[p];
+      const float* wr = W + (long)indices[p] * kk;
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+        if (k < kk) acc[k] = fmaf(v, wr[k], acc[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = group_sum<G>(acc[k]);
+    // lane k of the group writes column k
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      if (k < kk && (k % G) == l) Z[r * kk + k] = acc[k] + (bias ? bias[k] : 0.f);
+  }
+}
+
+template <typename T, int G, int K>
+__global__ __launch_bounds__(256) void csr_spmtm_kernel(const long* __restrict__ indptr, const int* __restrict__ indices,
+                                                        const T* __restrict__ data, long m,
+                                                        const float* __restrict__ R, int kk, double* __restrict__ out) {
+  constexpr int GPB = 256 / G;
+  const int g = threadIdx.x / G;
+  const int l = threadIdx.x % G;
+  for (long r = (long)blockIdx.x * GPB + g; r < m; r += (long)gridDim.x * GPB) {
+    float rr[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) rr[k] = k < kk ? R[r * kk + k] : 0.f;
+    const long p1 = indptr[r + 1];
+    for (long p = indptr[r] + l; p < p1; p += G) {
+      const double v = (double)data[p];
+      double* o = out + (long)indices[p] * kk;
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+        if (k < kk && rr[k] != 0.f) atomicAdd(&o[k], v * (double)rr[k]);
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void csr_col_moments_kernel(const int* __restrict__ indices, const T* __restrict__ data,
+                                                              long nnz, double* __restrict__ s, double* __restrict__ q) {
+  for (long p = (long)blockIdx.x * 256 + threadIdx.x; p < nnz; p += (long)gridDim.x * 256) {
+    const double v = (double)data[p];
+    if (v != 0.0) {
+      atomicAdd(&s[indices[p]], v);
+      atomicAdd(&q[indices[p]], v * v);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Lanes per row: the smallest power of two >= mean nnz / 2 (so each lane handles ~2 non-zeros),
+// clamped to [4, 64].
+static int pick_group(long m, long nnz) {
+  const double mean = m > 0 ? (double)nnz / (double)m : 0.0;
+  int G = 4;
+  while (G < 64 && G * 2 < mean) G <<= 1;
+  return G;
+}
+
+static unsigned grid_for(long rows, int G) {
+  const long groups_per_block = 256 / G;
+  long blocks = (rows + groups_per_block - 1) / groups_per_block;
+  if (blocks > 8192) blocks = 8192;  // grid-stride beyond 32 blocks per CU
+  return (unsigned)(blocks < 1 ? 1 : blocks);
+}
+
+template <typename T>
+static int csr_logreg_launch(const long* indptr, const int* indices, const T* data, long m, long nnz, const float* y,
+                             const double* w, double b, double* grad, double* tail, hipStream_t s) {
+  if (m <= 0) return 0;
+  const int G = pick_group(m, nnz);
+  const dim3 grid(grid_for(m, G)), blk(256);
+#define SRML_CSR_LR(GG) \
+  hipLaunchKernelGGL((csr_logreg_binary_kernel<T, GG>), grid, blk, 0, s, indptr, indices, data, m, y, w, b, grad, tail)
+  switch (G) {
+    case 4: SRML_CSR_LR(4); break;
+    case 8: SRML_CSR_LR(8); break;
+    case 16: SRML_CSR_LR(16); break;
+    case 32: SRML_CSR_LR(32); break;
+    default: SRML_CSR_LR(64); break;
+  }
+#undef SRML_CSR_LR
+  return srml_status();
+}
+
+template <typename T, int K>
+static void csr_spmm_k(int G, dim3 grid, hipStream_t s, const long* indptr, const int* indices, const T* data, long m,
+                       const float* W, int kk, const float* bias, float* Z) {
+  switch (G) {
+    case 4: hipLaunchKernelGGL((csr_spmm_kernel<T, 4, K>), grid, dim3(256), 0, s, indptr, indices, data, m, W, kk, bias, Z); break;
+    case 8: hipLaunchKernelGGL((csr_spmm_kernel<T, 8, K>), grid, dim3(256), 0, s, indptr, indices, data, m, W, kk, bias, Z); break;
+    case 16: hipLaunchKernelGGL((csr_spmm_kernel<T, 16, K>), grid, dim3(256), 0, s, indptr, indices, data, m, W, kk, bias, Z); break;
+    case 32: hipLaunchKernelGGL((csr_spmm_kernel<T, 32, K>), grid, dim3(256), 0, s, indptr, indices, data, m, W, kk, bias, Z); break;
+    default: hipLaunchKernelGGL((csr_spmm_kernel<T, 64, K>), grid, dim3(256), 0, s, indptr, indices, data, m, W, kk, bias, Z); break;
+  }
+}
+
+template <typename T, int K>
+static void csr_spmtm_k(int G, dim3 grid, hipStream_t s, const long* indptr, const int* indices, const T* data, long m,
+                        const float* R, int kk, double* out) {
+  switch (G) {
+    case 4: hipLaunchKernelGGL((csr_spmtm_kernel<T, 4, K>), grid, dim3(256), 0, s, indptr, indices, data, m, R, kk, out); break;
+    case 8: hipLaunchKernelGGL((csr_spmtm_kernel<T, 8, K>), grid, dim3(256), 0, s, indptr, indices, data, m, R, kk, out); break;
+    case 16: hipLaunchKernelGGL((csr_spmtm_kernel<T, 16, K>), grid, dim3(256), 0, s, indptr, indices, data, m, R, kk, out); break;
+    case 32: hipLaunchKernelGGL((csr_spmtm_kernel<T, 32, K>), grid, dim3(256), 0, s, indptr, indices, data, m, R, kk, out); break;
+    default: hipLaunchKernelGGL((csr_spmtm_kernel<T, 64, K>), grid, dim3(256), 0, s, indptr, indices, data, m, R, kk, out); break;
+  }
+}
+
+template <typename T>
+static int csr_spmm_launch(const long* indptr, const int* indices, const T* data, long m, long nnz, const float* W,
+                           int kk, const float* bias, float* Z, hipStream_t s) {
+  if (m <= 0) return 0;
+  if (kk < 1 || kk > 16) return (int)hipErrorInvalidValue;
+  const int G = pick_group(m, nnz);
+  const dim3 grid(grid_for(m, G));
+  if (kk <= 4) csr_spmm_k<T, 4>(G, grid, s, indptr, indices, data, m, W, kk, bias, Z);
+  else if (kk <= 8) csr_spmm_k<T, 8>(G, grid, s, indptr, indices, data, m, W, kk, bias, Z);
+  else csr_spmm_k<T, 16>(G, grid, s, indptr, indices, data, m, W, kk, bias, Z);
+  return srml_status();
+}
+
+template <typename T>
+static int csr_spmtm_launch(const long* indptr, const int* indices, const T* data, long m, long nnz, const float* R,
+                            int kk, double* out, hipStream_t s) {
+  if (m <= 0) return 0;
+  if (kk < 1 || kk > 16) return (int)hipErrorInvalidValue;
+  const int G = pick_group(m, nnz);
+  const dim3 grid(grid_for(m, G));
+  if (kk <= 4) csr_spmtm_k<T, 4>(G, grid, s, indptr, indices, data, m, R, kk, out);
+  else if (kk <= 8) csr_spmtm_k<T, 8>(G, grid, s, indptr, indices, data, m, R, kk, out);
+  else csr_spmtm_k<T, 16>(G, grid, s, indptr, indices, data, m, R, kk, out);
+  return srml_status();
+}
+
+template <typename T>
+static int csr_moments_launch(const int* indices, const T* data, long nnz, double* sum, double* sq, hipStream_t s) {
+  if (nnz <= 0) return 0;
+  long blocks = (nnz + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL((csr_col_moments_kernel<T>), dim3((unsigned)blocks), dim3(256), 0, s, indices, data, nnz, sum, sq);
+  return srml_status();
+}
+
+// out: [grad (n) | grad_b | loss], fp64, accumulated (caller zeroes it)
+SRML_API int srml_csr_logreg_binary_f32(const long* indptr, const int* indices, const float* data, long m, int n,
+                                        long nnz, const float* y, const double* w, double b, double* out,
+                                        hipStream_t s) {
+  return csr_logreg_launch<float>(indptr, indices, data, m, nnz, y, w, b, out, out + n, s);
+}
+SRML_API int srml_csr_logreg_binary_f64(const long* indptr, const int* indices, const double* data, long m, int n,
+                                        long nnz, const float* y, const double* w, double b, double* out,
+                                        hipStream_t s) {
+  return csr_logreg_launch<double>(indptr, indices, data, m, nnz, y, w, b, out, out + n, s);
+}
+SRML_API int srml_csr_spmm_f32(const long* indptr, const int* indices, const float* data, long m, long nnz,
+                               const float* W, int k, const float* bias, float* Z, hipStream_t s) {
+  return csr_spmm_launch<float>(indptr, indices, data, m, nnz, W, k, bias, Z, s);
+}
+SRML_API int srml_csr_spmm_f64(const long* indptr, const int* indices, const double* data, long m, long nnz,
+                               const float* W, int k, const float* bias, float* Z, hipStream_t s) {
+  return csr_spmm_launch<double>(indptr, indices, data, m, nnz, W, k, bias, Z, s);
+}
+SRML_API int srml_csr_spmtm_f32(const long* indptr, const int* indices, const float* data, long m, long nnz,
+                                const float* R, int k, double* out, hipStream_t s) {
+  return csr_spmtm_launch<float>(indptr, indices, data, m, nnz, R, k, out, s);
+}
+SRML_API int srml_csr_spmtm_f64(const long* indptr, const int* indices, const double* data, long m, long nnz,
+                                const float* R, int k, double* out, hipStream_t s) {
+  return csr_spmtm_launch<double>(indptr, indices, data, m, nnz, R, k, out, s);
+}
+SRML_API int srml_csr_col_moments_f32(const int* indices, const float* data, long nnz, double* sum, double* sq,
+                                      hipStream_t s) {
+  return csr_moments_launch<float>(indices, data, nnz, sum, sq, s);
+}
+SRML_API int srml_csr_col_moments_f64(const int* indices, const double* data, long nnz, double* sum, double* sq,
+                                      hipStream_t s) {
+  return csr_moments_launch<double>(indices, data, nnz, sum, sq, s);
+}
