@@ -175,6 +175,130 @@ __global__ __launch_bounds__(1024) void cd_gram_kernel(const double* __restrict_
   for (int i = t; i < n; i += blockDim.x) w_out[i] = w[i];
   if (t == 0) *iters = it;
 }
+
+// Block-cyclic form of the same Gauss-Seidel sweep (identical coordinate order and updates):
+// the CB x CB diagonal block of A is staged in LDS and ONE wave runs the CB sequential
+// coordinate updates on it — its lanes own g / w of the block's coordinates, the coordinate's
+// delta is broadcast with a lane shuffle, so there is no workgroup barrier and no global load
+// inside the sequential chain. The rest of g is then brought up to date with one coalesced
+// rank-CB update g += A[blk, :]^T d (A symmetric) by all 1024 threads. Per sweep A is streamed
+// once; the per-coordinate cost drops from two barriers plus a dependent 24 KB row fetch to
+// ~20 fp64 VALU instructions.
+constexpr int CD_CB = 64;
+
+__global__ __launch_bounds__(1024) void cd_gram_block_kernel(const double* __restrict__ A, int n, long lda,
+                                                             const double* __restrict__ b, const double* __restrict__ l1,
+                                                             const double* __restrict__ l2, double* __restrict__ w_out,
+                                                             int max_iter, double tol, int* __restrict__ iters) {
+  extern __shared__ double sm[];  // w[n], g[n], blk[CB][CB + 1], dv[CB]
+  double* w = sm;
+  double* g = sm + n;
+  double* blk = g + n;
+  double* dv = blk + CD_CB * (CD_CB + 1);
+  __shared__ int done;
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  for (int i = t; i < n; i += blockDim.x) w[i] = w_out[i];
+  __syncthreads();
+  for (int i = t; i < n; i += blockDim.x) {  // g = A w, column reads (A symmetric) -> coalesced
+    double s = 0.0;
+#pragma unroll 8
+    for (int j = 0; j < n; ++j) s = fma(A[(long)j * lda + i], w[j], s);
+    g[i] = s;
+  }
+  __syncthreads();
+  int it = 0;
+  double max_delta = 0.0, max_w = 0.0;  // wave 0 (lane-partial, reduced at the sweep end)
+  for (; it < max_iter; ++it) {
+    max_delta = 0.0;
+    max_w = 0.0;
+    for (int j0 = 0; j0 < n; j0 += CD_CB) {
+      const int nb = n - j0 < CD_CB ? n - j0 : CD_CB;
+      for (int e = t; e < nb * nb; e += blockDim.x) {
+        const int r = e / nb, c = e - r * nb;
+        blk[r * (CD_CB + 1) + c] = A[(long)(j0 + r) * lda + j0 + c];
+      }
+      __syncthreads();
+      if (t < 64) {
+        const bool own = lane < nb;
+        const int jj = j0 + (own ? lane : 0);
+        double gl = own ? g[jj] : 0.0;
+        double wl = own ? w[jj] : 0.0;
+        const double w0 = wl;
+        const double ajj = own ? blk[lane * (CD_CB + 1) + lane] : 0.0;
+        const double diag = own ? ajj + l2[jj] : 0.0;
+        const double inv_diag = diag > 0.0 ? 1.0 / diag : 0.0;
+        const double bj = own ? b[jj] : 0.0;
+        const double l1j = own ? l1[jj] : 0.0;
+        for (int c = 0; c < nb; ++c) {
+          // every lane evaluates its own coordinate's update; lane c's is the one applied
+          double d = 0.0, nw = wl;
+          if (diag > 0.0) {
+            const double rho = bj - gl + ajj * wl;
+            nw = rho > l1j ? (rho - l1j) * inv_diag : (rho < -l1j ? (rho + l1j) * inv_diag : 0.0);
+            d = nw - wl;
+          }
+          {  // c is wave-uniform: broadcast through scalar readlanes instead of ds_bpermute
+            const long long bits = __double_as_longlong(d);
+            const int lo = __builtin_amdgcn_readlane((int)(bits & 0xffffffffLL), c);
+            const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), c);
+            d = __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+          }
+          if (lane == c) {
+            if (diag > 0.0) {
+              wl = nw;
+              max_w = fmax(max_w, fabs(nw));
+              max_delta = fmax(max_delta, fabs(d));
+            }
+          }
+          if (d != 0.0 && own) gl = fma(blk[c * (CD_CB + 1) + lane], d, gl);
+        }
+        if (own) {
+          g[jj] = gl;
+          w[jj] = wl;
+          dv[lane] = wl - w0;
+        }
+      }
+      __syncthreads();
+      // unconditional, unrolled loads: 16 independent row reads in flight per thread (a
+      // data-dependent skip here serialised one HBM round trip per coordinate)
+      for (int i = t; i < n; i += blockDim.x) {
+        if (i >= j0 && i < j0 + nb) continue;
+        const double* col = A + (long)j0 * lda + i;
+        double s0 = 0.0, s1 = 0.0;
+        int c = 0;
+        for (; c + 16 <= nb; c += 16) {
+          double v[16];
+#pragma unroll
+          for (int u = 0; u < 16; ++u) v[u] = col[(long)(c + u) * lda];
+#pragma unroll
+          for (int u = 0; u < 16; u += 2) {
+            s0 = fma(v[u], dv[c + u], s0);
+            s1 = fma(v[u + 1], dv[c + u + 1], s1);
+          }
+        }
+        for (; c < nb; ++c) s0 = fma(col[(long)c * lda], dv[c], s0);
+        g[i] += s0 + s1;
+      }
+      __syncthreads();
+    }
+    if (t < 64) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        max_delta = fmax(max_delta, __shfl_xor(max_delta, o, 64));
+        max_w = fmax(max_w, __shfl_xor(max_w, o, 64));
+      }
+      if (t == 0) done = (max_delta <= tol * fmax(max_w, 1e-300)) ? 1 : 0;
+    }
+    __syncthreads();
+    if (done) {
+      ++it;
+      break;
+    }
+  }
+  for (int i = t; i < n; i += blockDim.x) w_out[i] = w[i];
+  if (t == 0) *iters = it;
+}
 }  // namespace
 
 SRML_API int srml_potrf_f64(double* A, int n, long lda, int* info, hipStream_t stream) {
@@ -209,6 +333,14 @@ SRML_API int srml_potrs_f64(const double* L, int n, long lda, double* b, hipStre
 SRML_API int srml_cd_gram_f64(const double* A, int n, long lda, const double* b, const double* l1, const double* l2,
                               double* w, int max_iter, double tol, int* iters, hipStream_t stream) {
   if (n <= 0) return 0;
+  const size_t lds_blk = ((size_t)2 * n + CD_CB * (CD_CB + 1) + CD_CB) * sizeof(double);
+  if (lds_blk <= 150 * 1024) {  // n <= ~7500
+    (void)hipFuncSetAttribute((const void*)cd_gram_block_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds_blk);
+    hipLaunchKernelGGL(cd_gram_block_kernel, dim3(1), dim3(1024), lds_blk, stream, A, n, lda, b, l1, l2, w, max_iter,
+                       tol, iters);
+    return srml_status();
+  }
   const size_t lds = (size_t)2 * n * sizeof(double);
   if (lds > 150 * 1024) return -9;  // n <= 9600
   (void)hipFuncSetAttribute((const void*)cd_gram_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

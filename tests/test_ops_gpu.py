@@ -426,7 +426,7 @@ def test_spd_solve_detects_singular(gpu_device):
     assert not ok
 
 
-@pytest.mark.parametrize("n", [3, 50, 700])
+@pytest.mark.parametrize("n", [3, 50, 130, 700, 3000])
 def test_cd_gram(gpu_device, n):
     g = torch.Generator().manual_seed(n)
     M = torch.randn(4 * n, n, generator=g, dtype=torch.float64)
