@@ -7,8 +7,8 @@ is a restarted block-Krylov Rayleigh–Ritz iteration:
 
 * the n x n fp64 matrix stays on the device; every Krylov product ``C @ Q`` runs on the f64
   MFMA GEMM (``srml_dgemm``) — the only O(n^2) work;
-* orthogonalisation / Rayleigh–Ritz on the tiny (n x b·q) basis and (b·q)^2 projected matrix
-  run in fp64 LAPACK on the host (microseconds to a few ms at n = 3000);
+* the (n x b·q) basis stays on the device too: block Gram–Schmidt and CholeskyQR2 are device
+  GEMMs; only the tiny (b·q)^2 Gram / projected matrices go to host LAPACK (Cholesky, eigh);
 * convergence is checked with true residuals ``||C u - θ u|| <= tol · θ_max`` and the basis is
   restarted from the best Ritz vectors;
 * the epilogue orders eigenpairs descending and fixes signs on the device (``srml_sign_flip``,
@@ -33,6 +33,26 @@ def _orth(V: np.ndarray) -> np.ndarray:
     return q
 
 
+def _dorth(V: torch.Tensor) -> torch.Tensor:
+    """Orthonormal basis of the columns of a device (n x b) fp64 block: CholeskyQR2 (two passes
+    of G = V^T V on the device GEMM, a b x b Cholesky on the host, V <- V R^-1 on the device).
+    Falls back to a host Householder QR when the Gram matrix is numerically singular."""
+    W = V
+    for _ in range(2):
+        G = ops.dgemm(W, W, ta=True).cpu().numpy()
+        G = (G + G.T) * 0.5
+        try:
+            L = np.linalg.cholesky(G)
+        except np.linalg.LinAlgError:
+            return torch.from_numpy(_orth(V.cpu().numpy())).to(V.device)
+        d = np.diag(L)
+        if d.min() <= 1e-7 * d.max():  # nearly rank-deficient: CholQR loses orthogonality
+            return torch.from_numpy(_orth(V.cpu().numpy())).to(V.device)
+        Rinv = np.linalg.solve(L, np.eye(L.shape[0])).T  # (L^T)^-1 = R^-1
+        W = ops.dgemm(W, torch.from_numpy(np.ascontiguousarray(Rinv)).to(V.device))
+    return W
+
+
 def topk_eigh(C: torch.Tensor, k: int, tol: float = 1e-10, max_restarts: int = 60,
               seed: int = 0) -> Tuple[np.ndarray, np.ndarray]:
     """Largest-k eigenpairs of the symmetric fp64 matrix C (device or host).
@@ -55,7 +75,7 @@ def topk_eigh(C: torch.Tensor, k: int, tol: float = 1e-10, max_restarts: int = 6
     b = min(n, max(2 * k, k + 16))          # block width
     q = 4                                   # Krylov depth per restart
     rng = np.random.default_rng(seed)
-    Q0 = _orth(rng.standard_normal((n, b)))
+    Q0 = _dorth(torch.from_numpy(rng.standard_normal((n, b))).to(dev))
     theta = None
     U = None
     scale = None
@@ -63,33 +83,33 @@ def topk_eigh(C: torch.Tensor, k: int, tol: float = 1e-10, max_restarts: int = 6
         blocks = [Q0]
         Qprev = Q0
         for _j in range(q):
-            W = ops.dgemm(C, torch.from_numpy(np.ascontiguousarray(Qprev)).to(dev)).cpu().numpy()
-            # block Gram–Schmidt against the basis so far (twice for stability), then QR
-            Vb = np.hstack(blocks)
+            W = ops.dgemm(C, Qprev)
+            # block Gram–Schmidt against the basis so far (twice for stability), then orthonormalise
+            Vb = torch.cat(blocks, 1)
             for _r in range(2):
-                W -= Vb @ (Vb.T @ W)
-            Qn = _orth(W)
+                ops.dgemm(Vb, ops.dgemm(Vb, W, ta=True), alpha=-1.0, beta=1.0, out=W)
+            Qn = _dorth(W)
             blocks.append(Qn)
             Qprev = Qn
-        V = np.hstack(blocks)
-        V = _orth(V)
-        CV = ops.dgemm(C, torch.from_numpy(np.ascontiguousarray(V)).to(dev)).cpu().numpy()
-        T = V.T @ CV
+        V = _dorth(torch.cat(blocks, 1))
+        CV = ops.dgemm(C, V)
+        T = ops.dgemm(V, CV, ta=True).cpu().numpy()
         w, S = np.linalg.eigh((T + T.T) * 0.5)
         order = np.argsort(w)[::-1]
         w, S = w[order], S[:, order]
-        U = V @ S[:, :b]
-        CU = CV @ S[:, :b]
+        Sd = torch.from_numpy(np.ascontiguousarray(S[:, :b])).to(dev)
+        U = ops.dgemm(V, Sd)
+        CU = ops.dgemm(CV, Sd)
         theta = w[:b]
         if scale is None:
             scale = max(abs(theta[0]), 1e-300)
-        res = np.linalg.norm(CU[:, :k] - U[:, :k] * theta[:k], axis=0)
+        th = torch.from_numpy(theta[:k].copy()).to(dev)
+        res = torch.linalg.vector_norm(CU[:, :k] - U[:, :k] * th, dim=0).cpu().numpy()
         if np.all(res <= tol * max(abs(theta[0]), 1e-300) * 10 + 1e-300) or np.all(res <= 1e-12 * scale):
             break
-        Q0 = _orth(U[:, :b])
+        Q0 = _dorth(U[:, :b].contiguous())
     assert theta is not None and U is not None
     vals = theta[:k].copy()
-    vecs = np.ascontiguousarray(U[:, :k])
-    Vt = torch.from_numpy(vecs).to(dev)
+    Vt = U[:, :k].contiguous()
     ops.sign_flip(Vt)
     return vals, Vt.cpu().numpy()

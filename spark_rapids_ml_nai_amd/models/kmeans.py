@@ -180,7 +180,7 @@ def kmeans_fit(X: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext, k
             break
     del XP
     return {
-        "cluster_centers_": C.cpu().numpy().tolist(),
+        "cluster_centers_": C.cpu().numpy(),  # ndarray: 3M-float .tolist() cost 40 ms per fit
         "n_cols": int(n),
         "dtype": "float32" if X.dtype == torch.float32 else "float64",
         "n_iter": n_iter,

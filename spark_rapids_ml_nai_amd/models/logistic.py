@@ -47,6 +47,13 @@ class _Evaluator:
         self.n_evals = 0
         if self.K > 1:
             self.Y = torch.nn.functional.one_hot(y.long(), self.K).to(torch.float32)
+        # per-evaluation H2D of the coefficients goes through one pinned staging buffer
+        self._w_host = torch.empty(self.n, dtype=torch.float64, pin_memory=self.dev.type == "cuda")
+        self._y32 = y if y.dtype == torch.float32 else y.to(torch.float32)
+
+    def _w_to_device(self, w: np.ndarray) -> torch.Tensor:
+        self._w_host.numpy()[:] = w
+        return self._w_host.to(self.dev, non_blocking=True)
 
     def _margins(self, W: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
         if self.sparse:
@@ -66,12 +73,12 @@ class _Evaluator:
         b = theta[K * n: K * n + K] if self.fit_intercept else np.zeros(K)
         W = (Wt * self.inv_sigma).T  # n x K, original-space coefficients
         if K == 1 and self.sparse:
-            w_dev = torch.from_numpy(np.ascontiguousarray(W[:, 0])).to(self.dev)
-            out = ops.csr_logreg_binary_loss_grad(self.X, self.y, w_dev, float(b[0]))
+            w_dev = self._w_to_device(W[:, 0])
+            out = ops.csr_logreg_binary_loss_grad(self.X, self._y32, w_dev, float(b[0]))
             g_w, g_b, loss = out[:n].view(n, 1), out[n: n + 1], out[n + 1: n + 2]
         elif K == 1 and self.X.dtype == torch.float32 and n <= 4096:
-            w_dev = torch.from_numpy(np.ascontiguousarray(W[:, 0])).to(self.dev)
-            out = ops.logreg_binary_loss_grad(self.X, self.y, w_dev, float(b[0]))
+            w_dev = self._w_to_device(W[:, 0])
+            out = ops.logreg_binary_loss_grad(self.X, self._y32, w_dev, float(b[0]))
             g_w, g_b, loss = out[:n].view(n, 1), out[n: n + 1], out[n + 1: n + 2]
         else:
             Wd = torch.from_numpy(W).to(self.dev)
