@@ -44,14 +44,20 @@ def main() -> None:
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     use_gpu = torch.cuda.is_available()
-    device = torch.device("cuda", local_rank) if use_gpu else torch.device("cpu")
+    device = torch.device("cuda", local_rank % torch.cuda.device_count()) if use_gpu else torch.device("cpu")
     if use_gpu:
         torch.cuda.set_device(device)
+        from spark_rapids_ml_nai_amd.parallel.context import bind_numa_local
+
+        bind_numa_local(device)  # pinned staging buffers on the GPU's own socket
     if world > 1:
         from datetime import timedelta
 
-        dist.init_process_group("nccl" if use_gpu else "gloo", timeout=timedelta(minutes=30),
-                                **({"device_id": device} if use_gpu else {}))
+        # SRML_DIST_BACKEND=gloo: multi-rank rehearsal with several ranks sharing one GPU
+        # (RCCL refuses two ranks on one device); the default on GPUs is RCCL ("nccl")
+        backend = os.environ.get("SRML_DIST_BACKEND", "nccl" if use_gpu else "gloo")
+        dist.init_process_group(backend, timeout=timedelta(minutes=30),
+                                **({"device_id": device} if use_gpu and backend == "nccl" else {}))
 
     from spark_rapids_ml_nai_amd import DataFrame
     from spark_rapids_ml_nai_amd.bench.suite import REF_GEOMEAN_SPEEDUP, REF_GPU_S, SPARK_CPU_S, geomean, make_shard, registry

@@ -27,6 +27,7 @@
 #include "common.h"
 
 #include "tile.h"
+#include <stdlib.h>
 
 namespace {
 using srml_tile::orderable;
@@ -87,7 +88,7 @@ struct SplitStage {
   unsigned short B[3][BN][ROWB];
 };
 
-template <int BM, int BN, int WM, int WN, int MINB>
+template <int BM, int BN, int WM, int WN, int MINB, int PF>
 __global__ __launch_bounds__(WM * WN * 64, MINB) void nearest_centroid_split_kernel(
     const unsigned short* __restrict__ XP, long m, long xrows, int kp, const unsigned short* __restrict__ CP, int k,
     long crows, const float* __restrict__ cnorm, unsigned long long* __restrict__ best, int n_ctiles) {
@@ -119,30 +120,8 @@ __global__ __launch_bounds__(WM * WN * 64, MINB) void nearest_centroid_split_ker
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 
-  uintx4 ra[3], rb[3];
-#pragma unroll
-  for (int p = 0; p < 3; ++p) {
-    ra[p] = *reinterpret_cast<const uintx4*>(xa + p * xplane);
-    rb[p] = *reinterpret_cast<const uintx4*>(ca + p * cplane);
-  }
-#pragma unroll
-  for (int p = 0; p < 3; ++p) {
-    *reinterpret_cast<uintx4*>(&st[0].A[p][sr][sh]) = ra[p];
-    *reinterpret_cast<uintx4*>(&st[0].B[p][sr][sh]) = rb[p];
-  }
-  __syncthreads();
-  const int nk = kp / SBK;
-  int cur = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    const bool more = kt + 1 < nk;
-    if (more) {
-      const long ko = (long)(kt + 1) * SBK;
-#pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        ra[p] = *reinterpret_cast<const uintx4*>(xa + p * xplane + ko);
-        rb[p] = *reinterpret_cast<const uintx4*>(ca + p * cplane + ko);
-      }
-    }
+  // One 16-wide k step of MFMAs on LDS stage `cur` (smallest terms first: l.h, m.m, h.l, m.h, h.m, h.h).
+  auto mma_step = [&](int cur) {
     bf16x8 fb[3][TN];
 #pragma unroll
     for (int p = 0; p < 3; ++p)
@@ -155,7 +134,6 @@ __global__ __launch_bounds__(WM * WN * 64, MINB) void nearest_centroid_split_ker
 #pragma unroll
       for (int p = 0; p < 3; ++p)
         fa[p] = *reinterpret_cast<const bf16x8*>(&st[cur].A[p][wm * (BM / WM) + mt * 32 + li][8 * lk]);
-      // smallest terms first: l.h, m.m, h.l, m.h, h.m, h.h
 #pragma unroll
       for (int nt = 0; nt < TN; ++nt) {
         acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[0][nt], acc[mt][nt], 0, 0, 0);
@@ -166,15 +144,59 @@ __global__ __launch_bounds__(WM * WN * 64, MINB) void nearest_centroid_split_ker
         acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0][nt], acc[mt][nt], 0, 0, 0);
       }
     }
-    if (more) {
+  };
+  auto gload = [&](int kt, uintx4 (&a)[3], uintx4 (&b)[3]) {
+    const long ko = (long)kt * SBK;
 #pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        *reinterpret_cast<uintx4*>(&st[cur ^ 1].A[p][sr][sh]) = ra[p];
-        *reinterpret_cast<uintx4*>(&st[cur ^ 1].B[p][sr][sh]) = rb[p];
-      }
+    for (int p = 0; p < 3; ++p) {
+      a[p] = *reinterpret_cast<const uintx4*>(xa + p * xplane + ko);
+      b[p] = *reinterpret_cast<const uintx4*>(ca + p * cplane + ko);
     }
+  };
+  auto lstore = [&](int stage, const uintx4 (&a)[3], const uintx4 (&b)[3]) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      *reinterpret_cast<uintx4*>(&st[stage].A[p][sr][sh]) = a[p];
+      *reinterpret_cast<uintx4*>(&st[stage].B[p][sr][sh]) = b[p];
+    }
+  };
+  const int nk = kp / SBK;
+  if (PF == 1) {
+    uintx4 ra[3], rb[3];
+    gload(0, ra, rb);
+    lstore(0, ra, rb);
     __syncthreads();
-    cur ^= 1;
+    int cur = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool more = kt + 1 < nk;
+      if (more) gload(kt + 1, ra, rb);
+      mma_step(cur);
+      if (more) lstore(cur ^ 1, ra, rb);
+      __syncthreads();
+      cur ^= 1;
+    }
+  } else {
+    // global loads run two k steps ahead (two register sets): the L2/HBM latency of a step's
+    // operands is covered by two steps of MFMAs instead of one
+    uintx4 ra0[3], rb0[3], ra1[3], rb1[3];
+    gload(0, ra0, rb0);
+    if (nk > 1) gload(1, ra1, rb1);
+    lstore(0, ra0, rb0);
+    __syncthreads();
+    int kt = 0;
+    for (; kt + 2 <= nk; kt += 2) {
+      // step kt on stage 0; data of kt+1 sits in set 1; set 0 is refilled with kt+2
+      if (kt + 2 < nk) gload(kt + 2, ra0, rb0);
+      mma_step(0);
+      lstore(1, ra1, rb1);
+      __syncthreads();
+      // step kt+1 on stage 1; data of kt+2 sits in set 0; set 1 is refilled with kt+3
+      if (kt + 3 < nk) gload(kt + 3, ra1, rb1);
+      mma_step(1);
+      if (kt + 2 < nk) lstore(0, ra0, rb0);
+      __syncthreads();
+    }
+    if (kt < nk) mma_step(0);  // odd step count: the last step's data is already in stage 0
   }
 
   // epilogue (C/D layout of the 32x32 MFMA: col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5))
@@ -235,7 +257,8 @@ SRML_API int srml_nearest_centroid_split(const unsigned short* XP, long m, long 
                                          const unsigned short* CP, int k, long crows, const float* cnorm,
                                          unsigned long long* best, hipStream_t stream) {
   if (m <= 0 || k <= 0) return 0;
-  const bool big = k > 256;  // 256 x 256 tiles: 4x fewer L2 bytes per MFMA than 128 x 128
+  static const int tile_env = getenv("SRML_SPLIT_TILE") ? atoi(getenv("SRML_SPLIT_TILE")) : 0;
+  const bool big = tile_env ? tile_env == 256 : k > 256;  // 256 x 256 tiles: half the L2 bytes per MFMA of 128 x 128
   const int T = big ? 256 : 128;
   if ((kp & 15) || xrows < m || crows < k || (crows % T) != 0) return -2;
   if ((reinterpret_cast<uintptr_t>(XP) & 15) || (reinterpret_cast<uintptr_t>(CP) & 15)) return -5;
@@ -243,11 +266,18 @@ SRML_API int srml_nearest_centroid_split(const unsigned short* XP, long m, long 
   const int ct = (k + T - 1) / T;
   const long nb = rt * ct;
   if (nb > 0x7fffffffL) return -3;
-  if (big)
-    hipLaunchKernelGGL((nearest_centroid_split_kernel<256, 256, 2, 4, 1>), dim3((unsigned)nb), dim3(512), 0, stream,
+  static const int pf = getenv("SRML_SPLIT_PF") ? atoi(getenv("SRML_SPLIT_PF")) : 2;
+  if (big && pf == 2)
+    hipLaunchKernelGGL((nearest_centroid_split_kernel<256, 256, 2, 4, 1, 2>), dim3((unsigned)nb), dim3(512), 0, stream,
+                       XP, m, xrows, kp, CP, k, crows, cnorm, best, ct);
+  else if (big)
+    hipLaunchKernelGGL((nearest_centroid_split_kernel<256, 256, 2, 4, 1, 1>), dim3((unsigned)nb), dim3(512), 0, stream,
+                       XP, m, xrows, kp, CP, k, crows, cnorm, best, ct);
+  else if (pf == 2)
+    hipLaunchKernelGGL((nearest_centroid_split_kernel<128, 128, 2, 2, 2, 2>), dim3((unsigned)nb), dim3(256), 0, stream,
                        XP, m, xrows, kp, CP, k, crows, cnorm, best, ct);
   else
-    hipLaunchKernelGGL((nearest_centroid_split_kernel<128, 128, 2, 2, 2>), dim3((unsigned)nb), dim3(256), 0, stream,
+    hipLaunchKernelGGL((nearest_centroid_split_kernel<128, 128, 2, 2, 2, 1>), dim3((unsigned)nb), dim3(256), 0, stream,
                        XP, m, xrows, kp, CP, k, crows, cnorm, best, ct);
   return srml_status();
 }

@@ -46,6 +46,53 @@ def local_device(local_rank: Optional[int] = None) -> torch.device:
     return torch.device("cuda", local_rank % n)
 
 
+def _parse_cpulist(text: str) -> List[int]:
+    cpus: List[int] = []
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        if "-" in part:
+            a, b = part.split("-")
+            cpus.extend(range(int(a), int(b) + 1))
+        else:
+            cpus.append(int(part))
+    return cpus
+
+
+_numa_bound: dict = {}
+
+
+def bind_numa_local(device: torch.device) -> Optional[List[int]]:
+    """Restrict this process's CPU affinity to the cores on the GPU's own NUMA node.
+
+    Pinned host staging buffers are first-touch allocated on the node of the allocating thread,
+    so a process left on the far socket pushes every host->device byte of the ingest across the
+    inter-socket link as well as PCIe. Called before any staging buffer is allocated (worker
+    device pinning, bench start). ``SRML_NUMA_BIND=0`` disables it; a failure leaves affinity
+    unchanged. Returns the CPU list applied (None if nothing changed).
+    """
+    if device.type != "cuda" or os.environ.get("SRML_NUMA_BIND", "1") == "0" or not hasattr(os, "sched_setaffinity"):
+        return None
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    if idx in _numa_bound:
+        return _numa_bound[idx]
+    applied = None
+    try:
+        p = torch.cuda.get_device_properties(idx)
+        bdf = "%04x:%02x:%02x.0" % (int(getattr(p, "pci_domain_id", 0)), int(p.pci_bus_id), int(p.pci_device_id))
+        with open(f"/sys/bus/pci/devices/{bdf}/local_cpulist") as f:
+            local = set(_parse_cpulist(f.read()))
+        cur = os.sched_getaffinity(0)
+        want = sorted(local & cur)
+        if want and set(want) != cur:
+            os.sched_setaffinity(0, want)
+            applied = want
+    except Exception:  # noqa: BLE001 - topology info is best-effort
+        applied = None
+    _numa_bound[idx] = applied
+    return applied
+
+
 def spmd_active() -> bool:
     """True when the caller already runs one process per GPU inside a torch.distributed world."""
     return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
@@ -82,6 +129,8 @@ class WorkerContext:
     @staticmethod
     def single(device: Optional[torch.device] = None) -> "WorkerContext":
         dev = device if device is not None else local_device()
+        if dev.type == "cuda":
+            bind_numa_local(dev)
         return WorkerContext(0, 1, dev, Communicator(0, 1, dev))
 
     @staticmethod
@@ -90,6 +139,7 @@ class WorkerContext:
         dev = device if device is not None else local_device()
         if dev.type == "cuda":
             torch.cuda.set_device(dev)
+            bind_numa_local(dev)
         return WorkerContext(rank, size, dev, Communicator(rank, size, dev), partition_id=rank)
 
 

@@ -46,6 +46,9 @@ def _child(rank: int, world: int, port: int, use_gpu: bool, payload: bytes, q: A
         device = local_device(rank) if use_gpu else torch.device("cpu")
         if device.type == "cuda":
             torch.cuda.set_device(device)
+            from .context import bind_numa_local
+
+            bind_numa_local(device)
         dist.init_process_group(
             "nccl" if device.type == "cuda" else "gloo",
             rank=rank,

@@ -145,6 +145,9 @@ def init_barrier_group(task_ctx: Any, use_gpu: bool, timeout_s: float = 1800.0) 
     device = _task_device(task_ctx, use_gpu)
     if device.type == "cuda":
         torch.cuda.set_device(device)
+        from .context import bind_numa_local
+
+        bind_numa_local(device)
     store = dist.TCPStore(master_host, int(master_port), world, is_master=(rank == 0),
                           timeout=timedelta(seconds=timeout_s))
     dist.init_process_group("nccl" if device.type == "cuda" else "gloo", store=store, rank=rank, world_size=world,

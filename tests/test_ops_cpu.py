@@ -20,3 +20,12 @@ def test_split_bf16x3_exact_and_distance():
     ref_d = D.min(1).values
     assert torch.all(D[torch.arange(m), lab_s.long()] <= ref_d + 1e-4 * (1 + ref_d))
     torch.testing.assert_close(d_s.double(), ref_d, rtol=1e-4, atol=1e-3)
+
+
+def test_parse_cpulist_and_numa_bind_noop_on_cpu():
+    import torch
+
+    from spark_rapids_ml_nai_amd.parallel.context import _parse_cpulist, bind_numa_local
+
+    assert _parse_cpulist("0-3,8,10-11\n") == [0, 1, 2, 3, 8, 10, 11]
+    assert bind_numa_local(torch.device("cpu")) is None
