@@ -18,6 +18,8 @@ Initialisation:
 """
 from __future__ import annotations
 
+import os
+
 from typing import Any, Dict, Optional
 
 import numpy as np
@@ -158,7 +160,9 @@ def kmeans_fit(X: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext, k
         raise ValueError("Unsupported init mode %s" % init)
     C = C.double()
     tol2 = float(tol) ** 2
-    XP = ops.split_bf16x3(X) if _use_split(X, k) else None
+    # k > 256: 256 x 256 LDS-DMA kernel on the tiled plane layout (SRML_SPLIT_TILED=0: plain layout)
+    tiled = k > 256 and os.environ.get("SRML_SPLIT_TILED", "1") == "1"
+    XP = ops.split_bf16x3(X, tiled=tiled) if _use_split(X, k) else None
     n_iter = 0
     inertia = 0.0
     for it in range(max(0, max_iter)):

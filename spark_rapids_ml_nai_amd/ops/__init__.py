@@ -241,12 +241,22 @@ def nearest_centroid(X: torch.Tensor, C: torch.Tensor, xnorm: Optional[torch.Ten
     return labels, dist
 
 
-def split_bf16x3(X: torch.Tensor, row_multiple: int = 128) -> torch.Tensor:
+def split_bf16x3(X: torch.Tensor, row_multiple: int = 128, tiled: bool = False) -> torch.Tensor:
     """Exact three-way bf16 split of a fp32 matrix: planes P[3][rows_pad][kp] (bf16) with
     X = P[0] + P[1] + P[2] (each plane the round-to-nearest bf16 of the remaining residual),
-    rows padded to ``row_multiple`` and columns to a multiple of 16 with zeros."""
+    rows padded to ``row_multiple`` and columns to a multiple of 16 with zeros.
+
+    ``tiled`` (GPU only): the LDS-DMA kernel's layout P[3][rows_pad/256][kp/16][256][16] — each
+    (256-row tile, 16-wide k step) block one contiguous, bank-swizzled 8 KiB image."""
     m, n = X.shape
     kp = (n + 15) // 16 * 16
+    if tiled and X.is_cuda and X.dtype == torch.float32:
+        rows_pad = max(256, (m + 255) // 256 * 256)
+        X = X if X.stride(1) == 1 else X.contiguous()
+        P = torch.empty((3, rows_pad // 256, kp // 16, 256, 16), dtype=torch.bfloat16, device=X.device)
+        native.call("srml_split_bf16x3_tiled", X.data_ptr(), m, n, X.stride(0), kp, rows_pad, P.data_ptr(),
+                    native.stream(X.device))
+        return P
     rows_pad = max(row_multiple, (m + row_multiple - 1) // row_multiple * row_multiple)
     if not X.is_cuda or X.dtype != torch.float32:
         P = torch.zeros((3, rows_pad, kp), dtype=torch.bfloat16, device=X.device)
@@ -270,7 +280,8 @@ def nearest_centroid_split(XP: torch.Tensor, m: int, C: torch.Tensor, xnorm: tor
     Cf = C.float()
     if cnorm is None:
         cnorm = (Cf * Cf).sum(1)
-    CP = split_bf16x3(_c(Cf).to(XP.device), 256 if k > 256 else 128)
+    tiled = XP.dim() == 5
+    CP = split_bf16x3(_c(Cf).to(XP.device), 256 if (k > 256 or tiled) else 128, tiled=tiled)
     if not XP.is_cuda:
         Xh, Xm, Xl = (XP[p, :m].float() for p in range(3))
         Ch, Cm, Cl = (CP[p, :k].float() for p in range(3))
@@ -280,8 +291,12 @@ def nearest_centroid_split(XP: torch.Tensor, m: int, C: torch.Tensor, xnorm: tor
     cn = _c(cnorm.to(torch.float32))
     best = torch.full((m,), -1, dtype=torch.int64, device=XP.device)
     st = native.stream(XP.device)
-    native.call("srml_nearest_centroid_split", XP.data_ptr(), m, XP.shape[1], XP.shape[2], CP.data_ptr(), k,
-                CP.shape[1], cn.data_ptr(), best.data_ptr(), st)
+    if tiled:
+        native.call("srml_nearest_centroid_split_tiled", XP.data_ptr(), m, XP.shape[1] * 256, XP.shape[2] * 16,
+                    CP.data_ptr(), k, CP.shape[1] * 256, cn.data_ptr(), best.data_ptr(), st)
+    else:
+        native.call("srml_nearest_centroid_split", XP.data_ptr(), m, XP.shape[1], XP.shape[2], CP.data_ptr(), k,
+                    CP.shape[1], cn.data_ptr(), best.data_ptr(), st)
     labels = torch.empty(m, dtype=torch.int32, device=XP.device)
     dist = torch.empty(m, dtype=torch.float32, device=XP.device)
     native.call("srml_nn_finalize", best.data_ptr(), m, _c(xnorm.float()).data_ptr(), labels.data_ptr(),

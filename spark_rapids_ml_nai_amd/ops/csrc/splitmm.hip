@@ -68,6 +68,63 @@ __global__ __launch_bounds__(256) void split_kernel(const float* __restrict__ X,
   }
 }
 
+// Tiled + swizzled plane layout for the LDS-DMA kernel: P[3][rows_pad / 256][kp / 16][256][16],
+// i.e. every (256-row tile, 16-wide k step) block of a plane is one contiguous 8 KiB image, with
+// row r's 16-B half h stored at half h ^ ((r >> 3) & 1) (the bank-conflict-free fragment image).
+// A k step of a tile is then streamed with fully sequential 1 KiB LDS-DMA wave loads (every
+// 128-B line used whole) instead of 32-B pieces of 256 rows 6 KB apart.
+__global__ __launch_bounds__(256) void split_tiled_kernel(const float* __restrict__ X, long m, int n, long ld, int kp,
+                                                          long rows_pad, unsigned short* __restrict__ P) {
+  // one thread = one row's 16-wide k step (64 B of X in, one 32-B slot per plane out); a block =
+  // the 256 rows of one (tile, k step) image, so each block writes three contiguous 8 KiB images
+  const int ks_n = kp >> 4;
+  const long total = rows_pad * ks_n;
+  const long plane = rows_pad * (long)kp;
+  const bool vec = (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long img = i >> 8;  // = tile * ks_n + ks
+    const int rr = (int)(i & 255);
+    const long tile = img / ks_n;
+    const int c0 = (int)(img - tile * ks_n) * 16;
+    const long r = tile * 256 + rr;
+    float x[16];
+    if (vec && r < m && c0 + 16 <= n) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const floatx4 v = *reinterpret_cast<const floatx4*>(X + r * ld + c0 + 4 * q);
+        x[4 * q] = v[0]; x[4 * q + 1] = v[1]; x[4 * q + 2] = v[2]; x[4 * q + 3] = v[3];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) x[j] = (r < m && c0 + j < n) ? X[r * ld + c0 + j] : 0.f;
+    }
+    unsigned hw[8], mw[8], lw[8];
+#pragma unroll
+    for (int j = 0; j < 16; j += 2) {
+      unsigned h2[2], m2[2], l2[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        h2[u] = bf16_rn(x[j + u]);
+        const float r1 = x[j + u] - bf16_f(h2[u]);
+        m2[u] = bf16_rn(r1);
+        l2[u] = bf16_rn(r1 - bf16_f(m2[u]));
+      }
+      hw[j / 2] = h2[0] | (h2[1] << 16);
+      mw[j / 2] = m2[0] | (m2[1] << 16);
+      lw[j / 2] = l2[0] | (l2[1] << 16);
+    }
+    const int sw = (rr >> 3) & 1;  // logical half h lands at physical half h ^ sw
+    unsigned short* o = P + (img << 12) + rr * 16;
+    const unsigned* W[3] = {hw, mw, lw};
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      uintx4* d = reinterpret_cast<uintx4*>(o + p * plane);
+      d[sw] = uintx4{W[p][0], W[p][1], W[p][2], W[p][3]};
+      d[sw ^ 1] = uintx4{W[p][4], W[p][5], W[p][6], W[p][7]};
+    }
+  }
+}
+
 constexpr int SBK = 16;
 constexpr int ROWB = 24;  // padded LDS row: 16 bf16 + 8 pad = 48 B
 
@@ -81,6 +138,51 @@ struct SplitCfg {
   static constexpr int TN = BN / WN / 32;
   static_assert(BM == NT / 2 && BN == NT / 2, "staging assumes one A row and one B row per thread pair");
 };
+
+// Fused arg-min epilogue shared by the split kernels: d = ||c||^2 - 2 x.c per accumulator element,
+// row-wise arg-min over the wave's columns, then one packed 64-bit atomicMin per row.
+template <int BM, int BN, int WM, int WN>
+__device__ __forceinline__ void split_epilogue(const floatx16 (&acc)[BM / WM / 32][BN / WN / 32], long row0, int col0,
+                                               long m, int k, const float* __restrict__ cnorm,
+                                               unsigned long long* __restrict__ best, int wm, int wn, int li, int lk) {
+  constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+  // C/D layout of the 32x32 MFMA: col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5))
+  float cn[TN];
+  int cj[TN];
+#pragma unroll
+  for (int nt = 0; nt < TN; ++nt) {
+    cj[nt] = col0 + wn * (BN / WN) + nt * 32 + li;
+    cn[nt] = (cj[nt] < k) ? cnorm[cj[nt]] : 0.f;
+  }
+#pragma unroll
+  for (int mt = 0; mt < TM; ++mt) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float bv = __builtin_huge_valf();
+      int bi = 0x7fffffff;
+#pragma unroll
+      for (int nt = 0; nt < TN; ++nt) {
+        if (cj[nt] < k) {
+          const float d = fmaf(-2.f, acc[mt][nt][r], cn[nt]);
+          if (d < bv) { bv = d; bi = cj[nt]; }
+        }
+      }
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) {
+        const float ov = __shfl_xor(bv, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ov < bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+      }
+      if (li == 0 && bi != 0x7fffffff) {
+        const long row = row0 + wm * (BM / WM) + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        if (row < m) {
+          const unsigned long long key = ((unsigned long long)orderable(bv) << 32) | (unsigned)bi;
+          atomicMin(&best[row], key);
+        }
+      }
+    }
+  }
+}
 
 template <int BM, int BN>
 struct SplitStage {
@@ -199,42 +301,112 @@ __global__ __launch_bounds__(WM * WN * 64, MINB) void nearest_centroid_split_ker
     if (kt < nk) mma_step(0);  // odd step count: the last step's data is already in stage 0
   }
 
-  // epilogue (C/D layout of the 32x32 MFMA: col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5))
-  float cn[TN];
-  int cj[TN];
+  split_epilogue<BM, BN, WM, WN>(acc, row0, col0, m, k, cnorm, best, wm, wn, li, lk);
+}
+
+// ------------------------------------------------------------------------------------------
+// LDS-DMA variant (BM = BN = 256, 8 waves as 2 x 4): operand tiles go global -> LDS with
+// `global_load_lds_dwordx4` (no VGPR staging, no ds_write pass) into a 3-stage ring of unpadded
+// 32-B rows (3 stages x 6 planes x 256 x 32 B = 144 KiB), two k steps in flight across each raw
+// barrier with a counted vmcnt. One LDS-DMA wave-instruction writes 1 KiB lane-linearly (32 rows x
+// 32 B), so the bank-conflict swizzle (16-B half h of row r stored at half h ^ ((r >> 3) & 1))
+// is applied on the per-lane SOURCE address and undone on the fragment read
+// (cdna_hip_programming.md §5 "Async global->LDS copy", rule 21).
+typedef __attribute__((address_space(3))) void* lds_vptr;
+typedef __attribute__((address_space(1))) void* gbl_vptr;
+
+// TILED: operands in the split_tiled_kernel layout (contiguous, pre-swizzled 8 KiB k-step images).
+template <bool TILED>
+__global__ __launch_bounds__(512, 1) void nearest_centroid_split_glds_kernel(
+    const unsigned short* __restrict__ XP, long m, long xrows, int kp, const unsigned short* __restrict__ CP, int k,
+    long crows, const float* __restrict__ cnorm, unsigned long long* __restrict__ best, int n_ctiles) {
+  constexpr int BM = 256, BN = 256, WM = 2, WN = 4, TM = 4, TN = 2, NS = 3;
+  __shared__ __attribute__((aligned(1024))) unsigned short lds[NS][6][256][16];
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const long rtile = bid / n_ctiles;
+  const int ctile = bid % n_ctiles;
+  const long row0 = rtile * BM;
+  const int col0 = ctile * BN;
+  const int t = threadIdx.x;
+  const int lane = t & 63, wid = t >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int li = lane & 31, lk = lane >> 5;
+  const long xplane = xrows * (long)kp, cplane = crows * (long)kp;
+
+  // this wave's 6 staging chunks per stage: chunk c = wid * 6 + i -> plane q = c / 8, rows 32 (c % 8) ..
+  const unsigned short* src[6];
+  int dst_off[6];  // element offset of the chunk inside one stage
 #pragma unroll
-  for (int nt = 0; nt < TN; ++nt) {
-    cj[nt] = col0 + wn * (BN / WN) + nt * 32 + li;
-    cn[nt] = (cj[nt] < k) ? cnorm[cj[nt]] : 0.f;
+  for (int i = 0; i < 6; ++i) {
+    const int c = wid * 6 + i;
+    const int q = c >> 3, j = c & 7;
+    const int r = 32 * j + (lane >> 1);
+    const int lh = (lane & 1) ^ ((lane >> 4) & 1);  // logical half stored at physical half (lane & 1)
+    if (TILED) {  // the image is already swizzled: lane-linear 16-B pieces of one contiguous 1 KiB
+      const int ks_n = kp / SBK;
+      if (q < 3) src[i] = XP + q * xplane + ((rtile * ks_n) << 12) + 512 * j + lane * 8;
+      else src[i] = CP + (q - 3) * cplane + (((long)ctile * ks_n) << 12) + 512 * j + lane * 8;
+    } else if (q < 3) {
+      long xr = row0 + r;
+      if (xr >= xrows) xr = xrows - 1;  // clamp: those rows are never reported
+      src[i] = XP + q * xplane + xr * kp + 8 * lh;
+    } else {
+      src[i] = CP + (q - 3) * cplane + (long)(col0 + r) * kp + 8 * lh;  // crows % 256 == 0
+    }
+    dst_off[i] = (q * 256 + 32 * j) * 16;
   }
+  auto issue = [&](int kt, int stage) {
+    unsigned short* base = &lds[stage][0][0][0];
 #pragma unroll
-  for (int mt = 0; mt < TM; ++mt) {
+    for (int i = 0; i < 6; ++i) {
+      __builtin_amdgcn_global_load_lds((gbl_vptr)(src[i] + (TILED ? ((long)kt << 12) : (long)kt * SBK)),
+                                       (lds_vptr)(base + dst_off[i]), 16, 0, 0);
+    }
+  };
+
+  floatx16 acc[TM][TN];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      float bv = __builtin_huge_valf();
-      int bi = 0x7fffffff;
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  const int ph = lk ^ ((li >> 3) & 1);  // physical half of this lane's fragment
+  const int nk = kp / SBK;
+  issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  int stage = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // step kt landed for every wave; every wave finished step kt - 1
+    if (kt + 2 < nk) issue(kt + 2, stage == 0 ? 2 : stage - 1);
+    bf16x8 fb[3][TN];
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int nt = 0; nt < TN; ++nt)
+        fb[p][nt] = *reinterpret_cast<const bf16x8*>(&lds[stage][3 + p][wn * (BN / WN) + nt * 32 + li][8 * ph]);
+#pragma unroll
+    for (int mt = 0; mt < TM; ++mt) {
+      bf16x8 fa[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        fa[p] = *reinterpret_cast<const bf16x8*>(&lds[stage][p][wm * (BM / WM) + mt * 32 + li][8 * ph]);
 #pragma unroll
       for (int nt = 0; nt < TN; ++nt) {
-        if (cj[nt] < k) {
-          const float d = fmaf(-2.f, acc[mt][nt][r], cn[nt]);
-          if (d < bv) { bv = d; bi = cj[nt]; }
-        }
-      }
-#pragma unroll
-      for (int o = 1; o < 32; o <<= 1) {
-        const float ov = __shfl_xor(bv, o, 64);
-        const int oi = __shfl_xor(bi, o, 64);
-        if (ov < bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
-      }
-      if (li == 0 && bi != 0x7fffffff) {
-        const long row = row0 + wm * (BM / WM) + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
-        if (row < m) {
-          const unsigned long long key = ((unsigned long long)orderable(bv) << 32) | (unsigned)bi;
-          atomicMin(&best[row], key);
-        }
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[0][nt], acc[mt][nt], 0, 0, 0);
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1][nt], acc[mt][nt], 0, 0, 0);
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[2][nt], acc[mt][nt], 0, 0, 0);
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[0][nt], acc[mt][nt], 0, 0, 0);
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[1][nt], acc[mt][nt], 0, 0, 0);
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0][nt], acc[mt][nt], 0, 0, 0);
       }
     }
+    stage = stage == 2 ? 0 : stage + 1;
   }
+  split_epilogue<BM, BN, WM, WN>(acc, row0, col0, m, k, cnorm, best, wm, wn, li, lk);
 }
 }  // namespace
 
@@ -267,7 +439,11 @@ SRML_API int srml_nearest_centroid_split(const unsigned short* XP, long m, long 
   const long nb = rt * ct;
   if (nb > 0x7fffffffL) return -3;
   static const int pf = getenv("SRML_SPLIT_PF") ? atoi(getenv("SRML_SPLIT_PF")) : 2;
-  if (big && pf == 2)
+  static const int glds = getenv("SRML_SPLIT_GLDS") ? atoi(getenv("SRML_SPLIT_GLDS")) : 0;
+  if (big && glds)
+    hipLaunchKernelGGL(nearest_centroid_split_glds_kernel<false>, dim3((unsigned)nb), dim3(512), 0, stream, XP, m, xrows, kp,
+                       CP, k, crows, cnorm, best, ct);
+  else if (big && pf == 2)
     hipLaunchKernelGGL((nearest_centroid_split_kernel<256, 256, 2, 4, 1, 2>), dim3((unsigned)nb), dim3(512), 0, stream,
                        XP, m, xrows, kp, CP, k, crows, cnorm, best, ct);
   else if (big)
@@ -279,5 +455,34 @@ SRML_API int srml_nearest_centroid_split(const unsigned short* XP, long m, long 
   else
     hipLaunchKernelGGL((nearest_centroid_split_kernel<128, 128, 2, 2, 2, 1>), dim3((unsigned)nb), dim3(256), 0, stream,
                        XP, m, xrows, kp, CP, k, crows, cnorm, best, ct);
+  return srml_status();
+}
+
+// Tiled layout (split_tiled_kernel): P = [3][rows_pad / 256][kp / 16][256][16], rows_pad % 256 == 0.
+SRML_API int srml_split_bf16x3_tiled(const float* X, long m, int n, long ld, int kp, long rows_pad, unsigned short* P,
+                                     hipStream_t stream) {
+  if (rows_pad <= 0) return 0;
+  if ((kp & 15) || kp < n || rows_pad < m || (rows_pad & 255)) return -2;
+  if ((reinterpret_cast<uintptr_t>(P) & 15) != 0) return -5;
+  long total = rows_pad * (long)(kp / 4);
+  long blocks = (total + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(split_tiled_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, X, m, n, ld, kp, rows_pad, P);
+  return srml_status();
+}
+
+// Nearest centroid on tiled planes of X (xrows % 256 == 0) and of the centroids (crows % 256 == 0).
+SRML_API int srml_nearest_centroid_split_tiled(const unsigned short* XP, long m, long xrows, int kp,
+                                               const unsigned short* CP, int k, long crows, const float* cnorm,
+                                               unsigned long long* best, hipStream_t stream) {
+  if (m <= 0 || k <= 0) return 0;
+  if ((kp & 15) || xrows < m || crows < k || (crows & 255) || (xrows & 255)) return -2;
+  if ((reinterpret_cast<uintptr_t>(XP) & 15) || (reinterpret_cast<uintptr_t>(CP) & 15)) return -5;
+  const long rt = (m + 255) / 256;
+  const int ct = (k + 255) / 256;
+  const long nb = rt * ct;
+  if (nb > 0x7fffffffL) return -3;
+  hipLaunchKernelGGL((nearest_centroid_split_glds_kernel<true>), dim3((unsigned)nb), dim3(512), 0, stream, XP, m,
+                     xrows, kp, CP, k, crows, cnorm, best, (int)ct);
   return srml_status();
 }

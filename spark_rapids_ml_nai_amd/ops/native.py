@@ -42,6 +42,8 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_nn_finalize": (_P, _L, _P, _P, _P, _P),
     "srml_split_bf16x3": (_P, _L, _I, _L, _I, _L, _P, _P),
     "srml_nearest_centroid_split": (_P, _L, _L, _I, _P, _I, _L, _P, _P, _P),
+    "srml_split_bf16x3_tiled": (_P, _L, _I, _L, _I, _L, _P, _P),
+    "srml_nearest_centroid_split_tiled": (_P, _L, _L, _I, _P, _I, _L, _P, _P, _P),
     "srml_kmeans_accumulate_f32": (_P, _L, _I, _L, _P, _I, _P, _P, _P, _P),
     "srml_kmeans_accumulate_sorted_f32": (_P, _L, _I, _L, _P, _P, _P, _P),
     "srml_knn_f32": (_P, _L, _I, _L, _P, _L, _L, _P, _I, _I, _P, _P, ctypes.c_longlong, _P),

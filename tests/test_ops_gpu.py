@@ -499,3 +499,19 @@ def test_uvm_managed_ingest(gpu_device, monkeypatch):
     t = managed_empty((1000,), torch.float32, gpu_device)
     t.fill_(2.0)
     assert float(t.sum()) == 2000.0
+
+
+@pytest.mark.parametrize("m,n,k", [(1024, 3000, 257), (4099, 130, 1000), (300, 40, 5), (70000, 200, 600)])
+def test_nearest_centroid_split_tiled(gpu_device, m, n, k):
+    """LDS-DMA kernel on the tiled plane layout == the fp32 reference arg-min (ties within 1e-5)."""
+    X = _rand(m, n, gpu_device, seed=11)
+    C = _rand(k, n, gpu_device, seed=12)
+    xnorm = ops.row_sqnorm(X)
+    XP = ops.split_bf16x3(X, tiled=True)
+    assert XP.dim() == 5
+    lab, d2 = ops.nearest_centroid_split(XP, m, C, xnorm)
+    D = torch.cdist(X.double(), C.double()) ** 2
+    ref = D.min(1).values
+    got = D.gather(1, lab.long().view(-1, 1)).view(-1)
+    assert (got - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+    torch.testing.assert_close(d2.double(), ref, rtol=1e-5, atol=1e-3)

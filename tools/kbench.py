@@ -70,8 +70,9 @@ def main():
     if want("nearest_split"):
         C = torch.randn(a.k, a.n, device=dev, generator=g)
         xn = ops.row_sqnorm(X)
-        t0 = timeit(lambda: ops.split_bf16x3(X), 2)
-        P = ops.split_bf16x3(X)
+        tiled = os.environ.get("SRML_SPLIT_TILED", "1") == "1"
+        t0 = timeit(lambda: ops.split_bf16x3(X, tiled=tiled), 2)
+        P = ops.split_bf16x3(X, tiled=tiled)
         t = timeit(lambda: ops.nearest_centroid_split(P, a.m, C, xn), 3)
         res["nearest_centroid_split"] = {"ms": t, "split_X_ms": t0,
                                          "TFLOP/s(fp32-equiv)": 2 * a.m * a.k * a.n / t / 1e9,
