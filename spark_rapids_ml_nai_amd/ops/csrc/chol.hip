@@ -118,6 +118,89 @@ __global__ __launch_bounds__(1024) void potrs_kernel(const double* __restrict__ 
   for (int i = threadIdx.x; i < n; i += blockDim.x) b[i] = x[i];
 }
 
+// Blocked triangular solves (L L^T x = b) in one workgroup: 64-row blocks; the off-diagonal part
+// of each block is a coalesced GEMV by all 16 waves, the 64 x 64 diagonal block is staged in LDS
+// and solved by ONE wave with scalar broadcasts (no barrier per row). Replaces a row-at-a-time
+// loop with two barriers per row (~9 ms at n = 3000).
+constexpr int TS_B = 64;
+
+__global__ __launch_bounds__(1024) void potrs_blocked_kernel(const double* __restrict__ L, int n, long lda,
+                                                             double* __restrict__ b) {
+  extern __shared__ double x[];               // n
+  __shared__ double blk[TS_B][TS_B + 1];      // diagonal block
+  __shared__ double part[16][TS_B];           // partial sums of the backward GEMV
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  for (int i = t; i < n; i += blockDim.x) x[i] = b[i];
+  __syncthreads();
+  auto bcast = [](double v, int src) {
+    const long long bits = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(bits & 0xffffffffLL), src);
+    const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), src);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+  };
+  // forward: L z = b
+  for (int j0 = 0; j0 < n; j0 += TS_B) {
+    const int nb = n - j0 < TS_B ? n - j0 : TS_B;
+    // x[j0 + r] -= L[j0 + r, 0:j0] . x[0:j0]: wave w takes rows r = w, w + 16, ...
+    for (int r = wid; r < nb; r += 16) {
+      const double* row = L + (long)(j0 + r) * lda;
+      double s = 0.0;
+      for (int c = lane; c < j0; c += 64) s = fma(row[c], x[c], s);
+      s = wave_sum(s);
+      if (lane == 0) x[j0 + r] -= s;
+    }
+    for (int e = t; e < nb * nb; e += blockDim.x) {
+      const int r = e / nb, c = e - r * nb;
+      blk[r][c] = L[(long)(j0 + r) * lda + j0 + c];
+    }
+    __syncthreads();
+    if (wid == 0) {
+      double xr = lane < nb ? x[j0 + lane] : 0.0;
+      for (int c = 0; c < nb; ++c) {
+        const double xc = bcast(xr, c) / blk[c][c];
+        if (lane == c) xr = xc;
+        if (lane > c && lane < nb) xr = fma(-blk[lane][c], xc, xr);
+      }
+      if (lane < nb) x[j0 + lane] = xr;
+    }
+    __syncthreads();
+  }
+  // backward: L^T x = z
+  const int last0 = ((n - 1) / TS_B) * TS_B;
+  for (int j0 = last0; j0 >= 0; j0 -= TS_B) {
+    const int nb = n - j0 < TS_B ? n - j0 : TS_B;
+    // x[j0 + i] -= sum_{j >= j0 + nb} L[j][j0 + i] x[j]: lane = column i, waves split the rows j
+    {
+      double s = 0.0;
+      if (lane < nb)
+        for (int j = j0 + nb + wid; j < n; j += 16) s = fma(L[(long)j * lda + j0 + lane], x[j], s);
+      part[wid][lane] = s;
+    }
+    for (int e = t; e < nb * nb; e += blockDim.x) {
+      const int r = e / nb, c = e - r * nb;
+      blk[r][c] = L[(long)(j0 + r) * lda + j0 + c];
+    }
+    __syncthreads();
+    if (wid == 0) {
+      double xr = 0.0;
+      if (lane < nb) {
+        double s = 0.0;
+#pragma unroll
+        for (int w = 0; w < 16; ++w) s += part[w][lane];
+        xr = x[j0 + lane] - s;
+      }
+      for (int c = nb - 1; c >= 0; --c) {
+        const double xc = bcast(xr, c) / blk[c][c];
+        if (lane == c) xr = xc;
+        if (lane < c) xr = fma(-blk[c][lane], xc, xr);
+      }
+      if (lane < nb) x[j0 + lane] = xr;
+    }
+    __syncthreads();
+  }
+  for (int i = t; i < n; i += blockDim.x) b[i] = x[i];
+}
+
 // A: n x n (row-major, symmetric), b, l1, l2: n. w: in/out (initial guess). Result iterations in *iters.
 __global__ __launch_bounds__(1024) void cd_gram_kernel(const double* __restrict__ A, int n, long lda,
                                                        const double* __restrict__ b, const double* __restrict__ l1,
@@ -325,6 +408,12 @@ SRML_API int srml_potrs_f64(const double* L, int n, long lda, double* b, hipStre
   if (n <= 0) return 0;
   const size_t lds = (size_t)n * sizeof(double);
   if (lds > 150 * 1024) return -9;
+  if (lds <= 110 * 1024) {  // + 41 KB static (diagonal block, partial sums)
+    (void)hipFuncSetAttribute((const void*)potrs_blocked_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    hipLaunchKernelGGL(potrs_blocked_kernel, dim3(1), dim3(1024), lds, stream, L, n, lda, b);
+    return srml_status();
+  }
   (void)hipFuncSetAttribute((const void*)potrs_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(potrs_kernel, dim3(1), dim3(1024), lds, stream, L, n, lda, b);
   return srml_status();

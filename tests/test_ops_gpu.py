@@ -406,7 +406,7 @@ def test_umap_epoch_negative_samples(gpu_device):
     assert emb.std(0).sum().item() > before
 
 
-@pytest.mark.parametrize("n", [1, 5, 64, 65, 200, 1000])
+@pytest.mark.parametrize("n", [1, 5, 64, 65, 129, 200, 1000, 3000])
 def test_spd_solve(gpu_device, n):
     g = torch.Generator().manual_seed(n)
     M = torch.randn(n, n + 3, generator=g, dtype=torch.float64)
