@@ -97,7 +97,10 @@ def main() -> None:
             barrier_sync()
             t0 = time.perf_counter()
             for _ in range(args.steps):
+                ts = time.perf_counter()
                 model = est.fit(df)
+                if os.environ.get("SRML_BENCH_VERBOSE") == "1":
+                    print(f"[bench] {name} step {time.perf_counter() - ts:.4f} s", file=sys.stderr)
             barrier_sync()
             dt = time.perf_counter() - t0
             if world > 1:

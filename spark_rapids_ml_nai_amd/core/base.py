@@ -362,7 +362,11 @@ def _fit_worker(ctx: WorkerContext, payload: Tuple[HostPartition, Callable, Dict
     desc = PartitionDescriptor.build(ctx, hp.rows, hp.n_cols)
     inp = FitInput(X=X, y=y, cols=hp.cols, desc=desc, host=hp, stream=streamed)
     _maybe_inject_fault(ctx, "fit")
-    return fit_fn(inp, ctx, params)
+    out = fit_fn(inp, ctx, params)
+    if ctx.is_gpu and os.environ.get("SRML_FIT_DEVICE_SYNC", "1") == "1":
+        # leave the device idle (copy stream included) before the task returns
+        torch.cuda.synchronize(ctx.device)
+    return out
 
 
 def _maybe_inject_fault(ctx: WorkerContext, stage: str) -> None:

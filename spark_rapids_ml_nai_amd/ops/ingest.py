@@ -8,6 +8,8 @@ the host fills chunk i+1 (two buffers, event-guarded reuse). Small arrays take t
 """
 from __future__ import annotations
 
+import os
+
 import warnings
 from typing import Any, Optional
 
@@ -99,6 +101,30 @@ def host_to_device(X: Any, device: torch.device, dtype: Optional[torch.dtype] = 
     return _dense_to_device(a, device, dtype if a.dtype.kind == "f" else None)
 
 
+_copy_streams: dict = {}
+
+
+def copy_stream(device: torch.device) -> "torch.cuda.Stream":
+    """One persistent, HIGH-priority H2D stream per device.
+
+    HIP maps streams onto a few hardware queues (GPU_MAX_HW_QUEUES, 4 by default) round-robin
+    per priority level. A fresh normal-priority pool stream per ingest landed on the compute
+    stream's queue about one fit in four: the chunk copies then serialised behind the statistics
+    kernels instead of overlapping them (+0.11 s on a 12 GB LinearRegression fit). A
+    high-priority stream never shares a queue with normal-priority compute.
+    ``SRML_COPY_STREAM=new`` restores a fresh normal-priority pool stream per ingest."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    if os.environ.get("SRML_COPY_STREAM", "persistent") == "new":
+        return torch.cuda.Stream(device)
+    st = _copy_streams.get(idx)
+    if st is None:
+        hi, _lo = torch.cuda.Stream.priority_range()
+        lo_num = min(hi, _lo)  # numerically lower = higher priority
+        st = torch.cuda.Stream(device, priority=lo_num)
+        _copy_streams[idx] = st
+    return st
+
+
 class StreamedRows:
     """Row-chunked asynchronous H2D of a host matrix that lets the first pass over the data run
     while the rest of it is still crossing PCIe.
@@ -112,7 +138,9 @@ class StreamedRows:
     """
 
     def __init__(self, host: np.ndarray, device: torch.device, dtype: Optional[torch.dtype] = None,
-                 chunk_bytes: int = 96 << 20) -> None:
+                 chunk_bytes: int = 0) -> None:
+        if chunk_bytes <= 0:
+            chunk_bytes = int(os.environ.get("SRML_INGEST_CHUNK_MB", "96")) << 20
         with warnings.catch_warnings():
             warnings.simplefilter("ignore", UserWarning)
             t = torch.from_numpy(np.ascontiguousarray(host))
@@ -127,7 +155,7 @@ class StreamedRows:
         self.chunk_rows = max(256, int(chunk_bytes // row_bytes))
         cur = torch.cuda.current_stream(device)
         self.X = torch.empty(t.shape, dtype=t.dtype, device=device)
-        self._copy = torch.cuda.Stream(device)
+        self._copy = copy_stream(device)
         self._copy.wait_stream(cur)
         self.X.record_stream(self._copy)
         self.bounds = []
