@@ -149,6 +149,99 @@ def _impurity_np(tot: np.ndarray, crit: int) -> float:
     return float(-(nz * np.log2(nz)).sum())
 
 
+def _leaf_values_np(tot: np.ndarray, regression: bool) -> np.ndarray:
+    """Vectorised ``_leaf_value`` over segments: (L, 1) means or (L, S) class probabilities."""
+    if regression:
+        n = tot[:, 0]
+        return np.where(n > 0, tot[:, 1] / np.where(n > 0, n, 1.0), 0.0)[:, None]
+    s = tot.sum(1, keepdims=True)
+    return np.where(s > 0, tot / np.where(s > 0, s, 1.0), 0.0)
+
+
+def _impurities_np(tot: np.ndarray, crit: int) -> np.ndarray:
+    """Vectorised ``_impurity_np`` over segments."""
+    if crit == 2:
+        n = tot[:, 0]
+        safe = np.where(n > 0, n, 1.0)
+        mu = tot[:, 1] / safe
+        return np.where(n > 0, np.maximum(tot[:, 2] / safe - mu * mu, 0.0), 0.0)
+    n = tot.sum(1)
+    safe = np.where(n > 0, n, 1.0)[:, None]
+    pr = tot / safe
+    if crit == 0:
+        v = 1.0 - (pr * pr).sum(1)
+    else:
+        with np.errstate(divide="ignore", invalid="ignore"):
+            v = -np.where(pr > 0, pr * np.log2(np.where(pr > 0, pr, 1.0)), 0.0).sum(1)
+    return np.where(n > 0, v, 0.0)
+
+
+class _ForestRecords:
+    """Level-wise node records of a forest grown level-synchronously, assembled into ``Tree``s
+    once at the end (per-node Python bookkeeping cost ~10 us/node: 0.25 s for a 50-tree,
+    depth-13 forest)."""
+
+    def __init__(self, n_trees: int) -> None:
+        self.nn = np.ones(n_trees, dtype=np.int64)  # nodes per tree (roots = node 0)
+        self.seg: List[Tuple[np.ndarray, ...]] = []    # (tree, nid, value (L, V), count, impurity)
+        self.split: List[Tuple[np.ndarray, ...]] = []  # (tree, nid, feature, threshold, gain, left, right)
+        self.depth = 0
+
+    def add_children(self, t_i: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+        """Left/right ids for splits of trees ``t_i`` (in order), numbered like sequential
+        ``add_node`` calls: per tree, in order of appearance."""
+        order_t = np.argsort(t_i, kind="stable")
+        ts = t_i[order_t]
+        starts = np.r_[0, np.nonzero(np.diff(ts))[0] + 1]
+        lens = np.diff(np.r_[starts, len(ts)])
+        rank_sorted = np.arange(len(ts)) - np.repeat(starts, lens)
+        rank = np.empty_like(rank_sorted)
+        rank[order_t] = rank_sorted
+        left = self.nn[t_i] + 2 * rank
+        np.add.at(self.nn, t_i, 2)
+        return left, left + 1
+
+    def build(self) -> List[Tree]:
+        T = len(self.nn)
+        V = self.seg[0][2].shape[1] if self.seg else 1
+        trees = []
+        seg = [np.concatenate([r[i] for r in self.seg]) for i in range(5)] if self.seg else None
+        spl = [np.concatenate([r[i] for r in self.split]) for i in range(7)] if self.split else None
+        seg_by = np.argsort(seg[0], kind="stable") if seg is not None else None
+        seg_bounds = np.searchsorted(seg[0][seg_by], np.arange(T + 1)) if seg is not None else None
+        spl_by = np.argsort(spl[0], kind="stable") if spl is not None else None
+        spl_bounds = np.searchsorted(spl[0][spl_by], np.arange(T + 1)) if spl is not None else None
+        for t in range(T):
+            nn = int(self.nn[t])
+            feature = np.full(nn, -1, dtype=np.int64)
+            threshold = np.zeros(nn)
+            left = np.full(nn, -1, dtype=np.int64)
+            right = np.full(nn, -1, dtype=np.int64)
+            value = np.zeros((nn, V))
+            impurity = np.zeros(nn)
+            gain = np.zeros(nn)
+            count = np.zeros(nn)
+            if seg is not None:
+                sel = seg_by[seg_bounds[t]: seg_bounds[t + 1]]
+                nid = seg[1][sel]
+                value[nid] = seg[2][sel]
+                count[nid] = seg[3][sel]
+                impurity[nid] = seg[4][sel]
+            if spl is not None:
+                sel = spl_by[spl_bounds[t]: spl_bounds[t + 1]]
+                nid = spl[1][sel]
+                feature[nid] = spl[2][sel]
+                threshold[nid] = spl[3][sel]
+                gain[nid] = spl[4][sel]
+                left[nid] = spl[5][sel]
+                right[nid] = spl[6][sel]
+            tr = Tree(feature=feature.tolist(), threshold=threshold.tolist(), left=left.tolist(),
+                      right=right.tolist(), value=value.tolist(), impurity=impurity.tolist(), gain=gain.tolist(),
+                      count=count.tolist(), depth=self.depth)
+            trees.append(tr)
+        return trees
+
+
 def _node_stats(yv: torch.Tensor, idx: torch.Tensor, wpos: torch.Tensor, bounds: torch.Tensor, S: int,
                 regression: bool) -> torch.Tensor:
     return ops.rf_node_stats(idx, wpos, yv, bounds, S, regression)
@@ -176,7 +269,7 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
     nf = int(p["_nf"])
     max_leaves = int(p.get("max_leaves", -1))
     yv = y.float().contiguous()
-    trees = [Tree() for _ in range(n_trees)]
+    rec = _ForestRecords(n_trees)
     # bootstrap multiplicities per tree (Spark: Poisson(subsamplingRate) bagging); positions of
     # all trees are concatenated: segment = (tree, node), rows stay ascending inside a segment
     idx_l, w_l, cnt0 = [], [], []
@@ -194,7 +287,7 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
     wpos = torch.cat(w_l).contiguous()
     del idx_l, w_l
     seg_tree = np.arange(n_trees, dtype=np.int64)
-    seg_nid = np.array([t.add_node() for t in trees], dtype=np.int64)
+    seg_nid = np.zeros(n_trees, dtype=np.int64)  # every tree's root is node 0
     counts = np.asarray(cnt0, dtype=np.int64)
     bounds_h = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
     bounds = torch.from_numpy(bounds_h).to(dev)
@@ -208,17 +301,11 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
     depth = 0
     while len(seg_tree):
         L = len(seg_tree)
-        tot_h = tot.cpu().numpy()
+        tot_h = tot.cpu().numpy().astype(np.float64)
         wsum = tot_h[:, 0] if regression else tot_h.sum(1)
-        imps = np.empty(L)
-        for j in range(L):
-            t = trees[seg_tree[j]]
-            nid = int(seg_nid[j])
-            t.value[nid] = _leaf_value(tot_h[j], regression)
-            t.count[nid] = float(wsum[j])
-            imps[j] = t.impurity[nid] = _impurity_np(tot_h[j], crit)
-        for t in trees:
-            t.depth = depth
+        imps = _impurities_np(tot_h, crit)
+        rec.seg.append((seg_tree.copy(), seg_nid.copy(), _leaf_values_np(tot_h, regression), wsum.copy(), imps))
+        rec.depth = depth
         if depth >= max_depth:
             break
         cand = np.nonzero((wsum >= max(min_split, 2 * min_leaf)) & (imps > 0.0))[0]
@@ -288,34 +375,25 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
         node_feature = np.full(L, -1, dtype=np.int32)
         node_bin = np.zeros(L, dtype=np.int32)
         child_base = np.zeros(L, dtype=np.int32)
-        new_tree: List[int] = []
-        new_nid: List[int] = []
-        sel_rows: List[int] = []  # index into the concatenated winning histograms (classification)
-        k = 0
-        sel_i = -1
-        for ci in order:
-            sel_i += 1
-            if keep_set is not None and int(ci) not in keep_set:
-                continue
-            j = int(cand[ci])
-            t_i = int(seg_tree[j])
-            t = trees[t_i]
-            nid = int(seg_nid[j])
-            b = int(out_all[ci, 2])
-            f = int(feat_all[ci])
-            t.feature[nid] = f
-            t.threshold[nid] = float(edges_h[f, b])
-            t.gain[nid] = float(out_all[ci, 0])
-            lnode, rnode = t.add_node(), t.add_node()
-            t.left[nid], t.right[nid] = lnode, rnode
-            new_tree += [t_i, t_i]
-            new_nid += [lnode, rnode]
-            node_feature[j] = f
-            node_bin[j] = b
-            child_base[j] = 2 * k
-            sel_rows.append(sel_i)
-            k += 1
-            n_leaves[t_i] += 1
+        sel_mask = np.ones(order.size, dtype=bool) if keep_set is None else \
+            np.fromiter((int(ci) in keep_set for ci in order), dtype=bool, count=order.size)
+        ci_sel = order[sel_mask]
+        sel_rows = np.nonzero(sel_mask)[0]  # index into the concatenated winning histograms (classification)
+        k = int(ci_sel.size)
+        if k:
+            j_sel = cand[ci_sel]
+            t_sel = seg_tree[j_sel]
+            b_sel = out_all[ci_sel, 2].astype(np.int64)
+            f_sel = feat_all[ci_sel].astype(np.int64)
+            lnode, rnode = rec.add_children(t_sel)
+            rec.split.append((t_sel, seg_nid[j_sel], f_sel, edges_h[f_sel, b_sel], out_all[ci_sel, 0].astype(np.float64),
+                              lnode, rnode))
+            node_feature[j_sel] = f_sel
+            node_bin[j_sel] = b_sel
+            child_base[j_sel] = 2 * np.arange(k, dtype=np.int32)
+            np.add.at(n_leaves, t_sel, 1)
+            new_tree = np.repeat(t_sel, 2)
+            new_nid = np.stack([lnode, rnode], 1).reshape(-1)
         if k == 0:
             break
         # ---- route + stable partition into child segments ----
@@ -333,7 +411,7 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
             tot = _node_stats(yv, idx, wpos, bounds, S, regression)
         else:
             # children totals = prefix of each winning histogram up to its split bin
-            sel = torch.cat(res_sel, 0)[torch.tensor(sel_rows, device=dev)]  # (k, B, S)
+            sel = torch.cat(res_sel, 0)[torch.from_numpy(sel_rows).to(dev)]  # (k, B, S)
             split_bin = torch.from_numpy(node_bin[node_feature >= 0].astype(np.int64)).to(dev)
             # node_feature >= 0 segments are in cand order == split order
             left = sel.cumsum(1)[torch.arange(k, device=dev), split_bin]
@@ -347,7 +425,7 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
         seg_tree = np.asarray(new_tree, dtype=np.int64)
         seg_nid = np.asarray(new_nid, dtype=np.int64)
         depth += 1
-    return trees
+    return rec.build()
 
 
 def grow_tree(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: WorkerContext, gen: torch.Generator,
