@@ -180,26 +180,52 @@ def _spectral_host(rows: np.ndarray, cols: np.ndarray, vals: np.ndarray, n: int,
     return v[:, order]
 
 
+def _cholqr2(Y: torch.Tensor) -> torch.Tensor:
+    """Orthonormal basis of a tall-skinny device block: two CholeskyQR passes (fp64 Gram on the
+    device, p x p Cholesky on the host); Householder QR only if the Gram is numerically singular."""
+    W = Y
+    for _ in range(2):
+        Wd = W.double()
+        G = (Wd.T @ Wd).cpu().numpy()
+        try:
+            L = np.linalg.cholesky((G + G.T) * 0.5)
+        except np.linalg.LinAlgError:
+            return torch.linalg.qr(Y)[0]
+        d = np.diag(L)
+        if d.min() <= 1e-6 * d.max():
+            return torch.linalg.qr(Y)[0]
+        Rinv = torch.from_numpy(np.linalg.solve(L, np.eye(L.shape[0])).T.copy()).to(Y.device)
+        W = (Wd @ Rinv).to(Y.dtype)
+    return W
+
+
 def _spectral_device(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n: int, dim: int, seed: int,
                      iters: int = 300) -> torch.Tensor:
+    """Top eigenvectors of D^-1/2 A D^-1/2 by subspace iteration: the SpMM is the in-tree CSR
+    kernel (``ops.csr_spmm``, one row group per graph row), orthonormalisation is CholeskyQR2."""
+    from ..core.base import CSR
+
     dev = vals.device
     deg = torch.zeros(n, dtype=torch.float64, device=dev).index_add_(0, rows.long(), vals.double())
     dinv = 1.0 / torch.sqrt(deg.clamp_min(1e-30))
     mv = (dinv[rows.long()] * vals.double() * dinv[cols.long()]).float()
-    M = torch.sparse_coo_tensor(torch.stack([rows.long(), cols.long()]), mv, (n, n)).coalesce().to_sparse_csr()
+    Mt = torch.sparse_coo_tensor(torch.stack([rows.long(), cols.long()]), mv, (n, n)).coalesce().to_sparse_csr()
+    M = CSR(indptr=Mt.crow_indices().to(torch.int64).contiguous(), indices=Mt.col_indices().to(torch.int32).contiguous(),
+            data=Mt.values().contiguous(), shape=(n, n))
+    del Mt
     p = min(n, dim + 1 + 8)
     g = torch.Generator(device="cpu").manual_seed(int(seed))
     Y = torch.randn(n, p, generator=g).to(dev)
     Y[:, 0] = torch.sqrt(deg).float()
-    Y, _ = torch.linalg.qr(Y)
+    Y = _cholqr2(Y)
     for it in range(iters):
-        Y = 0.5 * (torch.sparse.mm(M, Y) + Y)  # (M + I) / 2: eigenvalues in [0, 1], order kept
+        Y = 0.5 * (ops.csr_spmm(M, Y) + Y)  # (M + I) / 2: eigenvalues in [0, 1], order kept
         if it % 5 == 4 or it == iters - 1:
-            Y, _ = torch.linalg.qr(Y)
-    T = Y.T @ (0.5 * (torch.sparse.mm(M, Y) + Y))
-    w, V = torch.linalg.eigh(T.double())
-    order = torch.argsort(w, descending=True)[1: dim + 1]
-    return (Y.double() @ V[:, order]).float()
+            Y = _cholqr2(Y)
+    T = Y.T @ (0.5 * (ops.csr_spmm(M, Y) + Y))
+    w, V = np.linalg.eigh(T.double().cpu().numpy())
+    order = np.argsort(w)[::-1][1: dim + 1].copy()
+    return (Y.double() @ torch.from_numpy(V[:, order]).to(dev)).float()
 
 
 def spectral_init(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n: int, dim: int, seed: int) -> torch.Tensor:
