@@ -50,6 +50,14 @@ class _Evaluator:
         # per-evaluation H2D of the coefficients goes through one pinned staging buffer
         self._w_host = torch.empty(self.n, dtype=torch.float64, pin_memory=self.dev.type == "cuda")
         self._y32 = y if y.dtype == torch.float32 else y.to(torch.float32)
+        # binomial fused path on the GPU: persistent device w / result and a pinned result buffer,
+        # moved with raw stream-ordered copies (no per-copy allocator events, no pageable D2H)
+        self._fast = (self.K == 1 and self.dev.type == "cuda"
+                      and (sparse or (X.dtype == torch.float32 and self.n <= 4096)))
+        if self._fast:
+            self._w_dev = torch.empty(self.n, dtype=torch.float64, device=self.dev)
+            self._out_dev = torch.empty(self.n + 2, dtype=torch.float64, device=self.dev)
+            self._out_host = torch.empty(self.n + 2, dtype=torch.float64, pin_memory=True)
 
     def _w_to_device(self, w: np.ndarray) -> torch.Tensor:
         self._w_host.numpy()[:] = w
@@ -72,6 +80,24 @@ class _Evaluator:
         Wt = theta[: K * n].reshape(K, n)
         b = theta[K * n: K * n + K] if self.fit_intercept else np.zeros(K)
         W = (Wt * self.inv_sigma).T  # n x K, original-space coefficients
+        if self._fast:
+            self._w_host.numpy()[:] = W[:, 0]
+            ops.h2d_async(self._w_dev, self._w_host)
+            if self.sparse:
+                ops.csr_logreg_binary_loss_grad(self.X, self._y32, self._w_dev, float(b[0]), out=self._out_dev)
+            else:
+                ops.logreg_binary_loss_grad(self.X, self._y32, self._w_dev, float(b[0]), out=self._out_dev)
+            self.ctx.comm.allreduce(self._out_dev)
+            ops.d2h_sync(self._out_host, self._out_dev)
+            h = self._out_host.numpy()
+            gw = h[:n].reshape(n, 1)
+            gb = h[n: n + 1]
+            f = h[n + 1] / self.m
+            grad = np.zeros_like(theta)
+            grad[: K * n] = ((gw / self.m) * self.inv_sigma[:, None]).T.reshape(-1)
+            if self.fit_intercept:
+                grad[K * n: K * n + K] = gb / self.m
+            return float(f), grad
         if K == 1 and self.sparse:
             w_dev = self._w_to_device(W[:, 0])
             out = ops.csr_logreg_binary_loss_grad(self.X, self._y32, w_dev, float(b[0]))

@@ -187,8 +187,10 @@ def row_sqnorm(X: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def logreg_binary_loss_grad(X: torch.Tensor, y: torch.Tensor, w: torch.Tensor, b: float) -> torch.Tensor:
-    """fp64 [grad_w (n), grad_b, loss_sum] of sum_r softplus(z_r) - y_r z_r, z = X w + b (one pass)."""
+def logreg_binary_loss_grad(X: torch.Tensor, y: torch.Tensor, w: torch.Tensor, b: float,
+                            out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """fp64 [grad_w (n), grad_b, loss_sum] of sum_r softplus(z_r) - y_r z_r, z = X w + b (one pass).
+    ``out`` (device, n + 2 fp64): reused result buffer (zeroed here)."""
     m, n = X.shape
     if not X.is_cuda or X.dtype != torch.float32 or n > 4096:
         Xd = X.double()
@@ -199,7 +201,7 @@ def logreg_binary_loss_grad(X: torch.Tensor, y: torch.Tensor, w: torch.Tensor, b
         loss = torch.nn.functional.softplus(z).sum() - (yd * z).sum()
         return torch.cat([Xd.T @ r, r.sum().view(1), loss.view(1)])
     X = _c(X)
-    out = torch.zeros(n + 2, dtype=torch.float64, device=X.device)
+    out = torch.zeros(n + 2, dtype=torch.float64, device=X.device) if out is None else zero_(out)
     wf = _c(w.to(device=X.device, dtype=torch.float64))
     yf = _c(y.to(torch.float32))
     native.call("srml_logreg_binary_f32", X.data_ptr(), m, n, X.stride(0), yf.data_ptr(), wf.data_ptr(), float(b),
@@ -980,8 +982,10 @@ def _sfx(A) -> str:
     return "f32" if A.data.dtype == torch.float32 else "f64"
 
 
-def csr_logreg_binary_loss_grad(A, y: torch.Tensor, w: torch.Tensor, b: float) -> torch.Tensor:
-    """fp64 [grad_w (n), grad_b, loss_sum] for CSR features: one pass over the non-zeros."""
+def csr_logreg_binary_loss_grad(A, y: torch.Tensor, w: torch.Tensor, b: float,
+                                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """fp64 [grad_w (n), grad_b, loss_sum] for CSR features: one pass over the non-zeros.
+    ``out`` (device, n + 2 fp64): reused result buffer (zeroed here)."""
     m, n = A.shape
     if not A.data.is_cuda:
         Xs = _csr_torch(A).to(torch.float64) if A.data.dtype != torch.float64 else _csr_torch(A)
@@ -992,7 +996,7 @@ def csr_logreg_binary_loss_grad(A, y: torch.Tensor, w: torch.Tensor, b: float) -
         g = (Xs.t() @ r.view(-1, 1)).view(-1)
         return torch.cat([g, r.sum().view(1), loss.view(1)])
     _csr_check(A)
-    out = torch.zeros(n + 2, dtype=torch.float64, device=A.data.device)
+    out = torch.zeros(n + 2, dtype=torch.float64, device=A.data.device) if out is None else zero_(out)
     wf = _c(w.to(device=A.data.device, dtype=torch.float64))
     yf = _c(y.to(torch.float32))
     native.call("srml_csr_logreg_binary_" + _sfx(A), A.indptr.data_ptr(), A.indices.data_ptr(), A.data.data_ptr(),
@@ -1048,3 +1052,33 @@ def csr_col_moments(A) -> Tuple[torch.Tensor, torch.Tensor]:
     native.call("srml_csr_col_moments_" + _sfx(A), A.indices.data_ptr(), A.data.data_ptr(), A.data.numel(),
                 s.data_ptr(), q.data_ptr(), native.stream(dev))
     return s, q
+
+
+# ------------------------------------------------------------------------------------------
+# Small transfers for host-driven solver loops (see csrc/xfer.hip)
+def h2d_async(dst: torch.Tensor, src: torch.Tensor) -> None:
+    """Enqueue a copy of a page-locked host tensor into a device tensor on the current stream.
+    ``src`` must stay untouched until a later synchronising transfer on that stream."""
+    if not dst.is_cuda:
+        dst.copy_(src)
+        return
+    assert src.is_pinned() and dst.is_contiguous() and src.is_contiguous() and dst.nbytes == src.nbytes
+    native.call("srml_memcpy_h2d_async", dst.data_ptr(), src.data_ptr(), dst.nbytes, native.stream(dst.device))
+
+
+def d2h_sync(dst: torch.Tensor, src: torch.Tensor) -> None:
+    """Copy a device tensor into a page-locked host tensor and wait for the current stream."""
+    if not src.is_cuda:
+        dst.copy_(src)
+        return
+    assert dst.is_pinned() and dst.is_contiguous() and src.is_contiguous() and dst.nbytes == src.nbytes
+    native.call("srml_memcpy_d2h_sync", dst.data_ptr(), src.data_ptr(), src.nbytes, native.stream(src.device))
+
+
+def zero_(t: torch.Tensor) -> torch.Tensor:
+    """Stream-ordered memset of a contiguous tensor (no fill kernel launch through the dispatcher)."""
+    if not t.is_cuda:
+        return t.zero_()
+    assert t.is_contiguous()
+    native.call("srml_memset_async", t.data_ptr(), 0, t.nbytes, native.stream(t.device))
+    return t

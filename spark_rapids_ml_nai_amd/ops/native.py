@@ -72,6 +72,9 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_csr_spmtm_f64": (_P, _P, _P, _L, _L, _P, _I, _P, _P),
     "srml_csr_col_moments_f32": (_P, _P, _L, _P, _P, _P),
     "srml_csr_col_moments_f64": (_P, _P, _L, _P, _P, _P),
+    "srml_memcpy_h2d_async": (_P, _P, _L, _P),
+    "srml_memcpy_d2h_sync": (_P, _P, _L, _P),
+    "srml_memset_async": (_P, _I, _L, _P),
     "srml_rf_predict": (_P, _L, _L, _P, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P),
 }
 
