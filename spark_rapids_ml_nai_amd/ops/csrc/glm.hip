@@ -304,7 +304,7 @@ __global__ __launch_bounds__(256, 2) void logreg_binary_split_kernel(const float
 // loaded into a second register set while the current batch's margins are reduced / exchanged
 // through LDS and its gradient is accumulated, so each wave keeps 2 * R * V * 1 KiB of X in flight
 // across the per-batch barrier (the kernel is HBM-latency bound, not VALU bound).
-template <int V, int R, int D>
+template <int V, int R, int D, bool NT = false>
 __global__ __launch_bounds__(256, 2) void logreg_binary_pf_kernel(const float* __restrict__ X, long m, int n, long ld,
                                                                   const float* __restrict__ y,
                                                                   const double* __restrict__ w, double b,
@@ -337,7 +337,9 @@ __global__ __launch_bounds__(256, 2) void logreg_binary_pf_kernel(const float* _
       const long r = rb + i < r1 ? rb + i : r1 - 1;
       const float* row = X + r * ld;
 #pragma unroll
-      for (int v = 0; v < V; ++v) x[i][v] = *reinterpret_cast<const floatx4*>(row + coff[v]);
+      for (int v = 0; v < V; ++v)
+        x[i][v] = NT ? __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(row + coff[v]))
+                     : *reinterpret_cast<const floatx4*>(row + coff[v]);
     }
   };
   int buf = 0;
@@ -427,6 +429,7 @@ SRML_API int srml_logreg_binary_f32(const float* X, long m, int n, long ld, cons
       (reinterpret_cast<uintptr_t>(X) & 15) == 0) {
     static const int rsel = getenv("SRML_LOGREG_R") ? atoi(getenv("SRML_LOGREG_R")) : 1;
     static const int dsel = getenv("SRML_LOGREG_D") ? atoi(getenv("SRML_LOGREG_D")) : 3;
+    static const int nt = getenv("SRML_LOGREG_NT") ? atoi(getenv("SRML_LOGREG_NT")) : 1;  // nontemporal X stream: +2%
     const int VS = (n + 1023) / 1024;
 #define SRML_LR_PF(VV, RR, DD) \
     hipLaunchKernelGGL((logreg_binary_pf_kernel<VV, RR, DD>), grid, blk, 0, stream, X, m, n, ld, y, w, b, out, rpb)
@@ -435,6 +438,11 @@ SRML_API int srml_logreg_binary_f32(const float* X, long m, int n, long ld, cons
     if (rsel == 2 && dsel == 1) SRML_LR_PF_V(2, 1);
     else if (rsel == 2) SRML_LR_PF_V(2, 2);
     else if (dsel == 1) SRML_LR_PF_V(1, 1);
+    else if (dsel == 3 && nt) {
+      if (VS == 2) hipLaunchKernelGGL((logreg_binary_pf_kernel<2, 1, 3, true>), grid, blk, 0, stream, X, m, n, ld, y, w, b, out, rpb);
+      else if (VS == 3) hipLaunchKernelGGL((logreg_binary_pf_kernel<3, 1, 3, true>), grid, blk, 0, stream, X, m, n, ld, y, w, b, out, rpb);
+      else hipLaunchKernelGGL((logreg_binary_pf_kernel<4, 1, 3, true>), grid, blk, 0, stream, X, m, n, ld, y, w, b, out, rpb);
+    }
     else if (dsel == 3) SRML_LR_PF_V(1, 3);
     else SRML_LR_PF_V(1, 2);
     return srml_status();
