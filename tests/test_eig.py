@@ -37,3 +37,17 @@ def test_topk_eigh_cpu(n, kind, k):
 @pytest.mark.parametrize("n,kind,k", [(700, "rand", 3), (3000, "lowrank", 3), (2000, "rand", 10)])
 def test_topk_eigh_gpu(gpu_device, n, kind, k):
     _check(gpu_device, n, kind, k)
+
+
+@pytest.mark.gpu
+def test_topk_eigh_gpu_rank_deficient_falls_back(gpu_device):
+    """Exactly rank-2 matrix, k=3: the Krylov blocks lose rank, the device CholeskyQR breaks down
+    and the solver must redo the restart with the host-checked orthonormalisation."""
+    rng = np.random.default_rng(3)
+    n = 1200
+    U = np.linalg.qr(rng.standard_normal((n, 2)))[0]
+    A = (U * np.array([5.0, 2.0])) @ U.T
+    w, V = topk_eigh(torch.from_numpy(A).to(gpu_device), 3)
+    assert np.isfinite(w).all() and np.isfinite(V).all()
+    np.testing.assert_allclose(w[:2], [5.0, 2.0], rtol=1e-9)
+    np.testing.assert_allclose(np.abs(V[:, :2].T @ U), np.eye(2), atol=1e-8)
