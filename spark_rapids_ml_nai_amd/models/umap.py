@@ -186,7 +186,9 @@ def _cholqr2(Y: torch.Tensor) -> torch.Tensor:
     W = Y
     for _ in range(2):
         Wd = W.double()
-        G = (Wd.T @ Wd).cpu().numpy()
+        # Gram of a tall-skinny block: the streaming SYRK kernel (fp32 in, fp64 out); a library
+        # fp64 GEMM with K = n rows picks a non-split-K tile and took 53 ms at 2M x 11
+        G = (ops.gram(W.float()) if W.is_cuda else Wd.T @ Wd).cpu().numpy()
         try:
             L = np.linalg.cholesky((G + G.T) * 0.5)
         except np.linalg.LinAlgError:
@@ -222,7 +224,9 @@ def _spectral_device(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor,
         Y = 0.5 * (ops.csr_spmm(M, Y) + Y)  # (M + I) / 2: eigenvalues in [0, 1], order kept
         if it % 5 == 4 or it == iters - 1:
             Y = _cholqr2(Y)
-    T = Y.T @ (0.5 * (ops.csr_spmm(M, Y) + Y))
+    Z = 0.5 * (ops.csr_spmm(M, Y) + Y)
+    # Y^T Z over row chunks: library GEMMs with K in the millions pick non-split-K tiles
+    T = sum(Y[i: i + 65536].double().T @ Z[i: i + 65536].double() for i in range(0, n, 65536))
     w, V = np.linalg.eigh(T.double().cpu().numpy())
     order = np.argsort(w)[::-1][1: dim + 1].copy()
     return (Y.double() @ torch.from_numpy(V[:, order]).to(dev)).float()
