@@ -11,7 +11,8 @@
 //    lanes stride the row's non-zeros, reduce the dot product with intra-group shuffles, then
 //    reuse the same (index, value) registers for the scatter of the gradient (fp64 atomics in
 //    L2; sparse columns rarely collide within a wave). Non-zeros beyond 4*G per row are re-read.
-//  * srml_csr_spmm_{f32,f64}   — Z (m x K fp32) = X W + bias, W (n x K fp32 row-major), K <= 16:
+//  * srml_csr_spmm_{f32,f64}   — Z (m x K fp32) = X W + bias, W (n x K fp32 row-major), K <= 16
+//    (K > 4: one lane per output column; also the SpMM of UMAP's spectral initialisation):
 //    multinomial margins for every class in one pass.
 //  * srml_csr_spmtm_{f32,f64}  — out (n x K fp64) += X^T R, R (m x K fp32): multinomial gradient.
 //  * srml_csr_col_moments_{f32,f64} — column sum and sum of squares (fp64) over the non-zeros
@@ -120,6 +121,38 @@ __global__ __launch_bounds__(256) void csr_spmm_kernel(const long* __restrict__ 
   }
 }
 
+// Column-per-lane variant for 4 < K <= 16: a group of G >= K lanes owns one row and lane k
+// accumulates output column k over the row's non-zeros (index / value loads are group-uniform
+// broadcasts, the W-row reads are one contiguous K-float segment): no cross-lane reduction,
+// where the nnz-split kernel spent 4 shuffles per column per row.
+template <typename T, int G>
+__global__ __launch_bounds__(256) void csr_spmm_cols_kernel(const long* __restrict__ indptr,
+                                                            const int* __restrict__ indices,
+                                                            const T* __restrict__ data, long m,
+                                                            const float* __restrict__ W, int kk,
+                                                            const float* __restrict__ bias, float* __restrict__ Z) {
+  constexpr int GPB = 256 / G;
+  const int g = threadIdx.x / G;
+  const int l = threadIdx.x % G;
+  const bool act = l < kk;
+  const float b0 = (bias && act) ? bias[l] : 0.f;
+  for (long r = (long)blockIdx.x * GPB + g; r < m; r += (long)gridDim.x * GPB) {
+    const long p0 = indptr[r], p1 = indptr[r + 1];
+    float a0 = 0.f, a1 = 0.f;
+    long p = p0;
+    for (; p + 1 < p1; p += 2) {
+      const int c0 = indices[p], c1 = indices[p + 1];
+      const float v0 = (float)data[p], v1 = (float)data[p + 1];
+      if (act) {
+        a0 = fmaf(v0, W[(long)c0 * kk + l], a0);
+        a1 = fmaf(v1, W[(long)c1 * kk + l], a1);
+      }
+    }
+    if (p < p1 && act) a0 = fmaf((float)data[p], W[(long)indices[p] * kk + l], a0);
+    if (act) Z[r * kk + l] = a0 + a1 + b0;
+  }
+}
+
 template <typename T, int G, int K>
 __global__ __launch_bounds__(256) void csr_spmtm_kernel(const long* __restrict__ indptr, const int* __restrict__ indices,
                                                         const T* __restrict__ data, long m,
@@ -219,6 +252,15 @@ static int csr_spmm_launch(const long* indptr, const int* indices, const T* data
                            int kk, const float* bias, float* Z, hipStream_t s) {
   if (m <= 0) return 0;
   if (kk < 1 || kk > 16) return (int)hipErrorInvalidValue;
+  if (kk > 4) {  // column-per-lane groups
+    const int Gc = kk <= 8 ? 8 : 16;
+    const dim3 gridc(grid_for(m, Gc));
+    if (Gc == 8)
+      hipLaunchKernelGGL((csr_spmm_cols_kernel<T, 8>), gridc, dim3(256), 0, s, indptr, indices, data, m, W, kk, bias, Z);
+    else
+      hipLaunchKernelGGL((csr_spmm_cols_kernel<T, 16>), gridc, dim3(256), 0, s, indptr, indices, data, m, W, kk, bias, Z);
+    return srml_status();
+  }
   const int G = pick_group(m, nnz);
   const dim3 grid(grid_for(m, G));
   if (kk <= 4) csr_spmm_k<T, 4>(G, grid, s, indptr, indices, data, m, W, kk, bias, Z);
