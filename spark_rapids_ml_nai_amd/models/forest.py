@@ -96,17 +96,6 @@ class Tree:
     count: List[float] = field(default_factory=list)
     depth: int = 0
 
-    def add_node(self) -> int:
-        self.feature.append(-1)
-        self.threshold.append(0.0)
-        self.left.append(-1)
-        self.right.append(-1)
-        self.value.append([])
-        self.impurity.append(0.0)
-        self.gain.append(0.0)
-        self.count.append(0.0)
-        return len(self.feature) - 1
-
     def to_dict(self) -> Dict[str, Any]:
         return {"feature": self.feature, "threshold": self.threshold, "left": self.left, "right": self.right,
                 "value": self.value, "impurity": self.impurity, "gain": self.gain, "count": self.count,
@@ -125,32 +114,8 @@ class Tree:
         return len(self.feature)
 
 
-def _leaf_value(tot: np.ndarray, regression: bool) -> List[float]:
-    if regression:
-        return [float(tot[1] / tot[0]) if tot[0] > 0 else 0.0]
-    s = tot.sum()
-    return [float(v / s) if s > 0 else 0.0 for v in tot]
-
-
-def _impurity_np(tot: np.ndarray, crit: int) -> float:
-    if crit == 2:
-        n = tot[0]
-        if n <= 0:
-            return 0.0
-        mu = tot[1] / n
-        return float(max(tot[2] / n - mu * mu, 0.0))
-    n = tot.sum()
-    if n <= 0:
-        return 0.0
-    p = tot / n
-    if crit == 0:
-        return float(1.0 - (p * p).sum())
-    nz = p[p > 0]
-    return float(-(nz * np.log2(nz)).sum())
-
-
 def _leaf_values_np(tot: np.ndarray, regression: bool) -> np.ndarray:
-    """Vectorised ``_leaf_value`` over segments: (L, 1) means or (L, S) class probabilities."""
+    """Leaf values of all segments: (L, 1) weighted means or (L, S) class probabilities."""
     if regression:
         n = tot[:, 0]
         return np.where(n > 0, tot[:, 1] / np.where(n > 0, n, 1.0), 0.0)[:, None]
@@ -159,7 +124,7 @@ def _leaf_values_np(tot: np.ndarray, regression: bool) -> np.ndarray:
 
 
 def _impurities_np(tot: np.ndarray, crit: int) -> np.ndarray:
-    """Vectorised ``_impurity_np`` over segments."""
+    """Impurity of all segments: variance (crit 2), Gini (0) or entropy (1)."""
     if crit == 2:
         n = tot[:, 0]
         safe = np.where(n > 0, n, 1.0)
@@ -188,8 +153,8 @@ class _ForestRecords:
         self.depth = 0
 
     def add_children(self, t_i: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
-        """Left/right ids for splits of trees ``t_i`` (in order), numbered like sequential
-        ``add_node`` calls: per tree, in order of appearance."""
+        """Left/right ids for splits of trees ``t_i`` (in order): per tree, consecutive ids in
+        order of appearance."""
         order_t = np.argsort(t_i, kind="stable")
         ts = t_i[order_t]
         starts = np.r_[0, np.nonzero(np.diff(ts))[0] + 1]
