@@ -385,6 +385,10 @@ __global__ __launch_bounds__(256, 1) void knn_kernel(const float* __restrict__ Q
 // merged at the end (reference: cuML NearestNeighbors(algorithm="ivfflat"), knn.py:1295-1380).
 // ------------------------------------------------------------------------------------------
 namespace {
+// G lanes per item (G = pow2 >= n/4, <= 64): a wave scores 64/G items per step, each group
+// reduces its dot product with in-group shuffles; candidates are inserted in item order with
+// wave-uniform threshold tests (a 128-wide item used only 32 lanes of a 64-lane wave per step).
+template <int G>
 __global__ __launch_bounds__(256) void ivf_search_kernel(const float* __restrict__ Q, long nq, int n, long ldq,
                                                          const int* __restrict__ probes, int nprobe,
                                                          const long long* __restrict__ list_off,
@@ -392,11 +396,13 @@ __global__ __launch_bounds__(256) void ivf_search_kernel(const float* __restrict
                                                          const float* __restrict__ inorm,
                                                          const long long* __restrict__ ids, int k,
                                                          float* __restrict__ out_d, long long* __restrict__ out_i) {
+  constexpr int IPW = 64 / G;  // items per wave step
   extern __shared__ __attribute__((aligned(16))) float qs[];  // n floats (padded to 4)
   __shared__ float wd[4][KNN_KMAX];
   __shared__ long long wi[4][KNN_KMAX];
   const long q = blockIdx.x;
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int gi = lane / G, gl = lane % G;
   for (int d = t; d < n; d += 256) qs[d] = Q[q * ldq + d];
   for (int j = t; j < 4 * KNN_KMAX; j += 256) {
     (&wd[0][0])[j] = __builtin_huge_valf();
@@ -409,31 +415,40 @@ __global__ __launch_bounds__(256) void ivf_search_kernel(const float* __restrict
     const int l = probes[q * nprobe + p];
     if (l < 0) continue;
     const long s = list_off[l], e = list_off[l + 1];
-    for (long j = s + wid; j < e; j += 4) {
-      const float* row = items + j * ldi;
+    for (long j0 = s + (long)wid * IPW; j0 < e; j0 += 4 * IPW) {
+      const long j = j0 + gi;
       float acc = 0.f;
-      if (vec) {
-        for (int d = lane * 4; d < n; d += 256) {
-          const floatx4 x = *reinterpret_cast<const floatx4*>(row + d);
-          acc = fmaf(x[0], qs[d], fmaf(x[1], qs[d + 1], fmaf(x[2], qs[d + 2], fmaf(x[3], qs[d + 3], acc))));
-        }
-      } else {
-        for (int d = lane; d < n; d += 64) acc = fmaf(row[d], qs[d], acc);
-      }
-      const float dist = fmaf(-2.f, wave_sum(acc), inorm[j]);
-      if (dist < thr) {  // wave-uniform
-        if (lane == 0) {
-          int pos = k - 1;
-          while (pos > 0 && wd[wid][pos - 1] > dist) {
-            wd[wid][pos] = wd[wid][pos - 1];
-            wi[wid][pos] = wi[wid][pos - 1];
-            --pos;
+      if (j < e) {
+        const float* row = items + j * ldi;
+        if (vec) {
+          for (int d = gl * 4; d < n; d += 4 * G) {
+            const floatx4 x = *reinterpret_cast<const floatx4*>(row + d);
+            acc = fmaf(x[0], qs[d], fmaf(x[1], qs[d + 1], fmaf(x[2], qs[d + 2], fmaf(x[3], qs[d + 3], acc))));
           }
-          wd[wid][pos] = dist;
-          wi[wid][pos] = ids[j];
+        } else {
+          for (int d = gl; d < n; d += G) acc = fmaf(row[d], qs[d], acc);
         }
-        __builtin_amdgcn_wave_barrier();
-        thr = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(wd[wid][k - 1])));
+      }
+#pragma unroll
+      for (int o = G / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+      const float dist = j < e ? fmaf(-2.f, acc, inorm[j]) : __builtin_huge_valf();
+#pragma unroll
+      for (int g = 0; g < IPW; ++g) {
+        const float dg = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dist), g * G));
+        if (dg < thr) {  // wave-uniform
+          if (lane == 0) {
+            int pos = k - 1;
+            while (pos > 0 && wd[wid][pos - 1] > dg) {
+              wd[wid][pos] = wd[wid][pos - 1];
+              wi[wid][pos] = wi[wid][pos - 1];
+              --pos;
+            }
+            wd[wid][pos] = dg;
+            wi[wid][pos] = ids[j0 + g];
+          }
+          __builtin_amdgcn_wave_barrier();
+          thr = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(wd[wid][k - 1])));
+        }
       }
     }
   }
@@ -459,8 +474,15 @@ SRML_API int srml_ivf_search_f32(const float* Q, long nq, int n, long ldq, const
   if (nq <= 0) return 0;
   if (k < 1 || k > KNN_KMAX) return -8;
   const size_t lds = (size_t)((n + 3) / 4) * 4 * sizeof(float);
-  hipLaunchKernelGGL(ivf_search_kernel, dim3((unsigned)nq), dim3(256), lds, stream, Q, nq, n, ldq, probes, nprobe,
-                     list_off, items, ldi, inorm, ids, k, out_d, out_i);
+  const int need = (n + 3) / 4;  // lanes that a 16-B-per-lane pass over one item occupies
+#define SRML_IVF(GG)                                                                                        \
+  hipLaunchKernelGGL((ivf_search_kernel<GG>), dim3((unsigned)nq), dim3(256), lds, stream, Q, nq, n, ldq, probes, \
+                     nprobe, list_off, items, ldi, inorm, ids, k, out_d, out_i)
+  if (need <= 8) SRML_IVF(8);
+  else if (need <= 16) SRML_IVF(16);
+  else if (need <= 32) SRML_IVF(32);
+  else SRML_IVF(64);
+#undef SRML_IVF
   return srml_status();
 }
 

@@ -257,7 +257,7 @@ def test_knn_id_offset(gpu_device):
     assert torch.equal(i0 + 1000, i1)
 
 
-@pytest.mark.parametrize("n,nlist,nprobe,k", [(16, 10, 3, 10), (130, 32, 8, 5), (3, 5, 5, 64)])
+@pytest.mark.parametrize("n,nlist,nprobe,k", [(16, 10, 3, 10), (130, 32, 8, 5), (3, 5, 5, 64), (128, 40, 6, 10), (64, 20, 4, 7), (33, 12, 3, 1)])
 def test_ivf_search(gpu_device, n, nlist, nprobe, k):
     from spark_rapids_ml_nai_amd.models.knn import build_ivf
 
