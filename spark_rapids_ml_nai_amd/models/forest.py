@@ -200,9 +200,9 @@ class _ForestRecords:
                 gain[nid] = spl[4][sel]
                 left[nid] = spl[5][sel]
                 right[nid] = spl[6][sel]
-            tr = Tree(feature=feature.tolist(), threshold=threshold.tolist(), left=left.tolist(),
-                      right=right.tolist(), value=value.tolist(), impurity=impurity.tolist(), gain=gain.tolist(),
-                      count=count.tolist(), depth=self.depth)
+            # numpy node arrays (JSON conversion happens only when a model is persisted)
+            tr = Tree(feature=feature, threshold=threshold, left=left, right=right, value=value, impurity=impurity,
+                      gain=gain, count=count, depth=self.depth)
             trees.append(tr)
         return trees
 
@@ -429,27 +429,33 @@ def fit_forest(X: torch.Tensor, y: torch.Tensor, ctx: WorkerContext, m_total: in
 
 
 def pack_forest(trees: List[Dict[str, Any]], S: int, device: torch.device) -> Dict[str, torch.Tensor]:
+    """Flatten trees (node lists or arrays) into the breadth-first device arrays of ``rf_predict``."""
     feats, thr, left, right, voff, vals, roots = [], [], [], [], [], [], []
     base = 0
-    vbase = 0
     for t in trees:
-        nn_ = len(t["feature"])
+        f = np.asarray(t["feature"], dtype=np.int64).reshape(-1)
+        nn_ = f.shape[0]
         roots.append(base)
-        feats.extend(t["feature"])
-        thr.extend(t["threshold"])
-        left.extend([(l + base) if l >= 0 else -1 for l in t["left"]])
-        right.extend([(r + base) if r >= 0 else -1 for r in t["right"]])
-        for v in t["value"]:
-            vv = list(v) + [0.0] * (S - len(v))
-            voff.append(vbase)
-            vals.extend(vv[:S])
-            vbase += S
+        feats.append(f)
+        thr.append(np.asarray(t["threshold"], dtype=np.float64).reshape(-1))
+        lt = np.asarray(t["left"], dtype=np.int64).reshape(-1)
+        rt = np.asarray(t["right"], dtype=np.int64).reshape(-1)
+        left.append(np.where(lt >= 0, lt + base, -1))
+        right.append(np.where(rt >= 0, rt + base, -1))
+        v = np.zeros((nn_, S))
+        if nn_:
+            tv = np.asarray(t["value"], dtype=np.float64).reshape(nn_, -1)[:, :S]
+            v[:, : tv.shape[1]] = tv
+        vals.append(v.reshape(-1))
         base += nn_
-    i32 = lambda a: torch.tensor(a, dtype=torch.int32, device=device)
+    cat = lambda parts, dt: np.concatenate(parts).astype(dt) if parts else np.zeros(0, dt)  # noqa: E731
+    i32 = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.int32)).to(device)  # noqa: E731
     return {
-        "roots": i32(roots), "feature": i32(feats), "threshold": torch.tensor(thr, dtype=torch.float32, device=device),
-        "left": i32(left), "right": i32(right), "value_off": i32(voff),
-        "values": torch.tensor(vals, dtype=torch.float32, device=device),
+        "roots": i32(np.asarray(roots, dtype=np.int32)), "feature": i32(cat(feats, np.int32)),
+        "threshold": torch.from_numpy(cat(thr, np.float32)).to(device),
+        "left": i32(cat(left, np.int32)), "right": i32(cat(right, np.int32)),
+        "value_off": i32(np.arange(base, dtype=np.int64) * S),
+        "values": torch.from_numpy(cat(vals, np.float32)).to(device),
     }
 
 
@@ -465,9 +471,9 @@ def feature_importances(trees: List[Dict[str, Any]], n: int) -> np.ndarray:
     total = np.zeros(n)
     for t in trees:
         imp = np.zeros(n)
-        for f, g, c in zip(t["feature"], t["gain"], t["count"]):
-            if f >= 0:
-                imp[f] += g * c
+        f = np.asarray(t["feature"], dtype=np.int64)
+        split = f >= 0
+        np.add.at(imp, f[split], (np.asarray(t["gain"], dtype=np.float64) * np.asarray(t["count"], dtype=np.float64))[split])
         s = imp.sum()
         if s > 0:
             total += imp / s

@@ -244,10 +244,13 @@ class _RandomForestEstimator(_RandomForestClass, _EstimatorSupervised, _RandomFo
                 trees = fit_forest(X, y, ctx, inp.desc.m, p, n_local, classification, num_classes, data_parallel,
                                    rank_seed=seed * 1000003 + ctx.rank)
                 if not data_parallel and ctx.world_size > 1:
-                    import json
+                    # forests of peer ranks of this same job (numpy node arrays), device all-gather
+                    import pickle
 
-                    blobs = ctx.comm.allgather_bytes(json.dumps(trees).encode())
-                    trees = [t for b in blobs for t in json.loads(b.decode())]
+                    from .parallel.comm import pickle_obj
+
+                    blobs = ctx.comm.allgather_bytes(pickle_obj(trees))
+                    trees = [t for b in blobs for t in pickle.loads(b)]
                 res = {"trees": trees, "n_cols": int(n), "dtype": "float32", "num_classes": num_classes}
                 outs.append(res)
             return outs if params["fit_multiple_params"] else outs[0]
