@@ -253,7 +253,7 @@ def binary_auc(label: np.ndarray, score: np.ndarray) -> float:
         return 0.0
     tpr = np.r_[0.0, tps / P, 1.0]
     fpr = np.r_[0.0, fps / N, 1.0]
-    return float(np.trapz(tpr, fpr)) if hasattr(np, "trapz") else float(np.trapezoid(tpr, fpr))
+    return float(np.trapezoid(tpr, fpr)) if hasattr(np, "trapezoid") else float(np.trapz(tpr, fpr))
 
 
 def binary_aupr(label: np.ndarray, score: np.ndarray) -> float:

@@ -1,0 +1,137 @@
+"""CPU coverage of the model-level API surface: random-forest model
+accessors and quality vs scikit-learn, ML persistence round trips for every persistable
+family, and the Spark-equivalent evaluators vs scikit-learn's metrics.
+
+Reference parity: ``python/tests/test_random_forest.py`` (accessors, accuracy / RMSE bounds,
+persistence), ``python/tests/test_logistic_regression.py`` (save/load), and the metric
+definitions in ``python/src/spark_rapids_ml/metrics/*.py``.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+from sklearn.datasets import make_classification, make_regression
+from sklearn.metrics import accuracy_score, f1_score, mean_absolute_error, mean_squared_error, r2_score, \
+    roc_auc_score
+
+from spark_rapids_ml_nai_amd import DataFrame
+from spark_rapids_ml_nai_amd.classification import (LogisticRegression, LogisticRegressionModel,
+                                                     RandomForestClassificationModel, RandomForestClassifier)
+from spark_rapids_ml_nai_amd.evaluation import (BinaryClassificationEvaluator, MulticlassClassificationEvaluator,
+                                                 RegressionEvaluator)
+from spark_rapids_ml_nai_amd.regression import RandomForestRegressionModel, RandomForestRegressor
+
+
+def _clf_data(n=1500, d=12, classes=2, seed=0):
+    X, y = make_classification(n_samples=n, n_features=d, n_informative=6, n_redundant=2, n_classes=classes,
+                               random_state=seed)
+    return X.astype(np.float32), y.astype(np.float64)
+
+
+def test_rf_classifier_accessors_and_accuracy():
+    X, y = _clf_data()
+    df = DataFrame.from_numpy(X, y)
+    est = RandomForestClassifier(numTrees=8, maxDepth=6, seed=1)
+    assert est.getNumTrees() == 8 and est.getMaxDepth() == 6
+    model = est.fit(df)
+    assert isinstance(model, RandomForestClassificationModel)
+    n_trees = model.getNumTrees
+    assert (n_trees() if callable(n_trees) else n_trees) == 8
+    assert model.numClasses == 2
+    assert len(model.trees) == 8
+    assert all(t.depth <= 6 for t in model.trees)
+    assert model.totalNumNodes == sum(t.numNodes for t in model.trees)
+    assert list(model.treeWeights) == [1.0] * 8
+    imp = np.asarray(model.featureImportances.toArray())
+    assert imp.shape == (12,) and np.all(imp >= 0) and abs(imp.sum() - 1.0) < 1e-6
+    s = model.toDebugString
+    s = s() if callable(s) else s
+    assert "Tree 0" in s or "tree 0" in s.lower()
+
+    out = model.transform(df)
+    pred = out.to_numpy("prediction")
+    prob = out.to_numpy("probability")
+    raw = out.to_numpy("rawPrediction")
+    assert prob.shape == (1500, 2) and raw.shape == (1500, 2)
+    np.testing.assert_allclose(prob.sum(1), 1.0, atol=1e-5)
+    np.testing.assert_array_equal(pred, raw.argmax(1))
+    assert accuracy_score(y, pred) > 0.85
+    # single-row helpers agree with the batch path
+    for i in (0, 7, 123):
+        assert model.predict(X[i]) == pred[i]
+        np.testing.assert_allclose(np.asarray(model.predictProbability(X[i]).toArray()), prob[i], atol=1e-5)
+
+
+def test_rf_classifier_multiclass_and_persistence(tmp_path):
+    X, y = _clf_data(n=1200, classes=3, seed=3)
+    df = DataFrame.from_numpy(X, y)
+    model = RandomForestClassifier(numTrees=6, maxDepth=7, seed=2).fit(df)
+    assert model.numClasses == 3
+    pred = model.transform(df).to_numpy("prediction")
+    assert accuracy_score(y, pred) > 0.8
+    path = str(tmp_path / "rfc")
+    model.write().overwrite().save(path)
+    m2 = RandomForestClassificationModel.load(path)
+    np.testing.assert_array_equal(m2.transform(df).to_numpy("prediction"), pred)
+    assert m2.totalNumNodes == model.totalNumNodes
+
+
+def test_rf_regressor_quality_and_persistence(tmp_path):
+    X, y = make_regression(n_samples=2000, n_features=10, n_informative=5, noise=5.0, random_state=4)
+    X = X.astype(np.float32)
+    df = DataFrame.from_numpy(X, y)
+    model = RandomForestRegressor(numTrees=10, maxDepth=8, seed=5).fit(df)
+    assert isinstance(model, RandomForestRegressionModel)
+    pred = model.transform(df).to_numpy("prediction")
+    assert r2_score(y, pred) > 0.8
+    assert abs(model.predict(X[3]) - pred[3]) < 1e-3 * max(1.0, abs(pred[3]))
+    path = str(tmp_path / "rfr")
+    model.write().overwrite().save(path)
+    m2 = RandomForestRegressionModel.load(path)
+    np.testing.assert_allclose(m2.transform(df).to_numpy("prediction"), pred, rtol=1e-6, atol=1e-6)
+
+
+def test_logistic_regression_persistence(tmp_path):
+    X, y = _clf_data(n=800, seed=6)
+    df = DataFrame.from_numpy(X, y)
+    est = LogisticRegression(maxIter=50, regParam=0.01)
+    model = est.fit(df)
+    path = str(tmp_path / "logreg")
+    model.write().overwrite().save(path)
+    m2 = LogisticRegressionModel.load(path)
+    np.testing.assert_allclose(np.asarray(m2.coefficients.toArray()), np.asarray(model.coefficients.toArray()))
+    assert m2.intercept == pytest.approx(model.intercept)
+    np.testing.assert_array_equal(m2.transform(df).to_numpy("prediction"), model.transform(df).to_numpy("prediction"))
+    est.save(str(tmp_path / "logreg_est"))
+    assert LogisticRegression.load(str(tmp_path / "logreg_est")).getMaxIter() == 50
+
+
+def test_regression_evaluator_matches_sklearn():
+    rng = np.random.default_rng(7)
+    y = rng.standard_normal(500)
+    p = y + 0.3 * rng.standard_normal(500)
+    df = DataFrame.from_numpy(np.zeros((500, 1), np.float32), y, extra={"prediction": p})
+    ev = RegressionEvaluator()
+    assert ev.setMetricName("rmse").evaluate(df) == pytest.approx(np.sqrt(mean_squared_error(y, p)), rel=1e-9)
+    assert ev.setMetricName("mse").evaluate(df) == pytest.approx(mean_squared_error(y, p), rel=1e-9)
+    assert ev.setMetricName("mae").evaluate(df) == pytest.approx(mean_absolute_error(y, p), rel=1e-9)
+    assert ev.setMetricName("r2").evaluate(df) == pytest.approx(r2_score(y, p), rel=1e-9)
+    assert ev.isLargerBetter()
+    assert not ev.setMetricName("rmse").isLargerBetter()
+
+
+def test_classification_evaluators_match_sklearn():
+    rng = np.random.default_rng(8)
+    y = rng.integers(0, 3, 600).astype(np.float64)
+    p = np.where(rng.random(600) < 0.7, y, rng.integers(0, 3, 600)).astype(np.float64)
+    df = DataFrame.from_numpy(np.zeros((600, 1), np.float32), y, extra={"prediction": p})
+    ev = MulticlassClassificationEvaluator(metricName="accuracy")
+    assert ev.evaluate(df) == pytest.approx(accuracy_score(y, p), rel=1e-9)
+    assert ev.setMetricName("f1").evaluate(df) == pytest.approx(f1_score(y, p, average="weighted"), rel=1e-9)
+
+    yb = rng.integers(0, 2, 700).astype(np.float64)
+    score = yb + 1.2 * rng.standard_normal(700)
+    raw = np.stack([-score, score], 1)
+    dfb = DataFrame.from_numpy(np.zeros((700, 1), np.float32), yb, extra={"rawPrediction": raw})
+    auc = BinaryClassificationEvaluator(metricName="areaUnderROC").evaluate(dfb)
+    assert auc == pytest.approx(roc_auc_score(yb, score), abs=1e-6)
