@@ -135,3 +135,49 @@ def test_classification_evaluators_match_sklearn():
     dfb = DataFrame.from_numpy(np.zeros((700, 1), np.float32), yb, extra={"rawPrediction": raw})
     auc = BinaryClassificationEvaluator(metricName="areaUnderROC").evaluate(dfb)
     assert auc == pytest.approx(roc_auc_score(yb, score), abs=1e-6)
+
+
+def test_pca_attributes_match_sklearn():
+    from sklearn.decomposition import PCA as SkPCA
+
+    from spark_rapids_ml_nai_amd.feature import PCA
+
+    rng = np.random.default_rng(9)
+    X = (rng.standard_normal((800, 6)) @ rng.standard_normal((6, 6))).astype(np.float32)
+    m = PCA(k=3, inputCol="features", outputCol="o").fit(DataFrame.from_numpy(X))
+    sk = SkPCA(n_components=3).fit(X.astype(np.float64))
+    comp = np.asarray(m.components_)
+    signs = np.sign((comp * sk.components_).sum(1))
+    np.testing.assert_allclose(comp * signs[:, None], sk.components_, atol=1e-4)
+    np.testing.assert_allclose(m.explained_variance_ratio_, sk.explained_variance_ratio_, rtol=1e-4)
+    np.testing.assert_allclose(m.singular_values_, sk.singular_values_, rtol=1e-4)
+    np.testing.assert_allclose(m.mean_, sk.mean_, atol=1e-5)
+    pc = m.pc.toArray()
+    assert pc.shape == (6, 3)
+    np.testing.assert_allclose(pc.T, comp, atol=1e-6)
+
+
+def test_kmeans_and_logreg_model_accessors():
+    from spark_rapids_ml_nai_amd.clustering import KMeans
+
+    rng = np.random.default_rng(10)
+    X = np.concatenate([rng.standard_normal((200, 4)) + 8 * i for i in range(3)]).astype(np.float32)
+    df = DataFrame.from_numpy(X, (X[:, 0] > 8).astype(np.float64))
+    km = KMeans(k=3, seed=1).fit(df)
+    assert not km.hasSummary
+    assert np.asarray(km.cluster_centers_).shape == (3, 4)
+    pred = km.transform(df).to_numpy("prediction")
+    assert len(np.unique(pred)) == 3
+    assert all(km.predict(X[i]) == pred[i] for i in (0, 250, 599))
+    with pytest.raises(ValueError):
+        KMeans().setWeightCol("w")
+
+    g = LogisticRegression(maxIter=30).fit(df)
+    assert g.numClasses == 2 and list(g.classes_) == [0.0, 1.0]
+    assert g.coefficientMatrix.numRows == 1 and g.coefficientMatrix.numCols == 4
+    assert len(g.interceptVector) == 1 and g.num_iters > 0 and np.isfinite(g.objective)
+    assert not g.hasSummary
+    with pytest.raises(RuntimeError):
+        _ = g.summary
+    raw = g.transform(df).to_numpy("rawPrediction")
+    np.testing.assert_allclose(np.asarray(g.predictRaw(X[5]).toArray()), raw[5], rtol=1e-5, atol=1e-6)
