@@ -22,13 +22,26 @@ from spark_rapids_ml_nai_amd.evaluation import (BinaryClassificationEvaluator, M
 from spark_rapids_ml_nai_amd.regression import RandomForestRegressionModel, RandomForestRegressor
 
 
+DEVICES = ["cpu", pytest.param("gpu", marks=pytest.mark.gpu)]
+
+
+@pytest.fixture(params=DEVICES)
+def device(request, monkeypatch):
+    """cpu: PyTorch reference path (CI); gpu: the HIP kernels on an MI355X."""
+    if request.param == "cpu":
+        monkeypatch.setenv("SRML_FORCE_CPU", "1")
+    else:
+        monkeypatch.delenv("SRML_FORCE_CPU", raising=False)
+    return request.param
+
+
 def _clf_data(n=1500, d=12, classes=2, seed=0):
     X, y = make_classification(n_samples=n, n_features=d, n_informative=6, n_redundant=2, n_classes=classes,
                                random_state=seed)
     return X.astype(np.float32), y.astype(np.float64)
 
 
-def test_rf_classifier_accessors_and_accuracy():
+def test_rf_classifier_accessors_and_accuracy(device):
     X, y = _clf_data()
     df = DataFrame.from_numpy(X, y)
     est = RandomForestClassifier(numTrees=8, maxDepth=6, seed=1)
@@ -62,7 +75,7 @@ def test_rf_classifier_accessors_and_accuracy():
         np.testing.assert_allclose(np.asarray(model.predictProbability(X[i]).toArray()), prob[i], atol=1e-5)
 
 
-def test_rf_classifier_multiclass_and_persistence(tmp_path):
+def test_rf_classifier_multiclass_and_persistence(device, tmp_path):
     X, y = _clf_data(n=1200, classes=3, seed=3)
     df = DataFrame.from_numpy(X, y)
     model = RandomForestClassifier(numTrees=6, maxDepth=7, seed=2).fit(df)
@@ -76,7 +89,7 @@ def test_rf_classifier_multiclass_and_persistence(tmp_path):
     assert m2.totalNumNodes == model.totalNumNodes
 
 
-def test_rf_regressor_quality_and_persistence(tmp_path):
+def test_rf_regressor_quality_and_persistence(device, tmp_path):
     X, y = make_regression(n_samples=2000, n_features=10, n_informative=5, noise=5.0, random_state=4)
     X = X.astype(np.float32)
     df = DataFrame.from_numpy(X, y)
@@ -91,7 +104,7 @@ def test_rf_regressor_quality_and_persistence(tmp_path):
     np.testing.assert_allclose(m2.transform(df).to_numpy("prediction"), pred, rtol=1e-6, atol=1e-6)
 
 
-def test_logistic_regression_persistence(tmp_path):
+def test_logistic_regression_persistence(device, tmp_path):
     X, y = _clf_data(n=800, seed=6)
     df = DataFrame.from_numpy(X, y)
     est = LogisticRegression(maxIter=50, regParam=0.01)
@@ -137,7 +150,7 @@ def test_classification_evaluators_match_sklearn():
     assert auc == pytest.approx(roc_auc_score(yb, score), abs=1e-6)
 
 
-def test_pca_attributes_match_sklearn():
+def test_pca_attributes_match_sklearn(device):
     from sklearn.decomposition import PCA as SkPCA
 
     from spark_rapids_ml_nai_amd.feature import PCA
@@ -157,7 +170,7 @@ def test_pca_attributes_match_sklearn():
     np.testing.assert_allclose(pc.T, comp, atol=1e-6)
 
 
-def test_kmeans_and_logreg_model_accessors():
+def test_kmeans_and_logreg_model_accessors(device):
     from spark_rapids_ml_nai_amd.clustering import KMeans
 
     rng = np.random.default_rng(10)
