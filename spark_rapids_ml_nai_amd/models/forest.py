@@ -260,7 +260,7 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
     if data_parallel:
         ctx.comm.allreduce(tot)
     n_leaves = np.ones(n_trees, dtype=np.int64)
-    nfc = (nf + 7) // 8
+    nfc = (nf + ops.RF_HIST_FB - 1) // ops.RF_HIST_FB
     hist_cell = (8 if regression else 4) * nf * B * SH
     group = max(1, HIST_BUDGET_BYTES // max(hist_cell, 1))
     depth = 0

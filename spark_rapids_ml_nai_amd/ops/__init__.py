@@ -353,6 +353,9 @@ def rf_quantize(X: torch.Tensor, edges: torch.Tensor) -> torch.Tensor:
     return out
 
 
+RF_HIST_FB = 8  # features per histogram work item (FB in csrc/forest.hip)
+
+
 def rf_hist(bins: torch.Tensor, idx: torch.Tensor, label: torch.Tensor, wcnt: Optional[torch.Tensor],
             items: torch.Tensor, node_feats: torch.Tensor, nodes: int, B: int, S: int,
             regression: bool, pos_weight: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -376,7 +379,7 @@ def rf_hist(bins: torch.Tensor, idx: torch.Tensor, label: torch.Tensor, wcnt: Op
             else:
                 w = wcnt[rows].double() if wcnt is not None else torch.ones(len(rows), dtype=torch.float64)
             y = label[rows]
-            for j in range(fc * 8, min(nf, fc * 8 + 8)):
+            for j in range(fc * RF_HIST_FB, min(nf, (fc + 1) * RF_HIST_FB)):
                 f = int(node_feats[node, j])
                 b = bins[f, rows].long()
                 if regression:

@@ -23,7 +23,7 @@
 #include "common.h"
 
 namespace {
-constexpr int FB = 8;  // features per histogram work item
+constexpr int FB = 8;   // features per histogram work item (ops.RF_HIST_FB)
 }
 
 // ------------------------------------------------------------------------------------------

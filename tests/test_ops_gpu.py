@@ -183,7 +183,8 @@ def test_rf_hist_split_route(gpu_device, regression):
     idx = torch.nonzero(w).view(-1).int()
     # two nodes: first 60% / rest of the in-bag rows
     cut = int(0.6 * idx.shape[0])
-    feats = torch.stack([torch.randperm(40, generator=torch.Generator().manual_seed(s))[:12] for s in (2, 3)]).int()
+    nf = ops.RF_HIST_FB + 4  # two feature chunks, the second one partial
+    feats = torch.stack([torch.randperm(40, generator=torch.Generator().manual_seed(s))[:nf] for s in (2, 3)]).int()
     items = []
     for node, (rb, re) in enumerate([(0, cut), (cut, idx.shape[0])]):
         for r0 in range(rb, re, 1000):
