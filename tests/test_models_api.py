@@ -194,3 +194,15 @@ def test_kmeans_and_logreg_model_accessors(device):
         _ = g.summary
     raw = g.transform(df).to_numpy("rawPrediction")
     np.testing.assert_allclose(np.asarray(g.predictRaw(X[5]).toArray()), raw[5], rtol=1e-5, atol=1e-6)
+
+
+def test_rf_hist_feature_chunk_constant_matches_kernel():
+    """The Python work-item builder and the HIP kernel must agree on features per item."""
+    import os
+    import re
+
+    from spark_rapids_ml_nai_amd import ops
+
+    src = open(os.path.join(os.path.dirname(ops.__file__), "csrc", "forest.hip")).read()
+    fb = int(re.search(r"constexpr int FB = (\d+);", src).group(1))
+    assert fb == ops.RF_HIST_FB
