@@ -60,7 +60,8 @@ def main() -> None:
                                 **({"device_id": device} if use_gpu and backend == "nccl" else {}))
 
     from spark_rapids_ml_nai_amd import DataFrame
-    from spark_rapids_ml_nai_amd.bench.suite import REF_GEOMEAN_SPEEDUP, REF_GPU_S, SPARK_CPU_S, geomean, make_shard, registry
+    from spark_rapids_ml_nai_amd.bench.suite import (REF_GEOMEAN_SPEEDUP, REF_GPU_S, SPARK_CPU_S, geomean, make_shard,
+                                                      model_evidence, registry)
     from spark_rapids_ml_nai_amd.ops import native
 
     if use_gpu:
@@ -114,6 +115,7 @@ def main() -> None:
                 "ref_gpu_fit_s": REF_GPU_S[name],
                 "vs_ref_gpu": round(REF_GPU_S[name] / per_fit, 1),
                 "phases": {k: round(v, 4) for k, v in getattr(model, "_fit_timings", {}).items()},
+                "evidence": model_evidence(name, model),
             }
             del df, Xh, yh, model
         except Exception as e:  # noqa: BLE001

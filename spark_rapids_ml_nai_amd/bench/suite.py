@@ -120,6 +120,33 @@ def registry() -> Dict[str, Workload]:
     return _registry()
 
 
+def model_evidence(name: str, model: Any) -> Dict[str, Any]:
+    """Per-workload proof that the fit did the work the reference config asks for (iteration
+    counts, objective, tree sizes), recorded next to its time in the bench JSON."""
+    ev: Dict[str, Any] = {}
+    try:
+        if name == "kmeans":
+            ev["n_iter"] = int(model._model_attributes.get("n_iter", 0))
+            ev["k"] = len(model.cluster_centers_)
+        elif name == "logistic_regression":
+            ev["num_iters"] = int(model.num_iters)
+            ev["objective"] = float(model.objective)
+            info = getattr(model, "_solver_info", None) or {}
+            ev.update({k: info[k] for k in ("n_evals", "status", "path") if k in info})
+        elif name.startswith("random_forest"):
+            ev["num_trees"] = int(model.getNumTrees)
+            ev["total_nodes"] = int(model.totalNumNodes)
+        elif name == "pca":
+            ev["explained_variance"] = [round(float(v), 6) for v in model.explained_variance_ratio_]
+        elif name.startswith("linear_regression"):
+            coef = np.asarray(model.coef_, dtype=np.float64)
+            ev["coef_l1"] = float(np.abs(coef).sum())
+            ev["nnz_coef"] = int(np.count_nonzero(coef))
+    except Exception as e:  # noqa: BLE001 - evidence is best effort, never fails the bench
+        ev["error"] = repr(e)[:120]
+    return ev
+
+
 def make_shard(family: str, m_local: int, n: int, device: torch.device, rank: int, m_total: int) -> Tuple[np.ndarray, Optional[np.ndarray]]:
     seed = 1000 + rank
     if family == "low_rank_matrix":

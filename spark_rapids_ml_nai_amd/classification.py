@@ -197,7 +197,11 @@ class LogisticRegression(LogisticRegressionClass, _EstimatorSupervised, _Logisti
         return _fit
 
     def _create_model(self, result: Dict[str, Any]) -> "LogisticRegressionModel":
-        return LogisticRegressionModel._from_row(result)
+        result = dict(result)
+        info = result.pop("_solver", None)  # device QN diagnostics (evaluations, stop reason, pass)
+        model = LogisticRegressionModel._from_row(result)
+        model._solver_info = info
+        return model
 
 
 class LogisticRegressionModel(LogisticRegressionClass, _ModelWithPredictionCol, _LogisticRegressionParams):

@@ -6,15 +6,16 @@ Reference: cuML ``LogisticRegressionMG`` (QN: L-BFGS / OWL-QN, ``lbfgs_memory=10
 done by the reference in cupy and the moments exchanged as JSON through the Spark driver.
 
 MI355X design:
-* the objective/gradient evaluation is ONE fused pass over the resident shard
-  (``srml_logreg_binary_f32``: margin, softplus loss, residual and X^T r from registers) plus ONE
-  coalesced RCCL all-reduce of [grad (n), grad_b, loss] in fp64; multinomial uses the
-  skinny ``xw`` GEMM (margins for all classes in one pass) + device softmax + ``xtv``;
+* every objective/gradient evaluation is ONE fused pass over the resident shard: binary
+  ``srml_logreg_binary2_f32`` (margin, softplus loss, residual and X^T r from registers),
+  multinomial ``srml_mlogit_f32`` (K margins, softmax, K gradient rows from one read of each row),
+  CSR kernels for sparse input, an LDS-accumulating pass for fp64 / wide rows; then ONE RCCL
+  all-reduce of [grad (K n), grad_b (K), loss] in fp64;
+* the quasi-Newton iteration (L-BFGS memory 10; OWL-QN for L1 / elastic-net) runs ON THE DEVICE
+  (``models/qn.py`` + ``ops/csrc/qn.hip``): no host round trip per evaluation; all ranks advance
+  identical optimiser states from the identical all-reduced sums;
 * standardisation never rewrites X: it is folded into the coefficients (z = X (w~/sigma) + b)
-  and the chain rule, with the column moments from one ``col_moments`` pass + all-reduce;
-* the quasi-Newton driver (L-BFGS-B, memory 10; L1 via the standard w = w+ - w- bound-
-  constrained split, i.e. the OWL-QN problem) runs replicated on every rank in fp64 — it is
-  deterministic, so all ranks take identical steps with no extra communication.
+  and the chain rule, with the column moments from one ``col_moments`` pass + all-reduce.
 
 Objective (Spark): 1/m sum_i loss_i + reg * [ (1-a)/2 sum_j q2_j w_j^2 + a sum_j q1_j |w_j| ]
 with q = sigma (standardization=True) or 1, intercepts unpenalised.
@@ -28,120 +29,13 @@ import torch
 
 from .. import ops
 from ..parallel.context import WorkerContext
-
-
-class _Evaluator:
-    """f(theta), grad(theta) of the data term, summed over ranks; theta in scaled coordinates."""
-
-    def __init__(self, X: Any, y: torch.Tensor, m_total: int, ctx: WorkerContext, sigma: np.ndarray,
-                 n_classes: int, fit_intercept: bool, sparse: bool) -> None:
-        self.X, self.y, self.m = X, y, float(m_total)
-        self.ctx = ctx
-        self.inv_sigma = np.where(sigma > 0, 1.0 / np.where(sigma > 0, sigma, 1.0), 0.0)
-        self.C = n_classes
-        self.K = 1 if n_classes <= 2 else n_classes
-        self.fit_intercept = fit_intercept
-        self.sparse = sparse
-        self.n = len(sigma)
-        self.dev = y.device
-        self.n_evals = 0
-        if self.K > 1:
-            self.Y = torch.nn.functional.one_hot(y.long(), self.K).to(torch.float32)
-        # per-evaluation H2D of the coefficients goes through one pinned staging buffer
-        self._w_host = torch.empty(self.n, dtype=torch.float64, pin_memory=self.dev.type == "cuda")
-        self._y32 = y if y.dtype == torch.float32 else y.to(torch.float32)
-        # binomial fused path on the GPU: persistent device w / result and a pinned result buffer,
-        # moved with raw stream-ordered copies (no per-copy allocator events, no pageable D2H)
-        self._fast = (self.K == 1 and self.dev.type == "cuda"
-                      and (sparse or (X.dtype == torch.float32 and self.n <= 4096)))
-        if self._fast:
-            self._w_dev = torch.empty(self.n, dtype=torch.float64, device=self.dev)
-            self._out_dev = torch.empty(self.n + 2, dtype=torch.float64, device=self.dev)
-            self._out_host = torch.empty(self.n + 2, dtype=torch.float64, pin_memory=True)
-
-    def _w_to_device(self, w: np.ndarray) -> torch.Tensor:
-        self._w_host.numpy()[:] = w
-        return self._w_host.to(self.dev, non_blocking=True)
-
-    def _margins(self, W: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-        if self.sparse:
-            return ops.csr_spmm(self.X, W.float(), b.float())
-        return ops.xw(self.X, W.float(), b.float())
-
-    def _xt(self, R: torch.Tensor) -> torch.Tensor:
-        if self.sparse:
-            return ops.csr_spmtm(self.X, R)
-        return ops.xtv(self.X, R)
-
-    def __call__(self, theta: np.ndarray) -> Tuple[float, np.ndarray]:
-        """theta = [w~ (K*n row-major), b (K)] -> (mean loss, gradient)."""
-        self.n_evals += 1
-        n, K = self.n, self.K
-        Wt = theta[: K * n].reshape(K, n)
-        b = theta[K * n: K * n + K] if self.fit_intercept else np.zeros(K)
-        W = (Wt * self.inv_sigma).T  # n x K, original-space coefficients
-        if self._fast:
-            self._w_host.numpy()[:] = W[:, 0]
-            ops.h2d_async(self._w_dev, self._w_host)
-            if self.sparse:
-                ops.csr_logreg_binary_loss_grad(self.X, self._y32, self._w_dev, float(b[0]), out=self._out_dev)
-            else:
-                ops.logreg_binary_loss_grad(self.X, self._y32, self._w_dev, float(b[0]), out=self._out_dev)
-            self.ctx.comm.allreduce(self._out_dev)
-            ops.d2h_sync(self._out_host, self._out_dev)
-            h = self._out_host.numpy()
-            gw = h[:n].reshape(n, 1)
-            gb = h[n: n + 1]
-            f = h[n + 1] / self.m
-            grad = np.zeros_like(theta)
-            grad[: K * n] = ((gw / self.m) * self.inv_sigma[:, None]).T.reshape(-1)
-            if self.fit_intercept:
-                grad[K * n: K * n + K] = gb / self.m
-            return float(f), grad
-        if K == 1 and self.sparse:
-            w_dev = self._w_to_device(W[:, 0])
-            out = ops.csr_logreg_binary_loss_grad(self.X, self._y32, w_dev, float(b[0]))
-            g_w, g_b, loss = out[:n].view(n, 1), out[n: n + 1], out[n + 1: n + 2]
-        elif K == 1 and self.X.dtype == torch.float32 and n <= 4096:
-            w_dev = self._w_to_device(W[:, 0])
-            out = ops.logreg_binary_loss_grad(self.X, self._y32, w_dev, float(b[0]))
-            g_w, g_b, loss = out[:n].view(n, 1), out[n: n + 1], out[n + 1: n + 2]
-        else:
-            Wd = torch.from_numpy(W).to(self.dev)
-            bd = torch.from_numpy(b).to(self.dev)
-            Z = self._margins(Wd, bd)
-            if K == 1:
-                z = Z.view(-1)
-                p = torch.sigmoid(z)
-                r = (p - self.y.float()).view(-1, 1)
-                loss = (torch.nn.functional.softplus(z) - self.y.float() * z).double().sum().view(1)
-            else:
-                lse = torch.logsumexp(Z, 1)
-                P = torch.exp(Z - lse.view(-1, 1))
-                r = P - self.Y
-                loss = (lse - (Z * self.Y).sum(1)).double().sum().view(1)
-            g_w = self._xt(r)
-            g_b = r.double().sum(0)
-            out = None
-        buf = torch.cat([g_w.reshape(-1).double(), g_b.reshape(-1).double(), loss.reshape(-1).double()])
-        self.ctx.comm.allreduce(buf)
-        h = buf.cpu().numpy()
-        gw = h[: n * K].reshape(n, K)
-        gb = h[n * K: n * K + K]
-        f = h[-1] / self.m
-        grad = np.zeros_like(theta)
-        grad[: K * n] = ((gw / self.m) * self.inv_sigma[:, None]).T.reshape(-1)
-        if self.fit_intercept:
-            grad[K * n: K * n + K] = gb / self.m
-        return float(f), grad
+from .qn import QNProblem, minimize
 
 
 def logistic_fit(X: Any, y: torch.Tensor, m_total: int, ctx: WorkerContext, reg: float, l1_ratio: float,
                  fit_intercept: bool, standardization: bool, max_iter: int, tol: float,
                  n_classes: Optional[int] = None, sparse: bool = False,
                  stats: Optional[Dict[str, Any]] = None) -> Dict[str, Any]:
-    from scipy.optimize import minimize
-
     n = X.shape[1]
     if stats is None:
         stats = logistic_stats(X, y, m_total, ctx, sparse)
@@ -159,7 +53,7 @@ def logistic_fit(X: Any, y: torch.Tensor, m_total: int, ctx: WorkerContext, reg:
         base.update(coef_=[[0.0] * n], intercept_=[float("inf") if cv == 1.0 else float("-inf")], num_iters=0,
                     objective=0.0)
         return base
-    ev = _Evaluator(X, y, m_total, ctx, sigma, C, fit_intercept, sparse)
+    inv_sigma = np.where(sigma > 0, 1.0 / np.where(sigma > 0, sigma, 1.0), 0.0)
     q1 = sigma if standardization else np.ones(n)
     q2 = sigma * sigma if standardization else np.ones(n)
     # penalties act on scaled coefficients w~ = w * sigma
@@ -176,53 +70,31 @@ def logistic_fit(X: Any, y: torch.Tensor, m_total: int, ctx: WorkerContext, reg:
         else:
             lc = np.log(np.maximum(counts[:K], 1.0))
             theta0[K * n:] = lc - lc.mean()
-    use_l1 = reg > 0 and l1_ratio > 0
-    l2_full = np.tile(pen_l2, K)
-    l1_full = np.tile(pen_l1, K)
+    P = QNProblem(n=n, K=K, fit_intercept=fit_intercept, m_total=float(m_total),
+                  l2=np.concatenate([np.tile(pen_l2, K), np.zeros(nb)]),
+                  l1=np.concatenate([np.tile(pen_l1 if l1_ratio > 0 and reg > 0 else np.zeros(n), K), np.zeros(nb)]),
+                  inv_sigma=inv_sigma, max_iter=max(0, int(max_iter)), tol=float(tol), M=10)
+    y32 = y if y.dtype == torch.float32 else y.to(torch.float32)
+    y32 = y32.contiguous()
 
-    def smooth(theta: np.ndarray) -> Tuple[float, np.ndarray]:
-        f, g = ev(theta)
-        w = theta[: K * n]
-        f += 0.5 * float(np.sum(l2_full * w * w))
-        g = g.copy()
-        g[: K * n] += l2_full * w
-        return f, g
+    def evaluate(w: torch.Tensor, b: torch.Tensor, flag: Optional[torch.Tensor], out: torch.Tensor) -> None:
+        ops.logistic_loss_grad(X, y32, w, b, K, out, flag)
 
-    # Breeze (Spark) stops on a 10-iteration relative function-value history; L-BFGS-B's one-step
-    # ftol test fires much earlier, so it is tightened to land on the same optimum
-    opts = {"maxiter": max(1, int(max_iter)), "maxcor": 10, "ftol": max(float(tol) * 1e-4, 1e-300), "gtol": 1e-12,
-            "maxfun": max(15000, 4 * int(max_iter))}
-    if not use_l1:
-        res = minimize(smooth, theta0, jac=True, method="L-BFGS-B", options=opts)
-        theta = res.x
-        nit = int(res.nit)
-        obj = float(res.fun)
-    else:
-        # OWL-QN problem as bound-constrained smooth problem: w = u - v, u, v >= 0
-        Kn = K * n
-
-        def split(z: np.ndarray) -> Tuple[float, np.ndarray]:
-            u, v, rest = z[:Kn], z[Kn: 2 * Kn], z[2 * Kn:]
-            th = np.concatenate([u - v, rest])
-            f, g = smooth(th)
-            f += float(np.sum(l1_full * (u + v)))
-            gz = np.concatenate([g[:Kn] + l1_full, -g[:Kn] + l1_full, g[Kn:]])
-            return f, gz
-
-        z0 = np.concatenate([np.maximum(theta0[:Kn], 0), np.maximum(-theta0[:Kn], 0), theta0[Kn:]])
-        bounds = [(0, None)] * (2 * Kn) + [(None, None)] * nb
-        res = minimize(split, z0, jac=True, method="L-BFGS-B", bounds=bounds, options=opts)
-        zz = res.x
-        theta = np.concatenate([zz[:Kn] - zz[Kn: 2 * Kn], zz[2 * Kn:]])
-        nit = int(res.nit)
-        obj = float(res.fun)
-    Wt = theta[: K * n].reshape(K, n)
-    inv_sigma = np.where(sigma > 0, 1.0 / np.where(sigma > 0, sigma, 1.0), 0.0)
-    W = Wt * inv_sigma
+    allreduce = ctx.comm.allreduce if ctx.world_size > 1 else None
+    path = ops.logistic_path(X, K)
+    res = minimize(P, theta0, evaluate, allreduce, y.device, batch=8 if not path.startswith("torch") else 2)
+    theta = res["theta"]
+    if ctx.world_size > 1:  # every rank holds the same state; make the model bit-identical anyway
+        th = torch.from_numpy(theta).to(ctx.device)
+        ctx.comm.broadcast(th, 0)
+        theta = th.cpu().numpy()
+    W = theta[: K * n].reshape(K, n) * inv_sigma
     b = theta[K * n:] if fit_intercept else np.zeros(K)
     if fit_intercept and K > 1:
         b = b - b.mean()  # Spark centres multinomial intercepts
-    base.update(coef_=W.tolist(), intercept_=[float(v) for v in b], num_iters=nit, objective=obj)
+    base.update(coef_=W.tolist(), intercept_=[float(v) for v in b], num_iters=int(res["iter"]),
+                objective=float(res["f"]))
+    base["_solver"] = {"n_evals": int(res["n_evals"]), "status": res["status"], "path": path}
     return base
 
 

@@ -13,7 +13,7 @@ from . import native
 
 __all__ = ["col_moments", "gram", "xw", "dgemm", "sign_flip", "is_native", "xtv", "row_sqnorm",
            "logreg_binary_loss_grad", "nearest_centroid", "cluster_sums", "csr_logreg_binary_loss_grad",
-           "csr_spmm", "csr_spmtm", "csr_col_moments"]
+           "csr_spmm", "csr_spmtm", "csr_col_moments", "logistic_loss_grad"]
 
 
 def is_native(t: torch.Tensor) -> bool:
@@ -204,8 +204,8 @@ def logreg_binary_loss_grad(X: torch.Tensor, y: torch.Tensor, w: torch.Tensor, b
     out = torch.zeros(n + 2, dtype=torch.float64, device=X.device) if out is None else zero_(out)
     wf = _c(w.to(device=X.device, dtype=torch.float64))
     yf = _c(y.to(torch.float32))
-    native.call("srml_logreg_binary_f32", X.data_ptr(), m, n, X.stride(0), yf.data_ptr(), wf.data_ptr(), float(b),
-                out.data_ptr(), native.stream(X.device))
+    native.call("srml_logreg_binary2_f32", X.data_ptr(), m, n, X.stride(0), yf.data_ptr(), wf.data_ptr(), float(b),
+                None, None, out.data_ptr(), native.stream(X.device))
     return out
 
 
@@ -1003,7 +1003,7 @@ def csr_logreg_binary_loss_grad(A, y: torch.Tensor, w: torch.Tensor, b: float,
     wf = _c(w.to(device=A.data.device, dtype=torch.float64))
     yf = _c(y.to(torch.float32))
     native.call("srml_csr_logreg_binary_" + _sfx(A), A.indptr.data_ptr(), A.indices.data_ptr(), A.data.data_ptr(),
-                m, n, A.data.numel(), yf.data_ptr(), wf.data_ptr(), float(b), out.data_ptr(),
+                m, n, A.data.numel(), yf.data_ptr(), wf.data_ptr(), float(b), None, None, out.data_ptr(),
                 native.stream(A.data.device))
     return out
 
@@ -1055,6 +1055,107 @@ def csr_col_moments(A) -> Tuple[torch.Tensor, torch.Tensor]:
     native.call("srml_csr_col_moments_" + _sfx(A), A.indices.data_ptr(), A.data.data_ptr(), A.data.numel(),
                 s.data_ptr(), q.data_ptr(), native.stream(dev))
     return s, q
+
+
+# ------------------------------------------------------------------------------------------
+# Logistic loss + gradient accumulation for the on-device quasi-Newton driver (models/qn.py)
+def _is_csr(X) -> bool:
+    return hasattr(X, "indptr") and hasattr(X, "indices")
+
+
+def logistic_path(X, K: int) -> str:
+    """Which device pass ``logistic_loss_grad`` uses for X (reported by the fit / asserted in tests)."""
+    if _is_csr(X):
+        if not X.data.is_cuda:
+            return "torch-cpu"
+        return "csr_binary" if K == 1 else ("csr_spmm" if K <= 16 else "torch")
+    if not X.is_cuda:
+        return "torch-cpu"
+    m, n = X.shape
+    if K == 1:
+        if X.dtype == torch.float32 and n <= 4096:
+            return "fused_binary_f32"
+        if X.dtype in (torch.float32, torch.float64) and n <= 16384:
+            return "lds_binary_" + ("f32" if X.dtype == torch.float32 else "f64")
+        return "torch"
+    if X.dtype == torch.float32 and int(native.lib().srml_mlogit_supported(n, K)):
+        return "fused_multinomial_f32"
+    return "torch"
+
+
+def logistic_loss_grad(X, y32: torch.Tensor, w: torch.Tensor, b: torch.Tensor, K: int, out: torch.Tensor,
+                       flag: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """ADD the summed logistic data term at (W, b) into ``out`` = [grad W (K*n, class-major) |
+    grad b (K) | loss sum] (fp64). K == 1: binary (labels 0/1, sigmoid); K >= 2: softmax over K
+    classes (labels 0..K-1). ``w`` (K*n) and ``b`` (K) are fp64 device tensors read by the kernel
+    (no host round trip); ``flag`` (device int32, optional): the kernels skip once it is non-zero.
+    X: dense (m, n) or CSR."""
+    path = logistic_path(X, K)
+    if _is_csr(X):
+        m, n = X.shape
+        dev = X.data.device
+    else:
+        X = _c(X)
+        m, n = X.shape
+        dev = X.device
+    if path.startswith("torch"):
+        if _is_csr(X):
+            Xs = _csr_torch(X)
+            Xs = Xs.to(torch.float64) if Xs.dtype != torch.float64 else Xs
+            W = w.double().view(K, n)
+            Z = (Xs @ W.t()) + b.double().view(1, K)
+        else:
+            Xd = X.double()
+            W = w.double().view(K, n)
+            Z = Xd @ W.t() + b.double().view(1, K)
+        yd = y32.double()
+        if K == 1:
+            z = Z.view(-1)
+            r = (torch.sigmoid(z) - yd).view(-1, 1)
+            loss = (torch.nn.functional.softplus(z) - yd * z).sum()
+        else:
+            lse = torch.logsumexp(Z, 1)
+            Y = torch.nn.functional.one_hot(yd.long(), K).double()
+            r = torch.exp(Z - lse.view(-1, 1)) - Y
+            loss = (lse - (Z * Y).sum(1)).sum()
+        if _is_csr(X):
+            G = (Xs.t() @ r).t()
+        else:
+            G = r.t() @ Xd
+        out[: K * n] += G.reshape(-1)
+        out[K * n: K * n + K] += r.sum(0)
+        out[K * n + K] += loss
+        return out
+    st = native.stream(dev)
+    fp = flag.data_ptr() if flag is not None else None
+    assert w.dtype == torch.float64 and b.dtype == torch.float64 and out.dtype == torch.float64
+    assert w.numel() == K * n and b.numel() == K and out.numel() == K * n + K + 1
+    if path == "csr_binary":
+        _csr_check(X)
+        native.call("srml_csr_logreg_binary_" + _sfx(X), X.indptr.data_ptr(), X.indices.data_ptr(), X.data.data_ptr(),
+                    m, n, X.data.numel(), y32.data_ptr(), w.data_ptr(), 0.0, b.data_ptr(), fp, out.data_ptr(), st)
+    elif path == "csr_spmm":
+        # margins (one SpMM pass, all classes) -> softmax residual on the device -> X^T R pass
+        Wt = w.view(K, n).t()
+        Z = csr_spmm(X, Wt, b).double()
+        lse = torch.logsumexp(Z, 1)
+        Y = torch.nn.functional.one_hot(y32.long(), K).double()
+        R = torch.exp(Z - lse.view(-1, 1)) - Y
+        out[K * n + K] += (lse - (Z * Y).sum(1)).sum()
+        out[K * n: K * n + K] += R.sum(0)
+        out[: K * n] += csr_spmtm(X, R.float()).t().reshape(-1)
+    elif path == "fused_binary_f32":
+        native.call("srml_logreg_binary2_f32", X.data_ptr(), m, n, X.stride(0), y32.data_ptr(), w.data_ptr(), 0.0,
+                    b.data_ptr(), fp, out.data_ptr(), st)
+    elif path.startswith("lds_binary"):
+        native.call("srml_logreg_binary_lds_" + path[-3:], X.data_ptr(), m, n, X.stride(0), y32.data_ptr(),
+                    w.data_ptr(), 0.0, b.data_ptr(), fp, out.data_ptr(), st)
+    elif path == "fused_multinomial_f32":
+        native.call("srml_mlogit_f32", X.data_ptr(), m, n, X.stride(0), y32.data_ptr(), w.data_ptr(), b.data_ptr(),
+                    fp, K, out.data_ptr(), st)
+    else:  # pragma: no cover
+        raise AssertionError(path)
+    return out
 
 
 # ------------------------------------------------------------------------------------------

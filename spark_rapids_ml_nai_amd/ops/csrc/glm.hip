@@ -127,7 +127,11 @@ __device__ __forceinline__ float softplus_f(float z) {
 template <int V, bool REREAD>
 __global__ __launch_bounds__(256) void logreg_binary_kernel(const float* __restrict__ X, long m, int n, long ld,
                                                             const float* __restrict__ y, const double* __restrict__ w,
-                                                            double b, double* __restrict__ out, long rows_per_block) {
+                                                            double b_in, const double* __restrict__ bptr,
+                                                            const int* __restrict__ flag, double* __restrict__ out,
+                                                            long rows_per_block) {
+  if (flag && *flag) return;  // the on-device quasi-Newton driver has converged
+  const double b = bptr ? *bptr : b_in;
   // w is kept in fp64 (LDS) and margins / losses are evaluated in fp64 so that the objective the
   // quasi-Newton line search sees is smooth to ~1e-15; X stays fp32 and the kernel stays
   // HBM-bound (fp64 FMA rate is far above the 1 FMA per 4 streamed bytes needed here).
@@ -217,8 +221,12 @@ __global__ __launch_bounds__(256) void logreg_binary_kernel(const float* __restr
 template <int V, int R>
 __global__ __launch_bounds__(256, 2) void logreg_binary_split_kernel(const float* __restrict__ X, long m, int n,
                                                                      long ld, const float* __restrict__ y,
-                                                                     const double* __restrict__ w, double b,
+                                                                     const double* __restrict__ w, double b_in,
+                                                                     const double* __restrict__ bptr,
+                                                                     const int* __restrict__ flag,
                                                                      double* __restrict__ out, long rows_per_block) {
+  if (flag && *flag) return;
+  const double b = bptr ? *bptr : b_in;
   __shared__ double part[2][R][4];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -307,8 +315,12 @@ __global__ __launch_bounds__(256, 2) void logreg_binary_split_kernel(const float
 template <int V, int R, int D, bool NT = false>
 __global__ __launch_bounds__(256, 2) void logreg_binary_pf_kernel(const float* __restrict__ X, long m, int n, long ld,
                                                                   const float* __restrict__ y,
-                                                                  const double* __restrict__ w, double b,
+                                                                  const double* __restrict__ w, double b_in,
+                                                                  const double* __restrict__ bptr,
+                                                                  const int* __restrict__ flag,
                                                                   double* __restrict__ out, long rows_per_block) {
+  if (flag && *flag) return;
+  const double b = bptr ? *bptr : b_in;
   __shared__ double part[2][R][4];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -404,8 +416,9 @@ __global__ __launch_bounds__(256, 2) void logreg_binary_pf_kernel(const float* _
   }
 }
 
-SRML_API int srml_logreg_binary_f32(const float* X, long m, int n, long ld, const float* y, const double* w, double b,
-                                    double* out, hipStream_t stream) {
+// b: intercept by value, or (bptr != null) read on the device; flag (optional): skip when *flag != 0
+SRML_API int srml_logreg_binary2_f32(const float* X, long m, int n, long ld, const float* y, const double* w, double b,
+                                     const double* bptr, const int* flag, double* out, hipStream_t stream) {
   if (m <= 0) return 0;
   // ~>= 120 rows per block: each block pays a w load and an n-wide fp64 atomic flush, so small
   // shards (the per-rank rows of a multi-GPU fit) want fewer blocks (125k rows: 1024 blocks
@@ -432,16 +445,16 @@ SRML_API int srml_logreg_binary_f32(const float* X, long m, int n, long ld, cons
     static const int nt = getenv("SRML_LOGREG_NT") ? atoi(getenv("SRML_LOGREG_NT")) : 1;  // nontemporal X stream: +2%
     const int VS = (n + 1023) / 1024;
 #define SRML_LR_PF(VV, RR, DD) \
-    hipLaunchKernelGGL((logreg_binary_pf_kernel<VV, RR, DD>), grid, blk, 0, stream, X, m, n, ld, y, w, b, out, rpb)
+    hipLaunchKernelGGL((logreg_binary_pf_kernel<VV, RR, DD>), grid, blk, 0, stream, X, m, n, ld, y, w, b, bptr, flag, out, rpb)
 #define SRML_LR_PF_V(RR, DD) \
     do { if (VS == 2) SRML_LR_PF(2, RR, DD); else if (VS == 3) SRML_LR_PF(3, RR, DD); else SRML_LR_PF(4, RR, DD); } while (0)
     if (rsel == 2 && dsel == 1) SRML_LR_PF_V(2, 1);
     else if (rsel == 2) SRML_LR_PF_V(2, 2);
     else if (dsel == 1) SRML_LR_PF_V(1, 1);
     else if (dsel == 3 && nt) {
-      if (VS == 2) hipLaunchKernelGGL((logreg_binary_pf_kernel<2, 1, 3, true>), grid, blk, 0, stream, X, m, n, ld, y, w, b, out, rpb);
-      else if (VS == 3) hipLaunchKernelGGL((logreg_binary_pf_kernel<3, 1, 3, true>), grid, blk, 0, stream, X, m, n, ld, y, w, b, out, rpb);
-      else hipLaunchKernelGGL((logreg_binary_pf_kernel<4, 1, 3, true>), grid, blk, 0, stream, X, m, n, ld, y, w, b, out, rpb);
+      if (VS == 2) hipLaunchKernelGGL((logreg_binary_pf_kernel<2, 1, 3, true>), grid, blk, 0, stream, X, m, n, ld, y, w, b, bptr, flag, out, rpb);
+      else if (VS == 3) hipLaunchKernelGGL((logreg_binary_pf_kernel<3, 1, 3, true>), grid, blk, 0, stream, X, m, n, ld, y, w, b, bptr, flag, out, rpb);
+      else hipLaunchKernelGGL((logreg_binary_pf_kernel<4, 1, 3, true>), grid, blk, 0, stream, X, m, n, ld, y, w, b, bptr, flag, out, rpb);
     }
     else if (dsel == 3) SRML_LR_PF_V(1, 3);
     else SRML_LR_PF_V(1, 2);
@@ -451,7 +464,7 @@ SRML_API int srml_logreg_binary_f32(const float* X, long m, int n, long ld, cons
     static const int rsel = getenv("SRML_LOGREG_R") ? atoi(getenv("SRML_LOGREG_R")) : 4;
     const int VS = (n + 1023) / 1024;
 #define SRML_LR_SPLIT(VV, RR) \
-    hipLaunchKernelGGL((logreg_binary_split_kernel<VV, RR>), grid, blk, 0, stream, X, m, n, ld, y, w, b, out, rpb)
+    hipLaunchKernelGGL((logreg_binary_split_kernel<VV, RR>), grid, blk, 0, stream, X, m, n, ld, y, w, b, bptr, flag, out, rpb)
     if (rsel == 8) {
       if (VS == 1) SRML_LR_SPLIT(1, 8); else if (VS == 2) SRML_LR_SPLIT(2, 8);
       else if (VS == 3) SRML_LR_SPLIT(3, 8); else SRML_LR_SPLIT(4, 8);
@@ -468,9 +481,9 @@ SRML_API int srml_logreg_binary_f32(const float* X, long m, int n, long ld, cons
 #define SRML_LR_LAUNCH(VV)                                                                                       \
   do {                                                                                                           \
     if (reread)                                                                                                  \
-      hipLaunchKernelGGL((logreg_binary_kernel<VV, true>), grid, blk, lds, stream, X, m, n, ld, y, w, b, out, rpb);  \
+      hipLaunchKernelGGL((logreg_binary_kernel<VV, true>), grid, blk, lds, stream, X, m, n, ld, y, w, b, bptr, flag, out, rpb);  \
     else                                                                                                         \
-      hipLaunchKernelGGL((logreg_binary_kernel<VV, false>), grid, blk, lds, stream, X, m, n, ld, y, w, b, out, rpb); \
+      hipLaunchKernelGGL((logreg_binary_kernel<VV, false>), grid, blk, lds, stream, X, m, n, ld, y, w, b, bptr, flag, out, rpb); \
   } while (0)
   if (V <= 1) SRML_LR_LAUNCH(1);
   else if (V <= 2) SRML_LR_LAUNCH(2);
@@ -480,4 +493,9 @@ SRML_API int srml_logreg_binary_f32(const float* X, long m, int n, long ld, cons
   else if (V <= 16) SRML_LR_LAUNCH(16);
   else return -2;  // n > 4096: caller uses the two-pass GEMV path
   return srml_status();
+}
+
+SRML_API int srml_logreg_binary_f32(const float* X, long m, int n, long ld, const float* y, const double* w, double b,
+                                    double* out, hipStream_t stream) {
+  return srml_logreg_binary2_f32(X, m, n, ld, y, w, b, nullptr, nullptr, out, stream);
 }

@@ -51,9 +51,13 @@ __global__ __launch_bounds__(256) void csr_logreg_binary_kernel(const long* __re
                                                                 const int* __restrict__ indices,
                                                                 const T* __restrict__ data, long m,
                                                                 const float* __restrict__ y,
-                                                                const double* __restrict__ w, double b,
+                                                                const double* __restrict__ w, double b_in,
+                                                                const double* __restrict__ bptr,
+                                                                const int* __restrict__ flag,
                                                                 double* __restrict__ grad,
                                                                 double* __restrict__ tail) {
+  if (flag && *flag) return;  // on-device quasi-Newton driver finished
+  const double b = bptr ? *bptr : b_in;
   constexpr int GPB = 256 / G;  // row groups per block
   constexpr int CACHE = 4;      // non-zeros per lane kept in registers between the two phases
   const int g = threadIdx.x / G;
@@ -206,12 +210,13 @@ static unsigned grid_for(long rows, int G) {
 
 template <typename T>
 static int csr_logreg_launch(const long* indptr, const int* indices, const T* data, long m, long nnz, const float* y,
-                             const double* w, double b, double* grad, double* tail, hipStream_t s) {
+                             const double* w, double b, const double* bptr, const int* flag, double* grad,
+                             double* tail, hipStream_t s) {
   if (m <= 0) return 0;
   const int G = pick_group(m, nnz);
   const dim3 grid(grid_for(m, G)), blk(256);
 #define SRML_CSR_LR(GG) \
-  hipLaunchKernelGGL((csr_logreg_binary_kernel<T, GG>), grid, blk, 0, s, indptr, indices, data, m, y, w, b, grad, tail)
+  hipLaunchKernelGGL((csr_logreg_binary_kernel<T, GG>), grid, blk, 0, s, indptr, indices, data, m, y, w, b, bptr, flag, grad, tail)
   switch (G) {
     case 4: SRML_CSR_LR(4); break;
     case 8: SRML_CSR_LR(8); break;
@@ -293,14 +298,14 @@ static int csr_moments_launch(const int* indices, const T* data, long nnz, doubl
 
 // out: [grad (n) | grad_b | loss], fp64, accumulated (caller zeroes it)
 SRML_API int srml_csr_logreg_binary_f32(const long* indptr, const int* indices, const float* data, long m, int n,
-                                        long nnz, const float* y, const double* w, double b, double* out,
-                                        hipStream_t s) {
-  return csr_logreg_launch<float>(indptr, indices, data, m, nnz, y, w, b, out, out + n, s);
+                                        long nnz, const float* y, const double* w, double b, const double* bptr,
+                                        const int* flag, double* out, hipStream_t s) {
+  return csr_logreg_launch<float>(indptr, indices, data, m, nnz, y, w, b, bptr, flag, out, out + n, s);
 }
 SRML_API int srml_csr_logreg_binary_f64(const long* indptr, const int* indices, const double* data, long m, int n,
-                                        long nnz, const float* y, const double* w, double b, double* out,
-                                        hipStream_t s) {
-  return csr_logreg_launch<double>(indptr, indices, data, m, nnz, y, w, b, out, out + n, s);
+                                        long nnz, const float* y, const double* w, double b, const double* bptr,
+                                        const int* flag, double* out, hipStream_t s) {
+  return csr_logreg_launch<double>(indptr, indices, data, m, nnz, y, w, b, bptr, flag, out, out + n, s);
 }
 SRML_API int srml_csr_spmm_f32(const long* indptr, const int* indices, const float* data, long m, long nnz,
                                const float* W, int k, const float* bias, float* Z, hipStream_t s) {

@@ -38,6 +38,14 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_xtv_f32": (_P, _L, _I, _L, _P, _I, _L, _P, _P),
     "srml_row_sqnorm_f32": (_P, _L, _I, _L, _P, _P),
     "srml_logreg_binary_f32": (_P, _L, _I, _L, _P, _P, _D, _P, _P),
+    "srml_logreg_binary2_f32": (_P, _L, _I, _L, _P, _P, _D, _P, _P, _P, _P),
+    "srml_logreg_binary_lds_f32": (_P, _L, _I, _L, _P, _P, _D, _P, _P, _P, _P),
+    "srml_logreg_binary_lds_f64": (_P, _L, _I, _L, _P, _P, _D, _P, _P, _P, _P),
+    "srml_mlogit_f32": (_P, _L, _I, _L, _P, _P, _P, _P, _I, _P, _P),
+    "srml_mlogit_supported": (_I, _I),
+    "srml_qn_step": (_P, _P),
+    "srml_qn_max_history": (),
+    "srml_qn_args_size": (),
     "srml_nearest_centroid_f32": (_P, _L, _I, _L, _P, _I, _L, _P, _P, _P),
     "srml_nn_finalize": (_P, _L, _P, _P, _P, _P),
     "srml_split_bf16x3": (_P, _L, _I, _L, _I, _L, _P, _P),
@@ -64,8 +72,8 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_rf_route": (_P, _L, _P, _P, _L, _P, _P, _P, _P, _P),
     "srml_rf_route_segments": (_P, _L, _P, _L, _P, _I, _P, _P, _P, _P, _P),
     "srml_rf_node_stats": (_P, _P, _P, _L, _P, _I, _I, _I, _P, _P),
-    "srml_csr_logreg_binary_f32": (_P, _P, _P, _L, _I, _L, _P, _P, _D, _P, _P),
-    "srml_csr_logreg_binary_f64": (_P, _P, _P, _L, _I, _L, _P, _P, _D, _P, _P),
+    "srml_csr_logreg_binary_f32": (_P, _P, _P, _L, _I, _L, _P, _P, _D, _P, _P, _P, _P),
+    "srml_csr_logreg_binary_f64": (_P, _P, _P, _L, _I, _L, _P, _P, _D, _P, _P, _P, _P),
     "srml_csr_spmm_f32": (_P, _P, _P, _L, _L, _P, _I, _P, _P, _P),
     "srml_csr_spmm_f64": (_P, _P, _P, _L, _L, _P, _I, _P, _P, _P),
     "srml_csr_spmtm_f32": (_P, _P, _P, _L, _L, _P, _I, _P, _P),
@@ -106,7 +114,7 @@ def _load() -> ctypes.CDLL:
             except AttributeError:
                 continue
             fn.argtypes = list(argt)
-            fn.restype = ctypes.c_int
+            fn.restype = ctypes.c_long if name == "srml_qn_args_size" else ctypes.c_int
         _lib = lib
         return lib
 

@@ -1,0 +1,245 @@
+"""On-device quasi-Newton (models/qn.py, ops/csrc/qn.hip) and LogisticRegression numerics.
+
+Oracles: scikit-learn's LogisticRegression under Spark's objective mapping
+(mean loss + reg * ((1 - a)/2 ||w||^2 + a ||w||_1)  <=>  sklearn C = 1 / (m * reg)), the reference's
+own test matrix (python/tests/test_logistic_regression.py: binomial / multinomial x L2 / L1 /
+elastic-net), and, for the kernels, the numpy state machine ``HostQN`` and a plain PyTorch fp64
+loss/gradient.
+"""
+import warnings
+
+import numpy as np
+import pytest
+import torch
+
+from spark_rapids_ml_nai_amd import DataFrame, ops
+from spark_rapids_ml_nai_amd.models.qn import HostQN, QNProblem, minimize
+
+warnings.filterwarnings("ignore")
+
+DEVICES = ["cpu", pytest.param("gpu", marks=pytest.mark.gpu)]
+
+
+@pytest.fixture(params=DEVICES)
+def device(request, monkeypatch):
+    if request.param == "cpu":
+        monkeypatch.setenv("SRML_FORCE_CPU", "1")
+    else:
+        monkeypatch.delenv("SRML_FORCE_CPU", raising=False)
+    return request.param
+
+
+def _data(m, n, classes, seed=0, dtype=np.float32):
+    from sklearn.datasets import make_classification
+
+    X, y = make_classification(n_samples=m, n_features=n, n_informative=max(2, n // 2), n_redundant=0,
+                               n_classes=classes, n_clusters_per_class=1, random_state=seed, class_sep=0.8)
+    return X.astype(dtype), y.astype(np.float64)
+
+
+def _sk(X, y, reg, a, multi):
+    from sklearn.linear_model import LogisticRegression as SK
+
+    m = X.shape[0]
+    C = 1.0 / (m * reg)
+    if a == 0.0:
+        sk = SK(C=C, penalty="l2", solver="lbfgs", tol=1e-12, max_iter=20000)
+    else:
+        sk = SK(C=C, penalty="elasticnet", l1_ratio=a, solver="saga", tol=1e-12, max_iter=200000)
+    sk.fit(X.astype(np.float64), y)
+    return sk.coef_, sk.intercept_
+
+
+def _spark_objective(X, y, W, b, reg, a):
+    """Spark's (unstandardised) objective evaluated in fp64."""
+    X = X.astype(np.float64)
+    Z = X @ W.T + b
+    if W.shape[0] == 1:
+        z = Z[:, 0]
+        loss = np.mean(np.logaddexp(0, z) - y * z)
+    else:
+        lse = np.logaddexp.reduce(Z, axis=1)
+        loss = np.mean(lse - Z[np.arange(len(y)), y.astype(int)])
+    return loss + reg * ((1 - a) / 2 * np.sum(W * W) + a * np.sum(np.abs(W)))
+
+
+@pytest.mark.parametrize("classes,reg,a", [(2, 1e-2, 0.0), (2, 3e-3, 1.0), (2, 1e-2, 0.5), (4, 1e-2, 0.0),
+                                           (3, 5e-3, 0.5)])
+def test_logistic_vs_sklearn(device, classes, reg, a):
+    """Binomial / multinomial x L2 / L1 / elastic-net against sklearn (Spark objective mapping)."""
+    from spark_rapids_ml_nai_amd.classification import LogisticRegression
+
+    X, y = _data(600, 12, classes, seed=classes)
+    model = LogisticRegression(regParam=reg, elasticNetParam=a, standardization=False, maxIter=2000,
+                               tol=1e-12).fit(DataFrame.from_numpy(X, y))
+    W = np.asarray(model.coef_)
+    b = np.asarray(model.intercept_)
+    Wsk, bsk = _sk(X, y, reg, a, classes > 2)
+    if classes > 2:
+        bsk = bsk - bsk.mean()
+    f_ours = _spark_objective(X, y, W, b, reg, a)
+    f_sk = _spark_objective(X, y, Wsk, bsk, reg, a)
+    # same optimum: objective within 1e-7 relative, coefficients within 2e-3
+    assert f_ours <= f_sk * (1 + 1e-7) + 1e-12, (f_ours, f_sk)
+    np.testing.assert_allclose(W, Wsk, atol=2e-3, rtol=2e-3)
+    np.testing.assert_allclose(b, bsk, atol=2e-3, rtol=2e-3)
+    if a > 0:  # OWL-QN produces exact zeros where sklearn's saga does
+        assert np.all((np.abs(Wsk) < 1e-6) <= (np.abs(W) < 1e-5))
+
+
+def test_logistic_standardization_matches_scaled_problem(device):
+    """standardization=True == the unstandardised fit of X / sigma (Spark's definition)."""
+    from spark_rapids_ml_nai_amd.classification import LogisticRegression
+
+    X, y = _data(500, 6, 2, seed=7)
+    X[:, 1] *= 25.0
+    sig = X.astype(np.float64).std(0, ddof=1)
+    m1 = LogisticRegression(regParam=0.02, standardization=True, maxIter=1000, tol=1e-12).fit(DataFrame.from_numpy(X, y))
+    m2 = LogisticRegression(regParam=0.02, standardization=False, maxIter=1000, tol=1e-12).fit(
+        DataFrame.from_numpy((X / sig).astype(np.float32), y))
+    np.testing.assert_allclose(np.asarray(m1.coef_)[0] * sig, np.asarray(m2.coef_)[0], rtol=2e-3, atol=2e-4)
+
+
+def test_host_qn_quadratic():
+    """L-BFGS on a convex quadratic reaches the exact minimiser (compact-form direction)."""
+    rng = np.random.default_rng(0)
+    n = 30
+    A = rng.standard_normal((n, n))
+    H = A @ A.T + n * np.eye(n)
+    c = rng.standard_normal(n)
+    P = QNProblem(n=n, K=1, fit_intercept=False, m_total=1.0, l2=np.zeros(n), l1=np.zeros(n),
+                  inv_sigma=np.ones(n), max_iter=500, tol=1e-14)
+    st = HostQN(P, np.zeros(n))
+    while not st.done:
+        w = st.wb()[:n]
+        out = np.concatenate([H @ w - c, [0.0], [0.5 * w @ H @ w - c @ w]])
+        st.step(out)
+    np.testing.assert_allclose(st.x, np.linalg.solve(H, c), rtol=1e-8, atol=1e-10)
+    assert st.iter < 100
+
+
+def test_host_qn_l1_sparsity():
+    """OWL-QN on a lasso problem: the known soft-threshold solution of a diagonal quadratic."""
+    n = 8
+    h = np.arange(1, n + 1, dtype=np.float64)
+    c = np.linspace(-2, 2, n)
+    lam = 0.7
+    P = QNProblem(n=n, K=1, fit_intercept=False, m_total=1.0, l2=np.zeros(n), l1=np.full(n, lam),
+                  inv_sigma=np.ones(n), max_iter=500, tol=1e-14)
+    st = HostQN(P, np.zeros(n))
+    while not st.done:
+        w = st.wb()[:n]
+        st.step(np.concatenate([h * w - c, [0.0], [0.5 * np.sum(h * w * w) - c @ w]]))
+    expect = np.sign(c) * np.maximum(np.abs(c) - lam, 0) / h
+    np.testing.assert_allclose(st.x, expect, atol=1e-8)
+    assert np.all(st.x[np.abs(c) <= lam] == 0.0)
+
+
+def test_logistic_reports_solver_path(device):
+    from spark_rapids_ml_nai_amd.classification import LogisticRegression
+
+    X, y = _data(300, 8, 3, seed=3)
+    model = LogisticRegression(regParam=1e-2, maxIter=50).fit(DataFrame.from_numpy(X, y))
+    info = model._solver_info
+    assert info["n_evals"] >= model.num_iters >= 1
+    if device == "gpu":
+        assert info["path"] == "fused_multinomial_f32"
+    else:
+        assert info["path"] == "torch-cpu"
+
+
+# ---------------------------------------------------------------------------------- GPU kernels
+def _ref_loss_grad(X, y, W, b, K):
+    Xd = X.double().cpu()
+    yd = y.double().cpu()
+    Wd = W.double().cpu().view(K, -1)
+    Z = Xd @ Wd.T + b.double().cpu().view(1, K)
+    if K == 1:
+        z = Z.view(-1)
+        r = (torch.sigmoid(z) - yd).view(-1, 1)
+        loss = (torch.nn.functional.softplus(z) - yd * z).sum()
+    else:
+        lse = torch.logsumexp(Z, 1)
+        Y = torch.nn.functional.one_hot(yd.long(), K).double()
+        r = torch.exp(Z - lse.view(-1, 1)) - Y
+        loss = (lse - (Z * Y).sum(1)).sum()
+    return torch.cat([(r.T @ Xd).reshape(-1), r.sum(0), loss.view(1)])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,n,K,dtype,path", [
+    (5000, 3000, 1, torch.float32, "fused_binary_f32"),
+    (3001, 130, 1, torch.float32, "fused_binary_f32"),
+    (2000, 5000, 1, torch.float32, "lds_binary_f32"),
+    (3000, 257, 1, torch.float64, "lds_binary_f64"),
+    (4000, 3000, 10, torch.float32, "fused_multinomial_f32"),
+    (3000, 129, 3, torch.float32, "fused_multinomial_f32"),
+    (2500, 1001, 16, torch.float32, "fused_multinomial_f32"),
+    (2000, 4096, 5, torch.float32, "fused_multinomial_f32"),
+    (1500, 300, 20, torch.float32, "torch"),
+])
+def test_logistic_loss_grad_kernels(gpu_device, m, n, K, dtype, path):
+    g = torch.Generator().manual_seed(m + n + K)
+    X = torch.randn(m, n, generator=g, dtype=torch.float64).to(dtype).to(gpu_device)
+    if K == 1:
+        y = (torch.rand(m, generator=g) < 0.4).float().to(gpu_device)
+    else:
+        y = torch.randint(0, K, (m,), generator=g).float().to(gpu_device)
+    Kk = K
+    W = (0.05 * torch.randn(Kk * n, generator=g, dtype=torch.float64)).to(gpu_device)
+    b = (0.3 * torch.randn(Kk, generator=g, dtype=torch.float64)).to(gpu_device)
+    assert ops.logistic_path(X, Kk) == path
+    out = torch.zeros(Kk * n + Kk + 1, dtype=torch.float64, device=gpu_device)
+    ops.logistic_loss_grad(X, y, W, b, Kk, out)
+    ops.logistic_loss_grad(X, y, W, b, Kk, out)  # accumulates
+    ref = 2 * _ref_loss_grad(X, y, W, b, Kk)
+    got = out.cpu()
+    scale = ref[:-1].abs().max().item()
+    assert (got[:-1] - ref[:-1]).abs().max().item() <= 2e-5 * scale + 1e-6
+    assert abs(got[-1].item() - ref[-1].item()) <= 1e-5 * abs(ref[-1].item())
+    # the done flag short-circuits the pass
+    flag = torch.ones(1, dtype=torch.int32, device=gpu_device)
+    out2 = torch.zeros_like(out)
+    ops.logistic_loss_grad(X, y, W, b, Kk, out2, flag)
+    if not path.startswith("torch"):
+        assert out2.abs().max().item() == 0.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K,l1", [(1, 0.0), (1, 0.01), (4, 0.0), (3, 0.02)])
+def test_qn_kernel_matches_host(gpu_device, K, l1):
+    """The device state machine takes the same path as HostQN on a logistic problem."""
+    m, n = 2000, 40
+    g = torch.Generator().manual_seed(11 + K)
+    Xc = torch.randn(m, n, generator=g, dtype=torch.float64)
+    if K == 1:
+        y = (Xc[:, 0] + 0.5 * torch.randn(m, generator=g, dtype=torch.float64) > 0).double()
+    else:
+        y = torch.argmax(Xc[:, :K] + 0.5 * torch.randn(m, K, generator=g, dtype=torch.float64), 1).double()
+    N = K * n + K
+    P = QNProblem(n=n, K=K, fit_intercept=True, m_total=float(m),
+                  l2=np.concatenate([np.full(K * n, 0.01), np.zeros(K)]),
+                  l1=np.concatenate([np.full(K * n, l1), np.zeros(K)]),
+                  inv_sigma=np.linspace(0.5, 1.5, n), max_iter=60 if l1 == 0.0 else 300, tol=1e-12)
+
+    def ev_cpu(w, b, flag, out):
+        out += _ref_loss_grad(Xc, y, w, b, K)
+
+    host = minimize(P, np.zeros(N), ev_cpu, None, torch.device("cpu"))
+    Xg, yg = Xc.to(gpu_device), y.to(gpu_device)
+
+    def ev_gpu(w, b, flag, out):
+        out += _ref_loss_grad(Xg, yg, w, b, K).to(gpu_device)
+
+    dev = minimize(P, np.zeros(N), ev_gpu, None, gpu_device, batch=4)
+    info = {k: (host[k], dev[k]) for k in ("iter", "n_evals", "status", "f")}
+    if l1 == 0.0:
+        # smooth problem: identical decisions, states equal to rounding
+        assert dev["iter"] == host["iter"] and dev["status"] == host["status"], info
+        assert abs(dev["f"] - host["f"]) <= 1e-10 * abs(host["f"]), info
+        np.testing.assert_allclose(dev["theta"], host["theta"], rtol=1e-6, atol=1e-8)
+    else:
+        # OWL-QN's orthant projections make the path sensitive to the last bit of the reductions:
+        # require the same optimum instead of the same trajectory
+        assert abs(dev["f"] - host["f"]) <= 1e-7 * abs(host["f"]), info
+        np.testing.assert_allclose(dev["theta"], host["theta"], atol=2e-3)
