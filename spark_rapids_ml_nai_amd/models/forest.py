@@ -63,12 +63,17 @@ def feature_subset_size(strategy: Any, n: int, n_trees: int, classification: boo
 
 
 def bin_edges(X: torch.Tensor, n_bins: int, ctx: WorkerContext, m_total: int, seed: int,
-              sample_rows: int = 1 << 16) -> torch.Tensor:
-    """(n, n_bins-1) fp32 quantile edges, identical on every rank (sampled rows all-gathered)."""
+              sample_rows: Optional[int] = None) -> torch.Tensor:
+    """(n, n_bins-1) fp32 quantile edges, identical on every rank (sampled rows all-gathered).
+
+    Sample size follows Spark's ``findSplits`` (max(maxBins^2, 10000) rows over the whole dataset,
+    capped at the 32768 the per-feature LDS sort holds)."""
     m, n = X.shape
+    if sample_rows is None:
+        sample_rows = min(32768, max(n_bins * n_bins, 10000))
     g = torch.Generator(device="cpu")
     g.manual_seed(int(seed) * 7919 + ctx.rank)
-    want = max(1, int(round(sample_rows * m / max(m_total, 1))))
+    want = max(1, int(sample_rows * m // max(m_total, 1)))
     if m > want:
         sel = torch.randperm(m, generator=g)[:want].sort().values.to(X.device)
         S = X.index_select(0, sel).float()
@@ -76,12 +81,7 @@ def bin_edges(X: torch.Tensor, n_bins: int, ctx: WorkerContext, m_total: int, se
         S = X.float()
     if ctx.world_size > 1:
         S = torch.cat([p.to(X.device) for p in ctx.comm.allgatherv(S.contiguous())], 0)
-    Ss, _ = torch.sort(S, 0)
-    k = Ss.shape[0]
-    q = torch.arange(1, n_bins, device=X.device, dtype=torch.float64) / n_bins
-    pos = (q * k).long().clamp(0, k - 1)
-    E = Ss.index_select(0, pos).T.contiguous()  # (n, B-1), non-decreasing per feature
-    return E
+    return ops.rf_quantiles(S, n_bins - 1)  # (n, B-1), non-decreasing per feature
 
 
 @dataclass
@@ -260,7 +260,9 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
     if data_parallel:
         ctx.comm.allreduce(tot)
     n_leaves = np.ones(n_trees, dtype=np.int64)
-    nfc = (nf + ops.RF_HIST_FB - 1) // ops.RF_HIST_FB
+    fb = ops.rf_hist_fb(B, SH, regression)  # features per histogram work item (fits the LDS slab)
+    nfc = (nf + fb - 1) // fb
+    yscale = ops.rf_yscale(yv) if regression and dev.type == "cuda" else None
     hist_cell = (8 if regression else 4) * nf * B * SH
     group = max(1, HIST_BUDGET_BYTES // max(hist_cell, 1))
     depth = 0
@@ -305,7 +307,8 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
             it[:, 2] = np.repeat(re, nfc)
             it[:, 3] = np.tile(np.arange(nfc), tot_ch)
             items_t = torch.from_numpy(it).to(dev, non_blocking=False)
-            hist = ops.rf_hist(bins, idx, yv, None, items_t, feats, C, B, SH, regression, pos_weight=wpos)
+            hist = ops.rf_hist(bins, idx, yv, None, items_t, feats, C, B, SH, regression, pos_weight=wpos, fb=fb,
+                               yscale=yscale)
             if data_parallel:
                 ctx.comm.allreduce(hist)
             out, _ = ops.rf_best_split(hist, B, SH, regression, crit, min_leaf, min_gain)

@@ -353,14 +353,53 @@ def rf_quantize(X: torch.Tensor, edges: torch.Tensor) -> torch.Tensor:
     return out
 
 
-RF_HIST_FB = 8  # features per histogram work item (FB in csrc/forest.hip)
+def rf_quantiles(S: torch.Tensor, nq: int) -> torch.Tensor:
+    """(n, nq) fp32 order statistics floor(q_j k), q_j = (j + 1) / (nq + 1), of every column of the
+    (k, n) sample S (NaN ranks as +inf). GPU: one LDS bitonic sort per feature (k <= 32768)."""
+    k, n = S.shape
+    if not S.is_cuda or k > 32768:
+        Ss, _ = torch.sort(torch.nan_to_num(S.float(), nan=float("inf")), 0)
+        q = torch.arange(1, nq + 1, device=S.device, dtype=torch.float64) / (nq + 1)
+        pos = (q * k).long().clamp(0, k - 1)
+        return Ss.index_select(0, pos).T.contiguous()
+    ST = S.float().T.contiguous()  # feature-major: each block reads one contiguous column
+    out = torch.empty((n, nq), dtype=torch.float32, device=S.device)
+    native.call("srml_rf_quantiles_f32", ST.data_ptr(), k, n, nq, out.data_ptr(), native.stream(S.device))
+    return out
+
+
+RF_HIST_FB_MAX = 8  # FB in csrc/forest.hip (checked against srml_rf_hist_fb_max on load in tests)
+
+
+def rf_yscale(y: torch.Tensor) -> float:
+    """Fixed-point scale of the regression histograms' i64 w*y sums: |block sum| <= 65536 rows *
+    255 * max|y| < 2^24 max|y|, so 2^38 / max|y| keeps 63 bits."""
+    ymax = float(y.abs().max().item()) if y.numel() else 0.0
+    return float(2.0 ** 38 / ymax) if ymax > 0 else 1.0
+
+
+def rf_hist_fb(B: int, S: int, regression: bool) -> int:
+    """Features per histogram work item for (B bins, S stats): the per-item LDS slab
+    fb * B * S' * 4 bytes (S' = 3 for regression: count + 64-bit fixed-point sum) fits 64 KiB;
+    mirrors ``srml_rf_hist_fb``. Raises for histograms that do not fit the 160 KiB LDS at all."""
+    per = B * (3 if regression else S) * 4
+    fb = min(RF_HIST_FB_MAX, (64 * 1024) // max(per, 1))
+    if fb < 1:
+        if per > 160 * 1024:
+            raise ValueError(f"histogram of {B} bins x {S} classes ({per} bytes per feature) exceeds the 160 KiB LDS")
+        fb = 1
+    return int(fb)
 
 
 def rf_hist(bins: torch.Tensor, idx: torch.Tensor, label: torch.Tensor, wcnt: Optional[torch.Tensor],
             items: torch.Tensor, node_feats: torch.Tensor, nodes: int, B: int, S: int,
-            regression: bool, pos_weight: Optional[torch.Tensor] = None) -> torch.Tensor:
+            regression: bool, pos_weight: Optional[torch.Tensor] = None, fb: Optional[int] = None,
+            yscale: Optional[float] = None) -> torch.Tensor:
     """Per-(node, feature slot, bin) statistics: uint32 class counts or fp64 (count, sum[, sumsq]).
-    Weights: per row (``wcnt``, indexed by row id) or per position of ``idx`` (``pos_weight``)."""
+    Weights: per row (``wcnt``, indexed by row id) or per position of ``idx`` (``pos_weight``).
+    ``items`` rows are (node, row_begin, row_end, feature_chunk) with chunks of ``fb`` features
+    (default ``rf_hist_fb(B, S, regression)``)."""
+    fb = rf_hist_fb(B, S, regression) if fb is None else int(fb)
     n, m = bins.shape
     nf = node_feats.shape[1]
     dev = bins.device
@@ -379,7 +418,7 @@ def rf_hist(bins: torch.Tensor, idx: torch.Tensor, label: torch.Tensor, wcnt: Op
             else:
                 w = wcnt[rows].double() if wcnt is not None else torch.ones(len(rows), dtype=torch.float64)
             y = label[rows]
-            for j in range(fc * RF_HIST_FB, min(nf, (fc + 1) * RF_HIST_FB)):
+            for j in range(fc * fb, min(nf, (fc + 1) * fb)):
                 f = int(node_feats[node, j])
                 b = bins[f, rows].long()
                 if regression:
@@ -398,16 +437,16 @@ def rf_hist(bins: torch.Tensor, idx: torch.Tensor, label: torch.Tensor, wcnt: Op
     else:
         wv = wcnt[rows].float() if wcnt is not None else torch.ones(rows.shape[0], dtype=torch.float32, device=dev)
     wy = torch.stack([wv, label[rows].float()], 1).contiguous()
-    yscale = 1.0
     if regression:
         if S != 2:
             raise ValueError("device regression histograms carry (count, sum): S must be 2")
-        # i64 fixed point for w*y: |block sum| <= 65536 rows * 255 * max|y| < 2^24 max|y|
-        ymax = float(wy[:, 1].abs().max().item()) if wy.shape[0] else 0.0
-        yscale = float(2.0 ** 38 / ymax) if ymax > 0 else 1.0
+        if yscale is None:  # callers growing many levels pass rf_yscale(y) once per fit (no host sync here)
+            yscale = rf_yscale(wy[:, 1])
+    else:
+        yscale = 1.0
     st = native.stream(dev)
     native.call("srml_rf_hist", bins.data_ptr(), m, idx.data_ptr(), wy.data_ptr(), _c(items).data_ptr(),
-                int(items.shape[0]), _c(node_feats).data_ptr(), nf, B, S, int(regression), yscale,
+                int(items.shape[0]), _c(node_feats).data_ptr(), nf, B, S, int(regression), float(yscale), fb,
                 hist.data_ptr() if not regression else None, hist.data_ptr() if regression else None, st)
     return hist
 

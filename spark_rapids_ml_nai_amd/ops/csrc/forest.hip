@@ -23,63 +23,133 @@
 #include "common.h"
 
 namespace {
-constexpr int FB = 8;   // features per histogram work item (ops.RF_HIST_FB)
+constexpr int FB = 8;   // max features per histogram work item (runtime fb <= FB; ops.rf_hist_fb)
 }
 
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void rf_quantize_kernel(const float* __restrict__ X, long m, int n, long ld,
-                                                          const float* __restrict__ edges, int nedges,
-                                                          unsigned char* __restrict__ out) {
-  __shared__ unsigned char tile[32][256 + 4];
-  const long r0 = (long)blockIdx.x * 256;
-  const int f0 = blockIdx.y * 32;
-  const int t = threadIdx.x;
-  const int fl = t & 31;
-  const int f = f0 + fl;
-  const float* e = edges + (long)min(f, n - 1) * nedges;
-#pragma unroll 4
-  for (int p = 0; p < 32; ++p) {
-    const int rl = (t >> 5) + 8 * p;
-    const long r = r0 + rl;
-    unsigned char b = 0;
-    if (r < m && f < n) {
-      const float x = X[r * ld + f];
-      // number of edges strictly below x  (x <= e[b]  <=>  bin(x) <= b)
-      int lo = 0, hi = nedges;
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (e[mid] < x) lo = mid + 1; else hi = mid;
-      }
-      b = (unsigned char)lo;
-    }
-    tile[fl][rl] = b;
+// Quantile bin edges: one block per feature sorts that feature's (transposed, contiguous) sample
+// column in LDS with a bitonic network (k <= 32768, padded to a power of two with +inf; NaN sorts
+// as +inf) and writes the order statistics floor(q_j * k), q_j = (j + 1) / (nq + 1). Replaces a
+// segmented device sort of the whole (k x n) sample plus its index permutations (~15 ms / fit).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void rf_quantiles_kernel(const float* __restrict__ ST, int k, int kpad, int nq,
+                                                            float* __restrict__ out) {
+  extern __shared__ float key[];  // [kpad]
+  const int f = blockIdx.x;
+  const float* col = ST + (long)f * k;
+  for (int i = threadIdx.x; i < kpad; i += 1024) {
+    float v = i < k ? col[i] : INFINITY;
+    key[i] = (v != v) ? INFINITY : v;
   }
   __syncthreads();
-  // 32 features x 256 rows: each thread writes 4 consecutive bytes of one feature row
+  for (int size = 2; size <= kpad; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = threadIdx.x; i < (kpad >> 1); i += 1024) {
+        const int pos = 2 * i - (i & (stride - 1));
+        const int q = pos + stride;
+        const float a = key[pos], b = key[q];
+        const bool asc = (pos & size) == 0;
+        if ((a > b) == asc) {
+          key[pos] = b;
+          key[q] = a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int j = threadIdx.x; j < nq; j += 1024) {
+    long p = (long)((double)(j + 1) / (double)(nq + 1) * (double)k);
+    if (p > k - 1) p = k - 1;
+    if (p < 0) p = 0;
+    out[(long)f * nq + j] = key[p];
+  }
+}
+
+SRML_API int srml_rf_quantiles_f32(const float* ST, int k, int n, int nq, float* out, hipStream_t stream) {
+  if (n <= 0 || nq <= 0) return 0;
+  if (k <= 0 || k > 32768) return (int)hipErrorInvalidValue;
+  int kpad = 2;
+  while (kpad < k) kpad <<= 1;
+  const size_t lds = (size_t)kpad * sizeof(float);
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)rf_quantiles_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(rf_quantiles_kernel, dim3((unsigned)n), dim3(1024), lds, stream, ST, k, kpad, nq, out);
+  return srml_status();
+}
+
+// ------------------------------------------------------------------------------------------
+// Quantisation: a block owns 32 features x QROWS rows. The 32 edge tables are staged in LDS
+// (row stride NE2 + 1 floats: table f starts in bank f, so the first search step of the 32 lanes
+// reading one row is conflict-free), and bin(x) = #edges strictly below x is a branchless
+// lower_bound over the +inf-padded power-of-two table (log2 NE2 LDS reads, no divergence).
+// Rows are processed 256 at a time: coalesced fp32 reads (32 features = 128 B per row), the
+// byte tile is transposed in LDS and written as 256-byte feature rows.
+// ------------------------------------------------------------------------------------------
+constexpr int QROWS = 1024;
+
+__global__ __launch_bounds__(256) void rf_quantize_kernel(const float* __restrict__ X, long m, int n, long ld,
+                                                          const float* __restrict__ edges, int nedges, int ne2,
+                                                          unsigned char* __restrict__ out) {
+  extern __shared__ float etab[];  // [32][ne2 + 1]
+  __shared__ unsigned char tile[32][256 + 4];
+  const int f0 = blockIdx.y * 32;
+  const int t = threadIdx.x;
+  const int es = ne2 + 1;
+  for (int i = t; i < 32 * ne2; i += 256) {
+    const int fl = i / ne2, j = i - fl * ne2;
+    const int f = f0 + fl;
+    etab[fl * es + j] = (f < n && j < nedges) ? edges[(long)f * nedges + j] : INFINITY;
+  }
+  __syncthreads();
+  const int fl = t & 31;
+  const int f = f0 + fl;
+  const float* e = etab + fl * es;
+  for (long r0 = (long)blockIdx.x * QROWS; r0 < min(m, (long)(blockIdx.x + 1) * QROWS); r0 += 256) {
+#pragma unroll 4
+    for (int p = 0; p < 32; ++p) {
+      const int rl = (t >> 5) + 8 * p;
+      const long r = r0 + rl;
+      unsigned char b = 0;
+      if (r < m && f < n) {
+        const float x = X[r * ld + f];
+        int lo = 0;
+        for (int step = ne2 >> 1; step > 0; step >>= 1) lo = (e[lo + step - 1] < x) ? lo + step : lo;
+        b = (unsigned char)lo;
+      }
+      tile[fl][rl] = b;
+    }
+    __syncthreads();
+    // 32 features x 256 rows: each thread writes 4 consecutive bytes of one feature row
 #pragma unroll
-  for (int p = 0; p < 8; ++p) {
-    const int idx = t + 256 * p;  // 0..2047
-    const int fl2 = idx >> 6;     // 64 x 4-byte words per feature row
-    const int w = idx & 63;
-    const int ff = f0 + fl2;
-    const long rr = r0 + w * 4;
-    if (ff < n) {
-      unsigned char* dst = out + (long)ff * m + rr;
-      if (rr + 3 < m && ((reinterpret_cast<uintptr_t>(dst) & 3) == 0)) {
-        *reinterpret_cast<unsigned*>(dst) = *reinterpret_cast<const unsigned*>(&tile[fl2][w * 4]);
-      } else {
-        for (int q = 0; q < 4; ++q)
-          if (rr + q < m) dst[q] = tile[fl2][w * 4 + q];
+    for (int p = 0; p < 8; ++p) {
+      const int idx = t + 256 * p;  // 0..2047
+      const int fl2 = idx >> 6;     // 64 x 4-byte words per feature row
+      const int w = idx & 63;
+      const int ff = f0 + fl2;
+      const long rr = r0 + w * 4;
+      if (ff < n) {
+        unsigned char* dst = out + (long)ff * m + rr;
+        if (rr + 3 < m && ((reinterpret_cast<uintptr_t>(dst) & 3) == 0)) {
+          *reinterpret_cast<unsigned*>(dst) = *reinterpret_cast<const unsigned*>(&tile[fl2][w * 4]);
+        } else {
+          for (int q = 0; q < 4; ++q)
+            if (rr + q < m) dst[q] = tile[fl2][w * 4 + q];
+        }
       }
     }
+    __syncthreads();
   }
 }
 
 SRML_API int srml_rf_quantize_u8(const float* X, long m, int n, long ld, const float* edges, int nedges,
                                  unsigned char* out, hipStream_t stream) {
   if (m <= 0 || n <= 0) return 0;
-  dim3 grid(ceil_div(m, 256), ceil_div(n, 32));
-  hipLaunchKernelGGL(rf_quantize_kernel, grid, dim3(256), 0, stream, X, m, n, ld, edges, nedges, out);
+  if (nedges < 0 || nedges > 255) return (int)hipErrorInvalidValue;
+  int ne2 = 1;
+  while (ne2 < nedges + 1) ne2 <<= 1;
+  const size_t lds = (size_t)32 * (ne2 + 1) * sizeof(float);
+  dim3 grid(ceil_div(m, QROWS), ceil_div(n, 32));
+  hipLaunchKernelGGL(rf_quantize_kernel, grid, dim3(256), lds, stream, X, m, n, ld, edges, nedges, ne2, out);
   return srml_status();
 }
 
@@ -95,19 +165,19 @@ template <bool REG>
 __global__ __launch_bounds__(256) void rf_hist_kernel(const unsigned char* __restrict__ bins, long m,
                                                       const int* __restrict__ idx, const float2* __restrict__ wy,
                                                       const int4* __restrict__ items, const int* __restrict__ node_feats,
-                                                      int nf, int B, int S, double yscale, unsigned* __restrict__ hist_u,
-                                                      double* __restrict__ hist_d) {
+                                                      int nf, int B, int S, int fb, double yscale,
+                                                      unsigned* __restrict__ hist_u, double* __restrict__ hist_d) {
   // LDS (classification): u32 counts [feature][class][bin].
   // LDS (regression): u32 weighted counts [feature][bin] then i64 fixed-point sums of w*y
   //   [feature][bin]. Integer LDS atomics: ds_add_f32 issues ~50x slower than ds_add_u32 on
   //   gfx950 (SQ_WAIT_INST_LDS), and the 2^-38·max|y| fixed-point step is finer than fp32.
   extern __shared__ __attribute__((aligned(16))) unsigned lh_u[];
-  unsigned long long* lh_s = reinterpret_cast<unsigned long long*>(lh_u + FB * B);
+  unsigned long long* lh_s = reinterpret_cast<unsigned long long*>(lh_u + fb * B);
   const int4 it = items[blockIdx.x];
   const int node = it.x, rb = it.y, re = it.z, fc = it.w;
-  const int f_begin = fc * FB;
-  const int nfb = min(FB, nf - f_begin);
-  const int words = REG ? FB * B * 3 : FB * B * S;
+  const int f_begin = fc * fb;
+  const int nfb = min(fb, nf - f_begin);
+  const int words = REG ? fb * B * 3 : fb * B * S;
   for (int i = threadIdx.x; i < words; i += 256) lh_u[i] = 0u;
   const unsigned char* col[FB];
 #pragma unroll
@@ -170,22 +240,40 @@ __global__ __launch_bounds__(256) void rf_hist_kernel(const unsigned char* __res
 
 // wy: (weight, label) float pairs aligned with idx
 // regression: S must be 2 (weighted count, weighted sum); yscale = fixed-point scale for w*y
+// features per work item for a (B, S) histogram: the LDS slab (fb * B * S words) must fit 64 KiB
+SRML_API int srml_rf_hist_fb(int B, int S, int regression) {
+  const long per = (long)B * (regression ? 3 : S) * (long)sizeof(unsigned);
+  long fb = (64 * 1024) / (per > 0 ? per : 1);
+  if (fb > FB) fb = FB;
+  return (int)(fb < 1 ? (per <= 160 * 1024 ? 1 : 0) : fb);
+}
+
+// wy: (weight, label) float pairs aligned with idx; items use feature chunks of `fb` features
+// (srml_rf_hist_fb). regression: S must be 2 (weighted count, weighted sum); yscale = fixed-point
+// scale for w*y
 SRML_API int srml_rf_hist(const unsigned char* bins, long m, const int* idx, const float* wy, const int* items,
                           int n_items, const int* node_feats, int nf, int B, int S, int regression, double yscale,
-                          unsigned* hist_u, double* hist_d, hipStream_t stream) {
+                          int fb, unsigned* hist_u, double* hist_d, hipStream_t stream) {
   if (n_items <= 0) return 0;
   if (regression && S != 2) return -6;
-  const size_t lds = (size_t)FB * B * (regression ? 3 : S) * sizeof(unsigned);
-  if (lds > 64 * 1024) return -5;
+  if (fb < 1 || fb > FB) return -7;
+  const size_t lds = (size_t)fb * B * (regression ? 3 : S) * sizeof(unsigned);
+  if (lds > 160 * 1024) return -5;
+  if (lds > 64 * 1024) {
+    (void)hipFuncSetAttribute((const void*)rf_hist_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)rf_hist_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  }
   const float2* w2 = reinterpret_cast<const float2*>(wy);
   if (regression)
     hipLaunchKernelGGL(rf_hist_kernel<true>, dim3(n_items), dim3(256), lds, stream, bins, m, idx, w2,
-                       reinterpret_cast<const int4*>(items), node_feats, nf, B, S, yscale, hist_u, hist_d);
+                       reinterpret_cast<const int4*>(items), node_feats, nf, B, S, fb, yscale, hist_u, hist_d);
   else
     hipLaunchKernelGGL(rf_hist_kernel<false>, dim3(n_items), dim3(256), lds, stream, bins, m, idx, w2,
-                       reinterpret_cast<const int4*>(items), node_feats, nf, B, S, 1.0, hist_u, hist_d);
+                       reinterpret_cast<const int4*>(items), node_feats, nf, B, S, fb, 1.0, hist_u, hist_d);
   return srml_status();
 }
+
+SRML_API int srml_rf_hist_fb_max() { return FB; }
 
 // ------------------------------------------------------------------------------------------
 // split search. crit: 0 gini, 1 entropy, 2 variance.  out per node (double[6]):

@@ -67,7 +67,10 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_potrs_f64": (_P, _I, _L, _P, _P),
     "srml_cd_gram_f64": (_P, _I, _L, _P, _P, _P, _P, _I, _D, _P, _P),
     "srml_rf_quantize_u8": (_P, _L, _I, _L, _P, _I, _P, _P),
-    "srml_rf_hist": (_P, _L, _P, _P, _P, _I, _P, _I, _I, _I, _I, _D, _P, _P, _P),
+    "srml_rf_quantiles_f32": (_P, _I, _I, _I, _P, _P),
+    "srml_rf_hist": (_P, _L, _P, _P, _P, _I, _P, _I, _I, _I, _I, _D, _I, _P, _P, _P),
+    "srml_rf_hist_fb": (_I, _I, _I),
+    "srml_rf_hist_fb_max": (),
     "srml_rf_best_split": (_P, _P, _I, _I, _I, _I, _I, _I, _D, _D, _P, _P, _P),
     "srml_rf_route": (_P, _L, _P, _P, _L, _P, _P, _P, _P, _P),
     "srml_rf_route_segments": (_P, _L, _P, _L, _P, _I, _P, _P, _P, _P, _P),

@@ -196,13 +196,13 @@ def test_kmeans_and_logreg_model_accessors(device):
     np.testing.assert_allclose(np.asarray(g.predictRaw(X[5]).toArray()), raw[5], rtol=1e-5, atol=1e-6)
 
 
-def test_rf_hist_feature_chunk_constant_matches_kernel():
-    """The Python work-item builder and the HIP kernel must agree on features per item."""
-    import os
-    import re
-
+def test_rf_hist_features_per_item_rule():
+    """Features per histogram work item shrink so the LDS slab fits (20+ classes at
+    128 bins used to fail at launch); the library export is cross-checked in test_ops_gpu."""
     from spark_rapids_ml_nai_amd import ops
 
-    src = open(os.path.join(os.path.dirname(ops.__file__), "csrc", "forest.hip")).read()
-    fb = int(re.search(r"constexpr int FB = (\d+);", src).group(1))
-    assert fb == ops.RF_HIST_FB
+    assert ops.rf_hist_fb(128, 3, False) == ops.RF_HIST_FB_MAX
+    assert ops.rf_hist_fb(128, 2, True) == ops.RF_HIST_FB_MAX
+    for B, S in ((128, 20), (256, 12), (256, 32), (128, 32)):
+        fb = ops.rf_hist_fb(B, S, False)
+        assert 1 <= fb < ops.RF_HIST_FB_MAX and fb * B * S * 4 <= 64 * 1024

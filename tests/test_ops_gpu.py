@@ -170,6 +170,28 @@ def test_rf_quantize(gpu_device):
     assert torch.equal(ref, got)
 
 
+@pytest.mark.parametrize("m,n,nedges", [(3000, 37, 127), (1025, 70, 31), (5000, 33, 255), (700, 5, 1)])
+def test_rf_quantize_shapes(gpu_device, m, n, nedges):
+    g = torch.Generator().manual_seed(m + n)
+    X = torch.randn(m, n, generator=g)
+    X[::7, 3 % n] = 0.25  # ties with edges
+    edges = torch.sort(torch.randn(n, nedges, generator=g), 1).values
+    edges[:, nedges // 2] = 0.25
+    ref = ops.rf_quantize(X, edges)
+    got = ops.rf_quantize(X.to(gpu_device), edges.to(gpu_device)).cpu()
+    assert torch.equal(ref, got)
+
+
+@pytest.mark.parametrize("k,n,nq", [(16384, 300, 127), (10000, 64, 31), (32768, 9, 255), (1000, 3, 127), (1, 4, 7)])
+def test_rf_quantiles(gpu_device, k, n, nq):
+    g = torch.Generator().manual_seed(k + n)
+    S = torch.randn(k, n, generator=g)
+    S[::3, 0] = 1.5  # heavy ties
+    ref = ops.rf_quantiles(S, nq)
+    got = ops.rf_quantiles(S.to(gpu_device), nq).cpu()
+    assert torch.equal(ref, got)
+
+
 @pytest.mark.parametrize("regression", [False, True])
 def test_rf_hist_split_route(gpu_device, regression):
     X, edges, y = _rf_setup(gpu_device)
@@ -183,12 +205,13 @@ def test_rf_hist_split_route(gpu_device, regression):
     idx = torch.nonzero(w).view(-1).int()
     # two nodes: first 60% / rest of the in-bag rows
     cut = int(0.6 * idx.shape[0])
-    nf = ops.RF_HIST_FB + 4  # two feature chunks, the second one partial
+    fb = ops.rf_hist_fb(B, S, regression)
+    nf = fb + 4  # two feature chunks, the second one partial
     feats = torch.stack([torch.randperm(40, generator=torch.Generator().manual_seed(s))[:nf] for s in (2, 3)]).int()
     items = []
     for node, (rb, re) in enumerate([(0, cut), (cut, idx.shape[0])]):
         for r0 in range(rb, re, 1000):
-            for fc in range(2):
+            for fc in range((nf + fb - 1) // fb):
                 items.append((node, r0, min(re, r0 + 1000), fc))
     items = torch.tensor(items, dtype=torch.int32)
     ref = ops.rf_hist(bins, idx, y, w, items, feats, 2, B, S, regression)
@@ -516,3 +539,33 @@ def test_nearest_centroid_split_tiled(gpu_device, m, n, k):
     got = D.gather(1, lab.long().view(-1, 1)).view(-1)
     assert (got - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
     torch.testing.assert_close(d2.double(), ref, rtol=1e-5, atol=1e-3)
+
+
+def test_rf_hist_fb_matches_library(gpu_device):
+    """Python's work-item builder and the loaded kernel library agree on features per item."""
+    from spark_rapids_ml_nai_amd.ops import native
+
+    lib = native.lib()
+    assert int(lib.srml_rf_hist_fb_max()) == ops.RF_HIST_FB_MAX
+    for B in (2, 32, 128, 256):
+        for S in (2, 3, 10, 20, 32):
+            for reg in (False, True):
+                if reg and S != 2:
+                    continue
+                assert int(lib.srml_rf_hist_fb(B, S, int(reg))) == ops.rf_hist_fb(B, S, reg), (B, S, reg)
+
+
+@pytest.mark.parametrize("classes,bins", [(20, 128), (12, 256), (32, 256)])
+def test_rf_many_classes(gpu_device, classes, bins):
+    """Histograms wider than the default 8-feature slab: fewer features per item."""
+    from spark_rapids_ml_nai_amd import DataFrame
+    from spark_rapids_ml_nai_amd.classification import RandomForestClassifier
+
+    g = np.random.default_rng(classes)
+    m, n = 4000, 12
+    centers = g.standard_normal((classes, n)) * 3
+    y = g.integers(0, classes, m)
+    X = (centers[y] + g.standard_normal((m, n))).astype(np.float32)
+    model = RandomForestClassifier(numTrees=4, maxDepth=8, maxBins=bins, seed=1).fit(DataFrame.from_numpy(X, y.astype(np.float64)))
+    pred = model.transform(DataFrame.from_numpy(X, y.astype(np.float64))).to_numpy("prediction")
+    assert (pred == y).mean() > 0.8

@@ -157,7 +157,7 @@ def main():
         y = torch.randn(m_, device=dev, generator=g)
         nf = max(1, n_ // 3)
         feats = torch.randperm(n_, device=dev, generator=g)[:nf].int().view(1, -1).contiguous()
-        nfc = (nf + ops.RF_HIST_FB - 1) // ops.RF_HIST_FB
+        nfc = (nf + ops.rf_hist_fb(128, S, reg) - 1) // ops.rf_hist_fb(128, S, reg)
         rows = idx.shape[0]
         rpi = int(min(65536, max(4096, rows * nfc // 8192)))
         rpi = (rpi + 511) // 512 * 512
