@@ -34,6 +34,11 @@ def main() -> None:
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--cols", type=int, default=3000)
     ap.add_argument("--algos", type=str, default="all")
+    ap.add_argument("--global-data", action="store_true",
+                    help="every rank generates the whole dataset from one seed and keeps its row slice "
+                         "(N-invariant data: multi-rank rehearsals compare models against the 1-rank fit)")
+    ap.add_argument("--dump-models", type=str, default=None,
+                    help="rank 0 saves each workload's last fitted model under this directory")
     args = ap.parse_args()
 
     import numpy as np
@@ -43,7 +48,7 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    use_gpu = torch.cuda.is_available()
+    use_gpu = torch.cuda.is_available() and os.environ.get("SRML_FORCE_CPU", "0") != "1"
     device = torch.device("cuda", local_rank % torch.cuda.device_count()) if use_gpu else torch.device("cpu")
     if use_gpu:
         torch.cuda.set_device(device)
@@ -89,7 +94,14 @@ def main() -> None:
             errors[name] = "not implemented"
             continue
         try:
-            Xh, yh = make_shard(wl.data, m_local, args.cols, device, rank, m_total)
+            if args.global_data:
+                Xg, yg = make_shard(wl.data, m_total, args.cols, device, 0, m_total)
+                lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+                Xh = Xg[lo:hi]
+                yh = yg[lo:hi] if yg is not None else None
+                del Xg, yg
+            else:
+                Xh, yh = make_shard(wl.data, m_local, args.cols, device, rank, m_total)
             df = DataFrame.from_numpy(Xh, yh if wl.label else None)
             est = wl.make_estimator()
             est.num_workers = world
@@ -117,6 +129,8 @@ def main() -> None:
                 "phases": {k: round(v, 4) for k, v in getattr(model, "_fit_timings", {}).items()},
                 "evidence": model_evidence(name, model),
             }
+            if args.dump_models and rank == 0:
+                model.write().overwrite().save(os.path.join(args.dump_models, name))
             del df, Xh, yh, model
         except Exception as e:  # noqa: BLE001
             errors[name] = repr(e)[:400]

@@ -1,0 +1,112 @@
+"""Strong-scaling rehearsal of the headline bench on CPU ranks (gloo): ``bench.py`` under
+``torch.distributed.run`` with 1, 2, 4 and 8 ranks on the same global dataset (``--global-data``),
+every workload's N-rank model compared with the 1-rank model under the reference's own gates
+(multi-GPU vs single-GPU: PCA / KMeans <= 1e-3, tests/test_pca.py:344-349, tests/test_kmeans.py:274;
+RF accuracy gap < 0.07 / regressor < 0.09, tests/test_random_forest.py:401,491). This is the
+code path the driver's 8-GPU run takes, minus RCCL itself (same collectives on gloo)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROWS, COLS = 16000, 64
+pytestmark = [pytest.mark.dist, pytest.mark.slow]
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(n: int, out_dir: str) -> dict:
+    env = dict(os.environ, SRML_FORCE_CPU="1", OMP_NUM_THREADS="1", PYTHONPATH=ROOT,
+               SRML_NUM_WORKERS=str(n))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--rows", str(ROWS), "--cols", str(COLS),
+           "--steps", "1", "--warmup", "0", "--global-data", "--dump-models", out_dir]
+    if n == 1:
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py")] + cmd[cmd.index("--gpus"):]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=1500, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-4000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == n and not line["config"]["missing_or_failed"], line["config"]["missing_or_failed"]
+    return line
+
+
+@pytest.fixture(scope="module")
+def runs(tmp_path_factory):
+    out = {}
+    for n in (1, 2, 4, 8):
+        d = str(tmp_path_factory.mktemp(f"n{n}"))
+        out[n] = (_run(n, d), d)
+    return out
+
+
+def _global(name):
+    import torch
+
+    from spark_rapids_ml_nai_amd.bench.suite import make_shard, registry
+
+    wl = registry()[name]
+    return make_shard(wl.data, ROWS, COLS, torch.device("cpu"), 0, ROWS)
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_all_workloads_match_single_rank(runs, n, monkeypatch):
+    monkeypatch.setenv("SRML_FORCE_CPU", "1")
+    from spark_rapids_ml_nai_amd import DataFrame
+    from spark_rapids_ml_nai_amd.classification import LogisticRegressionModel, RandomForestClassificationModel
+    from spark_rapids_ml_nai_amd.clustering import KMeansModel
+    from spark_rapids_ml_nai_amd.feature import PCAModel
+    from spark_rapids_ml_nai_amd.regression import LinearRegressionModel, RandomForestRegressionModel
+
+    line1, d1 = runs[1]
+    linen, dn = runs[n]
+    assert set(linen["config"]["workloads"]) == set(line1["config"]["workloads"])
+    load = lambda cls, d, name: cls.load(os.path.join(d, name))  # noqa: E731
+    # PCA: components (sign-agnostic) and explained variance within 1e-3
+    a, b = load(PCAModel, d1, "pca"), load(PCAModel, dn, "pca")
+    np.testing.assert_allclose(np.abs(a.components_), np.abs(b.components_), atol=1e-3)
+    np.testing.assert_allclose(a.explained_variance_ratio_, b.explained_variance_ratio_, atol=1e-3)
+    # KMeans (same random init rows): centres within 1e-3
+    a, b = load(KMeansModel, d1, "kmeans"), load(KMeansModel, dn, "kmeans")
+    np.testing.assert_allclose(np.asarray(a.cluster_centers_), np.asarray(b.cluster_centers_), atol=1e-3)
+    # LinearRegression OLS / Ridge / ElasticNet: same coefficients
+    for name in ("linear_regression", "linear_regression_ridge", "linear_regression_elasticnet"):
+        a, b = load(LinearRegressionModel, d1, name), load(LinearRegressionModel, dn, name)
+        ca, cb = np.asarray(a.coef_, dtype=np.float64).ravel(), np.asarray(b.coef_, dtype=np.float64).ravel()
+        np.testing.assert_allclose(cb, ca, rtol=1e-4, atol=1e-4 * np.abs(ca).max())
+        assert abs(float(np.ravel(a.intercept_)[0]) - float(np.ravel(b.intercept_)[0])) <= 1e-3 * max(1.0, np.abs(ca).max())
+    # LogisticRegression: same objective, same predictions
+    Xc, yc = _global("logistic_regression")
+    a, b = load(LogisticRegressionModel, d1, "logistic_regression"), load(LogisticRegressionModel, dn, "logistic_regression")
+    assert abs(a.objective - b.objective) <= 1e-6 * abs(a.objective) + 1e-9
+    df = DataFrame.from_numpy(Xc, yc)
+    pa, pb = a.transform(df).to_numpy("prediction"), b.transform(df).to_numpy("prediction")
+    assert (pa == pb).mean() > 0.995
+    # RandomForest: trees split over ranks (reference semantics) -> quality gates
+    a = load(RandomForestClassificationModel, d1, "random_forest_classifier")
+    b = load(RandomForestClassificationModel, dn, "random_forest_classifier")
+    assert b.getNumTrees == a.getNumTrees == 50
+    acc = lambda m: (m.transform(df).to_numpy("prediction") == yc).mean()  # noqa: E731
+    assert abs(acc(a) - acc(b)) < 0.07
+    Xr, yr = _global("random_forest_regressor")
+    dfr = DataFrame.from_numpy(Xr, yr)
+    a = load(RandomForestRegressionModel, d1, "random_forest_regressor")
+    b = load(RandomForestRegressionModel, dn, "random_forest_regressor")
+    r2 = lambda m: 1 - np.mean((m.transform(dfr).to_numpy("prediction") - yr) ** 2) / np.var(yr)  # noqa: E731
+    assert abs(r2(a) - r2(b)) < 0.09
+
+
+def test_json_contract_multi_rank(runs):
+    for n, (line, _) in runs.items():
+        assert line["n_gpus"] == n and line["steps"] == 1 and line["warmup"] == 0
+        assert line["config"]["parallelism"] == f"dp{n}"
+        assert line["value"] > 0 and line["ms_per_step"] > 0
