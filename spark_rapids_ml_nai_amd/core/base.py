@@ -362,7 +362,8 @@ def _fit_worker(ctx: WorkerContext, payload: Tuple[HostPartition, Callable, Dict
     desc = PartitionDescriptor.build(ctx, hp.rows, hp.n_cols)
     inp = FitInput(X=X, y=y, cols=hp.cols, desc=desc, host=hp, stream=streamed)
     _maybe_inject_fault(ctx, "fit")
-    out = fit_fn(inp, ctx, params)
+    with ctx.comm.watchdog(what="fit"):  # SRML_COMM_TIMEOUT: abort the communicator on a stuck collective
+        out = fit_fn(inp, ctx, params)
     if ctx.is_gpu and os.environ.get("SRML_FIT_DEVICE_SYNC", "1") == "1":
         # leave the device idle (copy stream included) before the task returns
         torch.cuda.synchronize(ctx.device)
@@ -385,7 +386,7 @@ def _maybe_inject_fault(ctx: WorkerContext, stage: str) -> None:
     if mode == "hang":
         import time
 
-        time.sleep(3600)
+        time.sleep(float(os.environ.get("SRML_FAULT_HANG_S", "3600")))
     raise RuntimeError("injected fault on rank %d at %s" % (ctx.rank, stage))
 
 

@@ -15,11 +15,25 @@ Every numeric exchange here is a device collective on the compute stream:
 * ``broadcast``, ``barrier``, object collectives for tiny bootstrap metadata only.
 
 A world of size 1 short-circuits every call (no process group needed).
+
+Failure semantics (reference ``common/cuml_context.py:150-167``: ``nccl.destroy()`` on success,
+``nccl.abort()`` on exception): ``abort()`` aborts the process group's communicators
+(``ncclCommAbort`` for RCCL — non-blocking, in-flight collectives on every rank error out) and only
+then destroys the group; ``destroy_process_group`` alone can block forever on a dead peer.
+``watchdog(seconds)`` bounds a block of collectives: if it has not finished in time, a monitor
+thread aborts the communicator, so a rank waiting on the device (RCCL collectives are
+asynchronous; the host blocks in a stream sync) raises instead of hanging. gloo collectives block
+the calling thread inside the transport and cannot be interrupted, so ``comm_timeout()`` also
+becomes the process group's own per-operation timeout (``init_process_group(timeout=...)``);
+either way the stage fails with ``CommTimeout`` well before the barrier-stage timeout.
 """
 from __future__ import annotations
 
+import contextlib
+import os
 import pickle
-from typing import Any, List, Optional, Sequence
+import threading
+from typing import Any, Iterator, List, Optional, Sequence
 
 import torch
 import torch.distributed as dist
@@ -40,6 +54,7 @@ class Communicator:
         self.device = device if device is not None else torch.device("cpu")
         self.group = group
         self._backend = dist.get_backend(group) if (size > 1 and dist.is_initialized()) else "none"
+        self.aborted = False
 
     # -- helpers --------------------------------------------------------------------
     @property
@@ -145,12 +160,70 @@ class Communicator:
         return [bytes(p.cpu().numpy().tobytes()) for p in parts]
 
     def abort(self) -> None:
-        """Tear the group down after a failure so peers fail fast (cf. ``nccl.abort()``)."""
-        if self.size > 1 and dist.is_initialized():
+        """Abort the communicators (``ncclCommAbort`` / gloo abort: pending collectives fail on
+        every rank instead of waiting for a dead peer), then destroy the group."""
+        if self.size <= 1 or not dist.is_initialized():
+            return
+        self.aborted = True
+        try:
+            from torch.distributed import distributed_c10d as c10d
+
+            c10d._abort_process_group(self.group if self.group is not None else c10d.GroupMember.WORLD)
+        except Exception:  # noqa: BLE001 - fall back to the backend object's own abort
             try:
-                dist.destroy_process_group()
+                pg = self.group if self.group is not None else dist.group.WORLD
+                dev = self.device if self.device.type == "cuda" else torch.device("cpu")
+                pg._get_backend(dev).abort()
             except Exception:  # noqa: BLE001
                 pass
+        try:
+            dist.destroy_process_group()
+        except Exception:  # noqa: BLE001
+            pass
+
+    @contextlib.contextmanager
+    def watchdog(self, seconds: Optional[float] = None, what: str = "collective") -> Iterator[None]:
+        """Abort the communicator if the enclosed block runs longer than ``seconds``
+        (default ``SRML_COMM_TIMEOUT``, 0/unset = off); the block then raises ``CommTimeout``."""
+        if seconds is None:
+            seconds = float(os.environ.get("SRML_COMM_TIMEOUT", "0") or 0)
+        if self.size <= 1 or not seconds or seconds <= 0:
+            yield
+            return
+        done = threading.Event()
+        fired = threading.Event()
+
+        def _monitor() -> None:
+            if not done.wait(seconds):
+                fired.set()
+                self.abort()
+
+        t = threading.Thread(target=_monitor, name="srml-comm-watchdog", daemon=True)
+        t.start()
+        try:
+            yield
+        except Exception as e:  # noqa: BLE001
+            msg = str(e).lower()
+            if fired.is_set() or "timed out" in msg or "timeout" in msg:
+                done.set()
+                self.abort()
+                raise CommTimeout(f"{what} on rank {self.rank} exceeded {seconds:.0f}s; communicator aborted") from e
+            raise
+        finally:
+            done.set()
+        if fired.is_set():
+            raise CommTimeout(f"{what} on rank {self.rank} exceeded {seconds:.0f}s; communicator aborted")
+
+
+def comm_timeout(default_s: float) -> float:
+    """Per-operation timeout for new process groups: ``SRML_COMM_TIMEOUT`` if set, else the default
+    (the barrier-stage timeout)."""
+    v = float(os.environ.get("SRML_COMM_TIMEOUT", "0") or 0)
+    return v if v > 0 else float(default_s)
+
+
+class CommTimeout(RuntimeError):
+    """A watched block of collectives overran its deadline and the communicator was aborted."""
 
 
 def pickle_obj(o: Any) -> bytes:

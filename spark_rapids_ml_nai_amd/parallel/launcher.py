@@ -39,6 +39,7 @@ def _child(rank: int, world: int, port: int, use_gpu: bool, payload: bytes, q: A
     import torch
     import torch.distributed as dist
 
+    from .comm import comm_timeout
     from .context import WorkerContext, local_device, use_context
 
     ctx = None
@@ -53,7 +54,7 @@ def _child(rank: int, world: int, port: int, use_gpu: bool, payload: bytes, q: A
             "nccl" if device.type == "cuda" else "gloo",
             rank=rank,
             world_size=world,
-            timeout=timedelta(seconds=timeout_s),
+            timeout=timedelta(seconds=comm_timeout(timeout_s)),
             **({"device_id": device} if device.type == "cuda" else {}),
         )
         ctx = WorkerContext.from_process_group(device)

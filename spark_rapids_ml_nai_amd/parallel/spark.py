@@ -150,8 +150,10 @@ def init_barrier_group(task_ctx: Any, use_gpu: bool, timeout_s: float = 1800.0) 
         bind_numa_local(device)
     store = dist.TCPStore(master_host, int(master_port), world, is_master=(rank == 0),
                           timeout=timedelta(seconds=timeout_s))
+    from .comm import comm_timeout
+
     dist.init_process_group("nccl" if device.type == "cuda" else "gloo", store=store, rank=rank, world_size=world,
-                            timeout=timedelta(seconds=timeout_s),
+                            timeout=timedelta(seconds=comm_timeout(timeout_s)),
                             **({"device_id": device} if device.type == "cuda" else {}))
     return WorkerContext.from_process_group(device)
 

@@ -61,3 +61,20 @@ def test_runner(tmp_path, algo, kind, extra):
         assert rows[0]["inertia"] > 0
     if algo == "approximate_nearest_neighbors":
         assert rows[0]["avg_recall"] >= 0.95
+
+
+def test_comm_sweep_single_rank():
+    """tools/comm_sweep.py runs on one rank (the same code path the 8-GPU node runs under torchrun)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, SRML_FORCE_CPU="1", MASTER_ADDR="127.0.0.1", MASTER_PORT="29577")
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "comm_sweep.py"), "--max-bytes", "16K",
+                        "--iters", "2", "--warmup", "1", "--ops", "all_reduce,all_gather"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rows = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert {x["op"] for x in rows} == {"all_reduce", "all_gather"} and all(x["us"] > 0 for x in rows)

@@ -125,3 +125,24 @@ def test_hung_rank_hits_stage_timeout(monkeypatch):
     monkeypatch.setenv("SRML_BARRIER_TIMEOUT", "15")
     with pytest.raises(RuntimeError, match="timed out"):
         LinearRegression(num_workers=2).fit(df)
+
+
+def test_comm_watchdog_aborts_stuck_collective(monkeypatch):
+    """A rank stuck before its collectives: its peer's watchdog aborts the communicator (reference
+    nccl.abort(), common/cuml_context.py:155-159) and the stage fails fast with CommTimeout,
+    long before the barrier-stage timeout."""
+    import time
+
+    from spark_rapids_ml_nai_amd.regression import LinearRegression
+
+    X = _data(seed=8)
+    df = DataFrame.from_numpy(X, X[:, 2].astype(np.float64), num_partitions=2)
+    monkeypatch.setenv("SRML_FAULT_RANK", "1")
+    monkeypatch.setenv("SRML_FAULT_MODE", "hang")
+    monkeypatch.setenv("SRML_FAULT_HANG_S", "90")
+    monkeypatch.setenv("SRML_COMM_TIMEOUT", "5")
+    monkeypatch.setenv("SRML_BARRIER_TIMEOUT", "300")
+    t0 = time.time()
+    with pytest.raises(RuntimeError, match="exceeded 5s; communicator aborted"):
+        LinearRegression(num_workers=2).fit(df)
+    assert time.time() - t0 < 80
