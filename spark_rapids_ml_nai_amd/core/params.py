@@ -509,6 +509,58 @@ class HasEnableSparseDataOptim(Params):
 # --------------------------------------------------------------------------------------
 # Spark <-> backend parameter mapping
 # --------------------------------------------------------------------------------------
+class ParamBridge:
+    """Translation table between one class's Spark ML Params and its device-solver kwargs.
+
+    Built from the class hooks ``_param_mapping()`` (Spark name -> backend name, ``""`` = accepted
+    but unused, ``None`` = unsupported) and ``_param_value_mapping()`` (backend name -> value
+    translator returning ``None`` for unsupported values). Every estimator / model routes its
+    parameter traffic (constructor kwargs, setters, ``copy(extra)``, ``clear``, ``fitMultiple``
+    param maps) through ``lookup`` + ``to_backend`` so the semantics live in one place
+    (reference behaviour: ``python/src/spark_rapids_ml/params.py:268-531``).
+    """
+
+    UNSUPPORTED = None
+    IGNORED = ""
+
+    def __init__(self, names: Dict[str, Optional[str]], values: Dict[str, Callable[[Any], Any]]) -> None:
+        self.names = dict(names)
+        self.values = dict(values)
+
+    def lookup(self, spark_name: str, strict: bool) -> Optional[str]:
+        """Backend kwarg for a Spark Param; ``strict`` raises on unsupported params and warns on
+        ignored ones (silent lookups just return None for both)."""
+        if spark_name not in self.names:
+            return None
+        target = self.names[spark_name]
+        if target is self.UNSUPPORTED:
+            if strict:
+                raise ValueError(f"Spark Param '{spark_name}' is not supported on the device backend.")
+            return None
+        if target == self.IGNORED:
+            if strict:
+                warnings.warn(f"Spark Param '{spark_name}' is not used by the device backend.")
+            return None
+        return target
+
+    def to_backend(self, backend_name: str, value: Any) -> Any:
+        conv = self.values.get(backend_name)
+        if conv is None:
+            return value
+        out = conv(value)
+        if out is None:
+            raise ValueError(f"Value '{value}' for '{backend_name}' param is unsupported")
+        return out
+
+    def spark_names_for(self, backend_name: str) -> List[str]:
+        return [k for k, v in self.names.items() if v == backend_name]
+
+    def conflicting(self, kwargs: Dict[str, Any]) -> List[Tuple[str, str]]:
+        """(spark, backend) name pairs that were BOTH given (they alias one value)."""
+        return [(sp, be) for sp, be in self.names.items()
+                if be and sp != be and sp in kwargs and be in kwargs]
+
+
 class _BackendClass:
     """Helper hooks for mapping Spark ML Params to device-solver kwargs."""
 
@@ -522,16 +574,42 @@ class _BackendClass:
         """backend kwarg name -> function mapping a Spark value to a backend value (None = unsupported)."""
         return {}
 
+    @classmethod
+    def _bridge(cls) -> ParamBridge:
+        return ParamBridge(cls._param_mapping(), cls._param_value_mapping())
+
     def _get_backend_params_default(self) -> Dict[str, Any]:
         raise NotImplementedError()
 
 
+def _route_columns(single: str, multi: str) -> Callable[[Any, Any], None]:
+    """``inputCol`` / ``featuresCol`` accept one name or a list (which lands in the plural Param)."""
+
+    def route(obj: Any, value: Any) -> None:
+        if isinstance(value, (list, tuple)):
+            obj._set(**{multi: list(value)})
+        elif isinstance(value, str):
+            obj._set(**{single: value})
+
+    return route
+
+
 class _BackendParams(_BackendClass, Params):
-    """Common param handling for every estimator and model (reference ``params.py:215-554``)."""
+    """Common param handling for every estimator and model (reference ``params.py:215-554``):
+    Spark Params on the Params side, device kwargs in ``backend_params`` (``cuml_params`` alias),
+    kept consistent by ``ParamBridge``."""
 
     _backend_params: Dict[str, Any] = {}
     _num_workers: Optional[int] = None
     _float32_inputs: bool = True
+
+    # kwargs that are neither Spark Params nor backend kwargs
+    _FRAMEWORK_KWARGS: Dict[str, Callable[[Any, Any], None]] = {
+        "inputCol": _route_columns("inputCol", "inputCols"),
+        "featuresCol": _route_columns("featuresCol", "featuresCols"),
+        "num_workers": lambda obj, v: setattr(obj, "_num_workers", v),
+        "float32_inputs": lambda obj, v: setattr(obj, "_float32_inputs", v),
+    }
 
     # --- backend kwargs ------------------------------------------------------------
     @property
@@ -548,137 +626,115 @@ class _BackendParams(_BackendClass, Params):
         """Number of device workers (one rank per GPU)."""
         from ..parallel.context import infer_num_workers
 
-        inferred = infer_num_workers()
-        if self._num_workers is not None:
-            if self._num_workers < 1:
-                raise ValueError("num_workers must be >= 1")
-            return self._num_workers
-        return inferred
+        if self._num_workers is None:
+            return infer_num_workers()
+        if self._num_workers < 1:
+            raise ValueError("num_workers must be >= 1")
+        return self._num_workers
 
     @num_workers.setter
     def num_workers(self, value: int) -> None:
         self._num_workers = value
 
-    def copy(self: "BP", extra: Optional[Dict[Param, Any]] = None) -> "BP":
-        instance: BP = super().copy(extra)  # type: ignore[assignment]
-        backend_params = instance._backend_params.copy()
-        if isinstance(extra, dict):
-            for param, value in extra.items():
-                if isinstance(param, Param):
-                    name = instance._get_backend_param(param.name, silent=False)
-                    if name is not None:
-                        backend_params[name] = instance._get_backend_mapping_value(name, value)
-                else:
-                    raise TypeError("Expecting a valid instance of Param, but received: {}".format(param))
-        instance._backend_params = backend_params
-        return instance
-
     def _initialize_backend_params(self) -> None:
+        """Backend defaults, then every mapped Spark Param's default pushed through the bridge."""
         self._backend_params = self._get_backend_params_default()
-        for spark_param in self._param_mapping().keys():
-            if self.hasParam(spark_param) and self.hasDefault(spark_param):
-                self._set_backend_param(spark_param, self.getOrDefault(spark_param))
+        for name in self._bridge().names:
+            if self.hasParam(name) and self.hasDefault(name):
+                self._set_backend_param(name, self.getOrDefault(name))
 
-    # reference-compatible name
-    _initialize_cuml_params = _initialize_backend_params
+    _initialize_cuml_params = _initialize_backend_params  # reference-compatible name
+
+    def _mirror_spark(self, name: str, value: Any) -> None:
+        """Spark Param set by name: record it and translate it into the backend kwarg."""
+        self._set(**{name: value})
+        self._set_backend_param(name, value, silent=False)
+
+    def _mirror_backend(self, name: str, value: Any) -> None:
+        """Backend kwarg set by name: store it and reflect it in the Spark Params that alias it
+        (best effort: a backend value the Spark Param's type converter rejects stays backend-only)."""
+        self._backend_params[name] = value
+        for spark_name in self._bridge().spark_names_for(name):
+            if not self.hasParam(spark_name):
+                continue
+            try:
+                self._set(**{spark_name: value})
+            except TypeError:
+                continue
 
     def _set_params(self: "BP", **kwargs: Any) -> "BP":
-        param_map = self._param_mapping()
-        for spark_param, be_param in param_map.items():
-            if spark_param != be_param and spark_param in kwargs and be_param in kwargs:
-                raise ValueError(f"'{be_param}' is an alias of '{spark_param}', set one or the other.")
-
-        for k, v in kwargs.items():
-            if k == "inputCol":
-                if isinstance(v, str):
-                    self._set(**{"inputCol": v})
-                elif isinstance(v, (list, tuple)):
-                    self._set(**{"inputCols": list(v)})
-            elif k == "featuresCol":
-                if isinstance(v, str):
-                    self._set(**{"featuresCol": v})
-                elif isinstance(v, (list, tuple)):
-                    self._set(**{"featuresCols": list(v)})
-            elif self.hasParam(k):
-                self._set(**{str(k): v})
-                self._set_backend_param(k, v, silent=False)
-            elif k in self._backend_params:
-                self._backend_params[k] = v
-                for spark_param, be_param in param_map.items():
-                    if k == be_param and self.hasParam(spark_param):
-                        try:
-                            self._set(**{str(spark_param): v})
-                        except TypeError:
-                            pass
-            elif k == "num_workers":
-                self._num_workers = v
-            elif k == "float32_inputs":
-                self._float32_inputs = v
+        clash = self._bridge().conflicting(kwargs)
+        if clash:
+            sp, be = clash[0]
+            raise ValueError(f"'{be}' is an alias of '{sp}', set one or the other.")
+        for key, value in kwargs.items():
+            special = self._FRAMEWORK_KWARGS.get(key)
+            if special is not None:
+                special(self, value)
+            elif self.hasParam(key):
+                self._mirror_spark(key, value)
+            elif key in self._backend_params:
+                self._mirror_backend(key, value)
             else:
-                raise ValueError(f"Unsupported param '{k}'.")
+                raise ValueError(f"Unsupported param '{key}'.")
         return self
 
+    def copy(self: "BP", extra: Optional[Dict[Param, Any]] = None) -> "BP":
+        """Params copy (Spark semantics) with ``extra`` also translated into the backend kwargs."""
+        clone: BP = super().copy(extra)  # type: ignore[assignment]
+        backend = dict(clone._backend_params)
+        bridge = self._bridge()
+        for param, value in (extra or {}).items():
+            if not isinstance(param, Param):
+                raise TypeError("Expecting a valid instance of Param, but received: {}".format(param))
+            target = bridge.lookup(param.name, strict=True)
+            if target is not None:
+                backend[target] = bridge.to_backend(target, value)
+        clone._backend_params = backend
+        return clone
+
     def clear(self, param: Param) -> None:
+        """Unset a Spark Param and restore its backend kwarg from the Param's default."""
         super().clear(param)
-        be = self._param_mapping().get(param.name)
-        if be:
-            self._backend_params[be] = self._get_backend_mapping_value(be, self.getOrDefault(param.name))
+        target = self._bridge().names.get(param.name)
+        if target:
+            self._backend_params[target] = self._get_backend_mapping_value(target, self.getOrDefault(param.name))
 
     def _copy_backend_params(self, to: "BP") -> "BP":
-        for k, v in self._backend_params.items():
-            if k in to._backend_params:
-                to._backend_params[k] = v
+        to._backend_params.update({k: v for k, v in self._backend_params.items() if k in to._backend_params})
         return to
 
     _copy_cuml_params = _copy_backend_params
 
     def _get_input_columns(self) -> Tuple[Optional[str], Optional[List[str]]]:
-        if self.hasParam("inputCols") and self.isDefined("inputCols"):
-            return None, self.getOrDefault("inputCols")
-        if self.hasParam("inputCol") and self.isDefined("inputCol"):
-            return self.getOrDefault("inputCol"), None
-        if self.hasParam("featuresCols") and self.isDefined("featuresCols"):
-            return None, self.getOrDefault("featuresCols")
-        if self.hasParam("featuresCol") and self.isDefined("featuresCol"):
-            return self.getOrDefault("featuresCol"), None
+        """(single column, None) or (None, column list), plural Params first."""
+        for plural, single in (("inputCols", "inputCol"), ("featuresCols", "featuresCol")):
+            if self.hasParam(plural) and self.isDefined(plural):
+                return None, self.getOrDefault(plural)
+            if self.hasParam(single) and self.isDefined(single):
+                return self.getOrDefault(single), None
         raise ValueError("Please set inputCol(s) or featuresCol(s)")
 
     def _get_backend_param(self, spark_param: str, silent: bool = True) -> Optional[str]:
-        param_map = self._param_mapping()
-        if spark_param not in param_map:
-            return None
-        be = param_map[spark_param]
-        if be is None:
-            if not silent:
-                raise ValueError(f"Spark Param '{spark_param}' is not supported on the device backend.")
-            return None
-        if be == "":
-            if not silent:
-                warnings.warn(f"Spark Param '{spark_param}' is not used by the device backend.")
-            return None
-        return be
+        return self._bridge().lookup(spark_param, strict=not silent)
 
     _get_cuml_param = _get_backend_param
 
     def _set_backend_param(self, spark_param: str, spark_value: Any, silent: bool = True) -> None:
-        be = self._get_backend_param(spark_param, silent)
-        if be is not None:
-            try:
-                self._backend_params[be] = self._get_backend_mapping_value(be, spark_value)
-            except ValueError:
-                ref = be + " or " + spark_param if be != spark_param else spark_param
-                raise ValueError(f"{ref} given invalid value {spark_value}")
+        bridge = self._bridge()
+        target = bridge.lookup(spark_param, strict=not silent)
+        if target is None:
+            return
+        try:
+            self._backend_params[target] = bridge.to_backend(target, spark_value)
+        except ValueError:
+            names = spark_param if target == spark_param else f"{target} or {spark_param}"
+            raise ValueError(f"{names} given invalid value {spark_value}")
 
     _set_cuml_param = _set_backend_param
 
     def _get_backend_mapping_value(self, k: str, v: Any) -> Any:
-        vm = self._param_value_mapping()
-        if k not in vm:
-            return v
-        mapped = vm[k](v)
-        if mapped is None:
-            raise ValueError(f"Value '{v}' for '{k}' param is unsupported")
-        return mapped
+        return self._bridge().to_backend(k, v)
 
     _get_cuml_mapping_value = _get_backend_mapping_value
 
