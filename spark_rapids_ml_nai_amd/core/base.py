@@ -49,7 +49,17 @@ from .dataframe import (
     vector_column_to_dense,
     array_column_to_dense,
 )
-from .params import Param, _BackendParams
+from .params import PYSPARK_PARAMS, Param, _BackendParams
+
+if PYSPARK_PARAMS:  # estimators / models are genuine pyspark.ml stages (Pipeline, tuning, ...)
+    from pyspark.ml import Estimator as _SparkEstimator  # type: ignore
+    from pyspark.ml import Model as _SparkModel  # type: ignore
+
+    _ESTIMATOR_BASES: Tuple[type, ...] = (_SparkEstimator,)
+    _MODEL_BASES: Tuple[type, ...] = (_SparkModel,)
+else:
+    _ESTIMATOR_BASES = ()
+    _MODEL_BASES = ()
 from .persistence import (
     EstimatorReader,
     EstimatorWriter,
@@ -178,7 +188,7 @@ def _split_rows(n: int, parts: int) -> List[Tuple[int, int]]:
     return [(int(b[i]), int(b[i + 1])) for i in range(parts)]
 
 
-class _Estimator(_CommonBase):
+class _Estimator(_CommonBase, *_ESTIMATOR_BASES):  # type: ignore[misc]
     """Base of every estimator (reference ``_CumlEstimator`` + ``_CumlCaller``)."""
 
     def __init__(self) -> None:
@@ -487,7 +497,7 @@ class _ThreadSafeIter:
 TransformFn = Callable[[Any, Any, WorkerContext], Dict[str, np.ndarray]]
 
 
-class _Model(_CommonBase):
+class _Model(_CommonBase, *_MODEL_BASES):  # type: ignore[misc]
     """Base of every fitted model (reference ``_CumlModel``)."""
 
     def __init__(self, **model_attributes: Any) -> None:

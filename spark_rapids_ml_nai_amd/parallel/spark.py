@@ -10,8 +10,11 @@ and yields the model attributes from rank 0. Here the same stage runs our worker
   or gloo for CPU tasks. Only this tiny bootstrap blob goes through the driver — every numeric
   exchange (partition sizes, moments, forests, kNN partials) is a device collective;
 * device: the task's ``gpu`` resource address (cluster) or ``partitionId % device_count`` (local);
-* the pandas batches of the partition become one Arrow table -> ``HostPartition`` -> device
-  (pinned staging) exactly like the Spark-free paths, so the same ``_fit_worker`` runs;
+* ingest is Arrow end to end (``mapInArrow``): the partition's ``RecordBatch``es are wrapped into
+  one table without copying, ``array<float>`` / VectorUDT values buffers are viewed as 2-D numpy
+  arrays (no per-row Python objects, the reference's ``np.array(list(pdf[...]))`` at core.py:733),
+  then -> ``HostPartition`` -> device (pinned staging) exactly like the Spark-free paths, so the same
+  ``_fit_worker`` runs; transform builds its output columns as Arrow arrays the same way;
 * failure: an exception aborts the communicator (``ncclCommAbort``), the barrier stage fails and
   Spark retries it as a whole (reference semantics);
 * stage-level scheduling (``core.py:901-1004``): training tasks ask for a whole GPU and more than
@@ -159,21 +162,35 @@ def init_barrier_group(task_ctx: Any, use_gpu: bool, timeout_s: float = 1800.0) 
 
 
 def batches_to_table(batches: Iterable[Any], vector_cols: List[str]) -> Any:
-    """pandas batches of one partition -> one Arrow table (vector structs tagged as VectorUDT)."""
+    """Arrow ``RecordBatch``es (``mapInArrow``) — or pandas frames from older callers — of one
+    partition -> ONE Arrow table without copying the column buffers (vector structs tagged as
+    VectorUDT so the ingest reads their values buffers directly)."""
     import pyarrow as pa
 
     from ..core.dataframe import vector_field
 
-    tables = [pa.Table.from_pandas(b, preserve_index=False) for b in batches]
-    tables = [t for t in tables if t.num_rows > 0] or tables[:1]
+    rbs, tables = [], []
+    for b in batches:
+        if isinstance(b, pa.RecordBatch):
+            rbs.append(b)
+        elif isinstance(b, pa.Table):
+            tables.append(b)
+        else:  # pandas.DataFrame
+            tables.append(pa.Table.from_pandas(b, preserve_index=False))
+    if rbs:
+        nonempty = [b for b in rbs if b.num_rows > 0] or rbs[:1]
+        tables.append(pa.Table.from_batches(nonempty))
+    if not tables:
+        raise RuntimeError("A worker received no data. Please increase amount of data or use fewer workers.")
     t = pa.concat_tables(tables) if len(tables) > 1 else tables[0]
     fields = [vector_field(f.name) if f.name in vector_cols else f for f in t.schema]
     return pa.Table.from_arrays(t.columns, schema=pa.schema(fields))
 
 
 def spark_worker_entry(task_ctx: Any, batches: Iterable[Any], payload: bytes) -> Iterator[Any]:
-    """Body of one barrier fit task (reference ``_train_udf``, core.py:694-779)."""
-    import pandas as pd
+    """Body of one barrier fit task (reference ``_train_udf``, core.py:694-779): Arrow batches in,
+    one ``RecordBatch`` with the pickled model attributes out (rank 0)."""
+    import pyarrow as pa
 
     from ..core.base import _fit_worker
     from ..core.dataframe import DataFrame
@@ -196,7 +213,7 @@ def spark_worker_entry(task_ctx: Any, batches: Iterable[Any], payload: bytes) ->
 
     dist.destroy_process_group()
     if task_ctx.partitionId() == 0:
-        yield pd.DataFrame({"result": [cloudpickle.dumps(res)]})
+        yield pa.RecordBatch.from_pydict({"result": pa.array([cloudpickle.dumps(res)], type=pa.binary())})
 
 
 # ------------------------------------------------------------------------------------------
@@ -237,7 +254,7 @@ def run_spark_fit(est: Any, sdf: Any, fit_fn: Callable, params: Dict[str, Any]) 
 
         return spark_worker_entry(BarrierTaskContext.get(), it, payload)
 
-    rdd = sdf.mapInPandas(_train, schema="result binary").rdd.barrier().mapPartitions(lambda x: x)
+    rdd = sdf.mapInArrow(_train, schema="result binary").rdd.barrier().mapPartitions(lambda x: x)
     rdd = _try_stage_level_scheduling(rdd, spark)
     rows = rdd.collect()
     return cloudpickle.loads(rows[0]["result"])
@@ -249,12 +266,13 @@ def _cluster_has_gpus(spark: Any) -> bool:
 
 def spark_transform(model: Any, sdf: Any) -> Any:
     """Per-batch transform with the model's device predict function (reference ``_transform``,
-    core.py:1419-1435 / 1537-1557): one model construction per task, pinned device per task."""
+    core.py:1419-1435 / 1537-1557): one model construction per task, pinned device per task,
+    Arrow in / Arrow out (``mapInArrow``): outputs are appended as Arrow columns (2-D results as
+    ``list<double>`` over the flat values buffer), never as per-row Python lists."""
     import numpy as np
-    import pandas as pd
     import pyarrow as pa
 
-    from ..core.dataframe import DataFrame
+    from ..core.dataframe import DataFrame, dense_to_list_array
 
     sdf_u, vec = _unwrap_vectors(sdf)
     blob = cloudpickle.dumps((model, vec))
@@ -273,21 +291,21 @@ def spark_transform(model: Any, sdf: Any) -> Any:
         ctx = WorkerContext.single(dev)
         construct, predict = m._get_transform_func(None)
         state = construct(ctx)
-        for pdf in it:
-            if len(pdf) == 0:
+        for rb in it:
+            if rb.num_rows == 0:
                 continue
-            table = batches_to_table([pdf], vcols)
-            part = DataFrame([table])
-            X = m._transform_features(part)
+            table = batches_to_table([rb], vcols)
+            X = m._transform_features(DataFrame([table]))
             res = predict(state, X, ctx)
-            out = pdf.copy()
+            cols, names = list(rb.columns), list(rb.schema.names)
             for k, v in res.items():
                 v = np.asarray(v)
-                out[k] = list(v) if v.ndim == 2 else v
-            yield out
+                cols.append(dense_to_list_array(v.astype(np.float64)) if v.ndim == 2 else pa.array(v.astype(np.float64)))
+                names.append(k)
+            yield pa.RecordBatch.from_arrays(cols, names=names)
 
     schema = sdf_u.schema
     from pyspark.sql.types import StructType  # type: ignore
 
     out_schema = StructType(list(schema.fields) + out_fields)
-    return sdf_u.mapInPandas(_predict, schema=out_schema)
+    return sdf_u.mapInArrow(_predict, schema=out_schema)
