@@ -38,8 +38,12 @@ from ..parallel.context import (
 )
 from ..utils.log import get_logger
 from ..utils.timer import PhaseTimer
+import pyarrow as pa
+
 from .dataframe import (
+    ChunkedRows,
     DataFrame,
+    array_column_chunks,
     as_dataframe,
     is_array_field,
     is_vector_field,
@@ -154,7 +158,10 @@ def to_device(X: Any, device: torch.device, dtype: Optional[torch.dtype] = None)
     return host_to_device(X, device, dtype)
 
 
-def _dense_from_df(df: DataFrame, col: Optional[str], cols: Optional[List[str]], np_dtype: Any) -> Any:
+def _dense_from_df(df: DataFrame, col: Optional[str], cols: Optional[List[str]], np_dtype: Any,
+                   chunked: bool = False) -> Any:
+    """Features of a partition as a host matrix. ``chunked`` (fit ingest): a multi-batch array
+    column stays a list of per-batch zero-copy views (``ChunkedRows``) for the streaming H2D."""
     if cols:
         mats = [df.to_numpy(c).reshape(-1, 1) for c in cols]
         return np.ascontiguousarray(np.hstack(mats).astype(np_dtype))
@@ -162,7 +169,10 @@ def _dense_from_df(df: DataFrame, col: Optional[str], cols: Optional[List[str]],
     if is_vector_field(f):
         return vector_column_to_dense(df.column(col), np_dtype)
     if is_array_field(f):
-        return array_column_to_dense(df.column(col), np_dtype)
+        c = df.column(col)
+        if chunked and isinstance(c, pa.ChunkedArray) and c.num_chunks > 1:
+            return array_column_chunks(c, np_dtype)
+        return array_column_to_dense(c, np_dtype)
     return df.to_numpy(col).astype(np_dtype).reshape(-1, 1)
 
 
@@ -251,7 +261,7 @@ class _Estimator(_CommonBase, *_ESTIMATOR_BASES):  # type: ignore[misc]
         if self._use_sparse(df, col):
             X = vector_column_to_csr(df.column(col), np_dtype)
         else:
-            X = _dense_from_df(df, col, cols, np_dtype)
+            X = _dense_from_df(df, col, cols, np_dtype, chunked=True)
         y = None
         if self._fit_uses_label():
             lc = self.getOrDefault("labelCol")
@@ -358,13 +368,17 @@ def _fit_worker(ctx: WorkerContext, payload: Tuple[HostPartition, Callable, Dict
         raise RuntimeError("A worker received no data. Please increase amount of data or use fewer workers.")
     dtype = torch.float32 if float32 else torch.float64
     streamed = None
-    from ..ops.ingest import StreamedRows, is_pinned, uvm_enabled
+    from ..ops.ingest import StreamedParts, StreamedRows, is_pinned, uvm_enabled
 
-    if (ctx.is_gpu and isinstance(hp.X, np.ndarray) and hp.X.ndim == 2 and hp.X.shape[0] > 0
+    stream_ok = (ctx.is_gpu and getattr(fit_fn, "streaming_ingest", False) and not uvm_enabled()
+                 and os.environ.get("SRML_STREAM_INGEST", "1") == "1")
+    if (stream_ok and isinstance(hp.X, np.ndarray) and hp.X.ndim == 2 and hp.X.shape[0] > 0
             and hp.X.dtype == (np.float32 if float32 else np.float64) and hp.X.flags.c_contiguous
-            and getattr(fit_fn, "streaming_ingest", False) and os.environ.get("SRML_STREAM_INGEST", "1") == "1"
-            and not uvm_enabled() and is_pinned(hp.X)):
+            and is_pinned(hp.X)):
         streamed = StreamedRows(hp.X, ctx.device, dtype)
+        X = streamed.X
+    elif stream_ok and isinstance(hp.X, ChunkedRows) and hp.X.shape[0] > 0:
+        streamed = StreamedParts(hp.X, ctx.device, dtype)  # Spark batches: fill/DMA/compute pipelined
         X = streamed.X
     else:
         X = to_device(hp.X, ctx.device, dtype) if hp.X is not None else None

@@ -179,6 +179,39 @@ def array_column_to_dense(col: Union[pa.ChunkedArray, pa.Array], dtype: Optional
     return X
 
 
+class ChunkedRows:
+    """Row blocks of one host partition, each a zero-copy (rows_i, n) view of one Arrow batch's
+    values buffer (Spark delivers ``maxRecordsPerBatch``-row batches in separate buffers).
+    ``ops.ingest.parts_to_device`` streams them to the device without first concatenating the
+    partition on the host (a full extra copy of the data)."""
+
+    ndim = 2
+
+    def __init__(self, parts: List[np.ndarray]) -> None:
+        self.parts = [p for p in parts if p.shape[0] > 0] or parts[:1]
+        n = int(self.parts[0].shape[1]) if self.parts else 0
+        if any(int(p.shape[1]) != n for p in self.parts):
+            raise ValueError("array column has rows of different lengths")
+        self.shape = (int(sum(p.shape[0] for p in self.parts)), n)
+        self.dtype = self.parts[0].dtype if self.parts else np.dtype(np.float32)
+
+    def __len__(self) -> int:
+        return self.shape[0]
+
+    def to_numpy(self) -> np.ndarray:
+        return np.concatenate(self.parts, 0) if len(self.parts) > 1 else self.parts[0]
+
+
+def array_column_chunks(col: Union[pa.ChunkedArray, pa.Array], dtype: Optional[np.dtype] = None) -> ChunkedRows:
+    """list<float> column -> ``ChunkedRows``: one zero-copy 2-D view per Arrow chunk (a per-chunk
+    cast only when the element type differs from ``dtype``)."""
+    chunks = col.chunks if isinstance(col, pa.ChunkedArray) else [col]
+    parts = [array_column_to_dense(c, dtype) for c in chunks if len(c) > 0]
+    if not parts:
+        parts = [np.zeros((0, 0), dtype=dtype or np.float32)]
+    return ChunkedRows(parts)
+
+
 def vector_column_is_sparse(col: Union[pa.ChunkedArray, pa.Array]) -> bool:
     arr = _combine(col)
     if len(arr) == 0:

@@ -77,10 +77,172 @@ def _dense_to_device(a: np.ndarray, device: torch.device, dtype: Optional[torch.
     return out
 
 
+# ------------------------------------------------------------------------------------------
+# Batch-stream ingest: many pageable row blocks (Spark Arrow batches) -> one device matrix
+# ------------------------------------------------------------------------------------------
+_RING_SLOTS = 3
+_ring: dict = {}  # device index -> [(pinned uint8 buffer, event or None)] * slots
+_pool = None
+
+
+def _ingest_threads() -> int:
+    return max(1, int(os.environ.get("SRML_INGEST_THREADS", str(min(8, os.cpu_count() or 1)))))
+
+
+def _thread_pool():
+    global _pool
+    from concurrent.futures import ThreadPoolExecutor
+
+    n = _ingest_threads()
+    if _pool is None or _pool._max_workers != n:
+        _pool = ThreadPoolExecutor(max_workers=n, thread_name_prefix="srml-ingest")
+    return _pool
+
+
+def parts_to_device(parts: Any, device: torch.device, dtype: Optional[torch.dtype] = None,
+                    mode: Optional[str] = None) -> torch.Tensor:
+    """Row blocks (list of (rows_i, n) arrays, or ``ChunkedRows``) -> one (sum rows_i, n) device
+    tensor, never concatenating them on the host.
+
+    ``staged`` (default): a ring of pinned buffers; each is filled by ``SRML_INGEST_THREADS``
+    threads (numpy copies release the GIL; the element-type cast, if any, happens in the same
+    copy) and DMA'd on the high-priority copy stream while the next one fills. ``register``: each
+    block is page-locked in place (hipHostRegister), DMA'd directly and unregistered. The compute
+    stream waits for the last copy on the device; the host never blocks on the transfer except to
+    recycle a ring slot."""
+    blocks = list(getattr(parts, "parts", parts))
+    blocks = [np.ascontiguousarray(b) for b in blocks if b.shape[0] > 0]
+    if not blocks:
+        raise ValueError("no rows")
+    n = int(blocks[0].shape[1])
+    rows = int(sum(b.shape[0] for b in blocks))
+    np_dt = blocks[0].dtype if dtype is None else {torch.float32: np.dtype(np.float32),
+                                                    torch.float64: np.dtype(np.float64)}[dtype]
+    tdt = torch.from_numpy(np.zeros(0, dtype=np_dt)).dtype
+    if device.type != "cuda":
+        return torch.from_numpy(np.concatenate(blocks, 0).astype(np_dt, copy=False)).to(device)
+    mode = mode or os.environ.get("SRML_INGEST_MODE", "staged")
+    out = torch.empty((rows, n), dtype=tdt, device=device)
+    cur = torch.cuda.current_stream(device)
+    cs = copy_stream(device)
+    cs.wait_stream(cur)
+    out.record_stream(cs)
+    if mode == "register" and all(b.dtype == np_dt for b in blocks):
+        cudart = torch.cuda.cudart()
+        regs = []
+        r0 = 0
+        with torch.cuda.stream(cs):
+            for b in blocks:
+                cudart.cudaHostRegister(b.ctypes.data, b.nbytes, 0)
+                regs.append(b)
+                with warnings.catch_warnings():
+                    warnings.simplefilter("ignore", UserWarning)
+                    out[r0: r0 + b.shape[0]].copy_(torch.from_numpy(b), non_blocking=True)
+                r0 += b.shape[0]
+        cs.synchronize()  # blocks must stay registered until their DMA has landed
+        for b in regs:
+            cudart.cudaHostUnregister(b.ctypes.data)
+        cur.wait_stream(cs)
+        return out
+    for _ in _staged_fill(blocks, out, device, cs):
+        pass
+    cur.wait_stream(cs)
+    return out
+
+
+def _staged_fill(blocks: list, out: torch.Tensor, device: torch.device, cs: "torch.cuda.Stream"):
+    """Generator: fill the pinned ring slot by slot from the row blocks (threaded copies, cast on
+    the fly), DMA each slot into ``out`` on ``cs``; yields (row0, row1, event) per slot."""
+    rows, n = out.shape
+    tdt = out.dtype
+    esz = out.element_size()
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    slot_bytes = int(os.environ.get("SRML_INGEST_SLOT_MB", "64")) << 20
+    ring = _ring.get(idx)
+    if ring is None or ring[0][0].numel() < slot_bytes:
+        ring = [[torch.empty(slot_bytes, dtype=torch.uint8, pin_memory=True), None] for _ in range(_RING_SLOTS)]
+        _ring[idx] = ring
+    slot_rows = max(1, slot_bytes // (n * esz))
+    flat_out = out.view(-1)
+    pool = _thread_pool()
+    nth = _ingest_threads()
+    s_i = 0
+    row_out = 0
+    bi, br = 0, 0  # block index, row within block
+    while row_out < rows:
+        buf, ev = ring[s_i]
+        if ev is not None:
+            ev.synchronize()
+        stage = buf[: slot_rows * n * esz].view(tdt).view(slot_rows, n).numpy()
+        jobs = []
+        filled = 0
+        while filled < slot_rows and bi < len(blocks):
+            b = blocks[bi]
+            take = min(slot_rows - filled, b.shape[0] - br)
+            jobs.append((stage[filled: filled + take], b[br: br + take]))
+            filled += take
+            br += take
+            if br == b.shape[0]:
+                bi, br = bi + 1, 0
+        pieces = []
+        for dst, src in jobs:  # split every copy over the threads by rows
+            step = max(1, -(-dst.shape[0] // nth))
+            for r in range(0, dst.shape[0], step):
+                pieces.append((dst[r: r + step], src[r: r + step]))
+        list(pool.map(lambda ds: np.copyto(ds[0], ds[1], casting="unsafe"), pieces))
+        with torch.cuda.stream(cs):
+            flat_out[row_out * n: (row_out + filled) * n].copy_(buf[: filled * n * esz].view(tdt), non_blocking=True)
+            e = torch.cuda.Event()
+            e.record(cs)
+        ring[s_i][1] = e
+        yield row_out, row_out + filled, e
+        row_out += filled
+        s_i = (s_i + 1) % _RING_SLOTS
+
+
+class StreamedParts:
+    """``StreamedRows`` for a multi-batch pageable partition (``ChunkedRows``): ``chunks()`` fills
+    and DMAs the pinned ring slot by slot and yields each slot's rows as soon as its copy is queued,
+    so the first pass (moments / Gram / X^T y) runs on slot i while slot i+1 is being filled and
+    copied; ``wait_all()`` finishes the transfer (host fill + device ordering)."""
+
+    def __init__(self, parts: Any, device: torch.device, dtype: Optional[torch.dtype] = None) -> None:
+        blocks = [np.ascontiguousarray(b) for b in getattr(parts, "parts", parts) if b.shape[0] > 0]
+        n = int(blocks[0].shape[1])
+        rows = int(sum(b.shape[0] for b in blocks))
+        np_dt = blocks[0].dtype if dtype is None else {torch.float32: np.dtype(np.float32),
+                                                        torch.float64: np.dtype(np.float64)}[dtype]
+        tdt = torch.from_numpy(np.zeros(0, dtype=np_dt)).dtype
+        self.device = device
+        cur = torch.cuda.current_stream(device)
+        self.X = torch.empty((rows, n), dtype=tdt, device=device)
+        self._copy = copy_stream(device)
+        self._copy.wait_stream(cur)
+        self.X.record_stream(self._copy)
+        self._gen = _staged_fill(blocks, self.X, device, self._copy)
+        self._last = None
+
+    def chunks(self):
+        cur = torch.cuda.current_stream(self.device)
+        for r0, r1, ev in self._gen:
+            self._last = ev
+            cur.wait_event(ev)
+            yield r0, r1, self.X[r0:r1]
+
+    def wait_all(self) -> torch.Tensor:
+        for _, _, ev in self._gen:
+            self._last = ev
+        if self._last is not None:
+            torch.cuda.current_stream(self.device).wait_event(self._last)
+        return self.X
+
+
 def host_to_device(X: Any, device: torch.device, dtype: Optional[torch.dtype] = None) -> Any:
-    """numpy dense / scipy CSR / torch tensor -> device tensor (or ``core.base.CSR``)."""
+    """numpy dense / ``ChunkedRows`` / scipy CSR / torch tensor -> device tensor (or ``core.base.CSR``)."""
     import scipy.sparse as sp
 
+    if hasattr(X, "parts") and getattr(X, "ndim", 0) == 2:  # ChunkedRows (multi-batch partition)
+        return parts_to_device(X, device, dtype)
     if isinstance(X, torch.Tensor):
         X = X.to(device)
         return X.to(dtype) if dtype is not None and X.is_floating_point() else X

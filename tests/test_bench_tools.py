@@ -78,3 +78,27 @@ def test_comm_sweep_single_rank():
     assert r.returncode == 0, r.stderr[-2000:]
     rows = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert {x["op"] for x in rows} == {"all_reduce", "all_gather"} and all(x["us"] > 0 for x in rows)
+
+
+def test_chunked_rows_ingest_matches_contiguous():
+    """A multi-batch Arrow partition is fitted from per-batch zero-copy views (no host concat)
+    and gives the same model as the contiguous array."""
+    import numpy as np
+    import pyarrow as pa
+
+    from spark_rapids_ml_nai_amd import DataFrame
+    from spark_rapids_ml_nai_amd.core.dataframe import ChunkedRows, array_column_chunks, dense_to_list_array
+    from spark_rapids_ml_nai_amd.regression import LinearRegression
+
+    rng = np.random.default_rng(1)
+    X = rng.standard_normal((1000, 6)).astype(np.float32)
+    y = X @ np.arange(1, 7) + 0.5
+    rbs = [pa.RecordBatch.from_pydict({"features": dense_to_list_array(X[i:i + 128].copy()),
+                                       "label": pa.array(y[i:i + 128])}) for i in range(0, 1000, 128)]
+    df = DataFrame([pa.Table.from_batches(rbs)])
+    ch = array_column_chunks(df.column("features"), np.float32)
+    assert isinstance(ch, ChunkedRows) and ch.shape == (1000, 6) and len(ch.parts) == 8
+    assert np.shares_memory(ch.parts[1], rbs[1].column(0).values.to_numpy())
+    a = LinearRegression().fit(df)
+    b = LinearRegression().fit(DataFrame.from_numpy(X, y))
+    np.testing.assert_allclose(a.coefficients.toArray(), b.coefficients.toArray(), rtol=1e-6)

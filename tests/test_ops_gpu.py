@@ -569,3 +569,19 @@ def test_rf_many_classes(gpu_device, classes, bins):
     model = RandomForestClassifier(numTrees=4, maxDepth=8, maxBins=bins, seed=1).fit(DataFrame.from_numpy(X, y.astype(np.float64)))
     pred = model.transform(DataFrame.from_numpy(X, y.astype(np.float64))).to_numpy("prediction")
     assert (pred == y).mean() > 0.8
+
+
+@pytest.mark.parametrize("mode", ["staged", "register"])
+@pytest.mark.parametrize("src_dtype,dst", [(np.float32, torch.float32), (np.float64, torch.float32),
+                                           (np.float32, torch.float64)])
+def test_parts_to_device(gpu_device, mode, src_dtype, dst, monkeypatch):
+    """Multi-batch pageable ingest (Spark-like record batches) lands exactly where it belongs."""
+    from spark_rapids_ml_nai_amd.ops import ingest
+
+    monkeypatch.setenv("SRML_INGEST_SLOT_MB", "1")  # many ring slots per call, blocks straddling slots
+    rng = np.random.default_rng(0)
+    sizes = [1, 700, 0, 1333, 257, 4096, 3]
+    parts = [rng.standard_normal((s, 77)).astype(src_dtype) for s in sizes]
+    got = ingest.parts_to_device(parts, gpu_device, dst, mode=mode).cpu()
+    ref = torch.from_numpy(np.concatenate(parts, 0).astype(np.float32 if dst == torch.float32 else np.float64))
+    assert got.dtype == dst and torch.equal(got, ref)
