@@ -71,6 +71,12 @@ def _registry() -> Dict[str, Workload]:
             "kmeans", "uniform",
             lambda: KMeans(k=1000, maxIter=30, tol=1e-20, initMode="random", featuresCol="features", seed=1),
         )
+        # not in the reference table (no Spark CPU number; outside the geomean): the same fit with
+        # the DEFAULT initMode (k-means||), to show the device seeding cost next to the Lloyd loop
+        reg["kmeans_init_parallel"] = Workload(
+            "kmeans_init_parallel", "uniform",
+            lambda: KMeans(k=1000, maxIter=30, tol=1e-20, featuresCol="features", seed=1),
+        )
     except ImportError:
         pass
     try:
@@ -125,7 +131,7 @@ def model_evidence(name: str, model: Any) -> Dict[str, Any]:
     counts, objective, tree sizes), recorded next to its time in the bench JSON."""
     ev: Dict[str, Any] = {}
     try:
-        if name == "kmeans":
+        if name.startswith("kmeans"):
             ev["n_iter"] = int(model._model_attributes.get("n_iter", 0))
             ev["k"] = len(model.cluster_centers_)
         elif name == "logistic_regression":

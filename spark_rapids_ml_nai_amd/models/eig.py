@@ -6,9 +6,9 @@ cuML PCAMG internally). PCA needs only the top-k eigenpairs with k << n, so the 
 is a restarted block-Krylov Rayleigh–Ritz iteration:
 
 * the n x n fp64 matrix stays on the device; every Krylov product ``C @ Q`` and the skinny basis
-  products are plain library fp64 GEMMs (``torch.matmul`` -> hipBLASLt/rocBLAS: 3000 x 3000 x 19
-  in tens of us, where the generic ``srml_dgemm`` tile kernel took ~0.26 ms on these
-  tall-skinny shapes) — the only O(n^2) work;
+  products run on our f64-MFMA GEMM (``ops.dgemm`` -> ``srml_dgemm_splitk``: K split over
+  grid.z so a 3000 x 3000 x 19 product launches ~1000 blocks instead of 47 output tiles, the
+  splits folded in index order) — the only O(n^2) work;
 * the (n x b·q) basis stays on the device too: block Gram–Schmidt and CholeskyQR2 are device
   GEMMs; only the tiny (b·q)^2 Gram / projected matrices go to host LAPACK (Cholesky, eigh);
 * convergence is checked with true residuals ``||C u - θ u|| <= tol · θ_max`` and the basis is
@@ -41,7 +41,7 @@ def _dorth(V: torch.Tensor) -> torch.Tensor:
     Falls back to a host Householder QR when the Gram matrix is numerically singular."""
     W = V
     for _ in range(2):
-        G = (W.T @ W).cpu().numpy()
+        G = ops.dgemm(W, W, ta=True).cpu().numpy()
         G = (G + G.T) * 0.5
         try:
             L = np.linalg.cholesky(G)
@@ -51,7 +51,7 @@ def _dorth(V: torch.Tensor) -> torch.Tensor:
         if d.min() <= 1e-7 * d.max():  # nearly rank-deficient: CholQR loses orthogonality
             return torch.from_numpy(_orth(V.cpu().numpy())).to(V.device)
         Rinv = np.linalg.solve(L, np.eye(L.shape[0])).T  # (L^T)^-1 = R^-1
-        W = W @ torch.from_numpy(np.ascontiguousarray(Rinv)).to(V.device)
+        W = ops.dgemm(W, torch.from_numpy(np.ascontiguousarray(Rinv)).to(V.device))
     return W
 
 
@@ -85,23 +85,23 @@ def topk_eigh(C: torch.Tensor, k: int, tol: float = 1e-10, max_restarts: int = 6
         blocks = [Q0]
         Qprev = Q0
         for _j in range(q):
-            W = C @ Qprev
+            W = ops.dgemm(C, Qprev)
             # block Gram–Schmidt against the basis so far (twice for stability), then orthonormalise
             Vb = torch.cat(blocks, 1)
             for _r in range(2):
-                W = W - Vb @ (Vb.T @ W)
+                W = ops.dgemm(Vb, ops.dgemm(Vb, W, ta=True), alpha=-1.0, beta=1.0, out=W.clone())
             Qn = _dorth(W)
             blocks.append(Qn)
             Qprev = Qn
         V = _dorth(torch.cat(blocks, 1))
-        CV = C @ V
-        T = (V.T @ CV).cpu().numpy()
+        CV = ops.dgemm(C, V)
+        T = ops.dgemm(V, CV, ta=True).cpu().numpy()
         w, S = np.linalg.eigh((T + T.T) * 0.5)
         order = np.argsort(w)[::-1]
         w, S = w[order], S[:, order]
         Sd = torch.from_numpy(np.ascontiguousarray(S[:, :b])).to(dev)
-        U = V @ Sd
-        CU = CV @ Sd
+        U = ops.dgemm(V, Sd)
+        CU = ops.dgemm(CV, Sd)
         theta = w[:b]
         if scale is None:
             scale = max(abs(theta[0]), 1e-300)

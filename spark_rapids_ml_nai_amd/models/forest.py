@@ -305,10 +305,13 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
             it[:, 0] = np.repeat(node_rep, nfc)
             it[:, 1] = np.repeat(rb, nfc)
             it[:, 2] = np.repeat(re, nfc)
-            it[:, 3] = np.tile(np.arange(nfc), tot_ch)
+            # single-chunk nodes own their histogram cells: plain stores, no zeroing, no atomics
+            single = np.repeat(nch[node_rep] == 1, nfc)
+            it[:, 3] = np.tile(np.arange(nfc), tot_ch) | np.where(single, 1 << 30, 0).astype(np.int32)
             items_t = torch.from_numpy(it).to(dev, non_blocking=False)
+            excl = {"multi_nodes": torch.from_numpy(np.nonzero(nch != 1)[0]).to(dev)} if dev.type == "cuda" else None
             hist = ops.rf_hist(bins, idx, yv, None, items_t, feats, C, B, SH, regression, pos_weight=wpos, fb=fb,
-                               yscale=yscale)
+                               yscale=yscale, exclusive=excl)
             if data_parallel:
                 ctx.comm.allreduce(hist)
             out, _ = ops.rf_best_split(hist, B, SH, regression, crit, min_leaf, min_gain)

@@ -20,7 +20,7 @@ from __future__ import annotations
 
 import os
 
-from typing import Any, Dict, Optional
+from typing import Any, Dict, Optional, Tuple
 
 import numpy as np
 import torch
@@ -52,76 +52,93 @@ def init_random(X: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext, 
     return C
 
 
-def _weighted_kmeanspp(P: torch.Tensor, w: torch.Tensor, k: int, gen: torch.Generator) -> torch.Tensor:
-    """Weighted k-means++ seeding of the (small) candidate set on the device."""
-    npts = P.shape[0]
-    Pf = P.float()
-    first = int(torch.multinomial(w.float(), 1, generator=gen).item())
-    centers = [first]
-    d2 = ((Pf - Pf[first]) ** 2).sum(1)
-    for _ in range(1, k):
-        prob = (w * d2).double()
-        tot = float(prob.sum().item())
-        if tot <= 0:
-            nxt = int(torch.randint(0, npts, (1,), generator=gen, device=P.device).item())
-        else:
-            nxt = int(torch.multinomial((prob / tot).float(), 1, generator=gen).item())
-        centers.append(nxt)
-        d2 = torch.minimum(d2, ((Pf - Pf[nxt]) ** 2).sum(1))
-    return P[torch.tensor(centers, device=P.device)].clone()
-
-
 def _weighted_lloyd(P: torch.Tensor, w: torch.Tensor, C: torch.Tensor, iters: int = 30) -> torch.Tensor:
+    """Weighted Lloyd on the (small) candidate set (Spark's LocalKMeans step): the fused distance /
+    arg-min kernel, the cluster-sum kernel over the pre-weighted rows; stops as soon as no
+    candidate changes cluster (the centres are then a fixed point)."""
     Pf = P.float().contiguous()
     pn = ops.row_sqnorm(Pf) if Pf.is_cuda else (Pf * Pf).sum(1)
     k = C.shape[0]
+    Pw = (P.double() * w.double().view(-1, 1)).float().contiguous()
+    wd = w.double()
+    C = C.double()
+    prev = None
     for _ in range(iters):
         lab, _ = ops.nearest_centroid(Pf, C.float(), pn)
-        lab = lab.long()
-        sums = torch.zeros_like(C, dtype=torch.float64)
-        sums.index_add_(0, lab, P.double() * w.double().view(-1, 1))
-        cnt = torch.zeros(k, dtype=torch.float64, device=P.device).index_add_(0, lab, w.double())
-        newC = torch.where(cnt.view(-1, 1) > 0, sums / cnt.clamp_min(1e-300).view(-1, 1), C.double())
-        if torch.allclose(newC, C.double()):
-            C = newC
+        if prev is not None and torch.equal(lab, prev):
             break
-        C = newC
+        prev = lab
+        sums, _ = ops.cluster_sums(Pw, lab, k)
+        cnt = torch.zeros(k, dtype=torch.float64, device=P.device).index_add_(0, lab.long(), wd)
+        C = torch.where(cnt.view(-1, 1) > 0, sums / cnt.clamp_min(1e-300).view(-1, 1), C)
     return C
 
 
 def init_kmeans_parallel(X: torch.Tensor, xnorm: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext,
-                         k: int, seed: int, oversampling: float = 2.0, steps: int = 2) -> torch.Tensor:
+                         k: int, seed: int, oversampling: float = 2.0, steps: int = 2,
+                         XP: Optional[torch.Tensor] = None, trials: int = 1) -> torch.Tensor:
+    """k-means|| (scalable k-means++, reference cuML ``init="scalable-k-means++"`` / Spark
+    ``initMode="k-means||"``): ``steps`` rounds of D^2 over-sampling (ell = oversampling * k rows
+    per round, device RNG), candidates all-gathered, weighted by the rows they attract, then reduced
+    to k centres by ``trials`` (Spark: 1) seeded weighted k-means++ draws on the device
+    (``kmeanspp_gram``: distances from the candidates' MFMA Gram matrix) + weighted Lloyd, keeping
+    the lowest cost.
+    The distance passes over X use the split-bf16 MFMA kernel when the Lloyd loop will (``XP``),
+    in its 3-product approximate form (D^2 sampling and candidate weights tolerate ~1e-5
+    relative distance error; half the MFMA work of the exact Lloyd passes)."""
     dev = X.device
+    m = X.shape[0]
+
+    def nearest(C: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        if XP is not None:  # sampling / weighting only need approximate distances
+            return ops.nearest_centroid_split(XP, m, C.float(), xnorm, approx=True)
+        return ops.nearest_centroid(X, C.float(), xnorm)
+
     rng = np.random.default_rng(seed)
     C = _global_rows(X, desc, ctx, np.array([int(rng.integers(0, desc.m))]))
     gen = torch.Generator(device=dev)
     gen.manual_seed(int(seed) * 1000003 + ctx.rank)
     ell = oversampling * k
-    for _ in range(max(1, steps)):
-        _, d2 = ops.nearest_centroid(X, C.float(), xnorm)
-        phi = d2.double().sum().view(1)
+    # running (min d^2, arg-min) over all candidates so far: each pass only scores the centres
+    # added by the previous round, and the candidate weights come from the same running arg-min
+    best_d2 = best_lab = None
+    new = C
+    for r in range(max(1, steps) + 1):
+        lab, d2 = nearest(new)
+        off = C.shape[0] - new.shape[0]
+        if best_d2 is None:
+            best_d2, best_lab = d2, lab.long() + off
+        else:
+            better = d2 < best_d2
+            best_d2 = torch.where(better, d2, best_d2)
+            best_lab = torch.where(better, lab.long() + off, best_lab)
+        if r == max(1, steps):
+            break
+        phi = best_d2.double().sum().view(1)
         ctx.comm.allreduce(phi)
-        p = (ell * d2.double() / max(float(phi.item()), 1e-300)).clamp_max(1.0)
+        p = (ell * best_d2.double() / phi.clamp_min(1e-300)).clamp_max(1.0)
         pick = torch.rand(X.shape[0], generator=gen, device=dev, dtype=torch.float64) < p
         local = X[pick].double()
         parts = ctx.comm.allgatherv(local)
-        C = torch.cat([C] + [q.to(dev) for q in parts], 0)
+        new = torch.cat([q.to(dev) for q in parts], 0)
+        if new.shape[0] == 0:
+            break
+        C = torch.cat([C, new], 0)
     # weight every candidate by the points it attracts
-    lab, _ = ops.nearest_centroid(X, C.float(), xnorm)
-    w = torch.bincount(lab.long(), minlength=C.shape[0]).double()
+    w = torch.bincount(best_lab, minlength=C.shape[0]).double()
     ctx.comm.allreduce(w)
     if C.shape[0] <= k:
         extra = init_random(X, desc, ctx, k - C.shape[0], seed + 1) if C.shape[0] < k else None
         return torch.cat([C, extra], 0) if extra is not None else C
-    # the candidate set is tiny (~ steps * oversampling * k points): run a few seeded k-means++
-    # + weighted Lloyd trials on it and keep the lowest weighted cost (deterministic per seed)
-    g2 = torch.Generator(device=dev)
-    g2.manual_seed(int(seed))
     Cf = C.float().contiguous()
+    G = ops.gram(Cf.T.contiguous()) if Cf.is_cuda else Cf.double() @ Cf.double().T  # C C^T (nc x nc)
     cn = ops.row_sqnorm(Cf) if Cf.is_cuda else (Cf * Cf).sum(1)
     best, best_cost = None, float("inf")
-    for _ in range(5):
-        Ct = _weighted_lloyd(C, w, _weighted_kmeanspp(C, w, k, g2))
+    for t in range(max(1, trials)):
+        idx = ops.kmeanspp_gram(G, w, k, int(seed) * 7919 + t)
+        Ct = _weighted_lloyd(C, w, C[idx])
+        if trials <= 1:
+            return Ct
         _, d2 = ops.nearest_centroid(Cf, Ct.float(), cn)
         cost = float((d2.double() * w).sum().item())
         if cost < best_cost:
@@ -152,17 +169,17 @@ def kmeans_fit(X: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext, k
                timer: Any = None) -> Dict[str, Any]:
     n = X.shape[1]
     xnorm = ops.row_sqnorm(X)
+    # k > 256: 256 x 256 LDS-DMA kernel on the tiled plane layout (SRML_SPLIT_TILED=0: plain layout)
+    tiled = k > 256 and os.environ.get("SRML_SPLIT_TILED", "1") == "1"
+    XP = ops.split_bf16x3(X, tiled=tiled) if _use_split(X, k) else None
     if init in ("random",):
         C = init_random(X, desc, ctx, k, seed)
     elif init in ("scalable-k-means++", "k-means||", "k-means++"):
-        C = init_kmeans_parallel(X, xnorm, desc, ctx, k, seed, oversampling, init_steps)
+        C = init_kmeans_parallel(X, xnorm, desc, ctx, k, seed, oversampling, init_steps, XP=XP)
     else:
         raise ValueError("Unsupported init mode %s" % init)
     C = C.double()
     tol2 = float(tol) ** 2
-    # k > 256: 256 x 256 LDS-DMA kernel on the tiled plane layout (SRML_SPLIT_TILED=0: plain layout)
-    tiled = k > 256 and os.environ.get("SRML_SPLIT_TILED", "1") == "1"
-    XP = ops.split_bf16x3(X, tiled=tiled) if _use_split(X, k) else None
     n_iter = 0
     inertia = 0.0
     for it in range(max(0, max_iter)):

@@ -4,12 +4,13 @@ the numerics oracle in the kernel tests).
 """
 from __future__ import annotations
 
-from typing import Optional, Tuple
+from typing import Dict, Optional, Tuple
 
 import numpy as np
 import torch
 
 from . import native
+from ..utils.determinism import deterministic
 
 __all__ = ["col_moments", "gram", "xw", "dgemm", "sign_flip", "is_native", "xtv", "row_sqnorm",
            "logreg_binary_loss_grad", "nearest_centroid", "cluster_sums", "csr_logreg_binary_loss_grad",
@@ -63,14 +64,19 @@ def gram(X: torch.Tensor, mean: Optional[torch.Tensor] = None, out: Optional[tor
     X = _c(X)
     mu = _c(mean.to(torch.float32)) if mean is not None else None
     st = native.stream(X.device)
+    ws, wsc = None, 0
+    if deterministic():  # per-chunk partial tiles folded in order (<= 64 chunks, <= 1 GB)
+        wsc = int(max(1, min(64, (1 << 30) // (8 * n * n))))
+        ws = torch.empty(wsc * n * n, dtype=torch.float64, device=X.device)
+    wsp = ws.data_ptr() if ws is not None else None
     if not finalize:
-        native.call("srml_gram_f32", X.data_ptr(), m, n, X.stride(0), mu.data_ptr() if mu is not None else None,
-                    out.data_ptr(), st)
+        native.call("srml_gram_f32_ex", X.data_ptr(), m, n, X.stride(0), mu.data_ptr() if mu is not None else None,
+                    out.data_ptr(), wsp, wsc, st)
         return out
     # the kernel accumulates only the upper triangle; mirror into a temporary, then add
     up = torch.zeros_like(out)
-    native.call("srml_gram_f32", X.data_ptr(), m, n, X.stride(0), mu.data_ptr() if mu is not None else None,
-                up.data_ptr(), st)
+    native.call("srml_gram_f32_ex", X.data_ptr(), m, n, X.stride(0), mu.data_ptr() if mu is not None else None,
+                up.data_ptr(), wsp, wsc, st)
     native.call("srml_mirror_upper_f64", up.data_ptr(), n, st)
     out += up
     return out
@@ -90,15 +96,24 @@ _XW_WIDTHS = (1, 2, 3, 4, 8, 16, 32)
 
 
 def xw(X: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """out = X @ W (+ bias): X (m, n) fp32, W (n, k). One bandwidth-bound pass over X."""
+    """out = X @ W (+ bias): X (m, n), W (n, k). fp32: one bandwidth-bound pass over X per 32
+    output columns (``srml_xw_f32``); fp64: the f64-MFMA GEMM (``srml_dgemm``)."""
     m, n = X.shape
     k = W.shape[1]
     if not X.is_cuda:
         out = X.to(W.dtype) @ W
         return out + bias if bias is not None else out
-    if X.dtype != torch.float32 or k > 32:
-        out = X @ W.to(X.dtype)
-        return out + bias.to(X.dtype) if bias is not None else out
+    if X.dtype == torch.float64:
+        out = torch.empty((m, k), dtype=torch.float64, device=X.device)
+        if bias is not None:
+            out.copy_(bias.to(device=X.device, dtype=torch.float64).view(1, k).expand(m, k))
+        dgemm(_c(X), W.to(device=X.device, dtype=torch.float64), beta=1.0 if bias is not None else 0.0, out=out)
+        return out
+    if X.dtype != torch.float32:
+        raise TypeError("xw supports fp32/fp64 inputs, got %s" % X.dtype)
+    if k > 32:
+        cols = [xw(X, W[:, c0: c0 + 32], bias[c0: c0 + 32] if bias is not None else None) for c0 in range(0, k, 32)]
+        return torch.cat(cols, 1)
     X = _c(X)
     kk = next(w for w in _XW_WIDTHS if w >= k)
     Wp = torch.zeros((n, kk), dtype=torch.float32, device=X.device)
@@ -132,9 +147,30 @@ def dgemm(A: torch.Tensor, B: torch.Tensor, ta: bool = False, tb: bool = False, 
         return out
     A = _c(A.double())
     B = _c(B.double())
+    if out.stride(1) != 1:
+        raise ValueError("dgemm: out must have unit column stride")
+    st = native.stream(A.device)
+    tiles = ((M + 63) // 64) * ((N + 63) // 64)
+    splits = _dgemm_splits(M, N, K, tiles)
+    if splits > 1:
+        ws = torch.empty(splits * M * N, dtype=torch.float64, device=A.device)
+        native.call("srml_dgemm_splitk", int(ta), int(tb), M, N, K, float(alpha), A.data_ptr(), A.stride(0),
+                    B.data_ptr(), B.stride(0), float(beta), out.data_ptr(), out.stride(0), splits, ws.data_ptr(), st)
+        return out
     native.call("srml_dgemm", int(ta), int(tb), M, N, K, float(alpha), A.data_ptr(), A.stride(0), B.data_ptr(),
-                B.stride(0), float(beta), out.data_ptr(), out.stride(0), native.stream(A.device))
+                B.stride(0), float(beta), out.data_ptr(), out.stride(0), st)
     return out
+
+
+def _dgemm_splits(M: int, N: int, K: int, tiles: int) -> int:
+    """K splits for the fp64 GEMM: enough 64x64 tiles x splits to cover the 256 CUs ~4x, each
+    split >= 64 deep, workspace (splits x M x N fp64) <= 256 MB."""
+    if tiles >= 512 or K < 128:
+        return 1
+    want = (1024 + tiles - 1) // tiles
+    by_k = K // 64
+    by_mem = max(1, (256 << 20) // max(1, 8 * M * N))
+    return max(1, min(want, by_k, by_mem))
 
 
 def sign_flip(U: torch.Tensor) -> torch.Tensor:
@@ -163,9 +199,11 @@ def xtv(X: torch.Tensor, V: torch.Tensor, out: Optional[torch.Tensor] = None) ->
     if not X.is_cuda:
         out += X.double().T @ V2.double()
         return out
-    if X.dtype != torch.float32:
-        out += (X.T @ V2.to(X.dtype)).double()
+    if X.dtype == torch.float64:
+        dgemm(_c(X), _c(V2.to(torch.float64)), ta=True, beta=1.0, out=out)  # split-K f64 MFMA
         return out
+    if X.dtype != torch.float32:
+        raise TypeError("xtv supports fp32/fp64 inputs, got %s" % X.dtype)
     X = _c(X)
     for c0 in range(0, k, 4):
         kk = min(4, k - c0)
@@ -178,7 +216,13 @@ def xtv(X: torch.Tensor, V: torch.Tensor, out: Optional[torch.Tensor] = None) ->
 
 
 def row_sqnorm(X: torch.Tensor) -> torch.Tensor:
+    """||x_r||^2 per row: fp32 for fp32 inputs, fp64 for fp64 inputs on the device."""
     m, n = X.shape
+    if X.is_cuda and X.dtype == torch.float64:
+        X = _c(X)
+        out = torch.empty(m, dtype=torch.float64, device=X.device)
+        native.call("srml_row_sqnorm_f64", X.data_ptr(), m, n, X.stride(0), out.data_ptr(), native.stream(X.device))
+        return out
     if not X.is_cuda or X.dtype != torch.float32:
         return (X.float() * X.float()).sum(1)
     X = _c(X)
@@ -214,6 +258,17 @@ def nearest_centroid(X: torch.Tensor, C: torch.Tensor, xnorm: Optional[torch.Ten
     """(labels int32 [m], squared distance fp32 [m]) of each row's nearest centroid (fused, no m x k matrix)."""
     m, n = X.shape
     k = C.shape[0]
+    if X.is_cuda and X.dtype == torch.float64:
+        X = _c(X)
+        Cd = _c(C.to(device=X.device, dtype=torch.float64))
+        cn = (Cd * Cd).sum(1) if cnorm is None or cnorm.dtype != torch.float64 else _c(cnorm)
+        xn = xnorm if xnorm is not None and xnorm.dtype == torch.float64 else row_sqnorm(X)
+        labels = torch.empty(m, dtype=torch.int32, device=X.device)
+        dist = torch.empty(m, dtype=torch.float32, device=X.device)
+        native.call("srml_nearest_centroid_f64", X.data_ptr(), m, n, X.stride(0), Cd.data_ptr(), k, Cd.stride(0),
+                    cn.data_ptr(), _c(xn).data_ptr(), labels.data_ptr(), dist.data_ptr(), None,
+                    native.stream(X.device))
+        return labels, dist
     if cnorm is None:
         cnorm = (C.float() * C.float()).sum(1)
     if not X.is_cuda or X.dtype != torch.float32:
@@ -275,9 +330,12 @@ def split_bf16x3(X: torch.Tensor, row_multiple: int = 128, tiled: bool = False) 
 
 
 def nearest_centroid_split(XP: torch.Tensor, m: int, C: torch.Tensor, xnorm: torch.Tensor,
-                           cnorm: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+                           cnorm: Optional[torch.Tensor] = None, approx: bool = False
+                           ) -> Tuple[torch.Tensor, torch.Tensor]:
     """``nearest_centroid`` on pre-split X planes (``split_bf16x3``): the distance GEMM runs on
-    the bf16 matrix cores as six cross products of the planes (fp32-accurate; see splitmm.hip)."""
+    the bf16 matrix cores as six cross products of the planes (fp32-accurate; see splitmm.hip).
+    ``approx=True`` (tiled planes): only the three leading products (~2^-16 relative dot error,
+    half the MFMAs) — for consumers of approximate distances (k-means|| sampling)."""
     k = C.shape[0]
     Cf = C.float()
     if cnorm is None:
@@ -287,15 +345,17 @@ def nearest_centroid_split(XP: torch.Tensor, m: int, C: torch.Tensor, xnorm: tor
     if not XP.is_cuda:
         Xh, Xm, Xl = (XP[p, :m].float() for p in range(3))
         Ch, Cm, Cl = (CP[p, :k].float() for p in range(3))
-        dot = Xl @ Ch.T + Xm @ Cm.T + Xh @ Cl.T + Xm @ Ch.T + Xh @ Cm.T + Xh @ Ch.T
+        dot = Xm @ Ch.T + Xh @ Cm.T + Xh @ Ch.T
+        if not (approx and tiled):
+            dot = Xl @ Ch.T + Xm @ Cm.T + Xh @ Cl.T + dot
         v, i = (cnorm.float().view(1, -1) - 2.0 * dot).min(1)
         return i.int(), (v + xnorm.float()).clamp_min(0)
     cn = _c(cnorm.to(torch.float32))
     best = torch.full((m,), -1, dtype=torch.int64, device=XP.device)
     st = native.stream(XP.device)
     if tiled:
-        native.call("srml_nearest_centroid_split_tiled", XP.data_ptr(), m, XP.shape[1] * 256, XP.shape[2] * 16,
-                    CP.data_ptr(), k, CP.shape[1] * 256, cn.data_ptr(), best.data_ptr(), st)
+        native.call("srml_nearest_centroid_split_tiled_np", XP.data_ptr(), m, XP.shape[1] * 256, XP.shape[2] * 16,
+                    CP.data_ptr(), k, CP.shape[1] * 256, cn.data_ptr(), best.data_ptr(), 3 if approx else 6, st)
     else:
         native.call("srml_nearest_centroid_split", XP.data_ptr(), m, XP.shape[1], XP.shape[2], CP.data_ptr(), k,
                     CP.shape[1], cn.data_ptr(), best.data_ptr(), st)
@@ -306,16 +366,78 @@ def nearest_centroid_split(XP: torch.Tensor, m: int, C: torch.Tensor, xnorm: tor
     return labels, dist
 
 
+_M64 = (1 << 64) - 1
+
+
+def _splitmix64(x: int) -> int:
+    x = (x + 0x9E3779B97F4A7C15) & _M64
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & _M64
+    return x ^ (x >> 31)
+
+
+def _uniform01(seed: int, ctr: int) -> float:
+    return (_splitmix64((seed * 0x2545F4914F6CDD1D + ctr) & _M64) >> 11) * (1.0 / 9007199254740992.0)
+
+
+KMEANSPP_MAX_CANDIDATES = 8192  # KPP_T * KPP_PER in csrc/kmeans.hip
+
+
+def kmeanspp_gram(G: torch.Tensor, w: torch.Tensor, k: int, seed: int) -> torch.Tensor:
+    """Weighted k-means++ seeding (indices of k candidates) from the candidates' Gram matrix
+    G = C C^T: pick 0 ~ w, then pick t ~ w_i min_j<t ||c_i - c_j||^2. GPU: one block, no host
+    round trip per pick; CPU: the same draws (same counter-based uniforms) in numpy."""
+    nc = G.shape[0]
+    seed = int(seed) & _M64
+    if G.is_cuda and nc <= KMEANSPP_MAX_CANDIDATES:
+        out = torch.empty(k, dtype=torch.int32, device=G.device)
+        native.call("srml_kmeanspp_gram", _c(G.double()).data_ptr(), nc, _c(w.double()).data_ptr(), int(k), seed,
+                    out.data_ptr(), native.stream(G.device))
+        return out.long()
+    Gh = G.double().cpu().numpy()
+    wh = w.double().cpu().numpy()
+    diag = np.diag(Gh).copy()
+    d2 = np.full(nc, np.inf)
+
+    def draw(p: np.ndarray, ctr: int) -> int:
+        cs = np.cumsum(p)
+        tot = cs[-1] if nc else 0.0
+        if not tot > 0:
+            return -1
+        i = int(np.searchsorted(cs, _uniform01(seed, ctr) * tot, side="right"))
+        return min(i, nc - 1)
+
+    c = max(draw(wh, 0), 0)
+    picks = [c]
+    for t in range(1, k):
+        d2 = np.minimum(d2, np.maximum(diag + Gh[c, c] - 2.0 * Gh[c], 0.0))
+        nx = draw(wh * d2, t)
+        c = nx if nx >= 0 else int(_splitmix64((seed + 77 * t) & _M64) % nc)
+        picks.append(c)
+    return torch.tensor(picks, dtype=torch.long, device=G.device)
+
+
 def cluster_sums(X: torch.Tensor, labels: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
     """(sums fp64 [k, n], counts int64 [k]) of rows grouped by label."""
     m, n = X.shape
-    if not X.is_cuda or X.dtype != torch.float32:
+    if not X.is_cuda or X.dtype not in (torch.float32, torch.float64):
         sums = torch.zeros((k, n), dtype=torch.float64, device=X.device)
         sums.index_add_(0, labels.long(), X.double())
         counts = torch.bincount(labels.long(), minlength=k)
         return sums, counts
     X = _c(X)
     lab = _c(labels.to(torch.int32))
+    if X.dtype == torch.float64 or deterministic():
+        # label-sorted segments, one block per (cluster, column chunk), fixed order, no atomics
+        slab, perm = torch.sort(lab, stable=True)
+        counts = torch.bincount(lab, minlength=k).long()
+        off = torch.zeros(k + 1, dtype=torch.int64, device=X.device)
+        torch.cumsum(counts, 0, out=off[1:])
+        sums = torch.empty((k, n), dtype=torch.float64, device=X.device)
+        name = "srml_kmeans_segment_sums_f64" if X.dtype == torch.float64 else "srml_kmeans_segment_sums_f32"
+        native.call(name, X.data_ptr(), m, n, X.stride(0), _c(perm.to(torch.int32)).data_ptr(), off.data_ptr(), k,
+                    sums.data_ptr(), native.stream(X.device))
+        return sums, counts
     counts = torch.zeros(k, dtype=torch.int32, device=X.device)
     st = native.stream(X.device)
     if k * n * 4 + k * 4 <= 64 * 1024:
@@ -394,7 +516,7 @@ def rf_hist_fb(B: int, S: int, regression: bool) -> int:
 def rf_hist(bins: torch.Tensor, idx: torch.Tensor, label: torch.Tensor, wcnt: Optional[torch.Tensor],
             items: torch.Tensor, node_feats: torch.Tensor, nodes: int, B: int, S: int,
             regression: bool, pos_weight: Optional[torch.Tensor] = None, fb: Optional[int] = None,
-            yscale: Optional[float] = None) -> torch.Tensor:
+            yscale: Optional[float] = None, exclusive: Optional[Dict[str, torch.Tensor]] = None) -> torch.Tensor:
     """Per-(node, feature slot, bin) statistics: uint32 class counts or fp64 (count, sum[, sumsq]).
     Weights: per row (``wcnt``, indexed by row id) or per position of ``idx`` (``pos_weight``).
     ``items`` rows are (node, row_begin, row_end, feature_chunk) with chunks of ``fb`` features
@@ -403,15 +525,23 @@ def rf_hist(bins: torch.Tensor, idx: torch.Tensor, label: torch.Tensor, wcnt: Op
     n, m = bins.shape
     nf = node_feats.shape[1]
     dev = bins.device
-    if regression:
-        hist = torch.zeros((nodes, nf, B, S), dtype=torch.float64, device=dev)
+    hdt = torch.float64 if regression else torch.int32
+    if not bins.is_cuda or items.shape[0] == 0:
+        hist = torch.zeros((nodes, nf, B, S), dtype=hdt, device=dev)
+        if items.shape[0] == 0:
+            return hist
+    elif exclusive is not None:
+        # nodes served by ONE row chunk are written with plain stores by their items (flag bit 30 of
+        # item.w); only the multi-chunk nodes accumulate with atomics and need zeroing
+        hist = torch.empty((nodes, nf, B, S), dtype=hdt, device=dev)
+        if exclusive["multi_nodes"].numel():
+            hist.index_fill_(0, exclusive["multi_nodes"], 0)
     else:
-        hist = torch.zeros((nodes, nf, B, S), dtype=torch.int32, device=dev)
-    if items.shape[0] == 0:
-        return hist
+        hist = torch.zeros((nodes, nf, B, S), dtype=hdt, device=dev)
     if not bins.is_cuda:
         it = items.cpu().numpy()
         for node, rb, re, fc in it:
+            fc = int(fc) & 0x3FFFFFFF
             rows = idx[rb:re].long()
             if pos_weight is not None:
                 w = pos_weight[rb:re].double()
@@ -616,15 +746,61 @@ def rf_predict(X: torch.Tensor, roots: torch.Tensor, feature: torch.Tensor, thre
 # ------------------------------------------------------------------------------------------
 # Nearest-neighbour search
 # ------------------------------------------------------------------------------------------
-KNN_KMAX = 64
+KNN_KMAX = 64          # register/LDS insertion-list kernel (srml_knn_f32)
+TOPK_KMAX = 1024       # distance-chunk + radix-select path (srml_knn_dist_f32 + srml_topk_rows_f32)
+_TOPK_SLICE = 65536    # columns per select block
+_KNN_DIST_BYTES = 1 << 30  # distance chunk budget
+
+
+def topk_rows(vals: torch.Tensor, k: int, ids: Optional[torch.Tensor] = None, id_base: int = 0,
+              slice_len: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """k smallest values of every row (ascending, ties -> lower column) and their ids
+    (``ids[r, c]``, or ``id_base + c``). Rows longer than ``slice_len`` are selected per slice and
+    merged. Device: ``srml_topk_rows_f32``; host: torch.topk."""
+    rows, L = vals.shape
+    if not vals.is_cuda:
+        kk = min(k, L)
+        v, j = torch.sort(vals.float(), dim=1, stable=True)  # ties keep the lower column
+        v, j = v[:, :kk], j[:, :kk]
+        outv = torch.full((rows, k), float("inf"), dtype=torch.float32, device=vals.device)
+        outi = torch.full((rows, k), -1, dtype=torch.int64, device=vals.device)
+        outv[:, :kk] = v
+        outi[:, :kk] = ids.gather(1, j) if ids is not None else j + id_base
+        return outv, outi
+    if k > TOPK_KMAX:
+        raise ValueError("topk_rows: k=%d > %d" % (k, TOPK_KMAX))
+    if vals.dtype != torch.float32 or vals.stride(1) != 1:
+        vals = vals.float().contiguous()
+    S = int(slice_len or _TOPK_SLICE)
+    S = max(S, k)
+    nsl = (L + S - 1) // S
+    ids_c = _c(ids.long()) if ids is not None else None
+    st = native.stream(vals.device)
+    if nsl == 1:
+        outv = torch.empty((rows, k), dtype=torch.float32, device=vals.device)
+        outi = torch.empty((rows, k), dtype=torch.int64, device=vals.device)
+        native.call("srml_topk_rows_f32", vals.data_ptr(), rows, vals.stride(0), S, L,
+                    ids_c.data_ptr() if ids_c is not None else None, ids_c.stride(0) if ids_c is not None else 0,
+                    int(id_base), k, outv.data_ptr(), outi.data_ptr(), k, 0, st)
+        return outv, outi
+    pv = torch.empty((rows, nsl * k), dtype=torch.float32, device=vals.device)
+    pi = torch.empty((rows, nsl * k), dtype=torch.int64, device=vals.device)
+    native.call("srml_topk_rows_f32", vals.data_ptr(), rows, vals.stride(0), S, L,
+                ids_c.data_ptr() if ids_c is not None else None, ids_c.stride(0) if ids_c is not None else 0,
+                int(id_base), k, pv.data_ptr(), pi.data_ptr(), nsl * k, k, st)
+    return topk_rows(pv, k, ids=pi, slice_len=nsl * k)  # one merge block per row
 
 
 def knn(Q: torch.Tensor, I: torch.Tensor, k: int, inorm: Optional[torch.Tensor] = None,
         qnorm: Optional[torch.Tensor] = None, id_offset: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Exact k nearest items of every query: (squared L2 distances fp32 [mq, k], item ids int64 [mq, k])."""
+    """Exact k nearest items of every query: (squared L2 distances fp32 [mq, k], item ids int64 [mq, k]).
+    Device: k <= 64 -> fused MFMA tiles + LDS insertion lists (``srml_knn_f32``); 64 < k <= 1024 ->
+    bounded distance chunks on the MFMA tile + radix select (``_knn_large_k``)."""
     mq, n = Q.shape
     mi = I.shape[0]
     kk = min(k, mi)
+    if Q.is_cuda and Q.dtype == torch.float32 and KNN_KMAX < k <= TOPK_KMAX:
+        return _knn_large_k(Q, I, kk, inorm, qnorm, id_offset)
     if inorm is None:
         inorm = row_sqnorm(I)
     if qnorm is None:
@@ -652,10 +828,46 @@ def knn(Q: torch.Tensor, I: torch.Tensor, k: int, inorm: Optional[torch.Tensor] 
     od = od.view(mq, slices * kk)
     oi = oi.view(mq, slices * kk)
     if slices > 1:
-        v, j = torch.topk(od, kk, dim=1, largest=False)
-        oi = oi.gather(1, j)
-        od = v
+        od, oi = topk_rows(od, kk, ids=oi)
     return (od + qnorm.float().view(-1, 1)).clamp_min(0), oi
+
+
+def _knn_large_k(Q: torch.Tensor, I: torch.Tensor, k: int, inorm: Optional[torch.Tensor],
+                 qnorm: Optional[torch.Tensor], id_offset: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """64 < k <= 1024: per (query chunk, item chunk) the partial distances ||i||^2 - 2 q.i are
+    materialised (<= 1 GB) by the MFMA tile kernel, selected per 64k-column slice by the radix-
+    select kernel, and the per-chunk lists merged by the same kernel with ids."""
+    mq, n = Q.shape
+    mi = I.shape[0]
+    Q = _c(Q)
+    I = _c(I.to(torch.float32))
+    inorm = _c(row_sqnorm(I) if inorm is None else inorm.float())
+    qnorm = row_sqnorm(Q) if qnorm is None else qnorm.float()
+    st = native.stream(Q.device)
+    Lc = min(mi, 16 * _TOPK_SLICE)
+    R = max(128, min(4096, (_KNN_DIST_BYTES // (Lc * 4)) // 128 * 128))
+    nchunks = (mi + Lc - 1) // Lc
+    outv = torch.empty((mq, k), dtype=torch.float32, device=Q.device)
+    outi = torch.empty((mq, k), dtype=torch.int64, device=Q.device)
+    D = torch.empty((min(R, mq), Lc), dtype=torch.float32, device=Q.device)
+    for q0 in range(0, mq, R):
+        r = min(R, mq - q0)
+        parts_v, parts_i = [], []
+        for c in range(nchunks):
+            i0 = c * Lc
+            L = min(Lc, mi - i0)
+            native.call("srml_knn_dist_f32", Q[q0:].data_ptr(), r, n, Q.stride(0), I[i0:].data_ptr(), L, I.stride(0),
+                        inorm[i0:].data_ptr(), D.data_ptr(), Lc, st)
+            v, i = topk_rows(D[:r, :L], k, id_base=i0 + int(id_offset))
+            parts_v.append(v)
+            parts_i.append(i)
+        if nchunks > 1:
+            v, i = topk_rows(torch.cat(parts_v, 1), k, ids=torch.cat(parts_i, 1))
+        else:
+            v, i = parts_v[0], parts_i[0]
+        outv[q0: q0 + r] = (v + qnorm[q0: q0 + r].view(-1, 1)).clamp_min(0)
+        outi[q0: q0 + r] = i
+    return outv, outi
 
 
 def ivf_search(Q: torch.Tensor, probes: torch.Tensor, list_off: torch.Tensor, items: torch.Tensor,

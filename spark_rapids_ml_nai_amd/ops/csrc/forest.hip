@@ -174,7 +174,11 @@ __global__ __launch_bounds__(256) void rf_hist_kernel(const unsigned char* __res
   extern __shared__ __attribute__((aligned(16))) unsigned lh_u[];
   unsigned long long* lh_s = reinterpret_cast<unsigned long long*>(lh_u + fb * B);
   const int4 it = items[blockIdx.x];
-  const int node = it.x, rb = it.y, re = it.z, fc = it.w;
+  // item.w = feature chunk | RF_ITEM_EXCLUSIVE: this item is its node's only row chunk, so it owns
+  // its histogram cells outright (plain stores of every cell, zeros included; the caller does not
+  // pre-zero such nodes) instead of atomics into a zeroed buffer
+  const bool excl = (it.w >> 30) & 1;
+  const int node = it.x, rb = it.y, re = it.z, fc = it.w & 0x3fffffff;
   const int f_begin = fc * fb;
   const int nfb = min(fb, nf - f_begin);
   const int words = REG ? fb * B * 3 : fb * B * S;
@@ -230,10 +234,12 @@ __global__ __launch_bounds__(256) void rf_hist_kernel(const unsigned char* __res
       double v;
       if (st == 0) v = (double)lh_u[j * B + b];
       else v = (double)(long long)lh_s[j * B + b] * inv;
-      if (v != 0.0) atomicAdd(&hist_d[out_base + i], v);
+      if (excl) hist_d[out_base + i] = v;
+      else if (v != 0.0) atomicAdd(&hist_d[out_base + i], v);
     } else {
       const unsigned v = lh_u[(j * S + st) * B + b];
-      if (v) atomicAdd(&hist_u[out_base + i], v);
+      if (excl) hist_u[out_base + i] = v;
+      else if (v) atomicAdd(&hist_u[out_base + i], v);
     }
   }
 }

@@ -98,7 +98,8 @@ __device__ __forceinline__ void store_stage(float (*As)[BT], float (*Bs)[BT], bo
 template <bool CENTER, bool VEC>
 __global__ __launch_bounds__(NTHREADS, 2) void gram_f32_kernel(const float* __restrict__ X, long m, int n, long ld,
                                                                const float* __restrict__ mu, double* __restrict__ C,
-                                                               int T, int ntiles, long rows_per_chunk) {
+                                                               int T, int ntiles, long rows_per_chunk,
+                                                               double* __restrict__ ws) {
   __shared__ __attribute__((aligned(16))) float As[2][BK][BT];
   __shared__ __attribute__((aligned(16))) float Bs[2][BK][BT];
 
@@ -170,10 +171,27 @@ __global__ __launch_bounds__(NTHREADS, 2) void gram_f32_kernel(const float* __re
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int gi = i0 + wi * 64 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
-        if (gi < n && gj < n && gi <= gj) atomicAdd(&C[(long)gi * n + gj], (double)acc[mt][nt][r]);
+        if (gi < n && gj < n && gi <= gj) {
+          if (ws)
+            ws[((long)chunk * n + gi) * n + gj] = (double)acc[mt][nt][r];
+          else
+            atomicAdd(&C[(long)gi * n + gj], (double)acc[mt][nt][r]);
+        }
       }
     }
   }
+}
+
+// C[i][j] (i <= j) += sum over chunks in index order (deterministic mode)
+__global__ void gram_fold_kernel(const double* __restrict__ ws, int chunks, int n, double* __restrict__ C) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long nn = (long)n * n;
+  if (idx >= nn) return;
+  const int i = (int)(idx / n), j = (int)(idx % n);
+  if (i > j) return;
+  double s = 0.0;
+  for (int c = 0; c < chunks; ++c) s += ws[c * nn + idx];
+  C[idx] += s;
 }
 
 __global__ void mirror_upper_kernel(double* __restrict__ C, int n) {
@@ -185,8 +203,13 @@ __global__ void mirror_upper_kernel(double* __restrict__ C, int n) {
 }
 }  // namespace
 
-// C (n x n fp64, zeroed by the caller or holding a running sum) += (X-mu)^T (X-mu), full matrix.
-SRML_API int srml_gram_f32(const float* X, long m, int n, long ld, const float* mu, double* C, hipStream_t stream) {
+// C (n x n fp64, zeroed by the caller or holding a running sum) += (X-mu)^T (X-mu), upper triangle.
+// ws != null (deterministic mode): at most ws_chunks row chunks, each storing its partial tiles
+// into ws[chunk] (ws_chunks * n * n fp64) with plain stores, folded into C in chunk order — the
+// same fp32-per-chunk / fp64-across-chunk precision as the atomic path, bit-reproducible.
+SRML_API int srml_gram_f32_ex(const float* X, long m, int n, long ld, const float* mu, double* C, double* ws,
+                              int ws_chunks, hipStream_t stream) {
+  const int max_chunks = ws ? ws_chunks : 0;
   if (n <= 0) return 0;
   if (m > 0) {
     const int T = (n + BT - 1) / BT;
@@ -194,8 +217,9 @@ SRML_API int srml_gram_f32(const float* X, long m, int n, long ld, const float* 
     // split rows so that tiles*chunks ~ 2-4 blocks per CU, chunks >= 1 k-step each
     long want_blocks = 2048;
     long chunks = (want_blocks + ntiles - 1) / ntiles;
-    long max_chunks = (m + BK - 1) / BK;
-    if (chunks > max_chunks) chunks = max_chunks;
+    long ksteps = (m + BK - 1) / BK;
+    if (chunks > ksteps) chunks = ksteps;
+    if (max_chunks > 0 && chunks > max_chunks) chunks = max_chunks;
     if (chunks < 1) chunks = 1;
     long rows_per_chunk = (m + chunks - 1) / chunks;
     rows_per_chunk = ((rows_per_chunk + BK - 1) / BK) * BK;
@@ -205,22 +229,32 @@ SRML_API int srml_gram_f32(const float* X, long m, int n, long ld, const float* 
     if (mu) {
       if (vec)
         hipLaunchKernelGGL((gram_f32_kernel<true, true>), dim3(nblocks), dim3(NTHREADS), 0, stream, X, m, n, ld, mu, C, T,
-                           ntiles, rows_per_chunk);
+                           ntiles, rows_per_chunk, ws);
       else
         hipLaunchKernelGGL((gram_f32_kernel<true, false>), dim3(nblocks), dim3(NTHREADS), 0, stream, X, m, n, ld, mu, C,
-                           T, ntiles, rows_per_chunk);
+                           T, ntiles, rows_per_chunk, ws);
     } else {
       if (vec)
         hipLaunchKernelGGL((gram_f32_kernel<false, true>), dim3(nblocks), dim3(NTHREADS), 0, stream, X, m, n, ld, mu, C,
-                           T, ntiles, rows_per_chunk);
+                           T, ntiles, rows_per_chunk, ws);
       else
         hipLaunchKernelGGL((gram_f32_kernel<false, false>), dim3(nblocks), dim3(NTHREADS), 0, stream, X, m, n, ld, mu, C,
-                           T, ntiles, rows_per_chunk);
+                           T, ntiles, rows_per_chunk, ws);
     }
     int st = srml_status();
     if (st) return st;
+    if (ws) {
+      const long nn = (long)n * n;
+      hipLaunchKernelGGL(gram_fold_kernel, dim3(ceil_div(nn, 256)), dim3(256), 0, stream, ws, (int)chunks, n, C);
+      st = srml_status();
+      if (st) return st;
+    }
   }
   return 0;
+}
+
+SRML_API int srml_gram_f32(const float* X, long m, int n, long ld, const float* mu, double* C, hipStream_t stream) {
+  return srml_gram_f32_ex(X, m, n, ld, mu, C, nullptr, 0, stream);
 }
 
 SRML_API int srml_mirror_upper_f64(double* C, int n, hipStream_t stream) {

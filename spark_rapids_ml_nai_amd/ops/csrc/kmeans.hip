@@ -588,3 +588,162 @@ SRML_API int srml_kmeans_accumulate_sorted_f32(const float* X, long m, int n, lo
   }
   return srml_status();
 }
+
+// Deterministic / fp64 cluster sums: rows visited in label-sorted order (perm), cluster l owns
+// the segment [off[l], off[l+1]). One block per (cluster, 256-column chunk) sums its segment in
+// row order into fp64 registers and stores the result once: no atomics, bit-reproducible run to
+// run (SRML_DETERMINISTIC=1), and the fp64-input path (T = double) of the Lloyd update.
+template <typename T>
+__global__ __launch_bounds__(256) void segment_sums_kernel(const T* __restrict__ X, int n, long ld,
+                                                           const int* __restrict__ perm,
+                                                           const long* __restrict__ off, double* __restrict__ sums) {
+  const int l = blockIdx.x;
+  const int c = blockIdx.y * 256 + threadIdx.x;
+  if (c >= n) return;
+  const long s0 = off[l], s1 = off[l + 1];
+  constexpr int U = 8;
+  double acc = 0.0;
+  long i = s0;
+  for (; i + U <= s1; i += U) {
+    T v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = X[(long)perm[i + u] * ld + c];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += (double)v[u];
+  }
+  for (; i < s1; ++i) acc += (double)X[(long)perm[i] * ld + c];
+  sums[(long)l * n + c] = acc;
+}
+
+template <typename T>
+static int launch_segment_sums(const T* X, long m, int n, long ld, const int* perm, const long* off, int k,
+                               double* sums, hipStream_t stream) {
+  if (k <= 0 || n <= 0) return 0;
+  (void)m;
+  dim3 grid((unsigned)k, ceil_div(n, 256));
+  hipLaunchKernelGGL(segment_sums_kernel<T>, grid, dim3(256), 0, stream, X, n, ld, perm, off, sums);
+  return srml_status();
+}
+
+// sums (k*n fp64, fully written) of the rows perm[off[l]:off[l+1]] per cluster l.
+SRML_API int srml_kmeans_segment_sums_f32(const float* X, long m, int n, long ld, const int* perm, const long* off,
+                                          int k, double* sums, hipStream_t stream) {
+  return launch_segment_sums<float>(X, m, n, ld, perm, off, k, sums, stream);
+}
+SRML_API int srml_kmeans_segment_sums_f64(const double* X, long m, int n, long ld, const int* perm, const long* off,
+                                          int k, double* sums, hipStream_t stream) {
+  return launch_segment_sums<double>(X, m, n, ld, perm, off, k, sums, stream);
+}
+
+// ------------------------------------------------------------------------------------------
+// Weighted k-means++ seeding of a small candidate set entirely on the device (the reduction step
+// of k-means||, Spark's LocalKMeans): ONE block runs the k sequential picks with no host round
+// trip (the previous path did two .item() syncs per centre: ~10k for k=1000 and 5 trials).
+// Distances come from the candidates' Gram matrix G = C C^T (MFMA SYRK), so a pick costs one
+// pass over nc values: d2[i] = min(d2[i], G_ii + G_cc - 2 G_ic); the next centre is drawn with
+// probability w_i d2_i / sum (block-wide inclusive scan + a counter-based uniform).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__device__ __forceinline__ double uniform01(unsigned long long seed, unsigned long long ctr) {
+  return (double)(splitmix64(seed * 0x2545F4914F6CDD1Dull + ctr) >> 11) * (1.0 / 9007199254740992.0);
+}
+
+constexpr int KPP_T = 1024;
+constexpr int KPP_PER = 8;   // candidates per thread (nc <= 8192)
+
+// block-wide sample: returns the smallest i with prefix(p)[i] > u * total (p >= 0), or -1 if total == 0
+__device__ int kpp_sample(const double (&p)[KPP_PER], int base, int cnt, double u, double* lds, int* pick) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  double loc = 0.0;
+#pragma unroll
+  for (int q = 0; q < KPP_PER; ++q) loc += q < cnt ? p[q] : 0.0;
+  // inclusive scan of the per-thread sums within the wave, then across the 16 waves
+  double x = loc;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) lds[wid] = x;
+  if (threadIdx.x == 0) *pick = -1;
+  __syncthreads();
+  double wave_off = 0.0, total = 0.0;
+  for (int w = 0; w < KPP_T / 64; ++w) {
+    const double v = lds[w];
+    if (w < wid) wave_off += v;
+    total += v;
+  }
+  const double excl = wave_off + x - loc;  // sum of all candidates before this thread's
+  const double target = u * total;
+  if (total > 0.0 && excl <= target && target < excl + loc) {
+    double run = excl;
+    int hit = cnt - 1;
+    for (int q = 0; q < cnt; ++q) {
+      run += p[q];
+      if (target < run) { hit = q; break; }
+    }
+    *pick = base + hit;  // exactly one thread owns the target (half-open ranges)
+  }
+  __syncthreads();
+  int r = *pick;
+  if (total > 0.0 && r < 0) {  // rounding at the very top of the range: last positive candidate
+    __syncthreads();
+    if (loc > 0.0) atomicMax(pick, base + cnt - 1);
+    __syncthreads();
+    r = *pick;
+  }
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(KPP_T) void kmeanspp_gram_kernel(const double* __restrict__ G, int nc,
+                                                              const double* __restrict__ w, int k,
+                                                              unsigned long long seed, int* __restrict__ out) {
+  __shared__ double lds[KPP_T / 64];
+  __shared__ int pick;
+  const int base = threadIdx.x * KPP_PER;
+  const int cnt = max(0, min(KPP_PER, nc - base));
+  double d2[KPP_PER], wv[KPP_PER], gii[KPP_PER], p[KPP_PER];
+#pragma unroll
+  for (int q = 0; q < KPP_PER; ++q) {
+    const int i = base + q;
+    const bool ok = q < cnt;
+    wv[q] = ok ? w[i] : 0.0;
+    gii[q] = ok ? G[(long)i * nc + i] : 0.0;
+    d2[q] = INFINITY;
+    p[q] = wv[q];
+  }
+  int c = kpp_sample(p, base, cnt, uniform01(seed, 0), lds, &pick);
+  if (c < 0) c = 0;
+  if (threadIdx.x == 0) out[0] = c;
+  for (int t = 1; t < k; ++t) {
+    const double gcc = G[(long)c * nc + c];
+    const double* gc = G + (long)c * nc;
+#pragma unroll
+    for (int q = 0; q < KPP_PER; ++q) {
+      if (q < cnt) {
+        const double dd = fmax(gii[q] + gcc - 2.0 * gc[base + q], 0.0);
+        d2[q] = fmin(d2[q], dd);
+        p[q] = wv[q] * d2[q];
+      }
+    }
+    int nx = kpp_sample(p, base, cnt, uniform01(seed, (unsigned long long)t), lds, &pick);
+    if (nx < 0) nx = (int)(splitmix64(seed + 77 * t) % (unsigned long long)nc);  // all mass on chosen points
+    c = nx;
+    if (threadIdx.x == 0) out[t] = c;
+  }
+}
+
+SRML_API int srml_kmeanspp_gram(const double* G, int nc, const double* w, int k, unsigned long long seed, int* out,
+                                hipStream_t stream) {
+  if (nc <= 0 || k <= 0) return 0;
+  if (nc > KPP_T * KPP_PER) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(kmeanspp_gram_kernel, dim3(1), dim3(KPP_T), 0, stream, G, nc, w, k, seed, out);
+  return srml_status();
+}

@@ -10,6 +10,10 @@
 //                      Krylov products with the fp64 covariance (PCA eigensolver), normal-
 //                      equation solves, and the C-ABI `srml_dgemm` (reference JNI dgemm,
 //                      rapidsml_jni.cu:131-212).
+//                      Tall-skinny / long-K shapes (X^T V, C·Q with few output tiles) split K over
+//                      grid.z: every split writes its partial tile to a workspace with plain stores
+//                      and one ordered pass folds the splits (alpha, beta applied there), so the
+//                      result is bit-reproducible (no atomics) and the grid still fills the chip.
 //  * srml_sign_flip_f64 — deterministic eigenvector signs: one wave per column finds the
 //                      max-|x| entry with a wave64 arg-max and negates the column if that entry
 //                      is negative (reference N1 `signFlip`, rapidsml_jni.cu:35-61, which used
@@ -179,7 +183,8 @@ constexpr int DK = 16;
 // v_mfma_f64_16x16x4_f64: A[i=l&15][k=l>>4], B[k=l>>4][j=l&15]; D: col=l&15, row=(l>>4)+4*r
 __global__ __launch_bounds__(256) void dgemm_kernel(int M, int N, int K, double alpha, const double* __restrict__ A,
                                                     long lda, int ta, const double* __restrict__ B, long ldb, int tb,
-                                                    double beta, double* __restrict__ C, long ldc) {
+                                                    double beta, double* __restrict__ C, long ldc, int kchunk,
+                                                    double* __restrict__ ws) {
   __shared__ double As[DK][DT + 1];  // As[k][i]
   __shared__ double Bs[DK][DT + 1];  // Bs[k][j]
   const int i0 = blockIdx.y * DT, j0 = blockIdx.x * DT;
@@ -191,7 +196,9 @@ __global__ __launch_bounds__(256) void dgemm_kernel(int M, int N, int K, double 
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = doublex4{0, 0, 0, 0};
 
-  for (int k0 = 0; k0 < K; k0 += DK) {
+  const int kbeg = blockIdx.z * kchunk;
+  const int kend = min(K, kbeg + kchunk);
+  for (int k0 = kbeg; k0 < kend; k0 += DK) {
     // stage 64x16 of op(A) and 16x64 of op(B): 1024 elements each, 4 per thread
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
@@ -200,11 +207,11 @@ __global__ __launch_bounds__(256) void dgemm_kernel(int M, int N, int K, double 
       int gi = i0 + ii, gk = k0 + kk;
       double va = 0.0;
       if (ta) {
-        if (gi < M && gk < K) va = A[(long)gk * lda + gi];
+        if (gi < M && gk < kend) va = A[(long)gk * lda + gi];
       } else {
         int kk2 = e % DK, ii2 = e / DK;  // A row-major: k contiguous
         gi = i0 + ii2; gk = k0 + kk2;
-        if (gi < M && gk < K) va = A[(long)gi * lda + gk];
+        if (gi < M && gk < kend) va = A[(long)gi * lda + gk];
         kk = kk2; ii = ii2;
       }
       As[kk][ii] = va;
@@ -212,11 +219,11 @@ __global__ __launch_bounds__(256) void dgemm_kernel(int M, int N, int K, double 
       int gj = j0 + jj, gkb = k0 + kb;
       double vb = 0.0;
       if (!tb) {
-        if (gj < N && gkb < K) vb = B[(long)gkb * ldb + gj];
+        if (gj < N && gkb < kend) vb = B[(long)gkb * ldb + gj];
       } else {
         int kb2 = e % DK, jj2 = e / DK;  // B^T: B stored N x K row-major
         gj = j0 + jj2; gkb = k0 + kb2;
-        if (gj < N && gkb < K) vb = B[(long)gj * ldb + gkb];
+        if (gj < N && gkb < kend) vb = B[(long)gj * ldb + gkb];
         kb = kb2; jj = jj2;
       }
       Bs[kb][jj] = vb;
@@ -245,17 +252,57 @@ __global__ __launch_bounds__(256) void dgemm_kernel(int M, int N, int K, double 
         int gi = i0 + wi * 32 + mt * 16 + (lane >> 4) + 4 * r;
         int gj = j0 + wj * 32 + nt * 16 + (lane & 15);
         if (gi < M && gj < N) {
-          double* c = &C[(long)gi * ldc + gj];
-          *c = alpha * acc[mt][nt][r] + (beta != 0.0 ? beta * *c : 0.0);
+          if (ws) {
+            ws[((long)blockIdx.z * M + gi) * N + gj] = acc[mt][nt][r];
+          } else {
+            double* c = &C[(long)gi * ldc + gj];
+            *c = alpha * acc[mt][nt][r] + (beta != 0.0 ? beta * *c : 0.0);
+          }
         }
       }
+}
+
+// C = alpha * sum_z ws[z] + beta C, splits folded in index order (deterministic)
+__global__ __launch_bounds__(256) void dgemm_fold_kernel(int M, int N, int splits, double alpha,
+                                                         const double* __restrict__ ws, double beta,
+                                                         double* __restrict__ C, long ldc) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long)M * N) return;
+  const long MN = (long)M * N;
+  double s = 0.0;
+  for (int z = 0; z < splits; ++z) s += ws[z * MN + idx];
+  const int i = (int)(idx / N), j = (int)(idx % N);
+  double* c = &C[(long)i * ldc + j];
+  *c = alpha * s + (beta != 0.0 ? beta * *c : 0.0);
 }
 
 SRML_API int srml_dgemm(int ta, int tb, int M, int N, int K, double alpha, const double* A, long lda, const double* B,
                         long ldb, double beta, double* C, long ldc, hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
-  dim3 grid(ceil_div(N, DT), ceil_div(M, DT));
-  hipLaunchKernelGGL(dgemm_kernel, grid, dim3(256), 0, stream, M, N, K, alpha, A, lda, ta, B, ldb, tb, beta, C, ldc);
+  dim3 grid(ceil_div(N, DT), ceil_div(M, DT), 1);
+  hipLaunchKernelGGL(dgemm_kernel, grid, dim3(256), 0, stream, M, N, K, alpha, A, lda, ta, B, ldb, tb, beta, C, ldc,
+                     K > 0 ? K : 1, (double*)nullptr);
+  return srml_status();
+}
+
+// Split-K variant: `splits` slices of K (multiples of the 16-deep k-step) into `ws`
+// (splits * M * N doubles), then the ordered fold.
+SRML_API int srml_dgemm_splitk(int ta, int tb, int M, int N, int K, double alpha, const double* A, long lda,
+                               const double* B, long ldb, double beta, double* C, long ldc, int splits, double* ws,
+                               hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (splits <= 1 || ws == nullptr) return srml_dgemm(ta, tb, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, stream);
+  int kchunk = (K + splits - 1) / splits;
+  kchunk = ((kchunk + DK - 1) / DK) * DK;
+  splits = (K + kchunk - 1) / kchunk;
+  dim3 grid(ceil_div(N, DT), ceil_div(M, DT), (unsigned)splits);
+  hipLaunchKernelGGL(dgemm_kernel, grid, dim3(256), 0, stream, M, N, K, alpha, A, lda, ta, B, ldb, tb, beta, C, ldc,
+                     kchunk, ws);
+  int st = srml_status();
+  if (st) return st;
+  const long MN = (long)M * N;
+  hipLaunchKernelGGL(dgemm_fold_kernel, dim3(ceil_div(MN, 256)), dim3(256), 0, stream, M, N, splits, alpha, ws, beta,
+                     C, ldc);
   return srml_status();
 }
 

@@ -316,7 +316,9 @@ typedef __attribute__((address_space(3))) void* lds_vptr;
 typedef __attribute__((address_space(1))) void* gbl_vptr;
 
 // TILED: operands in the split_tiled_kernel layout (contiguous, pre-swizzled 8 KiB k-step images).
-template <bool TILED>
+// NP = 6: the fp32-exact product set; NP = 3: h.h + h.m + m.h only (~2^-16 relative, half the
+// MFMAs) for consumers that only need approximate distances (k-means|| D^2 sampling / weighting).
+template <bool TILED, int NP = 6>
 __global__ __launch_bounds__(512, 1) void nearest_centroid_split_glds_kernel(
     const unsigned short* __restrict__ XP, long m, long xrows, int kp, const unsigned short* __restrict__ CP, int k,
     long crows, const float* __restrict__ cnorm, unsigned long long* __restrict__ best, int n_ctiles) {
@@ -396,9 +398,11 @@ __global__ __launch_bounds__(512, 1) void nearest_centroid_split_glds_kernel(
         fa[p] = *reinterpret_cast<const bf16x8*>(&lds[stage][p][wm * (BM / WM) + mt * 32 + li][8 * ph]);
 #pragma unroll
       for (int nt = 0; nt < TN; ++nt) {
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[0][nt], acc[mt][nt], 0, 0, 0);
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1][nt], acc[mt][nt], 0, 0, 0);
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[2][nt], acc[mt][nt], 0, 0, 0);
+        if (NP == 6) {
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[0][nt], acc[mt][nt], 0, 0, 0);
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1][nt], acc[mt][nt], 0, 0, 0);
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[2][nt], acc[mt][nt], 0, 0, 0);
+        }
         acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[0][nt], acc[mt][nt], 0, 0, 0);
         acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[1][nt], acc[mt][nt], 0, 0, 0);
         acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0][nt], acc[mt][nt], 0, 0, 0);
@@ -472,9 +476,10 @@ SRML_API int srml_split_bf16x3_tiled(const float* X, long m, int n, long ld, int
 }
 
 // Nearest centroid on tiled planes of X (xrows % 256 == 0) and of the centroids (crows % 256 == 0).
-SRML_API int srml_nearest_centroid_split_tiled(const unsigned short* XP, long m, long xrows, int kp,
-                                               const unsigned short* CP, int k, long crows, const float* cnorm,
-                                               unsigned long long* best, hipStream_t stream) {
+// nprod: 6 (fp32-exact) or 3 (approximate, half the MFMAs).
+SRML_API int srml_nearest_centroid_split_tiled_np(const unsigned short* XP, long m, long xrows, int kp,
+                                                  const unsigned short* CP, int k, long crows, const float* cnorm,
+                                                  unsigned long long* best, int nprod, hipStream_t stream) {
   if (m <= 0 || k <= 0) return 0;
   if ((kp & 15) || xrows < m || crows < k || (crows & 255) || (xrows & 255)) return -2;
   if ((reinterpret_cast<uintptr_t>(XP) & 15) || (reinterpret_cast<uintptr_t>(CP) & 15)) return -5;
@@ -482,7 +487,19 @@ SRML_API int srml_nearest_centroid_split_tiled(const unsigned short* XP, long m,
   const int ct = (k + 255) / 256;
   const long nb = rt * ct;
   if (nb > 0x7fffffffL) return -3;
-  hipLaunchKernelGGL((nearest_centroid_split_glds_kernel<true>), dim3((unsigned)nb), dim3(512), 0, stream, XP, m,
-                     xrows, kp, CP, k, crows, cnorm, best, (int)ct);
+  if (nprod == 3)
+    hipLaunchKernelGGL((nearest_centroid_split_glds_kernel<true, 3>), dim3((unsigned)nb), dim3(512), 0, stream, XP, m,
+                       xrows, kp, CP, k, crows, cnorm, best, (int)ct);
+  else if (nprod == 6)
+    hipLaunchKernelGGL((nearest_centroid_split_glds_kernel<true, 6>), dim3((unsigned)nb), dim3(512), 0, stream, XP, m,
+                       xrows, kp, CP, k, crows, cnorm, best, (int)ct);
+  else
+    return -2;
   return srml_status();
+}
+
+SRML_API int srml_nearest_centroid_split_tiled(const unsigned short* XP, long m, long xrows, int kp,
+                                               const unsigned short* CP, int k, long crows, const float* cnorm,
+                                               unsigned long long* best, hipStream_t stream) {
+  return srml_nearest_centroid_split_tiled_np(XP, m, xrows, kp, CP, k, crows, cnorm, best, 6, stream);
 }

@@ -1,0 +1,218 @@
+// Large-k exact kNN (64 < k <= 1024) and the row-wise top-k selection shared with the k <= 64
+// slice merge.
+//
+//  * srml_knn_dist_f32 — D[q][i] = ||i||^2 - 2 q.i for a (query chunk x item chunk) on the fp32
+//      matrices cores (the 128x128 `gemm_tile_128` MFMA tile shared with KMeans/DBSCAN), XCD-
+//      remapped so the item tiles of one query panel share an L2. The register/LDS-resident
+//      insertion lists of `srml_knn_f32` stop paying past k = 64 (the list no longer fits and every
+//      candidate pays an O(k) insertion), so for large k the distances of a bounded chunk are
+//      materialised (<= 1 GB, sized by the caller) and selected by:
+//  * srml_topk_rows_f32 — one block per (row, column slice): exact k-smallest by a three-pass
+//      radix select on orderable 32-bit keys (11/11/10-bit digits, LDS histograms, block scan to
+//      find the digit holding the k-th key), then ONE ordered collection pass (block scans in
+//      index order, so ties at the threshold keep the lowest columns and the result is
+//      deterministic) and a bitonic sort of (key, column) pairs in LDS. Optional input ids turn
+//      the same kernel into the merge of per-slice / per-chunk partial lists.
+// Reference: cuML NearestNeighborsMG brute force + RAFT select_k (knn.py:638-749).
+#include "common.h"
+
+#include "tile.h"
+
+namespace {
+using namespace srml_tile;
+
+constexpr int TK_T = 256;
+constexpr int TK_KMAX = 1024;
+
+template <bool VEC>
+__global__ __launch_bounds__(256, 2) void knn_dist_kernel(const float* __restrict__ Q, long mq, int n, long ldq,
+                                                          const float* __restrict__ I, long mi, long ldi,
+                                                          const float* __restrict__ inorm, float* __restrict__ D,
+                                                          long ldd, int n_itiles) {
+  __shared__ Stage128 st;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const long qt = bid / n_itiles;
+  const int it = bid % n_itiles;
+  floatx16 acc[2][2];
+  gemm_tile_128<VEC>(Q, ldq, mq, qt * 128, I, ldi, mi, (long)it * 128, n, st, acc);
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const long i = (long)it * 128 + acc_col(nt);
+    const float in = i < mi ? inorm[i] : 0.f;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const long q = qt * 128 + acc_row(mt, r);
+        if (q < mq && i < mi) D[q * ldd + i] = fmaf(-2.f, acc[mt][nt][r], in);
+      }
+  }
+}
+
+// exclusive block scan of one int per thread (256 threads); `total` = block sum
+__device__ __forceinline__ int block_excl_scan(int v, int* s_w, int& total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_w[wid] = x;
+  __syncthreads();
+  int base = 0;
+  total = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const int tw = s_w[w];
+    if (w < wid) base += tw;
+    total += tw;
+  }
+  __syncthreads();
+  return base + x - v;
+}
+
+__global__ __launch_bounds__(TK_T) void topk_rows_kernel(const float* __restrict__ vals, long ldv, long slice_len,
+                                                         int L_total, const long long* __restrict__ ids, long ldid,
+                                                         long long id_base, int k, float* __restrict__ out_v,
+                                                         long long* __restrict__ out_i, long ldo, long slice_ldo) {
+  __shared__ int hist[2048];
+  __shared__ unsigned skey[TK_KMAX];
+  __shared__ int spos[TK_KMAX];
+  __shared__ int s_w[4];
+  __shared__ int s_digit, s_below;
+  const long row = blockIdx.x;
+  const long c0 = (long)blockIdx.y * slice_len;
+  const int L = (int)min(slice_len, (long)L_total - c0);
+  const float* v = vals + row * ldv + c0;
+  const int t = threadIdx.x;
+  const int kk = L < k ? (L > 0 ? L : 0) : k;
+  const bool take_all = kk == L;
+  unsigned prefix = 0u, mask = 0u;
+  int need = kk;
+  if (!take_all) {
+    for (int pass = 0; pass < 3; ++pass) {
+      const int shift = pass == 0 ? 21 : (pass == 1 ? 10 : 0);
+      const unsigned nb = pass == 2 ? 1024u : 2048u;
+      for (int i = t; i < 2048; i += TK_T) hist[i] = 0;
+      __syncthreads();
+      for (int i = t; i < L; i += TK_T) {
+        const unsigned key = orderable(v[i]);
+        if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & (nb - 1u)], 1);
+      }
+      __syncthreads();
+      int loc[8];
+      int s = 0;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) { loc[b] = hist[8 * t + b]; s += loc[b]; }
+      int total;
+      const int base = block_excl_scan(s, s_w, total);
+      if (base < need && need <= base + s) {
+        int cum = base;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+          if (cum + loc[b] >= need) { s_digit = 8 * t + b; s_below = cum; break; }
+          cum += loc[b];
+        }
+      }
+      __syncthreads();
+      prefix |= (unsigned)s_digit << shift;
+      mask |= (nb - 1u) << shift;
+      need -= s_below;
+      __syncthreads();
+    }
+  }
+  // ordered collection: keys < T in column order, then the first `need` keys == T
+  const unsigned T = prefix;
+  const int nless = kk - need;
+  int run_lt = 0, run_eq = 0;
+  for (int b0 = 0; b0 < L; b0 += TK_T) {
+    const int i = b0 + t;
+    const unsigned key = i < L ? orderable(v[i]) : 0xffffffffu;
+    const bool lt = i < L && (take_all || key < T);
+    const bool eq = i < L && !take_all && key == T;
+    int total;
+    const int ex = block_excl_scan((lt ? 1 : 0) | (eq ? (1 << 16) : 0), s_w, total);
+    if (lt) {
+      const int p = run_lt + (ex & 0xffff);
+      skey[p] = key;
+      spos[p] = i;
+    }
+    if (eq) {
+      const int r = run_eq + (ex >> 16);
+      if (r < need) {
+        skey[nless + r] = key;
+        spos[nless + r] = i;
+      }
+    }
+    run_lt += total & 0xffff;
+    run_eq += total >> 16;
+  }
+  int kpad = 1;
+  while (kpad < kk) kpad <<= 1;
+  for (int p = kk + t; p < kpad; p += TK_T) { skey[p] = 0xffffffffu; spos[p] = 0x7fffffff; }
+  __syncthreads();
+  for (int size = 2; size <= kpad; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = t; i < kpad; i += TK_T) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const bool up = (i & size) == 0;
+          const unsigned ki = skey[i], kj = skey[j];
+          const int pi = spos[i], pj = spos[j];
+          const bool gt = ki > kj || (ki == kj && pi > pj);
+          if (gt == up) { skey[i] = kj; skey[j] = ki; spos[i] = pj; spos[j] = pi; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  float* ov = out_v + row * ldo + (long)blockIdx.y * slice_ldo;
+  long long* oi = out_i + row * ldo + (long)blockIdx.y * slice_ldo;
+  for (int p = t; p < k; p += TK_T) {
+    if (p < kk) {
+      const int c = spos[p];
+      ov[p] = unorderable(skey[p]);
+      oi[p] = ids ? ids[row * ldid + c0 + c] : id_base + c0 + c;
+    } else {
+      ov[p] = __builtin_huge_valf();
+      oi[p] = -1;
+    }
+  }
+}
+}  // namespace
+
+// D (mq x mi, leading dim ldd) = inorm[i] - 2 Q I^T for one (query chunk, item chunk).
+SRML_API int srml_knn_dist_f32(const float* Q, long mq, int n, long ldq, const float* I, long mi, long ldi,
+                               const float* inorm, float* D, long ldd, hipStream_t stream) {
+  if (mq <= 0 || mi <= 0) return 0;
+  const long nq = (mq + 127) / 128, ni = (mi + 127) / 128;
+  if (nq * ni > 0x7fffffffL || ni > 0x7fffffffL) return -1;
+  const bool vec = ((ldq & 3) == 0) && ((ldi & 3) == 0) && ((n & 3) == 0) &&
+                   ((reinterpret_cast<uintptr_t>(Q) & 15) == 0) && ((reinterpret_cast<uintptr_t>(I) & 15) == 0);
+  if (vec)
+    hipLaunchKernelGGL(knn_dist_kernel<true>, dim3((unsigned)(nq * ni)), dim3(256), 0, stream, Q, mq, n, ldq, I, mi, ldi,
+                       inorm, D, ldd, (int)ni);
+  else
+    hipLaunchKernelGGL(knn_dist_kernel<false>, dim3((unsigned)(nq * ni)), dim3(256), 0, stream, Q, mq, n, ldq, I, mi,
+                       ldi, inorm, D, ldd, (int)ni);
+  return srml_status();
+}
+
+// Row-wise k smallest (ascending, ties by column) of `rows` rows of L_total values (leading dim
+// ldv), split into column slices of `slice_len` (grid.y); slice s of row r writes k results at
+// out[r * ldo + s * slice_ldo]. ids: optional int64 ids of the input values (leading dim ldid);
+// without them the id of column c is id_base + c. k <= 1024.
+SRML_API int srml_topk_rows_f32(const float* vals, long rows, long ldv, long slice_len, int L_total,
+                                const long long* ids, long ldid, long long id_base, int k, float* out_v,
+                                long long* out_i, long ldo, long slice_ldo, hipStream_t stream) {
+  if (rows <= 0) return 0;
+  if (k <= 0 || k > TK_KMAX || slice_len <= 0 || L_total <= 0) return -1;
+  const long slices = (L_total + slice_len - 1) / slice_len;
+  if (rows > 0x7fffffffL || slices > 65535) return -1;
+  hipLaunchKernelGGL(topk_rows_kernel, dim3((unsigned)rows, (unsigned)slices), dim3(TK_T), 0, stream, vals, ldv,
+                     slice_len, L_total, ids, ldid, id_base, k, out_v, out_i, ldo, slice_ldo);
+  return srml_status();
+}
+
+SRML_API int srml_topk_kmax() { return TK_KMAX; }

@@ -31,9 +31,11 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_col_moments_f64": (_P, _L, _I, _L, _P, _P, _P),
     "srml_standardize_f32": (_P, _L, _I, _L, _P, _P, _P),
     "srml_gram_f32": (_P, _L, _I, _L, _P, _P, _P),
+    "srml_gram_f32_ex": (_P, _L, _I, _L, _P, _P, _P, _I, _P),
     "srml_mirror_upper_f64": (_P, _I, _P),
     "srml_xw_f32": (_P, _L, _I, _L, _P, _I, _P, _P, _L, _P),
     "srml_dgemm": (_I, _I, _I, _I, _I, _D, _P, _L, _P, _L, _D, _P, _L, _P),
+    "srml_dgemm_splitk": (_I, _I, _I, _I, _I, _D, _P, _L, _P, _L, _D, _P, _L, _I, _P, _P),
     "srml_sign_flip_f64": (_P, _I, _I, _L, _P),
     "srml_xtv_f32": (_P, _L, _I, _L, _P, _I, _L, _P, _P),
     "srml_row_sqnorm_f32": (_P, _L, _I, _L, _P, _P),
@@ -44,6 +46,7 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_mlogit_f32": (_P, _L, _I, _L, _P, _P, _P, _P, _I, _P, _P),
     "srml_mlogit_supported": (_I, _I),
     "srml_qn_step": (_P, _P),
+    "srml_kmeanspp_gram": (_P, _I, _P, _I, ctypes.c_ulonglong, _P, _P),
     "srml_qn_max_history": (),
     "srml_qn_args_size": (),
     "srml_nearest_centroid_f32": (_P, _L, _I, _L, _P, _I, _L, _P, _P, _P),
@@ -52,8 +55,15 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_nearest_centroid_split": (_P, _L, _L, _I, _P, _I, _L, _P, _P, _P),
     "srml_split_bf16x3_tiled": (_P, _L, _I, _L, _I, _L, _P, _P),
     "srml_nearest_centroid_split_tiled": (_P, _L, _L, _I, _P, _I, _L, _P, _P, _P),
+    "srml_nearest_centroid_split_tiled_np": (_P, _L, _L, _I, _P, _I, _L, _P, _P, _I, _P),
     "srml_kmeans_accumulate_f32": (_P, _L, _I, _L, _P, _I, _P, _P, _P, _P),
     "srml_kmeans_accumulate_sorted_f32": (_P, _L, _I, _L, _P, _P, _P, _P),
+    "srml_kmeans_segment_sums_f32": (_P, _L, _I, _L, _P, _P, _I, _P, _P),
+    "srml_kmeans_segment_sums_f64": (_P, _L, _I, _L, _P, _P, _I, _P, _P),
+    "srml_nearest_centroid_f64": (_P, _L, _I, _L, _P, _I, _L, _P, _P, _P, _P, _P, _P),
+    "srml_row_sqnorm_f64": (_P, _L, _I, _L, _P, _P),
+    "srml_knn_dist_f32": (_P, _L, _I, _L, _P, _L, _L, _P, _P, _L, _P),
+    "srml_topk_rows_f32": (_P, _L, _L, _L, _I, _P, _L, ctypes.c_longlong, _I, _P, _P, _L, _L, _P),
     "srml_knn_f32": (_P, _L, _I, _L, _P, _L, _L, _P, _I, _I, _P, _P, ctypes.c_longlong, _P),
     "srml_ivf_search_f32": (_P, _L, _I, _L, _P, _I, _P, _P, _L, _P, _P, _I, _P, _P, _P),
     "srml_knn_lists_f32": (_P, _I, _L, _P, _P, _P, _I, _P, _P, _I, _I, _P, _P, _P),

@@ -1,0 +1,39 @@
+"""Seeded deterministic mode (SURVEY §5 "Sanitizers / deterministic mode").
+
+The fast reductions accumulate with fp64/fp32 atomics (block partials folded in arrival order), so
+their last bits can differ run to run. ``SRML_DETERMINISTIC=1`` (or ``set_deterministic(True)``,
+or the Spark conf ``spark.rocm.ml.deterministic=true`` forwarded to the workers as the env var)
+switches the affected kernels to fixed-order variants:
+
+* KMeans cluster sums -> label-sorted segment sums, one block per (cluster, column chunk), no
+  atomics (``srml_kmeans_segment_sums_*``);
+* Gram / covariance (PCA, LinearRegression normal equations) -> each row chunk stores its
+  partial tiles into a workspace (<= 64 chunks, <= 1 GB) folded in chunk order, instead of
+  fp64 atomics (same fp32-per-chunk / fp64-across-chunk precision);
+* fp64 GEMMs (``ops.dgemm``: X^T V, Krylov products) always fold split-K partials in index
+  order, deterministic in either mode.
+
+Not covered yet (their block partials still fold with atomics): the LogisticRegression fused
+loss/gradient kernels and the RandomForest regression histograms (classification histograms
+are integer-valued counts, exact in any order). Device RNG streams are counter-based and seeded
+(k-means|| sampling, bootstrap, k-means++ draws), so PCA, LinearRegression and KMeans fits on
+the same data and partitioning are bit-reproducible with the flag on.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+_override: Optional[bool] = None
+
+
+def deterministic() -> bool:
+    if _override is not None:
+        return _override
+    return os.environ.get("SRML_DETERMINISTIC", "0") == "1"
+
+
+def set_deterministic(flag: Optional[bool]) -> None:
+    """Force the mode on/off for this process (None: follow ``SRML_DETERMINISTIC``)."""
+    global _override
+    _override = flag

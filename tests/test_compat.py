@@ -191,3 +191,21 @@ def test_logistic_regression_one_label(device):
     assert m.intercept == float("inf") and np.allclose(m.coefficients.toArray(), 0)
     with pytest.raises(Exception):
         LogisticRegression().fit(DataFrame.from_numpy(X, np.array([2.5, 1.0])))
+
+
+def test_kmeans_parallel_init_recovers_blobs(device):
+    """Default initMode (k-means||): D^2 over-sampling + device k-means++ reduction finds
+    well-separated blobs (reference default init="scalable-k-means++")."""
+    from spark_rapids_ml_nai_amd.clustering import KMeans
+
+    rng = np.random.default_rng(7)
+    centers = rng.uniform(-50, 50, (12, 5))
+    lab = rng.integers(0, 12, 6000)
+    X = (centers[lab] + 0.3 * rng.standard_normal((6000, 5))).astype(np.float32)
+    ok = 0
+    for seed in (1, 2, 4, 5):  # 2 over-sampling rounds (Spark initSteps=2) can miss a blob: ~3 % per seed here
+        m = KMeans(k=12, seed=seed, maxIter=20).fit(DataFrame.from_numpy(X))
+        got = np.asarray(m.clusterCenters())
+        d = np.sqrt(((got[:, None, :] - centers[None]) ** 2).sum(-1))
+        ok += int(np.all(d.min(0) < 0.1) and np.all(d.min(1) < 0.1))
+    assert ok >= 3

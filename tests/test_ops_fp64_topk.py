@@ -1,0 +1,197 @@
+"""fp64-input kernels, deterministic reductions and the large-k kNN selection (GPU), each against
+a plain PyTorch fp64 reference of the same op; plus the host mirrors (CPU)."""
+import numpy as np
+import pytest
+import torch
+
+from spark_rapids_ml_nai_amd import ops
+from spark_rapids_ml_nai_amd.utils import determinism
+
+
+def _rand(m, n, dev, seed=0, dtype=torch.float64, shift=0.0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(m, n, generator=g, dtype=torch.float64) + shift).to(dtype).to(dev)
+
+
+# ---------------------------------------------------------------- fp64 inputs -------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,n,k", [(1, 3, 1), (1000, 77, 130), (5000, 300, 64), (4097, 16, 7)])
+def test_nearest_centroid_f64(gpu_device, m, n, k):
+    X = _rand(m, n, gpu_device, seed=1)
+    C = _rand(k, n, gpu_device, seed=2)
+    lab, d2 = ops.nearest_centroid(X, C)
+    Xh, Ch = X.cpu(), C.cpu()
+    D = torch.cdist(Xh, Ch) ** 2
+    ref_d, ref_l = D.min(1)
+    torch.testing.assert_close(d2.cpu().double(), ref_d, rtol=1e-5, atol=1e-6)
+    # labels agree except at exact fp64 near-ties
+    got = D.gather(1, lab.cpu().long().view(-1, 1)).view(-1)
+    assert torch.all(got <= ref_d + 1e-9 * ref_d.abs().clamp_min(1))
+
+
+@pytest.mark.gpu
+def test_row_sqnorm_f64(gpu_device):
+    X = _rand(3001, 129, gpu_device, seed=3)
+    out = ops.row_sqnorm(X)
+    assert out.dtype == torch.float64
+    torch.testing.assert_close(out.cpu(), (X.cpu() ** 2).sum(1), rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K,ta,tb", [(3000, 19, 3000, False, False), (76, 19, 3000, True, False),
+                                         (300, 4, 100000, True, False), (64, 64, 64, False, True)])
+def test_dgemm_splitk_deterministic(gpu_device, M, N, K, ta, tb):
+    A = _rand(K, M, gpu_device, seed=4) if ta else _rand(M, K, gpu_device, seed=4)
+    B = _rand(N, K, gpu_device, seed=5) if tb else _rand(K, N, gpu_device, seed=5)
+    C0 = _rand(M, N, gpu_device, seed=6)
+    out1 = ops.dgemm(A, B, ta=ta, tb=tb, alpha=0.5, beta=2.0, out=C0.clone())
+    out2 = ops.dgemm(A, B, ta=ta, tb=tb, alpha=0.5, beta=2.0, out=C0.clone())
+    a = A.cpu().T if ta else A.cpu()
+    b = B.cpu().T if tb else B.cpu()
+    ref = 0.5 * (a @ b) + 2.0 * C0.cpu()
+    torch.testing.assert_close(out1.cpu(), ref, rtol=1e-10, atol=1e-9)
+    assert torch.equal(out1, out2)  # split-K folds in index order: bitwise reproducible
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [3, 40])
+def test_xw_f64_and_wide_f32(gpu_device, k):
+    X = _rand(2000, 300, gpu_device, seed=7)
+    W = _rand(300, k, gpu_device, seed=8)
+    b = _rand(1, k, gpu_device, seed=9).view(-1)
+    out = ops.xw(X, W, b)
+    assert out.dtype == torch.float64
+    ref = X.cpu() @ W.cpu() + b.cpu()
+    torch.testing.assert_close(out.cpu(), ref, rtol=1e-10, atol=1e-9)
+    out32 = ops.xw(X.float(), W.float(), b.float())
+    torch.testing.assert_close(out32.cpu().double(), ref, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.gpu
+def test_xtv_f64(gpu_device):
+    X = _rand(50000, 200, gpu_device, seed=10)
+    V = _rand(50000, 3, gpu_device, seed=11)
+    out = ops.xtv(X, V)
+    torch.testing.assert_close(out.cpu(), X.cpu().T @ V.cpu(), rtol=1e-10, atol=1e-8)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_cluster_sums_segments(gpu_device, dtype, monkeypatch):
+    monkeypatch.setenv("SRML_DETERMINISTIC", "1")
+    X = _rand(20000, 300, gpu_device, seed=12, dtype=dtype)
+    g = torch.Generator().manual_seed(0)
+    lab = torch.randint(0, 37, (20000,), generator=g).to(torch.int32)
+    lab[lab == 5] = 6  # an empty cluster
+    s1, c1 = ops.cluster_sums(X, lab.to(gpu_device), 37)
+    s2, _ = ops.cluster_sums(X, lab.to(gpu_device), 37)
+    ref = torch.zeros(37, 300, dtype=torch.float64).index_add_(0, lab.long(), X.cpu().double())
+    torch.testing.assert_close(s1.cpu(), ref, rtol=1e-10, atol=1e-9)
+    assert torch.equal(s1, s2)
+    assert torch.equal(c1.cpu(), torch.bincount(lab.long(), minlength=37))
+
+
+@pytest.mark.gpu
+def test_gram_deterministic(gpu_device, monkeypatch):
+    monkeypatch.setenv("SRML_DETERMINISTIC", "1")
+    X = _rand(100000, 200, gpu_device, seed=13, dtype=torch.float32, shift=1.0)
+    G1 = ops.gram(X)
+    G2 = ops.gram(X)
+    assert torch.equal(G1, G2)
+    ref = X.cpu().double().T @ X.cpu().double()
+    assert ((G1.cpu() - ref).abs().max() / ref.abs().max()).item() < 2e-6
+
+
+@pytest.mark.gpu
+def test_kmeans_fp64_fit_matches_fp32(gpu_device):
+    from spark_rapids_ml_nai_amd.models.kmeans import kmeans_fit
+    from spark_rapids_ml_nai_amd.parallel.context import PartitionDescriptor, WorkerContext
+
+    rng = np.random.default_rng(0)
+    centers = rng.normal(size=(5, 20)) * 10
+    Xh = np.concatenate([c + rng.normal(size=(400, 20)) for c in centers])
+    ctx = WorkerContext.single(gpu_device)
+    desc = PartitionDescriptor.build(ctx, Xh.shape[0], Xh.shape[1])
+    r64 = kmeans_fit(torch.from_numpy(Xh).to(gpu_device), desc, ctx, 5, 20, 1e-4, 1)
+    r32 = kmeans_fit(torch.from_numpy(Xh).float().to(gpu_device), desc, ctx, 5, 20, 1e-4, 1)
+    c64 = np.sort(r64["cluster_centers_"][:, 0])
+    c32 = np.sort(r32["cluster_centers_"][:, 0])
+    np.testing.assert_allclose(c64, c32, rtol=1e-4, atol=1e-4)
+
+
+# ---------------------------------------------------------------- top-k / large-k kNN ---------
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows,L,k", [(3, 10, 20), (7, 5000, 100), (5, 70000, 1024), (4, 1000, 1)])
+def test_topk_rows_matches_sort(gpu_device, rows, L, k):
+    g = torch.Generator().manual_seed(1)
+    v = torch.randn(rows, L, generator=g)
+    v[:, ::7] = 0.25  # heavy ties at one value
+    gv, gi = ops.topk_rows(v.to(gpu_device), k, id_base=100)
+    cv, ci = ops.topk_rows(v, k, id_base=100)
+    torch.testing.assert_close(gv.cpu(), cv)
+    assert torch.equal(gi.cpu(), ci)
+
+
+@pytest.mark.gpu
+def test_topk_rows_with_ids_multi_slice(gpu_device):
+    g = torch.Generator().manual_seed(2)
+    v = torch.randn(6, 9000, generator=g)
+    ids = torch.randperm(6 * 9000, generator=g).view(6, 9000)
+    gv, gi = ops.topk_rows(v.to(gpu_device), 300, ids=ids.to(gpu_device), slice_len=1000)
+    cv, ci = ops.topk_rows(v, 300, ids=ids)
+    torch.testing.assert_close(gv.cpu(), cv)
+    assert torch.equal(gi.cpu(), ci)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mq,mi,n,k", [(300, 5000, 64, 100), (129, 3000, 37, 1024), (50, 800, 16, 200),
+                                         (60, 20000, 16, 100)])
+def test_knn_large_k(gpu_device, mq, mi, n, k, monkeypatch):
+    monkeypatch.setattr(ops, "_TOPK_SLICE", 1024)  # several slices and item chunks at test sizes
+    Q = _rand(mq, n, gpu_device, seed=20, dtype=torch.float32)
+    I = _rand(mi, n, gpu_device, seed=21, dtype=torch.float32)
+    d, i = ops.knn(Q, I, k, id_offset=7)
+    kk = min(k, mi)
+    ref = torch.cdist(Q.cpu().double(), I.cpu().double()) ** 2
+    rv, _ = torch.sort(ref, 1)
+    torch.testing.assert_close(d.cpu().double(), rv[:, :kk], rtol=1e-4, atol=1e-3)
+    got = ref.gather(1, i.cpu() - 7)
+    torch.testing.assert_close(got, rv[:, :kk], rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.gpu
+def test_knn_small_k_many_slices_native_merge(gpu_device):
+    Q = _rand(40, 32, gpu_device, seed=22, dtype=torch.float32)
+    I = _rand(60000, 32, gpu_device, seed=23, dtype=torch.float32)
+    d, i = ops.knn(Q, I, 10)
+    ref = torch.cdist(Q.cpu().double(), I.cpu().double()) ** 2
+    rv, _ = torch.sort(ref, 1)
+    torch.testing.assert_close(d.cpu().double(), rv[:, :10], rtol=1e-4, atol=1e-3)
+
+
+# ---------------------------------------------------------------- CPU mirrors ----------------
+def test_topk_rows_cpu_ties_and_padding():
+    v = torch.tensor([[3.0, 1.0, 1.0, 2.0], [0.0, 0.0, 0.0, 0.0]])
+    out_v, out_i = ops.topk_rows(v, 6, id_base=10)
+    assert out_i[0, :4].tolist() == [11, 12, 13, 10]
+    assert out_i[1, :4].tolist() == [10, 11, 12, 13]
+    assert out_i[0, 4:].tolist() == [-1, -1] and torch.isinf(out_v[0, 4:]).all()
+
+
+def test_determinism_flag(monkeypatch):
+    monkeypatch.delenv("SRML_DETERMINISTIC", raising=False)
+    assert not determinism.deterministic()
+    monkeypatch.setenv("SRML_DETERMINISTIC", "1")
+    assert determinism.deterministic()
+    determinism.set_deterministic(False)
+    try:
+        assert not determinism.deterministic()
+    finally:
+        determinism.set_deterministic(None)
+
+
+def test_dgemm_cpu_matches_torch():
+    A = _rand(50, 30, "cpu", seed=1)
+    B = _rand(50, 20, "cpu", seed=2)
+    torch.testing.assert_close(ops.dgemm(A, B, ta=True), A.T @ B)
+    assert ops._dgemm_splits(3000, 19, 3000, 47) > 1 and ops._dgemm_splits(3000, 3000, 3000, 2209) == 1

@@ -585,3 +585,34 @@ def test_parts_to_device(gpu_device, mode, src_dtype, dst, monkeypatch):
     got = ingest.parts_to_device(parts, gpu_device, dst, mode=mode).cpu()
     ref = torch.from_numpy(np.concatenate(parts, 0).astype(np.float32 if dst == torch.float32 else np.float64))
     assert got.dtype == dst and torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("nc,k", [(300, 20), (4001, 1000), (8000, 64)])
+def test_kmeanspp_gram_matches_host(gpu_device, nc, k):
+    """Device k-means++ seeding draws the same centres as the numpy reference (same uniforms)."""
+    g = torch.Generator().manual_seed(nc)
+    C = torch.randn(nc, 32, generator=g, dtype=torch.float64) * torch.rand(nc, 1, generator=g, dtype=torch.float64)
+    w = torch.randint(1, 50, (nc,), generator=g).double()
+    G = C @ C.T
+    ref = ops.kmeanspp_gram(G, w, k, 1234)
+    got = ops.kmeanspp_gram(G.to(gpu_device), w.to(gpu_device), k, 1234).cpu()
+    assert got[0] == ref[0]
+    assert (got == ref).float().mean().item() > 0.95  # prefix-sum order may flip a boundary draw
+    assert len(set(got.tolist())) == k  # D^2 sampling never re-picks a chosen candidate
+
+
+@pytest.mark.parametrize("m,n,k", [(1024, 3000, 257), (70000, 200, 600)])
+def test_nearest_centroid_split_tiled_approx(gpu_device, m, n, k):
+    """3-product variant (k-means|| passes): distances within ~1e-4 relative of fp64, and the
+    chosen centre is within that tolerance of the true nearest."""
+    X = _rand(m, n, gpu_device, seed=13)
+    C = _rand(k, n, gpu_device, seed=14)
+    xnorm = ops.row_sqnorm(X)
+    XP = ops.split_bf16x3(X, tiled=True)
+    lab, d2 = ops.nearest_centroid_split(XP, m, C, xnorm, approx=True)
+    D = torch.cdist(X.double(), C.double()) ** 2
+    ref = D.min(1).values
+    got = D.gather(1, lab.long().view(-1, 1)).view(-1)
+    scale = (xnorm.double().view(-1) + (C.double() ** 2).sum(1).max()).max().item()
+    assert (got - ref).abs().max().item() <= 1e-4 * scale
+    assert (d2.double() - ref).abs().max().item() <= 1e-4 * scale

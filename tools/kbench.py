@@ -157,16 +157,17 @@ def main():
         y = torch.randn(m_, device=dev, generator=g)
         nf = max(1, n_ // 3)
         feats = torch.randperm(n_, device=dev, generator=g)[:nf].int().view(1, -1).contiguous()
-        nfc = (nf + ops.rf_hist_fb(128, S, reg) - 1) // ops.rf_hist_fb(128, S, reg)
         rows = idx.shape[0]
-        rpi = int(min(65536, max(4096, rows * nfc // 8192)))
-        rpi = (rpi + 511) // 512 * 512
-        it = []
-        for r0 in range(0, rows, rpi):
-            for fc in range(nfc):
-                it.append((0, r0, min(rows, r0 + rpi), fc))
-        items = torch.tensor(np.array(it, dtype=np.int32), device=dev)
         for reg, S, nm in ((True, 2, "rf_hist_reg_root"), (False, 3, "rf_hist_clf3_root")):
+            fb = ops.rf_hist_fb(128, S, reg)
+            nfc = (nf + fb - 1) // fb
+            rpi = int(min(65536, max(4096, rows * nfc // 8192)))
+            rpi = (rpi + 511) // 512 * 512
+            it = []
+            for r0 in range(0, rows, rpi):
+                for fc in range(nfc):
+                    it.append((0, r0, min(rows, r0 + rpi), fc))
+            items = torch.tensor(np.array(it, dtype=np.int32), device=dev)
             yy = y if reg else torch.randint(0, 3, (m_,), device=dev, generator=g).float()
             t = timeit(lambda: ops.rf_hist(bins, idx, yy, w, items, feats, 1, 128, S, reg), 3)
             res[nm] = {"ms": t, "Gpairs/s": rows * nf / t / 1e6}
