@@ -60,6 +60,8 @@ def main() -> None:
                     help="pinned: each rank's shard is one page-locked buffer (headline); batches: pageable "
                          "Arrow record batches of --batch-rows rows, as Spark's mapInArrow delivers them")
     ap.add_argument("--batch-rows", type=int, default=20000)
+    ap.add_argument("--no-transform", action="store_true",
+                    help="skip the per-workload transform timing (outside the timed fit steps)")
     ap.add_argument("--dump-models", type=str, default=None,
                     help="rank 0 saves each workload's last fitted model under this directory")
     args = ap.parse_args()
@@ -157,6 +159,26 @@ def main() -> None:
                 "phases": {k: round(v, 4) for k, v in getattr(model, "_fit_timings", {}).items()},
                 "evidence": model_evidence(name, model),
             }
+            if not args.no_transform:
+                # reference BenchmarkBase times transform separately (benchmark/base.py:221-271):
+                # one pass of model.transform over this rank's rows (H2D + kernels + D2H of the
+                # output columns), outside the fit steps; failures are recorded, never fatal
+                try:
+                    barrier_sync()
+                    t1 = time.perf_counter()
+                    out = model.transform(df)
+                    nout = out.count()
+                    barrier_sync()
+                    tr = time.perf_counter() - t1
+                    if world > 1:
+                        t = torch.tensor([tr], dtype=torch.float64, device=device)
+                        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                        tr = float(t.item())
+                    results[name]["transform_s"] = round(tr, 4)
+                    results[name]["transform_rows"] = int(nout)
+                    del out
+                except Exception as e:  # noqa: BLE001
+                    results[name]["transform_error"] = repr(e)[:200]
             if args.dump_models and rank == 0:
                 model.write().overwrite().save(os.path.join(args.dump_models, name))
             del df, Xh, yh, model

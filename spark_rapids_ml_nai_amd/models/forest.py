@@ -456,19 +456,33 @@ def pack_forest(trees: List[Dict[str, Any]], S: int, device: torch.device) -> Di
         base += nn_
     cat = lambda parts, dt: np.concatenate(parts).astype(dt) if parts else np.zeros(0, dt)  # noqa: E731
     i32 = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.int32)).to(device)  # noqa: E731
+    f_all, thr_all = cat(feats, np.int32), cat(thr, np.float32)
+    l_all, r_all = cat(left, np.int32), cat(right, np.int32)
+    voff = (np.arange(base, dtype=np.int64) * S).astype(np.int32)
+    # 16-B node records for the wave-per-row kernel: splits {feature, left, right, thr bits},
+    # leaves {-1, value offset, leaf id within its tree, 0}
+    local = np.concatenate([np.arange(len(f), dtype=np.int32) for f in feats]) if feats else np.zeros(0, np.int32)
+    leaf = f_all < 0
+    nodes = np.zeros((base, 4), dtype=np.int32)
+    nodes[:, 0] = np.where(leaf, -1, f_all)
+    nodes[:, 1] = np.where(leaf, voff, l_all)
+    nodes[:, 2] = np.where(leaf, local, r_all)
+    nodes[:, 3] = np.where(leaf, 0, thr_all.view(np.int32))
     return {
-        "roots": i32(np.asarray(roots, dtype=np.int32)), "feature": i32(cat(feats, np.int32)),
-        "threshold": torch.from_numpy(cat(thr, np.float32)).to(device),
-        "left": i32(cat(left, np.int32)), "right": i32(cat(right, np.int32)),
-        "value_off": i32(np.arange(base, dtype=np.int64) * S),
+        "roots": i32(np.asarray(roots, dtype=np.int32)), "feature": i32(f_all),
+        "threshold": torch.from_numpy(thr_all).to(device),
+        "left": i32(l_all), "right": i32(r_all),
+        "value_off": i32(voff),
         "values": torch.from_numpy(cat(vals, np.float32)).to(device),
+        "nodes": i32(nodes),
     }
 
 
 def forest_predict(X: torch.Tensor, packed: Dict[str, torch.Tensor], S: int, want_leaves: bool = False
                    ) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
     return ops.rf_predict(X.float(), packed["roots"], packed["feature"], packed["threshold"], packed["left"],
-                          packed["right"], packed["value_off"], packed["values"], S, want_leaves)
+                          packed["right"], packed["value_off"], packed["values"], S, want_leaves,
+                          nodes=packed.get("nodes"))
 
 
 def feature_importances(trees: List[Dict[str, Any]], n: int) -> np.ndarray:

@@ -72,7 +72,8 @@ def _min_norm_solve(A: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     w, V = ops.syevj(A) if A.is_cuda and A.shape[0] <= 4096 else torch.linalg.eigh(A)
     tol = max(float(w.max()), 0.0) * A.shape[0] * float(np.finfo(np.float64).eps)
     inv = torch.where(w > tol, 1.0 / torch.where(w > tol, w, torch.ones_like(w)), torch.zeros_like(w))
-    return V @ (inv * (V.T @ b))
+    Vtb = ops.dgemm(V, b.view(-1, 1), ta=True).view(-1)
+    return ops.dgemm(V, (inv * Vtb).view(-1, 1)).view(-1)
 
 
 def lsq_solve(st: LSQStats, reg: float, l1_ratio: float, fit_intercept: bool, standardization: bool,
@@ -109,7 +110,7 @@ def lsq_solve(st: LSQStats, reg: float, l1_ratio: float, fit_intercept: bool, st
         wt, _ = ops.cd_gram(A, b, l1, l2, max_iter, tol)
     wt = wt * keep
     w = wt * ystd / safe
-    intercept = float(st.ybar - float(st.xbar @ w)) if fit_intercept else 0.0
+    intercept = float(st.ybar - float((st.xbar * w).sum())) if fit_intercept else 0.0
     return {"coef_": w.cpu().tolist(), "intercept_": intercept}
 
 

@@ -3,13 +3,16 @@
 Semantics follow umap-learn / cuML UMAP (what the reference calls on one GPU, ``umap.py:924-958``):
 * kNN graph: exact, from the fused MFMA distance + top-k kernel (``ops.knn``), self included;
 * ``smooth_knn_dist`` (per-row bisection for sigma, rho = nearest non-zero distance with
-  ``local_connectivity``) vectorised over all rows on device;
-* membership strengths exp(-(d - rho) / sigma) and the fuzzy union A + Aᵀ - A∘Aᵀ
-  (``set_op_mix_ratio`` blends with the intersection) via one device sort of edge keys;
+  ``local_connectivity``) and the membership strengths exp(-(d - rho) / sigma) fused in one
+  thread-per-row kernel (``ops.umap_smooth_knn``); torch reference on CPU;
+* fuzzy union A + Aᵀ - A∘Aᵀ (``set_op_mix_ratio`` blends with the intersection): one thread per
+  kNN edge finds the reverse edge in the neighbour's row and emits each union entry exactly
+  once (``ops.umap_fuzzy_union_knn``), then one device sort of the edge keys;
 * optional supervised intersection with a categorical target (far_dist 5, unknown 1) followed
   by ``reset_local_connectivity``;
-* spectral init: top eigenvectors of D^-1/2 A D^-1/2 by block subspace iteration with sparse
-  CSR products on device (host ``eigsh`` for small graphs), scaled like umap-learn;
+* spectral init on the device for every n: top eigenvectors of D^-1/2 A D^-1/2 by the dense
+  parallel-Jacobi kernel (n <= 2048) or block subspace iteration with the CSR SpMM kernel and
+  split-K fp64 GEMMs (larger n); host ``eigsh`` only on CPU; scaled like umap-learn;
 * SGD: ``srml_umap_epoch`` (edge-parallel HIP kernel, hash RNG negative sampling), alpha decays
   linearly, edges below max_w / n_epochs dropped, epochs_per_sample = n_epochs / (n_epochs·w/max_w);
 * transform: kNN to the training data, local_connectivity - 1, l1-normalised weighted init
@@ -28,6 +31,7 @@ from .. import ops
 
 SMOOTH_K_TOLERANCE = 1e-5
 MIN_K_DIST_SCALE = 1e-3
+SPECTRAL_DENSE_N = 2048  # device Jacobi on the dense normalised adjacency up to this many vertices
 
 
 def find_ab_params(spread: float, min_dist: float) -> Tuple[float, float]:
@@ -197,7 +201,7 @@ def _cholqr2(Y: torch.Tensor) -> torch.Tensor:
         if d.min() <= 1e-6 * d.max():
             return torch.linalg.qr(Y)[0]
         Rinv = torch.from_numpy(np.linalg.solve(L, np.eye(L.shape[0])).T.copy()).to(Y.device)
-        W = (Wd @ Rinv).to(Y.dtype)
+        W = ops.dgemm(Wd, Rinv).to(Y.dtype)
     return W
 
 
@@ -225,18 +229,35 @@ def _spectral_device(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor,
         if it % 5 == 4 or it == iters - 1:
             Y = _cholqr2(Y)
     Z = 0.5 * (ops.csr_spmm(M, Y) + Y)
-    # Y^T Z over row chunks: library GEMMs with K in the millions pick non-split-K tiles
-    T = sum(Y[i: i + 65536].double().T @ Z[i: i + 65536].double() for i in range(0, n, 65536))
-    w, V = np.linalg.eigh(T.double().cpu().numpy())
+    # Y^T Z: K = n rows in the millions -> the split-K fp64 MFMA GEMM (ordered fold)
+    Yd = Y.double().contiguous()
+    T = ops.dgemm(Yd, Z.double().contiguous(), ta=True)
+    w, V = np.linalg.eigh(T.cpu().numpy())
     order = np.argsort(w)[::-1][1: dim + 1].copy()
-    return (Y.double() @ torch.from_numpy(V[:, order]).to(dev)).float()
+    return ops.dgemm(Yd, torch.from_numpy(np.ascontiguousarray(V[:, order])).to(dev)).float()
+
+
+def _spectral_dense_device(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n: int, dim: int) -> torch.Tensor:
+    """Small graphs on the device: dense D^-1/2 A D^-1/2 and all its eigenpairs by the parallel
+    Jacobi kernel (``ops.syevj``); the top non-trivial eigenvectors of M are the smallest
+    non-trivial ones of the normalised Laplacian (umap-learn's spectral_layout)."""
+    dev = vals.device
+    deg = torch.zeros(n, dtype=torch.float64, device=dev).index_add_(0, rows.long(), vals.double())
+    dinv = 1.0 / torch.sqrt(deg.clamp_min(1e-30))
+    M = torch.zeros((n, n), dtype=torch.float64, device=dev)
+    M.index_put_((rows.long(), cols.long()), dinv[rows.long()] * vals.double() * dinv[cols.long()], accumulate=True)
+    M = 0.5 * (M + M.T)
+    w, V = ops.syevj(M)  # descending
+    return V[:, 1: dim + 1].float().contiguous()
 
 
 def spectral_init(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n: int, dim: int, seed: int) -> torch.Tensor:
     dev = vals.device
-    if dev.type != "cuda" or n <= 20000:
+    if dev.type != "cuda":
         coords = torch.from_numpy(_spectral_host(rows.cpu().numpy(), cols.cpu().numpy(), vals.cpu().numpy(), n, dim,
                                                  seed)).float().to(dev)
+    elif n <= SPECTRAL_DENSE_N:
+        coords = _spectral_dense_device(rows, cols, vals, n, dim)
     else:
         coords = _spectral_device(rows, cols, vals, n, dim, seed)
     expansion = 10.0 / coords.abs().max().clamp_min(1e-30)
@@ -332,13 +353,18 @@ def umap_fit(X: torch.Tensor, params: Dict[str, Any], y: Optional[torch.Tensor] 
             dist = 0.5 * dist * dist  # 1 - cos for unit rows
         elif metric == "sqeuclidean":
             dist = dist * dist
-    sigma, rho = smooth_knn_dist(dist, float(k), local_connectivity=float(params.get("local_connectivity", 1.0)))
-    self_rows = torch.arange(N, device=X.device)
-    w = membership_strengths(idx, dist, sigma, rho, self_rows)
-    rows = self_rows.view(-1, 1).expand_as(idx).reshape(-1)
-    cols = idx.reshape(-1)
-    rows, cols, vals = fuzzy_union(rows, cols.clamp_min(0), w.reshape(-1), N,
-                                   float(params.get("set_op_mix_ratio", 1.0)))
+    lc = float(params.get("local_connectivity", 1.0))
+    mix = float(params.get("set_op_mix_ratio", 1.0))
+    if X.is_cuda:  # fused kernels: smooth_knn_dist + membership, then the kNN-structured union
+        _, _, w = ops.umap_smooth_knn(dist, idx, float(k), local_connectivity=lc, self_rows=True)
+        rows, cols, vals = ops.umap_fuzzy_union_knn(idx, w, mix)
+    else:
+        sigma, rho = smooth_knn_dist(dist, float(k), local_connectivity=lc)
+        self_rows = torch.arange(N, device=X.device)
+        w = membership_strengths(idx, dist, sigma, rho, self_rows)
+        rows = self_rows.view(-1, 1).expand_as(idx).reshape(-1)
+        cols = idx.reshape(-1)
+        rows, cols, vals = fuzzy_union(rows, cols.clamp_min(0), w.reshape(-1), N, mix)
     if y is not None:
         yy = y.to(X.device).long().view(-1)
         rows, cols, vals = categorical_intersection(rows, cols, vals, yy, N)
@@ -385,8 +411,11 @@ def umap_transform(X: torch.Tensor, raw: torch.Tensor, embedding: torch.Tensor, 
     elif metric == "sqeuclidean":
         dist = dist * dist
     adj_lc = max(0.0, float(params.get("local_connectivity", 1.0)) - 1.0)
-    sigma, rho = smooth_knn_dist(dist, float(k), local_connectivity=adj_lc)
-    w = membership_strengths(idx, dist, sigma, rho)
+    if X.is_cuda:
+        _, _, w = ops.umap_smooth_knn(dist, idx, float(k), local_connectivity=adj_lc, self_rows=False)
+    else:
+        sigma, rho = smooth_knn_dist(dist, float(k), local_connectivity=adj_lc)
+        w = membership_strengths(idx, dist, sigma, rho)
     wn = w / w.sum(1, keepdim=True).clamp_min(1e-30)
     emb_tr = embedding.float().contiguous()
     init = (wn.unsqueeze(-1) * emb_tr[idx.clamp_min(0)]).sum(1).contiguous()

@@ -4,6 +4,7 @@ the numerics oracle in the kernel tests).
 """
 from __future__ import annotations
 
+import math
 from typing import Dict, Optional, Tuple
 
 import numpy as np
@@ -709,8 +710,10 @@ def rf_node_stats(idx: torch.Tensor, wpos: torch.Tensor, label: torch.Tensor, bo
 
 def rf_predict(X: torch.Tensor, roots: torch.Tensor, feature: torch.Tensor, threshold: torch.Tensor,
                left: torch.Tensor, right: torch.Tensor, value_off: torch.Tensor, values: torch.Tensor, S: int,
-               want_leaves: bool = False) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
-    """Sum over trees of leaf value vectors (rows, S) (+ per-tree leaf ids)."""
+               want_leaves: bool = False, nodes: Optional[torch.Tensor] = None
+               ) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """Sum over trees of leaf value vectors (rows, S) (+ per-tree leaf ids). Device with packed
+    16-B ``nodes`` (``pack_forest``): wave-per-row kernel, trees over the lanes."""
     m = X.shape[0]
     T = roots.shape[0]
     if not X.is_cuda or X.dtype != torch.float32 or S > 32:
@@ -734,9 +737,15 @@ def rf_predict(X: torch.Tensor, roots: torch.Tensor, feature: torch.Tensor, thre
             off = value_off[node].long()
             out += values[off.view(-1, 1) + torch.arange(S, device=X.device).view(1, -1)]
         return out, leaves
-    X = _c(X)
+    X = X if X.stride(1) == 1 else X.contiguous()
     out = torch.empty((m, S), dtype=torch.float32, device=X.device)
     leaves = torch.empty((m, T), dtype=torch.int32, device=X.device) if want_leaves else None
+    if nodes is not None and nodes.is_cuda:
+        native.call("srml_rf_predict_nodes2", X.data_ptr(), m, X.stride(0), X.shape[1], _c(nodes).data_ptr(),
+                    roots.data_ptr(), T,
+                    values.data_ptr(), S, out.data_ptr(), leaves.data_ptr() if leaves is not None else None,
+                    native.stream(X.device))
+        return out, leaves
     native.call("srml_rf_predict", X.data_ptr(), m, X.stride(0), roots.data_ptr(), T, feature.data_ptr(),
                 threshold.data_ptr(), left.data_ptr(), right.data_ptr(), value_off.data_ptr(), values.data_ptr(), S,
                 out.data_ptr(), leaves.data_ptr() if leaves is not None else None, native.stream(X.device))
@@ -1080,6 +1089,41 @@ def uf_compress(parent: torch.Tensor) -> None:
 # ------------------------------------------------------------------------------------------
 # UMAP: one SGD epoch over the fuzzy-graph edges
 # ------------------------------------------------------------------------------------------
+def umap_smooth_knn(dist: torch.Tensor, idx: torch.Tensor, k: float, local_connectivity: float = 1.0,
+                    bandwidth: float = 1.0, self_rows: bool = True, n_iter: int = 64
+                    ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Device smooth_knn_dist + membership strengths of a kNN graph (dist fp32, idx int64, [m, kk]):
+    (sigma fp64 [m], rho fp64 [m], w fp32 [m, kk]); ``self_rows``: neighbour == row -> weight 0."""
+    m, kk = dist.shape
+    d = _c(dist.float())
+    ix = _c(idx.long())
+    sigma = torch.empty(m, dtype=torch.float64, device=d.device)
+    rho = torch.empty(m, dtype=torch.float64, device=d.device)
+    w = torch.empty((m, kk), dtype=torch.float32, device=d.device)
+    mean_all = d.double().mean().view(1)
+    native.call("srml_umap_smooth_knn", d.data_ptr(), ix.data_ptr(), m, kk, kk, float(math.log2(k) * bandwidth),
+                float(local_connectivity), int(n_iter), mean_all.data_ptr(), int(bool(self_rows)), sigma.data_ptr(),
+                rho.data_ptr(), w.data_ptr(), native.stream(d.device))
+    return sigma, rho, w
+
+
+def umap_fuzzy_union_knn(idx: torch.Tensor, w: torch.Tensor, mix: float = 1.0
+                         ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Fuzzy union of the kNN membership matrix A (row i: neighbours idx[i], weights w[i]):
+    mix·(A + Aᵀ - A∘Aᵀ) + (1 - mix)·A∘Aᵀ as (rows, cols, vals) sorted by (row, col)."""
+    m, kk = idx.shape
+    ix = _c(idx.long())
+    wv = _c(w.float())
+    keys = torch.empty(2 * m * kk, dtype=torch.int64, device=ix.device)
+    vals = torch.empty(2 * m * kk, dtype=torch.float32, device=ix.device)
+    native.call("srml_umap_fuzzy_union_knn", ix.data_ptr(), wv.data_ptr(), m, kk, kk, float(mix), keys.data_ptr(),
+                vals.data_ptr(), native.stream(ix.device))
+    keep = keys >= 0
+    keys, vals = keys[keep], vals[keep]
+    keys, order = torch.sort(keys)
+    return keys // m, keys % m, vals[order]
+
+
 def umap_epoch(head: torch.Tensor, tail: torch.Tensor, eps: torch.Tensor, next_sample: torch.Tensor,
                next_neg: torch.Tensor, eps_neg: torch.Tensor, emb_head: torch.Tensor, emb_tail: torch.Tensor,
                a: float, b: float, gamma: float, alpha: float, epoch: int, move_other: bool, seed: int) -> None:

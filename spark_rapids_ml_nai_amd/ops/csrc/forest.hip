@@ -18,8 +18,14 @@
 //    child), then a block arg-max (ties -> lowest feature slot, lowest bin).
 //  * srml_rf_route — child key per row (2*slot + goes_right; dropped rows -> sentinel) for the
 //    stable re-partition of the row-index array.
-//  * srml_rf_predict — FIL-equivalent inference on raw fp32 rows: one thread per row walks every
-//    tree (nodes in breadth-first flat arrays) and accumulates leaf vectors.
+//  * srml_rf_predict_nodes2 — FIL-equivalent inference on raw fp32 rows, wave per row with the
+//    trees spread over the 64 lanes. n <= 4096: the wave first streams its row into its own LDS
+//    slice with coalesced 16-B loads, so the ~depth x trees feature gathers hit LDS and HBM sees X
+//    exactly once; wider rows gather from global (all lanes on one row's lines at once, L1/L2
+//    hits after the first touch). Nodes are one 16-B load each ({feature, left, right,
+//    threshold}, breadth-first, L2-resident); per-lane class sums folded with DPP wave
+//    reductions (fixed order: deterministic). srml_rf_predict (thread per row) stays for the
+//    C ABI.
 #include "common.h"
 
 namespace {
@@ -616,5 +622,128 @@ SRML_API int srml_rf_predict(const float* X, long m, long ld, const int* roots, 
   if (S > 32) return -7;
   hipLaunchKernelGGL(rf_predict_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream, X, m, ld, roots,
                      ntrees, feature, threshold, left, right, value_off, values, S, out, leaves);
+  return srml_status();
+}
+
+// node: {feature, left, right, threshold bits}; leaf: {-1, value offset, leaf id within its tree, 0}
+template <int SV>
+__global__ __launch_bounds__(256) void rf_predict_wave_kernel(const float* __restrict__ X, long m, long ld,
+                                                              const int4* __restrict__ nodes,
+                                                              const int* __restrict__ roots, int ntrees,
+                                                              const float* __restrict__ values, int S,
+                                                              float* __restrict__ out, int* __restrict__ leaves) {
+  const int lane = threadIdx.x & 63;
+  const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const long nw = (long)gridDim.x * 4;
+  for (long r = wave; r < m; r += nw) {
+    const float* row = X + r * ld;
+    float acc[SV];
+#pragma unroll
+    for (int c = 0; c < SV; ++c) acc[c] = 0.f;
+    for (int t = lane; t < ntrees; t += 64) {
+      int4 nd = nodes[roots[t]];
+      while (nd.x >= 0) {
+        const float xv = row[nd.x];
+        nd = nodes[xv <= __int_as_float(nd.w) ? nd.y : nd.z];
+      }
+      if (leaves) leaves[r * ntrees + t] = nd.z;
+      const float* v = values + nd.y;
+#pragma unroll
+      for (int c = 0; c < SV; ++c)
+        if (c < S) acc[c] += v[c];
+    }
+    float mine = 0.f;
+#pragma unroll
+    for (int c = 0; c < SV; ++c) {
+      const float tot = wave_sum(acc[c]);
+      if (c == lane) mine = tot;
+    }
+    if (lane < S) out[r * S + lane] = mine;
+  }
+}
+
+// Rows staged in LDS (n <= RF_LDS_N): each wave streams its row with coalesced 16-B loads into
+// its own LDS slice (12 KB at n = 3000), then the lanes' tree walks gather from LDS instead of
+// issuing one scattered global load per level; HBM traffic is exactly X once, at full width.
+constexpr int RF_LDS_N = 4096;
+
+template <int SV>
+__global__ __launch_bounds__(256) void rf_predict_lds_kernel(const float* __restrict__ X, long m, long ld, int n,
+                                                             const int4* __restrict__ nodes,
+                                                             const int* __restrict__ roots, int ntrees,
+                                                             const float* __restrict__ values, int S,
+                                                             float* __restrict__ out, int* __restrict__ leaves) {
+  extern __shared__ __attribute__((aligned(16))) float srow_all[];  // [4][npad]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int npad = (n + 3) & ~3;
+  float* srow = srow_all + wid * npad;
+  const long nw = (long)gridDim.x * 4;
+  for (long r0 = (long)blockIdx.x * 4; r0 < m; r0 += nw) {
+    const long r = r0 + wid;
+    const bool active = r < m;
+    if (active) {
+      const float* row = X + r * ld;
+      for (int c = lane * 4; c < npad; c += 256) *reinterpret_cast<floatx4*>(&srow[c]) = *reinterpret_cast<const floatx4*>(row + c);
+    }
+    __syncthreads();
+    if (active) {
+      float acc[SV];
+#pragma unroll
+      for (int c = 0; c < SV; ++c) acc[c] = 0.f;
+      for (int t = lane; t < ntrees; t += 64) {
+        int4 nd = nodes[roots[t]];
+        while (nd.x >= 0) nd = nodes[srow[nd.x] <= __int_as_float(nd.w) ? nd.y : nd.z];
+        if (leaves) leaves[r * ntrees + t] = nd.z;
+        const float* v = values + nd.y;
+#pragma unroll
+        for (int c = 0; c < SV; ++c)
+          if (c < S) acc[c] += v[c];
+      }
+      float mine = 0.f;
+#pragma unroll
+      for (int c = 0; c < SV; ++c) {
+        const float tot = wave_sum(acc[c]);
+        if (c == lane) mine = tot;
+      }
+      if (lane < S) out[r * S + lane] = mine;
+    }
+    __syncthreads();
+  }
+}
+
+SRML_API int srml_rf_predict_nodes2(const float* X, long m, long ld, int n, const int* nodes, const int* roots,
+                                    int ntrees, const float* values, int S, float* out, int* leaves,
+                                    hipStream_t stream) {
+  if (m <= 0) return 0;
+  if (S < 1 || S > 32) return -7;
+  long blocks = (m + 3) / 4;
+  if (blocks > 16384) blocks = 16384;
+  const int4* nd = reinterpret_cast<const int4*>(nodes);
+  const bool lds = n <= RF_LDS_N && ((ld & 3) == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0) &&
+                   (n % 4 == 0 || (long)((n + 3) & ~3) <= ld);
+  if (lds) {
+    const size_t shm = (size_t)4 * ((n + 3) & ~3) * sizeof(float);
+#define SRML_RF_PRED_LDS(SVV)                                                                                     \
+    hipLaunchKernelGGL(rf_predict_lds_kernel<SVV>, dim3((unsigned)blocks), dim3(256), shm, stream, X, m, ld, n, nd, \
+                       roots, ntrees, values, S, out, leaves)
+    if (S <= 1) SRML_RF_PRED_LDS(1);
+    else if (S <= 2) SRML_RF_PRED_LDS(2);
+    else if (S <= 4) SRML_RF_PRED_LDS(4);
+    else if (S <= 8) SRML_RF_PRED_LDS(8);
+    else if (S <= 16) SRML_RF_PRED_LDS(16);
+    else SRML_RF_PRED_LDS(32);
+#undef SRML_RF_PRED_LDS
+    return srml_status();
+  }
+#define SRML_RF_PRED(SVV)                                                                                        \
+  hipLaunchKernelGGL(rf_predict_wave_kernel<SVV>, dim3((unsigned)blocks), dim3(256), 0, stream, X, m, ld, nd, roots, \
+                     ntrees, values, S, out, leaves)
+  if (S <= 1) SRML_RF_PRED(1);
+  else if (S <= 2) SRML_RF_PRED(2);
+  else if (S <= 4) SRML_RF_PRED(4);
+  else if (S <= 8) SRML_RF_PRED(8);
+  else if (S <= 16) SRML_RF_PRED(16);
+  else SRML_RF_PRED(32);
+#undef SRML_RF_PRED
   return srml_status();
 }

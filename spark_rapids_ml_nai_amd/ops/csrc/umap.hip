@@ -8,6 +8,17 @@
 // (attraction + all repulsions) and committed with one atomicAdd per coordinate, the tail
 // update is an atomicAdd too (Hogwild-style like the CPU/GPU references, but without lost
 // updates). Gradients are clipped to [-4, 4] as in umap-learn.
+//
+// Fuzzy simplicial set of a kNN graph (umap-learn smooth_knn_dist / compute_membership_strengths
+// / fuzzy union; cuML UMAP's fuzzy_simplicial_set):
+//  * srml_umap_smooth_knn — one thread per row: rho = local_connectivity-th smallest non-zero
+//    distance (interpolated), sigma by the 64-step bisection on sum_j exp(-(d_j - rho)/sigma) =
+//    log2(k)·bandwidth in fp64 (umap-learn's loop, same early exit and MIN_K_DIST_SCALE floors),
+//    then the row's membership strengths written directly (self / missing neighbours -> 0);
+//  * srml_umap_fuzzy_union_knn — one thread per directed edge i->c: v_ci is found by scanning
+//    row c's k neighbours, the union value mix·(v + v' - v v') + (1 - mix)·v v' goes to slot 2e
+//    as (i, c), and when c->i is not an edge of A (or has zero weight) the transposed entry
+//    (c, i) goes to slot 2e+1, so every entry of A ∪ Aᵀ is produced exactly once, no hashing.
 #include "common.h"
 
 namespace {
@@ -121,5 +132,150 @@ SRML_API int srml_umap_epoch(const int* head, const int* tail, long n_edges, con
     default: SRML_UMAP_LAUNCH(0); break;
   }
 #undef SRML_UMAP_LAUNCH
+  return srml_status();
+}
+
+// ------------------------------------------------------------------------------------------
+namespace {
+constexpr double SMOOTH_K_TOLERANCE = 1e-5;
+constexpr double MIN_K_DIST_SCALE = 1e-3;
+
+// t-th smallest (0-based, with multiplicity) strictly positive value of d[0..k)
+__device__ double nth_positive(const float* d, int k, int t) {
+  double cur = 0.0;
+  int count = 0;
+  while (true) {
+    double nxt = __builtin_huge_val();
+    for (int j = 0; j < k; ++j) {
+      const double v = d[j];
+      if (v > cur && v < nxt) nxt = v;
+    }
+    if (nxt == __builtin_huge_val()) return cur;
+    int mult = 0;
+    for (int j = 0; j < k; ++j) mult += ((double)d[j] == nxt) ? 1 : 0;
+    if (count + mult > t) return nxt;
+    count += mult;
+    cur = nxt;
+  }
+}
+
+__global__ __launch_bounds__(256) void umap_smooth_knn_kernel(const float* __restrict__ dist, const long long* __restrict__ idx,
+                                                              long m, int k, long ld, double target, double local_conn,
+                                                              int n_iter, const double* __restrict__ mean_all,
+                                                              int self_rows, double* __restrict__ sigma_out,
+                                                              double* __restrict__ rho_out, float* __restrict__ w) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const float* d = dist + i * ld;
+  int n_nz = 0;
+  double mean_row = 0.0, max_nz = 0.0;
+  for (int j = 0; j < k; ++j) {
+    const double v = d[j];
+    mean_row += v;
+    if (v > 0.0) { ++n_nz; max_nz = v > max_nz ? v : max_nz; }
+  }
+  mean_row /= (double)k;
+  double rho = 0.0;
+  const int index = (int)floor(local_conn);
+  const double interp = local_conn - (double)index;
+  if ((double)n_nz >= local_conn) {
+    if (index > 0) {
+      const double base = nth_positive(d, k, index - 1);
+      rho = base;
+      if (interp > SMOOTH_K_TOLERANCE && index < k) rho = base + interp * (nth_positive(d, k, index) - base);
+    } else {
+      rho = interp * nth_positive(d, k, 0);
+    }
+  } else if (n_nz > 0) {
+    rho = max_nz;
+  }
+  double lo = 0.0, hi = __builtin_huge_val(), mid = 1.0;
+  for (int it = 0; it < n_iter; ++it) {
+    double psum = 0.0;
+    for (int j = 1; j < k; ++j) {
+      const double dd = (double)d[j] - rho;
+      psum += dd > 0.0 ? exp(-(dd / mid)) : 1.0;
+    }
+    if (fabs(psum - target) < SMOOTH_K_TOLERANCE) break;
+    if (psum > target) {
+      hi = mid;
+      mid = (lo + hi) * 0.5;
+    } else {
+      lo = mid;
+      mid = (hi == __builtin_huge_val()) ? mid * 2.0 : (lo + hi) * 0.5;
+    }
+  }
+  double sig = mid;
+  const double floor_v = MIN_K_DIST_SCALE * (rho > 0.0 ? mean_row : mean_all[0]);
+  if (sig < floor_v) sig = floor_v;
+  sigma_out[i] = sig;
+  rho_out[i] = rho;
+  if (w) {
+    const long long* row_idx = idx + i * ld;
+    for (int j = 0; j < k; ++j) {
+      const long long c = row_idx[j];
+      float v;
+      if (c < 0 || (self_rows && c == i)) {
+        v = 0.f;
+      } else {
+        const double dd = (double)d[j] - rho;
+        v = (dd <= 0.0 || sig == 0.0) ? 1.f : (float)exp(-(dd / sig));
+      }
+      w[i * ld + j] = v;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void umap_fuzzy_union_knn_kernel(const long long* __restrict__ idx,
+                                                                   const float* __restrict__ w, long m, int k, long ld,
+                                                                   float mix, long long* __restrict__ keys,
+                                                                   float* __restrict__ vals) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= m * (long)k) return;
+  const long i = e / k;
+  const int j = (int)(e % k);
+  const long long c = idx[i * ld + j];
+  const float v = w[i * ld + j];
+  long long k0 = -1, k1 = -1;
+  float o0 = 0.f, o1 = 0.f;
+  if (c >= 0 && c < m && v > 0.f) {
+    float vt = 0.f;
+    const long long* rc = idx + c * ld;
+    for (int q = 0; q < k; ++q)
+      if (rc[q] == i) { vt = w[c * ld + q]; break; }
+    const float prod = v * vt;
+    o0 = mix * (v + vt - prod) + (1.f - mix) * prod;
+    if (o0 > 0.f) k0 = (long long)i * m + c;
+    if (!(vt > 0.f)) {  // (c, i) is only in Aᵀ: emit it here
+      o1 = mix * v;
+      if (o1 > 0.f) k1 = c * m + (long long)i;
+    }
+  }
+  keys[2 * e] = k0;
+  keys[2 * e + 1] = k1;
+  vals[2 * e] = o0;
+  vals[2 * e + 1] = o1;
+}
+}  // namespace
+
+// dist fp32 / idx int64 [m][k] (leading dim ld); mean_all: device fp64 scalar (mean of all dist);
+// outputs sigma, rho (fp64 [m]) and, when w != null, membership strengths fp32 [m][ld].
+SRML_API int srml_umap_smooth_knn(const float* dist, const long long* idx, long m, int k, long ld, double target,
+                                  double local_conn, int n_iter, const double* mean_all, int self_rows, double* sigma,
+                                  double* rho, float* w, hipStream_t stream) {
+  if (m <= 0) return 0;
+  if (k < 1 || ld < k || !mean_all) return -1;
+  hipLaunchKernelGGL(umap_smooth_knn_kernel, dim3(ceil_div(m, 256)), dim3(256), 0, stream, dist, idx, m, k, ld, target,
+                     local_conn, n_iter, mean_all, self_rows, sigma, rho, w);
+  return srml_status();
+}
+
+// keys int64 [2 m k] (row * m + col, -1 = no entry), vals fp32 [2 m k].
+SRML_API int srml_umap_fuzzy_union_knn(const long long* idx, const float* w, long m, int k, long ld, float mix,
+                                       long long* keys, float* vals, hipStream_t stream) {
+  if (m <= 0) return 0;
+  if (k < 1 || ld < k) return -1;
+  hipLaunchKernelGGL(umap_fuzzy_union_knn_kernel, dim3(ceil_div(m * (long)k, 256)), dim3(256), 0, stream, idx, w, m, k,
+                     ld, mix, keys, vals);
   return srml_status();
 }

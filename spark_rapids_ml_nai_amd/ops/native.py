@@ -71,6 +71,8 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_dbscan_link_f32": (_P, _L, _I, _L, _P, _F, _L, _L, _P, _P, _P, _P),
     "srml_uf_unite_pairs": (_P, _L, _P, _P),
     "srml_uf_compress": (_P, _L, _P),
+    "srml_umap_smooth_knn": (_P, _P, _L, _I, _L, _D, _D, _I, _P, _I, _P, _P, _P, _P),
+    "srml_umap_fuzzy_union_knn": (_P, _P, _L, _I, _L, ctypes.c_float, _P, _P, _P),
     "srml_umap_epoch": (_P, _P, _L, _P, _P, _P, _P, _P, _P, _I, _I, _F, _F, _F, _F, _F, _I, ctypes.c_uint, _P),
     "srml_syevj_f64": (_P, _I, _P, _P, _I, _D, _P),
     "srml_potrf_f64": (_P, _I, _L, _P, _P),
@@ -96,6 +98,7 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_memcpy_h2d_async": (_P, _P, _L, _P),
     "srml_memcpy_d2h_sync": (_P, _P, _L, _P),
     "srml_memset_async": (_P, _I, _L, _P),
+    "srml_rf_predict_nodes2": (_P, _L, _L, _I, _P, _P, _I, _P, _I, _P, _P, _P),
     "srml_rf_predict": (_P, _L, _L, _P, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P),
 }
 

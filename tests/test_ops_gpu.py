@@ -252,6 +252,50 @@ def test_rf_predict(gpu_device):
                                   pg["right"], pg["value_off"], pg["values"], 2, True)
     torch.testing.assert_close(r_got.cpu(), r_ref)
     assert torch.equal(l_got.cpu(), l_ref)
+    r_n, l_n = ops.rf_predict(X.to(gpu_device), pg["roots"], pg["feature"], pg["threshold"], pg["left"],
+                              pg["right"], pg["value_off"], pg["values"], 2, True, nodes=pg["nodes"])
+    torch.testing.assert_close(r_n.cpu(), r_ref)
+    assert torch.equal(l_n.cpu(), l_ref)
+
+
+def _random_tree(rng, n, S, depth):
+    feat, thr, left, right, val = [], [], [], [], []
+
+    def grow(d):
+        i = len(feat)
+        feat.append(-1); thr.append(0.0); left.append(-1); right.append(-1)
+        val.append(list(rng.random(S)))
+        if d < depth and rng.random() < 0.85:
+            feat[i] = int(rng.integers(0, n)); thr[i] = float(rng.normal())
+            left[i] = grow(d + 1)
+            right[i] = grow(d + 1)
+        return i
+
+    grow(0)
+    return {"feature": feat, "threshold": thr, "left": left, "right": right, "value": val}
+
+
+@pytest.mark.parametrize("ntrees,S,depth", [(50, 2, 8), (130, 20, 6), (7, 1, 12)])
+def test_rf_predict_nodes_random_forest(gpu_device, ntrees, S, depth):
+    from spark_rapids_ml_nai_amd.models.forest import pack_forest
+
+    rng = np.random.default_rng(ntrees)
+    n = 40
+    trees = [_random_tree(rng, n, S, depth) for _ in range(ntrees)]
+    X = torch.randn(3000, n, generator=torch.Generator().manual_seed(1))
+    pc = pack_forest(trees, S, torch.device("cpu"))
+    pg = pack_forest(trees, S, gpu_device)
+    r_ref, l_ref = ops.rf_predict(X, pc["roots"], pc["feature"], pc["threshold"], pc["left"], pc["right"],
+                                  pc["value_off"], pc["values"], S, True)
+    r_got, l_got = forest_predict_gpu(X.to(gpu_device), pg, S)
+    torch.testing.assert_close(r_got.cpu(), r_ref, rtol=1e-5, atol=1e-4)
+    assert torch.equal(l_got.cpu(), l_ref)
+
+
+def forest_predict_gpu(X, packed, S):
+    from spark_rapids_ml_nai_amd.models.forest import forest_predict
+
+    return forest_predict(X, packed, S, want_leaves=True)
 
 
 @pytest.mark.parametrize("mq,mi,n,k", [(1, 50, 3, 5), (300, 5000, 17, 10), (1000, 20000, 128, 64), (129, 300, 256, 1),
