@@ -97,10 +97,15 @@ def lsq_solve(st: LSQStats, reg: float, l1_ratio: float, fit_intercept: bool, st
     keep = nz.double()
     A = A * torch.outer(keep, keep)
     b = b * keep
+    # Penalties of the reference's solvers (regression.py:508-560: cuML RidgeMG with alpha * m, CD
+    # with alpha / l1_ratio; i.e. sklearn Ridge / Lasso / ElasticNet): in raw units
+    #   1/(2m) ||y - Xw - b||^2 + reg * (l1_ratio ||s w||_1 + (1 - l1_ratio)/2 ||s w||^2),
+    # s = feature std (standardization) or 1. Solved here in standardised units (w_t = w s_x / ystd,
+    # objective scaled by 1/ystd^2), which moves one 1/ystd onto the L1 weight and none onto L2.
     lam = reg / ystd
     ones = torch.ones(n, dtype=torch.float64, device=dev)
     l1 = lam * l1_ratio * (ones if standardization else 1.0 / safe)
-    l2 = lam * (1.0 - l1_ratio) * (ones if standardization else 1.0 / (safe * safe))
+    l2 = reg * (1.0 - l1_ratio) * (ones if standardization else 1.0 / (safe * safe))
     if reg == 0.0 or l1_ratio == 0.0:
         Areg = A + torch.diag(l2 + (1.0 - keep))  # constant columns: identity rows, zero rhs
         wt, ok = ops.spd_solve(Areg, b)

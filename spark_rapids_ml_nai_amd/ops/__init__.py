@@ -435,9 +435,14 @@ def cluster_sums(X: torch.Tensor, labels: torch.Tensor, k: int) -> Tuple[torch.T
         off = torch.zeros(k + 1, dtype=torch.int64, device=X.device)
         torch.cumsum(counts, 0, out=off[1:])
         sums = torch.empty((k, n), dtype=torch.float64, device=X.device)
+        # split every segment so (clusters x column chunks x splits) covers the chip; the
+        # partials are folded in split order (deterministic)
+        cblocks = k * ((n + 255) // 256)
+        splits = int(max(1, min(64, m // max(1, k * 256), (4096 + cblocks - 1) // cblocks)))
+        ws = torch.empty(splits * k * n, dtype=torch.float64, device=X.device) if splits > 1 else None
         name = "srml_kmeans_segment_sums_f64" if X.dtype == torch.float64 else "srml_kmeans_segment_sums_f32"
         native.call(name, X.data_ptr(), m, n, X.stride(0), _c(perm.to(torch.int32)).data_ptr(), off.data_ptr(), k,
-                    sums.data_ptr(), native.stream(X.device))
+                    sums.data_ptr(), splits, ws.data_ptr() if ws is not None else None, native.stream(X.device))
         return sums, counts
     counts = torch.zeros(k, dtype=torch.int32, device=X.device)
     st = native.stream(X.device)

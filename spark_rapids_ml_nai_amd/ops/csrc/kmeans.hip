@@ -590,17 +590,21 @@ SRML_API int srml_kmeans_accumulate_sorted_f32(const float* X, long m, int n, lo
 }
 
 // Deterministic / fp64 cluster sums: rows visited in label-sorted order (perm), cluster l owns
-// the segment [off[l], off[l+1]). One block per (cluster, 256-column chunk) sums its segment in
-// row order into fp64 registers and stores the result once: no atomics, bit-reproducible run to
-// run (SRML_DETERMINISTIC=1), and the fp64-input path (T = double) of the Lloyd update.
+// the segment [off[l], off[l+1]), cut into S equal splits. One block per (cluster, 256-column
+// chunk, split) sums its rows in order into fp64 registers and stores the partial into ws[split];
+// a second pass folds the S partials in split order. No atomics: bit-reproducible run to run
+// (SRML_DETERMINISTIC=1), and the fp64-input path (T = double) of the Lloyd update.
 template <typename T>
 __global__ __launch_bounds__(256) void segment_sums_kernel(const T* __restrict__ X, int n, long ld,
                                                            const int* __restrict__ perm,
-                                                           const long* __restrict__ off, double* __restrict__ sums) {
+                                                           const long* __restrict__ off, int k,
+                                                           double* __restrict__ ws) {
   const int l = blockIdx.x;
   const int c = blockIdx.y * 256 + threadIdx.x;
+  const int sp = blockIdx.z, S = gridDim.z;
   if (c >= n) return;
-  const long s0 = off[l], s1 = off[l + 1];
+  const long a = off[l], len = off[l + 1] - a;
+  const long s0 = a + len * sp / S, s1 = a + len * (sp + 1) / S;
   constexpr int U = 8;
   double acc = 0.0;
   long i = s0;
@@ -612,27 +616,42 @@ __global__ __launch_bounds__(256) void segment_sums_kernel(const T* __restrict__
     for (int u = 0; u < U; ++u) acc += (double)v[u];
   }
   for (; i < s1; ++i) acc += (double)X[(long)perm[i] * ld + c];
-  sums[(long)l * n + c] = acc;
+  ws[((long)sp * k + l) * n + c] = acc;
+}
+
+__global__ __launch_bounds__(256) void segment_fold_kernel(const double* __restrict__ ws, int S, long kn,
+                                                           double* __restrict__ sums) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= kn) return;
+  double s = 0.0;
+  for (int z = 0; z < S; ++z) s += ws[z * kn + i];
+  sums[i] = s;
 }
 
 template <typename T>
 static int launch_segment_sums(const T* X, long m, int n, long ld, const int* perm, const long* off, int k,
-                               double* sums, hipStream_t stream) {
+                               double* sums, int splits, double* ws, hipStream_t stream) {
   if (k <= 0 || n <= 0) return 0;
   (void)m;
-  dim3 grid((unsigned)k, ceil_div(n, 256));
-  hipLaunchKernelGGL(segment_sums_kernel<T>, grid, dim3(256), 0, stream, X, n, ld, perm, off, sums);
+  if (splits < 1 || !ws) { splits = 1; ws = sums; }
+  dim3 grid((unsigned)k, ceil_div(n, 256), (unsigned)splits);
+  hipLaunchKernelGGL(segment_sums_kernel<T>, grid, dim3(256), 0, stream, X, n, ld, perm, off, k, ws);
+  int st = srml_status();
+  if (st || ws == sums) return st;
+  const long kn = (long)k * n;
+  hipLaunchKernelGGL(segment_fold_kernel, dim3(ceil_div(kn, 256)), dim3(256), 0, stream, ws, splits, kn, sums);
   return srml_status();
 }
 
-// sums (k*n fp64, fully written) of the rows perm[off[l]:off[l+1]] per cluster l.
+// sums (k*n fp64, fully written) of the rows perm[off[l]:off[l+1]] per cluster l; each segment is
+// cut into `splits` parts summed into ws (splits * k * n fp64; null / splits = 1: direct).
 SRML_API int srml_kmeans_segment_sums_f32(const float* X, long m, int n, long ld, const int* perm, const long* off,
-                                          int k, double* sums, hipStream_t stream) {
-  return launch_segment_sums<float>(X, m, n, ld, perm, off, k, sums, stream);
+                                          int k, double* sums, int splits, double* ws, hipStream_t stream) {
+  return launch_segment_sums<float>(X, m, n, ld, perm, off, k, sums, splits, ws, stream);
 }
 SRML_API int srml_kmeans_segment_sums_f64(const double* X, long m, int n, long ld, const int* perm, const long* off,
-                                          int k, double* sums, hipStream_t stream) {
-  return launch_segment_sums<double>(X, m, n, ld, perm, off, k, sums, stream);
+                                          int k, double* sums, int splits, double* ws, hipStream_t stream) {
+  return launch_segment_sums<double>(X, m, n, ld, perm, off, k, sums, splits, ws, stream);
 }
 
 // ------------------------------------------------------------------------------------------

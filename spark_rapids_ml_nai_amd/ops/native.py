@@ -58,8 +58,8 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_nearest_centroid_split_tiled_np": (_P, _L, _L, _I, _P, _I, _L, _P, _P, _I, _P),
     "srml_kmeans_accumulate_f32": (_P, _L, _I, _L, _P, _I, _P, _P, _P, _P),
     "srml_kmeans_accumulate_sorted_f32": (_P, _L, _I, _L, _P, _P, _P, _P),
-    "srml_kmeans_segment_sums_f32": (_P, _L, _I, _L, _P, _P, _I, _P, _P),
-    "srml_kmeans_segment_sums_f64": (_P, _L, _I, _L, _P, _P, _I, _P, _P),
+    "srml_kmeans_segment_sums_f32": (_P, _L, _I, _L, _P, _P, _I, _P, _I, _P, _P),
+    "srml_kmeans_segment_sums_f64": (_P, _L, _I, _L, _P, _P, _I, _P, _I, _P, _P),
     "srml_nearest_centroid_f64": (_P, _L, _I, _L, _P, _I, _L, _P, _P, _P, _P, _P, _P),
     "srml_row_sqnorm_f64": (_P, _L, _I, _L, _P, _P),
     "srml_knn_dist_f32": (_P, _L, _I, _L, _P, _L, _L, _P, _P, _L, _P),

@@ -151,6 +151,21 @@ class _RandomForestParams(_BackendParams, HasFeaturesCol, HasFeaturesCols, HasLa
     def getMinInfoGain(self) -> float:
         return self.getOrDefault("minInfoGain")
 
+    def getMinWeightFractionPerNode(self) -> float:
+        return self.getOrDefault("minWeightFractionPerNode")
+
+    def getMaxMemoryInMB(self) -> int:
+        return self.getOrDefault("maxMemoryInMB")
+
+    def getCacheNodeIds(self) -> bool:
+        return self.getOrDefault("cacheNodeIds")
+
+    def setLeafCol(self, value: str) -> Any:
+        """Records the Spark Param only: like the reference (tests/test_random_forest.py:573-628),
+        leaf-index output is not produced by transform (no backend mapping)."""
+        self._set(leafCol=value)
+        return self
+
 
 def _stable_seed(name: str) -> int:
     import zlib
