@@ -94,3 +94,92 @@ def to_pinned_numpy(t: torch.Tensor) -> np.ndarray:
     h = torch.empty(t.shape, dtype=t.dtype, pin_memory=torch.cuda.is_available())
     h.copy_(t)
     return h.numpy()
+
+
+def sparse_density_values(density, density_curve: str, n_chunks: int, cols: int, rows: int,
+                          num_partitions: int):
+    """Per-column-chunk target densities (reference gen_data_distributed.py:672-723): a scalar or
+    list of densities, or a Linear / Exponential curve from ~1 nnz per partition up to ``density``,
+    rescaled so the average stays ``density``; values above 1 are cropped."""
+    if density_curve not in ("None", None, ""):
+        d = float(density[0] if isinstance(density, (list, tuple)) else density)
+        n_chunks = min(int(n_chunks), cols)
+        lo = num_partitions / float(rows)
+        if density_curve == "Linear":
+            vals = np.linspace(lo, d, n_chunks)
+        elif density_curve == "Exponential":
+            vals = np.logspace(np.log10(lo), np.log10(d), n_chunks)
+        else:
+            raise ValueError("Unsupported density curve %r (None | Linear | Exponential)" % density_curve)
+        vals = vals * (n_chunks * d / vals.sum())
+    else:
+        vals = np.asarray(density if isinstance(density, (list, tuple)) else [density], dtype=np.float64)
+    return np.minimum(vals, 1.0)
+
+
+def sparse_regression(rows: int, cols: int, seed: int = 1, partition_seed: int = 1, density=0.1,
+                      density_curve: str = "None", n_chunk: int = 10, redundant_cols: int = 0,
+                      n_informative: int = 10, noise: float = 0.0, bias=0.0, shuffle: bool = True,
+                      logistic_regression: bool = False, n_classes: int = 2, num_partitions: int = 1,
+                      dtype=np.float64):
+    """One partition of the reference's ``SparseRegressionDataGen`` (gen_data_distributed.py:581-944)
+    generated directly in CSR (no dense m x n intermediate): per column chunk a scipy random sparse
+    block at that chunk's density, optional redundant columns = informative columns x U(0,1)
+    mixing, the shared column shuffle, y = X w + bias (+ noise), logistic / multinomial sampling.
+
+    ``seed`` fixes what every partition shares (ground truth, column order); ``partition_seed`` the
+    rows of this partition. Returns (X csr_matrix (rows, cols), y ndarray, ground_truth)."""
+    import scipy.sparse as sp
+
+    gen = np.random.RandomState(seed)
+    multinomial = logistic_regression and n_classes > 2
+    orig_cols = cols - int(redundant_cols)
+    dens = sparse_density_values(density, density_curve, n_chunk, orig_cols, rows, num_partitions)
+    if (redundant_cols > 0 and density_curve in ("None", None, "")
+            and redundant_cols / cols > float(np.mean(dens))):
+        redundant_cols, orig_cols = 0, cols  # the reference drops them: they would break the density
+    nt = n_classes if multinomial else 1
+    n_informative = min(int(n_informative), orig_cols)
+    truth = np.zeros((cols, nt))
+    truth[:n_informative, :] = 100 * gen.uniform(size=(n_informative, nt))
+    col_idx = np.arange(cols)
+    if shuffle:
+        gen.shuffle(col_idx)
+        truth = truth[col_idx]
+    pg = np.random.RandomState(partition_seed)
+    nch = len(dens)
+    per = np.full(nch, orig_cols // nch)
+    per[: orig_cols % nch] += 1
+    blocks = []
+    if redundant_cols > 0 and density_curve in ("None", None, ""):
+        d0 = float(dens[0])
+        blocks.append(sp.random(rows, orig_cols, density=(d0 - redundant_cols / cols) / (1 - redundant_cols / cols),
+                                random_state=pg, format="csr", dtype=dtype, data_rvs=pg.standard_normal))
+    else:
+        for c, d in zip(per, dens):
+            blocks.append(sp.random(rows, int(c), density=float(d), random_state=pg, format="csr", dtype=dtype,
+                                    data_rvs=pg.standard_normal))
+    X = sp.hstack(blocks, format="csr") if len(blocks) > 1 else blocks[0]
+    if redundant_cols > 0:
+        mix = pg.random_sample((n_informative, int(redundant_cols)))
+        red = sp.csr_matrix(X[:, :n_informative] @ mix)
+        X = sp.hstack([X, red], format="csr")
+    if shuffle:
+        X = X[:, col_idx]
+    X.sum_duplicates()
+    X.sort_indices()
+    y = np.asarray(X @ truth) + (np.asarray(bias, dtype=np.float64) if multinomial else float(np.ravel(bias)[0]
+                                                                                              if np.ndim(bias) else bias))
+    if noise > 0.0:
+        y = y + pg.normal(scale=noise, size=y.shape)
+    if logistic_regression:
+        if multinomial:
+            z = y - y.max(1, keepdims=True)
+            p = np.exp(z)
+            p /= p.sum(1, keepdims=True)
+            y = (pg.random_sample((rows, 1)) > np.cumsum(p, 1)).sum(1).astype(np.float64)
+        else:
+            y = pg.binomial(1, 1.0 / (1.0 + np.exp(-y[:, 0]))).astype(np.float64)
+    else:
+        y = y[:, 0]
+    return X.astype(dtype), y, np.squeeze(truth)

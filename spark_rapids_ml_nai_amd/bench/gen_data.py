@@ -53,7 +53,14 @@ def _parser() -> argparse.ArgumentParser:
     p.add_argument("--logistic_regression", action="store_true", help="regression: emit 0/1 labels")
     p.add_argument("--effective_rank", type=int, default=10)
     p.add_argument("--tail_strength", type=float, default=0.5)
-    p.add_argument("--density", type=float, default=0.1, help="sparse_regression: fraction of non-zeros")
+    p.add_argument("--density", type=str, default="0.1",
+                   help="sparse_regression: fraction of non-zeros, or a comma list (one per column chunk)")
+    p.add_argument("--density_curve", choices=["None", "Linear", "Exponential"], default="None",
+                   help="sparse_regression: density ramp over --n_chunk column chunks, averaging --density")
+    p.add_argument("--n_chunk", type=int, default=10)
+    p.add_argument("--redundant_cols", type=int, default=0,
+                   help="sparse_regression: columns that are random mixes of the informative ones")
+    p.add_argument("--no_shuffle", action="store_true")
     return p
 
 
@@ -65,19 +72,18 @@ def gen_partition(args: argparse.Namespace, rows: int, seed: int, device: torch.
         X = datagen.uniform(rows, n, device, seed)
     elif args.type == "blobs":
         X, y = datagen.blobs(rows, n, device, seed, centers=args.centers, cluster_std=args.cluster_std)
-    elif args.type in ("regression", "sparse_regression"):
+    elif args.type == "sparse_regression":
+        dens = [float(v) for v in str(args.density).split(",")]
+        X, y, _ = datagen.sparse_regression(
+            rows, n, seed=args.seed + 1, partition_seed=seed + 1000003, density=dens if len(dens) > 1 else dens[0],
+            density_curve=args.density_curve, n_chunk=args.n_chunk, redundant_cols=args.redundant_cols,
+            n_informative=args.n_informative or 10, noise=args.noise, bias=args.bias, shuffle=not args.no_shuffle,
+            logistic_regression=args.logistic_regression, n_classes=args.n_classes,
+            num_partitions=args.output_num_files or 1)
+        return X, y  # CSR (float64, as the reference's sparse VectorUDT) + labels
+    elif args.type == "regression":
         X, y = datagen.regression(rows, n, device, seed, n_informative=args.n_informative, noise=args.noise,
                                   bias=args.bias)
-        if args.type == "sparse_regression":
-            g = torch.Generator(device=device).manual_seed(seed + 1)
-            mask = torch.rand(X.shape, device=device, generator=g) < args.density
-            X = X * mask
-            gw = torch.Generator(device=device).manual_seed(777)
-            k = args.n_informative or max(1, n // 10)
-            w = torch.zeros(n, device=device)
-            idx = torch.randperm(n, device=device, generator=gw)[:k]
-            w[idx] = 100.0 * torch.rand(k, device=device, generator=gw)
-            y = X @ w + args.bias + args.noise * torch.randn(rows, device=device, generator=g)
         if args.logistic_regression:
             y = (torch.sigmoid((y - y.mean()) / y.std().clamp_min(1e-12)) > 0.5).float()
     elif args.type == "classification":
@@ -94,10 +100,11 @@ def gen_partition(args: argparse.Namespace, rows: int, seed: int, device: torch.
     return Xh, yh
 
 
-def _sparse_vector_array(X: np.ndarray) -> pa.Array:
+def _sparse_vector_array(X) -> pa.Array:
     import scipy.sparse as sp
 
-    csr = sp.csr_matrix(X)
+    csr = X if sp.issparse(X) else sp.csr_matrix(X)
+    csr = csr.tocsr()
     m, n = csr.shape
     return pa.StructArray.from_arrays(
         [pa.array(np.zeros(m, dtype=np.int8)), pa.array(np.full(m, n, dtype=np.int32)),
@@ -150,6 +157,8 @@ def generate(argv: Optional[List[str]] = None) -> Dict[str, int]:
         if rows == 0:
             continue
         X, y = gen_partition(args, rows, args.seed + i, device)
+        if y is not None:
+            y = np.asarray(y, dtype=np.float64 if args.type == "sparse_regression" else y.dtype)
         if args.train_fraction is None:
             pq.write_table(to_table(args, X, y), os.path.join(out, "part-%05d.parquet" % i))
             counts[out] += rows

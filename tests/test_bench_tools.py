@@ -102,3 +102,44 @@ def test_chunked_rows_ingest_matches_contiguous():
     a = LinearRegression().fit(df)
     b = LinearRegression().fit(DataFrame.from_numpy(X, y))
     np.testing.assert_allclose(a.coefficients.toArray(), b.coefficients.toArray(), rtol=1e-6)
+
+
+def test_sparse_regression_density_curves_and_redundant_columns():
+    import scipy.sparse as sp
+
+    from spark_rapids_ml_nai_amd.bench import datagen
+
+    for curve in ("Linear", "Exponential"):
+        d = datagen.sparse_density_values(0.05, curve, 10, 400, 20000, 4)
+        assert d.shape == (10,) and np.isclose(d.mean(), 0.05) and np.all(np.diff(d) > 0)
+    X, y, w = datagen.sparse_regression(20000, 400, seed=3, partition_seed=9, density=0.05,
+                                        density_curve="Exponential", n_chunk=10, shuffle=False, n_informative=8)
+    assert sp.issparse(X) and X.shape == (20000, 400)
+    nnz_per_col = np.diff(X.tocsc().indptr)
+    first, last = nnz_per_col[:40].mean(), nnz_per_col[-40:].mean()
+    assert last > 5 * first  # density ramps across the column chunks
+    assert abs(X.nnz / (20000 * 400) - 0.05) < 0.01
+    np.testing.assert_allclose(y, X @ w, rtol=1e-10, atol=1e-8)  # noise 0, bias 0
+    # redundant columns: exact linear mixes of the informative block
+    X2, y2, _ = datagen.sparse_regression(5000, 100, seed=1, partition_seed=2, density=0.3, redundant_cols=10,
+                                          n_informative=6, shuffle=False)
+    red = X2[:, 90:].toarray()
+    inf = X2[:, :6].toarray()
+    coef, res, *_ = np.linalg.lstsq(inf, red, rcond=None)
+    assert np.allclose(inf @ coef, red, atol=1e-8)
+    # binary / multinomial labels
+    _, yb, _ = datagen.sparse_regression(3000, 50, density=0.2, logistic_regression=True)
+    assert set(np.unique(yb)) <= {0.0, 1.0}
+    _, ym, _ = datagen.sparse_regression(3000, 50, density=0.2, logistic_regression=True, n_classes=4)
+    assert set(np.unique(ym)) <= {0.0, 1.0, 2.0, 3.0} and len(np.unique(ym)) > 1
+
+
+def test_gen_data_sparse_regression_cli(tmp_path):
+    from spark_rapids_ml_nai_amd import DataFrame
+    from spark_rapids_ml_nai_amd.bench.gen_data import generate
+
+    out = str(tmp_path / "sp")
+    generate(["sparse_regression", "--num_rows", "3000", "--num_cols", "64", "--density", "0.02,0.2",
+              "--output_num_files", "2", "--output_dir", out, "--device", "cpu"])
+    df = DataFrame.read_parquet(out)
+    assert df.count() == 3000 and df.is_vector("feature_array")
