@@ -6,18 +6,22 @@ driver); approximate — one cuML IVF-Flat index per item partition, queries bro
 merged by a Spark SQL ``groupBy(query_id)`` (``knn.py:1154-1380``).
 
 MI355X design (per rank = per item partition):
-* queries are all-gathered over RCCL (device collective, no driver hop);
-* exact: the fused MFMA distance + LDS top-k kernel (``srml_knn_f32``) over the local items;
+* query fan-out is a point-to-point RING (the role of the reference's UCX send/recv): every
+  rank's query block travels once around the ranks together with its running top-k; at each hop
+  the holder scores it against its local items and merges (device radix-select top-k with ids),
+  and the NEXT block's transfer (isend/irecv over RCCL/xGMI) overlaps that compute. After W hops
+  the finished block is back at its owner. Per-rank memory is two query blocks + their top-k
+  lists, instead of every rank's queries (the all-gather's O(Q·n) per rank);
+* exact: the fused MFMA distance + LDS top-k kernel (``srml_knn_f32``, k <= 64) or the distance
+  chunk + radix-select path (k <= 1024) over the local items, candidates refined exactly;
 * IVF-Flat: coarse quantiser trained with the device KMeans kernels, items bucketed into
   contiguous inverted lists (device sort), probes chosen with the same top-k kernel against the
-  centroids, lists scanned by ``srml_ivf_search_f32``;
-* partial (distance, global id) lists all-gathered and merged with one device top-k; each rank
-  keeps the rows of its own queries.
+  centroids, lists scanned by ``srml_ivf_search_f32``; queries ride the same ring.
 """
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import Optional, Tuple
+from typing import Callable, Optional, Tuple
 
 import numpy as np
 import torch
@@ -26,26 +30,56 @@ from .. import ops
 from ..parallel.context import WorkerContext
 
 
-def _gather_queries(Q: torch.Tensor, ctx: WorkerContext) -> Tuple[torch.Tensor, int, int]:
-    parts = ctx.comm.allgatherv(Q.contiguous())
-    sizes = [p.shape[0] for p in parts]
-    start = sum(sizes[: ctx.rank])
-    return torch.cat([p.to(Q.device) for p in parts], 0), start, Q.shape[0]
+def _merge_lists(d1: torch.Tensor, i1: torch.Tensor, d2: torch.Tensor, i2: torch.Tensor, k: int
+                 ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """k smallest of two (distance, id) lists per row (ties keep the earlier list)."""
+    D = torch.cat([d1, d2], 1)
+    I = torch.cat([i1, i2], 1)
+    if k <= ops.TOPK_KMAX:
+        return ops.topk_rows(D, k, ids=I)
+    v, j = torch.sort(D, dim=1, stable=True)
+    return v[:, :k], I.gather(1, j[:, :k])
 
 
-def _merge_partials(d: torch.Tensor, i: torch.Tensor, k: int, ctx: WorkerContext, start: int, nloc: int,
-                    largest: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
-    if ctx.world_size > 1:
-        dd = ctx.comm.allgather(d.contiguous().unsqueeze(0))  # (w, q, k)
-        ii = ctx.comm.allgather(i.contiguous().unsqueeze(0))
-        d = dd.permute(1, 0, 2).reshape(d.shape[0], -1)
-        i = ii.permute(1, 0, 2).reshape(i.shape[0], -1)
-        d = d[start: start + nloc]
-        i = i[start: start + nloc]
-        kk = min(k, d.shape[1])
-        v, j = torch.topk(d, kk, dim=1, largest=largest)
-        return v, i.gather(1, j)
-    return d[start: start + nloc], i[start: start + nloc]
+def _ring_search(queries: torch.Tensor, k: int, ctx: WorkerContext, local: Callable[[torch.Tensor], Tuple[
+        torch.Tensor, torch.Tensor]]) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Run ``local(Q) -> (d [q, k], global ids [q, k])`` for every rank's query block on every
+    rank's items by passing (block, running top-k) around the ring; returns this rank's merged
+    lists. One hop = one overlapped isend/irecv of the next query block + a small exchange of the
+    running lists."""
+    W, r = ctx.world_size, ctx.rank
+    dev = queries.device
+    nq = queries.shape[0]
+    if W == 1:
+        return local(queries)
+    sizes = [int(v) for v in ctx.comm.allgather(torch.tensor([nq], dtype=torch.int64, device=ctx.device)).tolist()]
+    n = queries.shape[1]
+    nxt, prv = (r + 1) % W, (r - 1) % W
+    Qc = queries.contiguous()
+    dc = torch.full((nq, k), float("inf"), dtype=torch.float32, device=dev)
+    ic = torch.full((nq, k), -1, dtype=torch.int64, device=dev)
+    for s in range(W):
+        h = None
+        if s < W - 1:  # the next block is already on its way while this one is scored
+            rows = sizes[(r - s - 1) % W]
+            Qn = torch.empty((rows, n), dtype=Qc.dtype, device=dev)
+            h = ctx.comm.isendrecv(Qc, nxt, Qn, prv)
+        if Qc.shape[0]:
+            ld, li = local(Qc)
+            dc, ic = _merge_lists(dc, ic, ld.float(), li, k)
+        if s < W - 1:
+            ctx.comm.wait_sendrecv(h)
+            dn = torch.empty((rows, k), dtype=torch.float32, device=dev)
+            inn = torch.empty((rows, k), dtype=torch.int64, device=dev)
+            ctx.comm.sendrecv(dc.contiguous(), nxt, dn, prv)
+            ctx.comm.sendrecv(ic.contiguous(), nxt, inn, prv)
+            Qc, dc, ic = Qn, dn, inn
+    # the block now held belongs to the next rank: hand it home, receive ours
+    d_own = torch.empty((nq, k), dtype=torch.float32, device=dev)
+    i_own = torch.empty((nq, k), dtype=torch.int64, device=dev)
+    ctx.comm.sendrecv(dc.contiguous(), nxt, d_own, prv)
+    ctx.comm.sendrecv(ic.contiguous(), nxt, i_own, prv)
+    return d_own, i_own
 
 
 def _finish(d: torch.Tensor, metric: str) -> torch.Tensor:
@@ -80,26 +114,31 @@ def _resort(d: torch.Tensor, i: torch.Tensor) -> Tuple[torch.Tensor, torch.Tenso
     return v, i.gather(1, j)
 
 
+def _pad_k(d: torch.Tensor, gi: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    if d.shape[1] < k:  # fewer local items than k
+        pad = k - d.shape[1]
+        d = torch.cat([d, torch.full((d.shape[0], pad), float("inf"), device=d.device)], 1)
+        gi = torch.cat([gi, torch.full((gi.shape[0], pad), -1, dtype=torch.int64, device=gi.device)], 1)
+    return d, gi
+
+
 def exact_knn(items: torch.Tensor, item_ids: torch.Tensor, queries: torch.Tensor, k: int, ctx: WorkerContext,
               metric: str = "euclidean") -> Tuple[np.ndarray, np.ndarray]:
-    Qall, start, nloc = _gather_queries(queries, ctx)
-    if items.shape[0] == 0:
-        d = torch.full((Qall.shape[0], k), float("inf"), device=Qall.device)
-        gi = torch.full((Qall.shape[0], k), -1, dtype=torch.int64, device=Qall.device)
-    else:
+    def local(Q: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        if items.shape[0] == 0:
+            return (torch.full((Q.shape[0], k), float("inf"), device=Q.device),
+                    torch.full((Q.shape[0], k), -1, dtype=torch.int64, device=Q.device))
         if metric == "inner_product":
             z_i = torch.zeros(items.shape[0], device=items.device)
-            z_q = torch.zeros(Qall.shape[0], device=items.device)
-            d, li = ops.knn(Qall, items, k, inorm=z_i, qnorm=z_q)  # d = -2 q.i
+            z_q = torch.zeros(Q.shape[0], device=items.device)
+            d, li = ops.knn(Q, items, k, inorm=z_i, qnorm=z_q)  # d = -2 q.i
         else:
-            d, li = ops.knn(Qall, items, k)
-        d, li = _resort(_refine(Qall, items, li, metric), li)
+            d, li = ops.knn(Q, items, k)
+        d, li = _resort(_refine(Q, items, li, metric), li)
         gi = torch.where(li >= 0, item_ids[li.clamp_min(0)], torch.full_like(li, -1))
-        if d.shape[1] < k:  # fewer local items than k
-            pad = k - d.shape[1]
-            d = torch.cat([d, torch.full((d.shape[0], pad), float("inf"), device=d.device)], 1)
-            gi = torch.cat([gi, torch.full((gi.shape[0], pad), -1, dtype=torch.int64, device=gi.device)], 1)
-    d, gi = _merge_partials(d, gi, k, ctx, start, nloc)
+        return _pad_k(d, gi, k)
+
+    d, gi = _ring_search(queries, k, ctx, local)
     return _finish(d, metric).cpu().numpy(), gi.cpu().numpy()
 
 
@@ -139,22 +178,23 @@ def build_ivf(X: torch.Tensor, ids: torch.Tensor, nlist: int, seed: int = 1, ite
 
 def ivf_knn(index: Optional[IVFIndex], queries: torch.Tensor, k: int, nprobe: int, ctx: WorkerContext,
             metric: str = "euclidean") -> Tuple[np.ndarray, np.ndarray]:
-    Qall, start, nloc = _gather_queries(queries, ctx)
-    if index is None:
-        d = torch.full((Qall.shape[0], k), float("inf"), device=Qall.device)
-        gi = torch.full((Qall.shape[0], k), -1, dtype=torch.int64, device=Qall.device)
-    else:
-        nprobe = max(1, min(int(nprobe), index.centroids.shape[0], ops.KNN_KMAX))
-        qn = ops.row_sqnorm(Qall)
-        _, probes = ops.knn(Qall, index.centroids, nprobe, inorm=index.cnorm, qnorm=qn)
-        pos_ids = torch.arange(index.items.shape[0], dtype=torch.int64, device=Qall.device)
+    def local(Q: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        if index is None:
+            return (torch.full((Q.shape[0], k), float("inf"), device=Q.device),
+                    torch.full((Q.shape[0], k), -1, dtype=torch.int64, device=Q.device))
+        npb = max(1, min(int(nprobe), index.centroids.shape[0], ops.KNN_KMAX))
+        qn = ops.row_sqnorm(Q)
+        _, probes = ops.knn(Q, index.centroids, npb, inorm=index.cnorm, qnorm=qn)
+        pos_ids = torch.arange(index.items.shape[0], dtype=torch.int64, device=Q.device)
         if metric == "inner_product":
             z = torch.zeros_like(index.inorm)
-            d, pos = ops.ivf_search(Qall, probes.int(), index.list_off, index.items, z, pos_ids, k,
+            d, pos = ops.ivf_search(Q, probes.int(), index.list_off, index.items, z, pos_ids, k,
                                     qnorm=torch.zeros_like(qn))
         else:
-            d, pos = ops.ivf_search(Qall, probes.int(), index.list_off, index.items, index.inorm, pos_ids, k, qnorm=qn)
-        d, pos = _resort(_refine(Qall, index.items, pos, metric), pos)
+            d, pos = ops.ivf_search(Q, probes.int(), index.list_off, index.items, index.inorm, pos_ids, k, qnorm=qn)
+        d, pos = _resort(_refine(Q, index.items, pos, metric), pos)
         gi = torch.where(pos >= 0, index.ids[pos.clamp_min(0)], torch.full_like(pos, -1))
-    d, gi = _merge_partials(d, gi, k, ctx, start, nloc)
+        return _pad_k(d, gi, k)
+
+    d, gi = _ring_search(queries, k, ctx, local)
     return _finish(d, metric).cpu().numpy(), gi.cpu().numpy()

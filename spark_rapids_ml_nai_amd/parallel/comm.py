@@ -117,6 +117,35 @@ class Communicator:
         g = self.allgather(pad).view((self.size, mx) + tuple(t.shape[1:]))
         return [g[r, : sizes[r]] for r in range(self.size)]
 
+    def isendrecv(self, send: torch.Tensor, dst: int, recv: torch.Tensor, src: int) -> Any:
+        """Start a paired point-to-point exchange (send ``send`` to ``dst``, receive into ``recv``
+        from ``src``; group-local ranks). Returns a handle for ``wait_sendrecv``. RCCL batches the
+        pair into one group call (the ring steps of the kNN query pass); gloo stages through host."""
+        if self.size == 1:
+            recv.copy_(send)
+            return None
+        cs = self._comm_tensor(send.contiguous())
+        cr = self._comm_tensor(recv)
+        g = self.group
+        gd = dist.get_global_rank(g, dst) if g is not None else dst
+        gs = dist.get_global_rank(g, src) if g is not None else src
+        works = dist.batch_isend_irecv([dist.P2POp(dist.isend, cs, gd, group=g),
+                                        dist.P2POp(dist.irecv, cr, gs, group=g)])
+        return (works, cs, cr, recv)
+
+    def wait_sendrecv(self, handle: Any) -> None:
+        if handle is None:
+            return
+        works, _cs, cr, recv = handle
+        for w in works:
+            w.wait()
+        if cr is not recv:
+            recv.copy_(cr)
+
+    def sendrecv(self, send: torch.Tensor, dst: int, recv: torch.Tensor, src: int) -> torch.Tensor:
+        self.wait_sendrecv(self.isendrecv(send, dst, recv, src))
+        return recv
+
     def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if self.size == 1:
             return t

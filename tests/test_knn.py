@@ -160,3 +160,20 @@ def test_ann_two_ranks(monkeypatch):
     _, exact = SkNN(n_neighbors=5, algorithm="brute").fit(X).kneighbors(X[:300])
     recall = np.mean([len(set(a) & set(b)) / 5.0 for a, b in zip(ind, exact)])
     assert recall >= 0.95
+
+
+@pytest.mark.dist
+@pytest.mark.parametrize("world", [3, 4])
+def test_exact_knn_ring_fanout_matches_sklearn(world, monkeypatch):
+    """Queries travel the p2p ring (uneven blocks, one rank with fewer queries than others)."""
+    monkeypatch.setenv("SRML_FORCE_CPU", "1")
+    X = _blobs(m=900, n=8, seed=17)
+    Q = X[::5][:151] + 0.03
+    items = DataFrame.from_numpy(X, num_partitions=world)
+    model = NearestNeighbors(k=7, inputCol="features", num_workers=world).fit(items)
+    _, _, kdf = model.kneighbors(DataFrame.from_numpy(Q, num_partitions=world))
+    qid, ind, dist = _knn_arrays(kdf)
+    ref_d, ref_i = SkNN(n_neighbors=7, algorithm="brute").fit(X).kneighbors(Q)
+    order = np.argsort(qid)
+    np.testing.assert_allclose(dist[order], ref_d, rtol=1e-4, atol=1e-4)
+    assert (ind[order] == ref_i).mean() > 0.99
