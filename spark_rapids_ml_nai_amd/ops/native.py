@@ -71,6 +71,11 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_dbscan_link_f32": (_P, _L, _I, _L, _P, _F, _L, _L, _P, _P, _P, _P),
     "srml_uf_unite_pairs": (_P, _L, _P, _P),
     "srml_uf_compress": (_P, _L, _P),
+    "srml_oneshot_alloc": (_L, _P, _P),
+    "srml_oneshot_open": (_P, _P),
+    "srml_oneshot_close": (_P,),
+    "srml_oneshot_free": (_P,),
+    "srml_oneshot_allreduce": (_P, _P, _L, _I, _P, _I, _I, ctypes.c_ulonglong, _L, ctypes.c_longlong, _P, _P),
     "srml_umap_smooth_knn": (_P, _P, _L, _I, _L, _D, _D, _I, _P, _I, _P, _P, _P, _P),
     "srml_umap_fuzzy_union_knn": (_P, _P, _L, _I, _L, ctypes.c_float, _P, _P, _P),
     "srml_umap_epoch": (_P, _P, _L, _P, _P, _P, _P, _P, _P, _I, _I, _F, _F, _F, _F, _F, _I, ctypes.c_uint, _P),

@@ -70,10 +70,34 @@ class Communicator:
         return t
 
     # -- collectives ----------------------------------------------------------------
+    def _oneshot_for(self, t: torch.Tensor, op: str) -> Any:
+        """The peer-mapped one-shot path (``SRML_COMM=oneshot``) when it applies to this payload."""
+        if op != "sum" or not t.is_cuda or self._backend != "nccl" or not t.is_contiguous():
+            return None
+        if t.dtype not in (torch.float32, torch.float64):
+            return None
+        from . import oneshot
+
+        if oneshot.comm_mode() != "oneshot" or t.numel() * 8 > oneshot.MAX_BYTES:
+            return None
+        if getattr(self, "_oneshot", None) is None and not getattr(self, "_oneshot_failed", False):
+            try:
+                self._oneshot = oneshot.OneShotAllreduce(self, self.device)
+            except Exception as e:  # noqa: BLE001 - fall back to RCCL, loudly
+                import warnings
+
+                warnings.warn("one-shot all-reduce unavailable (%s); using RCCL" % e)
+                self._oneshot_failed = True
+                self._oneshot = None
+        return getattr(self, "_oneshot", None)
+
     def allreduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
         """In-place all-reduce; returns ``t``."""
         if self.size == 1:
             return t
+        os_ = self._oneshot_for(t, op)
+        if os_ is not None:
+            return os_.allreduce(t)
         ct = self._comm_tensor(t)
         dist.all_reduce(ct, op=_OPS[op], group=self.group)
         if ct is not t:

@@ -42,6 +42,10 @@ def main() -> None:
     ap.add_argument("--ops", default="all_reduce,all_gather,reduce_scatter,broadcast,all_to_all")
     ap.add_argument("--dtype", default="float32")
     ap.add_argument("--out", default=None, help="also append the JSON lines to this file (rank 0)")
+    ap.add_argument("--backend", choices=("auto", "nccl", "gloo"), default="auto",
+                    help="gloo with GPUs: ranks may share one device (one-shot rehearsal on a 1-GPU box)")
+    ap.add_argument("--oneshot", action="store_true",
+                    help="add the peer-mapped one-shot all-reduce (<= 256 KB) next to the collectives")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -53,9 +57,15 @@ def main() -> None:
         torch.cuda.set_device(dev)
     if "MASTER_ADDR" not in os.environ:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ.get("MASTER_PORT", "29531"))
-    backend = "nccl" if gpu else "gloo"
+    backend = a.backend if a.backend != "auto" else ("nccl" if gpu else "gloo")
     dist.init_process_group(backend, rank=rank, world_size=world, timeout=timedelta(minutes=10),
-                            **({"device_id": dev} if gpu else {}))
+                            **({"device_id": dev} if backend == "nccl" else {}))
+    oneshot = None
+    if a.oneshot and gpu:
+        from spark_rapids_ml_nai_amd.parallel.comm import Communicator
+        from spark_rapids_ml_nai_amd.parallel.oneshot import MAX_BYTES, OneShotAllreduce
+
+        oneshot = OneShotAllreduce(Communicator(rank, world, dev if backend == "nccl" else torch.device("cpu")), dev)
     dt = getattr(torch, a.dtype)
     esz = torch.tensor([], dtype=dt).element_size()
     sizes = []
@@ -70,14 +80,20 @@ def main() -> None:
 
     n = world
     bus = {"all_reduce": 2 * (n - 1) / n, "all_gather": (n - 1) / n, "reduce_scatter": (n - 1) / n,
-           "broadcast": 1.0, "all_to_all": (n - 1) / n}
+           "broadcast": 1.0, "all_to_all": (n - 1) / n, "oneshot_all_reduce": 2 * (n - 1) / n}
+    ops = a.ops.split(",") + (["oneshot_all_reduce"] if oneshot is not None else [])
     rows = []
-    for op in a.ops.split(","):
+    for op in ops:
         for nbytes in sizes:
+            if op == "oneshot_all_reduce" and nbytes > MAX_BYTES:
+                continue
             cnt = max(n, nbytes // esz // n * n)
             x = torch.ones(cnt, dtype=dt, device=dev)
             if op == "all_reduce":
                 f = lambda: dist.all_reduce(x)  # noqa: E731
+            elif op == "oneshot_all_reduce":
+                x = torch.ones(min(cnt, MAX_BYTES // 8), dtype=torch.float64, device=dev)
+                f = lambda: oneshot.allreduce(x)  # noqa: E731
             elif op == "all_gather":
                 out = torch.empty(cnt * n, dtype=dt, device=dev)
                 f = lambda: dist.all_gather_into_tensor(out, x)  # noqa: E731
@@ -111,6 +127,9 @@ def main() -> None:
             rows.append(row)
             if rank == 0:
                 print(json.dumps(row), flush=True)
+    if oneshot is not None:
+        oneshot.check()
+        oneshot.close()
     if rank == 0 and a.out:
         with open(a.out, "a") as fh:
             for r in rows:
