@@ -12,7 +12,7 @@ Spark executor's batches.
 """
 from __future__ import annotations
 
-from typing import Optional, Tuple
+from typing import Any, Optional, Tuple
 
 import numpy as np
 import torch
@@ -96,8 +96,8 @@ def to_pinned_numpy(t: torch.Tensor) -> np.ndarray:
     return h.numpy()
 
 
-def sparse_density_values(density, density_curve: str, n_chunks: int, cols: int, rows: int,
-                          num_partitions: int):
+def sparse_density_values(density: Any, density_curve: str, n_chunks: int, cols: int, rows: int,
+                          num_partitions: int) -> np.ndarray:
     """Per-column-chunk target densities (reference gen_data_distributed.py:672-723): a scalar or
     list of densities, or a Linear / Exponential curve from ~1 nnz per partition up to ``density``,
     rescaled so the average stays ``density``; values above 1 are cropped."""
@@ -117,11 +117,11 @@ def sparse_density_values(density, density_curve: str, n_chunks: int, cols: int,
     return np.minimum(vals, 1.0)
 
 
-def sparse_regression(rows: int, cols: int, seed: int = 1, partition_seed: int = 1, density=0.1,
+def sparse_regression(rows: int, cols: int, seed: int = 1, partition_seed: int = 1, density: Any = 0.1,
                       density_curve: str = "None", n_chunk: int = 10, redundant_cols: int = 0,
-                      n_informative: int = 10, noise: float = 0.0, bias=0.0, shuffle: bool = True,
+                      n_informative: int = 10, noise: float = 0.0, bias: Any = 0.0, shuffle: bool = True,
                       logistic_regression: bool = False, n_classes: int = 2, num_partitions: int = 1,
-                      dtype=np.float64):
+                      dtype=np.float64) -> Tuple[Any, np.ndarray, np.ndarray]:
     """One partition of the reference's ``SparseRegressionDataGen`` (gen_data_distributed.py:581-944)
     generated directly in CSR (no dense m x n intermediate): per column chunk a scipy random sparse
     block at that chunk's density, optional redundant columns = informative columns x U(0,1)

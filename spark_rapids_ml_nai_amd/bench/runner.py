@@ -97,12 +97,12 @@ class Bench:
 class KMeansBench(Bench):
     name = "kmeans"
 
-    def estimator(self, train):
+    def estimator(self, train: DataFrame) -> Any:
         from ..clustering import KMeans
 
         return KMeans(num_workers=self.args.num_gpus, **_feature_kwargs(train, self.args.feature_col), **self.params)
 
-    def score(self, model, out, X, y):
+    def score(self, model: Any, out: Optional[DataFrame], X: np.ndarray, y: Optional[np.ndarray]) -> Dict[str, float]:
         C = np.asarray(model.cluster_centers_, dtype=np.float64)
         d = ((X[:, None, :] - C[None]) ** 2).sum(-1) if X.shape[0] * C.shape[0] < 5e7 else None
         if d is None:
@@ -115,7 +115,7 @@ class KMeansBench(Bench):
             return {"inertia": float(dist.double().sum())}
         return {"inertia": float(d.min(1).sum())}
 
-    def cpu(self, X, y, Xt):
+    def cpu(self, X: np.ndarray, y: Optional[np.ndarray], Xt: np.ndarray) -> Tuple[Any, Any]:
         from sklearn.cluster import KMeans as SK
 
         k = int(self.params.get("k", 2))
@@ -127,13 +127,13 @@ class KMeansBench(Bench):
 class PCABench(Bench):
     name = "pca"
 
-    def estimator(self, train):
+    def estimator(self, train: DataFrame) -> Any:
         from ..feature import PCA
 
         kw = _feature_kwargs(train, self.args.feature_col, "inputCol")
         return PCA(num_workers=self.args.num_gpus, outputCol="pca_features", **kw, **self.params)
 
-    def score(self, model, out, X, y):
+    def score(self, model: Any, out: Optional[DataFrame], X: np.ndarray, y: Optional[np.ndarray]) -> Dict[str, float]:
         pc = np.asarray(model.components_, dtype=np.float64)
         ortho = float(np.abs(pc @ pc.T - np.eye(pc.shape[0])).max())
         idx = _sample(X, 100000)
@@ -141,7 +141,7 @@ class PCABench(Bench):
         proj = Xs @ pc.T
         return {"orthonormality_err": ortho, "projected_variance": float(proj.var(0).sum())}
 
-    def cpu(self, X, y, Xt):
+    def cpu(self, X: np.ndarray, y: Optional[np.ndarray], Xt: np.ndarray) -> Tuple[Any, Any]:
         from sklearn.decomposition import PCA as SK
 
         m = SK(n_components=int(self.params.get("k", 3)), svd_solver="full").fit(X)
@@ -152,19 +152,19 @@ class LinearRegressionBench(Bench):
     name = "linear_regression"
     supervised = True
 
-    def estimator(self, train):
+    def estimator(self, train: DataFrame) -> Any:
         from ..regression import LinearRegression
 
         return LinearRegression(num_workers=self.args.num_gpus, labelCol=self.args.label_col,
                                 **_feature_kwargs(train, self.args.feature_col), **self.params)
 
-    def score(self, model, out, X, y):
+    def score(self, model: Any, out: Optional[DataFrame], X: np.ndarray, y: Optional[np.ndarray]) -> Dict[str, float]:
         pred = out.to_numpy(model.getPredictionCol()) if out is not None else None
         if pred is None or y is None:
             return {}
         return {"rmse": float(np.sqrt(np.mean((pred - y) ** 2)))}
 
-    def cpu(self, X, y, Xt):
+    def cpu(self, X: np.ndarray, y: Optional[np.ndarray], Xt: np.ndarray) -> Tuple[Any, Any]:
         from sklearn.linear_model import ElasticNet, LinearRegression as SK, Ridge
 
         reg = float(self.params.get("regParam", 0.0))
@@ -182,13 +182,13 @@ class LogisticRegressionBench(Bench):
     name = "logistic_regression"
     supervised = True
 
-    def estimator(self, train):
+    def estimator(self, train: DataFrame) -> Any:
         from ..classification import LogisticRegression
 
         return LogisticRegression(num_workers=self.args.num_gpus, labelCol=self.args.label_col,
                                   **_feature_kwargs(train, self.args.feature_col), **self.params)
 
-    def score(self, model, out, X, y):
+    def score(self, model: Any, out: Optional[DataFrame], X: np.ndarray, y: Optional[np.ndarray]) -> Dict[str, float]:
         if out is None or y is None:
             return {}
         from ..metrics import binary_auc
@@ -202,7 +202,7 @@ class LogisticRegressionBench(Bench):
             res["auc"] = float(binary_auc(y, p1))
         return res
 
-    def cpu(self, X, y, Xt):
+    def cpu(self, X: np.ndarray, y: Optional[np.ndarray], Xt: np.ndarray) -> Tuple[Any, Any]:
         from sklearn.linear_model import LogisticRegression as SK
 
         reg = float(self.params.get("regParam", 0.0))
@@ -214,18 +214,18 @@ class RandomForestClassifierBench(Bench):
     name = "random_forest_classifier"
     supervised = True
 
-    def estimator(self, train):
+    def estimator(self, train: DataFrame) -> Any:
         from ..classification import RandomForestClassifier
 
         return RandomForestClassifier(num_workers=self.args.num_gpus, labelCol=self.args.label_col,
                                       **_feature_kwargs(train, self.args.feature_col), **self.params)
 
-    def score(self, model, out, X, y):
+    def score(self, model: Any, out: Optional[DataFrame], X: np.ndarray, y: Optional[np.ndarray]) -> Dict[str, float]:
         if out is None or y is None:
             return {}
         return {"accuracy": float((out.to_numpy(model.getPredictionCol()) == y).mean())}
 
-    def cpu(self, X, y, Xt):
+    def cpu(self, X: np.ndarray, y: Optional[np.ndarray], Xt: np.ndarray) -> Tuple[Any, Any]:
         from sklearn.ensemble import RandomForestClassifier as SK
 
         m = SK(n_estimators=int(self.params.get("numTrees", 20)), max_depth=int(self.params.get("maxDepth", 5)),
@@ -236,18 +236,18 @@ class RandomForestClassifierBench(Bench):
 class RandomForestRegressorBench(RandomForestClassifierBench):
     name = "random_forest_regressor"
 
-    def estimator(self, train):
+    def estimator(self, train: DataFrame) -> Any:
         from ..regression import RandomForestRegressor
 
         return RandomForestRegressor(num_workers=self.args.num_gpus, labelCol=self.args.label_col,
                                      **_feature_kwargs(train, self.args.feature_col), **self.params)
 
-    def score(self, model, out, X, y):
+    def score(self, model: Any, out: Optional[DataFrame], X: np.ndarray, y: Optional[np.ndarray]) -> Dict[str, float]:
         if out is None or y is None:
             return {}
         return {"rmse": float(np.sqrt(np.mean((out.to_numpy(model.getPredictionCol()) - y) ** 2)))}
 
-    def cpu(self, X, y, Xt):
+    def cpu(self, X: np.ndarray, y: Optional[np.ndarray], Xt: np.ndarray) -> Tuple[Any, Any]:
         from sklearn.ensemble import RandomForestRegressor as SK
 
         m = SK(n_estimators=int(self.params.get("numTrees", 20)), max_depth=int(self.params.get("maxDepth", 5)),
@@ -258,31 +258,31 @@ class RandomForestRegressorBench(RandomForestClassifierBench):
 class UMAPBench(Bench):
     name = "umap"
 
-    def estimator(self, train):
+    def estimator(self, train: DataFrame) -> Any:
         from ..umap import UMAP
 
         return UMAP(num_workers=self.args.num_gpus, **_feature_kwargs(train, self.args.feature_col), **self.params)
 
-    def score(self, model, out, X, y):
+    def score(self, model: Any, out: Optional[DataFrame], X: np.ndarray, y: Optional[np.ndarray]) -> Dict[str, float]:
         from sklearn.manifold import trustworthiness
 
         emb = out.to_numpy(model.getOutputCol()) if out is not None else np.asarray(model.embedding_)
         idx = _sample(X, 5000)
         return {"trustworthiness": float(trustworthiness(X[idx], emb[idx], n_neighbors=15))}
 
-    def cpu(self, X, y, Xt):
+    def cpu(self, X: np.ndarray, y: Optional[np.ndarray], Xt: np.ndarray) -> Tuple[Any, Any]:
         raise RuntimeError("umap-learn is not installed in this image")
 
 
 class DBSCANBench(Bench):
     name = "dbscan"
 
-    def estimator(self, train):
+    def estimator(self, train: DataFrame) -> Any:
         from ..clustering import DBSCAN
 
         return DBSCAN(num_workers=self.args.num_gpus, **_feature_kwargs(train, self.args.feature_col), **self.params)
 
-    def score(self, model, out, X, y):
+    def score(self, model: Any, out: Optional[DataFrame], X: np.ndarray, y: Optional[np.ndarray]) -> Dict[str, float]:
         from sklearn.metrics import silhouette_score
 
         lab = out.to_numpy(model.getPredictionCol())
@@ -291,7 +291,7 @@ class DBSCANBench(Bench):
             return {"n_clusters": int(lab.max() + 1)}
         return {"silhouette": float(silhouette_score(X[idx], lab[idx])), "n_clusters": int(lab.max() + 1)}
 
-    def cpu(self, X, y, Xt):
+    def cpu(self, X: np.ndarray, y: Optional[np.ndarray], Xt: np.ndarray) -> Tuple[Any, Any]:
         from sklearn.cluster import DBSCAN as SK
 
         m = SK(eps=float(self.params.get("eps", 0.5)), min_samples=int(self.params.get("min_samples", 5))).fit(X)
@@ -301,13 +301,13 @@ class DBSCANBench(Bench):
 class KNNBench(Bench):
     name = "knn"
 
-    def estimator(self, train):
+    def estimator(self, train: DataFrame) -> Any:
         from ..knn import NearestNeighbors
 
         return NearestNeighbors(num_workers=self.args.num_gpus,
                                 **_feature_kwargs(train, self.args.feature_col, "inputCol"), **self.params)
 
-    def cpu(self, X, y, Xt):
+    def cpu(self, X: np.ndarray, y: Optional[np.ndarray], Xt: np.ndarray) -> Tuple[Any, Any]:
         from sklearn.neighbors import NearestNeighbors as SK
 
         m = SK(n_neighbors=int(self.params.get("k", 5)), algorithm="brute").fit(X)
@@ -317,7 +317,7 @@ class KNNBench(Bench):
 class ANNBench(KNNBench):
     name = "approximate_nearest_neighbors"
 
-    def estimator(self, train):
+    def estimator(self, train: DataFrame) -> Any:
         from ..knn import ApproximateNearestNeighbors
 
         return ApproximateNearestNeighbors(num_workers=self.args.num_gpus,

@@ -8,7 +8,7 @@ parameters, the same row x feature shape and the same data family, generated on 
 from __future__ import annotations
 
 import math
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import Any, Callable, Dict, List, Optional, Tuple
 
 import numpy as np
@@ -153,7 +153,8 @@ def model_evidence(name: str, model: Any) -> Dict[str, Any]:
     return ev
 
 
-def make_shard(family: str, m_local: int, n: int, device: torch.device, rank: int, m_total: int) -> Tuple[np.ndarray, Optional[np.ndarray]]:
+def make_shard(family: str, m_local: int, n: int, device: torch.device, rank: int, m_total: int
+               ) -> Tuple[np.ndarray, Optional[np.ndarray]]:
     seed = 1000 + rank
     if family == "low_rank_matrix":
         X = datagen.low_rank_matrix(m_local, n, device, seed=seed, m_total=m_total)

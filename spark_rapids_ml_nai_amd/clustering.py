@@ -15,7 +15,7 @@ from typing import Any, Callable, Dict, List, Optional, Tuple, Union
 import numpy as np
 import torch
 
-from .core.base import FitInput, _Estimator, _ModelWithPredictionCol, _Model
+from .core.base import FitInput, _Estimator, _ModelWithPredictionCol
 from .core.dataframe import DataFrame
 from .core.linalg import as_dense_array
 from .core.params import (

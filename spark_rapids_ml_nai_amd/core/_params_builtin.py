@@ -74,7 +74,7 @@ class TypeConverters:
 
     @staticmethod
     def toVector(value: Any) -> Any:
-        from .linalg import DenseVector, Vectors
+        from .linalg import Vectors
 
         if hasattr(value, "toArray") and hasattr(value, "size"):
             return value

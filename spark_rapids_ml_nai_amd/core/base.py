@@ -18,24 +18,16 @@ Re-design of the reference's framework core (``core.py:426-1647``):
 """
 from __future__ import annotations
 
-import logging
 import os
 import threading
 from abc import abstractmethod
 from dataclasses import dataclass, field
-from typing import Any, Callable, Dict, Iterator, List, Optional, Sequence, Tuple, Type, Union
+from typing import Any, Callable, Dict, Iterator, List, Optional, Sequence, Tuple, Union
 
 import numpy as np
 import torch
 
-from ..parallel.context import (
-    PartitionDescriptor,
-    WorkerContext,
-    current_context,
-    gpu_available,
-    spmd_active,
-    use_context,
-)
+from ..parallel.context import PartitionDescriptor, WorkerContext, current_context, spmd_active, use_context
 from ..utils.log import get_logger
 from ..utils.timer import PhaseTimer
 import pyarrow as pa
@@ -552,7 +544,8 @@ class _Model(_CommonBase, *_MODEL_BASES):  # type: ignore[misc]
     def _transform_features(self, part: DataFrame) -> Any:
         col, cols = self._transform_input_cols()
         dt = self._transform_dtype()
-        if col is not None and part.is_vector(col) and self._transform_supports_sparse() and vector_column_is_sparse(part.column(col)):
+        if (col is not None and part.is_vector(col) and self._transform_supports_sparse()
+                and vector_column_is_sparse(part.column(col))):
             return vector_column_to_csr(part.column(col), dt)
         return _dense_from_df(part, col, cols, dt)
 

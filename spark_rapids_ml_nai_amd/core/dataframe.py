@@ -15,7 +15,7 @@ its tests use: ``columns``, ``schema``, ``select``, ``withColumn``, ``drop``, ``
 """
 from __future__ import annotations
 
-from typing import Any, Callable, Dict, Iterable, List, Optional, Sequence, Tuple, Union
+from typing import Any, Dict, List, Optional, Sequence, Tuple, Union
 
 import numpy as np
 import pandas as pd

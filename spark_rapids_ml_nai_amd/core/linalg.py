@@ -51,7 +51,7 @@ except Exception:  # noqa: BLE001
         def __getitem__(self, i: Any) -> Any:
             return self.array[i]
 
-        def __iter__(self):  # type: ignore[no-untyped-def]
+        def __iter__(self) -> Any:
             return iter(self.array)
 
         def dot(self, other: Any) -> float:

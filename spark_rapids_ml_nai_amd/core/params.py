@@ -20,7 +20,6 @@ import os
 import warnings
 from typing import Any, Callable, Dict, Iterable, List, Optional, Tuple, TypeVar, Union
 
-import numpy as np
 
 __all__ = [
     "Param",

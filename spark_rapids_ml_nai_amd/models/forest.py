@@ -24,7 +24,6 @@ RCCL — the north-star mode for datasets larger than one GPU's share).
 """
 from __future__ import annotations
 
-import json
 import math
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Tuple

@@ -22,7 +22,7 @@ with q = sigma (standardization=True) or 1, intercepts unpenalised.
 """
 from __future__ import annotations
 
-from typing import Any, Dict, List, Optional, Tuple
+from typing import Any, Dict, Optional
 
 import numpy as np
 import torch

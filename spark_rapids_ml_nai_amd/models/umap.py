@@ -38,7 +38,7 @@ def find_ab_params(spread: float, min_dist: float) -> Tuple[float, float]:
     """Fit 1 / (1 + a x^(2b)) to the target membership curve (umap-learn ``find_ab_params``)."""
     from scipy.optimize import curve_fit
 
-    def curve(x, a, b):
+    def curve(x: Any, a: float, b: float) -> Any:
         return 1.0 / (1.0 + a * x ** (2 * b))
 
     xv = np.linspace(0, spread * 3, 300)
@@ -124,7 +124,7 @@ def membership_strengths(idx: torch.Tensor, dist: torch.Tensor, sigma: torch.Ten
     return w.float()
 
 
-def _coalesce(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n: int):
+def _coalesce(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n: int) -> Tuple[Any, Any, Any, int]:
     key = rows.long() * n + cols.long()
     uk, inv = torch.unique(key, return_inverse=True)
     return uk // n, uk % n, inv, uk.numel()
@@ -149,7 +149,8 @@ def fuzzy_union(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n: i
 
 
 def categorical_intersection(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, y: torch.Tensor,
-                             n: int, unknown_dist: float = 1.0, far_dist: float = 5.0):
+                             n: int, unknown_dist: float = 1.0, far_dist: float = 5.0
+                             ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     yr, yc = y[rows], y[cols]
     unknown = (yr == -1) | (yc == -1)
     differ = (yr != yc) & ~unknown

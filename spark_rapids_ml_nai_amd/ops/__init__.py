@@ -5,7 +5,7 @@ the numerics oracle in the kernel tests).
 from __future__ import annotations
 
 import math
-from typing import Dict, Optional, Tuple
+from typing import Any, Dict, Iterator, Optional, Tuple
 
 import numpy as np
 import torch
@@ -981,7 +981,7 @@ def _tri_decode(t: int) -> Tuple[int, int]:
     return i, t - i * (i + 1) // 2
 
 
-def _db_tiles(X: torch.Tensor, xnorm: torch.Tensor, eps2: float, t0: int, t1: int):
+def _db_tiles(X: torch.Tensor, xnorm: torch.Tensor, eps2: float, t0: int, t1: int) -> Iterator[Any]:
     """CPU reference: yields (r0, c0, masked squared distances) per tile pair of the range."""
     N = X.shape[0]
     for t in range(t0, t1):

@@ -683,7 +683,8 @@ __global__ __launch_bounds__(256) void rf_predict_lds_kernel(const float* __rest
     const bool active = r < m;
     if (active) {
       const float* row = X + r * ld;
-      for (int c = lane * 4; c < npad; c += 256) *reinterpret_cast<floatx4*>(&srow[c]) = *reinterpret_cast<const floatx4*>(row + c);
+      for (int c = lane * 4; c < npad; c += 256)
+        *reinterpret_cast<floatx4*>(&srow[c]) = *reinterpret_cast<const floatx4*>(row + c);
     }
     __syncthreads();
     if (active) {

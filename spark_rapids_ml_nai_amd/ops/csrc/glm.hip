@@ -434,7 +434,8 @@ SRML_API int srml_logreg_binary2_f32(const float* X, long m, int n, long ld, con
   if (rpb < 16) rpb = 16;
   blocks = (m + rpb - 1) / rpb;
   int V = (n + 255) / 256;
-  size_t lds = 256 * (size_t)(V <= 1 ? 1 : V <= 2 ? 2 : V <= 4 ? 4 : V <= 8 ? 8 : V <= 12 ? 12 : 16) * (sizeof(double) + sizeof(float));
+  const size_t vpad = V <= 1 ? 1 : V <= 2 ? 2 : V <= 4 ? 4 : V <= 8 ? 8 : V <= 12 ? 12 : 16;
+  size_t lds = 256 * vpad * (sizeof(double) + sizeof(float));
   dim3 grid((unsigned)blocks), blk(256);
   static const int split = getenv("SRML_LOGREG_SPLIT") ? atoi(getenv("SRML_LOGREG_SPLIT")) : 2;
   // prefetching column-split kernel: needs 16-B aligned rows and n % 4 == 0 (no tail columns)
@@ -452,9 +453,13 @@ SRML_API int srml_logreg_binary2_f32(const float* X, long m, int n, long ld, con
     else if (rsel == 2) SRML_LR_PF_V(2, 2);
     else if (dsel == 1) SRML_LR_PF_V(1, 1);
     else if (dsel == 3 && nt) {
-      if (VS == 2) hipLaunchKernelGGL((logreg_binary_pf_kernel<2, 1, 3, true>), grid, blk, 0, stream, X, m, n, ld, y, w, b, bptr, flag, out, rpb);
-      else if (VS == 3) hipLaunchKernelGGL((logreg_binary_pf_kernel<3, 1, 3, true>), grid, blk, 0, stream, X, m, n, ld, y, w, b, bptr, flag, out, rpb);
-      else hipLaunchKernelGGL((logreg_binary_pf_kernel<4, 1, 3, true>), grid, blk, 0, stream, X, m, n, ld, y, w, b, bptr, flag, out, rpb);
+#define SRML_LR_PF_NT(VV)                                                                                        \
+  hipLaunchKernelGGL((logreg_binary_pf_kernel<VV, 1, 3, true>), grid, blk, 0, stream, X, m, n, ld, y, w, b, bptr, \
+                     flag, out, rpb)
+      if (VS == 2) SRML_LR_PF_NT(2);
+      else if (VS == 3) SRML_LR_PF_NT(3);
+      else SRML_LR_PF_NT(4);
+#undef SRML_LR_PF_NT
     }
     else if (dsel == 3) SRML_LR_PF_V(1, 3);
     else SRML_LR_PF_V(1, 2);

@@ -215,8 +215,9 @@ static int csr_logreg_launch(const long* indptr, const int* indices, const T* da
   if (m <= 0) return 0;
   const int G = pick_group(m, nnz);
   const dim3 grid(grid_for(m, G)), blk(256);
-#define SRML_CSR_LR(GG) \
-  hipLaunchKernelGGL((csr_logreg_binary_kernel<T, GG>), grid, blk, 0, s, indptr, indices, data, m, y, w, b, bptr, flag, grad, tail)
+#define SRML_CSR_LR(GG)                                                                                           \
+  hipLaunchKernelGGL((csr_logreg_binary_kernel<T, GG>), grid, blk, 0, s, indptr, indices, data, m, y, w, b, bptr, flag, \
+                     grad, tail)
   switch (G) {
     case 4: SRML_CSR_LR(4); break;
     case 8: SRML_CSR_LR(8); break;
@@ -231,13 +232,16 @@ static int csr_logreg_launch(const long* indptr, const int* indices, const T* da
 template <typename T, int K>
 static void csr_spmm_k(int G, dim3 grid, hipStream_t s, const long* indptr, const int* indices, const T* data, long m,
                        const float* W, int kk, const float* bias, float* Z) {
+#define SRML_CSR_MM(GG) \
+  hipLaunchKernelGGL((csr_spmm_kernel<T, GG, K>), grid, dim3(256), 0, s, indptr, indices, data, m, W, kk, bias, Z)
   switch (G) {
-    case 4: hipLaunchKernelGGL((csr_spmm_kernel<T, 4, K>), grid, dim3(256), 0, s, indptr, indices, data, m, W, kk, bias, Z); break;
-    case 8: hipLaunchKernelGGL((csr_spmm_kernel<T, 8, K>), grid, dim3(256), 0, s, indptr, indices, data, m, W, kk, bias, Z); break;
-    case 16: hipLaunchKernelGGL((csr_spmm_kernel<T, 16, K>), grid, dim3(256), 0, s, indptr, indices, data, m, W, kk, bias, Z); break;
-    case 32: hipLaunchKernelGGL((csr_spmm_kernel<T, 32, K>), grid, dim3(256), 0, s, indptr, indices, data, m, W, kk, bias, Z); break;
-    default: hipLaunchKernelGGL((csr_spmm_kernel<T, 64, K>), grid, dim3(256), 0, s, indptr, indices, data, m, W, kk, bias, Z); break;
+    case 4: SRML_CSR_MM(4); break;
+    case 8: SRML_CSR_MM(8); break;
+    case 16: SRML_CSR_MM(16); break;
+    case 32: SRML_CSR_MM(32); break;
+    default: SRML_CSR_MM(64); break;
   }
+#undef SRML_CSR_MM
 }
 
 template <typename T, int K>

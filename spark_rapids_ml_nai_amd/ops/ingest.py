@@ -11,7 +11,7 @@ from __future__ import annotations
 import os
 
 import warnings
-from typing import Any, Optional
+from typing import Any, Iterator, Optional
 
 import numpy as np
 import torch
@@ -89,7 +89,7 @@ def _ingest_threads() -> int:
     return max(1, int(os.environ.get("SRML_INGEST_THREADS", str(min(8, os.cpu_count() or 1)))))
 
 
-def _thread_pool():
+def _thread_pool() -> Any:
     global _pool
     from concurrent.futures import ThreadPoolExecutor
 
@@ -150,7 +150,7 @@ def parts_to_device(parts: Any, device: torch.device, dtype: Optional[torch.dtyp
     return out
 
 
-def _staged_fill(blocks: list, out: torch.Tensor, device: torch.device, cs: "torch.cuda.Stream"):
+def _staged_fill(blocks: list, out: torch.Tensor, device: torch.device, cs: "torch.cuda.Stream") -> Iterator[Any]:
     """Generator: fill the pinned ring slot by slot from the row blocks (threaded copies, cast on
     the fly), DMA each slot into ``out`` on ``cs``; yields (row0, row1, event) per slot."""
     rows, n = out.shape
@@ -222,7 +222,7 @@ class StreamedParts:
         self._gen = _staged_fill(blocks, self.X, device, self._copy)
         self._last = None
 
-    def chunks(self):
+    def chunks(self) -> Iterator[Any]:
         cur = torch.cuda.current_stream(self.device)
         for r0, r1, ev in self._gen:
             self._last = ev
@@ -331,7 +331,7 @@ class StreamedRows:
                 self.bounds.append((r0, r1))
                 self.events.append(ev)
 
-    def chunks(self):
+    def chunks(self) -> Iterator[Any]:
         cur = torch.cuda.current_stream(self.device)
         for (r0, r1), ev in zip(self.bounds, self.events):
             cur.wait_event(ev)

@@ -18,7 +18,7 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
-from typing import Any, List, Optional
+from typing import Any, List
 
 import numpy as np
 import torch

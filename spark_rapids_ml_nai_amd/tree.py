@@ -10,7 +10,7 @@ form (flat breadth-first node arrays) instead of a pickled treelite handle.
 """
 from __future__ import annotations
 
-from typing import Any, Callable, Dict, List, Optional, Tuple, Union
+from typing import Any, Callable, Dict, List, Optional, Union
 
 import numpy as np
 import torch

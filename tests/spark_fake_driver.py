@@ -59,7 +59,8 @@ def main() -> None:
     out["kmeans_centers"] = len(km.clusterCenters())
     pca = PCA(k=2, num_workers=2, inputCol="features", outputCol="pca").fit(sdf(X, None))
     pca_local = PCA(k=2, num_workers=1, inputCol="features").fit(SRDF.from_numpy(X))
-    out["pca_comp_maxdiff"] = float(np.abs(np.abs(np.asarray(pca.components_)) - np.abs(np.asarray(pca_local.components_))).max())
+    comp_diff = np.abs(np.asarray(pca.components_)) - np.abs(np.asarray(pca_local.components_))
+    out["pca_comp_maxdiff"] = float(np.abs(comp_diff).max())
     rf = RandomForestClassifier(numTrees=4, maxDepth=5, seed=3, num_workers=2).fit(sdf(X, yc))
     out["rf_trees"] = rf.getNumTrees
 

@@ -2,7 +2,6 @@
 test_linear_model.py:389-490, test_logistic_regression.py:441-600). Expected values are the ones
 Apache Spark (and the reference) produce on the same inputs. Each check runs on the CPU path
 (CI) and, marked ``gpu``, through the HIP kernels on an MI355X."""
-import os
 import warnings
 
 import numpy as np

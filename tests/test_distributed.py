@@ -2,7 +2,6 @@
 the same worker closures that run one-rank-per-MI355X over RCCL. Oracle: the single-rank fit on
 the same data (reference test strategy: multi-GPU vs single-GPU cuML, tests/test_pca.py:307-355,
 tests/test_kmeans.py:257-330, tests/test_random_forest.py:322-417)."""
-import os
 import warnings
 
 import numpy as np

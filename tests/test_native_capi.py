@@ -1,6 +1,5 @@
 """C ABI / JNI-parity layer (reference jvm/native/src/rapidsml_jni.cu) and the
 device Jacobi eigensolver. Oracle: numpy fp64."""
-import os
 import subprocess
 
 import numpy as np

@@ -145,7 +145,8 @@ def test_nearest_centroid_split(gpu_device, m, n, k):
     assert torch.all((dist.double().cpu() - ref_d).abs() <= 1e-5 * scale + 1e-3)
 
 
-@pytest.mark.parametrize("m,n,k", [(5000, 16, 20), (20000, 3000, 50), (3000, 64, 200), (5000, 301, 300), (70000, 1024, 1000)])
+@pytest.mark.parametrize("m,n,k", [(5000, 16, 20), (20000, 3000, 50), (3000, 64, 200), (5000, 301, 300),
+                                   (70000, 1024, 1000)])
 def test_cluster_sums(gpu_device, m, n, k):
     X = _rand(m, n, gpu_device, seed=15)
     labels = torch.randint(0, k, (m,), generator=torch.Generator().manual_seed(4)).int()
@@ -158,7 +159,8 @@ def test_cluster_sums(gpu_device, m, n, k):
 def _rf_setup(dev, m=5000, n=40, B=32, C=3, seed=0):
     g = torch.Generator().manual_seed(seed)
     X = torch.randn(m, n, generator=g)
-    edges = torch.sort(X[torch.randperm(m, generator=g)[:1000]], 0).values[torch.linspace(30, 970, B - 1).long()].T.contiguous()
+    sample = torch.sort(X[torch.randperm(m, generator=g)[:1000]], 0).values
+    edges = sample[torch.linspace(30, 970, B - 1).long()].T.contiguous()
     y = torch.randint(0, C, (m,), generator=g).float()
     return X, edges, y
 
@@ -325,7 +327,8 @@ def test_knn_id_offset(gpu_device):
     assert torch.equal(i0 + 1000, i1)
 
 
-@pytest.mark.parametrize("n,nlist,nprobe,k", [(16, 10, 3, 10), (130, 32, 8, 5), (3, 5, 5, 64), (128, 40, 6, 10), (64, 20, 4, 7), (33, 12, 3, 1)])
+@pytest.mark.parametrize("n,nlist,nprobe,k", [(16, 10, 3, 10), (130, 32, 8, 5), (3, 5, 5, 64), (128, 40, 6, 10),
+                                              (64, 20, 4, 7), (33, 12, 3, 1)])
 def test_ivf_search(gpu_device, n, nlist, nprobe, k):
     from spark_rapids_ml_nai_amd.models.knn import build_ivf
 
@@ -610,7 +613,8 @@ def test_rf_many_classes(gpu_device, classes, bins):
     centers = g.standard_normal((classes, n)) * 3
     y = g.integers(0, classes, m)
     X = (centers[y] + g.standard_normal((m, n))).astype(np.float32)
-    model = RandomForestClassifier(numTrees=4, maxDepth=8, maxBins=bins, seed=1).fit(DataFrame.from_numpy(X, y.astype(np.float64)))
+    model = RandomForestClassifier(numTrees=4, maxDepth=8, maxBins=bins, seed=1).fit(
+        DataFrame.from_numpy(X, y.astype(np.float64)))
     pred = model.transform(DataFrame.from_numpy(X, y.astype(np.float64))).to_numpy("prediction")
     assert (pred == y).mean() > 0.8
 

@@ -11,6 +11,9 @@ C = (Xc.T @ Xc) / (X.shape[0] - 1)
 del X, Xc
 topk_eigh(C, 3); torch.cuda.synchronize()
 for _ in range(3):
-    t0 = time.perf_counter(); w, V = topk_eigh(C, 3); torch.cuda.synchronize(); print("eig s", round(time.perf_counter() - t0, 4), w)
+    t0 = time.perf_counter()
+    w, V = topk_eigh(C, 3)
+    torch.cuda.synchronize()
+    print("eig s", round(time.perf_counter() - t0, 4), w)
 pr = cProfile.Profile(); pr.enable(); topk_eigh(C, 3); torch.cuda.synchronize(); pr.disable()
 out = io.StringIO(); pstats.Stats(pr, stream=out).sort_stats("tottime").print_stats(12); print(out.getvalue()[:3000])
