@@ -207,28 +207,48 @@ def _cholqr2(Y: torch.Tensor) -> torch.Tensor:
 
 
 def _spectral_device(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n: int, dim: int, seed: int,
-                     iters: int = 300) -> torch.Tensor:
+                     iters: int = 300, tol: float = 1e-8, min_iters: int = 20) -> torch.Tensor:
     """Top eigenvectors of D^-1/2 A D^-1/2 by subspace iteration: the SpMM is the in-tree CSR
-    kernel (``ops.csr_spmm``, one row group per graph row), orthonormalisation is CholeskyQR2."""
+    kernel (``ops.csr_spmm``, one row group per graph row), orthonormalisation is CholeskyQR2.
+    The (row, col)-sorted union edges ARE the CSR (no sparse-tensor coalesce); the iteration
+    stops once the Ritz values of the leading dim + 1 directions move by <= ``tol`` (checked at
+    every re-orthonormalisation, from the product the next step needs anyway) — umap-learn's
+    eigsh runs at tol 1e-4 and the layout only needs a starting point."""
     from ..core.base import CSR
 
     dev = vals.device
-    deg = torch.zeros(n, dtype=torch.float64, device=dev).index_add_(0, rows.long(), vals.double())
+    r64 = rows.long()
+    if r64.numel() > 1 and not bool((r64[1:] >= r64[:-1]).all()):
+        order = torch.argsort(r64 * n + cols.long())
+        r64, cols, vals = r64[order], cols[order], vals[order]
+    deg = torch.zeros(n, dtype=torch.float64, device=dev).index_add_(0, r64, vals.double())
     dinv = 1.0 / torch.sqrt(deg.clamp_min(1e-30))
-    mv = (dinv[rows.long()] * vals.double() * dinv[cols.long()]).float()
-    Mt = torch.sparse_coo_tensor(torch.stack([rows.long(), cols.long()]), mv, (n, n)).coalesce().to_sparse_csr()
-    M = CSR(indptr=Mt.crow_indices().to(torch.int64).contiguous(), indices=Mt.col_indices().to(torch.int32).contiguous(),
-            data=Mt.values().contiguous(), shape=(n, n))
-    del Mt
+    mv = (dinv[r64] * vals.double() * dinv[cols.long()]).float().contiguous()
+    indptr = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(torch.bincount(r64, minlength=n), 0, out=indptr[1:])
+    M = CSR(indptr=indptr, indices=cols.to(torch.int32).contiguous(), data=mv, shape=(n, n))
     p = min(n, dim + 1 + 8)
     g = torch.Generator(device="cpu").manual_seed(int(seed))
     Y = torch.randn(n, p, generator=g).to(dev)
     Y[:, 0] = torch.sqrt(deg).float()
     Y = _cholqr2(Y)
-    for it in range(iters):
-        Y = 0.5 * (ops.csr_spmm(M, Y) + Y)  # (M + I) / 2: eigenvalues in [0, 1], order kept
-        if it % 5 == 4 or it == iters - 1:
+    prev = None
+    it = 0
+    while it < iters:
+        Z = 0.5 * (ops.csr_spmm(M, Y) + Y)  # (M + I) / 2: eigenvalues in [0, 1], order kept
+        it += 1
+        if it % 5 == 1:  # Y is orthonormal here: Ritz values of the current subspace
+            T = ops.dgemm(Y.double().contiguous(), Z.double().contiguous(), ta=True).cpu().numpy()
+            ritz = np.sort(np.linalg.eigvalsh((T + T.T) * 0.5))[::-1][: dim + 1]
+            if prev is not None and it >= min_iters and \
+                    np.max(np.abs(ritz - prev)) <= tol * max(float(np.max(np.abs(ritz))), 1e-30):
+                Y = Z
+                break
+            prev = ritz
+        Y = Z
+        if it % 5 == 0:
             Y = _cholqr2(Y)
+    Y = _cholqr2(Y)
     Z = 0.5 * (ops.csr_spmm(M, Y) + Y)
     # Y^T Z: K = n rows in the millions -> the split-K fp64 MFMA GEMM (ordered fold)
     Yd = Y.double().contiguous()

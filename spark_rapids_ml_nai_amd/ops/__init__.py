@@ -384,15 +384,26 @@ def _uniform01(seed: int, ctr: int) -> float:
 KMEANSPP_MAX_CANDIDATES = 8192  # KPP_T * KPP_PER in csrc/kmeans.hip
 
 
-def kmeanspp_gram(G: torch.Tensor, w: torch.Tensor, k: int, seed: int) -> torch.Tensor:
-    """Weighted k-means++ seeding (indices of k candidates) from the candidates' Gram matrix
-    G = C C^T: pick 0 ~ w, then pick t ~ w_i min_j<t ||c_i - c_j||^2. GPU: one block, no host
-    round trip per pick; CPU: the same draws (same counter-based uniforms) in numpy."""
+KMEANSPP_MAX_TRIALS = 16
+
+
+def kmeanspp_trials(k: int) -> int:
+    """Greedy k-means++ candidates per centre (scikit-learn / cuML: 2 + floor(ln k))."""
+    return int(min(KMEANSPP_MAX_TRIALS, 2 + int(math.log(max(k, 1)))))
+
+
+def kmeanspp_gram(G: torch.Tensor, w: torch.Tensor, k: int, seed: int, trials: Optional[int] = None) -> torch.Tensor:
+    """Greedy weighted k-means++ seeding (indices of k candidates) from the candidates' Gram matrix
+    G = C C^T: pick 0 ~ w; every later pick draws ``trials`` candidates ~ w_i min_j ||c_i - c_j||^2
+    and keeps the one with the lowest resulting potential. GPU: one block, no host round trip
+    per pick; CPU: the same draws (same counter-based uniforms) in numpy."""
     nc = G.shape[0]
     seed = int(seed) & _M64
+    L = int(trials) if trials is not None else kmeanspp_trials(k)
+    L = max(1, min(L, KMEANSPP_MAX_TRIALS))
     if G.is_cuda and nc <= KMEANSPP_MAX_CANDIDATES:
         out = torch.empty(k, dtype=torch.int32, device=G.device)
-        native.call("srml_kmeanspp_gram", _c(G.double()).data_ptr(), nc, _c(w.double()).data_ptr(), int(k), seed,
+        native.call("srml_kmeanspp_gram", _c(G.double()).data_ptr(), nc, _c(w.double()).data_ptr(), int(k), L, seed,
                     out.data_ptr(), native.stream(G.device))
         return out.long()
     Gh = G.double().cpu().numpy()
@@ -412,8 +423,13 @@ def kmeanspp_gram(G: torch.Tensor, w: torch.Tensor, k: int, seed: int) -> torch.
     picks = [c]
     for t in range(1, k):
         d2 = np.minimum(d2, np.maximum(diag + Gh[c, c] - 2.0 * Gh[c], 0.0))
-        nx = draw(wh * d2, t)
-        c = nx if nx >= 0 else int(_splitmix64((seed + 77 * t) & _M64) % nc)
+        p = wh * d2
+        cands = [draw(p, t * KMEANSPP_MAX_TRIALS + j) for j in range(L)]
+        if cands[0] < 0:
+            c = int(_splitmix64((seed + 77 * t) & _M64) % nc)
+        else:
+            pots = [float((wh * np.minimum(d2, np.maximum(diag + Gh[x, x] - 2.0 * Gh[x], 0.0))).sum()) for x in cands]
+            c = cands[int(np.argmin(pots))]
         picks.append(c)
     return torch.tensor(picks, dtype=torch.long, device=G.device)
 

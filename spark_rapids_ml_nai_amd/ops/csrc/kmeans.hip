@@ -674,10 +674,13 @@ __device__ __forceinline__ double uniform01(unsigned long long seed, unsigned lo
 }
 
 constexpr int KPP_T = 1024;
-constexpr int KPP_PER = 8;   // candidates per thread (nc <= 8192)
+constexpr int KPP_PER = 8;     // candidates per thread (nc <= 8192)
+constexpr int KPP_TRIALS = 16; // max greedy trials per centre
 
-// block-wide sample: returns the smallest i with prefix(p)[i] > u * total (p >= 0), or -1 if total == 0
-__device__ int kpp_sample(const double (&p)[KPP_PER], int base, int cnt, double u, double* lds, int* pick) {
+// block-wide inverse-CDF draws of L targets u[j] * total over p >= 0 (candidate base + q of the
+// thread that owns the target's half-open prefix range); picks[j] = -1 if total == 0
+__device__ void kpp_sample(const double (&p)[KPP_PER], int base, int cnt, const double* u, int L, double* lds,
+                           int* picks) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   double loc = 0.0;
 #pragma unroll
@@ -690,7 +693,7 @@ __device__ int kpp_sample(const double (&p)[KPP_PER], int base, int cnt, double 
     if (lane >= o) x += y;
   }
   if (lane == 63) lds[wid] = x;
-  if (threadIdx.x == 0) *pick = -1;
+  if (threadIdx.x < L) picks[threadIdx.x] = -1;
   __syncthreads();
   double wave_off = 0.0, total = 0.0;
   for (int w = 0; w < KPP_T / 64; ++w) {
@@ -699,33 +702,41 @@ __device__ int kpp_sample(const double (&p)[KPP_PER], int base, int cnt, double 
     total += v;
   }
   const double excl = wave_off + x - loc;  // sum of all candidates before this thread's
-  const double target = u * total;
-  if (total > 0.0 && excl <= target && target < excl + loc) {
-    double run = excl;
-    int hit = cnt - 1;
-    for (int q = 0; q < cnt; ++q) {
-      run += p[q];
-      if (target < run) { hit = q; break; }
+  for (int j = 0; j < L; ++j) {
+    const double target = u[j] * total;
+    if (total > 0.0 && excl <= target && target < excl + loc) {
+      double run = excl;
+      int hit = cnt - 1;
+      for (int q = 0; q < cnt; ++q) {
+        run += p[q];
+        if (target < run) { hit = q; break; }
+      }
+      picks[j] = base + hit;  // exactly one thread owns the target (half-open ranges)
     }
-    *pick = base + hit;  // exactly one thread owns the target (half-open ranges)
   }
   __syncthreads();
-  int r = *pick;
-  if (total > 0.0 && r < 0) {  // rounding at the very top of the range: last positive candidate
-    __syncthreads();
-    if (loc > 0.0) atomicMax(pick, base + cnt - 1);
-    __syncthreads();
-    r = *pick;
+  for (int j = 0; j < L; ++j) {  // rounding at the very top of the range: last positive candidate
+    if (total > 0.0 && picks[j] < 0) {
+      __syncthreads();
+      if (loc > 0.0) atomicMax(&picks[j], base + cnt - 1);
+      __syncthreads();
+    }
   }
   __syncthreads();
-  return r;
 }
 
+// Greedy weighted k-means++ (the reduction step of k-means||, as cuML / scikit-learn run it):
+// centre 0 ~ w; every later centre draws L candidates ~ w_i d2_i and keeps the one that lowers
+// the potential sum_i w_i min(d2_i, ||c_i - cand||^2) the most (single-draw k-means++ merged two
+// of eight separated blobs in ~1 of 4 seeds). Distances from the Gram matrix G = C C^T.
 __global__ __launch_bounds__(KPP_T) void kmeanspp_gram_kernel(const double* __restrict__ G, int nc,
-                                                              const double* __restrict__ w, int k,
+                                                              const double* __restrict__ w, int k, int L,
                                                               unsigned long long seed, int* __restrict__ out) {
   __shared__ double lds[KPP_T / 64];
-  __shared__ int pick;
+  __shared__ double pot[KPP_T / 64][KPP_TRIALS];
+  __shared__ double u[KPP_TRIALS];
+  __shared__ int picks[KPP_TRIALS];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int base = threadIdx.x * KPP_PER;
   const int cnt = max(0, min(KPP_PER, nc - base));
   double d2[KPP_PER], wv[KPP_PER], gii[KPP_PER], p[KPP_PER];
@@ -738,8 +749,10 @@ __global__ __launch_bounds__(KPP_T) void kmeanspp_gram_kernel(const double* __re
     d2[q] = INFINITY;
     p[q] = wv[q];
   }
-  int c = kpp_sample(p, base, cnt, uniform01(seed, 0), lds, &pick);
-  if (c < 0) c = 0;
+  if (threadIdx.x == 0) u[0] = uniform01(seed, 0);
+  __syncthreads();
+  kpp_sample(p, base, cnt, u, 1, lds, picks);
+  int c = picks[0] < 0 ? 0 : picks[0];
   if (threadIdx.x == 0) out[0] = c;
   for (int t = 1; t < k; ++t) {
     const double gcc = G[(long)c * nc + c];
@@ -752,17 +765,43 @@ __global__ __launch_bounds__(KPP_T) void kmeanspp_gram_kernel(const double* __re
         p[q] = wv[q] * d2[q];
       }
     }
-    int nx = kpp_sample(p, base, cnt, uniform01(seed, (unsigned long long)t), lds, &pick);
-    if (nx < 0) nx = (int)(splitmix64(seed + 77 * t) % (unsigned long long)nc);  // all mass on chosen points
-    c = nx;
+    __syncthreads();  // picks / u of the previous step fully consumed
+    if (threadIdx.x < L) u[threadIdx.x] = uniform01(seed, (unsigned long long)t * KPP_TRIALS + threadIdx.x);
+    __syncthreads();
+    kpp_sample(p, base, cnt, u, L, lds, picks);
+    if (picks[0] < 0) {  // all mass on chosen points: any candidate
+      c = (int)(splitmix64(seed + 77 * t) % (unsigned long long)nc);
+    } else {
+      // potential of each trial: one pass over this thread's candidates per trial, block-reduced
+      for (int j = 0; j < L; ++j) {
+        const int tj = picks[j];
+        const double gtt = G[(long)tj * nc + tj];
+        const double* gt = G + (long)tj * nc;
+        double s = 0.0;
+#pragma unroll
+        for (int q = 0; q < KPP_PER; ++q)
+          if (q < cnt) s += wv[q] * fmin(d2[q], fmax(gii[q] + gtt - 2.0 * gt[base + q], 0.0));
+        s = wave_sum(s);
+        if (lane == 0) pot[wid][j] = s;
+      }
+      __syncthreads();
+      int best = 0;
+      double bv = INFINITY;
+      for (int j = 0; j < L; ++j) {
+        double tot = 0.0;
+        for (int v = 0; v < KPP_T / 64; ++v) tot += pot[v][j];
+        if (tot < bv) { bv = tot; best = j; }
+      }
+      c = picks[best];
+    }
     if (threadIdx.x == 0) out[t] = c;
   }
 }
 
-SRML_API int srml_kmeanspp_gram(const double* G, int nc, const double* w, int k, unsigned long long seed, int* out,
-                                hipStream_t stream) {
+SRML_API int srml_kmeanspp_gram(const double* G, int nc, const double* w, int k, int trials, unsigned long long seed,
+                                int* out, hipStream_t stream) {
   if (nc <= 0 || k <= 0) return 0;
-  if (nc > KPP_T * KPP_PER) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(kmeanspp_gram_kernel, dim3(1), dim3(KPP_T), 0, stream, G, nc, w, k, seed, out);
+  if (nc > KPP_T * KPP_PER || trials < 1 || trials > KPP_TRIALS) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(kmeanspp_gram_kernel, dim3(1), dim3(KPP_T), 0, stream, G, nc, w, k, trials, seed, out);
   return srml_status();
 }

@@ -50,12 +50,15 @@ def _child(rank: int, world: int, port: int, use_gpu: bool, payload: bytes, q: A
             from .context import bind_numa_local
 
             bind_numa_local(device)
+        # RCCL needs one device per rank: more workers than visible GPUs (ranks sharing a device,
+        # e.g. num_workers=2 on a one-GPU box) run their collectives over gloo instead
+        rccl = device.type == "cuda" and world <= torch.cuda.device_count()
         dist.init_process_group(
-            "nccl" if device.type == "cuda" else "gloo",
+            "nccl" if rccl else "gloo",
             rank=rank,
             world_size=world,
             timeout=timedelta(seconds=comm_timeout(timeout_s)),
-            **({"device_id": device} if device.type == "cuda" else {}),
+            **({"device_id": device} if rccl else {}),
         )
         ctx = WorkerContext.from_process_group(device)
         fn, inp = cloudpickle.loads(payload)
