@@ -177,21 +177,22 @@ class LogisticRegression(LogisticRegressionClass, _EstimatorSupervised, _Logisti
     def _get_fit_func(self, dataset: DataFrame, extra_params: Optional[List[Dict[str, Any]]] = None) -> Callable:
         def _fit(inp: FitInput, ctx: WorkerContext, params: Dict[str, Any]) -> Any:
             from .core.base import CSR
-            from .models.logistic import logistic_fit, logistic_stats
+            from .models.logistic import logistic_fit_multi, logistic_stats
 
             sparse = isinstance(inp.X, CSR)
             stats = logistic_stats(inp.X, inp.y, inp.desc.m, ctx, sparse)
             init = params["cuml_init"]
             maps = params["fit_multiple_params"] or [{}]
-            out = []
+            settings = []
             for mp in maps:
                 p = dict(init, **mp)
                 C = float(p["C"])
-                reg = 0.0 if C == 0.0 else 1.0 / C
-                l1 = float(p["l1_ratio"]) if p.get("l1_ratio") is not None else 0.0
-                out.append(logistic_fit(inp.X, inp.y, inp.desc.m, ctx, reg, l1, bool(p["fit_intercept"]),
-                                        bool(p["standardization"]), int(p["max_iter"]), float(p["tol"]),
-                                        sparse=sparse, stats=stats))
+                settings.append({"reg": 0.0 if C == 0.0 else 1.0 / C,
+                                 "l1_ratio": float(p["l1_ratio"]) if p.get("l1_ratio") is not None else 0.0,
+                                 "fit_intercept": bool(p["fit_intercept"]), "standardization": bool(p["standardization"]),
+                                 "max_iter": int(p["max_iter"]), "tol": float(p["tol"])})
+            # one setting: the single-model path; several: batched passes over X (hyper-parameter batching)
+            out = logistic_fit_multi(inp.X, inp.y, inp.desc.m, ctx, settings, sparse=sparse, stats=stats)
             return out if params["fit_multiple_params"] else out[0]
 
         return _fit

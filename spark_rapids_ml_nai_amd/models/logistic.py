@@ -22,7 +22,7 @@ with q = sigma (standardization=True) or 1, intercepts unpenalised.
 """
 from __future__ import annotations
 
-from typing import Any, Dict, Optional
+from typing import Any, Dict, List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -32,27 +32,11 @@ from ..parallel.context import WorkerContext
 from .qn import QNProblem, minimize
 
 
-def logistic_fit(X: Any, y: torch.Tensor, m_total: int, ctx: WorkerContext, reg: float, l1_ratio: float,
-                 fit_intercept: bool, standardization: bool, max_iter: int, tol: float,
-                 n_classes: Optional[int] = None, sparse: bool = False,
-                 stats: Optional[Dict[str, Any]] = None) -> Dict[str, Any]:
-    n = X.shape[1]
-    if stats is None:
-        stats = logistic_stats(X, y, m_total, ctx, sparse)
-    classes = stats["classes"]
+def _problem(n: int, m_total: int, stats: Dict[str, Any], reg: float, l1_ratio: float, fit_intercept: bool,
+             standardization: bool, max_iter: int, tol: float, K: int) -> Tuple[QNProblem, np.ndarray, np.ndarray]:
+    """Spark's objective as a QN problem on the sigma-scaled coefficients: (problem, theta0,
+    inv_sigma)."""
     sigma = stats["sigma"]
-    C = n_classes if n_classes is not None else stats["num_classes"]
-    K = 1 if C <= 2 else C
-    dtype = "float32" if (X.dtype if not sparse else X.data.dtype) == torch.float32 else "float64"
-    base = {"classes_": [float(c) for c in classes], "n_cols": int(n), "dtype": dtype}
-    # one-class edge case (Spark: +-inf intercept, zero coefficients)
-    if len(classes) == 1 and fit_intercept:
-        cv = classes[0]
-        if cv not in (0.0, 1.0):
-            raise RuntimeError("class value must be either 1. or 0. when dataset has one label")
-        base.update(coef_=[[0.0] * n], intercept_=[float("inf") if cv == 1.0 else float("-inf")], num_iters=0,
-                    objective=0.0)
-        return base
     inv_sigma = np.where(sigma > 0, 1.0 / np.where(sigma > 0, sigma, 1.0), 0.0)
     q1 = sigma if standardization else np.ones(n)
     q2 = sigma * sigma if standardization else np.ones(n)
@@ -74,15 +58,11 @@ def logistic_fit(X: Any, y: torch.Tensor, m_total: int, ctx: WorkerContext, reg:
                   l2=np.concatenate([np.tile(pen_l2, K), np.zeros(nb)]),
                   l1=np.concatenate([np.tile(pen_l1 if l1_ratio > 0 and reg > 0 else np.zeros(n), K), np.zeros(nb)]),
                   inv_sigma=inv_sigma, max_iter=max(0, int(max_iter)), tol=float(tol), M=10)
-    y32 = y if y.dtype == torch.float32 else y.to(torch.float32)
-    y32 = y32.contiguous()
+    return P, theta0, inv_sigma
 
-    def evaluate(w: torch.Tensor, b: torch.Tensor, flag: Optional[torch.Tensor], out: torch.Tensor) -> None:
-        ops.logistic_loss_grad(X, y32, w, b, K, out, flag)
 
-    allreduce = ctx.comm.allreduce if ctx.world_size > 1 else None
-    path = ops.logistic_path(X, K)
-    res = minimize(P, theta0, evaluate, allreduce, y.device, batch=8 if not path.startswith("torch") else 2)
+def _result(res: Dict[str, Any], base: Dict[str, Any], ctx: WorkerContext, n: int, K: int, fit_intercept: bool,
+            inv_sigma: np.ndarray, path: str) -> Dict[str, Any]:
     theta = res["theta"]
     if ctx.world_size > 1:  # every rank holds the same state; make the model bit-identical anyway
         th = torch.from_numpy(theta).to(ctx.device)
@@ -92,10 +72,94 @@ def logistic_fit(X: Any, y: torch.Tensor, m_total: int, ctx: WorkerContext, reg:
     b = theta[K * n:] if fit_intercept else np.zeros(K)
     if fit_intercept and K > 1:
         b = b - b.mean()  # Spark centres multinomial intercepts
-    base.update(coef_=W.tolist(), intercept_=[float(v) for v in b], num_iters=int(res["iter"]),
-                objective=float(res["f"]))
-    base["_solver"] = {"n_evals": int(res["n_evals"]), "status": res["status"], "path": path}
-    return base
+    out = dict(base)
+    out.update(coef_=W.tolist(), intercept_=[float(v) for v in b], num_iters=int(res["iter"]),
+               objective=float(res["f"]))
+    out["_solver"] = {"n_evals": int(res["n_evals"]), "status": res["status"], "path": path}
+    return out
+
+
+def _one_class(classes: list, base: Dict[str, Any], n: int) -> Dict[str, Any]:
+    cv = classes[0]
+    if cv not in (0.0, 1.0):
+        raise RuntimeError("class value must be either 1. or 0. when dataset has one label")
+    out = dict(base)
+    out.update(coef_=[[0.0] * n], intercept_=[float("inf") if cv == 1.0 else float("-inf")], num_iters=0,
+               objective=0.0)
+    return out
+
+
+def logistic_fit(X: Any, y: torch.Tensor, m_total: int, ctx: WorkerContext, reg: float, l1_ratio: float,
+                 fit_intercept: bool, standardization: bool, max_iter: int, tol: float,
+                 n_classes: Optional[int] = None, sparse: bool = False,
+                 stats: Optional[Dict[str, Any]] = None) -> Dict[str, Any]:
+    n = X.shape[1]
+    if stats is None:
+        stats = logistic_stats(X, y, m_total, ctx, sparse)
+    classes = stats["classes"]
+    C = n_classes if n_classes is not None else stats["num_classes"]
+    K = 1 if C <= 2 else C
+    dtype = "float32" if (X.dtype if not sparse else X.data.dtype) == torch.float32 else "float64"
+    base = {"classes_": [float(c) for c in classes], "n_cols": int(n), "dtype": dtype}
+    # one-class edge case (Spark: +-inf intercept, zero coefficients)
+    if len(classes) == 1 and fit_intercept:
+        return _one_class(classes, base, n)
+    P, theta0, inv_sigma = _problem(n, m_total, stats, reg, l1_ratio, fit_intercept, standardization, max_iter, tol, K)
+    y32 = y if y.dtype == torch.float32 else y.to(torch.float32)
+    y32 = y32.contiguous()
+
+    def evaluate(w: torch.Tensor, b: torch.Tensor, flag: Optional[torch.Tensor], out: torch.Tensor) -> None:
+        ops.logistic_loss_grad(X, y32, w, b, K, out, flag)
+
+    allreduce = ctx.comm.allreduce if ctx.world_size > 1 else None
+    path = ops.logistic_path(X, K)
+    res = minimize(P, theta0, evaluate, allreduce, y.device, batch=8 if not path.startswith("torch") else 2)
+    return _result(res, base, ctx, n, K, fit_intercept, inv_sigma, path)
+
+
+MAX_BATCH = 12  # models per fused multi-model pass (register-resident weights, like the multinomial pass)
+
+
+def logistic_fit_multi(X: Any, y: torch.Tensor, m_total: int, ctx: WorkerContext, settings: List[Dict[str, Any]],
+                       sparse: bool = False, stats: Optional[Dict[str, Any]] = None) -> List[Dict[str, Any]]:
+    """fitMultiple for LogisticRegression (SURVEY §2.6 hyper-parameter batching): binary problems
+    on the device run in batches of <= 12 that share every pass over X (margins of all models in
+    one skinny-GEMM pass, residuals, one X^T R pass: ``ops.logistic_loss_grad_multi``) and one
+    batched optimiser launch per evaluation (``minimize_batch``); anything else (multinomial,
+    sparse, fp64, CPU, a single setting) fits one setting at a time. ``settings`` entries:
+    reg, l1_ratio, fit_intercept, standardization, max_iter, tol."""
+    n = X.shape[1]
+    if stats is None:
+        stats = logistic_stats(X, y, m_total, ctx, sparse)
+    K = 1 if stats["num_classes"] <= 2 else stats["num_classes"]
+    if sparse or K != 1 or len(settings) < 2 or not ops.mbin_supported(X, min(len(settings), MAX_BATCH)):
+        return [logistic_fit(X, y, m_total, ctx, s["reg"], s["l1_ratio"], s["fit_intercept"], s["standardization"],
+                             s["max_iter"], s["tol"], sparse=sparse, stats=stats) for s in settings]
+    from .qn import minimize_batch
+
+    classes = stats["classes"]
+    base = {"classes_": [float(c) for c in classes], "n_cols": int(n), "dtype": "float32"}
+    y32 = (y if y.dtype == torch.float32 else y.to(torch.float32)).contiguous()
+    allreduce = ctx.comm.allreduce if ctx.world_size > 1 else None
+    out: List[Optional[Dict[str, Any]]] = [None] * len(settings)
+    todo = []
+    for i, s in enumerate(settings):
+        if len(classes) == 1 and s["fit_intercept"]:
+            out[i] = _one_class(classes, base, n)
+        else:
+            todo.append(i)
+    for g0 in range(0, len(todo), MAX_BATCH):
+        grp = todo[g0: g0 + MAX_BATCH]
+        probs = [_problem(n, m_total, stats, settings[i]["reg"], settings[i]["l1_ratio"], settings[i]["fit_intercept"],
+                          settings[i]["standardization"], settings[i]["max_iter"], settings[i]["tol"], 1) for i in grp]
+
+        def evaluate(WB: torch.Tensor, OUT: torch.Tensor) -> None:
+            ops.logistic_loss_grad_multi(X, y32, WB, OUT)
+
+        res = minimize_batch([p[0] for p in probs], [p[1] for p in probs], evaluate, allreduce, y.device)
+        for i, (P, _, inv_sigma), r in zip(grp, probs, res):
+            out[i] = _result(r, base, ctx, n, 1, P.fit_intercept, inv_sigma, "batched_binary_f32")
+    return [o for o in out if o is not None]
 
 
 def logistic_stats(X: Any, y: torch.Tensor, m_total: int, ctx: WorkerContext, sparse: bool) -> Dict[str, Any]:

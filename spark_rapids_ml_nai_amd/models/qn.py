@@ -27,7 +27,7 @@ from __future__ import annotations
 
 import ctypes
 from dataclasses import dataclass
-from typing import Callable, Optional
+from typing import Callable, List, Optional
 
 import numpy as np
 import torch
@@ -256,7 +256,10 @@ class _QnArgs(ctypes.Structure):
 class DeviceQN:
     """Optimiser state in device memory, advanced by ``srml_qn_step`` (one launch per evaluation)."""
 
-    def __init__(self, P: QNProblem, theta0: np.ndarray, device: torch.device) -> None:
+    def __init__(self, P: QNProblem, theta0: np.ndarray, device: torch.device, wb: Optional[torch.Tensor] = None,
+                 out: Optional[torch.Tensor] = None, flags: Optional[torch.Tensor] = None) -> None:
+        """``wb`` / ``out`` / ``flags``: optional preallocated (contiguous) views, so a batch of
+        problems shares one trial-point matrix, one result matrix and one flag block."""
         from ..ops import native
 
         self.P = P
@@ -272,9 +275,10 @@ class DeviceQN:
         self.Y = v[(6 + M) * N:]
         self.small = torch.zeros(2 * M * M + max(P.past, 1) + 8, **f64)  # SY YY fh sc
         self.coef = torch.from_numpy(np.concatenate([P.l2, P.l1, P.inv_sigma]).astype(np.float64)).to(device)
-        self.flags = torch.zeros(16, dtype=torch.int32, device=device)
-        self.wb = torch.zeros(P.Kn + P.K, **f64)
-        self.out = torch.zeros(P.out_len, **f64)
+        self.flags = flags if flags is not None else torch.zeros(16, dtype=torch.int32, device=device)
+        self.wb = wb if wb is not None else torch.zeros(P.Kn + P.K, **f64)
+        self.out = out if out is not None else torch.zeros(P.out_len, **f64)
+        assert self.wb.numel() == P.Kn + P.K and self.out.numel() == P.out_len and self.flags.numel() == 16
         th = torch.from_numpy(np.asarray(theta0, dtype=np.float64)).to(device)
         self.xt.copy_(th)
         isg = torch.from_numpy(np.tile(P.inv_sigma, P.K)).to(device)
@@ -382,3 +386,59 @@ def minimize(P: QNProblem, theta0: np.ndarray, evaluate: Callable[[torch.Tensor,
     if not res["done"]:
         res["status"] = "evaluation cap"
     return res
+
+
+def minimize_batch(Ps: List[QNProblem], theta0s: List[np.ndarray],
+                   evaluate: Callable[[torch.Tensor, torch.Tensor], None],
+                   allreduce: Optional[Callable[[torch.Tensor], None]], device: torch.device,
+                   batch: int = 8) -> List[dict]:
+    """Hyper-parameter batching: B independent binary problems of one width advance together.
+    ``evaluate(WB, OUT)`` must ADD the data terms of all B models at the rows of WB (B, n + 1) into
+    OUT (B, n + 2) — one pass over X for the whole batch; the B optimiser steps run as ONE launch
+    (``srml_qn_step_batch``, a block per problem). Problems that converged keep their state while
+    the others continue; the loop ends when every done flag is set."""
+    from ..ops import native
+
+    B = len(Ps)
+    n = Ps[0].n
+    assert all(P.K == 1 and P.n == n for P in Ps), "batched QN needs binary problems of one width"
+    f64 = dict(dtype=torch.float64, device=device)
+    WB = torch.zeros((B, n + 1), **f64)
+    OUT = torch.zeros((B, n + 2), **f64)
+    FL = torch.zeros((B, 16), dtype=torch.int32, device=device)
+    qs = [DeviceQN(P, th, device, wb=WB[j], out=OUT[j], flags=FL[j]) for j, (P, th) in enumerate(zip(Ps, theta0s))]
+    raw = b"".join(bytes(q._args) for q in qs)
+    args_dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
+    st = native.stream(device)
+    host = torch.zeros(2, dtype=torch.int32, pin_memory=True)
+    cap = max(max(1, P.max_iter) * (P.max_ls + 1) + 2 for P in Ps)
+    evals, j = 0, 0
+    events: list = []
+    stream = torch.cuda.current_stream(device)
+    while evals < cap:
+        for _ in range(batch):
+            evaluate(WB, OUT)
+            if allreduce is not None:
+                allreduce(OUT)
+            native.call("srml_qn_step_batch", args_dev.data_ptr(), B, st)
+        evals += batch
+        slot = host[j % 2: j % 2 + 1]
+        slot.copy_(FL[:, F_DONE].min().view(1), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        events.append((ev, slot))
+        j += 1
+        if len(events) >= 2:
+            ev0, s0 = events.pop(0)
+            ev0.synchronize()
+            if int(s0.item()):
+                break
+    torch.cuda.synchronize(device)
+    out = []
+    for q in qs:
+        r = q.info()
+        r["theta"] = q.theta()
+        if not r["done"]:
+            r["status"] = "evaluation cap"
+        out.append(r)
+    return out

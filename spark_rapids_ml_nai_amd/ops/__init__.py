@@ -5,6 +5,7 @@ the numerics oracle in the kernel tests).
 from __future__ import annotations
 
 import math
+import os
 from typing import Any, Dict, Iterator, Optional, Tuple
 
 import numpy as np
@@ -116,6 +117,8 @@ def xw(X: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor] = None) ->
         cols = [xw(X, W[:, c0: c0 + 32], bias[c0: c0 + 32] if bias is not None else None) for c0 in range(0, k, 32)]
         return torch.cat(cols, 1)
     X = _c(X)
+    if k >= XW_MFMA_MIN_K:
+        return xw_t(X, W.t().to(torch.float32).contiguous(), bias)
     kk = next(w for w in _XW_WIDTHS if w >= k)
     Wp = torch.zeros((n, kk), dtype=torch.float32, device=X.device)
     Wp[:, :k] = W.to(torch.float32)
@@ -127,6 +130,32 @@ def xw(X: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor] = None) ->
     native.call("srml_xw_f32", X.data_ptr(), m, n, X.stride(0), Wp.data_ptr(), kk,
                 bp.data_ptr() if bp is not None else None, out.data_ptr(), kk, native.stream(X.device))
     return out[:, :k] if kk != k else out
+
+
+# K from which the skinny products run on the fp32 MFMA kernels (tools/skinny_bench.py at 1M x 3000:
+# the VALU X W kernel re-reads W from LDS per element and loses to the MFMA one from K = 3 up).
+XW_MFMA_MIN_K = 3
+XTV_MFMA_MIN_K = 5
+
+
+def xw_t(X: torch.Tensor, Wt: torch.Tensor, bias: Optional[torch.Tensor] = None,
+         out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """fp32 out (m, K) = X Wt^T (+ bias) for K <= 32 on the exact-fp32 MFMA (``srml_xw_t_f32``):
+    Wt (K, n) fp32 with unit column stride (any row stride), one bandwidth-bound pass over X."""
+    m, n = X.shape
+    K = Wt.shape[0]
+    if out is None:
+        out = torch.empty((m, K), dtype=torch.float32, device=X.device)
+    if not X.is_cuda:
+        out.copy_(X.float() @ Wt.float().t() + (bias.float() if bias is not None else 0.0))
+        return out
+    if K > 32 or Wt.dtype != torch.float32 or Wt.stride(1) != 1 or out.stride(1) != 1:
+        raise ValueError("xw_t: Wt must be fp32 (K <= 32, n) with unit column stride")
+    X = _c(X)
+    bp = _c(bias.to(device=X.device, dtype=torch.float32)) if bias is not None else None
+    native.call("srml_xw_t_f32", X.data_ptr(), m, n, X.stride(0), Wt.data_ptr(), K, Wt.stride(0),
+                bp.data_ptr() if bp is not None else None, out.data_ptr(), out.stride(0), native.stream(X.device))
+    return out
 
 
 def dgemm(A: torch.Tensor, B: torch.Tensor, ta: bool = False, tb: bool = False, alpha: float = 1.0,
@@ -206,6 +235,14 @@ def xtv(X: torch.Tensor, V: torch.Tensor, out: Optional[torch.Tensor] = None) ->
     if X.dtype != torch.float32:
         raise TypeError("xtv supports fp32/fp64 inputs, got %s" % X.dtype)
     X = _c(X)
+    if k >= XTV_MFMA_MIN_K:
+        for c0 in range(0, k, 16):
+            kk = min(16, k - c0)
+            Vc = _c(V2[:, c0: c0 + kk].to(torch.float32))
+            oc = out[:, c0: c0 + kk]
+            native.call("srml_xtv_mfma_f32", X.data_ptr(), m, n, X.stride(0), Vc.data_ptr(), kk, Vc.stride(0),
+                        oc.data_ptr(), oc.stride(0), oc.stride(1), None, native.stream(X.device))
+        return out
     for c0 in range(0, k, 4):
         kk = min(4, k - c0)
         Vc = _c(V2[:, c0: c0 + kk].to(torch.float32))
@@ -1394,9 +1431,61 @@ def logistic_path(X, K: int) -> str:
         if X.dtype in (torch.float32, torch.float64) and n <= 16384:
             return "lds_binary_" + ("f32" if X.dtype == torch.float32 else "f64")
         return "torch"
-    if X.dtype == torch.float32 and int(native.lib().srml_mlogit_supported(n, K)):
-        return "fused_multinomial_f32"
+    if X.dtype == torch.float32 and K <= 16:
+        fused = os.environ.get("SRML_LOGREG_FUSED", "0") == "1" and int(native.lib().srml_mlogit_supported(n, K))
+        return "fused_multinomial_f32" if fused else "two_pass_multinomial_f32"
     return "torch"
+
+
+def mbin_supported(X, M: int) -> bool:
+    """Whether ``logistic_loss_grad_multi`` runs on the device kernels for this input."""
+    return (not _is_csr(X)) and X.is_cuda and X.dtype == torch.float32 and 1 <= M <= 16
+
+
+def _glm_two_pass(X: torch.Tensor, y32: torch.Tensor, W: torch.Tensor, b: torch.Tensor, sb: int, mode: int,
+                  grad: torch.Tensor, so_c: int, so_k: int, gb: torch.Tensor, sgb: int, loss: torch.Tensor, sl: int,
+                  flag: Optional[torch.Tensor]) -> None:
+    """Two passes over X for K margins: Z = X W^T (``srml_xw_f32``, one bandwidth-bound pass for
+    K <= 32), the residual stage on the device (``srml_logit_residual_f32``: softmax (mode 0) or K
+    independent sigmoids (mode 1), bias gradients and losses block-reduced into fp64), then
+    grad += R^T X (``srml_xtv2_f32``, one pass for K <= 16). ``W`` (K, n) rows (any row stride),
+    output locations given by base tensors + element strides."""
+    m, n = X.shape
+    K = W.shape[0]
+    Z = xw_t(X, W.to(torch.float32).contiguous()) if K >= XW_MFMA_MIN_K else xw(X, W.t().float().contiguous())
+    R = torch.empty((m, K), dtype=torch.float32, device=X.device)
+    st = native.stream(X.device)
+    fp = flag.data_ptr() if flag is not None else None
+    native.call("srml_logit_residual_f32", Z.data_ptr(), m, K, Z.stride(0), _c(y32).data_ptr(), b.data_ptr(), sb,
+                mode, R.data_ptr(), K, gb.data_ptr(), sgb, loss.data_ptr(), sl, fp, st)
+    fn = "srml_xtv_mfma_f32" if K >= XTV_MFMA_MIN_K else "srml_xtv2_f32"
+    native.call(fn, X.data_ptr(), m, n, X.stride(0), R.data_ptr(), K, K, grad.data_ptr(), so_c, so_k, fp, st)
+
+
+def logistic_loss_grad_multi(X: torch.Tensor, y32: torch.Tensor, WB: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """ADD the data terms of M independent binary models into ``out`` (M, n + 2) rows
+    [grad w_j | grad b_j | loss_j], model j at WB[j] = [w_j (n) | b_j] — ONE pass over X for all
+    M models (hyper-parameter batching). Device: ``srml_mbin_f32``; otherwise per-model torch."""
+    m, n = X.shape
+    M = WB.shape[0]
+    if mbin_supported(X, M) and WB.stride(1) == 1 and out.stride(1) == 1:
+        X = _c(X)
+        if os.environ.get("SRML_LOGREG_FUSED", "0") == "1" and int(native.lib().srml_mlogit_supported(n, max(2, M))):
+            native.call("srml_mbin_f32", X.data_ptr(), m, n, X.stride(0), _c(y32).data_ptr(), WB.data_ptr(),
+                        WB.stride(0), M, out.data_ptr(), out.stride(0), native.stream(X.device))
+            return out
+        ld = out.stride(0)
+        _glm_two_pass(X, y32, WB[:, :n], WB[:, n:], WB.stride(0), 1, out, 1, ld, out[:, n:], ld, out[:, n + 1:], ld,
+                      None)
+        return out
+    Xd = X.double()
+    yd = y32.double()
+    Z = Xd @ WB[:, :n].double().t() + WB[:, n].double().view(1, M)
+    R = torch.sigmoid(Z) - yd.view(-1, 1)
+    out[:, :n] += (R.t() @ Xd)
+    out[:, n] += R.sum(0)
+    out[:, n + 1] += (torch.nn.functional.softplus(Z) - yd.view(-1, 1) * Z).sum(0)
+    return out
 
 
 def logistic_loss_grad(X, y32: torch.Tensor, w: torch.Tensor, b: torch.Tensor, K: int, out: torch.Tensor,
@@ -1469,6 +1558,8 @@ def logistic_loss_grad(X, y32: torch.Tensor, w: torch.Tensor, b: torch.Tensor, K
     elif path == "fused_multinomial_f32":
         native.call("srml_mlogit_f32", X.data_ptr(), m, n, X.stride(0), y32.data_ptr(), w.data_ptr(), b.data_ptr(),
                     fp, K, out.data_ptr(), st)
+    elif path == "two_pass_multinomial_f32":
+        _glm_two_pass(X, y32, w.view(K, n), b, 1, 0, out, 1, n, out[K * n:], 1, out[K * n + K:], 0, flag)
     else:  # pragma: no cover
         raise AssertionError(path)
     return out

@@ -83,6 +83,210 @@ SRML_API int srml_xtv_f32(const float* X, long m, int n, long ld, const float* V
   return srml_status();
 }
 
+// Wider / strided variant for the two-pass multi-class and multi-model GLM gradients:
+// out[c * so_c + k * so_k] += sum_r X[r][c] V[r][k], k < K <= 16, skipped once *flag != 0.
+template <int K>
+__global__ __launch_bounds__(256) void xtv2_kernel(const float* __restrict__ X, long m, int n, long ld,
+                                                   const float* __restrict__ V, long ldv, double* __restrict__ out,
+                                                   long so_c, long so_k, long rows_per_block, int kk,
+                                                   const int* __restrict__ flag) {
+  if (flag && *flag) return;
+  const int c0 = (blockIdx.x * 256 + threadIdx.x) * 4;
+  const long r0 = (long)blockIdx.y * rows_per_block;
+  const long r1 = min(m, r0 + rows_per_block);
+  if (c0 >= n) return;
+  double acc[K][4];
+  float facc[K][4];
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { acc[k][j] = 0.0; facc[k][j] = 0.f; }
+  const bool full = (c0 + 3 < n) && ((ld & 3) == 0);
+  int cnt = 0;
+  for (long r = r0; r < r1; ++r) {
+    floatx4 x;
+    if (full) {
+      x = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(X + r * ld + c0));
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) x[j] = (c0 + j < n) ? X[r * ld + c0 + j] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const float v = k < kk ? V[r * ldv + k] : 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) facc[k][j] = fmaf(x[j], v, facc[k][j]);
+    }
+    if (++cnt == 256) {
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { acc[k][j] += facc[k][j]; facc[k][j] = 0.f; }
+      cnt = 0;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc[k][j] += facc[k][j];
+      if (k < kk && c0 + j < n) atomicAdd(&out[(long)(c0 + j) * so_c + (long)k * so_k], acc[k][j]);
+    }
+}
+
+SRML_API int srml_xtv2_f32(const float* X, long m, int n, long ld, const float* V, int k, long ldv, double* out,
+                           long so_c, long so_k, const int* flag, hipStream_t stream) {
+  if (m <= 0 || n <= 0) return 0;
+  unsigned gx = ceil_div(n, 1024);
+  long gy = (2048 + gx - 1) / gx;
+  long rpb = (m + gy - 1) / gy;
+  if (rpb < 64) rpb = 64;
+  gy = (m + rpb - 1) / rpb;
+  dim3 grid(gx, (unsigned)gy);
+#define SRML_XTV2(KK)                                                                                            \
+  hipLaunchKernelGGL(xtv2_kernel<KK>, grid, dim3(256), 0, stream, X, m, n, ld, V, ldv, out, so_c, so_k, rpb, k, flag)
+  if (k <= 1) SRML_XTV2(1);
+  else if (k <= 2) SRML_XTV2(2);
+  else if (k <= 4) SRML_XTV2(4);
+  else if (k <= 8) SRML_XTV2(8);
+  else if (k <= 12) SRML_XTV2(12);
+  else if (k <= 16) SRML_XTV2(16);
+  else return -1;
+#undef SRML_XTV2
+  return srml_status();
+}
+
+// MFMA variant of the same product for K <= 16: out^T (K x n) = V^T X accumulated on
+// v_mfma_f32_16x16x4_f32 with the reduction running over rows. A = V^T (lane: V[r + (l>>4)][l&15]);
+// B = 4 rows x 16 columns of X where lane l loads ONE 16-B vector X[r + (l>>4)][c0 + 4(l&15) .. +3]
+// and component q feeds column tile q (columns c0 + 4j + q), so every X load is a full 256-B row
+// segment. fp32 partials fold into fp64 registers every 256 rows (the VALU kernel's precision
+// contract); a wave owns 64 columns, a block 256 columns x rows_per_block rows.
+template <int WPB>
+__global__ __launch_bounds__(64 * WPB) void xtv_mfma_kernel(const float* __restrict__ X, long m, int n, long ld,
+                                                       const float* __restrict__ V, int K, long ldv,
+                                                       double* __restrict__ out, long so_c, long so_k,
+                                                       long rows_per_block, int vec, const int* __restrict__ flag) {
+  if (flag && *flag) return;
+  const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
+  const int c0 = (blockIdx.x * WPB + (threadIdx.x >> 6)) * 64;
+  if (c0 >= n) return;
+  const long r0 = (long)blockIdx.y * rows_per_block;
+  const long r1 = min(m, r0 + rows_per_block);
+  const int cl = c0 + 4 * li;
+  const bool cfull = vec && (c0 + 63 < n);  // wave-uniform: MFMAs ignore EXEC, so no lane may diverge
+  const bool kok = li < K;
+  double accd[4][4];
+  floatx4 acc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    acc[q] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) accd[q][e] = 0.0;
+  }
+  const int kl = kok ? li : 0;
+  long rc = r0;
+  if (cfull) {
+    // branch-free body over whole 256-row chunks: 16 rows (4 MFMA steps) per group, the next
+    // group's 16-B X loads and V words issued before this group's MFMAs
+    const float* xp = X + (rc + g) * ld + cl;
+    const float* vp = V + (rc + g) * ldv + kl;
+    for (; rc + 256 <= r1; rc += 256) {
+      floatx4 x[4];
+      float a[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        x[s] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(xp + 4 * s * ld));
+        a[s] = vp[4 * s * ldv];
+      }
+#pragma unroll 1
+      for (int grp = 0; grp < 16; ++grp) {
+        xp += 16 * ld;
+        vp += 16 * ldv;
+        floatx4 xn[4];
+        float an[4];
+        if (grp < 15) {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            xn[s] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(xp + 4 * s * ld));
+            an[s] = vp[4 * s * ldv];
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const float av = kok ? a[s] : 0.f;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, x[s][q], acc[q], 0, 0, 0);
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          x[s] = xn[s];
+          a[s] = an[s];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) accd[q][e] += (double)acc[q][e];
+        acc[q] = floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  }
+  for (; rc < r1; rc += 256) {  // ragged chunk / partial column group: guarded loads
+#pragma unroll 4
+    for (int s = 0; s < 64; ++s) {
+      const long r = rc + 4 * s + g;
+      const bool ok = r < r1;
+      floatx4 x;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) x[q] = (ok && cl + q < n) ? X[r * ld + cl + q] : 0.f;
+      const float a = (ok && kok) ? V[r * ldv + li] : 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, x[q], acc[q], 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) accd[q][e] += (double)acc[q][e];
+      acc[q] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  // lane holds D[i = 4g + e][j = l & 15] of tile q: class k = 4g + e, column c0 + 4j + q
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int col = cl + q;
+    if (col >= n) continue;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = 4 * g + e;
+      if (k < K) atomicAdd(&out[(long)col * so_c + (long)k * so_k], accd[q][e]);
+    }
+  }
+}
+
+SRML_API int srml_xtv_mfma_f32(const float* X, long m, int n, long ld, const float* V, int k, long ldv, double* out,
+                               long so_c, long so_k, const int* flag, hipStream_t stream) {
+  if (m <= 0 || n <= 0) return 0;
+  if (k < 1 || k > 16) return -2;
+  const int vec = ((ld & 3) == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
+  // 16 waves (1024 columns = 4 KB of every row) per block when n is wide enough: one block streams
+  // long contiguous row segments; narrow n keeps 4-wave blocks so the grid still fills the chip.
+  const int wpb = n >= 2048 ? 16 : 4;
+  const unsigned gx = ceil_div(n, 64 * wpb);
+  const long target = wpb == 16 ? 512 : 2048;
+  long gy = (target + gx - 1) / gx;
+  long rpb = (m + gy - 1) / gy;
+  rpb = ((rpb + 255) / 256) * 256;
+  gy = (m + rpb - 1) / rpb;
+  if (wpb == 16)
+    hipLaunchKernelGGL(xtv_mfma_kernel<16>, dim3(gx, (unsigned)gy), dim3(1024), 0, stream, X, m, n, ld, V, k, ldv, out,
+                       so_c, so_k, rpb, vec, flag);
+  else
+    hipLaunchKernelGGL(xtv_mfma_kernel<4>, dim3(gx, (unsigned)gy), dim3(256), 0, stream, X, m, n, ld, V, k, ldv, out,
+                       so_c, so_k, rpb, vec, flag);
+  return srml_status();
+}
+
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void row_sqnorm_kernel(const float* __restrict__ X, long m, int n, long ld,
                                                          float* __restrict__ out) {

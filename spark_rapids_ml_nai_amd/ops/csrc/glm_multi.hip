@@ -10,6 +10,9 @@
 //    every lane evaluates the (max-shifted) softmax, the residuals p_k - [y == k] and the loss,
 //    then updates its K gradient slices from the row still in registers.
 //    out layout (fp64): [grad W (K x n, class-major) | grad b (K) | loss sum].
+//  * srml_mbin_f32 — the same pass for M INDEPENDENT binary models (hyper-parameter batching:
+//    fitMultiple / CrossValidator grids share every read of X): model k's margin x.w_k + b_k,
+//    sigmoid residual and softplus loss, gradients [grad w_k | grad b_k | loss_k] per model row.
 //  * srml_logreg_binary_lds_{f32,f64} — binary loss + gradient for fp64 inputs and for fp32 rows
 //    wider than the register-resident fast path (n <= 16384): one wave per row, the gradient of
 //    the block accumulates in LDS (fp64 ds_add), one fp64 atomic per column per block.
@@ -17,16 +20,21 @@
 // on-device quasi-Newton step (qn.hip) without host round trips.
 #include "common.h"
 
-template <int KB, int V, int D>
+// SIG = false: softmax over K classes, W (K x n, ldw = n), bvec[k], out = [grad W | grad b | loss].
+// SIG = true : K independent binary models, W rows of stride ldw with the intercept at W[k*ldw + n]
+//              (bvec = W + n, ldb = ldw), out rows of stride ldo = [grad w_k (n) | grad b_k | loss_k].
+template <int KB, int V, int G, bool SIG>
 __global__ __launch_bounds__(256, 1) void mlogit_pf_kernel(const float* __restrict__ X, long m, int n, long ld,
                                                            const float* __restrict__ y,
-                                                           const double* __restrict__ W,
-                                                           const double* __restrict__ bvec,
+                                                           const double* __restrict__ W, long ldw,
+                                                           const double* __restrict__ bvec, long ldb,
                                                            const int* __restrict__ flag, int K,
-                                                           double* __restrict__ out, long rows_per_block,
-                                                           int vec) {
+                                                           double* __restrict__ out, long ldo,
+                                                           long rows_per_block, int vec) {
   if (flag && *flag) return;
-  __shared__ float part[2][KB][4];
+  // G rows per LDS exchange / barrier (the 4 waves' column-slice margins of a row must meet);
+  // the next G rows stream into the other register buffer meanwhile
+  __shared__ float part[2][G][KB][4];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int cbase = wid * 256 * V;
@@ -39,94 +47,115 @@ __global__ __launch_bounds__(256, 1) void mlogit_pf_kernel(const float* __restri
     for (int k = 0; k < KB; ++k)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        wreg[k][v][q] = (k < K && c + q < n) ? (float)W[(long)k * n + c + q] : 0.f;
+        wreg[k][v][q] = (k < K && c + q < n) ? (float)W[(long)k * ldw + c + q] : 0.f;
         g[k][v][q] = 0.f;
       }
   }
   double bb[KB];
 #pragma unroll
-  for (int k = 0; k < KB; ++k) bb[k] = (k < K && bvec) ? bvec[k] : 0.0;
+  for (int k = 0; k < KB; ++k) bb[k] = (k < K && bvec) ? bvec[(long)k * ldb] : 0.0;
   double gb[KB];
+  double lk[SIG ? KB : 1];
 #pragma unroll
   for (int k = 0; k < KB; ++k) gb[k] = 0.0;
+#pragma unroll
+  for (int k = 0; k < (SIG ? KB : 1); ++k) lk[k] = 0.0;
   double loss = 0.0;
   const long r0 = (long)blockIdx.x * rows_per_block;
   const long r1 = min(m, r0 + rows_per_block);
   if (r0 >= r1) return;
 
-  auto load = [&](long r, floatx4 (&x)[V]) {
-    const float* row = X + r * ld;
+  auto load = [&](long rg, floatx4 (&x)[G][V]) {
 #pragma unroll
-    for (int v = 0; v < V; ++v) {
-      const int c = cbase + (v * 64 + lane) * 4;
-      if (vec && c + 3 < n) {
-        x[v] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(row + c));
-      } else {
+    for (int gi = 0; gi < G; ++gi) {
+      const long r = rg + gi < r1 ? rg + gi : r1 - 1;  // clamped: the tail rows are never processed
+      const float* row = X + r * ld;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) x[v][q] = (c + q < n) ? row[c + q] : 0.f;
+      for (int v = 0; v < V; ++v) {
+        const int c = cbase + (v * 64 + lane) * 4;
+        if (vec && c + 3 < n) {
+          x[gi][v] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(row + c));
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) x[gi][v][q] = (c + q < n) ? row[c + q] : 0.f;
+        }
       }
     }
   };
   int buf = 0;
-  auto process = [&](long r, const floatx4 (&x)[V]) {
-    float pk[KB];
+  auto process = [&](long rg, const floatx4 (&x)[G][V]) {
 #pragma unroll
-    for (int k = 0; k < KB; ++k) {
-      float a = 0.f;
+    for (int gi = 0; gi < G; ++gi)
 #pragma unroll
-      for (int v = 0; v < V; ++v)
+      for (int k = 0; k < KB; ++k) {
+        float a = 0.f;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) a = fmaf(x[v][q], wreg[k][v][q], a);
-      pk[k] = wave_sum(a);
-    }
-    if (lane == 0) {
+        for (int v = 0; v < V; ++v)
 #pragma unroll
-      for (int k = 0; k < KB; ++k) part[buf][k][wid] = pk[k];
-    }
+          for (int q = 0; q < 4; ++q) a = fmaf(x[gi][v][q], wreg[k][v][q], a);
+        a = wave_sum(a);
+        if (lane == 0) part[buf][gi][k][wid] = a;
+      }
     __syncthreads();
-    double z[KB];
-    double zmax = -1e300;
 #pragma unroll
-    for (int k = 0; k < KB; ++k) {
-      z[k] = (double)part[buf][k][0] + (double)part[buf][k][1] + (double)part[buf][k][2] + (double)part[buf][k][3] + bb[k];
-      if (k < K) zmax = fmax(zmax, z[k]);
+    for (int gi = 0; gi < G; ++gi) {
+      const long r = rg + gi;
+      if (r >= r1) break;
+      double z[KB];
+      double zmax = -1e300;
+#pragma unroll
+      for (int k = 0; k < KB; ++k) {
+        z[k] = (double)part[buf][gi][k][0] + (double)part[buf][gi][k][1] + (double)part[buf][gi][k][2] +
+               (double)part[buf][gi][k][3] + bb[k];
+        if (k < K) zmax = fmax(zmax, z[k]);
+      }
+      if constexpr (SIG) {
+        const double yr = (double)y[r];
+#pragma unroll
+        for (int k = 0; k < KB; ++k) {
+          double res = 0.0, l = 0.0;
+          if (k < K) logistic_terms(z[k], yr, res, l);
+          const float rf = (float)res;
+          if (wid == 0 && lane == 0) { gb[k] += res; lk[k] += l; }
+#pragma unroll
+          for (int v = 0; v < V; ++v)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) g[k][v][q] = fmaf(rf, x[gi][v][q], g[k][v][q]);
+        }
+      } else {
+        float e[KB];
+        float se = 0.f;
+#pragma unroll
+        for (int k = 0; k < KB; ++k) {
+          e[k] = k < K ? __expf((float)(z[k] - zmax)) : 0.f;
+          se += e[k];
+        }
+        const int yi = (int)y[r];
+        const float inv = 1.f / se;
+        double zy = 0.0;
+#pragma unroll
+        for (int k = 0; k < KB; ++k) {
+          const float res = e[k] * inv - (k == yi ? 1.f : 0.f);
+          if (k == yi) zy = z[k];
+          if (wid == 0 && lane == 0) gb[k] += (double)res;
+#pragma unroll
+          for (int v = 0; v < V; ++v)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) g[k][v][q] = fmaf(res, x[gi][v][q], g[k][v][q]);
+        }
+        if (wid == 0 && lane == 0) loss += zmax + (double)__logf(se) - zy;
+      }
     }
-    float e[KB];
-    float se = 0.f;
-#pragma unroll
-    for (int k = 0; k < KB; ++k) {
-      e[k] = k < K ? __expf((float)(z[k] - zmax)) : 0.f;
-      se += e[k];
-    }
-    const int yi = (int)y[r];
-    const float inv = 1.f / se;
-    double zy = 0.0;
-#pragma unroll
-    for (int k = 0; k < KB; ++k) {
-      const float res = e[k] * inv - (k == yi ? 1.f : 0.f);
-      if (k == yi) zy = z[k];
-      if (wid == 0 && lane == 0) gb[k] += (double)res;
-#pragma unroll
-      for (int v = 0; v < V; ++v)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) g[k][v][q] = fmaf(res, x[v][q], g[k][v][q]);
-    }
-    if (wid == 0 && lane == 0) loss += zmax + (double)__logf(se) - zy;
     buf ^= 1;
   };
-  floatx4 x[D + 1][V];
-#pragma unroll
-  for (int d = 0; d < D; ++d)
-    if (r0 + d < r1) load(r0 + d, x[d]);
-  for (long rb = r0; rb < r1; rb += D + 1) {
-#pragma unroll
-    for (int ph = 0; ph <= D; ++ph) {
-      const long cur = rb + ph;
-      if (cur < r1) {
-        const long nxt = cur + D;
-        if (nxt < r1) load(nxt, x[(ph + D) % (D + 1)]);
-        process(cur, x[ph]);
-      }
+  floatx4 xa[G][V], xb[G][V];
+  load(r0, xa);
+  for (long rg = r0; rg < r1; rg += 2 * G) {
+    if (rg + G < r1) load(rg + G, xb);
+    process(rg, xa);
+    if (rg + G < r1) {
+      if (rg + 2 * G < r1) load(rg + 2 * G, xa);
+      process(rg + G, xb);
     }
   }
 #pragma unroll
@@ -137,13 +166,20 @@ __global__ __launch_bounds__(256, 1) void mlogit_pf_kernel(const float* __restri
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int c = cbase + (v * 64 + lane) * 4 + q;
-        if (c < n) atomicAdd(&out[(long)k * n + c], (double)g[k][v][q]);
+        if (c < n) atomicAdd(&out[(long)k * ldo + c], (double)g[k][v][q]);
       }
   }
   if (wid == 0 && lane == 0) {
-    const long base = (long)K * n;
-    for (int k = 0; k < K; ++k) atomicAdd(&out[base + k], gb[k]);
-    atomicAdd(&out[base + K], loss);
+    if constexpr (SIG) {
+      for (int k = 0; k < K; ++k) {
+        atomicAdd(&out[(long)k * ldo + n], gb[k]);
+        atomicAdd(&out[(long)k * ldo + n + 1], lk[k]);
+      }
+    } else {
+      const long base = (long)K * n;
+      for (int k = 0; k < K; ++k) atomicAdd(&out[base + k], gb[k]);
+      atomicAdd(&out[base + K], loss);
+    }
   }
 }
 
@@ -169,8 +205,9 @@ SRML_API int srml_mlogit_f32(const float* X, long m, int n, long ld, const float
   blocks = (m + rpb - 1) / rpb;
   const int vec = ((ld & 3) == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
   dim3 grid((unsigned)blocks), blk(256);
-#define SRML_ML(KK, VV) \
-  hipLaunchKernelGGL((mlogit_pf_kernel<KK, VV, 2>), grid, blk, 0, stream, X, m, n, ld, y, W, b, flag, K, out, rpb, vec)
+#define SRML_ML(KK, VV)                                                                                          \
+  hipLaunchKernelGGL((mlogit_pf_kernel<KK, VV, (KK <= 4 ? 4 : KK <= 8 ? 2 : 1), false>), grid, blk, 0, stream, X, m, \
+                     n, ld, y, W, (long)n, b, 1L, flag, K, out, (long)n, rpb, vec)
   if (KB == 4) {
     if (V == 1) SRML_ML(4, 1); else if (V == 2) SRML_ML(4, 2); else if (V == 3) SRML_ML(4, 3); else SRML_ML(4, 4);
   } else if (KB == 8) {
@@ -181,6 +218,145 @@ SRML_API int srml_mlogit_f32(const float* X, long m, int n, long ld, const float
     if (V == 1) SRML_ML(16, 1); else SRML_ML(16, 2);
   }
 #undef SRML_ML
+  return srml_status();
+}
+
+// M independent binary models in one pass: WB (M rows of stride ldw: w (n) then b), out (M rows of
+// stride ldo: grad w (n), grad b, loss), both fp64; same support rule as the multinomial pass.
+SRML_API int srml_mbin_f32(const float* X, long m, int n, long ld, const float* y, const double* WB, long ldw, int M,
+                           double* out, long ldo, hipStream_t stream) {
+  if (m <= 0) return 0;
+  if (M < 1 || ldw < n + 1 || ldo < n + 2) return -2;
+  if (M == 1 ? !srml_mlogit_supported(n, 2) : !srml_mlogit_supported(n, M)) return -2;
+  const int V = (n + 1023) / 1024;
+  const int KB = M <= 4 ? 4 : M <= 8 ? 8 : M <= 12 ? 12 : 16;
+  long blocks = m / 256;
+  if (blocks > 1024) blocks = 1024;
+  if (blocks < 1) blocks = 1;
+  long rpb = (m + blocks - 1) / blocks;
+  blocks = (m + rpb - 1) / rpb;
+  const int vec = ((ld & 3) == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
+  dim3 grid((unsigned)blocks), blk(256);
+#define SRML_MB(KK, VV)                                                                                             \
+  hipLaunchKernelGGL((mlogit_pf_kernel<KK, VV, (KK <= 4 ? 4 : KK <= 8 ? 2 : 1), true>), grid, blk, 0, stream, X, m, n, \
+                     ld, y, WB, ldw, WB + n, ldw, (const int*)nullptr, M, out, ldo, rpb, vec)
+  if (KB == 4) {
+    if (V == 1) SRML_MB(4, 1); else if (V == 2) SRML_MB(4, 2); else if (V == 3) SRML_MB(4, 3); else SRML_MB(4, 4);
+  } else if (KB == 8) {
+    if (V == 1) SRML_MB(8, 1); else if (V == 2) SRML_MB(8, 2); else if (V == 3) SRML_MB(8, 3); else SRML_MB(8, 4);
+  } else if (KB == 12) {
+    if (V == 1) SRML_MB(12, 1); else if (V == 2) SRML_MB(12, 2); else SRML_MB(12, 3);
+  } else {
+    if (V == 1) SRML_MB(16, 1); else SRML_MB(16, 2);
+  }
+#undef SRML_MB
+  return srml_status();
+}
+
+// ------------------------------------------------------------------------------------------
+// Residual stage of the two-pass GLM gradients (margins Z = X W^T from srml_xw_f32, then
+// X^T R from srml_xtv2_f32): per row, z_k = Z[r][k] + b_k (fp64 bias from device memory);
+//   mode 0 (softmax over K classes): R[r][k] = p_k - [y == k], loss += logsumexp(z) - z_y;
+//   mode 1 (K independent binary models): R[r][k] = sigmoid(z_k) - y, loss_k += softplus(z_k) - y z_k.
+// Bias gradients (column sums of R) and the loss(es) are block-reduced and added into out:
+// gb_k at gb[k * sgb], loss at loss[0] (mode 0) or loss[k * sl] (mode 1).
+template <int KB>
+__global__ __launch_bounds__(256) void logit_residual_kernel(const float* __restrict__ Z, long m, int K, long ldz,
+                                                             const float* __restrict__ y,
+                                                             const double* __restrict__ b, long sb, int mode,
+                                                             float* __restrict__ R, long ldr,
+                                                             double* __restrict__ gb, long sgb,
+                                                             double* __restrict__ loss, long sl,
+                                                             const int* __restrict__ flag) {
+  if (flag && *flag) return;
+  __shared__ double red[4][2 * KB + 1];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  double bk[KB], sg[KB], sls[KB];
+#pragma unroll
+  for (int k = 0; k < KB; ++k) {
+    bk[k] = (k < K && b) ? b[(long)k * sb] : 0.0;
+    sg[k] = 0.0;
+    sls[k] = 0.0;
+  }
+  double lsum = 0.0;
+  for (long r = (long)blockIdx.x * 256 + threadIdx.x; r < m; r += (long)gridDim.x * 256) {
+    double z[KB];
+    const float yr = y[r];
+#pragma unroll
+    for (int k = 0; k < KB; ++k) z[k] = k < K ? (double)Z[r * ldz + k] + bk[k] : 0.0;
+    if (mode == 0) {
+      double zmax = -1e300;
+#pragma unroll
+      for (int k = 0; k < KB; ++k)
+        if (k < K) zmax = fmax(zmax, z[k]);
+      // fp64 softmax: the loss feeds the line search, whose sufficient-decrease test must resolve
+      // changes far below fp32's log/exp error
+      double e[KB];
+      double se = 0.0;
+#pragma unroll
+      for (int k = 0; k < KB; ++k) {
+        e[k] = k < K ? exp(z[k] - zmax) : 0.0;
+        se += e[k];
+      }
+      const int yi = (int)yr;
+      const double inv = 1.0 / se;
+      double zy = 0.0;
+#pragma unroll
+      for (int k = 0; k < KB; ++k) {
+        if (k < K) {
+          const double res = e[k] * inv - (k == yi ? 1.0 : 0.0);
+          if (k == yi) zy = z[k];
+          R[r * ldr + k] = (float)res;
+          sg[k] += res;
+        }
+      }
+      lsum += zmax + log(se) - zy;
+    } else {
+#pragma unroll
+      for (int k = 0; k < KB; ++k) {
+        if (k < K) {
+          double res, l;
+          logistic_terms(z[k], (double)yr, res, l);
+          R[r * ldr + k] = (float)res;
+          sg[k] += res;
+          sls[k] += l;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < KB; ++k) {
+    const double a = wave_sum(sg[k]);
+    const double c = wave_sum(sls[k]);
+    if (lane == 0) { red[wid][k] = a; red[wid][KB + k] = c; }
+  }
+  const double lw = wave_sum(lsum);
+  if (lane == 0) red[wid][2 * KB] = lw;
+  __syncthreads();
+  if (threadIdx.x < K) {
+    const int k = threadIdx.x;
+    atomicAdd(&gb[(long)k * sgb], red[0][k] + red[1][k] + red[2][k] + red[3][k]);
+    if (mode == 1)
+      atomicAdd(&loss[(long)k * sl], red[0][KB + k] + red[1][KB + k] + red[2][KB + k] + red[3][KB + k]);
+  }
+  if (threadIdx.x == 0 && mode == 0)
+    atomicAdd(&loss[0], red[0][2 * KB] + red[1][2 * KB] + red[2][2 * KB] + red[3][2 * KB]);
+}
+
+SRML_API int srml_logit_residual_f32(const float* Z, long m, int K, long ldz, const float* y, const double* b, long sb,
+                                     int mode, float* R, long ldr, double* gb, long sgb, double* loss, long sl,
+                                     const int* flag, hipStream_t stream) {
+  if (m <= 0) return 0;
+  if (K < 1 || K > 16) return -2;
+  long blocks = (m + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+#define SRML_RES(KK)                                                                                             \
+  hipLaunchKernelGGL(logit_residual_kernel<KK>, dim3((unsigned)blocks), dim3(256), 0, stream, Z, m, K, ldz, y, b, sb, \
+                     mode, R, ldr, gb, sgb, loss, sl, flag)
+  if (K <= 4) SRML_RES(4);
+  else if (K <= 8) SRML_RES(8);
+  else SRML_RES(16);
+#undef SRML_RES
   return srml_status();
 }
 

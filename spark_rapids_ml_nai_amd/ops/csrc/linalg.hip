@@ -173,6 +173,194 @@ SRML_API int srml_xw_f32(const float* X, long m, int n, long ld, const float* W,
 }
 
 // ------------------------------------------------------------------------------------------
+// Skinny GEMM on the exact-fp32 MFMA: Z (m x K) = X (m x n) Wt^T (+ bias), Wt (K x n) row-major,
+// K <= 16 * NT. A wave owns 64 rows (4 row tiles of 16) and all K columns; per 16-deep k step each
+// lane issues one 16-B load per row tile (row l&15, columns k0 + 4(l>>4) .. +3) and one per column
+// tile of Wt, then 4 x v_mfma_f32_16x16x4_f32 per tile pair, component q of the loaded vectors
+// feeding MFMA q: the reduction index is permuted identically for A and B, so the sum is exact.
+// The VALU variant above re-reads W from LDS per element (K LDS words per X element) and spills
+// to global W once n*K outgrows the LDS slice; here the W bytes per wave are 1/4 of the X bytes
+// (L1/L2 hits shared by the 4 waves of a block) and the math is on the matrix cores, so the pass
+// runs at the HBM rate for every K <= 32.
+template <int NT, int RT, bool PIPE>
+__global__ __launch_bounds__(256) void xw_mfma_kernel(const float* __restrict__ X, long m, int n, long ld,
+                                                      const float* __restrict__ Wt, int K, long ldw,
+                                                      const float* __restrict__ bias, float* __restrict__ out,
+                                                      long ldo, int vec) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
+  const long row0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * (16 * RT);
+  if (row0 >= m) return;
+  floatx4 acc[RT][NT];
+  const float* xr[RT];
+  const float* wr[NT];
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    const long r = row0 + t * 16 + li;
+    xr[t] = X + (r < m ? r : m - 1) * ld;
+#pragma unroll
+    for (int c = 0; c < NT; ++c) acc[t][c] = floatx4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int c = 0; c < NT; ++c) {
+    const int j = c * 16 + li;
+    wr[c] = Wt + (long)(j < K ? j : K - 1) * ldw;
+  }
+  // Main loop: 64 columns per step, four 16-B loads per row tile = 256 contiguous bytes of each of
+  // the wave's 64 rows in flight (DRAM page locality); the fp32 chain is folded into `tot` every
+  // 256 columns so the rounding error grows with 256 + n/256 terms rather than n.
+  floatx4 tot[RT][NT];
+#pragma unroll
+  for (int t = 0; t < RT; ++t)
+#pragma unroll
+    for (int c = 0; c < NT; ++c) tot[t][c] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int n64 = vec ? (n & ~63) : 0;
+  int k0 = 0;
+  if (n64 > 0) {
+    floatx4 a[RT][4], b[NT][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+      for (int t = 0; t < RT; ++t) a[t][u] = *reinterpret_cast<const floatx4*>(xr[t] + 16 * u + 4 * g);
+#pragma unroll
+      for (int c = 0; c < NT; ++c) b[c][u] = *reinterpret_cast<const floatx4*>(wr[c] + 16 * u + 4 * g);
+    }
+    for (int step = 0; k0 < n64; ++step) {
+      const int kn = k0 + 64;
+      floatx4 an[RT][4], bn[NT][4];
+      if (PIPE && kn < n64) {  // next step's loads in flight under this step's MFMAs
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+          for (int t = 0; t < RT; ++t) an[t][u] = *reinterpret_cast<const floatx4*>(xr[t] + kn + 16 * u + 4 * g);
+#pragma unroll
+          for (int c = 0; c < NT; ++c) bn[c][u] = *reinterpret_cast<const floatx4*>(wr[c] + kn + 16 * u + 4 * g);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int t = 0; t < RT; ++t)
+#pragma unroll
+            for (int c = 0; c < NT; ++c)
+              acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][u][q], b[c][u][q], acc[t][c], 0, 0, 0);
+      if ((step & 3) == 3) {
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+#pragma unroll
+          for (int c = 0; c < NT; ++c) {
+            tot[t][c] += acc[t][c];
+            acc[t][c] = floatx4{0.f, 0.f, 0.f, 0.f};
+          }
+      }
+      k0 = kn;
+      if (k0 >= n64) break;
+      if (PIPE) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+          for (int t = 0; t < RT; ++t) a[t][u] = an[t][u];
+#pragma unroll
+          for (int c = 0; c < NT; ++c) b[c][u] = bn[c][u];
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+          for (int t = 0; t < RT; ++t) a[t][u] = *reinterpret_cast<const floatx4*>(xr[t] + k0 + 16 * u + 4 * g);
+#pragma unroll
+          for (int c = 0; c < NT; ++c) b[c][u] = *reinterpret_cast<const floatx4*>(wr[c] + k0 + 16 * u + 4 * g);
+        }
+      }
+    }
+  }
+  const int nfull = vec ? (n & ~15) : 0;
+  for (; k0 < nfull; k0 += 16) {
+    const int kk = k0 + 4 * g;
+    floatx4 a[RT], b[NT];
+#pragma unroll
+    for (int t = 0; t < RT; ++t) a[t] = *reinterpret_cast<const floatx4*>(xr[t] + kk);
+#pragma unroll
+    for (int c = 0; c < NT; ++c) b[c] = *reinterpret_cast<const floatx4*>(wr[c] + kk);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int c = 0; c < NT; ++c) acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][q], b[c][q], acc[t][c], 0, 0, 0);
+  }
+  for (; k0 < n; k0 += 16) {  // tail / unaligned rows: guarded scalar loads
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int kk = k0 + 4 * g + q;
+      const bool ok = kk < n;
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        const float av = ok ? xr[t][kk] : 0.f;
+#pragma unroll
+        for (int c = 0; c < NT; ++c) {
+          const float bv = ok ? wr[c][kk] : 0.f;
+          acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[t][c], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // D layout: lane holds D[i = 4g + e][j = l & 15], e = 0..3
+#pragma unroll
+  for (int c = 0; c < NT; ++c) {
+    const int col = c * 16 + li;
+    if (col >= K) continue;
+    const float bb = bias ? bias[col] : 0.f;
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const long r = row0 + t * 16 + 4 * g + e;
+        if (r < m) out[r * ldo + col] = (tot[t][c][e] + acc[t][c][e]) + bb;
+      }
+  }
+}
+
+static int xw_t_launch(const float* X, long m, int n, long ld, const float* Wt, int K, long ldw, const float* bias,
+                       float* out, long ldo, int variant, hipStream_t stream) {
+  if (m <= 0) return 0;
+  if (n <= 0 || K < 1 || K > 32) return -2;
+  const int vec = ((ld & 3) == 0) && ((ldw & 3) == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0) &&
+                  ((reinterpret_cast<uintptr_t>(Wt) & 15) == 0);
+  const int rt = (variant & 1) ? 2 : 4;
+  const bool pipe = (variant & 2) != 0;
+  const long blocks = (m + 64 * rt - 1) / (64 * rt);
+  if (blocks > 0x7fffffffL) return -2;
+#define SRML_XWT(NT_, RT_, P_)                                                                                    \
+  hipLaunchKernelGGL((xw_mfma_kernel<NT_, RT_, P_>), dim3((unsigned)blocks), dim3(256), 0, stream, X, m, n, ld, Wt, K, \
+                     ldw, bias, out, ldo, vec)
+  if (K <= 16) {
+    if (rt == 4) { if (pipe) SRML_XWT(1, 4, true); else SRML_XWT(1, 4, false); }
+    else { if (pipe) SRML_XWT(1, 2, true); else SRML_XWT(1, 2, false); }
+  } else {
+    if (rt == 4) { if (pipe) SRML_XWT(2, 4, true); else SRML_XWT(2, 4, false); }
+    else { if (pipe) SRML_XWT(2, 2, true); else SRML_XWT(2, 2, false); }
+  }
+#undef SRML_XWT
+  return srml_status();
+}
+
+SRML_API int srml_xw_t_f32(const float* X, long m, int n, long ld, const float* Wt, int K, long ldw, const float* bias,
+                           float* out, long ldo, hipStream_t stream) {
+  // measured at 1M x 3000 (tools/skinny_bench.py --variants): double-buffered loads win everywhere;
+  // 2 row tiles per wave (more waves in flight) up to K = 12, 4 (half the Wt re-reads) above
+  return xw_t_launch(X, m, n, ld, Wt, K, ldw, bias, out, ldo, K <= 12 ? 3 : 2, stream);
+}
+
+// Tuning entry (tools/skinny_bench.py): variant bit 0 = 2 row tiles per wave (else 4), bit 1 =
+// double-buffered loads.
+SRML_API int srml_xw_t_f32_variant(const float* X, long m, int n, long ld, const float* Wt, int K, long ldw,
+                                   const float* bias, float* out, long ldo, int variant, hipStream_t stream) {
+  return xw_t_launch(X, m, n, ld, Wt, K, ldw, bias, out, ldo, variant, stream);
+}
+
+// ------------------------------------------------------------------------------------------
 // fp64 GEMM on f64 MFMA (16x16x4): block tile 64x64, 4 waves each 32x32 (2x2 MFMA tiles), BK=16
 // ------------------------------------------------------------------------------------------
 namespace {

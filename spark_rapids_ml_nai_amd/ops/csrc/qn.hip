@@ -145,7 +145,7 @@ __device__ void qn_set_trial(const QnArgs& A, double alpha) {
 #define QN_PROBE(k) \
   do { if (A.probe && threadIdx.x == 0) A.probe[k] = wall_clock64(); } while (0)
 
-__global__ __launch_bounds__(QN_T) void qn_step_kernel(QnArgs A) {
+__device__ __forceinline__ void qn_step_body(const QnArgs& A) {
   __shared__ double red[QN_NV * (QN_NW + 1)];
   __shared__ double cf_a[QN_MMAX], cf_t[QN_MMAX];
   __shared__ double s_sy[QN_MMAX * QN_MMAX], s_yy[QN_MMAX * QN_MMAX];
@@ -571,6 +571,20 @@ __global__ __launch_bounds__(QN_T) void qn_step_kernel(QnArgs A) {
     A.sc[SC_ALPHA] = alpha;
     A.sc[SC_DGINIT] = dg;
   }
+}
+
+__global__ __launch_bounds__(QN_T) void qn_step_kernel(QnArgs A) { qn_step_body(A); }
+
+// hyper-parameter batching: one block per independent problem, args array in device memory
+__global__ __launch_bounds__(QN_T) void qn_step_batch_kernel(const QnArgs* __restrict__ args) {
+  const QnArgs A = args[blockIdx.x];
+  qn_step_body(A);
+}
+
+SRML_API int srml_qn_step_batch(const QnArgs* args_dev, int count, hipStream_t stream) {
+  if (count <= 0) return 0;
+  hipLaunchKernelGGL(qn_step_batch_kernel, dim3((unsigned)count), dim3(QN_T), 0, stream, args_dev);
+  return srml_status();
 }
 
 SRML_API int srml_qn_step(const QnArgs* a, hipStream_t stream) {

@@ -43,6 +43,13 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_logreg_binary2_f32": (_P, _L, _I, _L, _P, _P, _D, _P, _P, _P, _P),
     "srml_logreg_binary_lds_f32": (_P, _L, _I, _L, _P, _P, _D, _P, _P, _P, _P),
     "srml_logreg_binary_lds_f64": (_P, _L, _I, _L, _P, _P, _D, _P, _P, _P, _P),
+    "srml_xtv2_f32": (_P, _L, _I, _L, _P, _I, _L, _P, _L, _L, _P, _P),
+    "srml_xtv_mfma_f32": (_P, _L, _I, _L, _P, _I, _L, _P, _L, _L, _P, _P),
+    "srml_xw_t_f32": (_P, _L, _I, _L, _P, _I, _L, _P, _P, _L, _P),
+    "srml_xw_t_f32_variant": (_P, _L, _I, _L, _P, _I, _L, _P, _P, _L, _I, _P),
+    "srml_logit_residual_f32": (_P, _L, _I, _L, _P, _P, _L, _I, _P, _L, _P, _L, _P, _L, _P, _P),
+    "srml_mbin_f32": (_P, _L, _I, _L, _P, _P, _L, _I, _P, _L, _P),
+    "srml_qn_step_batch": (_P, _I, _P),
     "srml_mlogit_f32": (_P, _L, _I, _L, _P, _P, _P, _P, _I, _P, _P),
     "srml_mlogit_supported": (_I, _I),
     "srml_qn_step": (_P, _P),

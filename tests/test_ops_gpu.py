@@ -47,7 +47,8 @@ def test_gram_asymmetric_columns(gpu_device):
     torch.testing.assert_close(G, ref)
 
 
-@pytest.mark.parametrize("m,n,k", [(1000, 3000, 3), (12345, 128, 1), (999, 37, 5), (4000, 256, 16), (300, 64, 32)])
+@pytest.mark.parametrize("m,n,k", [(1000, 3000, 3), (12345, 128, 1), (999, 37, 5), (4000, 256, 16), (300, 64, 32),
+                                   (3001, 1000, 10), (257, 333, 20), (70, 3, 4)])
 def test_xw(gpu_device, m, n, k):
     X = _rand(m, n, gpu_device, seed=2)
     W = _rand(n, k, gpu_device, seed=3)
@@ -78,13 +79,25 @@ def test_sign_flip(gpu_device):
     assert torch.all(out[idx, torch.arange(7)] > 0)
 
 
-@pytest.mark.parametrize("m,n,k", [(1000, 3, 1), (5000, 300, 2), (20000, 3000, 1), (777, 129, 4), (100, 10, 7)])
+@pytest.mark.parametrize("m,n,k", [(1000, 3, 1), (5000, 300, 2), (20000, 3000, 1), (777, 129, 4), (100, 10, 7),
+                                   (20000, 3000, 10), (3001, 2050, 16), (999, 70, 21)])
 def test_xtv(gpu_device, m, n, k):
     X = _rand(m, n, gpu_device, seed=11)
     V = _rand(m, k, gpu_device, seed=12)
     out = ops.xtv(X, V).cpu()
     ref = X.double().cpu().T @ V.double().cpu()
     torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-3)
+
+
+def test_xw_t_unaligned_rows(gpu_device):
+    """MFMA skinny GEMM on a row-strided view (ld % 4 != 0 -> guarded scalar path) and a strided Wt."""
+    base = _rand(513, 303, gpu_device, seed=21)
+    X = base[:, 1:300]
+    Wbase = _rand(12, 310, gpu_device, seed=22)
+    Wt = Wbase[:, 2:301]
+    out = ops.xw_t(X, Wt).cpu().double()
+    ref = X.double().cpu() @ Wt.double().cpu().T
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-4)
 
 
 def test_row_sqnorm(gpu_device):

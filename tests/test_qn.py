@@ -143,7 +143,7 @@ def test_logistic_reports_solver_path(device):
     info = model._solver_info
     assert info["n_evals"] >= model.num_iters >= 1
     if device == "gpu":
-        assert info["path"] == "fused_multinomial_f32"
+        assert info["path"] == "two_pass_multinomial_f32"
     else:
         assert info["path"] == "torch-cpu"
 
@@ -172,13 +172,17 @@ def _ref_loss_grad(X, y, W, b, K):
     (3001, 130, 1, torch.float32, "fused_binary_f32"),
     (2000, 5000, 1, torch.float32, "lds_binary_f32"),
     (3000, 257, 1, torch.float64, "lds_binary_f64"),
+    (4000, 3000, 10, torch.float32, "two_pass_multinomial_f32"),
+    (3000, 129, 3, torch.float32, "two_pass_multinomial_f32"),
+    (2500, 1001, 16, torch.float32, "two_pass_multinomial_f32"),
+    (2000, 4096, 5, torch.float32, "two_pass_multinomial_f32"),
     (4000, 3000, 10, torch.float32, "fused_multinomial_f32"),
     (3000, 129, 3, torch.float32, "fused_multinomial_f32"),
-    (2500, 1001, 16, torch.float32, "fused_multinomial_f32"),
-    (2000, 4096, 5, torch.float32, "fused_multinomial_f32"),
     (1500, 300, 20, torch.float32, "torch"),
 ])
-def test_logistic_loss_grad_kernels(gpu_device, m, n, K, dtype, path):
+def test_logistic_loss_grad_kernels(gpu_device, m, n, K, dtype, path, monkeypatch):
+    if path == "fused_multinomial_f32":
+        monkeypatch.setenv("SRML_LOGREG_FUSED", "1")
     g = torch.Generator().manual_seed(m + n + K)
     X = torch.randn(m, n, generator=g, dtype=torch.float64).to(dtype).to(gpu_device)
     if K == 1:
@@ -243,3 +247,55 @@ def test_qn_kernel_matches_host(gpu_device, K, l1):
         # require the same optimum instead of the same trajectory
         assert abs(dev["f"] - host["f"]) <= 1e-7 * abs(host["f"]), info
         np.testing.assert_allclose(dev["theta"], host["theta"], atol=2e-3)
+
+
+@pytest.mark.gpu
+def test_logistic_fit_multi_batched_matches_single(gpu_device):
+    """Hyper-parameter batching: a grid of binary fits sharing every pass over X (srml_mbin_f32 +
+    srml_qn_step_batch) reproduces the one-at-a-time fits."""
+    import torch
+
+    from spark_rapids_ml_nai_amd import ops
+    from spark_rapids_ml_nai_amd.models.logistic import logistic_fit, logistic_fit_multi, logistic_stats
+    from spark_rapids_ml_nai_amd.parallel.context import WorkerContext
+
+    rng = np.random.default_rng(3)
+    m, n = 6000, 40
+    X = (rng.standard_normal((m, n)) * rng.uniform(0.5, 2.0, n)).astype(np.float32)
+    w = rng.standard_normal(n)
+    y = (X @ w + 0.3 * rng.standard_normal(m) > 0).astype(np.float32)
+    Xt = torch.from_numpy(X).to(gpu_device)
+    yt = torch.from_numpy(y).to(gpu_device)
+    ctx = WorkerContext.single(gpu_device)
+    stats = logistic_stats(Xt, yt, m, ctx, False)
+    settings = [dict(reg=r, l1_ratio=a, fit_intercept=fi, standardization=sd, max_iter=100, tol=1e-10)
+                for r, a, fi, sd in [(1e-3, 0.0, True, True), (1e-2, 0.0, True, False), (1e-3, 0.5, True, True),
+                                     (1e-2, 1.0, False, True), (0.1, 0.0, True, True)]]
+    assert ops.mbin_supported(Xt, len(settings))
+    batched = logistic_fit_multi(Xt, yt, m, ctx, settings, stats=stats)
+    for s, b in zip(settings, batched):
+        assert b["_solver"]["path"] == "batched_binary_f32"
+        one = logistic_fit(Xt, yt, m, ctx, s["reg"], s["l1_ratio"], s["fit_intercept"], s["standardization"],
+                           s["max_iter"], s["tol"], stats=stats)
+        assert abs(b["objective"] - one["objective"]) <= 1e-6 * max(1.0, abs(one["objective"]))
+        np.testing.assert_allclose(np.asarray(b["coef_"]), np.asarray(one["coef_"]), rtol=2e-3, atol=2e-3)
+        np.testing.assert_allclose(b["intercept_"], one["intercept_"], rtol=2e-3, atol=2e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fused", ["0", "1"])
+def test_mbin_kernel_matches_torch(gpu_device, fused, monkeypatch):
+    monkeypatch.setenv("SRML_LOGREG_FUSED", fused)
+    import torch
+
+    from spark_rapids_ml_nai_amd import ops
+
+    rng = np.random.default_rng(4)
+    m, n, M = 5000, 300, 7
+    X = torch.from_numpy(rng.standard_normal((m, n)).astype(np.float32))
+    y = torch.from_numpy((rng.random(m) > 0.4).astype(np.float32))
+    WB = torch.from_numpy(rng.standard_normal((M, n + 1)) * 0.05)
+    ref = ops.logistic_loss_grad_multi(X, y, WB, torch.zeros((M, n + 2), dtype=torch.float64))
+    got = ops.logistic_loss_grad_multi(X.to(gpu_device), y.to(gpu_device), WB.to(gpu_device),
+                                       torch.zeros((M, n + 2), dtype=torch.float64, device=gpu_device))
+    torch.testing.assert_close(got.cpu(), ref, rtol=1e-4, atol=1e-3)
