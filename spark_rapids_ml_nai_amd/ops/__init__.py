@@ -1425,6 +1425,8 @@ def logistic_path(X, K: int) -> str:
     if not X.is_cuda:
         return "torch-cpu"
     m, n = X.shape
+    if deterministic() and X.dtype == torch.float32 and K <= 16:
+        return "two_pass_deterministic_f32"
     if K == 1:
         if X.dtype == torch.float32 and n <= 4096:
             return "fused_binary_f32"
@@ -1456,7 +1458,19 @@ def _glm_two_pass(X: torch.Tensor, y32: torch.Tensor, W: torch.Tensor, b: torch.
     R = torch.empty((m, K), dtype=torch.float32, device=X.device)
     st = native.stream(X.device)
     fp = flag.data_ptr() if flag is not None else None
-    native.call("srml_logit_residual_f32", Z.data_ptr(), m, K, Z.stride(0), _c(y32).data_ptr(), b.data_ptr(), sb,
+    yp = _c(y32).data_ptr()
+    if deterministic():
+        # no atomics: per-block partials into workspaces, folded in block order (bit-reproducible);
+        # the margin pass has none to begin with
+        L = native.lib()
+        ws = torch.empty(max(int(L.srml_logit_residual_ws(m, K)), int(L.srml_xtv_mfma_ws(m, n, K)), 1),
+                         dtype=torch.float64, device=X.device)
+        native.call("srml_logit_residual_det_f32", Z.data_ptr(), m, K, Z.stride(0), yp, b.data_ptr(), sb, mode,
+                    R.data_ptr(), K, gb.data_ptr(), sgb, loss.data_ptr(), sl, fp, ws.data_ptr(), st)
+        native.call("srml_xtv_mfma_det_f32", X.data_ptr(), m, n, X.stride(0), R.data_ptr(), K, K, grad.data_ptr(),
+                    so_c, so_k, fp, ws.data_ptr(), st)
+        return
+    native.call("srml_logit_residual_f32", Z.data_ptr(), m, K, Z.stride(0), yp, b.data_ptr(), sb,
                 mode, R.data_ptr(), K, gb.data_ptr(), sgb, loss.data_ptr(), sl, fp, st)
     fn = "srml_xtv_mfma_f32" if K >= XTV_MFMA_MIN_K else "srml_xtv2_f32"
     native.call(fn, X.data_ptr(), m, n, X.stride(0), R.data_ptr(), K, K, grad.data_ptr(), so_c, so_k, fp, st)
@@ -1470,7 +1484,8 @@ def logistic_loss_grad_multi(X: torch.Tensor, y32: torch.Tensor, WB: torch.Tenso
     M = WB.shape[0]
     if mbin_supported(X, M) and WB.stride(1) == 1 and out.stride(1) == 1:
         X = _c(X)
-        if os.environ.get("SRML_LOGREG_FUSED", "0") == "1" and int(native.lib().srml_mlogit_supported(n, max(2, M))):
+        if (os.environ.get("SRML_LOGREG_FUSED", "0") == "1" and not deterministic()
+                and int(native.lib().srml_mlogit_supported(n, max(2, M)))):
             native.call("srml_mbin_f32", X.data_ptr(), m, n, X.stride(0), _c(y32).data_ptr(), WB.data_ptr(),
                         WB.stride(0), M, out.data_ptr(), out.stride(0), native.stream(X.device))
             return out
@@ -1558,8 +1573,10 @@ def logistic_loss_grad(X, y32: torch.Tensor, w: torch.Tensor, b: torch.Tensor, K
     elif path == "fused_multinomial_f32":
         native.call("srml_mlogit_f32", X.data_ptr(), m, n, X.stride(0), y32.data_ptr(), w.data_ptr(), b.data_ptr(),
                     fp, K, out.data_ptr(), st)
-    elif path == "two_pass_multinomial_f32":
+    elif path == "two_pass_multinomial_f32" or (path == "two_pass_deterministic_f32" and K > 1):
         _glm_two_pass(X, y32, w.view(K, n), b, 1, 0, out, 1, n, out[K * n:], 1, out[K * n + K:], 0, flag)
+    elif path == "two_pass_deterministic_f32":  # binary: one sigmoid model
+        _glm_two_pass(X, y32, w.view(1, n), b, 1, 1, out, 1, n, out[n:], 1, out[n + 1:], 1, flag)
     else:  # pragma: no cover
         raise AssertionError(path)
     return out

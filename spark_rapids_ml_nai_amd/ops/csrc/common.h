@@ -90,6 +90,12 @@ __device__ __forceinline__ void logistic_terms(double z, double y, double& res, 
 
 static inline int srml_status() { return (int)hipGetLastError(); }
 
+// Ordered fold of per-block partials (deterministic mode, defined in glm.hip):
+// out[(i / inner) * so_outer + (i % inner) * so_inner] += sum_{p = 0..parts-1} ws[p * pstride + i], i < width,
+// summed in block order so the result is bit-identical run to run; skipped once *flag != 0.
+SRML_API int srml_fold_partials_f64(const double* ws, long parts, long pstride, long width, long inner, double* out,
+                                    long so_outer, long so_inner, const int* flag, hipStream_t stream);
+
 // keep the first failing HIP runtime status of a multi-call host routine in `err`
 #define SRML_TRY(err, call)                                  \
   do {                                                       \

@@ -166,7 +166,8 @@ template <int WPB>
 __global__ __launch_bounds__(64 * WPB) void xtv_mfma_kernel(const float* __restrict__ X, long m, int n, long ld,
                                                        const float* __restrict__ V, int K, long ldv,
                                                        double* __restrict__ out, long so_c, long so_k,
-                                                       long rows_per_block, int vec, const int* __restrict__ flag) {
+                                                       long rows_per_block, int vec, const int* __restrict__ flag,
+                                                       double* __restrict__ ws) {
   if (flag && *flag) return;
   const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
   const int c0 = (blockIdx.x * WPB + (threadIdx.x >> 6)) * 64;
@@ -259,31 +260,91 @@ __global__ __launch_bounds__(64 * WPB) void xtv_mfma_kernel(const float* __restr
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int k = 4 * g + e;
-      if (k < K) atomicAdd(&out[(long)col * so_c + (long)k * so_k], accd[q][e]);
+      if (k >= K) continue;
+      if (ws)  // deterministic mode: this block-row's partial, folded in order by the launcher
+        ws[((long)blockIdx.y * n + col) * K + k] = accd[q][e];
+      else
+        atomicAdd(&out[(long)col * so_c + (long)k * so_k], accd[q][e]);
     }
   }
 }
 
-SRML_API int srml_xtv_mfma_f32(const float* X, long m, int n, long ld, const float* V, int k, long ldv, double* out,
-                               long so_c, long so_k, const int* flag, hipStream_t stream) {
+namespace {
+struct XtvGrid {
+  int wpb;
+  unsigned gx;
+  long gy, rpb;
+};
+XtvGrid xtv_mfma_grid(long m, int n) {
+  // 16 waves (1024 columns = 4 KB of every row) per block when n is wide enough: one block streams
+  // long contiguous row segments; narrow n keeps 4-wave blocks so the grid still fills the chip.
+  XtvGrid gr;
+  gr.wpb = n >= 2048 ? 16 : 4;
+  gr.gx = ceil_div(n, 64 * gr.wpb);
+  const long target = gr.wpb == 16 ? 512 : 2048;
+  long gy = (target + gr.gx - 1) / gr.gx;
+  long rpb = (m + gy - 1) / gy;
+  rpb = ((rpb + 255) / 256) * 256;
+  gr.gy = (m + rpb - 1) / rpb;
+  gr.rpb = rpb;
+  return gr;
+}
+}  // namespace
+
+// Workspace (doubles) the deterministic variant needs: one n x K partial per block row.
+SRML_API long srml_xtv_mfma_ws(long m, int n, int k) {
+  if (m <= 0 || n <= 0) return 0;
+  return xtv_mfma_grid(m, n).gy * (long)n * k;
+}
+
+static int xtv_mfma_launch(const float* X, long m, int n, long ld, const float* V, int k, long ldv, double* out,
+                           long so_c, long so_k, const int* flag, double* ws, hipStream_t stream) {
   if (m <= 0 || n <= 0) return 0;
   if (k < 1 || k > 16) return -2;
   const int vec = ((ld & 3) == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
-  // 16 waves (1024 columns = 4 KB of every row) per block when n is wide enough: one block streams
-  // long contiguous row segments; narrow n keeps 4-wave blocks so the grid still fills the chip.
-  const int wpb = n >= 2048 ? 16 : 4;
-  const unsigned gx = ceil_div(n, 64 * wpb);
-  const long target = wpb == 16 ? 512 : 2048;
-  long gy = (target + gx - 1) / gx;
-  long rpb = (m + gy - 1) / gy;
-  rpb = ((rpb + 255) / 256) * 256;
-  gy = (m + rpb - 1) / rpb;
-  if (wpb == 16)
-    hipLaunchKernelGGL(xtv_mfma_kernel<16>, dim3(gx, (unsigned)gy), dim3(1024), 0, stream, X, m, n, ld, V, k, ldv, out,
-                       so_c, so_k, rpb, vec, flag);
+  const XtvGrid gr = xtv_mfma_grid(m, n);
+  if (gr.wpb == 16)
+    hipLaunchKernelGGL(xtv_mfma_kernel<16>, dim3(gr.gx, (unsigned)gr.gy), dim3(1024), 0, stream, X, m, n, ld, V, k,
+                       ldv, out, so_c, so_k, gr.rpb, vec, flag, ws);
   else
-    hipLaunchKernelGGL(xtv_mfma_kernel<4>, dim3(gx, (unsigned)gy), dim3(256), 0, stream, X, m, n, ld, V, k, ldv, out,
-                       so_c, so_k, rpb, vec, flag);
+    hipLaunchKernelGGL(xtv_mfma_kernel<4>, dim3(gr.gx, (unsigned)gr.gy), dim3(256), 0, stream, X, m, n, ld, V, k, ldv,
+                       out, so_c, so_k, gr.rpb, vec, flag, ws);
+  int st = srml_status();
+  if (st || !ws) return st;
+  return srml_fold_partials_f64(ws, gr.gy, (long)n * k, (long)n * k, k, out, so_c, so_k, flag, stream);
+}
+
+SRML_API int srml_xtv_mfma_f32(const float* X, long m, int n, long ld, const float* V, int k, long ldv, double* out,
+                               long so_c, long so_k, const int* flag, hipStream_t stream) {
+  return xtv_mfma_launch(X, m, n, ld, V, k, ldv, out, so_c, so_k, flag, nullptr, stream);
+}
+
+// Deterministic variant: block-row partials to ws (srml_xtv_mfma_ws doubles), then an ordered fold.
+SRML_API int srml_xtv_mfma_det_f32(const float* X, long m, int n, long ld, const float* V, int k, long ldv,
+                                   double* out, long so_c, long so_k, const int* flag, double* ws,
+                                   hipStream_t stream) {
+  if (!ws) return -2;
+  return xtv_mfma_launch(X, m, n, ld, V, k, ldv, out, so_c, so_k, flag, ws, stream);
+}
+
+__global__ __launch_bounds__(256) void fold_partials_kernel(const double* __restrict__ ws, long parts, long pstride,
+                                                            long width, long inner, double* __restrict__ out,
+                                                            long so_outer, long so_inner,
+                                                            const int* __restrict__ flag) {
+  if (flag && *flag) return;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= width) return;
+  double s = 0.0;
+  for (long p = 0; p < parts; ++p) s += ws[p * pstride + i];
+  out[(i / inner) * so_outer + (i % inner) * so_inner] += s;
+}
+
+SRML_API int srml_fold_partials_f64(const double* ws, long parts, long pstride, long width, long inner, double* out,
+                                    long so_outer, long so_inner, const int* flag, hipStream_t stream) {
+  if (width <= 0 || parts <= 0) return 0;
+  if (inner < 1) return -2;
+  hipLaunchKernelGGL(fold_partials_kernel, dim3(ceil_div(width, 256)), dim3(256), 0, stream, ws, parts, pstride, width,
+                     inner, out, so_outer, so_inner, flag);
   return srml_status();
 }
 

@@ -267,7 +267,7 @@ __global__ __launch_bounds__(256) void logit_residual_kernel(const float* __rest
                                                              float* __restrict__ R, long ldr,
                                                              double* __restrict__ gb, long sgb,
                                                              double* __restrict__ loss, long sl,
-                                                             const int* __restrict__ flag) {
+                                                             const int* __restrict__ flag, double* __restrict__ ws) {
   if (flag && *flag) return;
   __shared__ double red[4][2 * KB + 1];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -333,6 +333,16 @@ __global__ __launch_bounds__(256) void logit_residual_kernel(const float* __rest
   const double lw = wave_sum(lsum);
   if (lane == 0) red[wid][2 * KB] = lw;
   __syncthreads();
+  if (ws) {  // deterministic mode: [gb (K) | per-model loss (K) | loss] of this block, folded in order
+    double* wb = ws + (long)blockIdx.x * (2 * K + 1);
+    if (threadIdx.x < K) {
+      const int k = threadIdx.x;
+      wb[k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+      wb[K + k] = red[0][KB + k] + red[1][KB + k] + red[2][KB + k] + red[3][KB + k];
+    }
+    if (threadIdx.x == 0) wb[2 * K] = red[0][2 * KB] + red[1][2 * KB] + red[2][2 * KB] + red[3][2 * KB];
+    return;
+  }
   if (threadIdx.x < K) {
     const int k = threadIdx.x;
     atomicAdd(&gb[(long)k * sgb], red[0][k] + red[1][k] + red[2][k] + red[3][k]);
@@ -343,21 +353,48 @@ __global__ __launch_bounds__(256) void logit_residual_kernel(const float* __rest
     atomicAdd(&loss[0], red[0][2 * KB] + red[1][2 * KB] + red[2][2 * KB] + red[3][2 * KB]);
 }
 
-SRML_API int srml_logit_residual_f32(const float* Z, long m, int K, long ldz, const float* y, const double* b, long sb,
-                                     int mode, float* R, long ldr, double* gb, long sgb, double* loss, long sl,
-                                     const int* flag, hipStream_t stream) {
+static long logit_residual_blocks(long m) {
+  long blocks = (m + 255) / 256;
+  return blocks > 2048 ? 2048 : blocks;
+}
+
+// Workspace (doubles) of the deterministic residual stage.
+SRML_API long srml_logit_residual_ws(long m, int K) { return m <= 0 ? 0 : logit_residual_blocks(m) * (2L * K + 1); }
+
+static int logit_residual_launch(const float* Z, long m, int K, long ldz, const float* y, const double* b, long sb,
+                                 int mode, float* R, long ldr, double* gb, long sgb, double* loss, long sl,
+                                 const int* flag, double* ws, hipStream_t stream) {
   if (m <= 0) return 0;
   if (K < 1 || K > 16) return -2;
-  long blocks = (m + 255) / 256;
-  if (blocks > 2048) blocks = 2048;
+  const long blocks = logit_residual_blocks(m);
 #define SRML_RES(KK)                                                                                             \
   hipLaunchKernelGGL(logit_residual_kernel<KK>, dim3((unsigned)blocks), dim3(256), 0, stream, Z, m, K, ldz, y, b, sb, \
-                     mode, R, ldr, gb, sgb, loss, sl, flag)
+                     mode, R, ldr, gb, sgb, loss, sl, flag, ws)
   if (K <= 4) SRML_RES(4);
   else if (K <= 8) SRML_RES(8);
   else SRML_RES(16);
 #undef SRML_RES
-  return srml_status();
+  int st = srml_status();
+  if (st || !ws) return st;
+  const long pst = 2L * K + 1;
+  st = srml_fold_partials_f64(ws, blocks, pst, K, K, gb, 0, sgb, flag, stream);
+  if (st) return st;
+  if (mode == 1) return srml_fold_partials_f64(ws + K, blocks, pst, K, K, loss, 0, sl, flag, stream);
+  return srml_fold_partials_f64(ws + 2 * K, blocks, pst, 1, 1, loss, 0, 0, flag, stream);
+}
+
+SRML_API int srml_logit_residual_f32(const float* Z, long m, int K, long ldz, const float* y, const double* b, long sb,
+                                     int mode, float* R, long ldr, double* gb, long sgb, double* loss, long sl,
+                                     const int* flag, hipStream_t stream) {
+  return logit_residual_launch(Z, m, K, ldz, y, b, sb, mode, R, ldr, gb, sgb, loss, sl, flag, nullptr, stream);
+}
+
+// Deterministic variant: per-block partials to ws (srml_logit_residual_ws doubles), ordered folds.
+SRML_API int srml_logit_residual_det_f32(const float* Z, long m, int K, long ldz, const float* y, const double* b,
+                                         long sb, int mode, float* R, long ldr, double* gb, long sgb, double* loss,
+                                         long sl, const int* flag, double* ws, hipStream_t stream) {
+  if (!ws) return -2;
+  return logit_residual_launch(Z, m, K, ldz, y, b, sb, mode, R, ldr, gb, sgb, loss, sl, flag, ws, stream);
 }
 
 // ------------------------------------------------------------------------------------------

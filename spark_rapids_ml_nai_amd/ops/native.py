@@ -25,7 +25,8 @@ _L = ctypes.c_long
 _D = ctypes.c_double
 _F = ctypes.c_float
 
-# name -> argtypes (restype is always int status)
+# name -> argtypes (restype: int status, except the size queries in _LONG_RESULT)
+_LONG_RESULT = ("srml_qn_args_size", "srml_logit_residual_ws", "srml_xtv_mfma_ws")
 SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_col_moments_f32": (_P, _L, _I, _L, _P, _P, _P),
     "srml_col_moments_f64": (_P, _L, _I, _L, _P, _P, _P),
@@ -45,9 +46,14 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_logreg_binary_lds_f64": (_P, _L, _I, _L, _P, _P, _D, _P, _P, _P, _P),
     "srml_xtv2_f32": (_P, _L, _I, _L, _P, _I, _L, _P, _L, _L, _P, _P),
     "srml_xtv_mfma_f32": (_P, _L, _I, _L, _P, _I, _L, _P, _L, _L, _P, _P),
+    "srml_xtv_mfma_det_f32": (_P, _L, _I, _L, _P, _I, _L, _P, _L, _L, _P, _P, _P),
+    "srml_fold_partials_f64": (_P, _L, _L, _L, _L, _P, _L, _L, _P, _P),
     "srml_xw_t_f32": (_P, _L, _I, _L, _P, _I, _L, _P, _P, _L, _P),
     "srml_xw_t_f32_variant": (_P, _L, _I, _L, _P, _I, _L, _P, _P, _L, _I, _P),
     "srml_logit_residual_f32": (_P, _L, _I, _L, _P, _P, _L, _I, _P, _L, _P, _L, _P, _L, _P, _P),
+    "srml_logit_residual_det_f32": (_P, _L, _I, _L, _P, _P, _L, _I, _P, _L, _P, _L, _P, _L, _P, _P, _P),
+    "srml_logit_residual_ws": (_L, _I),
+    "srml_xtv_mfma_ws": (_L, _I, _I),
     "srml_mbin_f32": (_P, _L, _I, _L, _P, _P, _L, _I, _P, _L, _P),
     "srml_qn_step_batch": (_P, _I, _P),
     "srml_mlogit_f32": (_P, _L, _I, _L, _P, _P, _P, _P, _I, _P, _P),
@@ -142,7 +148,7 @@ def _load() -> ctypes.CDLL:
             except AttributeError:
                 continue
             fn.argtypes = list(argt)
-            fn.restype = ctypes.c_long if name == "srml_qn_args_size" else ctypes.c_int
+            fn.restype = ctypes.c_long if name in _LONG_RESULT else ctypes.c_int
         _lib = lib
         return lib
 

@@ -179,10 +179,16 @@ def _ref_loss_grad(X, y, W, b, K):
     (4000, 3000, 10, torch.float32, "fused_multinomial_f32"),
     (3000, 129, 3, torch.float32, "fused_multinomial_f32"),
     (1500, 300, 20, torch.float32, "torch"),
+    (5000, 3000, 1, torch.float32, "two_pass_deterministic_f32"),
+    (3001, 130, 1, torch.float32, "two_pass_deterministic_f32"),
+    (4000, 3000, 10, torch.float32, "two_pass_deterministic_f32"),
+    (3000, 129, 3, torch.float32, "two_pass_deterministic_f32"),
 ])
 def test_logistic_loss_grad_kernels(gpu_device, m, n, K, dtype, path, monkeypatch):
     if path == "fused_multinomial_f32":
         monkeypatch.setenv("SRML_LOGREG_FUSED", "1")
+    if path == "two_pass_deterministic_f32":
+        monkeypatch.setenv("SRML_DETERMINISTIC", "1")
     g = torch.Generator().manual_seed(m + n + K)
     X = torch.randn(m, n, generator=g, dtype=torch.float64).to(dtype).to(gpu_device)
     if K == 1:
@@ -299,3 +305,22 @@ def test_mbin_kernel_matches_torch(gpu_device, fused, monkeypatch):
     got = ops.logistic_loss_grad_multi(X.to(gpu_device), y.to(gpu_device), WB.to(gpu_device),
                                        torch.zeros((M, n + 2), dtype=torch.float64, device=gpu_device))
     torch.testing.assert_close(got.cpu(), ref, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("classes", [2, 4])
+def test_logistic_deterministic_mode_bit_identical(gpu_device, classes, monkeypatch):
+    """SRML_DETERMINISTIC=1: two fits give bit-identical coefficients (ordered folds, no atomics)
+    and agree with the default (atomic) path to solver tolerance."""
+    from spark_rapids_ml_nai_amd.classification import LogisticRegression
+
+    X, y = _data(20000, 300, classes, seed=3)
+    df = DataFrame.from_numpy(X, y)
+    est = LogisticRegression(regParam=1e-3, maxIter=60, tol=1e-10, standardization=False)
+    ref = est.fit(df)
+    monkeypatch.setenv("SRML_DETERMINISTIC", "1")
+    a = est.fit(df)
+    b = est.fit(df)
+    assert np.array_equal(np.asarray(a.coef_), np.asarray(b.coef_))
+    assert np.array_equal(np.asarray(a.intercept_), np.asarray(b.intercept_))
+    np.testing.assert_allclose(np.asarray(a.coef_), np.asarray(ref.coef_), atol=2e-3, rtol=2e-3)
