@@ -1,8 +1,10 @@
 /*
- * JNI entry points of libsrml_jni.so (native/jni/srml_jni.cpp) over the MI355X C ABI.
+ * JNI entry points of libsrml_jni.so (native/jni/srml_jni.cpp) over the MI355X C ABI (libsrml.so).
  * Parity with the reference's JniRAPIDSML (jvm/src/main/java/com/nvidia/spark/ml/linalg/
- * JniRAPIDSML.java:26-78): the shared library is extracted from the jar (or found on
- * java.library.path) and loaded once.
+ * JniRAPIDSML.java:26-78): the shared libraries are found on java.library.path or extracted from
+ * the jar (/<os.arch>/<os.name>/, where the Maven build bundles them) and loaded once.
+ * libsrml.so (the gfx950 kernels) is loaded first so the shim's DT_NEEDED entry resolves from the
+ * same temporary directory.
  */
 package com.amd.spark.ml.linalg;
 
@@ -14,33 +16,60 @@ import java.nio.file.StandardCopyOption;
 
 public final class JniSRML {
   private static volatile boolean loaded = false;
+  private static volatile Throwable loadError = null;
 
   private JniSRML() {}
 
+  /** Loads the native libraries; throws UnsatisfiedLinkError when they are unavailable. */
   public static synchronized void load() {
     if (loaded) {
       return;
     }
-    try {
-      System.loadLibrary("srml_jni");
-    } catch (UnsatisfiedLinkError e) {
-      String res = "/" + System.getProperty("os.arch") + "/" + System.getProperty("os.name") + "/libsrml_jni.so";
-      try (InputStream in = JniSRML.class.getResourceAsStream(res)) {
-        if (in == null) {
-          throw new UnsatisfiedLinkError("libsrml_jni.so not found on java.library.path nor at " + res);
-        }
-        File tmp = File.createTempFile("libsrml_jni", ".so");
-        tmp.deleteOnExit();
-        Files.copy(in, tmp.toPath(), StandardCopyOption.REPLACE_EXISTING);
-        System.load(tmp.getAbsolutePath());
-      } catch (IOException io) {
-        throw new UnsatisfiedLinkError("cannot extract libsrml_jni.so: " + io);
-      }
+    if (loadError != null) {
+      throw new UnsatisfiedLinkError("libsrml_jni unavailable: " + loadError);
     }
-    loaded = true;
+    try {
+      try {
+        System.loadLibrary("srml");
+        System.loadLibrary("srml_jni");
+      } catch (UnsatisfiedLinkError e) {
+        File dir = Files.createTempDirectory("srml_native").toFile();
+        dir.deleteOnExit();
+        System.load(extract("libsrml.so", dir));
+        System.load(extract("libsrml_jni.so", dir));
+      }
+      loaded = true;
+    } catch (Throwable t) {
+      loadError = t;
+      throw (t instanceof UnsatisfiedLinkError) ? (UnsatisfiedLinkError) t
+          : new UnsatisfiedLinkError("cannot load libsrml_jni: " + t);
+    }
   }
 
-  /** C (rows x k) = X (rows x n) . P (n x k); row-major host arrays. */
+  /** True when the native path can be used (loads on first call; never throws). */
+  public static boolean isAvailable() {
+    try {
+      load();
+      return true;
+    } catch (Throwable t) {
+      return false;
+    }
+  }
+
+  private static String extract(String name, File dir) throws IOException {
+    String res = "/" + System.getProperty("os.arch") + "/" + System.getProperty("os.name") + "/" + name;
+    try (InputStream in = JniSRML.class.getResourceAsStream(res)) {
+      if (in == null) {
+        throw new UnsatisfiedLinkError(name + " not found on java.library.path nor at " + res);
+      }
+      File out = new File(dir, name);
+      out.deleteOnExit();
+      Files.copy(in, out.toPath(), StandardCopyOption.REPLACE_EXISTING);
+      return out.getAbsolutePath();
+    }
+  }
+
+  /** C (rows x k) = X (rows x n) . P (n x k); row-major host arrays; P column-major like Spark's DenseMatrix. */
   public static native double[] dgemm(double[] x, long rows, int n, double[] pc, int k, int device);
 
   /** X^T X (cols x cols) of a rows x cols row-major matrix. */
@@ -51,4 +80,7 @@ public final class JniSRML {
 
   /** acc += c (element-wise). */
   public static native void accumulateCov(double[] acc, double[] c);
+
+  /** Version string of the native library (for diagnostics). */
+  public static native String version();
 }

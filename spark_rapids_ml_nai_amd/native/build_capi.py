@@ -34,6 +34,18 @@ def build(verbose: bool = False) -> str:
         if verbose:
             print(" ".join(cmd))
         subprocess.check_call(cmd)
+    # the JNI shim compiled against the test JNIEnv (native/tests/jni_harness) and driven by a
+    # C++ harness: runs every JniSRML entry point without a JVM (tests/test_native_capi.py)
+    shim = os.path.join(OUT, "srml_jni_shim_test")
+    shim_src = [os.path.join(NATIVE, "tests", "jni_shim_test.cpp"), os.path.join(NATIVE, "jni", "srml_jni.cpp")]
+    if not os.path.exists(shim) or os.path.getmtime(shim) < max([os.path.getmtime(f) for f in shim_src] +
+                                                                [os.path.getmtime(lib)]):
+        cmd = [_hipcc(), "-O2", "-std=c++17", "-I", os.path.join(NATIVE, "tests", "jni_harness"), "-I",
+               os.path.join(NATIVE, "include")] + shim_src + ["-L", libdir, "-l:" + os.path.basename(lib),
+                                                              "-Wl,-rpath," + libdir, "-o", shim]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.check_call(cmd)
     jni_inc = _find_jni()
     if jni_inc:
         so = os.path.join(OUT, "libsrml_jni.so")
@@ -44,6 +56,10 @@ def build(verbose: bool = False) -> str:
                 "-Wl,-rpath," + libdir, "-o", so]
         subprocess.check_call(cmd)
     return exe
+
+
+def shim_test_path() -> str:
+    return os.path.join(OUT, "srml_jni_shim_test")
 
 
 def _find_jni() -> list:

@@ -634,6 +634,12 @@ def rf_hist(bins: torch.Tensor, idx: torch.Tensor, label: torch.Tensor, wcnt: Op
     else:
         yscale = 1.0
     st = native.stream(dev)
+    if regression and deterministic():
+        # exact i64 fixed-point cross-chunk folds, converted in place: bit-reproducible histograms
+        native.call("srml_rf_hist_fixed", bins.data_ptr(), m, idx.data_ptr(), wy.data_ptr(), _c(items).data_ptr(),
+                    int(items.shape[0]), _c(node_feats).data_ptr(), nf, B, float(yscale), fb, hist.data_ptr(), st)
+        native.call("srml_rf_hist_fixed_finish", hist.data_ptr(), hist.numel(), float(yscale), st)
+        return hist
     native.call("srml_rf_hist", bins.data_ptr(), m, idx.data_ptr(), wy.data_ptr(), _c(items).data_ptr(),
                 int(items.shape[0]), _c(node_feats).data_ptr(), nf, B, S, int(regression), float(yscale), fb,
                 hist.data_ptr() if not regression else None, hist.data_ptr() if regression else None, st)
@@ -759,6 +765,12 @@ def rf_node_stats(idx: torch.Tensor, wpos: torch.Tensor, label: torch.Tensor, bo
         cs = torch.cat([torch.zeros((K, 1), dtype=torch.float64), vals.cumsum(1)], 1)
         b = bounds.long()
         return (cs[:, b[1:]] - cs[:, b[:-1]]).T.contiguous()
+    if deterministic():  # one block per segment, fixed-order reduction, no atomics
+        out = torch.empty((nseg, K), dtype=torch.float64, device=dev)
+        native.call("srml_rf_node_stats_det", idx.data_ptr(), _c(wpos.float()).data_ptr(),
+                    _c(label.float()).data_ptr(), _c(bounds.long()).data_ptr(), nseg, int(S), int(regression),
+                    out.data_ptr(), native.stream(dev))
+        return out
     out = torch.zeros((nseg, K), dtype=torch.float64, device=dev)
     native.call("srml_rf_node_stats", idx.data_ptr(), _c(wpos.float()).data_ptr(), _c(label.float()).data_ptr(),
                 int(idx.shape[0]), _c(bounds.long()).data_ptr(), nseg, int(S), int(regression), out.data_ptr(),

@@ -167,7 +167,7 @@ SRML_API int srml_rf_quantize_u8(const float* X, long m, int n, long ld, const f
 // sum, fp32 in LDS folded into the fp64 output). Two rows per thread per step: all 16 bin gathers are
 // issued before the first LDS atomic (ILP instead of a load->atomic chain per row).
 // ------------------------------------------------------------------------------------------
-template <bool REG>
+template <bool REG, bool FIXED = false>
 __global__ __launch_bounds__(256) void rf_hist_kernel(const unsigned char* __restrict__ bins, long m,
                                                       const int* __restrict__ idx, const float2* __restrict__ wy,
                                                       const int4* __restrict__ items, const int* __restrict__ node_feats,
@@ -236,7 +236,14 @@ __global__ __launch_bounds__(256) void rf_hist_kernel(const unsigned char* __res
   const double inv = 1.0 / yscale;
   for (int i = threadIdx.x; i < valid_cells; i += 256) {
     const int j = i / (B * S), rem = i % (B * S), b = rem / S, st = rem % S;
-    if (REG) {
+    if (REG && FIXED) {
+      // deterministic mode: the cells hold i64 fixed-point integers (two's complement u64
+      // atomics add exactly, in any order); srml_rf_hist_fixed_finish converts them to fp64
+      const unsigned long long q = st == 0 ? (unsigned long long)lh_u[j * B + b] : lh_s[j * B + b];
+      unsigned long long* cell = reinterpret_cast<unsigned long long*>(hist_d) + out_base + i;
+      if (excl) *cell = q;
+      else if (q) atomicAdd(cell, q);
+    } else if (REG) {
       double v;
       if (st == 0) v = (double)lh_u[j * B + b];
       else v = (double)(long long)lh_s[j * B + b] * inv;
@@ -286,6 +293,43 @@ SRML_API int srml_rf_hist(const unsigned char* bins, long m, const int* idx, con
 }
 
 SRML_API int srml_rf_hist_fb_max() { return FB; }
+
+// Deterministic regression histograms (SRML_DETERMINISTIC): same work items as srml_rf_hist, but
+// the cross-chunk fold adds exact i64 fixed-point integers (order-independent) into the fp64
+// buffer's bits; srml_rf_hist_fixed_finish then converts every cell in place (count -> double,
+// sum -> integer / yscale). Bit-identical results for any block scheduling.
+SRML_API int srml_rf_hist_fixed(const unsigned char* bins, long m, const int* idx, const float* wy, const int* items,
+                                int n_items, const int* node_feats, int nf, int B, double yscale, int fb,
+                                double* hist_d, hipStream_t stream) {
+  if (n_items <= 0) return 0;
+  if (fb < 1 || fb > FB) return -7;
+  const size_t lds = (size_t)fb * B * 3 * sizeof(unsigned);
+  if (lds > 160 * 1024) return -5;
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)rf_hist_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+  hipLaunchKernelGGL((rf_hist_kernel<true, true>), dim3(n_items), dim3(256), lds, stream, bins, m, idx,
+                     reinterpret_cast<const float2*>(wy), reinterpret_cast<const int4*>(items), node_feats, nf, B, 2,
+                     fb, yscale, nullptr, hist_d);
+  return srml_status();
+}
+
+__global__ __launch_bounds__(256) void rf_hist_fixed_finish_kernel(double* __restrict__ hist, long pairs, double inv) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= pairs) return;
+  const long long* q = reinterpret_cast<const long long*>(hist) + 2 * i;
+  const long long c = q[0], s = q[1];
+  hist[2 * i] = (double)c;
+  hist[2 * i + 1] = (double)s * inv;
+}
+
+SRML_API int srml_rf_hist_fixed_finish(double* hist_d, long cells, double yscale, hipStream_t stream) {
+  const long pairs = cells / 2;
+  if (pairs <= 0) return 0;
+  hipLaunchKernelGGL(rf_hist_fixed_finish_kernel, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, stream, hist_d,
+                     pairs, 1.0 / yscale);
+  return srml_status();
+}
 
 // ------------------------------------------------------------------------------------------
 // split search. crit: 0 gini, 1 entropy, 2 variance.  out per node (double[6]):
@@ -564,6 +608,54 @@ __global__ __launch_bounds__(256) void rf_node_stats_kernel(const int* __restric
     }
     __syncthreads();
   }
+}
+
+// deterministic variant (SRML_DETERMINISTIC): one block per segment, strided per-thread sums and
+// a fixed-order block reduction, plain stores (no atomics: bit-identical run to run)
+__global__ __launch_bounds__(256) void rf_node_stats_seg_kernel(const int* __restrict__ idx,
+                                                                const float* __restrict__ wpos,
+                                                                const float* __restrict__ label,
+                                                                const long long* __restrict__ bounds, int S,
+                                                                int regression, double* __restrict__ out) {
+  __shared__ double red[4][32];
+  const int seg = blockIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int NS = regression ? 3 : S;
+  double acc[32];
+#pragma unroll
+  for (int k = 0; k < 32; ++k) acc[k] = 0.0;
+  for (long i = bounds[seg] + threadIdx.x; i < bounds[seg + 1]; i += 256) {
+    const double w = wpos[i];
+    const double y = label[idx[i]];
+    if (regression) {
+      acc[0] += w;
+      acc[1] += w * y;
+      acc[2] += w * y * y;
+    } else {
+      const int c = (int)y;
+#pragma unroll
+      for (int k = 0; k < 32; ++k)
+        if (k == c) acc[k] += w;
+    }
+  }
+  for (int k = 0; k < NS; ++k) {
+    const double v = wave_sum(acc[k]);
+    if (lane == 0) red[wid][k] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < NS)
+    out[(long)seg * NS + threadIdx.x] =
+        ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+}
+
+SRML_API int srml_rf_node_stats_det(const int* idx, const float* wpos, const float* label,
+                                    const long long* bounds, int nseg, int S, int regression, double* out,
+                                    hipStream_t stream) {
+  if (nseg <= 0) return 0;
+  if (!regression && S > 32) return -7;
+  hipLaunchKernelGGL(rf_node_stats_seg_kernel, dim3((unsigned)nseg), dim3(256), 0, stream, idx, wpos, label, bounds,
+                     S, regression, out);
+  return srml_status();
 }
 
 SRML_API int srml_rf_node_stats(const int* idx, const float* wpos, const float* label, long total,

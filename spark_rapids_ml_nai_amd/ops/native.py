@@ -105,6 +105,9 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_rf_route": (_P, _L, _P, _P, _L, _P, _P, _P, _P, _P),
     "srml_rf_route_segments": (_P, _L, _P, _L, _P, _I, _P, _P, _P, _P, _P),
     "srml_rf_node_stats": (_P, _P, _P, _L, _P, _I, _I, _I, _P, _P),
+    "srml_rf_node_stats_det": (_P, _P, _P, _P, _I, _I, _I, _P, _P),
+    "srml_rf_hist_fixed": (_P, _L, _P, _P, _P, _I, _P, _I, _I, _D, _I, _P, _P),
+    "srml_rf_hist_fixed_finish": (_P, _L, _D, _P),
     "srml_csr_logreg_binary_f32": (_P, _P, _P, _L, _I, _L, _P, _P, _D, _P, _P, _P, _P),
     "srml_csr_logreg_binary_f64": (_P, _P, _P, _L, _I, _L, _P, _P, _D, _P, _P, _P, _P),
     "srml_csr_spmm_f32": (_P, _P, _P, _L, _L, _P, _I, _P, _P, _P),

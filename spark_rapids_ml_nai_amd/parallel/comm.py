@@ -136,7 +136,15 @@ class Communicator:
         n = torch.tensor([t.shape[0]], dtype=torch.int64, device=self.device)
         sizes = self.allgather(n).tolist()
         mx = max(sizes)
-        pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        tail = tuple(t.shape[1:])
+        if self._backend == "nccl" and min(sizes) != mx:
+            # RCCL: ragged blocks travel at their own size (ProcessGroupNCCL turns an uneven
+            # all_gather into one group of per-root broadcasts), no padding to the largest block
+            ct = self._comm_tensor(t.contiguous())
+            out = [torch.empty((s,) + tail, dtype=t.dtype, device=ct.device) for s in sizes]
+            dist.all_gather(out, ct, group=self.group)
+            return out
+        pad = torch.zeros((mx,) + tail, dtype=t.dtype, device=t.device)
         pad[: t.shape[0]] = t
         g = self.allgather(pad).view((self.size, mx) + tuple(t.shape[1:]))
         return [g[r, : sizes[r]] for r in range(self.size)]

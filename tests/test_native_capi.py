@@ -18,6 +18,18 @@ def test_capi_program():
     assert r.returncode == 0, r.stdout + r.stderr
 
 
+def test_jni_shim_program():
+    """native/jni/srml_jni.cpp executed through the test JNIEnv (no JVM): dgemm layout, cov,
+    calSVD conventions, accumulateCov, argument checks, pin balance."""
+    from spark_rapids_ml_nai_amd.native import build_capi
+
+    build_capi.build()
+    r = subprocess.run([build_capi.shim_test_path()], capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "jni shim: ok" in r.stdout
+
+
 def test_capi_python_bindings():
     from spark_rapids_ml_nai_amd import native
 

@@ -195,3 +195,77 @@ def test_dgemm_cpu_matches_torch():
     B = _rand(50, 20, "cpu", seed=2)
     torch.testing.assert_close(ops.dgemm(A, B, ta=True), A.T @ B)
     assert ops._dgemm_splits(3000, 19, 3000, 47) > 1 and ops._dgemm_splits(3000, 3000, 3000, 2209) == 1
+
+
+# ---------------------------------------------------------------- RF regression determinism ---
+@pytest.mark.gpu
+def test_rf_regression_hist_deterministic(gpu_device, monkeypatch):
+    """Fixed-point cross-chunk folds: bit-identical repeats, equal to the fp64 CPU histogram
+    within the fixed-point step, and to the default (atomic fp64) kernel within rounding."""
+    g = torch.Generator().manual_seed(5)
+    n, m, B, nf, nodes = 12, 60000, 32, 10, 3
+    bins = torch.randint(0, B, (n, m), generator=g, dtype=torch.uint8)
+    y = torch.randn(m, generator=g) * 3.0 + 1.0
+    idx = torch.randperm(m, generator=g)[:50000].sort().values.int()
+    w = torch.randint(0, 3, (50000,), generator=g).float()
+    feats = torch.stack([torch.randperm(n, generator=g)[:nf] for _ in range(nodes)]).int()
+    fb = ops.rf_hist_fb(B, 2, True)
+    bounds = [0, 9000, 30000, 50000]
+    items = []
+    for node in range(nodes):  # several row chunks per node -> cross-chunk folds
+        for rb in range(bounds[node], bounds[node + 1], 4096):
+            for fc in range((nf + fb - 1) // fb):
+                items.append([node, rb, min(rb + 4096, bounds[node + 1]), fc])
+    items = torch.tensor(items, dtype=torch.int32)
+    dev = lambda t: t.to(gpu_device)  # noqa: E731
+    ys = ops.rf_yscale(dev(y))
+    monkeypatch.setenv("SRML_DETERMINISTIC", "1")
+    h1 = ops.rf_hist(dev(bins), dev(idx), dev(y), None, dev(items), dev(feats), nodes, B, 2, True,
+                     pos_weight=dev(w), yscale=ys)
+    h2 = ops.rf_hist(dev(bins), dev(idx), dev(y), None, dev(items), dev(feats), nodes, B, 2, True,
+                     pos_weight=dev(w), yscale=ys)
+    assert torch.equal(h1, h2)
+    ref = ops.rf_hist(bins, idx, y, None, items, feats, nodes, B, 2, True, pos_weight=w)
+    torch.testing.assert_close(h1.cpu(), ref, rtol=1e-6, atol=1e-5)
+    monkeypatch.setenv("SRML_DETERMINISTIC", "0")
+    h3 = ops.rf_hist(dev(bins), dev(idx), dev(y), None, dev(items), dev(feats), nodes, B, 2, True,
+                     pos_weight=dev(w), yscale=ys)
+    torch.testing.assert_close(h3, h1, rtol=1e-9, atol=1e-7)
+
+
+@pytest.mark.gpu
+def test_rf_node_stats_deterministic(gpu_device, monkeypatch):
+    g = torch.Generator().manual_seed(6)
+    m = 200000
+    y = torch.randn(m, generator=g)
+    idx = torch.randperm(m, generator=g).int()
+    w = torch.randint(0, 4, (m,), generator=g).float()
+    bounds = torch.tensor([0, 5, 70000, 70001, 150000, m], dtype=torch.int64)
+    ref = ops.rf_node_stats(idx, w, y, bounds, 3, True)
+    monkeypatch.setenv("SRML_DETERMINISTIC", "1")
+    a = ops.rf_node_stats(idx.to(gpu_device), w.to(gpu_device), y.to(gpu_device), bounds.to(gpu_device), 3, True)
+    b = ops.rf_node_stats(idx.to(gpu_device), w.to(gpu_device), y.to(gpu_device), bounds.to(gpu_device), 3, True)
+    assert torch.equal(a, b)
+    torch.testing.assert_close(a.cpu(), ref, rtol=1e-10, atol=1e-8)
+    yc = torch.randint(0, 5, (m,), generator=g).float()
+    rc = ops.rf_node_stats(idx, w, yc, bounds, 5, False)
+    c = ops.rf_node_stats(idx.to(gpu_device), w.to(gpu_device), yc.to(gpu_device), bounds.to(gpu_device), 5, False)
+    torch.testing.assert_close(c.cpu(), rc)
+
+
+@pytest.mark.gpu
+def test_rf_regressor_fit_bit_reproducible(gpu_device, monkeypatch):
+    from spark_rapids_ml_nai_amd import DataFrame
+    from spark_rapids_ml_nai_amd.regression import RandomForestRegressor
+
+    monkeypatch.setenv("SRML_DETERMINISTIC", "1")
+    rng = np.random.default_rng(3)
+    X = rng.standard_normal((30000, 16)).astype(np.float32)
+    y = X[:, 0] * 2 + np.sin(X[:, 1]) + 0.1 * rng.standard_normal(30000)
+    df = DataFrame.from_numpy(X, y)
+    est = RandomForestRegressor(numTrees=6, maxDepth=7, seed=11)
+    a, b = est.fit(df), est.fit(df)
+    pa = a.transform(df).to_numpy("prediction")
+    pb = b.transform(df).to_numpy("prediction")
+    assert np.array_equal(pa, pb)
+    assert np.corrcoef(pa, y)[0, 1] > 0.9
