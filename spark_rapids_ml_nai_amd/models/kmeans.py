@@ -172,6 +172,9 @@ def kmeans_fit(X: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext, k
     # k > 256: 256 x 256 LDS-DMA kernel on the tiled plane layout (SRML_SPLIT_TILED=0: plain layout)
     tiled = k > 256 and os.environ.get("SRML_SPLIT_TILED", "1") == "1"
     XP = ops.split_bf16x3(X, tiled=tiled) if _use_split(X, k) else None
+    # filter-and-refine Lloyd search on the tiled planes: 3-product pass + exact re-search of the
+    # near-tie rows (SRML_KMEANS_CERTIFIED=0: always the 6-product search)
+    certified = tiled and XP is not None and X.is_cuda and os.environ.get("SRML_KMEANS_CERTIFIED", "1") == "1"
     if init in ("random",):
         C = init_random(X, desc, ctx, k, seed)
     elif init in ("scalable-k-means++", "k-means||", "k-means++"):
@@ -185,7 +188,7 @@ def kmeans_fit(X: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext, k
     for it in range(max(0, max_iter)):
         n_iter = it + 1
         if XP is not None:
-            labels, d2 = ops.nearest_centroid_split(XP, X.shape[0], C.float(), xnorm)
+            labels, d2 = ops.nearest_centroid_split(XP, X.shape[0], C.float(), xnorm, X=X if certified else None)
         else:
             labels, d2 = ops.nearest_centroid(X, C.float(), xnorm)
         sums, counts = ops.cluster_sums(X, labels, k)

@@ -367,13 +367,59 @@ def split_bf16x3(X: torch.Tensor, row_multiple: int = 128, tiled: bool = False) 
     return P
 
 
+CERTIFY_TAU = 2.0 ** -13  # dot-product error bound of the 3-product search, relative to ||x|| ||c||
+
+
+def _nearest_centroid_certified(XP: torch.Tensor, X: torch.Tensor, m: int, k: int, CP: torch.Tensor,
+                                cn: torch.Tensor, xnorm: torch.Tensor, st: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Filter-and-refine arg-min: the 3-product search (half the MFMAs of the fp32-exact one)
+    keeps every row's best and second-best distance; rows whose gap exceeds the error bound of
+    the dropped products (4 tau ||x|| max||c||) are certified — the exact search would pick the
+    same centroid — and only the remaining near-tie rows are re-searched with the 6-product
+    kernel (their labels and distances are then bit-identical to the exact path)."""
+    dev = XP.device
+    nslot = int(native.lib().srml_nearest_centroid_split_top2_nslot(k))
+    keys = torch.empty(m * nslot, dtype=torch.int64, device=dev)
+    sec = torch.empty(m * nslot, dtype=torch.float32, device=dev)
+    xrows, kp, crows = XP.shape[1] * 256, XP.shape[2] * 16, CP.shape[1] * 256
+    native.call("srml_nearest_centroid_split_top2", XP.data_ptr(), m, xrows, kp, CP.data_ptr(), k, crows,
+                cn.data_ptr(), keys.data_ptr(), sec.data_ptr(), st)
+    xn = _c(xnorm.float())
+    cmax2 = cn.max().view(1)
+    labels = torch.empty(m, dtype=torch.int32, device=dev)
+    dist = torch.empty(m, dtype=torch.float32, device=dev)
+    flagged = torch.empty(m, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    native.call("srml_split_top2_select", keys.data_ptr(), sec.data_ptr(), m, nslot, xn.data_ptr(),
+                cmax2.data_ptr(), float(CERTIFY_TAU), labels.data_ptr(), dist.data_ptr(), flagged.data_ptr(),
+                cnt.data_ptr(), st)
+    del keys, sec
+    nf = int(cnt.item())
+    _CERTIFY_STATS["rows"] += m
+    _CERTIFY_STATS["refined"] += nf
+    if nf:
+        rows = flagged[:nf]
+        XPr = split_bf16x3(X.index_select(0, rows.long()), tiled=True)
+        best = torch.full((nf,), -1, dtype=torch.int64, device=dev)
+        native.call("srml_nearest_centroid_split_tiled_np", XPr.data_ptr(), nf, XPr.shape[1] * 256, kp,
+                    CP.data_ptr(), k, crows, cn.data_ptr(), best.data_ptr(), 6, st)
+        native.call("srml_split_scatter_refined", best.data_ptr(), rows.data_ptr(), nf, xn.data_ptr(),
+                    labels.data_ptr(), dist.data_ptr(), st)
+    return labels, dist
+
+
+_CERTIFY_STATS = {"rows": 0, "refined": 0}  # filter-and-refine counters (diagnostics / tests)
+
+
 def nearest_centroid_split(XP: torch.Tensor, m: int, C: torch.Tensor, xnorm: torch.Tensor,
-                           cnorm: Optional[torch.Tensor] = None, approx: bool = False
-                           ) -> Tuple[torch.Tensor, torch.Tensor]:
+                           cnorm: Optional[torch.Tensor] = None, approx: bool = False,
+                           X: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """``nearest_centroid`` on pre-split X planes (``split_bf16x3``): the distance GEMM runs on
     the bf16 matrix cores as six cross products of the planes (fp32-accurate; see splitmm.hip).
     ``approx=True`` (tiled planes): only the three leading products (~2^-16 relative dot error,
-    half the MFMAs) — for consumers of approximate distances (k-means|| sampling)."""
+    half the MFMAs) — for consumers of approximate distances (k-means|| sampling).
+    ``X`` given (tiled planes, GPU): certified filter-and-refine search — the 3-product pass plus
+    an exact 6-product re-search of the near-tie rows only; same labels as the exact search."""
     k = C.shape[0]
     Cf = C.float()
     if cnorm is None:
@@ -389,8 +435,10 @@ def nearest_centroid_split(XP: torch.Tensor, m: int, C: torch.Tensor, xnorm: tor
         v, i = (cnorm.float().view(1, -1) - 2.0 * dot).min(1)
         return i.int(), (v + xnorm.float()).clamp_min(0)
     cn = _c(cnorm.to(torch.float32))
-    best = torch.full((m,), -1, dtype=torch.int64, device=XP.device)
     st = native.stream(XP.device)
+    if X is not None and tiled and not approx:
+        return _nearest_centroid_certified(XP, X, m, k, CP, cn, xnorm, st)
+    best = torch.full((m,), -1, dtype=torch.int64, device=XP.device)
     if tiled:
         native.call("srml_nearest_centroid_split_tiled_np", XP.data_ptr(), m, XP.shape[1] * 256, XP.shape[2] * 16,
                     CP.data_ptr(), k, CP.shape[1] * 256, cn.data_ptr(), best.data_ptr(), 3 if approx else 6, st)

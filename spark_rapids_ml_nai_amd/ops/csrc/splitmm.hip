@@ -31,6 +31,7 @@
 
 namespace {
 using srml_tile::orderable;
+using srml_tile::unorderable;
 
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned uintx4 __attribute__((ext_vector_type(4)));
@@ -184,6 +185,63 @@ __device__ __forceinline__ void split_epilogue(const floatx16 (&acc)[BM / WM / 3
   }
 }
 
+// Top-2 epilogue for the certified 3-product search: per (row, wave column slot) the best
+// (value, index) and the second-best value of the wave's BN/WN columns, plain stores into
+// keys/sec[row * nslot + slot] (slot = ctile * WN + wn). srml_split_top2_select merges the slots.
+template <int BM, int BN, int WM, int WN>
+__device__ __forceinline__ void split_epilogue_top2(const floatx16 (&acc)[BM / WM / 32][BN / WN / 32], long row0,
+                                                    int col0, int ctile, long m, int k,
+                                                    const float* __restrict__ cnorm,
+                                                    unsigned long long* __restrict__ keys, float* __restrict__ sec,
+                                                    int nslot, int wm, int wn, int li, int lk) {
+  constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+  float cn[TN];
+  int cj[TN];
+#pragma unroll
+  for (int nt = 0; nt < TN; ++nt) {
+    cj[nt] = col0 + wn * (BN / WN) + nt * 32 + li;
+    cn[nt] = (cj[nt] < k) ? cnorm[cj[nt]] : 0.f;
+  }
+  const int slot = ctile * WN + wn;
+#pragma unroll
+  for (int mt = 0; mt < TM; ++mt) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float bv = __builtin_huge_valf(), b2 = __builtin_huge_valf();
+      int bi = 0x7fffffff;
+#pragma unroll
+      for (int nt = 0; nt < TN; ++nt) {
+        if (cj[nt] < k) {
+          const float d = fmaf(-2.f, acc[mt][nt][r], cn[nt]);
+          if (d < bv) { b2 = bv; bv = d; bi = cj[nt]; }
+          else if (d < b2) b2 = d;
+        }
+      }
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) {
+        const float ov = __shfl_xor(bv, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        const float o2 = __shfl_xor(b2, o, 64);
+        if (ov < bv || (ov == bv && oi < bi)) {
+          b2 = fminf(bv, o2);
+          bv = ov;
+          bi = oi;
+        } else {
+          b2 = fminf(b2, ov);
+        }
+      }
+      if (li == 0) {
+        const long row = row0 + wm * (BM / WM) + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        if (row < m) {
+          const long o = row * nslot + slot;
+          keys[o] = bi == 0x7fffffff ? ~0ull : (((unsigned long long)orderable(bv) << 32) | (unsigned)bi);
+          sec[o] = b2;
+        }
+      }
+    }
+  }
+}
+
 template <int BM, int BN>
 struct SplitStage {
   unsigned short A[3][BM][ROWB];
@@ -318,10 +376,11 @@ typedef __attribute__((address_space(1))) void* gbl_vptr;
 // TILED: operands in the split_tiled_kernel layout (contiguous, pre-swizzled 8 KiB k-step images).
 // NP = 6: the fp32-exact product set; NP = 3: h.h + h.m + m.h only (~2^-16 relative, half the
 // MFMAs) for consumers that only need approximate distances (k-means|| D^2 sampling / weighting).
-template <bool TILED, int NP = 6>
+template <bool TILED, int NP = 6, bool TOP2 = false>
 __global__ __launch_bounds__(512, 1) void nearest_centroid_split_glds_kernel(
     const unsigned short* __restrict__ XP, long m, long xrows, int kp, const unsigned short* __restrict__ CP, int k,
-    long crows, const float* __restrict__ cnorm, unsigned long long* __restrict__ best, int n_ctiles) {
+    long crows, const float* __restrict__ cnorm, unsigned long long* __restrict__ best, int n_ctiles,
+    float* __restrict__ sec = nullptr) {
   constexpr int BM = 256, BN = 256, WM = 2, WN = 4, TM = 4, TN = 2, NS = 3;
   __shared__ __attribute__((aligned(1024))) unsigned short lds[NS][6][256][16];
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -410,7 +469,62 @@ __global__ __launch_bounds__(512, 1) void nearest_centroid_split_glds_kernel(
     }
     stage = stage == 2 ? 0 : stage + 1;
   }
-  split_epilogue<BM, BN, WM, WN>(acc, row0, col0, m, k, cnorm, best, wm, wn, li, lk);
+  if (TOP2)
+    split_epilogue_top2<BM, BN, WM, WN>(acc, row0, col0, ctile, m, k, cnorm, best, sec, n_ctiles * WN, wm, wn, li, lk);
+  else
+    split_epilogue<BM, BN, WM, WN>(acc, row0, col0, m, k, cnorm, best, wm, wn, li, lk);
+}
+
+// Merge the top-2 slots of every row and certify the 3-product arg-min: with the dropped
+// products bounded by |x.c - (x.c)_3| <= tau ||x|| ||c|| (tau = 2^-13 covers the 3 * 2^-16
+// truncation with 8x slack for fp32 accumulation order), a row whose best / second-best gap
+// exceeds 4 tau ||x|| max||c|| has the same arg-min as the fp32-exact 6-product search. Certified
+// rows get their label and distance; the rest are appended to `flagged` (count in *n_flagged)
+// for an exact re-search.
+__global__ __launch_bounds__(256) void split_top2_select_kernel(const unsigned long long* __restrict__ keys,
+                                                                const float* __restrict__ sec, long m, int nslot,
+                                                                const float* __restrict__ xnorm,
+                                                                const float* __restrict__ cmax2, float tau,
+                                                                int* __restrict__ labels, float* __restrict__ dist,
+                                                                int* __restrict__ flagged, int* __restrict__ n_flagged) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= m) return;
+  const unsigned long long* kr = keys + i * nslot;
+  const float* sr = sec + i * nslot;
+  unsigned long long k1 = ~0ull;
+  int s1 = 0;
+  for (int s = 0; s < nslot; ++s) {
+    const unsigned long long v = kr[s];
+    if (v < k1) { k1 = v; s1 = s; }
+  }
+  float second = __builtin_huge_valf();
+  for (int s = 0; s < nslot; ++s) {
+    second = fminf(second, sr[s]);
+    if (s != s1 && kr[s] != ~0ull) second = fminf(second, unorderable((unsigned)(kr[s] >> 32)));
+  }
+  const float bv = unorderable((unsigned)(k1 >> 32));
+  const float xn = xnorm[i];
+  const float thr = 4.f * tau * sqrtf(fmaxf(xn, 0.f) * fmaxf(cmax2[0], 0.f));
+  if (k1 != ~0ull && second - bv > thr) {
+    labels[i] = (int)(k1 & 0xffffffffu);
+    const float d = bv + xn;
+    dist[i] = d > 0.f ? d : 0.f;
+  } else {
+    flagged[atomicAdd(n_flagged, 1)] = (int)i;
+  }
+}
+
+__global__ __launch_bounds__(256) void split_scatter_refined_kernel(const unsigned long long* __restrict__ best,
+                                                                    const int* __restrict__ rows, int nf,
+                                                                    const float* __restrict__ xnorm,
+                                                                    int* __restrict__ labels, float* __restrict__ dist) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= nf) return;
+  const int r = rows[j];
+  const unsigned long long key = best[j];
+  labels[r] = (int)(key & 0xffffffffu);
+  const float d = unorderable((unsigned)(key >> 32)) + xnorm[r];
+  dist[r] = d > 0.f ? d : 0.f;
 }
 }  // namespace
 
@@ -502,4 +616,42 @@ SRML_API int srml_nearest_centroid_split_tiled(const unsigned short* XP, long m,
                                                const unsigned short* CP, int k, long crows, const float* cnorm,
                                                unsigned long long* best, hipStream_t stream) {
   return srml_nearest_centroid_split_tiled_np(XP, m, xrows, kp, CP, k, crows, cnorm, best, 6, stream);
+}
+
+// Certified 3-product nearest-centroid search, phase 1 (tiled planes, as
+// srml_nearest_centroid_split_tiled_np): top-2 slots per row, keys/sec sized m * ceil(k/256) * 4.
+SRML_API int srml_nearest_centroid_split_top2(const unsigned short* XP, long m, long xrows, int kp,
+                                              const unsigned short* CP, int k, long crows, const float* cnorm,
+                                              unsigned long long* keys, float* sec, hipStream_t stream) {
+  if (m <= 0 || k <= 0) return 0;
+  if ((kp & 15) || xrows < m || crows < k || (crows & 255) || (xrows & 255)) return -2;
+  if ((reinterpret_cast<uintptr_t>(XP) & 15) || (reinterpret_cast<uintptr_t>(CP) & 15)) return -5;
+  const long rt = (m + 255) / 256;
+  const int ct = (k + 255) / 256;
+  const long nb = rt * ct;
+  if (nb > 0x7fffffffL) return -3;
+  hipLaunchKernelGGL((nearest_centroid_split_glds_kernel<true, 3, true>), dim3((unsigned)nb), dim3(512), 0, stream, XP,
+                     m, xrows, kp, CP, k, crows, cnorm, keys, (int)ct, sec);
+  return srml_status();
+}
+
+SRML_API int srml_nearest_centroid_split_top2_nslot(int k) { return ((k + 255) / 256) * 4; }
+
+// phase 2: merge slots, certify, emit labels / distances of certified rows, list the others
+SRML_API int srml_split_top2_select(const unsigned long long* keys, const float* sec, long m, int nslot,
+                                    const float* xnorm, const float* cmax2, float tau, int* labels, float* dist,
+                                    int* flagged, int* n_flagged, hipStream_t stream) {
+  if (m <= 0) return 0;
+  hipLaunchKernelGGL(split_top2_select_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream, keys, sec, m,
+                     nslot, xnorm, cmax2, tau, labels, dist, flagged, n_flagged);
+  return srml_status();
+}
+
+// phase 3 epilogue: exact keys of the re-searched rows -> labels / distances at their positions
+SRML_API int srml_split_scatter_refined(const unsigned long long* best, const int* rows, int nf, const float* xnorm,
+                                        int* labels, float* dist, hipStream_t stream) {
+  if (nf <= 0) return 0;
+  hipLaunchKernelGGL(split_scatter_refined_kernel, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, stream, best,
+                     rows, nf, xnorm, labels, dist);
+  return srml_status();
 }

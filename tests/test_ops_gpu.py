@@ -677,3 +677,28 @@ def test_nearest_centroid_split_tiled_approx(gpu_device, m, n, k):
     scale = (xnorm.double().view(-1) + (C.double() ** 2).sum(1).max()).max().item()
     assert (got - ref).abs().max().item() <= 1e-4 * scale
     assert (d2.double() - ref).abs().max().item() <= 1e-4 * scale
+
+
+@pytest.mark.parametrize("m,n,k,ties", [(1024, 3000, 257, False), (70000, 200, 1000, False),
+                                        (20000, 512, 600, True), (5000, 64, 300, True)])
+def test_nearest_centroid_certified_matches_exact(gpu_device, m, n, k, ties):
+    """Filter-and-refine (3-product pass + exact re-search of near ties) == the 6-product search:
+    identical labels, identical distances on re-searched rows, 3-product-accurate elsewhere."""
+    X = _rand(m, n, gpu_device, seed=21)
+    C = _rand(k, n, gpu_device, seed=22)
+    if ties:  # near-duplicate centres and rows sitting on bisectors: many sub-tolerance gaps
+        C[1::2] = C[0::2][: C[1::2].shape[0]] + 1e-6 * torch.randn_like(C[1::2])
+        X[: m // 4] = 0.5 * (C[0].view(1, -1) + C[2].view(1, -1)) + 1e-7 * torch.randn_like(X[: m // 4])
+    xnorm = ops.row_sqnorm(X)
+    XP = ops.split_bf16x3(X, tiled=True)
+    lab_e, d_e = ops.nearest_centroid_split(XP, m, C, xnorm)
+    before = dict(ops._CERTIFY_STATS)
+    lab_c, d_c = ops.nearest_centroid_split(XP, m, C, xnorm, X=X)
+    refined = ops._CERTIFY_STATS["refined"] - before["refined"]
+    assert torch.equal(lab_c, lab_e)
+    scale = (xnorm.double().view(-1) + (C.double() ** 2).sum(1).max()).max().item()
+    assert (d_c.double() - d_e.double()).abs().max().item() <= 1e-4 * scale
+    if ties:
+        assert refined >= m // 4  # every bisector row was re-searched
+    else:
+        assert refined < m  # the filter certifies rows on generic data
