@@ -134,6 +134,9 @@ def model_evidence(name: str, model: Any) -> Dict[str, Any]:
         if name.startswith("kmeans"):
             ev["n_iter"] = int(model._model_attributes.get("n_iter", 0))
             ev["k"] = len(model.cluster_centers_)
+            rf = model._model_attributes.get("refined_frac")
+            if rf is not None:
+                ev["refined_frac"] = float(rf)
         elif name == "logistic_regression":
             ev["num_iters"] = int(model.num_iters)
             ev["objective"] = float(model.objective)

@@ -76,7 +76,8 @@ def _weighted_lloyd(P: torch.Tensor, w: torch.Tensor, C: torch.Tensor, iters: in
 
 def init_kmeans_parallel(X: torch.Tensor, xnorm: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext,
                          k: int, seed: int, oversampling: float = 2.0, steps: int = 2,
-                         XP: Optional[torch.Tensor] = None, trials: int = 1) -> torch.Tensor:
+                         XP: Optional[torch.Tensor] = None, trials: int = 1, mu: Optional[torch.Tensor] = None,
+                         xnorm_split: Optional[torch.Tensor] = None) -> torch.Tensor:
     """k-means|| (scalable k-means++, reference cuML ``init="scalable-k-means++"`` / Spark
     ``initMode="k-means||"``): ``steps`` rounds of D^2 over-sampling (ell = oversampling * k rows
     per round, device RNG), candidates all-gathered, weighted by the rows they attract, then reduced
@@ -91,7 +92,8 @@ def init_kmeans_parallel(X: torch.Tensor, xnorm: torch.Tensor, desc: PartitionDe
 
     def nearest(C: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         if XP is not None:  # sampling / weighting only need approximate distances
-            return ops.nearest_centroid_split(XP, m, C.float(), xnorm, approx=True)
+            return ops.nearest_centroid_split(XP, m, C.float(), xnorm if xnorm_split is None else xnorm_split,
+                                              approx=True, mu=mu)
         return ops.nearest_centroid(X, C.float(), xnorm)
 
     rng = np.random.default_rng(seed)
@@ -171,24 +173,35 @@ def kmeans_fit(X: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext, k
     xnorm = ops.row_sqnorm(X)
     # k > 256: 256 x 256 LDS-DMA kernel on the tiled plane layout (SRML_SPLIT_TILED=0: plain layout)
     tiled = k > 256 and os.environ.get("SRML_SPLIT_TILED", "1") == "1"
-    XP = ops.split_bf16x3(X, tiled=tiled) if _use_split(X, k) else None
+    use_split = _use_split(X, k)
     # filter-and-refine Lloyd search on the tiled planes: 3-product pass + exact re-search of the
-    # near-tie rows (SRML_KMEANS_CERTIFIED=0: always the 6-product search)
-    certified = tiled and XP is not None and X.is_cuda and os.environ.get("SRML_KMEANS_CERTIFIED", "1") == "1"
+    # near-tie rows (SRML_KMEANS_CERTIFIED=0: always the 6-product search). The split search runs
+    # on centred data (planes of X - mu, centroids - mu, ||x - mu||^2): distances are unchanged,
+    # and the dropped-product error bound scales with ||x - mu|| ||c - mu||, far below the gaps.
+    certified = tiled and use_split and X.is_cuda and os.environ.get("SRML_KMEANS_CERTIFIED", "1") == "1"
+    mu = None
+    xnorm_s = xnorm
+    if use_split and tiled and X.is_cuda:
+        mu = ops.col_moments(X, need_sq=False)[0].div_(max(X.shape[0], 1)).float()
+        xnorm_s = ops.row_sqnorm(X, mu)
+    XP = ops.split_bf16x3(X, tiled=tiled, mu=mu) if use_split else None
     if init in ("random",):
         C = init_random(X, desc, ctx, k, seed)
     elif init in ("scalable-k-means++", "k-means||", "k-means++"):
-        C = init_kmeans_parallel(X, xnorm, desc, ctx, k, seed, oversampling, init_steps, XP=XP)
+        C = init_kmeans_parallel(X, xnorm, desc, ctx, k, seed, oversampling, init_steps, XP=XP, mu=mu,
+                                 xnorm_split=xnorm_s)
     else:
         raise ValueError("Unsupported init mode %s" % init)
     C = C.double()
     tol2 = float(tol) ** 2
     n_iter = 0
     inertia = 0.0
+    st0 = dict(ops._CERTIFY_STATS)
     for it in range(max(0, max_iter)):
         n_iter = it + 1
         if XP is not None:
-            labels, d2 = ops.nearest_centroid_split(XP, X.shape[0], C.float(), xnorm, X=X if certified else None)
+            labels, d2 = ops.nearest_centroid_split(XP, X.shape[0], C.float(), xnorm_s, X=X if certified else None,
+                                                    mu=mu)
         else:
             labels, d2 = ops.nearest_centroid(X, C.float(), xnorm)
         sums, counts = ops.cluster_sums(X, labels, k)
@@ -208,6 +221,9 @@ def kmeans_fit(X: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext, k
         "n_cols": int(n),
         "dtype": "float32" if X.dtype == torch.float32 else "float64",
         "n_iter": n_iter,
+        # filter-and-refine Lloyd search: fraction of row assignments re-searched exactly
+        "refined_frac": round((ops._CERTIFY_STATS["refined"] - st0["refined"]) /
+                              max(1, ops._CERTIFY_STATS["rows"] - st0["rows"]), 4) if certified else None,
     }
 
 

@@ -253,9 +253,19 @@ def xtv(X: torch.Tensor, V: torch.Tensor, out: Optional[torch.Tensor] = None) ->
     return out
 
 
-def row_sqnorm(X: torch.Tensor) -> torch.Tensor:
-    """||x_r||^2 per row: fp32 for fp32 inputs, fp64 for fp64 inputs on the device."""
+def row_sqnorm(X: torch.Tensor, mu: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """||x_r||^2 per row: fp32 for fp32 inputs, fp64 for fp64 inputs on the device.
+    ``mu`` (fp32 inputs): ||x_r - mu||^2 (centred norms of the KMeans split search)."""
     m, n = X.shape
+    if mu is not None:
+        muf = _c(mu.float().view(-1))
+        if not X.is_cuda or X.dtype != torch.float32:
+            return ((X.float() - muf) ** 2).sum(1)
+        X = _c(X)
+        out = torch.empty(m, dtype=torch.float32, device=X.device)
+        native.call("srml_row_sqnorm_centered_f32", X.data_ptr(), m, n, X.stride(0), muf.data_ptr(), out.data_ptr(),
+                    native.stream(X.device))
+        return out
     if X.is_cuda and X.dtype == torch.float64:
         X = _c(X)
         out = torch.empty(m, dtype=torch.float64, device=X.device)
@@ -336,22 +346,31 @@ def nearest_centroid(X: torch.Tensor, C: torch.Tensor, xnorm: Optional[torch.Ten
     return labels, dist
 
 
-def split_bf16x3(X: torch.Tensor, row_multiple: int = 128, tiled: bool = False) -> torch.Tensor:
+def split_bf16x3(X: torch.Tensor, row_multiple: int = 128, tiled: bool = False,
+                 mu: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Exact three-way bf16 split of a fp32 matrix: planes P[3][rows_pad][kp] (bf16) with
     X = P[0] + P[1] + P[2] (each plane the round-to-nearest bf16 of the remaining residual),
     rows padded to ``row_multiple`` and columns to a multiple of 16 with zeros.
 
     ``tiled`` (GPU only): the LDS-DMA kernel's layout P[3][rows_pad/256][kp/16][256][16] — each
-    (256-row tile, 16-wide k step) block one contiguous, bank-swizzled 8 KiB image."""
+    (256-row tile, 16-wide k step) block one contiguous, bank-swizzled 8 KiB image.
+    ``mu``: planes of X - mu (centred; fp32 subtraction fused into the split)."""
     m, n = X.shape
     kp = (n + 15) // 16 * 16
     if tiled and X.is_cuda and X.dtype == torch.float32:
         rows_pad = max(256, (m + 255) // 256 * 256)
         X = X if X.stride(1) == 1 else X.contiguous()
         P = torch.empty((3, rows_pad // 256, kp // 16, 256, 16), dtype=torch.bfloat16, device=X.device)
-        native.call("srml_split_bf16x3_tiled", X.data_ptr(), m, n, X.stride(0), kp, rows_pad, P.data_ptr(),
-                    native.stream(X.device))
+        if mu is not None:
+            muf = _c(mu.float().view(-1))
+            native.call("srml_split_bf16x3_tiled_centered", X.data_ptr(), m, n, X.stride(0), muf.data_ptr(), kp,
+                        rows_pad, P.data_ptr(), native.stream(X.device))
+        else:
+            native.call("srml_split_bf16x3_tiled", X.data_ptr(), m, n, X.stride(0), kp, rows_pad, P.data_ptr(),
+                        native.stream(X.device))
         return P
+    if mu is not None:
+        X = X.float() - mu.float().view(1, -1)
     rows_pad = max(row_multiple, (m + row_multiple - 1) // row_multiple * row_multiple)
     if not X.is_cuda or X.dtype != torch.float32:
         P = torch.zeros((3, rows_pad, kp), dtype=torch.bfloat16, device=X.device)
@@ -371,7 +390,8 @@ CERTIFY_TAU = 2.0 ** -13  # dot-product error bound of the 3-product search, rel
 
 
 def _nearest_centroid_certified(XP: torch.Tensor, X: torch.Tensor, m: int, k: int, CP: torch.Tensor,
-                                cn: torch.Tensor, xnorm: torch.Tensor, st: int) -> Tuple[torch.Tensor, torch.Tensor]:
+                                cn: torch.Tensor, xnorm: torch.Tensor, st: int, mu: Optional[torch.Tensor]
+                                ) -> Tuple[torch.Tensor, torch.Tensor]:
     """Filter-and-refine arg-min: the 3-product search (half the MFMAs of the fp32-exact one)
     keeps every row's best and second-best distance; rows whose gap exceeds the error bound of
     the dropped products (4 tau ||x|| max||c||) are certified — the exact search would pick the
@@ -380,26 +400,25 @@ def _nearest_centroid_certified(XP: torch.Tensor, X: torch.Tensor, m: int, k: in
     dev = XP.device
     nslot = int(native.lib().srml_nearest_centroid_split_top2_nslot(k))
     keys = torch.empty(m * nslot, dtype=torch.int64, device=dev)
-    sec = torch.empty(m * nslot, dtype=torch.float32, device=dev)
+    lob = torch.empty(m * nslot, dtype=torch.float32, device=dev)
     xrows, kp, crows = XP.shape[1] * 256, XP.shape[2] * 16, CP.shape[1] * 256
-    native.call("srml_nearest_centroid_split_top2", XP.data_ptr(), m, xrows, kp, CP.data_ptr(), k, crows,
-                cn.data_ptr(), keys.data_ptr(), sec.data_ptr(), st)
     xn = _c(xnorm.float())
-    cmax2 = cn.max().view(1)
+    cg = (2.0 * CERTIFY_TAU) * cn.clamp_min(0).sqrt()  # error radius per unit ||x||, per centroid
+    native.call("srml_nearest_centroid_split_top2", XP.data_ptr(), m, xrows, kp, CP.data_ptr(), k, crows,
+                cn.data_ptr(), cg.data_ptr(), xn.data_ptr(), keys.data_ptr(), lob.data_ptr(), st)
     labels = torch.empty(m, dtype=torch.int32, device=dev)
     dist = torch.empty(m, dtype=torch.float32, device=dev)
     flagged = torch.empty(m, dtype=torch.int32, device=dev)
     cnt = torch.zeros(1, dtype=torch.int32, device=dev)
-    native.call("srml_split_top2_select", keys.data_ptr(), sec.data_ptr(), m, nslot, xn.data_ptr(),
-                cmax2.data_ptr(), float(CERTIFY_TAU), labels.data_ptr(), dist.data_ptr(), flagged.data_ptr(),
-                cnt.data_ptr(), st)
-    del keys, sec
+    native.call("srml_split_top2_select", keys.data_ptr(), lob.data_ptr(), m, nslot, xn.data_ptr(), cg.data_ptr(),
+                labels.data_ptr(), dist.data_ptr(), flagged.data_ptr(), cnt.data_ptr(), st)
+    del keys, lob
     nf = int(cnt.item())
     _CERTIFY_STATS["rows"] += m
     _CERTIFY_STATS["refined"] += nf
     if nf:
         rows = flagged[:nf]
-        XPr = split_bf16x3(X.index_select(0, rows.long()), tiled=True)
+        XPr = split_bf16x3(X.index_select(0, rows.long()), tiled=True, mu=mu)
         best = torch.full((nf,), -1, dtype=torch.int64, device=dev)
         native.call("srml_nearest_centroid_split_tiled_np", XPr.data_ptr(), nf, XPr.shape[1] * 256, kp,
                     CP.data_ptr(), k, crows, cn.data_ptr(), best.data_ptr(), 6, st)
@@ -413,15 +432,21 @@ _CERTIFY_STATS = {"rows": 0, "refined": 0}  # filter-and-refine counters (diagno
 
 def nearest_centroid_split(XP: torch.Tensor, m: int, C: torch.Tensor, xnorm: torch.Tensor,
                            cnorm: Optional[torch.Tensor] = None, approx: bool = False,
-                           X: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+                           X: Optional[torch.Tensor] = None, mu: Optional[torch.Tensor] = None
+                           ) -> Tuple[torch.Tensor, torch.Tensor]:
     """``nearest_centroid`` on pre-split X planes (``split_bf16x3``): the distance GEMM runs on
     the bf16 matrix cores as six cross products of the planes (fp32-accurate; see splitmm.hip).
     ``approx=True`` (tiled planes): only the three leading products (~2^-16 relative dot error,
     half the MFMAs) — for consumers of approximate distances (k-means|| sampling).
     ``X`` given (tiled planes, GPU): certified filter-and-refine search — the 3-product pass plus
-    an exact 6-product re-search of the near-tie rows only; same labels as the exact search."""
+    an exact 6-product re-search of the near-tie rows only; same labels as the exact search.
+    ``mu``: XP holds planes of X - mu (``split_bf16x3(..., mu=mu)``) and ``xnorm`` = ||x - mu||^2;
+    the centroids are centred the same way (distances are translation invariant)."""
     k = C.shape[0]
     Cf = C.float()
+    if mu is not None:
+        Cf = Cf - mu.float().view(1, -1).to(Cf.device)
+        cnorm = None
     if cnorm is None:
         cnorm = (Cf * Cf).sum(1)
     tiled = XP.dim() == 5
@@ -437,7 +462,7 @@ def nearest_centroid_split(XP: torch.Tensor, m: int, C: torch.Tensor, xnorm: tor
     cn = _c(cnorm.to(torch.float32))
     st = native.stream(XP.device)
     if X is not None and tiled and not approx:
-        return _nearest_centroid_certified(XP, X, m, k, CP, cn, xnorm, st)
+        return _nearest_centroid_certified(XP, X, m, k, CP, cn, xnorm, st, mu)
     best = torch.full((m,), -1, dtype=torch.int64, device=XP.device)
     if tiled:
         native.call("srml_nearest_centroid_split_tiled_np", XP.data_ptr(), m, XP.shape[1] * 256, XP.shape[2] * 16,

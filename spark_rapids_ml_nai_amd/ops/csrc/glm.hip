@@ -350,7 +350,7 @@ SRML_API int srml_fold_partials_f64(const double* ws, long parts, long pstride, 
 
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void row_sqnorm_kernel(const float* __restrict__ X, long m, int n, long ld,
-                                                         float* __restrict__ out) {
+                                                         float* __restrict__ out, const float* __restrict__ mu) {
   const int lane = threadIdx.x & 63;
   const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const long nw = (long)gridDim.x * 4;
@@ -361,10 +361,17 @@ __global__ __launch_bounds__(256) void row_sqnorm_kernel(const float* __restrict
     if (vec) {
       for (int d = lane * 4; d < n; d += 256) {
         floatx4 v = *reinterpret_cast<const floatx4*>(row + d);
+        if (mu) {
+          const floatx4 c = *reinterpret_cast<const floatx4*>(mu + d);
+          v[0] -= c[0]; v[1] -= c[1]; v[2] -= c[2]; v[3] -= c[3];
+        }
         s = fmaf(v[0], v[0], fmaf(v[1], v[1], fmaf(v[2], v[2], fmaf(v[3], v[3], s))));
       }
     } else {
-      for (int d = lane; d < n; d += 64) s = fmaf(row[d], row[d], s);
+      for (int d = lane; d < n; d += 64) {
+        const float v = mu ? row[d] - mu[d] : row[d];
+        s = fmaf(v, v, s);
+      }
     }
     s = wave_sum(s);
     if (lane == 0) out[r] = s;
@@ -375,7 +382,19 @@ SRML_API int srml_row_sqnorm_f32(const float* X, long m, int n, long ld, float* 
   if (m <= 0) return 0;
   long blocks = (m + 3) / 4;
   if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(row_sqnorm_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, X, m, n, ld, out);
+  hipLaunchKernelGGL(row_sqnorm_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, X, m, n, ld, out,
+                     (const float*)nullptr);
+  return srml_status();
+}
+
+// ||x_r - mu||^2 per row (mu: n floats, 16-B aligned): the centred norms of the KMeans search
+SRML_API int srml_row_sqnorm_centered_f32(const float* X, long m, int n, long ld, const float* mu, float* out,
+                                          hipStream_t stream) {
+  if (m <= 0) return 0;
+  if (reinterpret_cast<uintptr_t>(mu) & 15) return -5;
+  long blocks = (m + 3) / 4;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(row_sqnorm_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, X, m, n, ld, out, mu);
   return srml_status();
 }
 

@@ -75,7 +75,8 @@ __global__ __launch_bounds__(256) void split_kernel(const float* __restrict__ X,
 // A k step of a tile is then streamed with fully sequential 1 KiB LDS-DMA wave loads (every
 // 128-B line used whole) instead of 32-B pieces of 256 rows 6 KB apart.
 __global__ __launch_bounds__(256) void split_tiled_kernel(const float* __restrict__ X, long m, int n, long ld, int kp,
-                                                          long rows_pad, unsigned short* __restrict__ P) {
+                                                          long rows_pad, unsigned short* __restrict__ P,
+                                                          const float* __restrict__ mu) {
   // one thread = one row's 16-wide k step (64 B of X in, one 32-B slot per plane out); a block =
   // the 256 rows of one (tile, k step) image, so each block writes three contiguous 8 KiB images
   const int ks_n = kp >> 4;
@@ -98,6 +99,11 @@ __global__ __launch_bounds__(256) void split_tiled_kernel(const float* __restric
     } else {
 #pragma unroll
       for (int j = 0; j < 16; ++j) x[j] = (r < m && c0 + j < n) ? X[r * ld + c0 + j] : 0.f;
+    }
+    if (mu && r < m) {  // centred planes (x - mu): same distances, smaller operands
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (c0 + j < n) x[j] -= mu[c0 + j];
     }
     unsigned hw[8], mw[8], lw[8];
 #pragma unroll
@@ -185,58 +191,64 @@ __device__ __forceinline__ void split_epilogue(const floatx16 (&acc)[BM / WM / 3
   }
 }
 
-// Top-2 epilogue for the certified 3-product search: per (row, wave column slot) the best
-// (value, index) and the second-best value of the wave's BN/WN columns, plain stores into
-// keys/sec[row * nslot + slot] (slot = ctile * WN + wn). srml_split_top2_select merges the slots.
+// Top-2 epilogue for the certified 3-product search. Each candidate j carries an error radius
+// e_j = sqrt(||x||^2) * g_j (g_j = 2 tau ||c_j||, the bound on |d~_j - d_j| of the dropped
+// products); per (row, wave column slot) it keeps the best (d~, index) and the smallest LOWER
+// bound d~_j - e_j over the slot's other candidates, plain stores into keys / lob[row * nslot + slot]
+// (slot = ctile * WN + wn); srml_split_top2_select merges the slots.
 template <int BM, int BN, int WM, int WN>
 __device__ __forceinline__ void split_epilogue_top2(const floatx16 (&acc)[BM / WM / 32][BN / WN / 32], long row0,
                                                     int col0, int ctile, long m, int k,
-                                                    const float* __restrict__ cnorm,
-                                                    unsigned long long* __restrict__ keys, float* __restrict__ sec,
+                                                    const float* __restrict__ cnorm, const float* __restrict__ cg,
+                                                    const float* __restrict__ xnorm,
+                                                    unsigned long long* __restrict__ keys, float* __restrict__ lob,
                                                     int nslot, int wm, int wn, int li, int lk) {
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
-  float cn[TN];
+  float cn[TN], g[TN];
   int cj[TN];
 #pragma unroll
   for (int nt = 0; nt < TN; ++nt) {
     cj[nt] = col0 + wn * (BN / WN) + nt * 32 + li;
     cn[nt] = (cj[nt] < k) ? cnorm[cj[nt]] : 0.f;
+    g[nt] = (cj[nt] < k) ? cg[cj[nt]] : 0.f;
   }
   const int slot = ctile * WN + wn;
 #pragma unroll
   for (int mt = 0; mt < TM; ++mt) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      float bv = __builtin_huge_valf(), b2 = __builtin_huge_valf();
+      const long row = row0 + wm * (BM / WM) + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+      const float xs = row < m ? sqrtf(fmaxf(xnorm[row], 0.f)) : 0.f;
+      float bv = __builtin_huge_valf(), badj = __builtin_huge_valf(), sadj = __builtin_huge_valf();
       int bi = 0x7fffffff;
 #pragma unroll
       for (int nt = 0; nt < TN; ++nt) {
         if (cj[nt] < k) {
           const float d = fmaf(-2.f, acc[mt][nt][r], cn[nt]);
-          if (d < bv) { b2 = bv; bv = d; bi = cj[nt]; }
-          else if (d < b2) b2 = d;
+          const float adj = fmaf(-xs, g[nt], d);
+          if (d < bv) { sadj = fminf(sadj, badj); bv = d; bi = cj[nt]; badj = adj; }
+          else sadj = fminf(sadj, adj);
         }
       }
 #pragma unroll
       for (int o = 1; o < 32; o <<= 1) {
         const float ov = __shfl_xor(bv, o, 64);
         const int oi = __shfl_xor(bi, o, 64);
-        const float o2 = __shfl_xor(b2, o, 64);
+        const float oadj = __shfl_xor(badj, o, 64);
+        const float osadj = __shfl_xor(sadj, o, 64);
         if (ov < bv || (ov == bv && oi < bi)) {
-          b2 = fminf(bv, o2);
+          sadj = fminf(fminf(sadj, badj), osadj);
           bv = ov;
           bi = oi;
+          badj = oadj;
         } else {
-          b2 = fminf(b2, ov);
+          sadj = fminf(fminf(sadj, oadj), osadj);
         }
       }
-      if (li == 0) {
-        const long row = row0 + wm * (BM / WM) + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
-        if (row < m) {
-          const long o = row * nslot + slot;
-          keys[o] = bi == 0x7fffffff ? ~0ull : (((unsigned long long)orderable(bv) << 32) | (unsigned)bi);
-          sec[o] = b2;
-        }
+      if (li == 0 && row < m) {
+        const long o = row * nslot + slot;
+        keys[o] = bi == 0x7fffffff ? ~0ull : (((unsigned long long)orderable(bv) << 32) | (unsigned)bi);
+        lob[o] = sadj;
       }
     }
   }
@@ -380,7 +392,7 @@ template <bool TILED, int NP = 6, bool TOP2 = false>
 __global__ __launch_bounds__(512, 1) void nearest_centroid_split_glds_kernel(
     const unsigned short* __restrict__ XP, long m, long xrows, int kp, const unsigned short* __restrict__ CP, int k,
     long crows, const float* __restrict__ cnorm, unsigned long long* __restrict__ best, int n_ctiles,
-    float* __restrict__ sec = nullptr) {
+    float* __restrict__ lob = nullptr, const float* __restrict__ cg = nullptr, const float* __restrict__ xnorm = nullptr) {
   constexpr int BM = 256, BN = 256, WM = 2, WN = 4, TM = 4, TN = 2, NS = 3;
   __shared__ __attribute__((aligned(1024))) unsigned short lds[NS][6][256][16];
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -470,42 +482,43 @@ __global__ __launch_bounds__(512, 1) void nearest_centroid_split_glds_kernel(
     stage = stage == 2 ? 0 : stage + 1;
   }
   if (TOP2)
-    split_epilogue_top2<BM, BN, WM, WN>(acc, row0, col0, ctile, m, k, cnorm, best, sec, n_ctiles * WN, wm, wn, li, lk);
+    split_epilogue_top2<BM, BN, WM, WN>(acc, row0, col0, ctile, m, k, cnorm, cg, xnorm, best, lob, n_ctiles * WN, wm,
+                                        wn, li, lk);
   else
     split_epilogue<BM, BN, WM, WN>(acc, row0, col0, m, k, cnorm, best, wm, wn, li, lk);
 }
 
-// Merge the top-2 slots of every row and certify the 3-product arg-min: with the dropped
-// products bounded by |x.c - (x.c)_3| <= tau ||x|| ||c|| (tau = 2^-13 covers the 3 * 2^-16
-// truncation with 8x slack for fp32 accumulation order), a row whose best / second-best gap
-// exceeds 4 tau ||x|| max||c|| has the same arg-min as the fp32-exact 6-product search. Certified
-// rows get their label and distance; the rest are appended to `flagged` (count in *n_flagged)
-// for an exact re-search.
+// Merge the slots of every row and certify the 3-product arg-min b: with |d~_j - d_j| <= e_j =
+// ||x|| g_j (g_j = 2 tau ||c_j||; tau = 2^-13 covers the 3 * 2^-16 dropped products with 8x slack
+// for fp32 accumulation order), d~_j - e_j > d~_b + e_b for every j != b proves d_j > d_b, i.e. the
+// fp32-exact 6-product search picks b too. Certified rows get their label and distance; the rest
+// are appended to `flagged` (count in *n_flagged) for an exact re-search.
 __global__ __launch_bounds__(256) void split_top2_select_kernel(const unsigned long long* __restrict__ keys,
-                                                                const float* __restrict__ sec, long m, int nslot,
+                                                                const float* __restrict__ lob, long m, int nslot,
                                                                 const float* __restrict__ xnorm,
-                                                                const float* __restrict__ cmax2, float tau,
+                                                                const float* __restrict__ cg,
                                                                 int* __restrict__ labels, float* __restrict__ dist,
                                                                 int* __restrict__ flagged, int* __restrict__ n_flagged) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= m) return;
   const unsigned long long* kr = keys + i * nslot;
-  const float* sr = sec + i * nslot;
+  const float* lr = lob + i * nslot;
   unsigned long long k1 = ~0ull;
   int s1 = 0;
   for (int s = 0; s < nslot; ++s) {
     const unsigned long long v = kr[s];
     if (v < k1) { k1 = v; s1 = s; }
   }
-  float second = __builtin_huge_valf();
+  const float xn = xnorm[i];
+  const float xs = sqrtf(fmaxf(xn, 0.f));
+  float low = __builtin_huge_valf();  // min over j != b of d~_j - e_j
   for (int s = 0; s < nslot; ++s) {
-    second = fminf(second, sr[s]);
-    if (s != s1 && kr[s] != ~0ull) second = fminf(second, unorderable((unsigned)(kr[s] >> 32)));
+    low = fminf(low, lr[s]);
+    if (s != s1 && kr[s] != ~0ull)
+      low = fminf(low, fmaf(-xs, cg[(int)(kr[s] & 0xffffffffu)], unorderable((unsigned)(kr[s] >> 32))));
   }
   const float bv = unorderable((unsigned)(k1 >> 32));
-  const float xn = xnorm[i];
-  const float thr = 4.f * tau * sqrtf(fmaxf(xn, 0.f) * fmaxf(cmax2[0], 0.f));
-  if (k1 != ~0ull && second - bv > thr) {
+  if (k1 != ~0ull && low > fmaf(xs, cg[(int)(k1 & 0xffffffffu)], bv)) {
     labels[i] = (int)(k1 & 0xffffffffu);
     const float d = bv + xn;
     dist[i] = d > 0.f ? d : 0.f;
@@ -585,7 +598,23 @@ SRML_API int srml_split_bf16x3_tiled(const float* X, long m, int n, long ld, int
   long total = rows_pad * (long)(kp / 4);
   long blocks = (total + 255) / 256;
   if (blocks > 65536) blocks = 65536;
-  hipLaunchKernelGGL(split_tiled_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, X, m, n, ld, kp, rows_pad, P);
+  hipLaunchKernelGGL(split_tiled_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, X, m, n, ld, kp, rows_pad, P,
+                     (const float*)nullptr);
+  return srml_status();
+}
+
+// Tiled planes of X - mu (mu: n floats): the certified KMeans search works on centred data, where
+// the dropped-product error bound (relative to ||x - mu|| ||c - mu||) is small next to the gaps.
+SRML_API int srml_split_bf16x3_tiled_centered(const float* X, long m, int n, long ld, const float* mu, int kp,
+                                              long rows_pad, unsigned short* P, hipStream_t stream) {
+  if (rows_pad <= 0) return 0;
+  if ((kp & 15) || kp < n || rows_pad < m || (rows_pad & 255)) return -2;
+  if ((reinterpret_cast<uintptr_t>(P) & 15) != 0) return -5;
+  long total = rows_pad * (long)(kp / 4);
+  long blocks = (total + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(split_tiled_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, X, m, n, ld, kp, rows_pad, P,
+                     mu);
   return srml_status();
 }
 
@@ -619,10 +648,12 @@ SRML_API int srml_nearest_centroid_split_tiled(const unsigned short* XP, long m,
 }
 
 // Certified 3-product nearest-centroid search, phase 1 (tiled planes, as
-// srml_nearest_centroid_split_tiled_np): top-2 slots per row, keys/sec sized m * ceil(k/256) * 4.
+// srml_nearest_centroid_split_tiled_np): best + lower-bound slots per row, keys / lob sized
+// m * ceil(k/256) * 4; cg = 2 tau ||c_j|| per centroid, xnorm = ||x||^2 of the (centred) rows.
 SRML_API int srml_nearest_centroid_split_top2(const unsigned short* XP, long m, long xrows, int kp,
                                               const unsigned short* CP, int k, long crows, const float* cnorm,
-                                              unsigned long long* keys, float* sec, hipStream_t stream) {
+                                              const float* cg, const float* xnorm, unsigned long long* keys,
+                                              float* lob, hipStream_t stream) {
   if (m <= 0 || k <= 0) return 0;
   if ((kp & 15) || xrows < m || crows < k || (crows & 255) || (xrows & 255)) return -2;
   if ((reinterpret_cast<uintptr_t>(XP) & 15) || (reinterpret_cast<uintptr_t>(CP) & 15)) return -5;
@@ -631,19 +662,19 @@ SRML_API int srml_nearest_centroid_split_top2(const unsigned short* XP, long m, 
   const long nb = rt * ct;
   if (nb > 0x7fffffffL) return -3;
   hipLaunchKernelGGL((nearest_centroid_split_glds_kernel<true, 3, true>), dim3((unsigned)nb), dim3(512), 0, stream, XP,
-                     m, xrows, kp, CP, k, crows, cnorm, keys, (int)ct, sec);
+                     m, xrows, kp, CP, k, crows, cnorm, keys, (int)ct, lob, cg, xnorm);
   return srml_status();
 }
 
 SRML_API int srml_nearest_centroid_split_top2_nslot(int k) { return ((k + 255) / 256) * 4; }
 
 // phase 2: merge slots, certify, emit labels / distances of certified rows, list the others
-SRML_API int srml_split_top2_select(const unsigned long long* keys, const float* sec, long m, int nslot,
-                                    const float* xnorm, const float* cmax2, float tau, int* labels, float* dist,
-                                    int* flagged, int* n_flagged, hipStream_t stream) {
+SRML_API int srml_split_top2_select(const unsigned long long* keys, const float* lob, long m, int nslot,
+                                    const float* xnorm, const float* cg, int* labels, float* dist, int* flagged,
+                                    int* n_flagged, hipStream_t stream) {
   if (m <= 0) return 0;
-  hipLaunchKernelGGL(split_top2_select_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream, keys, sec, m,
-                     nslot, xnorm, cmax2, tau, labels, dist, flagged, n_flagged);
+  hipLaunchKernelGGL(split_top2_select_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream, keys, lob, m,
+                     nslot, xnorm, cg, labels, dist, flagged, n_flagged);
   return srml_status();
 }
 

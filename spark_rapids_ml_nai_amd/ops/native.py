@@ -69,9 +69,11 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_split_bf16x3_tiled": (_P, _L, _I, _L, _I, _L, _P, _P),
     "srml_nearest_centroid_split_tiled": (_P, _L, _L, _I, _P, _I, _L, _P, _P, _P),
     "srml_nearest_centroid_split_tiled_np": (_P, _L, _L, _I, _P, _I, _L, _P, _P, _I, _P),
-    "srml_nearest_centroid_split_top2": (_P, _L, _L, _I, _P, _I, _L, _P, _P, _P, _P),
+    "srml_nearest_centroid_split_top2": (_P, _L, _L, _I, _P, _I, _L, _P, _P, _P, _P, _P, _P),
+    "srml_split_bf16x3_tiled_centered": (_P, _L, _I, _L, _P, _I, _L, _P, _P),
+    "srml_row_sqnorm_centered_f32": (_P, _L, _I, _L, _P, _P, _P),
     "srml_nearest_centroid_split_top2_nslot": (_I,),
-    "srml_split_top2_select": (_P, _P, _L, _I, _P, _P, _F, _P, _P, _P, _P, _P),
+    "srml_split_top2_select": (_P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _P),
     "srml_split_scatter_refined": (_P, _P, _I, _P, _P, _P, _P),
     "srml_kmeans_accumulate_f32": (_P, _L, _I, _L, _P, _I, _P, _P, _P, _P),
     "srml_kmeans_accumulate_sorted_f32": (_P, _L, _I, _L, _P, _P, _P, _P),
