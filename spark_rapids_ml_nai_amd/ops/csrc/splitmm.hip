@@ -394,7 +394,10 @@ __global__ __launch_bounds__(512, 1) void nearest_centroid_split_glds_kernel(
     long crows, const float* __restrict__ cnorm, unsigned long long* __restrict__ best, int n_ctiles,
     float* __restrict__ lob = nullptr, const float* __restrict__ cg = nullptr, const float* __restrict__ xnorm = nullptr) {
   constexpr int BM = 256, BN = 256, WM = 2, WN = 4, TM = 4, TN = 2, NS = 3;
-  __shared__ __attribute__((aligned(1024))) unsigned short lds[NS][6][256][16];
+  // planes staged per operand: h, m, l for the 6-product set; the 3-product set (h.h, h.m, m.h)
+  // never touches the l planes, so it stages 2 per operand (2/3 of the DMA and LDS traffic)
+  constexpr int NPL = NP == 6 ? 3 : 2, CPW = 2 * NPL;  // staging chunks per wave per k step
+  __shared__ __attribute__((aligned(1024))) unsigned short lds[NS][2 * NPL][256][16];
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const long rtile = bid / n_ctiles;
   const int ctile = bid % n_ctiles;
@@ -406,32 +409,33 @@ __global__ __launch_bounds__(512, 1) void nearest_centroid_split_glds_kernel(
   const int li = lane & 31, lk = lane >> 5;
   const long xplane = xrows * (long)kp, cplane = crows * (long)kp;
 
-  // this wave's 6 staging chunks per stage: chunk c = wid * 6 + i -> plane q = c / 8, rows 32 (c % 8) ..
-  const unsigned short* src[6];
-  int dst_off[6];  // element offset of the chunk inside one stage
+  // this wave's CPW staging chunks per stage: chunk c = wid * CPW + i -> LDS plane q = c / 8 (X planes
+  // 0 .. NPL-1, then C planes), rows 32 (c % 8) ..
+  const unsigned short* src[CPW];
+  int dst_off[CPW];  // element offset of the chunk inside one stage
 #pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    const int c = wid * 6 + i;
+  for (int i = 0; i < CPW; ++i) {
+    const int c = wid * CPW + i;
     const int q = c >> 3, j = c & 7;
     const int r = 32 * j + (lane >> 1);
     const int lh = (lane & 1) ^ ((lane >> 4) & 1);  // logical half stored at physical half (lane & 1)
     if (TILED) {  // the image is already swizzled: lane-linear 16-B pieces of one contiguous 1 KiB
       const int ks_n = kp / SBK;
-      if (q < 3) src[i] = XP + q * xplane + ((rtile * ks_n) << 12) + 512 * j + lane * 8;
-      else src[i] = CP + (q - 3) * cplane + (((long)ctile * ks_n) << 12) + 512 * j + lane * 8;
-    } else if (q < 3) {
+      if (q < NPL) src[i] = XP + q * xplane + ((rtile * ks_n) << 12) + 512 * j + lane * 8;
+      else src[i] = CP + (q - NPL) * cplane + (((long)ctile * ks_n) << 12) + 512 * j + lane * 8;
+    } else if (q < NPL) {
       long xr = row0 + r;
       if (xr >= xrows) xr = xrows - 1;  // clamp: those rows are never reported
       src[i] = XP + q * xplane + xr * kp + 8 * lh;
     } else {
-      src[i] = CP + (q - 3) * cplane + (long)(col0 + r) * kp + 8 * lh;  // crows % 256 == 0
+      src[i] = CP + (q - NPL) * cplane + (long)(col0 + r) * kp + 8 * lh;  // crows % 256 == 0
     }
     dst_off[i] = (q * 256 + 32 * j) * 16;
   }
   auto issue = [&](int kt, int stage) {
     unsigned short* base = &lds[stage][0][0][0];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
+    for (int i = 0; i < CPW; ++i) {
       __builtin_amdgcn_global_load_lds((gbl_vptr)(src[i] + (TILED ? ((long)kt << 12) : (long)kt * SBK)),
                                        (lds_vptr)(base + dst_off[i]), 16, 0, 0);
     }
@@ -451,25 +455,29 @@ __global__ __launch_bounds__(512, 1) void nearest_centroid_split_glds_kernel(
   if (nk > 1) issue(1, 1);
   int stage = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (kt + 1 < nk) {  // the next step's CPW loads may stay in flight
+      if (CPW == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_s_barrier();  // step kt landed for every wave; every wave finished step kt - 1
     if (kt + 2 < nk) issue(kt + 2, stage == 0 ? 2 : stage - 1);
-    bf16x8 fb[3][TN];
+    bf16x8 fb[NPL][TN];
 #pragma unroll
-    for (int p = 0; p < 3; ++p)
+    for (int p = 0; p < NPL; ++p)
 #pragma unroll
       for (int nt = 0; nt < TN; ++nt)
-        fb[p][nt] = *reinterpret_cast<const bf16x8*>(&lds[stage][3 + p][wn * (BN / WN) + nt * 32 + li][8 * ph]);
+        fb[p][nt] = *reinterpret_cast<const bf16x8*>(&lds[stage][NPL + p][wn * (BN / WN) + nt * 32 + li][8 * ph]);
 #pragma unroll
     for (int mt = 0; mt < TM; ++mt) {
-      bf16x8 fa[3];
+      bf16x8 fa[NPL];
 #pragma unroll
-      for (int p = 0; p < 3; ++p)
+      for (int p = 0; p < NPL; ++p)
         fa[p] = *reinterpret_cast<const bf16x8*>(&lds[stage][p][wm * (BM / WM) + mt * 32 + li][8 * ph]);
 #pragma unroll
       for (int nt = 0; nt < TN; ++nt) {
-        if (NP == 6) {
+        if constexpr (NP == 6) {
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[0][nt], acc[mt][nt], 0, 0, 0);
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1][nt], acc[mt][nt], 0, 0, 0);
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[2][nt], acc[mt][nt], 0, 0, 0);
