@@ -13,6 +13,8 @@
 // Reference: cuML LinearRegressionMG / RidgeMG / CDMG solves (regression.py:498-613).
 #include "common.h"
 
+#include <stdlib.h>
+
 extern "C" int srml_dgemm(int ta, int tb, int M, int N, int K, double alpha, const double* A, long lda,
                           const double* B, long ldb, double beta, double* C, long ldc, hipStream_t stream);
 
@@ -382,6 +384,152 @@ __global__ __launch_bounds__(1024) void cd_gram_block_kernel(const double* __res
   for (int i = t; i < n; i += blockDim.x) w_out[i] = w[i];
   if (t == 0) *iters = it;
 }
+
+// Pipelined block-cyclic sweep (same coordinate order and updates as cd_gram_block_kernel). The
+// rank-CB update of g by block b's delta no longer sits between two chains: while wave 0 runs
+// the sequential chain of block b, waves 1..15 apply the PREVIOUS block's delta to every other
+// row of g (the 64 x n panel stream, the bandwidth-heavy part), and only the 64 x 64 piece that
+// block b itself needs is applied before its chain. One barrier per block; the chain (latency)
+// and the panel stream (one CU's L2 bandwidth) overlap instead of adding up.
+__global__ __launch_bounds__(1024) void cd_gram_pipe_kernel(const double* __restrict__ A, int n, long lda,
+                                                            const double* __restrict__ b, const double* __restrict__ l1,
+                                                            const double* __restrict__ l2, double* __restrict__ w_out,
+                                                            int max_iter, double tol, int* __restrict__ iters,
+                                                            int w0_zero) {
+  extern __shared__ double sm[];  // w[n], g[n], blk[CB][CB + 1], dv[2][CB], part[16][CB]
+  double* w = sm;
+  double* g = sm + n;
+  double* blk = g + n;
+  double* dvb = blk + CD_CB * (CD_CB + 1);
+  double* part = dvb + 2 * CD_CB;
+  __shared__ int done;
+  const int t = threadIdx.x;
+  const int lane = t & 63, wid = t >> 6;
+  for (int i = t; i < n; i += blockDim.x) w[i] = w0_zero ? 0.0 : w_out[i];
+  __syncthreads();
+  for (int i = t; i < n; i += blockDim.x) {  // g = A w (skipped for a zero start)
+    double s = 0.0;
+    if (!w0_zero) {
+#pragma unroll 8
+      for (int j = 0; j < n; ++j) s = fma(A[(long)j * lda + i], w[j], s);
+    }
+    g[i] = s;
+  }
+  for (int i = t; i < 2 * CD_CB; i += blockDim.x) dvb[i] = 0.0;
+  __syncthreads();
+  const int nblk = (n + CD_CB - 1) / CD_CB;
+  int it = 0, step = 0;
+  int p0 = -1, pnb = 0;  // previous block (cyclic across sweeps): start row, size
+  double max_delta = 0.0, max_w = 0.0;
+  for (; it < max_iter; ++it) {
+    max_delta = 0.0;
+    max_w = 0.0;
+    for (int bi = 0; bi < nblk; ++bi, ++step) {
+      const int j0 = bi * CD_CB;
+      const int nb = n - j0 < CD_CB ? n - j0 : CD_CB;
+      double* dprev = dvb + ((step + 1) & 1) * CD_CB;  // delta of the previous block
+      double* dcur = dvb + (step & 1) * CD_CB;
+      // phase A (all waves): stage block b's diagonal tile; partial sums of the previous block's
+      // delta onto block b's rows (wave w takes previous-block columns 4w .. 4w + 3)
+      for (int e = t; e < nb * nb; e += blockDim.x) {
+        const int r = e / nb, c = e - r * nb;
+        blk[r * (CD_CB + 1) + c] = A[(long)(j0 + r) * lda + j0 + c];
+      }
+      {
+        double s = 0.0;
+        if (p0 >= 0 && p0 != j0 && lane < nb) {  // (one block only: its chain already updated g)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int c = 4 * wid + u;
+            if (c < pnb) s = fma(A[(long)(p0 + c) * lda + j0 + lane], dprev[c], s);
+          }
+        }
+        part[wid * CD_CB + lane] = s;
+      }
+      __syncthreads();
+      if (wid == 0) {  // sequential chain of block b
+        const bool own = lane < nb;
+        const int jj = j0 + (own ? lane : 0);
+        double gl = 0.0;
+        if (own) {
+          gl = g[jj];
+#pragma unroll
+          for (int q = 0; q < 16; ++q) gl += part[q * CD_CB + lane];
+        }
+        double wl = own ? w[jj] : 0.0;
+        const double w0 = wl;
+        const double ajj = own ? blk[lane * (CD_CB + 1) + lane] : 0.0;
+        const double diag = own ? ajj + l2[jj] : 0.0;
+        const double inv_diag = diag > 0.0 ? 1.0 / diag : 0.0;
+        const double bj = own ? b[jj] : 0.0;
+        const double l1j = own ? l1[jj] : 0.0;
+        for (int c = 0; c < nb; ++c) {
+          double d = 0.0, nw = wl;
+          if (diag > 0.0) {
+            const double rho = bj - gl + ajj * wl;
+            nw = rho > l1j ? (rho - l1j) * inv_diag : (rho < -l1j ? (rho + l1j) * inv_diag : 0.0);
+            d = nw - wl;
+          }
+          {
+            const long long bits = __double_as_longlong(d);
+            const int lo = __builtin_amdgcn_readlane((int)(bits & 0xffffffffLL), c);
+            const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), c);
+            d = __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+          }
+          if (lane == c && diag > 0.0) {
+            wl = nw;
+            max_w = fmax(max_w, fabs(nw));
+            max_delta = fmax(max_delta, fabs(d));
+          }
+          if (d != 0.0 && own) gl = fma(blk[c * (CD_CB + 1) + lane], d, gl);
+        }
+        if (own) {
+          g[jj] = gl;
+          w[jj] = wl;
+        }
+        dcur[lane] = own ? wl - w0 : 0.0;
+      } else if (p0 >= 0) {
+        // waves 1..15: previous block's delta onto every row outside blocks (b-1, b)
+        for (int i = t - 64; i < n; i += blockDim.x - 64) {
+          if ((i >= p0 && i < p0 + pnb) || (i >= j0 && i < j0 + nb)) continue;
+          const double* col = A + (long)p0 * lda + i;
+          double s0 = 0.0, s1 = 0.0;
+          int c = 0;
+          for (; c + 16 <= pnb; c += 16) {
+            double v[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) v[u] = col[(long)(c + u) * lda];
+#pragma unroll
+            for (int u = 0; u < 16; u += 2) {
+              s0 = fma(v[u], dprev[c + u], s0);
+              s1 = fma(v[u + 1], dprev[c + u + 1], s1);
+            }
+          }
+          for (; c < pnb; ++c) s0 = fma(col[(long)c * lda], dprev[c], s0);
+          g[i] += s0 + s1;
+        }
+      }
+      __syncthreads();
+      p0 = j0;
+      pnb = nb;
+    }
+    if (t < 64) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        max_delta = fmax(max_delta, __shfl_xor(max_delta, o, 64));
+        max_w = fmax(max_w, __shfl_xor(max_w, o, 64));
+      }
+      if (t == 0) done = (max_delta <= tol * fmax(max_w, 1e-300)) ? 1 : 0;
+    }
+    __syncthreads();
+    if (done) {
+      ++it;
+      break;
+    }
+  }
+  for (int i = t; i < n; i += blockDim.x) w_out[i] = w[i];
+  if (t == 0) *iters = it;
+}
 }  // namespace
 
 SRML_API int srml_potrf_f64(double* A, int n, long lda, int* info, hipStream_t stream) {
@@ -422,6 +570,15 @@ SRML_API int srml_potrs_f64(const double* L, int n, long lda, double* b, hipStre
 SRML_API int srml_cd_gram_f64(const double* A, int n, long lda, const double* b, const double* l1, const double* l2,
                               double* w, int max_iter, double tol, int* iters, hipStream_t stream) {
   if (n <= 0) return 0;
+  static const int pipe = getenv("SRML_CD_PIPE") ? atoi(getenv("SRML_CD_PIPE")) : 1;
+  const size_t lds_pipe = ((size_t)2 * n + CD_CB * (CD_CB + 1) + 18 * CD_CB) * sizeof(double);
+  if (pipe && lds_pipe <= 150 * 1024) {  // n <= ~6900
+    (void)hipFuncSetAttribute((const void*)cd_gram_pipe_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds_pipe);
+    hipLaunchKernelGGL(cd_gram_pipe_kernel, dim3(1), dim3(1024), lds_pipe, stream, A, n, lda, b, l1, l2, w, max_iter,
+                       tol, iters, 0);
+    return srml_status();
+  }
   const size_t lds_blk = ((size_t)2 * n + CD_CB * (CD_CB + 1) + CD_CB) * sizeof(double);
   if (lds_blk <= 150 * 1024) {  // n <= ~7500
     (void)hipFuncSetAttribute((const void*)cd_gram_block_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -11,13 +11,18 @@ switches the affected kernels to fixed-order variants:
   partial tiles into a workspace (<= 64 chunks, <= 1 GB) folded in chunk order, instead of
   fp64 atomics (same fp32-per-chunk / fp64-across-chunk precision);
 * fp64 GEMMs (``ops.dgemm``: X^T V, Krylov products) always fold split-K partials in index
-  order, deterministic in either mode.
+  order, deterministic in either mode;
+* LogisticRegression -> the two-pass path (residual stage + MFMA X^T R) with ordered block-partial
+  folds instead of the fused atomics kernel;
+* RandomForest regression histograms -> the cross-chunk fold adds exact i64 fixed-point integers
+  (order-independent) converted to fp64 once (``srml_rf_hist_fixed``), node statistics one block
+  per segment with a fixed-order reduction (``srml_rf_node_stats_det``); classification histograms
+  are integer counts, exact in any order.
 
-Not covered yet (their block partials still fold with atomics): the LogisticRegression fused
-loss/gradient kernels and the RandomForest regression histograms (classification histograms
-are integer-valued counts, exact in any order). Device RNG streams are counter-based and seeded
-(k-means|| sampling, bootstrap, k-means++ draws), so PCA, LinearRegression and KMeans fits on
-the same data and partitioning are bit-reproducible with the flag on.
+Device RNG streams are counter-based and seeded
+(k-means|| sampling, bootstrap, k-means++ draws), so PCA, LinearRegression, KMeans,
+LogisticRegression and RandomForestRegressor fits on the same data and partitioning are
+bit-reproducible with the flag on.
 """
 from __future__ import annotations
 
