@@ -393,10 +393,13 @@ __global__ __launch_bounds__(512, 1) void nearest_centroid_split_glds_kernel(
     const unsigned short* __restrict__ XP, long m, long xrows, int kp, const unsigned short* __restrict__ CP, int k,
     long crows, const float* __restrict__ cnorm, unsigned long long* __restrict__ best, int n_ctiles,
     float* __restrict__ lob = nullptr, const float* __restrict__ cg = nullptr, const float* __restrict__ xnorm = nullptr) {
-  constexpr int BM = 256, BN = 256, WM = 2, WN = 4, TM = 4, TN = 2, NS = 3;
+  constexpr int BM = 256, BN = 256, WM = 2, WN = 4, TM = 4, TN = 2;
   // planes staged per operand: h, m, l for the 6-product set; the 3-product set (h.h, h.m, m.h)
   // never touches the l planes, so it stages 2 per operand (2/3 of the DMA and LDS traffic)
   constexpr int NPL = NP == 6 ? 3 : 2, CPW = 2 * NPL;  // staging chunks per wave per k step
+  // ring depth: a 3-product k step is half the MFMA time of a 6-product one, so its loads get one
+  // more step of lead (4 stages x 32 KiB = 128 KiB; the 6-product ring is 3 x 48 KiB)
+  constexpr int NS = NP == 6 ? 3 : 4;
   __shared__ __attribute__((aligned(1024))) unsigned short lds[NS][2 * NPL][256][16];
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const long rtile = bid / n_ctiles;
@@ -451,18 +454,23 @@ __global__ __launch_bounds__(512, 1) void nearest_centroid_split_glds_kernel(
 
   const int ph = lk ^ ((li >> 3) & 1);  // physical half of this lane's fragment
   const int nk = kp / SBK;
-  issue(0, 0);
-  if (nk > 1) issue(1, 1);
+#pragma unroll
+  for (int q = 0; q < NS - 1; ++q)
+    if (q < nk) issue(q, q);
   int stage = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) {  // the next step's CPW loads may stay in flight
-      if (CPW == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    // step kt must have landed; the (at most NS - 2) later steps already issued may stay in flight
+    const int ahead = nk - 1 - kt < NS - 2 ? nk - 1 - kt : NS - 2;
+    if constexpr (CPW == 6) {
+      if (ahead >= 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __builtin_amdgcn_s_barrier();  // step kt landed for every wave; every wave finished step kt - 1
-    if (kt + 2 < nk) issue(kt + 2, stage == 0 ? 2 : stage - 1);
+    if (kt + NS - 1 < nk) issue(kt + NS - 1, stage == 0 ? NS - 1 : stage - 1);  // kt - 1's stage
     bf16x8 fb[NPL][TN];
 #pragma unroll
     for (int p = 0; p < NPL; ++p)
@@ -487,7 +495,7 @@ __global__ __launch_bounds__(512, 1) void nearest_centroid_split_glds_kernel(
         acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0][nt], acc[mt][nt], 0, 0, 0);
       }
     }
-    stage = stage == 2 ? 0 : stage + 1;
+    stage = stage == NS - 1 ? 0 : stage + 1;
   }
   if (TOP2)
     split_epilogue_top2<BM, BN, WM, WN>(acc, row0, col0, ctile, m, k, cnorm, cg, xnorm, best, lob, n_ctiles * WN, wm,
