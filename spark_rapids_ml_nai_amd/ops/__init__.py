@@ -1346,9 +1346,22 @@ def spd_solve(A: torch.Tensor, b: torch.Tensor) -> Tuple[torch.Tensor, bool]:
         if int(info) != 0:
             return torch.zeros(n, dtype=torch.float64), False
         return torch.cholesky_solve(b.double().view(-1, 1), L).view(-1), True
-    L = A.double().contiguous().clone()
-    info = torch.zeros(1, dtype=torch.int32, device=A.device)
     st = native.stream(A.device)
+    info = torch.zeros(1, dtype=torch.int32, device=A.device)
+    if n * 8 <= 110 * 1024:
+        # augmented factorisation of [A b; b^T 1]: the trailing updates carry b along, so the last
+        # row of the factor is z^T = (L^-1 b)^T and only the backward sweep L^T x = z remains. A
+        # non-positive LAST pivot only reflects the arbitrary corner value: info > n is ignored.
+        aug = torch.empty((n + 1, n + 1), dtype=torch.float64, device=A.device)
+        aug[:n, :n] = A
+        aug[n, :n] = b
+        aug[n, n] = 1.0
+        native.call("srml_potrf_f64", aug.data_ptr(), n + 1, aug.stride(0), info.data_ptr(), st)
+        x = aug[n, :n].contiguous()
+        native.call("srml_potrs_backward_f64", aug.data_ptr(), n, aug.stride(0), x.data_ptr(), st)
+        iv = int(info.item())
+        return x, iv == 0 or iv > n
+    L = A.double().contiguous().clone()
     native.call("srml_potrf_f64", L.data_ptr(), n, L.stride(0), info.data_ptr(), st)
     x = b.double().contiguous().clone()
     native.call("srml_potrs_f64", L.data_ptr(), n, L.stride(0), x.data_ptr(), st)

@@ -127,7 +127,7 @@ __global__ __launch_bounds__(1024) void potrs_kernel(const double* __restrict__ 
 constexpr int TS_B = 64;
 
 __global__ __launch_bounds__(1024) void potrs_blocked_kernel(const double* __restrict__ L, int n, long lda,
-                                                             double* __restrict__ b) {
+                                                             double* __restrict__ b, int backward_only) {
   extern __shared__ double x[];               // n
   __shared__ double blk[TS_B][TS_B + 1];      // diagonal block
   __shared__ double part[16][TS_B];           // partial sums of the backward GEMV
@@ -140,8 +140,8 @@ __global__ __launch_bounds__(1024) void potrs_blocked_kernel(const double* __res
     const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), src);
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
   };
-  // forward: L z = b
-  for (int j0 = 0; j0 < n; j0 += TS_B) {
+  // forward: L z = b (skipped when b already holds z: the augmented factorisation computed it)
+  for (int j0 = 0; j0 < (backward_only ? 0 : n); j0 += TS_B) {
     const int nb = n - j0 < TS_B ? n - j0 : TS_B;
     // x[j0 + r] -= L[j0 + r, 0:j0] . x[0:j0]: wave w takes rows r = w, w + 16, ...
     for (int r = wid; r < nb; r += 16) {
@@ -559,11 +559,22 @@ SRML_API int srml_potrs_f64(const double* L, int n, long lda, double* b, hipStre
   if (lds <= 110 * 1024) {  // + 41 KB static (diagonal block, partial sums)
     (void)hipFuncSetAttribute((const void*)potrs_blocked_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
-    hipLaunchKernelGGL(potrs_blocked_kernel, dim3(1), dim3(1024), lds, stream, L, n, lda, b);
+    hipLaunchKernelGGL(potrs_blocked_kernel, dim3(1), dim3(1024), lds, stream, L, n, lda, b, 0);
     return srml_status();
   }
   (void)hipFuncSetAttribute((const void*)potrs_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(potrs_kernel, dim3(1), dim3(1024), lds, stream, L, n, lda, b);
+  return srml_status();
+}
+
+// L^T x = z only (z = L^-1 b from the augmented factorisation of [A b; b^T c], whose last row
+// is z^T: the forward sweep rides along with the Cholesky's panel updates for free)
+SRML_API int srml_potrs_backward_f64(const double* L, int n, long lda, double* z, hipStream_t stream) {
+  if (n <= 0) return 0;
+  const size_t lds = (size_t)n * sizeof(double);
+  if (lds > 110 * 1024) return -9;
+  (void)hipFuncSetAttribute((const void*)potrs_blocked_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(potrs_blocked_kernel, dim3(1), dim3(1024), lds, stream, L, n, lda, z, 1);
   return srml_status();
 }
 

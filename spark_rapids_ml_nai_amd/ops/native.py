@@ -101,6 +101,7 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_syevj_f64": (_P, _I, _P, _P, _I, _D, _P),
     "srml_potrf_f64": (_P, _I, _L, _P, _P),
     "srml_potrs_f64": (_P, _I, _L, _P, _P),
+    "srml_potrs_backward_f64": (_P, _I, _L, _P, _P),
     "srml_cd_gram_f64": (_P, _I, _L, _P, _P, _P, _P, _I, _D, _P, _P),
     "srml_rf_quantize_u8": (_P, _L, _I, _L, _P, _I, _P, _P),
     "srml_rf_quantiles_f32": (_P, _I, _I, _I, _P, _P),
