@@ -57,6 +57,50 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
   }
 }
 
+// Register-resident variant of the diagonal-block factorisation (one wave, lane i = row i, the
+// row in 64 VGPR pairs with compile-time indices): per pivot column j the pivot and every S[l][j]
+// reach all lanes by scalar readlane broadcasts, and the right-looking update is one FMA per
+// (l, lane). Entries above the diagonal are updated too but never read, so no masking is needed;
+// padded rows (i >= nb) hold identity rows. No LDS and no barriers inside the 64-step chain.
+__device__ __forceinline__ double bcast_f64(double v, int src) {
+  const long long bits = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(bits & 0xffffffffLL), src);
+  const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), src);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+__global__ __launch_bounds__(64) void potrf_diag_reg_kernel(double* __restrict__ A, long lda, int k0, int nb,
+                                                            int* __restrict__ info) {
+  const int i = threadIdx.x;
+  double c[NB];
+  const double* row = A + (long)(k0 + (i < nb ? i : 0)) * lda + k0;
+#pragma unroll
+  for (int l = 0; l < NB; ++l) c[l] = (i < nb && l < nb) ? row[l] : (i == l ? 1.0 : 0.0);
+  int bad = 0;
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    double d = bcast_f64(c[j], j);
+    if (!(d > 0.0)) {
+      if (!bad && j < nb) bad = k0 + j + 1;
+      d = 1.0;
+    } else {
+      d = sqrt(d);
+    }
+    const double rd = 1.0 / d;  // one division per column, the scaling is a multiply
+    if (i == j) c[j] = d;
+    else if (i > j) c[j] *= rd;
+#pragma unroll
+    for (int l = j + 1; l < NB; ++l) c[l] = fma(-c[j], bcast_f64(c[j], l), c[l]);
+  }
+  if (i == 0 && bad && *info == 0) *info = bad;
+  if (i < nb) {
+    double* out = A + (long)(k0 + i) * lda + k0;
+#pragma unroll
+    for (int l = 0; l < NB; ++l)
+      if (l < nb) out[l] = l <= i ? c[l] : 0.0;
+  }
+}
+
 // rows r >= k1: x (1 x NB) solves x L11^T = A[r, k0:k0+NB] (only full panels reach the TRSM: the
 // last, possibly narrower, diagonal block has no rows below it)
 __global__ __launch_bounds__(256) void potrf_trsm_kernel(double* __restrict__ A, long lda, int k0, int k1, int n) {
@@ -534,12 +578,16 @@ __global__ __launch_bounds__(1024) void cd_gram_pipe_kernel(const double* __rest
 
 SRML_API int srml_potrf_f64(double* A, int n, long lda, int* info, hipStream_t stream) {
   if (n <= 0) return 0;
+  static const int diag_reg = getenv("SRML_POTRF_REG") ? atoi(getenv("SRML_POTRF_REG")) : 1;
   hipError_t err = hipSuccess;
   SRML_TRY(err, hipMemsetAsync(info, 0, sizeof(int), stream));
   for (int k0 = 0; k0 < n; k0 += NB) {
     const int nb = n - k0 < NB ? n - k0 : NB;
     const int k1 = k0 + nb;
-    hipLaunchKernelGGL(potrf_diag_kernel, dim3(1), dim3(256), 0, stream, A, lda, k0, nb, info);
+    if (diag_reg)
+      hipLaunchKernelGGL(potrf_diag_reg_kernel, dim3(1), dim3(64), 0, stream, A, lda, k0, nb, info);
+    else
+      hipLaunchKernelGGL(potrf_diag_kernel, dim3(1), dim3(256), 0, stream, A, lda, k0, nb, info);
     if (k1 < n) {
       const int m2 = n - k1;
       hipLaunchKernelGGL(potrf_trsm_kernel, dim3((m2 + 255) / 256), dim3(256), 0, stream, A, lda, k0, k1, n);
