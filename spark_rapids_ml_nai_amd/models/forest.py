@@ -404,17 +404,24 @@ def grow_tree(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: Wor
     return grow_forest(bins, edges_h, y, ctx, gen, p, S, regression, data_parallel, gen_boot, 1)[0]
 
 
-def fit_forest(X: torch.Tensor, y: torch.Tensor, ctx: WorkerContext, m_total: int, p: Dict[str, Any],
-               n_trees_local: int, classification: bool, num_classes: int, data_parallel: bool,
-               rank_seed: int) -> List[Dict[str, Any]]:
-    m, n = X.shape
-    n_bins = int(p["n_bins"])
+def quantize_features(X: torch.Tensor, n_bins: int, ctx: WorkerContext, m_total: int, seed: int
+                      ) -> Tuple[torch.Tensor, np.ndarray]:
+    """(feature-major uint8 bins, host fp64 edges) of the shard: the quantile binning every tree
+    of a fit shares (and every param map of a fitMultiple with the same maxBins / seed)."""
     if n_bins > 256:
         raise ValueError("maxBins > 256 is not supported (uint8 bins)")
-    seed = int(p["random_state"]) if p.get("random_state") is not None else 0
     edges = bin_edges(X, n_bins, ctx, m_total, seed)
     bins = ops.rf_quantize(X, edges)
-    edges_h = edges.double().cpu().numpy()
+    return bins, edges.double().cpu().numpy()
+
+
+def fit_forest(X: torch.Tensor, y: torch.Tensor, ctx: WorkerContext, m_total: int, p: Dict[str, Any],
+               n_trees_local: int, classification: bool, num_classes: int, data_parallel: bool,
+               rank_seed: int, binned: Optional[Tuple[torch.Tensor, np.ndarray]] = None) -> List[Dict[str, Any]]:
+    m, n = X.shape
+    n_bins = int(p["n_bins"])
+    seed = int(p["random_state"]) if p.get("random_state") is not None else 0
+    bins, edges_h = binned if binned is not None else quantize_features(X, n_bins, ctx, m_total, seed)
     S = num_classes if classification else 3
     # feature-subset RNG: shared by all ranks in data-parallel mode (same trees everywhere);
     # bootstrap RNG: always rank-specific (each rank bags its own rows)
@@ -429,7 +436,6 @@ def fit_forest(X: torch.Tensor, y: torch.Tensor, ctx: WorkerContext, m_total: in
         nt = min(per_batch, n_trees_local - t0)
         for t in grow_forest(bins, edges_h, y, ctx, gen, p, S, not classification, data_parallel, gen_boot, nt):
             trees.append(t.to_dict())
-    del bins
     return trees
 
 

@@ -225,7 +225,7 @@ class _RandomForestEstimator(_RandomForestClass, _EstimatorSupervised, _RandomFo
         nw = self.num_workers
 
         def _fit(inp: FitInput, ctx: WorkerContext, params: Dict[str, Any]) -> Any:
-            from .models.forest import feature_subset_size, fit_forest
+            from .models.forest import feature_subset_size, fit_forest, quantize_features
 
             X, y = inp.X, inp.y
             n = inp.desc.n
@@ -240,6 +240,9 @@ class _RandomForestEstimator(_RandomForestClass, _EstimatorSupervised, _RandomFo
                     raise ValueError("RandomForestClassifier supports at most 32 classes")
             maps = params["fit_multiple_params"] or [{}]
             outs = []
+            # hyper-parameter batching: param maps with the same (maxBins, seed) share one quantile
+            # binning of the shard (bin edges + uint8 matrix), the per-fit pass over X
+            binned: Dict[Any, Any] = {}
             for mp in maps:
                 p = dict(params["cuml_init"], **mp)
                 mode = p.get("split_mode", "ensemble")
@@ -256,8 +259,11 @@ class _RandomForestEstimator(_RandomForestClass, _EstimatorSupervised, _RandomFo
                 if crit in ("variance", "mse"):
                     p["split_criterion"] = "variance"
                 seed = int(p["random_state"]) if p.get("random_state") is not None else 0
+                key = (int(p["n_bins"]), seed)
+                if key not in binned:
+                    binned[key] = quantize_features(X, key[0], ctx, inp.desc.m, seed)
                 trees = fit_forest(X, y, ctx, inp.desc.m, p, n_local, classification, num_classes, data_parallel,
-                                   rank_seed=seed * 1000003 + ctx.rank)
+                                   rank_seed=seed * 1000003 + ctx.rank, binned=binned[key])
                 if not data_parallel and ctx.world_size > 1:
                     # forests of peer ranks of this same job (numpy node arrays), device all-gather
                     import pickle

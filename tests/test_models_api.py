@@ -206,3 +206,28 @@ def test_rf_hist_features_per_item_rule():
     for B, S in ((128, 20), (256, 12), (256, 32), (128, 32)):
         fb = ops.rf_hist_fb(B, S, False)
         assert 1 <= fb < ops.RF_HIST_FB_MAX and fb * B * S * 4 <= 64 * 1024
+
+
+def test_rf_fit_multiple_shares_binning_and_matches_single_fits(monkeypatch):
+    """RF hyper-parameter batching: param maps with the same maxBins / seed share ONE quantile
+    binning pass; every model equals the model of its own single fit."""
+    from spark_rapids_ml_nai_amd import DataFrame
+    from spark_rapids_ml_nai_amd.models import forest
+    from spark_rapids_ml_nai_amd.regression import RandomForestRegressor
+
+    rng = np.random.default_rng(4)
+    X = rng.standard_normal((3000, 8)).astype(np.float32)
+    y = X[:, 0] - 2 * X[:, 3] + 0.1 * rng.standard_normal(3000)
+    df = DataFrame.from_numpy(X, y)
+    calls = []
+    orig = forest.quantize_features
+    monkeypatch.setattr(forest, "quantize_features", lambda *a, **k: calls.append(1) or orig(*a, **k))
+    est = RandomForestRegressor(numTrees=3, maxDepth=4, seed=7)
+    maps = [{est.numTrees: 3}, {est.numTrees: 5, est.maxDepth: 3}, {est.maxBins: 16}]
+    models = dict(est.fitMultiple(df, maps))
+    assert len(calls) == 2  # maxBins 32 (two maps) + maxBins 16
+    for i, mp in enumerate(maps):
+        single = est.copy(mp).fit(df)
+        a = models[i].transform(df).to_numpy("prediction")
+        b = single.transform(df).to_numpy("prediction")
+        np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-6)
