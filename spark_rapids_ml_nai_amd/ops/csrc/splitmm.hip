@@ -191,6 +191,29 @@ __device__ __forceinline__ void split_epilogue(const floatx16 (&acc)[BM / WM / 3
   }
 }
 
+// One merge step of the (best value, best index, best's lower bound, others' lower bound) state
+// with the state DPP-moved from another lane; lanes the DPP pattern does not write receive the
+// identity (+inf, INT_MAX, +inf, +inf) and keep their state.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ void top2_merge_dpp(float& bv, int& bi, float& badj, float& sadj) {
+  const float inf = __builtin_huge_valf();
+  const float ov = __int_as_float(
+      __builtin_amdgcn_update_dpp(__float_as_int(inf), __float_as_int(bv), CTRL, ROW_MASK, 0xf, false));
+  const int oi = __builtin_amdgcn_update_dpp(0x7fffffff, bi, CTRL, ROW_MASK, 0xf, false);
+  const float oadj = __int_as_float(
+      __builtin_amdgcn_update_dpp(__float_as_int(inf), __float_as_int(badj), CTRL, ROW_MASK, 0xf, false));
+  const float osadj = __int_as_float(
+      __builtin_amdgcn_update_dpp(__float_as_int(inf), __float_as_int(sadj), CTRL, ROW_MASK, 0xf, false));
+  if (ov < bv || (ov == bv && oi < bi)) {
+    sadj = fminf(fminf(sadj, badj), osadj);
+    bv = ov;
+    bi = oi;
+    badj = oadj;
+  } else {
+    sadj = fminf(fminf(sadj, oadj), osadj);
+  }
+}
+
 // Top-2 epilogue for the certified 3-product search. Each candidate j carries an error radius
 // e_j = sqrt(||x||^2) * g_j (g_j = 2 tau ||c_j||, the bound on |d~_j - d_j| of the dropped
 // products); per (row, wave column slot) it keeps the best (d~, index) and the smallest LOWER
@@ -230,22 +253,15 @@ __device__ __forceinline__ void split_epilogue_top2(const floatx16 (&acc)[BM / W
           else sadj = fminf(sadj, adj);
         }
       }
-#pragma unroll
-      for (int o = 1; o < 32; o <<= 1) {
-        const float ov = __shfl_xor(bv, o, 64);
-        const int oi = __shfl_xor(bi, o, 64);
-        const float oadj = __shfl_xor(badj, o, 64);
-        const float osadj = __shfl_xor(sadj, o, 64);
-        if (ov < bv || (ov == bv && oi < bi)) {
-          sadj = fminf(fminf(sadj, badj), osadj);
-          bv = ov;
-          bi = oi;
-          badj = oadj;
-        } else {
-          sadj = fminf(fminf(sadj, oadj), osadj);
-        }
-      }
-      if (li == 0 && row < m) {
+      // 32-lane merge on DPP (no LDS round trips): quad_perm xor 1 / xor 2, row_half_mirror and
+      // row_mirror leave every lane with its 16-lane row's state, row_bcast:15 folds row 0 into
+      // row 1 (and row 2 into row 3); lane 31 / 63 then holds the 32-lane result of its lk half
+      top2_merge_dpp<0xb1, 0xf>(bv, bi, badj, sadj);
+      top2_merge_dpp<0x4e, 0xf>(bv, bi, badj, sadj);
+      top2_merge_dpp<0x141, 0xf>(bv, bi, badj, sadj);
+      top2_merge_dpp<0x140, 0xf>(bv, bi, badj, sadj);
+      top2_merge_dpp<0x142, 0xa>(bv, bi, badj, sadj);
+      if (li == 31 && row < m) {
         const long o = row * nslot + slot;
         keys[o] = bi == 0x7fffffff ? ~0ull : (((unsigned long long)orderable(bv) << 32) | (unsigned)bi);
         lob[o] = sadj;
