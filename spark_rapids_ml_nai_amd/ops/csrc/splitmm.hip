@@ -470,35 +470,20 @@ __global__ __launch_bounds__(512, 1) void nearest_centroid_split_glds_kernel(
 
   const int ph = lk ^ ((li >> 3) & 1);  // physical half of this lane's fragment
   const int nk = kp / SBK;
-#pragma unroll
-  for (int q = 0; q < NS - 1; ++q)
-    if (q < nk) issue(q, q);
-  int stage = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    // step kt must have landed; the (at most NS - 2) later steps already issued may stay in flight
-    const int ahead = nk - 1 - kt < NS - 2 ? nk - 1 - kt : NS - 2;
-    if constexpr (CPW == 6) {
-      if (ahead >= 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();  // step kt landed for every wave; every wave finished step kt - 1
-    if (kt + NS - 1 < nk) issue(kt + NS - 1, stage == 0 ? NS - 1 : stage - 1);  // kt - 1's stage
+  // one k step of this wave's 32x32 tiles from LDS stage `st`
+  auto compute = [&](int st) {
     bf16x8 fb[NPL][TN];
 #pragma unroll
     for (int p = 0; p < NPL; ++p)
 #pragma unroll
       for (int nt = 0; nt < TN; ++nt)
-        fb[p][nt] = *reinterpret_cast<const bf16x8*>(&lds[stage][NPL + p][wn * (BN / WN) + nt * 32 + li][8 * ph]);
+        fb[p][nt] = *reinterpret_cast<const bf16x8*>(&lds[st][NPL + p][wn * (BN / WN) + nt * 32 + li][8 * ph]);
 #pragma unroll
     for (int mt = 0; mt < TM; ++mt) {
       bf16x8 fa[NPL];
 #pragma unroll
       for (int p = 0; p < NPL; ++p)
-        fa[p] = *reinterpret_cast<const bf16x8*>(&lds[stage][p][wm * (BM / WM) + mt * 32 + li][8 * ph]);
+        fa[p] = *reinterpret_cast<const bf16x8*>(&lds[st][p][wm * (BM / WM) + mt * 32 + li][8 * ph]);
 #pragma unroll
       for (int nt = 0; nt < TN; ++nt) {
         if constexpr (NP == 6) {
@@ -511,7 +496,34 @@ __global__ __launch_bounds__(512, 1) void nearest_centroid_split_glds_kernel(
         acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0][nt], acc[mt][nt], 0, 0, 0);
       }
     }
-    stage = stage == NS - 1 ? 0 : stage + 1;
+  };
+  if constexpr (NP == 6) {
+    // 3-stage ring, one k step per barrier, two steps of load lead
+    issue(0, 0);
+    if (nk > 1) issue(1, 1);
+    int stage = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // step kt + 1 may stay in flight
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // step kt landed for every wave; every wave finished step kt - 1
+      if (kt + 2 < nk) issue(kt + 2, stage == 0 ? 2 : stage - 1);
+      compute(stage);
+      stage = stage == 2 ? 0 : stage + 1;
+    }
+  } else {
+    // 3-product steps carry half the MFMA work: two k steps per barrier on a 4-stage ring (pair p
+    // computes from stages 2p, 2p + 1 mod 4 while pair p + 1 lands in the other two), so the
+    // barrier and the first fragment reads are paid once per 24 MFMAs per wave instead of 12
+    issue(0, 0);
+    if (nk > 1) issue(1, 1);
+    for (int kt = 0; kt < nk; kt += 2) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // steps kt, kt + 1 landed; every wave finished kt - 2, kt - 1
+      if (kt + 2 < nk) issue(kt + 2, (kt + 2) & 3);
+      if (kt + 3 < nk) issue(kt + 3, (kt + 3) & 3);
+      compute(kt & 3);
+      if (kt + 1 < nk) compute((kt + 1) & 3);
+    }
   }
   if (TOP2)
     split_epilogue_top2<BM, BN, WM, WN>(acc, row0, col0, ctile, m, k, cnorm, cg, xnorm, best, lob, n_ctiles * WN, wm,

@@ -78,6 +78,16 @@ def main():
                                          "TFLOP/s(fp32-equiv)": 2 * a.m * a.k * a.n / t / 1e9,
                                          "TFLOP/s(bf16 issued)": 12 * a.m * a.k * a.n / t / 1e9}
         del P
+    if want("nearest_certified"):  # the Lloyd search: centred planes, certified 3-product pass
+        C = torch.randn(a.k, a.n, device=dev, generator=g) * 0.05 + X[:1]
+        mu = X.double().mean(0).float()
+        xn = ops.row_sqnorm(X, mu)
+        P = ops.split_bf16x3(X, tiled=True, mu=mu)
+        t = timeit(lambda: ops.nearest_centroid_split(P, a.m, C, xn, X=X, mu=mu), 3)
+        st = ops._CERTIFY_STATS
+        res["nearest_centroid_certified"] = {"ms": t, "refined_frac": st["refined"] / max(1, st["rows"]),
+                                             "TFLOP/s(bf16 issued)": 6 * a.m * a.k * a.n / t / 1e9}
+        del P
     if want("sums"):
         lab = torch.randint(0, a.k, (a.m,), device=dev, dtype=torch.int32)
         t = timeit(lambda: ops.cluster_sums(X, lab, a.k), 3)
