@@ -217,8 +217,8 @@ __device__ __forceinline__ void top2_merge_dpp(float& bv, int& bi, float& badj, 
 // Top-2 epilogue for the certified 3-product search. Each candidate j carries an error radius
 // e_j = sqrt(||x||^2) * g_j (g_j = 2 tau ||c_j||, the bound on |d~_j - d_j| of the dropped
 // products); per (row, wave column slot) it keeps the best (d~, index) and the smallest LOWER
-// bound d~_j - e_j over the slot's other candidates, plain stores into keys / lob[row * nslot + slot]
-// (slot = ctile * WN + wn); srml_split_top2_select merges the slots.
+// bound d~_j - e_j over the slot's other candidates, plain stores into keys / lob[slot * m + row]
+// (slot = ctile * WN + wn, slot-major: [slot][row]); srml_split_top2_select merges the slots.
 template <int BM, int BN, int WM, int WN>
 __device__ __forceinline__ void split_epilogue_top2(const floatx16 (&acc)[BM / WM / 32][BN / WN / 32], long row0,
                                                     int col0, int ctile, long m, int k,
@@ -262,7 +262,7 @@ __device__ __forceinline__ void split_epilogue_top2(const floatx16 (&acc)[BM / W
       top2_merge_dpp<0x140, 0xf>(bv, bi, badj, sadj);
       top2_merge_dpp<0x142, 0xa>(bv, bi, badj, sadj);
       if (li == 31 && row < m) {
-        const long o = row * nslot + slot;
+        const long o = (long)slot * m + row;  // slot-major: the select kernel reads rows coalesced
         keys[o] = bi == 0x7fffffff ? ~0ull : (((unsigned long long)orderable(bv) << 32) | (unsigned)bi);
         lob[o] = sadj;
       }
@@ -545,21 +545,20 @@ __global__ __launch_bounds__(256) void split_top2_select_kernel(const unsigned l
                                                                 int* __restrict__ flagged, int* __restrict__ n_flagged) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= m) return;
-  const unsigned long long* kr = keys + i * nslot;
-  const float* lr = lob + i * nslot;
+  // slot-major layout (keys / lob[slot * m + row]): consecutive lanes read consecutive rows
   unsigned long long k1 = ~0ull;
   int s1 = 0;
   for (int s = 0; s < nslot; ++s) {
-    const unsigned long long v = kr[s];
+    const unsigned long long v = keys[(long)s * m + i];
     if (v < k1) { k1 = v; s1 = s; }
   }
   const float xn = xnorm[i];
   const float xs = sqrtf(fmaxf(xn, 0.f));
   float low = __builtin_huge_valf();  // min over j != b of d~_j - e_j
   for (int s = 0; s < nslot; ++s) {
-    low = fminf(low, lr[s]);
-    if (s != s1 && kr[s] != ~0ull)
-      low = fminf(low, fmaf(-xs, cg[(int)(kr[s] & 0xffffffffu)], unorderable((unsigned)(kr[s] >> 32))));
+    low = fminf(low, lob[(long)s * m + i]);
+    const unsigned long long v = keys[(long)s * m + i];
+    if (s != s1 && v != ~0ull) low = fminf(low, fmaf(-xs, cg[(int)(v & 0xffffffffu)], unorderable((unsigned)(v >> 32))));
   }
   const float bv = unorderable((unsigned)(k1 >> 32));
   if (k1 != ~0ull && low > fmaf(xs, cg[(int)(k1 & 0xffffffffu)], bv)) {
