@@ -700,10 +700,141 @@ __global__ __launch_bounds__(256, 2) void logreg_binary_pf_kernel(const float* _
   }
 }
 
+// Narrow rows (n <= 512, the BASELINE north-star LogisticRegression is 200M x 256): a 64-lane wave
+// per row leaves 3/4 of the lanes idle below n = 256 and keeps one 1 KiB row in flight per wave
+// behind its dependent reduce -> exp/log chain. Here 16 lanes own a row (G float4 of it per lane),
+// a wave works on 4 rows at once, the row dot product is a 16-lane DPP reduction (the DPP row
+// size) and D row batches are loaded ahead into a register ring, so each wave keeps up to
+// 4 (D + 1) rows of X in flight.
+template <int G, int D>
+__global__ __launch_bounds__(256) void logreg_binary_narrow_kernel(const float* __restrict__ X, long m, int n, long ld,
+                                                                   const float* __restrict__ y,
+                                                                   const double* __restrict__ w, double b_in,
+                                                                   const double* __restrict__ bptr,
+                                                                   const int* __restrict__ flag,
+                                                                   double* __restrict__ out, long rows_per_block) {
+  if (flag && *flag) return;
+  __shared__ float gsum[4][64 * G];
+  __shared__ double red[2][4];
+  const double b = bptr ? *bptr : b_in;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int sub = lane & 15, grp = lane >> 4;
+  double wr[G][4];
+  bool cok[G];
+#pragma unroll
+  for (int k = 0; k < G; ++k) {
+    const int c = (k * 16 + sub) * 4;
+    cok[k] = c + 3 < n;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) wr[k][q] = cok[k] ? w[c + q] : 0.0;
+  }
+  floatx4 g[G];
+#pragma unroll
+  for (int k = 0; k < G; ++k) g[k] = floatx4{0.f, 0.f, 0.f, 0.f};
+  double gb = 0.0, loss = 0.0;
+  const long r0 = (long)blockIdx.x * rows_per_block;
+  const long r1 = min(m, r0 + rows_per_block);
+  const int roff = wid * 4 + grp;  // this lane group's row within a 16-row step of the block
+  auto load = [&](long base, floatx4 (&x)[G]) {
+    long r = base + roff;
+    if (r >= r1) r = r1 - 1;  // clamped rows are loaded but never accumulated
+    const float* row = X + r * ld;
+#pragma unroll
+    for (int k = 0; k < G; ++k)
+      x[k] = cok[k] ? __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(row + (k * 16 + sub) * 4))
+                    : floatx4{0.f, 0.f, 0.f, 0.f};
+  };
+  auto process = [&](long base, const floatx4 (&x)[G]) {
+    const long r = base + roff;
+    double dot = 0.0;
+#pragma unroll
+    for (int k = 0; k < G; ++k)
+      dot = fma((double)x[k][0], wr[k][0], fma((double)x[k][1], wr[k][1],
+            fma((double)x[k][2], wr[k][2], fma((double)x[k][3], wr[k][3], dot))));
+    dot += dpp_d<0xb1>(dot);   // quad_perm [1,0,3,2]
+    dot += dpp_d<0x4e>(dot);   // quad_perm [2,3,0,1]
+    dot += dpp_d<0x141>(dot);  // row_half_mirror
+    dot += dpp_d<0x140>(dot);  // row_mirror: every lane of the 16-lane row holds the row's dot
+    if (r < r1) {
+      double res, lt;
+      logistic_terms(dot + b, (double)y[r], res, lt);
+      if (sub == 0) {
+        loss += lt;
+        gb += res;
+      }
+      const float rf = (float)res;
+#pragma unroll
+      for (int k = 0; k < G; ++k)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) g[k][q] = fmaf(rf, x[k][q], g[k][q]);
+    }
+  };
+  floatx4 xs[D + 1][G];
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+    if (r0 + d * 16 < r1) load(r0 + d * 16, xs[d]);
+  for (long rb = r0; rb < r1; rb += (D + 1) * 16) {
+#pragma unroll
+    for (int ph = 0; ph <= D; ++ph) {
+      const long cur = rb + ph * 16;
+      if (cur < r1) {
+        const long nxt = cur + D * 16;
+        if (nxt < r1) load(nxt, xs[(ph + D) % (D + 1)]);
+        process(cur, xs[ph]);
+      }
+    }
+  }
+  // fold the 4 row groups of the wave (lanes sub, sub + 16, sub + 32, sub + 48 share columns),
+  // then the 4 waves through LDS, then one fp64 atomic per column per block
+#pragma unroll
+  for (int k = 0; k < G; ++k)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float v = g[k][q];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (grp == 0) gsum[wid][(k * 16 + sub) * 4 + q] = v;
+    }
+  loss = wave_sum(loss);
+  gb = wave_sum(gb);
+  if (lane == 0) {
+    red[0][wid] = gb;
+    red[1][wid] = loss;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < n; c += 256) {
+    const float v = (gsum[0][c] + gsum[1][c]) + (gsum[2][c] + gsum[3][c]);
+    if (v != 0.f) atomicAdd(&out[c], (double)v);
+  }
+  if (threadIdx.x == 0) {
+    atomicAdd(&out[n], (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]));
+    atomicAdd(&out[n + 1], (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]));
+  }
+}
+
 // b: intercept by value, or (bptr != null) read on the device; flag (optional): skip when *flag != 0
 SRML_API int srml_logreg_binary2_f32(const float* X, long m, int n, long ld, const float* y, const double* w, double b,
                                      const double* bptr, const int* flag, double* out, hipStream_t stream) {
   if (m <= 0) return 0;
+  static const int narrow = getenv("SRML_LOGREG_NARROW") ? atoi(getenv("SRML_LOGREG_NARROW")) : 1;
+  if (narrow && n <= 512 && (n & 3) == 0 && (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0) {
+    long nb = m / 256;  // ~256 rows (16 steps of 16) per block, 512 .. 4096 blocks
+    if (nb > 4096) nb = 4096;
+    if (nb < 1) nb = 1;
+    long rpb = (m + nb - 1) / nb;
+    rpb = (rpb + 15) / 16 * 16;
+    const long blocks = (m + rpb - 1) / rpb;
+    const int G = (n + 63) / 64;
+#define SRML_LR_NARROW(GG, DD)                                                                                       \
+  hipLaunchKernelGGL((logreg_binary_narrow_kernel<GG, DD>), dim3((unsigned)blocks), dim3(256), 0, stream, X, m, n, ld, \
+                     y, w, b, bptr, flag, out, rpb)
+    if (G <= 1) SRML_LR_NARROW(1, 3);
+    else if (G <= 2) SRML_LR_NARROW(2, 3);
+    else if (G <= 4) SRML_LR_NARROW(4, 3);
+    else SRML_LR_NARROW(8, 2);
+#undef SRML_LR_NARROW
+    return srml_status();
+  }
   // ~>= 120 rows per block: each block pays a w load and an n-wide fp64 atomic flush, so small
   // shards (the per-rank rows of a multi-GPU fit) want fewer blocks (125k rows: 1024 blocks
   // 0.334 ms vs 2048 blocks 0.385 ms; 1M rows: 2048 blocks best)
