@@ -69,10 +69,10 @@ def train_quantizer(X: torch.Tensor, nlist: int, seed: int, iters: int = 10,
     """IVF coarse quantiser: Lloyd iterations (fused MFMA nearest-centroid + cluster sums) on a
     row subsample, as IVF trainers do."""
     m = X.shape[0]
-    gen = torch.Generator().manual_seed(int(seed))
+    gen = torch.Generator(device=X.device).manual_seed(int(seed))  # device permutations: no host RNG
     ntrain = min(m, max(nlist * train_rows_per_list, 4 * nlist))
-    T = X if ntrain == m else X.index_select(0, torch.randperm(m, generator=gen)[:ntrain].to(X.device))
-    C = T.index_select(0, torch.randperm(T.shape[0], generator=gen)[:nlist].to(X.device)).float().clone()
+    T = X if ntrain == m else X.index_select(0, torch.randperm(m, generator=gen, device=X.device)[:ntrain])
+    C = T.index_select(0, torch.randperm(T.shape[0], generator=gen, device=X.device)[:nlist]).float().clone()
     tn = ops.row_sqnorm(T)
     for _ in range(max(1, iters)):
         lab, _d = ops.nearest_centroid(T, C, tn)
@@ -122,7 +122,7 @@ def knn_graph_ivf(X: torch.Tensor, k: int, nlist: Optional[int] = None, nprobe: 
     lab, _ = ops.nearest_centroid(X, C)
     lab = lab.long()
     order = torch.argsort(lab, stable=True)
-    counts = torch.bincount(lab, minlength=nlist)
+    counts = ops.sorted_counts(lab[order], nlist)
     off = torch.zeros(nlist + 1, dtype=torch.int64, device=X.device)
     off[1:] = torch.cumsum(counts, 0)
     Xs = X.index_select(0, order).contiguous()

@@ -224,8 +224,8 @@ def _spectral_device(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor,
     deg = torch.zeros(n, dtype=torch.float64, device=dev).index_add_(0, r64, vals.double())
     dinv = 1.0 / torch.sqrt(deg.clamp_min(1e-30))
     mv = (dinv[r64] * vals.double() * dinv[cols.long()]).float().contiguous()
-    indptr = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-    torch.cumsum(torch.bincount(r64, minlength=n), 0, out=indptr[1:])
+    # rows are sorted: the CSR row pointer is a binary search per row boundary (no atomics)
+    indptr = torch.searchsorted(r64.contiguous(), torch.arange(n + 1, device=dev, dtype=torch.int64))
     M = CSR(indptr=indptr, indices=cols.to(torch.int32).contiguous(), data=mv, shape=(n, n))
     p = min(n, dim + 1 + 8)
     g = torch.Generator(device="cpu").manual_seed(int(seed))
@@ -282,8 +282,8 @@ def spectral_init(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n:
     else:
         coords = _spectral_device(rows, cols, vals, n, dim, seed)
     expansion = 10.0 / coords.abs().max().clamp_min(1e-30)
-    g = torch.Generator(device="cpu").manual_seed(int(seed) + 1)
-    return coords * expansion + (torch.randn(coords.shape, generator=g) * 1e-4).to(dev)
+    g = torch.Generator(device=dev).manual_seed(int(seed) + 1)
+    return coords * expansion + torch.randn(coords.shape, generator=g, device=dev) * 1e-4
 
 
 def make_epochs_per_sample(w: torch.Tensor, n_epochs: int) -> torch.Tensor:

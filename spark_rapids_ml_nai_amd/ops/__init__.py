@@ -544,6 +544,14 @@ def kmeanspp_gram(G: torch.Tensor, w: torch.Tensor, k: int, seed: int, trials: O
     return torch.tensor(picks, dtype=torch.long, device=G.device)
 
 
+def sorted_counts(sorted_labels: torch.Tensor, k: int) -> torch.Tensor:
+    """int64 counts of labels 0..k-1 from an ascending label vector: segment boundaries by binary
+    search (no atomics, no host synchronisation - torch.bincount reads the maximum back first)."""
+    bounds = torch.searchsorted(sorted_labels.contiguous(),
+                                torch.arange(k + 1, device=sorted_labels.device, dtype=sorted_labels.dtype))
+    return (bounds[1:] - bounds[:-1]).long()
+
+
 def cluster_sums(X: torch.Tensor, labels: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
     """(sums fp64 [k, n], counts int64 [k]) of rows grouped by label."""
     m, n = X.shape
@@ -557,7 +565,7 @@ def cluster_sums(X: torch.Tensor, labels: torch.Tensor, k: int) -> Tuple[torch.T
     if X.dtype == torch.float64 or deterministic():
         # label-sorted segments, one block per (cluster, column chunk), fixed order, no atomics
         slab, perm = torch.sort(lab, stable=True)
-        counts = torch.bincount(lab, minlength=k).long()
+        counts = sorted_counts(slab, k)
         off = torch.zeros(k + 1, dtype=torch.int64, device=X.device)
         torch.cumsum(counts, 0, out=off[1:])
         sums = torch.empty((k, n), dtype=torch.float64, device=X.device)
@@ -584,7 +592,7 @@ def cluster_sums(X: torch.Tensor, labels: torch.Tensor, k: int) -> Tuple[torch.T
     sums = torch.zeros((k, n), dtype=torch.float64, device=X.device)
     native.call("srml_kmeans_accumulate_sorted_f32", X.data_ptr(), m, n, X.stride(0), perm.data_ptr(),
                 slab.data_ptr(), sums.data_ptr(), st)
-    return sums, torch.bincount(lab, minlength=k).long()
+    return sums, sorted_counts(slab, k)
 
 
 # ------------------------------------------------------------------------------------------
