@@ -29,3 +29,20 @@ def test_parse_cpulist_and_numa_bind_noop_on_cpu():
 
     assert _parse_cpulist("0-3,8,10-11\n") == [0, 1, 2, 3, 8, 10, 11]
     assert bind_numa_local(torch.device("cpu")) is None
+
+
+def test_sorted_counts_matches_bincount():
+    """Label counts by binary search over sorted labels (cluster sums, IVF lists, UMAP CSR) equal
+    torch.bincount, including empty labels at both ends and in the middle."""
+    import torch
+
+    from spark_rapids_ml_nai_amd import ops
+
+    g = torch.Generator().manual_seed(3)
+    for k in (1, 7, 1000):
+        lab = torch.randint(0, k, (5000,), generator=g)
+        lab = lab[(lab != k // 2) | (k == 1)]  # a gap
+        s, _ = torch.sort(lab)
+        assert torch.equal(ops.sorted_counts(s, k), torch.bincount(lab, minlength=k))
+    s32 = torch.tensor([1, 1, 4], dtype=torch.int32)
+    assert ops.sorted_counts(s32, 6).tolist() == [0, 2, 0, 0, 1, 0]
