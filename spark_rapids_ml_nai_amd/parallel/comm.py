@@ -142,8 +142,11 @@ class Communicator:
             # all_gather into one group of per-root broadcasts), no padding to the largest block
             ct = self._comm_tensor(t.contiguous())
             out = [torch.empty((s,) + tail, dtype=t.dtype, device=ct.device) for s in sizes]
-            dist.all_gather(out, ct, group=self.group)
-            return out
+            try:
+                dist.all_gather(out, ct, group=self.group)
+                return out
+            except (RuntimeError, ValueError):  # a backend build without ragged all_gather: pad
+                pass
         pad = torch.zeros((mx,) + tail, dtype=t.dtype, device=t.device)
         pad[: t.shape[0]] = t
         g = self.allgather(pad).view((self.size, mx) + tuple(t.shape[1:]))
