@@ -676,15 +676,16 @@ __device__ __forceinline__ double uniform01(unsigned long long seed, unsigned lo
 constexpr int KPP_T = 1024;
 constexpr int KPP_PER = 8;     // candidates per thread (nc <= 8192)
 constexpr int KPP_TRIALS = 16; // max greedy trials per centre
+constexpr int KPP_CHUNK = 4;   // greedy trials whose G-row loads are issued together
 
 // block-wide inverse-CDF draws of L targets u[j] * total over p >= 0 (candidate base + q of the
 // thread that owns the target's half-open prefix range); picks[j] = -1 if total == 0
-__device__ void kpp_sample(const double (&p)[KPP_PER], int base, int cnt, const double* u, int L, double* lds,
+__device__ void kpp_sample(const double (*wv)[KPP_T], const double (&d2)[KPP_PER], int base, int cnt, const double* u, int L, double* lds,
                            int* picks) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   double loc = 0.0;
 #pragma unroll
-  for (int q = 0; q < KPP_PER; ++q) loc += q < cnt ? p[q] : 0.0;
+  for (int q = 0; q < KPP_PER; ++q) loc += q < cnt ? wv[q][threadIdx.x] * d2[q] : 0.0;
   // inclusive scan of the per-thread sums within the wave, then across the 16 waves
   double x = loc;
 #pragma unroll
@@ -706,12 +707,15 @@ __device__ void kpp_sample(const double (&p)[KPP_PER], int base, int cnt, const 
     const double target = u[j] * total;
     if (total > 0.0 && excl <= target && target < excl + loc) {
       double run = excl;
-      int hit = cnt - 1;
-      for (int q = 0; q < cnt; ++q) {
-        run += p[q];
-        if (target < run) { hit = q; break; }
+      int hit = -1;
+#pragma unroll
+      for (int q = 0; q < KPP_PER; ++q) {  // static indices: the candidate arrays stay in VGPRs
+        if (q < cnt) {
+          run += wv[q][threadIdx.x] * d2[q];
+          if (hit < 0 && target < run) hit = q;
+        }
       }
-      picks[j] = base + hit;  // exactly one thread owns the target (half-open ranges)
+      picks[j] = base + (hit < 0 ? cnt - 1 : hit);  // exactly one thread owns the target (half-open ranges)
     }
   }
   __syncthreads();
@@ -736,22 +740,27 @@ __global__ __launch_bounds__(KPP_T) void kmeanspp_gram_kernel(const double* __re
   __shared__ double pot[KPP_T / 64][KPP_TRIALS];
   __shared__ double u[KPP_TRIALS];
   __shared__ int picks[KPP_TRIALS];
+  // ||c_i||^2 and w_i of this thread's candidates live in LDS (128 KB), so the 128-VGPR budget of
+  // a 1024-thread block holds d2 plus the in-flight G-row loads without scratch spills
+  __shared__ double s_gii[KPP_PER][KPP_T];
+  __shared__ double s_w[KPP_PER][KPP_T];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int base = threadIdx.x * KPP_PER;
   const int cnt = max(0, min(KPP_PER, nc - base));
-  double d2[KPP_PER], wv[KPP_PER], gii[KPP_PER], p[KPP_PER];
+  double d2[KPP_PER];  // p_q = w_q d2_q is formed where it is used
 #pragma unroll
   for (int q = 0; q < KPP_PER; ++q) {
     const int i = base + q;
     const bool ok = q < cnt;
-    wv[q] = ok ? w[i] : 0.0;
-    gii[q] = ok ? G[(long)i * nc + i] : 0.0;
-    d2[q] = INFINITY;
-    p[q] = wv[q];
+    s_w[q][threadIdx.x] = ok ? w[i] : 0.0;
+    s_gii[q][threadIdx.x] = ok ? G[(long)i * nc + i] : 0.0;
+    d2[q] = 1.0;  // the first draw is ~ w alone
   }
   if (threadIdx.x == 0) u[0] = uniform01(seed, 0);
   __syncthreads();
-  kpp_sample(p, base, cnt, u, 1, lds, picks);
+  kpp_sample(s_w, d2, base, cnt, u, 1, lds, picks);
+#pragma unroll
+  for (int q = 0; q < KPP_PER; ++q) d2[q] = INFINITY;
   int c = picks[0] < 0 ? 0 : picks[0];
   if (threadIdx.x == 0) out[0] = c;
   for (int t = 1; t < k; ++t) {
@@ -759,30 +768,42 @@ __global__ __launch_bounds__(KPP_T) void kmeanspp_gram_kernel(const double* __re
     const double* gc = G + (long)c * nc;
 #pragma unroll
     for (int q = 0; q < KPP_PER; ++q) {
-      if (q < cnt) {
-        const double dd = fmax(gii[q] + gcc - 2.0 * gc[base + q], 0.0);
-        d2[q] = fmin(d2[q], dd);
-        p[q] = wv[q] * d2[q];
-      }
+      const double dd = fmax(s_gii[q][threadIdx.x] + gcc - 2.0 * gc[min(base + q, nc - 1)], 0.0);
+      if (q < cnt) d2[q] = fmin(d2[q], dd);
     }
     __syncthreads();  // picks / u of the previous step fully consumed
     if (threadIdx.x < L) u[threadIdx.x] = uniform01(seed, (unsigned long long)t * KPP_TRIALS + threadIdx.x);
     __syncthreads();
-    kpp_sample(p, base, cnt, u, L, lds, picks);
+    kpp_sample(s_w, d2, base, cnt, u, L, lds, picks);
     if (picks[0] < 0) {  // all mass on chosen points: any candidate
       c = (int)(splitmix64(seed + 77 * t) % (unsigned long long)nc);
     } else {
-      // potential of each trial: one pass over this thread's candidates per trial, block-reduced
-      for (int j = 0; j < L; ++j) {
-        const int tj = picks[j];
-        const double gtt = G[(long)tj * nc + tj];
-        const double* gt = G + (long)tj * nc;
-        double s = 0.0;
+      // potential of each trial: one pass over this thread's candidates per trial, block-reduced.
+      // KPP_CHUNK trials at a time with branch-free (clamped) loads, so their G-row reads are in
+      // flight together instead of one latency per trial; a candidate past nc has wv = 0 and adds
+      // +0.0, so every trial's sum is bit-identical to the one-trial-at-a-time order.
+      for (int j0 = 0; j0 < L; j0 += KPP_CHUNK) {
+        double s[KPP_CHUNK];
 #pragma unroll
-        for (int q = 0; q < KPP_PER; ++q)
-          if (q < cnt) s += wv[q] * fmin(d2[q], fmax(gii[q] + gtt - 2.0 * gt[base + q], 0.0));
-        s = wave_sum(s);
-        if (lane == 0) pot[wid][j] = s;
+        for (int jj = 0; jj < KPP_CHUNK; ++jj) {
+          const int tj = picks[min(j0 + jj, L - 1)];
+          const double* gt = G + (long)tj * nc;
+          const double gtt = gt[tj];
+          double a = 0.0;
+#pragma unroll
+          for (int q = 0; q < KPP_PER; ++q) {
+            const double g = gt[min(base + q, nc - 1)];
+            if (q < cnt) a += s_w[q][threadIdx.x] * fmin(d2[q], fmax(s_gii[q][threadIdx.x] + gtt - 2.0 * g, 0.0));
+          }
+          s[jj] = a;
+        }
+#pragma unroll
+        for (int jj = 0; jj < KPP_CHUNK; ++jj) {
+          if (j0 + jj < L) {  // block-uniform
+            const double r = wave_sum(s[jj]);
+            if (lane == 0) pot[wid][j0 + jj] = r;
+          }
+        }
       }
       __syncthreads();
       int best = 0;

@@ -88,6 +88,14 @@ def main():
         res["nearest_centroid_certified"] = {"ms": t, "refined_frac": st["refined"] / max(1, st["rows"]),
                                              "TFLOP/s(bf16 issued)": 6 * a.m * a.k * a.n / t / 1e9}
         del P
+    if want("kpp"):  # greedy k-means++ over the k-means|| candidates (one block, k sequential steps)
+        for nc in (4001, 8000):
+            gk = torch.Generator().manual_seed(nc)
+            Cc = torch.randn(nc, 32, generator=gk, dtype=torch.float64)
+            G = (Cc @ Cc.T).to(dev)
+            w = torch.randint(1, 50, (nc,), generator=gk).double().to(dev)
+            t = timeit(lambda: ops.kmeanspp_gram(G, w, a.k, 1234), 3)
+            res[f"kmeanspp_gram_nc{nc}"] = {"ms": t, "us_per_centre": 1e3 * t / a.k}
     if want("sums"):
         lab = torch.randint(0, a.k, (a.m,), device=dev, dtype=torch.int32)
         t = timeit(lambda: ops.cluster_sums(X, lab, a.k), 3)
