@@ -228,5 +228,16 @@ def kmeans_fit(X: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext, k
 
 
 def kmeans_predict(X: torch.Tensor, C: torch.Tensor) -> torch.Tensor:
+    """Labels of ``X`` under centres ``C``. Large batches with k > 256 on a GPU run the fit's
+    certified search (centred split-bf16 planes, 3-product pass + exact re-search of near-tie rows:
+    the exact search's labels); otherwise the fp32 MFMA search. ``SRML_KMEANS_PREDICT_SPLIT=0``
+    forces the latter."""
+    k = C.shape[0]
+    if (X.is_cuda and k > 256 and X.shape[0] >= 65536 and _use_split(X, k)
+            and os.environ.get("SRML_KMEANS_PREDICT_SPLIT", "1") == "1"):
+        mu = ops.col_moments(X, need_sq=False)[0].div_(X.shape[0]).float()
+        XP = ops.split_bf16x3(X, tiled=True, mu=mu)
+        labels, _ = ops.nearest_centroid_split(XP, X.shape[0], C.float(), ops.row_sqnorm(X, mu), X=X, mu=mu)
+        return labels
     labels, _ = ops.nearest_centroid(X, C)
     return labels

@@ -708,3 +708,25 @@ def test_nearest_centroid_certified_matches_exact(gpu_device, m, n, k, ties):
         assert refined >= m // 4  # every bisector row was re-searched
     else:
         assert refined < m // 2  # the filter certifies most rows on generic data
+
+
+def test_kmeans_predict_certified_matches_exact(gpu_device, monkeypatch):
+    """Large-batch k > 256 predict runs the certified split search: fp64 arg-min labels (up to
+    near-ties) and the same labels as the fp32 MFMA search it replaces."""
+    from spark_rapids_ml_nai_amd.models.kmeans import kmeans_predict
+
+    g = torch.Generator(device=gpu_device).manual_seed(5)
+    X = torch.randn(70000, 256, device=gpu_device, generator=g) + 3.0
+    C = X[torch.randperm(70000, device=gpu_device, generator=g)[:300]] + 0.1 * torch.randn(
+        300, 256, device=gpu_device, generator=g)
+    st0 = dict(ops._CERTIFY_STATS)
+    got = kmeans_predict(X, C)
+    assert ops._CERTIFY_STATS["rows"] > st0.get("rows", 0)  # the certified path ran
+    monkeypatch.setenv("SRML_KMEANS_PREDICT_SPLIT", "0")
+    fp32 = kmeans_predict(X, C)
+    Xd, Cd = X.double(), C.double()
+    d = (Xd * Xd).sum(1, keepdim=True) - 2.0 * Xd @ Cd.T + (Cd * Cd).sum(1).view(1, -1)
+    ref = d.argmin(1).int()
+    assert got.dtype == torch.int32 and got.shape == (70000,)
+    assert (got == ref).float().mean().item() > 0.9999
+    assert (got == fp32).float().mean().item() > 0.9999
