@@ -680,8 +680,8 @@ constexpr int KPP_CHUNK = 4;   // greedy trials whose G-row loads are issued tog
 
 // block-wide inverse-CDF draws of L targets u[j] * total over p >= 0 (candidate base + q of the
 // thread that owns the target's half-open prefix range); picks[j] = -1 if total == 0
-__device__ void kpp_sample(const double (*wv)[KPP_T], const double (&d2)[KPP_PER], int base, int cnt, const double* u, int L, double* lds,
-                           int* picks) {
+__device__ void kpp_sample(const double (*wv)[KPP_T], const double (&d2)[KPP_PER], int base, int cnt,
+                           const double* u, int L, double* lds, int* picks) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   double loc = 0.0;
 #pragma unroll
