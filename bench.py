@@ -45,6 +45,19 @@ def _batched_frame(X, y, batch_rows):
     return DataFrame([pa.Table.from_batches(rbs)])
 
 
+def _spawn_ranks(n: int) -> int:
+    """Re-run this command as an n-rank torch.distributed job on this node (127.0.0.1 rendezvous)."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -66,11 +79,22 @@ def main() -> None:
                     help="rank 0 saves each workload's last fitted model under this directory")
     args = ap.parse_args()
 
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # not under a launcher: start the N ranks ourselves (one process per GPU) from this parent,
+        # which has not touched the GPU, and exit with the launcher's status
+        sys.exit(_spawn_ranks(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE=%d; launch one rank per GPU (torch.distributed.run "
+              "--nproc-per-node %d) or drop --gpus" % (args.gpus, world, args.gpus), file=sys.stderr)
+        sys.exit(2)
+
     import numpy as np
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     use_gpu = torch.cuda.is_available() and os.environ.get("SRML_FORCE_CPU", "0") != "1"
@@ -151,6 +175,14 @@ def main() -> None:
                 dist.all_reduce(t, op=dist.ReduceOp.MAX)
                 dt = float(t.item())
             per_fit = dt / args.steps
+            # per-rank split of the last timed fit (wall / H2D / compute / comm-wait), gathered
+            # after the clock stopped
+            rs = getattr(model, "_rank_stats", None) or {}
+            if world > 1:
+                per_rank = [None] * world
+                dist.all_gather_object(per_rank, rs)
+            else:
+                per_rank = [rs]
             results[name] = {
                 "fit_s": round(per_fit, 4),
                 "speedup_vs_spark_cpu": round(SPARK_CPU_S[name] / per_fit, 1) if name in SPARK_CPU_S else None,
@@ -158,6 +190,7 @@ def main() -> None:
                 "vs_ref_gpu": round(REF_GPU_S[name] / per_fit, 1) if name in REF_GPU_S else None,
                 "phases": {k: round(v, 4) for k, v in getattr(model, "_fit_timings", {}).items()},
                 "evidence": model_evidence(name, model),
+                "per_rank": per_rank,
             }
             if not args.no_transform:
                 # reference BenchmarkBase times transform separately (benchmark/base.py:221-271):

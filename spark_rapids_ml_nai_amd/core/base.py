@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import os
 import threading
+import time
 from abc import abstractmethod
 from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, Iterator, List, Optional, Sequence, Tuple, Union
@@ -27,7 +28,8 @@ from typing import Any, Callable, Dict, Iterator, List, Optional, Sequence, Tupl
 import numpy as np
 import torch
 
-from ..parallel.context import PartitionDescriptor, WorkerContext, current_context, spmd_active, use_context
+from ..parallel.context import (PartitionDescriptor, WorkerContext, current_context, spmd_active, spmd_context,
+                                use_context)
 from ..utils.log import get_logger
 from ..utils.timer import PhaseTimer
 import pyarrow as pa
@@ -336,6 +338,7 @@ class _Estimator(_CommonBase, *_ESTIMATOR_BASES):  # type: ignore[misc]
                 est_i._copyValues(model)
                 est_i._copy_backend_params(model)
             model._fit_timings = dict(timer.times)
+            model._rank_stats = getattr(timer, "rank_stats", None)
             models.append(model)
         return models
 
@@ -355,6 +358,8 @@ class _EstimatorSupervised(_Estimator):
 def _fit_worker(ctx: WorkerContext, payload: Tuple[HostPartition, Callable, Dict[str, Any], bool]) -> Any:
     """Body of one barrier task: ingest to device, describe partitions, run the fit closure."""
     hp, fit_fn, params, float32 = payload
+    t_start = time.perf_counter()
+    ctx.comm.stats.reset()
     _maybe_inject_fault(ctx, "ingest")
     if hp.rows == 0:
         raise RuntimeError("A worker received no data. Please increase amount of data or use fewer workers.")
@@ -374,15 +379,22 @@ def _fit_worker(ctx: WorkerContext, payload: Tuple[HostPartition, Callable, Dict
         X = streamed.X
     else:
         X = to_device(hp.X, ctx.device, dtype) if hp.X is not None else None
+    h2d_host_s = time.perf_counter() - t_start  # blocking ingest paths (the streamed ones are timed on device)
     y = to_device(hp.y, ctx.device) if hp.y is not None else None
     desc = PartitionDescriptor.build(ctx, hp.rows, hp.n_cols)
     inp = FitInput(X=X, y=y, cols=hp.cols, desc=desc, host=hp, stream=streamed)
     _maybe_inject_fault(ctx, "fit")
     with ctx.comm.watchdog(what="fit"):  # SRML_COMM_TIMEOUT: abort the communicator on a stuck collective
         out = fit_fn(inp, ctx, params)
+        ctx.comm.check()  # asynchronous collectives (one-shot) all succeeded, else CommError
     if ctx.is_gpu and os.environ.get("SRML_FIT_DEVICE_SYNC", "1") == "1":
         # leave the device idle (copy stream included) before the task returns
         torch.cuda.synchronize(ctx.device)
+    wall = time.perf_counter() - t_start
+    h2d = streamed.h2d_seconds() if streamed is not None else h2d_host_s
+    st = ctx.comm.stats.snapshot()
+    ctx.timers["rank"] = dict(rank=ctx.rank, wall_s=round(wall, 6), h2d_s=round(h2d, 6),
+                              compute_s=round(max(0.0, wall - st["comm_s"]), 6), **st)
     return out
 
 
@@ -411,20 +423,15 @@ def run_fit_job(est: _Estimator, df: DataFrame, fit_fn: Callable, params: Dict[s
     """Dispatch the worker closure to SPMD / in-process / LocalBarrierRunner (or Spark)."""
     timer = timer or PhaseTimer()
     float32 = est._float32_inputs
-    if spmd_active():
-        ctx = current_context() or WorkerContext.from_process_group()
+    if spmd_active() or est.num_workers <= 1:
+        ctx = current_context() or (spmd_context() if spmd_active() else WorkerContext.single())
         with timer.phase("ingest"):
             hp = est._host_partition(df)
         with use_context(ctx), timer.phase("fit"):
             res = _fit_worker(ctx, (hp, fit_fn, params, float32))
+        timer.rank_stats = ctx.timers.get("rank")
         return res
     nw = est.num_workers
-    if nw <= 1:
-        ctx = current_context() or WorkerContext.single()
-        with timer.phase("ingest"):
-            hp = est._host_partition(df)
-        with use_context(ctx), timer.phase("fit"):
-            return _fit_worker(ctx, (hp, fit_fn, params, float32))
     from ..parallel.launcher import run_barrier_job
 
     with timer.phase("ingest"):
@@ -444,7 +451,7 @@ def run_worker_job(fn: Callable[[WorkerContext, Any], Any], payloads: Sequence[A
     LocalBarrierRunner stage (one process per GPU).
     """
     if spmd_active():
-        ctx = current_context() or WorkerContext.from_process_group()
+        ctx = current_context() or spmd_context()
         with use_context(ctx):
             return [fn(ctx, payloads[0])]
     if len(payloads) <= 1:

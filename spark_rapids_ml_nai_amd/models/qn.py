@@ -330,6 +330,11 @@ class DeviceQN:
 
 
 # ------------------------------------------------------------------------------------------
+def _comm_poll(allreduce: Optional[Callable]) -> Optional[Callable[[], None]]:
+    """The non-blocking error poll of the communicator behind a bound ``allreduce`` (if any)."""
+    return getattr(getattr(allreduce, "__self__", None), "poll", None)
+
+
 def minimize(P: QNProblem, theta0: np.ndarray, evaluate: Callable[[torch.Tensor, torch.Tensor, Optional[torch.Tensor],
                                                                    torch.Tensor], None],
              allreduce: Optional[Callable[[torch.Tensor], None]], device: torch.device,
@@ -355,6 +360,7 @@ def minimize(P: QNProblem, theta0: np.ndarray, evaluate: Callable[[torch.Tensor,
         return {"theta": st.theta(), "f": st.f, "iter": st.iter, "n_evals": st.n_evals,
                 "status": STATUS[st.status if st.done else 3]}
     q = DeviceQN(P, theta0, device)
+    poll = _comm_poll(allreduce)
     flag = q.flags[F_DONE: F_DONE + 1]
     host_flag = torch.zeros(2, dtype=torch.int32, pin_memory=True)
     events: list = []
@@ -375,6 +381,8 @@ def minimize(P: QNProblem, theta0: np.ndarray, evaluate: Callable[[torch.Tensor,
         ev.record(stream)
         events.append((ev, slot))
         j += 1
+        if poll is not None:
+            poll()  # a collective of an earlier batch lost a peer: raise instead of iterating on NaN
         if len(events) >= 2:
             ev0, s0 = events.pop(0)
             ev0.synchronize()
@@ -415,6 +423,7 @@ def minimize_batch(Ps: List[QNProblem], theta0s: List[np.ndarray],
     evals, j = 0, 0
     events: list = []
     stream = torch.cuda.current_stream(device)
+    poll = _comm_poll(allreduce)
     while evals < cap:
         for _ in range(batch):
             evaluate(WB, OUT)
@@ -428,6 +437,8 @@ def minimize_batch(Ps: List[QNProblem], theta0s: List[np.ndarray],
         ev.record(stream)
         events.append((ev, slot))
         j += 1
+        if poll is not None:
+            poll()
         if len(events) >= 2:
             ev0, s0 = events.pop(0)
             ev0.synchronize()

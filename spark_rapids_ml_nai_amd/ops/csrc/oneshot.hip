@@ -11,8 +11,9 @@
 // [slot 0: max_elems fp64][slot 1: max_elems fp64]. Epoch e (1, 2, ...) uses slot e & 1: when a
 // rank reaches epoch e every peer has raised flag >= e-1, i.e. has finished reading slot (e & 1)
 // of epoch e-2, so two slots make the reuse safe without a second barrier.
-// Spins are bounded: a peer that does not arrive within `timeout_cycles` sets *err and the kernel
-// exits (the host raises); no wave waits forever.
+// Spins are bounded: a peer that does not arrive within `timeout_cycles` sets the sticky *err, the
+// output is poisoned with NaN and the kernel exits; later calls see *err, publish nothing (so the
+// peers time out too) and return NaN. The host polls *err (Communicator.poll/check) and raises.
 #include "common.h"
 
 #include <string.h>
@@ -29,7 +30,12 @@ __global__ __launch_bounds__(OS_T) void oneshot_allreduce_kernel(const T* __rest
                                                                  int* __restrict__ err) {
   __shared__ int s_fail;
   const int t = threadIdx.x;
-  if (t == 0) s_fail = 0;
+  if (t == 0) s_fail = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (s_fail) {  // sticky: a rank that already lost a peer publishes nothing and returns NaN
+    for (long i = t; i < n; i += OS_T) out[i] = (T)__builtin_nan("");
+    return;
+  }
   double* mine = bufs[rank];
   const long slot = OS_HDR + (long)(epoch & 1ull) * max_elems;
   for (long i = t; i < n; i += OS_T) mine[slot + i] = (double)in[i];
@@ -51,7 +57,8 @@ __global__ __launch_bounds__(OS_T) void oneshot_allreduce_kernel(const T* __rest
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   }
   __syncthreads();
-  if (s_fail) {
+  if (s_fail) {  // never leave the local partial in `out`: poison it, flag the error
+    for (long i = t; i < n; i += OS_T) out[i] = (T)__builtin_nan("");
     if (t == 0) atomicExch(err, 1);
     return;
   }

@@ -219,8 +219,23 @@ class StreamedParts:
         self._copy = copy_stream(device)
         self._copy.wait_stream(cur)
         self.X.record_stream(self._copy)
+        self._t0 = torch.cuda.Event(enable_timing=True)
+        self._t1: Optional[Any] = None
+        self._t0.record(self._copy)
         self._gen = _staged_fill(blocks, self.X, device, self._copy)
         self._last = None
+
+    def _finished(self) -> None:
+        if self._t1 is None:
+            self._t1 = torch.cuda.Event(enable_timing=True)
+            self._t1.record(self._copy)
+
+    def h2d_seconds(self) -> float:
+        """Copy-stream span of the transfer (host fill of the staging ring included)."""
+        self.wait_all()
+        assert self._t1 is not None
+        self._t1.synchronize()
+        return self._t0.elapsed_time(self._t1) / 1e3
 
     def chunks(self) -> Iterator[Any]:
         cur = torch.cuda.current_stream(self.device)
@@ -228,10 +243,12 @@ class StreamedParts:
             self._last = ev
             cur.wait_event(ev)
             yield r0, r1, self.X[r0:r1]
+        self._finished()
 
     def wait_all(self) -> torch.Tensor:
         for _, _, ev in self._gen:
             self._last = ev
+        self._finished()
         if self._last is not None:
             torch.cuda.current_stream(self.device).wait_event(self._last)
         return self.X
@@ -322,7 +339,10 @@ class StreamedRows:
         self.X.record_stream(self._copy)
         self.bounds = []
         self.events = []
+        self._t0 = torch.cuda.Event(enable_timing=True)
+        self._t1 = torch.cuda.Event(enable_timing=True)
         with torch.cuda.stream(self._copy):
+            self._t0.record(self._copy)
             for r0 in range(0, m, self.chunk_rows):
                 r1 = min(m, r0 + self.chunk_rows)
                 self.X[r0:r1].copy_(t[r0:r1], non_blocking=True)
@@ -330,6 +350,12 @@ class StreamedRows:
                 ev.record(self._copy)
                 self.bounds.append((r0, r1))
                 self.events.append(ev)
+            self._t1.record(self._copy)
+
+    def h2d_seconds(self) -> float:
+        """Copy-stream time of the whole transfer (synchronises on its end)."""
+        self._t1.synchronize()
+        return self._t0.elapsed_time(self._t1) / 1e3
 
     def chunks(self) -> Iterator[Any]:
         cur = torch.cuda.current_stream(self.device)

@@ -16,6 +16,12 @@ Every numeric exchange here is a device collective on the compute stream:
 
 A world of size 1 short-circuits every call (no process group needed).
 
+Accounting: every collective is counted (calls, payload bytes) and timed into ``Communicator.stats``
+(``CommStats``) — on RCCL by a pair of timing events on the compute stream around the call (so the
+time includes waiting for the slowest peer: the rank's comm-wait), on gloo by host wall time. The
+fit driver resets it per fit and reports it with the H2D and wall times as the per-rank breakdown
+(reference logs each worker stage, ``core.py:720-770``).
+
 Failure semantics (reference ``common/cuml_context.py:150-167``: ``nccl.destroy()`` on success,
 ``nccl.abort()`` on exception): ``abort()`` aborts the process group's communicators
 (``ncclCommAbort`` for RCCL — non-blocking, in-flight collectives on every rank error out) and only
@@ -33,6 +39,7 @@ import contextlib
 import os
 import pickle
 import threading
+import time
 from typing import Any, Iterator, List, Optional, Sequence
 
 import torch
@@ -55,6 +62,9 @@ class Communicator:
         self.group = group
         self._backend = dist.get_backend(group) if (size > 1 and dist.is_initialized()) else "none"
         self.aborted = False
+        self.stats = CommStats()
+        self._oneshot: Any = None
+        self._oneshot_failed = False
 
     # -- helpers --------------------------------------------------------------------
     @property
@@ -70,39 +80,80 @@ class Communicator:
         return t
 
     # -- collectives ----------------------------------------------------------------
+    def _timed(self, t: torch.Tensor) -> Any:
+        return self.stats.record(t.numel() * t.element_size(), self.device if self._backend == "nccl" else None)
+
     def _oneshot_for(self, t: torch.Tensor, op: str) -> Any:
-        """The peer-mapped one-shot path (``SRML_COMM=oneshot``) when it applies to this payload."""
+        """The peer-mapped one-shot path when it applies to this payload: ``SRML_COMM=oneshot``
+        always, ``auto`` when every rank of the group lives on this node (peer-mappable memory)."""
         if op != "sum" or not t.is_cuda or self._backend != "nccl" or not t.is_contiguous():
             return None
         if t.dtype not in (torch.float32, torch.float64):
             return None
         from . import oneshot
 
-        if oneshot.comm_mode() != "oneshot" or t.numel() * 8 > oneshot.MAX_BYTES:
+        mode = oneshot.comm_mode()
+        if mode not in ("oneshot", "auto") or t.numel() * 8 > oneshot.MAX_BYTES:
             return None
-        if getattr(self, "_oneshot", None) is None and not getattr(self, "_oneshot_failed", False):
-            try:
-                self._oneshot = oneshot.OneShotAllreduce(self, self.device)
-            except Exception as e:  # noqa: BLE001 - fall back to RCCL, loudly
-                import warnings
-
-                warnings.warn("one-shot all-reduce unavailable (%s); using RCCL" % e)
+        if self._oneshot is None and not self._oneshot_failed:
+            # every rank reaches this point for the same payload (all-reduce shapes agree), so the
+            # set-up collectives line up; the constructor agrees on success across ranks itself
+            if mode == "auto" and not oneshot.single_node(self):
                 self._oneshot_failed = True
-                self._oneshot = None
-        return getattr(self, "_oneshot", None)
+                return None
+            os_ = oneshot.OneShotAllreduce(self, self.device)
+            if os_.ok:
+                self._oneshot = os_
+            else:
+                if mode == "oneshot":
+                    import warnings
+
+                    warnings.warn("one-shot all-reduce unavailable (%s); using RCCL" % os_.reason)
+                self._oneshot_failed = True
+        return self._oneshot
 
     def allreduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
         """In-place all-reduce; returns ``t``."""
         if self.size == 1:
             return t
         os_ = self._oneshot_for(t, op)
-        if os_ is not None:
-            return os_.allreduce(t)
-        ct = self._comm_tensor(t)
-        dist.all_reduce(ct, op=_OPS[op], group=self.group)
-        if ct is not t:
-            t.copy_(ct)
+        with self._timed(t):
+            if os_ is not None:
+                return os_.allreduce(t)
+            ct = self._comm_tensor(t)
+            dist.all_reduce(ct, op=_OPS[op], group=self.group)
+            if ct is not t:
+                t.copy_(ct)
         return t
+
+    def poll(self) -> None:
+        """Non-blocking error check for the asynchronous device paths (one-shot all-reduce): raises
+        ``CommError`` (after aborting) if a call issued before the previous ``poll`` failed."""
+        if self._oneshot is not None and self._oneshot.poll():
+            self._fail_oneshot()
+
+    def check(self) -> None:
+        """Blocking error check before a fit's results are used: every rank's asynchronous collectives
+        (one-shot) succeeded AND every rank issued the same number of them, else abort and raise
+        ``CommError`` on every rank. A rank that made fewer calls than its peers cannot see the
+        peer's timeout by itself, so the verdict is agreed over the group's own backend (one tiny
+        MAX all-reduce of [error, calls, -calls]; only when the one-shot path is active)."""
+        if self._oneshot is None:
+            return
+        v = torch.tensor([1.0 if self._oneshot.failed() else 0.0, float(self._oneshot.epoch),
+                          -float(self._oneshot.epoch)], dtype=torch.float64, device=self.device)
+        ct = self._comm_tensor(v)
+        dist.all_reduce(ct, op=dist.ReduceOp.MAX, group=self.group)
+        err, hi, lo = (float(a) for a in ct.cpu().tolist())
+        if err > 0 or hi != -lo:
+            self._fail_oneshot()
+
+    def _fail_oneshot(self) -> None:
+        from . import oneshot
+
+        self.abort()
+        raise CommError("one-shot all-reduce on rank %d: a peer did not arrive within %.1f s; communicator "
+                        "aborted" % (self.rank, oneshot.TIMEOUT_S))
 
     def allreduce_coalesced(self, tensors: Sequence[torch.Tensor], op: str = "sum") -> List[torch.Tensor]:
         """Pack same-dtype tensors into one flat buffer -> one collective -> unpack (in place)."""
@@ -123,33 +174,27 @@ class Communicator:
         """Equal-shaped blocks -> concatenated along dim 0."""
         if self.size == 1:
             return t
-        ct = self._comm_tensor(t.contiguous())
-        out = [torch.empty_like(ct) for _ in range(self.size)]
-        dist.all_gather(out, ct, group=self.group)
-        res = torch.cat(out, 0)
+        with self._timed(t):
+            ct = self._comm_tensor(t.contiguous())
+            out = [torch.empty_like(ct) for _ in range(self.size)]
+            dist.all_gather(out, ct, group=self.group)
+            res = torch.cat(out, 0)
         return res.to(t.device) if res.device != t.device else res
 
     def allgatherv(self, t: torch.Tensor) -> List[torch.Tensor]:
-        """Ragged dim-0 blocks -> list of per-rank tensors (sizes exchanged first)."""
+        """Ragged dim-0 blocks -> list of per-rank tensors. One implementation for every backend:
+        the sizes are all-gathered, each block is padded to the largest and ONE equal-shaped
+        all-gather moves them (a single ring pass on RCCL instead of W per-root broadcasts; the
+        padding is bounded by the imbalance, which the row-balanced partitioning keeps small)."""
         if self.size == 1:
             return [t]
         n = torch.tensor([t.shape[0]], dtype=torch.int64, device=self.device)
         sizes = self.allgather(n).tolist()
         mx = max(sizes)
         tail = tuple(t.shape[1:])
-        if self._backend == "nccl" and min(sizes) != mx:
-            # RCCL: ragged blocks travel at their own size (ProcessGroupNCCL turns an uneven
-            # all_gather into one group of per-root broadcasts), no padding to the largest block
-            ct = self._comm_tensor(t.contiguous())
-            out = [torch.empty((s,) + tail, dtype=t.dtype, device=ct.device) for s in sizes]
-            try:
-                dist.all_gather(out, ct, group=self.group)
-                return out
-            except (RuntimeError, ValueError):  # a backend build without ragged all_gather: pad
-                pass
         pad = torch.zeros((mx,) + tail, dtype=t.dtype, device=t.device)
         pad[: t.shape[0]] = t
-        g = self.allgather(pad).view((self.size, mx) + tuple(t.shape[1:]))
+        g = self.allgather(pad).view((self.size, mx) + tail)
         return [g[r, : sizes[r]] for r in range(self.size)]
 
     def isendrecv(self, send: torch.Tensor, dst: int, recv: torch.Tensor, src: int) -> Any:
@@ -164,6 +209,8 @@ class Communicator:
         g = self.group
         gd = dist.get_global_rank(g, dst) if g is not None else dst
         gs = dist.get_global_rank(g, src) if g is not None else src
+        self.stats.calls += 1
+        self.stats.bytes += cs.numel() * cs.element_size()
         works = dist.batch_isend_irecv([dist.P2POp(dist.isend, cs, gd, group=g),
                                         dist.P2POp(dist.irecv, cr, gs, group=g)])
         return (works, cs, cr, recv)
@@ -172,8 +219,9 @@ class Communicator:
         if handle is None:
             return
         works, _cs, cr, recv = handle
-        for w in works:
-            w.wait()
+        with self.stats.record(0, self.device if self._backend == "nccl" else None, count=False):
+            for w in works:
+                w.wait()
         if cr is not recv:
             recv.copy_(cr)
 
@@ -184,10 +232,11 @@ class Communicator:
     def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if self.size == 1:
             return t
-        ct = self._comm_tensor(t)
-        dist.broadcast(ct, src=src, group=self.group)
-        if ct is not t:
-            t.copy_(ct)
+        with self._timed(t):
+            ct = self._comm_tensor(t)
+            dist.broadcast(ct, src=src, group=self.group)
+            if ct is not t:
+                t.copy_(ct)
         return t
 
     def barrier(self) -> None:
@@ -226,7 +275,7 @@ class Communicator:
     def abort(self) -> None:
         """Abort the communicators (``ncclCommAbort`` / gloo abort: pending collectives fail on
         every rank instead of waiting for a dead peer), then destroy the group."""
-        if self.size <= 1 or not dist.is_initialized():
+        if self.size <= 1 or not dist.is_initialized() or self.aborted:
             return
         self.aborted = True
         try:
@@ -286,8 +335,64 @@ def comm_timeout(default_s: float) -> float:
     return v if v > 0 else float(default_s)
 
 
-class CommTimeout(RuntimeError):
+class CommError(RuntimeError):
+    """A collective failed (a peer never arrived); the communicator was aborted."""
+
+
+class CommTimeout(CommError):
     """A watched block of collectives overran its deadline and the communicator was aborted."""
+
+
+def _rank_timers_enabled() -> bool:
+    return os.environ.get("SRML_RANK_TIMERS", "1") == "1"
+
+
+class CommStats:
+    """Per-rank collective accounting: calls, payload bytes and time spent in collectives.
+
+    Device collectives (RCCL) are timed by a pair of timing events on the current stream around
+    the call: the span is how long the compute stream stood at that collective, i.e. the transfer
+    plus the wait for the slowest peer. Host-blocking ones (gloo) add their wall time. ``seconds()``
+    resolves the events (it synchronises on the last one), so call it after the fit."""
+
+    def __init__(self) -> None:
+        self.reset()
+
+    def reset(self) -> None:
+        self.calls = 0
+        self.bytes = 0
+        self.host_s = 0.0
+        self._pairs: List[Any] = []
+
+    @contextlib.contextmanager
+    def record(self, nbytes: int, device: Optional[torch.device], count: bool = True) -> Iterator[None]:
+        if count:
+            self.calls += 1
+            self.bytes += int(nbytes)
+        if device is not None and device.type == "cuda" and _rank_timers_enabled():
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            try:
+                yield
+            finally:
+                e.record()
+                self._pairs.append((s, e))
+            return
+        t0 = time.perf_counter()
+        try:
+            yield
+        finally:
+            self.host_s += time.perf_counter() - t0
+
+    def seconds(self) -> float:
+        dev = 0.0
+        if self._pairs:
+            self._pairs[-1][1].synchronize()
+            dev = sum(s.elapsed_time(e) for s, e in self._pairs) / 1e3
+        return self.host_s + dev
+
+    def snapshot(self) -> dict:
+        return {"comm_s": round(self.seconds(), 6), "comm_calls": self.calls, "comm_bytes": self.bytes}
 
 
 def pickle_obj(o: Any) -> bytes:

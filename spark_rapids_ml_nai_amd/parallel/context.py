@@ -143,6 +143,21 @@ class WorkerContext:
         return WorkerContext(rank, size, dev, Communicator(rank, size, dev), partition_id=rank)
 
 
+_SPMD: List[Any] = []  # [(world group, WorkerContext)] of the live process group
+
+
+def spmd_context() -> WorkerContext:
+    """The rank's context in an SPMD job (torchrun / Spark barrier group), built once per process
+    group: every fit of the job reuses one Communicator, so its lazily mapped one-shot buffers and
+    its accounting persist instead of being re-created per fit."""
+    grp = dist.group.WORLD
+    if _SPMD and _SPMD[0][0] is grp and not _SPMD[0][1].comm.aborted:
+        return _SPMD[0][1]
+    ctx = WorkerContext.from_process_group()
+    _SPMD[:] = [(grp, ctx)]
+    return ctx
+
+
 def current_context() -> Optional[WorkerContext]:
     return getattr(_tls, "ctx", None)
 

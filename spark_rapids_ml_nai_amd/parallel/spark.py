@@ -199,6 +199,8 @@ def spark_worker_entry(task_ctx: Any, batches: Iterable[Any], payload: bytes) ->
     est, fit_fn, params, float32, vector_cols, use_gpu, *rest = cloudpickle.loads(payload)
     if rest and rest[0]:
         os.environ["SRML_UVM"] = "1"  # spark.rocm.ml.uvm.enabled: managed-memory ingest
+    if len(rest) > 1 and rest[1]:
+        os.environ["SRML_COMM"] = rest[1]  # spark.rocm.ml.comm: rccl | oneshot | auto
     ctx = init_barrier_group(task_ctx, use_gpu)
     try:
         table = batches_to_table(batches, vector_cols)
@@ -247,7 +249,7 @@ def run_spark_fit(est: Any, sdf: Any, fit_fn: Callable, params: Dict[str, Any]) 
     sdf, vec = _unwrap_vectors(sdf)
     use_gpu = os.environ.get("SRML_FORCE_CPU", "0") != "1" and (gpu_available() or _cluster_has_gpus(spark))
     uvm = str(spark.conf.get("spark.rocm.ml.uvm.enabled", "false")).lower() == "true"
-    payload = cloudpickle.dumps((est, fit_fn, params, est._float32_inputs, vec, use_gpu, uvm))
+    payload = cloudpickle.dumps((est, fit_fn, params, est._float32_inputs, vec, use_gpu, uvm, spark_comm_mode(spark)))
 
     def _train(it: Iterator[Any]) -> Iterator[Any]:
         from pyspark import BarrierTaskContext  # type: ignore
@@ -258,6 +260,17 @@ def run_spark_fit(est: Any, sdf: Any, fit_fn: Callable, params: Dict[str, Any]) 
     rdd = _try_stage_level_scheduling(rdd, spark)
     rows = rdd.collect()
     return cloudpickle.loads(rows[0]["result"])
+
+
+def spark_comm_mode(spark: Any) -> str:
+    """``spark.rocm.ml.comm`` (rccl | oneshot | auto; default: the driver's ``SRML_COMM`` or rccl),
+    validated on the driver so a typo fails before any barrier task starts."""
+    from .oneshot import MODES
+
+    mode = str(spark.conf.get("spark.rocm.ml.comm", os.environ.get("SRML_COMM", "rccl"))).lower()
+    if mode not in MODES:
+        raise ValueError("spark.rocm.ml.comm must be one of %s, got %r" % (MODES, mode))
+    return mode
 
 
 def _cluster_has_gpus(spark: Any) -> bool:

@@ -48,6 +48,7 @@ class PhaseTimer:
     def __init__(self, sync_device: Optional[object] = None) -> None:
         self.times: Dict[str, float] = {}
         self.sync_device = sync_device
+        self.rank_stats: Optional[dict] = None  # this rank's wall / H2D / compute / comm split of the fit
 
     @contextmanager
     def phase(self, name: str) -> Iterator[None]:

@@ -27,11 +27,13 @@ def _free_port() -> int:
 def _run(n: int, out_dir: str) -> dict:
     env = dict(os.environ, SRML_FORCE_CPU="1", OMP_NUM_THREADS="1", PYTHONPATH=ROOT,
                SRML_NUM_WORKERS=str(n))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--rows", str(ROWS), "--cols", str(COLS),
            "--steps", "1", "--warmup", "0", "--global-data", "--dump-models", out_dir]
-    if n == 1:
+    if n <= 2:  # n == 2: bench.py spawns its own ranks when no launcher is present
         cmd = [sys.executable, os.path.join(ROOT, "bench.py")] + cmd[cmd.index("--gpus"):]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=1500, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-4000:]
@@ -110,3 +112,20 @@ def test_json_contract_multi_rank(runs):
         assert line["n_gpus"] == n and line["steps"] == 1 and line["warmup"] == 0
         assert line["config"]["parallelism"] == f"dp{n}"
         assert line["value"] > 0 and line["ms_per_step"] > 0
+
+
+def test_per_rank_breakdown(runs):
+    """Every workload reports each rank's wall / H2D / compute / comm-wait split of its last fit."""
+    for n, (line, _) in runs.items():
+        for name, w in line["config"]["workloads"].items():
+            pr = w["per_rank"]
+            assert [p["rank"] for p in pr] == list(range(n)), (n, name)
+            for p in pr:
+                assert p["wall_s"] > 0 and 0 <= p["compute_s"] <= p["wall_s"] + 1e-9
+                assert p["h2d_s"] >= 0 and p["comm_s"] >= 0
+                assert (p["comm_calls"] > 0) == (n > 1), (n, name, p)
+            if n == 8:
+                print("\n[%s n=%d] " % (name, n) + " | ".join(
+                    "r%d wall %.3f h2d %.3f comm %.3f (%d calls, %d B)" % (
+                        p["rank"], p["wall_s"], p["h2d_s"], p["comm_s"], p["comm_calls"], p["comm_bytes"])
+                    for p in pr))
