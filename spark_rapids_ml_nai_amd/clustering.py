@@ -296,6 +296,32 @@ def _dbscan_worker(ctx: WorkerContext, payload: Tuple[Any, ...]) -> Tuple[np.nda
     return dbscan_fit_predict(Xd, ctx, eps, min_samples, metric)
 
 
+def _spark_dbscan_task(ctx: WorkerContext, table: Any, extra: Tuple[Any, ...]) -> Any:
+    """One rank of the Spark DBSCAN barrier job: this rank's rows are clustered together with every
+    other rank's (device-gathered over RCCL, ``models/dbscan.py``) and it emits (id, label) for its
+    own rows. Replaces the reference's driver ``toPandas`` + <= 8 GiB broadcasts of the whole
+    dataset (``clustering.py:1013-1069``)."""
+    import pyarrow as pa
+
+    from .core.base import _dense_from_df
+    from .core.dataframe import DataFrame as _DF
+
+    col, cols, id_col, pred_col, eps, min_samples, metric = extra
+    if table is not None and table.num_rows:
+        part = _DF([table])
+        X = _dense_from_df(part, col, cols, np.float32)
+        ids = np.asarray(part.to_numpy(id_col)).astype(np.int64)
+    else:
+        X, ids = None, np.zeros(0, np.int64)
+    nt = torch.tensor([float(X.shape[1] if X is not None else 0)], dtype=torch.float64, device=ctx.device)
+    ctx.comm.allreduce(nt, op="max")  # an empty rank still joins every collective
+    if X is None:
+        X = np.zeros((0, int(nt.item())), np.float32)
+    labels, _core = _dbscan_worker(ctx, (X, eps, min_samples, metric))
+    yield pa.RecordBatch.from_arrays([pa.array(ids), pa.array(np.asarray(labels).astype(np.int32))],
+                                     names=[id_col, pred_col])
+
+
 class DBSCAN(DBSCANClass, _Estimator, _DBSCANParams):
     """Density-based clustering. Like the reference, ``fit`` does no work: it returns a
     ``DBSCANModel`` whose ``transform`` clusters the dataset it is given (``clustering.py:820-833``).
@@ -345,6 +371,32 @@ class DBSCANModel(DBSCANClass, _ModelWithPredictionCol, _DBSCANParams):
 
     def _get_transform_func(self, dataset: DataFrame) -> Tuple[Callable, Callable]:
         raise NotImplementedError("DBSCANModel clusters the whole dataset in transform()")
+
+    def _transform(self, dataset: Any) -> Any:
+        from .parallel.spark import is_spark_dataframe
+
+        if is_spark_dataframe(dataset):
+            return self._spark_transform(dataset)
+        return super()._transform(dataset)
+
+    def _spark_transform(self, sdf: Any) -> Any:
+        """Spark DataFrame: an id column is ensured, ONE barrier job labels every row and the labels
+        are joined back on the id (reference ``clustering.py:1013-1091``; output keeps the id)."""
+        from pyspark.sql.types import IntegerType, LongType, StructField, StructType  # type: ignore
+
+        from .parallel.spark import spark_barrier_job
+
+        df_withid = self._ensureIdCol(sdf)
+        id_col = self.getIdCol()
+        fc = self.getFeaturesCol()
+        col, cols = (fc, None) if isinstance(fc, str) else (None, list(fc))
+        sel = ([col] if col else list(cols)) + [id_col]
+        job_in = df_withid.select(*sel).repartition(max(1, self.num_workers))
+        pred = self.getPredictionCol()
+        schema = StructType([StructField(id_col, LongType()), StructField(pred, IntegerType())])
+        labels = spark_barrier_job(job_in, _spark_dbscan_task, (col, cols, id_col, pred, self.getEps(),
+                                                                self.getMinSamples(), self.getMetric()), schema)
+        return df_withid.join(labels, on=id_col)
 
     def _features_all(self, df: DataFrame) -> np.ndarray:
         from .core.base import _dense_from_df

@@ -378,8 +378,13 @@ def _fit_worker(ctx: WorkerContext, payload: Tuple[HostPartition, Callable, Dict
         streamed = StreamedParts(hp.X, ctx.device, dtype)  # Spark batches: fill/DMA/compute pipelined
         X = streamed.X
     else:
+        h2d_ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)] if ctx.is_gpu else None
+        if h2d_ev:
+            h2d_ev[0].record()
         X = to_device(hp.X, ctx.device, dtype) if hp.X is not None else None
-    h2d_host_s = time.perf_counter() - t_start  # blocking ingest paths (the streamed ones are timed on device)
+        if h2d_ev:
+            h2d_ev[1].record()  # pinned sources are queued asynchronously: time them on the stream
+    h2d_host_s = time.perf_counter() - t_start
     y = to_device(hp.y, ctx.device) if hp.y is not None else None
     desc = PartitionDescriptor.build(ctx, hp.rows, hp.n_cols)
     inp = FitInput(X=X, y=y, cols=hp.cols, desc=desc, host=hp, stream=streamed)
@@ -391,7 +396,13 @@ def _fit_worker(ctx: WorkerContext, payload: Tuple[HostPartition, Callable, Dict
         # leave the device idle (copy stream included) before the task returns
         torch.cuda.synchronize(ctx.device)
     wall = time.perf_counter() - t_start
-    h2d = streamed.h2d_seconds() if streamed is not None else h2d_host_s
+    if streamed is not None:
+        h2d = streamed.h2d_seconds()
+    elif ctx.is_gpu and h2d_ev:
+        h2d_ev[1].synchronize()
+        h2d = max(h2d_host_s, h2d_ev[0].elapsed_time(h2d_ev[1]) / 1e3)
+    else:
+        h2d = h2d_host_s
     st = ctx.comm.stats.snapshot()
     ctx.timers["rank"] = dict(rank=ctx.rank, wall_s=round(wall, 6), h2d_s=round(h2d, 6),
                               compute_s=round(max(0.0, wall - st["comm_s"]), 6), **st)
@@ -563,6 +574,11 @@ class _Model(_CommonBase, *_MODEL_BASES):  # type: ignore[misc]
     def _vector_output_cols(self) -> List[str]:
         return []
 
+    def _spark_vector_output_cols(self, input_is_vector: bool) -> List[str]:
+        """Output columns a Spark transform returns as VectorUDT (reference ``core.py:1559-1610``:
+        probability / rawPrediction always; array outputs mirror a vector input column)."""
+        return [c for c in self._vector_output_cols() if c]
+
     def _spark_output_fields(self, sdf: Any) -> List[Any]:
         """Spark schema of the columns ``transform`` appends (prediction double, array outputs)."""
         from pyspark.sql.types import ArrayType, DoubleType, StructField  # type: ignore
@@ -630,49 +646,42 @@ class _Model(_CommonBase, *_MODEL_BASES):  # type: ignore[misc]
     # ---- evaluation in the transform pass (CrossValidator fast path) ----------------------
     def _transformEvaluate(self, dataset: Any, evaluator: Any, num_models: int = 1, params: Any = None) -> List[float]:
         """Transform + evaluate every combined model in ONE pass over ``dataset`` (reference
-        ``core.py:1318-1468``): each partition's features are moved to the device once and all
-        models predict from that copy; the evaluator then scores each model's predictions."""
+        ``core.py:1318-1468``). Each partition's features are moved to the device once, all models
+        predict from that copy, and the partition emits only mergeable sufficient statistics per
+        model (``metrics.ClassificationSummary`` — per-class tp / fp / label counts + log-loss
+        sum — or ``RegressionSummary`` — moments of [label, label - prediction, prediction]); the
+        predictions themselves never leave the worker. Partitions run where the data lives: Spark
+        tasks (``mapInArrow``), the ranks of an SPMD job (summaries all-gathered, every rank gets
+        the metrics) or LocalBarrierRunner workers; the driver merges the records (Chan merges)
+        and applies Spark's formulas."""
         models = getattr(self, "_combined_models", None) or [self]
         if params:
             models = [m.copy(params) for m in models]
-        df, _ = as_dataframe(dataset)
+        info = _eval_info(evaluator)
         label_col = evaluator.getLabelCol()
-        if label_col not in df.columns:
-            raise RuntimeError("Label column is not existing.")
-        ctx = current_context() or WorkerContext.single(self._device())
-        fns = [m._get_transform_func(df) for m in models]
-        states = [c(ctx) for c, _ in fns]
-        outs: List[Dict[str, List[np.ndarray]]] = [dict() for _ in models]
-        dt = torch.float32 if self._transform_dtype() == np.float32 else torch.float64
-        for p in df.partitions:
-            if p.num_rows == 0:
-                continue
-            X = self._transform_features(DataFrame([p]))
-            Xd = to_device(X, ctx.device, dt)
-            for i, ((_, predict), st) in enumerate(zip(fns, states)):
-                for k, v in predict(st, Xd, ctx).items():
-                    outs[i].setdefault(k, []).append(np.asarray(v))
-        label = df.to_numpy(label_col)
-        metrics = []
-        for m, o in zip(models, outs):
-            cols: Dict[str, Any] = {label_col: label}
-            for k, parts in o.items():
-                cols[k] = np.concatenate(parts) if parts else np.zeros(0)
-            ev = evaluator.copy()
-            pc = m.getOrDefault("predictionCol") if m.hasParam("predictionCol") else "prediction"
-            if ev.hasParam("predictionCol") and pc in cols:
-                ev._set(predictionCol=pc)
-            for pname in ("probabilityCol", "rawPredictionCol"):
-                if ev.hasParam(pname) and m.hasParam(pname) and m.getOrDefault(pname) in cols:
-                    ev._set(**{pname: m.getOrDefault(pname)})
-            import pyarrow as pa
+        from ..parallel.spark import is_spark_dataframe
 
-            from .dataframe import dense_to_list_array
-
-            edf = DataFrame([pa.table({k: dense_to_list_array(v) if v.ndim == 2 else pa.array(v)
-                                       for k, v in cols.items()})])
-            metrics.append(float(ev.evaluate(edf)))
-        return metrics
+        if is_spark_dataframe(dataset):
+            if label_col not in dataset.columns:
+                raise RuntimeError("Label column is not existing.")
+            partials = _spark_eval_partials(models, dataset, label_col, info)
+        else:
+            df, _ = as_dataframe(dataset)
+            if label_col not in df.columns:
+                raise RuntimeError("Label column is not existing.")
+            if spmd_active():
+                ctx = current_context() or spmd_context()
+                mine = _eval_worker(ctx, (models, df.partitions, label_col, info))
+                partials = [p for r in ctx.comm.allgather_object(mine) for p in r]
+            elif self.num_workers > 1 and df.getNumPartitions() > 1:
+                nw = min(self.num_workers, df.getNumPartitions())
+                parts = df.repartition(nw).partitions if df.getNumPartitions() != nw else df.partitions
+                res = run_worker_job(_eval_worker, [(models, [p], label_col, info) for p in parts])
+                partials = [p for r in res for p in r]
+            else:
+                ctx = current_context() or WorkerContext.single(self._device())
+                partials = _eval_worker(ctx, (models, df.partitions, label_col, info))
+        return [_metric_from_partials([p[i] for p in partials], info, evaluator) for i in range(len(models))]
 
     @classmethod
     def _combine(cls, models: List["_Model"]) -> "_Model":
@@ -700,3 +709,80 @@ def _have_pyspark() -> bool:
         return True
     except Exception:  # noqa: BLE001
         return False
+
+
+# --------------------------------------------------------------------------------------
+# single-pass transform-evaluate helpers
+# --------------------------------------------------------------------------------------
+def _eval_info(evaluator: Any) -> Tuple[str, bool, float]:
+    """(kind, needs probabilities, eps) of a supported evaluator (pyspark's or ours)."""
+    name = type(evaluator).__name__
+    if name == "RegressionEvaluator":
+        return "regression", False, 0.0
+    if name == "MulticlassClassificationEvaluator":
+        logloss = evaluator.getMetricName() == "logLoss"
+        eps = float(evaluator.getOrDefault("eps")) if evaluator.hasParam("eps") else 1e-15
+        return "classification", logloss, eps
+    raise ValueError("transform-evaluate does not support %s" % name)
+
+
+def _eval_worker(ctx: WorkerContext, payload: Tuple[Any, ...]) -> List[List[Any]]:
+    """Per-partition summaries of every model: [[summary of model i] for each non-empty partition]."""
+    from ..metrics import ClassificationSummary, RegressionSummary
+
+    models, tables, label_col, (kind, need_prob, eps) = payload
+    fns = [m._get_transform_func(None) for m in models]
+    states = [c(ctx) for c, _ in fns]
+    dt = torch.float32 if models[0]._transform_dtype() == np.float32 else torch.float64
+    out = []
+    for t in tables:
+        if t is None or t.num_rows == 0:
+            continue
+        part = DataFrame([t])
+        Xd = to_device(models[0]._transform_features(part), ctx.device, dt)
+        y = part.to_numpy(label_col, np.float64)
+        row = []
+        for m, (_, predict), st in zip(models, fns, states):
+            res = predict(st, Xd, ctx)
+            p = np.asarray(res[m.getOrDefault("predictionCol")], np.float64)
+            if kind == "regression":
+                row.append(RegressionSummary.from_arrays(y, p))
+            else:
+                prob = np.asarray(res[m.getOrDefault("probabilityCol")]) if need_prob else None
+                row.append(ClassificationSummary.from_arrays(y, p, prob, eps))
+        out.append(row)
+    return out
+
+
+def _eval_task(ctx: WorkerContext, table: Any, extra: Tuple[Any, ...]) -> Iterator[Any]:
+    """Spark partition -> one row holding the pickled per-model summaries (nothing else leaves)."""
+    import cloudpickle
+
+    models, label_col, info = extra
+    rows = _eval_worker(ctx, (models, [table], label_col, info))
+    yield pa.RecordBatch.from_pydict({"result": pa.array([cloudpickle.dumps(rows)], type=pa.binary())})
+
+
+def _spark_eval_partials(models: List[Any], sdf: Any, label_col: str, info: Tuple[str, bool, float]) -> List[Any]:
+    import cloudpickle
+
+    from ..parallel.spark import spark_map_partitions
+
+    col, cols = models[0]._transform_input_cols()
+    sel = ([col] if col else list(cols)) + [label_col]
+    out = spark_map_partitions(sdf.select(*sel), _eval_task, (models, label_col, info), "result binary")
+    return [p for r in out.collect() for p in cloudpickle.loads(r["result"])]
+
+
+def _metric_from_partials(parts: List[Any], info: Tuple[str, bool, float], evaluator: Any) -> float:
+    from ..metrics import ClassificationSummary, MulticlassMetrics, RegressionMetrics, RegressionSummary
+
+    if info[0] == "regression":
+        s = RegressionSummary()
+        for p in parts:
+            s = s.merge(p)
+        return float(RegressionMetrics(s).evaluate(evaluator))
+    c = ClassificationSummary()
+    for p in parts:
+        c = c.merge(p)
+    return float(MulticlassMetrics(c).evaluate(evaluator))

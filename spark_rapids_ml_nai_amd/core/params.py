@@ -164,13 +164,21 @@ class HasIDCol(Params):
         return self.getOrDefault("idCol")
 
     def _ensureIdCol(self, df: Any) -> Any:
-        """Add a monotonically increasing id column unless the user set one that exists."""
+        """Add a monotonically increasing id column unless the user set one that exists (a Spark
+        DataFrame gets ``monotonically_increasing_id()``, reference ``params.py:107-128``)."""
+        def add(d: Any) -> Any:
+            if hasattr(d, "with_row_id"):
+                return d.with_row_id(self.getIdCol())
+            from pyspark.sql import functions as F  # type: ignore
+
+            return d.withColumn(self.getIdCol(), F.monotonically_increasing_id())
+
         if not self.isSet("idCol"):
             while self.getIdCol() in df.columns:
                 self._set(**{"idCol": self.getIdCol() + "_dedup"})
-            return df.with_row_id(self.getIdCol())
+            return add(df)
         if self.getIdCol() not in df.columns:
-            return df.with_row_id(self.getIdCol())
+            return add(df)
         return df
 
 

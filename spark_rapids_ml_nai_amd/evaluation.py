@@ -19,6 +19,19 @@ from .metrics import ClassificationSummary, MulticlassMetrics, RegressionMetrics
     binary_auc
 
 
+def _local(dataset: Any, cols: list) -> DataFrame:
+    """The evaluated columns as a local DataFrame; a Spark DataFrame is reduced to those columns
+    and brought to the driver through Arrow (``toArrow`` on Spark 4, ``toPandas`` before)."""
+    from .parallel.spark import is_spark_dataframe
+
+    if is_spark_dataframe(dataset):
+        sel = dataset.select(*[c for c in cols if c in dataset.columns])
+        if hasattr(sel, "toArrow"):
+            return DataFrame([sel.toArrow()])
+        return as_dataframe(sel.toPandas())[0]
+    return as_dataframe(dataset)[0]
+
+
 class Evaluator(Params):
     def evaluate(self, dataset: Any, params: Optional[dict] = None) -> float:
         if params:
@@ -65,7 +78,7 @@ class RegressionEvaluator(Evaluator, HasLabelCol, HasPredictionCol):
         return self.getMetricName() in ("r2", "var")
 
     def _evaluate(self, dataset: Any) -> float:
-        df, _ = as_dataframe(dataset)
+        df = _local(dataset, [self.getOrDefault("labelCol"), self.getOrDefault("predictionCol")])
         y = df.to_numpy(self.getOrDefault("labelCol"), np.float64)
         p = df.to_numpy(self.getOrDefault("predictionCol"), np.float64)
         return RegressionMetrics(RegressionSummary.from_arrays(y, p)).evaluate(self)
@@ -103,7 +116,7 @@ class MulticlassClassificationEvaluator(Evaluator, HasLabelCol, HasPredictionCol
                                             "logLoss")
 
     def _evaluate(self, dataset: Any) -> float:
-        df, _ = as_dataframe(dataset)
+        df = _local(dataset, [self.getOrDefault(c) for c in ("labelCol", "predictionCol", "probabilityCol")])
         y = df.to_numpy(self.getOrDefault("labelCol"), np.float64)
         p = df.to_numpy(self.getOrDefault("predictionCol"), np.float64)
         prob = None
@@ -124,7 +137,7 @@ class BinaryClassificationEvaluator(Evaluator, HasLabelCol, HasRawPredictionCol)
         self._set(**{k: v for k, v in self._input_kwargs.items() if v is not None and k != "weightCol"})
 
     def _evaluate(self, dataset: Any) -> float:
-        df, _ = as_dataframe(dataset)
+        df = _local(dataset, [self.getOrDefault("labelCol"), self.getOrDefault("rawPredictionCol")])
         y = df.to_numpy(self.getOrDefault("labelCol"), np.float64)
         rc = self.getOrDefault("rawPredictionCol")
         raw = df.to_numpy(rc, np.float64)

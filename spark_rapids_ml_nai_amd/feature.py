@@ -152,6 +152,9 @@ class PCAModel(PCAClass, _Model, _PCAParams):
     def _vector_output_cols(self) -> List[str]:
         return []
 
+    def _spark_vector_output_cols(self, input_is_vector: bool) -> List[str]:
+        return [self.getOrDefault("outputCol")] if input_is_vector else []
+
     def _transform_df(self, df: DataFrame) -> DataFrame:
         out = super()._transform_df(df)
         col, _ = self._get_input_columns()

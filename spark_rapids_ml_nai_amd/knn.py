@@ -17,6 +17,10 @@ Distances: ``euclidean``/``l2`` are true L2 distances, ``sqeuclidean`` squared L
 Execution: items and queries are split over ``num_workers`` ranks; each rank all-gathers the
 queries over RCCL, searches its local items with the MFMA kernels and the partial top-k lists are
 merged on device (``models/knn.py``). Unlike the reference no item ids travel through a driver.
+On a Spark DataFrame the same rank code runs as ONE barrier job over the tagged item u query
+union for both classes (the reference's ANN instead broadcasts the queries to a non-barrier job
+and merges with a SQL ``groupBy``; here the IVF partial lists are merged on the device); the join
+methods use Spark SQL explode + joins on the ids.
 """
 from __future__ import annotations
 
@@ -87,6 +91,53 @@ def _ivf_worker(ctx: WorkerContext, payload: Tuple[Any, ...]) -> Tuple[np.ndarra
     npb = nprobe if nprobe else _default_nprobe(index.centroids.shape[0] if index is not None else 1)
     d, i = ivf_knn(index, Q, k, npb, ctx, metric)
     return query_ids, i, d
+
+
+_TAG = "__srml_is_query"
+_ITEM_KEY = "__srml_item_id"
+
+
+def _spark_knn_task(ctx: WorkerContext, table: Any, extra: Tuple[Any, ...]) -> Any:
+    """One rank of the Spark kNN barrier job over the item u query union (reference
+    ``knn.py:638-749``): split the partition by the query tag, search this rank's items for every
+    rank's queries (device ring over RCCL), emit (query id, indices, distances) for this rank's
+    queries. Item ids stay on the device: no id list travels through the driver."""
+    import torch
+
+    col, cols, id_col, qname, k, metric, ivf = extra
+    if table is not None and table.num_rows:
+        part = DataFrame([table])
+        tag = np.asarray(part.to_numpy(_TAG)).astype(bool)
+        ids = np.asarray(part.to_numpy(id_col)).astype(np.int64)
+        X = _dense_from_df(part, col, cols, np.float32)
+        items, item_ids, queries, query_ids = X[~tag], ids[~tag], X[tag], ids[tag]
+        n_local = X.shape[1]
+    else:
+        n_local = 0
+    nt = torch.tensor([float(n_local)], dtype=torch.float64, device=ctx.device)
+    ctx.comm.allreduce(nt, op="max")  # an empty rank still takes part in every collective
+    n = int(nt.item())
+    if n_local == 0:
+        items, queries = np.zeros((0, n), np.float32), np.zeros((0, n), np.float32)
+        item_ids, query_ids = np.zeros(0, np.int64), np.zeros(0, np.int64)
+    if ivf is None:
+        qid, ind, dist = _exact_worker(ctx, (items, item_ids, queries, query_ids, k, metric))
+    else:
+        qid, ind, dist = _ivf_worker(ctx, (items, item_ids, queries, query_ids, k, metric) + tuple(ivf) + (None,))
+    yield _knn_batch(qname, np.asarray(qid, np.int64), np.asarray(ind), np.asarray(dist))
+
+
+def _knn_batch(qname: str, qid: np.ndarray, ind: np.ndarray, dist: np.ndarray) -> Any:
+    """(query id, indices list<int64>, distances list<float>) record batch; neighbours padded with
+    -1 (k > number of items) are dropped from their row."""
+    m = qid.shape[0]
+    kk = ind.shape[1] if ind.ndim == 2 else 0
+    valid = ind >= 0 if m else np.zeros((0, kk), bool)
+    counts = valid.sum(1).astype(np.int32) if m else np.zeros(0, np.int32)
+    offsets = pa.array(np.concatenate([[0], np.cumsum(counts)]).astype(np.int32))
+    ind_a = pa.ListArray.from_arrays(offsets, pa.array(ind[valid].astype(np.int64) if m else np.zeros(0, np.int64)))
+    dist_a = pa.ListArray.from_arrays(offsets, pa.array(dist[valid].astype(np.float32) if m else np.zeros(0, np.float32)))
+    return pa.RecordBatch.from_arrays([pa.array(qid), ind_a, dist_a], names=[qname, "indices", "distances"])
 
 
 def _default_nlist(m: int) -> int:
@@ -191,9 +242,67 @@ class _NNModelBase(_NoPersistence, _NNParams):
     def _worker(self) -> Any:
         return _exact_worker
 
+    def _ivf_args(self) -> Optional[Tuple[Any, ...]]:
+        return None
+
+    def _feature_spec(self) -> Tuple[Optional[str], Optional[List[str]]]:
+        col, cols = self._get_input_columns()
+        if col is None and not cols:
+            col = "features"
+        return col, cols
+
+    def _spark_kneighbors(self, query_df: Any, sort_knn_df_by_query_id: bool) -> Tuple[Any, Any, Any]:
+        """Spark path: ONE barrier job over items u queries (tagged), like the reference
+        (``knn.py:558-624``); the result is a lazily computed Spark DataFrame."""
+        from pyspark.sql import functions as F  # type: ignore
+        from pyspark.sql.types import ArrayType, FloatType, LongType, StructField, StructType  # type: ignore
+
+        from .parallel.spark import spark_barrier_job
+
+        query_df_withid = self._ensureIdCol(query_df)
+        id_col = self._getIdColOrDefault()
+        col, cols = self._feature_spec()
+        sel = ([col] if col else list(cols)) + [id_col]
+        union = self._item_df_withid.select(*sel).withColumn(_TAG, F.lit(0)).union(
+            query_df_withid.select(*sel).withColumn(_TAG, F.lit(1)))
+        nw = max(1, self.num_workers)
+        union = union.repartition(nw)
+        qname = "query_%s" % id_col
+        schema = StructType([StructField(qname, LongType()), StructField("indices", ArrayType(LongType())),
+                             StructField("distances", ArrayType(FloatType()))])
+        k = self.getK()
+        if k < 1:
+            raise ValueError("k must be >= 1")
+        knn_df = spark_barrier_job(union, _spark_knn_task, (col, cols, id_col, qname, k, self._metric(),
+                                                            self._ivf_args()), schema)
+        if sort_knn_df_by_query_id:
+            knn_df = knn_df.sort(qname)
+        return self._item_df_withid, query_df_withid, knn_df
+
+    def _spark_join(self, query_df: Any, distCol: str) -> Any:
+        """Every (query, neighbour) pair as ``item_df`` / ``query_df`` structs + distance, with Spark
+        SQL explode + joins on the ids (reference ``knn.py:419-466``)."""
+        from pyspark.sql import functions as F  # type: ignore
+
+        id_col = self._getIdColOrDefault()
+        item_df, query_df_withid, knn_df = self._spark_kneighbors(query_df, False)
+        qname = "query_%s" % id_col
+        pairs = knn_df.select(F.col(qname), F.explode(F.arrays_zip("indices", "distances")).alias("__z"))
+        pairs = pairs.select(F.col(qname), F.col("__z.indices").alias(_ITEM_KEY), F.col("__z.distances").alias(distCol))
+        keep_id = self.isSet("idCol")
+        icols = [c for c in item_df.columns if keep_id or c != id_col]
+        qcols = [c for c in query_df_withid.columns if keep_id or c != id_col]
+        items = item_df.select(F.struct(*icols).alias("item_df"), F.col(id_col).alias(_ITEM_KEY))
+        queries = query_df_withid.select(F.struct(*qcols).alias("query_df"), F.col(id_col).alias(qname))
+        return pairs.join(items, on=_ITEM_KEY).join(queries, on=qname).select("item_df", "query_df", distCol)
+
     def kneighbors(self, query_df: Any, sort_knn_df_by_query_id: bool = True) -> Tuple[DataFrame, DataFrame, DataFrame]:
         """Return ``(item_df_withid, query_df_withid, knn_df)``; knn_df has one row per query:
         ``query_<idCol>``, ``indices`` (array of item ids) and ``distances`` (array<float>)."""
+        from .parallel.spark import is_spark_dataframe
+
+        if is_spark_dataframe(self._item_df_withid) or is_spark_dataframe(query_df):
+            return self._spark_kneighbors(query_df, sort_knn_df_by_query_id)
         query_df, _ = as_dataframe(query_df)
         query_df_withid = self._ensureIdCol(query_df)
         id_col = self._getIdColOrDefault()
@@ -233,6 +342,10 @@ class _NNModelBase(_NoPersistence, _NNParams):
         return self._item_df_withid, query_df_withid, knn_df
 
     def _nearest_neighbors_join(self, query_df: Any, distCol: str = "distCol") -> DataFrame:
+        from .parallel.spark import is_spark_dataframe
+
+        if is_spark_dataframe(self._item_df_withid) or is_spark_dataframe(query_df):
+            return self._spark_join(query_df, distCol)
         id_col = self._getIdColOrDefault()
         item_df, query_df_withid, knn_df = self.kneighbors(query_df, sort_knn_df_by_query_id=False)
         knn = knn_df._concat()
@@ -292,7 +405,9 @@ class NearestNeighbors(NearestNeighborsClass, _NoPersistence, _NNParams):
         return est._fit(dataset)
 
     def _fit(self, dataset: Any) -> "NearestNeighborsModel":
-        df, _ = as_dataframe(dataset)
+        from .parallel.spark import is_spark_dataframe
+
+        df = dataset if is_spark_dataframe(dataset) else as_dataframe(dataset)[0]
         item_df_withid = self._ensureIdCol(df)
         model = NearestNeighborsModel(item_df_withid)
         model._num_workers = self._num_workers
@@ -387,7 +502,9 @@ class ApproximateNearestNeighbors(ApproximateNearestNeighborsClass, _NoPersisten
 
     def _fit(self, dataset: Any) -> "ApproximateNearestNeighborsModel":
         self._validate()
-        df, _ = as_dataframe(dataset)
+        from .parallel.spark import is_spark_dataframe
+
+        df = dataset if is_spark_dataframe(dataset) else as_dataframe(dataset)[0]
         item_df_withid = self._ensureIdCol(df).coalesce(max(1, self.num_workers))
         model = ApproximateNearestNeighborsModel(item_df_withid)
         model._num_workers = self._num_workers
@@ -409,6 +526,11 @@ class ApproximateNearestNeighborsModel(ApproximateNearestNeighborsClass, _NNMode
 
     def _worker(self) -> Any:
         return _ivf_worker
+
+    def _ivf_args(self) -> Optional[Tuple[Any, ...]]:
+        ap = dict(self.getAlgoParams() or {})
+        return (self.getAlgorithm(), ap.get("nlist", ap.get("n_lists")), ap.get("nprobe", ap.get("n_probes")),
+                int(ap.get("seed", 1)))
 
     def _payload_extra(self) -> Tuple[Any, ...]:
         ap = dict(self.getAlgoParams() or {})

@@ -161,10 +161,11 @@ def init_barrier_group(task_ctx: Any, use_gpu: bool, timeout_s: float = 1800.0) 
     return WorkerContext.from_process_group(device)
 
 
-def batches_to_table(batches: Iterable[Any], vector_cols: List[str]) -> Any:
+def batches_to_table(batches: Iterable[Any], vector_cols: List[str], allow_empty: bool = False) -> Any:
     """Arrow ``RecordBatch``es (``mapInArrow``) — or pandas frames from older callers — of one
     partition -> ONE Arrow table without copying the column buffers (vector structs tagged as
-    VectorUDT so the ingest reads their values buffers directly)."""
+    VectorUDT so the ingest reads their values buffers directly). An empty partition raises like
+    the reference's fit UDF, or gives None with ``allow_empty``."""
     import pyarrow as pa
 
     from ..core.dataframe import vector_field
@@ -181,6 +182,8 @@ def batches_to_table(batches: Iterable[Any], vector_cols: List[str]) -> Any:
         nonempty = [b for b in rbs if b.num_rows > 0] or rbs[:1]
         tables.append(pa.Table.from_batches(nonempty))
     if not tables:
+        if allow_empty:
+            return None
         raise RuntimeError("A worker received no data. Please increase amount of data or use fewer workers.")
     t = pa.concat_tables(tables) if len(tables) > 1 else tables[0]
     fields = [vector_field(f.name) if f.name in vector_cols else f for f in t.schema]
@@ -216,6 +219,104 @@ def spark_worker_entry(task_ctx: Any, batches: Iterable[Any], payload: bytes) ->
     dist.destroy_process_group()
     if task_ctx.partitionId() == 0:
         yield pa.RecordBatch.from_pydict({"result": pa.array([cloudpickle.dumps(res)], type=pa.binary())})
+
+
+def barrier_job_entry(task_ctx: Any, batches: Iterable[Any], payload: bytes) -> Iterator[Any]:
+    """Body of one task of a generic barrier job (``spark_barrier_job``): bring up the rank's
+    communicator, run ``fn(ctx, table, extra)`` on the partition's Arrow table (None when the
+    partition is empty) and emit either its record batches or, for a collecting job, one row
+    with the pickled ``(rank, result)``."""
+    import pyarrow as pa
+
+    from .context import use_context
+
+    fn, extra, vector_cols, use_gpu, env, collect = cloudpickle.loads(payload)
+    os.environ.update(env)
+    ctx = init_barrier_group(task_ctx, use_gpu)
+    try:
+        table = batches_to_table(batches, vector_cols, allow_empty=True)
+        with use_context(ctx):
+            res = fn(ctx, table, extra)
+            if collect:
+                out = [pa.RecordBatch.from_pydict({"result": pa.array([cloudpickle.dumps((ctx.rank, res))],
+                                                                      type=pa.binary())})]
+            else:
+                out = list(res)
+        ctx.comm.barrier()
+    except BaseException:
+        ctx.comm.abort()
+        raise
+    import torch.distributed as dist
+
+    dist.destroy_process_group()
+    yield from out
+
+
+def _worker_env(spark: Any) -> Dict[str, str]:
+    """Driver-side settings every barrier task applies before it touches the device."""
+    env = {"SRML_COMM": spark_comm_mode(spark)}
+    if str(spark.conf.get("spark.rocm.ml.uvm.enabled", "false")).lower() == "true":
+        env["SRML_UVM"] = "1"
+    return env
+
+
+def spark_barrier_job(sdf: Any, fn: Callable, extra: Any, out_schema: Any = None) -> Any:
+    """Run ``fn(ctx, table, extra)`` in ONE barrier task per partition of ``sdf`` (one rank per GPU,
+    RCCL bootstrapped through ``allGather``) — the shape of the reference's kNN / DBSCAN / UMAP
+    jobs (``knn.py:558-624``, ``clustering.py:940-998``, ``umap.py:959-1077``).
+
+    ``out_schema`` None: every rank's return value is collected to the driver (list in rank order).
+    Otherwise ``fn`` yields Arrow record batches of that schema and the result is a DataFrame
+    (computed lazily by Spark, like any other; nothing is collected)."""
+    from .context import gpu_available
+
+    spark = sdf.sparkSession
+    sdf_u, vec = _unwrap_vectors(sdf)
+    use_gpu = os.environ.get("SRML_FORCE_CPU", "0") != "1" and (gpu_available() or _cluster_has_gpus(spark))
+    collect = out_schema is None
+    payload = cloudpickle.dumps((fn, extra, vec, use_gpu, _worker_env(spark), collect))
+
+    def _task(it: Iterator[Any]) -> Iterator[Any]:
+        from pyspark import BarrierTaskContext  # type: ignore
+
+        return barrier_job_entry(BarrierTaskContext.get(), it, payload)
+
+    schema = "result binary" if collect else out_schema
+    try:
+        out = sdf_u.mapInArrow(_task, schema=schema, barrier=True)  # Spark >= 3.5
+        rdd = None
+    except TypeError:  # older Spark: barrier RDD over the mapped frame
+        out = None
+        rdd = sdf_u.mapInArrow(_task, schema=schema).rdd.barrier().mapPartitions(lambda x: x)
+    if collect:
+        rows = out.collect() if out is not None else rdd.collect()
+        res = sorted((cloudpickle.loads(r["result"]) for r in rows), key=lambda t: t[0])
+        return [r for _, r in res]
+    return out if out is not None else spark.createDataFrame(rdd, out_schema)
+
+
+def spark_map_partitions(sdf: Any, fn: Callable, extra: Any, out_schema: Any) -> Any:
+    """Non-barrier per-partition job: ``fn(ctx, table, extra)`` yields record batches, on the task's
+    pinned device (reference ``_transform_evaluate_internal``, core.py:1318-1417)."""
+    sdf_u, vec = _unwrap_vectors(sdf)
+    blob = cloudpickle.dumps((fn, extra, vec))
+
+    def _run(it: Iterator[Any]) -> Iterator[Any]:
+        import torch
+
+        from pyspark import TaskContext  # type: ignore
+
+        from .context import WorkerContext, gpu_available, use_context
+
+        f, ex, vcols = cloudpickle.loads(blob)
+        tc = TaskContext.get()
+        dev = _task_device(tc, gpu_available()) if tc is not None else torch.device("cpu")
+        ctx = WorkerContext.single(dev)
+        table = batches_to_table(it, vcols, allow_empty=True)
+        with use_context(ctx):
+            yield from f(ctx, table, ex)
+
+    return sdf_u.mapInArrow(_run, schema=out_schema)
 
 
 # ------------------------------------------------------------------------------------------
@@ -287,9 +388,13 @@ def spark_transform(model: Any, sdf: Any) -> Any:
 
     from ..core.dataframe import DataFrame, dense_to_list_array
 
+    out_fields = model._spark_output_fields(sdf)
+    if _vector_columns(sdf):
+        # Spark < 4 cannot move a VectorUDT through Arrow: pass the features as arrays through a
+        # scalar-iterator pandas UDF and keep every original column (reference core.py:1537-1557)
+        return _spark_transform_udf(model, sdf, out_fields)
     sdf_u, vec = _unwrap_vectors(sdf)
     blob = cloudpickle.dumps((model, vec))
-    out_fields = model._spark_output_fields(sdf)
 
     def _predict(it: Iterator[Any]) -> Iterator[Any]:
         import torch
@@ -321,4 +426,77 @@ def spark_transform(model: Any, sdf: Any) -> Any:
     from pyspark.sql.types import StructType  # type: ignore
 
     out_schema = StructType(list(schema.fields) + out_fields)
-    return sdf_u.mapInArrow(_predict, schema=out_schema)
+    out = sdf_u.mapInArrow(_predict, schema=out_schema)
+    return _wrap_vector_outputs(model, out, out_fields, False)
+
+
+def _vector_columns(sdf: Any) -> List[str]:
+    try:
+        from pyspark.ml.linalg import VectorUDT  # type: ignore
+    except Exception:  # noqa: BLE001
+        return []
+    return [f.name for f in sdf.schema.fields if isinstance(f.dataType, VectorUDT)]
+
+
+def _wrap_vector_outputs(model: Any, out: Any, out_fields: List[Any], input_is_vector: bool) -> Any:
+    """Vector-typed outputs travel as list<double>; Spark wraps them as VectorUDT (array_to_vector)
+    so pyspark evaluators / VectorAssembler consume them directly (reference core.py:1559-1610)."""
+    names = [f.name for f in out_fields]
+    to_vec = [c for c in model._spark_vector_output_cols(input_is_vector) if c in names]
+    if to_vec:
+        from pyspark.ml.functions import array_to_vector  # type: ignore
+        from pyspark.sql import functions as F  # type: ignore
+
+        for c in to_vec:
+            out = out.withColumn(c, array_to_vector(F.col(c)))
+    return out
+
+
+def _spark_transform_udf(model: Any, sdf: Any, out_fields: List[Any]) -> Any:
+    """Transform of a frame holding VectorUDT columns: ``withColumn`` of a scalar-iterator pandas UDF
+    over ``struct(vector_to_array(features))`` returning a struct of the outputs, expanded into
+    columns — every input column (vectors included) is kept as it was."""
+    import numpy as np
+    import pandas as pd
+    import pyarrow as pa
+
+    from pyspark.ml.functions import vector_to_array  # type: ignore
+    from pyspark.sql import functions as F  # type: ignore
+    from pyspark.sql.functions import pandas_udf  # type: ignore
+    from pyspark.sql.types import StructType  # type: ignore
+
+    from ..core.dataframe import DataFrame
+
+    col, cols = model._transform_input_cols()
+    vec = _vector_columns(sdf)
+    dt = "float32" if getattr(model, "_float32_inputs", True) else "float64"
+    inputs = [vector_to_array(F.col(c), dt).alias(c) if c in vec else F.col(c) for c in ([col] if col else cols)]
+    blob = cloudpickle.dumps(model)
+
+    def _udf(it: Iterator[pd.DataFrame]) -> Iterator[pd.DataFrame]:
+        import torch
+
+        from pyspark import TaskContext  # type: ignore
+
+        from .context import WorkerContext, gpu_available
+
+        m = cloudpickle.loads(blob)
+        tc = TaskContext.get()
+        dev = _task_device(tc, gpu_available()) if tc is not None else torch.device("cpu")
+        ctx = WorkerContext.single(dev)
+        construct, predict = m._get_transform_func(None)
+        state = construct(ctx)
+        for pdf in it:
+            table = pa.Table.from_pandas(pdf, preserve_index=False)
+            res = predict(state, m._transform_features(DataFrame([table])), ctx) if table.num_rows else {}
+            yield pd.DataFrame({k: (list(np.asarray(v, np.float64)) if np.ndim(v) == 2 else np.asarray(v, np.float64))
+                                for k, v in res.items()})
+
+    _udf.__annotations__ = {"it": Iterator[pd.DataFrame], "return": Iterator[pd.DataFrame]}
+    predict_udf = pandas_udf(_udf, returnType=StructType(out_fields))
+    tmp = "__srml_out"
+    out = sdf.withColumn(tmp, predict_udf(F.struct(*inputs)))
+    for f in out_fields:
+        out = out.withColumn(f.name, F.col("%s.%s" % (tmp, f.name)))
+    out = out.drop(tmp)
+    return _wrap_vector_outputs(model, out, out_fields, bool(col) and col in vec)

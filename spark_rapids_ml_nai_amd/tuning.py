@@ -21,7 +21,7 @@ from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
-from .core.dataframe import DataFrame, as_dataframe
+from .core.dataframe import as_dataframe
 from .core.params import HasSeed, Param, Params, TypeConverters, keyword_only
 from .core.persistence import MLReadable, MLWritable, MLReader, MLWriter, _jsonable, _load_class, _read_text, \
     _write_text
@@ -123,7 +123,23 @@ class _CrossValidatorParams(HasSeed):
         return self._set(seed=value)
 
 
-class CrossValidator(_CrossValidatorParams, MLWritable, MLReadable):
+def _pyspark_tuning() -> Tuple[Any, Any]:
+    try:
+        from pyspark.ml.tuning import CrossValidator as _S, CrossValidatorModel as _SM  # type: ignore
+
+        return _S, _SM
+    except Exception:  # noqa: BLE001 - pyspark absent: standalone classes
+        return None, None
+
+
+_SparkCV, _SparkCVModel = _pyspark_tuning()
+# With pyspark the classes ARE pyspark CrossValidator / CrossValidatorModel subclasses (reference
+# tuning.py:39): isinstance checks, pyspark's params and _kFold on Spark DataFrames all hold.
+_CV_BASES = (_SparkCV,) if _SparkCV is not None else (_CrossValidatorParams, MLWritable, MLReadable)
+_CVM_BASES = (_SparkCVModel,) if _SparkCVModel is not None else (_CrossValidatorParams, MLWritable, MLReadable)
+
+
+class CrossValidator(*_CV_BASES):  # type: ignore[misc]
     """K-fold cross validation with single-pass multi-model fit and evaluation.
 
     >>> from spark_rapids_ml_nai_amd.tuning import CrossValidator, ParamGridBuilder
@@ -139,15 +155,20 @@ class CrossValidator(_CrossValidatorParams, MLWritable, MLReadable):
     def __init__(self, *, estimator: Any = None, estimatorParamMaps: Optional[List[Dict[Param, Any]]] = None,
                  evaluator: Any = None, numFolds: int = 3, seed: Optional[int] = None, parallelism: int = 1,
                  collectSubModels: bool = False, foldCol: str = "") -> None:
+        kwargs = dict(self._input_kwargs)  # a pyspark base __init__ resets _input_kwargs
         super().__init__()
-        self._set(**{k: v for k, v in self._input_kwargs.items() if v is not None})
+        self._set(**{k: v for k, v in kwargs.items() if v is not None})
 
     def fit(self, dataset: Any, params: Optional[Dict[Param, Any]] = None) -> "CrossValidatorModel":
         if params:
             return self.copy(params)._fit(dataset)
         return self._fit(dataset)
 
-    def _kFold(self, dataset: DataFrame) -> List[Tuple[DataFrame, DataFrame]]:
+    def _kFold(self, dataset: Any) -> List[Tuple[Any, Any]]:
+        from .parallel.spark import is_spark_dataframe
+
+        if is_spark_dataframe(dataset):  # pyspark's rand(seed)-column split, evaluated by Spark
+            return super()._kFold(dataset)  # type: ignore[misc]
         nFolds = self.getNumFolds()
         foldCol = self.getFoldCol()
         m = dataset.count()
@@ -168,15 +189,22 @@ class CrossValidator(_CrossValidatorParams, MLWritable, MLReadable):
         return out
 
     def _fit(self, dataset: Any) -> "CrossValidatorModel":
-        df, _ = as_dataframe(dataset)
+        from .parallel.spark import is_spark_dataframe
+
         est = self.getEstimator()
         eva = self.getEvaluator()
+        fast = hasattr(est, "_supportsTransformEvaluate") and est._supportsTransformEvaluate(eva)
+        if is_spark_dataframe(dataset):
+            if not fast:  # not one of ours / unsupported evaluator: pyspark's generic loop
+                return super()._fit(dataset)  # type: ignore[misc]
+            df = dataset
+        else:
+            df, _ = as_dataframe(dataset)
         epm = self.getEstimatorParamMaps()
         numModels = len(epm)
         nFolds = self.getNumFolds()
         collect = self.getCollectSubModels()
         datasets = self._kFold(df)
-        fast = hasattr(est, "_supportsTransformEvaluate") and est._supportsTransformEvaluate(eva)
 
         def single_pass(fold: int) -> Tuple[int, List[float], Optional[List[Any]]]:
             train, validation = datasets[fold]
@@ -230,10 +258,13 @@ class CrossValidator(_CrossValidatorParams, MLWritable, MLReadable):
         return _CVReader(cls)
 
 
-class CrossValidatorModel(_CrossValidatorParams, MLWritable, MLReadable):
+class CrossValidatorModel(*_CVM_BASES):  # type: ignore[misc]
     def __init__(self, bestModel: Any = None, avgMetrics: Optional[List[float]] = None,
                  subModels: Optional[List[List[Any]]] = None, stdMetrics: Optional[List[float]] = None) -> None:
-        super().__init__()
+        if _SparkCVModel is not None:
+            super().__init__(bestModel, avgMetrics, subModels, stdMetrics)
+        else:
+            super().__init__()
         self.bestModel = bestModel
         self.avgMetrics = list(avgMetrics or [])
         self.subModels = subModels

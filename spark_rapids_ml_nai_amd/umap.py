@@ -144,6 +144,24 @@ def _umap_fit_worker(ctx: WorkerContext, payload: Tuple[Any, ...]) -> Tuple[np.n
     return emb, Xd.cpu().numpy()
 
 
+def _spark_umap_task(ctx: WorkerContext, table: Any, extra: Tuple[Any, ...]) -> Any:
+    """One rank of the Spark UMAP fit (barrier job): the ranks' rows are device-gathered and fitted
+    together (``_umap_fit_worker``); rank 0 returns (embedding, training rows). The reference fits in
+    ONE non-barrier task on one GPU (``umap.py:830-909``); ``num_workers=1`` gives exactly that."""
+    col, cols, label_col, params = extra
+    if table is not None and table.num_rows:
+        part = DataFrame([table])
+        X = _dense_from_df(part, col, cols, np.float32)
+        y = part.to_numpy(label_col).astype(np.int64) if label_col else None
+    else:
+        X, y = None, (np.zeros(0, np.int64) if label_col else None)
+    nt = torch.tensor([float(X.shape[1] if X is not None else 0)], dtype=torch.float64, device=ctx.device)
+    ctx.comm.allreduce(nt, op="max")
+    if X is None:
+        X = np.zeros((0, int(nt.item())), np.float32)
+    return _umap_fit_worker(ctx, (X, y, params))
+
+
 class UMAP(UMAPClass, _Estimator, _UMAPParams):
     """Uniform Manifold Approximation and Projection.
 
@@ -172,7 +190,26 @@ class UMAP(UMAPClass, _Estimator, _UMAPParams):
     def _create_model(self, result: Dict[str, Any]) -> "UMAPModel":
         return UMAPModel._from_row(result)
 
+    def _spark_fit(self, sdf: Any) -> Tuple[np.ndarray, np.ndarray]:
+        from .parallel.spark import spark_barrier_job
+
+        frac = self.getSampleFraction()
+        if frac is not None and frac < 1.0:
+            sdf = sdf.sample(False, frac, seed=self._backend_params.get("random_state"))
+        fc = self.getFeaturesCol()
+        col, cols = (fc, None) if isinstance(fc, str) else (None, list(fc))
+        label = self.getLabelCol() if self.isDefined("labelCol") and self.getLabelCol() in sdf.columns else None
+        sel = ([col] if col else list(cols)) + ([label] if label else [])
+        res = spark_barrier_job(sdf.select(*sel).repartition(max(1, self.num_workers)), _spark_umap_task,
+                                (col, cols, label, self._umap_params()))
+        return res[0]
+
     def _fit(self, dataset: Any) -> "UMAPModel":
+        from .parallel.spark import is_spark_dataframe
+
+        if is_spark_dataframe(dataset):
+            emb, Xall = self._spark_fit(dataset)
+            return self._make_model(emb, Xall)
         df, _ = as_dataframe(dataset)
         frac = self.getSampleFraction()
         if frac is not None and frac < 1.0:
@@ -198,6 +235,9 @@ class UMAP(UMAPClass, _Estimator, _UMAPParams):
                 yp = part.to_numpy(self.getLabelCol()).astype(np.int64) if y is not None else None
                 payloads.append((self._features(part), yp, params))
         emb, Xall = run_worker_job(_umap_fit_worker, payloads)[0]
+        return self._make_model(emb, Xall)
+
+    def _make_model(self, emb: np.ndarray, Xall: np.ndarray) -> "UMAPModel":
         model = UMAPModel(embedding_=emb, raw_data_=Xall, n_cols=int(Xall.shape[1]), dtype="float32")
         model._num_workers = self._num_workers
         model._float32_inputs = True
@@ -241,6 +281,17 @@ class UMAPModel(UMAPClass, _Model, _UMAPParams):
             return {out_col: umap_transform(Xd, Rd, Ed, params)}
 
         return construct, predict
+
+    def _transform(self, dataset: Any) -> Any:
+        from .parallel.spark import is_spark_dataframe, spark_transform
+
+        if is_spark_dataframe(dataset):
+            # per-partition transform (kNN to the training rows + SGD placement); like the reference
+            # the output holds the features and the embedding only (umap.py:1149-1241)
+            fc = self.getFeaturesCol()
+            out = spark_transform(self, dataset)
+            return out.select(*(([fc] if isinstance(fc, str) else list(fc)) + [self.getOutputCol()]))
+        return super()._transform(dataset)
 
     def _transform_df(self, df: DataFrame) -> DataFrame:
         out = super()._transform_df(df)

@@ -118,3 +118,26 @@ def __getattr__(name: str) -> Any:  # anything else is outside the modelled slic
 
 __all__: List[str] = ["Column", "col", "lit", "unwrap_udt", "monotonically_increasing_id", "rand", "struct",
                       "arrays_zip", "explode"]
+
+
+def pandas_udf(f=None, returnType=None, functionType=None):
+    """Scalar-iterator pandas UDF over one struct column (the only shape the library uses)."""
+    def make(*cols):
+        arg = _c(cols[0])
+
+        def run(t, pid):
+            import pandas as pd
+
+            from .types import to_arrow_type
+
+            a = arg.eval(t, pid)
+            pdf = pa.Table.from_arrays(a.flatten(), names=[fl.name for fl in a.type]).to_pandas()
+            outs = list(f(iter([pdf])))
+            out = pd.concat(outs) if outs else pd.DataFrame()
+            arrays = [pa.array(list(out[fl.name]) if len(out) else [], type=to_arrow_type(fl.dataType))
+                      for fl in returnType.fields]
+            return pa.StructArray.from_arrays(arrays, names=returnType.names)
+
+        return Column("pandas_udf", fn=run)
+
+    return make

@@ -53,7 +53,8 @@ def main() -> None:
     tr = lr.transform(sdf(X, yc)).toArrow()
     out["logreg_columns"] = tr.schema.names
     out["logreg_acc"] = float((tr.column("prediction").to_numpy() == yc).mean())
-    out["logreg_prob_rows"] = len(tr.column("probability").to_pylist()[0])
+    prob0 = tr.column("probability").to_pylist()[0]  # VectorUDT struct (type, size, indices, values)
+    out["logreg_prob_rows"] = len(prob0["values"]) if isinstance(prob0, dict) else len(prob0)
 
     km = KMeans(k=3, seed=1, num_workers=2, maxIter=20).fit(sdf(X, None))
     out["kmeans_centers"] = len(km.clusterCenters())

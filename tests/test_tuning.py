@@ -101,3 +101,29 @@ def test_fold_col():
     cvm = CrossValidator(estimator=est, estimatorParamMaps=grid, evaluator=RegressionEvaluator(),
                          foldCol="fold").fit(df)
     assert cvm.avgMetrics[0] < cvm.avgMetrics[1]
+
+
+@pytest.mark.dist
+@pytest.mark.parametrize("nw", [2, 4])
+@pytest.mark.parametrize("task", ["regression", "logloss", "f1"])
+def test_distributed_transform_evaluate_matches_generic(monkeypatch, nw, task):
+    """Single-pass transform-evaluate on nw gloo ranks (per-partition sufficient statistics merged
+    on the driver) equals evaluating each model's transformed frame with the evaluator."""
+    monkeypatch.setenv("SRML_FORCE_CPU", "1")
+    rng = np.random.default_rng(5)
+    X = rng.standard_normal((900, 4)).astype(np.float32)
+    if task == "regression":
+        y = X @ np.array([1.0, -2.0, 0.5, 3.0]) + 0.1 * rng.standard_normal(900)
+        est, ev = LinearRegression(num_workers=nw), RegressionEvaluator(metricName="r2")
+        grid = ParamGridBuilder().addGrid(est.regParam, [0.0, 1.0]).build()
+    else:
+        y = (X[:, 0] - 0.5 * X[:, 1] + 0.3 * rng.standard_normal(900) > 0).astype(np.float64)
+        est = LogisticRegression(num_workers=nw)
+        ev = MulticlassClassificationEvaluator(metricName="logLoss" if task == "logloss" else "f1")
+        grid = ParamGridBuilder().addGrid(est.regParam, [0.01, 0.5]).build()
+    df = DataFrame.from_numpy(X, y, num_partitions=nw)
+    models = [m for _, m in sorted(est.fitMultiple(df, grid), key=lambda t: t[0])]
+    combined = models[0]._combine(models)
+    fast = combined._transformEvaluate(df, ev)
+    generic = [ev.evaluate(m.transform(df)) for m in models]
+    np.testing.assert_allclose(fast, generic, rtol=1e-9, atol=1e-12)

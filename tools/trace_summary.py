@@ -1,0 +1,33 @@
+"""Summarise a rocprofv3 kernel_trace.csv: per-kernel totals over the timed step (the second
+half of the dispatches when warmup == steps) and the per-call durations of selected kernels."""
+import csv
+import glob
+import os
+import sys
+from collections import defaultdict
+
+
+def main(out_dir: str) -> None:
+    files = glob.glob(os.path.join(out_dir, "raw", "**", "*kernel_trace.csv"), recursive=True)
+    rows = []
+    for f in files:
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    rows.sort()
+    tot = defaultdict(lambda: [0, 0.0])
+    for s, e, k in rows:
+        tot[k][0] += 1
+        tot[k][1] += (e - s) / 1e6
+    span = (rows[-1][1] - rows[0][0]) / 1e6 if rows else 0.0
+    print("dispatches %d, first-to-last span %.1f ms (warmup + timed)" % (len(rows), span))
+    for k, (n, ms) in sorted(tot.items(), key=lambda kv: -kv[1][1])[:25]:
+        print("%9.2f ms %6d  %s" % (ms, n, k[:110]))
+    for pat in ("rf_hist_kernel", "nearest", "splitmm", "kmeanspp"):
+        calls = [(e - s) / 1e6 for s, e, k in rows if pat in k]
+        if calls:
+            print("%s per call (ms): %s" % (pat, " ".join("%.2f" % c for c in calls[:64])))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
