@@ -261,7 +261,8 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
     n_leaves = np.ones(n_trees, dtype=np.int64)
     fb = ops.rf_hist_fb(B, SH, regression)  # features per histogram work item (fits the LDS slab)
     nfc = (nf + fb - 1) // fb
-    yscale = ops.rf_yscale(yv) if regression and dev.type == "cuda" else None
+    # i64 fixed-point scale bounded by the heaviest tree's total bootstrap weight (no cell overflows)
+    yscale = ops.rf_yscale(yv, float(tot[:, 0].max().item())) if regression and dev.type == "cuda" else None
     hist_cell = (8 if regression else 4) * nf * B * SH
     group = max(1, HIST_BUDGET_BYTES // max(hist_cell, 1))
     depth = 0

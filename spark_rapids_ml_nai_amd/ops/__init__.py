@@ -386,24 +386,35 @@ def split_bf16x3(X: torch.Tensor, row_multiple: int = 128, tiled: bool = False,
     return P
 
 
-CERTIFY_TAU = 2.0 ** -13  # dot-product error bound of the 3-product search, relative to ||x|| ||c||
+CERTIFY_TAU = 2.0 ** -13  # dropped-product bound of the 3-product search (3 * 2^-16, 8x slack), per ||x|| ||c||
+
+
+def certify_tau(n: int) -> float:
+    """Worst-case |d~ - d| of the 3-product search vs the fp32 6-product search, relative to
+    ||x|| ||c||: the dropped products (``CERTIFY_TAU``) plus the fp32 accumulation error of BOTH
+    searches over n terms (each <= n * 2^-24 * sum|x_i c_i| <= n * 2^-24 ||x|| ||c||, the standard
+    gamma_n bound with Cauchy-Schwarz). With this radius a certified row provably gets the label
+    the exact search gives it; without the n term the guarantee would only be empirical."""
+    return CERTIFY_TAU + 2.0 * float(n) * 2.0 ** -24
 
 
 def _nearest_centroid_certified(XP: torch.Tensor, X: torch.Tensor, m: int, k: int, CP: torch.Tensor,
                                 cn: torch.Tensor, xnorm: torch.Tensor, st: int, mu: Optional[torch.Tensor]
                                 ) -> Tuple[torch.Tensor, torch.Tensor]:
     """Filter-and-refine arg-min: the 3-product search (half the MFMAs of the fp32-exact one)
-    keeps every row's best and second-best distance; rows whose gap exceeds the error bound of
-    the dropped products (4 tau ||x|| max||c||) are certified — the exact search would pick the
-    same centroid — and only the remaining near-tie rows are re-searched with the 6-product
-    kernel (their labels and distances are then bit-identical to the exact path)."""
+    keeps every row's best and second-best distance; rows whose gap exceeds twice the error
+    radius (``certify_tau(n)``: dropped products + worst-case fp32 accumulation of both searches)
+    are certified — the exact search provably picks the same centroid — and only the remaining
+    near-tie rows are re-searched with the 6-product kernel (their labels and distances are then
+    bit-identical to the exact path)."""
     dev = XP.device
     nslot = int(native.lib().srml_nearest_centroid_split_top2_nslot(k))
     keys = torch.empty(m * nslot, dtype=torch.int64, device=dev)
     lob = torch.empty(m * nslot, dtype=torch.float32, device=dev)
     xrows, kp, crows = XP.shape[1] * 256, XP.shape[2] * 16, CP.shape[1] * 256
     xn = _c(xnorm.float())
-    cg = (2.0 * CERTIFY_TAU) * cn.clamp_min(0).sqrt()  # error radius per unit ||x||, per centroid
+    tau = certify_tau(int(X.shape[1]) if X is not None else kp)
+    cg = (2.0 * tau) * cn.clamp_min(0).sqrt()  # error radius per unit ||x||, per centroid
     native.call("srml_nearest_centroid_split_top2", XP.data_ptr(), m, xrows, kp, CP.data_ptr(), k, crows,
                 cn.data_ptr(), cg.data_ptr(), xn.data_ptr(), keys.data_ptr(), lob.data_ptr(), st)
     labels = torch.empty(m, dtype=torch.int32, device=dev)
@@ -633,11 +644,18 @@ def rf_quantiles(S: torch.Tensor, nq: int) -> torch.Tensor:
 RF_HIST_FB_MAX = 8  # FB in csrc/forest.hip (checked against srml_rf_hist_fb_max on load in tests)
 
 
-def rf_yscale(y: torch.Tensor) -> float:
-    """Fixed-point scale of the regression histograms' i64 w*y sums: |block sum| <= 65536 rows *
-    255 * max|y| < 2^24 max|y|, so 2^38 / max|y| keeps 63 bits."""
+def rf_yscale(y: torch.Tensor, total_weight: Optional[float] = None) -> float:
+    """Fixed-point scale of the regression histograms' i64 w*y sums. Every sum the kernels form —
+    a block's LDS cell and the global cross-chunk fold of one (node, feature, bin) cell — covers
+    rows of ONE tree, so |sum| <= W * max|y| * yscale with W the largest per-tree bootstrap weight
+    total (<= rows * 255); yscale = 2^62 / (W max|y|) keeps every such sum inside i64 whatever the
+    row count (1M rows: 2^42 steps per max|y|; 50M: 2^36). Without ``total_weight`` the bound is
+    the per-item one (65536 rows * 255)."""
     ymax = float(y.abs().max().item()) if y.numel() else 0.0
-    return float(2.0 ** 38 / ymax) if ymax > 0 else 1.0
+    if ymax <= 0:
+        return 1.0
+    W = float(total_weight) if total_weight is not None and total_weight > 0 else 65536.0 * 255.0
+    return float(2.0 ** 62 / (max(W, 1.0) * ymax))
 
 
 def rf_hist_fb(B: int, S: int, regression: bool) -> int:
@@ -711,7 +729,7 @@ def rf_hist(bins: torch.Tensor, idx: torch.Tensor, label: torch.Tensor, wcnt: Op
         if S != 2:
             raise ValueError("device regression histograms carry (count, sum): S must be 2")
         if yscale is None:  # callers growing many levels pass rf_yscale(y) once per fit (no host sync here)
-            yscale = rf_yscale(wy[:, 1])
+            yscale = rf_yscale(wy[:, 1], float(wy[:, 0].sum().item()))
     else:
         yscale = 1.0
     st = native.stream(dev)

@@ -10,6 +10,7 @@
 // so callers (JNI shim, Python, C++) never see partially written outputs.
 #include <cstring>
 
+#include "capi_check.h"
 #include "common.h"
 
 extern "C" int srml_dgemm(int ta, int tb, int M, int N, int K, double alpha, const double* A, long lda,
@@ -63,18 +64,21 @@ __global__ void transpose_kernel(const double* __restrict__ in, double* __restri
 
 SRML_API int srml_capi_dgemm(int transa, int transb, int m, int n, int k, double alpha, const double* A, int lda,
                              const double* B, int ldb, double beta, double* C, int ldc, int device) {
-  if (m <= 0 || n <= 0) return 0;
+  // column-major r x c with leading dimension ld == row-major (c x ld) buffer
+  size_t na = 0, nb = 0, nc = 0;
+  const int chk = srml_check_gemm(transa, transb, m, n, k, lda, ldb, ldc, &na, &nb, &nc);
+  if (chk) return chk;
+  if (m == 0 || n == 0) return 0;
+  if ((na && !A) || (nb && !B) || !C) return SRML_EARG;
   DeviceGuard g(device);
   if (!g.ok) return -1;
-  // column-major r x c with leading dimension ld == row-major (c x ld) buffer
-  const size_t na = (size_t)lda * (transa ? m : k), nb = (size_t)ldb * (transb ? k : n), nc = (size_t)ldc * n;
   DevBuf<double> a(na), b(nb), c(nc);
-  if (!a.p || !b.p || !c.p) return -2;
+  if ((na && !a.p) || (nb && !b.p) || !c.p) return -2;
   hipStream_t s;
   if (hipStreamCreate(&s) != hipSuccess) return -1;
   hipError_t err = hipSuccess;
-  SRML_TRY(err, hipMemcpyAsync(a.p, A, na * sizeof(double), hipMemcpyHostToDevice, s));
-  SRML_TRY(err, hipMemcpyAsync(b.p, B, nb * sizeof(double), hipMemcpyHostToDevice, s));
+  if (na) SRML_TRY(err, hipMemcpyAsync(a.p, A, na * sizeof(double), hipMemcpyHostToDevice, s));
+  if (nb) SRML_TRY(err, hipMemcpyAsync(b.p, B, nb * sizeof(double), hipMemcpyHostToDevice, s));
   if (beta != 0.0) SRML_TRY(err, hipMemcpyAsync(c.p, C, nc * sizeof(double), hipMemcpyHostToDevice, s));
   // C_colmajor = op(A) op(B)  <=>  row-major C^T (n x m) = op(B)^T op(A)^T with the same flags
   int rc = srml_dgemm(transb, transa, n, m, k, alpha, b.p, ldb, a.p, lda, beta, c.p, ldc, s);
@@ -88,7 +92,11 @@ SRML_API int srml_capi_dgemm(int transa, int transb, int m, int n, int k, double
 // C (rows x k, row-major, device) = X (rows x n, row-major, device) . P (n x k row-major, host or device)
 SRML_API int srml_capi_dgemm_device(const double* X, long rows, int n, const double* P, int k, int p_on_host,
                                     double* C, hipStream_t stream) {
-  if (rows <= 0 || k <= 0) return 0;
+  size_t nx = 0, np = 0, nc = 0;
+  const int chk = srml_check_xp(rows, n, k, &nx, &np, &nc);
+  if (chk) return chk;
+  if (rows == 0 || k == 0) return 0;
+  if ((nx && !X) || (np && !P) || !C) return SRML_EARG;
   const double* pd = P;
   DevBuf<double> tmp(p_on_host ? (size_t)n * k : 0);
   hipError_t err = hipSuccess;
@@ -104,7 +112,11 @@ SRML_API int srml_capi_dgemm_device(const double* X, long rows, int n, const dou
 }
 
 SRML_API int srml_capi_dgemm_cov(const double* X, long rows, int cols, double* C, int device) {
-  if (cols <= 0) return 0;
+  size_t nx = 0, ncov = 0;
+  const int chk = srml_check_cov(rows, cols, &nx, &ncov);
+  if (chk) return chk;
+  if (cols == 0) return 0;
+  if ((nx && !X) || !C) return SRML_EARG;
   DeviceGuard g(device);
   if (!g.ok) return -1;
   DevBuf<double> x((size_t)rows * cols), c((size_t)cols * cols);
@@ -126,7 +138,11 @@ SRML_API int srml_capi_dgemm_cov(const double* X, long rows, int cols, double* C
 }
 
 SRML_API int srml_capi_cal_svd(const double* A, int m, double* U, double* S, int device) {
-  if (m <= 0) return 0;
+  size_t nm = 0;
+  const int chk = srml_check_svd(m, &nm);
+  if (chk) return chk;
+  if (m == 0) return 0;
+  if (!A || !U || !S) return SRML_EARG;
   DeviceGuard g(device);
   if (!g.ok) return -1;
   DevBuf<double> a((size_t)m * m), v((size_t)m * m), w(m), ut((size_t)m * m);
@@ -152,6 +168,7 @@ SRML_API int srml_capi_cal_svd(const double* A, int m, double* U, double* S, int
 }
 
 SRML_API int srml_capi_accumulate_cov(double* acc, const double* c, long len) {
+  if (len < 0 || (len && (!acc || !c))) return SRML_EARG;
   for (long i = 0; i < len; ++i) acc[i] += c[i];
   return 0;
 }

@@ -533,10 +533,11 @@ __global__ __launch_bounds__(512, 1) void nearest_centroid_split_glds_kernel(
 }
 
 // Merge the slots of every row and certify the 3-product arg-min b: with |d~_j - d_j| <= e_j =
-// ||x|| g_j (g_j = 2 tau ||c_j||; tau = 2^-13 covers the 3 * 2^-16 dropped products with 8x slack
-// for fp32 accumulation order), d~_j - e_j > d~_b + e_b for every j != b proves d_j > d_b, i.e. the
-// fp32-exact 6-product search picks b too. Certified rows get their label and distance; the rest
-// are appended to `flagged` (count in *n_flagged) for an exact re-search.
+// ||x|| g_j (g_j = 2 tau ||c_j||; tau = ops.certify_tau(n) = 2^-13 for the 3 * 2^-16 dropped
+// products + 2 n 2^-24 for the worst-case fp32 accumulation of both searches), d~_j - e_j >
+// d~_b + e_b for every j != b proves d_j > d_b, i.e. the fp32 6-product search picks b too.
+// Certified rows get their label and distance; the rest are appended to `flagged` (count in
+// *n_flagged) for an exact re-search.
 __global__ __launch_bounds__(256) void split_top2_select_kernel(const unsigned long long* __restrict__ keys,
                                                                 const float* __restrict__ lob, long m, int nslot,
                                                                 const float* __restrict__ xnorm,

@@ -234,6 +234,28 @@ def test_rf_regression_hist_deterministic(gpu_device, monkeypatch):
 
 
 @pytest.mark.gpu
+def test_rf_regression_fixed_point_no_overflow(gpu_device, monkeypatch):
+    """One bin holding 200k rows of weight 255 at y = max|y| (5.1e7 weighted rows > 2^25): the old
+    per-item scale (2^38 / max|y|) wraps the i64 cross-chunk fold; the total-weight scale must not."""
+    m, n, B = 200000, 2, 8
+    bins = torch.zeros((n, m), dtype=torch.uint8)
+    y = torch.full((m,), 7.5)
+    idx = torch.arange(m, dtype=torch.int32)
+    w = torch.full((m,), 255.0)
+    feats = torch.tensor([[0, 1]], dtype=torch.int32)
+    items = torch.tensor([[0, rb, min(rb + 4096, m), 0] for rb in range(0, m, 4096)], dtype=torch.int32)
+    dev = lambda t: t.to(gpu_device)  # noqa: E731
+    ys = ops.rf_yscale(dev(y), float(w.sum()))
+    assert 255.0 * m * 7.5 * ys < 2.0 ** 63
+    monkeypatch.setenv("SRML_DETERMINISTIC", "1")
+    h = ops.rf_hist(dev(bins), dev(idx), dev(y), None, dev(items), dev(feats), 1, B, 2, True,
+                    pos_weight=dev(w), yscale=ys).cpu()
+    assert h[0, 0, 0, 0].item() == 255.0 * m
+    assert h[0, 0, 0, 1].item() == pytest.approx(255.0 * m * 7.5, rel=1e-12)
+    assert float(h[0, :, 1:].abs().sum()) == 0.0
+
+
+@pytest.mark.gpu
 def test_rf_node_stats_deterministic(gpu_device, monkeypatch):
     g = torch.Generator().manual_seed(6)
     m = 200000
