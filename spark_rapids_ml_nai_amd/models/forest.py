@@ -24,6 +24,8 @@ RCCL — the north-star mode for datasets larger than one GPU's share).
 """
 from __future__ import annotations
 
+import os
+
 import math
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Tuple
@@ -35,6 +37,7 @@ from .. import ops
 from ..parallel.context import WorkerContext
 
 ROWS_PER_ITEM = 4096
+CHUNK_MAJOR_ITEMS = os.environ.get("SRML_RF_ITEM_ORDER", "chunk") == "chunk"
 INT_MAX = 2**31 - 1
 
 
@@ -289,7 +292,10 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
             if nf >= n:
                 feats = torch.arange(n, device=dev, dtype=torch.int32).repeat(C, 1)
             else:
-                feats = torch.rand((C, n), generator=gen, device=dev).argsort(1)[:, :nf].to(torch.int32).contiguous()
+                # each node's feature sample in ascending feature order: chunk c of every node then
+                # covers nearby columns of the feature-major bin matrix (see the item order below)
+                feats = torch.rand((C, n), generator=gen, device=dev).argsort(1)[:, :nf].sort(1).values
+                feats = feats.to(torch.int32).contiguous()
             c_start, c_cnt = bounds_h[cg], counts[cg]
             # rows per work item: ~8K blocks to fill the chip, few blocks per (node, feature chunk)
             rpi = int(min(65536, max(ROWS_PER_ITEM, (int(c_cnt.sum()) * nfc) // 8192)))
@@ -302,12 +308,23 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
             rb = c_start[node_rep] + chunk * rpi
             re = np.minimum(rb + rpi, c_start[node_rep] + c_cnt[node_rep])
             it = np.empty((tot_ch * nfc, 4), dtype=np.int32)
-            it[:, 0] = np.repeat(node_rep, nfc)
-            it[:, 1] = np.repeat(rb, nfc)
-            it[:, 2] = np.repeat(re, nfc)
             # single-chunk nodes own their histogram cells: plain stores, no zeroing, no atomics
-            single = np.repeat(nch[node_rep] == 1, nfc)
-            it[:, 3] = np.tile(np.arange(nfc), tot_ch) | np.where(single, 1 << 30, 0).astype(np.int32)
+            single = np.where(nch[node_rep] == 1, 1 << 30, 0).astype(np.int32)
+            if CHUNK_MAJOR_ITEMS:
+                # feature-chunk-major launch order: the blocks in flight at any time all read
+                # feature chunk c of their nodes — a few dozen adjacent bin columns, so every column
+                # comes from HBM about once per level and the other nodes' gathers hit L2 / MALL
+                # (node-major order streamed each node's own sample: deep levels re-read the whole
+                # matrix once per node)
+                it[:, 0] = np.tile(node_rep, nfc)
+                it[:, 1] = np.tile(rb, nfc)
+                it[:, 2] = np.tile(re, nfc)
+                it[:, 3] = np.repeat(np.arange(nfc, dtype=np.int32), tot_ch) | np.tile(single, nfc)
+            else:
+                it[:, 0] = np.repeat(node_rep, nfc)
+                it[:, 1] = np.repeat(rb, nfc)
+                it[:, 2] = np.repeat(re, nfc)
+                it[:, 3] = np.tile(np.arange(nfc), tot_ch) | np.repeat(single, nfc)
             items_t = torch.from_numpy(it).to(dev, non_blocking=False)
             excl = {"multi_nodes": torch.from_numpy(np.nonzero(nch != 1)[0]).to(dev)} if dev.type == "cuda" else None
             hist = ops.rf_hist(bins, idx, yv, None, items_t, feats, C, B, SH, regression, pos_weight=wpos, fb=fb,
@@ -371,13 +388,7 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
         meta = torch.from_numpy(np.stack([node_feature, node_bin, child_base])).to(dev)
         keys = ops.rf_route_segments(bins, idx, bounds, meta[0].contiguous(), meta[1].contiguous(),
                                      meta[2].contiguous())
-        keys_sorted, perm = torch.sort(keys, stable=True)
-        nb = torch.searchsorted(keys_sorted.contiguous(), torch.arange(2 * k + 1, device=dev, dtype=keys_sorted.dtype))
-        kept = int(nb[-1].item())
-        perm = perm[:kept]
-        idx = idx[perm].contiguous()
-        wpos = wpos[perm].contiguous()
-        bounds = nb.to(torch.int64)
+        idx, wpos, bounds = ops.rf_partition(keys, bounds, meta[0].contiguous(), meta[2].contiguous(), k, idx, wpos)
         if regression:
             tot = _node_stats(yv, idx, wpos, bounds, S, regression)
         else:

@@ -847,6 +847,32 @@ def rf_route_segments(bins: torch.Tensor, idx: torch.Tensor, bounds: torch.Tenso
     return keys
 
 
+def rf_partition(keys: torch.Tensor, bounds: torch.Tensor, node_feature: torch.Tensor, child_base: torch.Tensor,
+                 k: int, idx: torch.Tensor, wpos: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Stable re-partition of (idx, wpos) into the 2k child segments of the k split parents
+    (child keys from ``rf_route_segments``; other positions leave the tree): (idx, wpos, bounds
+    of the 2k children). Device: prefix-count kernels + one scatter (``srml_rf_partition``)."""
+    total = int(keys.shape[0])
+    if not keys.is_cuda:
+        keys_sorted, perm = torch.sort(keys, stable=True)
+        nb = torch.searchsorted(keys_sorted.contiguous(), torch.arange(2 * k + 1, dtype=keys_sorted.dtype))
+        kept = int(nb[-1].item())
+        perm = perm[:kept]
+        return idx[perm].contiguous(), wpos[perm].contiguous(), nb.to(torch.int64)
+    dev = keys.device
+    nseg = int(bounds.shape[0]) - 1
+    ws = torch.empty(int(native.lib().srml_rf_partition_ws(total, k)), dtype=torch.int64, device=dev)
+    idx_out = torch.empty(max(total, 1), dtype=torch.int32, device=dev)
+    w_out = torch.empty(max(total, 1), dtype=torch.float32, device=dev)
+    nb = torch.empty(2 * k + 1, dtype=torch.int64, device=dev)
+    native.call("srml_rf_partition", keys.data_ptr(), total, _c(bounds.long()).data_ptr(), nseg,
+                _c(node_feature.int()).data_ptr(), _c(child_base.int()).data_ptr(), int(k), _c(idx).data_ptr(),
+                _c(wpos.float()).data_ptr(), idx_out.data_ptr(), w_out.data_ptr(), nb.data_ptr(), ws.data_ptr(),
+                native.stream(dev))
+    kept = int(nb[-1].item())
+    return idx_out[:kept], w_out[:kept], nb
+
+
 def rf_node_stats(idx: torch.Tensor, wpos: torch.Tensor, label: torch.Tensor, bounds: torch.Tensor, S: int,
                   regression: bool) -> torch.Tensor:
     """Per segment [bounds[s], bounds[s+1]): regression (sum w, sum w y, sum w y^2) or per-class sum w
@@ -1048,6 +1074,50 @@ def _knn_large_k(Q: torch.Tensor, I: torch.Tensor, k: int, inorm: Optional[torch
     return outv, outi
 
 
+IVF_CAND_NMAX = 620  # feature width the candidate kernel stages in LDS (query + 64-row tile)
+_IVF_CAND_BYTES = 1 << 30  # candidate matrix budget of the large-k IVF paths (distances + ids)
+
+
+def _ivf_large_k(Q: torch.Tensor, nq: int, probes: torch.Tensor, list_off: torch.Tensor, items: torch.Tensor,
+                 inorm: torch.Tensor, ids: Optional[torch.Tensor], k: int, qlist: Optional[torch.Tensor] = None
+                 ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """64 < k <= 1024 over IVF lists on the device: every (query, probe) writes its list's partial
+    distances ||i||^2 - 2 q.i (+ ids / list positions) into the query's candidate row
+    (``srml_ivf_candidates_f32``), then the radix-select kernel keeps k per row (ids carried).
+    Query chunks bound the candidate matrix to ``_IVF_CAND_BYTES``. Padding: +inf / -1."""
+    dev = Q.device
+    n = Q.shape[1]
+    st = native.stream(dev)
+    pr = _c(probes.int())
+    lo = _c(list_off.long())
+    ql = _c(qlist.int()) if qlist is not None else None
+    nprobe = int(pr.shape[1])
+    cmax = torch.zeros(1, dtype=torch.int64, device=dev)
+    native.call("srml_ivf_candidate_max", pr.data_ptr(), nprobe, ql.data_ptr() if ql is not None else None, nq,
+                lo.data_ptr(), cmax.data_ptr(), st)
+    L = int(cmax.item())
+    od = torch.full((nq, k), float("inf"), dtype=torch.float32, device=dev)
+    oi = torch.full((nq, k), -1, dtype=torch.int64, device=dev)
+    if L == 0 or nq == 0:
+        return od, oi
+    kk = min(k, L)
+    R = max(1, min(nq, _IVF_CAND_BYTES // (L * 12)))
+    D = torch.empty((R, L), dtype=torch.float32, device=dev)
+    DI = torch.empty((R, L), dtype=torch.int64, device=dev)
+    Qc, Ic = _c(Q.float()), _c(items.float())
+    idc = _c(ids.long()) if ids is not None else None
+    inc = _c(inorm.float())
+    for q0 in range(0, nq, R):
+        r = min(R, nq - q0)
+        native.call("srml_ivf_candidates_f32", Qc.data_ptr(), q0, r, n, Qc.stride(0), pr.data_ptr(), nprobe,
+                    ql.data_ptr() if ql is not None else None, lo.data_ptr(), Ic.data_ptr(), Ic.stride(0),
+                    inc.data_ptr(), idc.data_ptr() if idc is not None else None, D.data_ptr(), DI.data_ptr(), L, st)
+        v, i = topk_rows(D[:r], kk, ids=DI[:r])
+        od[q0: q0 + r, :kk] = v
+        oi[q0: q0 + r, :kk] = i
+    return od, oi
+
+
 def ivf_search(Q: torch.Tensor, probes: torch.Tensor, list_off: torch.Tensor, items: torch.Tensor,
                inorm: torch.Tensor, ids: torch.Tensor, k: int, qnorm: Optional[torch.Tensor] = None
                ) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -1055,6 +1125,9 @@ def ivf_search(Q: torch.Tensor, probes: torch.Tensor, list_off: torch.Tensor, it
     nq, n = Q.shape
     if qnorm is None:
         qnorm = row_sqnorm(Q)
+    if Q.is_cuda and Q.dtype == torch.float32 and KNN_KMAX < k <= TOPK_KMAX and n <= IVF_CAND_NMAX:
+        od, oi = _ivf_large_k(Q, nq, probes, list_off, items, inorm, ids, k)
+        return (od + qnorm.float().view(-1, 1)).clamp_min(0), oi
     if not Q.is_cuda or Q.dtype != torch.float32 or k > KNN_KMAX:
         od = torch.full((nq, k), float("inf"), dtype=torch.float32, device=Q.device)
         oi = torch.full((nq, k), -1, dtype=torch.int64, device=Q.device)
@@ -1099,6 +1172,19 @@ def knn_lists(X: torch.Tensor, xnorm: torch.Tensor, list_off: torch.Tensor, prob
         return od, oi
     if tile_list.shape[0] != ntiles or list_off.shape[0] != probes.shape[0] + 1:
         raise ValueError("knn_lists: inconsistent tile / list descriptors")
+    if X.is_cuda and X.dtype == torch.float32 and KNN_KMAX < k <= TOPK_KMAX and n <= IVF_CAND_NMAX:
+        # the given tiles cover one contiguous row range (a rank's slice of the tile list); each of
+        # those rows probes its own list's probe set
+        lo = _c(list_off.long())
+        last = int(tile_list[-1].item())
+        r0 = int(tile_q0[0].item())
+        r1 = min(int(tile_q0[-1].item()) + 128, int(lo[last + 1].item()))
+        qlist = torch.empty(N, dtype=torch.int32, device=X.device)
+        native.call("srml_row_list", lo.data_ptr(), int(probes.shape[0]), N, qlist.data_ptr(), native.stream(X.device))
+        d, pos = _ivf_large_k(X[r0:r1], r1 - r0, probes, lo, X, xnorm, None, k, qlist=qlist[r0:r1])
+        od[r0:r1] = d
+        oi[r0:r1] = pos.int()
+        return od, oi
     if not X.is_cuda or X.dtype != torch.float32 or k > KNN_KMAX:
         lo = list_off.cpu().numpy()
         pr = probes.cpu().numpy()
@@ -1399,7 +1485,26 @@ def cd_gram(A: torch.Tensor, b: torch.Tensor, l1: torch.Tensor, l2: torch.Tensor
     """Cyclic coordinate descent: argmin 1/2 w'Aw - b'w + sum l1|w| + 1/2 sum l2 w^2 (fp64)."""
     n = A.shape[0]
     w = (torch.zeros(n, dtype=torch.float64, device=A.device) if w0 is None else w0.double().clone()).contiguous()
-    if not A.is_cuda or 2 * n * 8 > 150 * 1024:
+    if A.is_cuda and 2 * n * 8 > 150 * 1024:
+        # wider than the LDS-resident kernels: global-memory block-cyclic sweeps, one launch
+        # sequence per sweep, the convergence word read once per sweep
+        A = A.double().contiguous()
+        g = torch.zeros(n, dtype=torch.float64, device=A.device)
+        dv = torch.zeros(64, dtype=torch.float64, device=A.device)
+        stats = torch.zeros(2, dtype=torch.float64, device=A.device)
+        bb, l1c, l2c = _c(b.double()), _c(l1.double()), _c(l2.double())
+        st = native.stream(A.device)
+        it = 0
+        for it in range(1, max(1, max_iter) + 1):
+            stats.zero_()
+            native.call("srml_cd_sweep_global_f64", A.data_ptr(), n, A.stride(0), bb.data_ptr(), l1c.data_ptr(),
+                        l2c.data_ptr(), w.data_ptr(), g.data_ptr(), dv.data_ptr(), stats.data_ptr(),
+                        int(it == 1 and w0 is not None), st)
+            md, mw = stats.tolist()
+            if md <= tol * max(mw, 1e-300):
+                break
+        return w, it
+    if not A.is_cuda:
         Ah, bh, l1h, l2h = (t.double().cpu().numpy() for t in (A, b, l1, l2))
         wh = w.cpu().numpy()
         g = Ah @ wh
@@ -1541,11 +1646,13 @@ def _is_csr(X) -> bool:
 
 
 def logistic_path(X, K: int) -> str:
-    """Which device pass ``logistic_loss_grad`` uses for X (reported by the fit / asserted in tests)."""
+    """Which device pass ``logistic_loss_grad`` uses for X (reported by the fit / asserted in tests).
+    Every fp32 / CSR input runs on the srml kernels; only dense fp64 inputs wider than the LDS
+    kernels (``float32_inputs=False``) take the fp64 torch fallback."""
     if _is_csr(X):
         if not X.data.is_cuda:
             return "torch-cpu"
-        return "csr_binary" if K == 1 else ("csr_spmm" if K <= 16 else "torch")
+        return "csr_binary" if K == 1 else ("csr_spmm" if K <= 16 else "csr_wide")
     if not X.is_cuda:
         return "torch-cpu"
     m, n = X.shape
@@ -1556,11 +1663,50 @@ def logistic_path(X, K: int) -> str:
             return "fused_binary_f32"
         if X.dtype in (torch.float32, torch.float64) and n <= 16384:
             return "lds_binary_" + ("f32" if X.dtype == torch.float32 else "f64")
-        return "torch"
+        return "two_pass_binary_f32" if X.dtype == torch.float32 else "torch"
     if X.dtype == torch.float32 and K <= 16:
         fused = os.environ.get("SRML_LOGREG_FUSED", "0") == "1" and int(native.lib().srml_mlogit_supported(n, K))
         return "fused_multinomial_f32" if fused else "two_pass_multinomial_f32"
+    if X.dtype == torch.float32:
+        return "two_pass_wide_f32"
     return "torch"
+
+
+def _glm_wide(X, y32: torch.Tensor, W: torch.Tensor, b: torch.Tensor, out: torch.Tensor,
+              flag: Optional[torch.Tensor]) -> None:
+    """Softmax data term for K > 16 classes (dense fp32 or CSR): margins in 32-class (dense,
+    ``srml_xw_t_f32``) / 16-class (CSR SpMM) column panels of one Z, the wide residual kernel
+    (``srml_logit_residual_wide_f32``: R and the loss), the bias gradient as the column sums of R
+    (``srml_col_moments_f32``) and the X^T R panels (``srml_xtv_mfma_f32`` / CSR SpMTM)."""
+    csr = _is_csr(X)
+    m, n = X.shape
+    K = W.shape[0]
+    dev = X.data.device if csr else X.device
+    st = native.stream(dev)
+    fp = flag.data_ptr() if flag is not None else None
+    Wf = W.to(torch.float32)
+    if csr:
+        Z = torch.cat([csr_spmm(X, Wf[c0: c0 + 16].t()) for c0 in range(0, K, 16)], 1).contiguous()
+    else:
+        Z = torch.empty((m, K), dtype=torch.float32, device=dev)
+        for c0 in range(0, K, 32):
+            xw_t(X, _c(Wf[c0: c0 + 32]), out=Z[:, c0: c0 + 32])
+    R = torch.zeros((m, K), dtype=torch.float32, device=dev)  # stays 0 if the done flag skips the residual
+    Kn = K * n
+    native.call("srml_logit_residual_wide_f32", Z.data_ptr(), m, K, K, _c(y32).data_ptr(), _c(b).data_ptr(), 1,
+                R.data_ptr(), K, out[Kn + K:].data_ptr(), fp, st)
+    del Z
+    gb, _ = col_moments(R, need_sq=False)
+    out[Kn: Kn + K] += gb
+    if csr:
+        for c0 in range(0, K, 16):
+            kk = min(16, K - c0)
+            out[c0 * n: (c0 + kk) * n] += csr_spmtm(X, _c(R[:, c0: c0 + kk])).t().reshape(-1)
+        return
+    for c0 in range(0, K, 16):
+        kk = min(16, K - c0)
+        native.call("srml_xtv_mfma_f32", X.data_ptr(), m, n, X.stride(0), R[:, c0:].data_ptr(), kk, K,
+                    out[c0 * n:].data_ptr(), 1, n, fp, st)
 
 
 def mbin_supported(X, M: int) -> bool:
@@ -1679,15 +1825,17 @@ def logistic_loss_grad(X, y32: torch.Tensor, w: torch.Tensor, b: torch.Tensor, K
         native.call("srml_csr_logreg_binary_" + _sfx(X), X.indptr.data_ptr(), X.indices.data_ptr(), X.data.data_ptr(),
                     m, n, X.data.numel(), y32.data_ptr(), w.data_ptr(), 0.0, b.data_ptr(), fp, out.data_ptr(), st)
     elif path == "csr_spmm":
-        # margins (one SpMM pass, all classes) -> softmax residual on the device -> X^T R pass
-        Wt = w.view(K, n).t()
-        Z = csr_spmm(X, Wt, b).double()
-        lse = torch.logsumexp(Z, 1)
-        Y = torch.nn.functional.one_hot(y32.long(), K).double()
-        R = torch.exp(Z - lse.view(-1, 1)) - Y
-        out[K * n + K] += (lse - (Z * Y).sum(1)).sum()
-        out[K * n: K * n + K] += R.sum(0)
-        out[: K * n] += csr_spmtm(X, R.float()).t().reshape(-1)
+        # margins (one SpMM pass, all classes) -> the softmax residual kernel (R, bias gradient,
+        # loss) -> the X^T R SpMTM pass
+        Z = csr_spmm(X, w.view(K, n).t())
+        R = torch.zeros((m, K), dtype=torch.float32, device=dev)  # stays 0 if the done flag skips the residual
+        native.call("srml_logit_residual_f32", Z.data_ptr(), m, K, K, _c(y32).data_ptr(), b.data_ptr(), 1, 0,
+                    R.data_ptr(), K, out[K * n:].data_ptr(), 1, out[K * n + K:].data_ptr(), 0, fp, st)
+        out[: K * n] += csr_spmtm(X, R).t().reshape(-1)
+    elif path in ("csr_wide", "two_pass_wide_f32"):
+        _glm_wide(X, y32, w.view(K, n), b, out, flag)
+    elif path == "two_pass_binary_f32":  # wider than the LDS-resident binary kernels
+        _glm_two_pass(X, y32, w.view(1, n), b, 1, 1, out, 1, n, out[n:], 1, out[n + 1:], 1, flag)
     elif path == "fused_binary_f32":
         native.call("srml_logreg_binary2_f32", X.data_ptr(), m, n, X.stride(0), y32.data_ptr(), w.data_ptr(), 0.0,
                     b.data_ptr(), fp, out.data_ptr(), st)

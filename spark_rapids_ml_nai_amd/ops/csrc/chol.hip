@@ -626,6 +626,97 @@ SRML_API int srml_potrs_backward_f64(const double* L, int n, long lda, double* z
   return srml_status();
 }
 
+// ------------------------------------------------------------------------------------------
+// Global-memory block-cyclic coordinate descent for Gram matrices too wide for the LDS-resident
+// kernels (n > ~9600 — w and g no longer fit 150 KiB). Same coordinate order and updates as the
+// cyclic sweep: per block of CD_CB coordinates, `cd_chain_kernel` (one wave) runs the sequential
+// soft-threshold chain against a block-local copy of g (A_bb staged in LDS) and emits the deltas;
+// `cd_panel_kernel` (a grid over all n rows, coalesced row reads of the symmetric A) then applies
+// the block's rank-CB update g += A[:, block] dv before the next block's chain. w and g live in
+// device memory (L2-resident); the host launches one sweep at a time and reads the convergence
+// word once per sweep.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void cd_chain_kernel(const double* __restrict__ A, int n, long lda,
+                                                      const double* __restrict__ b, const double* __restrict__ l1,
+                                                      const double* __restrict__ l2, double* __restrict__ w,
+                                                      const double* __restrict__ g, int c0, double* __restrict__ dv,
+                                                      double* __restrict__ stats) {
+  __shared__ double ab[CD_CB][CD_CB + 1];
+  const int lane = threadIdx.x;
+  const int cb = min(CD_CB, n - c0);
+  for (int r = 0; r < cb; ++r)
+    if (lane < cb) ab[r][lane] = A[(long)(c0 + r) * lda + c0 + lane];
+  double gl = lane < cb ? g[c0 + lane] : 0.0;
+  double wl = lane < cb ? w[c0 + lane] : 0.0;
+  double mx_d = 0.0, mx_w = 0.0, dl = 0.0;
+  __syncthreads();
+  for (int c = 0; c < cb; ++c) {
+    const double gc = __shfl(gl, c, 64), wc = __shfl(wl, c, 64);
+    const double ajj = ab[c][c];
+    const double diag = ajj + l2[c0 + c];
+    double d = 0.0, nw = wc;
+    if (diag > 0.0) {
+      const double rho = b[c0 + c] - gc + ajj * wc;
+      const double lc = l1[c0 + c];
+      nw = rho > lc ? (rho - lc) / diag : (rho < -lc ? (rho + lc) / diag : 0.0);
+      d = nw - wc;
+      mx_w = fmax(mx_w, fabs(nw));  // coordinates with a non-positive diagonal are skipped entirely
+    }
+    if (d != 0.0) {
+      if (lane < cb) gl = fma(d, ab[c][lane], gl);  // A symmetric: row c of the block = column c
+      if (lane == c) wl = nw;
+      mx_d = fmax(mx_d, fabs(d));
+    }
+    if (lane == c) dl = d;
+  }
+  if (lane < cb) {
+    w[c0 + lane] = wl;
+    dv[lane] = dl;
+  }
+  if (lane == 0) {  // non-negative doubles order like their bit patterns
+    atomicMax(reinterpret_cast<unsigned long long*>(stats), __double_as_longlong(mx_d));
+    atomicMax(reinterpret_cast<unsigned long long*>(stats) + 1, __double_as_longlong(mx_w));
+  }
+}
+
+__global__ __launch_bounds__(256) void cd_panel_kernel(const double* __restrict__ A, int n, long lda, int c0,
+                                                       const double* __restrict__ dv, double* __restrict__ g) {
+  __shared__ double d[CD_CB];
+  const int cb = min(CD_CB, n - c0);
+  if (threadIdx.x < CD_CB) d[threadIdx.x] = threadIdx.x < cb ? dv[threadIdx.x] : 0.0;
+  __syncthreads();
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  double acc = 0.0;
+  for (int c = 0; c < cb; ++c)
+    if (d[c] != 0.0) acc = fma(A[(long)(c0 + c) * lda + i], d[c], acc);
+  g[i] += acc;
+}
+
+__global__ __launch_bounds__(256) void cd_gemv_kernel(const double* __restrict__ A, int n, long lda,
+                                                      const double* __restrict__ w, double* __restrict__ g) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  double acc = 0.0;
+  for (int j = 0; j < n; ++j) acc = fma(A[(long)j * lda + i], w[j], acc);
+  g[i] = acc;
+}
+
+// One sweep of the global-memory CD (g = A w maintained in `g`; stats[0..1] = max |delta|, max |w|
+// of the sweep, zeroed by the caller). init != 0: g = A w first.
+SRML_API int srml_cd_sweep_global_f64(const double* A, int n, long lda, const double* b, const double* l1,
+                                      const double* l2, double* w, double* g, double* dv, double* stats, int init,
+                                      hipStream_t stream) {
+  if (n <= 0) return 0;
+  const unsigned gb = (unsigned)((n + 255) / 256);
+  if (init) hipLaunchKernelGGL(cd_gemv_kernel, dim3(gb), dim3(256), 0, stream, A, n, lda, w, g);
+  for (int c0 = 0; c0 < n; c0 += CD_CB) {
+    hipLaunchKernelGGL(cd_chain_kernel, dim3(1), dim3(64), 0, stream, A, n, lda, b, l1, l2, w, g, c0, dv, stats);
+    hipLaunchKernelGGL(cd_panel_kernel, dim3(gb), dim3(256), 0, stream, A, n, lda, c0, dv, g);
+  }
+  return srml_status();
+}
+
 SRML_API int srml_cd_gram_f64(const double* A, int n, long lda, const double* b, const double* l1, const double* l2,
                               double* w, int max_iter, double tol, int* iters, hipStream_t stream) {
   if (n <= 0) return 0;

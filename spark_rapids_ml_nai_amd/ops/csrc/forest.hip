@@ -555,6 +555,194 @@ SRML_API int srml_rf_route_segments(const unsigned char* bins, long m, const int
 }
 
 // ------------------------------------------------------------------------------------------
+// Stable re-partition of the position arrays into child segments (replaces a device radix sort of
+// the child keys + searchsorted + two gathers per level). Every split parent segment s (split rank
+// j, child_base = 2j) sends its positions to children 2j (left) and 2j + 1 (right), keeping their
+// order; positions of unsplit segments leave the tree. With P = exclusive prefix over positions of
+// (is_left | is_right << 32) the rank of a position inside its child is a difference of P values,
+// the child sizes come from P at the parent's bounds, and the child offsets from a scan over the
+// split parents. Kernels: flags + block scans, scan of the block totals, offsets, per-parent
+// sizes, child bounds, scatter.
+// ------------------------------------------------------------------------------------------
+constexpr int PS_T = 256, PS_E = 4, PS_B = PS_T * PS_E;  // 1024 elements per scan block
+
+__device__ __forceinline__ unsigned long long block_excl_scan_u64(unsigned long long v, unsigned long long* s_w,
+                                                                  unsigned long long& total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  unsigned long long x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_w[wid] = x;
+  __syncthreads();
+  unsigned long long base = 0;
+  total = 0;
+#pragma unroll
+  for (int w = 0; w < PS_T / 64; ++w) {
+    const unsigned long long tw = s_w[w];
+    if (w < wid) base += tw;
+    total += tw;
+  }
+  __syncthreads();
+  return base + x - v;
+}
+
+// in == nullptr: the values are the partition flags of `keys` (left = even key, right = odd,
+// dropped = 0x7fffffff); otherwise a plain u64 exclusive scan of `in`.
+__global__ __launch_bounds__(PS_T) void scan_blocks_u64_kernel(const unsigned long long* __restrict__ in,
+                                                               const int* __restrict__ keys, long n,
+                                                               unsigned long long* __restrict__ out,
+                                                               unsigned long long* __restrict__ tot) {
+  __shared__ unsigned long long s_w[PS_T / 64];
+  const long b0 = (long)blockIdx.x * PS_B + (long)threadIdx.x * PS_E;
+  unsigned long long v[PS_E], sum = 0;
+#pragma unroll
+  for (int e = 0; e < PS_E; ++e) {
+    const long i = b0 + e;
+    unsigned long long x = 0;
+    if (i < n) {
+      if (in) {
+        x = in[i];
+      } else {
+        const int k = keys[i];
+        x = k == 0x7fffffff ? 0ull : ((k & 1) ? (1ull << 32) : 1ull);
+      }
+    }
+    v[e] = x;
+    sum += x;
+  }
+  unsigned long long total;
+  unsigned long long run = block_excl_scan_u64(sum, s_w, total);
+#pragma unroll
+  for (int e = 0; e < PS_E; ++e) {
+    const long i = b0 + e;
+    if (i < n) out[i] = run;
+    run += v[e];
+  }
+  if (threadIdx.x == 0) tot[blockIdx.x] = total;
+}
+
+// exclusive scan of the nb block totals in place (one block), grand total to *grand
+__global__ __launch_bounds__(PS_T) void scan_totals_u64_kernel(unsigned long long* __restrict__ tot, long nb,
+                                                               unsigned long long* __restrict__ grand) {
+  __shared__ unsigned long long s_w[PS_T / 64];
+  unsigned long long carry = 0;
+  for (long c0 = 0; c0 < nb; c0 += PS_T) {
+    const long i = c0 + threadIdx.x;
+    const unsigned long long x = i < nb ? tot[i] : 0ull;
+    unsigned long long total;
+    const unsigned long long ex = block_excl_scan_u64(x, s_w, total);
+    if (i < nb) tot[i] = carry + ex;
+    carry += total;
+  }
+  if (threadIdx.x == 0) *grand = carry;
+}
+
+__global__ __launch_bounds__(PS_T) void scan_add_u64_kernel(unsigned long long* __restrict__ out, long n,
+                                                            const unsigned long long* __restrict__ tot,
+                                                            const unsigned long long* __restrict__ grand) {
+  const long i = (long)blockIdx.x * PS_T + threadIdx.x;
+  if (i < n) out[i] += tot[i / PS_B];
+  if (i == n) out[n] = *grand;
+}
+
+// out[0..n] = exclusive prefix (out[n] = total) of in[0..n) (or of the partition flags of keys)
+static int scan_u64(const unsigned long long* in, const int* keys, long n, unsigned long long* out,
+                    unsigned long long* ws, hipStream_t stream) {
+  const long nb = (n + PS_B - 1) / PS_B;
+  if (nb > 0x7fffffffL) return -3;
+  if (nb > 0)
+    hipLaunchKernelGGL(scan_blocks_u64_kernel, dim3((unsigned)nb), dim3(PS_T), 0, stream, in, keys, n, out, ws);
+  hipLaunchKernelGGL(scan_totals_u64_kernel, dim3(1), dim3(PS_T), 0, stream, ws, nb, ws + nb);
+  hipLaunchKernelGGL(scan_add_u64_kernel, dim3((unsigned)((n + 1 + PS_T - 1) / PS_T)), dim3(PS_T), 0, stream, out, n,
+                     ws, ws + nb);
+  return srml_status();
+}
+
+// per split parent j: cnt[j] = |left| + |right|, lcnt[j] = |left|, pstart[j] = the parent's start
+__global__ __launch_bounds__(256) void part_parent_kernel(const long long* __restrict__ bounds, int nseg,
+                                                          const int* __restrict__ node_feature,
+                                                          const int* __restrict__ child_base,
+                                                          const unsigned long long* __restrict__ P,
+                                                          unsigned long long* __restrict__ cnt,
+                                                          long long* __restrict__ lcnt, long long* __restrict__ pstart) {
+  const int s = blockIdx.x * 256 + threadIdx.x;
+  if (s >= nseg || node_feature[s] < 0) return;
+  const int j = child_base[s] >> 1;
+  const unsigned long long a = P[bounds[s]], b = P[bounds[s + 1]];
+  const long long l = (long long)((b & 0xffffffffull) - (a & 0xffffffffull));
+  const long long r = (long long)((b >> 32) - (a >> 32));
+  cnt[j] = (unsigned long long)(l + r);
+  lcnt[j] = l;
+  pstart[j] = bounds[s];
+}
+
+// child bounds nb[2j] = off[j], nb[2j + 1] = off[j] + |left_j|, nb[2k] = kept total
+__global__ __launch_bounds__(256) void part_bounds_kernel(const unsigned long long* __restrict__ off, int k,
+                                                          const long long* __restrict__ lcnt,
+                                                          long long* __restrict__ nb) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j < k) {
+    nb[2 * j] = (long long)off[j];
+    nb[2 * j + 1] = (long long)off[j] + lcnt[j];
+  }
+  if (j == k) nb[2 * k] = (long long)off[k];
+}
+
+__global__ __launch_bounds__(256) void part_scatter_kernel(const int* __restrict__ keys, long total,
+                                                           const unsigned long long* __restrict__ P,
+                                                           const long long* __restrict__ pstart,
+                                                           const long long* __restrict__ nb,
+                                                           const int* __restrict__ idx, const float* __restrict__ w,
+                                                           int* __restrict__ idx_out, float* __restrict__ w_out) {
+  const long p = (long)blockIdx.x * 256 + threadIdx.x;
+  if (p >= total) return;
+  const int c = keys[p];
+  if (c == 0x7fffffff) return;
+  const int j = c >> 1;
+  const unsigned long long a = P[pstart[j]], x = P[p];
+  const long long rank = (c & 1) ? (long long)((x >> 32) - (a >> 32)) : (long long)((x & 0xffffffffull) - (a & 0xffffffffull));
+  const long long q = nb[c] + rank;
+  idx_out[q] = idx[p];
+  w_out[q] = w[p];
+}
+
+// Workspace (u64 elements) for srml_rf_partition with `total` positions and k split parents.
+SRML_API long srml_rf_partition_ws(long total, int k) {
+  return (total + 1) + ((total + PS_B - 1) / PS_B + 1) + 3L * (k + 1) + ((k + PS_B) / PS_B + 1);
+}
+
+// keys: child key per position (srml_rf_route_segments); nseg parent segments (bounds nseg + 1);
+// k split parents. Writes idx_out / w_out (kept positions, child order) and nb (2k + 1 bounds).
+SRML_API int srml_rf_partition(const int* keys, long total, const long long* bounds, int nseg,
+                               const int* node_feature, const int* child_base, int k, const int* idx, const float* w,
+                               int* idx_out, float* w_out, long long* nb, unsigned long long* ws, hipStream_t stream) {
+  if (total < 0 || k < 0 || total >= (1L << 32)) return -2;
+  unsigned long long* P = ws;                                   // total + 1
+  unsigned long long* tws = P + total + 1;                      // block totals + grand
+  const long nbt = (total + PS_B - 1) / PS_B + 1;
+  unsigned long long* cnt = tws + nbt;                          // k + 1 (scanned into offsets)
+  long long* lcnt = reinterpret_cast<long long*>(cnt + k + 1);  // k + 1
+  long long* pstart = lcnt + k + 1;                             // k + 1
+  unsigned long long* tws2 = reinterpret_cast<unsigned long long*>(pstart + k + 1);
+  if (k == 0) return (int)hipMemsetAsync(nb, 0, sizeof(long long), stream);  // every position leaves
+  int st = scan_u64(nullptr, keys, total, P, tws, stream);
+  if (st) return st;
+  if (nseg > 0)
+    hipLaunchKernelGGL(part_parent_kernel, dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, stream, bounds, nseg,
+                       node_feature, child_base, P, cnt, lcnt, pstart);
+  st = scan_u64(cnt, nullptr, k, cnt, tws2, stream);  // in place: off[0..k]
+  if (st) return st;
+  hipLaunchKernelGGL(part_bounds_kernel, dim3((unsigned)((k + 1 + 255) / 256)), dim3(256), 0, stream, cnt, k, lcnt, nb);
+  if (total > 0)
+    hipLaunchKernelGGL(part_scatter_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, keys, total, P,
+                       pstart, nb, idx, w, idx_out, w_out);
+  return srml_status();
+}
+
+// ------------------------------------------------------------------------------------------
 // per-segment node statistics (replaces cumsum-based segment sums): each block reduces a
 // contiguous chunk of positions in registers and flushes one fp64 atomic per (segment, stat)
 // it touched; chunks are sorted so a block rarely spans more than a couple of segments.

@@ -216,3 +216,125 @@ SRML_API int srml_topk_rows_f32(const float* vals, long rows, long ldv, long sli
 }
 
 SRML_API int srml_topk_kmax() { return TK_KMAX; }
+
+// ------------------------------------------------------------------------------------------
+// IVF large-k candidates (64 < k <= 1024; the k <= 64 paths keep LDS insertion lists): for every
+// (query, probe) the distances ||i||^2 - 2 q.i to each item of the probed list are written, with
+// the item's id (or list position), into the query's row of a candidate matrix at the prefix
+// offset of its earlier probes; columns past the query's candidate count are +inf / -1. One block
+// per (query, probe): the query vector is staged in LDS once, the list's items stream through
+// 64-row LDS tiles (coalesced 16-B row loads, row stride n + 1 words: conflict-free column reads)
+// and each thread forms one item's dot product. srml_topk_rows_f32 (with ids) then selects k per
+// query. qlist: optional query -> list map (all-points kNN over IVF lists: a row probes the lists
+// of its own list's probe set); without it probes are per query.
+// ------------------------------------------------------------------------------------------
+constexpr int IVC_T = 256;
+constexpr int IVC_ROWS = 64;
+
+__global__ __launch_bounds__(IVC_T) void ivf_candidates_kernel(const float* __restrict__ Q, long q0, int n, long ldq,
+                                                               const int* __restrict__ probes, int nprobe,
+                                                               const int* __restrict__ qlist,
+                                                               const long long* __restrict__ list_off,
+                                                               const float* __restrict__ items, long ldi,
+                                                               const float* __restrict__ inorm,
+                                                               const long long* __restrict__ ids, float* __restrict__ D,
+                                                               long long* __restrict__ DI, long ldd) {
+  extern __shared__ float ivc_s[];  // q[n] | tile[IVC_ROWS][n + 1]
+  float* qs = ivc_s;
+  float* tile = ivc_s + n;
+  const int tn = n + 1;
+  const long qi = q0 + blockIdx.x;  // global query (row) index
+  const int p = blockIdx.y;
+  const int* pr = probes + (long)(qlist ? qlist[qi] : qi) * nprobe;
+  const int l = pr[p];
+  // this probe's offset in the query's candidate row
+  long off = 0;
+  for (int j = 0; j < p; ++j)
+    if (pr[j] >= 0) off += list_off[pr[j] + 1] - list_off[pr[j]];
+  if (l < 0) return;
+  const long b0 = list_off[l], b1 = list_off[l + 1];
+  for (int c = threadIdx.x; c < n; c += IVC_T) qs[c] = Q[qi * ldq + c];
+  float* drow = D + (long)blockIdx.x * ldd + off;
+  long long* irow = DI + (long)blockIdx.x * ldd + off;
+  for (long r0 = b0; r0 < b1; r0 += IVC_ROWS) {
+    const int rows = (int)min((long)IVC_ROWS, b1 - r0);
+    __syncthreads();  // previous tile consumed (and qs written on the first pass)
+    for (int e = threadIdx.x; e < rows * n; e += IVC_T) {
+      const int rr = e / n, cc = e - rr * n;
+      tile[rr * tn + cc] = items[(r0 + rr) * ldi + cc];
+    }
+    __syncthreads();
+    if (threadIdx.x < rows) {
+      const float* row = tile + threadIdx.x * tn;
+      float acc = 0.f;
+      for (int c = 0; c < n; ++c) acc = fmaf(qs[c], row[c], acc);
+      const long it = r0 + threadIdx.x;
+      drow[it - b0] = inorm[it] - 2.f * acc;
+      irow[it - b0] = ids ? ids[it] : it;
+    }
+  }
+}
+
+__global__ void ivf_count_kernel(const int* __restrict__ probes, int nprobe, const int* __restrict__ qlist, long nq,
+                                 const long long* __restrict__ list_off, unsigned long long* __restrict__ cmax) {
+  const long q = (long)blockIdx.x * 256 + threadIdx.x;
+  if (q >= nq) return;
+  const int* pr = probes + (long)(qlist ? qlist[q] : q) * nprobe;
+  unsigned long long c = 0;
+  for (int j = 0; j < nprobe; ++j)
+    if (pr[j] >= 0) c += (unsigned long long)(list_off[pr[j] + 1] - list_off[pr[j]]);
+  atomicMax(cmax, c);
+}
+
+// Largest candidate count over nq queries (-> *cmax, which the caller zeroes): sizes the matrix.
+SRML_API int srml_ivf_candidate_max(const int* probes, int nprobe, const int* qlist, long nq, const long long* list_off,
+                                    unsigned long long* cmax, hipStream_t stream) {
+  if (nq <= 0) return 0;
+  hipLaunchKernelGGL(ivf_count_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, stream, probes, nprobe, qlist,
+                     nq, list_off, cmax);
+  return srml_status();
+}
+
+__global__ void row_list_kernel(const long long* __restrict__ list_off, int nlist, long N, int* __restrict__ qlist) {
+  const long r = (long)blockIdx.x * 256 + threadIdx.x;
+  if (r >= N) return;
+  int lo = 0, hi = nlist - 1;  // largest l with list_off[l] <= r
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (list_off[mid] <= r) lo = mid; else hi = mid - 1;
+  }
+  qlist[r] = lo;
+}
+
+// List of every row of a list-sorted matrix (list_off: nlist + 1 offsets covering the N rows).
+SRML_API int srml_row_list(const long long* list_off, int nlist, long N, int* qlist, hipStream_t stream) {
+  if (N <= 0 || nlist <= 0) return 0;
+  hipLaunchKernelGGL(row_list_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, stream, list_off, nlist, N, qlist);
+  return srml_status();
+}
+
+__global__ void ivf_fill_kernel(float* __restrict__ D, long long* __restrict__ DI, long total) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  D[i] = __builtin_huge_valf();
+  DI[i] = -1;
+}
+
+// Candidate matrix rows for queries [q0, q0 + nq) (row r of D / DI = query q0 + r, ldd columns,
+// ldd >= the largest candidate count of these queries; the caller sizes it).
+SRML_API int srml_ivf_candidates_f32(const float* Q, long q0, long nq, int n, long ldq, const int* probes, int nprobe,
+                                     const int* qlist, const long long* list_off, const float* items, long ldi,
+                                     const float* inorm, const long long* ids, float* D, long long* DI, long ldd,
+                                     hipStream_t stream) {
+  if (nq <= 0) return 0;
+  if (n <= 0 || nprobe <= 0 || nprobe > 65535 || nq > 0x7fffffffL || ldd <= 0) return -1;
+  const size_t shm = (size_t)(n + IVC_ROWS * (n + 1)) * sizeof(float);
+  if (shm > 160 * 1024) return -2;  // n <= ~620 dims: wider data takes the exact MFMA path
+  const long total = nq * ldd;
+  hipLaunchKernelGGL(ivf_fill_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, D, DI, total);
+  if (shm > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)ivf_candidates_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+  hipLaunchKernelGGL(ivf_candidates_kernel, dim3((unsigned)nq, (unsigned)nprobe), dim3(IVC_T), shm, stream, Q, q0, n,
+                     ldq, probes, nprobe, qlist, list_off, items, ldi, inorm, ids, D, DI, ldd);
+  return srml_status();
+}

@@ -26,7 +26,7 @@ _D = ctypes.c_double
 _F = ctypes.c_float
 
 # name -> argtypes (restype: int status, except the size queries in _LONG_RESULT)
-_LONG_RESULT = ("srml_qn_args_size", "srml_logit_residual_ws", "srml_xtv_mfma_ws")
+_LONG_RESULT = ("srml_qn_args_size", "srml_logit_residual_ws", "srml_xtv_mfma_ws", "srml_rf_partition_ws")
 SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_col_moments_f32": (_P, _L, _I, _L, _P, _P, _P),
     "srml_col_moments_f64": (_P, _L, _I, _L, _P, _P, _P),
@@ -128,6 +128,13 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_memset_async": (_P, _I, _L, _P),
     "srml_rf_predict_nodes2": (_P, _L, _L, _I, _P, _P, _I, _P, _I, _P, _P, _P),
     "srml_rf_predict": (_P, _L, _L, _P, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P),
+    "srml_rf_partition": (_P, _L, _P, _I, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P),
+    "srml_rf_partition_ws": (_L, _I),
+    "srml_ivf_candidate_max": (_P, _I, _P, _L, _P, _P, _P),
+    "srml_ivf_candidates_f32": (_P, _L, _L, _I, _L, _P, _I, _P, _P, _P, _L, _P, _P, _P, _P, _L, _P),
+    "srml_row_list": (_P, _I, _L, _P, _P),
+    "srml_cd_sweep_global_f64": (_P, _I, _L, _P, _P, _P, _P, _P, _P, _P, _I, _P),
+    "srml_logit_residual_wide_f32": (_P, _L, _I, _L, _P, _P, _L, _P, _L, _P, _P, _P),
 }
 
 _lock = threading.Lock()
@@ -187,6 +194,10 @@ def stream(device: torch.device) -> int:
 
 
 def call(name: str, *args: Any) -> None:
+    """Launch ``name`` with its declared ctypes signature. An entry point without one would get
+    ctypes' default int conversion (64-bit pointers and sizes truncated), so it is refused."""
+    if name not in SIGNATURES:
+        raise KeyError("native.call: %s has no entry in ops/native.py SIGNATURES" % name)
     fn = getattr(lib(), name)
     rc = fn(*args)
     if rc != 0:

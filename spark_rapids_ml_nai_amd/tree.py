@@ -246,7 +246,7 @@ class _RandomForestEstimator(_RandomForestClass, _EstimatorSupervised, _RandomFo
             for mp in maps:
                 p = dict(params["cuml_init"], **mp)
                 mode = p.get("split_mode", "ensemble")
-                data_parallel = mode == "data_parallel" and ctx.world_size > 1
+                data_parallel = mode == "data_parallel"  # world 1: the same path, its all-reduces are no-ops
                 n_est = int(p["n_estimators"])
                 if data_parallel:
                     n_local = n_est

@@ -341,7 +341,7 @@ def test_knn_id_offset(gpu_device):
 
 
 @pytest.mark.parametrize("n,nlist,nprobe,k", [(16, 10, 3, 10), (130, 32, 8, 5), (3, 5, 5, 64), (128, 40, 6, 10),
-                                              (64, 20, 4, 7), (33, 12, 3, 1)])
+                                              (64, 20, 4, 7), (33, 12, 3, 1), (32, 16, 4, 100), (96, 8, 2, 700)])
 def test_ivf_search(gpu_device, n, nlist, nprobe, k):
     from spark_rapids_ml_nai_amd.models.knn import build_ivf
 
@@ -363,7 +363,7 @@ def test_ivf_search(gpu_device, n, nlist, nprobe, k):
 
 
 @pytest.mark.parametrize("N,n,nlist,nprobe,k", [(3000, 16, 12, 4, 15), (5000, 128, 20, 6, 10), (700, 7, 3, 3, 64),
-                                                (2000, 130, 9, 2, 5)])
+                                                (2000, 130, 9, 2, 5), (3000, 24, 10, 3, 150), (1500, 65, 6, 4, 600)])
 def test_knn_lists(gpu_device, N, n, nlist, nprobe, k):
     """IVF-list all-points kNN tile kernel vs brute force over exactly the probed lists."""
     from spark_rapids_ml_nai_amd.models.knn_graph import ivf_tiles
@@ -524,6 +524,23 @@ def test_cd_gram(gpu_device, n):
     torch.testing.assert_close(w.cpu(), w_ref, rtol=1e-9, atol=1e-12)
     if n >= 50:
         assert (w_ref == 0).any()  # the L1 term produced exact zeros
+
+
+def test_cd_gram_wide_global_memory(gpu_device):
+    """n beyond the LDS-resident kernels: the block-cyclic global-memory sweeps run the same
+    coordinate order as the CPU cyclic sweep (same iteration count, same solution)."""
+    n = 10000
+    g = torch.Generator().manual_seed(9)
+    U = torch.randn(n, 40, generator=g, dtype=torch.float64)
+    A = U @ U.T / 40.0 + 0.5 * torch.eye(n, dtype=torch.float64)
+    b = torch.randn(n, generator=g, dtype=torch.float64) * 0.3
+    l1 = torch.full((n,), 0.05, dtype=torch.float64)
+    l2 = torch.full((n,), 0.02, dtype=torch.float64)
+    w_ref, it_ref = ops.cd_gram(A, b, l1, l2, 25, 1e-9)
+    w, it = ops.cd_gram(A.to(gpu_device), b.to(gpu_device), l1.to(gpu_device), l2.to(gpu_device), 25, 1e-9)
+    assert it == it_ref
+    torch.testing.assert_close(w.cpu(), w_ref, rtol=1e-8, atol=1e-11)
+    assert (w_ref == 0).any()
 
 
 def test_streamed_ingest_scatter_stats(gpu_device):
@@ -730,3 +747,25 @@ def test_kmeans_predict_certified_matches_exact(gpu_device, monkeypatch):
     assert got.dtype == torch.int32 and got.shape == (70000,)
     assert (got == ref).float().mean().item() > 0.9999
     assert (got == fp32).float().mean().item() > 0.9999
+
+
+@pytest.mark.parametrize("nseg,total", [(1, 5000), (37, 100000), (3000, 2_000_000)])
+def test_rf_partition_matches_stable_sort(gpu_device, nseg, total):
+    """Native prefix-count re-partition == stable sort of the child keys (positions, weights, bounds)."""
+    g = torch.Generator().manual_seed(nseg)
+    cuts = torch.sort(torch.randint(0, total + 1, (nseg - 1,), generator=g)).values
+    bounds = torch.cat([torch.zeros(1, dtype=torch.int64), cuts, torch.tensor([total])])
+    split = torch.rand(nseg, generator=g) < 0.7
+    node_feature = torch.where(split, torch.randint(0, 50, (nseg,), generator=g), torch.full((nseg,), -1)).int()
+    k = int(split.sum())
+    child_base = torch.zeros(nseg, dtype=torch.int32)
+    child_base[split] = 2 * torch.arange(k, dtype=torch.int32)
+    seg = torch.repeat_interleave(torch.arange(nseg), bounds[1:] - bounds[:-1])
+    right = torch.randint(0, 2, (total,), generator=g).int()
+    keys = torch.where(split[seg], child_base[seg] + right, torch.full((total,), 0x7FFFFFFF, dtype=torch.int32)).int()
+    idx = torch.randperm(total, generator=g).int()
+    w = torch.rand(total, generator=g)
+    ri, rw, rb = ops.rf_partition(keys, bounds, node_feature, child_base, k, idx, w)
+    di, dw, db = ops.rf_partition(keys.to(gpu_device), bounds.to(gpu_device), node_feature.to(gpu_device),
+                                  child_base.to(gpu_device), k, idx.to(gpu_device), w.to(gpu_device))
+    assert torch.equal(db.cpu(), rb) and torch.equal(di.cpu(), ri) and torch.equal(dw.cpu(), rw)

@@ -119,3 +119,33 @@ def test_sparse_logreg_matches_dense_gpu(gpu_device, multiclass):
     ms, md = _fit_pair(multiclass)
     assert abs(ms.objective - md.objective) <= 1e-6 * abs(md.objective)
     np.testing.assert_allclose(ms.coefficientMatrix.toArray(), md.coefficientMatrix.toArray(), rtol=1e-3, atol=5e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K", [4, 16, 23])
+def test_csr_multinomial_loss_grad_native(gpu_device, K):
+    """CSR softmax data term on the srml kernels (SpMM margins, residual kernel, SpMTM) for K <= 16
+    (``csr_spmm``) and K > 16 (``csr_wide``) vs the dense fp64 reference."""
+    m, n = 3000, 400
+    A, t = _csr(m, n, 0.02, torch.float32, gpu_device, seed=K)
+    D = _dense(A).float().double()
+    rng = np.random.default_rng(K)
+    y = torch.from_numpy(rng.integers(0, K, m).astype(np.float32))
+    W = torch.from_numpy(rng.standard_normal(K * n) * 0.2)
+    b = torch.from_numpy(rng.standard_normal(K) * 0.3)
+    assert ops.logistic_path(t, K) == ("csr_spmm" if K <= 16 else "csr_wide")
+    out = torch.zeros(K * n + K + 1, dtype=torch.float64, device=gpu_device)
+    ops.logistic_loss_grad(t, y.to(gpu_device), W.to(gpu_device), b.to(gpu_device), K, out)
+    Z = D @ W.view(K, n).T + b.view(1, K)
+    lse = torch.logsumexp(Z, 1)
+    Y = torch.nn.functional.one_hot(y.long(), K).double()
+    R = torch.exp(Z - lse.view(-1, 1)) - Y
+    ref = torch.cat([(R.T @ D).reshape(-1), R.sum(0), (lse - (Z * Y).sum(1)).sum().view(1)])
+    got = out.cpu()
+    scale = ref[:-1].abs().max().item()
+    assert (got[:-1] - ref[:-1]).abs().max().item() <= 2e-5 * scale + 1e-6
+    assert abs(got[-1].item() - ref[-1].item()) <= 1e-5 * abs(ref[-1].item())
+    flag = torch.ones(1, dtype=torch.int32, device=gpu_device)
+    out2 = torch.zeros_like(out)
+    ops.logistic_loss_grad(t, y.to(gpu_device), W.to(gpu_device), b.to(gpu_device), K, out2, flag)
+    assert out2.abs().max().item() == 0.0

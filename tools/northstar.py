@@ -52,8 +52,10 @@ def _estimator(name: str, world: int):
     if name == "rf":
         from spark_rapids_ml_nai_amd.classification import RandomForestClassifier
 
+        # data-parallel histogram mode (north-star config 4): every level's histograms are
+        # all-reduced; SRML_NS_RF_MODE=ensemble gives the reference's tree-split ensemble instead
         return RandomForestClassifier(numTrees=100, maxDepth=16, maxBins=128, seed=1, featuresCol="features",
-                                      labelCol="label", split_mode="data_parallel" if world > 1 else "ensemble")
+                                      labelCol="label", split_mode=os.environ.get("SRML_NS_RF_MODE", "data_parallel"))
     if name == "umap":
         from spark_rapids_ml_nai_amd.umap import UMAP
 
@@ -133,12 +135,18 @@ def main() -> None:
                 dt = float(t.item())
             rec["fit_s"] = round(dt, 3)
             rec["rows_per_s"] = round(rows / dt, 1)
+            ma = getattr(model, "_model_attributes", {}) or {}
+            rec["phases"] = {k: round(v, 4) for k, v in getattr(model, "_fit_timings", {}).items()}
+            rs = getattr(model, "_rank_stats", None)
+            if rs:
+                rec["rank0"] = rs
             if name == "kmeans":
-                rec["iters"] = int(getattr(model, "num_iters", -1) or -1)
+                rec["iters"] = int(ma.get("n_iter", getattr(model, "num_iters", -1)) or -1)
             if name == "logreg":
                 rec["iters"] = int(getattr(model, "num_iters", -1))
             if name == "rf":
                 rec["total_nodes"] = int(model.totalNumNodes)
+                rec["split_mode"] = os.environ.get("SRML_NS_RF_MODE", "data_parallel")
             if name == "umap":
                 emb = np.asarray(model.embedding_)
                 rec["finite"] = bool(np.isfinite(emb).all())
