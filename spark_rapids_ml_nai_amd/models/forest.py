@@ -38,6 +38,13 @@ from ..parallel.context import WorkerContext
 
 ROWS_PER_ITEM = 4096
 CHUNK_MAJOR_ITEMS = os.environ.get("SRML_RF_ITEM_ORDER", "chunk") == "chunk"
+# The histogram gathers from the 32-byte record layout of the bins (when a node's feature chunks
+# are dense enough, ops.rf_il_useful) at levels whose nodes hold on average less than IL_DENSITY
+# of the rows: there one record load per row beats one cache line per (row, feature), while
+# denser nodes share the lines of the feature-major columns (1M x 3000 regression trace: levels
+# 5-6 37 / 31 ms vs 63 / 53 ms, levels 2-3 23 / 39 ms feature-major vs 56 / 63 ms).
+# SRML_RF_IL_DENSITY=0 turns the record layout off.
+IL_DENSITY = float(os.environ.get("SRML_RF_IL_DENSITY", "0.03"))
 INT_MAX = 2**31 - 1
 
 
@@ -264,6 +271,12 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
     n_leaves = np.ones(n_trees, dtype=np.int64)
     fb = ops.rf_hist_fb(B, SH, regression)  # features per histogram work item (fits the LDS slab)
     nfc = (nf + fb - 1) // fb
+    # one draw of the fit's generator per call seeds every level's feature subsets (identical on
+    # the ranks of a data-parallel fit, whose generators share the seed)
+    call_seed = int(torch.randint(0, 1 << 62, (1,), generator=gen, device=dev).item())
+    bins_il = None
+    use_il = (dev.type == "cuda" and IL_DENSITY > 0 and max_depth >= 4 and ops.rf_il_useful(n, nf, fb)
+              and 3 * bins.numel() < torch.cuda.mem_get_info(dev)[0])
     # i64 fixed-point scale bounded by the heaviest tree's total bootstrap weight (no cell overflows)
     yscale = ops.rf_yscale(yv, float(tot[:, 0].max().item())) if regression and dev.type == "cuda" else None
     hist_cell = (8 if regression else 4) * nf * B * SH
@@ -292,10 +305,10 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
             if nf >= n:
                 feats = torch.arange(n, device=dev, dtype=torch.int32).repeat(C, 1)
             else:
-                # each node's feature sample in ascending feature order: chunk c of every node then
-                # covers nearby columns of the feature-major bin matrix (see the item order below)
-                feats = torch.rand((C, n), generator=gen, device=dev).argsort(1)[:, :nf].sort(1).values
-                feats = feats.to(torch.int32).contiguous()
+                # each node's feature sample in ascending feature order (selection sampling on the
+                # device): chunk c of every node then covers nearby columns of the bin matrix (see
+                # the item order below) and few 32-feature records (the record-layout gathers)
+                feats = ops.rf_sample_features(C, n, nf, call_seed ^ (depth * 1000003 + g0 * 7919 + 1), dev)
             c_start, c_cnt = bounds_h[cg], counts[cg]
             # rows per work item: ~8K blocks to fill the chip, few blocks per (node, feature chunk)
             rpi = int(min(65536, max(ROWS_PER_ITEM, (int(c_cnt.sum()) * nfc) // 8192)))
@@ -327,8 +340,13 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
                 it[:, 3] = np.tile(np.arange(nfc), tot_ch) | np.repeat(single, nfc)
             items_t = torch.from_numpy(it).to(dev, non_blocking=False)
             excl = {"multi_nodes": torch.from_numpy(np.nonzero(nch != 1)[0]).to(dev)} if dev.type == "cuda" else None
+            il = None
+            if use_il and float(c_cnt.mean()) < IL_DENSITY * m:
+                if bins_il is None:
+                    bins_il = ops.rf_interleave(bins)  # built once, at the first sparse level
+                il = bins_il
             hist = ops.rf_hist(bins, idx, yv, None, items_t, feats, C, B, SH, regression, pos_weight=wpos, fb=fb,
-                               yscale=yscale, exclusive=excl)
+                               yscale=yscale, exclusive=excl, bins_il=il)
             if data_parallel:
                 ctx.comm.allreduce(hist)
             out, _ = ops.rf_best_split(hist, B, SH, regression, crit, min_leaf, min_gain)

@@ -671,14 +671,33 @@ def rf_hist_fb(B: int, S: int, regression: bool) -> int:
     return int(fb)
 
 
+def rf_interleave(bins: torch.Tensor) -> torch.Tensor:
+    """32-byte record layout of a feature-major (n, m) uint8 bin matrix: record (g, r) holds the
+    bins of features 32g .. 32g + 31 of row r (``srml_rf_interleave_u8``); flat uint8 tensor."""
+    n, m = bins.shape
+    G = (n + 31) // 32
+    out = torch.empty(G * m * 32, dtype=torch.uint8, device=bins.device)
+    native.call("srml_rf_interleave_u8", _c(bins).data_ptr(), m, n, out.data_ptr(), native.stream(bins.device))
+    return out
+
+
+def rf_il_useful(n: int, nf: int, fb: int) -> bool:
+    """Whether a node's chunk of ``fb`` ascending sampled features (nf of n) spans few enough
+    32-feature records that the record layout halves the bin loads per row (at least)."""
+    span = fb * n / max(nf, 1)
+    return span / 32.0 + 1.0 <= fb / 2.0
+
+
 def rf_hist(bins: torch.Tensor, idx: torch.Tensor, label: torch.Tensor, wcnt: Optional[torch.Tensor],
             items: torch.Tensor, node_feats: torch.Tensor, nodes: int, B: int, S: int,
             regression: bool, pos_weight: Optional[torch.Tensor] = None, fb: Optional[int] = None,
-            yscale: Optional[float] = None, exclusive: Optional[Dict[str, torch.Tensor]] = None) -> torch.Tensor:
+            yscale: Optional[float] = None, exclusive: Optional[Dict[str, torch.Tensor]] = None,
+            bins_il: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Per-(node, feature slot, bin) statistics: uint32 class counts or fp64 (count, sum[, sumsq]).
     Weights: per row (``wcnt``, indexed by row id) or per position of ``idx`` (``pos_weight``).
     ``items`` rows are (node, row_begin, row_end, feature_chunk) with chunks of ``fb`` features
-    (default ``rf_hist_fb(B, S, regression)``)."""
+    (default ``rf_hist_fb(B, S, regression)``). ``bins_il``: the record layout of ``bins``
+    (``rf_interleave``) for the device kernel to gather from (same results)."""
     fb = rf_hist_fb(B, S, regression) if fb is None else int(fb)
     n, m = bins.shape
     nf = node_feats.shape[1]
@@ -735,13 +754,17 @@ def rf_hist(bins: torch.Tensor, idx: torch.Tensor, label: torch.Tensor, wcnt: Op
     st = native.stream(dev)
     if regression and deterministic():
         # exact i64 fixed-point cross-chunk folds, converted in place: bit-reproducible histograms
-        native.call("srml_rf_hist_fixed", bins.data_ptr(), m, idx.data_ptr(), wy.data_ptr(), _c(items).data_ptr(),
-                    int(items.shape[0]), _c(node_feats).data_ptr(), nf, B, float(yscale), fb, hist.data_ptr(), st)
+        src = bins_il if bins_il is not None else bins
+        native.call("srml_rf_hist_fixed", src.data_ptr(), m, idx.data_ptr(), wy.data_ptr(), _c(items).data_ptr(),
+                    int(items.shape[0]), _c(node_feats).data_ptr(), nf, B, float(yscale), fb, hist.data_ptr(),
+                    int(bins_il is not None), st)
         native.call("srml_rf_hist_fixed_finish", hist.data_ptr(), hist.numel(), float(yscale), st)
         return hist
-    native.call("srml_rf_hist", bins.data_ptr(), m, idx.data_ptr(), wy.data_ptr(), _c(items).data_ptr(),
+    src = bins_il if bins_il is not None else bins
+    native.call("srml_rf_hist", src.data_ptr(), m, idx.data_ptr(), wy.data_ptr(), _c(items).data_ptr(),
                 int(items.shape[0]), _c(node_feats).data_ptr(), nf, B, S, int(regression), float(yscale), fb,
-                hist.data_ptr() if not regression else None, hist.data_ptr() if regression else None, st)
+                hist.data_ptr() if not regression else None, hist.data_ptr() if regression else None,
+                int(bins_il is not None), st)
     return hist
 
 
@@ -845,6 +868,19 @@ def rf_route_segments(bins: torch.Tensor, idx: torch.Tensor, bounds: torch.Tenso
                     _c(bounds.long()).data_ptr(), int(bounds.shape[0] - 1), node_feature.data_ptr(),
                     node_bin.data_ptr(), child_base.data_ptr(), keys.data_ptr(), native.stream(bins.device))
     return keys
+
+
+def rf_sample_features(C: int, n: int, nf: int, seed: int, device: torch.device) -> torch.Tensor:
+    """(C, nf) int32: per node a uniform random subset of nf of n features, ascending
+    (``srml_rf_sample_features``, selection sampling; CPU: the same draw order in numpy)."""
+    seed &= (1 << 64) - 1
+    if device.type != "cuda":
+        rng = np.random.default_rng(seed)
+        return torch.from_numpy(np.sort(np.stack([rng.choice(n, nf, replace=False) for _ in range(C)]), 1)
+                                .astype(np.int32)) if C else torch.zeros((0, nf), dtype=torch.int32)
+    out = torch.empty((C, nf), dtype=torch.int32, device=device)
+    native.call("srml_rf_sample_features", C, n, nf, seed, out.data_ptr(), native.stream(device))
+    return out
 
 
 def rf_partition(keys: torch.Tensor, bounds: torch.Tensor, node_feature: torch.Tensor, child_base: torch.Tensor,

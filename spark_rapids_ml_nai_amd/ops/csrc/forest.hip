@@ -167,7 +167,25 @@ SRML_API int srml_rf_quantize_u8(const float* X, long m, int n, long ld, const f
 // sum, fp32 in LDS folded into the fp64 output). Two rows per thread per step: all 16 bin gathers are
 // issued before the first LDS atomic (ILP instead of a load->atomic chain per row).
 // ------------------------------------------------------------------------------------------
-template <bool REG, bool FIXED = false>
+// 32-byte record layout of the bins ("interleaved"): record (g, r) = the bins of features 32g ..
+// 32g + 31 of row r, at byte (g * m + r) * 32 (srml_rf_interleave_u8). A node's feature chunk
+// (ascending sampled features) usually falls into one or two groups, so a row costs one or two
+// 32-byte loads instead of one scattered byte gather per feature — the deep levels, where a
+// node's rows are sparse, stop paying a full cache line per (row, feature).
+__device__ __forceinline__ unsigned rec_word(const uint4& lo, const uint4& hi, int q) {
+  switch (q) {  // q is wave-uniform: scalar branches, no register indexing
+    case 0: return lo.x;
+    case 1: return lo.y;
+    case 2: return lo.z;
+    case 3: return lo.w;
+    case 4: return hi.x;
+    case 5: return hi.y;
+    case 6: return hi.z;
+    default: return hi.w;
+  }
+}
+
+template <bool REG, bool FIXED = false, bool IL = false>
 __global__ __launch_bounds__(256) void rf_hist_kernel(const unsigned char* __restrict__ bins, long m,
                                                       const int* __restrict__ idx, const float2* __restrict__ wy,
                                                       const int4* __restrict__ items, const int* __restrict__ node_feats,
@@ -190,8 +208,14 @@ __global__ __launch_bounds__(256) void rf_hist_kernel(const unsigned char* __res
   const int words = REG ? fb * B * 3 : fb * B * S;
   for (int i = threadIdx.x; i < words; i += 256) lh_u[i] = 0u;
   const unsigned char* col[FB];
+  int grp[FB], byo[FB];
 #pragma unroll
-  for (int j = 0; j < FB; ++j) col[j] = bins + (long)((j < nfb) ? node_feats[(long)node * nf + f_begin + j] : 0) * m;
+  for (int j = 0; j < FB; ++j) {
+    const int f = (j < nfb) ? node_feats[(long)node * nf + f_begin + j] : 0;
+    col[j] = bins + (long)f * m;
+    grp[j] = f >> 5;
+    byo[j] = f & 31;
+  }
   __syncthreads();
   for (int i = rb + threadIdx.x; i < re; i += 512) {
     const int i2 = i + 256;
@@ -201,10 +225,32 @@ __global__ __launch_bounds__(256) void rf_hist_kernel(const unsigned char* __res
     const float2 a1 = wy[i];
     const float2 a2 = has2 ? wy[i2] : make_float2(0.f, 0.f);
     int b1[FB], b2[FB];
+    if (IL) {
+      uint4 lo1 = make_uint4(0, 0, 0, 0), hi1 = lo1, lo2 = lo1, hi2 = lo1;
 #pragma unroll
-    for (int j = 0; j < FB; ++j) {
-      b1[j] = col[j][r1];
-      b2[j] = col[j][r2];
+      for (int j = 0; j < FB; ++j) {
+        if (j < nfb) {
+          if (j == 0 || grp[j] != grp[j - 1]) {  // sorted features: each record loaded once per row
+            const uint4* p1 = reinterpret_cast<const uint4*>(bins + ((long)grp[j] * m + r1) * 32);
+            const uint4* p2 = reinterpret_cast<const uint4*>(bins + ((long)grp[j] * m + r2) * 32);
+            lo1 = p1[0];
+            hi1 = p1[1];
+            lo2 = p2[0];
+            hi2 = p2[1];
+          }
+          const int sh = 8 * (byo[j] & 3);
+          b1[j] = (rec_word(lo1, hi1, byo[j] >> 2) >> sh) & 0xff;
+          b2[j] = (rec_word(lo2, hi2, byo[j] >> 2) >> sh) & 0xff;
+        } else {
+          b1[j] = b2[j] = 0;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < FB; ++j) {
+        b1[j] = col[j][r1];
+        b2[j] = col[j][r2];
+      }
     }
     const unsigned w1 = (unsigned)a1.x, w2 = (unsigned)a2.x;
     unsigned long long s1 = 0ull, s2 = 0ull;
@@ -270,25 +316,68 @@ SRML_API int srml_rf_hist_fb(int B, int S, int regression) {
 // wy: (weight, label) float pairs aligned with idx; items use feature chunks of `fb` features
 // (srml_rf_hist_fb). regression: S must be 2 (weighted count, weighted sum); yscale = fixed-point
 // scale for w*y
+// il != 0: `bins` is the 32-byte record layout (srml_rf_interleave_u8), else feature-major.
 SRML_API int srml_rf_hist(const unsigned char* bins, long m, const int* idx, const float* wy, const int* items,
                           int n_items, const int* node_feats, int nf, int B, int S, int regression, double yscale,
-                          int fb, unsigned* hist_u, double* hist_d, hipStream_t stream) {
+                          int fb, unsigned* hist_u, double* hist_d, int il, hipStream_t stream) {
   if (n_items <= 0) return 0;
   if (regression && S != 2) return -6;
   if (fb < 1 || fb > FB) return -7;
+  if (il && (reinterpret_cast<uintptr_t>(bins) & 15)) return -8;
   const size_t lds = (size_t)fb * B * (regression ? 3 : S) * sizeof(unsigned);
   if (lds > 160 * 1024) return -5;
-  if (lds > 64 * 1024) {
-    (void)hipFuncSetAttribute((const void*)rf_hist_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    (void)hipFuncSetAttribute((const void*)rf_hist_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  }
   const float2* w2 = reinterpret_cast<const float2*>(wy);
-  if (regression)
-    hipLaunchKernelGGL(rf_hist_kernel<true>, dim3(n_items), dim3(256), lds, stream, bins, m, idx, w2,
-                       reinterpret_cast<const int4*>(items), node_feats, nf, B, S, fb, yscale, hist_u, hist_d);
-  else
-    hipLaunchKernelGGL(rf_hist_kernel<false>, dim3(n_items), dim3(256), lds, stream, bins, m, idx, w2,
-                       reinterpret_cast<const int4*>(items), node_feats, nf, B, S, fb, 1.0, hist_u, hist_d);
+  const int4* it = reinterpret_cast<const int4*>(items);
+#define SRML_RF_HIST(RG, ILV, YS)                                                                                   \
+  do {                                                                                                             \
+    if (lds > 64 * 1024)                                                                                           \
+      (void)hipFuncSetAttribute((const void*)rf_hist_kernel<RG, false, ILV>,                                       \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                             \
+    hipLaunchKernelGGL((rf_hist_kernel<RG, false, ILV>), dim3(n_items), dim3(256), lds, stream, bins, m, idx, w2,  \
+                       it, node_feats, nf, B, S, fb, YS, hist_u, hist_d);                                          \
+  } while (0)
+  if (regression) {
+    if (il) SRML_RF_HIST(true, true, yscale);
+    else SRML_RF_HIST(true, false, yscale);
+  } else {
+    if (il) SRML_RF_HIST(false, true, 1.0);
+    else SRML_RF_HIST(false, false, 1.0);
+  }
+#undef SRML_RF_HIST
+  return srml_status();
+}
+
+// 32-byte record layout of a feature-major (n x m) uint8 bin matrix: out[(g * m + r) * 32 + j] =
+// bins[(32 g + j) * m + r] (features past n are 0). One thread per row and group: 32 coalesced
+// byte reads across the rows, two 16-B stores.
+__global__ __launch_bounds__(256) void rf_interleave_kernel(const unsigned char* __restrict__ bins, long m, int n,
+                                                            unsigned char* __restrict__ out) {
+  const long r = (long)blockIdx.x * 256 + threadIdx.x;
+  const int g = blockIdx.y;
+  if (r >= m) return;
+  unsigned w[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    unsigned v = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int f = 32 * g + 4 * q + b;
+      if (f < n) v |= (unsigned)bins[(long)f * m + r] << (8 * b);
+    }
+    w[q] = v;
+  }
+  uint4* dst = reinterpret_cast<uint4*>(out + ((long)g * m + r) * 32);
+  dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+
+SRML_API int srml_rf_interleave_u8(const unsigned char* bins, long m, int n, unsigned char* out, hipStream_t stream) {
+  if (m <= 0 || n <= 0) return 0;
+  if (reinterpret_cast<uintptr_t>(out) & 15) return -8;
+  const int G = (n + 31) / 32;
+  if (G > 65535) return -2;
+  hipLaunchKernelGGL(rf_interleave_kernel, dim3((unsigned)((m + 255) / 256), (unsigned)G), dim3(256), 0, stream, bins,
+                     m, n, out);
   return srml_status();
 }
 
@@ -300,17 +389,27 @@ SRML_API int srml_rf_hist_fb_max() { return FB; }
 // sum -> integer / yscale). Bit-identical results for any block scheduling.
 SRML_API int srml_rf_hist_fixed(const unsigned char* bins, long m, const int* idx, const float* wy, const int* items,
                                 int n_items, const int* node_feats, int nf, int B, double yscale, int fb,
-                                double* hist_d, hipStream_t stream) {
+                                double* hist_d, int il, hipStream_t stream) {
   if (n_items <= 0) return 0;
   if (fb < 1 || fb > FB) return -7;
+  if (il && (reinterpret_cast<uintptr_t>(bins) & 15)) return -8;
   const size_t lds = (size_t)fb * B * 3 * sizeof(unsigned);
   if (lds > 160 * 1024) return -5;
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute((const void*)rf_hist_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-  hipLaunchKernelGGL((rf_hist_kernel<true, true>), dim3(n_items), dim3(256), lds, stream, bins, m, idx,
-                     reinterpret_cast<const float2*>(wy), reinterpret_cast<const int4*>(items), node_feats, nf, B, 2,
-                     fb, yscale, nullptr, hist_d);
+  const float2* w2 = reinterpret_cast<const float2*>(wy);
+  const int4* it = reinterpret_cast<const int4*>(items);
+  if (il) {
+    if (lds > 64 * 1024)
+      (void)hipFuncSetAttribute((const void*)rf_hist_kernel<true, true, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((rf_hist_kernel<true, true, true>), dim3(n_items), dim3(256), lds, stream, bins, m, idx, w2, it,
+                       node_feats, nf, B, 2, fb, yscale, nullptr, hist_d);
+  } else {
+    if (lds > 64 * 1024)
+      (void)hipFuncSetAttribute((const void*)rf_hist_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds);
+    hipLaunchKernelGGL((rf_hist_kernel<true, true>), dim3(n_items), dim3(256), lds, stream, bins, m, idx, w2, it,
+                       node_feats, nf, B, 2, fb, yscale, nullptr, hist_d);
+  }
   return srml_status();
 }
 
@@ -551,6 +650,44 @@ SRML_API int srml_rf_route_segments(const unsigned char* bins, long m, const int
   if (total <= 0 || nseg <= 0) return 0;
   hipLaunchKernelGGL(rf_route_segments_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, bins, m,
                      idx, total, bounds, nseg, node_feature, node_bin, child_base, keys);
+  return srml_status();
+}
+
+// ------------------------------------------------------------------------------------------
+// Per-node feature subsets (featureSubsetStrategy): node c draws nf of n features uniformly without
+// replacement by selection sampling (Knuth's Algorithm S: feature f is taken with probability
+// needed / (n - f)), which emits them in ascending order — the order the histogram items want —
+// with no sort. Counter-based randomness (splitmix64 of seed, node, feature): reproducible, the
+// same on every rank of a data-parallel fit.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long mix64(unsigned long long x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__global__ __launch_bounds__(256) void rf_sample_features_kernel(int C, int n, int nf, unsigned long long seed,
+                                                                 int* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const unsigned long long base = mix64(seed ^ mix64((unsigned long long)c + 1));
+  int need = nf;
+  int* o = out + (long)c * nf;
+  for (int f = 0; f < n && need > 0; ++f) {
+    const double u = (double)(mix64(base + (unsigned long long)f) >> 11) * 0x1.0p-53;
+    if (u * (double)(n - f) < (double)need) {
+      o[nf - need] = f;
+      --need;
+    }
+  }
+}
+
+SRML_API int srml_rf_sample_features(int C, int n, int nf, unsigned long long seed, int* out, hipStream_t stream) {
+  if (C <= 0 || nf <= 0) return 0;
+  if (nf > n) return -2;
+  hipLaunchKernelGGL(rf_sample_features_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, stream, C, n, nf,
+                     seed, out);
   return srml_status();
 }
 

@@ -105,7 +105,8 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_cd_gram_f64": (_P, _I, _L, _P, _P, _P, _P, _I, _D, _P, _P),
     "srml_rf_quantize_u8": (_P, _L, _I, _L, _P, _I, _P, _P),
     "srml_rf_quantiles_f32": (_P, _I, _I, _I, _P, _P),
-    "srml_rf_hist": (_P, _L, _P, _P, _P, _I, _P, _I, _I, _I, _I, _D, _I, _P, _P, _P),
+    "srml_rf_hist": (_P, _L, _P, _P, _P, _I, _P, _I, _I, _I, _I, _D, _I, _P, _P, _I, _P),
+    "srml_rf_interleave_u8": (_P, _L, _I, _P, _P),
     "srml_rf_hist_fb": (_I, _I, _I),
     "srml_rf_hist_fb_max": (),
     "srml_rf_best_split": (_P, _P, _I, _I, _I, _I, _I, _I, _D, _D, _P, _P, _P),
@@ -113,7 +114,7 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_rf_route_segments": (_P, _L, _P, _L, _P, _I, _P, _P, _P, _P, _P),
     "srml_rf_node_stats": (_P, _P, _P, _L, _P, _I, _I, _I, _P, _P),
     "srml_rf_node_stats_det": (_P, _P, _P, _P, _I, _I, _I, _P, _P),
-    "srml_rf_hist_fixed": (_P, _L, _P, _P, _P, _I, _P, _I, _I, _D, _I, _P, _P),
+    "srml_rf_hist_fixed": (_P, _L, _P, _P, _P, _I, _P, _I, _I, _D, _I, _P, _I, _P),
     "srml_rf_hist_fixed_finish": (_P, _L, _D, _P),
     "srml_csr_logreg_binary_f32": (_P, _P, _P, _L, _I, _L, _P, _P, _D, _P, _P, _P, _P),
     "srml_csr_logreg_binary_f64": (_P, _P, _P, _L, _I, _L, _P, _P, _D, _P, _P, _P, _P),
@@ -128,6 +129,7 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_memset_async": (_P, _I, _L, _P),
     "srml_rf_predict_nodes2": (_P, _L, _L, _I, _P, _P, _I, _P, _I, _P, _P, _P),
     "srml_rf_predict": (_P, _L, _L, _P, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P),
+    "srml_rf_sample_features": (_I, _I, _I, ctypes.c_ulonglong, _P, _P),
     "srml_rf_partition": (_P, _L, _P, _I, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P),
     "srml_rf_partition_ws": (_L, _I),
     "srml_ivf_candidate_max": (_P, _I, _P, _L, _P, _P, _P),

@@ -291,3 +291,49 @@ def test_rf_regressor_fit_bit_reproducible(gpu_device, monkeypatch):
     pb = b.transform(df).to_numpy("prediction")
     assert np.array_equal(pa, pb)
     assert np.corrcoef(pa, y)[0, 1] > 0.9
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("regression", [False, True])
+def test_rf_hist_record_layout_identical(gpu_device, monkeypatch, regression):
+    """Histograms gathered from the 32-byte record layout (rf_interleave) equal the feature-major
+    ones exactly (classification counts; deterministic fixed-point regression sums)."""
+    if regression:
+        monkeypatch.setenv("SRML_DETERMINISTIC", "1")
+    g = torch.Generator().manual_seed(17)
+    n, m, B, nf, nodes = 70, 30000, 64, 24, 4
+    bins = torch.randint(0, B, (n, m), generator=g, dtype=torch.uint8)
+    S = 2 if regression else 3
+    y = torch.randn(m, generator=g) if regression else torch.randint(0, S, (m,), generator=g).float()
+    idx = torch.randperm(m, generator=g)[:20000].sort().values.int()
+    w = torch.randint(1, 4, (20000,), generator=g).float()
+    feats = torch.stack([torch.randperm(n, generator=g)[:nf].sort().values for _ in range(nodes)]).int()
+    fb = ops.rf_hist_fb(B, S, regression)
+    bounds = [0, 3000, 9000, 15000, 20000]
+    items = [[node, rb, min(rb + 2048, bounds[node + 1]), fc] for node in range(nodes)
+             for rb in range(bounds[node], bounds[node + 1], 2048) for fc in range((nf + fb - 1) // fb)]
+    items = torch.tensor(items, dtype=torch.int32)
+    d = lambda t: t.to(gpu_device)  # noqa: E731
+    ys = ops.rf_yscale(d(y), float(w.sum())) if regression else None
+    a = ops.rf_hist(d(bins), d(idx), d(y), None, d(items), d(feats), nodes, B, S, regression, pos_weight=d(w),
+                    fb=fb, yscale=ys)
+    il = ops.rf_interleave(d(bins))
+    assert il.numel() == ((n + 31) // 32) * m * 32
+    b = ops.rf_hist(d(bins), d(idx), d(y), None, d(items), d(feats), nodes, B, S, regression, pos_weight=d(w),
+                    fb=fb, yscale=ys, bins_il=il)
+    assert torch.equal(a, b)
+    assert ops.rf_il_useful(3000, 1000, 8) and not ops.rf_il_useful(3000, 55, 8) and ops.rf_il_useful(64, 8, 8)
+
+
+@pytest.mark.gpu
+def test_rf_sample_features_uniform_sorted(gpu_device):
+    C, n, nf = 4000, 300, 100
+    f = ops.rf_sample_features(C, n, nf, 12345, gpu_device).cpu()
+    assert f.shape == (C, nf)
+    assert bool((f[:, 1:] > f[:, :-1]).all())  # strictly ascending = distinct
+    assert int(f.min()) >= 0 and int(f.max()) < n
+    freq = torch.bincount(f.reshape(-1).long(), minlength=n).double() / C  # each feature: p = nf / n
+    assert abs(freq.mean().item() - nf / n) < 1e-9 and (freq - nf / n).abs().max().item() < 0.04
+    again = ops.rf_sample_features(C, n, nf, 12345, gpu_device).cpu()
+    other = ops.rf_sample_features(C, n, nf, 12346, gpu_device).cpu()
+    assert torch.equal(f, again) and not torch.equal(f, other)
