@@ -44,7 +44,14 @@ CHUNK_MAJOR_ITEMS = os.environ.get("SRML_RF_ITEM_ORDER", "chunk") == "chunk"
 # denser nodes share the lines of the feature-major columns (1M x 3000 regression trace: levels
 # 5-6 37 / 31 ms vs 63 / 53 ms, levels 2-3 23 / 39 ms feature-major vs 56 / 63 ms).
 # SRML_RF_IL_DENSITY=0 turns the record layout off.
-IL_DENSITY = float(os.environ.get("SRML_RF_IL_DENSITY", "0.03"))
+IL_DENSITY = float(os.environ.get("SRML_RF_IL_DENSITY", "0.12"))
+# Record-layout kernel: "wide" = one 1024-thread block per (row chunk, ~100-400 features), each
+# row's records fetched once per block (ops.rf_hist_fb_wide); "narrow" = 8-feature items.
+IL_KERNEL = os.environ.get("SRML_RF_IL_KERNEL", "wide")
+# record bytes of the wide kernel's layout: 64-B records use half of each 128-B line a sparse
+# row gather touches where 32-B records used a quarter
+WIDE_REC_BYTES = int(os.environ.get("SRML_RF_REC_BYTES", "64"))
+WIDE_ROWS_PER_ITEM = 8192
 INT_MAX = 2**31 - 1
 
 
@@ -275,7 +282,10 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
     # the ranks of a data-parallel fit, whose generators share the seed)
     call_seed = int(torch.randint(0, 1 << 62, (1,), generator=gen, device=dev).item())
     bins_il = None
-    use_il = (dev.type == "cuda" and IL_DENSITY > 0 and max_depth >= 4 and ops.rf_il_useful(n, nf, fb)
+    wide_fb = ops.rf_hist_fb_wide(B, SH, regression) if dev.type == "cuda" and IL_KERNEL == "wide" else 0
+    wide_fb = wide_fb if wide_fb > fb and ops.rf_il_useful(n, nf, min(wide_fb, nf)) else 0
+    use_il = (dev.type == "cuda" and IL_DENSITY > 0 and max_depth >= 4
+              and (wide_fb > 0 or ops.rf_il_useful(n, nf, fb))
               and 3 * bins.numel() < torch.cuda.mem_get_info(dev)[0])
     # i64 fixed-point scale bounded by the heaviest tree's total bootstrap weight (no cell overflows)
     yscale = ops.rf_yscale(yv, float(tot[:, 0].max().item())) if regression and dev.type == "cuda" else None
@@ -310,8 +320,19 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
                 # the item order below) and few 32-feature records (the record-layout gathers)
                 feats = ops.rf_sample_features(C, n, nf, call_seed ^ (depth * 1000003 + g0 * 7919 + 1), dev)
             c_start, c_cnt = bounds_h[cg], counts[cg]
-            # rows per work item: ~8K blocks to fill the chip, few blocks per (node, feature chunk)
-            rpi = int(min(65536, max(ROWS_PER_ITEM, (int(c_cnt.sum()) * nfc) // 8192)))
+            il = None
+            fb_l, nfc_l, rpi_min, blocks = fb, nfc, ROWS_PER_ITEM, 8192
+            if use_il and float(c_cnt.mean()) < IL_DENSITY * m:
+                if bins_il is None:
+                    # built once, at the first sparse level
+                    bins_il = ops.rf_interleave(bins, WIDE_REC_BYTES if wide_fb else 32)
+                il = bins_il
+                if wide_fb:
+                    # 1024-thread blocks over ~100-400 features: fewer, longer work items
+                    fb_l, rpi_min, blocks = wide_fb, WIDE_ROWS_PER_ITEM, 2048
+                    nfc_l = (nf + fb_l - 1) // fb_l
+            # rows per work item: enough blocks to fill the chip, few per (node, feature chunk)
+            rpi = int(min(65536, max(rpi_min, (int(c_cnt.sum()) * nfc_l) // blocks)))
             rpi = (rpi + 511) // 512 * 512
             nch = (c_cnt + rpi - 1) // rpi
             tot_ch = int(nch.sum())
@@ -320,7 +341,7 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
             chunk = np.arange(tot_ch) - first
             rb = c_start[node_rep] + chunk * rpi
             re = np.minimum(rb + rpi, c_start[node_rep] + c_cnt[node_rep])
-            it = np.empty((tot_ch * nfc, 4), dtype=np.int32)
+            it = np.empty((tot_ch * nfc_l, 4), dtype=np.int32)
             # single-chunk nodes own their histogram cells: plain stores, no zeroing, no atomics
             single = np.where(nch[node_rep] == 1, 1 << 30, 0).astype(np.int32)
             if CHUNK_MAJOR_ITEMS:
@@ -329,24 +350,20 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
                 # comes from HBM about once per level and the other nodes' gathers hit L2 / MALL
                 # (node-major order streamed each node's own sample: deep levels re-read the whole
                 # matrix once per node)
-                it[:, 0] = np.tile(node_rep, nfc)
-                it[:, 1] = np.tile(rb, nfc)
-                it[:, 2] = np.tile(re, nfc)
-                it[:, 3] = np.repeat(np.arange(nfc, dtype=np.int32), tot_ch) | np.tile(single, nfc)
+                it[:, 0] = np.tile(node_rep, nfc_l)
+                it[:, 1] = np.tile(rb, nfc_l)
+                it[:, 2] = np.tile(re, nfc_l)
+                it[:, 3] = np.repeat(np.arange(nfc_l, dtype=np.int32), tot_ch) | np.tile(single, nfc_l)
             else:
-                it[:, 0] = np.repeat(node_rep, nfc)
-                it[:, 1] = np.repeat(rb, nfc)
-                it[:, 2] = np.repeat(re, nfc)
-                it[:, 3] = np.tile(np.arange(nfc), tot_ch) | np.repeat(single, nfc)
+                it[:, 0] = np.repeat(node_rep, nfc_l)
+                it[:, 1] = np.repeat(rb, nfc_l)
+                it[:, 2] = np.repeat(re, nfc_l)
+                it[:, 3] = np.tile(np.arange(nfc_l), tot_ch) | np.repeat(single, nfc_l)
             items_t = torch.from_numpy(it).to(dev, non_blocking=False)
             excl = {"multi_nodes": torch.from_numpy(np.nonzero(nch != 1)[0]).to(dev)} if dev.type == "cuda" else None
-            il = None
-            if use_il and float(c_cnt.mean()) < IL_DENSITY * m:
-                if bins_il is None:
-                    bins_il = ops.rf_interleave(bins)  # built once, at the first sparse level
-                il = bins_il
-            hist = ops.rf_hist(bins, idx, yv, None, items_t, feats, C, B, SH, regression, pos_weight=wpos, fb=fb,
-                               yscale=yscale, exclusive=excl, bins_il=il)
+            hist = ops.rf_hist(bins, idx, yv, None, items_t, feats, C, B, SH, regression, pos_weight=wpos, fb=fb_l,
+                               yscale=yscale, exclusive=excl, bins_il=il, wide=il is not None and fb_l == wide_fb,
+                               rec_bytes=WIDE_REC_BYTES if wide_fb else 32)
             if data_parallel:
                 ctx.comm.allreduce(hist)
             out, _ = ops.rf_best_split(hist, B, SH, regression, crit, min_leaf, min_gain)

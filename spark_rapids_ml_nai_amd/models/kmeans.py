@@ -127,7 +127,7 @@ def init_kmeans_parallel(X: torch.Tensor, xnorm: torch.Tensor, desc: PartitionDe
             break
         C = torch.cat([C, new], 0)
     # weight every candidate by the points it attracts
-    w = torch.bincount(best_lab, minlength=C.shape[0]).double()
+    w = ops.label_counts(best_lab, C.shape[0]).double()
     ctx.comm.allreduce(w)
     if C.shape[0] <= k:
         extra = init_random(X, desc, ctx, k - C.shape[0], seed + 1) if C.shape[0] < k else None

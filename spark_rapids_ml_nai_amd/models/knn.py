@@ -114,6 +114,16 @@ def _resort(d: torch.Tensor, i: torch.Tensor) -> Tuple[torch.Tensor, torch.Tenso
     return v, i.gather(1, j)
 
 
+def _refine_sorted(Q: torch.Tensor, items: torch.Tensor, pos: torch.Tensor, metric: str
+                   ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Exact re-scored candidates sorted per query: the fused device kernel
+    (``ops.knn_refine_sort``) when it applies, else the chunked torch re-score + sort."""
+    r = ops.knn_refine_sort(Q, items, pos, inner_product=metric == "inner_product")
+    if r is not None:
+        return r
+    return _resort(_refine(Q, items, pos, metric), pos)
+
+
 def _pad_k(d: torch.Tensor, gi: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
     if d.shape[1] < k:  # fewer local items than k
         pad = k - d.shape[1]
@@ -134,7 +144,7 @@ def exact_knn(items: torch.Tensor, item_ids: torch.Tensor, queries: torch.Tensor
             d, li = ops.knn(Q, items, k, inorm=z_i, qnorm=z_q)  # d = -2 q.i
         else:
             d, li = ops.knn(Q, items, k)
-        d, li = _resort(_refine(Q, items, li, metric), li)
+        d, li = _refine_sorted(Q, items, li, metric)
         gi = torch.where(li >= 0, item_ids[li.clamp_min(0)], torch.full_like(li, -1))
         return _pad_k(d, gi, k)
 
@@ -167,11 +177,8 @@ def build_ivf(X: torch.Tensor, ids: torch.Tensor, nlist: int, seed: int = 1, ite
         sums, counts = ops.cluster_sums(T, lab, nlist)
         C = torch.where(counts.view(-1, 1) > 0, (sums / counts.clamp_min(1).double().view(-1, 1)).float(), C)
     lab, _ = ops.nearest_centroid(X, C)
-    lab = lab.long()
-    order = torch.argsort(lab, stable=True)
-    counts = torch.bincount(lab, minlength=nlist)
-    off = torch.zeros(nlist + 1, dtype=torch.int64, device=X.device)
-    off[1:] = torch.cumsum(counts, 0)
+    order, off, _ = ops.label_sort(lab, nlist)  # stable: rows keep their order inside a list
+    order = order.long()
     items = X.index_select(0, order).contiguous()
     return IVFIndex(C.contiguous(), ops.row_sqnorm(C), off, items, ops.row_sqnorm(items), ids.index_select(0, order))
 
@@ -192,7 +199,7 @@ def ivf_knn(index: Optional[IVFIndex], queries: torch.Tensor, k: int, nprobe: in
                                     qnorm=torch.zeros_like(qn))
         else:
             d, pos = ops.ivf_search(Q, probes.int(), index.list_off, index.items, index.inorm, pos_ids, k, qnorm=qn)
-        d, pos = _resort(_refine(Q, index.items, pos, metric), pos)
+        d, pos = _refine_sorted(Q, index.items, pos, metric)
         gi = torch.where(pos >= 0, index.ids[pos.clamp_min(0)], torch.full_like(pos, -1))
         return _pad_k(d, gi, k)
 

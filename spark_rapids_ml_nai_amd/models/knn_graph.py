@@ -40,6 +40,9 @@ def gather_rows(t: torch.Tensor, ctx: Any) -> torch.Tensor:
 def refine_sorted(Q: torch.Tensor, I: torch.Tensor, idx: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     """Exact squared distances q - i of the selected candidates (no ||q||^2 + ||i||^2 - 2 q.i
     cancellation), sorted ascending; missing candidates (-1) sort last at +inf."""
+    r = ops.knn_refine_sort(Q, I, idx)  # fused device kernel (k <= 64, fp32)
+    if r is not None:
+        return r
     k = idx.shape[1]
     step = max(1, (1 << 26) // max(1, k * Q.shape[1]))
     out = torch.empty(idx.shape, dtype=torch.float32, device=Q.device)
@@ -120,11 +123,9 @@ def knn_graph_ivf(X: torch.Tensor, k: int, nlist: Optional[int] = None, nprobe: 
     if world > 1:
         C = ctx.comm.broadcast(C, 0)
     lab, _ = ops.nearest_centroid(X, C)
-    lab = lab.long()
-    order = torch.argsort(lab, stable=True)
-    counts = ops.sorted_counts(lab[order], nlist)
-    off = torch.zeros(nlist + 1, dtype=torch.int64, device=X.device)
-    off[1:] = torch.cumsum(counts, 0)
+    order, off, _ = ops.label_sort(lab, nlist)  # stable counting sort by list
+    order = order.long()
+    counts = off[1:] - off[:-1]
     Xs = X.index_select(0, order).contiguous()
     xn = ops.row_sqnorm(Xs)
     # probe lists: nearest non-empty lists to each list's centroid (itself first)

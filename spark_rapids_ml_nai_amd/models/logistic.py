@@ -113,7 +113,12 @@ def logistic_fit(X: Any, y: torch.Tensor, m_total: int, ctx: WorkerContext, reg:
 
     allreduce = ctx.comm.allreduce if ctx.world_size > 1 else None
     path = ops.logistic_path(X, K)
-    res = minimize(P, theta0, evaluate, allreduce, y.device, batch=8 if not path.startswith("torch") else 2)
+    # stream-ordered device evaluations (no host sync; allocations come from the graph's pool) may
+    # be replayed from a HIP graph
+    graph_safe = path in ("fused_binary_f32", "fused_multinomial_f32", "csr_binary", "two_pass_multinomial_f32",
+                          "two_pass_binary_f32") or path.startswith("lds_binary")
+    res = minimize(P, theta0, evaluate, allreduce, y.device, batch=8 if not path.startswith("torch") else 2,
+                   graph_safe=graph_safe)
     return _result(res, base, ctx, n, K, fit_intercept, inv_sigma, path)
 
 
@@ -178,7 +183,7 @@ def logistic_stats(X: Any, y: torch.Tensor, m_total: int, ctx: WorkerContext, sp
     mx = torch.tensor([float(yl.max().item()) if yl.numel() else 0.0], dtype=torch.float64, device=y.device)
     ctx.comm.allreduce(mx, op="max")
     ncls = int(mx.item()) + 1
-    hist = torch.bincount(yl, minlength=ncls).double()[:ncls]
+    hist = ops.label_counts(yl, ncls).double()
     buf = torch.cat([s, q, hist])
     ctx.comm.allreduce(buf)
     s, q, hist = buf[:n], buf[n: 2 * n], buf[2 * n:]

@@ -26,12 +26,15 @@ search (the last accepted point is returned).
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 from typing import Callable, List, Optional
 
 import numpy as np
 import torch
 
+QN_GRAPH = os.environ.get("SRML_QN_GRAPH", "1") != "0"
+GRAPH_STATS = {"captures": 0, "replays": 0}  # observability / tests
 STATUS = {0: "running", 1: "converged (gradient)", 2: "converged (objective change)", 3: "max iterations",
           4: "line search failed"}
 F_DONE, F_STATUS, F_ITER, F_NEVAL, F_LS, F_COUNT, F_HEAD, F_STARTED, F_BRACKET = range(9)
@@ -297,7 +300,6 @@ class DeviceQN:
                     isg=self.coef[2 * N:], fl=self.flags, wb=self.wb, out=self.out)
         for k, t in ptrs.items():
             setattr(a, k, t.data_ptr())
-        import os
 
         if os.environ.get("SRML_QN_PROBE") == "1":  # per-section wall-clock stamps of the step kernel
             self.probe = torch.zeros(16, dtype=torch.int64, device=device)
@@ -338,11 +340,13 @@ def _comm_poll(allreduce: Optional[Callable]) -> Optional[Callable[[], None]]:
 def minimize(P: QNProblem, theta0: np.ndarray, evaluate: Callable[[torch.Tensor, torch.Tensor, Optional[torch.Tensor],
                                                                    torch.Tensor], None],
              allreduce: Optional[Callable[[torch.Tensor], None]], device: torch.device,
-             batch: int = 8) -> dict:
+             batch: int = 8, graph_safe: bool = False) -> dict:
     """Run the QN iteration. ``evaluate(w, b, flag, out)`` must ADD the summed data-term
     [grad_w (K*n) | grad_b (K) | loss] of this rank's rows at (w, b) into ``out`` (device
     tensors; ``flag`` is the device done-flag it may use to early-exit, None on the host path).
-    ``allreduce(out)`` sums ``out`` over ranks in place (None for one rank).
+    ``allreduce(out)`` sums ``out`` over ranks in place (None for one rank). ``graph_safe``: the
+    evaluation is stream-ordered device work only (no host sync, no allocation), so a one-rank fit
+    may capture the batch in a HIP graph (``SRML_QN_GRAPH=0`` disables).
 
     Returns {theta, f, iter, n_evals, status}.
     """
@@ -368,12 +372,40 @@ def minimize(P: QNProblem, theta0: np.ndarray, evaluate: Callable[[torch.Tensor,
     evals = 0
     stream = torch.cuda.current_stream(device)
     j = 0
-    while evals < cap:
+
+    def run_batch() -> None:
         for _ in range(batch):
             evaluate(q.w_dev, q.b_dev, flag, q.out)
             if allreduce is not None:
                 allreduce(q.out)
             q.step()
+
+    # one-rank fits on a single-launch evaluation replay the batch as ONE HIP graph: 2 x batch
+    # kernels with no per-launch host work (the first batch runs eagerly: one-time kernel set-up)
+    graph = None
+    use_graph = graph_safe and allreduce is None and QN_GRAPH
+    while evals < cap:
+        if graph is not None:
+            graph.replay()
+            GRAPH_STATS["replays"] += 1
+        else:
+            run_batch()
+            if use_graph and evals + batch < cap:
+                # raw capture on a side stream (torch.cuda.graph's context manager also runs
+                # gc.collect + empty_cache: milliseconds inside the fit)
+                graph = torch.cuda.CUDAGraph()
+                side = torch.cuda.Stream(device)
+                side.wait_stream(stream)
+                with torch.cuda.stream(side):
+                    graph.capture_begin()
+                    try:
+                        run_batch()
+                    finally:
+                        graph.capture_end()
+                stream.wait_stream(side)
+                GRAPH_STATS["captures"] += 1
+                # capture records without running: the captured batch is still to be executed
+                # (replayed at the top of the next pass)
         evals += batch
         slot = host_flag[j % 2: j % 2 + 1]
         slot.copy_(flag, non_blocking=True)

@@ -54,6 +54,9 @@ def knn_graph(Q: torch.Tensor, I: torch.Tensor, k: int) -> Tuple[torch.Tensor, t
     inorm = ops.row_sqnorm(I)
     d2, idx = ops.knn(Q, I, k, inorm=inorm)
     # refine the selected distances directly to avoid expansion cancellation
+    r = ops.knn_refine_sort(Q, I, idx)  # fused device kernel (k <= 64, fp32)
+    if r is not None:
+        return torch.sqrt(r[0].clamp_min(0)), r[1]
     step = max(1, (1 << 26) // max(1, k * Q.shape[1]))
     out = torch.empty_like(d2)
     for s in range(0, Q.shape[0], step):

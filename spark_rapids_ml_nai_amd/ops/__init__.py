@@ -555,6 +555,39 @@ def kmeanspp_gram(G: torch.Tensor, w: torch.Tensor, k: int, seed: int, trials: O
     return torch.tensor(picks, dtype=torch.long, device=G.device)
 
 
+def label_sort(labels: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Stable grouping of rows by label in [0, k): (perm int32 — row ids in (label, row) order,
+    off int64 (k + 1) — start of every label's run, sorted labels int32). Device: counting sort
+    (``srml_label_sort``: per-tile LDS histograms, one scan, ballot-ranked stable scatter; no
+    library sort, no host sync). Rows with labels outside [0, k) trail after off[k]."""
+    m = labels.shape[0]
+    dev = labels.device
+    lab = _c(labels.to(torch.int32))
+    if not lab.is_cuda or k > int(native.lib().srml_label_sort_kmax()):
+        slab, perm = torch.sort(lab, stable=True)
+        off = torch.searchsorted(slab, torch.arange(k + 1, device=dev, dtype=slab.dtype)).long()
+        return perm.to(torch.int32), off, slab
+    perm = torch.empty(m, dtype=torch.int32, device=dev)
+    slab = torch.empty(m, dtype=torch.int32, device=dev)
+    off = torch.empty(k + 1, dtype=torch.int64, device=dev)
+    ws = torch.empty(int(native.lib().srml_label_sort_ws(m, k)), dtype=torch.int64, device=dev)
+    native.call("srml_label_sort", lab.data_ptr(), m, int(k), perm.data_ptr(), slab.data_ptr(), off.data_ptr(),
+                ws.data_ptr(), native.stream(dev))
+    return perm, off, slab
+
+
+def label_counts(labels: torch.Tensor, k: int) -> torch.Tensor:
+    """int64 counts of labels 0..k-1 (others ignored) without a host read-back (``torch.bincount``
+    syncs on the maximum): per-block LDS histograms + one u64 atomic per (block, label)."""
+    lab = _c(labels.to(torch.int32))
+    if not lab.is_cuda or k > int(native.lib().srml_label_sort_kmax()) + 1:
+        ok = lab[(lab >= 0) & (lab < k)].long()
+        return torch.bincount(ok, minlength=k)[:k]
+    counts = torch.zeros(k, dtype=torch.int64, device=lab.device)
+    native.call("srml_label_counts", lab.data_ptr(), lab.shape[0], int(k), counts.data_ptr(), native.stream(lab.device))
+    return counts
+
+
 def sorted_counts(sorted_labels: torch.Tensor, k: int) -> torch.Tensor:
     """int64 counts of labels 0..k-1 from an ascending label vector: segment boundaries by binary
     search (no atomics, no host synchronisation - torch.bincount reads the maximum back first)."""
@@ -575,10 +608,8 @@ def cluster_sums(X: torch.Tensor, labels: torch.Tensor, k: int) -> Tuple[torch.T
     lab = _c(labels.to(torch.int32))
     if X.dtype == torch.float64 or deterministic():
         # label-sorted segments, one block per (cluster, column chunk), fixed order, no atomics
-        slab, perm = torch.sort(lab, stable=True)
-        counts = sorted_counts(slab, k)
-        off = torch.zeros(k + 1, dtype=torch.int64, device=X.device)
-        torch.cumsum(counts, 0, out=off[1:])
+        perm, off, _ = label_sort(lab, k)
+        counts = off[1:] - off[:-1]
         sums = torch.empty((k, n), dtype=torch.float64, device=X.device)
         # split every segment so (clusters x column chunks x splits) covers the chip; the
         # partials are folded in split order (deterministic)
@@ -586,7 +617,7 @@ def cluster_sums(X: torch.Tensor, labels: torch.Tensor, k: int) -> Tuple[torch.T
         splits = int(max(1, min(64, m // max(1, k * 256), (4096 + cblocks - 1) // cblocks)))
         ws = torch.empty(splits * k * n, dtype=torch.float64, device=X.device) if splits > 1 else None
         name = "srml_kmeans_segment_sums_f64" if X.dtype == torch.float64 else "srml_kmeans_segment_sums_f32"
-        native.call(name, X.data_ptr(), m, n, X.stride(0), _c(perm.to(torch.int32)).data_ptr(), off.data_ptr(), k,
+        native.call(name, X.data_ptr(), m, n, X.stride(0), perm.data_ptr(), off.data_ptr(), k,
                     sums.data_ptr(), splits, ws.data_ptr() if ws is not None else None, native.stream(X.device))
         return sums, counts
     counts = torch.zeros(k, dtype=torch.int32, device=X.device)
@@ -597,13 +628,11 @@ def cluster_sums(X: torch.Tensor, labels: torch.Tensor, k: int) -> Tuple[torch.T
                     None, counts.data_ptr(), st)
         return sums, counts.long()
     # large k*n: visit rows in label-sorted order (segment sums, ~(m/256 + k) * n fp64 atomics)
-    slab, perm = torch.sort(lab)
-    slab = slab.to(torch.int32)
-    perm = perm.to(torch.int32)
+    perm, off, slab = label_sort(lab, k)
     sums = torch.zeros((k, n), dtype=torch.float64, device=X.device)
     native.call("srml_kmeans_accumulate_sorted_f32", X.data_ptr(), m, n, X.stride(0), perm.data_ptr(),
                 slab.data_ptr(), sums.data_ptr(), st)
-    return sums, sorted_counts(slab, k)
+    return sums, off[1:] - off[:-1]
 
 
 # ------------------------------------------------------------------------------------------
@@ -671,13 +700,22 @@ def rf_hist_fb(B: int, S: int, regression: bool) -> int:
     return int(fb)
 
 
-def rf_interleave(bins: torch.Tensor) -> torch.Tensor:
-    """32-byte record layout of a feature-major (n, m) uint8 bin matrix: record (g, r) holds the
-    bins of features 32g .. 32g + 31 of row r (``srml_rf_interleave_u8``); flat uint8 tensor."""
+def rf_hist_fb_wide(B: int, S: int, regression: bool) -> int:
+    """Features per work item of the wide record-layout histogram (``srml_rf_hist_wide_fb``): the
+    1024-thread block's LDS slab (fb * B * S' words + feature metadata) within 150 KiB."""
+    per = B * (3 if regression else S) * 4 + 4
+    return int(min(512, (150 * 1024 - 64) // max(per, 1)))
+
+
+def rf_interleave(bins: torch.Tensor, rec_bytes: int = 32) -> torch.Tensor:
+    """Record layout of a feature-major (n, m) uint8 bin matrix: record (g, r) holds the bins of
+    features R g .. R g + R - 1 of row r, R = ``rec_bytes`` (32: the 8-feature item kernel; 32 or
+    64: the wide kernel) (``srml_rf_interleave_u8``); flat uint8 tensor."""
     n, m = bins.shape
-    G = (n + 31) // 32
-    out = torch.empty(G * m * 32, dtype=torch.uint8, device=bins.device)
-    native.call("srml_rf_interleave_u8", _c(bins).data_ptr(), m, n, out.data_ptr(), native.stream(bins.device))
+    G = (n + rec_bytes - 1) // rec_bytes
+    out = torch.empty(G * m * rec_bytes, dtype=torch.uint8, device=bins.device)
+    native.call("srml_rf_interleave_u8", _c(bins).data_ptr(), m, n, int(rec_bytes), out.data_ptr(),
+                native.stream(bins.device))
     return out
 
 
@@ -692,12 +730,16 @@ def rf_hist(bins: torch.Tensor, idx: torch.Tensor, label: torch.Tensor, wcnt: Op
             items: torch.Tensor, node_feats: torch.Tensor, nodes: int, B: int, S: int,
             regression: bool, pos_weight: Optional[torch.Tensor] = None, fb: Optional[int] = None,
             yscale: Optional[float] = None, exclusive: Optional[Dict[str, torch.Tensor]] = None,
-            bins_il: Optional[torch.Tensor] = None) -> torch.Tensor:
+            bins_il: Optional[torch.Tensor] = None, wide: bool = False, rec_bytes: int = 32) -> torch.Tensor:
     """Per-(node, feature slot, bin) statistics: uint32 class counts or fp64 (count, sum[, sumsq]).
     Weights: per row (``wcnt``, indexed by row id) or per position of ``idx`` (``pos_weight``).
     ``items`` rows are (node, row_begin, row_end, feature_chunk) with chunks of ``fb`` features
     (default ``rf_hist_fb(B, S, regression)``). ``bins_il``: the record layout of ``bins``
-    (``rf_interleave``) for the device kernel to gather from (same results)."""
+    (``rf_interleave``) for the device kernel to gather from (same results); ``wide``: the
+    1024-thread record-layout kernel with chunks of ``fb = rf_hist_fb_wide(...)`` features, on
+    records of ``rec_bytes`` (the value ``bins_il`` was built with)."""
+    if wide and fb is None:
+        fb = rf_hist_fb_wide(B, S, regression)
     fb = rf_hist_fb(B, S, regression) if fb is None else int(fb)
     n, m = bins.shape
     nf = node_feats.shape[1]
@@ -752,6 +794,17 @@ def rf_hist(bins: torch.Tensor, idx: torch.Tensor, label: torch.Tensor, wcnt: Op
     else:
         yscale = 1.0
     st = native.stream(dev)
+    if wide:
+        if bins_il is None:
+            raise ValueError("the wide histogram kernel reads the record layout: pass bins_il")
+        fixed = bool(regression and deterministic())
+        native.call("srml_rf_hist_wide", bins_il.data_ptr(), m, idx.data_ptr(), wy.data_ptr(), _c(items).data_ptr(),
+                    int(items.shape[0]), _c(node_feats).data_ptr(), nf, B, S, int(regression), float(yscale), fb,
+                    int(fixed), int(rec_bytes), hist.data_ptr() if not regression else None,
+                    hist.data_ptr() if regression else None, st)
+        if fixed:
+            native.call("srml_rf_hist_fixed_finish", hist.data_ptr(), hist.numel(), float(yscale), st)
+        return hist
     if regression and deterministic():
         # exact i64 fixed-point cross-chunk folds, converted in place: bit-reproducible histograms
         src = bins_il if bins_il is not None else bins
@@ -1398,6 +1451,48 @@ def umap_smooth_knn(dist: torch.Tensor, idx: torch.Tensor, k: float, local_conne
     return sigma, rho, w
 
 
+def knn_refine_sort(Q: torch.Tensor, X: torch.Tensor, pos: torch.Tensor, inner_product: bool = False
+                    ) -> Optional[Tuple[torch.Tensor, torch.Tensor]]:
+    """Exact distances of each query's selected candidate rows ``pos`` (int64, -1 = none) of X —
+    squared euclidean, or -2 q.x for ``inner_product`` — sorted ascending per row (ties keep the
+    candidate order; missing candidates last at +inf): (d fp32, pos int64), both (mq, k).
+    ``srml_knn_refine_sort_f32`` (one wave per query, no gathered copy of the rows) for fp32
+    device data with k <= 64 and n <= 1024; None otherwise (the caller keeps its torch path)."""
+    mq, k = pos.shape
+    n = Q.shape[1]
+    if (not Q.is_cuda or Q.dtype != torch.float32 or X.dtype != torch.float32 or k < 1 or k > 64
+            or n > 1024 or n < 1 or Q.stride(1) != 1 or X.stride(1) != 1):
+        return None
+    p = _c(pos.to(torch.int64))
+    d = torch.empty((mq, k), dtype=torch.float32, device=Q.device)
+    po = torch.empty((mq, k), dtype=torch.int64, device=Q.device)
+    native.call("srml_knn_refine_sort_f32", Q.data_ptr(), mq, n, Q.stride(0), X.data_ptr(), X.stride(0), p.data_ptr(),
+                k, p.stride(0), int(bool(inner_product)), d.data_ptr(), po.data_ptr(), native.stream(Q.device))
+    return d, po
+
+
+def radix_sort_pairs(keys: torch.Tensor, vals: torch.Tensor, key_bits: int = 64) -> None:
+    """In-place stable ascending sort of (int64 key, 32-bit value) pairs by the low ``key_bits``
+    bits of the keys (non-negative, < 2^key_bits): ``srml_radix_sort_u64``, 8-bit LSD passes
+    (tile histograms, one scan, ballot-multisplit stable scatter); torch.sort on the CPU."""
+    n = keys.shape[0]
+    assert keys.dtype == torch.int64 and vals.element_size() == 4 and vals.shape[0] == n
+    assert keys.is_contiguous() and vals.is_contiguous(), "sorted in place: contiguous tensors"
+    if n <= 1:
+        return
+    if not keys.is_cuda:
+        k2, order = torch.sort(keys, stable=True)
+        keys.copy_(k2)
+        vals.copy_(vals[order])
+        return
+    dev = keys.device
+    ka = torch.empty_like(keys)
+    va = torch.empty_like(vals)
+    ws = torch.empty(int(native.lib().srml_radix_sort_ws(n)), dtype=torch.int64, device=dev)
+    native.call("srml_radix_sort_u64", keys.data_ptr(), vals.data_ptr(), ka.data_ptr(), va.data_ptr(), n,
+                int(key_bits), ws.data_ptr(), native.stream(dev))
+
+
 def umap_fuzzy_union_knn(idx: torch.Tensor, w: torch.Tensor, mix: float = 1.0
                          ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """Fuzzy union of the kNN membership matrix A (row i: neighbours idx[i], weights w[i]):
@@ -1405,14 +1500,17 @@ def umap_fuzzy_union_knn(idx: torch.Tensor, w: torch.Tensor, mix: float = 1.0
     m, kk = idx.shape
     ix = _c(idx.long())
     wv = _c(w.float())
-    keys = torch.empty(2 * m * kk, dtype=torch.int64, device=ix.device)
-    vals = torch.empty(2 * m * kk, dtype=torch.float32, device=ix.device)
+    dev = ix.device
+    keys = torch.empty(2 * m * kk, dtype=torch.int64, device=dev)
+    vals = torch.empty(2 * m * kk, dtype=torch.float32, device=dev)
+    kept = torch.zeros(1, dtype=torch.int64, device=dev)
     native.call("srml_umap_fuzzy_union_knn", ix.data_ptr(), wv.data_ptr(), m, kk, kk, float(mix), keys.data_ptr(),
-                vals.data_ptr(), native.stream(ix.device))
-    keep = keys >= 0
-    keys, vals = keys[keep], vals[keep]
-    keys, order = torch.sort(keys)
-    return keys // m, keys % m, vals[order]
+                vals.data_ptr(), kept.data_ptr(), native.stream(dev))
+    # absent entries carry key m*m: after the (row, col) sort they trail the kept ones
+    radix_sort_pairs(keys, vals, max(1, int(m * m).bit_length()))
+    nk = int(kept.item())
+    keys = keys[:nk]
+    return keys // m, keys % m, vals[:nk]
 
 
 def umap_epoch(head: torch.Tensor, tail: torch.Tensor, eps: torch.Tensor, next_sample: torch.Tensor,

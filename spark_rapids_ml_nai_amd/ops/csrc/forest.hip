@@ -196,7 +196,7 @@ __global__ __launch_bounds__(256) void rf_hist_kernel(const unsigned char* __res
   //   [feature][bin]. Integer LDS atomics: ds_add_f32 issues ~50x slower than ds_add_u32 on
   //   gfx950 (SQ_WAIT_INST_LDS), and the 2^-38·max|y| fixed-point step is finer than fp32.
   extern __shared__ __attribute__((aligned(16))) unsigned lh_u[];
-  unsigned long long* lh_s = reinterpret_cast<unsigned long long*>(lh_u + fb * B);
+  unsigned long long* lh_s = reinterpret_cast<unsigned long long*>(lh_u + ((fb * B + 1) & ~1));  // 8-B aligned
   const int4 it = items[blockIdx.x];
   // item.w = feature chunk | RF_ITEM_EXCLUSIVE: this item is its node's only row chunk, so it owns
   // its histogram cells outright (plain stores of every cell, zeros included; the caller does not
@@ -205,7 +205,7 @@ __global__ __launch_bounds__(256) void rf_hist_kernel(const unsigned char* __res
   const int node = it.x, rb = it.y, re = it.z, fc = it.w & 0x3fffffff;
   const int f_begin = fc * fb;
   const int nfb = min(fb, nf - f_begin);
-  const int words = REG ? fb * B * 3 : fb * B * S;
+  const int words = REG ? ((fb * B + 1) & ~1) + 2 * fb * B : fb * B * S;
   for (int i = threadIdx.x; i < words; i += 256) lh_u[i] = 0u;
   const unsigned char* col[FB];
   int grp[FB], byo[FB];
@@ -324,7 +324,7 @@ SRML_API int srml_rf_hist(const unsigned char* bins, long m, const int* idx, con
   if (regression && S != 2) return -6;
   if (fb < 1 || fb > FB) return -7;
   if (il && (reinterpret_cast<uintptr_t>(bins) & 15)) return -8;
-  const size_t lds = (size_t)fb * B * (regression ? 3 : S) * sizeof(unsigned);
+  const size_t lds = ((size_t)fb * B * (regression ? 3 : S) + 1) * sizeof(unsigned);
   if (lds > 160 * 1024) return -5;
   const float2* w2 = reinterpret_cast<const float2*>(wy);
   const int4* it = reinterpret_cast<const int4*>(items);
@@ -347,37 +347,221 @@ SRML_API int srml_rf_hist(const unsigned char* bins, long m, const int* idx, con
   return srml_status();
 }
 
+// ------------------------------------------------------------------------------------------
+// Wide record-layout histogram for sparse (deep) levels: a block of 1024 threads owns up to fbw
+// (~100) of its node's sampled features at once (LDS slab sized to 150 KiB), so each row's
+// 32-byte bin records are fetched ONCE per ~100 features instead of once per 8-feature item —
+// the row's bytes cross L2 about once per level instead of ~3x (measured: 8-feature record
+// items read ~130 GB per 1M x 3000 regression level, L2/MALL-bound at ~65 ms). The feature
+// metadata (record group, byte) sits in LDS; the group is made wave-uniform (readfirstlane), so
+// the "new record?" test and the byte pick are scalar branches. Same cells, same fold as
+// rf_hist_kernel.
+// ------------------------------------------------------------------------------------------
+constexpr int RHW_T = 1024;
+
+// byte o (wave-uniform) of a record held as four 16-B pieces: scalar branches pick piece and word
+__device__ __forceinline__ int rec_pick(uint4 a, uint4 b, uint4 c, uint4 d, int o) {
+  const int t = o >> 4;
+  const uint4 piece = t == 0 ? a : t == 1 ? b : t == 2 ? c : d;
+  const int wq = (o >> 2) & 3;
+  const unsigned word = wq == 0 ? piece.x : wq == 1 ? piece.y : wq == 2 ? piece.z : piece.w;
+  return (int)((word >> (8 * (o & 3))) & 0xff);
+}
+
+template <bool REG, bool FIXED, int RB>
+__global__ __launch_bounds__(RHW_T) void rf_hist_wide_kernel(const unsigned char* __restrict__ rec, long m,
+                                                              const int* __restrict__ idx,
+                                                              const float2* __restrict__ wy,
+                                                              const int4* __restrict__ items,
+                                                              const int* __restrict__ node_feats, int nf, int B, int S,
+                                                              int fbw, double yscale, unsigned* __restrict__ hist_u,
+                                                              double* __restrict__ hist_d) {
+  extern __shared__ __attribute__((aligned(16))) unsigned hw_u[];
+  const int4 it = items[blockIdx.x];
+  const bool excl = (it.w >> 30) & 1;
+  const int node = it.x, rb = it.y, re = it.z, fc = it.w & 0x3fffffff;
+  const int f_begin = fc * fbw;
+  const int nfb = min(fbw, nf - f_begin);
+  // LDS: [grp | byo] shorts for fbw features, then counts (u32) and, for regression, u64 sums
+  short* s_grp = reinterpret_cast<short*>(hw_u);
+  short* s_byo = s_grp + fbw;
+  unsigned* cnt = hw_u + ((2 * fbw * (int)sizeof(short) + 15) / 16) * 4;
+  const int cntw = (fbw * B + 1) & ~1;  // u64 sums stay 8-byte aligned for any B
+  unsigned long long* sum = reinterpret_cast<unsigned long long*>(cnt + cntw);
+  const int words = REG ? cntw + 2 * fbw * B : fbw * B * S;
+  for (int i = threadIdx.x; i < words; i += RHW_T) cnt[i] = 0u;
+  for (int j = threadIdx.x; j < fbw; j += RHW_T) {
+    const int f = j < nfb ? node_feats[(long)node * nf + f_begin + j] : 0;
+    s_grp[j] = (short)(f / RB);
+    s_byo[j] = (short)(f % RB);
+  }
+  __syncthreads();
+  // two rows per thread and the next record group prefetched while the current one is binned:
+  // four record loads in flight per lane instead of one dependent load per group
+  for (int i = rb + threadIdx.x; i < re; i += 2 * RHW_T) {
+    const int i2 = i + RHW_T;
+    const bool has2 = i2 < re;
+    const int r1 = idx[i];
+    const int r2 = has2 ? idx[i2] : r1;
+    const float2 a1 = wy[i];
+    const float2 a2 = has2 ? wy[i2] : make_float2(0.f, 0.f);
+    const unsigned w1 = (unsigned)a1.x, w2 = (unsigned)a2.x;
+    unsigned long long s1 = 0ull, s2 = 0ull;
+    if (REG) {
+      s1 = (unsigned long long)(long long)rint((double)a1.x * (double)a1.y * yscale);
+      s2 = (unsigned long long)(long long)rint((double)a2.x * (double)a2.y * yscale);
+    }
+    const int c1 = REG ? 0 : (int)a1.y, c2 = REG ? 0 : (int)a2.y;
+    const uint4 z4 = make_uint4(0, 0, 0, 0);
+    uint4 qa1 = z4, qb1 = z4, qc1 = z4, qd1 = z4, qa2 = z4, qb2 = z4, qc2 = z4, qd2 = z4;
+    uint4 na1 = z4, nb1 = z4, nc1 = z4, nd1 = z4, na2 = z4, nb2 = z4, nc2 = z4, nd2 = z4;
+#define SRML_REC_LOAD(A, Bq, C, D, G, R)                                                    \
+  do {                                                                                     \
+    const uint4* p_ = reinterpret_cast<const uint4*>(rec + ((long)(G) * m + (R)) * RB);    \
+    A = p_[0];                                                                             \
+    Bq = p_[1];                                                                            \
+    if (RB == 64) {                                                                        \
+      C = p_[2];                                                                           \
+      D = p_[3];                                                                           \
+    }                                                                                      \
+  } while (0)
+    int j = 0;
+    int g = __builtin_amdgcn_readfirstlane((int)s_grp[0]);
+    SRML_REC_LOAD(qa1, qb1, qc1, qd1, g, r1);
+    SRML_REC_LOAD(qa2, qb2, qc2, qd2, g, r2);
+    while (j < nfb) {  // one trip per record group of the item's (ascending) features
+      int je = j + 1;
+      while (je < nfb && __builtin_amdgcn_readfirstlane((int)s_grp[je]) == g) ++je;
+      const int gn = je < nfb ? __builtin_amdgcn_readfirstlane((int)s_grp[je]) : g;
+      if (je < nfb) {
+        SRML_REC_LOAD(na1, nb1, nc1, nd1, gn, r1);
+        SRML_REC_LOAD(na2, nb2, nc2, nd2, gn, r2);
+      }
+      for (int jj = j; jj < je; ++jj) {
+        const int o = __builtin_amdgcn_readfirstlane((int)s_byo[jj]);
+        const int b1 = rec_pick(qa1, qb1, qc1, qd1, o), b2 = rec_pick(qa2, qb2, qc2, qd2, o);
+        if (REG) {
+          atomicAdd(&cnt[jj * B + b1], w1);
+          atomicAdd(&sum[jj * B + b1], s1);
+          if (w2) {
+            atomicAdd(&cnt[jj * B + b2], w2);
+            atomicAdd(&sum[jj * B + b2], s2);
+          }
+        } else {
+          atomicAdd(&cnt[(jj * S + c1) * B + b1], w1);
+          if (w2) atomicAdd(&cnt[(jj * S + c2) * B + b2], w2);
+        }
+      }
+      if (je < nfb) {
+        qa1 = na1; qb1 = nb1; qc1 = nc1; qd1 = nd1;
+        qa2 = na2; qb2 = nb2; qc2 = nc2; qd2 = nd2;
+      }
+      j = je;
+      g = gn;
+    }
+#undef SRML_REC_LOAD
+  }
+  __syncthreads();
+  const long out_base = ((long)node * nf + f_begin) * B * S;
+  const int valid_cells = nfb * B * S;
+  const double inv = 1.0 / yscale;
+  for (int i = threadIdx.x; i < valid_cells; i += RHW_T) {
+    const int j = i / (B * S), rem = i % (B * S), b = rem / S, st = rem % S;
+    if (REG && FIXED) {
+      const unsigned long long q = st == 0 ? (unsigned long long)cnt[j * B + b] : sum[j * B + b];
+      unsigned long long* cell = reinterpret_cast<unsigned long long*>(hist_d) + out_base + i;
+      if (excl) *cell = q;
+      else if (q) atomicAdd(cell, q);
+    } else if (REG) {
+      const double v = st == 0 ? (double)cnt[j * B + b] : (double)(long long)sum[j * B + b] * inv;
+      if (excl) hist_d[out_base + i] = v;
+      else if (v != 0.0) atomicAdd(&hist_d[out_base + i], v);
+    } else {
+      const unsigned v = cnt[(j * S + st) * B + b];
+      if (excl) hist_u[out_base + i] = v;
+      else if (v) atomicAdd(&hist_u[out_base + i], v);
+    }
+  }
+}
+
+// Features per item of the wide kernel for (B, S): the LDS slab (metadata + fbw * B * S' words)
+// within 150 KiB (S' = 3 for regression: count + 64-bit fixed-point sum).
+SRML_API int srml_rf_hist_wide_fb(int B, int S, int regression) {
+  const long per = (long)B * (regression ? 3 : S) * (long)sizeof(unsigned) + 2 * (long)sizeof(short);
+  const long fbw = (150L * 1024 - 64) / (per > 0 ? per : 1);
+  return (int)(fbw > 512 ? 512 : fbw);
+}
+
+// items: {node, row_begin, row_end, feature chunk (of fbw features) | exclusive << 30} on the
+// record layout `rec` (srml_rf_interleave_u8). fixed: deterministic i64 cells (regression).
+SRML_API int srml_rf_hist_wide(const unsigned char* rec, long m, const int* idx, const float* wy, const int* items,
+                               int n_items, const int* node_feats, int nf, int B, int S, int regression, double yscale,
+                               int fbw, int fixed, int rb, unsigned* hist_u, double* hist_d, hipStream_t stream) {
+  if (n_items <= 0) return 0;
+  if (regression && S != 2) return -6;
+  if (fbw < 1 || (reinterpret_cast<uintptr_t>(rec) & 15)) return -7;
+  if (rb != 32 && rb != 64) return -2;
+  const size_t lds = (size_t)((2 * fbw * sizeof(short) + 15) / 16) * 16 +
+                     ((size_t)fbw * B * (regression ? 3 : S) + 1) * sizeof(unsigned);
+  if (lds > 160 * 1024) return -5;
+  const float2* w2 = reinterpret_cast<const float2*>(wy);
+  const int4* it = reinterpret_cast<const int4*>(items);
+#define SRML_RF_HW(RG, FX, RBB, YS)                                                                           \
+  do {                                                                                                       \
+    (void)hipFuncSetAttribute((const void*)rf_hist_wide_kernel<RG, FX, RBB>,                                 \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                         \
+    hipLaunchKernelGGL((rf_hist_wide_kernel<RG, FX, RBB>), dim3(n_items), dim3(RHW_T), lds, stream, rec, m, idx, \
+                       w2, it, node_feats, nf, B, S, fbw, YS, hist_u, hist_d);                               \
+  } while (0)
+#define SRML_RF_HW_RB(RBB)                                   \
+  do {                                                       \
+    if (regression && fixed) SRML_RF_HW(true, true, RBB, yscale);  \
+    else if (regression) SRML_RF_HW(true, false, RBB, yscale);     \
+    else SRML_RF_HW(false, false, RBB, 1.0);                       \
+  } while (0)
+  if (rb == 64) SRML_RF_HW_RB(64);
+  else SRML_RF_HW_RB(32);
+#undef SRML_RF_HW_RB
+#undef SRML_RF_HW
+  return srml_status();
+}
+
 // 32-byte record layout of a feature-major (n x m) uint8 bin matrix: out[(g * m + r) * 32 + j] =
 // bins[(32 g + j) * m + r] (features past n are 0). One thread per row and group: 32 coalesced
 // byte reads across the rows, two 16-B stores.
+template <int RB>
 __global__ __launch_bounds__(256) void rf_interleave_kernel(const unsigned char* __restrict__ bins, long m, int n,
                                                             unsigned char* __restrict__ out) {
   const long r = (long)blockIdx.x * 256 + threadIdx.x;
   const int g = blockIdx.y;
   if (r >= m) return;
-  unsigned w[8];
+  unsigned w[RB / 4];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
+  for (int q = 0; q < RB / 4; ++q) {
     unsigned v = 0;
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
-      const int f = 32 * g + 4 * q + b;
+      const int f = RB * g + 4 * q + b;
       if (f < n) v |= (unsigned)bins[(long)f * m + r] << (8 * b);
     }
     w[q] = v;
   }
-  uint4* dst = reinterpret_cast<uint4*>(out + ((long)g * m + r) * 32);
-  dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
-  dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
+  uint4* dst = reinterpret_cast<uint4*>(out + ((long)g * m + r) * RB);
+#pragma unroll
+  for (int q = 0; q < RB / 16; ++q) dst[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 }
 
-SRML_API int srml_rf_interleave_u8(const unsigned char* bins, long m, int n, unsigned char* out, hipStream_t stream) {
+// rb = record bytes (features per record): 32 (the 8-feature item kernel's layout) or 64
+SRML_API int srml_rf_interleave_u8(const unsigned char* bins, long m, int n, int rb, unsigned char* out,
+                                   hipStream_t stream) {
   if (m <= 0 || n <= 0) return 0;
   if (reinterpret_cast<uintptr_t>(out) & 15) return -8;
-  const int G = (n + 31) / 32;
+  if (rb != 32 && rb != 64) return -2;
+  const int G = (n + rb - 1) / rb;
   if (G > 65535) return -2;
-  hipLaunchKernelGGL(rf_interleave_kernel, dim3((unsigned)((m + 255) / 256), (unsigned)G), dim3(256), 0, stream, bins,
-                     m, n, out);
+  const dim3 grid((unsigned)((m + 255) / 256), (unsigned)G);
+  if (rb == 32) hipLaunchKernelGGL(rf_interleave_kernel<32>, grid, dim3(256), 0, stream, bins, m, n, out);
+  else hipLaunchKernelGGL(rf_interleave_kernel<64>, grid, dim3(256), 0, stream, bins, m, n, out);
   return srml_status();
 }
 
@@ -393,7 +577,7 @@ SRML_API int srml_rf_hist_fixed(const unsigned char* bins, long m, const int* id
   if (n_items <= 0) return 0;
   if (fb < 1 || fb > FB) return -7;
   if (il && (reinterpret_cast<uintptr_t>(bins) & 15)) return -8;
-  const size_t lds = (size_t)fb * B * 3 * sizeof(unsigned);
+  const size_t lds = ((size_t)fb * B * 3 + 1) * sizeof(unsigned);
   if (lds > 160 * 1024) return -5;
   const float2* w2 = reinterpret_cast<const float2*>(wy);
   const int4* it = reinterpret_cast<const int4*>(items);

@@ -404,19 +404,32 @@ typedef __attribute__((address_space(1))) void* gbl_vptr;
 // TILED: operands in the split_tiled_kernel layout (contiguous, pre-swizzled 8 KiB k-step images).
 // NP = 6: the fp32-exact product set; NP = 3: h.h + h.m + m.h only (~2^-16 relative, half the
 // MFMAs) for consumers that only need approximate distances (k-means|| D^2 sampling / weighting).
-template <bool TILED, int NP = 6, bool TOP2 = false>
-__global__ __launch_bounds__(512, 1) void nearest_centroid_split_glds_kernel(
+// WN_ = 4: 256 x 256 block tile, 8 waves, one block per CU. WN_ = 2 (3-product only): 256 x 128
+// block tile, 4 waves (one per SIMD) and a 3-stage 72 KiB ring, so TWO blocks share a CU: each
+// SIMD runs two waves of independent blocks whose barriers and LDS-DMA waits fall at different
+// times (the 8-wave block parks all its waves at every barrier together). Same per-wave 128 x 64
+// tile and fragment reads; C rows of a 128-wide tile are the first / second half of the 256-row
+// tiled image.
+template <bool TILED, int NP = 6, bool TOP2 = false, int WN_ = 4>
+__global__ __launch_bounds__(WN_ * 128, WN_ == 4 ? 1 : 2) void nearest_centroid_split_glds_kernel(
     const unsigned short* __restrict__ XP, long m, long xrows, int kp, const unsigned short* __restrict__ CP, int k,
     long crows, const float* __restrict__ cnorm, unsigned long long* __restrict__ best, int n_ctiles,
     float* __restrict__ lob = nullptr, const float* __restrict__ cg = nullptr, const float* __restrict__ xnorm = nullptr) {
-  constexpr int BM = 256, BN = 256, WM = 2, WN = 4, TM = 4, TN = 2;
+  static_assert(WN_ == 4 || (WN_ == 2 && NP == 3), "256 x 128 tiles are built for the 3-product pass");
+  constexpr int BM = 256, WM = 2, WN = WN_, BN = 64 * WN, TM = 4, TN = 2;
   // planes staged per operand: h, m, l for the 6-product set; the 3-product set (h.h, h.m, m.h)
   // never touches the l planes, so it stages 2 per operand (2/3 of the DMA and LDS traffic)
-  constexpr int NPL = NP == 6 ? 3 : 2, CPW = 2 * NPL;  // staging chunks per wave per k step
-  // ring depth: a 3-product k step is half the MFMA time of a 6-product one, so its loads get one
-  // more step of lead (4 stages x 32 KiB = 128 KiB; the 6-product ring is 3 x 48 KiB)
-  constexpr int NS = NP == 6 ? 3 : 4;
-  __shared__ __attribute__((aligned(1024))) unsigned short lds[NS][2 * NPL][256][16];
+  constexpr int NPL = NP == 6 ? 3 : 2;
+  constexpr int XCH = NPL * (BM / 32), CCH = NPL * (BN / 32);  // 1 KiB staging chunks per stage
+  constexpr int CPW = (XCH + CCH) / (WM * WN);                  // ... per wave
+  static_assert((XCH + CCH) % (WM * WN) == 0, "chunks split evenly over the waves");
+  // ring depth: a 3-product k step is half the MFMA time of a 6-product one, so the 8-wave block's
+  // loads get one more step of lead (4 stages x 32 KiB = 128 KiB; the 6-product ring is 3 x 48 KiB);
+  // the 4-wave block keeps 3 stages (3 x 24 KiB) so two blocks fit a CU
+  constexpr bool PAIRS = NP == 3 && WN_ == 4;
+  constexpr int NS = PAIRS ? 4 : 3;
+  constexpr int STAGE = NPL * (BM + BN) * 16;  // elements: X planes [NPL][BM][16], then C planes [NPL][BN][16]
+  __shared__ __attribute__((aligned(1024))) unsigned short lds[NS][STAGE];
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const long rtile = bid / n_ctiles;
   const int ctile = bid % n_ctiles;
@@ -428,31 +441,33 @@ __global__ __launch_bounds__(512, 1) void nearest_centroid_split_glds_kernel(
   const int li = lane & 31, lk = lane >> 5;
   const long xplane = xrows * (long)kp, cplane = crows * (long)kp;
 
-  // this wave's CPW staging chunks per stage: chunk c = wid * CPW + i -> LDS plane q = c / 8 (X planes
-  // 0 .. NPL-1, then C planes), rows 32 (c % 8) ..
+  // this wave's CPW staging chunks per stage: chunk c = wid * CPW + i -> X plane c / 8 (rows
+  // 32 (c % 8) ..) for c < XCH, else C plane (c - XCH) / (BN / 32)
   const unsigned short* src[CPW];
   int dst_off[CPW];  // element offset of the chunk inside one stage
 #pragma unroll
   for (int i = 0; i < CPW; ++i) {
     const int c = wid * CPW + i;
-    const int q = c >> 3, j = c & 7;
+    const bool isx = c < XCH;
+    const int q = isx ? c / (BM / 32) : (c - XCH) / (BN / 32);
+    const int j = isx ? c % (BM / 32) : (c - XCH) % (BN / 32);
     const int r = 32 * j + (lane >> 1);
     const int lh = (lane & 1) ^ ((lane >> 4) & 1);  // logical half stored at physical half (lane & 1)
     if (TILED) {  // the image is already swizzled: lane-linear 16-B pieces of one contiguous 1 KiB
       const int ks_n = kp / SBK;
-      if (q < NPL) src[i] = XP + q * xplane + ((rtile * ks_n) << 12) + 512 * j + lane * 8;
-      else src[i] = CP + (q - NPL) * cplane + (((long)ctile * ks_n) << 12) + 512 * j + lane * 8;
-    } else if (q < NPL) {
+      if (isx) src[i] = XP + q * xplane + ((rtile * ks_n) << 12) + 512 * j + lane * 8;
+      else src[i] = CP + q * cplane + (((long)(col0 >> 8) * ks_n) << 12) + 16 * (col0 & 255) + 512 * j + lane * 8;
+    } else if (isx) {
       long xr = row0 + r;
       if (xr >= xrows) xr = xrows - 1;  // clamp: those rows are never reported
       src[i] = XP + q * xplane + xr * kp + 8 * lh;
     } else {
-      src[i] = CP + (q - NPL) * cplane + (long)(col0 + r) * kp + 8 * lh;  // crows % 256 == 0
+      src[i] = CP + q * cplane + (long)(col0 + r) * kp + 8 * lh;  // crows % 256 == 0
     }
-    dst_off[i] = (q * 256 + 32 * j) * 16;
+    dst_off[i] = isx ? (q * BM + 32 * j) * 16 : (NPL * BM + q * BN + 32 * j) * 16;
   }
   auto issue = [&](int kt, int stage) {
-    unsigned short* base = &lds[stage][0][0][0];
+    unsigned short* base = &lds[stage][0];
 #pragma unroll
     for (int i = 0; i < CPW; ++i) {
       __builtin_amdgcn_global_load_lds((gbl_vptr)(src[i] + (TILED ? ((long)kt << 12) : (long)kt * SBK)),
@@ -477,13 +492,14 @@ __global__ __launch_bounds__(512, 1) void nearest_centroid_split_glds_kernel(
     for (int p = 0; p < NPL; ++p)
 #pragma unroll
       for (int nt = 0; nt < TN; ++nt)
-        fb[p][nt] = *reinterpret_cast<const bf16x8*>(&lds[st][NPL + p][wn * (BN / WN) + nt * 32 + li][8 * ph]);
+        fb[p][nt] = *reinterpret_cast<const bf16x8*>(
+            &lds[st][(NPL * BM + p * BN + wn * (BN / WN) + nt * 32 + li) * 16 + 8 * ph]);
 #pragma unroll
     for (int mt = 0; mt < TM; ++mt) {
       bf16x8 fa[NPL];
 #pragma unroll
       for (int p = 0; p < NPL; ++p)
-        fa[p] = *reinterpret_cast<const bf16x8*>(&lds[st][p][wm * (BM / WM) + mt * 32 + li][8 * ph]);
+        fa[p] = *reinterpret_cast<const bf16x8*>(&lds[st][(p * BM + wm * (BM / WM) + mt * 32 + li) * 16 + 8 * ph]);
 #pragma unroll
       for (int nt = 0; nt < TN; ++nt) {
         if constexpr (NP == 6) {
@@ -497,8 +513,9 @@ __global__ __launch_bounds__(512, 1) void nearest_centroid_split_glds_kernel(
       }
     }
   };
-  if constexpr (NP == 6) {
+  if constexpr (!PAIRS) {
     // 3-stage ring, one k step per barrier, two steps of load lead
+    static_assert(CPW == 6, "the counted wait below leaves one step (CPW loads) in flight");
     issue(0, 0);
     if (nk > 1) issue(1, 1);
     int stage = 0;
@@ -662,6 +679,12 @@ SRML_API int srml_split_bf16x3_tiled_centered(const float* X, long m, int n, lon
   return srml_status();
 }
 
+// Block tile of the 3-product passes: 256 x 128 (two blocks per CU) unless SRML_SPLIT_BN3=256.
+static int split3_bn() {
+  static const int bn = getenv("SRML_SPLIT_BN3") && atoi(getenv("SRML_SPLIT_BN3")) == 256 ? 256 : 128;
+  return bn;
+}
+
 // Nearest centroid on tiled planes of X (xrows % 256 == 0) and of the centroids (crows % 256 == 0).
 // nprod: 6 (fp32-exact) or 3 (approximate, half the MFMAs).
 SRML_API int srml_nearest_centroid_split_tiled_np(const unsigned short* XP, long m, long xrows, int kp,
@@ -671,10 +694,14 @@ SRML_API int srml_nearest_centroid_split_tiled_np(const unsigned short* XP, long
   if ((kp & 15) || xrows < m || crows < k || (crows & 255) || (xrows & 255)) return -2;
   if ((reinterpret_cast<uintptr_t>(XP) & 15) || (reinterpret_cast<uintptr_t>(CP) & 15)) return -5;
   const long rt = (m + 255) / 256;
-  const int ct = (k + 255) / 256;
+  const int bn = nprod == 3 ? split3_bn() : 256;
+  const int ct = (k + bn - 1) / bn;
   const long nb = rt * ct;
   if (nb > 0x7fffffffL) return -3;
-  if (nprod == 3)
+  if (nprod == 3 && bn == 128)
+    hipLaunchKernelGGL((nearest_centroid_split_glds_kernel<true, 3, false, 2>), dim3((unsigned)nb), dim3(256), 0, stream,
+                       XP, m, xrows, kp, CP, k, crows, cnorm, best, (int)ct);
+  else if (nprod == 3)
     hipLaunchKernelGGL((nearest_centroid_split_glds_kernel<true, 3>), dim3((unsigned)nb), dim3(512), 0, stream, XP, m,
                        xrows, kp, CP, k, crows, cnorm, best, (int)ct);
   else if (nprod == 6)
@@ -693,7 +720,7 @@ SRML_API int srml_nearest_centroid_split_tiled(const unsigned short* XP, long m,
 
 // Certified 3-product nearest-centroid search, phase 1 (tiled planes, as
 // srml_nearest_centroid_split_tiled_np): best + lower-bound slots per row, keys / lob sized
-// m * ceil(k/256) * 4; cg = 2 tau ||c_j|| per centroid, xnorm = ||x||^2 of the (centred) rows.
+// m * srml_nearest_centroid_split_top2_nslot(k); cg = 2 tau ||c_j|| per centroid, xnorm = ||x||^2 of the (centred) rows.
 SRML_API int srml_nearest_centroid_split_top2(const unsigned short* XP, long m, long xrows, int kp,
                                               const unsigned short* CP, int k, long crows, const float* cnorm,
                                               const float* cg, const float* xnorm, unsigned long long* keys,
@@ -702,15 +729,24 @@ SRML_API int srml_nearest_centroid_split_top2(const unsigned short* XP, long m, 
   if ((kp & 15) || xrows < m || crows < k || (crows & 255) || (xrows & 255)) return -2;
   if ((reinterpret_cast<uintptr_t>(XP) & 15) || (reinterpret_cast<uintptr_t>(CP) & 15)) return -5;
   const long rt = (m + 255) / 256;
-  const int ct = (k + 255) / 256;
+  const int bn = split3_bn();
+  const int ct = (k + bn - 1) / bn;
   const long nb = rt * ct;
   if (nb > 0x7fffffffL) return -3;
-  hipLaunchKernelGGL((nearest_centroid_split_glds_kernel<true, 3, true>), dim3((unsigned)nb), dim3(512), 0, stream, XP,
-                     m, xrows, kp, CP, k, crows, cnorm, keys, (int)ct, lob, cg, xnorm);
+  if (bn == 128)
+    hipLaunchKernelGGL((nearest_centroid_split_glds_kernel<true, 3, true, 2>), dim3((unsigned)nb), dim3(256), 0, stream,
+                       XP, m, xrows, kp, CP, k, crows, cnorm, keys, (int)ct, lob, cg, xnorm);
+  else
+    hipLaunchKernelGGL((nearest_centroid_split_glds_kernel<true, 3, true>), dim3((unsigned)nb), dim3(512), 0, stream,
+                       XP, m, xrows, kp, CP, k, crows, cnorm, keys, (int)ct, lob, cg, xnorm);
   return srml_status();
 }
 
-SRML_API int srml_nearest_centroid_split_top2_nslot(int k) { return ((k + 255) / 256) * 4; }
+// (row, slot) pairs of the top-2 phase: one slot per (centroid tile, wave column)
+SRML_API int srml_nearest_centroid_split_top2_nslot(int k) {
+  const int bn = split3_bn();
+  return ((k + bn - 1) / bn) * (bn / 64);
+}
 
 // phase 2: merge slots, certify, emit labels / distances of certified rows, list the others
 SRML_API int srml_split_top2_select(const unsigned long long* keys, const float* lob, long m, int nslot,

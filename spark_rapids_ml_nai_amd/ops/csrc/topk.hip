@@ -180,6 +180,78 @@ __global__ __launch_bounds__(TK_T) void topk_rows_kernel(const float* __restrict
     }
   }
 }
+
+// Exact re-scoring + sort of a query's <= 64 selected candidates (the kNN refine step: direct
+// q - x distances instead of ||x||^2 - 2 q.x, so near-duplicates keep their digits). One wave per
+// query: the query sits in registers (lanes over dimensions), every candidate row is read once
+// coalesced and wave-reduced on DPP, then the (distance, position) pairs are bitonic-sorted across
+// the 64 lanes (ties keep the candidate order). Replaces index_select of the candidate rows +
+// elementwise + reduction + torch.sort (the gathered rows never touch HBM).
+// metric 0: squared euclidean; 1: -2 q.x (inner product, ascending = most similar first).
+template <int QT>
+__global__ __launch_bounds__(256) void knn_refine_sort_kernel(const float* __restrict__ Q, long mq, int n, long ldq,
+                                                              const float* __restrict__ X, long ldx,
+                                                              const long long* __restrict__ pos, int k, long ldp,
+                                                              int metric, float* __restrict__ dout,
+                                                              long long* __restrict__ pout) {
+  const long q = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (q >= mq) return;  // wave-uniform
+  float qv[QT];
+#pragma unroll
+  for (int t = 0; t < QT; ++t) {
+    const int d = lane + 64 * t;
+    qv[t] = d < n ? Q[q * ldq + d] : 0.f;
+  }
+  const long long mine = lane < k ? pos[q * ldp + lane] : -1;
+  float my = __builtin_huge_valf();
+  for (int j = 0; j < k; ++j) {
+    const long long c = __shfl(mine, j, 64);  // wave-uniform candidate
+    if (c < 0) continue;
+    const float* xr = X + c * ldx;
+    float acc = 0.f;
+#pragma unroll
+    for (int t = 0; t < QT; ++t) {
+      const int d = lane + 64 * t;
+      if (d < n) {
+        const float x = xr[d];
+        if (metric == 0) {
+          const float df = qv[t] - x;
+          acc = fmaf(df, df, acc);
+        } else {
+          acc = fmaf(qv[t], x, acc);
+        }
+      }
+    }
+    const float tot = wave_sum(acc);
+    if (lane == j) my = metric == 0 ? tot : -2.f * tot;
+  }
+  // bitonic sort of (my, lane) ascending across the wave
+  float v = my;
+  int id = lane;
+#pragma unroll
+  for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const float ov = __shfl_xor(v, stride, 64);
+      const int oid = __shfl_xor(id, stride, 64);
+      const bool up = ((lane & size) == 0);
+      const bool lower = (lane & stride) == 0;
+      const bool o_less = ov < v || (ov == v && oid < id);
+      // the lower lane of an ascending pair keeps the smaller element
+      const bool take = (lower == up) ? o_less : !o_less;
+      if (take) {
+        v = ov;
+        id = oid;
+      }
+    }
+  }
+  const long long src = __shfl(mine, id, 64);
+  if (lane < k) {
+    dout[q * k + lane] = v;
+    pout[q * k + lane] = src < 0 ? -1 : src;
+  }
+}
 }  // namespace
 
 // D (mq x mi, leading dim ldd) = inorm[i] - 2 Q I^T for one (query chunk, item chunk).
@@ -336,5 +408,24 @@ SRML_API int srml_ivf_candidates_f32(const float* Q, long q0, long nq, int n, lo
     (void)hipFuncSetAttribute((const void*)ivf_candidates_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
   hipLaunchKernelGGL(ivf_candidates_kernel, dim3((unsigned)nq, (unsigned)nprobe), dim3(IVC_T), shm, stream, Q, q0, n,
                      ldq, probes, nprobe, qlist, list_off, items, ldi, inorm, ids, D, DI, ldd);
+  return srml_status();
+}
+
+// Q (mq x n, ld ldq) fp32, X (items x n, ld ldx) fp32, pos (mq x k, ld ldp) int64 candidate rows
+// of X (-1 = none, sorts last at +inf); k <= 64, n <= 1024. Outputs dout / pout (mq x k, dense).
+SRML_API int srml_knn_refine_sort_f32(const float* Q, long mq, int n, long ldq, const float* X, long ldx,
+                                      const long long* pos, int k, long ldp, int metric, float* dout, long long* pout,
+                                      hipStream_t stream) {
+  if (mq <= 0) return 0;
+  if (k < 1 || k > 64 || n < 1 || n > 1024 || ldq < n || ldx < n || ldp < k || (metric != 0 && metric != 1)) return -2;
+  const dim3 grid(ceil_div(mq, 4)), blk(256);
+#define SRML_KRS(QQ) \
+  hipLaunchKernelGGL(knn_refine_sort_kernel<QQ>, grid, blk, 0, stream, Q, mq, n, ldq, X, ldx, pos, k, ldp, metric, dout, pout)
+  if (n <= 64) SRML_KRS(1);
+  else if (n <= 128) SRML_KRS(2);
+  else if (n <= 256) SRML_KRS(4);
+  else if (n <= 512) SRML_KRS(8);
+  else SRML_KRS(16);
+#undef SRML_KRS
   return srml_status();
 }

@@ -228,33 +228,40 @@ __global__ __launch_bounds__(256) void umap_smooth_knn_kernel(const float* __res
 
 __global__ __launch_bounds__(256) void umap_fuzzy_union_knn_kernel(const long long* __restrict__ idx,
                                                                    const float* __restrict__ w, long m, int k, long ld,
-                                                                   float mix, long long* __restrict__ keys,
-                                                                   float* __restrict__ vals) {
+                                                                   float mix, unsigned long long* __restrict__ keys,
+                                                                   float* __restrict__ vals,
+                                                                   unsigned long long* __restrict__ kept) {
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= m * (long)k) return;
-  const long i = e / k;
-  const int j = (int)(e % k);
-  const long long c = idx[i * ld + j];
-  const float v = w[i * ld + j];
-  long long k0 = -1, k1 = -1;
+  const bool live = e < m * (long)k;
+  const unsigned long long none = (unsigned long long)m * (unsigned long long)m;  // sorts after every entry
+  unsigned long long k0 = none, k1 = none;
   float o0 = 0.f, o1 = 0.f;
-  if (c >= 0 && c < m && v > 0.f) {
-    float vt = 0.f;
-    const long long* rc = idx + c * ld;
-    for (int q = 0; q < k; ++q)
-      if (rc[q] == i) { vt = w[c * ld + q]; break; }
-    const float prod = v * vt;
-    o0 = mix * (v + vt - prod) + (1.f - mix) * prod;
-    if (o0 > 0.f) k0 = (long long)i * m + c;
-    if (!(vt > 0.f)) {  // (c, i) is only in Aᵀ: emit it here
-      o1 = mix * v;
-      if (o1 > 0.f) k1 = c * m + (long long)i;
+  if (live) {
+    const long i = e / k;
+    const int j = (int)(e % k);
+    const long long c = idx[i * ld + j];
+    const float v = w[i * ld + j];
+    if (c >= 0 && c < m && v > 0.f) {
+      float vt = 0.f;
+      const long long* rc = idx + c * ld;
+      for (int q = 0; q < k; ++q)
+        if (rc[q] == i) { vt = w[c * ld + q]; break; }
+      const float prod = v * vt;
+      o0 = mix * (v + vt - prod) + (1.f - mix) * prod;
+      if (o0 > 0.f) k0 = (unsigned long long)i * m + c;
+      if (!(vt > 0.f)) {  // (c, i) is only in Aᵀ: emit it here
+        o1 = mix * v;
+        if (o1 > 0.f) k1 = (unsigned long long)c * m + i;
+      }
     }
+    keys[2 * e] = k0;
+    keys[2 * e + 1] = k1;
+    vals[2 * e] = o0;
+    vals[2 * e + 1] = o1;
   }
-  keys[2 * e] = k0;
-  keys[2 * e + 1] = k1;
-  vals[2 * e] = o0;
-  vals[2 * e + 1] = o1;
+  // emitted-entry count: one atomic per wave
+  const unsigned long long n0 = __ballot(k0 != none), n1 = __ballot(k1 != none);
+  if ((threadIdx.x & 63) == 0 && (n0 | n1)) atomicAdd(kept, (unsigned long long)(__popcll(n0) + __popcll(n1)));
 }
 }  // namespace
 
@@ -270,12 +277,14 @@ SRML_API int srml_umap_smooth_knn(const float* dist, const long long* idx, long 
   return srml_status();
 }
 
-// keys int64 [2 m k] (row * m + col, -1 = no entry), vals fp32 [2 m k].
+// keys u64 [2 m k] (row * m + col; m * m = no entry, sorting after every entry), vals fp32
+// [2 m k]; *kept (zeroed by the caller) += number of entries.
 SRML_API int srml_umap_fuzzy_union_knn(const long long* idx, const float* w, long m, int k, long ld, float mix,
-                                       long long* keys, float* vals, hipStream_t stream) {
+                                       unsigned long long* keys, float* vals, unsigned long long* kept,
+                                       hipStream_t stream) {
   if (m <= 0) return 0;
-  if (k < 1 || ld < k) return -1;
+  if (k < 1 || ld < k || m >= (1L << 31)) return -1;
   hipLaunchKernelGGL(umap_fuzzy_union_knn_kernel, dim3(ceil_div(m * (long)k, 256)), dim3(256), 0, stream, idx, w, m, k,
-                     ld, mix, keys, vals);
+                     ld, mix, keys, vals, kept);
   return srml_status();
 }

@@ -26,7 +26,8 @@ _D = ctypes.c_double
 _F = ctypes.c_float
 
 # name -> argtypes (restype: int status, except the size queries in _LONG_RESULT)
-_LONG_RESULT = ("srml_qn_args_size", "srml_logit_residual_ws", "srml_xtv_mfma_ws", "srml_rf_partition_ws")
+_LONG_RESULT = ("srml_qn_args_size", "srml_logit_residual_ws", "srml_xtv_mfma_ws", "srml_rf_partition_ws",
+                "srml_label_sort_ws", "srml_radix_sort_ws")
 SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_col_moments_f32": (_P, _L, _I, _L, _P, _P, _P),
     "srml_col_moments_f64": (_P, _L, _I, _L, _P, _P, _P),
@@ -96,7 +97,7 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_oneshot_free": (_P,),
     "srml_oneshot_allreduce": (_P, _P, _L, _I, _P, _I, _I, ctypes.c_ulonglong, _L, ctypes.c_longlong, _P, _P),
     "srml_umap_smooth_knn": (_P, _P, _L, _I, _L, _D, _D, _I, _P, _I, _P, _P, _P, _P),
-    "srml_umap_fuzzy_union_knn": (_P, _P, _L, _I, _L, ctypes.c_float, _P, _P, _P),
+    "srml_umap_fuzzy_union_knn": (_P, _P, _L, _I, _L, ctypes.c_float, _P, _P, _P, _P),
     "srml_umap_epoch": (_P, _P, _L, _P, _P, _P, _P, _P, _P, _I, _I, _F, _F, _F, _F, _F, _I, ctypes.c_uint, _P),
     "srml_syevj_f64": (_P, _I, _P, _P, _I, _D, _P),
     "srml_potrf_f64": (_P, _I, _L, _P, _P),
@@ -106,7 +107,7 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_rf_quantize_u8": (_P, _L, _I, _L, _P, _I, _P, _P),
     "srml_rf_quantiles_f32": (_P, _I, _I, _I, _P, _P),
     "srml_rf_hist": (_P, _L, _P, _P, _P, _I, _P, _I, _I, _I, _I, _D, _I, _P, _P, _I, _P),
-    "srml_rf_interleave_u8": (_P, _L, _I, _P, _P),
+    "srml_rf_interleave_u8": (_P, _L, _I, _I, _P, _P),
     "srml_rf_hist_fb": (_I, _I, _I),
     "srml_rf_hist_fb_max": (),
     "srml_rf_best_split": (_P, _P, _I, _I, _I, _I, _I, _I, _D, _D, _P, _P, _P),
@@ -114,6 +115,15 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_rf_route_segments": (_P, _L, _P, _L, _P, _I, _P, _P, _P, _P, _P),
     "srml_rf_node_stats": (_P, _P, _P, _L, _P, _I, _I, _I, _P, _P),
     "srml_rf_node_stats_det": (_P, _P, _P, _P, _I, _I, _I, _P, _P),
+    "srml_label_sort": (_P, _L, _I, _P, _P, _P, _P, _P),
+    "srml_label_sort_ws": (_L, _I),
+    "srml_label_sort_kmax": (),
+    "srml_radix_sort_ws": (_L,),
+    "srml_knn_refine_sort_f32": (_P, _L, _I, _L, _P, _L, _P, _I, _L, _I, _P, _P, _P),
+    "srml_radix_sort_u64": (_P, _P, _P, _P, _L, _I, _P, _P),
+    "srml_label_counts": (_P, _L, _I, _P, _P),
+    "srml_rf_hist_wide": (_P, _L, _P, _P, _P, _I, _P, _I, _I, _I, _I, _D, _I, _I, _I, _P, _P, _P),
+    "srml_rf_hist_wide_fb": (_I, _I, _I),
     "srml_rf_hist_fixed": (_P, _L, _P, _P, _P, _I, _P, _I, _I, _D, _I, _P, _I, _P),
     "srml_rf_hist_fixed_finish": (_P, _L, _D, _P),
     "srml_csr_logreg_binary_f32": (_P, _P, _P, _L, _I, _L, _P, _P, _D, _P, _P, _P, _P),

@@ -326,6 +326,52 @@ def test_rf_hist_record_layout_identical(gpu_device, monkeypatch, regression):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("regression", [False, True])
+@pytest.mark.parametrize("n,nf", [(70, 24), (700, 450)])
+@pytest.mark.parametrize("rec_bytes", [32, 64])
+def test_rf_hist_wide_identical(gpu_device, monkeypatch, regression, n, nf, rec_bytes):
+    """The 1024-thread record-layout kernel (chunks of rf_hist_fb_wide features; 450 > that spans
+    several chunks) produces the same cells as the feature-major 8-feature items, including split
+    row chunks (atomic folds) and exclusive single-chunk nodes (plain stores)."""
+    if regression:
+        monkeypatch.setenv("SRML_DETERMINISTIC", "1")
+    g = torch.Generator().manual_seed(23)
+    m, B, nodes = 30000, 64, 4
+    bins = torch.randint(0, B, (n, m), generator=g, dtype=torch.uint8)
+    S = 2 if regression else 3
+    y = torch.randn(m, generator=g) if regression else torch.randint(0, S, (m,), generator=g).float()
+    idx = torch.randperm(m, generator=g)[:20000].sort().values.int()
+    w = torch.randint(1, 4, (20000,), generator=g).float()
+    feats = torch.stack([torch.randperm(n, generator=g)[:nf].sort().values for _ in range(nodes)]).int()
+    bounds = [0, 3000, 9000, 15000, 20000]
+
+    def items_for(fb, rows, excl):
+        out = []
+        for node in range(nodes):
+            starts = list(range(bounds[node], bounds[node + 1], rows))
+            flag = (1 << 30) if excl and len(starts) == 1 else 0
+            out += [[node, rb, min(rb + rows, bounds[node + 1]), fc | flag] for rb in starts
+                    for fc in range((nf + fb - 1) // fb)]
+        return torch.tensor(out, dtype=torch.int32)
+
+    d = lambda t: t.to(gpu_device)  # noqa: E731
+    ys = ops.rf_yscale(d(y), float(w.sum())) if regression else None
+    fb = ops.rf_hist_fb(B, S, regression)
+    a = ops.rf_hist(d(bins), d(idx), d(y), None, d(items_for(fb, 2048, False)), d(feats), nodes, B, S, regression,
+                    pos_weight=d(w), fb=fb, yscale=ys)
+    il = ops.rf_interleave(d(bins), rec_bytes)
+    assert il.numel() == ((n + rec_bytes - 1) // rec_bytes) * m * rec_bytes
+    fbw = ops.rf_hist_fb_wide(B, S, regression)
+    assert fbw > fb
+    # node 0 (3000 rows) is one exclusive chunk; the others split into 4096-row chunks
+    multi = d(torch.tensor([1, 2, 3]))
+    b = ops.rf_hist(d(bins), d(idx), d(y), None, d(items_for(fbw, 4096, True)), d(feats), nodes, B, S, regression,
+                    pos_weight=d(w), fb=fbw, yscale=ys, bins_il=il, wide=True, exclusive={"multi_nodes": multi},
+                    rec_bytes=rec_bytes)
+    assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
 def test_rf_sample_features_uniform_sorted(gpu_device):
     C, n, nf = 4000, 300, 100
     f = ops.rf_sample_features(C, n, nf, 12345, gpu_device).cpu()

@@ -630,6 +630,7 @@ def test_rf_hist_fb_matches_library(gpu_device):
                 if reg and S != 2:
                     continue
                 assert int(lib.srml_rf_hist_fb(B, S, int(reg))) == ops.rf_hist_fb(B, S, reg), (B, S, reg)
+                assert int(lib.srml_rf_hist_wide_fb(B, S, int(reg))) == ops.rf_hist_fb_wide(B, S, reg), (B, S, reg)
 
 
 @pytest.mark.parametrize("classes,bins", [(20, 128), (12, 256), (32, 256)])
@@ -769,3 +770,73 @@ def test_rf_partition_matches_stable_sort(gpu_device, nseg, total):
     di, dw, db = ops.rf_partition(keys.to(gpu_device), bounds.to(gpu_device), node_feature.to(gpu_device),
                                   child_base.to(gpu_device), k, idx.to(gpu_device), w.to(gpu_device))
     assert torch.equal(db.cpu(), rb) and torch.equal(di.cpu(), ri) and torch.equal(dw.cpu(), rw)
+
+
+@pytest.mark.parametrize("m,k", [(0, 5), (1, 1), (5000, 7), (300001, 1000), (70000, 16000)])
+def test_label_sort_stable_and_counts(gpu_device, m, k):
+    """Device counting sort (srml_label_sort) == stable torch sort on the CPU; out-of-range labels
+    trail after off[k]; label counts == bincount."""
+    g = torch.Generator().manual_seed(m + k)
+    lab = torch.randint(0, k, (m,), generator=g, dtype=torch.int32)
+    if m > 10:
+        lab[::97] = k + 3  # out of range: grouped after every valid row, not counted
+        lab[5::211] = -2
+    perm, off, slab = ops.label_sort(lab.to(gpu_device), k)
+    key = torch.where((lab >= 0) & (lab < k), lab, torch.full_like(lab, k))
+    ref_s, ref_p = torch.sort(key, stable=True)
+    assert torch.equal(perm.cpu().long(), ref_p)
+    assert torch.equal(slab.cpu(), ref_s)
+    ref_off = torch.searchsorted(ref_s, torch.arange(k + 1, dtype=torch.int32))
+    assert torch.equal(off.cpu(), ref_off.long())
+    cnt = ops.label_counts(lab.to(gpu_device), k)
+    ok = lab[(lab >= 0) & (lab < k)].long()
+    assert torch.equal(cnt.cpu(), torch.bincount(ok, minlength=k))
+
+
+@pytest.mark.parametrize("n,bits", [(2, 3), (1000, 8), (100003, 20), (300000, 49), (65536, 64)])
+def test_radix_sort_pairs_stable(gpu_device, n, bits):
+    """srml_radix_sort_u64 == stable torch sort (keys < 2^bits, many duplicates)."""
+    g = torch.Generator().manual_seed(n + bits)
+    hi = min(bits, 62)
+    keys = torch.randint(0, 1 << hi, (n,), generator=g, dtype=torch.int64)
+    keys[::3] = keys[0]  # duplicates: stability visible through the payload
+    if bits == 64:
+        keys[1::7] = -5  # the full 64-bit range: negative int64 = large u64
+    vals = torch.arange(n, dtype=torch.int32)
+    k, v = keys.to(gpu_device), vals.to(gpu_device)
+    ops.radix_sort_pairs(k, v, bits)
+    ku = keys.clone()
+    if bits == 64:  # compare as unsigned: flip the sign bit
+        ku = ku ^ (-(1 << 63))
+    ref_k, ref_o = torch.sort(ku, stable=True)
+    if bits == 64:
+        ref_k = ref_k ^ (-(1 << 63))
+    assert torch.equal(k.cpu(), ref_k)
+    assert torch.equal(v.cpu(), vals[ref_o])
+
+
+@pytest.mark.parametrize("mq,n,k,ip", [(1, 3, 1, False), (777, 128, 15, False), (300, 1000, 64, True),
+                                       (129, 65, 40, False)])
+def test_knn_refine_sort_matches_torch(gpu_device, mq, n, k, ip):
+    """Fused exact re-score + per-row sort of kNN candidates == fp64 torch oracle (-1 = missing)."""
+    g = torch.Generator().manual_seed(mq + n + k)
+    Q = torch.randn(mq, n, generator=g)
+    X = torch.randn(500, n, generator=g)
+    pos = torch.randint(0, 500, (mq, k), generator=g)
+    pos[::5, -1] = -1
+    X[7] = Q[0] + 1e-4  # a near-duplicate: the direct difference keeps its digits
+    pos[0, 0] = 7
+    r = ops.knn_refine_sort(Q.to(gpu_device), X.to(gpu_device), pos.to(gpu_device), inner_product=ip)
+    assert r is not None
+    d, p = r[0].cpu(), r[1].cpu()
+    rows = X.double()[pos.clamp_min(0)]
+    ref = -2.0 * (rows * Q.double().unsqueeze(1)).sum(-1) if ip else ((rows - Q.double().unsqueeze(1)) ** 2).sum(-1)
+    ref = torch.where(pos >= 0, ref, torch.full_like(ref, float("inf")))
+    rv, rj = torch.sort(ref, dim=1, stable=True)
+    fin = torch.isfinite(rv)
+    torch.testing.assert_close(d[fin].double(), rv[fin], rtol=1e-5, atol=1e-4)
+    assert torch.equal(torch.isinf(d), ~fin)
+    # the same multiset of candidates per row, ordered by distance (ties aside)
+    assert torch.equal(p.sort(1).values, pos.sort(1).values)
+    if not ip:
+        assert d[0, 0].item() < n * 2e-8 and p[0, 0].item() == 7

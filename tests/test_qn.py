@@ -327,3 +327,27 @@ def test_logistic_deterministic_mode_bit_identical(gpu_device, classes, monkeypa
     assert np.array_equal(np.asarray(a.coef_), np.asarray(b.coef_))
     assert np.array_equal(np.asarray(a.intercept_), np.asarray(b.intercept_))
     np.testing.assert_allclose(np.asarray(a.coef_), np.asarray(ref.coef_), atol=2e-3, rtol=2e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("classes", [2, 4])
+def test_logistic_graph_replay_matches_eager(gpu_device, classes, monkeypatch):
+    """One-rank fits replay the QN batch (evaluation + optimiser step, x8) from a HIP graph; the
+    fit matches the eager launches to solver tolerance (the fp64 atomic folds reorder between any
+    two runs) and the graph was really replayed."""
+    from spark_rapids_ml_nai_amd.classification import LogisticRegression
+    from spark_rapids_ml_nai_amd.models import qn
+
+    X, y = _data(20000, 300, classes, seed=5)
+    df = DataFrame.from_numpy(X, y)
+    est = LogisticRegression(regParam=1e-3, maxIter=80, tol=1e-10)
+    monkeypatch.setattr(qn, "QN_GRAPH", False)
+    r0 = dict(qn.GRAPH_STATS)
+    eager = est.fit(df)
+    assert qn.GRAPH_STATS == r0
+    monkeypatch.setattr(qn, "QN_GRAPH", True)
+    graph = est.fit(df)
+    assert qn.GRAPH_STATS["captures"] == r0["captures"] + 1 and qn.GRAPH_STATS["replays"] > r0["replays"]
+    np.testing.assert_allclose(np.asarray(graph.coef_), np.asarray(eager.coef_), atol=2e-3, rtol=2e-3)
+    np.testing.assert_allclose(graph.intercept_, eager.intercept_, atol=2e-3, rtol=2e-3)
+    assert abs(graph.objective - eager.objective) <= 1e-7 * abs(eager.objective)

@@ -7,5 +7,5 @@ TAG=${TAG:-$ALGOS}
 OUT=gpurun_out/trace_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d $OUT/raw -o run -- python3 -u bench.py --steps 1 --warmup 1 --algos $ALGOS --no-transform > $OUT/bench.json 2> $OUT/bench.err || { echo "trace failed"; tail -30 $OUT/bench.err; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d $OUT/raw -o run -- python3 -u bench.py --steps 1 --warmup 1 --algos $ALGOS --no-transform $BENCH_EXTRA > $OUT/bench.json 2> $OUT/bench.err || { echo "trace failed"; tail -30 $OUT/bench.err; exit 1; }
 python3 tools/trace_summary.py $OUT > $OUT/summary.txt && cat $OUT/summary.txt

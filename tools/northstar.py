@@ -95,14 +95,18 @@ def main() -> None:
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     use_gpu = torch.cuda.is_available()
-    device = torch.device("cuda", local_rank) if use_gpu else torch.device("cpu")
+    ndev = torch.cuda.device_count() if use_gpu else 0
+    device = torch.device("cuda", local_rank % max(1, ndev)) if use_gpu else torch.device("cpu")
     if use_gpu:
         torch.cuda.set_device(device)
     if world > 1:
         from datetime import timedelta
 
-        dist.init_process_group("nccl" if use_gpu else "gloo", timeout=timedelta(minutes=30),
-                                **({"device_id": device} if use_gpu else {}))
+        # SRML_NS_BACKEND=gloo: several ranks sharing ONE GPU (the development box), so the
+        # multi-rank paths (data-parallel RF histogram all-reduce, ...) run and are timed there
+        backend = os.environ.get("SRML_NS_BACKEND", "nccl" if use_gpu else "gloo")
+        dist.init_process_group(backend, timeout=timedelta(minutes=30),
+                                **({"device_id": device} if use_gpu and backend == "nccl" else {}))
     from spark_rapids_ml_nai_amd import DataFrame
 
     for name in a.configs.split(","):
@@ -110,7 +114,8 @@ def main() -> None:
         rows = max(1000, int(rows * a.scale)) if name != "pca" else rows
         b = np.linspace(0, rows, world + 1).astype(np.int64)
         m_local = int(b[rank + 1] - b[rank])
-        rec = {"config": name, "rows": rows, "cols": cols, "n_gpus": world, "scale": a.scale}
+        rec = {"config": name, "rows": rows, "cols": cols, "n_gpus": world, "scale": a.scale,
+               "backend": dist.get_backend() if world > 1 else None, "devices": ndev}
         try:
             t0 = time.perf_counter()
             Xh, yh = _shard(gen, m_local, cols, device, rank)

@@ -23,8 +23,8 @@ def main(out_dir: str) -> None:
     print("dispatches %d, first-to-last span %.1f ms (warmup + timed)" % (len(rows), span))
     for k, (n, ms) in sorted(tot.items(), key=lambda kv: -kv[1][1])[:25]:
         print("%9.2f ms %6d  %s" % (ms, n, k[:110]))
-    for pat in ("rf_hist_kernel", "nearest", "splitmm", "kmeanspp"):
-        calls = [(e - s) / 1e6 for s, e, k in rows if pat in k]
+    for pat in ("rf_hist_kernel|rf_hist_wide_kernel", "nearest", "splitmm", "kmeanspp"):
+        calls = [(e - s) / 1e6 for s, e, k in rows if any(p in k for p in pat.split("|"))]
         if calls:
             print("%s per call (ms): %s" % (pat, " ".join("%.2f" % c for c in calls[:64])))
 
