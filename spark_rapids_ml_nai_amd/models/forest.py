@@ -44,7 +44,7 @@ CHUNK_MAJOR_ITEMS = os.environ.get("SRML_RF_ITEM_ORDER", "chunk") == "chunk"
 # denser nodes share the lines of the feature-major columns (1M x 3000 regression trace: levels
 # 5-6 37 / 31 ms vs 63 / 53 ms, levels 2-3 23 / 39 ms feature-major vs 56 / 63 ms).
 # SRML_RF_IL_DENSITY=0 turns the record layout off.
-IL_DENSITY = float(os.environ.get("SRML_RF_IL_DENSITY", "0.12"))
+IL_DENSITY = float(os.environ.get("SRML_RF_IL_DENSITY", "0.3"))
 # Record-layout kernel: "wide" = one 1024-thread block per (row chunk, ~100-400 features), each
 # row's records fetched once per block (ops.rf_hist_fb_wide); "narrow" = 8-feature items.
 IL_KERNEL = os.environ.get("SRML_RF_IL_KERNEL", "wide")

@@ -712,8 +712,10 @@ def rf_interleave(bins: torch.Tensor, rec_bytes: int = 32) -> torch.Tensor:
     features R g .. R g + R - 1 of row r, R = ``rec_bytes`` (32: the 8-feature item kernel; 32 or
     64: the wide kernel) (``srml_rf_interleave_u8``); flat uint8 tensor."""
     n, m = bins.shape
-    G = (n + rec_bytes - 1) // rec_bytes
-    out = torch.empty(G * m * rec_bytes, dtype=torch.uint8, device=bins.device)
+    # 64-B records are stored in line-sized pairs (groups 2h, 2h + 1 of a row share 128 B)
+    span = 128 if rec_bytes == 64 else rec_bytes
+    G = (n + span - 1) // span
+    out = torch.empty(G * m * span, dtype=torch.uint8, device=bins.device)
     native.call("srml_rf_interleave_u8", _c(bins).data_ptr(), m, n, int(rec_bytes), out.data_ptr(),
                 native.stream(bins.device))
     return out

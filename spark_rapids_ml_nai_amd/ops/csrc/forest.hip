@@ -359,6 +359,15 @@ SRML_API int srml_rf_hist(const unsigned char* bins, long m, const int* idx, con
 // ------------------------------------------------------------------------------------------
 constexpr int RHW_T = 1024;
 
+// Byte offset of record (g, r). 32-B records: [g][r]. 64-B records come in line-sized PAIRS: the
+// records of groups 2h and 2h + 1 of row r share one 128-B line ([h][r][2][64]), so a row's
+// consecutive groups (the wide kernel walks them in order, prefetching the next) hit the line the
+// previous load brought in.
+template <int RB>
+__device__ __forceinline__ long rec_offset(int g, long r, long m) {
+  return RB == 64 ? (((long)(g >> 1) * m + r) * 128 + (g & 1) * 64) : (((long)g * m + r) * RB);
+}
+
 // byte o (wave-uniform) of a record held as four 16-B pieces: scalar branches pick piece and word
 __device__ __forceinline__ int rec_pick(uint4 a, uint4 b, uint4 c, uint4 d, int o) {
   const int t = o >> 4;
@@ -417,7 +426,7 @@ __global__ __launch_bounds__(RHW_T) void rf_hist_wide_kernel(const unsigned char
     uint4 na1 = z4, nb1 = z4, nc1 = z4, nd1 = z4, na2 = z4, nb2 = z4, nc2 = z4, nd2 = z4;
 #define SRML_REC_LOAD(A, Bq, C, D, G, R)                                                    \
   do {                                                                                     \
-    const uint4* p_ = reinterpret_cast<const uint4*>(rec + ((long)(G) * m + (R)) * RB);    \
+    const uint4* p_ = reinterpret_cast<const uint4*>(rec + rec_offset<RB>(G, R, m));         \
     A = p_[0];                                                                             \
     Bq = p_[1];                                                                            \
     if (RB == 64) {                                                                        \
@@ -546,7 +555,7 @@ __global__ __launch_bounds__(256) void rf_interleave_kernel(const unsigned char*
     }
     w[q] = v;
   }
-  uint4* dst = reinterpret_cast<uint4*>(out + ((long)g * m + r) * RB);
+  uint4* dst = reinterpret_cast<uint4*>(out + rec_offset<RB>(g, r, m));
 #pragma unroll
   for (int q = 0; q < RB / 16; ++q) dst[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 }

@@ -410,7 +410,9 @@ typedef __attribute__((address_space(1))) void* gbl_vptr;
 // times (the 8-wave block parks all its waves at every barrier together). Same per-wave 128 x 64
 // tile and fragment reads; C rows of a 128-wide tile are the first / second half of the 256-row
 // tiled image.
-template <bool TILED, int NP = 6, bool TOP2 = false, int WN_ = 4>
+// PRIO: s_setprio(1) / (0) around every MFMA cluster: keeps hipcc from moving MFMAs across the
+// raw barriers into the load phase (cdna_hip_programming.md T5).
+template <bool TILED, int NP = 6, bool TOP2 = false, int WN_ = 4, bool PRIO = false>
 __global__ __launch_bounds__(WN_ * 128, WN_ == 4 ? 1 : 2) void nearest_centroid_split_glds_kernel(
     const unsigned short* __restrict__ XP, long m, long xrows, int kp, const unsigned short* __restrict__ CP, int k,
     long crows, const float* __restrict__ cnorm, unsigned long long* __restrict__ best, int n_ctiles,
@@ -524,7 +526,9 @@ __global__ __launch_bounds__(WN_ * 128, WN_ == 4 ? 1 : 2) void nearest_centroid_
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // step kt landed for every wave; every wave finished step kt - 1
       if (kt + 2 < nk) issue(kt + 2, stage == 0 ? 2 : stage - 1);
+      if (PRIO) __builtin_amdgcn_s_setprio(1);
       compute(stage);
+      if (PRIO) __builtin_amdgcn_s_setprio(0);
       stage = stage == 2 ? 0 : stage + 1;
     }
   } else {
@@ -538,8 +542,10 @@ __global__ __launch_bounds__(WN_ * 128, WN_ == 4 ? 1 : 2) void nearest_centroid_
       __builtin_amdgcn_s_barrier();  // steps kt, kt + 1 landed; every wave finished kt - 2, kt - 1
       if (kt + 2 < nk) issue(kt + 2, (kt + 2) & 3);
       if (kt + 3 < nk) issue(kt + 3, (kt + 3) & 3);
+      if (PRIO) __builtin_amdgcn_s_setprio(1);
       compute(kt & 3);
       if (kt + 1 < nk) compute((kt + 1) & 3);
+      if (PRIO) __builtin_amdgcn_s_setprio(0);
     }
   }
   if (TOP2)
@@ -733,12 +739,15 @@ SRML_API int srml_nearest_centroid_split_top2(const unsigned short* XP, long m, 
   const int ct = (k + bn - 1) / bn;
   const long nb = rt * ct;
   if (nb > 0x7fffffffL) return -3;
-  if (bn == 128)
-    hipLaunchKernelGGL((nearest_centroid_split_glds_kernel<true, 3, true, 2>), dim3((unsigned)nb), dim3(256), 0, stream,
-                       XP, m, xrows, kp, CP, k, crows, cnorm, keys, (int)ct, lob, cg, xnorm);
-  else
-    hipLaunchKernelGGL((nearest_centroid_split_glds_kernel<true, 3, true>), dim3((unsigned)nb), dim3(512), 0, stream,
-                       XP, m, xrows, kp, CP, k, crows, cnorm, keys, (int)ct, lob, cg, xnorm);
+  static const bool prio = getenv("SRML_SPLIT_PRIO") && atoi(getenv("SRML_SPLIT_PRIO")) == 1;
+#define SRML_TOP2(WNN, PR, T)                                                                                    \
+  hipLaunchKernelGGL((nearest_centroid_split_glds_kernel<true, 3, true, WNN, PR>), dim3((unsigned)nb), dim3(T), 0, \
+                     stream, XP, m, xrows, kp, CP, k, crows, cnorm, keys, (int)ct, lob, cg, xnorm)
+  if (bn == 128 && prio) SRML_TOP2(2, true, 256);
+  else if (bn == 128) SRML_TOP2(2, false, 256);
+  else if (prio) SRML_TOP2(4, true, 512);
+  else SRML_TOP2(4, false, 512);
+#undef SRML_TOP2
   return srml_status();
 }
 

@@ -360,7 +360,8 @@ def test_rf_hist_wide_identical(gpu_device, monkeypatch, regression, n, nf, rec_
     a = ops.rf_hist(d(bins), d(idx), d(y), None, d(items_for(fb, 2048, False)), d(feats), nodes, B, S, regression,
                     pos_weight=d(w), fb=fb, yscale=ys)
     il = ops.rf_interleave(d(bins), rec_bytes)
-    assert il.numel() == ((n + rec_bytes - 1) // rec_bytes) * m * rec_bytes
+    span = 128 if rec_bytes == 64 else rec_bytes  # 64-B records in 128-B pairs
+    assert il.numel() == ((n + span - 1) // span) * m * span
     fbw = ops.rf_hist_fb_wide(B, S, regression)
     assert fbw > fb
     # node 0 (3000 rows) is one exclusive chunk; the others split into 4096-row chunks
