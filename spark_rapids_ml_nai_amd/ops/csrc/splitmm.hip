@@ -685,9 +685,10 @@ SRML_API int srml_split_bf16x3_tiled_centered(const float* X, long m, int n, lon
   return srml_status();
 }
 
-// Block tile of the 3-product passes: 256 x 128 (two blocks per CU) unless SRML_SPLIT_BN3=256.
+// Block tile of the 3-product passes: 256 x 256 (one 8-wave block per CU) unless
+// SRML_SPLIT_BN3=128 (256 x 128, two 4-wave blocks per CU: measured equal, 16.8 vs 16.7 ms).
 static int split3_bn() {
-  static const int bn = getenv("SRML_SPLIT_BN3") && atoi(getenv("SRML_SPLIT_BN3")) == 256 ? 256 : 128;
+  static const int bn = getenv("SRML_SPLIT_BN3") && atoi(getenv("SRML_SPLIT_BN3")) == 128 ? 128 : 256;
   return bn;
 }
 
@@ -739,7 +740,9 @@ SRML_API int srml_nearest_centroid_split_top2(const unsigned short* XP, long m, 
   const int ct = (k + bn - 1) / bn;
   const long nb = rt * ct;
   if (nb > 0x7fffffffL) return -3;
-  static const bool prio = getenv("SRML_SPLIT_PRIO") && atoi(getenv("SRML_SPLIT_PRIO")) == 1;
+  // s_setprio around the MFMA clusters: 16.7 -> 16.4 ms per pass on the 256 x 256 tile (neutral
+  // on 256 x 128); SRML_SPLIT_PRIO=0 turns it off
+  static const bool prio = !(getenv("SRML_SPLIT_PRIO") && atoi(getenv("SRML_SPLIT_PRIO")) == 0);
 #define SRML_TOP2(WNN, PR, T)                                                                                    \
   hipLaunchKernelGGL((nearest_centroid_split_glds_kernel<true, 3, true, WNN, PR>), dim3((unsigned)nb), dim3(T), 0, \
                      stream, XP, m, xrows, kp, CP, k, crows, cnorm, keys, (int)ct, lob, cg, xnorm)
