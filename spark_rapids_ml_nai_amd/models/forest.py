@@ -35,6 +35,7 @@ import torch
 
 from .. import ops
 from ..parallel.context import WorkerContext
+from ..utils.determinism import deterministic
 
 ROWS_PER_ITEM = 4096
 CHUNK_MAJOR_ITEMS = os.environ.get("SRML_RF_ITEM_ORDER", "chunk") == "chunk"
@@ -52,6 +53,11 @@ IL_KERNEL = os.environ.get("SRML_RF_IL_KERNEL", "wide")
 # row gather touches where 32-B records used a quarter
 WIDE_REC_BYTES = int(os.environ.get("SRML_RF_REC_BYTES", "64"))
 WIDE_ROWS_PER_ITEM = 8192
+WIDE_ROWS_MAX = 65536
+# packed regression cells in the wide kernel (one u64 LDS atomic per row and feature instead of a
+# u32 count + u64 sum; sums quantised to 2^-22 max|y| per row): SRML_RF_PACK=0 keeps the exact
+# fixed point; deterministic mode always does
+RF_PACK = os.environ.get("SRML_RF_PACK", "1") != "0"
 INT_MAX = 2**31 - 1
 
 
@@ -282,7 +288,13 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
     # the ranks of a data-parallel fit, whose generators share the seed)
     call_seed = int(torch.randint(0, 1 << 62, (1,), generator=gen, device=dev).item())
     bins_il = None
-    wide_fb = ops.rf_hist_fb_wide(B, SH, regression) if dev.type == "cuda" and IL_KERNEL == "wide" else 0
+    # packed cells need every item's weights <= 2^20: rows per item (<= WIDE_ROWS_MAX) x max weight
+    pack_scale = None
+    if (regression and RF_PACK and dev.type == "cuda" and IL_KERNEL == "wide" and not deterministic()
+            and float(wpos.max().item()) * WIDE_ROWS_MAX <= ops.RF_PACK_MAX_WEIGHT):
+        pack_scale = ops.rf_pack_scale(yv)
+    wide_fb = (ops.rf_hist_fb_wide(B, SH, regression, packed=pack_scale is not None)
+               if dev.type == "cuda" and IL_KERNEL == "wide" else 0)
     wide_fb = wide_fb if wide_fb > fb and ops.rf_il_useful(n, nf, min(wide_fb, nf)) else 0
     use_il = (dev.type == "cuda" and IL_DENSITY > 0 and max_depth >= 4
               and (wide_fb > 0 or ops.rf_il_useful(n, nf, fb))
@@ -332,7 +344,7 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
                     fb_l, rpi_min, blocks = wide_fb, WIDE_ROWS_PER_ITEM, 2048
                     nfc_l = (nf + fb_l - 1) // fb_l
             # rows per work item: enough blocks to fill the chip, few per (node, feature chunk)
-            rpi = int(min(65536, max(rpi_min, (int(c_cnt.sum()) * nfc_l) // blocks)))
+            rpi = int(min(WIDE_ROWS_MAX, max(rpi_min, (int(c_cnt.sum()) * nfc_l) // blocks)))
             rpi = (rpi + 511) // 512 * 512
             nch = (c_cnt + rpi - 1) // rpi
             tot_ch = int(nch.sum())
@@ -363,7 +375,8 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
             excl = {"multi_nodes": torch.from_numpy(np.nonzero(nch != 1)[0]).to(dev)} if dev.type == "cuda" else None
             hist = ops.rf_hist(bins, idx, yv, None, items_t, feats, C, B, SH, regression, pos_weight=wpos, fb=fb_l,
                                yscale=yscale, exclusive=excl, bins_il=il, wide=il is not None and fb_l == wide_fb,
-                               rec_bytes=WIDE_REC_BYTES if wide_fb else 32)
+                               rec_bytes=WIDE_REC_BYTES if wide_fb else 32,
+                               packed_scale=pack_scale if fb_l == wide_fb else None)
             if data_parallel:
                 ctx.comm.allreduce(hist)
             out, _ = ops.rf_best_split(hist, B, SH, regression, crit, min_leaf, min_gain)

@@ -700,11 +700,22 @@ def rf_hist_fb(B: int, S: int, regression: bool) -> int:
     return int(fb)
 
 
-def rf_hist_fb_wide(B: int, S: int, regression: bool) -> int:
+def rf_hist_fb_wide(B: int, S: int, regression: bool, packed: bool = False) -> int:
     """Features per work item of the wide record-layout histogram (``srml_rf_hist_wide_fb``): the
-    1024-thread block's LDS slab (fb * B * S' words + feature metadata) within 150 KiB."""
-    per = B * (3 if regression else S) * 4 + 4
+    1024-thread block's LDS slab (fb * B * S' words + feature metadata) within 150 KiB; S' = 2 for
+    the packed regression cells, 3 for count + fixed-point sum, S for class counts."""
+    per = B * (2 if (regression and packed) else 3 if regression else S) * 4 + 4
     return int(min(512, (150 * 1024 - 64) // max(per, 1)))
+
+
+RF_PACK_BITS = 22  # |rint(y * scale)| <= 2^22 (csrc/forest.hip RF_PACK_BIAS)
+RF_PACK_MAX_WEIGHT = float(1 << 20)  # per work item: (sum w) << 44 must not overflow
+
+
+def rf_pack_scale(y: torch.Tensor) -> float:
+    """Fixed-point scale of the packed regression cells: 2^22 / max|y| (one host read)."""
+    ymax = float(y.abs().max().item()) if y.numel() else 0.0
+    return float(1 << RF_PACK_BITS) / ymax if ymax > 0 else 1.0
 
 
 def rf_interleave(bins: torch.Tensor, rec_bytes: int = 32) -> torch.Tensor:
@@ -732,14 +743,18 @@ def rf_hist(bins: torch.Tensor, idx: torch.Tensor, label: torch.Tensor, wcnt: Op
             items: torch.Tensor, node_feats: torch.Tensor, nodes: int, B: int, S: int,
             regression: bool, pos_weight: Optional[torch.Tensor] = None, fb: Optional[int] = None,
             yscale: Optional[float] = None, exclusive: Optional[Dict[str, torch.Tensor]] = None,
-            bins_il: Optional[torch.Tensor] = None, wide: bool = False, rec_bytes: int = 32) -> torch.Tensor:
+            bins_il: Optional[torch.Tensor] = None, wide: bool = False, rec_bytes: int = 32,
+            packed_scale: Optional[float] = None) -> torch.Tensor:
     """Per-(node, feature slot, bin) statistics: uint32 class counts or fp64 (count, sum[, sumsq]).
     Weights: per row (``wcnt``, indexed by row id) or per position of ``idx`` (``pos_weight``).
     ``items`` rows are (node, row_begin, row_end, feature_chunk) with chunks of ``fb`` features
     (default ``rf_hist_fb(B, S, regression)``). ``bins_il``: the record layout of ``bins``
     (``rf_interleave``) for the device kernel to gather from (same results); ``wide``: the
     1024-thread record-layout kernel with chunks of ``fb = rf_hist_fb_wide(...)`` features, on
-    records of ``rec_bytes`` (the value ``bins_il`` was built with)."""
+    records of ``rec_bytes`` (the value ``bins_il`` was built with). ``packed_scale`` (wide
+    regression, not deterministic): one u64 LDS cell per (feature, bin) holding the weighted count
+    and the sum of w * rint(y * packed_scale), packed_scale = 2^22 / max|y| (``rf_pack_scale``);
+    the caller keeps the weights of one item <= 2^20."""
     if wide and fb is None:
         fb = rf_hist_fb_wide(B, S, regression)
     fb = rf_hist_fb(B, S, regression) if fb is None else int(fb)
@@ -800,9 +815,11 @@ def rf_hist(bins: torch.Tensor, idx: torch.Tensor, label: torch.Tensor, wcnt: Op
         if bins_il is None:
             raise ValueError("the wide histogram kernel reads the record layout: pass bins_il")
         fixed = bool(regression and deterministic())
+        mode = 1 if fixed else (2 if (regression and packed_scale is not None) else 0)
+        ys = float(packed_scale) if mode == 2 else float(yscale)
         native.call("srml_rf_hist_wide", bins_il.data_ptr(), m, idx.data_ptr(), wy.data_ptr(), _c(items).data_ptr(),
-                    int(items.shape[0]), _c(node_feats).data_ptr(), nf, B, S, int(regression), float(yscale), fb,
-                    int(fixed), int(rec_bytes), hist.data_ptr() if not regression else None,
+                    int(items.shape[0]), _c(node_feats).data_ptr(), nf, B, S, int(regression), ys, fb,
+                    mode, int(rec_bytes), hist.data_ptr() if not regression else None,
                     hist.data_ptr() if regression else None, st)
         if fixed:
             native.call("srml_rf_hist_fixed_finish", hist.data_ptr(), hist.numel(), float(yscale), st)

@@ -377,7 +377,16 @@ __device__ __forceinline__ int rec_pick(uint4 a, uint4 b, uint4 c, uint4 d, int 
   return (int)((word >> (8 * (o & 3))) & 0xff);
 }
 
-template <bool REG, bool FIXED, int RB>
+// PACK (regression, non-deterministic): ONE u64 LDS atomic per (row, feature) instead of a u32
+// count + u64 sum: cell = (sum w) << 44 | sum w (yq + 2^22), yq = rint(y * yscale) with yscale =
+// 2^22 / max|y| (|yq| <= 2^22, so every addend's low field is in [0, w 2^23] and never borrows);
+// with sum w <= 2^20 per block (rows per item x max weight, checked by the host) the low field
+// stays below 2^43. Count exact; sum quantised to 2^-22 max|y| per row (fp32-level), unpacked at
+// the flush. Two LDS words per cell instead of three: ~1.5x the features per block.
+constexpr int RF_PACK_SHIFT = 44;
+constexpr long long RF_PACK_BIAS = 1LL << 22;
+
+template <bool REG, bool FIXED, int RB, bool PACK = false>
 __global__ __launch_bounds__(RHW_T) void rf_hist_wide_kernel(const unsigned char* __restrict__ rec, long m,
                                                               const int* __restrict__ idx,
                                                               const float2* __restrict__ wy,
@@ -395,9 +404,9 @@ __global__ __launch_bounds__(RHW_T) void rf_hist_wide_kernel(const unsigned char
   short* s_grp = reinterpret_cast<short*>(hw_u);
   short* s_byo = s_grp + fbw;
   unsigned* cnt = hw_u + ((2 * fbw * (int)sizeof(short) + 15) / 16) * 4;
-  const int cntw = (fbw * B + 1) & ~1;  // u64 sums stay 8-byte aligned for any B
+  const int cntw = PACK ? 0 : (fbw * B + 1) & ~1;  // u64 sums stay 8-byte aligned for any B
   unsigned long long* sum = reinterpret_cast<unsigned long long*>(cnt + cntw);
-  const int words = REG ? cntw + 2 * fbw * B : fbw * B * S;
+  const int words = PACK ? 2 * fbw * B : REG ? cntw + 2 * fbw * B : fbw * B * S;
   for (int i = threadIdx.x; i < words; i += RHW_T) cnt[i] = 0u;
   for (int j = threadIdx.x; j < fbw; j += RHW_T) {
     const int f = j < nfb ? node_feats[(long)node * nf + f_begin + j] : 0;
@@ -416,7 +425,12 @@ __global__ __launch_bounds__(RHW_T) void rf_hist_wide_kernel(const unsigned char
     const float2 a2 = has2 ? wy[i2] : make_float2(0.f, 0.f);
     const unsigned w1 = (unsigned)a1.x, w2 = (unsigned)a2.x;
     unsigned long long s1 = 0ull, s2 = 0ull;
-    if (REG) {
+    if (PACK) {
+      const long long q1 = (long long)rint((double)a1.y * yscale) + RF_PACK_BIAS;
+      const long long q2 = (long long)rint((double)a2.y * yscale) + RF_PACK_BIAS;
+      s1 = ((unsigned long long)w1 << RF_PACK_SHIFT) + (unsigned long long)w1 * (unsigned long long)q1;
+      s2 = ((unsigned long long)w2 << RF_PACK_SHIFT) + (unsigned long long)w2 * (unsigned long long)q2;
+    } else if (REG) {
       s1 = (unsigned long long)(long long)rint((double)a1.x * (double)a1.y * yscale);
       s2 = (unsigned long long)(long long)rint((double)a2.x * (double)a2.y * yscale);
     }
@@ -449,7 +463,10 @@ __global__ __launch_bounds__(RHW_T) void rf_hist_wide_kernel(const unsigned char
       for (int jj = j; jj < je; ++jj) {
         const int o = __builtin_amdgcn_readfirstlane((int)s_byo[jj]);
         const int b1 = rec_pick(qa1, qb1, qc1, qd1, o), b2 = rec_pick(qa2, qb2, qc2, qd2, o);
-        if (REG) {
+        if (PACK) {
+          atomicAdd(&sum[jj * B + b1], s1);
+          if (w2) atomicAdd(&sum[jj * B + b2], s2);
+        } else if (REG) {
           atomicAdd(&cnt[jj * B + b1], w1);
           atomicAdd(&sum[jj * B + b1], s1);
           if (w2) {
@@ -476,7 +493,14 @@ __global__ __launch_bounds__(RHW_T) void rf_hist_wide_kernel(const unsigned char
   const double inv = 1.0 / yscale;
   for (int i = threadIdx.x; i < valid_cells; i += RHW_T) {
     const int j = i / (B * S), rem = i % (B * S), b = rem / S, st = rem % S;
-    if (REG && FIXED) {
+    if (PACK) {
+      const unsigned long long pk = sum[j * B + b];
+      const unsigned long long c = pk >> RF_PACK_SHIFT;
+      const long long lo = (long long)(pk & ((1ull << RF_PACK_SHIFT) - 1ull)) - (long long)c * RF_PACK_BIAS;
+      const double v = st == 0 ? (double)c : (double)lo * inv;
+      if (excl) hist_d[out_base + i] = v;
+      else if (v != 0.0) atomicAdd(&hist_d[out_base + i], v);
+    } else if (REG && FIXED) {
       const unsigned long long q = st == 0 ? (unsigned long long)cnt[j * B + b] : sum[j * B + b];
       unsigned long long* cell = reinterpret_cast<unsigned long long*>(hist_d) + out_base + i;
       if (excl) *cell = q;
@@ -496,7 +520,9 @@ __global__ __launch_bounds__(RHW_T) void rf_hist_wide_kernel(const unsigned char
 // Features per item of the wide kernel for (B, S): the LDS slab (metadata + fbw * B * S' words)
 // within 150 KiB (S' = 3 for regression: count + 64-bit fixed-point sum).
 SRML_API int srml_rf_hist_wide_fb(int B, int S, int regression) {
-  const long per = (long)B * (regression ? 3 : S) * (long)sizeof(unsigned) + 2 * (long)sizeof(short);
+  // regression > 1: the packed single-u64 cells (2 words per (feature, bin))
+  const long per = (long)B * (regression > 1 ? 2 : regression ? 3 : S) * (long)sizeof(unsigned) +
+                   2 * (long)sizeof(short);
   const long fbw = (150L * 1024 - 64) / (per > 0 ? per : 1);
   return (int)(fbw > 512 ? 512 : fbw);
 }
@@ -506,27 +532,31 @@ SRML_API int srml_rf_hist_wide_fb(int B, int S, int regression) {
 SRML_API int srml_rf_hist_wide(const unsigned char* rec, long m, const int* idx, const float* wy, const int* items,
                                int n_items, const int* node_feats, int nf, int B, int S, int regression, double yscale,
                                int fbw, int fixed, int rb, unsigned* hist_u, double* hist_d, hipStream_t stream) {
+  // fixed: 1 = deterministic i64 cells, 2 = packed count/sum cells (yscale = 2^22 / max|y|; the
+  // caller guarantees sum w <= 2^20 per item)
   if (n_items <= 0) return 0;
   if (regression && S != 2) return -6;
   if (fbw < 1 || (reinterpret_cast<uintptr_t>(rec) & 15)) return -7;
   if (rb != 32 && rb != 64) return -2;
+  if (fixed == 2 && !regression) return -2;
   const size_t lds = (size_t)((2 * fbw * sizeof(short) + 15) / 16) * 16 +
-                     ((size_t)fbw * B * (regression ? 3 : S) + 1) * sizeof(unsigned);
+                     ((size_t)fbw * B * (fixed == 2 ? 2 : regression ? 3 : S) + 1) * sizeof(unsigned);
   if (lds > 160 * 1024) return -5;
   const float2* w2 = reinterpret_cast<const float2*>(wy);
   const int4* it = reinterpret_cast<const int4*>(items);
-#define SRML_RF_HW(RG, FX, RBB, YS)                                                                           \
-  do {                                                                                                       \
-    (void)hipFuncSetAttribute((const void*)rf_hist_wide_kernel<RG, FX, RBB>,                                 \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                         \
-    hipLaunchKernelGGL((rf_hist_wide_kernel<RG, FX, RBB>), dim3(n_items), dim3(RHW_T), lds, stream, rec, m, idx, \
-                       w2, it, node_feats, nf, B, S, fbw, YS, hist_u, hist_d);                               \
+#define SRML_RF_HW(RG, FX, RBB, PK, YS)                                                                        \
+  do {                                                                                                        \
+    (void)hipFuncSetAttribute((const void*)rf_hist_wide_kernel<RG, FX, RBB, PK>,                              \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                          \
+    hipLaunchKernelGGL((rf_hist_wide_kernel<RG, FX, RBB, PK>), dim3(n_items), dim3(RHW_T), lds, stream, rec, m, \
+                       idx, w2, it, node_feats, nf, B, S, fbw, YS, hist_u, hist_d);                           \
   } while (0)
-#define SRML_RF_HW_RB(RBB)                                   \
-  do {                                                       \
-    if (regression && fixed) SRML_RF_HW(true, true, RBB, yscale);  \
-    else if (regression) SRML_RF_HW(true, false, RBB, yscale);     \
-    else SRML_RF_HW(false, false, RBB, 1.0);                       \
+#define SRML_RF_HW_RB(RBB)                                                \
+  do {                                                                    \
+    if (regression && fixed == 2) SRML_RF_HW(true, false, RBB, true, yscale); \
+    else if (regression && fixed) SRML_RF_HW(true, true, RBB, false, yscale); \
+    else if (regression) SRML_RF_HW(true, false, RBB, false, yscale);     \
+    else SRML_RF_HW(false, false, RBB, false, 1.0);                       \
   } while (0)
   if (rb == 64) SRML_RF_HW_RB(64);
   else SRML_RF_HW_RB(32);

@@ -373,6 +373,52 @@ def test_rf_hist_wide_identical(gpu_device, monkeypatch, regression, n, nf, rec_
 
 
 @pytest.mark.gpu
+def test_rf_hist_wide_packed_regression(gpu_device):
+    """Packed regression cells (one u64 LDS atomic per row and feature): counts exact, sums within
+    the 2^-22 max|y| per-row quantisation of the exact deterministic histogram; split rows and
+    exclusive nodes as in the unpacked test."""
+    g = torch.Generator().manual_seed(29)
+    n, nf, m, B, nodes = 700, 450, 30000, 64, 4
+    bins = torch.randint(0, B, (n, m), generator=g, dtype=torch.uint8)
+    y = torch.randn(m, generator=g) * 3.0 + 1.0
+    idx = torch.randperm(m, generator=g)[:20000].sort().values.int()
+    w = torch.randint(0, 5, (20000,), generator=g).float()
+    feats = torch.stack([torch.randperm(n, generator=g)[:nf].sort().values for _ in range(nodes)]).int()
+    bounds = [0, 3000, 9000, 15000, 20000]
+
+    def items_for(fb, rows, excl):
+        out = []
+        for node in range(nodes):
+            starts = list(range(bounds[node], bounds[node + 1], rows))
+            flag = (1 << 30) if excl and len(starts) == 1 else 0
+            out += [[node, rb, min(rb + rows, bounds[node + 1]), fc | flag] for rb in starts
+                    for fc in range((nf + fb - 1) // fb)]
+        return torch.tensor(out, dtype=torch.int32)
+
+    d = lambda t: t.to(gpu_device)  # noqa: E731
+    il = ops.rf_interleave(d(bins), 64)
+    fbp = ops.rf_hist_fb_wide(B, 2, True, packed=True)
+    assert fbp > ops.rf_hist_fb_wide(B, 2, True)
+    ps = ops.rf_pack_scale(d(y))
+    multi = d(torch.tensor([1, 2, 3]))
+    got = ops.rf_hist(d(bins), d(idx), d(y), None, d(items_for(fbp, 4096, True)), d(feats), nodes, B, 2, True,
+                      pos_weight=d(w), fb=fbp, yscale=1.0, bins_il=il, wide=True, exclusive={"multi_nodes": multi},
+                      rec_bytes=64, packed_scale=ps).cpu()
+    # exact fp64 oracle on the host
+    ref = torch.zeros((nodes, nf, B, 2), dtype=torch.float64)
+    for node in range(nodes):
+        rows = idx[bounds[node]: bounds[node + 1]].long()
+        wn = w[bounds[node]: bounds[node + 1]].double()
+        for j in range(nf):
+            b = bins[int(feats[node, j]), rows].long()
+            ref[node, j, :, 0].index_add_(0, b, wn)
+            ref[node, j, :, 1].index_add_(0, b, wn * y[rows].double())
+    assert torch.equal(got[..., 0], ref[..., 0])
+    tol = 0.5 / ps * ref[..., 0] + 1e-9  # per-row rounding of y to the 2^-22 max|y| grid
+    assert bool(((got[..., 1] - ref[..., 1]).abs() <= tol).all())
+
+
+@pytest.mark.gpu
 def test_rf_sample_features_uniform_sorted(gpu_device):
     C, n, nf = 4000, 300, 100
     f = ops.rf_sample_features(C, n, nf, 12345, gpu_device).cpu()
