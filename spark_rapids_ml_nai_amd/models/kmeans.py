@@ -77,7 +77,7 @@ def _weighted_lloyd(P: torch.Tensor, w: torch.Tensor, C: torch.Tensor, iters: in
 def init_kmeans_parallel(X: torch.Tensor, xnorm: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext,
                          k: int, seed: int, oversampling: float = 2.0, steps: int = 2,
                          XP: Optional[torch.Tensor] = None, trials: int = 1, mu: Optional[torch.Tensor] = None,
-                         xnorm_split: Optional[torch.Tensor] = None) -> torch.Tensor:
+                         xnorm_split: Optional[torch.Tensor] = None, F16: Any = None) -> torch.Tensor:
     """k-means|| (scalable k-means++, reference cuML ``init="scalable-k-means++"`` / Spark
     ``initMode="k-means||"``): ``steps`` rounds of D^2 over-sampling (ell = oversampling * k rows
     per round, device RNG), candidates all-gathered, weighted by the rows they attract, then reduced
@@ -86,11 +86,15 @@ def init_kmeans_parallel(X: torch.Tensor, xnorm: torch.Tensor, desc: PartitionDe
     the lowest cost.
     The distance passes over X use the split-bf16 MFMA kernel when the Lloyd loop will (``XP``),
     in its 3-product approximate form (D^2 sampling and candidate weights tolerate ~1e-5
-    relative distance error; half the MFMA work of the exact Lloyd passes)."""
+    relative distance error; half the MFMA work of the exact Lloyd passes), or — ``F16`` given
+    (``ops.F16Planes``) — the Lloyd loop's fp16 certified filter (exact labels, a sixth of the
+    exact pass's MFMAs)."""
     dev = X.device
     m = X.shape[0]
 
     def nearest(C: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        if F16 is not None:
+            return ops.nearest_centroid_f16(F16, C.float())
         if XP is not None:  # sampling / weighting only need approximate distances
             return ops.nearest_centroid_split(XP, m, C.float(), xnorm if xnorm_split is None else xnorm_split,
                                               approx=True, mu=mu)
@@ -170,26 +174,38 @@ def kmeans_fit(X: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext, k
                seed: int, init: str = "scalable-k-means++", oversampling: float = 2.0, init_steps: int = 2,
                timer: Any = None) -> Dict[str, Any]:
     n = X.shape[1]
-    xnorm = ops.row_sqnorm(X)
     # k > 256: 256 x 256 LDS-DMA kernel on the tiled plane layout (SRML_SPLIT_TILED=0: plain layout)
     tiled = k > 256 and os.environ.get("SRML_SPLIT_TILED", "1") == "1"
     use_split = _use_split(X, k)
+    centred = use_split and tiled and X.is_cuda
+    xnorm = None if centred else ops.row_sqnorm(X)  # the centred searches use ||x - mu||^2 only
     # filter-and-refine Lloyd search on the tiled planes: 3-product pass + exact re-search of the
     # near-tie rows (SRML_KMEANS_CERTIFIED=0: always the 6-product search). The split search runs
     # on centred data (planes of X - mu, centroids - mu, ||x - mu||^2): distances are unchanged,
     # and the dropped-product error bound scales with ||x - mu|| ||c - mu||, far below the gaps.
     certified = tiled and use_split and X.is_cuda and os.environ.get("SRML_KMEANS_CERTIFIED", "1") == "1"
+    # SRML_KMEANS_FILTER=f16 (default): the certified filter is ONE fp16 MFMA product per (row,
+    # centre) on a scaled fp16 plane of X - mu (ops.F16Planes; a third of the 3-product bf16
+    # filter's MFMAs) with a radius ~2.8x wider; bf16: the 3-product split-bf16 filter
     mu = None
     xnorm_s = xnorm
-    if use_split and tiled and X.is_cuda:
+    F16 = None
+    if centred:
         mu = ops.col_moments(X, need_sq=False)[0].div_(max(X.shape[0], 1)).float()
-        xnorm_s = ops.row_sqnorm(X, mu)
-    XP = ops.split_bf16x3(X, tiled=tiled, mu=mu) if use_split else None
+        if certified and ops.kmeans_filter_mode() == "f16":
+            F16 = ops.F16Planes(X, mu)
+            if F16.ok:
+                xnorm_s = F16.xnorm
+            else:
+                F16 = None
+        if F16 is None:
+            xnorm_s = ops.row_sqnorm(X, mu)
+    XP = ops.split_bf16x3(X, tiled=tiled, mu=mu) if use_split and F16 is None else None
     if init in ("random",):
         C = init_random(X, desc, ctx, k, seed)
     elif init in ("scalable-k-means++", "k-means||", "k-means++"):
         C = init_kmeans_parallel(X, xnorm, desc, ctx, k, seed, oversampling, init_steps, XP=XP, mu=mu,
-                                 xnorm_split=xnorm_s)
+                                 xnorm_split=xnorm_s, F16=F16)
     else:
         raise ValueError("Unsupported init mode %s" % init)
     C = C.double()
@@ -199,7 +215,9 @@ def kmeans_fit(X: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext, k
     st0 = dict(ops._CERTIFY_STATS)
     for it in range(max(0, max_iter)):
         n_iter = it + 1
-        if XP is not None:
+        if F16 is not None:
+            labels, d2 = ops.nearest_centroid_f16(F16, C.float())
+        elif XP is not None:
             labels, d2 = ops.nearest_centroid_split(XP, X.shape[0], C.float(), xnorm_s, X=X if certified else None,
                                                     mu=mu)
         else:
@@ -215,7 +233,7 @@ def kmeans_fit(X: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext, k
         C = newC
         if shift <= tol2:
             break
-    del XP
+    del XP, F16
     return {
         "cluster_centers_": C.cpu().numpy(),  # ndarray: 3M-float .tolist() cost 40 ms per fit
         "n_cols": int(n),
@@ -236,6 +254,10 @@ def kmeans_predict(X: torch.Tensor, C: torch.Tensor) -> torch.Tensor:
     if (X.is_cuda and k > 256 and X.shape[0] >= 65536 and _use_split(X, k)
             and os.environ.get("SRML_KMEANS_PREDICT_SPLIT", "1") == "1"):
         mu = ops.col_moments(X, need_sq=False)[0].div_(X.shape[0]).float()
+        if ops.kmeans_filter_mode() == "f16":
+            F16 = ops.F16Planes(X, mu)
+            if F16.ok:
+                return ops.nearest_centroid_f16(F16, C.float())[0]
         XP = ops.split_bf16x3(X, tiled=True, mu=mu)
         labels, _ = ops.nearest_centroid_split(XP, X.shape[0], C.float(), ops.row_sqnorm(X, mu), X=X, mu=mu)
         return labels

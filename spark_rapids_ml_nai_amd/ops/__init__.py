@@ -441,6 +441,127 @@ def _nearest_centroid_certified(XP: torch.Tensor, X: torch.Tensor, m: int, k: in
 _CERTIFY_STATS = {"rows": 0, "refined": 0}  # filter-and-refine counters (diagnostics / tests)
 
 
+# ---- fp16 certified filter -----------------------------------------------------------------
+F16_U = 2.0 ** -11  # unit roundoff of fp16
+F16_A = 2.0 ** -14  # absolute error of an fp16 element below the normal range (flushed or subnormal), scaled units
+
+
+def certify_tau16(n: int) -> float:
+    """Radius of the one-product fp16 filter relative to ||x - mu|| ||c - mu||: the fp16 rounding of
+    both operands (2u + u^2, u = 2^-11; the absolute subnormal term is separate, ``f16_radius_terms``),
+    the fp32 accumulation of the filter's n exact fp16 products and of the exact 6-product search
+    (each <= n 2^-24 ||x|| ||c||, Cauchy-Schwarz), the exact search's dropped products (< 2^-20),
+    times 1.01 (fp32 evaluation of the norms and of the test itself)."""
+    return 1.01 * (2.0 * F16_U + F16_U * F16_U + 2.0 ** -20 + 2.01 * float(n) * 2.0 ** -24)
+
+
+def f16_radius_terms(n: int, scale: float, tau: float) -> Tuple[float, float, float]:
+    """(xadd, z, z2) of the fp16 filter's certificate: with a = 2^-14 / scale (per-element absolute
+    error outside the normal range) the dot-product error gains 2 a sqrt(n) (1 + u)(||v|| + ||w||) + 2 n a^2
+    on top of tau ||v|| ||w||; written per candidate j as (||v|| + xadd) g_j + z ||v|| + z2 with
+    g_j = 2 tau ||w_j||, i.e. xadd = z / (2 tau)."""
+    a = F16_A / scale
+    z = 2.02 * a * math.sqrt(n) * (1.0 + F16_U)
+    z2 = 2.02 * float(n) * a * a
+    return z / (2.0 * tau), z, z2
+
+
+class F16Planes:
+    """The fp16 filter's operand for one X: ONE tiled fp16 plane of s (x - mu) (2 B per element
+    instead of the 3-product search's 4 staged / 6 stored), the centred row norms and s.
+
+    s is a power of two putting max |x - mu| in [2^13, 2^14) (fp16 max 65504): one pass over X
+    computes the centred norms and that maximum (``srml_row_sqnorm_centered_amax_f32``), and one
+    host read of it picks s. ``ok`` is False when the data have no finite non-zero range (the
+    caller then keeps the bf16 3-product filter)."""
+
+    def __init__(self, X: torch.Tensor, mu: torch.Tensor) -> None:
+        m, n = X.shape
+        self.X, self.m, self.n = X, m, n
+        self.mu = _c(mu.float().view(-1))
+        dev = X.device
+        st = native.stream(dev)
+        self.xnorm = torch.empty(m, dtype=torch.float32, device=dev)
+        amax = torch.zeros(1, dtype=torch.int32, device=dev)
+        native.call("srml_row_sqnorm_centered_amax_f32", X.data_ptr(), m, n, X.stride(0), self.mu.data_ptr(),
+                    self.xnorm.data_ptr(), amax.data_ptr(), st)
+        a = float(amax.view(torch.float32).item())
+        self.ok = math.isfinite(a) and a > 0.0
+        self.scale = 1.0
+        self.P = None
+        if not self.ok:
+            return
+        e = math.frexp(a)[1] - 1  # a in [2^e, 2^(e+1))
+        if not -100 <= 13 - e <= 100:
+            self.ok = False
+            return
+        self.scale = 2.0 ** (13 - e)
+        self.kp = (n + 15) // 16 * 16
+        self.rows_pad = max(256, (m + 255) // 256 * 256)
+        self.P = torch.empty((self.rows_pad // 256, self.kp // 16, 256, 16), dtype=torch.float16, device=dev)
+        self.ovf = torch.zeros(1, dtype=torch.int32, device=dev)
+        native.call("srml_split_f16_tiled_centered", X.data_ptr(), m, n, X.stride(0), self.mu.data_ptr(), self.kp,
+                    self.rows_pad, self.scale, self.P.data_ptr(), self.ovf.data_ptr(), st)
+        self.tau = certify_tau16(n)
+        self.xadd, self.z, self.z2 = f16_radius_terms(n, self.scale, self.tau)
+
+
+def nearest_centroid_f16(F: F16Planes, C: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(labels, squared distances) of F.X's rows under centres C by the fp16 certified filter:
+    one fp16 MFMA product per (row, centre) on the scaled planes (a third of the 3-product bf16
+    filter's MFMAs, half its staged bytes) keeps each row's best and the lowest lower bound of the
+    others under the radius ``certify_tau16`` / ``f16_radius_terms``; rows it cannot certify (and
+    every row if a centre fell outside the fp16 range) are re-searched with the fp32-exact
+    6-product kernel. The labels are those of the exact search; a certified row's distance is the
+    filter's (within its radius: inertia / D^2 weights), a re-searched row's the exact one."""
+    m, k, dev = F.m, C.shape[0], F.X.device
+    st = native.stream(dev)
+    W = _c(C.float().to(dev) - F.mu.view(1, -1))  # centred centres: the exact search's operands
+    cn = (W * W).sum(1)
+    crows = max(256, (k + 255) // 256 * 256)
+    CP = torch.empty((crows // 256, F.kp // 16, 256, 16), dtype=torch.float16, device=dev)
+    F.ovf.zero_()  # X's own plane never overflows (s comes from its maximum); only the centres can
+    native.call("srml_split_f16_tiled_centered", W.data_ptr(), k, F.n, W.stride(0), None, F.kp, crows, F.scale,
+                CP.data_ptr(), F.ovf.data_ptr(), st)
+    cg = (2.0 * F.tau) * cn.clamp_min(0).sqrt()
+    nslot = int(native.lib().srml_nearest_centroid_f16_top2_nslot(k))
+    keys = torch.empty(m * nslot, dtype=torch.int64, device=dev)
+    lob = torch.empty(m * nslot, dtype=torch.float32, device=dev)
+    native.call("srml_nearest_centroid_f16_top2", F.P.data_ptr(), m, F.rows_pad, F.kp, CP.data_ptr(), k, crows,
+                cn.data_ptr(), cg.data_ptr(), F.xnorm.data_ptr(), -2.0 / (F.scale * F.scale), F.xadd, keys.data_ptr(),
+                lob.data_ptr(), st)
+    labels = torch.empty(m, dtype=torch.int32, device=dev)
+    dist = torch.empty(m, dtype=torch.float32, device=dev)
+    flagged = torch.empty(m, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    native.call("srml_split_top2_select_f16", keys.data_ptr(), lob.data_ptr(), m, nslot, F.xnorm.data_ptr(),
+                cg.data_ptr(), F.xadd, F.z, F.z2, F.ovf.data_ptr(), labels.data_ptr(), dist.data_ptr(),
+                flagged.data_ptr(), cnt.data_ptr(), st)
+    del keys, lob
+    nf = int(cnt.item())
+    _CERTIFY_STATS["rows"] += m
+    _CERTIFY_STATS["refined"] += nf
+    if nf:
+        rows = flagged[:nf]
+        XPr = split_bf16x3(F.X.index_select(0, rows.long()), tiled=True, mu=F.mu)
+        CPb = split_bf16x3(W, 256, tiled=True)
+        best = torch.full((nf,), -1, dtype=torch.int64, device=dev)
+        native.call("srml_nearest_centroid_split_tiled_np", XPr.data_ptr(), nf, XPr.shape[1] * 256, F.kp,
+                    CPb.data_ptr(), k, CPb.shape[1] * 256, cn.data_ptr(), best.data_ptr(), 6, st)
+        native.call("srml_split_scatter_refined", best.data_ptr(), rows.data_ptr(), nf, F.xnorm.data_ptr(),
+                    labels.data_ptr(), dist.data_ptr(), st)
+    return labels, dist
+
+
+def kmeans_filter_mode() -> str:
+    """``SRML_KMEANS_FILTER``: ``f16`` (default: one-product fp16 certified filter) or ``bf16``
+    (3-product split-bf16 certified filter)."""
+    v = os.environ.get("SRML_KMEANS_FILTER", "f16").lower()
+    if v not in ("f16", "bf16"):
+        raise ValueError("SRML_KMEANS_FILTER must be f16 or bf16, got %r" % v)
+    return v
+
+
 def nearest_centroid_split(XP: torch.Tensor, m: int, C: torch.Tensor, xnorm: torch.Tensor,
                            cnorm: Optional[torch.Tensor] = None, approx: bool = False,
                            X: Optional[torch.Tensor] = None, mu: Optional[torch.Tensor] = None

@@ -350,11 +350,13 @@ SRML_API int srml_fold_partials_f64(const double* ws, long parts, long pstride, 
 
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void row_sqnorm_kernel(const float* __restrict__ X, long m, int n, long ld,
-                                                         float* __restrict__ out, const float* __restrict__ mu) {
+                                                         float* __restrict__ out, const float* __restrict__ mu,
+                                                         unsigned* __restrict__ amax = nullptr) {
   const int lane = threadIdx.x & 63;
   const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const long nw = (long)gridDim.x * 4;
   const bool vec = ((ld & 3) == 0) && ((n & 3) == 0);
+  float mx = 0.f;  // max |x - mu| seen by this lane (amax: the fp16 KMeans filter's plane scale)
   for (long r = wave; r < m; r += nw) {
     const float* row = X + r * ld;
     float s = 0.f;
@@ -366,15 +368,21 @@ __global__ __launch_bounds__(256) void row_sqnorm_kernel(const float* __restrict
           v[0] -= c[0]; v[1] -= c[1]; v[2] -= c[2]; v[3] -= c[3];
         }
         s = fmaf(v[0], v[0], fmaf(v[1], v[1], fmaf(v[2], v[2], fmaf(v[3], v[3], s))));
+        if (amax) mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
       }
     } else {
       for (int d = lane; d < n; d += 64) {
         const float v = mu ? row[d] - mu[d] : row[d];
         s = fmaf(v, v, s);
+        mx = fmaxf(mx, fabsf(v));
       }
     }
     s = wave_sum(s);
     if (lane == 0) out[r] = s;
+  }
+  if (amax) {
+    mx = wave_max(mx);  // non-negative floats order like their bit patterns
+    if (lane == 0) atomicMax(amax, __float_as_uint(mx));
   }
 }
 
@@ -395,6 +403,18 @@ SRML_API int srml_row_sqnorm_centered_f32(const float* X, long m, int n, long ld
   long blocks = (m + 3) / 4;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(row_sqnorm_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, X, m, n, ld, out, mu);
+  return srml_status();
+}
+
+// ||x_r - mu||^2 per row plus max |x - mu| over the whole matrix into *amax (float bits, caller
+// zeroes it): one pass over X for both the centred norms and the fp16 filter plane's scale
+SRML_API int srml_row_sqnorm_centered_amax_f32(const float* X, long m, int n, long ld, const float* mu, float* out,
+                                               unsigned* amax, hipStream_t stream) {
+  if (m <= 0) return 0;
+  if (reinterpret_cast<uintptr_t>(mu) & 15) return -5;
+  long blocks = (m + 3) / 4;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(row_sqnorm_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, X, m, n, ld, out, mu, amax);
   return srml_status();
 }
 

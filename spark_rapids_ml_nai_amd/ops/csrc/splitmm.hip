@@ -34,6 +34,7 @@ using srml_tile::orderable;
 using srml_tile::unorderable;
 
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
 typedef unsigned uintx4 __attribute__((ext_vector_type(4)));
 typedef unsigned uintx2 __attribute__((ext_vector_type(2)));
 
@@ -132,6 +133,59 @@ __global__ __launch_bounds__(256) void split_tiled_kernel(const float* __restric
   }
 }
 
+// One fp16 plane of s (x - mu) in the same tiled, swizzled image layout (the fp16 certified
+// filter, srml_nearest_centroid_f16_top2): s is a power of two chosen by the caller from
+// max |x - mu| so the largest element lands in [2^13, 2^14) (headroom for centroids, which are
+// convex combinations of rows); an element with |s v| >= 2^15 (a centroid outside the data's
+// range) sets *ovf, and the select phase then re-searches every row exactly.
+__global__ __launch_bounds__(256) void split_tiled_f16_kernel(const float* __restrict__ X, long m, int n, long ld, int kp,
+                                                              long rows_pad, unsigned short* __restrict__ P,
+                                                              const float* __restrict__ mu, float scale,
+                                                              int* __restrict__ ovf) {
+  const int ks_n = kp >> 4;
+  const long total = rows_pad * ks_n;
+  const bool vec = (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
+  bool over = false;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long img = i >> 8;
+    const int rr = (int)(i & 255);
+    const long tile = img / ks_n;
+    const int c0 = (int)(img - tile * ks_n) * 16;
+    const long r = tile * 256 + rr;
+    float x[16];
+    if (vec && r < m && c0 + 16 <= n) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const floatx4 v = *reinterpret_cast<const floatx4*>(X + r * ld + c0 + 4 * q);
+        x[4 * q] = v[0]; x[4 * q + 1] = v[1]; x[4 * q + 2] = v[2]; x[4 * q + 3] = v[3];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) x[j] = (r < m && c0 + j < n) ? X[r * ld + c0 + j] : 0.f;
+    }
+    unsigned hw[8];
+#pragma unroll
+    for (int j = 0; j < 16; j += 2) {
+      unsigned h2[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        float v = x[j + u];
+        if (mu && r < m && c0 + j + u < n) v -= mu[c0 + j + u];  // the same fp32 x - mu as the exact search
+        v *= scale;                                             // power of two: exact
+        if (fabsf(v) >= 32768.f) { over = true; v = v > 0.f ? 32768.f : -32768.f; }
+        const _Float16 hv = (_Float16)v;                        // round to nearest even
+        h2[u] = (unsigned)__builtin_bit_cast(unsigned short, hv);
+      }
+      hw[j / 2] = h2[0] | (h2[1] << 16);
+    }
+    const int sw = (rr >> 3) & 1;
+    uintx4* d = reinterpret_cast<uintx4*>(P + (img << 12) + rr * 16);
+    d[sw] = uintx4{hw[0], hw[1], hw[2], hw[3]};
+    d[sw ^ 1] = uintx4{hw[4], hw[5], hw[6], hw[7]};
+  }
+  if (over) atomicOr(ovf, 1);
+}
+
 constexpr int SBK = 16;
 constexpr int ROWB = 24;  // padded LDS row: 16 bf16 + 8 pad = 48 B
 
@@ -225,7 +279,8 @@ __device__ __forceinline__ void split_epilogue_top2(const floatx16 (&acc)[BM / W
                                                     const float* __restrict__ cnorm, const float* __restrict__ cg,
                                                     const float* __restrict__ xnorm,
                                                     unsigned long long* __restrict__ keys, float* __restrict__ lob,
-                                                    int nslot, int wm, int wn, int li, int lk) {
+                                                    int nslot, int wm, int wn, int li, int lk, float dscale,
+                                                    float xadd) {
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
   float cn[TN], g[TN];
   int cj[TN];
@@ -241,13 +296,13 @@ __device__ __forceinline__ void split_epilogue_top2(const floatx16 (&acc)[BM / W
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const long row = row0 + wm * (BM / WM) + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
-      const float xs = row < m ? sqrtf(fmaxf(xnorm[row], 0.f)) : 0.f;
+      const float xs = row < m ? sqrtf(fmaxf(xnorm[row], 0.f)) + xadd : 0.f;
       float bv = __builtin_huge_valf(), badj = __builtin_huge_valf(), sadj = __builtin_huge_valf();
       int bi = 0x7fffffff;
 #pragma unroll
       for (int nt = 0; nt < TN; ++nt) {
         if (cj[nt] < k) {
-          const float d = fmaf(-2.f, acc[mt][nt][r], cn[nt]);
+          const float d = fmaf(dscale, acc[mt][nt][r], cn[nt]);
           const float adj = fmaf(-xs, g[nt], d);
           if (d < bv) { sadj = fminf(sadj, badj); bv = d; bi = cj[nt]; badj = adj; }
           else sadj = fminf(sadj, adj);
@@ -416,20 +471,26 @@ template <bool TILED, int NP = 6, bool TOP2 = false, int WN_ = 4, bool PRIO = fa
 __global__ __launch_bounds__(WN_ * 128, WN_ == 4 ? 1 : 2) void nearest_centroid_split_glds_kernel(
     const unsigned short* __restrict__ XP, long m, long xrows, int kp, const unsigned short* __restrict__ CP, int k,
     long crows, const float* __restrict__ cnorm, unsigned long long* __restrict__ best, int n_ctiles,
-    float* __restrict__ lob = nullptr, const float* __restrict__ cg = nullptr, const float* __restrict__ xnorm = nullptr) {
+    float* __restrict__ lob = nullptr, const float* __restrict__ cg = nullptr, const float* __restrict__ xnorm = nullptr,
+    float dscale = -2.f, float xadd = 0.f) {
   static_assert(WN_ == 4 || (WN_ == 2 && NP == 3), "256 x 128 tiles are built for the 3-product pass");
+  static_assert(NP == 6 || NP == 3 || (NP == 1 && TOP2 && WN_ == 4), "NP = 1 is the fp16 certified filter");
   constexpr int BM = 256, WM = 2, WN = WN_, BN = 64 * WN, TM = 4, TN = 2;
   // planes staged per operand: h, m, l for the 6-product set; the 3-product set (h.h, h.m, m.h)
   // never touches the l planes, so it stages 2 per operand (2/3 of the DMA and LDS traffic)
-  constexpr int NPL = NP == 6 ? 3 : 2;
+  constexpr int NPL = NP == 6 ? 3 : (NP == 3 ? 2 : 1);
   constexpr int XCH = NPL * (BM / 32), CCH = NPL * (BN / 32);  // 1 KiB staging chunks per stage
   constexpr int CPW = (XCH + CCH) / (WM * WN);                  // ... per wave
   static_assert((XCH + CCH) % (WM * WN) == 0, "chunks split evenly over the waves");
   // ring depth: a 3-product k step is half the MFMA time of a 6-product one, so the 8-wave block's
   // loads get one more step of lead (4 stages x 32 KiB = 128 KiB; the 6-product ring is 3 x 48 KiB);
   // the 4-wave block keeps 3 stages (3 x 24 KiB) so two blocks fit a CU
-  constexpr bool PAIRS = NP == 3 && WN_ == 4;
-  constexpr int NS = PAIRS ? 4 : 3;
+  // NP = 1 (one fp16 plane per operand, 16 KiB stages): a k step is a third of a 3-product one,
+  // so three steps share a barrier and the ring holds three such groups (9 stages, 144 KiB): the
+  // loads of group g + 2 are issued while group g computes (two groups of HBM-latency cover)
+  constexpr int KPB = NP == 1 ? 3 : (NP == 3 && WN_ == 4 ? 2 : 1);  // k steps per barrier
+  constexpr int NG = NP == 1 ? 3 : 2;                                // groups in the ring
+  constexpr int NS = KPB > 1 ? NG * KPB : 3;
   constexpr int STAGE = NPL * (BM + BN) * 16;  // elements: X planes [NPL][BM][16], then C planes [NPL][BN][16]
   __shared__ __attribute__((aligned(1024))) unsigned short lds[NS][STAGE];
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -504,18 +565,24 @@ __global__ __launch_bounds__(WN_ * 128, WN_ == 4 ? 1 : 2) void nearest_centroid_
         fa[p] = *reinterpret_cast<const bf16x8*>(&lds[st][(p * BM + wm * (BM / WM) + mt * 32 + li) * 16 + 8 * ph]);
 #pragma unroll
       for (int nt = 0; nt < TN; ++nt) {
-        if constexpr (NP == 6) {
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[0][nt], acc[mt][nt], 0, 0, 0);
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1][nt], acc[mt][nt], 0, 0, 0);
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[2][nt], acc[mt][nt], 0, 0, 0);
+        if constexpr (NP == 1) {
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(halfx8, fa[0]),
+                                                               __builtin_bit_cast(halfx8, fb[0][nt]), acc[mt][nt], 0,
+                                                               0, 0);
+        } else {
+          if constexpr (NP == 6) {
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[0][nt], acc[mt][nt], 0, 0, 0);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1][nt], acc[mt][nt], 0, 0, 0);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[2][nt], acc[mt][nt], 0, 0, 0);
+          }
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[0][nt], acc[mt][nt], 0, 0, 0);
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[1][nt], acc[mt][nt], 0, 0, 0);
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0][nt], acc[mt][nt], 0, 0, 0);
         }
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[0][nt], acc[mt][nt], 0, 0, 0);
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[1][nt], acc[mt][nt], 0, 0, 0);
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0][nt], acc[mt][nt], 0, 0, 0);
       }
     }
   };
-  if constexpr (!PAIRS) {
+  if constexpr (KPB == 1) {
     // 3-stage ring, one k step per barrier, two steps of load lead
     static_assert(CPW == 6, "the counted wait below leaves one step (CPW loads) in flight");
     issue(0, 0);
@@ -532,25 +599,31 @@ __global__ __launch_bounds__(WN_ * 128, WN_ == 4 ? 1 : 2) void nearest_centroid_
       stage = stage == 2 ? 0 : stage + 1;
     }
   } else {
-    // 3-product steps carry half the MFMA work: two k steps per barrier on a 4-stage ring (pair p
-    // computes from stages 2p, 2p + 1 mod 4 while pair p + 1 lands in the other two), so the
-    // barrier and the first fragment reads are paid once per 24 MFMAs per wave instead of 12
-    issue(0, 0);
-    if (nk > 1) issue(1, 1);
-    for (int kt = 0; kt < nk; kt += 2) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // steps kt, kt + 1 landed; every wave finished kt - 2, kt - 1
-      if (kt + 2 < nk) issue(kt + 2, (kt + 2) & 3);
-      if (kt + 3 < nk) issue(kt + 3, (kt + 3) & 3);
+    // 3-product steps carry half the MFMA work (fp16 1-product steps a sixth): KPB k steps per
+    // barrier on a 2 KPB-stage ring (group g computes from its KPB stages while group g + 1 lands
+    // in the other KPB), so the barrier and the first fragment reads are paid once per KPB steps
+    // NG = 3: the newest group may stay in flight at the wait (counted vmcnt: the group after
+    // this one is full, else wait for everything)
+#pragma unroll
+    for (int j = 0; j < (NG - 1) * KPB; ++j)
+      if (j < nk) issue(j, j);
+    for (int kt = 0; kt < nk; kt += KPB) {
+      if (NG == 3 && kt + 2 * KPB <= nk) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(KPB * CPW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // steps kt .. kt + KPB - 1 landed; every wave finished the previous group
+#pragma unroll
+      for (int j = 0; j < KPB; ++j)
+        if (kt + (NG - 1) * KPB + j < nk) issue(kt + (NG - 1) * KPB + j, (kt + (NG - 1) * KPB + j) % NS);
       if (PRIO) __builtin_amdgcn_s_setprio(1);
-      compute(kt & 3);
-      if (kt + 1 < nk) compute((kt + 1) & 3);
+#pragma unroll
+      for (int j = 0; j < KPB; ++j)
+        if (kt + j < nk) compute((kt + j) % NS);
       if (PRIO) __builtin_amdgcn_s_setprio(0);
     }
   }
   if (TOP2)
     split_epilogue_top2<BM, BN, WM, WN>(acc, row0, col0, ctile, m, k, cnorm, cg, xnorm, best, lob, n_ctiles * WN, wm,
-                                        wn, li, lk);
+                                        wn, li, lk, dscale, xadd);
   else
     split_epilogue<BM, BN, WM, WN>(acc, row0, col0, m, k, cnorm, best, wm, wn, li, lk);
 }
@@ -566,7 +639,12 @@ __global__ __launch_bounds__(256) void split_top2_select_kernel(const unsigned l
                                                                 const float* __restrict__ xnorm,
                                                                 const float* __restrict__ cg,
                                                                 int* __restrict__ labels, float* __restrict__ dist,
-                                                                int* __restrict__ flagged, int* __restrict__ n_flagged) {
+                                                                int* __restrict__ flagged, int* __restrict__ n_flagged,
+                                                                float xadd = 0.f, float z = 0.f, float z2 = 0.f,
+                                                                const int* __restrict__ ovf = nullptr) {
+  // fp16 filter (srml_split_top2_select_f16): the radius of candidate j is (||x|| + xadd) g_j +
+  // z ||x|| + z2 (the last two terms: subnormal fp16 elements, the same for every j, so they enter
+  // the test once per side); an overflowed centroid plane (*ovf) certifies nothing
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= m) return;
   // slot-major layout (keys / lob[slot * m + row]): consecutive lanes read consecutive rows
@@ -577,7 +655,9 @@ __global__ __launch_bounds__(256) void split_top2_select_kernel(const unsigned l
     if (v < k1) { k1 = v; s1 = s; }
   }
   const float xn = xnorm[i];
-  const float xs = sqrtf(fmaxf(xn, 0.f));
+  const float xs0 = sqrtf(fmaxf(xn, 0.f));
+  const float xs = xs0 + xadd;
+  const float c2 = 2.f * fmaf(z, xs0, z2);
   float low = __builtin_huge_valf();  // min over j != b of d~_j - e_j
   for (int s = 0; s < nslot; ++s) {
     low = fminf(low, lob[(long)s * m + i]);
@@ -585,7 +665,7 @@ __global__ __launch_bounds__(256) void split_top2_select_kernel(const unsigned l
     if (s != s1 && v != ~0ull) low = fminf(low, fmaf(-xs, cg[(int)(v & 0xffffffffu)], unorderable((unsigned)(v >> 32))));
   }
   const float bv = unorderable((unsigned)(k1 >> 32));
-  if (k1 != ~0ull && low > fmaf(xs, cg[(int)(k1 & 0xffffffffu)], bv)) {
+  if (k1 != ~0ull && !(ovf && *ovf) && low > fmaf(xs, cg[(int)(k1 & 0xffffffffu)], bv) + c2) {
     labels[i] = (int)(k1 & 0xffffffffu);
     const float d = bv + xn;
     dist[i] = d > 0.f ? d : 0.f;
@@ -776,5 +856,61 @@ SRML_API int srml_split_scatter_refined(const unsigned long long* best, const in
   if (nf <= 0) return 0;
   hipLaunchKernelGGL(split_scatter_refined_kernel, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, stream, best,
                      rows, nf, xnorm, labels, dist);
+  return srml_status();
+}
+
+// ---- fp16 certified filter -----------------------------------------------------------------
+// One tiled fp16 plane of scale * (x - mu) (mu may be null), rows padded to rows_pad (% 256 == 0):
+// P = [rows_pad / 256][kp / 16][256][16]; *ovf |= 1 if an element of |scale v| >= 2^15 was clamped.
+SRML_API int srml_split_f16_tiled_centered(const float* X, long m, int n, long ld, const float* mu, int kp,
+                                           long rows_pad, float scale, unsigned short* P, int* ovf,
+                                           hipStream_t stream) {
+  if (rows_pad <= 0) return 0;
+  if ((kp & 15) || kp < n || rows_pad < m || (rows_pad & 255)) return -2;
+  if ((reinterpret_cast<uintptr_t>(P) & 15) != 0) return -5;
+  const long total = rows_pad * (long)(kp / 16);
+  long blocks = (total + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(split_tiled_f16_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, X, m, n, ld, kp, rows_pad, P,
+                     mu, scale, ovf);
+  return srml_status();
+}
+
+// Certified fp16 filter, phase 1: one fp16 MFMA product per (row, centroid) on the scaled planes
+// (XP, CP from srml_split_f16_tiled_centered with the same scale s); d~ = ||c||^2 + dscale acc with
+// dscale = -2 / s^2; lower bounds use the radius (||x|| + xadd) g_j. 256 x 256 tiles, keys / lob
+// sized m * srml_nearest_centroid_split_top2_nslot(k) as the 3-product pass at SRML_SPLIT_BN3=256.
+SRML_API int srml_nearest_centroid_f16_top2(const unsigned short* XP, long m, long xrows, int kp,
+                                            const unsigned short* CP, int k, long crows, const float* cnorm,
+                                            const float* cg, const float* xnorm, float dscale, float xadd,
+                                            unsigned long long* keys, float* lob, hipStream_t stream) {
+  if (m <= 0 || k <= 0) return 0;
+  if ((kp & 15) || xrows < m || crows < k || (crows & 255) || (xrows & 255)) return -2;
+  if ((reinterpret_cast<uintptr_t>(XP) & 15) || (reinterpret_cast<uintptr_t>(CP) & 15)) return -5;
+  const long rt = (m + 255) / 256;
+  const int ct = (k + 255) / 256;
+  const long nb = rt * ct;
+  if (nb > 0x7fffffffL) return -3;
+  static const bool prio = !(getenv("SRML_SPLIT_PRIO") && atoi(getenv("SRML_SPLIT_PRIO")) == 0);
+  if (prio)
+    hipLaunchKernelGGL((nearest_centroid_split_glds_kernel<true, 1, true, 4, true>), dim3((unsigned)nb), dim3(512), 0,
+                       stream, XP, m, xrows, kp, CP, k, crows, cnorm, keys, (int)ct, lob, cg, xnorm, dscale, xadd);
+  else
+    hipLaunchKernelGGL((nearest_centroid_split_glds_kernel<true, 1, true, 4, false>), dim3((unsigned)nb), dim3(512), 0,
+                       stream, XP, m, xrows, kp, CP, k, crows, cnorm, keys, (int)ct, lob, cg, xnorm, dscale, xadd);
+  return srml_status();
+}
+
+// (row, slot) pairs of the fp16 filter (256-wide centroid tiles, 4 wave columns each)
+SRML_API int srml_nearest_centroid_f16_top2_nslot(int k) { return ((k + 255) / 256) * 4; }
+
+// phase 2 of the fp16 filter: as srml_split_top2_select with the extra radius terms (see kernel)
+SRML_API int srml_split_top2_select_f16(const unsigned long long* keys, const float* lob, long m, int nslot,
+                                        const float* xnorm, const float* cg, float xadd, float z, float z2,
+                                        const int* ovf, int* labels, float* dist, int* flagged, int* n_flagged,
+                                        hipStream_t stream) {
+  if (m <= 0) return 0;
+  hipLaunchKernelGGL(split_top2_select_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream, keys, lob, m,
+                     nslot, xnorm, cg, labels, dist, flagged, n_flagged, xadd, z, z2, ovf);
   return srml_status();
 }

@@ -73,6 +73,11 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_nearest_centroid_split_top2": (_P, _L, _L, _I, _P, _I, _L, _P, _P, _P, _P, _P, _P),
     "srml_split_bf16x3_tiled_centered": (_P, _L, _I, _L, _P, _I, _L, _P, _P),
     "srml_row_sqnorm_centered_f32": (_P, _L, _I, _L, _P, _P, _P),
+    "srml_row_sqnorm_centered_amax_f32": (_P, _L, _I, _L, _P, _P, _P, _P),
+    "srml_split_f16_tiled_centered": (_P, _L, _I, _L, _P, _I, _L, _F, _P, _P, _P),
+    "srml_nearest_centroid_f16_top2": (_P, _L, _L, _I, _P, _I, _L, _P, _P, _P, _F, _F, _P, _P, _P),
+    "srml_nearest_centroid_f16_top2_nslot": (_I,),
+    "srml_split_top2_select_f16": (_P, _P, _L, _I, _P, _P, _F, _F, _F, _P, _P, _P, _P, _P, _P),
     "srml_nearest_centroid_split_top2_nslot": (_I,),
     "srml_split_top2_select": (_P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _P),
     "srml_split_scatter_refined": (_P, _P, _I, _P, _P, _P, _P),

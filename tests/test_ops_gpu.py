@@ -728,6 +728,62 @@ def test_nearest_centroid_certified_matches_exact(gpu_device, m, n, k, ties):
         assert refined < m // 2  # the filter certifies most rows on generic data
 
 
+@pytest.mark.parametrize("m,n,k,ties,shift", [(5000, 3000, 1000, False, 0.0), (4096, 200, 300, True, 0.0),
+                                               (3000, 517, 257, False, 1e4), (2000, 64, 600, True, -3.0)])
+def test_nearest_centroid_f16_certified_matches_exact(gpu_device, m, n, k, ties, shift):
+    """fp16 one-product certified filter + exact re-search == the fp32-exact 6-product search:
+    identical labels (incl. engineered near-ties, a large common offset and odd widths)."""
+    X = _rand(m, n, gpu_device, seed=31) + shift
+    C = _rand(k, n, gpu_device, seed=32) + shift
+    if ties:
+        C[1::2] = C[0::2][: C[1::2].shape[0]] + 1e-6 * torch.randn_like(C[1::2])
+        X[: m // 4] = 0.5 * (C[0].view(1, -1) + C[2].view(1, -1)) + 1e-7 * torch.randn_like(X[: m // 4])
+    mu = ops.col_moments(X, need_sq=False)[0].div_(m).float()
+    F = ops.F16Planes(X, mu)
+    assert F.ok and 2.0 ** 13 <= F.scale * (X - mu).abs().max().item() < 2.0 ** 14
+    torch.testing.assert_close(F.xnorm.double(), ((X.double() - mu.double()) ** 2).sum(1), rtol=1e-5, atol=1e-3)
+    # the plane holds fp16(s (x - mu)) in the tiled layout: undo the swizzle for a few rows
+    P = F.P.float()  # [tiles][ks][256][16]
+    for r in (0, 7, 8, 255 if m > 255 else m - 1):
+        ks = 0
+        phys = P[r // 256, ks, r % 256]
+        sw = (r % 256 >> 3) & 1
+        logical = torch.cat([phys[8 * sw: 8 * sw + 8], phys[8 * (sw ^ 1): 8 * (sw ^ 1) + 8]])
+        want = ((X[r, :16] - mu[:16]) * F.scale).half().float()
+        torch.testing.assert_close(logical[: min(16, n)], want[: min(16, n)], rtol=0, atol=0)
+    XP = ops.split_bf16x3(X, tiled=True, mu=mu)
+    lab_e, d_e = ops.nearest_centroid_split(XP, m, C, F.xnorm, mu=mu)  # exact 6-product search
+    before = dict(ops._CERTIFY_STATS)
+    lab_f, d_f = ops.nearest_centroid_f16(F, C)
+    refined = ops._CERTIFY_STATS["refined"] - before["refined"]
+    assert torch.equal(lab_f, lab_e)
+    cn = ((C.double() - mu.double()) ** 2).sum(1)
+    radius = 4.0 * ops.certify_tau16(n) * (F.xnorm.double().sqrt().max() * cn.sqrt().max()).item()
+    assert (d_f.double() - d_e.double()).abs().max().item() <= radius + 1e-6
+    if ties:
+        assert refined >= m // 4
+    else:
+        assert refined < m // 2
+
+
+def test_kmeans_fit_f16_filter_matches_bf16(gpu_device, monkeypatch):
+    """A k > 256 Lloyd fit on the fp16 filter gives the same centres as on the bf16 3-product filter
+    (both certified: identical labels every iteration)."""
+    from spark_rapids_ml_nai_amd.models.kmeans import kmeans_fit
+    from spark_rapids_ml_nai_amd.parallel.context import PartitionDescriptor, WorkerContext
+
+    X = _rand(20000, 300, gpu_device, seed=41)
+    ctx = WorkerContext.single(gpu_device)
+    desc = PartitionDescriptor.build(ctx, X.shape[0], X.shape[1])
+    out = {}
+    for mode in ("f16", "bf16"):
+        monkeypatch.setenv("SRML_KMEANS_FILTER", mode)
+        monkeypatch.setenv("SRML_KMEANS_SPLIT", "1")
+        out[mode] = kmeans_fit(X, desc, ctx, k=300, max_iter=5, tol=0.0, seed=3, init="random")
+        assert out[mode]["refined_frac"] is not None  # the certified path ran
+    np.testing.assert_allclose(out["f16"]["cluster_centers_"], out["bf16"]["cluster_centers_"], rtol=1e-9, atol=1e-12)
+
+
 def test_kmeans_predict_certified_matches_exact(gpu_device, monkeypatch):
     """Large-batch k > 256 predict runs the certified split search: fp64 arg-min labels (up to
     near-ties) and the same labels as the fp32 MFMA search it replaces."""

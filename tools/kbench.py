@@ -88,6 +88,17 @@ def main():
         res["nearest_centroid_certified"] = {"ms": t, "refined_frac": st["refined"] / max(1, st["rows"]),
                                              "TFLOP/s(bf16 issued)": 6 * a.m * a.k * a.n / t / 1e9}
         del P
+    if want("nearest_f16"):  # the Lloyd search on the fp16 certified filter (one product)
+        C = torch.randn(a.k, a.n, device=dev, generator=g) * 0.05 + X[:1]
+        mu = X.double().mean(0).float()
+        F = ops.F16Planes(X, mu)
+        st0 = dict(ops._CERTIFY_STATS)
+        t = timeit(lambda: ops.nearest_centroid_f16(F, C), 3)
+        st = ops._CERTIFY_STATS
+        res["nearest_centroid_f16"] = {"ms": t, "refined_frac": (st["refined"] - st0["refined"]) /
+                                       max(1, st["rows"] - st0["rows"]),
+                                       "TFLOP/s(f16 issued)": 2 * a.m * a.k * a.n / t / 1e9}
+        del F
     if want("kpp"):  # greedy k-means++ over the k-means|| candidates (one block, k sequential steps)
         for nc in (4001, 8000):
             gk = torch.Generator().manual_seed(nc)
