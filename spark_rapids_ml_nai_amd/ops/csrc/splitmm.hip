@@ -325,6 +325,68 @@ __device__ __forceinline__ void split_epilogue_top2(const floatx16 (&acc)[BM / W
   }
 }
 
+// Top-2 epilogue on TRANSPOSED accumulators (acc[mt][nt] = centres x rows: lane (li, lk) holds row
+// row0 + wm (BM / WM) + 32 mt + li against centres col0 + wn (BN / WN) + 32 nt + (r & 3) + 8 (r >> 2)
+// + 4 lk): same state and output as split_epilogue_top2, but each lane scans its 2 x 16 candidates
+// in registers and only the two lk halves are merged (one cross-half exchange per row instead of
+// five DPP merges of four values per (row, register)).
+template <int BM, int BN, int WM, int WN>
+__device__ __forceinline__ void split_epilogue_top2_t(const floatx16 (&acc)[BM / WM / 32][BN / WN / 32], long row0,
+                                                      int col0, int ctile, long m, int k,
+                                                      const float* __restrict__ cnorm, const float* __restrict__ cg,
+                                                      const float* __restrict__ xnorm,
+                                                      unsigned long long* __restrict__ keys, float* __restrict__ lob,
+                                                      int nslot, int wm, int wn, int li, int lk, float dscale,
+                                                      float xadd) {
+  constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+  float cn[TN][16], g[TN][16];
+#pragma unroll
+  for (int nt = 0; nt < TN; ++nt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int j = col0 + wn * (BN / WN) + nt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+      cn[nt][r] = j < k ? cnorm[j] : __builtin_huge_valf();  // +inf: never the best, never a bound
+      g[nt][r] = j < k ? cg[j] : 0.f;
+    }
+  const int slot = ctile * WN + wn;
+#pragma unroll
+  for (int mt = 0; mt < TM; ++mt) {
+    const long row = row0 + wm * (BM / WM) + mt * 32 + li;
+    const float xs = row < m ? sqrtf(fmaxf(xnorm[row], 0.f)) + xadd : 0.f;
+    float bv = __builtin_huge_valf(), badj = __builtin_huge_valf(), sadj = __builtin_huge_valf();
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int nt = 0; nt < TN; ++nt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float d = fmaf(dscale, acc[mt][nt][r], cn[nt][r]);
+        const float adj = fmaf(-xs, g[nt][r], d);
+        const int j = col0 + wn * (BN / WN) + nt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        if (d < bv) { sadj = fminf(sadj, badj); bv = d; bi = j; badj = adj; }  // ascending j per lane: ties keep the lower
+        else sadj = fminf(sadj, adj);
+      }
+    // merge with the other lk half (lane ^ 32: the same row, the other 16 centres of each tile)
+    const float ov = __shfl_xor(bv, 32, 64);
+    const int oi = __shfl_xor(bi, 32, 64);
+    const float oadj = __shfl_xor(badj, 32, 64);
+    const float osadj = __shfl_xor(sadj, 32, 64);
+    if (ov < bv || (ov == bv && oi < bi)) {
+      sadj = fminf(fminf(sadj, badj), osadj);
+      bv = ov;
+      bi = oi;
+      badj = oadj;
+    } else {
+      sadj = fminf(fminf(sadj, oadj), osadj);
+    }
+    if (lk == 0 && row < m) {
+      const long o = (long)slot * m + row;
+      keys[o] = (bi == 0x7fffffff || !(bv < __builtin_huge_valf())) ? ~0ull
+                                                                      : (((unsigned long long)orderable(bv) << 32) | (unsigned)bi);
+      lob[o] = sadj;
+    }
+  }
+}
+
 template <int BM, int BN>
 struct SplitStage {
   unsigned short A[3][BM][ROWB];
@@ -566,8 +628,10 @@ __global__ __launch_bounds__(WN_ * 128, WN_ == 4 ? 1 : 2) void nearest_centroid_
 #pragma unroll
       for (int nt = 0; nt < TN; ++nt) {
         if constexpr (NP == 1) {
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(halfx8, fa[0]),
-                                                               __builtin_bit_cast(halfx8, fb[0][nt]), acc[mt][nt], 0,
+          // transposed tile (centres x rows): a lane holds ONE data row's 16 centre values per
+          // 32 x 32 tile, so the arg-min epilogue is a register scan (split_epilogue_top2_t)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(halfx8, fb[0][nt]),
+                                                               __builtin_bit_cast(halfx8, fa[0]), acc[mt][nt], 0,
                                                                0, 0);
         } else {
           if constexpr (NP == 6) {
@@ -621,7 +685,10 @@ __global__ __launch_bounds__(WN_ * 128, WN_ == 4 ? 1 : 2) void nearest_centroid_
       if (PRIO) __builtin_amdgcn_s_setprio(0);
     }
   }
-  if (TOP2)
+  if (TOP2 && NP == 1)
+    split_epilogue_top2_t<BM, BN, WM, WN>(acc, row0, col0, ctile, m, k, cnorm, cg, xnorm, best, lob, n_ctiles * WN, wm,
+                                          wn, li, lk, dscale, xadd);
+  else if (TOP2)
     split_epilogue_top2<BM, BN, WM, WN>(acc, row0, col0, ctile, m, k, cnorm, cg, xnorm, best, lob, n_ctiles * WN, wm,
                                         wn, li, lk, dscale, xadd);
   else
