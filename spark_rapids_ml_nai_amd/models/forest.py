@@ -259,24 +259,21 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
     rec = _ForestRecords(n_trees)
     # bootstrap multiplicities per tree (Spark: Poisson(subsamplingRate) bagging); positions of
     # all trees are concatenated: segment = (tree, node), rows stay ascending inside a segment
-    idx_l, w_l, cnt0 = [], [], []
-    for _ in range(n_trees):
-        if p["bootstrap"]:
-            rate = float(p.get("max_samples", 1.0))
-            w = torch.poisson(torch.full((m,), rate, device=dev), generator=gen_boot or gen).clamp_max(255)
-        else:
-            w = torch.ones(m, device=dev)
-        ii = torch.nonzero(w, as_tuple=False).view(-1).to(torch.int32)
-        idx_l.append(ii)
-        w_l.append(w[ii.long()].float())
-        cnt0.append(int(ii.shape[0]))
-    idx = torch.cat(idx_l).contiguous()
-    wpos = torch.cat(w_l).contiguous()
-    del idx_l, w_l
+    if p["bootstrap"]:
+        # one native pass draws every tree's Poisson multiplicities and compacts the in-bag rows
+        # (tree-major, ascending); the seed is one draw of the bootstrap generator per call
+        boot_seed = int(torch.randint(0, 1 << 62, (1,), generator=gen_boot or gen,
+                                      device=(gen_boot or gen).device).item())
+        idx, wpos, bounds_h = ops.rf_bootstrap(n_trees, m, float(p.get("max_samples", 1.0)), boot_seed, dev)
+        idx, wpos = idx.to(dev).contiguous(), wpos.to(dev).contiguous()
+    else:
+        idx = torch.arange(m, dtype=torch.int32, device=dev).repeat(n_trees)
+        wpos = torch.ones(n_trees * m, dtype=torch.float32, device=dev)
+        bounds_h = np.arange(n_trees + 1, dtype=np.int64) * m
     seg_tree = np.arange(n_trees, dtype=np.int64)
     seg_nid = np.zeros(n_trees, dtype=np.int64)  # every tree's root is node 0
-    counts = np.asarray(cnt0, dtype=np.int64)
-    bounds_h = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    bounds_h = np.asarray(bounds_h, dtype=np.int64)
+    counts = np.diff(bounds_h)
     bounds = torch.from_numpy(bounds_h).to(dev)
     tot = _node_stats(yv, idx, wpos, bounds, S, regression)
     if data_parallel:

@@ -165,6 +165,8 @@ def _use_split(X: torch.Tensor, k: int) -> bool:
     m, n = X.shape
     if k < 128 or n < 128:
         return False
+    if m > ops.split_rows_per_launch(k):  # the 3-product / exact split kernels launch all rows at once
+        return False
     need = 3 * 2 * ((m + 127) // 128 * 128) * ((n + 15) // 16 * 16)
     free, _ = torch.cuda.mem_get_info(X.device)
     return need < 0.6 * free

@@ -525,19 +525,30 @@ def nearest_centroid_f16(F: F16Planes, C: torch.Tensor) -> Tuple[torch.Tensor, t
                 CP.data_ptr(), F.ovf.data_ptr(), st)
     cg = (2.0 * F.tau) * cn.clamp_min(0).sqrt()
     nslot = int(native.lib().srml_nearest_centroid_f16_top2_nslot(k))
-    keys = torch.empty(m * nslot, dtype=torch.int64, device=dev)
-    lob = torch.empty(m * nslot, dtype=torch.float32, device=dev)
-    native.call("srml_nearest_centroid_f16_top2", F.P.data_ptr(), m, F.rows_pad, F.kp, CP.data_ptr(), k, crows,
-                cn.data_ptr(), cg.data_ptr(), F.xnorm.data_ptr(), -2.0 / (F.scale * F.scale), F.xadd, keys.data_ptr(),
-                lob.data_ptr(), st)
     labels = torch.empty(m, dtype=torch.int32, device=dev)
     dist = torch.empty(m, dtype=torch.float32, device=dev)
     flagged = torch.empty(m, dtype=torch.int32, device=dev)
     cnt = torch.zeros(1, dtype=torch.int32, device=dev)
-    native.call("srml_split_top2_select_f16", keys.data_ptr(), lob.data_ptr(), m, nslot, F.xnorm.data_ptr(),
-                cg.data_ptr(), F.xadd, F.z, F.z2, F.ovf.data_ptr(), labels.data_ptr(), dist.data_ptr(),
-                flagged.data_ptr(), cnt.data_ptr(), st)
-    del keys, lob
+    # row chunks of whole 256-row tiles within the 2^32 work-item grid (512-thread blocks x
+    # centre tiles); the select appends each chunk's uncertified rows (chunk-relative) to flagged
+    step = split_rows_per_launch(k)
+    for r0 in range(0, m, step):
+        mc = min(step, m - r0)
+        keys = torch.empty(mc * nslot, dtype=torch.int64, device=dev)
+        lob = torch.empty(mc * nslot, dtype=torch.float32, device=dev)
+        Pc = F.P[r0 // 256: (r0 + mc + 255) // 256]
+        xn = F.xnorm[r0: r0 + mc]
+        native.call("srml_nearest_centroid_f16_top2", Pc.data_ptr(), mc, Pc.shape[0] * 256, F.kp, CP.data_ptr(), k,
+                    crows, cn.data_ptr(), cg.data_ptr(), xn.data_ptr(), -2.0 / (F.scale * F.scale), F.xadd,
+                    keys.data_ptr(), lob.data_ptr(), st)
+        c0 = int(cnt.item()) if r0 else 0
+        native.call("srml_split_top2_select_f16", keys.data_ptr(), lob.data_ptr(), mc, nslot, xn.data_ptr(),
+                    cg.data_ptr(), F.xadd, F.z, F.z2, F.ovf.data_ptr(), labels[r0:].data_ptr(), dist[r0:].data_ptr(),
+                    flagged.data_ptr(), cnt.data_ptr(), st)
+        if r0:
+            nc = int(cnt.item())
+            flagged[c0:nc] += r0
+        del keys, lob
     nf = int(cnt.item())
     _CERTIFY_STATS["rows"] += m
     _CERTIFY_STATS["refined"] += nf
@@ -551,6 +562,13 @@ def nearest_centroid_f16(F: F16Planes, C: torch.Tensor) -> Tuple[torch.Tensor, t
         native.call("srml_split_scatter_refined", best.data_ptr(), rows.data_ptr(), nf, F.xnorm.data_ptr(),
                     labels.data_ptr(), dist.data_ptr(), st)
     return labels, dist
+
+
+def split_rows_per_launch(k: int) -> int:
+    """Rows of one 256 x 256-tile split / fp16 filter launch: 512-thread blocks x ceil(k / 256)
+    centre tiles per 256-row tile must stay within the 2^32 work-item grid of a dispatch."""
+    ct = max(1, (int(k) + 255) // 256)
+    return max(256, (0xFFFFFFFF // 512 // ct) * 256)
 
 
 def kmeans_filter_mode() -> str:
@@ -1074,6 +1092,50 @@ def rf_sample_features(C: int, n: int, nf: int, seed: int, device: torch.device)
     out = torch.empty((C, nf), dtype=torch.int32, device=device)
     native.call("srml_rf_sample_features", C, n, nf, seed, out.data_ptr(), native.stream(device))
     return out
+
+
+def _mix64_np(x: np.ndarray) -> np.ndarray:
+    x = x + np.uint64(0x9E3779B97F4A7C15)
+    x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def rf_bootstrap(T: int, m: int, rate: float, seed: int, device: torch.device
+                 ) -> Tuple[torch.Tensor, torch.Tensor, np.ndarray]:
+    """Poisson(rate) bagging of T trees over m rows (Spark's bagging, cuML's bootstrap): (in-bag row
+    ids int32, their multiplicities float32 — tree-major, ascending inside a tree —, tree bounds
+    int64 [T + 1] on the host). Element i = t m + r draws by inversion from the counter-based
+    uniform (splitmix64(seed ^ splitmix64(i + 1)) >> 11) 2^-53, clamped to 255: one count pass, one
+    scan, one scatter (``srml_rf_bootstrap``); the CPU path is the same draw in numpy."""
+    seed &= (1 << 64) - 1
+    N = int(T) * int(m)
+    if device.type != "cuda":
+        i = np.arange(N, dtype=np.uint64)
+        with np.errstate(over="ignore"):
+            u = (_mix64_np(np.uint64(seed) ^ _mix64_np(i + np.uint64(1))) >> np.uint64(11)).astype(np.float64) \
+                * 2.0 ** -53
+        k = np.zeros(N, dtype=np.int64)
+        p = np.full(N, math.exp(-rate))
+        F = p.copy()
+        live = u > F
+        while live.any():
+            k[live] += 1
+            p[live] *= rate / k[live]
+            F[live] += p[live]
+            live &= (u > F) & (k < 255)
+        nz = np.nonzero(k)[0]
+        bounds = np.searchsorted(nz, np.arange(T + 1, dtype=np.int64) * m).astype(np.int64)
+        return (torch.from_numpy((nz % m).astype(np.int32)), torch.from_numpy(k[nz].astype(np.float32)), bounds)
+    idx = torch.empty(N, dtype=torch.int32, device=device)
+    w = torch.empty(N, dtype=torch.float32, device=device)
+    tb = torch.empty(T + 1, dtype=torch.int64, device=device)
+    ws = torch.empty(int(native.lib().srml_rf_bootstrap_ws(T, m)) + 1, dtype=torch.int64, device=device)
+    native.call("srml_rf_bootstrap", T, m, float(rate), seed, idx.data_ptr(), w.data_ptr(), tb.data_ptr(),
+                ws.data_ptr(), native.stream(device))
+    bounds = tb.cpu().numpy()
+    tot = int(bounds[-1])
+    return idx[:tot], w[:tot], bounds
 
 
 def rf_partition(keys: torch.Tensor, bounds: torch.Tensor, node_feature: torch.Tensor, child_base: torch.Tensor,

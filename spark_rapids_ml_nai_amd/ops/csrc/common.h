@@ -90,6 +90,11 @@ __device__ __forceinline__ void logistic_terms(double z, double y, double& res, 
 
 static inline int srml_status() { return (int)hipGetLastError(); }
 
+// An AMD dispatch packet carries the grid size in WORK-ITEMS as a 32-bit field: blocks * threads
+// per block must stay below 2^32 (a 1-D launch of 2^24 256-thread blocks silently covers nothing
+// past that). Tile-product launches (rows x centroid tiles) are split or checked against this.
+static inline long srml_max_blocks(int threads) { return 0xFFFFFFFFL / (long)threads; }
+
 // Ordered fold of per-block partials (deterministic mode, defined in glm.hip):
 // out[(i / inner) * so_outer + (i % inner) * so_inner] += sum_{p = 0..parts-1} ws[p * pstride + i], i < width,
 // summed in block order so the result is bit-identical run to run; skipped once *flag != 0.

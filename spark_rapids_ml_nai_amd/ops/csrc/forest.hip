@@ -1021,6 +1021,89 @@ static int scan_u64(const unsigned long long* in, const int* keys, long n, unsig
   return srml_status();
 }
 
+// ------------------------------------------------------------------------------------------
+// Bootstrap bagging of T trees over m rows in one pass (reference: cuML RF bootstrap / Spark
+// Poisson(subsamplingRate) bagging): element i = t m + r draws its multiplicity w ~ Poisson(rate)
+// by inversion of a counter-based uniform (splitmix64 of seed, i), clamped to 255; the in-bag rows
+// are compacted tree-major and ascending (the order the level segments keep). Kernels: per-block
+// in-bag counts, scan of the block counts (scan_totals_u64_kernel), scatter with an in-block
+// exclusive scan; tree bounds come out of the scatter (element t m marks tree t's start).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int poisson_draw(unsigned long long seed, long i, double rate, double e0) {
+  const double u = (double)(mix64(seed ^ mix64((unsigned long long)i + 1)) >> 11) * 0x1.0p-53;
+  int k = 0;
+  double p = e0, F = e0;  // e0 = exp(-rate)
+  while (u > F && k < 255) {
+    ++k;
+    p *= rate / (double)k;
+    F += p;
+  }
+  return k;
+}
+
+__global__ __launch_bounds__(PS_T) void rf_boot_count_kernel(long N, unsigned long long seed, double rate, double e0,
+                                                             unsigned long long* __restrict__ tot) {
+  __shared__ unsigned long long s_w[PS_T / 64];
+  const long b0 = (long)blockIdx.x * PS_B + (long)threadIdx.x * PS_E;
+  unsigned long long c = 0;
+#pragma unroll
+  for (int e = 0; e < PS_E; ++e)
+    if (b0 + e < N) c += poisson_draw(seed, b0 + e, rate, e0) > 0 ? 1ull : 0ull;
+  unsigned long long total;
+  block_excl_scan_u64(c, s_w, total);
+  if (threadIdx.x == 0) tot[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(PS_T) void rf_boot_scatter_kernel(long N, long m, unsigned long long seed, double rate,
+                                                               double e0, const unsigned long long* __restrict__ boff,
+                                                               const unsigned long long* __restrict__ grand,
+                                                               int* __restrict__ idx, float* __restrict__ w,
+                                                               long long* __restrict__ tbounds) {
+  __shared__ unsigned long long s_w[PS_T / 64];
+  const long b0 = (long)blockIdx.x * PS_B + (long)threadIdx.x * PS_E;
+  int k[PS_E];
+  unsigned long long c = 0;
+#pragma unroll
+  for (int e = 0; e < PS_E; ++e) {
+    k[e] = b0 + e < N ? poisson_draw(seed, b0 + e, rate, e0) : 0;
+    c += k[e] > 0 ? 1ull : 0ull;
+  }
+  unsigned long long total;
+  unsigned long long o = boff[blockIdx.x] + block_excl_scan_u64(c, s_w, total);
+#pragma unroll
+  for (int e = 0; e < PS_E; ++e) {
+    const long i = b0 + e;
+    if (i >= N) break;
+    const long r = i % m;
+    if (r == 0) tbounds[i / m] = (long long)o;
+    if (k[e] > 0) {
+      idx[o] = (int)r;
+      w[o] = (float)k[e];
+      ++o;
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) tbounds[N / m] = (long long)*grand;
+}
+
+// idx / w: capacity T m; tbounds: T + 1 (exclusive prefix of the per-tree in-bag counts); ws: at
+// least srml_rf_bootstrap_ws(T, m) u64
+SRML_API long srml_rf_bootstrap_ws(int T, long m) { return ((long)T * m + PS_B - 1) / PS_B + 1; }
+
+SRML_API int srml_rf_bootstrap(int T, long m, double rate, unsigned long long seed, int* idx, float* w,
+                               long long* tbounds, unsigned long long* ws, hipStream_t stream) {
+  if (T <= 0 || m <= 0) return 0;
+  if (!(rate > 0.0) || m > 0x7fffffffL) return -2;
+  const long N = (long)T * m;
+  const long nb = (N + PS_B - 1) / PS_B;
+  if (nb > 0x7fffffffL) return -3;
+  const double e0 = exp(-rate);
+  hipLaunchKernelGGL(rf_boot_count_kernel, dim3((unsigned)nb), dim3(PS_T), 0, stream, N, seed, rate, e0, ws);
+  hipLaunchKernelGGL(scan_totals_u64_kernel, dim3(1), dim3(PS_T), 0, stream, ws, nb, ws + nb);
+  hipLaunchKernelGGL(rf_boot_scatter_kernel, dim3((unsigned)nb), dim3(PS_T), 0, stream, N, m, seed, rate, e0, ws,
+                     ws + nb, idx, w, tbounds);
+  return srml_status();
+}
+
 // per split parent j: cnt[j] = |left| + |right|, lcnt[j] = |left|, pstart[j] = the parent's start
 __global__ __launch_bounds__(256) void part_parent_kernel(const long long* __restrict__ bounds, int nseg,
                                                           const int* __restrict__ node_feature,

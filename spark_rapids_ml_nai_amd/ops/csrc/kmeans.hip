@@ -513,29 +513,37 @@ SRML_API int srml_nearest_centroid_f32(const float* X, long m, int n, long ldx, 
   if (m <= 0 || k <= 0) return 0;
   const bool vec = ((ldx & 3) == 0) && ((ldc & 3) == 0) && ((n & 3) == 0) &&
                    ((reinterpret_cast<uintptr_t>(X) & 15) == 0) && ((reinterpret_cast<uintptr_t>(C) & 15) == 0);
+  // rows are independent: launches of at most srml_max_blocks(256) row x centroid tiles each
+  // (e.g. 20M rows x 19531 IVF lists is 23.9M tiles of 128 x 128, past the 2^32 work-item grid)
   if (k > 64) {
     constexpr int BM = 128, BN = 128;
-    const long rt = (m + BM - 1) / BM;
     const int ct = (k + BN - 1) / BN;
-    const long nb = rt * ct;
-    if (nb > 0x7fffffffL) return -3;
-    if (vec)
-      hipLaunchKernelGGL((nearest_centroid_kernel<BM, BN, 2, 2, 2, true>), dim3((unsigned)nb), dim3(256), 0, stream, X,
-                         m, n, ldx, C, k, ldc, cnorm, best, ct);
-    else
-      hipLaunchKernelGGL((nearest_centroid_kernel<BM, BN, 2, 2, 2, false>), dim3((unsigned)nb), dim3(256), 0, stream, X,
-                         m, n, ldx, C, k, ldc, cnorm, best, ct);
+    const long rows_per = (srml_max_blocks(256) / ct) * BM;
+    if (rows_per < BM) return -3;
+    for (long r0 = 0; r0 < m; r0 += rows_per) {
+      const long mc = m - r0 < rows_per ? m - r0 : rows_per;
+      const long nb = (mc + BM - 1) / BM * ct;
+      if (vec)
+        hipLaunchKernelGGL((nearest_centroid_kernel<BM, BN, 2, 2, 2, true>), dim3((unsigned)nb), dim3(256), 0, stream,
+                           X + r0 * ldx, mc, n, ldx, C, k, ldc, cnorm, best + r0, ct);
+      else
+        hipLaunchKernelGGL((nearest_centroid_kernel<BM, BN, 2, 2, 2, false>), dim3((unsigned)nb), dim3(256), 0, stream,
+                           X + r0 * ldx, mc, n, ldx, C, k, ldc, cnorm, best + r0, ct);
+    }
   } else {
     constexpr int BM = 256, BN = 64;
-    const long rt = (m + BM - 1) / BM;
     const int ct = (k + BN - 1) / BN;
-    const long nb = rt * ct;
-    if (vec)
-      hipLaunchKernelGGL((nearest_centroid_kernel<BM, BN, 4, 2, 2, true>), dim3((unsigned)nb), dim3(256), 0, stream, X,
-                         m, n, ldx, C, k, ldc, cnorm, best, ct);
-    else
-      hipLaunchKernelGGL((nearest_centroid_kernel<BM, BN, 4, 2, 2, false>), dim3((unsigned)nb), dim3(256), 0, stream, X,
-                         m, n, ldx, C, k, ldc, cnorm, best, ct);
+    const long rows_per = (srml_max_blocks(256) / ct) * BM;
+    for (long r0 = 0; r0 < m; r0 += rows_per) {
+      const long mc = m - r0 < rows_per ? m - r0 : rows_per;
+      const long nb = (mc + BM - 1) / BM * ct;
+      if (vec)
+        hipLaunchKernelGGL((nearest_centroid_kernel<BM, BN, 4, 2, 2, true>), dim3((unsigned)nb), dim3(256), 0, stream,
+                           X + r0 * ldx, mc, n, ldx, C, k, ldc, cnorm, best + r0, ct);
+      else
+        hipLaunchKernelGGL((nearest_centroid_kernel<BM, BN, 4, 2, 2, false>), dim3((unsigned)nb), dim3(256), 0, stream,
+                           X + r0 * ldx, mc, n, ldx, C, k, ldc, cnorm, best + r0, ct);
+    }
   }
   return srml_status();
 }

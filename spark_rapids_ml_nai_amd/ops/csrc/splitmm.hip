@@ -782,7 +782,7 @@ SRML_API int srml_nearest_centroid_split(const unsigned short* XP, long m, long 
   const long rt = (m + T - 1) / T;
   const int ct = (k + T - 1) / T;
   const long nb = rt * ct;
-  if (nb > 0x7fffffffL) return -3;
+  if (nb > srml_max_blocks(big ? 512 : 256)) return -3;
   static const int pf = getenv("SRML_SPLIT_PF") ? atoi(getenv("SRML_SPLIT_PF")) : 2;
   static const int glds = getenv("SRML_SPLIT_GLDS") ? atoi(getenv("SRML_SPLIT_GLDS")) : 0;
   if (big && glds)
@@ -851,7 +851,7 @@ SRML_API int srml_nearest_centroid_split_tiled_np(const unsigned short* XP, long
   const int bn = nprod == 3 ? split3_bn() : 256;
   const int ct = (k + bn - 1) / bn;
   const long nb = rt * ct;
-  if (nb > 0x7fffffffL) return -3;
+  if (nb > srml_max_blocks(512)) return -3;  // 2^32 work-item grid
   if (nprod == 3 && bn == 128)
     hipLaunchKernelGGL((nearest_centroid_split_glds_kernel<true, 3, false, 2>), dim3((unsigned)nb), dim3(256), 0, stream,
                        XP, m, xrows, kp, CP, k, crows, cnorm, best, (int)ct);
@@ -886,7 +886,7 @@ SRML_API int srml_nearest_centroid_split_top2(const unsigned short* XP, long m, 
   const int bn = split3_bn();
   const int ct = (k + bn - 1) / bn;
   const long nb = rt * ct;
-  if (nb > 0x7fffffffL) return -3;
+  if (nb > srml_max_blocks(512)) return -3;  // 2^32 work-item grid
   // s_setprio around the MFMA clusters: 16.7 -> 16.4 ms per pass on the 256 x 256 tile (neutral
   // on 256 x 128); SRML_SPLIT_PRIO=0 turns it off
   static const bool prio = !(getenv("SRML_SPLIT_PRIO") && atoi(getenv("SRML_SPLIT_PRIO")) == 0);
@@ -957,7 +957,7 @@ SRML_API int srml_nearest_centroid_f16_top2(const unsigned short* XP, long m, lo
   const long rt = (m + 255) / 256;
   const int ct = (k + 255) / 256;
   const long nb = rt * ct;
-  if (nb > 0x7fffffffL) return -3;
+  if (nb > srml_max_blocks(512)) return -3;  // 2^32 work-item grid
   static const bool prio = !(getenv("SRML_SPLIT_PRIO") && atoi(getenv("SRML_SPLIT_PRIO")) == 0);
   if (prio)
     hipLaunchKernelGGL((nearest_centroid_split_glds_kernel<true, 1, true, 4, true>), dim3((unsigned)nb), dim3(512), 0,

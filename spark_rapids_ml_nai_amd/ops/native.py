@@ -26,7 +26,7 @@ _D = ctypes.c_double
 _F = ctypes.c_float
 
 # name -> argtypes (restype: int status, except the size queries in _LONG_RESULT)
-_LONG_RESULT = ("srml_qn_args_size", "srml_logit_residual_ws", "srml_xtv_mfma_ws", "srml_rf_partition_ws",
+_LONG_RESULT = ("srml_rf_bootstrap_ws", "srml_qn_args_size", "srml_logit_residual_ws", "srml_xtv_mfma_ws", "srml_rf_partition_ws",
                 "srml_label_sort_ws", "srml_radix_sort_ws")
 SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_col_moments_f32": (_P, _L, _I, _L, _P, _P, _P),
@@ -74,6 +74,8 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_split_bf16x3_tiled_centered": (_P, _L, _I, _L, _P, _I, _L, _P, _P),
     "srml_row_sqnorm_centered_f32": (_P, _L, _I, _L, _P, _P, _P),
     "srml_row_sqnorm_centered_amax_f32": (_P, _L, _I, _L, _P, _P, _P, _P),
+    "srml_rf_bootstrap_ws": (_I, _L),
+    "srml_rf_bootstrap": (_I, _L, _D, ctypes.c_ulonglong, _P, _P, _P, _P, _P),
     "srml_split_f16_tiled_centered": (_P, _L, _I, _L, _P, _I, _L, _F, _P, _P, _P),
     "srml_nearest_centroid_f16_top2": (_P, _L, _L, _I, _P, _I, _L, _P, _P, _P, _F, _F, _P, _P, _P),
     "srml_nearest_centroid_f16_top2_nslot": (_I,),

@@ -896,3 +896,13 @@ def test_knn_refine_sort_matches_torch(gpu_device, mq, n, k, ip):
     assert torch.equal(p.sort(1).values, pos.sort(1).values)
     if not ip:
         assert d[0, 0].item() < n * 2e-8 and p[0, 0].item() == 7
+
+
+@pytest.mark.parametrize("T,m,rate", [(1, 1000, 1.0), (30, 100003, 1.0), (7, 5000, 0.3)])
+def test_rf_bootstrap_matches_cpu_draw(gpu_device, T, m, rate):
+    """Native Poisson bagging (count / scan / scatter) == the numpy draw of the same counter-based
+    RNG: identical in-bag rows, multiplicities and tree bounds."""
+    i_g, w_g, b_g = ops.rf_bootstrap(T, m, rate, 1234567, gpu_device)
+    i_c, w_c, b_c = ops.rf_bootstrap(T, m, rate, 1234567, torch.device("cpu"))
+    np.testing.assert_array_equal(b_g, b_c)
+    assert torch.equal(i_g.cpu(), i_c) and torch.equal(w_g.cpu(), w_c)

@@ -63,11 +63,33 @@ def _estimator(name: str, world: int):
     raise ValueError(name)
 
 
+CHUNK_BYTES = 16 << 30  # device generation in row chunks of <= 16 GB straight into the pinned shard
+
+
 def _shard(gen: str, m: int, n: int, device, rank: int):
     from spark_rapids_ml_nai_amd.bench import datagen
 
     seed = 7000 + rank
     y = None
+    step = max(1, CHUNK_BYTES // (4 * n))
+    if gen in ("blobs", "classification") and m > step and device.type == "cuda":
+        # large shards (the 200M x 256 LogisticRegression): the generators' class centres / mixing
+        # matrices come from fixed seeds, so chunks with their own row seeds draw from the same
+        # distribution; the device never holds more than one chunk plus its temporaries
+        Xh = torch.empty((m, n), dtype=torch.float32, pin_memory=True)
+        yh = np.empty(m, dtype=np.float64)
+        for c, r0 in enumerate(range(0, m, step)):
+            mc = min(step, m - r0)
+            if gen == "blobs":
+                Xc, yc = datagen.blobs(mc, n, device, seed=seed * 1000 + c, centers=20)
+            else:
+                Xc, yc = datagen.classification(mc, n, device, seed=seed * 1000 + c, n_informative=n // 2,
+                                                n_redundant=n // 4)
+            Xh[r0: r0 + mc].copy_(Xc)
+            yh[r0: r0 + mc] = yc.cpu().numpy()
+            del Xc, yc
+        torch.cuda.empty_cache()
+        return Xh.numpy(), (yh if gen == "classification" else None)
     if gen == "low_rank":
         X = datagen.low_rank_matrix(m, n, device, seed=seed)
     elif gen == "blobs":
