@@ -855,13 +855,13 @@ SRML_API int srml_logreg_binary2_f32(const float* X, long m, int n, long ld, con
 #undef SRML_LR_NARROW
     return srml_status();
   }
-  // ~>= 120 rows per block: each block pays a w load and an n-wide fp64 atomic flush, so small
-  // shards (the per-rank rows of a multi-GPU fit) want fewer blocks (125k rows: 1024 blocks
-  // 0.334 ms vs 2048 blocks 0.385 ms; 1M rows: 2048 blocks best)
+  // ~>= 160 rows per block: each block pays a w load and an n-wide fp64 atomic flush, so small
+  // shards (the per-rank rows of a multi-GPU fit) want fewer blocks (125k rows: 768 blocks
+  // 0.310 ms, 1024 0.331, 1536 0.345, 512 0.328 (tools/lr_small_sweep.sh); 1M rows: 2048 best)
   static const long blocks_env = getenv("SRML_LOGREG_BLOCKS") ? atol(getenv("SRML_LOGREG_BLOCKS")) : 0;
   long blocks = blocks_env;
   if (blocks <= 0) {
-    blocks = m / 122;
+    blocks = m / 163;
     if (blocks > 2048) blocks = 2048;
     if (blocks < 512) blocks = 512;
   }

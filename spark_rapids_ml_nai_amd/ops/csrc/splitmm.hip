@@ -535,8 +535,8 @@ __global__ __launch_bounds__(WN_ * 128, WN_ == 4 ? 1 : 2) void nearest_centroid_
     long crows, const float* __restrict__ cnorm, unsigned long long* __restrict__ best, int n_ctiles,
     float* __restrict__ lob = nullptr, const float* __restrict__ cg = nullptr, const float* __restrict__ xnorm = nullptr,
     float dscale = -2.f, float xadd = 0.f) {
-  static_assert(WN_ == 4 || (WN_ == 2 && NP == 3), "256 x 128 tiles are built for the 3-product pass");
-  static_assert(NP == 6 || NP == 3 || (NP == 1 && TOP2 && WN_ == 4), "NP = 1 is the fp16 certified filter");
+  static_assert(WN_ == 4 || (WN_ == 2 && NP != 6), "256 x 128 tiles are built for the filter passes");
+  static_assert(NP == 6 || NP == 3 || (NP == 1 && TOP2), "NP = 1 is the fp16 certified filter");
   constexpr int BM = 256, WM = 2, WN = WN_, BN = 64 * WN, TM = 4, TN = 2;
   // planes staged per operand: h, m, l for the 6-product set; the 3-product set (h.h, h.m, m.h)
   // never touches the l planes, so it stages 2 per operand (2/3 of the DMA and LDS traffic)
@@ -551,7 +551,7 @@ __global__ __launch_bounds__(WN_ * 128, WN_ == 4 ? 1 : 2) void nearest_centroid_
   // so three steps share a barrier and the ring holds three such groups (9 stages, 144 KiB): the
   // loads of group g + 2 are issued while group g computes (two groups of HBM-latency cover)
   constexpr int KPB = NP == 1 ? 3 : (NP == 3 && WN_ == 4 ? 2 : 1);  // k steps per barrier
-  constexpr int NG = NP == 1 ? 3 : 2;                                // groups in the ring
+  constexpr int NG = NP == 1 && WN_ == 4 ? 3 : 2;                    // groups in the ring (2 x 72 KiB per CU at WN_ = 2)
   constexpr int NS = KPB > 1 ? NG * KPB : 3;
   constexpr int STAGE = NPL * (BM + BN) * 16;  // elements: X planes [NPL][BM][16], then C planes [NPL][BN][16]
   __shared__ __attribute__((aligned(1024))) unsigned short lds[NS][STAGE];
@@ -927,6 +927,13 @@ SRML_API int srml_split_scatter_refined(const unsigned long long* best, const in
 }
 
 // ---- fp16 certified filter -----------------------------------------------------------------
+// Centroid-tile width of the fp16 filter: 256 (256 x 256 tile, one 8-wave block per CU, 3-group
+// ring) or SRML_F16_BN=128 (256 x 128 tiles, two 4-wave blocks per CU, 2-group rings)
+static int f16_bn() {
+  static const int bn = getenv("SRML_F16_BN") && atoi(getenv("SRML_F16_BN")) == 128 ? 128 : 256;
+  return bn;
+}
+
 // One tiled fp16 plane of scale * (x - mu) (mu may be null), rows padded to rows_pad (% 256 == 0):
 // P = [rows_pad / 256][kp / 16][256][16]; *ovf |= 1 if an element of |scale v| >= 2^15 was clamped.
 SRML_API int srml_split_f16_tiled_centered(const float* X, long m, int n, long ld, const float* mu, int kp,
@@ -955,21 +962,30 @@ SRML_API int srml_nearest_centroid_f16_top2(const unsigned short* XP, long m, lo
   if ((kp & 15) || xrows < m || crows < k || (crows & 255) || (xrows & 255)) return -2;
   if ((reinterpret_cast<uintptr_t>(XP) & 15) || (reinterpret_cast<uintptr_t>(CP) & 15)) return -5;
   const long rt = (m + 255) / 256;
-  const int ct = (k + 255) / 256;
+  const int bn = f16_bn();
+  const int ct = (k + bn - 1) / bn;
   const long nb = rt * ct;
-  if (nb > srml_max_blocks(512)) return -3;  // 2^32 work-item grid
+  if (nb > srml_max_blocks(bn * 2)) return -3;  // 2^32 work-item grid
   static const bool prio = !(getenv("SRML_SPLIT_PRIO") && atoi(getenv("SRML_SPLIT_PRIO")) == 0);
-  if (prio)
-    hipLaunchKernelGGL((nearest_centroid_split_glds_kernel<true, 1, true, 4, true>), dim3((unsigned)nb), dim3(512), 0,
-                       stream, XP, m, xrows, kp, CP, k, crows, cnorm, keys, (int)ct, lob, cg, xnorm, dscale, xadd);
-  else
-    hipLaunchKernelGGL((nearest_centroid_split_glds_kernel<true, 1, true, 4, false>), dim3((unsigned)nb), dim3(512), 0,
-                       stream, XP, m, xrows, kp, CP, k, crows, cnorm, keys, (int)ct, lob, cg, xnorm, dscale, xadd);
+#define SRML_F16(WNN, PR, T)                                                                                      \
+  hipLaunchKernelGGL((nearest_centroid_split_glds_kernel<true, 1, true, WNN, PR>), dim3((unsigned)nb), dim3(T), 0, \
+                     stream, XP, m, xrows, kp, CP, k, crows, cnorm, keys, (int)ct, lob, cg, xnorm, dscale, xadd)
+  if (f16_bn() == 128) {
+    if (prio) SRML_F16(2, true, 256);
+    else SRML_F16(2, false, 256);
+  } else {
+    if (prio) SRML_F16(4, true, 512);
+    else SRML_F16(4, false, 512);
+  }
+#undef SRML_F16
   return srml_status();
 }
 
-// (row, slot) pairs of the fp16 filter (256-wide centroid tiles, 4 wave columns each)
-SRML_API int srml_nearest_centroid_f16_top2_nslot(int k) { return ((k + 255) / 256) * 4; }
+// (row, slot) pairs of the fp16 filter (one slot per 64-wide wave column of each centroid tile)
+SRML_API int srml_nearest_centroid_f16_top2_nslot(int k) {
+  const int bn = f16_bn();
+  return ((k + bn - 1) / bn) * (bn / 64);
+}
 
 // phase 2 of the fp16 filter: as srml_split_top2_select with the extra radius terms (see kernel)
 SRML_API int srml_split_top2_select_f16(const unsigned long long* keys, const float* lob, long m, int nslot,

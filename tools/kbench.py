@@ -89,7 +89,7 @@ def main():
                                              "TFLOP/s(bf16 issued)": 6 * a.m * a.k * a.n / t / 1e9}
         del P
     if want("nearest_f16"):  # the Lloyd search on the fp16 certified filter (one product)
-        C = torch.randn(a.k, a.n, device=dev, generator=g) * 0.05 + X[:1]
+        C = X[torch.randperm(a.m, device=dev, generator=g)[: a.k]].clone()  # random-row centres
         mu = X.double().mean(0).float()
         F = ops.F16Planes(X, mu)
         st0 = dict(ops._CERTIFY_STATS)
