@@ -389,6 +389,22 @@ def split_bf16x3(X: torch.Tensor, row_multiple: int = 128, tiled: bool = False,
 CERTIFY_TAU = 2.0 ** -13  # dropped-product bound of the 3-product search (3 * 2^-16, 8x slack), per ||x|| ||c||
 
 
+def split_bf16x3_rows(X: torch.Tensor, rows: torch.Tensor, mu: torch.Tensor) -> torch.Tensor:
+    """``split_bf16x3(X[rows], tiled=True, mu=mu)`` without the gathered copy of the rows
+    (``srml_split_bf16x3_tiled_centered_rows`` reads them through the index list)."""
+    m, n = int(rows.shape[0]), X.shape[1]
+    if not X.is_cuda or X.dtype != torch.float32 or X.stride(1) != 1:
+        return split_bf16x3(X.index_select(0, rows.long()), tiled=True, mu=mu)
+    kp = (n + 15) // 16 * 16
+    rows_pad = max(256, (m + 255) // 256 * 256)
+    P = torch.empty((3, rows_pad // 256, kp // 16, 256, 16), dtype=torch.bfloat16, device=X.device)
+    muf = _c(mu.float().view(-1))
+    ri = _c(rows.to(torch.int32))
+    native.call("srml_split_bf16x3_tiled_centered_rows", X.data_ptr(), X.stride(0), ri.data_ptr(), m, n,
+                muf.data_ptr(), kp, rows_pad, P.data_ptr(), native.stream(X.device))
+    return P
+
+
 def certify_tau(n: int) -> float:
     """Worst-case |d~ - d| of the 3-product search vs the fp32 6-product search, relative to
     ||x|| ||c||: the dropped products (``CERTIFY_TAU``) plus the fp32 accumulation error of BOTH
@@ -429,7 +445,7 @@ def _nearest_centroid_certified(XP: torch.Tensor, X: torch.Tensor, m: int, k: in
     _CERTIFY_STATS["refined"] += nf
     if nf:
         rows = flagged[:nf]
-        XPr = split_bf16x3(X.index_select(0, rows.long()), tiled=True, mu=mu)
+        XPr = split_bf16x3_rows(X, rows, mu)
         best = torch.full((nf,), -1, dtype=torch.int64, device=dev)
         native.call("srml_nearest_centroid_split_tiled_np", XPr.data_ptr(), nf, XPr.shape[1] * 256, kp,
                     CP.data_ptr(), k, crows, cn.data_ptr(), best.data_ptr(), 6, st)
@@ -554,7 +570,7 @@ def nearest_centroid_f16(F: F16Planes, C: torch.Tensor) -> Tuple[torch.Tensor, t
     _CERTIFY_STATS["refined"] += nf
     if nf:
         rows = flagged[:nf]
-        XPr = split_bf16x3(F.X.index_select(0, rows.long()), tiled=True, mu=F.mu)
+        XPr = split_bf16x3_rows(F.X, rows, F.mu)
         CPb = split_bf16x3(W, 256, tiled=True)
         best = torch.full((nf,), -1, dtype=torch.int64, device=dev)
         native.call("srml_nearest_centroid_split_tiled_np", XPr.data_ptr(), nf, XPr.shape[1] * 256, F.kp,

@@ -77,7 +77,8 @@ __global__ __launch_bounds__(256) void split_kernel(const float* __restrict__ X,
 // 128-B line used whole) instead of 32-B pieces of 256 rows 6 KB apart.
 __global__ __launch_bounds__(256) void split_tiled_kernel(const float* __restrict__ X, long m, int n, long ld, int kp,
                                                           long rows_pad, unsigned short* __restrict__ P,
-                                                          const float* __restrict__ mu) {
+                                                          const float* __restrict__ mu,
+                                                          const int* __restrict__ ridx = nullptr) {
   // one thread = one row's 16-wide k step (64 B of X in, one 32-B slot per plane out); a block =
   // the 256 rows of one (tile, k step) image, so each block writes three contiguous 8 KiB images
   const int ks_n = kp >> 4;
@@ -90,16 +91,17 @@ __global__ __launch_bounds__(256) void split_tiled_kernel(const float* __restric
     const long tile = img / ks_n;
     const int c0 = (int)(img - tile * ks_n) * 16;
     const long r = tile * 256 + rr;
+    const long rs = ridx && r < m ? (long)ridx[r] : r;  // gathered rows (the filter's re-search list)
     float x[16];
     if (vec && r < m && c0 + 16 <= n) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const floatx4 v = *reinterpret_cast<const floatx4*>(X + r * ld + c0 + 4 * q);
+        const floatx4 v = *reinterpret_cast<const floatx4*>(X + rs * ld + c0 + 4 * q);
         x[4 * q] = v[0]; x[4 * q + 1] = v[1]; x[4 * q + 2] = v[2]; x[4 * q + 3] = v[3];
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < 16; ++j) x[j] = (r < m && c0 + j < n) ? X[r * ld + c0 + j] : 0.f;
+      for (int j = 0; j < 16; ++j) x[j] = (r < m && c0 + j < n) ? X[rs * ld + c0 + j] : 0.f;
     }
     if (mu && r < m) {  // centred planes (x - mu): same distances, smaller operands
 #pragma unroll
@@ -829,6 +831,22 @@ SRML_API int srml_split_bf16x3_tiled_centered(const float* X, long m, int n, lon
   if (blocks > 65536) blocks = 65536;
   hipLaunchKernelGGL(split_tiled_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, X, m, n, ld, kp, rows_pad, P,
                      mu);
+  return srml_status();
+}
+
+// Tiled centred planes of the rows X[ridx[0..m)] (a gathered copy never exists): the re-search
+// operand of the certified filters' flagged rows
+SRML_API int srml_split_bf16x3_tiled_centered_rows(const float* X, long ld, const int* ridx, long m, int n,
+                                                   const float* mu, int kp, long rows_pad, unsigned short* P,
+                                                   hipStream_t stream) {
+  if (rows_pad <= 0) return 0;
+  if ((kp & 15) || kp < n || rows_pad < m || (rows_pad & 255) || !ridx) return -2;
+  if ((reinterpret_cast<uintptr_t>(P) & 15) != 0) return -5;
+  long total = rows_pad * (long)(kp / 4);
+  long blocks = (total + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(split_tiled_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, X, m, n, ld, kp, rows_pad, P,
+                     mu, ridx);
   return srml_status();
 }
 

@@ -72,6 +72,7 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_nearest_centroid_split_tiled_np": (_P, _L, _L, _I, _P, _I, _L, _P, _P, _I, _P),
     "srml_nearest_centroid_split_top2": (_P, _L, _L, _I, _P, _I, _L, _P, _P, _P, _P, _P, _P),
     "srml_split_bf16x3_tiled_centered": (_P, _L, _I, _L, _P, _I, _L, _P, _P),
+    "srml_split_bf16x3_tiled_centered_rows": (_P, _L, _P, _L, _I, _P, _I, _L, _P, _P),
     "srml_row_sqnorm_centered_f32": (_P, _L, _I, _L, _P, _P, _P),
     "srml_row_sqnorm_centered_amax_f32": (_P, _L, _I, _L, _P, _P, _P, _P),
     "srml_rf_bootstrap_ws": (_I, _L),

@@ -906,3 +906,15 @@ def test_rf_bootstrap_matches_cpu_draw(gpu_device, T, m, rate):
     i_c, w_c, b_c = ops.rf_bootstrap(T, m, rate, 1234567, torch.device("cpu"))
     np.testing.assert_array_equal(b_g, b_c)
     assert torch.equal(i_g.cpu(), i_c) and torch.equal(w_g.cpu(), w_c)
+
+
+@pytest.mark.parametrize("m,n,nr", [(5000, 3000, 777), (1000, 130, 1000), (300, 64, 1)])
+def test_split_rows_matches_gathered_split(gpu_device, m, n, nr):
+    """Tiled centred planes read through a row index list == the planes of the gathered copy."""
+    X = _rand(m, n, gpu_device, seed=51)
+    mu = X.double().mean(0).float()
+    g = torch.Generator(device="cpu").manual_seed(nr)
+    rows = torch.randperm(m, generator=g)[:nr].to(gpu_device).int()
+    got = ops.split_bf16x3_rows(X, rows, mu)
+    ref = ops.split_bf16x3(X.index_select(0, rows.long()), tiled=True, mu=mu)
+    assert got.shape == ref.shape and torch.equal(got.view(torch.int16), ref.view(torch.int16))
