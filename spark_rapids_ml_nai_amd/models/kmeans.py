@@ -87,14 +87,15 @@ def init_kmeans_parallel(X: torch.Tensor, xnorm: torch.Tensor, desc: PartitionDe
     The distance passes over X use the split-bf16 MFMA kernel when the Lloyd loop will (``XP``),
     in its 3-product approximate form (D^2 sampling and candidate weights tolerate ~1e-5
     relative distance error; half the MFMA work of the exact Lloyd passes), or — ``F16`` given
-    (``ops.F16Planes``) — the Lloyd loop's fp16 certified filter (exact labels, a sixth of the
-    exact pass's MFMAs)."""
+    (``ops.F16Planes``) — the Lloyd loop's fp16 filter pass with radius 0 (its own arg-min, ~1e-3
+    relative distance error at worst; only exact ties re-searched): near-equidistant random
+    candidates would otherwise send most rows to the exact re-search."""
     dev = X.device
     m = X.shape[0]
 
     def nearest(C: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-        if F16 is not None:
-            return ops.nearest_centroid_f16(F16, C.float())
+        if F16 is not None:  # D^2 sampling / weights: the filter's own arg-min, no re-search
+            return ops.nearest_centroid_f16(F16, C.float(), approx=True)
         if XP is not None:  # sampling / weighting only need approximate distances
             return ops.nearest_centroid_split(XP, m, C.float(), xnorm if xnorm_split is None else xnorm_split,
                                               approx=True, mu=mu)

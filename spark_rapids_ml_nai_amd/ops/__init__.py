@@ -522,14 +522,16 @@ class F16Planes:
         self.xadd, self.z, self.z2 = f16_radius_terms(n, self.scale, self.tau)
 
 
-def nearest_centroid_f16(F: F16Planes, C: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+def nearest_centroid_f16(F: F16Planes, C: torch.Tensor, approx: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
     """(labels, squared distances) of F.X's rows under centres C by the fp16 certified filter:
     one fp16 MFMA product per (row, centre) on the scaled planes (a third of the 3-product bf16
     filter's MFMAs, half its staged bytes) keeps each row's best and the lowest lower bound of the
     others under the radius ``certify_tau16`` / ``f16_radius_terms``; rows it cannot certify (and
     every row if a centre fell outside the fp16 range) are re-searched with the fp32-exact
     6-product kernel. The labels are those of the exact search; a certified row's distance is the
-    filter's (within its radius: inertia / D^2 weights), a re-searched row's the exact one."""
+    filter's (within its radius: inertia / D^2 weights), a re-searched row's the exact one.
+    ``approx=True`` (k-means|| D^2 sampling and candidate weights): radius 0 — every row takes the
+    filter's arg-min and only exact ties of the filtered distances are re-searched."""
     m, k, dev = F.m, C.shape[0], F.X.device
     st = native.stream(dev)
     W = _c(C.float().to(dev) - F.mu.view(1, -1))  # centred centres: the exact search's operands
@@ -539,7 +541,8 @@ def nearest_centroid_f16(F: F16Planes, C: torch.Tensor) -> Tuple[torch.Tensor, t
     F.ovf.zero_()  # X's own plane never overflows (s comes from its maximum); only the centres can
     native.call("srml_split_f16_tiled_centered", W.data_ptr(), k, F.n, W.stride(0), None, F.kp, crows, F.scale,
                 CP.data_ptr(), F.ovf.data_ptr(), st)
-    cg = (2.0 * F.tau) * cn.clamp_min(0).sqrt()
+    cg = torch.zeros_like(cn) if approx else (2.0 * F.tau) * cn.clamp_min(0).sqrt()
+    xadd, z, z2 = (0.0, 0.0, 0.0) if approx else (F.xadd, F.z, F.z2)
     nslot = int(native.lib().srml_nearest_centroid_f16_top2_nslot(k))
     labels = torch.empty(m, dtype=torch.int32, device=dev)
     dist = torch.empty(m, dtype=torch.float32, device=dev)
@@ -555,11 +558,11 @@ def nearest_centroid_f16(F: F16Planes, C: torch.Tensor) -> Tuple[torch.Tensor, t
         Pc = F.P[r0 // 256: (r0 + mc + 255) // 256]
         xn = F.xnorm[r0: r0 + mc]
         native.call("srml_nearest_centroid_f16_top2", Pc.data_ptr(), mc, Pc.shape[0] * 256, F.kp, CP.data_ptr(), k,
-                    crows, cn.data_ptr(), cg.data_ptr(), xn.data_ptr(), -2.0 / (F.scale * F.scale), F.xadd,
+                    crows, cn.data_ptr(), cg.data_ptr(), xn.data_ptr(), -2.0 / (F.scale * F.scale), xadd,
                     keys.data_ptr(), lob.data_ptr(), st)
         c0 = int(cnt.item()) if r0 else 0
         native.call("srml_split_top2_select_f16", keys.data_ptr(), lob.data_ptr(), mc, nslot, xn.data_ptr(),
-                    cg.data_ptr(), F.xadd, F.z, F.z2, F.ovf.data_ptr(), labels[r0:].data_ptr(), dist[r0:].data_ptr(),
+                    cg.data_ptr(), xadd, z, z2, F.ovf.data_ptr(), labels[r0:].data_ptr(), dist[r0:].data_ptr(),
                     flagged.data_ptr(), cnt.data_ptr(), st)
         if r0:
             nc = int(cnt.item())

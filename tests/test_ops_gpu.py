@@ -918,3 +918,23 @@ def test_split_rows_matches_gathered_split(gpu_device, m, n, nr):
     got = ops.split_bf16x3_rows(X, rows, mu)
     ref = ops.split_bf16x3(X.index_select(0, rows.long()), tiled=True, mu=mu)
     assert got.shape == ref.shape and torch.equal(got.view(torch.int16), ref.view(torch.int16))
+
+
+def test_nearest_centroid_f16_approx_mode(gpu_device):
+    """k-means|| mode (radius 0): the filter's own arg-min — distances within the certified radius
+    of the exact ones, labels equal wherever the exact gap exceeds twice that radius."""
+    m, n, k = 20000, 700, 513
+    X = _rand(m, n, gpu_device, seed=61)
+    C = X[torch.randperm(m, generator=torch.Generator().manual_seed(3))[:k].to(gpu_device)] + 0.01
+    mu = ops.col_moments(X, need_sq=False)[0].div_(m).float()
+    F = ops.F16Planes(X, mu)
+    lab_a, d_a = ops.nearest_centroid_f16(F, C, approx=True)
+    Xd, Cd = X.double() - mu.double(), C.double() - mu.double()
+    D = (Xd * Xd).sum(1, keepdim=True) - 2.0 * Xd @ Cd.T + (Cd * Cd).sum(1).view(1, -1)
+    top2 = D.topk(2, dim=1, largest=False).values
+    radius = 2.0 * ops.certify_tau16(n) * Xd.norm(dim=1) * Cd.norm(dim=1).max()
+    got = D.gather(1, lab_a.long().view(-1, 1)).view(-1)
+    assert ((got - top2[:, 0]) <= 2.0 * radius + 1e-6).all()  # never worse than the radius allows
+    clear = (top2[:, 1] - top2[:, 0]) > 2.0 * radius
+    assert torch.equal(lab_a[clear].long(), D.argmin(1)[clear])
+    assert (d_a.double() - top2[:, 0]).abs().max().item() <= radius.max().item() + 1e-6
