@@ -463,12 +463,13 @@ F16_A = 2.0 ** -14  # absolute error of an fp16 element below the normal range (
 
 
 def certify_tau16(n: int) -> float:
-    """Radius of the one-product fp16 filter relative to ||x - mu|| ||c - mu||: the fp16 rounding of
-    both operands (2u + u^2, u = 2^-11; the absolute subnormal term is separate, ``f16_radius_terms``),
-    the fp32 accumulation of the filter's n exact fp16 products and of the exact 6-product search
-    (each <= n 2^-24 ||x|| ||c||, Cauchy-Schwarz), the exact search's dropped products (< 2^-20),
-    times 1.01 (fp32 evaluation of the norms and of the test itself)."""
-    return 1.01 * (2.0 * F16_U + F16_U * F16_U + 2.0 ** -20 + 2.01 * float(n) * 2.0 ** -24)
+    """Radius of the one-product fp16 filter relative to ||x - mu|| ||c - mu||, against the TRUE
+    distances of the fp32 centred operands (the re-search evaluates its candidates in fp64): the fp16
+    rounding of both operands (2u + u^2, u = 2^-11; the absolute subnormal term and the fp32 rounding
+    of ||c - mu||^2 are separate, ``f16_radius_terms``), the fp32 accumulation of the filter's n
+    exact fp16 products (<= n 2^-24 ||x|| ||c||, Cauchy-Schwarz), times 1.01 (fp32 evaluation of
+    the norms and of the test itself)."""
+    return 1.01 * (2.0 * F16_U + F16_U * F16_U + 1.01 * float(n) * 2.0 ** -24)
 
 
 def f16_radius_terms(n: int, scale: float, tau: float) -> Tuple[float, float, float]:
@@ -479,7 +480,11 @@ def f16_radius_terms(n: int, scale: float, tau: float) -> Tuple[float, float, fl
     a = F16_A / scale
     z = 2.02 * a * math.sqrt(n) * (1.0 + F16_U)
     z2 = 2.02 * float(n) * a * a
-    return z / (2.0 * tau), z, z2
+    # ||c_j - mu||^2 enters d~_j as an fp32 rounding of its fp64 value: <= 2^-24 ||w_j||^2
+    # <= (2^-24 wmax / (2 tau)) g_j with wmax = sqrt(n) 2^15 / scale (no element of s w reaches 2^15
+    # without raising the overflow flag)
+    wmax = math.sqrt(n) * 32768.0 / scale
+    return (z + 2.0 ** -24 * wmax) / (2.0 * tau), z, z2
 
 
 class F16Planes:
@@ -522,20 +527,26 @@ class F16Planes:
         self.xadd, self.z, self.z2 = f16_radius_terms(n, self.scale, self.tau)
 
 
+F16_CAND_CAP = 64  # candidate-list capacity per re-searched row (more: that row scans every centre)
+
+
 def nearest_centroid_f16(F: F16Planes, C: torch.Tensor, approx: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
     """(labels, squared distances) of F.X's rows under centres C by the fp16 certified filter:
     one fp16 MFMA product per (row, centre) on the scaled planes (a third of the 3-product bf16
     filter's MFMAs, half its staged bytes) keeps each row's best and the lowest lower bound of the
-    others under the radius ``certify_tau16`` / ``f16_radius_terms``; rows it cannot certify (and
-    every row if a centre fell outside the fp16 range) are re-searched with the fp32-exact
-    6-product kernel. The labels are those of the exact search; a certified row's distance is the
-    filter's (within its radius: inertia / D^2 weights), a re-searched row's the exact one.
+    others under the radius ``certify_tau16`` / ``f16_radius_terms`` (proven against the true
+    distances of the fp32 centred operands). Rows it cannot certify are re-searched: a second fp16
+    pass over just those rows lists every centre whose lower bound does not exceed the row's
+    certified upper bound on its best distance (the true arg-min is always listed), and those
+    candidates are evaluated exactly in fp64 (``srml_kmeans_cand_exact``). Labels are therefore the
+    exact arg-min (lowest index on exact ties) for every row; a certified row's distance is the
+    filter's (within its radius: inertia / D^2 weights), a re-searched row's the fp64 one.
     ``approx=True`` (k-means|| D^2 sampling and candidate weights): radius 0 — every row takes the
     filter's arg-min and only exact ties of the filtered distances are re-searched."""
     m, k, dev = F.m, C.shape[0], F.X.device
     st = native.stream(dev)
-    W = _c(C.float().to(dev) - F.mu.view(1, -1))  # centred centres: the exact search's operands
-    cn = (W * W).sum(1)
+    W = _c(C.float().to(dev) - F.mu.view(1, -1))  # centred centres: the operands of every search
+    cn = (W.double() * W.double()).sum(1).float()  # fp64 norms, one fp32 rounding (in the radius)
     crows = max(256, (k + 255) // 256 * 256)
     CP = torch.empty((crows // 256, F.kp // 16, 256, 16), dtype=torch.float16, device=dev)
     F.ovf.zero_()  # X's own plane never overflows (s comes from its maximum); only the centres can
@@ -543,10 +554,12 @@ def nearest_centroid_f16(F: F16Planes, C: torch.Tensor, approx: bool = False) ->
                 CP.data_ptr(), F.ovf.data_ptr(), st)
     cg = torch.zeros_like(cn) if approx else (2.0 * F.tau) * cn.clamp_min(0).sqrt()
     xadd, z, z2 = (0.0, 0.0, 0.0) if approx else (F.xadd, F.z, F.z2)
+    dscale = -2.0 / (F.scale * F.scale)
     nslot = int(native.lib().srml_nearest_centroid_f16_top2_nslot(k))
     labels = torch.empty(m, dtype=torch.int32, device=dev)
     dist = torch.empty(m, dtype=torch.float32, device=dev)
     flagged = torch.empty(m, dtype=torch.int32, device=dev)
+    thr = torch.empty(m, dtype=torch.float32, device=dev)
     cnt = torch.zeros(1, dtype=torch.int32, device=dev)
     # row chunks of whole 256-row tiles within the 2^32 work-item grid (512-thread blocks x
     # centre tiles); the select appends each chunk's uncertified rows (chunk-relative) to flagged
@@ -558,12 +571,12 @@ def nearest_centroid_f16(F: F16Planes, C: torch.Tensor, approx: bool = False) ->
         Pc = F.P[r0 // 256: (r0 + mc + 255) // 256]
         xn = F.xnorm[r0: r0 + mc]
         native.call("srml_nearest_centroid_f16_top2", Pc.data_ptr(), mc, Pc.shape[0] * 256, F.kp, CP.data_ptr(), k,
-                    crows, cn.data_ptr(), cg.data_ptr(), xn.data_ptr(), -2.0 / (F.scale * F.scale), xadd,
-                    keys.data_ptr(), lob.data_ptr(), st)
+                    crows, cn.data_ptr(), cg.data_ptr(), xn.data_ptr(), dscale, xadd, keys.data_ptr(), lob.data_ptr(),
+                    st)
         c0 = int(cnt.item()) if r0 else 0
-        native.call("srml_split_top2_select_f16", keys.data_ptr(), lob.data_ptr(), mc, nslot, xn.data_ptr(),
+        native.call("srml_split_top2_select_f16_thr", keys.data_ptr(), lob.data_ptr(), mc, nslot, xn.data_ptr(),
                     cg.data_ptr(), xadd, z, z2, F.ovf.data_ptr(), labels[r0:].data_ptr(), dist[r0:].data_ptr(),
-                    flagged.data_ptr(), cnt.data_ptr(), st)
+                    flagged.data_ptr(), cnt.data_ptr(), thr.data_ptr(), st)
         if r0:
             nc = int(cnt.item())
             flagged[c0:nc] += r0
@@ -573,13 +586,28 @@ def nearest_centroid_f16(F: F16Planes, C: torch.Tensor, approx: bool = False) ->
     _CERTIFY_STATS["refined"] += nf
     if nf:
         rows = flagged[:nf]
-        XPr = split_bf16x3_rows(F.X, rows, F.mu)
-        CPb = split_bf16x3(W, 256, tiled=True)
-        best = torch.full((nf,), -1, dtype=torch.int64, device=dev)
-        native.call("srml_nearest_centroid_split_tiled_np", XPr.data_ptr(), nf, XPr.shape[1] * 256, F.kp,
-                    CPb.data_ptr(), k, CPb.shape[1] * 256, cn.data_ptr(), best.data_ptr(), 6, st)
-        native.call("srml_split_scatter_refined", best.data_ptr(), rows.data_ptr(), nf, F.xnorm.data_ptr(),
-                    labels.data_ptr(), dist.data_ptr(), st)
+        X = F.X
+        assert X.stride(1) == 1
+        cap = F16_CAND_CAP
+        ccount = torch.zeros(nf, dtype=torch.int32, device=dev)
+        cand = torch.empty(nf * cap, dtype=torch.int32, device=dev)
+        scratch = torch.zeros(1, dtype=torch.int32, device=dev)
+        stepr = split_rows_per_launch(k)
+        for q0 in range(0, nf, stepr):
+            nq = min(stepr, nf - q0)
+            rq = rows[q0: q0 + nq]
+            rp = max(256, (nq + 255) // 256 * 256)
+            Pr = torch.empty((rp // 256, F.kp // 16, 256, 16), dtype=torch.float16, device=dev)
+            native.call("srml_split_f16_tiled_centered_rows", X.data_ptr(), X.stride(0), rq.data_ptr(), nq, F.n,
+                        F.mu.data_ptr(), F.kp, rp, F.scale, Pr.data_ptr(), scratch.data_ptr(), st)
+            xr = F.xnorm.index_select(0, rq.long())
+            native.call("srml_nearest_centroid_f16_cand", Pr.data_ptr(), nq, rp, F.kp, CP.data_ptr(), k, crows,
+                        cn.data_ptr(), cg.data_ptr(), xr.data_ptr(), dscale, xadd, thr[q0:].data_ptr(),
+                        ccount[q0:].data_ptr(), cand[q0 * cap:].data_ptr(), cap, st)
+            del Pr
+        native.call("srml_kmeans_cand_exact", X.data_ptr(), X.stride(0), F.mu.data_ptr(), W.data_ptr(), W.stride(0),
+                    F.n, k, rows.data_ptr(), nf, ccount.data_ptr(), cand.data_ptr(), cap, labels.data_ptr(),
+                    dist.data_ptr(), st)
     return labels, dist
 
 

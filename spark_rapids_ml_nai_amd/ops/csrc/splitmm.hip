@@ -143,7 +143,7 @@ __global__ __launch_bounds__(256) void split_tiled_kernel(const float* __restric
 __global__ __launch_bounds__(256) void split_tiled_f16_kernel(const float* __restrict__ X, long m, int n, long ld, int kp,
                                                               long rows_pad, unsigned short* __restrict__ P,
                                                               const float* __restrict__ mu, float scale,
-                                                              int* __restrict__ ovf) {
+                                                              int* __restrict__ ovf, const int* __restrict__ ridx = nullptr) {
   const int ks_n = kp >> 4;
   const long total = rows_pad * ks_n;
   const bool vec = (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
@@ -154,16 +154,17 @@ __global__ __launch_bounds__(256) void split_tiled_f16_kernel(const float* __res
     const long tile = img / ks_n;
     const int c0 = (int)(img - tile * ks_n) * 16;
     const long r = tile * 256 + rr;
+    const long rs = ridx && r < m ? (long)ridx[r] : r;
     float x[16];
     if (vec && r < m && c0 + 16 <= n) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const floatx4 v = *reinterpret_cast<const floatx4*>(X + r * ld + c0 + 4 * q);
+        const floatx4 v = *reinterpret_cast<const floatx4*>(X + rs * ld + c0 + 4 * q);
         x[4 * q] = v[0]; x[4 * q + 1] = v[1]; x[4 * q + 2] = v[2]; x[4 * q + 3] = v[3];
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < 16; ++j) x[j] = (r < m && c0 + j < n) ? X[r * ld + c0 + j] : 0.f;
+      for (int j = 0; j < 16; ++j) x[j] = (r < m && c0 + j < n) ? X[rs * ld + c0 + j] : 0.f;
     }
     unsigned hw[8];
 #pragma unroll
@@ -382,10 +383,44 @@ __device__ __forceinline__ void split_epilogue_top2_t(const floatx16 (&acc)[BM /
     }
     if (lk == 0 && row < m) {
       const long o = (long)slot * m + row;
-      keys[o] = (bi == 0x7fffffff || !(bv < __builtin_huge_valf())) ? ~0ull
-                                                                      : (((unsigned long long)orderable(bv) << 32) | (unsigned)bi);
+      const bool none = bi == 0x7fffffff || !(bv < __builtin_huge_valf());
+      keys[o] = none ? ~0ull : (((unsigned long long)orderable(bv) << 32) | (unsigned)bi);
       lob[o] = sadj;
     }
+  }
+}
+
+// Candidate epilogue of the fp16 re-search pass (transposed accumulators as split_epilogue_top2_t):
+// every centre j whose lower bound d~_j - (||x|| + xadd) g_j is <= thr[row] (the row's certified upper
+// bound on the best distance from the filter pass) is appended to the row's list (cap entries; the
+// count keeps growing past cap so the exact pass can tell an overflow)
+template <int BM, int BN, int WM, int WN>
+__device__ __forceinline__ void split_epilogue_cand_t(const floatx16 (&acc)[BM / WM / 32][BN / WN / 32], long row0,
+                                                      int col0, long m, int k, const float* __restrict__ cnorm,
+                                                      const float* __restrict__ cg, const float* __restrict__ xnorm,
+                                                      int wm, int wn, int li, int lk, float dscale, float xadd,
+                                                      const float* __restrict__ thr, int* __restrict__ ccount,
+                                                      int* __restrict__ cand, int cap) {
+  constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+#pragma unroll
+  for (int mt = 0; mt < TM; ++mt) {
+    const long row = row0 + wm * (BM / WM) + mt * 32 + li;
+    if (row >= m) continue;
+    const float xs = sqrtf(fmaxf(xnorm[row], 0.f)) + xadd;
+    const float t = thr[row];
+#pragma unroll
+    for (int nt = 0; nt < TN; ++nt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int j = col0 + wn * (BN / WN) + nt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        if (j < k) {
+          const float d = fmaf(dscale, acc[mt][nt][r], cnorm[j]);
+          if (fmaf(-xs, cg[j], d) <= t) {
+            const int p = atomicAdd(&ccount[row], 1);
+            if (p < cap) cand[row * (long)cap + p] = j;
+          }
+        }
+      }
   }
 }
 
@@ -531,12 +566,14 @@ typedef __attribute__((address_space(1))) void* gbl_vptr;
 // tiled image.
 // PRIO: s_setprio(1) / (0) around every MFMA cluster: keeps hipcc from moving MFMAs across the
 // raw barriers into the load phase (cdna_hip_programming.md T5).
-template <bool TILED, int NP = 6, bool TOP2 = false, int WN_ = 4, bool PRIO = false>
+template <bool TILED, int NP = 6, bool TOP2 = false, int WN_ = 4, bool PRIO = false, bool CAND = false>
 __global__ __launch_bounds__(WN_ * 128, WN_ == 4 ? 1 : 2) void nearest_centroid_split_glds_kernel(
     const unsigned short* __restrict__ XP, long m, long xrows, int kp, const unsigned short* __restrict__ CP, int k,
     long crows, const float* __restrict__ cnorm, unsigned long long* __restrict__ best, int n_ctiles,
     float* __restrict__ lob = nullptr, const float* __restrict__ cg = nullptr, const float* __restrict__ xnorm = nullptr,
-    float dscale = -2.f, float xadd = 0.f) {
+    float dscale = -2.f, float xadd = 0.f, const float* __restrict__ thr = nullptr, int* __restrict__ ccount = nullptr,
+    int* __restrict__ cand = nullptr, int cap = 0) {
+  static_assert(!CAND || (NP == 1 && TOP2), "candidate lists come from the fp16 filter");
   static_assert(WN_ == 4 || (WN_ == 2 && NP != 6), "256 x 128 tiles are built for the filter passes");
   static_assert(NP == 6 || NP == 3 || (NP == 1 && TOP2), "NP = 1 is the fp16 certified filter");
   constexpr int BM = 256, WM = 2, WN = WN_, BN = 64 * WN, TM = 4, TN = 2;
@@ -687,7 +724,10 @@ __global__ __launch_bounds__(WN_ * 128, WN_ == 4 ? 1 : 2) void nearest_centroid_
       if (PRIO) __builtin_amdgcn_s_setprio(0);
     }
   }
-  if (TOP2 && NP == 1)
+  if (CAND)
+    split_epilogue_cand_t<BM, BN, WM, WN>(acc, row0, col0, m, k, cnorm, cg, xnorm, wm, wn, li, lk, dscale, xadd, thr,
+                                          ccount, cand, cap);
+  else if (TOP2 && NP == 1)
     split_epilogue_top2_t<BM, BN, WM, WN>(acc, row0, col0, ctile, m, k, cnorm, cg, xnorm, best, lob, n_ctiles * WN, wm,
                                           wn, li, lk, dscale, xadd);
   else if (TOP2)
@@ -710,7 +750,8 @@ __global__ __launch_bounds__(256) void split_top2_select_kernel(const unsigned l
                                                                 int* __restrict__ labels, float* __restrict__ dist,
                                                                 int* __restrict__ flagged, int* __restrict__ n_flagged,
                                                                 float xadd = 0.f, float z = 0.f, float z2 = 0.f,
-                                                                const int* __restrict__ ovf = nullptr) {
+                                                                const int* __restrict__ ovf = nullptr,
+                                                                float* __restrict__ thr_out = nullptr) {
   // fp16 filter (srml_split_top2_select_f16): the radius of candidate j is (||x|| + xadd) g_j +
   // z ||x|| + z2 (the last two terms: subnormal fp16 elements, the same for every j, so they enter
   // the test once per side); an overflowed centroid plane (*ovf) certifies nothing
@@ -739,7 +780,49 @@ __global__ __launch_bounds__(256) void split_top2_select_kernel(const unsigned l
     const float d = bv + xn;
     dist[i] = d > 0.f ? d : 0.f;
   } else {
-    flagged[atomicAdd(n_flagged, 1)] = (int)i;
+    const int p = atomicAdd(n_flagged, 1);
+    flagged[p] = (int)i;
+    // the row's certified upper bound on its best distance: the re-search keeps every centre whose
+    // lower bound does not exceed it (an overflowed centre plane: no bound, every centre)
+    if (thr_out)
+      thr_out[p] = (k1 != ~0ull && !(ovf && *ovf)) ? fmaf(xs, cg[(int)(k1 & 0xffffffffu)], bv) + c2
+                                                   : __builtin_huge_valf();
+  }
+}
+
+// Exact pass of the fp16 re-search: one wave per flagged row, squared distances to its candidate
+// centres in fp64 ((x - mu) and (c - mu) as the fp32 values every search uses; each term exact in
+// fp64, the 3000-term sum ~n 2^-53 relative), arg-min with the lowest index on ties; a row whose
+// list overflowed (count > cap) scans every centre.
+__global__ __launch_bounds__(256) void cand_exact_kernel(const float* __restrict__ X, long ld,
+                                                         const float* __restrict__ mu, const float* __restrict__ W,
+                                                         long ldw, int n, int k, const int* __restrict__ rows, int nf,
+                                                         const int* __restrict__ ccount, const int* __restrict__ cand,
+                                                         int cap, int* __restrict__ labels, float* __restrict__ dist) {
+  const int lane = threadIdx.x & 63;
+  const long w = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (w >= nf) return;
+  const long i = rows[w];
+  const float* xr = X + i * ld;
+  const int cnt = ccount[w];
+  const bool full = cnt > cap || cnt <= 0;
+  const int nc = full ? k : cnt;
+  double bd = __builtin_huge_val();
+  int bj = 0x7fffffff;
+  for (int q = 0; q < nc; ++q) {
+    const int j = full ? q : cand[w * (long)cap + q];
+    const float* wr = W + (long)j * ldw;
+    double acc = 0.0;
+    for (int l = lane; l < n; l += 64) {
+      const double dv = (double)(xr[l] - mu[l]) - (double)wr[l];
+      acc = fma(dv, dv, acc);
+    }
+    acc = wave_sum(acc);
+    if (acc < bd || (acc == bd && j < bj)) { bd = acc; bj = j; }
+  }
+  if (lane == 0) {
+    labels[i] = bj;
+    dist[i] = (float)bd;
   }
 }
 
@@ -1013,5 +1096,61 @@ SRML_API int srml_split_top2_select_f16(const unsigned long long* keys, const fl
   if (m <= 0) return 0;
   hipLaunchKernelGGL(split_top2_select_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream, keys, lob, m,
                      nslot, xnorm, cg, labels, dist, flagged, n_flagged, xadd, z, z2, ovf);
+  return srml_status();
+}
+
+// ---- fp16 filter re-search (candidate lists + fp64 exact distances) -------------------------
+// fp16 plane of the gathered rows X[ridx[0..m)] (same scale / layout as srml_split_f16_tiled_centered)
+SRML_API int srml_split_f16_tiled_centered_rows(const float* X, long ld, const int* ridx, long m, int n,
+                                                const float* mu, int kp, long rows_pad, float scale, unsigned short* P,
+                                                int* ovf, hipStream_t stream) {
+  if (rows_pad <= 0) return 0;
+  if ((kp & 15) || kp < n || rows_pad < m || (rows_pad & 255) || !ridx) return -2;
+  if ((reinterpret_cast<uintptr_t>(P) & 15) != 0) return -5;
+  const long total = rows_pad * (long)(kp / 16);
+  long blocks = (total + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(split_tiled_f16_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, X, m, n, ld, kp, rows_pad, P,
+                     mu, scale, ovf, ridx);
+  return srml_status();
+}
+
+// select of the filter pass with the flagged rows' thresholds (thr_out[p] for flagged[p])
+SRML_API int srml_split_top2_select_f16_thr(const unsigned long long* keys, const float* lob, long m, int nslot,
+                                            const float* xnorm, const float* cg, float xadd, float z, float z2,
+                                            const int* ovf, int* labels, float* dist, int* flagged, int* n_flagged,
+                                            float* thr_out, hipStream_t stream) {
+  if (m <= 0) return 0;
+  hipLaunchKernelGGL(split_top2_select_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream, keys, lob, m,
+                     nslot, xnorm, cg, labels, dist, flagged, n_flagged, xadd, z, z2, ovf, thr_out);
+  return srml_status();
+}
+
+// candidate pass over the flagged rows' fp16 plane XP (m rows): ccount (m, zeroed by the caller),
+// cand (m x cap) — same tile / launch rules as srml_nearest_centroid_f16_top2
+SRML_API int srml_nearest_centroid_f16_cand(const unsigned short* XP, long m, long xrows, int kp,
+                                            const unsigned short* CP, int k, long crows, const float* cnorm,
+                                            const float* cg, const float* xnorm, float dscale, float xadd,
+                                            const float* thr, int* ccount, int* cand, int cap, hipStream_t stream) {
+  if (m <= 0 || k <= 0) return 0;
+  if ((kp & 15) || xrows < m || crows < k || (crows & 255) || (xrows & 255) || cap < 1) return -2;
+  if ((reinterpret_cast<uintptr_t>(XP) & 15) || (reinterpret_cast<uintptr_t>(CP) & 15)) return -5;
+  const long rt = (m + 255) / 256;
+  const int ct = (k + 255) / 256;
+  const long nb = rt * ct;
+  if (nb > srml_max_blocks(512)) return -3;
+  hipLaunchKernelGGL((nearest_centroid_split_glds_kernel<true, 1, true, 4, true, true>), dim3((unsigned)nb), dim3(512),
+                     0, stream, XP, m, xrows, kp, CP, k, crows, cnorm, (unsigned long long*)nullptr, (int)ct,
+                     (float*)nullptr, cg, xnorm, dscale, xadd, thr, ccount, cand, cap);
+  return srml_status();
+}
+
+// exact fp64 arg-min of each flagged row over its candidate list -> labels / dist at the row
+SRML_API int srml_kmeans_cand_exact(const float* X, long ld, const float* mu, const float* W, long ldw, int n, int k,
+                                    const int* rows, int nf, const int* ccount, const int* cand, int cap, int* labels,
+                                    float* dist, hipStream_t stream) {
+  if (nf <= 0) return 0;
+  hipLaunchKernelGGL(cand_exact_kernel, dim3((unsigned)((nf + 3) / 4)), dim3(256), 0, stream, X, ld, mu, W, ldw, n, k,
+                     rows, nf, ccount, cand, cap, labels, dist);
   return srml_status();
 }

@@ -26,7 +26,8 @@ _D = ctypes.c_double
 _F = ctypes.c_float
 
 # name -> argtypes (restype: int status, except the size queries in _LONG_RESULT)
-_LONG_RESULT = ("srml_rf_bootstrap_ws", "srml_qn_args_size", "srml_logit_residual_ws", "srml_xtv_mfma_ws", "srml_rf_partition_ws",
+_LONG_RESULT = ("srml_rf_bootstrap_ws", "srml_qn_args_size", "srml_logit_residual_ws", "srml_xtv_mfma_ws",
+                "srml_rf_partition_ws",
                 "srml_label_sort_ws", "srml_radix_sort_ws")
 SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_col_moments_f32": (_P, _L, _I, _L, _P, _P, _P),
@@ -81,6 +82,10 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_nearest_centroid_f16_top2": (_P, _L, _L, _I, _P, _I, _L, _P, _P, _P, _F, _F, _P, _P, _P),
     "srml_nearest_centroid_f16_top2_nslot": (_I,),
     "srml_split_top2_select_f16": (_P, _P, _L, _I, _P, _P, _F, _F, _F, _P, _P, _P, _P, _P, _P),
+    "srml_split_f16_tiled_centered_rows": (_P, _L, _P, _L, _I, _P, _I, _L, _F, _P, _P, _P),
+    "srml_split_top2_select_f16_thr": (_P, _P, _L, _I, _P, _P, _F, _F, _F, _P, _P, _P, _P, _P, _P, _P),
+    "srml_nearest_centroid_f16_cand": (_P, _L, _L, _I, _P, _I, _L, _P, _P, _P, _F, _F, _P, _P, _P, _I, _P),
+    "srml_kmeans_cand_exact": (_P, _L, _P, _P, _L, _I, _I, _P, _I, _P, _P, _I, _P, _P, _P),
     "srml_nearest_centroid_split_top2_nslot": (_I,),
     "srml_split_top2_select": (_P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _P),
     "srml_split_scatter_refined": (_P, _P, _I, _P, _P, _P, _P),

@@ -71,10 +71,11 @@ def test_f16_certified_rows_match_fp64_argmin(case):
 def test_f16_radius_terms_consistent():
     n, s = 3000, 2.0 ** 12
     tau = ops.certify_tau16(n)
-    assert tau > 2.0 * 2.0 ** -11 + 2 * n * 2.0 ** -24  # covers rounding + both accumulations
+    assert tau > 2.0 * 2.0 ** -11 + n * 2.0 ** -24  # covers the rounding + the filter's accumulation
     assert tau > ops.certify_tau(n)  # wider than the 3-product bf16 filter's radius
     xadd, z, z2 = ops.f16_radius_terms(n, s, tau)
-    assert xadd == pytest.approx(z / (2 * tau))
+    # xadd = (z + the fp32 rounding of ||c - mu||^2 at the largest representable centre) / (2 tau)
+    assert xadd == pytest.approx((z + 2.0 ** -24 * math.sqrt(n) * 32768.0 / s) / (2 * tau))
     a = 2.0 ** -14 / s
     assert z >= 2 * a * math.sqrt(n) and z2 >= 2 * n * a * a
     np.testing.assert_allclose(ops.f16_radius_terms(n, 2 * s, tau)[1], z / 2)

@@ -751,15 +751,22 @@ def test_nearest_centroid_f16_certified_matches_exact(gpu_device, m, n, k, ties,
         logical = torch.cat([phys[8 * sw: 8 * sw + 8], phys[8 * (sw ^ 1): 8 * (sw ^ 1) + 8]])
         want = ((X[r, :16] - mu[:16]) * F.scale).half().float()
         torch.testing.assert_close(logical[: min(16, n)], want[: min(16, n)], rtol=0, atol=0)
-    XP = ops.split_bf16x3(X, tiled=True, mu=mu)
-    lab_e, d_e = ops.nearest_centroid_split(XP, m, C, F.xnorm, mu=mu)  # exact 6-product search
     before = dict(ops._CERTIFY_STATS)
     lab_f, d_f = ops.nearest_centroid_f16(F, C)
     refined = ops._CERTIFY_STATS["refined"] - before["refined"]
-    assert torch.equal(lab_f, lab_e)
-    cn = ((C.double() - mu.double()) ** 2).sum(1)
-    radius = 4.0 * ops.certify_tau16(n) * (F.xnorm.double().sqrt().max() * cn.sqrt().max()).item()
-    assert (d_f.double() - d_e.double()).abs().max().item() <= radius + 1e-6
+    # truth: fp64 distances of the fp32 centred operands every search uses, lowest index on ties
+    V = (X - mu).double()
+    Wc = (C.float() - mu).double()
+    D = (V * V).sum(1, keepdim=True) - 2.0 * V @ Wc.T + (Wc * Wc).sum(1).view(1, -1)
+    best = D.min(1).values
+    got = D.gather(1, lab_f.long().view(-1, 1)).view(-1)
+    scale = (V.norm(dim=1) * Wc.norm(dim=1).max()).max().item()
+    assert (got - best).abs().max().item() <= 1e-11 * scale  # the exact arg-min (up to fp64 ties)
+    ref = D.argmin(1).int()
+    assert (lab_f == ref).float().mean().item() > 0.9999
+    radius = 2.0 * ops.certify_tau16(n) * scale
+    # certified rows report the filter's distance (within its radius; ||x - mu||^2 in fp32)
+    assert (d_f.double() - best).abs().max().item() <= radius + 1e-4 * (V * V).sum(1).max().item()
     if ties:
         assert refined >= m // 4
     else:
@@ -781,7 +788,9 @@ def test_kmeans_fit_f16_filter_matches_bf16(gpu_device, monkeypatch):
         monkeypatch.setenv("SRML_KMEANS_SPLIT", "1")
         out[mode] = kmeans_fit(X, desc, ctx, k=300, max_iter=5, tol=0.0, seed=3, init="random")
         assert out[mode]["refined_frac"] is not None  # the certified path ran
-    np.testing.assert_allclose(out["f16"]["cluster_centers_"], out["bf16"]["cluster_centers_"], rtol=1e-9, atol=1e-12)
+    # both filters certify against exact searches (fp64 for f16, fp32 6-product for bf16): equal labels
+    # away from fp32-level ties, hence (near-)identical centres
+    np.testing.assert_allclose(out["f16"]["cluster_centers_"], out["bf16"]["cluster_centers_"], rtol=1e-6, atol=1e-6)
 
 
 def test_kmeans_predict_certified_matches_exact(gpu_device, monkeypatch):
