@@ -1228,9 +1228,12 @@ __global__ __launch_bounds__(256) void rf_node_stats_kernel(const int* __restric
           if (k == c) acc[k] += w;
       }
     }
-    for (int k = 0; k < NS; ++k) {
-      const double v = wave_sum(acc[k]);
-      if (lane == 0) red[wid][k] = v;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {  // static indices: acc stays in registers (no scratch)
+      if (k < NS) {
+        const double v = wave_sum(acc[k]);
+        if (lane == 0) red[wid][k] = v;
+      }
     }
     __syncthreads();
     if (threadIdx.x < NS) {
@@ -1269,9 +1272,12 @@ __global__ __launch_bounds__(256) void rf_node_stats_seg_kernel(const int* __res
         if (k == c) acc[k] += w;
     }
   }
-  for (int k = 0; k < NS; ++k) {
-    const double v = wave_sum(acc[k]);
-    if (lane == 0) red[wid][k] = v;
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {  // static indices: acc stays in registers (no scratch)
+    if (k < NS) {
+      const double v = wave_sum(acc[k]);
+      if (lane == 0) red[wid][k] = v;
+    }
   }
   __syncthreads();
   if (threadIdx.x < NS)

@@ -51,15 +51,17 @@ __global__ __launch_bounds__(256, 1) void mlogit_pf_kernel(const float* __restri
         g[k][v][q] = 0.f;
       }
   }
-  double bb[KB];
-#pragma unroll
-  for (int k = 0; k < KB; ++k) bb[k] = (k < K && bvec) ? bvec[(long)k * ldb] : 0.0;
-  double gb[KB];
-  double lk[SIG ? KB : 1];
-#pragma unroll
-  for (int k = 0; k < KB; ++k) gb[k] = 0.0;
-#pragma unroll
-  for (int k = 0; k < (SIG ? KB : 1); ++k) lk[k] = 0.0;
+  // per-class intercepts and the intercept-gradient / loss accumulators live in LDS: only one lane
+  // updates them, and per-lane fp64 copies (3 KB doubles) would push the register-resident weight
+  // and gradient slices into scratch
+  __shared__ double s_bb[KB], s_gb[KB], s_lk[KB];
+  if (threadIdx.x < KB) {
+    const int k = threadIdx.x;
+    s_bb[k] = (k < K && bvec) ? bvec[(long)k * ldb] : 0.0;
+    s_gb[k] = 0.0;
+    s_lk[k] = 0.0;
+  }
+  __syncthreads();
   double loss = 0.0;
   const long r0 = (long)blockIdx.x * rows_per_block;
   const long r1 = min(m, r0 + rows_per_block);
@@ -106,7 +108,7 @@ __global__ __launch_bounds__(256, 1) void mlogit_pf_kernel(const float* __restri
 #pragma unroll
       for (int k = 0; k < KB; ++k) {
         z[k] = (double)part[buf][gi][k][0] + (double)part[buf][gi][k][1] + (double)part[buf][gi][k][2] +
-               (double)part[buf][gi][k][3] + bb[k];
+               (double)part[buf][gi][k][3] + s_bb[k];
         if (k < K) zmax = fmax(zmax, z[k]);
       }
       if constexpr (SIG) {
@@ -116,7 +118,7 @@ __global__ __launch_bounds__(256, 1) void mlogit_pf_kernel(const float* __restri
           double res = 0.0, l = 0.0;
           if (k < K) logistic_terms(z[k], yr, res, l);
           const float rf = (float)res;
-          if (wid == 0 && lane == 0) { gb[k] += res; lk[k] += l; }
+          if (wid == 0 && lane == 0) { s_gb[k] += res; s_lk[k] += l; }
 #pragma unroll
           for (int v = 0; v < V; ++v)
 #pragma unroll
@@ -137,7 +139,7 @@ __global__ __launch_bounds__(256, 1) void mlogit_pf_kernel(const float* __restri
         for (int k = 0; k < KB; ++k) {
           const float res = e[k] * inv - (k == yi ? 1.f : 0.f);
           if (k == yi) zy = z[k];
-          if (wid == 0 && lane == 0) gb[k] += (double)res;
+          if (wid == 0 && lane == 0) s_gb[k] += (double)res;
 #pragma unroll
           for (int v = 0; v < V; ++v)
 #pragma unroll
@@ -160,24 +162,31 @@ __global__ __launch_bounds__(256, 1) void mlogit_pf_kernel(const float* __restri
   }
 #pragma unroll
   for (int k = 0; k < KB; ++k) {
-    if (k >= K) break;
+    if (k < K) {  // a guard, not a break: the loop stays unrolled and g[k] static (no scratch)
 #pragma unroll
-    for (int v = 0; v < V; ++v)
+      for (int v = 0; v < V; ++v)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int c = cbase + (v * 64 + lane) * 4 + q;
-        if (c < n) atomicAdd(&out[(long)k * ldo + c], (double)g[k][v][q]);
-      }
+        for (int q = 0; q < 4; ++q) {
+          const int c = cbase + (v * 64 + lane) * 4 + q;
+          if (c < n) atomicAdd(&out[(long)k * ldo + c], (double)g[k][v][q]);
+        }
+    }
   }
   if (wid == 0 && lane == 0) {
+    // static indices (k < KB, guarded by K): the per-class accumulators stay in registers
     if constexpr (SIG) {
-      for (int k = 0; k < K; ++k) {
-        atomicAdd(&out[(long)k * ldo + n], gb[k]);
-        atomicAdd(&out[(long)k * ldo + n + 1], lk[k]);
+#pragma unroll
+      for (int k = 0; k < KB; ++k) {
+        if (k < K) {
+          atomicAdd(&out[(long)k * ldo + n], s_gb[k]);
+          atomicAdd(&out[(long)k * ldo + n + 1], s_lk[k]);
+        }
       }
     } else {
       const long base = (long)K * n;
-      for (int k = 0; k < K; ++k) atomicAdd(&out[base + k], gb[k]);
+#pragma unroll
+      for (int k = 0; k < KB; ++k)
+        if (k < K) atomicAdd(&out[base + k], s_gb[k]);
       atomicAdd(&out[base + K], loss);
     }
   }

@@ -38,28 +38,36 @@ __global__ __launch_bounds__(256) void xw_rows_kernel(const float* __restrict__ 
   const long nwaves = (long)gridDim.x * 4;
   for (long r0 = 2 * wave; r0 < m; r0 += 2 * nwaves) {
     const long ra = r0, rb = (r0 + 1 < m) ? r0 + 1 : r0;
-    floatx4 xa[V], xb[V];
-#pragma unroll
-    for (int v = 0; v < V; ++v) {
-      const int c = (v * 64 + lane) * 4;
-      const int cc = c < n ? c : 0;  // n % 4 == 0 on this path; padded W rows are zero
-      xa[v] = *reinterpret_cast<const floatx4*>(X + ra * ld + cc);
-      xb[v] = *reinterpret_cast<const floatx4*>(X + rb * ld + cc);
-    }
     float acca[K], accb[K];
 #pragma unroll
     for (int c = 0; c < K; ++c) { acca[c] = 0.f; accb[c] = 0.f; }
+    // the two rows stream through in chunks of VC float4 per lane: all V chunks at once when the
+    // row slices and the 2K accumulators fit the register budget, else VC = 2 per step (wide K x
+    // long rows would otherwise spill the row slices to scratch)
+    constexpr int VC = (2 * K + 8 * V <= 112) ? V : 2;
+#pragma unroll 1
+    for (int v0 = 0; v0 < V; v0 += VC) {
+      floatx4 xa[VC], xb[VC];
 #pragma unroll
-    for (int v = 0; v < V; ++v) {
-      const int c = (v * 64 + lane) * 4;
-      const float sel = c < n ? 1.f : 0.f;
+      for (int u = 0; u < VC; ++u) {
+        const int c = ((v0 + u) * 64 + lane) * 4;
+        const int cc = (v0 + u < V && c < n) ? c : 0;  // n % 4 == 0 on this path; padded W rows are zero
+        xa[u] = *reinterpret_cast<const floatx4*>(X + ra * ld + cc);
+        xb[u] = *reinterpret_cast<const floatx4*>(X + rb * ld + cc);
+      }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float* w = &Ws[(c + q) * K];
+      for (int u = 0; u < VC; ++u) {
+        const int c = ((v0 + u) * 64 + lane) * 4;
+        const float sel = (v0 + u < V && c < n) ? 1.f : 0.f;
+        const int cw = v0 + u < V ? c : 0;
 #pragma unroll
-        for (int j = 0; j < K; ++j) {
-          acca[j] = fmaf(xa[v][q] * sel, w[j], acca[j]);
-          accb[j] = fmaf(xb[v][q] * sel, w[j], accb[j]);
+        for (int q = 0; q < 4; ++q) {
+          const float* w = &Ws[(cw + q) * K];
+#pragma unroll
+          for (int j = 0; j < K; ++j) {
+            acca[j] = fmaf(xa[u][q] * sel, w[j], acca[j]);
+            accb[j] = fmaf(xb[u][q] * sel, w[j], accb[j]);
+          }
         }
       }
     }

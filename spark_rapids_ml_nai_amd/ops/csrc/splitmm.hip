@@ -566,7 +566,7 @@ typedef __attribute__((address_space(1))) void* gbl_vptr;
 // tiled image.
 // PRIO: s_setprio(1) / (0) around every MFMA cluster: keeps hipcc from moving MFMAs across the
 // raw barriers into the load phase (cdna_hip_programming.md T5).
-template <bool TILED, int NP = 6, bool TOP2 = false, int WN_ = 4, bool PRIO = false, bool CAND = false>
+template <bool TILED, int NP = 6, bool TOP2 = false, int WN_ = 4, bool PRIO = false, bool CAND = false, int RING = 0>
 __global__ __launch_bounds__(WN_ * 128, WN_ == 4 ? 1 : 2) void nearest_centroid_split_glds_kernel(
     const unsigned short* __restrict__ XP, long m, long xrows, int kp, const unsigned short* __restrict__ CP, int k,
     long crows, const float* __restrict__ cnorm, unsigned long long* __restrict__ best, int n_ctiles,
@@ -589,9 +589,11 @@ __global__ __launch_bounds__(WN_ * 128, WN_ == 4 ? 1 : 2) void nearest_centroid_
   // NP = 1 (one fp16 plane per operand, 16 KiB stages): a k step is a third of a 3-product one,
   // so three steps share a barrier and the ring holds three such groups (9 stages, 144 KiB): the
   // loads of group g + 2 are issued while group g computes (two groups of HBM-latency cover)
-  constexpr int KPB = NP == 1 ? 3 : (NP == 3 && WN_ == 4 ? 2 : 1);  // k steps per barrier
-  constexpr int NG = NP == 1 && WN_ == 4 ? 3 : 2;                    // groups in the ring (2 x 72 KiB per CU at WN_ = 2)
-  constexpr int NS = KPB > 1 ? NG * KPB : 3;
+  // RING (fp16 filter probes, SRML_F16_RING): 10 * KPB + NG overrides the defaults below
+  constexpr int KPB = RING ? RING / 10 : NP == 1 ? 3 : (NP == 3 && WN_ == 4 ? 2 : 1);  // k steps per barrier
+  constexpr int NG = RING ? RING % 10 : NP == 1 && WN_ == 4 ? 3 : 2;  // groups in the ring (2 x 72 KiB per CU at WN_ = 2)
+  static_assert(!RING || (NP == 1 && KPB >= 1 && NG >= 2), "ring override is for the fp16 filter");
+  constexpr int NS = (KPB > 1 || RING) ? NG * KPB : 3;
   constexpr int STAGE = NPL * (BM + BN) * 16;  // elements: X planes [NPL][BM][16], then C planes [NPL][BN][16]
   __shared__ __attribute__((aligned(1024))) unsigned short lds[NS][STAGE];
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -685,7 +687,7 @@ __global__ __launch_bounds__(WN_ * 128, WN_ == 4 ? 1 : 2) void nearest_centroid_
       }
     }
   };
-  if constexpr (KPB == 1) {
+  if constexpr (KPB == 1 && !RING) {
     // 3-stage ring, one k step per barrier, two steps of load lead
     static_assert(CPW == 6, "the counted wait below leaves one step (CPW loads) in flight");
     issue(0, 0);
@@ -705,13 +707,14 @@ __global__ __launch_bounds__(WN_ * 128, WN_ == 4 ? 1 : 2) void nearest_centroid_
     // 3-product steps carry half the MFMA work (fp16 1-product steps a sixth): KPB k steps per
     // barrier on a 2 KPB-stage ring (group g computes from its KPB stages while group g + 1 lands
     // in the other KPB), so the barrier and the first fragment reads are paid once per KPB steps
-    // NG = 3: the newest group may stay in flight at the wait (counted vmcnt: the group after
-    // this one is full, else wait for everything)
+    // NG >= 3: the NG - 2 newest groups may stay in flight at the wait (counted vmcnt: those groups
+    // are full, else wait for everything)
 #pragma unroll
     for (int j = 0; j < (NG - 1) * KPB; ++j)
       if (j < nk) issue(j, j);
     for (int kt = 0; kt < nk; kt += KPB) {
-      if (NG == 3 && kt + 2 * KPB <= nk) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(KPB * CPW) : "memory");
+      if (NG >= 3 && kt + (NG - 1) * KPB <= nk)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"((NG - 2) * KPB * CPW) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // steps kt .. kt + KPB - 1 landed; every wave finished the previous group
 #pragma unroll
@@ -1071,13 +1074,29 @@ SRML_API int srml_nearest_centroid_f16_top2(const unsigned short* XP, long m, lo
 #define SRML_F16(WNN, PR, T)                                                                                      \
   hipLaunchKernelGGL((nearest_centroid_split_glds_kernel<true, 1, true, WNN, PR>), dim3((unsigned)nb), dim3(T), 0, \
                      stream, XP, m, xrows, kp, CP, k, crows, cnorm, keys, (int)ct, lob, cg, xnorm, dscale, xadd)
+  static const int ring = getenv("SRML_F16_RING") ? atoi(getenv("SRML_F16_RING")) : 0;
+#define SRML_F16R(RG)                                                                                               \
+  hipLaunchKernelGGL((nearest_centroid_split_glds_kernel<true, 1, true, 4, true, false, RG>), dim3((unsigned)nb),      \
+                     dim3(512), 0, stream, XP, m, xrows, kp, CP, k, crows, cnorm, keys, (int)ct, lob, cg, xnorm,       \
+                     dscale, xadd)
   if (f16_bn() == 128) {
     if (prio) SRML_F16(2, true, 256);
     else SRML_F16(2, false, 256);
+  } else if (ring == 23) {
+    SRML_F16R(23);
+  } else if (ring == 24) {
+    SRML_F16R(24);
+  } else if (ring == 42) {
+    SRML_F16R(42);
+  } else if (ring == 18) {
+    SRML_F16R(18);
+  } else if (ring == 25) {
+    SRML_F16R(25);
   } else {
     if (prio) SRML_F16(4, true, 512);
     else SRML_F16(4, false, 512);
   }
+#undef SRML_F16R
 #undef SRML_F16
   return srml_status();
 }
