@@ -171,12 +171,13 @@ def build_ivf(X: torch.Tensor, ids: torch.Tensor, nlist: int, seed: int = 1, ite
     ntrain = min(m, max(nlist * train_rows_per_list, 4 * nlist))
     T = X if ntrain == m else X.index_select(0, torch.randperm(m, generator=gen)[:ntrain].to(X.device))
     C = T.index_select(0, torch.randperm(T.shape[0], generator=gen)[:nlist].to(X.device)).float().clone()
-    tn = ops.row_sqnorm(T)
+    FT = ops.quantizer_planes(T) if nlist > 256 else None  # bucketing only: the fp16 filter's arg-min
+    tn = ops.row_sqnorm(T) if FT is None else None
     for _ in range(max(1, iters)):
-        lab, _d = ops.nearest_centroid(T, C, tn)
+        lab = ops.nearest_list(T, C, FT, tn)
         sums, counts = ops.cluster_sums(T, lab, nlist)
         C = torch.where(counts.view(-1, 1) > 0, (sums / counts.clamp_min(1).double().view(-1, 1)).float(), C)
-    lab, _ = ops.nearest_centroid(X, C)
+    lab = ops.nearest_list(X, C, ops.quantizer_planes(X) if nlist > 256 else None)
     order, off, _ = ops.label_sort(lab, nlist)  # stable: rows keep their order inside a list
     order = order.long()
     items = X.index_select(0, order).contiguous()

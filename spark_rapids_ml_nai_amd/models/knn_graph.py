@@ -76,9 +76,10 @@ def train_quantizer(X: torch.Tensor, nlist: int, seed: int, iters: int = 10,
     ntrain = min(m, max(nlist * train_rows_per_list, 4 * nlist))
     T = X if ntrain == m else X.index_select(0, torch.randperm(m, generator=gen, device=X.device)[:ntrain])
     C = T.index_select(0, torch.randperm(T.shape[0], generator=gen, device=X.device)[:nlist]).float().clone()
-    tn = ops.row_sqnorm(T)
+    FT = ops.quantizer_planes(T) if nlist > 256 else None  # bucketing only: the fp16 filter's arg-min
+    tn = ops.row_sqnorm(T) if FT is None else None
     for _ in range(max(1, iters)):
-        lab, _d = ops.nearest_centroid(T, C, tn)
+        lab = ops.nearest_list(T, C, FT, tn)
         sums, counts = ops.cluster_sums(T, lab, nlist)
         C = torch.where(counts.view(-1, 1) > 0, (sums / counts.clamp_min(1).double().view(-1, 1)).float(), C)
     return C.contiguous()
@@ -122,7 +123,7 @@ def knn_graph_ivf(X: torch.Tensor, k: int, nlist: Optional[int] = None, nprobe: 
     world = ctx.world_size if ctx is not None else 1
     if world > 1:
         C = ctx.comm.broadcast(C, 0)
-    lab, _ = ops.nearest_centroid(X, C)
+    lab = ops.nearest_list(X, C, ops.quantizer_planes(X) if nlist > 256 else None)
     order, off, _ = ops.label_sort(lab, nlist)  # stable counting sort by list
     order = order.long()
     counts = off[1:] - off[:-1]

@@ -611,6 +611,26 @@ def nearest_centroid_f16(F: F16Planes, C: torch.Tensor, approx: bool = False) ->
     return labels, dist
 
 
+def quantizer_planes(X: torch.Tensor) -> Optional[F16Planes]:
+    """fp16 filter planes of X for APPROXIMATE nearest-centroid labels (IVF coarse quantisers, whose
+    lists only need a good bucketing, not the exact arg-min), or None off the fp32 device path."""
+    if not X.is_cuda or X.dtype != torch.float32 or X.dim() != 2 or X.shape[1] < 16 or X.stride(1) != 1:
+        return None
+    mu = col_moments(X, need_sq=False)[0].div_(max(X.shape[0], 1)).float()
+    F = F16Planes(X, mu)
+    return F if F.ok else None
+
+
+def nearest_list(X: torch.Tensor, C: torch.Tensor, F: Optional[F16Planes] = None,
+                 xnorm: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """int32 labels of X's rows under centres C for bucketing: the fp16 filter's own arg-min (one fp16
+    MFMA product per pair, ``nearest_centroid_f16(approx=True)``) when ``F`` (planes of X) is given
+    and C has > 256 rows; else the fp32 MFMA search."""
+    if F is not None and C.shape[0] > 256:
+        return nearest_centroid_f16(F, C, approx=True)[0]
+    return nearest_centroid(X, C, xnorm)[0]
+
+
 def split_rows_per_launch(k: int) -> int:
     """Rows of one 256 x 256-tile split / fp16 filter launch: 512-thread blocks x ceil(k / 256)
     centre tiles per 256-row tile must stay within the 2^32 work-item grid of a dispatch."""
