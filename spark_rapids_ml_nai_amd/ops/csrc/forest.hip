@@ -111,18 +111,28 @@ __global__ __launch_bounds__(256) void rf_quantize_kernel(const float* __restric
   const int f = f0 + fl;
   const float* e = etab + fl * es;
   for (long r0 = (long)blockIdx.x * QROWS; r0 < min(m, (long)(blockIdx.x + 1) * QROWS); r0 += 256) {
-#pragma unroll 4
-    for (int p = 0; p < 32; ++p) {
-      const int rl = (t >> 5) + 8 * p;
-      const long r = r0 + rl;
-      unsigned char b = 0;
-      if (r < m && f < n) {
-        const float x = X[r * ld + f];
-        int lo = 0;
-        for (int step = ne2 >> 1; step > 0; step >>= 1) lo = (e[lo + step - 1] < x) ? lo + step : lo;
-        b = (unsigned char)lo;
+    // QU rows per thread at a time: their loads are issued together and their binary searches
+    // advance in lockstep (QU independent LDS-read chains instead of one dependent chain)
+    constexpr int QU = 8;
+    for (int p0 = 0; p0 < 32; p0 += QU) {
+      float x[QU];
+      int lo[QU];
+#pragma unroll
+      for (int u = 0; u < QU; ++u) {
+        const long r = r0 + (t >> 5) + 8 * (p0 + u);
+        x[u] = (r < m && f < n) ? X[r * ld + f] : 0.f;
+        lo[u] = 0;
       }
-      tile[fl][rl] = b;
+      for (int step = ne2 >> 1; step > 0; step >>= 1) {
+#pragma unroll
+        for (int u = 0; u < QU; ++u) lo[u] = (e[lo[u] + step - 1] < x[u]) ? lo[u] + step : lo[u];
+      }
+#pragma unroll
+      for (int u = 0; u < QU; ++u) {
+        const int rl = (t >> 5) + 8 * (p0 + u);
+        const long r = r0 + rl;
+        tile[fl][rl] = (r < m && f < n) ? (unsigned char)lo[u] : (unsigned char)0;
+      }
     }
     __syncthreads();
     // 32 features x 256 rows: each thread writes 4 consecutive bytes of one feature row

@@ -173,6 +173,10 @@ def main():
         umap_transform(Xu, Xs, torch.from_numpy(emb).to(dev), dict(n_neighbors=15, random_state=1))
         torch.cuda.synchronize()
         res["umap_transform_100k_x3000"] = {"ms": (time.perf_counter() - t0) * 1e3}
+    if want("quantize"):  # RF binning of the whole shard: 127 quantile edges per feature
+        e = torch.sort(torch.randn(a.n, 127, device=dev, generator=g), dim=1).values.contiguous()
+        t = timeit(lambda: ops.rf_quantize(X, e), 3)
+        res["rf_quantize"] = {"ms": t, "TB/s(read X)": gb / t}
     if want("rfhist"):
         # root level of a regression tree at the headline shape: in-bag rows x 1000 sampled features
         import numpy as np
