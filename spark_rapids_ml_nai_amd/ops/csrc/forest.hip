@@ -96,20 +96,22 @@ constexpr int QROWS = 1024;
 __global__ __launch_bounds__(256) void rf_quantize_kernel(const float* __restrict__ X, long m, int n, long ld,
                                                           const float* __restrict__ edges, int nedges, int ne2,
                                                           unsigned char* __restrict__ out) {
-  extern __shared__ float etab[];  // [32][ne2 + 1]
+  // edge table transposed, [ne2][32]: lane fl (feature f0 + fl) reads e[j * 32] of its own column, so
+  // the 32 lanes of a ds_read_b32 group always sit in 32 distinct banks whatever their search
+  // positions (the [32][ne2 + 1] layout met random bank conflicts from the second step on)
+  extern __shared__ float etab[];
   __shared__ unsigned char tile[32][256 + 4];
   const int f0 = blockIdx.y * 32;
   const int t = threadIdx.x;
-  const int es = ne2 + 1;
   for (int i = t; i < 32 * ne2; i += 256) {
     const int fl = i / ne2, j = i - fl * ne2;
     const int f = f0 + fl;
-    etab[fl * es + j] = (f < n && j < nedges) ? edges[(long)f * nedges + j] : INFINITY;
+    etab[j * 32 + fl] = (f < n && j < nedges) ? edges[(long)f * nedges + j] : INFINITY;
   }
   __syncthreads();
   const int fl = t & 31;
   const int f = f0 + fl;
-  const float* e = etab + fl * es;
+  const float* e = etab + fl;
   for (long r0 = (long)blockIdx.x * QROWS; r0 < min(m, (long)(blockIdx.x + 1) * QROWS); r0 += 256) {
     // QU rows per thread at a time: their loads are issued together and their binary searches
     // advance in lockstep (QU independent LDS-read chains instead of one dependent chain)
@@ -125,7 +127,7 @@ __global__ __launch_bounds__(256) void rf_quantize_kernel(const float* __restric
       }
       for (int step = ne2 >> 1; step > 0; step >>= 1) {
 #pragma unroll
-        for (int u = 0; u < QU; ++u) lo[u] = (e[lo[u] + step - 1] < x[u]) ? lo[u] + step : lo[u];
+        for (int u = 0; u < QU; ++u) lo[u] = (e[(lo[u] + step - 1) * 32] < x[u]) ? lo[u] + step : lo[u];
       }
 #pragma unroll
       for (int u = 0; u < QU; ++u) {
@@ -163,7 +165,7 @@ SRML_API int srml_rf_quantize_u8(const float* X, long m, int n, long ld, const f
   if (nedges < 0 || nedges > 255) return (int)hipErrorInvalidValue;
   int ne2 = 1;
   while (ne2 < nedges + 1) ne2 <<= 1;
-  const size_t lds = (size_t)32 * (ne2 + 1) * sizeof(float);
+  const size_t lds = (size_t)32 * ne2 * sizeof(float);
   dim3 grid(ceil_div(m, QROWS), ceil_div(n, 32));
   hipLaunchKernelGGL(rf_quantize_kernel, grid, dim3(256), lds, stream, X, m, n, ld, edges, nedges, ne2, out);
   return srml_status();
@@ -600,6 +602,38 @@ __global__ __launch_bounds__(256) void rf_interleave_kernel(const unsigned char*
   for (int q = 0; q < RB / 16; ++q) dst[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 }
 
+// Four rows per thread (m % 4 == 0): one dword load per feature brings the feature's bins of rows
+// r .. r + 3, a byte transpose in registers forms the four rows' records — a quarter of the load
+// instructions of one byte load per (row, feature)
+template <int RB>
+__global__ __launch_bounds__(256) void rf_interleave4_kernel(const unsigned char* __restrict__ bins, long m, int n,
+                                                             unsigned char* __restrict__ out) {
+  const long r = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
+  const int g = blockIdx.y;
+  if (r >= m) return;
+  unsigned w[4][RB / 4];
+#pragma unroll
+  for (int q = 0; q < RB / 4; ++q) {
+    unsigned v[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int f = RB * g + 4 * q + b;
+      v[b] = f < n ? *reinterpret_cast<const unsigned*>(bins + (long)f * m + r) : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)  // row r + i: byte i of each feature's dword
+      w[i][q] = ((v[0] >> (8 * i)) & 0xffu) | (((v[1] >> (8 * i)) & 0xffu) << 8) |
+                (((v[2] >> (8 * i)) & 0xffu) << 16) | (((v[3] >> (8 * i)) & 0xffu) << 24);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    uint4* dst = reinterpret_cast<uint4*>(out + rec_offset<RB>(g, r + i, m));
+#pragma unroll
+    for (int q = 0; q < RB / 16; ++q)
+      dst[q] = make_uint4(w[i][4 * q], w[i][4 * q + 1], w[i][4 * q + 2], w[i][4 * q + 3]);
+  }
+}
+
 // rb = record bytes (features per record): 32 (the 8-feature item kernel's layout) or 64
 SRML_API int srml_rf_interleave_u8(const unsigned char* bins, long m, int n, int rb, unsigned char* out,
                                    hipStream_t stream) {
@@ -608,6 +642,12 @@ SRML_API int srml_rf_interleave_u8(const unsigned char* bins, long m, int n, int
   if (rb != 32 && rb != 64) return -2;
   const int G = (n + rb - 1) / rb;
   if (G > 65535) return -2;
+  if ((m & 3) == 0 && (reinterpret_cast<uintptr_t>(bins) & 3) == 0) {
+    const dim3 grid4((unsigned)((m / 4 + 255) / 256), (unsigned)G);
+    if (rb == 32) hipLaunchKernelGGL(rf_interleave4_kernel<32>, grid4, dim3(256), 0, stream, bins, m, n, out);
+    else hipLaunchKernelGGL(rf_interleave4_kernel<64>, grid4, dim3(256), 0, stream, bins, m, n, out);
+    return srml_status();
+  }
   const dim3 grid((unsigned)((m + 255) / 256), (unsigned)G);
   if (rb == 32) hipLaunchKernelGGL(rf_interleave_kernel<32>, grid, dim3(256), 0, stream, bins, m, n, out);
   else hipLaunchKernelGGL(rf_interleave_kernel<64>, grid, dim3(256), 0, stream, bins, m, n, out);

@@ -947,3 +947,21 @@ def test_nearest_centroid_f16_approx_mode(gpu_device):
     clear = (top2[:, 1] - top2[:, 0]) > 2.0 * radius
     assert torch.equal(lab_a[clear].long(), D.argmin(1)[clear])
     assert (d_a.double() - top2[:, 0]).abs().max().item() <= radius.max().item() + 1e-6
+
+
+@pytest.mark.parametrize("m,n,rb", [(4096, 3000, 64), (1000, 70, 32), (1003, 130, 64), (20000, 64, 32)])
+def test_rf_interleave_record_layout(gpu_device, m, n, rb):
+    """Record layout from the feature-major bins (four-rows-per-thread kernel when m % 4 == 0, the
+    row-per-thread one otherwise) == the layout built on the host byte by byte."""
+    g = torch.Generator().manual_seed(m + n)
+    bins = torch.randint(0, 256, (n, m), generator=g, dtype=torch.uint8)
+    got = ops.rf_interleave(bins.to(gpu_device), rb).cpu().numpy()
+    G = (n + rb - 1) // rb
+    b = np.zeros((G * rb, m), dtype=np.uint8)
+    b[:n] = bins.numpy()
+    rec = b.reshape(G, rb, m).transpose(0, 2, 1)  # [group][row][rb]
+    for gi in range(G):  # record (g, r) at the kernel's byte offset (64-B records line-paired)
+        r = np.arange(m)
+        off = ((gi >> 1) * m + r) * 128 + (gi & 1) * 64 if rb == 64 else (gi * m + r) * rb
+        got_g = got[off[:, None] + np.arange(rb)[None, :]]
+        np.testing.assert_array_equal(got_g, rec[gi])
