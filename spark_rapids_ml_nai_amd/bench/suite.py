@@ -137,6 +137,9 @@ def model_evidence(name: str, model: Any) -> Dict[str, Any]:
             rf = model._model_attributes.get("refined_frac")
             if rf is not None:
                 ev["refined_frac"] = float(rf)
+            di = model._model_attributes.get("delta_iters")
+            if di is not None:
+                ev["delta_iters"] = int(di)
         elif name == "logistic_regression":
             ev["num_iters"] = int(model.num_iters)
             ev["objective"] = float(model.objective)

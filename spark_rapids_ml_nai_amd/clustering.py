@@ -155,9 +155,9 @@ class KMeans(KMeansClass, _Estimator, _KMeansParams):
 
 class KMeansModel(KMeansClass, _ModelWithPredictionCol, _KMeansParams):
     def __init__(self, cluster_centers_: List[List[float]], n_cols: int, dtype: str, n_iter: int = 0,
-                 refined_frac: Optional[float] = None) -> None:
+                 refined_frac: Optional[float] = None, delta_iters: Optional[int] = None) -> None:
         super().__init__(cluster_centers_=cluster_centers_, n_cols=n_cols, dtype=dtype, n_iter=n_iter,
-                         refined_frac=refined_frac)
+                         refined_frac=refined_frac, delta_iters=delta_iters)
         self.cluster_centers_ = cluster_centers_
         self.n_cols = n_cols
         self.dtype = dtype

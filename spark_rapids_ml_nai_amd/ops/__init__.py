@@ -841,6 +841,24 @@ def cluster_sums(X: torch.Tensor, labels: torch.Tensor, k: int) -> Tuple[torch.T
     return sums, off[1:] - off[:-1]
 
 
+def cluster_sums_rows(X: torch.Tensor, rows: torch.Tensor, labels: torch.Tensor, k: int
+                      ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """``cluster_sums(X[rows], labels, k)`` without the gathered copy: the rows are label-sorted and
+    the sorted-segment kernel reads them from X through the index list (the Lloyd loop's delta
+    update over the rows that changed cluster)."""
+    n = X.shape[1]
+    if not X.is_cuda or X.dtype != torch.float32 or deterministic():
+        return cluster_sums(X.index_select(0, rows.long()), labels, k)
+    X = _c(X)
+    lab = _c(labels.to(torch.int32))
+    perm, off, slab = label_sort(lab, k)
+    prow = _c(rows.to(torch.int32).index_select(0, perm.long()))
+    sums = torch.zeros((k, n), dtype=torch.float64, device=X.device)
+    native.call("srml_kmeans_accumulate_sorted_f32", X.data_ptr(), int(rows.shape[0]), n, X.stride(0),
+                prow.data_ptr(), slab.data_ptr(), sums.data_ptr(), native.stream(X.device))
+    return sums, off[1:] - off[:-1]
+
+
 # ------------------------------------------------------------------------------------------
 # Random forest primitives
 # ------------------------------------------------------------------------------------------

@@ -965,3 +965,23 @@ def test_rf_interleave_record_layout(gpu_device, m, n, rb):
         off = ((gi >> 1) * m + r) * 128 + (gi & 1) * 64 if rb == 64 else (gi * m + r) * rb
         got_g = got[off[:, None] + np.arange(rb)[None, :]]
         np.testing.assert_array_equal(got_g, rec[gi])
+
+
+def test_kmeans_delta_sums_match_full_sums(gpu_device, monkeypatch):
+    """Lloyd sums updated from the moved rows only (+x new cluster, -x old) give the same centres
+    as recomputing every iteration's sums from all rows."""
+    from spark_rapids_ml_nai_amd.models import kmeans as km
+    from spark_rapids_ml_nai_amd.parallel.context import PartitionDescriptor, WorkerContext
+
+    X = _rand(30000, 300, gpu_device, seed=71)
+    ctx = WorkerContext.single(gpu_device)
+    desc = PartitionDescriptor.build(ctx, X.shape[0], X.shape[1])
+    monkeypatch.setenv("SRML_KMEANS_SPLIT", "1")
+    out = {}
+    for frac in (0.2, -1.0):
+        monkeypatch.setattr(km, "DELTA_FRAC", frac)
+        out[frac] = km.kmeans_fit(X, desc, ctx, k=300, max_iter=12, tol=0.0, seed=5, init="random")
+    assert out[0.2]["delta_iters"] > 0 and out[-1.0]["delta_iters"] == 0
+    # the sorted-segment kernel folds fp32 block partials into fp64 sums, so two groupings of the same
+    # rows agree to fp32 rounding of the partials (~1e-7 of a coordinate), not bit for bit
+    np.testing.assert_allclose(out[0.2]["cluster_centers_"], out[-1.0]["cluster_centers_"], rtol=1e-5, atol=2e-6)
