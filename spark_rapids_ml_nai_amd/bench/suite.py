@@ -140,6 +140,9 @@ def model_evidence(name: str, model: Any) -> Dict[str, Any]:
             di = model._model_attributes.get("delta_iters")
             if di is not None:
                 ev["delta_iters"] = int(di)
+            ph = model._model_attributes.get("phase_s")
+            if ph is not None:  # rank 0's planes / seeding / Lloyd-loop seconds
+                ev["phase_s"] = {"prep": ph[0], "init": ph[1], "lloyd": ph[2]}
         elif name == "logistic_regression":
             ev["num_iters"] = int(model.num_iters)
             ev["objective"] = float(model.objective)

@@ -155,9 +155,10 @@ class KMeans(KMeansClass, _Estimator, _KMeansParams):
 
 class KMeansModel(KMeansClass, _ModelWithPredictionCol, _KMeansParams):
     def __init__(self, cluster_centers_: List[List[float]], n_cols: int, dtype: str, n_iter: int = 0,
-                 refined_frac: Optional[float] = None, delta_iters: Optional[int] = None) -> None:
+                 refined_frac: Optional[float] = None, delta_iters: Optional[int] = None,
+                 phase_s: Optional[List[float]] = None) -> None:
         super().__init__(cluster_centers_=cluster_centers_, n_cols=n_cols, dtype=dtype, n_iter=n_iter,
-                         refined_frac=refined_frac, delta_iters=delta_iters)
+                         refined_frac=refined_frac, delta_iters=delta_iters, phase_s=phase_s)
         self.cluster_centers_ = cluster_centers_
         self.n_cols = n_cols
         self.dtype = dtype

@@ -19,6 +19,7 @@ Initialisation:
 from __future__ import annotations
 
 import os
+import time
 
 from typing import Any, Dict, Optional, Tuple
 
@@ -177,10 +178,17 @@ def _use_split(X: torch.Tensor, k: int) -> bool:
     return need < 0.6 * free
 
 
+def _now(X: torch.Tensor) -> float:
+    if X.is_cuda:
+        torch.cuda.synchronize(X.device)
+    return time.perf_counter()
+
+
 def kmeans_fit(X: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext, k: int, max_iter: int, tol: float,
                seed: int, init: str = "scalable-k-means++", oversampling: float = 2.0, init_steps: int = 2,
                timer: Any = None) -> Dict[str, Any]:
     n = X.shape[1]
+    t_start = _now(X)
     # k > 256: 256 x 256 LDS-DMA kernel on the tiled plane layout (SRML_SPLIT_TILED=0: plain layout)
     tiled = k > 256 and os.environ.get("SRML_SPLIT_TILED", "1") == "1"
     use_split = _use_split(X, k)
@@ -208,6 +216,7 @@ def kmeans_fit(X: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext, k
         if F16 is None:
             xnorm_s = ops.row_sqnorm(X, mu)
     XP = ops.split_bf16x3(X, tiled=tiled, mu=mu) if use_split and F16 is None else None
+    t_prep = _now(X)
     if init in ("random",):
         C = init_random(X, desc, ctx, k, seed)
     elif init in ("scalable-k-means++", "k-means||", "k-means++"):
@@ -216,6 +225,7 @@ def kmeans_fit(X: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext, k
     else:
         raise ValueError("Unsupported init mode %s" % init)
     C = C.double()
+    t_init = _now(X)
     tol2 = float(tol) ** 2
     n_iter = 0
     inertia = 0.0
@@ -262,6 +272,7 @@ def kmeans_fit(X: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext, k
         if shift <= tol2:
             break
     del XP, F16
+    t_end = _now(X)
     return {
         "cluster_centers_": C.cpu().numpy(),  # ndarray: 3M-float .tolist() cost 40 ms per fit
         "n_cols": int(n),
@@ -269,6 +280,9 @@ def kmeans_fit(X: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext, k
         "n_iter": n_iter,
         # filter-and-refine Lloyd search: fraction of row assignments re-searched exactly
         "delta_iters": n_delta,  # iterations whose cluster sums were updated from the moved rows only
+        # rank-local phase times (s): planes / means, seeding, Lloyd loop (each ends on a device sync;
+        # the Lloyd loop syncs every iteration for its shift test anyway)
+        "phase_s": [round(t_prep - t_start, 4), round(t_init - t_prep, 4), round(t_end - t_init, 4)],
         "refined_frac": round((ops._CERTIFY_STATS["refined"] - st0["refined"]) /
                               max(1, ops._CERTIFY_STATS["rows"] - st0["rows"]), 4) if certified else None,
     }

@@ -730,7 +730,14 @@ def kmeanspp_gram(G: torch.Tensor, w: torch.Tensor, k: int, seed: int, trials: O
     L = max(1, min(L, KMEANSPP_MAX_TRIALS))
     if G.is_cuda and nc <= KMEANSPP_MAX_CANDIDATES:
         out = torch.empty(k, dtype=torch.int32, device=G.device)
-        native.call("srml_kmeanspp_gram", _c(G.double()).data_ptr(), nc, _c(w.double()).data_ptr(), int(k), L, seed,
+        Gd = _c(G.double())
+        ldg = nc
+        if nc % 4 and nc <= 4096 and L <= 8:  # the register kernel reads 4-candidate groups from 32-B aligned rows
+            ldg = nc + (-nc) % 4
+            Gp = torch.zeros((nc, ldg), dtype=torch.float64, device=G.device)
+            Gp[:, :nc] = Gd
+            Gd = Gp
+        native.call("srml_kmeanspp_gram", Gd.data_ptr(), nc, ldg, _c(w.double()).data_ptr(), int(k), L, seed,
                     out.data_ptr(), native.stream(G.device))
         return out.long()
     Gh = G.double().cpu().numpy()

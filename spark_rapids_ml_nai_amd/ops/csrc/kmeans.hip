@@ -15,6 +15,9 @@
 //   small k*n: block-private sums in LDS (ds_add_f32), flushed with fp64 global atomics;
 //   large k*n: wave-per-row fp32 global atomics, 256 contiguous bytes per atomic instruction
 //   (the full-rate atomic shape on MI355X).
+#include <cstdlib>
+#include <cstring>
+
 #include "common.h"
 
 #include "tile.h"
@@ -741,7 +744,7 @@ __device__ void kpp_sample(const double (*wv)[KPP_T], const double (&d2)[KPP_PER
 // centre 0 ~ w; every later centre draws L candidates ~ w_i d2_i and keeps the one that lowers
 // the potential sum_i w_i min(d2_i, ||c_i - cand||^2) the most (single-draw k-means++ merged two
 // of eight separated blobs in ~1 of 4 seeds). Distances from the Gram matrix G = C C^T.
-__global__ __launch_bounds__(KPP_T) void kmeanspp_gram_kernel(const double* __restrict__ G, int nc,
+__global__ __launch_bounds__(KPP_T) void kmeanspp_gram_kernel(const double* __restrict__ G, int nc, long ldg,
                                                               const double* __restrict__ w, int k, int L,
                                                               unsigned long long seed, int* __restrict__ out) {
   __shared__ double lds[KPP_T / 64];
@@ -761,7 +764,7 @@ __global__ __launch_bounds__(KPP_T) void kmeanspp_gram_kernel(const double* __re
     const int i = base + q;
     const bool ok = q < cnt;
     s_w[q][threadIdx.x] = ok ? w[i] : 0.0;
-    s_gii[q][threadIdx.x] = ok ? G[(long)i * nc + i] : 0.0;
+    s_gii[q][threadIdx.x] = ok ? G[(long)i * ldg + i] : 0.0;
     d2[q] = 1.0;  // the first draw is ~ w alone
   }
   if (threadIdx.x == 0) u[0] = uniform01(seed, 0);
@@ -772,8 +775,8 @@ __global__ __launch_bounds__(KPP_T) void kmeanspp_gram_kernel(const double* __re
   int c = picks[0] < 0 ? 0 : picks[0];
   if (threadIdx.x == 0) out[0] = c;
   for (int t = 1; t < k; ++t) {
-    const double gcc = G[(long)c * nc + c];
-    const double* gc = G + (long)c * nc;
+    const double gcc = G[(long)c * ldg + c];
+    const double* gc = G + (long)c * ldg;
 #pragma unroll
     for (int q = 0; q < KPP_PER; ++q) {
       const double dd = fmax(s_gii[q][threadIdx.x] + gcc - 2.0 * gc[min(base + q, nc - 1)], 0.0);
@@ -795,7 +798,7 @@ __global__ __launch_bounds__(KPP_T) void kmeanspp_gram_kernel(const double* __re
 #pragma unroll
         for (int jj = 0; jj < KPP_CHUNK; ++jj) {
           const int tj = picks[min(j0 + jj, L - 1)];
-          const double* gt = G + (long)tj * nc;
+          const double* gt = G + (long)tj * ldg;
           const double gtt = gt[tj];
           double a = 0.0;
 #pragma unroll
@@ -827,10 +830,217 @@ __global__ __launch_bounds__(KPP_T) void kmeanspp_gram_kernel(const double* __re
   }
 }
 
-SRML_API int srml_kmeanspp_gram(const double* G, int nc, const double* w, int k, int trials, unsigned long long seed,
-                                int* out, hipStream_t stream) {
+// Register-resident variant for nc <= 4096 candidates and <= 8 trials (k <= 1096): every thread
+// owns 4 candidates, issues the G-row loads of ALL trials of a pick at once (one memory latency
+// instead of one per chunk) and keeps them in VGPRs, so the winner's row updates d2 without being
+// read again; trial potentials are reduced by a transposing butterfly (10 double shuffles instead
+// of 8 full wave sums) and each wave finds the winner itself (no extra barrier); the draw's
+// uniforms are computed per lane and broadcast with readlane. Three block barriers per pick.
+constexpr int KPR_PER = 4;
+constexpr int KPR_LT = 8;
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffLL), l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+__global__ __launch_bounds__(KPP_T) void kmeanspp_gram_reg_kernel(const double* __restrict__ G, int nc, long ldg,
+                                                                  const double* __restrict__ w, int k, int L,
+                                                                  unsigned long long seed, int* __restrict__ out) {
+  __shared__ double s_wave[KPP_T / 64];
+  __shared__ double s_pot[KPP_T / 64][KPR_LT];
+  __shared__ int s_pick[2][KPR_LT];  // double-buffered by pick parity: read after the last barrier of a pick
+  __shared__ double s_w[KPR_PER][KPP_T];
+  __shared__ double s_gii[KPR_PER][KPP_T];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int base = tid * KPR_PER;
+  const int cnt = max(0, min(KPR_PER, nc - base));
+  double d2[KPR_PER];
+#pragma unroll
+  for (int q = 0; q < KPR_PER; ++q) {
+    const int i = min(base + q, nc - 1);
+    s_w[q][tid] = q < cnt ? w[i] : 0.0;
+    s_gii[q][tid] = q < cnt ? G[(long)i * ldg + i] : 0.0;
+    d2[q] = 1.0;  // the first draw is ~ w alone
+  }
+  // inverse-CDF draws of nd targets (uniforms seed/ctr0 + j) over p_q = w_q d2_q -> s_pick[pb][0..nd);
+  // returns the first pick (-1: no mass)
+  auto draw = [&](int nd, unsigned long long ctr0, int pb) -> int {
+    int* pick = s_pick[pb];
+    double loc = 0.0;
+#pragma unroll
+    for (int q = 0; q < KPR_PER; ++q) loc += q < cnt ? s_w[q][tid] * d2[q] : 0.0;
+    double x = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const double y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) s_wave[wid] = x;
+    if (tid < KPR_LT) pick[tid] = -1;
+    const double uj = uniform01(seed, ctr0 + (unsigned long long)(lane & (KPR_LT - 1)));
+    __syncthreads();
+    double wave_off = 0.0, total = 0.0;
+#pragma unroll
+    for (int v = 0; v < KPP_T / 64; ++v) {
+      const double s = s_wave[v];
+      if (v < wid) wave_off += s;
+      total += s;
+    }
+    const double excl = wave_off + x - loc;
+#pragma unroll
+    for (int j = 0; j < KPR_LT; ++j) {
+      if (j < nd) {
+        const double target = readlane_d(uj, j) * total;
+        if (total > 0.0 && excl <= target && target < excl + loc) {
+          double run = excl;
+          int hit = -1;
+#pragma unroll
+          for (int q = 0; q < KPR_PER; ++q) {
+            if (q < cnt) {
+              run += s_w[q][tid] * d2[q];
+              if (hit < 0 && target < run) hit = q;
+            }
+          }
+          pick[j] = base + (hit < 0 ? cnt - 1 : hit);  // exactly one owner (half-open ranges)
+        }
+      }
+    }
+    __syncthreads();
+    bool miss = false;
+#pragma unroll
+    for (int j = 0; j < KPR_LT; ++j) miss |= j < nd && pick[j] < 0;
+    if (total > 0.0 && miss) {  // block-uniform; rounding at the very top: last positive candidate
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < KPR_LT; ++j)
+        if (j < nd && pick[j] < 0 && loc > 0.0) atomicMax(&pick[j], base + cnt - 1);
+      __syncthreads();
+    }
+    return pick[0];
+  };
+  const int p0 = draw(1, 0, 0);
+#pragma unroll
+  for (int q = 0; q < KPR_PER; ++q) d2[q] = INFINITY;
+  int c = p0 < 0 ? 0 : p0;
+  if (tid == 0) out[0] = c;
+  // this thread's 4 candidates of row r (32-B aligned: ldg % 4 == 0; threads past nc read column 0..3)
+  const int rb = cnt > 0 ? base : 0;
+  auto row4 = [&](const double* r, double (&v)[KPR_PER]) {
+    const double2* r2 = reinterpret_cast<const double2*>(r + rb);
+    const double2 lo = r2[0], hi = r2[1];
+    v[0] = lo.x;
+    v[1] = lo.y;
+    v[2] = hi.x;
+    v[3] = hi.y;
+  };
+  auto update_d2 = [&](int cc) {  // d2 = min(d2, ||c_i - c_cc||^2) from row cc (cc block-uniform)
+    const double* gc = G + (long)cc * ldg;
+    const double gcc = gc[cc];
+    double v[KPR_PER];
+    row4(gc, v);
+#pragma unroll
+    for (int q = 0; q < KPR_PER; ++q) {
+      const double dd = fmax(s_gii[q][tid] + gcc - 2.0 * v[q], 0.0);
+      if (q < cnt) d2[q] = fmin(d2[q], dd);
+    }
+  };
+  update_d2(c);
+  for (int t = 1; t < k; ++t) {
+    const int pb = t & 1;
+    if (draw(L, (unsigned long long)t * KPP_TRIALS, pb) < 0) {  // all mass on chosen points: any candidate (block-uniform)
+      c = (int)(splitmix64(seed + 77 * t) % (unsigned long long)nc);
+      update_d2(c);
+      if (tid == 0) out[t] = c;
+      __syncthreads();  // s_wave reads of this pick done before the next draw writes them
+      continue;
+    }
+    const int* pick = s_pick[pb];
+    double g[KPR_LT][KPR_PER], gtt[KPR_LT];
+#pragma unroll
+    for (int j = 0; j < KPR_LT; ++j) {  // all trials' row reads in flight together
+      const int tj = __builtin_amdgcn_readfirstlane(pick[j < L ? j : 0]);  // uniform: scalar row base
+      const double* r = G + (long)tj * ldg;
+      gtt[j] = r[tj];
+      row4(r, g[j]);
+    }
+    // g becomes the trial distances in place (gtt dies here)
+#pragma unroll
+    for (int q = 0; q < KPR_PER; ++q) {
+      const double gq = s_gii[q][tid];
+#pragma unroll
+      for (int j = 0; j < KPR_LT; ++j) g[j][q] = fmax(gq + gtt[j] - 2.0 * g[j][q], 0.0);
+    }
+    double pot[KPR_LT];
+#pragma unroll
+    for (int j = 0; j < KPR_LT; ++j) pot[j] = 0.0;
+#pragma unroll
+    for (int q = 0; q < KPR_PER; ++q) {
+      const double wq = s_w[q][tid];
+#pragma unroll
+      for (int j = 0; j < KPR_LT; ++j)
+        if (q < cnt) pot[j] += wq * fmin(d2[q], g[j][q]);
+    }
+    // transposing butterfly: after xor 32 / 16 / 8 a lane holds trial j = (lane >> 3) & 7's partial
+    const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8;
+    double h4[4], h2[2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const double send = b5 ? pot[i] : pot[i + 4];
+      h4[i] = (b5 ? pot[i + 4] : pot[i]) + __shfl_xor(send, 32, 64);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const double send = b4 ? h4[i] : h4[i + 2];
+      h2[i] = (b4 ? h4[i + 2] : h4[i]) + __shfl_xor(send, 16, 64);
+    }
+    double h1 = (b3 ? h2[1] : h2[0]) + __shfl_xor(b3 ? h2[0] : h2[1], 8, 64);
+    h1 += __shfl_xor(h1, 4, 64);
+    h1 += __shfl_xor(h1, 2, 64);
+    h1 += __shfl_xor(h1, 1, 64);
+    if ((lane & 7) == 0) s_pot[wid][lane >> 3] = h1;
+    __syncthreads();
+    // every wave: lane = 8 v + j sums waves v and v + 8 of trial j, then over v, then arg-min over j
+    const int jj = lane & 7, vv = lane >> 3;
+    double tot = s_pot[vv][jj] + s_pot[vv + 8][jj];
+    tot += __shfl_xor(tot, 8, 64);
+    tot += __shfl_xor(tot, 16, 64);
+    tot += __shfl_xor(tot, 32, 64);
+    if (jj >= L) tot = INFINITY;
+    int bj = jj;
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) {
+      const double ot = __shfl_xor(tot, o, 64);
+      const int oj = __shfl_xor(bj, o, 64);
+      if (ot < tot || (ot == tot && oj < bj)) { tot = ot; bj = oj; }
+    }
+    const int best = __builtin_amdgcn_readfirstlane(bj);
+#pragma unroll
+    for (int j = 0; j < KPR_LT; ++j) {
+      if (j == best) {
+#pragma unroll
+        for (int q = 0; q < KPR_PER; ++q)
+          if (q < cnt) d2[q] = fmin(d2[q], g[j][q]);
+      }
+    }
+    c = __builtin_amdgcn_readfirstlane(pick[best]);
+    if (tid == 0) out[t] = c;
+  }
+}
+
+// G: nc x nc, row stride ldg >= nc; the register kernel needs ldg % 4 == 0 and a 32-B aligned G
+SRML_API int srml_kmeanspp_gram(const double* G, int nc, long ldg, const double* w, int k, int trials,
+                                unsigned long long seed, int* out, hipStream_t stream) {
   if (nc <= 0 || k <= 0) return 0;
-  if (nc > KPP_T * KPP_PER || trials < 1 || trials > KPP_TRIALS) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(kmeanspp_gram_kernel, dim3(1), dim3(KPP_T), 0, stream, G, nc, w, k, trials, seed, out);
+  if (nc > KPP_T * KPP_PER || trials < 1 || trials > KPP_TRIALS || ldg < nc) return (int)hipErrorInvalidValue;
+  const char* e = getenv("SRML_KPP_KERNEL");  // =block forces the chunked kernel (A/B; read per call)
+  const int mode = e && !strcmp(e, "block") ? 1 : 0;
+  if (mode == 0 && nc <= KPP_T * KPR_PER && trials <= KPR_LT && ldg % KPR_PER == 0 && ((uintptr_t)G & 31) == 0)
+    hipLaunchKernelGGL(kmeanspp_gram_reg_kernel, dim3(1), dim3(KPP_T), 0, stream, G, nc, ldg, w, k, trials, seed,
+                       out);
+  else
+    hipLaunchKernelGGL(kmeanspp_gram_kernel, dim3(1), dim3(KPP_T), 0, stream, G, nc, ldg, w, k, trials, seed, out);
   return srml_status();
 }

@@ -61,7 +61,7 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_mlogit_f32": (_P, _L, _I, _L, _P, _P, _P, _P, _I, _P, _P),
     "srml_mlogit_supported": (_I, _I),
     "srml_qn_step": (_P, _P),
-    "srml_kmeanspp_gram": (_P, _I, _P, _I, _I, ctypes.c_ulonglong, _P, _P),
+    "srml_kmeanspp_gram": (_P, _I, _L, _P, _I, _I, ctypes.c_ulonglong, _P, _P),
     "srml_qn_max_history": (),
     "srml_qn_args_size": (),
     "srml_nearest_centroid_f32": (_P, _L, _I, _L, _P, _I, _L, _P, _P, _P),

@@ -666,7 +666,7 @@ def test_parts_to_device(gpu_device, mode, src_dtype, dst, monkeypatch):
     assert got.dtype == dst and torch.equal(got, ref)
 
 
-@pytest.mark.parametrize("nc,k", [(300, 20), (4001, 1000), (8000, 64)])
+@pytest.mark.parametrize("nc,k", [(300, 20), (4001, 1000), (4093, 1096), (8000, 64)])
 def test_kmeanspp_gram_matches_host(gpu_device, nc, k):
     """Device k-means++ seeding draws the same centres as the numpy reference (same uniforms)."""
     g = torch.Generator().manual_seed(nc)
@@ -678,6 +678,23 @@ def test_kmeanspp_gram_matches_host(gpu_device, nc, k):
     assert got[0] == ref[0]
     assert (got == ref).float().mean().item() > 0.95  # prefix-sum order may flip a boundary draw
     assert len(set(got.tolist())) == k  # D^2 sampling never re-picks a chosen candidate
+
+
+@pytest.mark.parametrize("nc,k", [(1000, 300), (4001, 1000)])
+def test_kmeanspp_register_kernel_matches_block_kernel(gpu_device, monkeypatch, nc, k):
+    """The register-resident k-means++ kernel (nc <= 4096, <= 8 trials; padded row stride) draws the
+    same centres as the chunked block kernel on the same uniforms (only the reduction order of the
+    trial potentials differs)."""
+    g = torch.Generator().manual_seed(nc + 1)
+    C = torch.randn(nc, 24, generator=g, dtype=torch.float64) * torch.rand(nc, 1, generator=g, dtype=torch.float64)
+    w = torch.randint(1, 50, (nc,), generator=g).double().to(gpu_device)
+    G = (C @ C.T).to(gpu_device)
+    got = ops.kmeanspp_gram(G, w, k, 99).cpu()
+    monkeypatch.setenv("SRML_KPP_KERNEL", "block")
+    ref = ops.kmeanspp_gram(G, w, k, 99).cpu()
+    assert got[0] == ref[0]
+    assert (got == ref).float().mean().item() > 0.95
+    assert len(set(got.tolist())) == k
 
 
 @pytest.mark.parametrize("m,n,k", [(1024, 3000, 257), (70000, 200, 600)])
