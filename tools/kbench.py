@@ -99,6 +99,17 @@ def main():
                                        max(1, st["rows"] - st0["rows"]),
                                        "TFLOP/s(f16 issued)": 2 * a.m * a.k * a.n / t / 1e9}
         del F
+    if want("hgemm"):  # library fp16 GEMM of the filter's shape (rows x centres x 3008): attainable MFMA rate
+        A = X[:, :].half()
+        kp = 3008 if a.n == 3000 else a.n
+        A = torch.nn.functional.pad(A, (0, kp - a.n))
+        B = A[torch.randperm(a.m, device=dev, generator=g)[: a.k]].clone()
+        t = timeit(lambda: torch.mm(A, B.T), 3)
+        res["hgemm_f16_out_f16"] = {"ms": t, "TFLOP/s": 2 * a.m * a.k * kp / t / 1e9}
+        B2 = B[:, :].contiguous()
+        t = timeit(lambda: torch.mm(B2, A.T), 3)
+        res["hgemm_f16_transposed"] = {"ms": t, "TFLOP/s": 2 * a.m * a.k * kp / t / 1e9}
+        del A, B, B2
     if want("kpp"):  # greedy k-means++ over the k-means|| candidates (one block, k sequential steps)
         for nc in (4001, 8000):
             gk = torch.Generator().manual_seed(nc)
