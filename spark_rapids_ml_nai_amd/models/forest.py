@@ -85,20 +85,29 @@ def feature_subset_size(strategy: Any, n: int, n_trees: int, classification: boo
 
 
 def bin_edges(X: torch.Tensor, n_bins: int, ctx: WorkerContext, m_total: int, seed: int,
-              sample_rows: Optional[int] = None) -> torch.Tensor:
+              sample_rows: Optional[int] = None, host: Optional[torch.Tensor] = None) -> torch.Tensor:
     """(n, n_bins-1) fp32 quantile edges, identical on every rank (sampled rows all-gathered).
 
     Sample size follows Spark's ``findSplits`` (max(maxBins^2, 10000) rows over the whole dataset,
-    capped at the 32768 the per-feature LDS sort holds)."""
+    capped at the 32768 the per-feature LDS sort holds). ``host``: the page-locked source of a
+    streamed ingest — the same sampled rows are gathered on the host and sent ahead of the shard,
+    so the edges exist before the shard has landed."""
     m, n = X.shape
     if sample_rows is None:
         sample_rows = min(32768, max(n_bins * n_bins, 10000))
     g = torch.Generator(device="cpu")
     g.manual_seed(int(seed) * 7919 + ctx.rank)
     want = max(1, int(sample_rows * m // max(m_total, 1)))
-    if m > want:
+    if m > want and host is not None:
+        sel = torch.randperm(m, generator=g)[:want].sort().values
+        Sh = torch.empty((want, n), dtype=host.dtype, pin_memory=True)
+        torch.index_select(host, 0, sel, out=Sh)
+        S = Sh.to(X.device, non_blocking=True).float()
+    elif m > want:
         sel = torch.randperm(m, generator=g)[:want].sort().values.to(X.device)
         S = X.index_select(0, sel).float()
+    elif host is not None:
+        S = host.to(X.device, non_blocking=True).float()
     else:
         S = X.float()
     if ctx.world_size > 1:
@@ -461,12 +470,27 @@ def grow_tree(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: Wor
     return grow_forest(bins, edges_h, y, ctx, gen, p, S, regression, data_parallel, gen_boot, 1)[0]
 
 
-def quantize_features(X: torch.Tensor, n_bins: int, ctx: WorkerContext, m_total: int, seed: int
-                      ) -> Tuple[torch.Tensor, np.ndarray]:
+def quantize_features(X: torch.Tensor, n_bins: int, ctx: WorkerContext, m_total: int, seed: int,
+                      stream: Any = None) -> Tuple[torch.Tensor, np.ndarray]:
     """(feature-major uint8 bins, host fp64 edges) of the shard: the quantile binning every tree
-    of a fit shares (and every param map of a fitMultiple with the same maxBins / seed)."""
+    of a fit shares (and every param map of a fitMultiple with the same maxBins / seed).
+
+    ``stream`` (``ops.ingest.StreamedRows`` of a pinned shard still in flight): the edges come from
+    host-gathered sample rows and every row chunk is binned as soon as its DMA lands, so the
+    binning pass runs under the PCIe transfer instead of after it (same rows, same edges, same
+    bins as the in-memory path)."""
     if n_bins > 256:
         raise ValueError("maxBins > 256 is not supported (uint8 bins)")
+    host = getattr(stream, "host", None) if stream is not None else None
+    if host is not None and X.is_cuda and X.dtype == torch.float32 and host.dtype == torch.float32:
+        edges = bin_edges(X, n_bins, ctx, m_total, seed, host=host)
+        m, n = X.shape
+        bins = torch.empty((n, m), dtype=torch.uint8, device=X.device)
+        for r0, _r1, Xc in stream.chunks():
+            ops.rf_quantize(Xc, edges, out=bins, col0=r0)
+        return bins, edges.double().cpu().numpy()
+    if stream is not None:
+        stream.wait_all()
     edges = bin_edges(X, n_bins, ctx, m_total, seed)
     bins = ops.rf_quantize(X, edges)
     return bins, edges.double().cpu().numpy()

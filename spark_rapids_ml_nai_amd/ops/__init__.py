@@ -869,20 +869,27 @@ def cluster_sums_rows(X: torch.Tensor, rows: torch.Tensor, labels: torch.Tensor,
 # ------------------------------------------------------------------------------------------
 # Random forest primitives
 # ------------------------------------------------------------------------------------------
-def rf_quantize(X: torch.Tensor, edges: torch.Tensor) -> torch.Tensor:
-    """Feature-major uint8 bins (n, m): bin(x) = #edges[f] strictly below x. edges: (n, B-1) fp32."""
+def rf_quantize(X: torch.Tensor, edges: torch.Tensor, out: Optional[torch.Tensor] = None, col0: int = 0
+                ) -> torch.Tensor:
+    """Feature-major uint8 bins (n, m): bin(x) = #edges[f] strictly below x. edges: (n, B-1) fp32.
+    ``out`` (n, M) with ``col0``: the rows of X are rows col0 .. col0 + m of a larger shard (a
+    streamed-ingest chunk binned as it lands); returns ``out``."""
     m, n = X.shape
     ne = edges.shape[1]
-    if not X.is_cuda or X.dtype != torch.float32:
+    if out is None:
         out = torch.empty((n, m), dtype=torch.uint8, device=X.device)
+        col0 = 0
+    if out.shape[0] != n or out.stride(1) != 1 or col0 < 0 or col0 + m > out.shape[1]:
+        raise ValueError("rf_quantize: out must be (n, >= col0 + m) with unit column stride")
+    if not X.is_cuda or X.dtype != torch.float32:
         for f in range(n):
-            out[f] = torch.searchsorted(edges[f].contiguous().to(X.dtype), X[:, f].contiguous(), right=False).to(torch.uint8)
+            out[f, col0: col0 + m] = torch.searchsorted(edges[f].contiguous().to(X.dtype), X[:, f].contiguous(),
+                                                        right=False).to(torch.uint8)
         return out
     X = _c(X)
     e = _c(edges.to(torch.float32))
-    out = torch.empty((n, m), dtype=torch.uint8, device=X.device)
-    native.call("srml_rf_quantize_u8", X.data_ptr(), m, n, X.stride(0), e.data_ptr(), ne, out.data_ptr(),
-                native.stream(X.device))
+    native.call("srml_rf_quantize_u8_ld", X.data_ptr(), m, n, X.stride(0), e.data_ptr(), ne, out.data_ptr() + col0,
+                out.stride(0), native.stream(X.device))
     return out
 
 

@@ -243,6 +243,7 @@ class _RandomForestEstimator(_RandomForestClass, _EstimatorSupervised, _RandomFo
             # hyper-parameter batching: param maps with the same (maxBins, seed) share one quantile
             # binning of the shard (bin edges + uint8 matrix), the per-fit pass over X
             binned: Dict[Any, Any] = {}
+            streamed = inp.stream  # streamed ingest: the first binning consumes the row chunks as they land
             for mp in maps:
                 p = dict(params["cuml_init"], **mp)
                 mode = p.get("split_mode", "ensemble")
@@ -261,7 +262,8 @@ class _RandomForestEstimator(_RandomForestClass, _EstimatorSupervised, _RandomFo
                 seed = int(p["random_state"]) if p.get("random_state") is not None else 0
                 key = (int(p["n_bins"]), seed)
                 if key not in binned:
-                    binned[key] = quantize_features(X, key[0], ctx, inp.desc.m, seed)
+                    binned[key] = quantize_features(X, key[0], ctx, inp.desc.m, seed, stream=streamed)
+                    streamed = None  # the whole shard is ordered before everything queued after it
                 trees = fit_forest(X, y, ctx, inp.desc.m, p, n_local, classification, num_classes, data_parallel,
                                    rank_seed=seed * 1000003 + ctx.rank, binned=binned[key])
                 if not data_parallel and ctx.world_size > 1:
@@ -276,6 +278,7 @@ class _RandomForestEstimator(_RandomForestClass, _EstimatorSupervised, _RandomFo
                 outs.append(res)
             return outs if params["fit_multiple_params"] else outs[0]
 
+        _fit.streaming_ingest = True  # type: ignore[attr-defined]
         return _fit
 
 

@@ -430,3 +430,32 @@ def test_rf_sample_features_uniform_sorted(gpu_device):
     again = ops.rf_sample_features(C, n, nf, 12345, gpu_device).cpu()
     other = ops.rf_sample_features(C, n, nf, 12346, gpu_device).cpu()
     assert torch.equal(f, again) and not torch.equal(f, other)
+
+
+def _algorithm_s_np(C: int, n: int, nf: int, seed: int) -> np.ndarray:
+    """Knuth's Algorithm S with the kernel's counter-based draws, one node at a time in numpy."""
+    M = (1 << 64) - 1
+    out = np.zeros((C, nf), dtype=np.int32)
+    f_all = np.arange(n, dtype=np.uint64)
+    for c in range(C):
+        base = int(ops._mix64_np(np.array([(seed ^ int(ops._mix64_np(np.array([c + 1], dtype=np.uint64))[0])) & M],
+                                          dtype=np.uint64))[0])
+        u = (ops._mix64_np(np.uint64(base) + f_all) >> np.uint64(11)).astype(np.float64) * 2.0 ** -53
+        need = nf
+        for f in range(n):
+            if need == 0:
+                break
+            if u[f] * float(n - f) < float(need):
+                out[c, nf - need] = f
+                need -= 1
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C,n,nf", [(37, 3000, 1000), (9, 70, 9), (5, 64, 64), (6, 129, 1)])
+def test_rf_sample_features_matches_algorithm_s(gpu_device, C, n, nf):
+    """The wave-parallel selection sampling (64 features per step, integer thresholds resolved by a
+    scalar pass) is bit-identical to the sequential Algorithm S on the same draws."""
+    seed = 0x9E3779B97F4A7C15 ^ (C * n + nf)
+    got = ops.rf_sample_features(C, n, nf, seed, gpu_device).cpu().numpy()
+    np.testing.assert_array_equal(got, _algorithm_s_np(C, n, nf, seed))

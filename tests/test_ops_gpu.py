@@ -572,6 +572,32 @@ def test_streamed_ingest_scatter_stats(gpu_device):
     torch.testing.assert_close(sr.wait_all().cpu(), h)
 
 
+def test_streamed_rf_binning_matches_in_memory(gpu_device):
+    """RF binning under a streamed ingest (host-gathered sample rows, every row chunk quantised as
+    it lands, ``rf_quantize(out=, col0=)``) gives the same edges and bins as the in-memory path."""
+    from spark_rapids_ml_nai_amd.models.forest import quantize_features
+    from spark_rapids_ml_nai_amd.ops.ingest import StreamedRows
+    from spark_rapids_ml_nai_amd.parallel.context import WorkerContext
+
+    m, n = 60001, 70  # odd row count: the last chunk and the unaligned byte-store path
+    h = torch.empty((m, n), dtype=torch.float32, pin_memory=True)
+    g = torch.Generator().manual_seed(5)
+    h.copy_(torch.randn(m, n, generator=g) * torch.rand(n, generator=g) * 10)
+    h[:, 3] = torch.randint(0, 4, (m,), generator=g).float()  # heavy ties
+    ctx = WorkerContext.single(gpu_device)
+    bins_ref, edges_ref = quantize_features(torch.from_numpy(h.numpy()).to(gpu_device), 128, ctx, m, 11)
+    sr = StreamedRows(h.numpy(), gpu_device, torch.float32, chunk_bytes=1 << 20)
+    assert len(sr.bounds) > 10
+    bins, edges = quantize_features(sr.X, 128, ctx, m, 11, stream=sr)
+    np.testing.assert_array_equal(edges, edges_ref)
+    assert torch.equal(bins.cpu(), bins_ref.cpu())
+    # a chunk binned into the middle of a larger matrix leaves the other columns alone
+    out = torch.full((n, 1000), 255, dtype=torch.uint8, device=gpu_device)
+    ops.rf_quantize(sr.X[100:300], torch.from_numpy(edges).float().to(gpu_device), out=out, col0=501)
+    assert torch.equal(out[:, 501:701].cpu(), bins_ref[:, 100:300].cpu())
+    assert bool((out[:, :501] == 255).all()) and bool((out[:, 701:] == 255).all())
+
+
 @pytest.mark.parametrize("regression", [True, False])
 def test_rf_node_stats(gpu_device, regression):
     g = torch.Generator().manual_seed(3)
