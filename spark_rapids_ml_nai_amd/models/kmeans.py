@@ -179,8 +179,8 @@ def _use_split(X: torch.Tensor, k: int) -> bool:
 
 
 def _now(X: torch.Tensor) -> float:
-    if X.is_cuda:
-        torch.cuda.synchronize(X.device)
+    if X.is_cuda:  # this stream only: a device-wide sync would also wait for a streamed ingest's copies
+        torch.cuda.current_stream(X.device).synchronize()
     return time.perf_counter()
 
 
