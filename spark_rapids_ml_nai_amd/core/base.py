@@ -372,7 +372,9 @@ def _fit_worker(ctx: WorkerContext, payload: Tuple[HostPartition, Callable, Dict
     if (stream_ok and isinstance(hp.X, np.ndarray) and hp.X.ndim == 2 and hp.X.shape[0] > 0
             and hp.X.dtype == (np.float32 if float32 else np.float64) and hp.X.flags.c_contiguous
             and is_pinned(hp.X)):
-        streamed = StreamedRows(hp.X, ctx.device, dtype)
+        # the fit's preferred chunk (bytes) unless SRML_INGEST_CHUNK_MB overrides it
+        chunk_mb = 0 if "SRML_INGEST_CHUNK_MB" in os.environ else int(getattr(fit_fn, "ingest_chunk_mb", 0))
+        streamed = StreamedRows(hp.X, ctx.device, dtype, chunk_bytes=chunk_mb << 20)
         X = streamed.X
     elif stream_ok and isinstance(hp.X, ChunkedRows) and hp.X.shape[0] > 0:
         streamed = StreamedParts(hp.X, ctx.device, dtype)  # Spark batches: fill/DMA/compute pipelined

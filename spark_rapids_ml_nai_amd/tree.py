@@ -279,6 +279,9 @@ class _RandomForestEstimator(_RandomForestClass, _EstimatorSupervised, _RandomFo
             return outs if params["fit_multiple_params"] else outs[0]
 
         _fit.streaming_ingest = True  # type: ignore[attr-defined]
+        # binning trails each chunk by one quantise launch: fewer, larger DMA chunks (measured -3 ms
+        # per fit at 384 MB vs the 96 MB default, profiles/bench_r3_ingest_chunk_ab.txt)
+        _fit.ingest_chunk_mb = 384  # type: ignore[attr-defined]
         return _fit
 
 
