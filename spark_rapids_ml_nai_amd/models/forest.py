@@ -246,13 +246,61 @@ def _node_stats(yv: torch.Tensor, idx: torch.Tensor, wpos: torch.Tensor, bounds:
 HIST_BUDGET_BYTES = 1 << 30
 
 
+def _root_hist_streamed(pending: PendingBins, bins: torch.Tensor, idx: torch.Tensor, wpos: torch.Tensor,
+                        yv: torch.Tensor, c_start: np.ndarray, c_cnt: np.ndarray, feats: torch.Tensor, C: int, B: int,
+                        SH: int, regression: bool, fb: int, yscale: Optional[float]) -> torch.Tensor:
+    """Root-level histograms of C segments (rows ascending inside each) built chunk by chunk as the
+    streamed shard lands: every chunk is binned, then the items over that chunk's positions of every
+    segment add into one zeroed histogram. The item lists of all chunks are built and uploaded
+    before the first chunk is queued (no host read waits for the transfer)."""
+    dev = bins.device
+    m = bins.shape[1]
+    nf = feats.shape[1]
+    nfc = (nf + fb - 1) // fb
+    hist = torch.zeros((C, nf, B, SH), dtype=torch.float64 if regression else torch.int32, device=dev)
+    wy = ops.rf_hist_wy(idx, yv, None, wpos)
+    rows_at = torch.tensor([r0 for r0, _ in pending.bounds] + [m], dtype=idx.dtype, device=dev)
+    # P[j, c]: first position of segment j whose row is >= the start of chunk c
+    P = torch.stack([torch.searchsorted(idx[int(s0): int(s0) + int(cn)], rows_at)
+                     for s0, cn in zip(c_start, c_cnt)]).cpu().numpy().astype(np.int64) + c_start[:, None]
+    per_chunk = []
+    for ci in range(len(pending.bounds)):
+        lo, hi = P[:, ci], P[:, ci + 1]
+        cnt = hi - lo
+        rpi = int(min(WIDE_ROWS_MAX, max(ROWS_PER_ITEM, (int(cnt.sum()) * nfc) // 8192)))
+        rpi = (rpi + 511) // 512 * 512
+        nch = (cnt + rpi - 1) // rpi
+        tot_ch = int(nch.sum())
+        node_rep = np.repeat(np.arange(C), nch)
+        chunk = np.arange(tot_ch) - np.repeat(np.cumsum(nch) - nch, nch)
+        rb = lo[node_rep] + chunk * rpi
+        re = np.minimum(rb + rpi, hi[node_rep])
+        it = np.empty((tot_ch * nfc, 4), dtype=np.int32)  # feature-chunk-major, atomics only
+        it[:, 0] = np.tile(node_rep, nfc)
+        it[:, 1] = np.tile(rb, nfc)
+        it[:, 2] = np.tile(re, nfc)
+        it[:, 3] = np.repeat(np.arange(nfc, dtype=np.int32), tot_ch)
+        per_chunk.append(it)
+    off = np.cumsum([0] + [a.shape[0] for a in per_chunk])
+    items_all = torch.from_numpy(np.concatenate(per_chunk, 0)).to(dev)
+    for ci, _rows in enumerate(pending.chunks()):
+        if off[ci + 1] > off[ci]:
+            ops.rf_hist(bins, idx, yv, None, items_all[off[ci]: off[ci + 1]], feats, C, B, SH, regression,
+                        pos_weight=wpos, fb=fb, yscale=yscale, out=hist, wy=wy)
+    return hist
+
+
 def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: WorkerContext,
                 gen: torch.Generator, p: Dict[str, Any], S: int, regression: bool, data_parallel: bool,
-                gen_boot: Optional[torch.Generator], n_trees: int) -> List[Tree]:
+                gen_boot: Optional[torch.Generator], n_trees: int, pending: Optional[PendingBins] = None) -> List[Tree]:
     """Grow ``n_trees`` trees level-synchronously: every level of every tree is ONE histogram /
     split / route / partition pass over the concatenated (tree, node) segments, so the per-level
     launches and host round trips are amortised over the whole forest (cuML grows trees
-    concurrently on streams for the same reason; here they share one batched launch)."""
+    concurrently on streams for the same reason; here they share one batched launch).
+
+    ``pending``: a streamed shard's chunks not binned yet — the root level's histograms are then
+    built chunk by chunk right behind each chunk's binning, under the PCIe transfer (every item
+    accumulates with atomics into one zeroed histogram: the same sums, in another order)."""
     dev = bins.device
     n, m = bins.shape
     B = edges_h.shape[1] + 1
@@ -327,6 +375,11 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
         res_out: List[np.ndarray] = []
         res_feat: List[np.ndarray] = []
         res_sel: List[torch.Tensor] = []
+        streamed_root = (pending is not None and depth == 0 and cand.size <= group and dev.type == "cuda"
+                         and not deterministic())
+        if pending is not None and not streamed_root:
+            pending.finish()
+            pending = None
         for g0 in range(0, cand.size, group):
             cg = cand[g0: g0 + group]
             C = int(cg.size)
@@ -338,6 +391,10 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
                 # the item order below) and few 32-feature records (the record-layout gathers)
                 feats = ops.rf_sample_features(C, n, nf, call_seed ^ (depth * 1000003 + g0 * 7919 + 1), dev)
             c_start, c_cnt = bounds_h[cg], counts[cg]
+            if streamed_root:
+                hist = _root_hist_streamed(pending, bins, idx, wpos, yv, c_start, c_cnt, feats, C, B, SH, regression,
+                                           fb, yscale)
+                pending = None
             il = None
             fb_l, nfc_l, rpi_min, blocks = fb, nfc, ROWS_PER_ITEM, 8192
             if use_il and float(c_cnt.mean()) < IL_DENSITY * m:
@@ -377,12 +434,14 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
                 it[:, 1] = np.repeat(rb, nfc_l)
                 it[:, 2] = np.repeat(re, nfc_l)
                 it[:, 3] = np.tile(np.arange(nfc_l), tot_ch) | np.repeat(single, nfc_l)
-            items_t = torch.from_numpy(it).to(dev, non_blocking=False)
-            excl = {"multi_nodes": torch.from_numpy(np.nonzero(nch != 1)[0]).to(dev)} if dev.type == "cuda" else None
-            hist = ops.rf_hist(bins, idx, yv, None, items_t, feats, C, B, SH, regression, pos_weight=wpos, fb=fb_l,
-                               yscale=yscale, exclusive=excl, bins_il=il, wide=il is not None and fb_l == wide_fb,
-                               rec_bytes=WIDE_REC_BYTES if wide_fb else 32,
-                               packed_scale=pack_scale if fb_l == wide_fb else None)
+            if not streamed_root:
+                items_t = torch.from_numpy(it).to(dev, non_blocking=False)
+                excl = ({"multi_nodes": torch.from_numpy(np.nonzero(nch != 1)[0]).to(dev)}
+                        if dev.type == "cuda" else None)
+                hist = ops.rf_hist(bins, idx, yv, None, items_t, feats, C, B, SH, regression, pos_weight=wpos,
+                                   fb=fb_l, yscale=yscale, exclusive=excl, bins_il=il,
+                                   wide=il is not None and fb_l == wide_fb, rec_bytes=WIDE_REC_BYTES if wide_fb else 32,
+                                   packed_scale=pack_scale if fb_l == wide_fb else None)
             if data_parallel:
                 ctx.comm.allreduce(hist)
             out, _ = ops.rf_best_split(hist, B, SH, regression, crit, min_leaf, min_gain)
@@ -470,25 +529,56 @@ def grow_tree(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: Wor
     return grow_forest(bins, edges_h, y, ctx, gen, p, S, regression, data_parallel, gen_boot, 1)[0]
 
 
+class PendingBins:
+    """Row chunks of a streamed shard whose bins are not computed yet. ``chunks()`` queues each
+    chunk's quantise pass behind its DMA and yields the chunk's row range, so per-chunk consumers
+    (the root-level histograms) interleave with the transfer; ``finish()`` bins whatever is left.
+    Nothing is queued before the first ``chunks()`` step, so host reads issued until then do not
+    wait for the transfer."""
+
+    def __init__(self, stream: Any, edges: torch.Tensor, bins: torch.Tensor) -> None:
+        self.bounds = list(stream.bounds)
+        self._it = stream.chunks()
+        self._edges = edges
+        self._bins = bins
+        self.done = False
+
+    def chunks(self) -> Any:
+        for r0, r1, Xc in self._it:
+            ops.rf_quantize(Xc, self._edges, out=self._bins, col0=r0)
+            yield r0, r1
+        self.done = True
+
+    def finish(self) -> None:
+        if not self.done:
+            for _ in self.chunks():
+                pass
+
+
 def quantize_features(X: torch.Tensor, n_bins: int, ctx: WorkerContext, m_total: int, seed: int,
-                      stream: Any = None) -> Tuple[torch.Tensor, np.ndarray]:
+                      stream: Any = None, defer: bool = False) -> Tuple[Any, ...]:
     """(feature-major uint8 bins, host fp64 edges) of the shard: the quantile binning every tree
     of a fit shares (and every param map of a fitMultiple with the same maxBins / seed).
 
     ``stream`` (``ops.ingest.StreamedRows`` of a pinned shard still in flight): the edges come from
     host-gathered sample rows and every row chunk is binned as soon as its DMA lands, so the
     binning pass runs under the PCIe transfer instead of after it (same rows, same edges, same
-    bins as the in-memory path)."""
+    bins as the in-memory path). ``defer`` (streamed only): return (bins, edges, PendingBins) with
+    the chunks not yet binned — the caller consumes them (or calls ``finish()``) before reading
+    the bins."""
     if n_bins > 256:
         raise ValueError("maxBins > 256 is not supported (uint8 bins)")
     host = getattr(stream, "host", None) if stream is not None else None
     if host is not None and X.is_cuda and X.dtype == torch.float32 and host.dtype == torch.float32:
         edges = bin_edges(X, n_bins, ctx, m_total, seed, host=host)
+        edges_h = edges.double().cpu().numpy()  # waits for the sample only: no chunk work is queued yet
         m, n = X.shape
         bins = torch.empty((n, m), dtype=torch.uint8, device=X.device)
-        for r0, _r1, Xc in stream.chunks():
-            ops.rf_quantize(Xc, edges, out=bins, col0=r0)
-        return bins, edges.double().cpu().numpy()
+        pending = PendingBins(stream, edges, bins)
+        if defer:
+            return bins, edges_h, pending
+        pending.finish()
+        return bins, edges_h
     if stream is not None:
         stream.wait_all()
     edges = bin_edges(X, n_bins, ctx, m_total, seed)
@@ -502,7 +592,8 @@ def fit_forest(X: torch.Tensor, y: torch.Tensor, ctx: WorkerContext, m_total: in
     m, n = X.shape
     n_bins = int(p["n_bins"])
     seed = int(p["random_state"]) if p.get("random_state") is not None else 0
-    bins, edges_h = binned if binned is not None else quantize_features(X, n_bins, ctx, m_total, seed)
+    bins, edges_h, *rest = binned if binned is not None else quantize_features(X, n_bins, ctx, m_total, seed)
+    pending = rest[0] if rest else None  # streamed chunks not binned yet: the first batch's root level bins them
     S = num_classes if classification else 3
     # feature-subset RNG: shared by all ranks in data-parallel mode (same trees everywhere);
     # bootstrap RNG: always rank-specific (each rank bags its own rows)
@@ -515,8 +606,12 @@ def fit_forest(X: torch.Tensor, y: torch.Tensor, ctx: WorkerContext, m_total: in
     per_batch = max(1, int((4 << 30) // max(8 * m, 1)))
     for t0 in range(0, n_trees_local, per_batch):
         nt = min(per_batch, n_trees_local - t0)
-        for t in grow_forest(bins, edges_h, y, ctx, gen, p, S, not classification, data_parallel, gen_boot, nt):
+        for t in grow_forest(bins, edges_h, y, ctx, gen, p, S, not classification, data_parallel, gen_boot, nt,
+                             pending=pending):
             trees.append(t.to_dict())
+        if pending is not None:
+            pending.finish()
+            pending = None
     return trees
 
 

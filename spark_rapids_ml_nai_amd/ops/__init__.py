@@ -977,12 +977,25 @@ def rf_il_useful(n: int, nf: int, fb: int) -> bool:
     return span / 32.0 + 1.0 <= fb / 2.0
 
 
+def rf_hist_wy(idx: torch.Tensor, label: torch.Tensor, wcnt: Optional[torch.Tensor] = None,
+               pos_weight: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """(weight, label) fp32 pairs in ``idx`` order: the histogram kernels' contiguous row stream."""
+    rows = idx.long()
+    if pos_weight is not None:
+        wv = pos_weight.float()
+    else:
+        wv = wcnt[rows].float() if wcnt is not None else torch.ones(rows.shape[0], dtype=torch.float32,
+                                                                    device=idx.device)
+    return torch.stack([wv, label[rows].float()], 1).contiguous()
+
+
 def rf_hist(bins: torch.Tensor, idx: torch.Tensor, label: torch.Tensor, wcnt: Optional[torch.Tensor],
             items: torch.Tensor, node_feats: torch.Tensor, nodes: int, B: int, S: int,
             regression: bool, pos_weight: Optional[torch.Tensor] = None, fb: Optional[int] = None,
             yscale: Optional[float] = None, exclusive: Optional[Dict[str, torch.Tensor]] = None,
             bins_il: Optional[torch.Tensor] = None, wide: bool = False, rec_bytes: int = 32,
-            packed_scale: Optional[float] = None) -> torch.Tensor:
+            packed_scale: Optional[float] = None, out: Optional[torch.Tensor] = None,
+            wy: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Per-(node, feature slot, bin) statistics: uint32 class counts or fp64 (count, sum[, sumsq]).
     Weights: per row (``wcnt``, indexed by row id) or per position of ``idx`` (``pos_weight``).
     ``items`` rows are (node, row_begin, row_end, feature_chunk) with chunks of ``fb`` features
@@ -992,7 +1005,12 @@ def rf_hist(bins: torch.Tensor, idx: torch.Tensor, label: torch.Tensor, wcnt: Op
     records of ``rec_bytes`` (the value ``bins_il`` was built with). ``packed_scale`` (wide
     regression, not deterministic): one u64 LDS cell per (feature, bin) holding the weighted count
     and the sum of w * rint(y * packed_scale), packed_scale = 2^22 / max|y| (``rf_pack_scale``);
-    the caller keeps the weights of one item <= 2^20."""
+    the caller keeps the weights of one item <= 2^20. ``out``: a zeroed / partly accumulated
+    histogram the items ADD into (no single-chunk stores: ``exclusive`` must be None) — a histogram
+    built over several launches, e.g. one per streamed row chunk; ``wy``: the (weight, label) pairs
+    in ``idx`` order from an earlier call (``rf_hist_wy``)."""
+    if out is not None and (exclusive is not None or (regression and deterministic())):
+        raise ValueError("rf_hist(out=): accumulating launches need atomics (no exclusive / fixed-point mode)")
     if wide and fb is None:
         fb = rf_hist_fb_wide(B, S, regression)
     fb = rf_hist_fb(B, S, regression) if fb is None else int(fb)
@@ -1000,7 +1018,11 @@ def rf_hist(bins: torch.Tensor, idx: torch.Tensor, label: torch.Tensor, wcnt: Op
     nf = node_feats.shape[1]
     dev = bins.device
     hdt = torch.float64 if regression else torch.int32
-    if not bins.is_cuda or items.shape[0] == 0:
+    if out is not None:
+        hist = out
+        if items.shape[0] == 0:
+            return hist
+    elif not bins.is_cuda or items.shape[0] == 0:
         hist = torch.zeros((nodes, nf, B, S), dtype=hdt, device=dev)
         if items.shape[0] == 0:
             return hist
@@ -1034,13 +1056,8 @@ def rf_hist(bins: torch.Tensor, idx: torch.Tensor, label: torch.Tensor, wcnt: Op
                     flat = b * S + y.long()
                     hist[node, j].view(-1).index_add_(0, flat, w.to(torch.int32))
         return hist
-    # compact (weight, label) into idx order once: contiguous loads in the row stream
-    rows = idx.long()
-    if pos_weight is not None:
-        wv = pos_weight.float()
-    else:
-        wv = wcnt[rows].float() if wcnt is not None else torch.ones(rows.shape[0], dtype=torch.float32, device=dev)
-    wy = torch.stack([wv, label[rows].float()], 1).contiguous()
+    if wy is None:
+        wy = rf_hist_wy(idx, label, wcnt, pos_weight)
     if regression:
         if S != 2:
             raise ValueError("device regression histograms carry (count, sum): S must be 2")

@@ -262,10 +262,12 @@ class _RandomForestEstimator(_RandomForestClass, _EstimatorSupervised, _RandomFo
                 seed = int(p["random_state"]) if p.get("random_state") is not None else 0
                 key = (int(p["n_bins"]), seed)
                 if key not in binned:
-                    binned[key] = quantize_features(X, key[0], ctx, inp.desc.m, seed, stream=streamed)
+                    binned[key] = quantize_features(X, key[0], ctx, inp.desc.m, seed, stream=streamed,
+                                                    defer=True)
                     streamed = None  # the whole shard is ordered before everything queued after it
                 trees = fit_forest(X, y, ctx, inp.desc.m, p, n_local, classification, num_classes, data_parallel,
                                    rank_seed=seed * 1000003 + ctx.rank, binned=binned[key])
+                binned[key] = binned[key][:2]  # its pending chunks (if any) are binned by now
                 if not data_parallel and ctx.world_size > 1:
                     # forests of peer ranks of this same job (numpy node arrays), device all-gather
                     import pickle

@@ -659,6 +659,44 @@ def test_rf_hist_fb_matches_library(gpu_device):
                 assert int(lib.srml_rf_hist_wide_fb(B, S, int(reg))) == ops.rf_hist_fb_wide(B, S, reg), (B, S, reg)
 
 
+@pytest.mark.parametrize("regression", [False, True])
+def test_rf_streamed_root_level_matches_in_memory(gpu_device, monkeypatch, regression):
+    """Forests on a pinned shard with the streamed ingest (chunks binned as they land, root-level
+    histograms accumulated chunk by chunk) vs the in-memory path: identical classifier trees (exact
+    integer counts); regressor trees of the same shape and predictions (fp64 sums in another order)."""
+    from spark_rapids_ml_nai_amd import DataFrame
+    from spark_rapids_ml_nai_amd.bench import datagen
+    from spark_rapids_ml_nai_amd.classification import RandomForestClassifier
+    from spark_rapids_ml_nai_amd.regression import RandomForestRegressor
+
+    g = torch.Generator(device=gpu_device).manual_seed(3)
+    m, n = 60000, 48
+    X = torch.randn(m, n, device=gpu_device, generator=g)
+    score = X[:, :6].sum(1) + 0.3 * torch.randn(m, device=gpu_device, generator=g)
+    y = (score if regression else (score > 0).float() + (score > 1.5).float()).double().cpu().numpy()
+    Xh = datagen.to_pinned_numpy(X)
+    est = (RandomForestRegressor if regression else RandomForestClassifier)(numTrees=6, maxDepth=7, maxBins=64,
+                                                                           seed=5)
+    monkeypatch.setenv("SRML_INGEST_CHUNK_MB", "1")  # ~48 chunks
+    monkeypatch.setenv("SRML_STREAM_INGEST", "1")
+    a = est.fit(DataFrame.from_numpy(Xh, y))
+    monkeypatch.setenv("SRML_STREAM_INGEST", "0")
+    b = est.fit(DataFrame.from_numpy(Xh, y))
+    ta, tb = a._trees, b._trees
+    assert len(ta) == len(tb) == 6
+    for u, v in zip(ta, tb):
+        assert np.asarray(u["feature"]).shape == np.asarray(v["feature"]).shape
+        if not regression:
+            np.testing.assert_array_equal(np.asarray(u["feature"]), np.asarray(v["feature"]))
+            np.testing.assert_array_equal(np.asarray(u["threshold"]), np.asarray(v["threshold"]))
+    pa = a.transform(DataFrame.from_numpy(Xh[:5000], y[:5000])).to_numpy("prediction")
+    pb = b.transform(DataFrame.from_numpy(Xh[:5000], y[:5000])).to_numpy("prediction")
+    if regression:
+        assert np.mean(np.abs(pa - pb) <= 1e-6 * (1 + np.abs(pb))) > 0.99
+    else:
+        np.testing.assert_array_equal(pa, pb)
+
+
 @pytest.mark.parametrize("classes,bins", [(20, 128), (12, 256), (32, 256)])
 def test_rf_many_classes(gpu_device, classes, bins):
     """Histograms wider than the default 8-feature slab: fewer features per item."""
