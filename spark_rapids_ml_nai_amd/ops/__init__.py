@@ -979,7 +979,15 @@ def rf_il_useful(n: int, nf: int, fb: int) -> bool:
 
 def rf_hist_wy(idx: torch.Tensor, label: torch.Tensor, wcnt: Optional[torch.Tensor] = None,
                pos_weight: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """(weight, label) fp32 pairs in ``idx`` order: the histogram kernels' contiguous row stream."""
+    """(weight, label) fp32 pairs in ``idx`` order: the histogram kernels' contiguous row stream
+    (device: one ``srml_rf_pack_wy`` pass)."""
+    if (idx.is_cuda and pos_weight is not None and wcnt is None and idx.dtype == torch.int32
+            and pos_weight.dtype == torch.float32 and label.dtype == torch.float32):
+        P = idx.shape[0]
+        wy = torch.empty((P, 2), dtype=torch.float32, device=idx.device)
+        native.call("srml_rf_pack_wy", _c(idx).data_ptr(), _c(pos_weight).data_ptr(), _c(label).data_ptr(), P,
+                    wy.data_ptr(), native.stream(idx.device))
+        return wy
     rows = idx.long()
     if pos_weight is not None:
         wv = pos_weight.float()

@@ -1163,6 +1163,21 @@ __global__ __launch_bounds__(PS_T) void rf_boot_scatter_kernel(long N, long m, u
 // least srml_rf_bootstrap_ws(T, m) u64
 SRML_API long srml_rf_bootstrap_ws(int T, long m) { return ((long)T * m + PS_B - 1) / PS_B + 1; }
 
+// (weight, label) pairs in position order, the histogram kernels' row stream: wy[i] = (w[i], y[idx[i]])
+// in one pass (replaces a gather, two conversions and a stack per tree level)
+__global__ __launch_bounds__(256) void rf_pack_wy_kernel(const int* __restrict__ idx, const float* __restrict__ w,
+                                                         const float* __restrict__ y, long P, float2* __restrict__ wy) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i < P) wy[i] = make_float2(w[i], y[idx[i]]);
+}
+
+SRML_API int srml_rf_pack_wy(const int* idx, const float* w, const float* y, long P, float* wy, hipStream_t stream) {
+  if (P <= 0) return 0;
+  hipLaunchKernelGGL(rf_pack_wy_kernel, dim3((unsigned)ceil_div(P, 256)), dim3(256), 0, stream, idx, w, y, P,
+                     reinterpret_cast<float2*>(wy));
+  return srml_status();
+}
+
 SRML_API int srml_rf_bootstrap(int T, long m, double rate, unsigned long long seed, int* idx, float* w,
                                long long* tbounds, unsigned long long* ws, hipStream_t stream) {
   if (T <= 0 || m <= 0) return 0;

@@ -119,6 +119,7 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_cd_gram_f64": (_P, _I, _L, _P, _P, _P, _P, _I, _D, _P, _P),
     "srml_rf_quantize_u8": (_P, _L, _I, _L, _P, _I, _P, _P),
     "srml_rf_quantize_u8_ld": (_P, _L, _I, _L, _P, _I, _P, _L, _P),
+    "srml_rf_pack_wy": (_P, _P, _P, _L, _P, _P),
     "srml_rf_quantiles_f32": (_P, _I, _I, _I, _P, _P),
     "srml_rf_hist": (_P, _L, _P, _P, _P, _I, _P, _I, _I, _I, _I, _D, _I, _P, _P, _I, _P),
     "srml_rf_interleave_u8": (_P, _L, _I, _I, _P, _P),

@@ -659,6 +659,17 @@ def test_rf_hist_fb_matches_library(gpu_device):
                 assert int(lib.srml_rf_hist_wide_fb(B, S, int(reg))) == ops.rf_hist_fb_wide(B, S, reg), (B, S, reg)
 
 
+def test_rf_pack_wy_matches_gather(gpu_device):
+    """One-pass (weight, label) packing in position order == the gather + stack it replaces."""
+    g = torch.Generator().manual_seed(9)
+    m, P = 5000, 123457
+    idx = torch.randint(0, m, (P,), generator=g, dtype=torch.int32)
+    w = torch.randint(1, 6, (P,), generator=g).float()
+    y = torch.randn(m, generator=g)
+    got = ops.rf_hist_wy(idx.to(gpu_device), y.to(gpu_device), None, w.to(gpu_device)).cpu()
+    assert torch.equal(got, torch.stack([w, y[idx.long()]], 1))
+
+
 @pytest.mark.parametrize("regression", [False, True])
 def test_rf_streamed_root_level_matches_in_memory(gpu_device, monkeypatch, regression):
     """Forests on a pinned shard with the streamed ingest (chunks binned as they land, root-level
