@@ -598,8 +598,13 @@ def nearest_centroid_f16(F: F16Planes, C: torch.Tensor, approx: bool = False) ->
             rq = rows[q0: q0 + nq]
             rp = max(256, (nq + 255) // 256 * 256)
             Pr = torch.empty((rp // 256, F.kp // 16, 256, 16), dtype=torch.float16, device=dev)
-            native.call("srml_split_f16_tiled_centered_rows", X.data_ptr(), X.stride(0), rq.data_ptr(), nq, F.n,
-                        F.mu.data_ptr(), F.kp, rp, F.scale, Pr.data_ptr(), scratch.data_ptr(), st)
+            if F.P is not None and os.environ.get("SRML_F16_GATHER", "plane") == "plane":
+                # the flagged rows' slots of the filter's own plane (32 B per k step, no re-conversion)
+                native.call("srml_f16_plane_gather_rows", F.P.data_ptr(), F.rows_pad, F.kp, rq.data_ptr(), nq, rp,
+                            Pr.data_ptr(), st)
+            else:
+                native.call("srml_split_f16_tiled_centered_rows", X.data_ptr(), X.stride(0), rq.data_ptr(), nq, F.n,
+                            F.mu.data_ptr(), F.kp, rp, F.scale, Pr.data_ptr(), scratch.data_ptr(), st)
             xr = F.xnorm.index_select(0, rq.long())
             native.call("srml_nearest_centroid_f16_cand", Pr.data_ptr(), nq, rp, F.kp, CP.data_ptr(), k, crows,
                         cn.data_ptr(), cg.data_ptr(), xr.data_ptr(), dscale, xadd, thr[q0:].data_ptr(),

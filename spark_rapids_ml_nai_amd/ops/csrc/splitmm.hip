@@ -1134,6 +1134,48 @@ SRML_API int srml_split_f16_tiled_centered_rows(const float* X, long ld, const i
   return srml_status();
 }
 
+// Gather rows of an existing tiled fp16 plane (the filter's X plane) into a new tiled plane: row
+// r of the output = row ridx[r] of the source, bit-identical to converting X[ridx[r]] again but
+// reading 32 B of fp16 per (row, k step) instead of 64 B of fp32; one thread per (row, k step),
+// each 32-B slot moved as two 16-B halves with the source / destination swizzles undone / applied.
+__global__ __launch_bounds__(256) void f16_plane_gather_kernel(const uintx4* __restrict__ src, int ks_n,
+                                                               const int* __restrict__ ridx, long m, long rows_pad,
+                                                               uintx4* __restrict__ dst) {
+  const long total = rows_pad * ks_n;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long img = i >> 8;
+    const int rr = (int)(i & 255);
+    const long tile = img / ks_n;
+    const long ks = img - tile * ks_n;
+    const long r = tile * 256 + rr;
+    uintx4 lo = uintx4{0u, 0u, 0u, 0u}, hi = lo;  // padding rows: zeros, as the converting kernel writes
+    if (r < m) {
+      const long rs = ridx[r];
+      const int ssw = (int)((rs >> 3) & 1);
+      const uintx4* s = src + ((((rs >> 8) * ks_n + ks) << 12) + (rs & 255) * 16) / 8;
+      lo = s[ssw];
+      hi = s[ssw ^ 1];
+    }
+    const int dsw = (rr >> 3) & 1;
+    uintx4* d = dst + ((img << 12) + rr * 16) / 8;
+    d[dsw] = lo;
+    d[dsw ^ 1] = hi;
+  }
+}
+
+SRML_API int srml_f16_plane_gather_rows(const unsigned short* P, long src_rows_pad, int kp, const int* ridx, long m,
+                                        long rows_pad, unsigned short* out, hipStream_t stream) {
+  if (rows_pad <= 0) return 0;
+  if ((kp & 15) || rows_pad < m || (rows_pad & 255) || (src_rows_pad & 255) || !ridx) return -2;
+  if ((reinterpret_cast<uintptr_t>(P) & 15) || (reinterpret_cast<uintptr_t>(out) & 15)) return -5;
+  const long total = rows_pad * (long)(kp / 16);
+  long blocks = (total + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(f16_plane_gather_kernel, dim3((unsigned)blocks), dim3(256), 0, stream,
+                     reinterpret_cast<const uintx4*>(P), kp / 16, ridx, m, rows_pad, reinterpret_cast<uintx4*>(out));
+  return srml_status();
+}
+
 // select of the filter pass with the flagged rows' thresholds (thr_out[p] for flagged[p])
 SRML_API int srml_split_top2_select_f16_thr(const unsigned long long* keys, const float* lob, long m, int nslot,
                                             const float* xnorm, const float* cg, float xadd, float z, float z2,

@@ -659,6 +659,29 @@ def test_rf_hist_fb_matches_library(gpu_device):
                 assert int(lib.srml_rf_hist_wide_fb(B, S, int(reg))) == ops.rf_hist_fb_wide(B, S, reg), (B, S, reg)
 
 
+def test_f16_plane_gather_matches_conversion(gpu_device):
+    """Rows gathered from the filter's tiled fp16 plane == the same rows converted from X again
+    (scale, centring, swizzle, zero padding rows)."""
+    from spark_rapids_ml_nai_amd.ops import native
+
+    g = torch.Generator(device=gpu_device).manual_seed(4)
+    m, n = 3000, 200
+    X = torch.randn(m, n, device=gpu_device, generator=g) * 3 + 1
+    mu = X.double().mean(0).float()
+    F = ops.F16Planes(X, mu)
+    assert F.ok and F.P is not None
+    rq = torch.randint(0, m, (777,), device=gpu_device, generator=g, dtype=torch.int32)
+    nq, rp = 777, 1024
+    st = native.stream(gpu_device)
+    A = torch.full((rp // 256, F.kp // 16, 256, 16), 7.0, dtype=torch.float16, device=gpu_device)
+    B = A.clone()
+    scratch = torch.zeros(1, dtype=torch.int32, device=gpu_device)
+    native.call("srml_f16_plane_gather_rows", F.P.data_ptr(), F.rows_pad, F.kp, rq.data_ptr(), nq, rp, A.data_ptr(), st)
+    native.call("srml_split_f16_tiled_centered_rows", X.data_ptr(), X.stride(0), rq.data_ptr(), nq, F.n,
+                F.mu.data_ptr(), F.kp, rp, F.scale, B.data_ptr(), scratch.data_ptr(), st)
+    assert torch.equal(A.view(torch.int16).cpu(), B.view(torch.int16).cpu())
+
+
 def test_rf_pack_wy_matches_gather(gpu_device):
     """One-pass (weight, label) packing in position order == the gather + stack it replaces."""
     g = torch.Generator().manual_seed(9)
