@@ -829,6 +829,65 @@ __global__ __launch_bounds__(256) void cand_exact_kernel(const float* __restrict
   }
 }
 
+// Same pass with the row's fp32 (x - mu) held in registers as NV float4 per lane (n <= 1024 NV,
+// n % 4 == 0, 16-B aligned rows): per candidate only its centre row is read, with all NV
+// vector loads of it in flight at once (the scalar kernel re-read x and mu for every candidate
+// and walked each row in a latency-bound 4-B loop).
+template <int NV>
+__global__ __launch_bounds__(256) void cand_exact_vec_kernel(const float* __restrict__ X, long ld,
+                                                             const float* __restrict__ mu, const float* __restrict__ W,
+                                                             long ldw, int n, int k, const int* __restrict__ rows,
+                                                             int nf, const int* __restrict__ ccount,
+                                                             const int* __restrict__ cand, int cap,
+                                                             int* __restrict__ labels, float* __restrict__ dist) {
+  const int lane = threadIdx.x & 63;
+  const long w = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (w >= nf) return;
+  const long i = rows[w];
+  const int n4 = n >> 2;
+  const floatx4* xr = reinterpret_cast<const floatx4*>(X + i * ld);
+  const floatx4* m4 = reinterpret_cast<const floatx4*>(mu);
+  floatx4 xm[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int c = v * 64 + lane;
+    xm[v] = floatx4{0.f, 0.f, 0.f, 0.f};
+    if (c < n4) {
+      const floatx4 a = xr[c], b = m4[c];
+      xm[v] = floatx4{a[0] - b[0], a[1] - b[1], a[2] - b[2], a[3] - b[3]};  // the fp32 x - mu of every search
+    }
+  }
+  const int cnt = ccount[w];
+  const bool full = cnt > cap || cnt <= 0;
+  const int nc = full ? k : cnt;
+  double bd = __builtin_huge_val();
+  int bj = 0x7fffffff;
+  for (int q = 0; q < nc; ++q) {
+    const int j = full ? q : cand[w * (long)cap + q];
+    const floatx4* wr = reinterpret_cast<const floatx4*>(W + (long)j * ldw);
+    floatx4 wv[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int c = v * 64 + lane;
+      wv[v] = c < n4 ? wr[c] : floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+    double acc = 0.0;
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const double dv = (double)xm[v][e] - (double)wv[v][e];
+        acc = fma(dv, dv, acc);
+      }
+    acc = wave_sum(acc);
+    if (acc < bd || (acc == bd && j < bj)) { bd = acc; bj = j; }
+  }
+  if (lane == 0) {
+    labels[i] = bj;
+    dist[i] = (float)bd;
+  }
+}
+
 __global__ __launch_bounds__(256) void split_scatter_refined_kernel(const unsigned long long* __restrict__ best,
                                                                     const int* __restrict__ rows, int nf,
                                                                     const float* __restrict__ xnorm,
@@ -1211,7 +1270,21 @@ SRML_API int srml_kmeans_cand_exact(const float* X, long ld, const float* mu, co
                                     const int* rows, int nf, const int* ccount, const int* cand, int cap, int* labels,
                                     float* dist, hipStream_t stream) {
   if (nf <= 0) return 0;
-  hipLaunchKernelGGL(cand_exact_kernel, dim3((unsigned)((nf + 3) / 4)), dim3(256), 0, stream, X, ld, mu, W, ldw, n, k,
-                     rows, nf, ccount, cand, cap, labels, dist);
+  const dim3 grid((unsigned)((nf + 3) / 4));
+  const bool vec = (n & 3) == 0 && (ld & 3) == 0 && (ldw & 3) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(W) & 15) == 0 && (reinterpret_cast<uintptr_t>(mu) & 15) == 0;
+  const int nv = (n / 4 + 63) / 64;
+  static const bool scalar = !(getenv("SRML_CAND_EXACT") && atoi(getenv("SRML_CAND_EXACT")) == 1);  // 1: vector kernel
+#define SRML_CE(NVV)                                                                                                  \
+  hipLaunchKernelGGL(cand_exact_vec_kernel<NVV>, grid, dim3(256), 0, stream, X, ld, mu, W, ldw, n, k, rows, nf, ccount, \
+                     cand, cap, labels, dist)
+  if (vec && !scalar && nv <= 4) SRML_CE(4);
+  else if (vec && !scalar && nv <= 8) SRML_CE(8);
+  else if (vec && !scalar && nv <= 12) SRML_CE(12);
+  else if (vec && !scalar && nv <= 16) SRML_CE(16);
+  else
+    hipLaunchKernelGGL(cand_exact_kernel, grid, dim3(256), 0, stream, X, ld, mu, W, ldw, n, k, rows, nf, ccount, cand,
+                       cap, labels, dist);
+#undef SRML_CE
   return srml_status();
 }
