@@ -1274,7 +1274,7 @@ SRML_API int srml_kmeans_cand_exact(const float* X, long ld, const float* mu, co
   const bool vec = (n & 3) == 0 && (ld & 3) == 0 && (ldw & 3) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0 &&
                    (reinterpret_cast<uintptr_t>(W) & 15) == 0 && (reinterpret_cast<uintptr_t>(mu) & 15) == 0;
   const int nv = (n / 4 + 63) / 64;
-  static const bool scalar = !(getenv("SRML_CAND_EXACT") && atoi(getenv("SRML_CAND_EXACT")) == 1);  // 1: vector kernel
+  static const bool scalar = getenv("SRML_CAND_EXACT") && atoi(getenv("SRML_CAND_EXACT")) == 0;  // 0: scalar kernel
 #define SRML_CE(NVV)                                                                                                  \
   hipLaunchKernelGGL(cand_exact_vec_kernel<NVV>, grid, dim3(256), 0, stream, X, ld, mu, W, ldw, n, k, rows, nf, ccount, \
                      cand, cap, labels, dist)
