@@ -75,6 +75,8 @@ def main() -> None:
     ap.add_argument("--batch-rows", type=int, default=20000)
     ap.add_argument("--no-transform", action="store_true",
                     help="skip the per-workload transform timing (outside the timed fit steps)")
+    ap.add_argument("--no-quality", action="store_true",
+                    help="skip the held-out quality metrics (scored after the timed fits)")
     ap.add_argument("--dump-models", type=str, default=None,
                     help="rank 0 saves each workload's last fitted model under this directory")
     args = ap.parse_args()
@@ -104,9 +106,15 @@ def main() -> None:
         from spark_rapids_ml_nai_amd.parallel.context import bind_numa_local
 
         bind_numa_local(device)  # pinned staging buffers on the GPU's own socket
-    if world > 1:
+    force_pg = os.environ.get("SRML_COMM_FORCE_PG", "0") == "1"
+    if world > 1 or force_pg:
         from datetime import timedelta
 
+        if world == 1:  # SRML_COMM_FORCE_PG (test-only): a 1-rank group, so the RCCL paths run
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29531")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         # SRML_DIST_BACKEND=gloo: multi-rank rehearsal with several ranks sharing one GPU
         # (RCCL refuses two ranks on one device); the default on GPUs is RCCL ("nccl")
         backend = os.environ.get("SRML_DIST_BACKEND", "nccl" if use_gpu else "gloo")
@@ -114,8 +122,9 @@ def main() -> None:
                                 **({"device_id": device} if use_gpu and backend == "nccl" else {}))
 
     from spark_rapids_ml_nai_amd import DataFrame
-    from spark_rapids_ml_nai_amd.bench.suite import (REF_GEOMEAN_SPEEDUP, REF_GPU_S, SPARK_CPU_S, geomean, make_shard,
-                                                      model_evidence, registry)
+    from spark_rapids_ml_nai_amd.bench.suite import (HOLDOUT_ROWS, HOLDOUT_SEED, REF_GEOMEAN_SPEEDUP, REF_GPU_S,
+                                                      SPARK_CPU_S, geomean, make_shard, model_evidence,
+                                                      model_quality, registry)
     from spark_rapids_ml_nai_amd.ops import native
 
     if use_gpu:
@@ -175,14 +184,9 @@ def main() -> None:
                 dist.all_reduce(t, op=dist.ReduceOp.MAX)
                 dt = float(t.item())
             per_fit = dt / args.steps
-            # per-rank split of the last timed fit (wall / H2D / compute / comm-wait), gathered
-            # after the clock stopped
-            rs = getattr(model, "_rank_stats", None) or {}
-            if world > 1:
-                per_rank = [None] * world
-                dist.all_gather_object(per_rank, rs)
-            else:
-                per_rank = [rs]
+            # per-rank split of the last timed fit (wall = h2d_exposed + compute + comm; all-gathered
+            # by the fit itself at its end)
+            per_rank = list(getattr(model, "_rank_stats", None) or [])
             results[name] = {
                 "fit_s": round(per_fit, 4),
                 "speedup_vs_spark_cpu": round(SPARK_CPU_S[name] / per_fit, 1) if name in SPARK_CPU_S else None,
@@ -212,6 +216,13 @@ def main() -> None:
                     del out
                 except Exception as e:  # noqa: BLE001
                     results[name]["transform_error"] = repr(e)[:200]
+            if rank == 0 and not args.no_quality:
+                # held-out quality next to the speed (outside every timed region): fresh rows of the
+                # same family and ground truth, scored through the public transform API
+                H = min(HOLDOUT_ROWS, max(1, m_local))
+                Xq, yq = make_shard(wl.data, H, args.cols, device, rank, m_total, seed=HOLDOUT_SEED)
+                results[name]["quality"] = model_quality(name, model, Xq, yq if wl.label else None)
+                del Xq, yq
             if args.dump_models and rank == 0:
                 model.write().overwrite().save(os.path.join(args.dump_models, name))
             del df, Xh, yh, model
@@ -252,11 +263,12 @@ def main() -> None:
             "missing_or_failed": errors,
             "ref_geomean_speedup": round(REF_GEOMEAN_SPEEDUP, 2),
             "ingest": args.ingest,
+            "comm_backend": dist.get_backend() if dist.is_initialized() else "none",
         },
     }
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if world > 1 or force_pg:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -162,9 +162,46 @@ def model_evidence(name: str, model: Any) -> Dict[str, Any]:
     return ev
 
 
-def make_shard(family: str, m_local: int, n: int, device: torch.device, rank: int, m_total: int
-               ) -> Tuple[np.ndarray, Optional[np.ndarray]]:
-    seed = 1000 + rank
+HOLDOUT_ROWS = 20000
+HOLDOUT_SEED = 900_000
+
+
+def model_quality(name: str, model: Any, Xh: np.ndarray, yh: Optional[np.ndarray]) -> Dict[str, Any]:
+    """Quality of a fitted headline model on held-out rows of the same synthetic family (fresh
+    seed, same shared ground truth), next to its time — the reference benchmark's per-run metrics
+    (bench_random_forest.py:111-137, bench_kmeans.py:59-113, bench_pca.py:58-110,
+    bench_linear_regression.py, bench_logistic_regression.py)."""
+    from .. import DataFrame
+
+    q: Dict[str, Any] = {"holdout_rows": int(Xh.shape[0])}
+    try:
+        if name == "pca":
+            C = np.asarray(model.components_, dtype=np.float64)
+            q["orthonormality_err"] = float(np.abs(C @ C.T - np.eye(C.shape[0])).max())
+            q["explained_variance_ratio"] = [round(float(v), 6) for v in model.explained_variance_ratio_]
+            return q
+        df = DataFrame.from_numpy(Xh, yh)
+        out = model.transform(df)
+        pred = np.asarray(out.to_numpy(model.getOrDefault("predictionCol")), dtype=np.float64)
+        if name.startswith("kmeans"):
+            Cc = np.asarray(model.cluster_centers_, dtype=np.float64)
+            lab = pred.astype(np.int64)
+            q["inertia_per_row"] = float(((Xh.astype(np.float64) - Cc[lab]) ** 2).sum(1).mean())
+            q["clusters_used"] = int(np.unique(lab).size)
+        elif name in ("logistic_regression", "random_forest_classifier"):
+            q["accuracy"] = float((pred == yh).mean())
+        else:  # regressors
+            err = pred - yh.astype(np.float64)
+            q["rmse"] = float(np.sqrt(np.mean(err ** 2)))
+            q["r2"] = float(1.0 - np.mean(err ** 2) / max(float(np.var(yh)), 1e-300))
+    except Exception as e:  # noqa: BLE001 - quality is best effort, never fails the bench
+        q["error"] = repr(e)[:160]
+    return q
+
+
+def make_shard(family: str, m_local: int, n: int, device: torch.device, rank: int, m_total: int,
+               seed: Optional[int] = None) -> Tuple[np.ndarray, Optional[np.ndarray]]:
+    seed = 1000 + rank if seed is None else int(seed)
     if family == "low_rank_matrix":
         X = datagen.low_rank_matrix(m_local, n, device, seed=seed, m_total=m_total)
         y = None

@@ -320,7 +320,7 @@ class LogisticRegressionModel(LogisticRegressionClass, _ModelWithPredictionCol, 
                 prob = torch.softmax(S, 1)
                 raw = S
                 lab = S.argmax(1).double()
-            return {pc: lab.cpu().numpy(), prc: prob.cpu().numpy(), rc: raw.cpu().numpy()}
+            return {pc: ctx.output(lab), prc: ctx.output(prob), rc: ctx.output(raw)}
 
         return construct, predict
 
@@ -420,7 +420,7 @@ class RandomForestClassificationModel(_RandomForestModel, HasProbabilityCol, Has
             tot = raw.sum(1, keepdim=True)
             prob = torch.where(tot > 0, raw / tot.clamp_min(1e-300), raw)
             lab = raw.argmax(1).double()
-            return {pc: lab.cpu().numpy(), prc: prob.cpu().numpy(), rc: raw.cpu().numpy()}
+            return {pc: ctx.output(lab), prc: ctx.output(prob), rc: ctx.output(raw)}
 
         return construct, predict
 

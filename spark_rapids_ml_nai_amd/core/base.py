@@ -320,12 +320,16 @@ class _Estimator(_CommonBase, *_ESTIMATOR_BASES):  # type: ignore[misc]
             fit_fn = self._get_fit_func(dataset, fit_multiple or None)
             with timer.phase("fit"):
                 results = run_spark_fit(self, dataset, fit_fn, params)
+            if isinstance(results, _FitOut):
+                timer.rank_stats = results.ranks
+                results = results.result
         else:
             df, _ = as_dataframe(dataset)
             fit_fn = self._get_fit_func(df, fit_multiple or None)
             results = run_fit_job(self, df, fit_fn, params, timer)
         if not isinstance(results, list):
             results = [results]
+        log_rank_split(self.logger, self.__class__.__name__ + " fit", getattr(timer, "rank_stats", None))
         models = []
         for i, r in enumerate(results):
             model = self._create_model(r)
@@ -355,11 +359,30 @@ class _EstimatorSupervised(_Estimator):
         return True
 
 
-def _fit_worker(ctx: WorkerContext, payload: Tuple[HostPartition, Callable, Dict[str, Any], bool]) -> Any:
-    """Body of one barrier task: ingest to device, describe partitions, run the fit closure."""
+class _FitOut:
+    """A worker's fit result plus the per-rank time split of that fit (every rank's, all-gathered
+    at the end of a multi-rank fit): what ``_fit_worker`` hands back to the driver side."""
+
+    def __init__(self, result: Any, ranks: List[Dict[str, Any]]) -> None:
+        self.result = result
+        self.ranks = ranks
+
+
+_worker_log = get_logger("worker")
+
+
+def _fit_worker(ctx: WorkerContext, payload: Tuple[HostPartition, Callable, Dict[str, Any], bool]) -> _FitOut:
+    """Body of one barrier task: ingest to device, describe partitions, run the fit closure.
+
+    Logs the reference's worker stages (``core.py:720-770``) and returns the rank's time split:
+    ``h2d_exposed_s`` (the compute stream waiting for the host->device copy; a streamed ingest's
+    chunks hidden under compute are not counted), ``comm_s`` (collectives, event-timed on RCCL),
+    ``compute_s`` = wall - h2d_exposed - comm, plus ``h2d_s`` (the copy stream's whole span)."""
     hp, fit_fn, params, float32 = payload
     t_start = time.perf_counter()
     ctx.comm.stats.reset()
+    tag = "rank %d/%d" % (ctx.rank, ctx.world_size)
+    _worker_log.info("%s: Loading data (%d rows x %d cols) onto %s", tag, hp.rows, hp.n_cols, ctx.device)
     _maybe_inject_fault(ctx, "ingest")
     if hp.rows == 0:
         raise RuntimeError("A worker received no data. Please increase amount of data or use fewer workers.")
@@ -388,9 +411,12 @@ def _fit_worker(ctx: WorkerContext, payload: Tuple[HostPartition, Callable, Dict
             h2d_ev[1].record()  # pinned sources are queued asynchronously: time them on the stream
     h2d_host_s = time.perf_counter() - t_start
     y = to_device(hp.y, ctx.device) if hp.y is not None else None
+    _worker_log.info("%s: Initializing context (partition descriptor, %s communicator)", tag,
+                     ctx.comm.backend if hasattr(ctx.comm, "backend") else "local")
     desc = PartitionDescriptor.build(ctx, hp.rows, hp.n_cols)
     inp = FitInput(X=X, y=y, cols=hp.cols, desc=desc, host=hp, stream=streamed)
     _maybe_inject_fault(ctx, "fit")
+    _worker_log.info("%s: Invoking fit (%d global rows)", tag, desc.m)
     with ctx.comm.watchdog(what="fit"):  # SRML_COMM_TIMEOUT: abort the communicator on a stuck collective
         out = fit_fn(inp, ctx, params)
         ctx.comm.check()  # asynchronous collectives (one-shot) all succeeded, else CommError
@@ -400,15 +426,49 @@ def _fit_worker(ctx: WorkerContext, payload: Tuple[HostPartition, Callable, Dict
     wall = time.perf_counter() - t_start
     if streamed is not None:
         h2d = streamed.h2d_seconds()
+        exposed = min(streamed.exposed_seconds(), h2d)
     elif ctx.is_gpu and h2d_ev:
         h2d_ev[1].synchronize()
         h2d = max(h2d_host_s, h2d_ev[0].elapsed_time(h2d_ev[1]) / 1e3)
+        exposed = h2d  # copied before any compute was queued: none of it is hidden
     else:
-        h2d = h2d_host_s
+        h2d = exposed = h2d_host_s
     st = ctx.comm.stats.snapshot()
-    ctx.timers["rank"] = dict(rank=ctx.rank, wall_s=round(wall, 6), h2d_s=round(h2d, 6),
-                              compute_s=round(max(0.0, wall - st["comm_s"]), 6), **st)
-    return out
+    exposed = min(exposed, wall)
+    mine = dict(rank=ctx.rank, wall_s=round(wall, 6), h2d_s=round(h2d, 6), h2d_exposed_s=round(exposed, 6),
+                compute_s=round(max(0.0, wall - exposed - st["comm_s"]), 6), **st)
+    ctx.timers["rank"] = mine
+    ranks = [mine]
+    if ctx.world_size > 1:
+        # one small all-gather at the end of the fit: every rank (and the driver, through rank 0's
+        # result) sees the whole split and the skew
+        import pickle
+
+        from ..parallel.comm import pickle_obj
+
+        ranks = [pickle.loads(b) for b in ctx.comm.allgather_bytes(pickle_obj(mine))]
+    ctx.timers["ranks"] = ranks
+    _worker_log.info("%s: Fit complete in %.4f s (h2d exposed %.4f, compute %.4f, comm %.4f)", tag, wall,
+                     mine["h2d_exposed_s"], mine["compute_s"], mine["comm_s"])
+    return _FitOut(out, ranks)
+
+
+def log_rank_split(logger: Any, what: str, ranks: Optional[List[Dict[str, Any]]]) -> None:
+    """One line per rank of a fit's time split plus the rank skew (max / min wall), from the driver
+    (or rank 0 of an SPMD job, whose every rank holds the gathered split)."""
+    if not ranks:
+        return
+    if spmd_active() and torch.distributed.get_rank() != 0:
+        return
+    for r in ranks:
+        logger.info("%s rank %d: wall %.4f s = h2d_exposed %.4f + compute %.4f + comm %.4f (h2d span %.4f, "
+                    "%d collectives, %d bytes)", what, r.get("rank", -1), r.get("wall_s", 0.0),
+                    r.get("h2d_exposed_s", 0.0), r.get("compute_s", 0.0), r.get("comm_s", 0.0), r.get("h2d_s", 0.0),
+                    r.get("comm_calls", 0), r.get("comm_bytes", 0))
+    walls = [float(r.get("wall_s", 0.0)) for r in ranks]
+    if len(walls) > 1:
+        logger.info("%s rank skew: max/min wall %.4f / %.4f s (%.3fx)", what, max(walls), min(walls),
+                    max(walls) / max(min(walls), 1e-12))
 
 
 def _maybe_inject_fault(ctx: WorkerContext, stage: str) -> None:
@@ -442,8 +502,8 @@ def run_fit_job(est: _Estimator, df: DataFrame, fit_fn: Callable, params: Dict[s
             hp = est._host_partition(df)
         with use_context(ctx), timer.phase("fit"):
             res = _fit_worker(ctx, (hp, fit_fn, params, float32))
-        timer.rank_stats = ctx.timers.get("rank")
-        return res
+        timer.rank_stats = res.ranks
+        return res.result
     nw = est.num_workers
     from ..parallel.launcher import run_barrier_job
 
@@ -453,7 +513,8 @@ def run_fit_job(est: _Estimator, df: DataFrame, fit_fn: Callable, params: Dict[s
         hps = [est._host_partition(DataFrame([p])) for p in df.partitions]
     with timer.phase("fit"):
         results = run_barrier_job(_fit_worker, [(hp, fit_fn, params, float32) for hp in hps])
-    return results[0]
+    timer.rank_stats = results[0].ranks
+    return results[0].result
 
 
 def run_worker_job(fn: Callable[[WorkerContext, Any], Any], payloads: Sequence[Any]) -> List[Any]:
@@ -729,7 +790,13 @@ def _eval_info(evaluator: Any) -> Tuple[str, bool, float]:
 
 
 def _eval_worker(ctx: WorkerContext, payload: Tuple[Any, ...]) -> List[List[Any]]:
-    """Per-partition summaries of every model: [[summary of model i] for each non-empty partition]."""
+    """Per-partition summaries of every model: [[summary of model i] for each non-empty partition].
+
+    The predictions stay on the device (``ctx.device_outputs``): the confusion counts, the log-loss
+    sum and the regression moments are reduced there (``ops.confusion_counts`` / ``logloss_sum`` /
+    ``reg_moments``, reference classification.py:113-155 / regression.py:144-173) and only those
+    C x C / 12-double partials come to the host."""
+    from .. import ops
     from ..metrics import ClassificationSummary, RegressionSummary
 
     models, tables, label_col, (kind, need_prob, eps) = payload
@@ -737,22 +804,45 @@ def _eval_worker(ctx: WorkerContext, payload: Tuple[Any, ...]) -> List[List[Any]
     states = [c(ctx) for c, _ in fns]
     dt = torch.float32 if models[0]._transform_dtype() == np.float32 else torch.float64
     out = []
-    for t in tables:
-        if t is None or t.num_rows == 0:
-            continue
-        part = DataFrame([t])
-        Xd = to_device(models[0]._transform_features(part), ctx.device, dt)
-        y = part.to_numpy(label_col, np.float64)
-        row = []
-        for m, (_, predict), st in zip(models, fns, states):
-            res = predict(st, Xd, ctx)
-            p = np.asarray(res[m.getOrDefault("predictionCol")], np.float64)
-            if kind == "regression":
-                row.append(RegressionSummary.from_arrays(y, p))
-            else:
-                prob = np.asarray(res[m.getOrDefault("probabilityCol")]) if need_prob else None
-                row.append(ClassificationSummary.from_arrays(y, p, prob, eps))
-        out.append(row)
+    prev = ctx.device_outputs
+    ctx.device_outputs = True
+    try:
+        for t in tables:
+            if t is None or t.num_rows == 0:
+                continue
+            part = DataFrame([t])
+            Xd = to_device(models[0]._transform_features(part), ctx.device, dt)
+            y = part.to_numpy(label_col, np.float64)
+            yd = torch.from_numpy(y).to(ctx.device)
+            row = []
+            for m, (_, predict), st in zip(models, fns, states):
+                res = predict(st, Xd, ctx)
+                p = res[m.getOrDefault("predictionCol")]
+                if not isinstance(p, torch.Tensor):  # a model without device outputs: host summary
+                    p = np.asarray(p, np.float64)
+                    if kind == "regression":
+                        row.append(RegressionSummary.from_arrays(y, p))
+                    else:
+                        prob = np.asarray(res[m.getOrDefault("probabilityCol")]) if need_prob else None
+                        row.append(ClassificationSummary.from_arrays(y, p, prob, eps))
+                    continue
+                if kind == "regression":
+                    row.append(RegressionSummary.from_moments(len(y), ops.reg_moments(yd, p)))
+                    continue
+                prob = res.get(m.getOrDefault("probabilityCol"))
+                width = int(prob.shape[1]) if isinstance(prob, torch.Tensor) and prob.dim() == 2 else 0
+                C = max(width, int(y.max()) + 1 if len(y) else 1, 1)
+                cm = ops.confusion_counts(yd, p, C)
+                if cm is None:  # a label / prediction outside [0, C): the host path handles any values
+                    ph = p.double().cpu().numpy()
+                    row.append(ClassificationSummary.from_arrays(
+                        y, ph, prob.cpu().numpy() if need_prob and prob is not None else None, eps))
+                    continue
+                ll = ops.logloss_sum(prob, yd, eps) if need_prob and prob is not None else 0.0
+                row.append(ClassificationSummary.from_confusion(cm, len(y), ll))
+            out.append(row)
+    finally:
+        ctx.device_outputs = prev
     return out
 
 

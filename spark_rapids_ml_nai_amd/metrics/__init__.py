@@ -53,6 +53,15 @@ class RegressionSummary:
         mean = M.mean(1)
         return cls(n, mean, ((M - mean[:, None]) ** 2).sum(1), (M * M).sum(1), np.abs(M).sum(1))
 
+    @classmethod
+    def from_moments(cls, n: int, mom: np.ndarray) -> "RegressionSummary":
+        """From the device reduction (``ops.reg_moments``): rows [sum, sum of squares, sum |x|,
+        sum of squared deviations] of the columns (label, label - prediction, prediction)."""
+        if n == 0:
+            return cls()
+        mom = np.asarray(mom, dtype=np.float64)
+        return cls(int(n), mom[0] / n, mom[3].copy(), mom[1].copy(), mom[2].copy())
+
     def merge(self, o: "RegressionSummary") -> "RegressionSummary":
         if o.count == 0:
             return self
@@ -149,6 +158,19 @@ class ClassificationSummary:
             idx = y.astype(np.int64)
             pl = prob[np.arange(len(y)), np.clip(idx, 0, prob.shape[1] - 1)]
             s.log_loss_sum = float(-np.log(np.maximum(pl, eps)).sum())
+        return s
+
+    @classmethod
+    def from_confusion(cls, cm: np.ndarray, count: int, log_loss_sum: float = 0.0) -> "ClassificationSummary":
+        """From (label, prediction) counts (``ops.confusion_counts``): the classes present as a
+        label or a prediction, like ``from_arrays``."""
+        cm = np.asarray(cm, dtype=np.float64)
+        rows, cols = cm.sum(1), cm.sum(0)
+        s = cls(count=int(count), log_loss_sum=float(log_loss_sum))
+        for c in np.nonzero((rows > 0) | (cols > 0))[0]:
+            s.tp[float(c)] = float(cm[c, c])
+            s.fp[float(c)] = float(cols[c] - cm[c, c])
+            s.label[float(c)] = float(rows[c])
         return s
 
     def merge(self, o: "ClassificationSummary") -> "ClassificationSummary":

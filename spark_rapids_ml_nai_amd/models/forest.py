@@ -604,14 +604,22 @@ def fit_forest(X: torch.Tensor, y: torch.Tensor, ctx: WorkerContext, m_total: in
     trees: List[Dict[str, Any]] = []
     # trees per batch: positions + weights cost ~8 B per in-bag row and tree
     per_batch = max(1, int((4 << 30) // max(8 * m, 1)))
-    for t0 in range(0, n_trees_local, per_batch):
-        nt = min(per_batch, n_trees_local - t0)
-        for t in grow_forest(bins, edges_h, y, ctx, gen, p, S, not classification, data_parallel, gen_boot, nt,
-                             pending=pending):
-            trees.append(t.to_dict())
+    try:
+        for t0 in range(0, n_trees_local, per_batch):
+            nt = min(per_batch, n_trees_local - t0)
+            for t in grow_forest(bins, edges_h, y, ctx, gen, p, S, not classification, data_parallel, gen_boot, nt,
+                                 pending=pending):
+                trees.append(t.to_dict())
+            if pending is not None:
+                pending.finish()
+                pending = None
+    finally:
+        # a rank with no trees of its own (numTrees < world size) never enters the loop: the shared
+        # bins (reused by later param maps with the same maxBins / seed) must still be complete;
+        # finishing also makes the current stream wait on every chunk's copy event, so later
+        # readers of X (another quantisation key, a transform) never race the DMA
         if pending is not None:
             pending.finish()
-            pending = None
     return trees
 
 

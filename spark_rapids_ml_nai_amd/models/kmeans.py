@@ -156,6 +156,9 @@ def init_kmeans_parallel(X: torch.Tensor, xnorm: torch.Tensor, desc: PartitionDe
 
 
 DELTA_FRAC = 0.2  # moved-row fraction below which the Lloyd sums are updated incrementally
+# a full cluster-sum pass re-anchors the incrementally updated sums after this many delta updates
+# (bounds the fp64 rounding of the +x / -x chains; cuML recomputes every iteration)
+REANCHOR = max(1, int(os.environ.get("SRML_KMEANS_REANCHOR", "16")))
 
 
 def _use_split(X: torch.Tensor, k: int) -> bool:
@@ -237,6 +240,7 @@ def kmeans_fit(X: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext, k
     prev = None
     sums_l = counts_l = None
     n_delta = 0
+    last_anchor = 0
     for it in range(max(0, max_iter)):
         n_iter = it + 1
         if F16 is not None:
@@ -249,10 +253,12 @@ def kmeans_fit(X: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext, k
         moved = None
         if prev is not None and X.is_cuda and not deterministic():
             moved = torch.nonzero(labels != prev).view(-1)
-            if moved.numel() > DELTA_FRAC * X.shape[0]:
+            if moved.numel() > DELTA_FRAC * X.shape[0] or (n_delta and n_delta % REANCHOR == 0 and
+                                                           n_delta != last_anchor):
                 moved = None
         if moved is None:
             sums_l, counts_l = ops.cluster_sums(X, labels, k)
+            last_anchor = n_delta
         elif moved.numel():
             s_new, c_new = ops.cluster_sums_rows(X, moved, labels.index_select(0, moved), k)
             s_old, c_old = ops.cluster_sums_rows(X, moved, prev.index_select(0, moved), k)

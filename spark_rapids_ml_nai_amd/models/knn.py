@@ -45,8 +45,12 @@ def _ring_search(queries: torch.Tensor, k: int, ctx: WorkerContext, local: Calla
         torch.Tensor, torch.Tensor]]) -> Tuple[torch.Tensor, torch.Tensor]:
     """Run ``local(Q) -> (d [q, k], global ids [q, k])`` for every rank's query block on every
     rank's items by passing (block, running top-k) around the ring; returns this rank's merged
-    lists. One hop = one overlapped isend/irecv of the next query block + a small exchange of the
-    running lists."""
+    lists.
+
+    Per hop: the NEXT query block's isend/irecv starts first and the held block is scored while it
+    travels; the held block's running lists (sent by the previous rank after ITS merge) are only
+    waited for after that scoring, merged, and forwarded at once — so each list exchange overlaps
+    the next hop's scoring instead of sitting between hops on the critical path."""
     W, r = ctx.world_size, ctx.rank
     dev = queries.device
     nq = queries.shape[0]
@@ -58,27 +62,38 @@ def _ring_search(queries: torch.Tensor, k: int, ctx: WorkerContext, local: Calla
     Qc = queries.contiguous()
     dc = torch.full((nq, k), float("inf"), dtype=torch.float32, device=dev)
     ic = torch.full((nq, k), -1, dtype=torch.int64, device=dev)
+    h_lists = None  # in-flight exchange of the running lists of the block held at this hop
     for s in range(W):
-        h = None
+        h_q = None
         if s < W - 1:  # the next block is already on its way while this one is scored
             rows = sizes[(r - s - 1) % W]
             Qn = torch.empty((rows, n), dtype=Qc.dtype, device=dev)
-            h = ctx.comm.isendrecv(Qc, nxt, Qn, prv)
+            h_q = ctx.comm.isendrecv(Qc, nxt, Qn, prv)
+        ld = li = None
         if Qc.shape[0]:
             ld, li = local(Qc)
+        if h_lists is not None:  # this block's lists, merged by the previous rank at the last hop
+            for h in h_lists:
+                ctx.comm.wait_sendrecv(h)
+            h_lists = None
+        if ld is not None:
             dc, ic = _merge_lists(dc, ic, ld.float(), li, k)
         if s < W - 1:
-            ctx.comm.wait_sendrecv(h)
+            ctx.comm.wait_sendrecv(h_q)
             dn = torch.empty((rows, k), dtype=torch.float32, device=dev)
             inn = torch.empty((rows, k), dtype=torch.int64, device=dev)
-            ctx.comm.sendrecv(dc.contiguous(), nxt, dn, prv)
-            ctx.comm.sendrecv(ic.contiguous(), nxt, inn, prv)
+            # forward the merged lists with the block they belong to (already sent); overlaps the
+            # next hop's scoring
+            h_lists = (ctx.comm.isendrecv(dc.contiguous(), nxt, dn, prv),
+                       ctx.comm.isendrecv(ic.contiguous(), nxt, inn, prv))
             Qc, dc, ic = Qn, dn, inn
     # the block now held belongs to the next rank: hand it home, receive ours
     d_own = torch.empty((nq, k), dtype=torch.float32, device=dev)
     i_own = torch.empty((nq, k), dtype=torch.int64, device=dev)
-    ctx.comm.sendrecv(dc.contiguous(), nxt, d_own, prv)
-    ctx.comm.sendrecv(ic.contiguous(), nxt, i_own, prv)
+    h1 = ctx.comm.isendrecv(dc.contiguous(), nxt, d_own, prv)
+    h2 = ctx.comm.isendrecv(ic.contiguous(), nxt, i_own, prv)
+    ctx.comm.wait_sendrecv(h1)
+    ctx.comm.wait_sendrecv(h2)
     return d_own, i_own
 
 

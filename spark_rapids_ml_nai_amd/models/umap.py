@@ -231,7 +231,7 @@ def _spectral_device(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor,
     ci = cols.to(torch.int32).contiguous()
     if dev.type == "cuda":
         A = CSR(indptr=indptr, indices=ci, data=vals.float().contiguous(), shape=(n, n))
-        deg = ops.csr_spmm(A, torch.ones(n, 1, device=dev, dtype=torch.float32)).view(-1).double()
+        deg = ops.csr_row_sums(A)  # fp64 per-row accumulation (high-degree nodes keep their precision)
     else:
         deg = torch.zeros(n, dtype=torch.float64, device=dev).index_add_(0, r64, vals.double())
     dinv = 1.0 / torch.sqrt(deg.clamp_min(1e-30))

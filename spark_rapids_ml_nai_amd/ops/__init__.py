@@ -2056,33 +2056,53 @@ def csr_logreg_binary_loss_grad(A, y: torch.Tensor, w: torch.Tensor, b: float,
 
 
 def csr_spmm(A, W: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """fp32 Z (m, K) = A W + bias for W (n, K), K <= 16 (multinomial margins)."""
+    """fp32 Z (m, K) = A W + bias for W (n, K) (multinomial margins). Device: ``srml_csr_spmm_ld``
+    over 16-column panels of W / Z (strided, no copies)."""
     m, n = A.shape
     K = W.shape[1]
-    if not A.data.is_cuda or K > 16:
+    if not A.data.is_cuda:
         Z = (_csr_torch(A) @ W.to(A.data.dtype)).float()
         return Z + bias.float() if bias is not None else Z
     _csr_check(A)
     Wf = _c(W.to(torch.float32))
     bf = _c(bias.to(torch.float32)) if bias is not None else None
     Z = torch.empty(m, K, dtype=torch.float32, device=A.data.device)
-    native.call("srml_csr_spmm_" + _sfx(A), A.indptr.data_ptr(), A.indices.data_ptr(), A.data.data_ptr(), m,
-                A.data.numel(), Wf.data_ptr(), K, bf.data_ptr() if bf is not None else None, Z.data_ptr(),
-                native.stream(A.data.device))
+    st = native.stream(A.data.device)
+    for c0 in range(0, K, 16):
+        kk = min(16, K - c0)
+        native.call("srml_csr_spmm_ld_" + _sfx(A), A.indptr.data_ptr(), A.indices.data_ptr(), A.data.data_ptr(), m,
+                    A.data.numel(), Wf[:, c0:].data_ptr(), kk, K, bf[c0:].data_ptr() if bf is not None else None,
+                    Z[:, c0:].data_ptr(), K, st)
     return Z
 
 
 def csr_spmtm(A, R: torch.Tensor) -> torch.Tensor:
-    """fp64 (n, K) = A^T R for R (m, K), K <= 16 (multinomial gradient)."""
+    """fp64 (n, K) = A^T R for R (m, K) (multinomial gradient). Device: ``srml_csr_spmtm_ld`` over
+    16-column panels."""
     m, n = A.shape
     K = R.shape[1]
-    if not A.data.is_cuda or K > 16:
+    if not A.data.is_cuda:
         return (_csr_torch(A).t() @ R.to(A.data.dtype)).double()
     _csr_check(A)
     Rf = _c(R.to(torch.float32))
     out = torch.zeros(n, K, dtype=torch.float64, device=A.data.device)
-    native.call("srml_csr_spmtm_" + _sfx(A), A.indptr.data_ptr(), A.indices.data_ptr(), A.data.data_ptr(), m,
-                A.data.numel(), Rf.data_ptr(), K, out.data_ptr(), native.stream(A.data.device))
+    st = native.stream(A.data.device)
+    for c0 in range(0, K, 16):
+        kk = min(16, K - c0)
+        native.call("srml_csr_spmtm_ld_" + _sfx(A), A.indptr.data_ptr(), A.indices.data_ptr(), A.data.data_ptr(), m,
+                    A.data.numel(), Rf[:, c0:].data_ptr(), kk, K, out[:, c0:].data_ptr(), K, st)
+    return out
+
+
+def csr_row_sums(A) -> torch.Tensor:
+    """fp64 row sums of a CSR matrix (fp32 values; one thread per row, no atomics)."""
+    m = A.shape[0]
+    if not A.data.is_cuda:
+        rows = torch.repeat_interleave(torch.arange(m), (A.indptr[1:] - A.indptr[:-1]).cpu())
+        return torch.zeros(m, dtype=torch.float64).index_add_(0, rows, A.data.double().cpu())
+    out = torch.empty(m, dtype=torch.float64, device=A.data.device)
+    native.call("srml_csr_row_sums_f32", A.indptr.data_ptr(), _c(A.data.float()).data_ptr(), m, out.data_ptr(),
+                native.stream(A.data.device))
     return out
 
 
@@ -2151,7 +2171,7 @@ def _glm_wide(X, y32: torch.Tensor, W: torch.Tensor, b: torch.Tensor, out: torch
     fp = flag.data_ptr() if flag is not None else None
     Wf = W.to(torch.float32)
     if csr:
-        Z = torch.cat([csr_spmm(X, Wf[c0: c0 + 16].t()) for c0 in range(0, K, 16)], 1).contiguous()
+        Z = csr_spmm(X, Wf.t())  # 16-class panels inside
     else:
         Z = torch.empty((m, K), dtype=torch.float32, device=dev)
         for c0 in range(0, K, 32):
@@ -2164,9 +2184,7 @@ def _glm_wide(X, y32: torch.Tensor, W: torch.Tensor, b: torch.Tensor, out: torch
     gb, _ = col_moments(R, need_sq=False)
     out[Kn: Kn + K] += gb
     if csr:
-        for c0 in range(0, K, 16):
-            kk = min(16, K - c0)
-            out[c0 * n: (c0 + kk) * n] += csr_spmtm(X, _c(R[:, c0: c0 + kk])).t().reshape(-1)
+        out[: K * n] += csr_spmtm(X, R).t().reshape(-1)
         return
     for c0 in range(0, K, 16):
         kk = min(16, K - c0)
@@ -2347,3 +2365,70 @@ def zero_(t: torch.Tensor) -> torch.Tensor:
     assert t.is_contiguous()
     native.call("srml_memset_async", t.data_ptr(), 0, t.nbytes, native.stream(t.device))
     return t
+
+
+# ------------------------------------------------------------------------------------------
+# Evaluation partials on the device (csrc/metrics.hip): the CrossValidator transform-evaluate pass
+_KIND = {torch.float64: 0, torch.float32: 1, torch.int64: 2, torch.int32: 3}
+
+
+def _kind(t: torch.Tensor) -> Tuple[torch.Tensor, int]:
+    t = _c(t)
+    if t.dtype not in _KIND:
+        t = t.double()
+    return t, _KIND[t.dtype]
+
+
+def confusion_counts(y: torch.Tensor, pred: torch.Tensor, C: int) -> Optional[np.ndarray]:
+    """(C, C) int64 counts of (label, prediction) pairs, or None when a label / prediction is not
+    an integer in [0, C) (the caller falls back to the host summary). Device: LDS-privatised
+    histogram (``srml_confusion_counts``); only the C x C counts come to the host."""
+    m = int(y.shape[0])
+    if not y.is_cuda:
+        yy, pp = y.double().cpu().numpy(), pred.double().cpu().numpy()
+        ok = (yy >= 0) & (yy < C) & (yy == np.floor(yy)) & (pp >= 0) & (pp < C) & (pp == np.floor(pp))
+        if not ok.all():
+            return None
+        out = np.zeros((C, C), np.int64)
+        np.add.at(out, (yy.astype(np.int64), pp.astype(np.int64)), 1)
+        return out
+    yk, yi = _kind(y)
+    pk, pi = _kind(pred)
+    cnt = torch.zeros(C * C + 1, dtype=torch.int64, device=y.device)
+    native.call("srml_confusion_counts", yk.data_ptr(), yi, pk.data_ptr(), pi, m, int(C), cnt.data_ptr(),
+                native.stream(y.device))
+    h = cnt.cpu().numpy()
+    if h[-1] != 0:
+        return None
+    return h[:-1].reshape(C, C)
+
+
+def logloss_sum(prob: torch.Tensor, y: torch.Tensor, eps: float) -> float:
+    """sum_r -log(max(prob[r, y_r], eps)) (labels clipped to [0, C - 1]); one double to the host."""
+    m, C = prob.shape
+    if not prob.is_cuda:
+        idx = np.clip(y.cpu().numpy().astype(np.int64), 0, C - 1)
+        pl = prob.double().cpu().numpy()[np.arange(m), idx]
+        return float(-np.log(np.maximum(pl, eps)).sum())
+    pk, pi = _kind(prob)
+    yk, yi = _kind(y)
+    out = torch.zeros(1, dtype=torch.float64, device=prob.device)
+    native.call("srml_logloss_sum", pk.data_ptr(), pi, m, C, pk.stride(0), yk.data_ptr(), yi, float(eps),
+                out.data_ptr(), native.stream(prob.device))
+    return float(out.item())
+
+
+def reg_moments(y: torch.Tensor, pred: torch.Tensor) -> np.ndarray:
+    """(4, 3) fp64 [sum, sum of squares, sum |x|, sum of squared deviations] of the columns
+    (label, label - prediction, prediction); 12 doubles to the host."""
+    if not y.is_cuda:
+        yy, pp = y.double().cpu().numpy(), pred.double().cpu().numpy()
+        M = np.stack([yy, yy - pp, pp])
+        mu = M.mean(1) if M.shape[1] else np.zeros(3)
+        return np.stack([M.sum(1), (M * M).sum(1), np.abs(M).sum(1), ((M - mu[:, None]) ** 2).sum(1)])
+    yk, yi = _kind(y)
+    pk, pi = _kind(pred)
+    out = torch.zeros(12, dtype=torch.float64, device=y.device)
+    native.call("srml_reg_moments", yk.data_ptr(), yi, pk.data_ptr(), pi, int(y.shape[0]), out.data_ptr(),
+                native.stream(y.device))
+    return out.cpu().numpy().reshape(4, 3)

@@ -622,7 +622,8 @@ __global__ __launch_bounds__(256, 2) void logreg_binary_pf_kernel(const float* _
                                                                   const double* __restrict__ w, double b_in,
                                                                   const double* __restrict__ bptr,
                                                                   const int* __restrict__ flag,
-                                                                  double* __restrict__ out, long rows_per_block) {
+                                                                  double* __restrict__ out, long rows_per_block,
+                                                                  float* __restrict__ ws) {
   if (flag && *flag) return;
   const double b = bptr ? *bptr : b_in;
   __shared__ double part[2][R][4];
@@ -645,7 +646,7 @@ __global__ __launch_bounds__(256, 2) void logreg_binary_pf_kernel(const float* _
   double gb = 0.0, loss = 0.0;
   const long r0 = (long)blockIdx.x * rows_per_block;
   const long r1 = min(m, r0 + rows_per_block);
-  if (r0 >= r1) return;
+  if (r0 >= r1 && ws == nullptr) return;  // (partial rows: an empty block still stores its zero row)
 
   auto load = [&](long rb, floatx4 (&x)[R][V]) {
 #pragma unroll
@@ -707,16 +708,36 @@ __global__ __launch_bounds__(256, 2) void logreg_binary_pf_kernel(const float* _
       }
     }
   }
+  if (ws == nullptr) {
 #pragma unroll
-  for (int v = 0; v < V; ++v)
+    for (int v = 0; v < V; ++v)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int c = cbase + (v * 64 + lane) * 4 + q;
-      if (cbase + (v * 64 + lane) * 4 + 3 < n) atomicAdd(&out[c], (double)g[v][q]);
+      for (int q = 0; q < 4; ++q) {
+        const int c = cbase + (v * 64 + lane) * 4 + q;
+        if (cbase + (v * 64 + lane) * 4 + 3 < n) atomicAdd(&out[c], (double)g[v][q]);
+      }
+    if (wid == 0 && lane == 0) {
+      atomicAdd(&out[n], gb);
+      atomicAdd(&out[n + 1], loss);
     }
+    return;
+  }
+  // Partial-row epilogue: when every block of a chip-filling grid ends at the same moment (all
+  // 768 blocks of a 125k-row shard are resident at once), n fp64 atomics per block arrive as one
+  // burst on the same n addresses (2.3M atomics: ~40 us of a 0.29 ms evaluation). Instead each
+  // block stores its fp32 partial row with plain vector stores and fold_rows_kernel sums them
+  // right after (same stream; the kernel boundary orders the stores).
+  const long wst = (long)((n + 3) & ~3) + 4;  // floats per partial row: columns, then gb, loss (fp64)
+  float* mine = ws + (long)blockIdx.x * wst;
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    const int c = cbase + (v * 64 + lane) * 4;
+    if (c + 3 < n) *reinterpret_cast<floatx4*>(mine + c) = g[v];
+  }
   if (wid == 0 && lane == 0) {
-    atomicAdd(&out[n], gb);
-    atomicAdd(&out[n + 1], loss);
+    double* md = reinterpret_cast<double*>(mine + wst - 4);
+    md[0] = gb;
+    md[1] = loss;
   }
 }
 
@@ -832,6 +853,64 @@ __global__ __launch_bounds__(256) void logreg_binary_narrow_kernel(const float* 
   }
 }
 
+// Sum of `parts` partial rows (fp32 columns + 2 trailing fp64 [gb, loss]) into out (fp64). Thread
+// = 4 columns of one slice of FOLD_ROWS consecutive rows (independent 16-B loads, fp64 sums), one
+// fp64 atomic per column and slice: ~parts / FOLD_ROWS atomics per column instead of parts.
+constexpr int FOLD_ROWS = 16;
+__global__ __launch_bounds__(256) void fold_rows_kernel(const float* __restrict__ ws, int parts, long wst, int n,
+                                                        double* __restrict__ out, const int* __restrict__ flag) {
+  if (flag && *flag) return;
+  const int c = ((int)blockIdx.x * 256 + (int)threadIdx.x) * 4;
+  const int p0 = (int)blockIdx.y * FOLD_ROWS, p1 = min(parts, p0 + FOLD_ROWS);
+  if (c < n) {
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    floatx4 t[FOLD_ROWS];
+#pragma unroll
+    for (int j = 0; j < FOLD_ROWS; ++j)
+      t[j] = p0 + j < p1 ? __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(ws + (long)(p0 + j) * wst + c))
+                         : floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < FOLD_ROWS; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[q] += (double)t[j][q];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (c + q < n) atomicAdd(&out[c + q], a[q]);
+  } else if (c == ((n + 3) & ~3)) {  // the thread just past the columns folds gb and loss
+    double gb = 0.0, loss = 0.0;
+    for (int p = p0; p < p1; ++p) {
+      const double* pd = reinterpret_cast<const double*>(ws + (long)p * wst + wst - 4);
+      gb += pd[0];
+      loss += pd[1];
+    }
+    atomicAdd(&out[n], gb);
+    atomicAdd(&out[n + 1], loss);
+  }
+}
+
+// Per-device workspace of the partial-row epilogue: `blocks` rows of `row_floats` floats. Grown on
+// demand (first evaluation of a fit); a device's evaluations run in stream order on it.
+static float* fold_workspace(long blocks, long row_floats) {
+  struct Ws { void* p = nullptr; size_t bytes = 0; };
+  static Ws cache[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  const size_t need = (size_t)blocks * row_floats * sizeof(float);
+  Ws& c = cache[dev];
+  if (c.bytes < need) {
+    if (c.p) {
+      if (hipDeviceSynchronize() != hipSuccess) return nullptr;  // in-flight launches may still use it
+      (void)hipFree(c.p);
+      c.p = nullptr;
+      c.bytes = 0;
+    }
+    const size_t bytes = need + need / 4;
+    if (hipMalloc(&c.p, bytes) != hipSuccess) return nullptr;
+    c.bytes = bytes;
+  }
+  return reinterpret_cast<float*>(c.p);
+}
+
 // b: intercept by value, or (bptr != null) read on the device; flag (optional): skip when *flag != 0
 SRML_API int srml_logreg_binary2_f32(const float* X, long m, int n, long ld, const float* y, const double* w, double b,
                                      const double* bptr, const int* flag, double* out, hipStream_t stream) {
@@ -880,8 +959,13 @@ SRML_API int srml_logreg_binary2_f32(const float* X, long m, int n, long ld, con
     static const int dsel = getenv("SRML_LOGREG_D") ? atoi(getenv("SRML_LOGREG_D")) : 3;
     static const int nt = getenv("SRML_LOGREG_NT") ? atoi(getenv("SRML_LOGREG_NT")) : 1;  // nontemporal X stream: +2%
     const int VS = (n + 1023) / 1024;
+    // partial-row epilogue + fold kernel (SRML_LOGREG_FOLD=0: one fp64 atomic flush per block)
+    static const int fold = getenv("SRML_LOGREG_FOLD") ? atoi(getenv("SRML_LOGREG_FOLD")) : 1;
+    const long wst = ((n + 3) & ~3) + 4;
+    float* fws = nullptr;
+    if (fold && !(fws = fold_workspace(blocks, wst))) return -3;
 #define SRML_LR_PF(VV, RR, DD) \
-    hipLaunchKernelGGL((logreg_binary_pf_kernel<VV, RR, DD>), grid, blk, 0, stream, X, m, n, ld, y, w, b, bptr, flag, out, rpb)
+    hipLaunchKernelGGL((logreg_binary_pf_kernel<VV, RR, DD>), grid, blk, 0, stream, X, m, n, ld, y, w, b, bptr, flag, out, rpb, fws)
 #define SRML_LR_PF_V(RR, DD) \
     do { if (VS == 2) SRML_LR_PF(2, RR, DD); else if (VS == 3) SRML_LR_PF(3, RR, DD); else SRML_LR_PF(4, RR, DD); } while (0)
     if (rsel == 2 && dsel == 1) SRML_LR_PF_V(2, 1);
@@ -890,7 +974,7 @@ SRML_API int srml_logreg_binary2_f32(const float* X, long m, int n, long ld, con
     else if (dsel == 3 && nt) {
 #define SRML_LR_PF_NT(VV)                                                                                        \
   hipLaunchKernelGGL((logreg_binary_pf_kernel<VV, 1, 3, true>), grid, blk, 0, stream, X, m, n, ld, y, w, b, bptr, \
-                     flag, out, rpb)
+                     flag, out, rpb, fws)
       if (VS == 2) SRML_LR_PF_NT(2);
       else if (VS == 3) SRML_LR_PF_NT(3);
       else SRML_LR_PF_NT(4);
@@ -898,6 +982,9 @@ SRML_API int srml_logreg_binary2_f32(const float* X, long m, int n, long ld, con
     }
     else if (dsel == 3) SRML_LR_PF_V(1, 3);
     else SRML_LR_PF_V(1, 2);
+    if (fws)
+      hipLaunchKernelGGL(fold_rows_kernel, dim3(ceil_div(wst, 1024), ceil_div(blocks, FOLD_ROWS)), dim3(256), 0, stream,
+                         fws, (int)blocks, wst, n, out, flag);
     return srml_status();
   }
   if (split == 1 && n > 1024 && n <= 4096) {

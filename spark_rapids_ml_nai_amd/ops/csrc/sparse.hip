@@ -100,7 +100,8 @@ template <typename T, int G, int K>
 __global__ __launch_bounds__(256) void csr_spmm_kernel(const long* __restrict__ indptr, const int* __restrict__ indices,
                                                        const T* __restrict__ data, long m,
                                                        const float* __restrict__ W, int kk,
-                                                       const float* __restrict__ bias, float* __restrict__ Z) {
+                                                       const float* __restrict__ bias, float* __restrict__ Z,
+                                                       long ldw, long ldz) {
   constexpr int GPB = 256 / G;
   const int g = threadIdx.x / G;
   const int l = threadIdx.x % G;
@@ -111,7 +112,7 @@ __global__ __launch_bounds__(256) void csr_spmm_kernel(const long* __restrict__ 
     const long p1 = indptr[r + 1];
     for (long p = indptr[r] + l; p < p1; p += G) {
       const float v = (float)data[p];
-      const float* wr = W + (long)indices[p] * kk;
+      const float* wr = W + (long)indices[p] * ldw;
 #pragma unroll
       for (int k = 0; k < K; ++k)
         if (k < kk) acc[k] = fmaf(v, wr[k], acc[k]);
@@ -121,7 +122,7 @@ __global__ __launch_bounds__(256) void csr_spmm_kernel(const long* __restrict__ 
     // lane k of the group writes column k
 #pragma unroll
     for (int k = 0; k < K; ++k)
-      if (k < kk && (k % G) == l) Z[r * kk + k] = acc[k] + (bias ? bias[k] : 0.f);
+      if (k < kk && (k % G) == l) Z[r * ldz + k] = acc[k] + (bias ? bias[k] : 0.f);
   }
 }
 
@@ -134,7 +135,8 @@ __global__ __launch_bounds__(256) void csr_spmm_cols_kernel(const long* __restri
                                                             const int* __restrict__ indices,
                                                             const T* __restrict__ data, long m,
                                                             const float* __restrict__ W, int kk,
-                                                            const float* __restrict__ bias, float* __restrict__ Z) {
+                                                            const float* __restrict__ bias, float* __restrict__ Z,
+                                                            long ldw, long ldz) {
   constexpr int GPB = 256 / G;
   const int g = threadIdx.x / G;
   const int l = threadIdx.x % G;
@@ -148,30 +150,31 @@ __global__ __launch_bounds__(256) void csr_spmm_cols_kernel(const long* __restri
       const int c0 = indices[p], c1 = indices[p + 1];
       const float v0 = (float)data[p], v1 = (float)data[p + 1];
       if (act) {
-        a0 = fmaf(v0, W[(long)c0 * kk + l], a0);
-        a1 = fmaf(v1, W[(long)c1 * kk + l], a1);
+        a0 = fmaf(v0, W[(long)c0 * ldw + l], a0);
+        a1 = fmaf(v1, W[(long)c1 * ldw + l], a1);
       }
     }
-    if (p < p1 && act) a0 = fmaf((float)data[p], W[(long)indices[p] * kk + l], a0);
-    if (act) Z[r * kk + l] = a0 + a1 + b0;
+    if (p < p1 && act) a0 = fmaf((float)data[p], W[(long)indices[p] * ldw + l], a0);
+    if (act) Z[r * ldz + l] = a0 + a1 + b0;
   }
 }
 
 template <typename T, int G, int K>
 __global__ __launch_bounds__(256) void csr_spmtm_kernel(const long* __restrict__ indptr, const int* __restrict__ indices,
                                                         const T* __restrict__ data, long m,
-                                                        const float* __restrict__ R, int kk, double* __restrict__ out) {
+                                                        const float* __restrict__ R, int kk, double* __restrict__ out,
+                                                        long ldr, long ldo) {
   constexpr int GPB = 256 / G;
   const int g = threadIdx.x / G;
   const int l = threadIdx.x % G;
   for (long r = (long)blockIdx.x * GPB + g; r < m; r += (long)gridDim.x * GPB) {
     float rr[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) rr[k] = k < kk ? R[r * kk + k] : 0.f;
+    for (int k = 0; k < K; ++k) rr[k] = k < kk ? R[r * ldr + k] : 0.f;
     const long p1 = indptr[r + 1];
     for (long p = indptr[r] + l; p < p1; p += G) {
       const double v = (double)data[p];
-      double* o = out + (long)indices[p] * kk;
+      double* o = out + (long)indices[p] * ldo;
 #pragma unroll
       for (int k = 0; k < K; ++k)
         if (k < kk && rr[k] != 0.f) atomicAdd(&o[k], v * (double)rr[k]);
@@ -231,9 +234,9 @@ static int csr_logreg_launch(const long* indptr, const int* indices, const T* da
 
 template <typename T, int K>
 static void csr_spmm_k(int G, dim3 grid, hipStream_t s, const long* indptr, const int* indices, const T* data, long m,
-                       const float* W, int kk, const float* bias, float* Z) {
+                       const float* W, int kk, const float* bias, float* Z, long ldw, long ldz) {
 #define SRML_CSR_MM(GG) \
-  hipLaunchKernelGGL((csr_spmm_kernel<T, GG, K>), grid, dim3(256), 0, s, indptr, indices, data, m, W, kk, bias, Z)
+  hipLaunchKernelGGL((csr_spmm_kernel<T, GG, K>), grid, dim3(256), 0, s, indptr, indices, data, m, W, kk, bias, Z, ldw, ldz)
   switch (G) {
     case 4: SRML_CSR_MM(4); break;
     case 8: SRML_CSR_MM(8); break;
@@ -246,48 +249,53 @@ static void csr_spmm_k(int G, dim3 grid, hipStream_t s, const long* indptr, cons
 
 template <typename T, int K>
 static void csr_spmtm_k(int G, dim3 grid, hipStream_t s, const long* indptr, const int* indices, const T* data, long m,
-                        const float* R, int kk, double* out) {
+                        const float* R, int kk, double* out, long ldr, long ldo) {
+#define SRML_CSR_TM(GG) \
+  hipLaunchKernelGGL((csr_spmtm_kernel<T, GG, K>), grid, dim3(256), 0, s, indptr, indices, data, m, R, kk, out, ldr, ldo)
   switch (G) {
-    case 4: hipLaunchKernelGGL((csr_spmtm_kernel<T, 4, K>), grid, dim3(256), 0, s, indptr, indices, data, m, R, kk, out); break;
-    case 8: hipLaunchKernelGGL((csr_spmtm_kernel<T, 8, K>), grid, dim3(256), 0, s, indptr, indices, data, m, R, kk, out); break;
-    case 16: hipLaunchKernelGGL((csr_spmtm_kernel<T, 16, K>), grid, dim3(256), 0, s, indptr, indices, data, m, R, kk, out); break;
-    case 32: hipLaunchKernelGGL((csr_spmtm_kernel<T, 32, K>), grid, dim3(256), 0, s, indptr, indices, data, m, R, kk, out); break;
-    default: hipLaunchKernelGGL((csr_spmtm_kernel<T, 64, K>), grid, dim3(256), 0, s, indptr, indices, data, m, R, kk, out); break;
+    case 4: SRML_CSR_TM(4); break;
+    case 8: SRML_CSR_TM(8); break;
+    case 16: SRML_CSR_TM(16); break;
+    case 32: SRML_CSR_TM(32); break;
+    default: SRML_CSR_TM(64); break;
   }
+#undef SRML_CSR_TM
 }
 
 template <typename T>
 static int csr_spmm_launch(const long* indptr, const int* indices, const T* data, long m, long nnz, const float* W,
-                           int kk, const float* bias, float* Z, hipStream_t s) {
+                           int kk, const float* bias, float* Z, long ldw, long ldz, hipStream_t s) {
   if (m <= 0) return 0;
-  if (kk < 1 || kk > 16) return (int)hipErrorInvalidValue;
+  if (kk < 1 || kk > 16 || ldw < kk || ldz < kk) return (int)hipErrorInvalidValue;
   if (kk > 4) {  // column-per-lane groups
     const int Gc = kk <= 8 ? 8 : 16;
     const dim3 gridc(grid_for(m, Gc));
     if (Gc == 8)
-      hipLaunchKernelGGL((csr_spmm_cols_kernel<T, 8>), gridc, dim3(256), 0, s, indptr, indices, data, m, W, kk, bias, Z);
+      hipLaunchKernelGGL((csr_spmm_cols_kernel<T, 8>), gridc, dim3(256), 0, s, indptr, indices, data, m, W, kk, bias, Z,
+                         ldw, ldz);
     else
-      hipLaunchKernelGGL((csr_spmm_cols_kernel<T, 16>), gridc, dim3(256), 0, s, indptr, indices, data, m, W, kk, bias, Z);
+      hipLaunchKernelGGL((csr_spmm_cols_kernel<T, 16>), gridc, dim3(256), 0, s, indptr, indices, data, m, W, kk, bias, Z,
+                         ldw, ldz);
     return srml_status();
   }
   const int G = pick_group(m, nnz);
   const dim3 grid(grid_for(m, G));
-  if (kk <= 4) csr_spmm_k<T, 4>(G, grid, s, indptr, indices, data, m, W, kk, bias, Z);
-  else if (kk <= 8) csr_spmm_k<T, 8>(G, grid, s, indptr, indices, data, m, W, kk, bias, Z);
-  else csr_spmm_k<T, 16>(G, grid, s, indptr, indices, data, m, W, kk, bias, Z);
+  if (kk <= 4) csr_spmm_k<T, 4>(G, grid, s, indptr, indices, data, m, W, kk, bias, Z, ldw, ldz);
+  else if (kk <= 8) csr_spmm_k<T, 8>(G, grid, s, indptr, indices, data, m, W, kk, bias, Z, ldw, ldz);
+  else csr_spmm_k<T, 16>(G, grid, s, indptr, indices, data, m, W, kk, bias, Z, ldw, ldz);
   return srml_status();
 }
 
 template <typename T>
 static int csr_spmtm_launch(const long* indptr, const int* indices, const T* data, long m, long nnz, const float* R,
-                            int kk, double* out, hipStream_t s) {
+                            int kk, double* out, long ldr, long ldo, hipStream_t s) {
   if (m <= 0) return 0;
-  if (kk < 1 || kk > 16) return (int)hipErrorInvalidValue;
+  if (kk < 1 || kk > 16 || ldr < kk || ldo < kk) return (int)hipErrorInvalidValue;
   const int G = pick_group(m, nnz);
   const dim3 grid(grid_for(m, G));
-  if (kk <= 4) csr_spmtm_k<T, 4>(G, grid, s, indptr, indices, data, m, R, kk, out);
-  else if (kk <= 8) csr_spmtm_k<T, 8>(G, grid, s, indptr, indices, data, m, R, kk, out);
-  else csr_spmtm_k<T, 16>(G, grid, s, indptr, indices, data, m, R, kk, out);
+  if (kk <= 4) csr_spmtm_k<T, 4>(G, grid, s, indptr, indices, data, m, R, kk, out, ldr, ldo);
+  else if (kk <= 8) csr_spmtm_k<T, 8>(G, grid, s, indptr, indices, data, m, R, kk, out, ldr, ldo);
+  else csr_spmtm_k<T, 16>(G, grid, s, indptr, indices, data, m, R, kk, out, ldr, ldo);
   return srml_status();
 }
 
@@ -313,19 +321,19 @@ SRML_API int srml_csr_logreg_binary_f64(const long* indptr, const int* indices, 
 }
 SRML_API int srml_csr_spmm_f32(const long* indptr, const int* indices, const float* data, long m, long nnz,
                                const float* W, int k, const float* bias, float* Z, hipStream_t s) {
-  return csr_spmm_launch<float>(indptr, indices, data, m, nnz, W, k, bias, Z, s);
+  return csr_spmm_launch<float>(indptr, indices, data, m, nnz, W, k, bias, Z, k, k, s);
 }
 SRML_API int srml_csr_spmm_f64(const long* indptr, const int* indices, const double* data, long m, long nnz,
                                const float* W, int k, const float* bias, float* Z, hipStream_t s) {
-  return csr_spmm_launch<double>(indptr, indices, data, m, nnz, W, k, bias, Z, s);
+  return csr_spmm_launch<double>(indptr, indices, data, m, nnz, W, k, bias, Z, k, k, s);
 }
 SRML_API int srml_csr_spmtm_f32(const long* indptr, const int* indices, const float* data, long m, long nnz,
                                 const float* R, int k, double* out, hipStream_t s) {
-  return csr_spmtm_launch<float>(indptr, indices, data, m, nnz, R, k, out, s);
+  return csr_spmtm_launch<float>(indptr, indices, data, m, nnz, R, k, out, k, k, s);
 }
 SRML_API int srml_csr_spmtm_f64(const long* indptr, const int* indices, const double* data, long m, long nnz,
                                 const float* R, int k, double* out, hipStream_t s) {
-  return csr_spmtm_launch<double>(indptr, indices, data, m, nnz, R, k, out, s);
+  return csr_spmtm_launch<double>(indptr, indices, data, m, nnz, R, k, out, k, k, s);
 }
 SRML_API int srml_csr_col_moments_f32(const int* indices, const float* data, long nnz, double* sum, double* sq,
                                       hipStream_t s) {
@@ -334,4 +342,46 @@ SRML_API int srml_csr_col_moments_f32(const int* indices, const float* data, lon
 SRML_API int srml_csr_col_moments_f64(const int* indices, const double* data, long nnz, double* sum, double* sq,
                                       hipStream_t s) {
   return csr_moments_launch<double>(indices, data, nnz, sum, sq, s);
+}
+
+// Strided panels (K > 16 classes in 16-column panels, no gather / scatter copies): W rows of
+// leading dim ldw, Z rows of leading dim ldz; R rows of leading dim ldr, out rows of ldo.
+SRML_API int srml_csr_spmm_ld_f32(const long* indptr, const int* indices, const float* data, long m, long nnz,
+                                  const float* W, int k, long ldw, const float* bias, float* Z, long ldz,
+                                  hipStream_t s) {
+  return csr_spmm_launch<float>(indptr, indices, data, m, nnz, W, k, bias, Z, ldw, ldz, s);
+}
+SRML_API int srml_csr_spmm_ld_f64(const long* indptr, const int* indices, const double* data, long m, long nnz,
+                                  const float* W, int k, long ldw, const float* bias, float* Z, long ldz,
+                                  hipStream_t s) {
+  return csr_spmm_launch<double>(indptr, indices, data, m, nnz, W, k, bias, Z, ldw, ldz, s);
+}
+SRML_API int srml_csr_spmtm_ld_f32(const long* indptr, const int* indices, const float* data, long m, long nnz,
+                                   const float* R, int k, long ldr, double* out, long ldo, hipStream_t s) {
+  return csr_spmtm_launch<float>(indptr, indices, data, m, nnz, R, k, out, ldr, ldo, s);
+}
+SRML_API int srml_csr_spmtm_ld_f64(const long* indptr, const int* indices, const double* data, long m, long nnz,
+                                   const float* R, int k, long ldr, double* out, long ldo, hipStream_t s) {
+  return csr_spmtm_launch<double>(indptr, indices, data, m, nnz, R, k, out, ldr, ldo, s);
+}
+
+// Row sums of a CSR matrix, accumulated in fp64 (one thread per row, no atomics): the UMAP
+// spectral-init degrees of the fuzzy graph.
+template <typename T>
+__global__ __launch_bounds__(256) void csr_row_sums_kernel(const long* __restrict__ indptr, const T* __restrict__ data,
+                                                           long m, double* __restrict__ out) {
+  for (long r = (long)blockIdx.x * 256 + threadIdx.x; r < m; r += (long)gridDim.x * 256) {
+    double acc = 0.0;
+    const long p1 = indptr[r + 1];
+    for (long p = indptr[r]; p < p1; ++p) acc += (double)data[p];
+    out[r] = acc;
+  }
+}
+
+SRML_API int srml_csr_row_sums_f32(const long* indptr, const float* data, long m, double* out, hipStream_t s) {
+  if (m <= 0) return 0;
+  long blocks = (m + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL((csr_row_sums_kernel<float>), dim3((unsigned)blocks), dim3(256), 0, s, indptr, data, m, out);
+  return srml_status();
 }

@@ -226,7 +226,10 @@ __global__ __launch_bounds__(256) void knn_refine_sort_kernel(const float* __res
     const float tot = wave_sum(acc);
     if (lane == j) my = metric == 0 ? tot : -2.f * tot;
   }
-  // bitonic sort of (my, lane) ascending across the wave
+  // bitonic sort of (my, lane) ascending across the wave. A NaN distance (NaN features) sorts as
+  // +inf: `<` / `==` give no order for NaN, which could let padding lanes (>= k) into the first k;
+  // +inf ties break by lane id, so every candidate lane (< k) still precedes the padding
+  if (my != my) my = __builtin_huge_valf();
   float v = my;
   int id = lane;
 #pragma unroll

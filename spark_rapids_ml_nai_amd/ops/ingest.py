@@ -192,7 +192,7 @@ def _staged_fill(blocks: list, out: torch.Tensor, device: torch.device, cs: "tor
         list(pool.map(lambda ds: np.copyto(ds[0], ds[1], casting="unsafe"), pieces))
         with torch.cuda.stream(cs):
             flat_out[row_out * n: (row_out + filled) * n].copy_(buf[: filled * n * esz].view(tdt), non_blocking=True)
-            e = torch.cuda.Event()
+            e = torch.cuda.Event(enable_timing=True)  # timed: the exposed-H2D accounting reads it
             e.record(cs)
         ring[s_i][1] = e
         yield row_out, row_out + filled, e
@@ -224,6 +224,7 @@ class StreamedParts:
         self._t0.record(self._copy)
         self._gen = _staged_fill(blocks, self.X, device, self._copy)
         self._last = None
+        self._stalls: list = []  # (compute-stream event before a wait, the copy event it waits on)
 
     def _finished(self) -> None:
         if self._t1 is None:
@@ -241,7 +242,7 @@ class StreamedParts:
         cur = torch.cuda.current_stream(self.device)
         for r0, r1, ev in self._gen:
             self._last = ev
-            cur.wait_event(ev)
+            _timed_wait(cur, ev, self._stalls)
             yield r0, r1, self.X[r0:r1]
         self._finished()
 
@@ -250,8 +251,31 @@ class StreamedParts:
             self._last = ev
         self._finished()
         if self._last is not None:
-            torch.cuda.current_stream(self.device).wait_event(self._last)
+            _timed_wait(torch.cuda.current_stream(self.device), self._last, self._stalls)
         return self.X
+
+    def exposed_seconds(self) -> float:
+        """Time the compute stream stood waiting for this transfer (the H2D NOT hidden under
+        compute); call after the fit has synchronised."""
+        return _stall_seconds(self._stalls)
+
+
+def _timed_wait(cur: "torch.cuda.Stream", ev: Any, stalls: list) -> None:
+    """``cur.wait_event(ev)`` with a timing event recorded on ``cur`` just before it: the gap
+    t(ev) - t(before), when positive, is how long the compute stream stood at this wait."""
+    before = torch.cuda.Event(enable_timing=True)
+    before.record(cur)
+    cur.wait_event(ev)
+    stalls.append((before, ev))
+
+
+def _stall_seconds(stalls: list) -> float:
+    tot = 0.0
+    for before, ev in stalls:
+        ev.synchronize()
+        before.synchronize()
+        tot += max(0.0, before.elapsed_time(ev)) / 1e3
+    return tot
 
 
 def host_to_device(X: Any, device: torch.device, dtype: Optional[torch.dtype] = None) -> Any:
@@ -339,6 +363,7 @@ class StreamedRows:
         self.X.record_stream(self._copy)
         self.bounds = []
         self.events = []
+        self._stalls: list = []
         self._t0 = torch.cuda.Event(enable_timing=True)
         self._t1 = torch.cuda.Event(enable_timing=True)
         with torch.cuda.stream(self._copy):
@@ -346,7 +371,7 @@ class StreamedRows:
             for r0 in range(0, m, self.chunk_rows):
                 r1 = min(m, r0 + self.chunk_rows)
                 self.X[r0:r1].copy_(t[r0:r1], non_blocking=True)
-                ev = torch.cuda.Event()
+                ev = torch.cuda.Event(enable_timing=True)
                 ev.record(self._copy)
                 self.bounds.append((r0, r1))
                 self.events.append(ev)
@@ -360,13 +385,18 @@ class StreamedRows:
     def chunks(self) -> Iterator[Any]:
         cur = torch.cuda.current_stream(self.device)
         for (r0, r1), ev in zip(self.bounds, self.events):
-            cur.wait_event(ev)
+            _timed_wait(cur, ev, self._stalls)
             yield r0, r1, self.X[r0:r1]
 
     def wait_all(self) -> torch.Tensor:
         if self.events:
-            torch.cuda.current_stream(self.device).wait_event(self.events[-1])
+            _timed_wait(torch.cuda.current_stream(self.device), self.events[-1], self._stalls)
         return self.X
+
+    def exposed_seconds(self) -> float:
+        """Time the compute stream stood waiting for this transfer (the H2D NOT hidden under
+        compute); call after the fit has synchronised."""
+        return _stall_seconds(self._stalls)
 
 
 def is_pinned(a: Any) -> bool:

@@ -148,6 +148,14 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_csr_spmm_f64": (_P, _P, _P, _L, _L, _P, _I, _P, _P, _P),
     "srml_csr_spmtm_f32": (_P, _P, _P, _L, _L, _P, _I, _P, _P),
     "srml_csr_spmtm_f64": (_P, _P, _P, _L, _L, _P, _I, _P, _P),
+    "srml_csr_spmm_ld_f32": (_P, _P, _P, _L, _L, _P, _I, _L, _P, _P, _L, _P),
+    "srml_csr_spmm_ld_f64": (_P, _P, _P, _L, _L, _P, _I, _L, _P, _P, _L, _P),
+    "srml_csr_spmtm_ld_f32": (_P, _P, _P, _L, _L, _P, _I, _L, _P, _L, _P),
+    "srml_csr_spmtm_ld_f64": (_P, _P, _P, _L, _L, _P, _I, _L, _P, _L, _P),
+    "srml_csr_row_sums_f32": (_P, _P, _L, _P, _P),
+    "srml_confusion_counts": (_P, _I, _P, _I, _L, _I, _P, _P),
+    "srml_logloss_sum": (_P, _I, _L, _I, _L, _P, _I, _D, _P, _P),
+    "srml_reg_moments": (_P, _I, _P, _I, _L, _P, _P),
     "srml_csr_col_moments_f32": (_P, _P, _L, _P, _P, _P),
     "srml_csr_col_moments_f64": (_P, _P, _L, _P, _P, _P),
     "srml_memcpy_h2d_async": (_P, _P, _L, _P),

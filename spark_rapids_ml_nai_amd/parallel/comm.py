@@ -14,7 +14,10 @@ Every numeric exchange here is a device collective on the compute stream:
 * ``allgather`` / ``allgatherv`` — ragged per-rank blocks (kNN partial results, RF forests).
 * ``broadcast``, ``barrier``, object collectives for tiny bootstrap metadata only.
 
-A world of size 1 short-circuits every call (no process group needed).
+A world of size 1 short-circuits every call (no process group needed), unless
+``SRML_COMM_FORCE_PG=1`` (test-only): then a size-1 communicator over an initialised process group
+runs every collective through the backend, so the RCCL code paths (event-timed ``CommStats``,
+``batch_isend_irecv``, ``allgatherv``, one-shot selection) execute on a one-GPU box.
 
 Accounting: every collective is counted (calls, payload bytes) and timed into ``Communicator.stats``
 (``CommStats``) — on RCCL by a pair of timing events on the compute stream around the call (so the
@@ -60,7 +63,10 @@ class Communicator:
         self.size = int(size)
         self.device = device if device is not None else torch.device("cpu")
         self.group = group
-        self._backend = dist.get_backend(group) if (size > 1 and dist.is_initialized()) else "none"
+        force = os.environ.get("SRML_COMM_FORCE_PG", "0") == "1" and dist.is_initialized()
+        # _solo: no peers and no process group to exercise -> every collective is the identity
+        self._solo = self.size == 1 and not force
+        self._backend = dist.get_backend(group) if (not self._solo and dist.is_initialized()) else "none"
         self.aborted = False
         self.stats = CommStats()
         self._oneshot: Any = None
@@ -114,7 +120,7 @@ class Communicator:
 
     def allreduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
         """In-place all-reduce; returns ``t``."""
-        if self.size == 1:
+        if self._solo:
             return t
         os_ = self._oneshot_for(t, op)
         with self._timed(t):
@@ -157,7 +163,7 @@ class Communicator:
 
     def allreduce_coalesced(self, tensors: Sequence[torch.Tensor], op: str = "sum") -> List[torch.Tensor]:
         """Pack same-dtype tensors into one flat buffer -> one collective -> unpack (in place)."""
-        if self.size == 1 or not tensors:
+        if self._solo or not tensors:
             return list(tensors)
         dtype = tensors[0].dtype
         assert all(t.dtype == dtype for t in tensors), "coalesced all-reduce needs one dtype"
@@ -172,7 +178,7 @@ class Communicator:
 
     def allgather(self, t: torch.Tensor) -> torch.Tensor:
         """Equal-shaped blocks -> concatenated along dim 0."""
-        if self.size == 1:
+        if self._solo:
             return t
         with self._timed(t):
             ct = self._comm_tensor(t.contiguous())
@@ -186,7 +192,7 @@ class Communicator:
         the sizes are all-gathered, each block is padded to the largest and ONE equal-shaped
         all-gather moves them (a single ring pass on RCCL instead of W per-root broadcasts; the
         padding is bounded by the imbalance, which the row-balanced partitioning keeps small)."""
-        if self.size == 1:
+        if self._solo:
             return [t]
         n = torch.tensor([t.shape[0]], dtype=torch.int64, device=self.device)
         sizes = self.allgather(n).tolist()
@@ -201,7 +207,7 @@ class Communicator:
         """Start a paired point-to-point exchange (send ``send`` to ``dst``, receive into ``recv``
         from ``src``; group-local ranks). Returns a handle for ``wait_sendrecv``. RCCL batches the
         pair into one group call (the ring steps of the kNN query pass); gloo stages through host."""
-        if self.size == 1:
+        if self._solo:
             recv.copy_(send)
             return None
         cs = self._comm_tensor(send.contiguous())
@@ -230,7 +236,7 @@ class Communicator:
         return recv
 
     def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
-        if self.size == 1:
+        if self._solo:
             return t
         with self._timed(t):
             ct = self._comm_tensor(t)
@@ -240,7 +246,7 @@ class Communicator:
         return t
 
     def barrier(self) -> None:
-        if self.size == 1:
+        if self._solo:
             return
         if self._backend == "nccl":
             # a tiny all-reduce is the stream-ordered barrier for RCCL
@@ -251,14 +257,14 @@ class Communicator:
             dist.barrier(group=self.group)
 
     def allgather_object(self, obj: Any) -> List[Any]:
-        if self.size == 1:
+        if self._solo:
             return [obj]
         out: List[Any] = [None] * self.size
         dist.all_gather_object(out, obj, group=self.group)
         return out
 
     def broadcast_object(self, obj: Any, src: int = 0) -> Any:
-        if self.size == 1:
+        if self._solo:
             return obj
         lst = [obj]
         dist.broadcast_object_list(lst, src=src, group=self.group)
@@ -266,7 +272,7 @@ class Communicator:
 
     def allgather_bytes(self, payload: bytes) -> List[bytes]:
         """Device all-gather of opaque byte blobs (e.g. serialized forests) — no driver hop."""
-        if self.size == 1:
+        if self._solo:
             return [payload]
         buf = torch.frombuffer(bytearray(payload), dtype=torch.uint8) if payload else torch.zeros(0, dtype=torch.uint8)
         parts = self.allgatherv(buf.to(self.device))
@@ -362,7 +368,24 @@ class CommStats:
         self.calls = 0
         self.bytes = 0
         self.host_s = 0.0
+        self._dev_s = 0.0  # resolved device spans (folded out of _pairs)
         self._pairs: List[Any] = []
+
+    _FOLD_AT = 256     # fold finished event pairs once this many are pending (non-blocking)
+    _HARD_CAP = 4096   # beyond this, wait for the oldest ones (a long-lived communicator's jobs)
+
+    def _fold(self) -> None:
+        """Resolve finished timing pairs into ``_dev_s`` so a communicator that lives across many
+        jobs (the SPMD context's transform / kneighbors / evaluate collectives) keeps a bounded
+        list; never blocks unless more than ``_HARD_CAP`` pairs are still in flight."""
+        i = 0
+        while i < len(self._pairs) and (self._pairs[i][1].query() or len(self._pairs) - i > self._HARD_CAP):
+            s, e = self._pairs[i]
+            e.synchronize()
+            self._dev_s += s.elapsed_time(e) / 1e3
+            i += 1
+        if i:
+            del self._pairs[:i]
 
     @contextlib.contextmanager
     def record(self, nbytes: int, device: Optional[torch.device], count: bool = True) -> Iterator[None]:
@@ -377,6 +400,8 @@ class CommStats:
             finally:
                 e.record()
                 self._pairs.append((s, e))
+                if len(self._pairs) >= self._FOLD_AT:
+                    self._fold()
             return
         t0 = time.perf_counter()
         try:
@@ -385,11 +410,11 @@ class CommStats:
             self.host_s += time.perf_counter() - t0
 
     def seconds(self) -> float:
-        dev = 0.0
         if self._pairs:
             self._pairs[-1][1].synchronize()
-            dev = sum(s.elapsed_time(e) for s, e in self._pairs) / 1e3
-        return self.host_s + dev
+            self._dev_s += sum(s.elapsed_time(e) for s, e in self._pairs) / 1e3
+            self._pairs = []
+        return self.host_s + self._dev_s
 
     def snapshot(self) -> dict:
         return {"comm_s": round(self.seconds(), 6), "comm_calls": self.calls, "comm_bytes": self.bytes}

@@ -117,10 +117,18 @@ class WorkerContext:
     comm: Communicator = field(default_factory=Communicator)
     partition_id: int = 0
     timers: dict = field(default_factory=dict)
+    # transform-evaluate passes set this: predict functions then hand back device tensors (the
+    # metric partials are computed where the predictions are) instead of host arrays
+    device_outputs: bool = False
 
     @property
     def is_gpu(self) -> bool:
         return self.device.type == "cuda"
+
+    def output(self, t: torch.Tensor) -> Any:
+        """A predict function's output column: the device tensor itself in a transform-evaluate
+        pass (``device_outputs``), otherwise a host numpy array."""
+        return t if self.device_outputs else t.cpu().numpy()
 
     def sync(self) -> None:
         if self.is_gpu:

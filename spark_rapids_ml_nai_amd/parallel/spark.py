@@ -60,33 +60,59 @@ def _ver(v: str) -> Tuple[int, ...]:
 
 
 def stage_level_scheduling_plan(spark_version: str, conf: Dict[str, Optional[str]], master: str,
-                                spark_plugins: str = "", rapids_sql_enabled: str = "true"
-                                ) -> Optional[Tuple[int, float]]:
-    """(task_cores, task_gpus) for the training stage, or None to leave scheduling alone."""
+                                spark_plugins: str = "", rapids_sql_enabled: str = "true",
+                                reasons: Optional[List[str]] = None) -> Optional[Tuple[int, float]]:
+    """(task_cores, task_gpus) for the training stage, or None to leave scheduling alone.
+    ``reasons`` (optional list) receives the decision in words, as the reference logs it
+    (``core.py:906-1004``)."""
+    why = reasons if reasons is not None else []
     if master.startswith("local[") or master == "local":
+        why.append("Stage level scheduling is not needed in local mode (%s)." % master)
         return None
     if _ver(spark_version) < (3, 4, 0):
+        why.append("Stage level scheduling requires spark version 3.4.0+ (found %s)." % spark_version)
         return None
     standalone = master.startswith("spark://") or master.startswith("local-cluster")
     if (3, 4, 0) <= _ver(spark_version) < (3, 5, 1) and not standalone:
+        why.append("Stage level scheduling on spark %s is supported only on standalone or local-cluster mode."
+                   % spark_version)
         return None
     cores, gpus = conf.get("spark.executor.cores"), conf.get("spark.executor.resource.gpu.amount")
-    if cores is None or gpus is None or int(cores) == 1 or float(gpus) > 1:
+    if cores is None or gpus is None:
+        why.append("Stage level scheduling requires spark.executor.cores and "
+                   "spark.executor.resource.gpu.amount to be set.")
+        return None
+    if int(cores) == 1:
+        why.append("Stage level scheduling is skipped: spark.executor.cores = 1 leaves nothing to reserve.")
+        return None
+    if float(gpus) > 1:
+        why.append("Stage level scheduling is skipped: more than one GPU per executor "
+                   "(spark.executor.resource.gpu.amount = %s)." % gpus)
         return None
     task_gpus = conf.get("spark.task.resource.gpu.amount")
     if task_gpus is not None and float(task_gpus) == float(gpus):
+        why.append("Stage level scheduling is skipped: spark.task.resource.gpu.amount already equals the "
+                   "executor's GPU amount, so a training task owns its GPU.")
         return None
     plugin_sql = "SQLPlugin" in (spark_plugins or "") and (rapids_sql_enabled or "true").lower() == "true"
     task_cores = int(cores) if plugin_sql else int(cores) // 2 + 1
+    why.append("Training tasks require the resource(cores=%d, gpu=1.0)%s." %
+               (task_cores, " (the SQL plugin is on: all executor cores)" if plugin_sql else ""))
     return task_cores, 1.0
 
 
 def _try_stage_level_scheduling(rdd: Any, spark: Any) -> Any:
+    from ..utils.log import get_logger
+
     sc = spark.sparkContext
     conf = {k: sc.getConf().get(k) for k in ("spark.executor.cores", "spark.executor.resource.gpu.amount",
                                              "spark.task.resource.gpu.amount")}
+    reasons: List[str] = []
     plan = stage_level_scheduling_plan(spark.version, conf, sc.master, spark.conf.get("spark.plugins", ""),
-                                       spark.conf.get("spark.rapids.sql.enabled", "true"))
+                                       spark.conf.get("spark.rapids.sql.enabled", "true"), reasons)
+    log = get_logger("stage_level_scheduling")
+    for r in reasons:
+        log.info(r)
     if plan is None:
         return rdd
     from pyspark.resource.profile import ResourceProfileBuilder  # type: ignore
@@ -394,7 +420,8 @@ def spark_transform(model: Any, sdf: Any) -> Any:
         # scalar-iterator pandas UDF and keep every original column (reference core.py:1537-1557)
         return _spark_transform_udf(model, sdf, out_fields)
     sdf_u, vec = _unwrap_vectors(sdf)
-    blob = cloudpickle.dumps((model, vec))
+    blob = cloudpickle.dumps((_task_model(model, sdf), vec))
+    model._spark_closure_bytes = len(blob)
 
     def _predict(it: Iterator[Any]) -> Iterator[Any]:
         import torch
@@ -428,6 +455,27 @@ def spark_transform(model: Any, sdf: Any) -> Any:
     out_schema = StructType(list(schema.fields) + out_fields)
     out = sdf_u.mapInArrow(_predict, schema=out_schema)
     return _wrap_vector_outputs(model, out, out_fields, False)
+
+
+def _task_model(model: Any, sdf: Any) -> Any:
+    """What the transform tasks unpickle: the model itself, or — for models holding training
+    data (UMAP: embedding + raw rows) — a light copy whose arrays travel as chunked Spark
+    broadcasts (``_spark_task_model``), so the task closure stays small at any data size."""
+    hook = getattr(model, "_spark_task_model", None)
+    return hook(sdf.sparkSession) if hook is not None else model
+
+
+def collect_arrow(sdf: Any) -> Any:
+    """The rows of ``sdf`` on the driver as ONE Arrow table (Spark 4 ``toArrow``, the Arrow
+    collection behind ``toPandas`` on older versions, or a pandas round trip)."""
+    import pyarrow as pa
+
+    if hasattr(sdf, "toArrow"):
+        return sdf.toArrow()
+    if hasattr(sdf, "_collect_as_arrow"):
+        rbs = sdf._collect_as_arrow()
+        return pa.Table.from_batches(rbs) if rbs else None
+    return pa.Table.from_pandas(sdf.toPandas(), preserve_index=False)
 
 
 def _vector_columns(sdf: Any) -> List[str]:
@@ -471,7 +519,8 @@ def _spark_transform_udf(model: Any, sdf: Any, out_fields: List[Any]) -> Any:
     vec = _vector_columns(sdf)
     dt = "float32" if getattr(model, "_float32_inputs", True) else "float64"
     inputs = [vector_to_array(F.col(c), dt).alias(c) if c in vec else F.col(c) for c in ([col] if col else cols)]
-    blob = cloudpickle.dumps(model)
+    blob = cloudpickle.dumps(_task_model(model, sdf))
+    model._spark_closure_bytes = len(blob)
 
     def _udf(it: Iterator[pd.DataFrame]) -> Iterator[pd.DataFrame]:
         import torch

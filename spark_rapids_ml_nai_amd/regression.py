@@ -262,7 +262,7 @@ class LinearRegressionModel(LinearRegressionClass, _ModelWithPredictionCol, _Lin
             from .models.linear import linear_predict
 
             Xd = to_device(X, ctx.device, w.dtype)
-            return {pred_col: linear_predict(Xd, w, intercept).double().cpu().numpy()}
+            return {pred_col: ctx.output(linear_predict(Xd, w, intercept).double())}
 
         return construct, predict
 
@@ -331,7 +331,7 @@ class RandomForestRegressionModel(_RandomForestModel):
 
         def predict(device: Any, X: Any, ctx: WorkerContext) -> Dict[str, np.ndarray]:
             raw = self._raw_sum(X, ctx.device)
-            return {pc: (raw[:, 0] / T).cpu().numpy()}
+            return {pc: ctx.output(raw[:, 0] / T)}
 
         return construct, predict
 

@@ -146,9 +146,12 @@ def _umap_fit_worker(ctx: WorkerContext, payload: Tuple[Any, ...]) -> Tuple[np.n
 
 def _spark_umap_task(ctx: WorkerContext, table: Any, extra: Tuple[Any, ...]) -> Any:
     """One rank of the Spark UMAP fit (barrier job): the ranks' rows are device-gathered and fitted
-    together (``_umap_fit_worker``); rank 0 returns (embedding, training rows). The reference fits in
-    ONE non-barrier task on one GPU (``umap.py:830-909``); ``num_workers=1`` gives exactly that."""
-    col, cols, label_col, params = extra
+    together (``_umap_fit_worker``); rank 0 then YIELDS the result as Arrow record batches of at most
+    ``maxRecordsPerBatch`` rows — one row per training sample, ``embedding_`` and ``raw_data_`` as
+    float lists — so no Arrow cell / task result holds the whole model (the reference streams
+    ``maxRecordsPerBatch``-row sections, ``umap.py:1060-1073``). The reference fits in ONE
+    non-barrier task on one GPU (``umap.py:830-909``); ``num_workers=1`` gives exactly that."""
+    col, cols, label_col, params, rows_per_batch = extra
     if table is not None and table.num_rows:
         part = DataFrame([table])
         X = _dense_from_df(part, col, cols, np.float32)
@@ -159,11 +162,66 @@ def _spark_umap_task(ctx: WorkerContext, table: Any, extra: Tuple[Any, ...]) -> 
     ctx.comm.allreduce(nt, op="max")
     if X is None:
         X = np.zeros((0, int(nt.item())), np.float32)
-    return _umap_fit_worker(ctx, (X, y, params))
+    emb, Xall = _umap_fit_worker(ctx, (X, y, params))
+    if emb is None:
+        return
+    import pyarrow as pa
+
+    from .core.dataframe import dense_to_list_array
+
+    step = max(1, int(rows_per_batch))
+    for r0 in range(0, emb.shape[0], step):
+        yield pa.RecordBatch.from_arrays([dense_to_list_array(np.ascontiguousarray(emb[r0: r0 + step])),
+                                          dense_to_list_array(np.ascontiguousarray(Xall[r0: r0 + step]))],
+                                         names=["embedding_", "raw_data_"])
+
+
+def _chunk_rows(arr: np.ndarray, limit: int) -> List[np.ndarray]:
+    """Row slices of ``arr`` of at most ``limit`` bytes each (one row at least): the pieces that
+    are broadcast separately (reference ``_chunk_arr``, ``umap.py:873-885``)."""
+    if arr.nbytes <= limit or arr.shape[0] <= 1:
+        return [arr]
+    row_bytes = max(1, arr.nbytes // arr.shape[0])
+    step = max(1, int(limit) // row_bytes)
+    return [arr[i: i + step] for i in range(0, arr.shape[0], step)]
+
+
+class _BroadcastChunks:
+    """A driver array shipped to Spark tasks as a list of broadcasts (each <= BROADCAST_LIMIT);
+    ``value()`` reassembles it once per executor process (cached by ``key``)."""
+
+    _cache: Dict[str, np.ndarray] = {}
+
+    def __init__(self, spark: Any, arr: np.ndarray, limit: int, key: str) -> None:
+        self.key = key
+        self.shape = tuple(arr.shape)
+        self.chunks = [spark.sparkContext.broadcast(c) for c in _chunk_rows(arr, limit)]
+
+    def __len__(self) -> int:
+        return len(self.chunks)
+
+    def value(self) -> np.ndarray:
+        v = _BroadcastChunks._cache.get(self.key)
+        if v is None:
+            parts = [np.asarray(b.value) for b in self.chunks]
+            v = parts[0] if len(parts) == 1 else np.concatenate(parts, 0)
+            _BroadcastChunks._cache.clear()  # keep one model's training data per executor process
+            _BroadcastChunks._cache[self.key] = v
+        return v
+
+    def unpersist(self) -> None:
+        for b in self.chunks:
+            try:
+                b.unpersist()
+            except Exception:  # noqa: BLE001
+                pass
 
 
 class UMAP(UMAPClass, _Estimator, _UMAPParams):
     """Uniform Manifold Approximation and Projection.
+
+    ``BROADCAST_LIMIT`` (bytes, default 8 GiB like the reference): the fitted embedding and raw
+    rows reach Spark transform tasks as broadcasts of at most this size each.
 
     >>> from spark_rapids_ml_nai_amd.umap import UMAP
     >>> model = UMAP(n_neighbors=15, n_components=2, random_state=1).fit(df)  # doctest: +SKIP
@@ -184,6 +242,8 @@ class UMAP(UMAPClass, _Estimator, _UMAPParams):
         super().__init__()
         self._set_params(**self._input_kwargs)
 
+    BROADCAST_LIMIT = 8 << 30
+
     def _get_fit_func(self, dataset: DataFrame, extra_params: Optional[List[Dict[str, Any]]] = None) -> Callable:
         raise NotImplementedError("UMAP fits through _fit")
 
@@ -200,9 +260,21 @@ class UMAP(UMAPClass, _Estimator, _UMAPParams):
         col, cols = (fc, None) if isinstance(fc, str) else (None, list(fc))
         label = self.getLabelCol() if self.isDefined("labelCol") and self.getLabelCol() in sdf.columns else None
         sel = ([col] if col else list(cols)) + ([label] if label else [])
-        res = spark_barrier_job(sdf.select(*sel).repartition(max(1, self.num_workers)), _spark_umap_task,
-                                (col, cols, label, self._umap_params()))
-        return res[0]
+        from pyspark.sql.types import ArrayType, FloatType, StructField, StructType  # type: ignore
+
+        from .parallel.spark import collect_arrow
+
+        rows = int(sdf.sparkSession.conf.get("spark.sql.execution.arrow.maxRecordsPerBatch", "10000"))
+        schema = StructType([StructField("embedding_", ArrayType(FloatType(), False), False),
+                             StructField("raw_data_", ArrayType(FloatType(), False), False)])
+        out = spark_barrier_job(sdf.select(*sel).repartition(max(1, self.num_workers)), _spark_umap_task,
+                                (col, cols, label, self._umap_params(), rows), out_schema=schema)
+        t = collect_arrow(out)
+        from .core.dataframe import array_column_to_dense
+
+        self._fit_result_batches = int(sum(c.num_chunks for c in t.columns[:1]))
+        return (array_column_to_dense(t.column("embedding_"), np.float32),
+                array_column_to_dense(t.column("raw_data_"), np.float32))
 
     def _fit(self, dataset: Any) -> "UMAPModel":
         from .parallel.spark import is_spark_dataframe
@@ -239,6 +311,7 @@ class UMAP(UMAPClass, _Estimator, _UMAPParams):
 
     def _make_model(self, emb: np.ndarray, Xall: np.ndarray) -> "UMAPModel":
         model = UMAPModel(embedding_=emb, raw_data_=Xall, n_cols=int(Xall.shape[1]), dtype="float32")
+        model.BROADCAST_LIMIT = int(self.BROADCAST_LIMIT)
         model._num_workers = self._num_workers
         model._float32_inputs = True
         self._copyValues(model)
@@ -247,6 +320,8 @@ class UMAP(UMAPClass, _Estimator, _UMAPParams):
 
 
 class UMAPModel(UMAPClass, _Model, _UMAPParams):
+    BROADCAST_LIMIT = 8 << 30
+
     def __init__(self, embedding_: Any, raw_data_: Any, n_cols: int, dtype: str) -> None:
         emb = np.asarray(embedding_, dtype=np.float32)
         raw = np.asarray(raw_data_, dtype=np.float32)
@@ -264,13 +339,39 @@ class UMAPModel(UMAPClass, _Model, _UMAPParams):
     def raw_data(self) -> List[List[float]]:
         return self.raw_data_.tolist()
 
+    def _spark_task_model(self, spark: Any) -> "UMAPModel":
+        """The copy of this model that Spark transform tasks unpickle: embedding and raw rows as
+        chunked broadcasts (<= BROADCAST_LIMIT bytes each, reference ``umap.py:873-895``), created
+        once per model and reused by later transforms; nothing large is pickled into the closure."""
+        import copy
+        import uuid
+
+        bc = getattr(self, "_broadcasts", None)
+        if bc is None or bc[0] != int(self.BROADCAST_LIMIT):
+            key = uuid.uuid4().hex
+            bc = (int(self.BROADCAST_LIMIT),
+                  _BroadcastChunks(spark, self.embedding_, self.BROADCAST_LIMIT, key + "e"),
+                  _BroadcastChunks(spark, self.raw_data_, self.BROADCAST_LIMIT, key + "r"))
+            self._broadcasts = bc
+        light = copy.copy(self)
+        light.embedding_ = np.zeros((0,) + self.embedding_.shape[1:], np.float32)
+        light.raw_data_ = np.zeros((0,) + self.raw_data_.shape[1:], np.float32)
+        light._model_attributes = {k: v for k, v in self._model_attributes.items()
+                                   if k not in ("embedding_", "raw_data_")}
+        light._device_state_cache = {}
+        light._broadcasts = None
+        light._sources = (bc[1], bc[2])
+        return light
+
     def _get_transform_func(self, dataset: DataFrame) -> Tuple[Callable, Callable]:
         params = self._umap_params()
         out_col = self.getOutputCol()
-        emb, raw = self.embedding_, self.raw_data_
+        src = getattr(self, "_sources", None)
+        emb, raw = (self.embedding_, self.raw_data_) if src is None else src
 
         def construct(ctx: WorkerContext) -> Tuple[torch.Tensor, torch.Tensor]:
-            return torch.from_numpy(raw).to(ctx.device), torch.from_numpy(emb).to(ctx.device)
+            e, r = (emb, raw) if src is None else (emb.value(), raw.value())
+            return torch.from_numpy(r).to(ctx.device), torch.from_numpy(e).to(ctx.device)
 
         def predict(state: Tuple[torch.Tensor, torch.Tensor], X: Any, ctx: WorkerContext) -> Dict[str, np.ndarray]:
             from .core.base import to_device

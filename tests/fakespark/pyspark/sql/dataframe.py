@@ -59,9 +59,42 @@ class _Conf:
         self._d[k] = str(v)
 
 
+_BROADCASTS: Dict[int, Any] = {}
+
+
+def _broadcast_lookup(bid: int) -> "Broadcast":
+    return _BROADCASTS[bid]
+
+
+class Broadcast:
+    """Like Spark's: pickles as a reference to the driver-registered value (a task closure that
+    holds one stays small); ``value`` resolves it where the task runs (in process here)."""
+
+    def __init__(self, value: Any):
+        self.id = len(_BROADCASTS)
+        self._value = value
+        _BROADCASTS[self.id] = self
+
+    @property
+    def value(self) -> Any:
+        return self._value
+
+    def unpersist(self, blocking: bool = False) -> None:
+        pass
+
+    def __reduce__(self):
+        return (_broadcast_lookup, (self.id,))
+
+
 class _SparkContext:
     def __init__(self, conf: _Conf, master: str):
         self._conf, self.master = conf, master
+        self.broadcasts: List[Broadcast] = []
+
+    def broadcast(self, value: Any) -> Broadcast:
+        b = Broadcast(value)
+        self.broadcasts.append(b)
+        return b
 
     def getConf(self):
         return self._conf

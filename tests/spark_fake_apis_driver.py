@@ -83,6 +83,28 @@ def main() -> None:
     out["umap_embedding_shape"] = list(np.asarray(um.embedding_).shape)
     out["umap_transform_columns"] = ut.schema.names
     out["umap_transform_rows"] = ut.num_rows
+    # chunked path (reference tests/test_umap.py:333-377): the fit streams maxRecordsPerBatch (64)
+    # row batches back, a tiny BROADCAST_LIMIT splits embedding / raw rows into several broadcasts,
+    # the task closure stays small, and fit + transform equal the in-process ones
+    est = UMAP(n_neighbors=10, n_epochs=60, random_state=0, num_workers=1, featuresCol="features")
+    est.BROADCAST_LIMIT = 2000  # bytes: 300 x 6 fp32 raw rows -> 4 chunks, 300 x 2 embedding -> 2
+    uc = est.fit(sdf(Xu, parts=1))
+    local_m = UMAP(n_neighbors=10, n_epochs=60, random_state=0, featuresCol="features").fit(SRDF.from_numpy(Xu))
+    out["umap_fit_batches"] = est._fit_result_batches
+    out["umap_chunked_fit_equal"] = bool(np.array_equal(uc.raw_data_, Xu)) and bool(
+        np.allclose(uc.embedding_, local_m.embedding_, atol=1e-5))
+    n_bc0 = len(spark.sparkContext.broadcasts)
+    tc = uc.transform(sdf(Xu, parts=2)).toArrow()
+    out["umap_broadcasts"] = [len(uc._broadcasts[1]), len(uc._broadcasts[2])]
+    out["umap_new_broadcasts"] = len(spark.sparkContext.broadcasts) - n_bc0
+    out["umap_closure_bytes"] = int(uc._spark_closure_bytes)
+    out["umap_raw_bytes"] = int(Xu.nbytes)
+    emb_t = np.asarray(tc.column("embedding").to_pylist(), np.float32)
+    uc.transform(sdf(Xu, parts=2)).toArrow()  # a second transform reuses the broadcasts
+    out["umap_new_broadcasts_2nd"] = len(spark.sparkContext.broadcasts) - n_bc0
+    uc.BROADCAST_LIMIT = 8 << 30  # one broadcast per array: the same transform, unchunked
+    emb_1 = np.asarray(uc.transform(sdf(Xu, parts=2)).toArrow().column("embedding").to_pylist(), np.float32)
+    out["umap_chunked_transform_maxdiff"] = float(np.abs(emb_t - emb_1).max())
 
     # ---- VectorUDT outputs: probability / rawPrediction always, PCA output mirrors a vector input
     from spark_rapids_ml_nai_amd.classification import LogisticRegression

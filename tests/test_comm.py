@@ -107,7 +107,8 @@ def test_bench_self_spawns_ranks():
     """``bench.py --gpus 2`` without a launcher runs 2 ranks and reports them with a per-rank split."""
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--rows", "4000", "--cols",
                         "16", "--algos", "pca,logistic_regression", "--steps", "1", "--warmup", "0", "--no-transform"],
-                       env=_bench_env(), capture_output=True, text=True, timeout=900, cwd=ROOT)
+                       env=dict(_bench_env(), SRML_LOG_LEVEL="INFO"), capture_output=True, text=True, timeout=900,
+                       cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == 2 and line["config"]["parallelism"] == "dp2"
@@ -116,6 +117,18 @@ def test_bench_self_spawns_ranks():
         assert [p["rank"] for p in pr] == [0, 1], name
         for p in pr:
             assert p["comm_calls"] > 0 and p["wall_s"] > 0 and p["compute_s"] <= p["wall_s"] + 1e-9
+            # the split adds up: wall = exposed H2D + compute + collectives (within 5 %)
+            parts = p["h2d_exposed_s"] + p["compute_s"] + p["comm_s"]
+            assert abs(parts - p["wall_s"]) <= 0.05 * p["wall_s"] + 1e-6, (name, p)
+    # the estimator logger prints one line per rank of every timed fit (from rank 0 only), plus the
+    # worker stages of each rank
+    for est in ("PCA", "LogisticRegression"):
+        for rk in (0, 1):
+            lines = [ln for ln in r.stderr.splitlines() if "srml.%s - INFO - %s fit rank %d:" % (est, est, rk) in ln]
+            assert len(lines) == 1, (est, rk, r.stderr[-3000:])
+    for stage in ("Loading data", "Initializing context", "Invoking fit", "Fit complete"):
+        for rk in (0, 1):
+            assert "rank %d/2: %s" % (rk, stage) in r.stderr, (stage, rk)
 
 
 _MISSING_PEER = textwrap.dedent("""

@@ -105,7 +105,8 @@ def test_row_sqnorm(gpu_device):
     torch.testing.assert_close(ops.row_sqnorm(X).cpu().double(), (X.double() ** 2).sum(1).cpu(), rtol=1e-5, atol=1e-4)
 
 
-@pytest.mark.parametrize("m,n", [(500, 7), (4000, 256), (3000, 1000), (5000, 3000), (2000, 4096), (1000, 1500)])
+@pytest.mark.parametrize("m,n", [(500, 7), (4000, 256), (3000, 1000), (5000, 3000), (2000, 4096), (1000, 1500),
+                                 (130001, 2052)])
 def test_logreg_binary_loss_grad(gpu_device, m, n):
     X = _rand(m, n, gpu_device, seed=14) * 0.1
     y = (torch.rand(m, generator=torch.Generator().manual_seed(1)) > 0.5).float().to(gpu_device)
@@ -120,6 +121,10 @@ def test_logreg_binary_loss_grad(gpu_device, m, n):
     torch.testing.assert_close(out[:n], Xd.T @ r, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(out[n], r.sum(), rtol=1e-6, atol=1e-6)
     torch.testing.assert_close(out[n + 1], loss, rtol=1e-7, atol=1e-6)
+    # the grouped-fold epilogue's counters reset themselves: repeated launches agree
+    for _ in range(2):
+        again = ops.logreg_binary_loss_grad(X, y, w, b).cpu()
+        torch.testing.assert_close(again, out, rtol=1e-5, atol=1e-5)
 
 
 @pytest.mark.parametrize("m,n,k", [(1000, 16, 20), (3000, 64, 5), (2000, 300, 130), (1024, 3000, 257), (777, 33, 1)])

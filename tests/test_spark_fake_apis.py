@@ -49,6 +49,17 @@ def test_umap_spark_fit_transform(result):
     assert result["umap_transform_columns"] == ["features", "embedding"] and result["umap_transform_rows"] == 300
 
 
+def test_umap_spark_chunked(result):
+    """Reference tests/test_umap.py:333-377: tiny limits force several fit batches and broadcasts;
+    the result equals the in-process fit / transform and no training data rides in the closure."""
+    assert result["umap_fit_batches"] == 5  # 300 rows / maxRecordsPerBatch 64
+    assert result["umap_chunked_fit_equal"]
+    assert result["umap_broadcasts"] == [2, 4] and result["umap_new_broadcasts"] == 6
+    assert result["umap_new_broadcasts_2nd"] == 6  # reused, not re-broadcast
+    assert result["umap_closure_bytes"] < result["umap_raw_bytes"]
+    assert result["umap_chunked_transform_maxdiff"] < 1e-4
+
+
 def test_vector_udt_outputs(result):
     assert result["lr_types"]["probability"] == result["lr_types"]["rawPrediction"] == "VectorUDT"
     assert result["lr_types"]["features"] == "ArrayType"
