@@ -59,6 +59,29 @@ WIDE_ROWS_MAX = 65536
 # fixed point; deterministic mode always does
 RF_PACK = os.environ.get("SRML_RF_PACK", "1") != "0"
 INT_MAX = 2**31 - 1
+# data-parallel forests: each level's histograms are REDUCE-SCATTERED by node (every rank gets the
+# summed histograms of 1/W of the candidate nodes), each rank searches its nodes' splits and only
+# the per-node split records + left-child totals are all-gathered — half the wire bytes of
+# all-reducing every histogram, identical splits. SRML_RF_DP_SCATTER=0: all-reduce every histogram.
+RF_DP_SCATTER = os.environ.get("SRML_RF_DP_SCATTER", "1") != "0"
+# sibling subtraction (nodes that see every feature, featureSubsetStrategy="all"): from depth 1 only
+# the smaller child of each split is histogrammed (and, data-parallel, all-reduced); the larger is
+# its parent's histogram minus the smaller's. Per-node feature sampling draws a fresh subset per
+# node, so there the parent's histogram does not cover the children's features and every node is
+# built. SRML_RF_SIBLING_SUB=0 turns it off.
+RF_SIBLING_SUB = os.environ.get("SRML_RF_SIBLING_SUB", "1") != "0"
+
+
+def _left_totals(hist: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """(C, S) fp64 class totals of each node's left child under its best split (zeros for nodes
+    without one): the winning feature's histogram summed up to the split bin."""
+    C = hist.shape[0]
+    ok = out[:, 1] >= 0
+    slot = torch.where(ok, out[:, 1], torch.zeros_like(out[:, 1])).long()
+    b = torch.where(ok, out[:, 2], torch.zeros_like(out[:, 2])).long()
+    ar = torch.arange(C, device=hist.device)
+    left = hist[ar, slot].double().cumsum(1)[ar, b]  # (C, S)
+    return torch.where(ok.view(-1, 1), left, torch.zeros_like(left))
 
 
 def feature_subset_size(strategy: Any, n: int, n_trees: int, classification: bool) -> int:
@@ -290,6 +313,28 @@ def _root_hist_streamed(pending: PendingBins, bins: torch.Tensor, idx: torch.Ten
     return hist
 
 
+def _expand_siblings(built: torch.Tensor, derive: np.ndarray, sib_pos: np.ndarray, prev_hist: torch.Tensor,
+                     parent_row: np.ndarray) -> torch.Tensor:
+    """Histograms of every candidate (cand order) from the built ones (cand[~derive] order): a
+    derived node's histogram is its parent's minus its (built) sibling's."""
+    dev = built.device
+    C = derive.size
+    full = torch.empty((C,) + tuple(built.shape[1:]), dtype=built.dtype, device=dev)
+    bpos = torch.from_numpy(np.nonzero(~derive)[0]).to(dev)
+    full.index_copy_(0, bpos, built)
+    d = np.nonzero(derive)[0]
+    if d.size:
+        dpos = torch.from_numpy(d).to(dev)
+        par = prev_hist.index_select(0, torch.from_numpy(parent_row[d]).to(dev))
+        full.index_copy_(0, dpos, par - full.index_select(0, torch.from_numpy(sib_pos[d]).to(dev)))
+    return full
+
+
+def _pad_rows(t: torch.Tensor, rows: int) -> torch.Tensor:
+    """``t`` with zero rows appended up to ``rows``."""
+    return torch.cat([t, torch.zeros((rows - t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)], 0)
+
+
 def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: WorkerContext,
                 gen: torch.Generator, p: Dict[str, Any], S: int, regression: bool, data_parallel: bool,
                 gen_boot: Optional[torch.Generator], n_trees: int, pending: Optional[PendingBins] = None) -> List[Tree]:
@@ -357,6 +402,11 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
     yscale = ops.rf_yscale(yv, float(tot[:, 0].max().item())) if regression and dev.type == "cuda" else None
     hist_cell = (8 if regression else 4) * nf * B * SH
     group = max(1, HIST_BUDGET_BYTES // max(hist_cell, 1))
+    W = ctx.world_size
+    sib_sub = RF_SIBLING_SUB and nf >= n
+    scatter = data_parallel and W > 1 and RF_DP_SCATTER and not sib_sub
+    prev_hist: Optional[torch.Tensor] = None  # last level's candidate histograms (cand order), summed
+    prev_parent = None  # per segment: its parent's row of prev_hist
     depth = 0
     while len(seg_tree):
         L = len(seg_tree)
@@ -374,15 +424,29 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
         # ---- histograms + split search, in groups of candidate segments bounded by memory ----
         res_out: List[np.ndarray] = []
         res_feat: List[np.ndarray] = []
-        res_sel: List[torch.Tensor] = []
+        res_left: List[torch.Tensor] = []  # classification: left-child totals of every candidate
         streamed_root = (pending is not None and depth == 0 and cand.size <= group and dev.type == "cuda"
                          and not deterministic())
         if pending is not None and not streamed_root:
             pending.finish()
             pending = None
+        derive = None
+        if sib_sub and prev_hist is not None and cand.size <= group and not streamed_root:
+            # sibling pairs that are both candidates: histogram the one with less (global, weighted)
+            # rows, derive the other (ties: derive the right child); children of split p are
+            # segments 2i, 2i + 1. The totals are the all-reduced ones: every rank picks the same.
+            pos = np.full(L, -1, dtype=np.int64)
+            pos[cand] = np.arange(cand.size)
+            sib_pos = pos[cand ^ 1]
+            mine, theirs = wsum[cand], wsum[cand ^ 1]
+            derive = (sib_pos >= 0) & ((mine > theirs) | ((mine == theirs) & ((cand & 1) == 1)))
+        keep_hist = sib_sub and cand.size <= group
         for g0 in range(0, cand.size, group):
-            cg = cand[g0: g0 + group]
+            cg = cand[g0: g0 + group] if derive is None else cand[~derive]
             C = int(cg.size)
+            # node-partitioned reduce-scatter needs the node count padded to a multiple of W (the
+            # padding nodes get no items: zero histograms, no split)
+            Cp = -(-C // W) * W if scatter else C
             if nf >= n:
                 feats = torch.arange(n, device=dev, dtype=torch.int32).repeat(C, 1)
             else:
@@ -392,8 +456,8 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
                 feats = ops.rf_sample_features(C, n, nf, call_seed ^ (depth * 1000003 + g0 * 7919 + 1), dev)
             c_start, c_cnt = bounds_h[cg], counts[cg]
             if streamed_root:
-                hist = _root_hist_streamed(pending, bins, idx, wpos, yv, c_start, c_cnt, feats, C, B, SH, regression,
-                                           fb, yscale)
+                hist = _root_hist_streamed(pending, bins, idx, wpos, yv, c_start, c_cnt,
+                                           feats if Cp == C else _pad_rows(feats, Cp), Cp, B, SH, regression, fb, yscale)
                 pending = None
             il = None
             fb_l, nfc_l, rpi_min, blocks = fb, nfc, ROWS_PER_ITEM, 8192
@@ -438,25 +502,40 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
                 items_t = torch.from_numpy(it).to(dev, non_blocking=False)
                 excl = ({"multi_nodes": torch.from_numpy(np.nonzero(nch != 1)[0]).to(dev)}
                         if dev.type == "cuda" else None)
-                hist = ops.rf_hist(bins, idx, yv, None, items_t, feats, C, B, SH, regression, pos_weight=wpos,
+                hist = ops.rf_hist(bins, idx, yv, None, items_t, feats if Cp == C else _pad_rows(feats, Cp), Cp, B,
+                                   SH, regression, pos_weight=wpos,
                                    fb=fb_l, yscale=yscale, exclusive=excl, bins_il=il,
                                    wide=il is not None and fb_l == wide_fb, rec_bytes=WIDE_REC_BYTES if wide_fb else 32,
                                    packed_scale=pack_scale if fb_l == wide_fb else None)
-            if data_parallel:
-                ctx.comm.allreduce(hist)
-            out, _ = ops.rf_best_split(hist, B, SH, regression, crit, min_leaf, min_gain)
+            if Cp > C:
+                hist[C:].zero_()  # padding nodes (no items; an `exclusive` histogram is not pre-zeroed)
+            if scatter:
+                own = ctx.comm.reduce_scatter(hist)  # summed histograms of this rank's Cp / W nodes
+                del hist
+                out_o, _ = ops.rf_best_split(own, B, SH, regression, crit, min_leaf, min_gain)
+                recs = [out_o] if regression else [out_o, _left_totals(own, out_o)]
+                del own
+                # every rank's split records (+ left totals): a few doubles per node
+                allr = ctx.comm.allgather(torch.cat(recs, 1).contiguous())[:C]
+                out = allr[:, :6]
+                if not regression:
+                    res_left.append(allr[:, 6:])
+            else:
+                if data_parallel:
+                    ctx.comm.allreduce(hist)  # (sibling subtraction: the built half only)
+                if derive is not None:
+                    hist, C = _expand_siblings(hist, derive, sib_pos, prev_hist, prev_parent[cand]), int(cand.size)
+                    feats = torch.arange(n, device=dev, dtype=torch.int32).repeat(C, 1)
+                out, _ = ops.rf_best_split(hist, B, SH, regression, crit, min_leaf, min_gain)
+                if not regression:
+                    res_left.append(_left_totals(hist, out))
+                prev_hist = hist if keep_hist else None
+                del hist
             out_h = out.cpu().numpy()
             res_out.append(out_h)
             feats_h = feats.cpu().numpy()
             ok = out_h[:, 1] >= 0
             res_feat.append(np.where(ok, feats_h[np.arange(C), np.where(ok, out_h[:, 1], 0).astype(np.int64)], -1))
-            if not regression:
-                okc = np.nonzero(ok)[0]
-                if okc.size:
-                    ci_t = torch.from_numpy(okc).to(dev)
-                    sl_t = torch.from_numpy(out_h[okc, 1].astype(np.int64)).to(dev)
-                    res_sel.append(hist[ci_t, sl_t].double())  # (k_g, B, S) winning histograms
-            del hist
         out_all = np.concatenate(res_out, 0)
         feat_all = np.concatenate(res_feat, 0)
         # ---- decide splits (honour max_leaves per tree) ----
@@ -479,7 +558,6 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
         sel_mask = np.ones(order.size, dtype=bool) if keep_set is None else \
             np.fromiter((int(ci) in keep_set for ci in order), dtype=bool, count=order.size)
         ci_sel = order[sel_mask]
-        sel_rows = np.nonzero(sel_mask)[0]  # index into the concatenated winning histograms (classification)
         k = int(ci_sel.size)
         if k:
             j_sel = cand[ci_sel]
@@ -505,11 +583,9 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
         if regression:
             tot = _node_stats(yv, idx, wpos, bounds, S, regression)
         else:
-            # children totals = prefix of each winning histogram up to its split bin
-            sel = torch.cat(res_sel, 0)[torch.from_numpy(sel_rows).to(dev)]  # (k, B, S)
-            split_bin = torch.from_numpy(node_bin[node_feature >= 0].astype(np.int64)).to(dev)
-            # node_feature >= 0 segments are in cand order == split order
-            left = sel.cumsum(1)[torch.arange(k, device=dev), split_bin]
+            # children totals: each split node's left-child totals (prefix of its winning histogram up
+            # to the split bin); node_feature >= 0 segments are in cand order == split order
+            left = torch.cat(res_left, 0)[torch.from_numpy(ci_sel).to(dev)]
             split_seg = torch.from_numpy(np.nonzero(node_feature >= 0)[0]).to(dev)
             right = tot[split_seg] - left
             tot = torch.stack([left, right], 1).reshape(2 * k, S)
@@ -517,6 +593,9 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
             ctx.comm.allreduce(tot)
         bounds_h = bounds.cpu().numpy().astype(np.int64)
         counts = np.diff(bounds_h)
+        prev_parent = np.repeat(ci_sel, 2)  # new segments 2i, 2i + 1 come from candidate ci_sel[i]
+        if not keep_hist:
+            prev_hist = None
         seg_tree = np.asarray(new_tree, dtype=np.int64)
         seg_nid = np.asarray(new_nid, dtype=np.int64)
         depth += 1

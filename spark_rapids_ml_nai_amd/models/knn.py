@@ -35,10 +35,7 @@ def _merge_lists(d1: torch.Tensor, i1: torch.Tensor, d2: torch.Tensor, i2: torch
     """k smallest of two (distance, id) lists per row (ties keep the earlier list)."""
     D = torch.cat([d1, d2], 1)
     I = torch.cat([i1, i2], 1)
-    if k <= ops.TOPK_KMAX:
-        return ops.topk_rows(D, k, ids=I)
-    v, j = torch.sort(D, dim=1, stable=True)
-    return v[:, :k], I.gather(1, j[:, :k])
+    return ops.topk_rows(D, k, ids=I)  # radix select on the device (k <= ops.TOPK_KMAX)
 
 
 def _ring_search(queries: torch.Tensor, k: int, ctx: WorkerContext, local: Callable[[torch.Tensor], Tuple[

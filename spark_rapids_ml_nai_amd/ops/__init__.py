@@ -1371,7 +1371,7 @@ def rf_predict(X: torch.Tensor, roots: torch.Tensor, feature: torch.Tensor, thre
 # Nearest-neighbour search
 # ------------------------------------------------------------------------------------------
 KNN_KMAX = 64          # register/LDS insertion-list kernel (srml_knn_f32)
-TOPK_KMAX = 1024       # distance-chunk + radix-select path (srml_knn_dist_f32 + srml_topk_rows_f32)
+TOPK_KMAX = 16384      # distance-chunk + radix-select path (srml_knn_dist_f32 + srml_topk_rows_f32)
 _TOPK_SLICE = 65536    # columns per select block
 _KNN_DIST_BYTES = 1 << 30  # distance chunk budget
 
@@ -1423,7 +1423,9 @@ def knn(Q: torch.Tensor, I: torch.Tensor, k: int, inorm: Optional[torch.Tensor] 
     mq, n = Q.shape
     mi = I.shape[0]
     kk = min(k, mi)
-    if Q.is_cuda and Q.dtype == torch.float32 and KNN_KMAX < k <= TOPK_KMAX:
+    if Q.is_cuda and Q.dtype == torch.float32 and k > TOPK_KMAX:
+        raise ValueError("knn: k=%d > %d" % (k, TOPK_KMAX))
+    if Q.is_cuda and Q.dtype == torch.float32 and KNN_KMAX < k:
         return _knn_large_k(Q, I, kk, inorm, qnorm, id_offset)
     if inorm is None:
         inorm = row_sqnorm(I)
@@ -1494,7 +1496,6 @@ def _knn_large_k(Q: torch.Tensor, I: torch.Tensor, k: int, inorm: Optional[torch
     return outv, outi
 
 
-IVF_CAND_NMAX = 620  # feature width the candidate kernel stages in LDS (query + 64-row tile)
 _IVF_CAND_BYTES = 1 << 30  # candidate matrix budget of the large-k IVF paths (distances + ids)
 
 
@@ -1545,7 +1546,9 @@ def ivf_search(Q: torch.Tensor, probes: torch.Tensor, list_off: torch.Tensor, it
     nq, n = Q.shape
     if qnorm is None:
         qnorm = row_sqnorm(Q)
-    if Q.is_cuda and Q.dtype == torch.float32 and KNN_KMAX < k <= TOPK_KMAX and n <= IVF_CAND_NMAX:
+    if Q.is_cuda and Q.dtype == torch.float32 and k > TOPK_KMAX:
+        raise ValueError("ivf_search: k=%d > %d" % (k, TOPK_KMAX))
+    if Q.is_cuda and Q.dtype == torch.float32 and KNN_KMAX < k:
         od, oi = _ivf_large_k(Q, nq, probes, list_off, items, inorm, ids, k)
         return (od + qnorm.float().view(-1, 1)).clamp_min(0), oi
     if not Q.is_cuda or Q.dtype != torch.float32 or k > KNN_KMAX:
@@ -1592,7 +1595,9 @@ def knn_lists(X: torch.Tensor, xnorm: torch.Tensor, list_off: torch.Tensor, prob
         return od, oi
     if tile_list.shape[0] != ntiles or list_off.shape[0] != probes.shape[0] + 1:
         raise ValueError("knn_lists: inconsistent tile / list descriptors")
-    if X.is_cuda and X.dtype == torch.float32 and KNN_KMAX < k <= TOPK_KMAX and n <= IVF_CAND_NMAX:
+    if X.is_cuda and X.dtype == torch.float32 and k > TOPK_KMAX:
+        raise ValueError("knn_lists: k=%d > %d" % (k, TOPK_KMAX))
+    if X.is_cuda and X.dtype == torch.float32 and KNN_KMAX < k:
         # the given tiles cover one contiguous row range (a rank's slice of the tile list); each of
         # those rows probes its own list's probe set
         lo = _c(list_off.long())
@@ -1788,12 +1793,17 @@ def knn_refine_sort(Q: torch.Tensor, X: torch.Tensor, pos: torch.Tensor, inner_p
     squared euclidean, or -2 q.x for ``inner_product`` — sorted ascending per row (ties keep the
     candidate order; missing candidates last at +inf): (d fp32, pos int64), both (mq, k).
     ``srml_knn_refine_sort_f32`` (one wave per query, no gathered copy of the rows) for fp32
-    device data with k <= 64 and n <= 1024; None otherwise (the caller keeps its torch path)."""
+    device data with n <= 1024: k <= 64 in one launch; larger k in 64-candidate column panels,
+    each re-scored and sorted by the kernel, merged by the radix-select kernel (``topk_rows``,
+    ties keep the candidate order). None otherwise (the caller keeps its torch path)."""
     mq, k = pos.shape
     n = Q.shape[1]
-    if (not Q.is_cuda or Q.dtype != torch.float32 or X.dtype != torch.float32 or k < 1 or k > 64
+    if (not Q.is_cuda or Q.dtype != torch.float32 or X.dtype != torch.float32 or k < 1 or k > TOPK_KMAX
             or n > 1024 or n < 1 or Q.stride(1) != 1 or X.stride(1) != 1):
         return None
+    if k > 64:
+        parts = [knn_refine_sort(Q, X, pos[:, c0: c0 + 64], inner_product) for c0 in range(0, k, 64)]
+        return topk_rows(torch.cat([a for a, _ in parts], 1), k, ids=torch.cat([b for _, b in parts], 1))
     p = _c(pos.to(torch.int64))
     d = torch.empty((mq, k), dtype=torch.float32, device=Q.device)
     po = torch.empty((mq, k), dtype=torch.int64, device=Q.device)
@@ -2148,7 +2158,7 @@ def logistic_path(X, K: int) -> str:
             return "fused_binary_f32"
         if X.dtype in (torch.float32, torch.float64) and n <= 16384:
             return "lds_binary_" + ("f32" if X.dtype == torch.float32 else "f64")
-        return "two_pass_binary_f32" if X.dtype == torch.float32 else "torch"
+        return "two_pass_binary_f32" if X.dtype == torch.float32 else "two_pass_binary_f64"
     if X.dtype == torch.float32 and K <= 16:
         fused = os.environ.get("SRML_LOGREG_FUSED", "0") == "1" and int(native.lib().srml_mlogit_supported(n, K))
         return "fused_multinomial_f32" if fused else "two_pass_multinomial_f32"
@@ -2193,8 +2203,9 @@ def _glm_wide(X, y32: torch.Tensor, W: torch.Tensor, b: torch.Tensor, out: torch
 
 
 def mbin_supported(X, M: int) -> bool:
-    """Whether ``logistic_loss_grad_multi`` runs on the device kernels for this input."""
-    return (not _is_csr(X)) and X.is_cuda and X.dtype == torch.float32 and 1 <= M <= 16
+    """Whether ``logistic_loss_grad_multi`` runs on the device kernels for this input (any M: models
+    beyond 16 run in 16-model panels)."""
+    return (not _is_csr(X)) and X.is_cuda and X.dtype == torch.float32 and M >= 1
 
 
 def _glm_two_pass(X: torch.Tensor, y32: torch.Tensor, W: torch.Tensor, b: torch.Tensor, sb: int, mode: int,
@@ -2235,6 +2246,10 @@ def logistic_loss_grad_multi(X: torch.Tensor, y32: torch.Tensor, WB: torch.Tenso
     M models (hyper-parameter batching). Device: ``srml_mbin_f32``; otherwise per-model torch."""
     m, n = X.shape
     M = WB.shape[0]
+    if mbin_supported(X, M) and WB.stride(1) == 1 and out.stride(1) == 1 and M > 16:
+        for j0 in range(0, M, 16):  # 16-model panels: one pass over X each
+            logistic_loss_grad_multi(X, y32, WB[j0: j0 + 16], out[j0: j0 + 16])
+        return out
     if mbin_supported(X, M) and WB.stride(1) == 1 and out.stride(1) == 1:
         X = _c(X)
         if (os.environ.get("SRML_LOGREG_FUSED", "0") == "1" and not deterministic()
@@ -2319,6 +2334,14 @@ def logistic_loss_grad(X, y32: torch.Tensor, w: torch.Tensor, b: torch.Tensor, K
         _glm_wide(X, y32, w.view(K, n), b, out, flag)
     elif path == "two_pass_binary_f32":  # wider than the LDS-resident binary kernels
         _glm_two_pass(X, y32, w.view(1, n), b, 1, 1, out, 1, n, out[n:], 1, out[n + 1:], 1, flag)
+    elif path == "two_pass_binary_f64":
+        # fp64 inputs wider than the LDS kernels: margins and X^T r on the fp64 MFMA GEMM (split-K
+        # over rows), the residual / loss / bias gradient in one fp64 pass (srml_logit_residual_f64)
+        z = dgemm(X, w.view(n, 1))
+        r = torch.zeros((m, 1), dtype=torch.float64, device=dev)  # stays 0 if the done flag skips it
+        native.call("srml_logit_residual_f64", z.data_ptr(), m, 1, 1, _c(y32).data_ptr(), b.data_ptr(), 1, 1,
+                    r.data_ptr(), 1, out[n:].data_ptr(), 1, out[n + 1:].data_ptr(), 1, fp, st)
+        dgemm(X, r, ta=True, beta=1.0, out=out[:n].view(n, 1))
     elif path == "fused_binary_f32":
         native.call("srml_logreg_binary2_f32", X.data_ptr(), m, n, X.stride(0), y32.data_ptr(), w.data_ptr(), 0.0,
                     b.data_ptr(), fp, out.data_ptr(), st)

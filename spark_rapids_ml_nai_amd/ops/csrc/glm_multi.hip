@@ -269,11 +269,11 @@ SRML_API int srml_mbin_f32(const float* X, long m, int n, long ld, const float* 
 //   mode 1 (K independent binary models): R[r][k] = sigmoid(z_k) - y, loss_k += softplus(z_k) - y z_k.
 // Bias gradients (column sums of R) and the loss(es) are block-reduced and added into out:
 // gb_k at gb[k * sgb], loss at loss[0] (mode 0) or loss[k * sl] (mode 1).
-template <int KB>
-__global__ __launch_bounds__(256) void logit_residual_kernel(const float* __restrict__ Z, long m, int K, long ldz,
+template <typename TZ, int KB>
+__global__ __launch_bounds__(256) void logit_residual_kernel(const TZ* __restrict__ Z, long m, int K, long ldz,
                                                              const float* __restrict__ y,
                                                              const double* __restrict__ b, long sb, int mode,
-                                                             float* __restrict__ R, long ldr,
+                                                             TZ* __restrict__ R, long ldr,
                                                              double* __restrict__ gb, long sgb,
                                                              double* __restrict__ loss, long sl,
                                                              const int* __restrict__ flag, double* __restrict__ ws) {
@@ -315,7 +315,7 @@ __global__ __launch_bounds__(256) void logit_residual_kernel(const float* __rest
         if (k < K) {
           const double res = e[k] * inv - (k == yi ? 1.0 : 0.0);
           if (k == yi) zy = z[k];
-          R[r * ldr + k] = (float)res;
+          R[r * ldr + k] = (TZ)res;
           sg[k] += res;
         }
       }
@@ -326,7 +326,7 @@ __global__ __launch_bounds__(256) void logit_residual_kernel(const float* __rest
         if (k < K) {
           double res, l;
           logistic_terms(z[k], (double)yr, res, l);
-          R[r * ldr + k] = (float)res;
+          R[r * ldr + k] = (TZ)res;
           sg[k] += res;
           sls[k] += l;
         }
@@ -370,14 +370,15 @@ static long logit_residual_blocks(long m) {
 // Workspace (doubles) of the deterministic residual stage.
 SRML_API long srml_logit_residual_ws(long m, int K) { return m <= 0 ? 0 : logit_residual_blocks(m) * (2L * K + 1); }
 
-static int logit_residual_launch(const float* Z, long m, int K, long ldz, const float* y, const double* b, long sb,
-                                 int mode, float* R, long ldr, double* gb, long sgb, double* loss, long sl,
+template <typename TZ>
+static int logit_residual_launch(const TZ* Z, long m, int K, long ldz, const float* y, const double* b, long sb,
+                                 int mode, TZ* R, long ldr, double* gb, long sgb, double* loss, long sl,
                                  const int* flag, double* ws, hipStream_t stream) {
   if (m <= 0) return 0;
   if (K < 1 || K > 16) return -2;
   const long blocks = logit_residual_blocks(m);
 #define SRML_RES(KK)                                                                                             \
-  hipLaunchKernelGGL(logit_residual_kernel<KK>, dim3((unsigned)blocks), dim3(256), 0, stream, Z, m, K, ldz, y, b, sb, \
+  hipLaunchKernelGGL((logit_residual_kernel<TZ, KK>), dim3((unsigned)blocks), dim3(256), 0, stream, Z, m, K, ldz, y, b, sb, \
                      mode, R, ldr, gb, sgb, loss, sl, flag, ws)
   if (K <= 4) SRML_RES(4);
   else if (K <= 8) SRML_RES(8);
@@ -394,6 +395,13 @@ static int logit_residual_launch(const float* Z, long m, int K, long ldz, const 
 
 SRML_API int srml_logit_residual_f32(const float* Z, long m, int K, long ldz, const float* y, const double* b, long sb,
                                      int mode, float* R, long ldr, double* gb, long sgb, double* loss, long sl,
+                                     const int* flag, hipStream_t stream) {
+  return logit_residual_launch(Z, m, K, ldz, y, b, sb, mode, R, ldr, gb, sgb, loss, sl, flag, nullptr, stream);
+}
+
+// fp64 margins / residuals (float32_inputs=False two-pass GLM: margins and X^T R on the fp64 MFMA GEMM)
+SRML_API int srml_logit_residual_f64(const double* Z, long m, int K, long ldz, const float* y, const double* b, long sb,
+                                     int mode, double* R, long ldr, double* gb, long sgb, double* loss, long sl,
                                      const int* flag, hipStream_t stream) {
   return logit_residual_launch(Z, m, K, ldz, y, b, sb, mode, R, ldr, gb, sgb, loss, sl, flag, nullptr, stream);
 }

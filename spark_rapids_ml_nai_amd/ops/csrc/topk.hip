@@ -22,7 +22,9 @@ namespace {
 using namespace srml_tile;
 
 constexpr int TK_T = 256;
-constexpr int TK_KMAX = 1024;
+// k <= TK_KMAX: the selected (key, column) pairs are bitonic-sorted in dynamic LDS sized to the
+// next power of two of k (8 B per pair: 128 KiB at k = 16384)
+constexpr int TK_KMAX = 16384;
 
 template <bool VEC>
 __global__ __launch_bounds__(256, 2) void knn_dist_kernel(const float* __restrict__ Q, long mq, int n, long ldq,
@@ -77,8 +79,11 @@ __global__ __launch_bounds__(TK_T) void topk_rows_kernel(const float* __restrict
                                                          long long id_base, int k, float* __restrict__ out_v,
                                                          long long* __restrict__ out_i, long ldo, long slice_ldo) {
   __shared__ int hist[2048];
-  __shared__ unsigned skey[TK_KMAX];
-  __shared__ int spos[TK_KMAX];
+  extern __shared__ unsigned tk_dyn[];  // skey[kpad] | spos[kpad]
+  int kp2 = 1;
+  while (kp2 < k) kp2 <<= 1;
+  unsigned* skey = tk_dyn;
+  int* spos = reinterpret_cast<int*>(tk_dyn + kp2);
   __shared__ int s_w[4];
   __shared__ int s_digit, s_below;
   const long row = blockIdx.x;
@@ -277,7 +282,7 @@ SRML_API int srml_knn_dist_f32(const float* Q, long mq, int n, long ldq, const f
 // Row-wise k smallest (ascending, ties by column) of `rows` rows of L_total values (leading dim
 // ldv), split into column slices of `slice_len` (grid.y); slice s of row r writes k results at
 // out[r * ldo + s * slice_ldo]. ids: optional int64 ids of the input values (leading dim ldid);
-// without them the id of column c is id_base + c. k <= 1024.
+// without them the id of column c is id_base + c. k <= 16384.
 SRML_API int srml_topk_rows_f32(const float* vals, long rows, long ldv, long slice_len, int L_total,
                                 const long long* ids, long ldid, long long id_base, int k, float* out_v,
                                 long long* out_i, long ldo, long slice_ldo, hipStream_t stream) {
@@ -285,7 +290,12 @@ SRML_API int srml_topk_rows_f32(const float* vals, long rows, long ldv, long sli
   if (k <= 0 || k > TK_KMAX || slice_len <= 0 || L_total <= 0) return -1;
   const long slices = (L_total + slice_len - 1) / slice_len;
   if (rows > 0x7fffffffL || slices > 65535) return -1;
-  hipLaunchKernelGGL(topk_rows_kernel, dim3((unsigned)rows, (unsigned)slices), dim3(TK_T), 0, stream, vals, ldv,
+  int kp2 = 1;
+  while (kp2 < k) kp2 <<= 1;
+  const size_t shm = (size_t)kp2 * (sizeof(unsigned) + sizeof(int));
+  if (shm > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)topk_rows_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+  hipLaunchKernelGGL(topk_rows_kernel, dim3((unsigned)rows, (unsigned)slices), dim3(TK_T), shm, stream, vals, ldv,
                      slice_len, L_total, ids, ldid, id_base, k, out_v, out_i, ldo, slice_ldo);
   return srml_status();
 }
@@ -305,6 +315,7 @@ SRML_API int srml_topk_kmax() { return TK_KMAX; }
 // ------------------------------------------------------------------------------------------
 constexpr int IVC_T = 256;
 constexpr int IVC_ROWS = 64;
+constexpr int IVC_NC = 512;  // feature chunk staged in LDS (133 KiB with the 64-row tile)
 
 __global__ __launch_bounds__(IVC_T) void ivf_candidates_kernel(const float* __restrict__ Q, long q0, int n, long ldq,
                                                                const int* __restrict__ probes, int nprobe,
@@ -313,11 +324,13 @@ __global__ __launch_bounds__(IVC_T) void ivf_candidates_kernel(const float* __re
                                                                const float* __restrict__ items, long ldi,
                                                                const float* __restrict__ inorm,
                                                                const long long* __restrict__ ids, float* __restrict__ D,
-                                                               long long* __restrict__ DI, long ldd) {
-  extern __shared__ float ivc_s[];  // q[n] | tile[IVC_ROWS][n + 1]
+                                                               long long* __restrict__ DI, long ldd, int nc) {
+  // features are staged in chunks of nc (= min(n, IVC_NC)) columns, so any width fits the LDS:
+  // each row's dot product accumulates in its thread's register across the chunks
+  extern __shared__ float ivc_s[];  // q chunk [nc] | tile[IVC_ROWS][nc + 1]
   float* qs = ivc_s;
-  float* tile = ivc_s + n;
-  const int tn = n + 1;
+  float* tile = ivc_s + nc;
+  const int tn = nc + 1;
   const long qi = q0 + blockIdx.x;  // global query (row) index
   const int p = blockIdx.y;
   const int* pr = probes + (long)(qlist ? qlist[qi] : qi) * nprobe;
@@ -328,21 +341,26 @@ __global__ __launch_bounds__(IVC_T) void ivf_candidates_kernel(const float* __re
     if (pr[j] >= 0) off += list_off[pr[j] + 1] - list_off[pr[j]];
   if (l < 0) return;
   const long b0 = list_off[l], b1 = list_off[l + 1];
-  for (int c = threadIdx.x; c < n; c += IVC_T) qs[c] = Q[qi * ldq + c];
   float* drow = D + (long)blockIdx.x * ldd + off;
   long long* irow = DI + (long)blockIdx.x * ldd + off;
   for (long r0 = b0; r0 < b1; r0 += IVC_ROWS) {
     const int rows = (int)min((long)IVC_ROWS, b1 - r0);
-    __syncthreads();  // previous tile consumed (and qs written on the first pass)
-    for (int e = threadIdx.x; e < rows * n; e += IVC_T) {
-      const int rr = e / n, cc = e - rr * n;
-      tile[rr * tn + cc] = items[(r0 + rr) * ldi + cc];
+    float acc = 0.f;
+    for (int c0 = 0; c0 < n; c0 += nc) {
+      const int w = min(nc, n - c0);
+      __syncthreads();  // previous chunk / tile consumed
+      for (int c = threadIdx.x; c < w; c += IVC_T) qs[c] = Q[qi * ldq + c0 + c];
+      for (int e = threadIdx.x; e < rows * w; e += IVC_T) {
+        const int rr = e / w, cc = e - rr * w;
+        tile[rr * tn + cc] = items[(r0 + rr) * ldi + c0 + cc];
+      }
+      __syncthreads();
+      if (threadIdx.x < rows) {
+        const float* row = tile + threadIdx.x * tn;
+        for (int c = 0; c < w; ++c) acc = fmaf(qs[c], row[c], acc);
+      }
     }
-    __syncthreads();
     if (threadIdx.x < rows) {
-      const float* row = tile + threadIdx.x * tn;
-      float acc = 0.f;
-      for (int c = 0; c < n; ++c) acc = fmaf(qs[c], row[c], acc);
       const long it = r0 + threadIdx.x;
       drow[it - b0] = inorm[it] - 2.f * acc;
       irow[it - b0] = ids ? ids[it] : it;
@@ -403,14 +421,14 @@ SRML_API int srml_ivf_candidates_f32(const float* Q, long q0, long nq, int n, lo
                                      hipStream_t stream) {
   if (nq <= 0) return 0;
   if (n <= 0 || nprobe <= 0 || nprobe > 65535 || nq > 0x7fffffffL || ldd <= 0) return -1;
-  const size_t shm = (size_t)(n + IVC_ROWS * (n + 1)) * sizeof(float);
-  if (shm > 160 * 1024) return -2;  // n <= ~620 dims: wider data takes the exact MFMA path
+  const int nc = n < IVC_NC ? n : IVC_NC;
+  const size_t shm = (size_t)(nc + IVC_ROWS * (nc + 1)) * sizeof(float);
   const long total = nq * ldd;
   hipLaunchKernelGGL(ivf_fill_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, D, DI, total);
   if (shm > 64 * 1024)
     (void)hipFuncSetAttribute((const void*)ivf_candidates_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
   hipLaunchKernelGGL(ivf_candidates_kernel, dim3((unsigned)nq, (unsigned)nprobe), dim3(IVC_T), shm, stream, Q, q0, n,
-                     ldq, probes, nprobe, qlist, list_off, items, ldi, inorm, ids, D, DI, ldd);
+                     ldq, probes, nprobe, qlist, list_off, items, ldi, inorm, ids, D, DI, ldd, nc);
   return srml_status();
 }
 

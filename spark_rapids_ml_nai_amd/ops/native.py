@@ -53,6 +53,7 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_xw_t_f32": (_P, _L, _I, _L, _P, _I, _L, _P, _P, _L, _P),
     "srml_xw_t_f32_variant": (_P, _L, _I, _L, _P, _I, _L, _P, _P, _L, _I, _P),
     "srml_logit_residual_f32": (_P, _L, _I, _L, _P, _P, _L, _I, _P, _L, _P, _L, _P, _L, _P, _P),
+    "srml_logit_residual_f64": (_P, _L, _I, _L, _P, _P, _L, _I, _P, _L, _P, _L, _P, _L, _P, _P),
     "srml_logit_residual_det_f32": (_P, _L, _I, _L, _P, _P, _L, _I, _P, _L, _P, _L, _P, _L, _P, _P, _P),
     "srml_logit_residual_ws": (_L, _I),
     "srml_xtv_mfma_ws": (_L, _I, _I),

@@ -86,8 +86,16 @@ class Communicator:
         return t
 
     # -- collectives ----------------------------------------------------------------
-    def _timed(self, t: torch.Tensor) -> Any:
-        return self.stats.record(t.numel() * t.element_size(), self.device if self._backend == "nccl" else None)
+    def _timed(self, t: torch.Tensor, wire: float = 1.0) -> Any:
+        """Account one collective on payload ``t``; ``wire``: bytes this rank sends per payload byte
+        under the ring algorithm (all-reduce 2 (W - 1) / W, reduce-scatter (W - 1) / W, all-gather
+        W - 1 per input byte)."""
+        nb = t.numel() * t.element_size()
+        return self.stats.record(nb, self.device if self._backend == "nccl" else None, wire_bytes=nb * wire)
+
+    def _ring(self, kind: str) -> float:
+        W = max(1, self.size)
+        return {"allreduce": 2.0 * (W - 1) / W, "reduce_scatter": (W - 1) / W, "allgather": float(W - 1)}[kind]
 
     def _oneshot_for(self, t: torch.Tensor, op: str) -> Any:
         """The peer-mapped one-shot path when it applies to this payload: ``SRML_COMM=oneshot``
@@ -123,7 +131,7 @@ class Communicator:
         if self._solo:
             return t
         os_ = self._oneshot_for(t, op)
-        with self._timed(t):
+        with self._timed(t, self._ring("allreduce")):
             if os_ is not None:
                 return os_.allreduce(t)
             ct = self._comm_tensor(t)
@@ -180,12 +188,27 @@ class Communicator:
         """Equal-shaped blocks -> concatenated along dim 0."""
         if self._solo:
             return t
-        with self._timed(t):
+        with self._timed(t, self._ring("allgather")):
             ct = self._comm_tensor(t.contiguous())
             out = [torch.empty_like(ct) for _ in range(self.size)]
             dist.all_gather(out, ct, group=self.group)
             res = torch.cat(out, 0)
         return res.to(t.device) if res.device != t.device else res
+
+    def reduce_scatter(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        """Sum over ranks of ``t`` (dim 0 divisible by the world size), of which this rank keeps
+        block ``rank`` of dim 0: half the bytes of an all-reduce on a ring, for consumers that only
+        need their own slice of the reduction (the data-parallel forest's node-partitioned split
+        search)."""
+        if self._solo:
+            return t
+        assert t.shape[0] % self.size == 0, "reduce_scatter: dim 0 must divide by the world size"
+        rows = t.shape[0] // self.size
+        with self._timed(t, self._ring("reduce_scatter")):
+            ct = self._comm_tensor(t.contiguous())
+            out = torch.empty((rows,) + tuple(ct.shape[1:]), dtype=ct.dtype, device=ct.device)
+            dist.reduce_scatter_tensor(out, ct, op=_OPS[op], group=self.group)
+        return out.to(t.device) if out.device != t.device else out
 
     def allgatherv(self, t: torch.Tensor) -> List[torch.Tensor]:
         """Ragged dim-0 blocks -> list of per-rank tensors. One implementation for every backend:
@@ -217,6 +240,7 @@ class Communicator:
         gs = dist.get_global_rank(g, src) if g is not None else src
         self.stats.calls += 1
         self.stats.bytes += cs.numel() * cs.element_size()
+        self.stats.wire_bytes += cs.numel() * cs.element_size()
         works = dist.batch_isend_irecv([dist.P2POp(dist.isend, cs, gd, group=g),
                                         dist.P2POp(dist.irecv, cr, gs, group=g)])
         return (works, cs, cr, recv)
@@ -238,7 +262,7 @@ class Communicator:
     def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if self._solo:
             return t
-        with self._timed(t):
+        with self._timed(t, 1.0 if self.rank == src or self.size > 2 else 0.0):
             ct = self._comm_tensor(t)
             dist.broadcast(ct, src=src, group=self.group)
             if ct is not t:
@@ -367,6 +391,7 @@ class CommStats:
     def reset(self) -> None:
         self.calls = 0
         self.bytes = 0
+        self.wire_bytes = 0.0  # bytes this rank sends (ring algorithms), see Communicator._timed
         self.host_s = 0.0
         self._dev_s = 0.0  # resolved device spans (folded out of _pairs)
         self._pairs: List[Any] = []
@@ -388,10 +413,12 @@ class CommStats:
             del self._pairs[:i]
 
     @contextlib.contextmanager
-    def record(self, nbytes: int, device: Optional[torch.device], count: bool = True) -> Iterator[None]:
+    def record(self, nbytes: int, device: Optional[torch.device], count: bool = True,
+               wire_bytes: Optional[float] = None) -> Iterator[None]:
         if count:
             self.calls += 1
             self.bytes += int(nbytes)
+            self.wire_bytes += float(nbytes if wire_bytes is None else wire_bytes)
         if device is not None and device.type == "cuda" and _rank_timers_enabled():
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
@@ -417,7 +444,8 @@ class CommStats:
         return self.host_s + self._dev_s
 
     def snapshot(self) -> dict:
-        return {"comm_s": round(self.seconds(), 6), "comm_calls": self.calls, "comm_bytes": self.bytes}
+        return {"comm_s": round(self.seconds(), 6), "comm_calls": self.calls, "comm_bytes": self.bytes,
+                "comm_wire_bytes": int(self.wire_bytes)}
 
 
 def pickle_obj(o: Any) -> bytes:

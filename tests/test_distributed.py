@@ -145,3 +145,70 @@ def test_comm_watchdog_aborts_stuck_collective(monkeypatch):
     with pytest.raises(RuntimeError, match="exceeded 5s; communicator aborted"):
         LinearRegression(num_workers=2).fit(df)
     assert time.time() - t0 < 80
+
+
+@pytest.mark.parametrize("world,classify", [(2, True), (3, True), (2, False)])
+def test_random_forest_dp_reduce_scatter_identical(world, classify, monkeypatch):
+    """Data-parallel forests: the node-partitioned reduce-scatter of each level's histograms (+ an
+    all-gather of the per-node split records) grows the same trees as all-reducing every
+    histogram, with about half the wire bytes (3 ranks: padded node counts)."""
+    from sklearn.datasets import make_classification, make_regression
+
+    from spark_rapids_ml_nai_amd.classification import RandomForestClassifier
+    from spark_rapids_ml_nai_amd.regression import RandomForestRegressor
+
+    if classify:
+        X, y = make_classification(n_samples=2400, n_features=12, n_informative=6, n_classes=3, random_state=1)
+        Est = RandomForestClassifier
+    else:
+        X, y = make_regression(n_samples=2400, n_features=12, n_informative=6, noise=5.0, random_state=1)
+        Est = RandomForestRegressor
+    df = DataFrame.from_numpy(X.astype(np.float32), y.astype(float), num_partitions=world)
+    models = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("SRML_RF_DP_SCATTER", flag)
+        models[flag] = Est(numTrees=3, maxDepth=7, seed=3, num_workers=world, split_mode="data_parallel").fit(df)
+    a, b = models["0"], models["1"]
+    assert len(a._trees) == len(b._trees) == 3
+    for ta, tb in zip(a._trees, b._trees):
+        for key in ("feature", "threshold", "left", "right"):
+            np.testing.assert_array_equal(np.asarray(ta[key]), np.asarray(tb[key]))
+        np.testing.assert_allclose(np.asarray(ta["value"], dtype=float), np.asarray(tb["value"], dtype=float),
+                                   rtol=1e-12, atol=1e-12)
+    wa = sum(r["comm_wire_bytes"] for r in a._rank_stats)
+    wb = sum(r["comm_wire_bytes"] for r in b._rank_stats)
+    assert wb < 0.62 * wa, (wa, wb)
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_random_forest_sibling_subtraction_identical(world, monkeypatch):
+    """featureSubsetStrategy="all": from depth 1 only the smaller child of each split is
+    histogrammed (and all-reduced) and the larger derived as parent - smaller; the classifier's
+    integer histograms make the trees identical to building every node."""
+    from sklearn.datasets import make_classification
+
+    from spark_rapids_ml_nai_amd.classification import RandomForestClassifier
+
+    X, y = make_classification(n_samples=3000, n_features=10, n_informative=6, n_classes=3, random_state=2)
+    df = DataFrame.from_numpy(X.astype(np.float32), y.astype(float), num_partitions=world)
+    models = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("SRML_RF_SIBLING_SUB", flag)
+        monkeypatch.setenv("SRML_RF_DP_SCATTER", "0")  # the baseline all-reduces every histogram
+        import importlib
+
+        import spark_rapids_ml_nai_amd.models.forest as F
+
+        importlib.reload(F)
+        models[flag] = RandomForestClassifier(numTrees=3, maxDepth=8, seed=5, featureSubsetStrategy="all",
+                                              num_workers=world, split_mode="data_parallel").fit(df)
+    monkeypatch.undo()
+    importlib.reload(F)  # module constants back to the environment's defaults
+    a, b = models["0"], models["1"]
+    for ta, tb in zip(a._trees, b._trees):
+        for key in ("feature", "threshold", "left", "right"):
+            np.testing.assert_array_equal(np.asarray(ta[key]), np.asarray(tb[key]))
+    if world > 1:
+        wa = sum(r["comm_wire_bytes"] for r in a._rank_stats)
+        wb = sum(r["comm_wire_bytes"] for r in b._rank_stats)
+        assert wb < 0.75 * wa, (wa, wb)

@@ -43,7 +43,9 @@ def _estimator(name: str, world: int):
     if name == "kmeans":
         from spark_rapids_ml_nai_amd.clustering import KMeans
 
-        return KMeans(k=20, maxIter=20, tol=1e-4, seed=1, featuresCol="features")
+        # tol 0 (-> float32 tiny, the reference's mapping): all maxIter Lloyd iterations run, so the
+        # timed fit is the Lloyd / centroid-all-reduce loop this config exists to stress
+        return KMeans(k=20, maxIter=20, tol=0.0, seed=1, featuresCol="features")
     if name == "logreg":
         from spark_rapids_ml_nai_amd.classification import LogisticRegression
 
@@ -104,6 +106,50 @@ def _shard(gen: str, m: int, n: int, device, rank: int):
     if device.type == "cuda":
         torch.cuda.empty_cache()
     return Xh, yh
+
+
+def trustworthiness(X: torch.Tensor, E: torch.Tensor, k: int = 15, chunk: int = 1024) -> float:
+    """sklearn.manifold.trustworthiness on the device (exact ranks, chunked rows): 1 - 2 / (n k
+    (2n - 3k - 1)) * sum_i sum_{j in kNN_E(i) \\ kNN_X(i)} (rank_X(i, j) - k)."""
+    n = X.shape[0]
+    X = X.float()
+    E = E.float()
+    xn = (X * X).sum(1)
+    en = (E * E).sum(1)
+    pen = 0.0
+    ar = torch.arange(n, device=X.device)
+    for r0 in range(0, n, chunk):
+        r1 = min(n, r0 + chunk)
+        dx = xn[r0:r1, None] + xn[None, :] - 2.0 * X[r0:r1] @ X.T
+        de = en[r0:r1, None] + en[None, :] - 2.0 * E[r0:r1] @ E.T
+        rows = ar[r0:r1]
+        dx[torch.arange(r1 - r0), rows] = float("inf")  # self excluded (rank 0 in sklearn)
+        de[torch.arange(r1 - r0), rows] = float("inf")
+        order = torch.argsort(dx, 1)
+        rank_x = torch.empty_like(order)
+        rank_x.scatter_(1, order, ar.view(1, -1).expand(r1 - r0, -1) + 1)  # 1-based ranks
+        nn_e = torch.topk(de, k, 1, largest=False).indices
+        rk = rank_x.gather(1, nn_e)
+        pen += float((rk - k).clamp_min(0).sum().item())
+    return 1.0 - 2.0 / (n * k * (2.0 * n - 3.0 * k - 1.0)) * pen
+
+
+def _umap_quality(model, Xh, device, sample: int = 20_000) -> dict:
+    """Trustworthiness of the fitted embedding on a row sample, and of a UMAP fitted on that sample
+    alone (the reference's "single-GPU" comparison, tests/test_umap.py:146,377: gap <= 0.15)."""
+    from spark_rapids_ml_nai_amd import DataFrame
+    from spark_rapids_ml_nai_amd.umap import UMAP
+
+    n = Xh.shape[0]
+    idx = np.sort(np.random.default_rng(0).choice(n, size=min(sample, n), replace=False))
+    Xs = torch.from_numpy(np.ascontiguousarray(Xh[idx])).to(device)
+    Es = torch.from_numpy(np.asarray(model.embedding_)[idx]).to(device)
+    t_big = trustworthiness(Xs, Es)
+    small = UMAP(n_neighbors=15, n_components=2, random_state=1, featuresCol="features").fit(
+        DataFrame.from_numpy(np.ascontiguousarray(Xh[idx])))
+    t_small = trustworthiness(Xs, torch.from_numpy(np.asarray(small.embedding_)).to(device))
+    return {"trust_sample": int(idx.size), "trustworthiness": round(t_big, 5),
+            "trustworthiness_small_fit": round(t_small, 5), "trust_gap": round(t_small - t_big, 5)}
 
 
 def main() -> None:
@@ -169,14 +215,25 @@ def main() -> None:
                 rec["rank0"] = rs
             if name == "kmeans":
                 rec["iters"] = int(ma.get("n_iter", getattr(model, "num_iters", -1)) or -1)
+                ph = ma.get("phase_s")
+                if ph:
+                    rec["phase_s"] = {"prep": ph[0], "init": ph[1], "lloyd": ph[2]}
+                    rec["lloyd_s_per_iter"] = round(ph[2] / max(1, rec["iters"]), 5)
             if name == "logreg":
                 rec["iters"] = int(getattr(model, "num_iters", -1))
             if name == "rf":
                 rec["total_nodes"] = int(model.totalNumNodes)
                 rec["split_mode"] = os.environ.get("SRML_NS_RF_MODE", "data_parallel")
+                if rank == 0:  # held-out accuracy: fresh rows of the same family
+                    Xq, yq = _shard(gen, 200_000, cols, device, 10_000 + rank)
+                    pred = model.transform(DataFrame.from_numpy(Xq, yq)).to_numpy("prediction")
+                    rec["holdout_accuracy"] = round(float((pred == yq).mean()), 5)
+                    del Xq, yq
             if name == "umap":
                 emb = np.asarray(model.embedding_)
                 rec["finite"] = bool(np.isfinite(emb).all())
+                if rank == 0:
+                    rec.update(_umap_quality(model, Xh, device))
             del model, df, Xh, yh
         except Exception as e:  # noqa: BLE001
             rec["error"] = repr(e)[:500]
