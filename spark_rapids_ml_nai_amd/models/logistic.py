@@ -108,8 +108,10 @@ def logistic_fit(X: Any, y: torch.Tensor, m_total: int, ctx: WorkerContext, reg:
     y32 = y if y.dtype == torch.float32 else y.to(torch.float32)
     y32 = y32.contiguous()
 
+    ws = ops.logreg_workspace(X) if not sparse and K == 1 else None  # this fit's own partial rows
+
     def evaluate(w: torch.Tensor, b: torch.Tensor, flag: Optional[torch.Tensor], out: torch.Tensor) -> None:
-        ops.logistic_loss_grad(X, y32, w, b, K, out, flag)
+        ops.logistic_loss_grad(X, y32, w, b, K, out, flag, ws=ws)
 
     allreduce = ctx.comm.allreduce if ctx.world_size > 1 else None
     path = ops.logistic_path(X, K)

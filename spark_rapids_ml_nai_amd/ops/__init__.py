@@ -296,9 +296,20 @@ def logreg_binary_loss_grad(X: torch.Tensor, y: torch.Tensor, w: torch.Tensor, b
     out = torch.zeros(n + 2, dtype=torch.float64, device=X.device) if out is None else zero_(out)
     wf = _c(w.to(device=X.device, dtype=torch.float64))
     yf = _c(y.to(torch.float32))
-    native.call("srml_logreg_binary2_f32", X.data_ptr(), m, n, X.stride(0), yf.data_ptr(), wf.data_ptr(), float(b),
-                None, None, out.data_ptr(), native.stream(X.device))
+    ws = logreg_workspace(X)
+    native.call("srml_logreg_binary3_f32", X.data_ptr(), m, n, X.stride(0), yf.data_ptr(), wf.data_ptr(), float(b),
+                None, None, out.data_ptr(), ws.data_ptr() if ws is not None else None, native.stream(X.device))
     return out
+
+
+def logreg_workspace(X: Any) -> Optional[torch.Tensor]:
+    """Partial-row workspace of the fused binary evaluation for this shard (one per fit: the
+    block partials and their fold are two launches), or None when its kernel needs none."""
+    if _is_csr(X) or not X.is_cuda or X.dtype != torch.float32:
+        return None
+    m, n = X.shape
+    nf = int(native.lib().srml_logreg_fold_ws(m, n))
+    return torch.empty(nf, dtype=torch.float32, device=X.device) if nf > 0 else None
 
 
 def nearest_centroid(X: torch.Tensor, C: torch.Tensor, xnorm: Optional[torch.Tensor] = None,
@@ -2272,7 +2283,7 @@ def logistic_loss_grad_multi(X: torch.Tensor, y32: torch.Tensor, WB: torch.Tenso
 
 
 def logistic_loss_grad(X, y32: torch.Tensor, w: torch.Tensor, b: torch.Tensor, K: int, out: torch.Tensor,
-                       flag: Optional[torch.Tensor] = None) -> torch.Tensor:
+                       flag: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None) -> torch.Tensor:
     """ADD the summed logistic data term at (W, b) into ``out`` = [grad W (K*n, class-major) |
     grad b (K) | loss sum] (fp64). K == 1: binary (labels 0/1, sigmoid); K >= 2: softmax over K
     classes (labels 0..K-1). ``w`` (K*n) and ``b`` (K) are fp64 device tensors read by the kernel
@@ -2343,8 +2354,9 @@ def logistic_loss_grad(X, y32: torch.Tensor, w: torch.Tensor, b: torch.Tensor, K
                     r.data_ptr(), 1, out[n:].data_ptr(), 1, out[n + 1:].data_ptr(), 1, fp, st)
         dgemm(X, r, ta=True, beta=1.0, out=out[:n].view(n, 1))
     elif path == "fused_binary_f32":
-        native.call("srml_logreg_binary2_f32", X.data_ptr(), m, n, X.stride(0), y32.data_ptr(), w.data_ptr(), 0.0,
-                    b.data_ptr(), fp, out.data_ptr(), st)
+        # ws: the fit's partial-row workspace (ops.logreg_workspace), None = per-block atomic flush
+        native.call("srml_logreg_binary3_f32", X.data_ptr(), m, n, X.stride(0), y32.data_ptr(), w.data_ptr(), 0.0,
+                    b.data_ptr(), fp, out.data_ptr(), ws.data_ptr() if ws is not None else None, st)
     elif path.startswith("lds_binary"):
         native.call("srml_logreg_binary_lds_" + path[-3:], X.data_ptr(), m, n, X.stride(0), y32.data_ptr(),
                     w.data_ptr(), 0.0, b.data_ptr(), fp, out.data_ptr(), st)

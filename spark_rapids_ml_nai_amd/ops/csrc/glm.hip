@@ -888,32 +888,50 @@ __global__ __launch_bounds__(256) void fold_rows_kernel(const float* __restrict_
   }
 }
 
-// Per-device workspace of the partial-row epilogue: `blocks` rows of `row_floats` floats. Grown on
-// demand (first evaluation of a fit); a device's evaluations run in stream order on it.
-static float* fold_workspace(long blocks, long row_floats) {
-  struct Ws { void* p = nullptr; size_t bytes = 0; };
-  static Ws cache[64];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  const size_t need = (size_t)blocks * row_floats * sizeof(float);
-  Ws& c = cache[dev];
-  if (c.bytes < need) {
-    if (c.p) {
-      if (hipDeviceSynchronize() != hipSuccess) return nullptr;  // in-flight launches may still use it
-      (void)hipFree(c.p);
-      c.p = nullptr;
-      c.bytes = 0;
-    }
-    const size_t bytes = need + need / 4;
-    if (hipMalloc(&c.p, bytes) != hipSuccess) return nullptr;
-    c.bytes = bytes;
+static long logreg_grid(long m) {
+  // ~>= 160 rows per block: each block pays a w load and an n-wide flush, so small shards (the
+  // per-rank rows of a multi-GPU fit) want fewer blocks (125k rows: 768 blocks = 3 per CU, all
+  // resident at once (149 VGPRs); 1M rows: 2048)
+  static const long blocks_env = getenv("SRML_LOGREG_BLOCKS") ? atol(getenv("SRML_LOGREG_BLOCKS")) : 0;
+  long blocks = blocks_env;
+  if (blocks <= 0) {
+    blocks = m / 163;
+    if (blocks > 2048) blocks = 2048;
+    if (blocks < 512) blocks = 512;
   }
-  return reinterpret_cast<float*>(c.p);
+  long rpb = (m + blocks - 1) / blocks;
+  if (rpb < 16) rpb = 16;
+  return (m + rpb - 1) / rpb;
 }
+
+// Floats of the partial-row workspace srml_logreg_binary3_f32 needs for (m, n) (0: that shape
+// takes a kernel without partial rows, pass nullptr).
+SRML_API long srml_logreg_fold_ws(long m, int n) {
+  if (m <= 0 || n <= 1024 || n > 4096) return 0;
+  return logreg_grid(m) * (((n + 3) & ~3) + 4);
+}
+
+static int logreg_binary_launch(const float* X, long m, int n, long ld, const float* y, const double* w, double b,
+                                const double* bptr, const int* flag, double* out, float* fold_ws,
+                                hipStream_t stream);
 
 // b: intercept by value, or (bptr != null) read on the device; flag (optional): skip when *flag != 0
 SRML_API int srml_logreg_binary2_f32(const float* X, long m, int n, long ld, const float* y, const double* w, double b,
                                      const double* bptr, const int* flag, double* out, hipStream_t stream) {
+  return logreg_binary_launch(X, m, n, ld, y, w, b, bptr, flag, out, nullptr, stream);
+}
+
+// Same with the caller's partial-row workspace (srml_logreg_fold_ws floats, owned by ONE fit: the
+// block partials and their fold are two launches, so interleaved fits need separate workspaces)
+SRML_API int srml_logreg_binary3_f32(const float* X, long m, int n, long ld, const float* y, const double* w, double b,
+                                     const double* bptr, const int* flag, double* out, float* fold_ws,
+                                     hipStream_t stream) {
+  return logreg_binary_launch(X, m, n, ld, y, w, b, bptr, flag, out, fold_ws, stream);
+}
+
+static int logreg_binary_launch(const float* X, long m, int n, long ld, const float* y, const double* w, double b,
+                                const double* bptr, const int* flag, double* out, float* fold_ws,
+                                hipStream_t stream) {
   if (m <= 0) return 0;
   static const int narrow = getenv("SRML_LOGREG_NARROW") ? atoi(getenv("SRML_LOGREG_NARROW")) : 1;
   if (narrow && n <= 512 && (n & 3) == 0 && (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0) {
@@ -934,19 +952,11 @@ SRML_API int srml_logreg_binary2_f32(const float* X, long m, int n, long ld, con
 #undef SRML_LR_NARROW
     return srml_status();
   }
-  // ~>= 160 rows per block: each block pays a w load and an n-wide fp64 atomic flush, so small
-  // shards (the per-rank rows of a multi-GPU fit) want fewer blocks (125k rows: 768 blocks
-  // 0.310 ms, 1024 0.331, 1536 0.345, 512 0.328 (tools/lr_small_sweep.sh); 1M rows: 2048 best)
-  static const long blocks_env = getenv("SRML_LOGREG_BLOCKS") ? atol(getenv("SRML_LOGREG_BLOCKS")) : 0;
-  long blocks = blocks_env;
-  if (blocks <= 0) {
-    blocks = m / 163;
-    if (blocks > 2048) blocks = 2048;
-    if (blocks < 512) blocks = 512;
-  }
+  // grid sweep (tools/lr_small_sweep.sh): 125k rows 768 blocks 0.310 ms, 1024 0.331, 1536 0.345,
+  // 512 0.328; 1M rows: 2048 best
+  const long blocks = logreg_grid(m);
   long rpb = (m + blocks - 1) / blocks;
   if (rpb < 16) rpb = 16;
-  blocks = (m + rpb - 1) / rpb;
   int V = (n + 255) / 256;
   const size_t vpad = V <= 1 ? 1 : V <= 2 ? 2 : V <= 4 ? 4 : V <= 8 ? 8 : V <= 12 ? 12 : 16;
   size_t lds = 256 * vpad * (sizeof(double) + sizeof(float));
@@ -959,11 +969,11 @@ SRML_API int srml_logreg_binary2_f32(const float* X, long m, int n, long ld, con
     static const int dsel = getenv("SRML_LOGREG_D") ? atoi(getenv("SRML_LOGREG_D")) : 3;
     static const int nt = getenv("SRML_LOGREG_NT") ? atoi(getenv("SRML_LOGREG_NT")) : 1;  // nontemporal X stream: +2%
     const int VS = (n + 1023) / 1024;
-    // partial-row epilogue + fold kernel (SRML_LOGREG_FOLD=0: one fp64 atomic flush per block)
+    // partial-row epilogue + fold kernel when the caller passed a workspace (SRML_LOGREG_FOLD=0:
+    // one fp64 atomic flush per block anyway)
     static const int fold = getenv("SRML_LOGREG_FOLD") ? atoi(getenv("SRML_LOGREG_FOLD")) : 1;
     const long wst = ((n + 3) & ~3) + 4;
-    float* fws = nullptr;
-    if (fold && !(fws = fold_workspace(blocks, wst))) return -3;
+    float* fws = fold ? fold_ws : nullptr;
 #define SRML_LR_PF(VV, RR, DD) \
     hipLaunchKernelGGL((logreg_binary_pf_kernel<VV, RR, DD>), grid, blk, 0, stream, X, m, n, ld, y, w, b, bptr, flag, out, rpb, fws)
 #define SRML_LR_PF_V(RR, DD) \

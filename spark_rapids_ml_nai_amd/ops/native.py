@@ -26,7 +26,7 @@ _D = ctypes.c_double
 _F = ctypes.c_float
 
 # name -> argtypes (restype: int status, except the size queries in _LONG_RESULT)
-_LONG_RESULT = ("srml_rf_bootstrap_ws", "srml_qn_args_size", "srml_logit_residual_ws", "srml_xtv_mfma_ws",
+_LONG_RESULT = ("srml_rf_bootstrap_ws", "srml_logreg_fold_ws", "srml_qn_args_size", "srml_logit_residual_ws", "srml_xtv_mfma_ws",
                 "srml_rf_partition_ws",
                 "srml_label_sort_ws", "srml_radix_sort_ws")
 SIGNATURES: Dict[str, Tuple[Any, ...]] = {
@@ -44,6 +44,8 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_row_sqnorm_f32": (_P, _L, _I, _L, _P, _P),
     "srml_logreg_binary_f32": (_P, _L, _I, _L, _P, _P, _D, _P, _P),
     "srml_logreg_binary2_f32": (_P, _L, _I, _L, _P, _P, _D, _P, _P, _P, _P),
+    "srml_logreg_binary3_f32": (_P, _L, _I, _L, _P, _P, _D, _P, _P, _P, _P, _P),
+    "srml_logreg_fold_ws": (_L, _I),
     "srml_logreg_binary_lds_f32": (_P, _L, _I, _L, _P, _P, _D, _P, _P, _P, _P),
     "srml_logreg_binary_lds_f64": (_P, _L, _I, _L, _P, _P, _D, _P, _P, _P, _P),
     "srml_xtv2_f32": (_P, _L, _I, _L, _P, _I, _L, _P, _L, _L, _P, _P),
