@@ -115,12 +115,22 @@ def logistic_fit(X: Any, y: torch.Tensor, m_total: int, ctx: WorkerContext, reg:
 
     allreduce = ctx.comm.allreduce if ctx.world_size > 1 else None
     path = ops.logistic_path(X, K)
+    fold = evaluate_partials = None
+    if ws is not None and allreduce is None and path == "fused_binary_f32":
+        # one rank: the evaluation leaves its per-block partial rows and the fused optimiser step
+        # folds them (one launch per evaluation instead of three)
+        parts, wst = ops.logreg_fold_layout(X)
+        fold = (ws, parts, wst)
+        _scratch = torch.zeros(K * n + 2, dtype=torch.float64, device=X.device)
+
+        def evaluate_partials(w: torch.Tensor, b: torch.Tensor, flag: Optional[torch.Tensor]) -> None:
+            ops.logistic_loss_grad(X, y32, w, b, K, _scratch, flag, ws=ws, leave_partials=True)
     # stream-ordered device evaluations (no host sync; allocations come from the graph's pool) may
     # be replayed from a HIP graph
     graph_safe = path in ("fused_binary_f32", "fused_multinomial_f32", "csr_binary", "two_pass_multinomial_f32",
                           "two_pass_binary_f32") or path.startswith("lds_binary")
     res = minimize(P, theta0, evaluate, allreduce, y.device, batch=8 if not path.startswith("torch") else 2,
-                   graph_safe=graph_safe)
+                   graph_safe=graph_safe, fold=fold, evaluate_partials=evaluate_partials)
     return _result(res, base, ctx, n, K, fit_intercept, inv_sigma, path)
 
 

@@ -34,9 +34,14 @@ import numpy as np
 import torch
 
 QN_GRAPH = os.environ.get("SRML_QN_GRAPH", "1") != "0"
+# the optimiser step: "fused" (default, N <= 16384) = ONE launch of G blocks with software grid
+# barriers, which can also fold the binary evaluation's partial rows itself (srml_qn_step_fused);
+# "mb" = four multi-block launches (srml_qn_step_mb); "single" = the one-block kernel
+QN_STEP = os.environ.get("SRML_QN_STEP", "fused")
+QN_MB = QN_STEP in ("fused", "mb")
 GRAPH_STATS = {"captures": 0, "replays": 0}  # observability / tests
 STATUS = {0: "running", 1: "converged (gradient)", 2: "converged (objective change)", 3: "max iterations",
-          4: "line search failed"}
+          4: "line search failed", 5: "barrier timeout"}
 F_DONE, F_STATUS, F_ITER, F_NEVAL, F_LS, F_COUNT, F_HEAD, F_STARTED, F_BRACKET = range(9)
 SC_F, SC_ALPHA, SC_DGINIT, SC_GAMMA, SC_GINF = range(5)
 
@@ -306,6 +311,13 @@ class DeviceQN:
             a.probe = self.probe.data_ptr()
         self._args = a
         self._keep = ptrs
+        self._mb = None
+        self._fused = QN_MB and QN_STEP == "fused"
+        self.fold: Optional[tuple] = None  # (partial-row workspace, rows, stride) the fused step folds
+        if QN_MB and N <= 16384 and os.environ.get("SRML_QN_PROBE") != "1":
+            lib = native.lib()
+            size = int(lib.srml_qn_fused_scratch() if self._fused else lib.srml_qn_mb_scratch())
+            self._mb = torch.zeros(size, **f64)  # zeroed: the fused step's barrier words start at 0
         assert ctypes.sizeof(_QnArgs) == int(native.lib().srml_qn_args_size()), "QnArgs layout mismatch"
 
     @property
@@ -319,7 +331,14 @@ class DeviceQN:
     def step(self) -> None:
         from ..ops import native
 
-        native.call("srml_qn_step", ctypes.addressof(self._args), native.stream(self.device))
+        if self._mb is not None and self._fused:
+            ws, parts, wst = self.fold if self.fold is not None else (None, 0, 0)
+            native.call("srml_qn_step_fused", ctypes.addressof(self._args), self._mb.data_ptr(),
+                        ws.data_ptr() if ws is not None else None, int(parts), int(wst), native.stream(self.device))
+        elif self._mb is not None:
+            native.call("srml_qn_step_mb", ctypes.addressof(self._args), self._mb.data_ptr(), native.stream(self.device))
+        else:
+            native.call("srml_qn_step", ctypes.addressof(self._args), native.stream(self.device))
 
     def theta(self) -> np.ndarray:
         return self.x.cpu().numpy().copy()
@@ -340,13 +359,18 @@ def _comm_poll(allreduce: Optional[Callable]) -> Optional[Callable[[], None]]:
 def minimize(P: QNProblem, theta0: np.ndarray, evaluate: Callable[[torch.Tensor, torch.Tensor, Optional[torch.Tensor],
                                                                    torch.Tensor], None],
              allreduce: Optional[Callable[[torch.Tensor], None]], device: torch.device,
-             batch: int = 8, graph_safe: bool = False) -> dict:
+             batch: int = 8, graph_safe: bool = False, fold: Optional[tuple] = None,
+             evaluate_partials: Optional[Callable] = None) -> dict:
     """Run the QN iteration. ``evaluate(w, b, flag, out)`` must ADD the summed data-term
     [grad_w (K*n) | grad_b (K) | loss] of this rank's rows at (w, b) into ``out`` (device
     tensors; ``flag`` is the device done-flag it may use to early-exit, None on the host path).
     ``allreduce(out)`` sums ``out`` over ranks in place (None for one rank). ``graph_safe``: the
     evaluation is stream-ordered device work only (no host sync, no allocation), so a one-rank fit
     may capture the batch in a HIP graph (``SRML_QN_GRAPH=0`` disables).
+
+    ``fold`` = (workspace, rows, stride) with ``evaluate_partials(w, b, flag)``: a one-rank fit
+    whose evaluation can leave per-block partial rows in the workspace instead of summing into
+    ``out``; the fused device step then folds them itself (one launch less per evaluation).
 
     Returns {theta, f, iter, n_evals, status}.
     """
@@ -364,6 +388,9 @@ def minimize(P: QNProblem, theta0: np.ndarray, evaluate: Callable[[torch.Tensor,
         return {"theta": st.theta(), "f": st.f, "iter": st.iter, "n_evals": st.n_evals,
                 "status": STATUS[st.status if st.done else 3]}
     q = DeviceQN(P, theta0, device)
+    if fold is not None and evaluate_partials is not None and allreduce is None and q._fused and q._mb is not None:
+        q.fold = fold
+        evaluate = lambda w, b, flag, out: evaluate_partials(w, b, flag)  # noqa: E731
     poll = _comm_poll(allreduce)
     flag = q.flags[F_DONE: F_DONE + 1]
     host_flag = torch.zeros(2, dtype=torch.int32, pin_memory=True)
@@ -422,6 +449,8 @@ def minimize(P: QNProblem, theta0: np.ndarray, evaluate: Callable[[torch.Tensor,
                 break
     torch.cuda.synchronize(device)
     res = q.info()
+    if res["status"] == "barrier timeout":
+        raise RuntimeError("device L-BFGS step: a grid barrier timed out (blocks not co-resident)")
     res["theta"] = q.theta()
     if not res["done"]:
         res["status"] = "evaluation cap"

@@ -298,8 +298,14 @@ def logreg_binary_loss_grad(X: torch.Tensor, y: torch.Tensor, w: torch.Tensor, b
     yf = _c(y.to(torch.float32))
     ws = logreg_workspace(X)
     native.call("srml_logreg_binary3_f32", X.data_ptr(), m, n, X.stride(0), yf.data_ptr(), wf.data_ptr(), float(b),
-                None, None, out.data_ptr(), ws.data_ptr() if ws is not None else None, native.stream(X.device))
+                None, None, out.data_ptr(), ws.data_ptr() if ws is not None else None, 0, native.stream(X.device))
     return out
+
+
+def logreg_fold_layout(X: Any) -> Tuple[int, int]:
+    """(partial rows, row stride in floats) of ``logreg_workspace(X)``."""
+    m, n = X.shape
+    return int(native.lib().srml_logreg_fold_parts(m)), ((n + 3) & ~3) + 4
 
 
 def logreg_workspace(X: Any) -> Optional[torch.Tensor]:
@@ -2283,7 +2289,8 @@ def logistic_loss_grad_multi(X: torch.Tensor, y32: torch.Tensor, WB: torch.Tenso
 
 
 def logistic_loss_grad(X, y32: torch.Tensor, w: torch.Tensor, b: torch.Tensor, K: int, out: torch.Tensor,
-                       flag: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None) -> torch.Tensor:
+                       flag: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None,
+                       leave_partials: bool = False) -> torch.Tensor:
     """ADD the summed logistic data term at (W, b) into ``out`` = [grad W (K*n, class-major) |
     grad b (K) | loss sum] (fp64). K == 1: binary (labels 0/1, sigmoid); K >= 2: softmax over K
     classes (labels 0..K-1). ``w`` (K*n) and ``b`` (K) are fp64 device tensors read by the kernel
@@ -2354,9 +2361,11 @@ def logistic_loss_grad(X, y32: torch.Tensor, w: torch.Tensor, b: torch.Tensor, K
                     r.data_ptr(), 1, out[n:].data_ptr(), 1, out[n + 1:].data_ptr(), 1, fp, st)
         dgemm(X, r, ta=True, beta=1.0, out=out[:n].view(n, 1))
     elif path == "fused_binary_f32":
-        # ws: the fit's partial-row workspace (ops.logreg_workspace), None = per-block atomic flush
+        # ws: the fit's partial-row workspace (ops.logreg_workspace), None = per-block atomic flush;
+        # leave_partials: the rows stay unfolded for the fused optimiser step (srml_qn_step_fused)
         native.call("srml_logreg_binary3_f32", X.data_ptr(), m, n, X.stride(0), y32.data_ptr(), w.data_ptr(), 0.0,
-                    b.data_ptr(), fp, out.data_ptr(), ws.data_ptr() if ws is not None else None, st)
+                    b.data_ptr(), fp, out.data_ptr(), ws.data_ptr() if ws is not None else None,
+                    int(bool(leave_partials and ws is not None)), st)
     elif path.startswith("lds_binary"):
         native.call("srml_logreg_binary_lds_" + path[-3:], X.data_ptr(), m, n, X.stride(0), y32.data_ptr(),
                     w.data_ptr(), 0.0, b.data_ptr(), fp, out.data_ptr(), st)

@@ -853,38 +853,67 @@ __global__ __launch_bounds__(256) void logreg_binary_narrow_kernel(const float* 
   }
 }
 
-// Sum of `parts` partial rows (fp32 columns + 2 trailing fp64 [gb, loss]) into out (fp64). Thread
-// = 4 columns of one slice of FOLD_ROWS consecutive rows (independent 16-B loads, fp64 sums), one
-// fp64 atomic per column and slice: ~parts / FOLD_ROWS atomics per column instead of parts.
-constexpr int FOLD_ROWS = 16;
+// Sum of `parts` partial rows (fp32 columns + 2 trailing fp64 [gb, loss]) into out (fp64), no
+// atomics: block b owns columns [64 b, 64 b + 64) — 16 lanes x float4 per row, 16 row groups
+// striding the rows (independent 16-B loads, fp64 sums), folded through LDS and added into its
+// own columns with plain read-modify-writes; the extra last block folds gb / loss. (A per-slice
+// fp64 atomic fold took 12 us at 768 partial rows: 48-way contention on every column.)
 __global__ __launch_bounds__(256) void fold_rows_kernel(const float* __restrict__ ws, int parts, long wst, int n,
                                                         double* __restrict__ out, const int* __restrict__ flag) {
   if (flag && *flag) return;
-  const int c = ((int)blockIdx.x * 256 + (int)threadIdx.x) * 4;
-  const int p0 = (int)blockIdx.y * FOLD_ROWS, p1 = min(parts, p0 + FOLD_ROWS);
-  if (c < n) {
-    double a[4] = {0.0, 0.0, 0.0, 0.0};
-    floatx4 t[FOLD_ROWS];
+  __shared__ double red[16][65];
+  const int t = threadIdx.x;
+  const int q = t & 15, rg = t >> 4;
+  const int ncb = (n + 63) / 64;
+  if ((int)blockIdx.x < ncb) {
+    const int c = (int)blockIdx.x * 64 + 4 * q;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    if (c < n) {
+      int p = rg;
+      for (; p + 48 < parts; p += 64) {  // 4 rows in flight per thread
+        floatx4 v[4];
 #pragma unroll
-    for (int j = 0; j < FOLD_ROWS; ++j)
-      t[j] = p0 + j < p1 ? __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(ws + (long)(p0 + j) * wst + c))
-                         : floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < 4; ++j)
+          v[j] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(ws + (long)(p + 16 * j) * wst + c));
 #pragma unroll
-    for (int j = 0; j < FOLD_ROWS; ++j)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) a[q] += (double)t[j][q];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (c + q < n) atomicAdd(&out[c + q], a[q]);
-  } else if (c == ((n + 3) & ~3)) {  // the thread just past the columns folds gb and loss
-    double gb = 0.0, loss = 0.0;
-    for (int p = p0; p < p1; ++p) {
-      const double* pd = reinterpret_cast<const double*>(ws + (long)p * wst + wst - 4);
-      gb += pd[0];
-      loss += pd[1];
+        for (int j = 0; j < 4; ++j) { a0 += v[j][0]; a1 += v[j][1]; a2 += v[j][2]; a3 += v[j][3]; }
+      }
+      for (; p < parts; p += 16) {
+        const floatx4 v = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(ws + (long)p * wst + c));
+        a0 += v[0]; a1 += v[1]; a2 += v[2]; a3 += v[3];
+      }
     }
-    atomicAdd(&out[n], gb);
-    atomicAdd(&out[n + 1], loss);
+    red[rg][4 * q] = a0;
+    red[rg][4 * q + 1] = a1;
+    red[rg][4 * q + 2] = a2;
+    red[rg][4 * q + 3] = a3;
+    __syncthreads();
+    if (t < 64) {
+      const int cc = (int)blockIdx.x * 64 + t;
+      double sum = 0.0;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) sum += red[g][t];
+      if (cc < n) out[cc] += sum;
+    }
+    return;
+  }
+  // last block: gb and loss
+  double gb = 0.0, loss = 0.0;
+  for (int p = t; p < parts; p += 256) {
+    const double* pd = reinterpret_cast<const double*>(ws + (long)p * wst + wst - 4);
+    gb += pd[0];
+    loss += pd[1];
+  }
+  gb = wave_sum(gb);
+  loss = wave_sum(loss);
+  if ((t & 63) == 0) {
+    red[0][t >> 6] = gb;
+    red[1][t >> 6] = loss;
+  }
+  __syncthreads();
+  if (t == 0) {
+    out[n] += (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    out[n + 1] += (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
   }
 }
 
@@ -911,26 +940,31 @@ SRML_API long srml_logreg_fold_ws(long m, int n) {
   return logreg_grid(m) * (((n + 3) & ~3) + 4);
 }
 
+// Partial rows (= blocks) the workspace holds for m rows; row stride ((n + 3) & ~3) + 4 floats.
+SRML_API long srml_logreg_fold_parts(long m) { return m <= 0 ? 0 : logreg_grid(m); }
+
 static int logreg_binary_launch(const float* X, long m, int n, long ld, const float* y, const double* w, double b,
-                                const double* bptr, const int* flag, double* out, float* fold_ws,
+                                const double* bptr, const int* flag, double* out, float* fold_ws, int leave,
                                 hipStream_t stream);
 
 // b: intercept by value, or (bptr != null) read on the device; flag (optional): skip when *flag != 0
 SRML_API int srml_logreg_binary2_f32(const float* X, long m, int n, long ld, const float* y, const double* w, double b,
                                      const double* bptr, const int* flag, double* out, hipStream_t stream) {
-  return logreg_binary_launch(X, m, n, ld, y, w, b, bptr, flag, out, nullptr, stream);
+  return logreg_binary_launch(X, m, n, ld, y, w, b, bptr, flag, out, nullptr, 0, stream);
 }
 
 // Same with the caller's partial-row workspace (srml_logreg_fold_ws floats, owned by ONE fit: the
-// block partials and their fold are two launches, so interleaved fits need separate workspaces)
+// block partials and their fold are two launches, so interleaved fits need separate workspaces).
+// leave != 0: the rows are NOT folded into `out` here — the consumer (the fused optimiser step,
+// srml_qn_step_fused) folds them itself.
 SRML_API int srml_logreg_binary3_f32(const float* X, long m, int n, long ld, const float* y, const double* w, double b,
-                                     const double* bptr, const int* flag, double* out, float* fold_ws,
+                                     const double* bptr, const int* flag, double* out, float* fold_ws, int leave,
                                      hipStream_t stream) {
-  return logreg_binary_launch(X, m, n, ld, y, w, b, bptr, flag, out, fold_ws, stream);
+  return logreg_binary_launch(X, m, n, ld, y, w, b, bptr, flag, out, fold_ws, leave, stream);
 }
 
 static int logreg_binary_launch(const float* X, long m, int n, long ld, const float* y, const double* w, double b,
-                                const double* bptr, const int* flag, double* out, float* fold_ws,
+                                const double* bptr, const int* flag, double* out, float* fold_ws, int leave,
                                 hipStream_t stream) {
   if (m <= 0) return 0;
   static const int narrow = getenv("SRML_LOGREG_NARROW") ? atoi(getenv("SRML_LOGREG_NARROW")) : 1;
@@ -992,9 +1026,9 @@ static int logreg_binary_launch(const float* X, long m, int n, long ld, const fl
     }
     else if (dsel == 3) SRML_LR_PF_V(1, 3);
     else SRML_LR_PF_V(1, 2);
-    if (fws)
-      hipLaunchKernelGGL(fold_rows_kernel, dim3(ceil_div(wst, 1024), ceil_div(blocks, FOLD_ROWS)), dim3(256), 0, stream,
-                         fws, (int)blocks, wst, n, out, flag);
+    if (fws && !leave)
+      hipLaunchKernelGGL(fold_rows_kernel, dim3(ceil_div(n, 64) + 1), dim3(256), 0, stream, fws, (int)blocks, wst, n,
+                         out, flag);
     return srml_status();
   }
   if (split == 1 && n > 1024 && n <= 4096) {

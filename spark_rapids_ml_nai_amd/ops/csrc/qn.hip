@@ -595,3 +595,972 @@ SRML_API int srml_qn_step(const QnArgs* a, hipStream_t stream) {
 
 SRML_API int srml_qn_max_history() { return QN_MMAX; }
 SRML_API long srml_qn_args_size() { return (long)sizeof(QnArgs); }
+
+// ------------------------------------------------------------------------------------------
+// Multi-block step (one problem): the single-block step above spends ~40 us walking ~1.7 MB of
+// optimiser state (x, g, pg, d, xt, gt and the S / Y history) through ONE CU. Here the same state
+// machine runs as four launches over G blocks of 256 threads (element i belongs to one thread of
+// one block), the kernel boundaries standing in for grid barriers:
+//   K1  pass 0 (gt, penalty / directional partials); pre-step scalars snapshotted to scratch;
+//   K2  every block reduces K1's partials (block order: all blocks see the same bits) and takes the
+//       same line-search decision; reject -> its share of the next trial point (block 0 updates
+//       the flags); accept -> pass 1 (pg, s, y and every compact-form dot product) partials;
+//   K3  every block reduces them, repeats the bookkeeping / convergence test / compact-form solve
+//       redundantly (identical inputs, identical results), stores its share of the new pair,
+//       x <- xt, g <- gt and the direction, and leaves the p.d / d.d partials;
+//   K4  reduce, descent check, its share of the next trial point; block 0 commits the optimiser
+//       scalars, flags and history Gram blocks (deferred so no block of K3 reads state another
+//       block of K3 already advanced).
+// Same arithmetic as the single-block step except the summation order of the reductions.
+// ------------------------------------------------------------------------------------------
+namespace {
+
+constexpr int MB_T = 256;
+constexpr int MB_NW = MB_T / 64;
+constexpr int MB_GMAX = 64;
+constexpr int MB_PW = 6 + 5 * QN_MMAX + 1;  // pass-1 partials: 6 dots, 5 history products per slot, max |pg|
+enum {
+  S_STARTED = 0, S_ITER, S_COUNT, S_HEAD, S_LS, S_NEVAL, S_BRACKET, S_F, S_ALPHA, S_DGINIT, S_GAMMA, S_FHN, S_LOSS,
+  S_PHASE = 16, S_STATUS, S_NEWP, S_CNT, S_HD, S_GAM, S_FT, S_GINF, S_ITERN, S_FN,
+  S_CF = 32,                              // cf_a[QN_MMAX] | cf_t[QN_MMAX]
+  S_SL = S_CF + 2 * QN_MMAX,              // chronological slots [QN_MMAX]
+  S_SY = S_SL + QN_MMAX,                  // updated SY [QN_MMAX^2] | YY [QN_MMAX^2] (committed by K4)
+  S_PA = S_SY + 2 * QN_MMAX * QN_MMAX,    // K1 partials [G][4]
+  S_PB = S_PA + 4 * MB_GMAX,              // K2 partials [G][MB_PW]
+  S_PC = S_PB + MB_PW * MB_GMAX,          // K3 partials [G][2]
+  S_END = S_PC + 2 * MB_GMAX
+};
+
+// block-wide sums of NV values (256 threads): thread j < NV gets total j in `out` (LDS)
+template <int NV>
+__device__ __forceinline__ void mb_block_sum(const double (&v)[NV], double* red, double* out) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const double t = wave_sum(v[i]);
+    if (lane == 0) red[i * MB_NW + wid] = t;
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  __syncthreads();
+  if (threadIdx.x < NV) {
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < MB_NW; ++w) s += red[threadIdx.x * MB_NW + w];
+    out[threadIdx.x] = s;
+  }
+  __syncthreads();
+}
+
+// grid totals of a [G][width] partial table, summed in block order into LDS `tot` (all threads)
+__device__ __forceinline__ void mb_grid_sum(const double* part, int G, int width, double* tot, bool max_last) {
+  for (int j = threadIdx.x; j < width; j += MB_T) {
+    double s = 0.0;
+    const bool mx = max_last && j == width - 1;
+    for (int b = 0; b < G; ++b) s = mx ? fmax(s, part[(long)b * width + j]) : s + part[(long)b * width + j];
+    tot[j] = s;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void mb_set_trial(const QnArgs& A, double alpha) {
+  const long i = (long)blockIdx.x * MB_T + threadIdx.x;
+  if (i >= A.N) return;
+  const double xv = A.x[i], dv = A.d[i];
+  double t = xv + alpha * dv;
+  if (A.l1) {
+    const double cv = A.l1c[i];
+    if (cv > 0.0) {
+      const double pv = A.pg[i];
+      const double orth = xv != 0.0 ? (xv > 0.0 ? 1.0 : -1.0) : (pv < 0.0 ? 1.0 : (pv > 0.0 ? -1.0 : 0.0));
+      if (t * orth <= 0.0) t = 0.0;
+    }
+  }
+  A.xt[i] = t;
+  A.wb[i] = t * (i < A.Kn ? A.isg[i % A.n] : 1.0);
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(MB_T) void qn_mb1_kernel(QnArgs A, double* __restrict__ scr) {
+  __shared__ double red[4 * MB_NW], tot[4];
+  const int* fl = A.fl;
+  const bool first = blockIdx.x == 0 && threadIdx.x == 0;
+  if (fl[F_DONE]) {
+    if (first) scr[S_PHASE] = 0.0;  // K3 / K4 must not act on a stale phase
+    return;
+  }
+  if (first) {  // pre-step snapshot: later kernels read these, block 0 of K2 / K4 rewrites the flags
+    const bool started = fl[F_STARTED] != 0;
+    scr[S_STARTED] = started ? 1.0 : 0.0;
+    scr[S_ITER] = fl[F_ITER];
+    scr[S_COUNT] = fl[F_COUNT];
+    scr[S_HEAD] = fl[F_HEAD];
+    scr[S_LS] = fl[F_LS];
+    scr[S_NEVAL] = fl[F_NEVAL];
+    scr[S_BRACKET] = fl[F_BRACKET];
+    scr[S_F] = A.sc[SC_F];
+    scr[S_ALPHA] = A.sc[SC_ALPHA];
+    scr[S_DGINIT] = A.sc[SC_DGINIT];
+    scr[S_GAMMA] = A.sc[SC_GAMMA];
+    scr[S_FHN] = (A.past > 0 && started) ? A.fh[(fl[F_ITER] + 1) % A.past] : 0.0;
+    scr[S_LOSS] = A.out[A.Kn + A.K];
+    scr[S_PHASE] = 0.0;
+  }
+  double p0[4] = {0.0, 0.0, 0.0, 0.0};
+  const long i = (long)blockIdx.x * MB_T + threadIdx.x;
+  if (i < A.N) {
+    const double xv = A.xt[i];
+    const double gi = A.out[i] * A.inv_m * (i < A.Kn ? A.isg[i % A.n] : 1.0) + A.l2[i] * xv;
+    A.gt[i] = gi;
+    p0[0] = A.l2[i] * xv * xv;
+    p0[1] = A.l1c[i] * fabs(xv);
+    p0[2] = gi * A.d[i];
+    p0[3] = A.pg[i] * (xv - A.x[i]);
+    if (i < A.Kn + A.K) A.out[i] = 0.0;  // this element's evaluation sum is consumed
+  }
+  mb_block_sum<4>(p0, red, tot);
+  if (threadIdx.x < 4) scr[S_PA + blockIdx.x * 4 + threadIdx.x] = tot[threadIdx.x];
+}
+
+__global__ __launch_bounds__(MB_T) void qn_mb2_kernel(QnArgs A, double* __restrict__ scr) {
+  __shared__ double red[MB_PW * MB_NW], tot[MB_PW], p0[4];
+  int* fl = A.fl;
+  if (fl[F_DONE]) return;
+  const int G = gridDim.x;
+  mb_grid_sum(scr + S_PA, G, 4, p0, false);
+  const bool started = scr[S_STARTED] != 0.0;
+  const double f = scr[S_F], dginit = scr[S_DGINIT];
+  double alpha = scr[S_ALPHA];
+  const double ft = scr[S_LOSS] * A.inv_m + 0.5 * p0[0] + p0[1];
+  const bool first = blockIdx.x == 0 && threadIdx.x == 0;
+  if (first)  // the loss sum (read from the snapshot) and bias sums without a parameter (no intercept)
+    for (long j = A.N; j < A.Kn + A.K + 1; ++j) A.out[j] = 0.0;
+  if (started) {
+    bool accept = true;
+    double width = 1.0;
+    if (!isfinite(ft)) {
+      accept = false;
+      width = 0.5;
+    } else {
+      const double dgtest = A.l1 ? p0[3] : alpha * dginit;
+      if (ft > f + A.c1 * dgtest) {
+        accept = false;
+        const double den = 2.0 * (ft - f - dgtest);
+        width = den > 0.0 ? -dgtest / den : 0.5;
+        width = isfinite(width) ? fmin(0.5, fmax(0.1, width)) : 0.5;
+      } else if (A.wolfe && !A.l1 && scr[S_BRACKET] == 0.0 && p0[2] < A.c2 * dginit) {
+        accept = false;
+        width = 2.1;
+      }
+    }
+    if (!accept) {
+      const int ls = (int)scr[S_LS] + 1;
+      if (ls >= A.max_ls) {
+        if (first) {
+          fl[F_LS] = ls;
+          fl[F_NEVAL] = (int)scr[S_NEVAL] + 1;
+          fl[F_STATUS] = ST_LS_FAIL;
+          fl[F_DONE] = 1;
+        }
+        return;
+      }
+      alpha *= width;
+      mb_set_trial(A, alpha);
+      if (first) {
+        fl[F_LS] = ls;
+        fl[F_NEVAL] = (int)scr[S_NEVAL] + 1;
+        if (width < 1.0) fl[F_BRACKET] = 1;
+        A.sc[SC_ALPHA] = alpha;
+      }
+      return;
+    }
+  }
+  if (first) {
+    scr[S_PHASE] = 1.0;
+    scr[S_FT] = ft;
+  }
+  // accepted: pass 1 partials of this block's elements
+  const int M = A.M;
+  const long N = A.N;
+  double v[MB_PW];
+#pragma unroll
+  for (int j = 0; j < MB_PW; ++j) v[j] = 0.0;
+  const long i = (long)blockIdx.x * MB_T + threadIdx.x;
+  if (i < N) {
+    const double xv = A.xt[i], gv = A.gt[i];
+    const double sx = started ? xv - A.x[i] : 0.0;
+    const double yx = started ? gv - A.g[i] : 0.0;
+    const double pgi = pseudo_grad(xv, gv, A.l1 ? A.l1c[i] : 0.0);
+    A.pg[i] = pgi;
+    A.d[i] = sx;
+    A.wb[i] = yx;
+    v[0] = sx * yx;
+    v[1] = yx * yx;
+    v[2] = sx * pgi;
+    v[3] = yx * pgi;
+    v[4] = pgi * pgi;
+    v[MB_PW - 1] = fabs(pgi);
+#pragma unroll
+    for (int j = 0; j < QN_MMAX; ++j) {
+      if (j < M) {
+        const double Sj = A.S[(long)j * N + i], Yj = A.Y[(long)j * N + i];
+        v[6 + j] = sx * Yj;
+        v[6 + QN_MMAX + j] = Sj * yx;
+        v[6 + 2 * QN_MMAX + j] = yx * Yj;
+        v[6 + 3 * QN_MMAX + j] = Sj * pgi;
+        v[6 + 4 * QN_MMAX + j] = Yj * pgi;
+      }
+    }
+  }
+  // block sums (the last entry is a max)
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < MB_PW - 1; ++j) {
+    const double t = wave_sum(v[j]);
+    if (lane == 0) red[j * MB_NW + wid] = t;
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  {
+    double mx = v[MB_PW - 1];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+    if (lane == 0) red[(MB_PW - 1) * MB_NW + wid] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x < MB_PW) {
+    const int j = threadIdx.x;
+    double s = 0.0;
+    for (int w = 0; w < MB_NW; ++w)
+      s = j == MB_PW - 1 ? fmax(s, red[j * MB_NW + w]) : s + red[j * MB_NW + w];
+    scr[S_PB + (long)blockIdx.x * MB_PW + j] = s;
+  }
+}
+
+__global__ __launch_bounds__(MB_T) void qn_mb3_kernel(QnArgs A, double* __restrict__ scr) {
+  __shared__ double tot[MB_PW], red[2 * MB_NW], t2[2];
+  __shared__ double s_sy[QN_MMAX * QN_MMAX], s_yy[QN_MMAX * QN_MMAX], s_p1[QN_MMAX], s_p2[QN_MMAX];
+  __shared__ double cf_a[QN_MMAX], cf_t[QN_MMAX], s_misc[2];
+  __shared__ int s_sl[QN_MMAX], s_ctl[4];
+  if (scr[S_PHASE] != 1.0) return;
+  const int G = gridDim.x, M = A.M, tid = threadIdx.x;
+  const long N = A.N;
+  mb_grid_sum(scr + S_PB, G, MB_PW, tot, true);
+  for (int i = tid; i < M * M; i += MB_T) {
+    s_sy[i] = A.SY[i];  // K4's block 0 commits the updated blocks: every block reads the old ones here
+    s_yy[i] = A.YY[i];
+  }
+  __syncthreads();
+  const bool started = scr[S_STARTED] != 0.0;
+  if (tid == 0) {
+    int cnt = (int)scr[S_COUNT], hd = (int)scr[S_HEAD], status = ST_RUNNING;
+    double gamma = started ? scr[S_GAMMA] : 1.0;
+    for (int j = 0; j < M; ++j) {
+      s_p1[j] = tot[6 + 3 * QN_MMAX + j];
+      s_p2[j] = tot[6 + 4 * QN_MMAX + j];
+    }
+    const double ys = tot[0], yy = tot[1];
+    const bool newp = started && yy > 0.0 && ys > 1e-10 * yy;
+    if (newp) {
+      const int h = hd;
+      for (int j = 0; j < M; ++j) {
+        if (j == h) continue;
+        s_sy[h * M + j] = tot[6 + j];
+        s_sy[j * M + h] = tot[6 + QN_MMAX + j];
+        s_yy[h * M + j] = tot[6 + 2 * QN_MMAX + j];
+        s_yy[j * M + h] = tot[6 + 2 * QN_MMAX + j];
+      }
+      s_sy[h * M + h] = ys;
+      s_yy[h * M + h] = yy;
+      s_p1[h] = tot[2];
+      s_p2[h] = tot[3];
+      hd = (h + 1) % M;
+      cnt = cnt < M ? cnt + 1 : M;
+      gamma = ys / yy;
+    }
+    const double fn = scr[S_FT];
+    const double ginf = tot[MB_PW - 1];
+    const int iter = (int)scr[S_ITER] + (started ? 1 : 0);
+    const double fmag = fmax(fabs(fn), A.tol);
+    if (ginf <= A.tol * fmag) status = ST_CONV_GRAD;
+    if (A.past > 0 && status == ST_RUNNING && started && iter >= A.past &&
+        fabs(scr[S_FHN] - fn) <= A.delta * fmag)
+      status = ST_CONV_F;
+    if (status == ST_RUNNING && iter >= A.max_iter) status = ST_MAXITER;
+    for (int c = 0; c < cnt; ++c) s_sl[c] = (hd - cnt + c + 2 * M) % M;
+    s_ctl[0] = status;
+    s_ctl[1] = newp ? 1 : 0;
+    s_ctl[2] = cnt;
+    s_ctl[3] = hd;
+    s_misc[0] = gamma;
+    s_misc[1] = ginf;
+    if (blockIdx.x == 0) {  // the commit record for K4
+      scr[S_STATUS] = status;
+      scr[S_NEWP] = newp ? 1.0 : 0.0;
+      scr[S_CNT] = cnt;
+      scr[S_HD] = hd;
+      scr[S_GAM] = gamma;
+      scr[S_GINF] = ginf;
+      scr[S_ITERN] = iter;
+      scr[S_FN] = fn;
+    }
+  }
+  __syncthreads();
+  // compact-form coefficients (wave 0, as the single-block step)
+  if (tid < 64) {
+    const int cnt = s_ctl[2];
+    const double gamma = s_misc[0];
+    const int c = tid;
+    const bool act = c < cnt;
+    const int slc = act ? s_sl[c] : 0;
+    double Rrow[QN_MMAX], Rcol[QN_MMAX], Yrow[QN_MMAX], tv[QN_MMAX];
+#pragma unroll
+    for (int e = 0; e < QN_MMAX; ++e) {
+      const bool ok = act && e < cnt;
+      const int sle = ok ? s_sl[e] : 0;
+      Rrow[e] = ok ? s_sy[slc * M + sle] : 0.0;
+      Rcol[e] = ok ? s_sy[sle * M + slc] : 0.0;
+      Yrow[e] = ok ? s_yy[slc * M + sle] : 0.0;
+      tv[e] = 0.0;
+    }
+    const double diag = act ? s_sy[slc * M + slc] : 1.0;
+    double acc = act ? s_p1[slc] : 0.0;
+    double tmine = 0.0;
+#pragma unroll
+    for (int e = QN_MMAX - 1; e >= 0; --e) {
+      if (e < cnt) {
+        const double te = __shfl(acc / diag, e, 64);
+        tv[e] = te;
+        if (c == e) tmine = te;
+        if (c < e) acc -= Rrow[e] * te;
+      }
+    }
+    acc = diag * tmine - gamma * (act ? s_p2[slc] : 0.0);
+#pragma unroll
+    for (int e = 0; e < QN_MMAX; ++e) acc += gamma * Yrow[e] * tv[e];
+    double amine = 0.0;
+#pragma unroll
+    for (int e = 0; e < QN_MMAX; ++e) {
+      if (e < cnt) {
+        const double ae = __shfl(acc / diag, e, 64);
+        if (c == e) amine = ae;
+        if (c > e) acc -= Rcol[e] * ae;
+      }
+    }
+    if (c < QN_MMAX) {
+      cf_a[c] = 0.0;
+      cf_t[c] = 0.0;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (act) {
+      cf_a[slc] = amine;
+      cf_t[slc] = gamma * tmine;
+    }
+  }
+  __syncthreads();
+  const int status = s_ctl[0];
+  const bool newp = s_ctl[1] != 0;
+  const int cnt = s_ctl[2];
+  const double gamma = s_misc[0];
+  if (blockIdx.x == 0 && newp)  // staged for K4 (other blocks of this launch still read A.SY / A.YY)
+    for (int i = tid; i < M * M; i += MB_T) {
+      scr[S_SY + i] = s_sy[i];
+      scr[S_SY + QN_MMAX * QN_MMAX + i] = s_yy[i];
+    }
+  // pass 2: store the pair, x <- xt, g <- gt, direction
+  double p2v[2] = {0.0, 0.0};
+  const long i = (long)blockIdx.x * MB_T + tid;
+  const int head = (int)scr[S_HEAD];
+  if (i < N) {
+    const double xv = A.xt[i], gv = A.gt[i], sv = A.d[i], yv = A.wb[i], pv = A.pg[i];
+    if (newp) {
+      A.S[(long)head * N + i] = sv;
+      A.Y[(long)head * N + i] = yv;
+    }
+    A.x[i] = xv;
+    A.g[i] = gv;
+    if (status == ST_RUNNING) {
+      double hg = gamma * pv;
+      for (int c = 0; c < cnt; ++c) {
+        const int j = s_sl[c];
+        hg += cf_a[j] * A.S[(long)j * N + i] - cf_t[j] * A.Y[(long)j * N + i];
+      }
+      double di = -hg;
+      if (A.l1 && A.l1c[i] > 0.0 && di * pv >= 0.0) di = 0.0;
+      A.d[i] = di;
+      p2v[0] = pv * di;
+      p2v[1] = di * di;
+    }
+  }
+  mb_block_sum<2>(p2v, red, t2);
+  if (tid < 2) scr[S_PC + blockIdx.x * 2 + tid] = t2[tid];
+}
+
+__global__ __launch_bounds__(MB_T) void qn_mb4_kernel(QnArgs A, double* __restrict__ scr) {
+  __shared__ double p2[2];
+  if (scr[S_PHASE] != 1.0) return;
+  const int G = gridDim.x, M = A.M, tid = threadIdx.x;
+  const bool first = blockIdx.x == 0 && tid == 0;
+  const int status = (int)scr[S_STATUS];
+  const bool newp = scr[S_NEWP] != 0.0;
+  int* fl = A.fl;
+  if (blockIdx.x == 0) {  // commit the step's history blocks and scalars
+    if (newp)
+      for (int i = tid; i < M * M; i += MB_T) {
+        A.SY[i] = scr[S_SY + i];
+        A.YY[i] = scr[S_SY + QN_MMAX * QN_MMAX + i];
+      }
+    if (tid == 0) {
+      const int iter = (int)scr[S_ITERN];
+      if (A.past > 0) A.fh[iter % A.past] = scr[S_FN];
+      fl[F_ITER] = iter;
+      fl[F_HEAD] = (int)scr[S_HD];
+      fl[F_COUNT] = (int)scr[S_CNT];
+      fl[F_NEVAL] = (int)scr[S_NEVAL] + 1;
+      fl[F_LS] = 0;
+      fl[F_BRACKET] = 0;
+      fl[F_STARTED] = 1;
+      A.sc[SC_F] = scr[S_FN];
+      A.sc[SC_GAMMA] = scr[S_GAM];
+      A.sc[SC_GINF] = scr[S_GINF];
+    }
+  }
+  if (status != ST_RUNNING) {
+    if (first) {
+      fl[F_STATUS] = status;
+      fl[F_DONE] = 1;
+    }
+    return;
+  }
+  mb_grid_sum(scr + S_PC, G, 2, p2, false);
+  double dg = p2[0], dd = p2[1];
+  int cnt2 = (int)scr[S_CNT];
+  const long i = (long)blockIdx.x * MB_T + tid;
+  if (!(dg < 0.0)) {  // not a descent direction: drop the history, steepest descent (rare)
+    // pg.pg (pass-1 total) is in the K2 partials: re-sum it
+    double pp = 0.0;
+    for (int b = 0; b < G; ++b) pp += scr[S_PB + (long)b * MB_PW + 4];
+    if (i < A.N) A.d[i] = -A.pg[i];
+    dg = -pp;
+    dd = pp;
+    cnt2 = 0;
+  }
+  const double alpha = cnt2 == 0 ? 1.0 / fmax(sqrt(dd), 1e-300) : 1.0;
+  mb_set_trial(A, alpha);
+  if (first) {
+    if (cnt2 == 0) {
+      fl[F_COUNT] = 0;
+      A.sc[SC_GAMMA] = 1.0;
+    }
+    A.sc[SC_ALPHA] = alpha;
+    A.sc[SC_DGINIT] = dg;
+  }
+}
+
+// doubles of scratch the multi-block step needs (independent of N)
+SRML_API long srml_qn_mb_scratch() { return (long)S_END; }
+
+// One optimiser step as four G-block launches (G = ceil(N / 256) <= 64; larger problems use the
+// single-block step). `scratch`: srml_qn_mb_scratch() doubles owned by this problem.
+SRML_API int srml_qn_step_mb(const QnArgs* a, double* scratch, hipStream_t stream) {
+  if (a->M < 1 || a->M > QN_MMAX || a->N <= 0 || !scratch) return (int)hipErrorInvalidValue;
+  const long G = (a->N + MB_T - 1) / MB_T;
+  if (G > MB_GMAX) return srml_qn_step(a, stream);
+  const dim3 grid((unsigned)G), blk(MB_T);
+  hipLaunchKernelGGL(qn_mb1_kernel, grid, blk, 0, stream, *a, scratch);
+  hipLaunchKernelGGL(qn_mb2_kernel, grid, blk, 0, stream, *a, scratch);
+  hipLaunchKernelGGL(qn_mb3_kernel, grid, blk, 0, stream, *a, scratch);
+  hipLaunchKernelGGL(qn_mb4_kernel, grid, blk, 0, stream, *a, scratch);
+  return srml_status();
+}
+
+// ------------------------------------------------------------------------------------------
+// Fused step: the whole optimiser step as ONE launch of G blocks (32 elements each) with three
+// software grid barriers (arrive counter + generation word in the scratch, agent-scope release /
+// acquire; G <= 512 blocks of 256 threads are co-resident on 256 CUs, and the wait is bounded by
+// wall-clock: a barrier that does not complete in ~1 s marks the step failed instead of hanging).
+// In front of pass 0 it can FOLD the binary evaluation's fp32 partial gradient rows itself
+// (`fws`: the fused binary kernel's per-block rows, single-rank fits), so an evaluation + step is
+// two launches: every kernel costs ~5 us of dispatch / ramp on its own, which the four-launch
+// step and a separate fold kernel paid six times per evaluation.
+// ------------------------------------------------------------------------------------------
+namespace {
+
+constexpr int FU_E = 32;       // elements per block
+constexpr int FU_GMAX = 512;   // N <= 16384
+constexpr int ST_BARRIER = 5;  // status: a grid barrier timed out (never expected)
+enum {
+  F_PA = S_END,                        // [G][6] pass-0 partials (+ folded loss, + folded bias grad)
+  F_PB = F_PA + 6 * FU_GMAX,           // [G][MB_PW] pass-1 partials
+  F_PC = F_PB + MB_PW * FU_GMAX,       // [G][2]
+  F_BAR = F_PC + 2 * FU_GMAX,          // 2 x u32 (arrive, generation) in one double slot
+  F_END = F_BAR + 2
+};
+
+__device__ __forceinline__ bool fu_barrier(double* scr, unsigned G) {
+  __shared__ int s_ok;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned* arrive = reinterpret_cast<unsigned*>(scr + F_BAR);
+    unsigned* gen = arrive + 1;
+    const unsigned my = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __threadfence();  // release this block's partials
+    int ok = 1;
+    if (atomicAdd(arrive, 1u) == G - 1) {
+      __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      const long long t0 = wall_clock64();
+      while (__hip_atomic_load(gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == my) {
+        if (wall_clock64() - t0 > 100000000LL) {  // ~1 s at the 100 MHz constant clock
+          ok = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __threadfence();  // acquire the other blocks' partials
+    s_ok = ok;
+  }
+  __syncthreads();
+  return s_ok != 0;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(MB_T) void qn_fused_kernel(QnArgs A, double* __restrict__ scr,
+                                                        const float* __restrict__ fws, int parts, long wst) {
+  __shared__ double red[MB_PW * MB_NW], tot[MB_PW], fold[32][33];
+  __shared__ double s_sy[QN_MMAX * QN_MMAX], s_yy[QN_MMAX * QN_MMAX], s_p1[QN_MMAX], s_p2[QN_MMAX];
+  __shared__ double cf_a[QN_MMAX], cf_t[QN_MMAX], s_misc[2];
+  __shared__ int s_sl[QN_MMAX], s_ctl[4];
+  int* fl = A.fl;
+  if (fl[F_DONE]) return;  // uniform: no block reaches a barrier
+  const unsigned G = gridDim.x;
+  const int tid = threadIdx.x, M = A.M;
+  const long N = A.N;
+  const long i = (long)blockIdx.x * FU_E + tid;  // this thread's element (tid < FU_E)
+  const bool own = tid < FU_E && i < N;
+  const bool first = blockIdx.x == 0 && tid == 0;
+  // ---- pre-step scalars (every block reads them here; only block 0 rewrites them, after the
+  //      last barrier it takes)
+  const bool started = fl[F_STARTED] != 0;
+  const int pre_iter = fl[F_ITER], count = fl[F_COUNT], head = fl[F_HEAD], pre_ls = fl[F_LS];
+  const int pre_neval = fl[F_NEVAL];
+  const bool bracket = fl[F_BRACKET] != 0;
+  const double f = A.sc[SC_F], dginit = A.sc[SC_DGINIT], pre_gamma = A.sc[SC_GAMMA];
+  double alpha = A.sc[SC_ALPHA];
+  const double pre_fh_next = (A.past > 0 && started) ? A.fh[(pre_iter + 1) % A.past] : 0.0;
+  // ---- this block's gradient sums: folded from the evaluation's partial rows, or from `out`
+  double oval = 0.0, lpart = 0.0, bpart = 0.0;
+  if (fws) {
+    const int q = tid & 7, rg = tid >> 3;  // 8 lanes x float4 = 32 columns, 32 row groups
+    const long c = (long)blockIdx.x * FU_E + 4 * q;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    if (c < A.Kn) {
+      int p = rg;
+      for (; p + 224 < parts; p += 256) {  // 8 rows in flight per thread
+        floatx4 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          v[j] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(fws + (long)(p + 32 * j) * wst + c));
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { a0 += v[j][0]; a1 += v[j][1]; a2 += v[j][2]; a3 += v[j][3]; }
+      }
+      for (; p < parts; p += 32) {
+        const floatx4 v = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(fws + (long)p * wst + c));
+        a0 += v[0]; a1 += v[1]; a2 += v[2]; a3 += v[3];
+      }
+    }
+    fold[rg][4 * q] = a0;
+    fold[rg][4 * q + 1] = a1;
+    fold[rg][4 * q + 2] = a2;
+    fold[rg][4 * q + 3] = a3;
+    // the bias gradient (element Kn, owned by one block) and the loss (block G - 1): trailing
+    // doubles of every row, summed over the block's 256 threads
+    const bool has_bias = A.K == 1 && A.Kn < N && (long)blockIdx.x == A.Kn / FU_E;
+    const bool has_loss = blockIdx.x == G - 1;
+    double gb = 0.0, ls = 0.0;
+    if (has_bias || has_loss)
+      for (int p = tid; p < parts; p += MB_T) {
+        const double* pd = reinterpret_cast<const double*>(fws + (long)p * wst + wst - 4);
+        gb += pd[0];
+        ls += pd[1];
+      }
+    const double sums[2] = {has_bias ? gb : 0.0, has_loss ? ls : 0.0};
+    double tv2[2];
+    {
+      const int lane = tid & 63, wid = tid >> 6;
+      for (int k = 0; k < 2; ++k) {
+        const double t = wave_sum(sums[k]);
+        if (lane == 0) red[k * MB_NW + wid] = t;
+      }
+    }
+    __syncthreads();
+    tv2[0] = (red[0] + red[1]) + (red[2] + red[3]);
+    tv2[1] = (red[MB_NW] + red[MB_NW + 1]) + (red[MB_NW + 2] + red[MB_NW + 3]);
+    if (own) {
+      if (i < A.Kn) {
+        double s = 0.0;
+#pragma unroll
+        for (int g2 = 0; g2 < 32; ++g2) s += fold[g2][tid];
+        oval = s;
+      } else {
+        oval = tv2[0];  // the bias element
+      }
+    }
+    lpart = tv2[1];
+    bpart = 0.0;
+    __syncthreads();
+  } else {
+    if (own) {
+      oval = A.out[i];
+      A.out[i] = 0.0;  // consumed
+    }
+    if (first) lpart = A.out[A.Kn + A.K];  // the loss sum; zeroed by block 0 after the barrier
+  }
+  (void)bpart;
+  // ---- pass 0
+  double p0[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  if (own) {
+    const double xv = A.xt[i];
+    const double gi = oval * A.inv_m * (i < A.Kn ? A.isg[i % A.n] : 1.0) + A.l2[i] * xv;
+    A.gt[i] = gi;
+    p0[0] = A.l2[i] * xv * xv;
+    p0[1] = A.l1c[i] * fabs(xv);
+    p0[2] = gi * A.d[i];
+    p0[3] = A.pg[i] * (xv - A.x[i]);
+  }
+  if (tid == 0) p0[4] = lpart;
+  mb_block_sum<5>(p0, red, tot);
+  if (tid < 5) scr[F_PA + blockIdx.x * 6 + tid] = tot[tid];
+  if (!fu_barrier(scr, G)) {
+    if (first) { fl[F_STATUS] = ST_BARRIER; fl[F_DONE] = 1; }
+    return;
+  }
+  if (tid < 5) {  // grid totals, block order (stride 6)
+    double s = 0.0;
+    for (unsigned b = 0; b < G; ++b) s += scr[F_PA + b * 6 + tid];
+    red[tid] = s;
+  }
+  __syncthreads();
+  const double q0 = red[0], q1 = red[1], q2 = red[2], q3 = red[3], lossv = red[4];
+  __syncthreads();
+  const double ft = lossv * A.inv_m + 0.5 * q0 + q1;
+  if (first && !fws)  // the loss sum (read before the barrier) and bias sums without a parameter
+    for (long j = N; j < A.Kn + A.K + 1; ++j) A.out[j] = 0.0;
+  if (started) {
+    bool accept = true;
+    double width = 1.0;
+    if (!isfinite(ft)) {
+      accept = false;
+      width = 0.5;
+    } else {
+      const double dgtest = A.l1 ? q3 : alpha * dginit;
+      if (ft > f + A.c1 * dgtest) {
+        accept = false;
+        const double den = 2.0 * (ft - f - dgtest);
+        width = den > 0.0 ? -dgtest / den : 0.5;
+        width = isfinite(width) ? fmin(0.5, fmax(0.1, width)) : 0.5;
+      } else if (A.wolfe && !A.l1 && !bracket && q2 < A.c2 * dginit) {
+        accept = false;
+        width = 2.1;
+      }
+    }
+    if (!accept) {
+      const int ls = pre_ls + 1;
+      if (ls >= A.max_ls) {
+        if (first) {
+          fl[F_LS] = ls;
+          fl[F_NEVAL] = pre_neval + 1;
+          fl[F_STATUS] = ST_LS_FAIL;
+          fl[F_DONE] = 1;
+        }
+        return;
+      }
+      alpha *= width;
+      if (own) {  // next trial point
+        const double xv = A.x[i], dv = A.d[i];
+        double t = xv + alpha * dv;
+        if (A.l1 && A.l1c[i] > 0.0) {
+          const double pv = A.pg[i];
+          const double orth = xv != 0.0 ? (xv > 0.0 ? 1.0 : -1.0) : (pv < 0.0 ? 1.0 : (pv > 0.0 ? -1.0 : 0.0));
+          if (t * orth <= 0.0) t = 0.0;
+        }
+        A.xt[i] = t;
+        A.wb[i] = t * (i < A.Kn ? A.isg[i % A.n] : 1.0);
+      }
+      if (first) {
+        fl[F_LS] = ls;
+        fl[F_NEVAL] = pre_neval + 1;
+        if (width < 1.0) fl[F_BRACKET] = 1;
+        A.sc[SC_ALPHA] = alpha;
+      }
+      return;
+    }
+  }
+  // ---- accepted: pass 1 partials (own elements)
+  {
+    double v[MB_PW];
+#pragma unroll
+    for (int j = 0; j < MB_PW; ++j) v[j] = 0.0;
+    if (own) {
+      const double xv = A.xt[i], gv = A.gt[i];
+      const double sx = started ? xv - A.x[i] : 0.0;
+      const double yx = started ? gv - A.g[i] : 0.0;
+      const double pgi = pseudo_grad(xv, gv, A.l1 ? A.l1c[i] : 0.0);
+      A.pg[i] = pgi;
+      A.d[i] = sx;
+      A.wb[i] = yx;
+      v[0] = sx * yx;
+      v[1] = yx * yx;
+      v[2] = sx * pgi;
+      v[3] = yx * pgi;
+      v[4] = pgi * pgi;
+      v[MB_PW - 1] = fabs(pgi);
+#pragma unroll
+      for (int j = 0; j < QN_MMAX; ++j) {
+        if (j < M) {
+          const double Sj = A.S[(long)j * N + i], Yj = A.Y[(long)j * N + i];
+          v[6 + j] = sx * Yj;
+          v[6 + QN_MMAX + j] = Sj * yx;
+          v[6 + 2 * QN_MMAX + j] = yx * Yj;
+          v[6 + 3 * QN_MMAX + j] = Sj * pgi;
+          v[6 + 4 * QN_MMAX + j] = Yj * pgi;
+        }
+      }
+    }
+    // only wave 0 holds elements (FU_E = 32 < 64): the wave sum is the block sum
+    const int lane = tid & 63;
+    if (tid < 64) {
+#pragma unroll
+      for (int j = 0; j < MB_PW - 1; ++j) {
+        const double t = wave_sum(v[j]);
+        if (lane == 0) scr[F_PB + (long)blockIdx.x * MB_PW + j] = t;
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      double mx = v[MB_PW - 1];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+      if (lane == 0) scr[F_PB + (long)blockIdx.x * MB_PW + MB_PW - 1] = mx;
+    }
+  }
+  for (int k = tid; k < M * M; k += MB_T) {  // old history blocks, before anyone commits new ones
+    s_sy[k] = A.SY[k];
+    s_yy[k] = A.YY[k];
+  }
+  if (!fu_barrier(scr, G)) {
+    if (first) { fl[F_STATUS] = ST_BARRIER; fl[F_DONE] = 1; }
+    return;
+  }
+  mb_grid_sum(scr + F_PB, G, MB_PW, tot, true);
+  if (tid == 0) {
+    int cnt = count, hd = head, status = ST_RUNNING;
+    double gamma = started ? pre_gamma : 1.0;
+    for (int j = 0; j < M; ++j) {
+      s_p1[j] = tot[6 + 3 * QN_MMAX + j];
+      s_p2[j] = tot[6 + 4 * QN_MMAX + j];
+    }
+    const double ys = tot[0], yy = tot[1];
+    const bool newp = started && yy > 0.0 && ys > 1e-10 * yy;
+    if (newp) {
+      const int h = hd;
+      for (int j = 0; j < M; ++j) {
+        if (j == h) continue;
+        s_sy[h * M + j] = tot[6 + j];
+        s_sy[j * M + h] = tot[6 + QN_MMAX + j];
+        s_yy[h * M + j] = tot[6 + 2 * QN_MMAX + j];
+        s_yy[j * M + h] = tot[6 + 2 * QN_MMAX + j];
+      }
+      s_sy[h * M + h] = ys;
+      s_yy[h * M + h] = yy;
+      s_p1[h] = tot[2];
+      s_p2[h] = tot[3];
+      hd = (h + 1) % M;
+      cnt = cnt < M ? cnt + 1 : M;
+      gamma = ys / yy;
+    }
+    const double ginf = tot[MB_PW - 1];
+    const int iter = pre_iter + (started ? 1 : 0);
+    const double fmag = fmax(fabs(ft), A.tol);
+    if (ginf <= A.tol * fmag) status = ST_CONV_GRAD;
+    if (A.past > 0 && status == ST_RUNNING && started && iter >= A.past && fabs(pre_fh_next - ft) <= A.delta * fmag)
+      status = ST_CONV_F;
+    if (status == ST_RUNNING && iter >= A.max_iter) status = ST_MAXITER;
+    for (int c = 0; c < cnt; ++c) s_sl[c] = (hd - cnt + c + 2 * M) % M;
+    s_ctl[0] = status;
+    s_ctl[1] = newp ? 1 : 0;
+    s_ctl[2] = cnt;
+    s_ctl[3] = hd;
+    s_misc[0] = gamma;
+    s_misc[1] = ginf;
+  }
+  __syncthreads();
+  if (tid < 64) {  // compact-form coefficients (wave 0)
+    const int cnt = s_ctl[2];
+    const double gamma = s_misc[0];
+    const int c = tid;
+    const bool act = c < cnt;
+    const int slc = act ? s_sl[c] : 0;
+    double Rrow[QN_MMAX], Rcol[QN_MMAX], Yrow[QN_MMAX], tv[QN_MMAX];
+#pragma unroll
+    for (int e = 0; e < QN_MMAX; ++e) {
+      const bool ok = act && e < cnt;
+      const int sle = ok ? s_sl[e] : 0;
+      Rrow[e] = ok ? s_sy[slc * M + sle] : 0.0;
+      Rcol[e] = ok ? s_sy[sle * M + slc] : 0.0;
+      Yrow[e] = ok ? s_yy[slc * M + sle] : 0.0;
+      tv[e] = 0.0;
+    }
+    const double diag = act ? s_sy[slc * M + slc] : 1.0;
+    double acc = act ? s_p1[slc] : 0.0;
+    double tmine = 0.0;
+#pragma unroll
+    for (int e = QN_MMAX - 1; e >= 0; --e) {
+      if (e < cnt) {
+        const double te = __shfl(acc / diag, e, 64);
+        tv[e] = te;
+        if (c == e) tmine = te;
+        if (c < e) acc -= Rrow[e] * te;
+      }
+    }
+    acc = diag * tmine - gamma * (act ? s_p2[slc] : 0.0);
+#pragma unroll
+    for (int e = 0; e < QN_MMAX; ++e) acc += gamma * Yrow[e] * tv[e];
+    double amine = 0.0;
+#pragma unroll
+    for (int e = 0; e < QN_MMAX; ++e) {
+      if (e < cnt) {
+        const double ae = __shfl(acc / diag, e, 64);
+        if (c == e) amine = ae;
+        if (c > e) acc -= Rcol[e] * ae;
+      }
+    }
+    if (c < QN_MMAX) {
+      cf_a[c] = 0.0;
+      cf_t[c] = 0.0;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (act) {
+      cf_a[slc] = amine;
+      cf_t[slc] = gamma * tmine;
+    }
+  }
+  __syncthreads();
+  const int status = s_ctl[0];
+  const bool newp = s_ctl[1] != 0;
+  const int cnt = s_ctl[2];
+  const double gamma = s_misc[0];
+  // ---- pass 2 (own elements): store the pair, x <- xt, g <- gt, direction
+  double p2v[2] = {0.0, 0.0};
+  if (own) {
+    const double xv = A.xt[i], gv = A.gt[i], sv = A.d[i], yv = A.wb[i], pv = A.pg[i];
+    if (newp) {
+      A.S[(long)head * N + i] = sv;
+      A.Y[(long)head * N + i] = yv;
+    }
+    A.x[i] = xv;
+    A.g[i] = gv;
+    if (status == ST_RUNNING) {
+      double hg = gamma * pv;
+      for (int c = 0; c < cnt; ++c) {
+        const int j = s_sl[c];
+        hg += cf_a[j] * A.S[(long)j * N + i] - cf_t[j] * A.Y[(long)j * N + i];
+      }
+      double di = -hg;
+      if (A.l1 && A.l1c[i] > 0.0 && di * pv >= 0.0) di = 0.0;
+      A.d[i] = di;
+      p2v[0] = pv * di;
+      p2v[1] = di * di;
+    }
+  }
+  if (tid < 64) {
+    const double a = wave_sum(p2v[0]), b = wave_sum(p2v[1]);
+    if (tid == 0) {
+      scr[F_PC + blockIdx.x * 2] = a;
+      scr[F_PC + blockIdx.x * 2 + 1] = b;
+    }
+  }
+  // every block is past its reads of the pre-step state and the old history blocks beyond this
+  // barrier: block 0 commits after it
+  if (!fu_barrier(scr, G)) {
+    if (first) { fl[F_STATUS] = ST_BARRIER; fl[F_DONE] = 1; }
+    return;
+  }
+  if (blockIdx.x == 0) {
+    if (newp)
+      for (int k = tid; k < M * M; k += MB_T) {
+        A.SY[k] = s_sy[k];
+        A.YY[k] = s_yy[k];
+      }
+    if (tid == 0) {
+      const int iter = pre_iter + (started ? 1 : 0);
+      if (A.past > 0) A.fh[iter % A.past] = ft;
+      fl[F_ITER] = iter;
+      fl[F_HEAD] = s_ctl[3];
+      fl[F_COUNT] = cnt;
+      fl[F_NEVAL] = pre_neval + 1;
+      fl[F_LS] = 0;
+      fl[F_BRACKET] = 0;
+      fl[F_STARTED] = 1;
+      A.sc[SC_F] = ft;
+      A.sc[SC_GAMMA] = gamma;
+      A.sc[SC_GINF] = s_misc[1];
+      if (status != ST_RUNNING) {
+        fl[F_STATUS] = status;
+        fl[F_DONE] = 1;
+      }
+    }
+  }
+  if (status != ST_RUNNING) return;
+  if (tid < 2) {
+    double s = 0.0;
+    for (unsigned b = 0; b < G; ++b) s += scr[F_PC + b * 2 + tid];
+    red[tid] = s;
+  }
+  __syncthreads();
+  double dg = red[0], dd = red[1];
+  int cnt2 = cnt;
+  if (!(dg < 0.0)) {  // not a descent direction: drop the history, steepest descent (rare)
+    if (own) A.d[i] = -A.pg[i];
+    dg = -tot[4];
+    dd = tot[4];
+    cnt2 = 0;
+  }
+  const double alpha2 = cnt2 == 0 ? 1.0 / fmax(sqrt(dd), 1e-300) : 1.0;
+  if (own) {
+    const double xv = A.x[i], dv = A.d[i];
+    double t = xv + alpha2 * dv;
+    if (A.l1 && A.l1c[i] > 0.0) {
+      const double pv = A.pg[i];
+      const double orth = xv != 0.0 ? (xv > 0.0 ? 1.0 : -1.0) : (pv < 0.0 ? 1.0 : (pv > 0.0 ? -1.0 : 0.0));
+      if (t * orth <= 0.0) t = 0.0;
+    }
+    A.xt[i] = t;
+    A.wb[i] = t * (i < A.Kn ? A.isg[i % A.n] : 1.0);
+  }
+  if (first) {
+    if (cnt2 == 0) {
+      fl[F_COUNT] = 0;
+      A.sc[SC_GAMMA] = 1.0;
+    }
+    A.sc[SC_ALPHA] = alpha2;
+    A.sc[SC_DGINIT] = dg;
+  }
+}
+
+SRML_API long srml_qn_fused_scratch() { return (long)F_END; }
+
+// One optimiser step as ONE launch (G = ceil(N / 32) <= 512 blocks; larger N: the single-block
+// step). fws (optional): the fused binary evaluation's partial rows (parts rows of wst floats,
+// srml_logreg_binary3_f32's workspace) folded in place of `out` — single-rank fits only (a
+// multi-rank fit all-reduces `out` between the evaluation and the step). The scratch's barrier
+// words must start at zero (a zeroed allocation) and every launch leaves them so.
+SRML_API int srml_qn_step_fused(const QnArgs* a, double* scratch, const float* fws, int parts, long wst,
+                                hipStream_t stream) {
+  if (a->M < 1 || a->M > QN_MMAX || a->N <= 0 || !scratch) return (int)hipErrorInvalidValue;
+  const long G = (a->N + FU_E - 1) / FU_E;
+  if (G > FU_GMAX) return srml_qn_step(a, stream);
+  if (fws && (a->K != 1 || (wst & 3) || parts <= 0)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(qn_fused_kernel, dim3((unsigned)G), dim3(MB_T), 0, stream, *a, scratch, fws, parts, wst);
+  return srml_status();
+}

@@ -26,7 +26,8 @@ _D = ctypes.c_double
 _F = ctypes.c_float
 
 # name -> argtypes (restype: int status, except the size queries in _LONG_RESULT)
-_LONG_RESULT = ("srml_rf_bootstrap_ws", "srml_logreg_fold_ws", "srml_qn_args_size", "srml_logit_residual_ws", "srml_xtv_mfma_ws",
+_LONG_RESULT = ("srml_rf_bootstrap_ws", "srml_logreg_fold_ws", "srml_qn_mb_scratch", "srml_qn_fused_scratch",
+                "srml_logreg_fold_parts", "srml_qn_args_size", "srml_logit_residual_ws", "srml_xtv_mfma_ws",
                 "srml_rf_partition_ws",
                 "srml_label_sort_ws", "srml_radix_sort_ws")
 SIGNATURES: Dict[str, Tuple[Any, ...]] = {
@@ -44,7 +45,8 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_row_sqnorm_f32": (_P, _L, _I, _L, _P, _P),
     "srml_logreg_binary_f32": (_P, _L, _I, _L, _P, _P, _D, _P, _P),
     "srml_logreg_binary2_f32": (_P, _L, _I, _L, _P, _P, _D, _P, _P, _P, _P),
-    "srml_logreg_binary3_f32": (_P, _L, _I, _L, _P, _P, _D, _P, _P, _P, _P, _P),
+    "srml_logreg_binary3_f32": (_P, _L, _I, _L, _P, _P, _D, _P, _P, _P, _P, _I, _P),
+    "srml_logreg_fold_parts": (_L,),
     "srml_logreg_fold_ws": (_L, _I),
     "srml_logreg_binary_lds_f32": (_P, _L, _I, _L, _P, _P, _D, _P, _P, _P, _P),
     "srml_logreg_binary_lds_f64": (_P, _L, _I, _L, _P, _P, _D, _P, _P, _P, _P),
@@ -64,6 +66,10 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_mlogit_f32": (_P, _L, _I, _L, _P, _P, _P, _P, _I, _P, _P),
     "srml_mlogit_supported": (_I, _I),
     "srml_qn_step": (_P, _P),
+    "srml_qn_step_mb": (_P, _P, _P),
+    "srml_qn_step_fused": (_P, _P, _P, _I, _L, _P),
+    "srml_qn_fused_scratch": (),
+    "srml_qn_mb_scratch": (),
     "srml_kmeanspp_gram": (_P, _I, _L, _P, _I, _I, ctypes.c_ulonglong, _P, _P),
     "srml_qn_max_history": (),
     "srml_qn_args_size": (),

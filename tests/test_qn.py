@@ -259,6 +259,77 @@ def test_qn_kernel_matches_host(gpu_device, K, l1):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("K,l1,n", [(1, 0.0, 3000), (4, 0.0, 700), (1, 0.01, 1500)])
+def test_qn_multiblock_step_matches_single_block(gpu_device, K, l1, n, monkeypatch):
+    """srml_qn_step_mb (four G-block launches) advances the same state machine as the single-block
+    step: same decisions and iterations on smooth problems, same optimum with OWL-QN."""
+    from spark_rapids_ml_nai_amd.models import qn as qnm
+
+    m = 3000
+    g = torch.Generator().manual_seed(21 + K)
+    Xc = torch.randn(m, n, generator=g, dtype=torch.float64)
+    if K == 1:
+        y = (Xc[:, 0] + 0.5 * torch.randn(m, generator=g, dtype=torch.float64) > 0).double()
+    else:
+        y = torch.argmax(Xc[:, :K] + 0.5 * torch.randn(m, K, generator=g, dtype=torch.float64), 1).double()
+    N = K * n + K
+    P = QNProblem(n=n, K=K, fit_intercept=True, m_total=float(m),
+                  l2=np.concatenate([np.full(K * n, 0.01), np.zeros(K)]),
+                  l1=np.concatenate([np.full(K * n, l1), np.zeros(K)]),
+                  inv_sigma=np.linspace(0.5, 1.5, n), max_iter=40 if l1 == 0.0 else 150, tol=1e-12)
+    Xg, yg = Xc.to(gpu_device), y.to(gpu_device)
+
+    def ev_gpu(w, b, flag, out):
+        out += _ref_loss_grad(Xg, yg, w, b, K).to(gpu_device)
+
+    res = {}
+    for mode in ("single", "mb", "fused"):  # srml_qn_step / srml_qn_step_mb / srml_qn_step_fused
+        monkeypatch.setattr(qnm, "QN_MB", mode != "single")
+        monkeypatch.setattr(qnm, "QN_STEP", mode)
+        res[mode] = minimize(P, np.zeros(N), ev_gpu, None, gpu_device, batch=4)
+    a = res["single"]
+    for mode in ("mb", "fused"):
+        b = res[mode]
+        info = {k: (a[k], b[k]) for k in ("iter", "n_evals", "status", "f")}
+        info["mode"] = mode
+        if l1 == 0.0:
+            assert a["iter"] == b["iter"] and a["status"] == b["status"] and a["n_evals"] == b["n_evals"], info
+            assert abs(a["f"] - b["f"]) <= 1e-10 * abs(a["f"]), info
+            np.testing.assert_allclose(b["theta"], a["theta"], rtol=1e-6, atol=1e-8)
+        else:
+            assert abs(a["f"] - b["f"]) <= 1e-7 * abs(a["f"]), info
+            np.testing.assert_allclose(b["theta"], a["theta"], atol=2e-3)
+
+
+@pytest.mark.gpu
+def test_logistic_fit_fused_fold_matches_unfused(gpu_device, monkeypatch):
+    """One-rank binary LogReg with the fold moved into the fused optimiser step (the evaluation
+    leaves its partial rows) reproduces the fit whose evaluation folds them itself."""
+    from spark_rapids_ml_nai_amd import ops
+    from spark_rapids_ml_nai_amd.models import qn as qnm
+    from spark_rapids_ml_nai_amd.models.logistic import logistic_fit
+    from spark_rapids_ml_nai_amd.parallel.context import WorkerContext
+
+    rng = np.random.default_rng(11)
+    m, n = 20000, 1500  # a fold-workspace shape (1024 < n <= 4096)
+    X = rng.standard_normal((m, n)).astype(np.float32)
+    y = (X[:, :8].sum(1) + 0.5 * rng.standard_normal(m) > 0).astype(np.float32)
+    Xt, yt = torch.from_numpy(X).to(gpu_device), torch.from_numpy(y).to(gpu_device)
+    assert ops.logreg_workspace(Xt) is not None and ops.logistic_path(Xt, 1) == "fused_binary_f32"
+    ctx = WorkerContext.single(gpu_device)
+    out = {}
+    for mode in ("mb", "fused"):
+        monkeypatch.setattr(qnm, "QN_MB", True)
+        monkeypatch.setattr(qnm, "QN_STEP", mode)
+        out[mode] = logistic_fit(Xt, yt, m, ctx, reg=1e-3, l1_ratio=0.0, fit_intercept=True,
+                                 standardization=True, max_iter=60, tol=1e-10)
+    a, b = out["mb"], out["fused"]
+    assert a["num_iters"] == b["num_iters"], (a["num_iters"], b["num_iters"])
+    assert abs(a["objective"] - b["objective"]) <= 1e-6 * abs(a["objective"])
+    np.testing.assert_allclose(np.asarray(b["coef_"]), np.asarray(a["coef_"]), rtol=1e-3, atol=1e-5)
+
+
+@pytest.mark.gpu
 def test_logistic_fit_multi_batched_matches_single(gpu_device):
     """Hyper-parameter batching: a grid of binary fits sharing every pass over X (srml_mbin_f32 +
     srml_qn_step_batch) reproduces the one-at-a-time fits."""

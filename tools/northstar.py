@@ -212,7 +212,7 @@ def main() -> None:
             rec["phases"] = {k: round(v, 4) for k, v in getattr(model, "_fit_timings", {}).items()}
             rs = getattr(model, "_rank_stats", None)
             if rs:
-                rec["rank0"] = rs
+                rec["ranks"] = rs
             if name == "kmeans":
                 rec["iters"] = int(ma.get("n_iter", getattr(model, "num_iters", -1)) or -1)
                 ph = ma.get("phase_s")
