@@ -34,10 +34,11 @@ import numpy as np
 import torch
 
 QN_GRAPH = os.environ.get("SRML_QN_GRAPH", "1") != "0"
-# the optimiser step: "fused" (default, N <= 16384) = ONE launch of G blocks with software grid
-# barriers, which can also fold the binary evaluation's partial rows itself (srml_qn_step_fused);
-# "mb" = four multi-block launches (srml_qn_step_mb); "single" = the one-block kernel
-QN_STEP = os.environ.get("SRML_QN_STEP", "fused")
+# the optimiser step for N <= 16384: "mb" (default) = four multi-block launches (srml_qn_step_mb;
+# a one-rank binary LogReg fit folds the evaluation's partial rows in the first: srml_qn_step_mbf);
+# "fused" = ONE launch with software grid barriers (srml_qn_step_fused, folds likewise);
+# "single" = the one-block kernel
+QN_STEP = os.environ.get("SRML_QN_STEP", "mb")
 QN_MB = QN_STEP in ("fused", "mb")
 GRAPH_STATS = {"captures": 0, "replays": 0}  # observability / tests
 STATUS = {0: "running", 1: "converged (gradient)", 2: "converged (objective change)", 3: "max iterations",
@@ -335,6 +336,10 @@ class DeviceQN:
             ws, parts, wst = self.fold if self.fold is not None else (None, 0, 0)
             native.call("srml_qn_step_fused", ctypes.addressof(self._args), self._mb.data_ptr(),
                         ws.data_ptr() if ws is not None else None, int(parts), int(wst), native.stream(self.device))
+        elif self._mb is not None and self.fold is not None:
+            ws, parts, wst = self.fold
+            native.call("srml_qn_step_mbf", ctypes.addressof(self._args), self._mb.data_ptr(), ws.data_ptr(),
+                        int(parts), int(wst), native.stream(self.device))
         elif self._mb is not None:
             native.call("srml_qn_step_mb", ctypes.addressof(self._args), self._mb.data_ptr(), native.stream(self.device))
         else:
@@ -388,7 +393,7 @@ def minimize(P: QNProblem, theta0: np.ndarray, evaluate: Callable[[torch.Tensor,
         return {"theta": st.theta(), "f": st.f, "iter": st.iter, "n_evals": st.n_evals,
                 "status": STATUS[st.status if st.done else 3]}
     q = DeviceQN(P, theta0, device)
-    if fold is not None and evaluate_partials is not None and allreduce is None and q._fused and q._mb is not None:
+    if fold is not None and evaluate_partials is not None and allreduce is None and q._mb is not None:
         q.fold = fold
         evaluate = lambda w, b, flag, out: evaluate_partials(w, b, flag)  # noqa: E731
     poll = _comm_poll(allreduce)

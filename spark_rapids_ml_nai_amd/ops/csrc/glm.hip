@@ -1008,8 +1008,9 @@ static int logreg_binary_launch(const float* X, long m, int n, long ld, const fl
     static const int fold = getenv("SRML_LOGREG_FOLD") ? atoi(getenv("SRML_LOGREG_FOLD")) : 1;
     const long wst = ((n + 3) & ~3) + 4;
     float* fws = fold ? fold_ws : nullptr;
-#define SRML_LR_PF(VV, RR, DD) \
-    hipLaunchKernelGGL((logreg_binary_pf_kernel<VV, RR, DD>), grid, blk, 0, stream, X, m, n, ld, y, w, b, bptr, flag, out, rpb, fws)
+#define SRML_LR_PF(VV, RR, DD)                                                                              \
+    hipLaunchKernelGGL((logreg_binary_pf_kernel<VV, RR, DD>), grid, blk, 0, stream, X, m, n, ld, y, w, b, bptr, \
+                       flag, out, rpb, fws)
 #define SRML_LR_PF_V(RR, DD) \
     do { if (VS == 2) SRML_LR_PF(2, RR, DD); else if (VS == 3) SRML_LR_PF(3, RR, DD); else SRML_LR_PF(4, RR, DD); } while (0)
     if (rsel == 2 && dsel == 1) SRML_LR_PF_V(2, 1);

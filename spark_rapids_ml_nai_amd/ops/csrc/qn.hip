@@ -618,6 +618,7 @@ namespace {
 constexpr int MB_T = 256;
 constexpr int MB_NW = MB_T / 64;
 constexpr int MB_GMAX = 64;
+constexpr int MB_GAMAX = 512;  // K1 partial rows: the folding K1 runs ceil(N / 32) blocks
 constexpr int MB_PW = 6 + 5 * QN_MMAX + 1;  // pass-1 partials: 6 dots, 5 history products per slot, max |pg|
 enum {
   S_STARTED = 0, S_ITER, S_COUNT, S_HEAD, S_LS, S_NEVAL, S_BRACKET, S_F, S_ALPHA, S_DGINIT, S_GAMMA, S_FHN, S_LOSS,
@@ -625,8 +626,8 @@ enum {
   S_CF = 32,                              // cf_a[QN_MMAX] | cf_t[QN_MMAX]
   S_SL = S_CF + 2 * QN_MMAX,              // chronological slots [QN_MMAX]
   S_SY = S_SL + QN_MMAX,                  // updated SY [QN_MMAX^2] | YY [QN_MMAX^2] (committed by K4)
-  S_PA = S_SY + 2 * QN_MMAX * QN_MMAX,    // K1 partials [G][4]
-  S_PB = S_PA + 4 * MB_GMAX,              // K2 partials [G][MB_PW]
+  S_PA = S_SY + 2 * QN_MMAX * QN_MMAX,    // K1 partials [G1][4]
+  S_PB = S_PA + 4 * MB_GAMAX,             // K2 partials [G][MB_PW]
   S_PC = S_PB + MB_PW * MB_GMAX,          // K3 partials [G][2]
   S_END = S_PC + 2 * MB_GMAX
 };
@@ -651,90 +652,196 @@ __device__ __forceinline__ void mb_block_sum(const double (&v)[NV], double* red,
   __syncthreads();
 }
 
-// grid totals of a [G][width] partial table, summed in block order into LDS `tot` (all threads)
+// grid totals of a [G][width] partial table (width <= MB_T) into LDS `tot` (all threads). Every
+// thread of the block loads: slice s = tid / width of the blocks, eight independent loads in flight
+// per thread, then an LDS combine of the slices in fixed order — the partials come from other CUs
+// (L2 / fabric latency ~1 us each), so a one-thread-per-column serial loop over G blocks costs
+// ~G us; this costs ~ceil(G / (8 * slices)) round trips.
 __device__ __forceinline__ void mb_grid_sum(const double* part, int G, int width, double* tot, bool max_last) {
-  for (int j = threadIdx.x; j < width; j += MB_T) {
-    double s = 0.0;
-    const bool mx = max_last && j == width - 1;
-    for (int b = 0; b < G; ++b) s = mx ? fmax(s, part[(long)b * width + j]) : s + part[(long)b * width + j];
-    tot[j] = s;
+  __shared__ double gs[MB_T];
+  const int t = threadIdx.x, S = MB_T / width;
+  const int j = t % width, sl = t / width;
+  const bool mx = max_last && j == width - 1;
+  double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  if (sl < S) {
+    int b = sl;
+    for (; b + 7 * S < G; b += 8 * S) {
+      double v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = part[(long)(b + k * S) * width + j];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) a[k] = mx ? fmax(a[k], v[k]) : a[k] + v[k];
+    }
+    for (; b < G; b += S) {
+      const double v = part[(long)b * width + j];
+      a[0] = mx ? fmax(a[0], v) : a[0] + v;
+    }
+  }
+  gs[t] = mx ? fmax(fmax(fmax(a[0], a[1]), fmax(a[2], a[3])), fmax(fmax(a[4], a[5]), fmax(a[6], a[7])))
+             : ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  __syncthreads();
+  if (t < width) {
+    double x = gs[t];
+    for (int q = 1; q < S; ++q) x = mx ? fmax(x, gs[q * width + t]) : x + gs[q * width + t];
+    tot[t] = x;
   }
   __syncthreads();
 }
 
-__device__ __forceinline__ void mb_set_trial(const QnArgs& A, double alpha) {
-  const long i = (long)blockIdx.x * MB_T + threadIdx.x;
-  if (i >= A.N) return;
-  const double xv = A.x[i], dv = A.d[i];
-  double t = xv + alpha * dv;
-  if (A.l1) {
-    const double cv = A.l1c[i];
-    if (cv > 0.0) {
-      const double pv = A.pg[i];
-      const double orth = xv != 0.0 ? (xv > 0.0 ? 1.0 : -1.0) : (pv < 0.0 ? 1.0 : (pv > 0.0 ? -1.0 : 0.0));
-      if (t * orth <= 0.0) t = 0.0;
-    }
-  }
-  A.xt[i] = t;
-  A.wb[i] = t * (i < A.Kn ? A.isg[i % A.n] : 1.0);
+}  // namespace
+
+// Each kernel issues EVERY load it may need at entry (element data, history columns, grid
+// partials, snapshot scalars), before its early exits and decisions: what the previous launch wrote
+// comes from beyond this CU's caches (~1 us per round trip), so the kernel's time is its count of
+// DEPENDENT round trips — one here, plus the boundary.
+
+// pre-step snapshot of the flags / scalars (block 0, thread 0 of K1): later kernels read these,
+// K2 / K4 rewrite the flags
+struct MbSnap {
+  int started, iter, count, head, ls, neval, bracket;
+  double f, alpha, dginit, gamma;
+};
+
+__device__ __forceinline__ MbSnap mb_snap_load(const QnArgs& A) {
+  const int* fl = A.fl;
+  MbSnap q;
+  q.started = fl[F_STARTED];
+  q.iter = fl[F_ITER];
+  q.count = fl[F_COUNT];
+  q.head = fl[F_HEAD];
+  q.ls = fl[F_LS];
+  q.neval = fl[F_NEVAL];
+  q.bracket = fl[F_BRACKET];
+  q.f = A.sc[SC_F];
+  q.alpha = A.sc[SC_ALPHA];
+  q.dginit = A.sc[SC_DGINIT];
+  q.gamma = A.sc[SC_GAMMA];
+  return q;
 }
 
-}  // namespace
+__device__ __forceinline__ void mb_snap_store(const QnArgs& A, const MbSnap& q, double* scr) {
+  scr[S_STARTED] = q.started ? 1.0 : 0.0;
+  scr[S_ITER] = q.iter;
+  scr[S_COUNT] = q.count;
+  scr[S_HEAD] = q.head;
+  scr[S_LS] = q.ls;
+  scr[S_NEVAL] = q.neval;
+  scr[S_BRACKET] = q.bracket;
+  scr[S_F] = q.f;
+  scr[S_ALPHA] = q.alpha;
+  scr[S_DGINIT] = q.dginit;
+  scr[S_GAMMA] = q.gamma;
+  scr[S_FHN] = (A.past > 0 && q.started) ? A.fh[(q.iter + 1) % A.past] : 0.0;
+  scr[S_PHASE] = 0.0;
+}
+
+// pass 0 of element i from its summed evaluation value `ov`
+struct MbP0In {
+  double xv, l2v, l1v, dv, pgv, xo, isg;
+};
+
+__device__ __forceinline__ MbP0In mb_p0_load(const QnArgs& A, long i, bool own) {
+  MbP0In e{0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 1.0};
+  if (own) {
+    e.xv = A.xt[i];
+    e.l2v = A.l2[i];
+    e.l1v = A.l1c[i];
+    e.dv = A.d[i];
+    e.pgv = A.pg[i];
+    e.xo = A.x[i];
+    if (i < A.Kn) e.isg = A.isg[i % A.n];
+  }
+  return e;
+}
+
+__device__ __forceinline__ void mb_p0(const QnArgs& A, long i, bool own, const MbP0In& e, double ov, double (&p0)[4]) {
+  if (!own) return;
+  const double gi = ov * A.inv_m * e.isg + e.l2v * e.xv;
+  A.gt[i] = gi;
+  p0[0] = e.l2v * e.xv * e.xv;
+  p0[1] = e.l1v * fabs(e.xv);
+  p0[2] = gi * e.dv;
+  p0[3] = e.pgv * (e.xv - e.xo);
+}
 
 __global__ __launch_bounds__(MB_T) void qn_mb1_kernel(QnArgs A, double* __restrict__ scr) {
   __shared__ double red[4 * MB_NW], tot[4];
-  const int* fl = A.fl;
   const bool first = blockIdx.x == 0 && threadIdx.x == 0;
-  if (fl[F_DONE]) {
+  const long i = (long)blockIdx.x * MB_T + threadIdx.x;
+  const bool own = i < A.N;
+  const int done = A.fl[F_DONE];
+  MbSnap q{};
+  double loss = 0.0;
+  if (first) {
+    q = mb_snap_load(A);
+    loss = A.out[A.Kn + A.K];
+  }
+  const MbP0In e = mb_p0_load(A, i, own);
+  const double ov = own ? A.out[i] : 0.0;
+  if (done) {
     if (first) scr[S_PHASE] = 0.0;  // K3 / K4 must not act on a stale phase
     return;
   }
-  if (first) {  // pre-step snapshot: later kernels read these, block 0 of K2 / K4 rewrites the flags
-    const bool started = fl[F_STARTED] != 0;
-    scr[S_STARTED] = started ? 1.0 : 0.0;
-    scr[S_ITER] = fl[F_ITER];
-    scr[S_COUNT] = fl[F_COUNT];
-    scr[S_HEAD] = fl[F_HEAD];
-    scr[S_LS] = fl[F_LS];
-    scr[S_NEVAL] = fl[F_NEVAL];
-    scr[S_BRACKET] = fl[F_BRACKET];
-    scr[S_F] = A.sc[SC_F];
-    scr[S_ALPHA] = A.sc[SC_ALPHA];
-    scr[S_DGINIT] = A.sc[SC_DGINIT];
-    scr[S_GAMMA] = A.sc[SC_GAMMA];
-    scr[S_FHN] = (A.past > 0 && started) ? A.fh[(fl[F_ITER] + 1) % A.past] : 0.0;
-    scr[S_LOSS] = A.out[A.Kn + A.K];
-    scr[S_PHASE] = 0.0;
+  if (first) {
+    mb_snap_store(A, q, scr);
+    scr[S_LOSS] = loss;
   }
   double p0[4] = {0.0, 0.0, 0.0, 0.0};
-  const long i = (long)blockIdx.x * MB_T + threadIdx.x;
-  if (i < A.N) {
-    const double xv = A.xt[i];
-    const double gi = A.out[i] * A.inv_m * (i < A.Kn ? A.isg[i % A.n] : 1.0) + A.l2[i] * xv;
-    A.gt[i] = gi;
-    p0[0] = A.l2[i] * xv * xv;
-    p0[1] = A.l1c[i] * fabs(xv);
-    p0[2] = gi * A.d[i];
-    p0[3] = A.pg[i] * (xv - A.x[i]);
-    if (i < A.Kn + A.K) A.out[i] = 0.0;  // this element's evaluation sum is consumed
-  }
+  mb_p0(A, i, own, e, ov, p0);
+  if (own && i < A.Kn + A.K) A.out[i] = 0.0;  // this element's evaluation sum is consumed
   mb_block_sum<4>(p0, red, tot);
   if (threadIdx.x < 4) scr[S_PA + blockIdx.x * 4 + threadIdx.x] = tot[threadIdx.x];
 }
 
-__global__ __launch_bounds__(MB_T) void qn_mb2_kernel(QnArgs A, double* __restrict__ scr) {
-  __shared__ double red[MB_PW * MB_NW], tot[MB_PW], p0[4];
+// trial point of element i: t = x + alpha d, projected onto x's orthant for L1 coordinates
+__device__ __forceinline__ void mb_trial(const QnArgs& A, long i, double xv, double dv, double pv, double cv,
+                                         double isg, double alpha) {
+  double t = xv + alpha * dv;
+  if (A.l1 && cv > 0.0) {
+    const double orth = xv != 0.0 ? (xv > 0.0 ? 1.0 : -1.0) : (pv < 0.0 ? 1.0 : (pv > 0.0 ? -1.0 : 0.0));
+    if (t * orth <= 0.0) t = 0.0;
+  }
+  A.xt[i] = t;
+  A.wb[i] = t * isg;
+}
+
+__global__ __launch_bounds__(MB_T) void qn_mb2_kernel(QnArgs A, double* __restrict__ scr, int ga) {
+  __shared__ double red[MB_PW * MB_NW], p0[4];
   int* fl = A.fl;
-  if (fl[F_DONE]) return;
-  const int G = gridDim.x;
-  mb_grid_sum(scr + S_PA, G, 4, p0, false);
-  const bool started = scr[S_STARTED] != 0.0;
-  const double f = scr[S_F], dginit = scr[S_DGINIT];
-  double alpha = scr[S_ALPHA];
-  const double ft = scr[S_LOSS] * A.inv_m + 0.5 * p0[0] + p0[1];
+  const int M = A.M;
+  const long N = A.N;
+  const long i = (long)blockIdx.x * MB_T + threadIdx.x;
+  const bool own = i < N;
   const bool first = blockIdx.x == 0 && threadIdx.x == 0;
+  // ---- every load up front
+  const int done = fl[F_DONE];
+  const bool started = scr[S_STARTED] != 0.0;
+  const double f = scr[S_F], dginit = scr[S_DGINIT], alpha0 = scr[S_ALPHA], loss = scr[S_LOSS];
+  const bool bracket = scr[S_BRACKET] != 0.0;
+  const int pre_ls = (int)scr[S_LS], pre_neval = (int)scr[S_NEVAL];
+  double xt = 0.0, gt = 0.0, xo = 0.0, go = 0.0, cv = 0.0, dv = 0.0, pv = 0.0, isg = 1.0;
+  double Sv[QN_MMAX], Yv[QN_MMAX];
+  if (own) {
+    xt = A.xt[i];
+    gt = A.gt[i];
+    xo = A.x[i];
+    go = A.g[i];
+    cv = A.l1c[i];
+    dv = A.d[i];
+    pv = A.pg[i];
+    if (i < A.Kn) isg = A.isg[i % A.n];
+  }
+#pragma unroll
+  for (int j = 0; j < QN_MMAX; ++j) {
+    Sv[j] = (own && j < M) ? A.S[(long)j * N + i] : 0.0;
+    Yv[j] = (own && j < M) ? A.Y[(long)j * N + i] : 0.0;
+  }
+  if (done) return;
+  mb_grid_sum(scr + S_PA, ga, 4, p0, false);  // ga: K1's block count
+  double alpha = alpha0;
+  const double ft = loss * A.inv_m + 0.5 * p0[0] + p0[1];
   if (first)  // the loss sum (read from the snapshot) and bias sums without a parameter (no intercept)
-    for (long j = A.N; j < A.Kn + A.K + 1; ++j) A.out[j] = 0.0;
+    for (long j = N; j < A.Kn + A.K + 1; ++j) A.out[j] = 0.0;
   if (started) {
     bool accept = true;
     double width = 1.0;
@@ -748,27 +855,27 @@ __global__ __launch_bounds__(MB_T) void qn_mb2_kernel(QnArgs A, double* __restri
         const double den = 2.0 * (ft - f - dgtest);
         width = den > 0.0 ? -dgtest / den : 0.5;
         width = isfinite(width) ? fmin(0.5, fmax(0.1, width)) : 0.5;
-      } else if (A.wolfe && !A.l1 && scr[S_BRACKET] == 0.0 && p0[2] < A.c2 * dginit) {
+      } else if (A.wolfe && !A.l1 && !bracket && p0[2] < A.c2 * dginit) {
         accept = false;
         width = 2.1;
       }
     }
     if (!accept) {
-      const int ls = (int)scr[S_LS] + 1;
+      const int ls = pre_ls + 1;
       if (ls >= A.max_ls) {
         if (first) {
           fl[F_LS] = ls;
-          fl[F_NEVAL] = (int)scr[S_NEVAL] + 1;
+          fl[F_NEVAL] = pre_neval + 1;
           fl[F_STATUS] = ST_LS_FAIL;
           fl[F_DONE] = 1;
         }
         return;
       }
       alpha *= width;
-      mb_set_trial(A, alpha);
+      if (own) mb_trial(A, i, xo, dv, pv, cv, isg, alpha);
       if (first) {
         fl[F_LS] = ls;
-        fl[F_NEVAL] = (int)scr[S_NEVAL] + 1;
+        fl[F_NEVAL] = pre_neval + 1;
         if (width < 1.0) fl[F_BRACKET] = 1;
         A.sc[SC_ALPHA] = alpha;
       }
@@ -780,17 +887,13 @@ __global__ __launch_bounds__(MB_T) void qn_mb2_kernel(QnArgs A, double* __restri
     scr[S_FT] = ft;
   }
   // accepted: pass 1 partials of this block's elements
-  const int M = A.M;
-  const long N = A.N;
   double v[MB_PW];
 #pragma unroll
   for (int j = 0; j < MB_PW; ++j) v[j] = 0.0;
-  const long i = (long)blockIdx.x * MB_T + threadIdx.x;
-  if (i < N) {
-    const double xv = A.xt[i], gv = A.gt[i];
-    const double sx = started ? xv - A.x[i] : 0.0;
-    const double yx = started ? gv - A.g[i] : 0.0;
-    const double pgi = pseudo_grad(xv, gv, A.l1 ? A.l1c[i] : 0.0);
+  if (own) {
+    const double sx = started ? xt - xo : 0.0;
+    const double yx = started ? gt - go : 0.0;
+    const double pgi = pseudo_grad(xt, gt, A.l1 ? cv : 0.0);
     A.pg[i] = pgi;
     A.d[i] = sx;
     A.wb[i] = yx;
@@ -802,21 +905,19 @@ __global__ __launch_bounds__(MB_T) void qn_mb2_kernel(QnArgs A, double* __restri
     v[MB_PW - 1] = fabs(pgi);
 #pragma unroll
     for (int j = 0; j < QN_MMAX; ++j) {
-      if (j < M) {
-        const double Sj = A.S[(long)j * N + i], Yj = A.Y[(long)j * N + i];
-        v[6 + j] = sx * Yj;
-        v[6 + QN_MMAX + j] = Sj * yx;
-        v[6 + 2 * QN_MMAX + j] = yx * Yj;
-        v[6 + 3 * QN_MMAX + j] = Sj * pgi;
-        v[6 + 4 * QN_MMAX + j] = Yj * pgi;
-      }
+      v[6 + j] = sx * Yv[j];
+      v[6 + QN_MMAX + j] = Sv[j] * yx;
+      v[6 + 2 * QN_MMAX + j] = yx * Yv[j];
+      v[6 + 3 * QN_MMAX + j] = Sv[j] * pgi;
+      v[6 + 4 * QN_MMAX + j] = Yv[j] * pgi;
     }
   }
-  // block sums (the last entry is a max)
+  // block sums (the last entry is a max); history slots >= M are zero and skipped
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
   for (int j = 0; j < MB_PW - 1; ++j) {
-    const double t = wave_sum(v[j]);
+    const bool live = j < 6 || ((j - 6) % QN_MMAX) < M;
+    const double t = live ? wave_sum(v[j]) : 0.0;
     if (lane == 0) red[j * MB_NW + wid] = t;
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -841,19 +942,41 @@ __global__ __launch_bounds__(MB_T) void qn_mb3_kernel(QnArgs A, double* __restri
   __shared__ double s_sy[QN_MMAX * QN_MMAX], s_yy[QN_MMAX * QN_MMAX], s_p1[QN_MMAX], s_p2[QN_MMAX];
   __shared__ double cf_a[QN_MMAX], cf_t[QN_MMAX], s_misc[2];
   __shared__ int s_sl[QN_MMAX], s_ctl[4];
-  if (scr[S_PHASE] != 1.0) return;
   const int G = gridDim.x, M = A.M, tid = threadIdx.x;
   const long N = A.N;
-  mb_grid_sum(scr + S_PB, G, MB_PW, tot, true);
-  for (int i = tid; i < M * M; i += MB_T) {
-    s_sy[i] = A.SY[i];  // K4's block 0 commits the updated blocks: every block reads the old ones here
-    s_yy[i] = A.YY[i];
-  }
-  __syncthreads();
+  const long i = (long)blockIdx.x * MB_T + tid;
+  const bool own = i < N;
+  // ---- every load up front
+  const double phase = scr[S_PHASE];
   const bool started = scr[S_STARTED] != 0.0;
+  const int pre_count = (int)scr[S_COUNT], head = (int)scr[S_HEAD], pre_iter = (int)scr[S_ITER];
+  const double pre_gamma = scr[S_GAMMA], fn = scr[S_FT], fhn = scr[S_FHN];
+  // K4's block 0 commits the updated blocks: every block reads the old ones here
+  const double sy0 = tid < M * M ? A.SY[tid] : 0.0, yy0 = tid < M * M ? A.YY[tid] : 0.0;
+  double xt = 0.0, gt = 0.0, sv = 0.0, yv = 0.0, pv = 0.0, cv = 0.0;
+  double Sv[QN_MMAX], Yv[QN_MMAX];
+  if (own) {
+    xt = A.xt[i];
+    gt = A.gt[i];
+    sv = A.d[i];
+    yv = A.wb[i];
+    pv = A.pg[i];
+    cv = A.l1c[i];
+  }
+#pragma unroll
+  for (int j = 0; j < QN_MMAX; ++j) {
+    Sv[j] = (own && j < M) ? A.S[(long)j * N + i] : 0.0;
+    Yv[j] = (own && j < M) ? A.Y[(long)j * N + i] : 0.0;
+  }
+  if (phase != 1.0) return;
+  if (tid < M * M) {
+    s_sy[tid] = sy0;
+    s_yy[tid] = yy0;
+  }
+  mb_grid_sum(scr + S_PB, G, MB_PW, tot, true);  // (its barriers also publish s_sy / s_yy)
   if (tid == 0) {
-    int cnt = (int)scr[S_COUNT], hd = (int)scr[S_HEAD], status = ST_RUNNING;
-    double gamma = started ? scr[S_GAMMA] : 1.0;
+    int cnt = pre_count, hd = head, status = ST_RUNNING;
+    double gamma = started ? pre_gamma : 1.0;
     for (int j = 0; j < M; ++j) {
       s_p1[j] = tot[6 + 3 * QN_MMAX + j];
       s_p2[j] = tot[6 + 4 * QN_MMAX + j];
@@ -877,13 +1000,11 @@ __global__ __launch_bounds__(MB_T) void qn_mb3_kernel(QnArgs A, double* __restri
       cnt = cnt < M ? cnt + 1 : M;
       gamma = ys / yy;
     }
-    const double fn = scr[S_FT];
     const double ginf = tot[MB_PW - 1];
-    const int iter = (int)scr[S_ITER] + (started ? 1 : 0);
+    const int iter = pre_iter + (started ? 1 : 0);
     const double fmag = fmax(fabs(fn), A.tol);
     if (ginf <= A.tol * fmag) status = ST_CONV_GRAD;
-    if (A.past > 0 && status == ST_RUNNING && started && iter >= A.past &&
-        fabs(scr[S_FHN] - fn) <= A.delta * fmag)
+    if (A.past > 0 && status == ST_RUNNING && started && iter >= A.past && fabs(fhn - fn) <= A.delta * fmag)
       status = ST_CONV_F;
     if (status == ST_RUNNING && iter >= A.max_iter) status = ST_MAXITER;
     for (int c = 0; c < cnt; ++c) s_sl[c] = (hd - cnt + c + 2 * M) % M;
@@ -959,33 +1080,32 @@ __global__ __launch_bounds__(MB_T) void qn_mb3_kernel(QnArgs A, double* __restri
   __syncthreads();
   const int status = s_ctl[0];
   const bool newp = s_ctl[1] != 0;
-  const int cnt = s_ctl[2];
   const double gamma = s_misc[0];
   if (blockIdx.x == 0 && newp)  // staged for K4 (other blocks of this launch still read A.SY / A.YY)
-    for (int i = tid; i < M * M; i += MB_T) {
-      scr[S_SY + i] = s_sy[i];
-      scr[S_SY + QN_MMAX * QN_MMAX + i] = s_yy[i];
+    for (int k = tid; k < M * M; k += MB_T) {
+      scr[S_SY + k] = s_sy[k];
+      scr[S_SY + QN_MMAX * QN_MMAX + k] = s_yy[k];
     }
-  // pass 2: store the pair, x <- xt, g <- gt, direction
+  // pass 2: store the pair, x <- xt, g <- gt, direction (inactive slots have zero coefficients)
   double p2v[2] = {0.0, 0.0};
-  const long i = (long)blockIdx.x * MB_T + tid;
-  const int head = (int)scr[S_HEAD];
-  if (i < N) {
-    const double xv = A.xt[i], gv = A.gt[i], sv = A.d[i], yv = A.wb[i], pv = A.pg[i];
+  if (own) {
     if (newp) {
       A.S[(long)head * N + i] = sv;
       A.Y[(long)head * N + i] = yv;
     }
-    A.x[i] = xv;
-    A.g[i] = gv;
+    A.x[i] = xt;
+    A.g[i] = gt;
     if (status == ST_RUNNING) {
       double hg = gamma * pv;
-      for (int c = 0; c < cnt; ++c) {
-        const int j = s_sl[c];
-        hg += cf_a[j] * A.S[(long)j * N + i] - cf_t[j] * A.Y[(long)j * N + i];
+#pragma unroll
+      for (int j = 0; j < QN_MMAX; ++j) {
+        if (j < M) {
+          const bool fresh = newp && j == head;  // the pair stored just above
+          hg += cf_a[j] * (fresh ? sv : Sv[j]) - cf_t[j] * (fresh ? yv : Yv[j]);
+        }
       }
       double di = -hg;
-      if (A.l1 && A.l1c[i] > 0.0 && di * pv >= 0.0) di = 0.0;
+      if (A.l1 && cv > 0.0 && di * pv >= 0.0) di = 0.0;
       A.d[i] = di;
       p2v[0] = pv * di;
       p2v[1] = di * di;
@@ -996,25 +1116,42 @@ __global__ __launch_bounds__(MB_T) void qn_mb3_kernel(QnArgs A, double* __restri
 }
 
 __global__ __launch_bounds__(MB_T) void qn_mb4_kernel(QnArgs A, double* __restrict__ scr) {
-  __shared__ double p2[2];
-  if (scr[S_PHASE] != 1.0) return;
+  __shared__ double p2[2], pbt[MB_PW];
   const int G = gridDim.x, M = A.M, tid = threadIdx.x;
   const bool first = blockIdx.x == 0 && tid == 0;
+  const long i = (long)blockIdx.x * MB_T + tid;
+  const bool own = i < A.N;
+  int* fl = A.fl;
+  // ---- every load up front
+  const double phase = scr[S_PHASE];
   const int status = (int)scr[S_STATUS];
   const bool newp = scr[S_NEWP] != 0.0;
-  int* fl = A.fl;
+  const int cnt0 = (int)scr[S_CNT];
+  double sy = 0.0, yy = 0.0;
+  if (blockIdx.x == 0 && tid < M * M) {
+    sy = scr[S_SY + tid];
+    yy = scr[S_SY + QN_MMAX * QN_MMAX + tid];
+  }
+  double xv = 0.0, dv = 0.0, pv = 0.0, cv = 0.0, isg = 1.0;
+  if (own) {
+    xv = A.x[i];
+    dv = A.d[i];
+    pv = A.pg[i];
+    cv = A.l1c[i];
+    if (i < A.Kn) isg = A.isg[i % A.n];
+  }
+  if (phase != 1.0) return;
   if (blockIdx.x == 0) {  // commit the step's history blocks and scalars
-    if (newp)
-      for (int i = tid; i < M * M; i += MB_T) {
-        A.SY[i] = scr[S_SY + i];
-        A.YY[i] = scr[S_SY + QN_MMAX * QN_MMAX + i];
-      }
+    if (newp && tid < M * M) {
+      A.SY[tid] = sy;
+      A.YY[tid] = yy;
+    }
     if (tid == 0) {
       const int iter = (int)scr[S_ITERN];
       if (A.past > 0) A.fh[iter % A.past] = scr[S_FN];
       fl[F_ITER] = iter;
       fl[F_HEAD] = (int)scr[S_HD];
-      fl[F_COUNT] = (int)scr[S_CNT];
+      fl[F_COUNT] = cnt0;
       fl[F_NEVAL] = (int)scr[S_NEVAL] + 1;
       fl[F_LS] = 0;
       fl[F_BRACKET] = 0;
@@ -1033,19 +1170,18 @@ __global__ __launch_bounds__(MB_T) void qn_mb4_kernel(QnArgs A, double* __restri
   }
   mb_grid_sum(scr + S_PC, G, 2, p2, false);
   double dg = p2[0], dd = p2[1];
-  int cnt2 = (int)scr[S_CNT];
-  const long i = (long)blockIdx.x * MB_T + tid;
+  int cnt2 = cnt0;
   if (!(dg < 0.0)) {  // not a descent direction: drop the history, steepest descent (rare)
-    // pg.pg (pass-1 total) is in the K2 partials: re-sum it
-    double pp = 0.0;
-    for (int b = 0; b < G; ++b) pp += scr[S_PB + (long)b * MB_PW + 4];
-    if (i < A.N) A.d[i] = -A.pg[i];
+    mb_grid_sum(scr + S_PB, G, MB_PW, pbt, true);  // pg.pg is in the K2 partials
+    const double pp = pbt[4];
+    dv = -pv;
+    if (own) A.d[i] = dv;
     dg = -pp;
     dd = pp;
     cnt2 = 0;
   }
   const double alpha = cnt2 == 0 ? 1.0 / fmax(sqrt(dd), 1e-300) : 1.0;
-  mb_set_trial(A, alpha);
+  if (own) mb_trial(A, i, xv, dv, pv, cv, isg, alpha);
   if (first) {
     if (cnt2 == 0) {
       fl[F_COUNT] = 0;
@@ -1067,7 +1203,7 @@ SRML_API int srml_qn_step_mb(const QnArgs* a, double* scratch, hipStream_t strea
   if (G > MB_GMAX) return srml_qn_step(a, stream);
   const dim3 grid((unsigned)G), blk(MB_T);
   hipLaunchKernelGGL(qn_mb1_kernel, grid, blk, 0, stream, *a, scratch);
-  hipLaunchKernelGGL(qn_mb2_kernel, grid, blk, 0, stream, *a, scratch);
+  hipLaunchKernelGGL(qn_mb2_kernel, grid, blk, 0, stream, *a, scratch, (int)G);
   hipLaunchKernelGGL(qn_mb3_kernel, grid, blk, 0, stream, *a, scratch);
   hipLaunchKernelGGL(qn_mb4_kernel, grid, blk, 0, stream, *a, scratch);
   return srml_status();
@@ -1127,6 +1263,84 @@ __device__ __forceinline__ bool fu_barrier(double* scr, unsigned G) {
 
 }  // namespace
 
+// Fold of the binary evaluation's fp32 partial gradient rows for this block's FU_E elements
+// (columns blockIdx.x * FU_E ...): 8 lanes x float4 per row, 32 row groups, 8 rows in flight per
+// thread; the bias element and the loss are the trailing doubles of every row (summed by the
+// block owning element Kn / the last block). Returns the element's sum in `oval` and the block's
+// loss contribution in `lpart`.
+__device__ __forceinline__ void fu_fold_block(const QnArgs& A, const float* __restrict__ fws, int parts, long wst,
+                                              double (*fold)[33], double* red, bool own, long i, unsigned G,
+                                              double& oval, double& lpart) {
+  const int tid = threadIdx.x;
+  const int q = tid & 7, rg = tid >> 3;  // 8 lanes x float4 = 32 columns, 32 row groups
+  const long c = (long)blockIdx.x * FU_E + 4 * q;
+  // the bias gradient (element Kn, owned by one block) and the loss (block G - 1): trailing
+  // doubles of every row, summed over the block's 256 threads; issued first, all in flight
+  const bool has_bias = A.K == 1 && A.Kn < A.N && (long)blockIdx.x == A.Kn / FU_E;
+  const bool has_loss = blockIdx.x == G - 1;
+  double gb = 0.0, ls = 0.0;
+  if (has_bias || has_loss)
+    for (int p = tid; p < parts; p += 4 * MB_T) {
+      double t0[4], t1[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int pk = p + k * MB_T;
+        const double* pd = reinterpret_cast<const double*>(fws + (long)(pk < parts ? pk : 0) * wst + wst - 4);
+        t0[k] = pk < parts ? pd[0] : 0.0;
+        t1[k] = pk < parts ? pd[1] : 0.0;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        gb += t0[k];
+        ls += t1[k];
+      }
+    }
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  if (c < A.Kn) {
+    int p = rg;
+    for (; p + 32 * 11 < parts; p += 32 * 12) {  // 12 rows in flight per thread
+      floatx4 v[12];
+#pragma unroll
+      for (int j = 0; j < 12; ++j)
+        v[j] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(fws + (long)(p + 32 * j) * wst + c));
+#pragma unroll
+      for (int j = 0; j < 12; ++j) { a0 += v[j][0]; a1 += v[j][1]; a2 += v[j][2]; a3 += v[j][3]; }
+    }
+    for (; p < parts; p += 32) {
+      const floatx4 v = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(fws + (long)p * wst + c));
+      a0 += v[0]; a1 += v[1]; a2 += v[2]; a3 += v[3];
+    }
+  }
+  fold[rg][4 * q] = a0;
+  fold[rg][4 * q + 1] = a1;
+  fold[rg][4 * q + 2] = a2;
+  fold[rg][4 * q + 3] = a3;
+  const double sums[2] = {has_bias ? gb : 0.0, has_loss ? ls : 0.0};
+  double tv2[2];
+  {
+    const int lane = tid & 63, wid = tid >> 6;
+    for (int k = 0; k < 2; ++k) {
+      const double t = wave_sum(sums[k]);
+      if (lane == 0) red[k * MB_NW + wid] = t;
+    }
+  }
+  __syncthreads();
+  tv2[0] = (red[0] + red[1]) + (red[2] + red[3]);
+  tv2[1] = (red[MB_NW] + red[MB_NW + 1]) + (red[MB_NW + 2] + red[MB_NW + 3]);
+  if (own) {
+    if (i < A.Kn) {
+      double s = 0.0;
+#pragma unroll
+      for (int g2 = 0; g2 < 32; ++g2) s += fold[g2][tid];
+      oval = s;
+    } else {
+      oval = tv2[0];  // the bias element
+    }
+  }
+  lpart = tv2[1];
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(MB_T) void qn_fused_kernel(QnArgs A, double* __restrict__ scr,
                                                         const float* __restrict__ fws, int parts, long wst) {
   __shared__ double red[MB_PW * MB_NW], tot[MB_PW], fold[32][33];
@@ -1151,66 +1365,9 @@ __global__ __launch_bounds__(MB_T) void qn_fused_kernel(QnArgs A, double* __rest
   double alpha = A.sc[SC_ALPHA];
   const double pre_fh_next = (A.past > 0 && started) ? A.fh[(pre_iter + 1) % A.past] : 0.0;
   // ---- this block's gradient sums: folded from the evaluation's partial rows, or from `out`
-  double oval = 0.0, lpart = 0.0, bpart = 0.0;
+  double oval = 0.0, lpart = 0.0;
   if (fws) {
-    const int q = tid & 7, rg = tid >> 3;  // 8 lanes x float4 = 32 columns, 32 row groups
-    const long c = (long)blockIdx.x * FU_E + 4 * q;
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-    if (c < A.Kn) {
-      int p = rg;
-      for (; p + 224 < parts; p += 256) {  // 8 rows in flight per thread
-        floatx4 v[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          v[j] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(fws + (long)(p + 32 * j) * wst + c));
-#pragma unroll
-        for (int j = 0; j < 8; ++j) { a0 += v[j][0]; a1 += v[j][1]; a2 += v[j][2]; a3 += v[j][3]; }
-      }
-      for (; p < parts; p += 32) {
-        const floatx4 v = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(fws + (long)p * wst + c));
-        a0 += v[0]; a1 += v[1]; a2 += v[2]; a3 += v[3];
-      }
-    }
-    fold[rg][4 * q] = a0;
-    fold[rg][4 * q + 1] = a1;
-    fold[rg][4 * q + 2] = a2;
-    fold[rg][4 * q + 3] = a3;
-    // the bias gradient (element Kn, owned by one block) and the loss (block G - 1): trailing
-    // doubles of every row, summed over the block's 256 threads
-    const bool has_bias = A.K == 1 && A.Kn < N && (long)blockIdx.x == A.Kn / FU_E;
-    const bool has_loss = blockIdx.x == G - 1;
-    double gb = 0.0, ls = 0.0;
-    if (has_bias || has_loss)
-      for (int p = tid; p < parts; p += MB_T) {
-        const double* pd = reinterpret_cast<const double*>(fws + (long)p * wst + wst - 4);
-        gb += pd[0];
-        ls += pd[1];
-      }
-    const double sums[2] = {has_bias ? gb : 0.0, has_loss ? ls : 0.0};
-    double tv2[2];
-    {
-      const int lane = tid & 63, wid = tid >> 6;
-      for (int k = 0; k < 2; ++k) {
-        const double t = wave_sum(sums[k]);
-        if (lane == 0) red[k * MB_NW + wid] = t;
-      }
-    }
-    __syncthreads();
-    tv2[0] = (red[0] + red[1]) + (red[2] + red[3]);
-    tv2[1] = (red[MB_NW] + red[MB_NW + 1]) + (red[MB_NW + 2] + red[MB_NW + 3]);
-    if (own) {
-      if (i < A.Kn) {
-        double s = 0.0;
-#pragma unroll
-        for (int g2 = 0; g2 < 32; ++g2) s += fold[g2][tid];
-        oval = s;
-      } else {
-        oval = tv2[0];  // the bias element
-      }
-    }
-    lpart = tv2[1];
-    bpart = 0.0;
-    __syncthreads();
+    fu_fold_block(A, fws, parts, wst, fold, red, own, i, G, oval, lpart);
   } else {
     if (own) {
       oval = A.out[i];
@@ -1218,7 +1375,6 @@ __global__ __launch_bounds__(MB_T) void qn_fused_kernel(QnArgs A, double* __rest
     }
     if (first) lpart = A.out[A.Kn + A.K];  // the loss sum; zeroed by block 0 after the barrier
   }
-  (void)bpart;
   // ---- pass 0
   double p0[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
   if (own) {
@@ -1237,12 +1393,7 @@ __global__ __launch_bounds__(MB_T) void qn_fused_kernel(QnArgs A, double* __rest
     if (first) { fl[F_STATUS] = ST_BARRIER; fl[F_DONE] = 1; }
     return;
   }
-  if (tid < 5) {  // grid totals, block order (stride 6)
-    double s = 0.0;
-    for (unsigned b = 0; b < G; ++b) s += scr[F_PA + b * 6 + tid];
-    red[tid] = s;
-  }
-  __syncthreads();
+  mb_grid_sum(scr + F_PA, (int)G, 6, red, false);
   const double q0 = red[0], q1 = red[1], q2 = red[2], q3 = red[3], lossv = red[4];
   __syncthreads();
   const double ft = lossv * A.inv_m + 0.5 * q0 + q1;
@@ -1512,12 +1663,7 @@ __global__ __launch_bounds__(MB_T) void qn_fused_kernel(QnArgs A, double* __rest
     }
   }
   if (status != ST_RUNNING) return;
-  if (tid < 2) {
-    double s = 0.0;
-    for (unsigned b = 0; b < G; ++b) s += scr[F_PC + b * 2 + tid];
-    red[tid] = s;
-  }
-  __syncthreads();
+  mb_grid_sum(scr + F_PC, (int)G, 2, red, false);
   double dg = red[0], dd = red[1];
   int cnt2 = cnt;
   if (!(dg < 0.0)) {  // not a descent direction: drop the history, steepest descent (rare)
@@ -1562,5 +1708,51 @@ SRML_API int srml_qn_step_fused(const QnArgs* a, double* scratch, const float* f
   if (G > FU_GMAX) return srml_qn_step(a, stream);
   if (fws && (a->K != 1 || (wst & 3) || parts <= 0)) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(qn_fused_kernel, dim3((unsigned)G), dim3(MB_T), 0, stream, *a, scratch, fws, parts, wst);
+  return srml_status();
+}
+
+// K1 of the multi-block step with the fold of the binary evaluation's partial rows in front
+// (one-rank fits): ceil(N / 32) blocks, each folds its 32 elements' columns (fu_fold_block) and
+// writes the pass-0 partials; K2..K4 as in srml_qn_step_mb. Replaces fold_rows_kernel + K1.
+__global__ __launch_bounds__(MB_T) void qn_mb1f_kernel(QnArgs A, double* __restrict__ scr,
+                                                       const float* __restrict__ fws, int parts, long wst) {
+  __shared__ double red[4 * MB_NW], tot[4], fold[32][33];
+  const bool first = blockIdx.x == 0 && threadIdx.x == 0;
+  const unsigned G = gridDim.x;
+  const long i = (long)blockIdx.x * FU_E + threadIdx.x;
+  const bool own = threadIdx.x < FU_E && i < A.N;
+  // every load up front (the fold's rows are read even when the fit is done: a finished fit's
+  // remaining graph replays cost one wasted read each, against a round trip on every step)
+  const int done = A.fl[F_DONE];
+  MbSnap q{};
+  if (first) q = mb_snap_load(A);
+  const MbP0In e = mb_p0_load(A, i, own);
+  double oval = 0.0, lpart = 0.0;
+  fu_fold_block(A, fws, parts, wst, fold, red, own, i, G, oval, lpart);
+  if (done) {
+    if (first) scr[S_PHASE] = 0.0;
+    return;
+  }
+  if (first) mb_snap_store(A, q, scr);
+  if (blockIdx.x == G - 1 && threadIdx.x == 0) scr[S_LOSS] = lpart;
+  double p0[4] = {0.0, 0.0, 0.0, 0.0};
+  mb_p0(A, i, own, e, oval, p0);
+  mb_block_sum<4>(p0, red, tot);
+  if (threadIdx.x < 4) scr[S_PA + blockIdx.x * 4 + threadIdx.x] = tot[threadIdx.x];
+}
+
+// One optimiser step of a one-rank binary fit as four launches with the evaluation's fold in K1:
+// fws = srml_logreg_binary3_f32's workspace left unfolded (leave = 1), parts rows of wst floats.
+SRML_API int srml_qn_step_mbf(const QnArgs* a, double* scratch, const float* fws, int parts, long wst,
+                              hipStream_t stream) {
+  if (a->M < 1 || a->M > QN_MMAX || a->N <= 0 || !scratch || !fws) return (int)hipErrorInvalidValue;
+  if (a->K != 1 || (wst & 3) || parts <= 0) return (int)hipErrorInvalidValue;
+  const long G = (a->N + MB_T - 1) / MB_T, G1 = (a->N + FU_E - 1) / FU_E;
+  if (G > MB_GMAX || G1 > MB_GAMAX) return (int)hipErrorInvalidValue;
+  const dim3 grid((unsigned)G), blk(MB_T);
+  hipLaunchKernelGGL(qn_mb1f_kernel, dim3((unsigned)G1), blk, 0, stream, *a, scratch, fws, parts, wst);
+  hipLaunchKernelGGL(qn_mb2_kernel, grid, blk, 0, stream, *a, scratch, (int)G1);
+  hipLaunchKernelGGL(qn_mb3_kernel, grid, blk, 0, stream, *a, scratch);
+  hipLaunchKernelGGL(qn_mb4_kernel, grid, blk, 0, stream, *a, scratch);
   return srml_status();
 }

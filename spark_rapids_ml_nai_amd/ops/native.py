@@ -68,6 +68,7 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_qn_step": (_P, _P),
     "srml_qn_step_mb": (_P, _P, _P),
     "srml_qn_step_fused": (_P, _P, _P, _I, _L, _P),
+    "srml_qn_step_mbf": (_P, _P, _P, _I, _L, _P),
     "srml_qn_fused_scratch": (),
     "srml_qn_mb_scratch": (),
     "srml_kmeanspp_gram": (_P, _I, _L, _P, _I, _I, ctypes.c_ulonglong, _P, _P),

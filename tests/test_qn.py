@@ -303,8 +303,9 @@ def test_qn_multiblock_step_matches_single_block(gpu_device, K, l1, n, monkeypat
 
 @pytest.mark.gpu
 def test_logistic_fit_fused_fold_matches_unfused(gpu_device, monkeypatch):
-    """One-rank binary LogReg with the fold moved into the fused optimiser step (the evaluation
-    leaves its partial rows) reproduces the fit whose evaluation folds them itself."""
+    """One-rank binary LogReg with the fold moved into the optimiser step (the evaluation leaves
+    its partial rows; srml_qn_step_mbf / srml_qn_step_fused fold them) reproduces the fit whose
+    evaluation folds them itself."""
     from spark_rapids_ml_nai_amd import ops
     from spark_rapids_ml_nai_amd.models import qn as qnm
     from spark_rapids_ml_nai_amd.models.logistic import logistic_fit
@@ -318,15 +319,19 @@ def test_logistic_fit_fused_fold_matches_unfused(gpu_device, monkeypatch):
     assert ops.logreg_workspace(Xt) is not None and ops.logistic_path(Xt, 1) == "fused_binary_f32"
     ctx = WorkerContext.single(gpu_device)
     out = {}
-    for mode in ("mb", "fused"):
-        monkeypatch.setattr(qnm, "QN_MB", True)
+    for mode in ("single", "mb", "fused"):  # unfolded single-block step / srml_qn_step_mbf / fused
+        monkeypatch.setattr(qnm, "QN_MB", mode != "single")
         monkeypatch.setattr(qnm, "QN_STEP", mode)
         out[mode] = logistic_fit(Xt, yt, m, ctx, reg=1e-3, l1_ratio=0.0, fit_intercept=True,
                                  standardization=True, max_iter=60, tol=1e-10)
-    a, b = out["mb"], out["fused"]
-    assert a["num_iters"] == b["num_iters"], (a["num_iters"], b["num_iters"])
-    assert abs(a["objective"] - b["objective"]) <= 1e-6 * abs(a["objective"])
-    np.testing.assert_allclose(np.asarray(b["coef_"]), np.asarray(a["coef_"]), rtol=1e-3, atol=1e-5)
+    a = out["single"]
+    for mode in ("mb", "fused"):
+        b = out[mode]
+        # the fp32 evaluation's partials are summed in another order, so a convergence test at
+        # tol 1e-10 (below fp32 noise) may stop at another iteration: compare the optimum
+        assert abs(a["objective"] - b["objective"]) <= 1e-6 * abs(a["objective"]), (mode, a["objective"],
+                                                                                    b["objective"])
+        np.testing.assert_allclose(np.asarray(b["coef_"]), np.asarray(a["coef_"]), rtol=1e-3, atol=1e-5)
 
 
 @pytest.mark.gpu

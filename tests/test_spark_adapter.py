@@ -73,7 +73,9 @@ def test_barrier_worker_linear_regression(monkeypatch):
     est = LinearRegression(featuresCol="features", labelCol="label", num_workers=2)
     rows = run_fake_barrier_stage(_task(_fit_payload(est)), parts)
     assert len(rows) == 1  # rank 0 yields the model
-    res = cloudpickle.loads(rows[0]["result"][0])
+    out = cloudpickle.loads(rows[0]["result"][0])
+    res = out.result  # core.base._FitOut: the model attributes + every rank's time split
+    assert len(out.ranks) == 2 and all("h2d_exposed_s" in r for r in out.ranks)
     ref = LinearRegression(num_workers=1).fit(DataFrame.from_numpy(X, y))
     assert np.allclose(res["coef_"], ref.coefficients.toArray(), atol=1e-5)
     assert np.isclose(res["intercept_"], ref.intercept, atol=1e-5)
