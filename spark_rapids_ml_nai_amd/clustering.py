@@ -193,8 +193,10 @@ class KMeansModel(KMeansClass, _ModelWithPredictionCol, _KMeansParams):
 
         def predict(Cd: torch.Tensor, X: Any, ctx: WorkerContext) -> Dict[str, np.ndarray]:
             from .core.base import to_device
-            from .models.kmeans import kmeans_predict
+            from .models.kmeans import kmeans_predict, kmeans_predict_streamed, predict_streams
 
+            if ctx.device.type == "cuda" and predict_streams(X, Cd.shape[0]):  # H2D under the search
+                return {pred_col: kmeans_predict_streamed(X, Cd, ctx.device).cpu().numpy().astype(np.int32)}
             Xd = to_device(X, ctx.device, torch.float32)
             return {pred_col: kmeans_predict(Xd, Cd).cpu().numpy().astype(np.int32)}
 

@@ -280,7 +280,9 @@ def _root_hist_streamed(pending: PendingBins, bins: torch.Tensor, idx: torch.Ten
     m = bins.shape[1]
     nf = feats.shape[1]
     nfc = (nf + fb - 1) // fb
-    hist = torch.zeros((C, nf, B, SH), dtype=torch.float64 if regression else torch.int32, device=dev)
+    Ch = feats.shape[0]  # histogram rows: C, or C padded for the node-partitioned reduce-scatter
+    assert C == len(c_start) and Ch >= C
+    hist = torch.zeros((Ch, nf, B, SH), dtype=torch.float64 if regression else torch.int32, device=dev)
     wy = ops.rf_hist_wy(idx, yv, None, wpos)
     rows_at = torch.tensor([r0 for r0, _ in pending.bounds] + [m], dtype=idx.dtype, device=dev)
     # P[j, c]: first position of segment j whose row is >= the start of chunk c
@@ -308,7 +310,7 @@ def _root_hist_streamed(pending: PendingBins, bins: torch.Tensor, idx: torch.Ten
     items_all = torch.from_numpy(np.concatenate(per_chunk, 0)).to(dev)
     for ci, _rows in enumerate(pending.chunks()):
         if off[ci + 1] > off[ci]:
-            ops.rf_hist(bins, idx, yv, None, items_all[off[ci]: off[ci + 1]], feats, C, B, SH, regression,
+            ops.rf_hist(bins, idx, yv, None, items_all[off[ci]: off[ci + 1]], feats, Ch, B, SH, regression,
                         pos_weight=wpos, fb=fb, yscale=yscale, out=hist, wy=wy)
     return hist
 
@@ -457,7 +459,7 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
             c_start, c_cnt = bounds_h[cg], counts[cg]
             if streamed_root:
                 hist = _root_hist_streamed(pending, bins, idx, wpos, yv, c_start, c_cnt,
-                                           feats if Cp == C else _pad_rows(feats, Cp), Cp, B, SH, regression, fb, yscale)
+                                           feats if Cp == C else _pad_rows(feats, Cp), C, B, SH, regression, fb, yscale)
                 pending = None
             il = None
             fb_l, nfc_l, rpi_min, blocks = fb, nfc, ROWS_PER_ITEM, 8192

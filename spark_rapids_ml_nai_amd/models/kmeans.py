@@ -241,8 +241,24 @@ def kmeans_fit(X: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext, k
     sums_l = counts_l = None
     n_delta = 0
     last_anchor = 0
+    # k <= 32, n <= 64 (the BASELINE k = 20 on 100M x 64): the fused one-pass step gives labels,
+    # full cluster sums and the inertia together (no delta bookkeeping needed)
+    fused_small = F16 is None and XP is None and ops.lloyd_small_ok(X, k) and not deterministic()
     for it in range(max(0, max_iter)):
         n_iter = it + 1
+        if fused_small:
+            _, _, sums_l, counts_l, d2s = ops.kmeans_lloyd_small(X, C.float())
+            buf = torch.cat([sums_l.view(-1), counts_l.double(), d2s])
+            ctx.comm.allreduce(buf)
+            sums = buf[: k * n].view(k, n)
+            counts = buf[k * n: k * n + k]
+            inertia = float(buf[-1].item()) if it == max_iter - 1 else inertia
+            newC = torch.where(counts.view(-1, 1) > 0, sums / counts.clamp_min(1.0).view(-1, 1), C)
+            shift = float(((newC - C) ** 2).sum(1).max().item())
+            C = newC
+            if shift <= tol2:
+                break
+            continue
         if F16 is not None:
             labels, d2 = ops.nearest_centroid_f16(F16, C.float())
         elif XP is not None:
@@ -312,3 +328,42 @@ def kmeans_predict(X: torch.Tensor, C: torch.Tensor) -> torch.Tensor:
         return labels
     labels, _ = ops.nearest_centroid(X, C)
     return labels
+
+
+def kmeans_predict_streamed(host: np.ndarray, C: torch.Tensor, device: torch.device,
+                            chunk_bytes: int = 0) -> torch.Tensor:
+    """``kmeans_predict`` of a page-locked host matrix with its H2D streamed under the search
+    (reference transform: ``clustering.py:493-499``, one cuML predict per batch): the rows cross
+    PCIe in ~256 MB chunks on the copy stream (``ops.ingest.StreamedRows``) while the certified
+    fp16 filter labels the chunks already on the device, so the transform costs about its H2D.
+
+    Each chunk is centred on the centres' mean (the filter's operands are x - mu and c - mu; any
+    mu keeps the labels exact, it only conditions the fp16 plane) with its own plane scale. Chunks
+    the fp16 filter cannot take (no finite range) use ``kmeans_predict``."""
+    from ..ops.ingest import StreamedRows
+
+    if chunk_bytes <= 0:
+        chunk_bytes = int(os.environ.get("SRML_PREDICT_CHUNK_MB", "256")) << 20
+    S = StreamedRows(host, device, torch.float32, chunk_bytes=chunk_bytes)
+    Cf = C.float().to(device)
+    mu = Cf.mean(0)
+    labels = torch.empty(host.shape[0], dtype=torch.int32, device=device)
+    for r0, r1, Xc in S.chunks():
+        F16 = ops.F16Planes(Xc, mu)
+        if F16.ok:
+            labels[r0:r1] = ops.nearest_centroid_f16(F16, Cf)[0]
+        else:
+            labels[r0:r1] = kmeans_predict(Xc, Cf).to(torch.int32)
+    return labels
+
+
+def predict_streams(host: Any, k: int) -> bool:
+    """Whether ``kmeans_predict_streamed`` takes this host batch: page-locked, large, k > 256 and
+    the fp16 certified filter (``SRML_KMEANS_PREDICT_STREAM=0`` disables)."""
+    from ..ops.ingest import is_pinned
+
+    return (isinstance(host, np.ndarray) and host.ndim == 2 and host.shape[0] >= 65536 and k > 256
+            and host.dtype == np.float32 and torch.cuda.is_available()
+            and os.environ.get("SRML_KMEANS_PREDICT_STREAM", "1") == "1"
+            and os.environ.get("SRML_KMEANS_PREDICT_SPLIT", "1") == "1"
+            and ops.kmeans_filter_mode() == "f16" and is_pinned(host))

@@ -351,6 +351,8 @@ def nearest_centroid(X: torch.Tensor, C: torch.Tensor, xnorm: Optional[torch.Ten
     X = _c(X)
     C = _c(C.to(torch.float32))
     cn = _c(cnorm.to(torch.float32))
+    if lloyd_small_ok(X, k, search_only=True):  # small k: one pass, VALU distances (MFMA tiles idle)
+        return kmeans_lloyd_small(X, C, cn, with_sums=False)[:2]
     best = torch.full((m,), -1, dtype=torch.int64, device=X.device)  # 0xFFFF... as uint64
     st = native.stream(X.device)
     native.call("srml_nearest_centroid_f32", X.data_ptr(), m, n, X.stride(0), C.data_ptr(), k, C.stride(0),
@@ -829,6 +831,43 @@ def sorted_counts(sorted_labels: torch.Tensor, k: int) -> torch.Tensor:
     bounds = torch.searchsorted(sorted_labels.contiguous(),
                                 torch.arange(k + 1, device=sorted_labels.device, dtype=sorted_labels.dtype))
     return (bounds[1:] - bounds[:-1]).long()
+
+
+def lloyd_small_ok(X: torch.Tensor, k: int, search_only: bool = False) -> bool:
+    """Whether ``kmeans_lloyd_small`` takes X (fp32 on the device, k <= 32, n <= 64, n % 4 == 0,
+    16-B aligned rows); ``SRML_KMEANS_SMALL=0`` disables it."""
+    del search_only  # the search alone has the same limits (k in (32, 64]: no faster than MFMA)
+    if not (X.is_cuda and X.dtype == torch.float32 and X.dim() == 2 and 1 <= k <= 32):
+        return False
+    m, n = X.shape
+    return (n <= 64 and n % 4 == 0 and X.stride(1) == 1 and X.stride(0) % 4 == 0 and X.data_ptr() % 16 == 0
+            and os.environ.get("SRML_KMEANS_SMALL", "1") != "0")
+
+
+def kmeans_lloyd_small(X: torch.Tensor, C: torch.Tensor, cnorm: Optional[torch.Tensor] = None,
+                       with_sums: bool = True) -> Tuple[torch.Tensor, ...]:
+    """Fused small-k Lloyd step (``srml_kmeans_lloyd_small``, ONE pass over X): (labels int32,
+    squared distances fp32) and, with ``with_sums``, (cluster sums fp64 [k, n], counts int64 [k],
+    inertia fp64 [1]) by those labels."""
+    m, n = X.shape
+    k = C.shape[0]
+    dev = X.device
+    C = _c(C.to(device=dev, dtype=torch.float32))
+    cn = _c((C * C).sum(1) if cnorm is None else cnorm.to(device=dev, dtype=torch.float32))
+    labels = torch.empty(m, dtype=torch.int32, device=dev)
+    dist = torch.empty(m, dtype=torch.float32, device=dev)
+    sums = counts = inertia = None
+    if with_sums:
+        sums = torch.zeros((k, n), dtype=torch.float64, device=dev)
+        counts = torch.zeros(k, dtype=torch.int32, device=dev)
+        inertia = torch.zeros(1, dtype=torch.float64, device=dev)
+    native.call("srml_kmeans_lloyd_small", X.data_ptr(), m, n, X.stride(0), C.data_ptr(), k, cn.data_ptr(),
+                labels.data_ptr(), dist.data_ptr(), sums.data_ptr() if with_sums else None,
+                counts.data_ptr() if with_sums else None, inertia.data_ptr() if with_sums else None,
+                native.stream(dev))
+    if not with_sums:
+        return labels, dist
+    return labels, dist, sums, counts.long(), inertia
 
 
 def cluster_sums(X: torch.Tensor, labels: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:

@@ -79,7 +79,8 @@ __global__ __launch_bounds__(256, 2) void nearest_centroid_kernel(const float* _
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
+          if (col0 + wn * NT * 32 + nt * 32 < k)  // wave-uniform: a tile of padding centres is skipped
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
     }
     if (more) {
       xt.store(Xs[cur ^ 1]);
@@ -97,8 +98,13 @@ __global__ __launch_bounds__(256, 2) void nearest_centroid_kernel(const float* _
     cj[nt] = col0 + wn * NT * 32 + nt * 32 + li;
     cn[nt] = (cj[nt] < k) ? cnorm[cj[nt]] : 0.f;
   }
+  // one centre tile, all of it in this wave's columns (small k): the row minima are final here, so
+  // lane li < 16 keeps row r = li of each half and ONE plain store per 32-row tile writes them
+  // (per-row atomicMin from one lane each cost more than the distance GEMM at k = 20)
+  const bool final_here = n_ctiles == 1 && WN == 1;
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
+    unsigned long long keep = ~0ull;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       float bv = __builtin_huge_valf();
@@ -116,13 +122,18 @@ __global__ __launch_bounds__(256, 2) void nearest_centroid_kernel(const float* _
         const int oi = __shfl_xor(bi, o, 64);
         if (ov < bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
       }
-      if (li == 0 && bi != 0x7fffffff) {
+      const unsigned long long key =
+          bi == 0x7fffffff ? ~0ull : (((unsigned long long)orderable(bv) << 32) | (unsigned)bi);
+      if (final_here) {
+        if (li == r) keep = key;
+      } else if (li == 0 && bi != 0x7fffffff) {
         const long row = row0 + wm * MT * 32 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
-        if (row < m) {
-          const unsigned long long key = ((unsigned long long)orderable(bv) << 32) | (unsigned)bi;
-          atomicMin(&best[row], key);
-        }
+        if (row < m) atomicMin(&best[row], key);
       }
+    }
+    if (final_here && li < 16) {
+      const long row = row0 + wm * MT * 32 + mt * 32 + (li & 3) + 8 * (li >> 2) + 4 * lk;
+      if (row < m) best[row] = keep;
     }
   }
 }
@@ -150,7 +161,26 @@ __global__ __launch_bounds__(256) void accumulate_lds_kernel(const float* __rest
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const long r0 = (long)blockIdx.x * rows_per_block;
   const long r1 = min(m, r0 + rows_per_block);
-  for (long r = r0 + wid; r < r1; r += 4) {
+  // U rows per wave step: their labels and values are loaded together (one dependent global
+  // round trip per U rows instead of per row), then added into the block's LDS sums
+  constexpr int U = 8;
+  long r = r0 + wid;
+  for (; r + 4 * (U - 1) < r1; r += 4 * U) {
+    int l[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) l[u] = labels[r + 4 * u];
+    if (lane < U) atomicAdd(&s_cnt[labels[r + 4 * lane]], 1);
+    for (int d0 = 0; d0 < n; d0 += 64) {
+      const int d = d0 + lane;
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = d < n ? X[(r + 4 * u) * ld + d] : 0.f;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (d < n) atomicAdd(&s_sum[(long)l[u] * n + d], v[u]);
+    }
+  }
+  for (; r < r1; r += 4) {
     const int l = labels[r];
     if (lane == 0) atomicAdd(&s_cnt[l], 1);
     float* dst = s_sum + (long)l * n;
@@ -534,17 +564,19 @@ SRML_API int srml_nearest_centroid_f32(const float* X, long m, int n, long ldx, 
                            X + r0 * ldx, mc, n, ldx, C, k, ldc, cnorm, best + r0, ct);
     }
   } else {
-    constexpr int BM = 256, BN = 64;
+    // k <= 64: 128-row x 64-centre tiles, 4 waves of 32 rows x 64 centres (the 256-row tile's
+    // 85 KB of LDS admitted one block per CU: the small-k search ran latency-bound at ~0.6 TB/s)
+    constexpr int BM = 128, BN = 64;
     const int ct = (k + BN - 1) / BN;
     const long rows_per = (srml_max_blocks(256) / ct) * BM;
     for (long r0 = 0; r0 < m; r0 += rows_per) {
       const long mc = m - r0 < rows_per ? m - r0 : rows_per;
       const long nb = (mc + BM - 1) / BM * ct;
       if (vec)
-        hipLaunchKernelGGL((nearest_centroid_kernel<BM, BN, 4, 2, 2, true>), dim3((unsigned)nb), dim3(256), 0, stream,
+        hipLaunchKernelGGL((nearest_centroid_kernel<BM, BN, 4, 1, 2, true>), dim3((unsigned)nb), dim3(256), 0, stream,
                            X + r0 * ldx, mc, n, ldx, C, k, ldc, cnorm, best + r0, ct);
       else
-        hipLaunchKernelGGL((nearest_centroid_kernel<BM, BN, 4, 2, 2, false>), dim3((unsigned)nb), dim3(256), 0, stream,
+        hipLaunchKernelGGL((nearest_centroid_kernel<BM, BN, 4, 1, 2, false>), dim3((unsigned)nb), dim3(256), 0, stream,
                            X + r0 * ldx, mc, n, ldx, C, k, ldc, cnorm, best + r0, ct);
     }
   }
@@ -1044,3 +1076,211 @@ SRML_API int srml_kmeanspp_gram(const double* G, int nc, long ldg, const double*
     hipLaunchKernelGGL(kmeanspp_gram_kernel, dim3(1), dim3(KPP_T), 0, stream, G, nc, ldg, w, k, trials, seed, out);
   return srml_status();
 }
+
+namespace {
+
+// ------------------------------------------------------------------------------------------
+// Small-k Lloyd step, fused (k <= 32, n <= 64, the BASELINE KMeans k = 20 on 100M x 64): ONE
+// pass over X per iteration computes every row's nearest centre AND the per-cluster sums / counts
+// by those labels (and the inertia), where the generic path read X twice (distance GEMM, then
+// cluster sums) with short-lived blocks that ran latency-bound (~0.6 TB/s at n = 64).
+//   * a thread owns one row (NV float4 in registers, the wave's 64 rows = 64 x 16 KB in flight);
+//   * distances on the VALU against the centres held transposed in LDS (cT[d][KP]: the KP values
+//     of column d are one broadcast ds_read per 4 centres), packed fp32 FMAs, arg-min with the
+//     lowest index on ties (the MFMA search's tie rule);
+//   * cluster sums as a one-hot GEMM on the fp32 matrix cores: the wave stages its 64 rows in LDS,
+//     A = one-hot(label) (32 clusters x 2 rows), B = the rows (2 x 32 columns) per
+//     v_mfma_f32_32x32x2f32, accumulators = sums[cluster][column] across all the wave's row groups;
+//   * persistent blocks (grid <= 2 per CU) loop over 256-row groups; at the end the 4 waves'
+//     accumulators are summed in LDS and each block adds its k x n partial with fp64 atomics
+//     (sums / counts / inertia must start at zero).
+// sums == nullptr: search only (labels / dist), e.g. the k-means|| passes.
+template <int NV, int KP>
+__global__ __launch_bounds__(256, 2) void lloyd_small_kernel(const float* __restrict__ X, long m, int n, long ld,
+                                                             const float* __restrict__ C, int k,
+                                                             const float* __restrict__ cnorm,
+                                                             int* __restrict__ labels, float* __restrict__ dist,
+                                                             double* __restrict__ sums, int* __restrict__ counts,
+                                                             double* __restrict__ inertia) {
+  constexpr int NT = (4 * NV + 31) / 32;  // 32-column tiles of the sums
+  constexpr int XST = 4 * NV + 4;          // staged row stride (floats): 16-B aligned, rotates banks
+  __shared__ __attribute__((aligned(16))) float cT[4 * NV][KP];
+  __shared__ float s_cn[KP];
+  __shared__ __attribute__((aligned(16))) float xs[4][64 * XST];
+  __shared__ int s_lab[4][64];
+  __shared__ int s_cnt[32];
+  __shared__ double s_in[4];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int li = lane & 31, lk = lane >> 5;
+  const bool acc_sums = sums != nullptr;
+  for (int i = t; i < 4 * NV * KP; i += 256) {
+    const int d = i / KP, j = i % KP;
+    cT[d][j] = (j < k && d < n) ? C[(long)j * n + d] : 0.f;
+  }
+  if (t < KP) s_cn[t] = t < k ? cnorm[t] : __builtin_huge_valf();
+  if (t < 32) s_cnt[t] = 0;
+  __syncthreads();
+  floatx16 acc[NT];
+#pragma unroll
+  for (int q = 0; q < NT; ++q)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[q][r] = 0.f;
+  double in_sum = 0.0;
+  const long groups = (m + 255) / 256;
+  float* xw = xs[wid];
+  // the wave's 64 rows are read lane-linearly (float4 f = lane + 64 i of the 64 x NV float4 chunk:
+  // consecutive lanes, consecutive 16 B when ld == n) one group AHEAD: the loads of group g + 1 are
+  // in flight while group g's distances and one-hot MFMAs run; staged rows then go to LDS, where
+  // each lane reads its own row back (XST = 4 NV + 4 keeps a 16-lane phase of ds_read_b128 on
+  // distinct banks) and the MFMA loop reads its B fragments
+  floatx4 pre[NV];
+  auto fetch = [&](long g) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int f = lane + 64 * i, rr = f / NV, comp = f % NV;
+      const long r = g * 256 + wid * 64 + rr;
+      pre[i] = (g < groups && r < m && 4 * comp < n) ? *reinterpret_cast<const floatx4*>(X + r * ld + 4 * comp)
+                                                    : floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  fetch(blockIdx.x);
+  for (long gi = blockIdx.x; gi < groups; gi += gridDim.x) {
+    const long row = gi * 256 + t;
+    const bool live = row < m;
+    __builtin_amdgcn_wave_barrier();  // every lane is done with the previous group's staged rows
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int f = lane + 64 * i;
+      *reinterpret_cast<floatx4*>(&xw[(f / NV) * XST + 4 * (f % NV)]) = pre[i];
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    floatx4 x[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) x[v] = *reinterpret_cast<const floatx4*>(&xw[lane * XST + 4 * v]);
+    fetch(gi + gridDim.x);  // next group's rows: in flight under this group's work
+    // distances: dp[j / 2] = (x.c_j, x.c_{j+1})
+    typedef float float2v __attribute__((ext_vector_type(2)));
+    float2v dp[KP / 2];
+#pragma unroll
+    for (int j = 0; j < KP / 2; ++j) dp[j] = float2v{0.f, 0.f};
+    float xn = 0.f;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float xv = x[v][q];
+        xn = fmaf(xv, xv, xn);
+        const float2v xx = float2v{xv, xv};
+        const floatx4* cp = reinterpret_cast<const floatx4*>(&cT[4 * v + q][0]);
+#pragma unroll
+        for (int j4 = 0; j4 < KP / 4; ++j4) {
+          const floatx4 c4 = cp[j4];
+          dp[2 * j4] = __builtin_elementwise_fma(xx, float2v{c4[0], c4[1]}, dp[2 * j4]);
+          dp[2 * j4 + 1] = __builtin_elementwise_fma(xx, float2v{c4[2], c4[3]}, dp[2 * j4 + 1]);
+        }
+      }
+    }
+    float bv = __builtin_huge_valf();
+    int bi = 0;
+#pragma unroll
+    for (int j = 0; j < KP; ++j) {
+      const float d = fmaf(-2.f, dp[j / 2][j & 1], s_cn[j]);  // +inf for j >= k
+      if (d < bv) { bv = d; bi = j; }
+    }
+    float dd = bv + xn;
+    dd = dd > 0.f ? dd : 0.f;
+    if (live) {
+      labels[row] = bi;
+      dist[row] = dd;
+      in_sum += (double)dd;
+    }
+    if (!acc_sums) continue;
+    // one-hot GEMM over the wave's 64 staged rows
+    s_lab[wid][lane] = live ? bi : -1;
+    if (live) atomicAdd(&s_cnt[bi], 1);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll 4
+    for (int s2 = 0; s2 < 32; ++s2) {
+      const int rr = 2 * s2 + lk;
+      const float a = s_lab[wid][rr] == li ? 1.f : 0.f;
+#pragma unroll
+      for (int q = 0; q < NT; ++q) {
+        const int col = q * 32 + li;
+        const float b = col < 4 * NV ? xw[rr * XST + col] : 0.f;
+        acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[q], 0, 0, 0);
+      }
+    }
+  }
+  // block totals: inertia, counts, sums (4 waves' accumulators through LDS, one wave flushes)
+  {
+    double v = in_sum;
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) s_in[wid] = v;
+  }
+  __syncthreads();
+  if (t == 0 && inertia) atomicAdd(inertia, (s_in[0] + s_in[1]) + (s_in[2] + s_in[3]));
+  if (!acc_sums) return;
+  if (t < k && s_cnt[t]) atomicAdd(&counts[t], s_cnt[t]);
+  // acc[q][r] = sums[cluster (r&3) + 8(r>>2) + 4 lk][column q * 32 + li]; reuse xs as [4][32][NT*32]
+  float* red = &xs[0][0];
+  constexpr int RW = NT * 32;
+#pragma unroll
+  for (int q = 0; q < NT; ++q)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int cl = (r & 3) + 8 * (r >> 2) + 4 * lk;
+      red[(wid * 32 + cl) * RW + q * 32 + li] = acc[q][r];
+    }
+  __syncthreads();
+  for (int i = t; i < k * n; i += 256) {
+    const int cl = i / n, col = i % n;
+    const float v = (red[(0 * 32 + cl) * RW + col] + red[(1 * 32 + cl) * RW + col]) +
+                    (red[(2 * 32 + cl) * RW + col] + red[(3 * 32 + cl) * RW + col]);
+    if (v != 0.f) atomicAdd(&sums[(long)cl * n + col], (double)v);
+  }
+}
+
+}  // namespace
+
+// Fused small-k Lloyd step (see lloyd_small_kernel): labels / squared distances of every row, and
+// when sums != null the per-cluster fp64 sums, int32 counts and the fp64 inertia (all three must be
+// zeroed by the caller). Needs k <= 32 (the VALU search of k = 41 measured 4.1 ms at 10M x 64,
+// no faster than the MFMA search), n <= 64,
+// n % 4 == 0, ld % 4 == 0, 16-B aligned X. (Centres through the scalar path instead of LDS
+// broadcast reads measured 3.7x slower.)
+SRML_API int srml_kmeans_lloyd_small(const float* X, long m, int n, long ld, const float* C, int k,
+                                     const float* cnorm, int* labels, float* dist, double* sums, int* counts,
+                                     double* inertia, hipStream_t stream) {
+  if (m <= 0) return 0;
+  if (k < 1 || k > 32 || n < 1 || n > 64 || (n & 3) || (ld & 3) ||
+      (reinterpret_cast<uintptr_t>(X) & 15))
+    return (int)hipErrorInvalidValue;
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  const long groups = (m + 255) / 256;
+  const unsigned grid = (unsigned)(groups < 2L * cus ? groups : 2L * cus);
+#define SRML_LLOYD(NV, KP)                                                                                         \
+  hipLaunchKernelGGL((lloyd_small_kernel<NV, KP>), dim3(grid), dim3(256), 0, stream, X, m, n, ld, C, k, cnorm, labels, \
+                     dist, sums, counts, inertia)
+#define SRML_LLOYD_K(NV)                  \
+  do {                                    \
+    if (k <= 8) SRML_LLOYD(NV, 8);        \
+    else if (k <= 16) SRML_LLOYD(NV, 16); \
+    else if (k <= 24) SRML_LLOYD(NV, 24); \
+    else SRML_LLOYD(NV, 32);              \
+  } while (0)
+  if (n <= 16) SRML_LLOYD_K(4);
+  else if (n <= 32) SRML_LLOYD_K(8);
+  else SRML_LLOYD_K(16);
+#undef SRML_LLOYD_K
+#undef SRML_LLOYD
+  return srml_status();
+}
+

@@ -24,6 +24,7 @@
 //    distinct 4-bank groups), double-buffered with register prefetch so the next k step's
 //    global loads are in flight under the current 24 MFMAs per wave. Grid is 1-D, centroid tile
 //    fastest and XCD-remapped so the blocks sharing one X row tile run on one XCD's L2.
+#include <cstring>
 #include "common.h"
 
 #include "tile.h"
@@ -342,50 +343,62 @@ __device__ __forceinline__ void split_epilogue_top2_t(const floatx16 (&acc)[BM /
                                                       int nslot, int wm, int wn, int li, int lk, float dscale,
                                                       float xadd) {
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
-  float cn[TN][16], g[TN][16];
+  // per-row state of the wave's TM rows of this lane; the centre tiles are scanned nt-outer (one
+  // tile's 16 norms / radii live at a time: TN = 4 tiles would need 128 more VGPRs), j ascending
+  // per lane either way, so ties keep the lower index
+  float bv[TM], badj[TM], sadj[TM], xs[TM];
+  int bi[TM];
 #pragma unroll
-  for (int nt = 0; nt < TN; ++nt)
+  for (int mt = 0; mt < TM; ++mt) {
+    const long row = row0 + wm * (BM / WM) + mt * 32 + li;
+    xs[mt] = row < m ? sqrtf(fmaxf(xnorm[row], 0.f)) + xadd : 0.f;
+    bv[mt] = badj[mt] = sadj[mt] = __builtin_huge_valf();
+    bi[mt] = 0x7fffffff;
+  }
+#pragma unroll
+  for (int nt = 0; nt < TN; ++nt) {
+    float cn[16], g[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int j = col0 + wn * (BN / WN) + nt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
-      cn[nt][r] = j < k ? cnorm[j] : __builtin_huge_valf();  // +inf: never the best, never a bound
-      g[nt][r] = j < k ? cg[j] : 0.f;
+      cn[r] = j < k ? cnorm[j] : __builtin_huge_valf();  // +inf: never the best, never a bound
+      g[r] = j < k ? cg[j] : 0.f;
     }
+#pragma unroll
+    for (int mt = 0; mt < TM; ++mt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float d = fmaf(dscale, acc[mt][nt][r], cn[r]);
+        const float adj = fmaf(-xs[mt], g[r], d);
+        const int j = col0 + wn * (BN / WN) + nt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        if (d < bv[mt]) { sadj[mt] = fminf(sadj[mt], badj[mt]); bv[mt] = d; bi[mt] = j; badj[mt] = adj; }
+        else sadj[mt] = fminf(sadj[mt], adj);
+      }
+  }
   const int slot = ctile * WN + wn;
 #pragma unroll
   for (int mt = 0; mt < TM; ++mt) {
     const long row = row0 + wm * (BM / WM) + mt * 32 + li;
-    const float xs = row < m ? sqrtf(fmaxf(xnorm[row], 0.f)) + xadd : 0.f;
-    float bv = __builtin_huge_valf(), badj = __builtin_huge_valf(), sadj = __builtin_huge_valf();
-    int bi = 0x7fffffff;
-#pragma unroll
-    for (int nt = 0; nt < TN; ++nt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float d = fmaf(dscale, acc[mt][nt][r], cn[nt][r]);
-        const float adj = fmaf(-xs, g[nt][r], d);
-        const int j = col0 + wn * (BN / WN) + nt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
-        if (d < bv) { sadj = fminf(sadj, badj); bv = d; bi = j; badj = adj; }  // ascending j per lane: ties keep the lower
-        else sadj = fminf(sadj, adj);
-      }
+    float b = bv[mt], ba = badj[mt], sa = sadj[mt];
+    int bj = bi[mt];
     // merge with the other lk half (lane ^ 32: the same row, the other 16 centres of each tile)
-    const float ov = __shfl_xor(bv, 32, 64);
-    const int oi = __shfl_xor(bi, 32, 64);
-    const float oadj = __shfl_xor(badj, 32, 64);
-    const float osadj = __shfl_xor(sadj, 32, 64);
-    if (ov < bv || (ov == bv && oi < bi)) {
-      sadj = fminf(fminf(sadj, badj), osadj);
-      bv = ov;
-      bi = oi;
-      badj = oadj;
+    const float ov = __shfl_xor(b, 32, 64);
+    const int oi = __shfl_xor(bj, 32, 64);
+    const float oadj = __shfl_xor(ba, 32, 64);
+    const float osadj = __shfl_xor(sa, 32, 64);
+    if (ov < b || (ov == b && oi < bj)) {
+      sa = fminf(fminf(sa, ba), osadj);
+      b = ov;
+      bj = oi;
+      ba = oadj;
     } else {
-      sadj = fminf(fminf(sadj, oadj), osadj);
+      sa = fminf(fminf(sa, oadj), osadj);
     }
     if (lk == 0 && row < m) {
       const long o = (long)slot * m + row;
-      const bool none = bi == 0x7fffffff || !(bv < __builtin_huge_valf());
-      keys[o] = none ? ~0ull : (((unsigned long long)orderable(bv) << 32) | (unsigned)bi);
-      lob[o] = sadj;
+      const bool none = bj == 0x7fffffff || !(b < __builtin_huge_valf());
+      keys[o] = none ? ~0ull : (((unsigned long long)orderable(b) << 32) | (unsigned)bj);
+      lob[o] = sa;
     }
   }
 }
@@ -566,8 +579,9 @@ typedef __attribute__((address_space(1))) void* gbl_vptr;
 // tiled image.
 // PRIO: s_setprio(1) / (0) around every MFMA cluster: keeps hipcc from moving MFMAs across the
 // raw barriers into the load phase (cdna_hip_programming.md T5).
-template <bool TILED, int NP = 6, bool TOP2 = false, int WN_ = 4, bool PRIO = false, bool CAND = false, int RING = 0>
-__global__ __launch_bounds__(WN_ * 128, WN_ == 4 ? 1 : 2) void nearest_centroid_split_glds_kernel(
+template <bool TILED, int NP = 6, bool TOP2 = false, int WN_ = 4, bool PRIO = false, bool CAND = false, int RING = 0,
+          int TNW = 2>
+__global__ __launch_bounds__(WN_ * 128, (WN_ == 4 || TNW == 4) ? 1 : 2) void nearest_centroid_split_glds_kernel(
     const unsigned short* __restrict__ XP, long m, long xrows, int kp, const unsigned short* __restrict__ CP, int k,
     long crows, const float* __restrict__ cnorm, unsigned long long* __restrict__ best, int n_ctiles,
     float* __restrict__ lob = nullptr, const float* __restrict__ cg = nullptr, const float* __restrict__ xnorm = nullptr,
@@ -576,7 +590,8 @@ __global__ __launch_bounds__(WN_ * 128, WN_ == 4 ? 1 : 2) void nearest_centroid_
   static_assert(!CAND || (NP == 1 && TOP2), "candidate lists come from the fp16 filter");
   static_assert(WN_ == 4 || (WN_ == 2 && NP != 6), "256 x 128 tiles are built for the filter passes");
   static_assert(NP == 6 || NP == 3 || (NP == 1 && TOP2), "NP = 1 is the fp16 certified filter");
-  constexpr int BM = 256, WM = 2, WN = WN_, BN = 64 * WN, TM = 4, TN = 2;
+  static_assert(TNW == 2 || (TNW == 4 && WN_ == 2 && NP == 1), "128 x 128 wave tiles: the fp16 filter's 4-wave block");
+  constexpr int BM = 256, WM = 2, WN = WN_, BN = 32 * TNW * WN, TM = 4, TN = TNW;
   // planes staged per operand: h, m, l for the 6-product set; the 3-product set (h.h, h.m, m.h)
   // never touches the l planes, so it stages 2 per operand (2/3 of the DMA and LDS traffic)
   constexpr int NPL = NP == 6 ? 3 : (NP == 3 ? 2 : 1);
@@ -591,7 +606,8 @@ __global__ __launch_bounds__(WN_ * 128, WN_ == 4 ? 1 : 2) void nearest_centroid_
   // loads of group g + 2 are issued while group g computes (two groups of HBM-latency cover)
   // RING (fp16 filter probes, SRML_F16_RING): 10 * KPB + NG overrides the defaults below
   constexpr int KPB = RING ? RING / 10 : NP == 1 ? 3 : (NP == 3 && WN_ == 4 ? 2 : 1);  // k steps per barrier
-  constexpr int NG = RING ? RING % 10 : NP == 1 && WN_ == 4 ? 3 : 2;  // groups in the ring (2 x 72 KiB per CU at WN_ = 2)
+  // groups in the ring (2 x 72 KiB per CU for the two-block WN_ = 2 config; 3 x 48 KiB for one block per CU)
+  constexpr int NG = RING ? RING % 10 : NP == 1 && (WN_ == 4 || TNW == 4) ? 3 : 2;
   static_assert(!RING || (NP == 1 && KPB >= 1 && NG >= 2), "ring override is for the fp16 filter");
   constexpr int NS = (KPB > 1 || RING) ? NG * KPB : 3;
   constexpr int STAGE = NPL * (BM + BN) * 16;  // elements: X planes [NPL][BM][16], then C planes [NPL][BN][16]
@@ -1090,12 +1106,26 @@ SRML_API int srml_split_scatter_refined(const unsigned long long* best, const in
 }
 
 // ---- fp16 certified filter -----------------------------------------------------------------
-// Centroid-tile width of the fp16 filter: 256 (256 x 256 tile, one 8-wave block per CU, 3-group
-// ring) or SRML_F16_BN=128 (256 x 128 tiles, two 4-wave blocks per CU, 2-group rings)
-static int f16_bn() {
-  static const int bn = getenv("SRML_F16_BN") && atoi(getenv("SRML_F16_BN")) == 128 ? 128 : 256;
-  return bn;
+// Tile shape of the fp16 filter (SRML_F16_TILE):
+//   "wide" = 256 x 256 tile, 4 waves each 128 x 128 (16 accumulator tiles in the unified register
+//            file, one block per CU, 3-group ring): 8 fragment reads per 16 MFMAs;
+//   "8w"   = 256 x 256 tile, 8 waves each 128 x 64, one block per CU: 6 reads per 8 MFMAs;
+//   "128"  = 256 x 128 tiles, two 4-wave blocks per CU, 2-group rings (also SRML_F16_BN=128).
+enum { F16_8W = 0, F16_128 = 1, F16_WIDE = 2 };
+static int f16_mode() {
+  static const int mode = [] {
+    const char* t = getenv("SRML_F16_TILE");
+    if (t && !strcmp(t, "wide")) return (int)F16_WIDE;
+    if (t && !strcmp(t, "128")) return (int)F16_128;
+    if (t && !strcmp(t, "8w")) return (int)F16_8W;
+    if (getenv("SRML_F16_BN") && atoi(getenv("SRML_F16_BN")) == 128) return (int)F16_128;
+    return (int)F16_8W;
+  }();
+  return mode;
 }
+static int f16_bn() { return f16_mode() == F16_128 ? 128 : 256; }
+// result slots per centroid tile: one per wave column
+static int f16_slots_per_tile() { return f16_mode() == F16_8W ? 4 : 2; }
 
 // One tiled fp16 plane of scale * (x - mu) (mu may be null), rows padded to rows_pad (% 256 == 0):
 // P = [rows_pad / 256][kp / 16][256][16]; *ovf |= 1 if an element of |scale v| >= 2^15 was clamped.
@@ -1138,7 +1168,11 @@ SRML_API int srml_nearest_centroid_f16_top2(const unsigned short* XP, long m, lo
   hipLaunchKernelGGL((nearest_centroid_split_glds_kernel<true, 1, true, 4, true, false, RG>), dim3((unsigned)nb),      \
                      dim3(512), 0, stream, XP, m, xrows, kp, CP, k, crows, cnorm, keys, (int)ct, lob, cg, xnorm,       \
                      dscale, xadd)
-  if (f16_bn() == 128) {
+  if (f16_mode() == F16_WIDE) {
+    hipLaunchKernelGGL((nearest_centroid_split_glds_kernel<true, 1, true, 2, true, false, 0, 4>), dim3((unsigned)nb),
+                       dim3(256), 0, stream, XP, m, xrows, kp, CP, k, crows, cnorm, keys, (int)ct, lob, cg, xnorm,
+                       dscale, xadd);
+  } else if (f16_bn() == 128) {
     if (prio) SRML_F16(2, true, 256);
     else SRML_F16(2, false, 256);
   } else if (ring == 23) {
@@ -1160,10 +1194,10 @@ SRML_API int srml_nearest_centroid_f16_top2(const unsigned short* XP, long m, lo
   return srml_status();
 }
 
-// (row, slot) pairs of the fp16 filter (one slot per 64-wide wave column of each centroid tile)
+// (row, slot) pairs of the fp16 filter (one slot per wave column of each centroid tile)
 SRML_API int srml_nearest_centroid_f16_top2_nslot(int k) {
   const int bn = f16_bn();
-  return ((k + bn - 1) / bn) * (bn / 64);
+  return ((k + bn - 1) / bn) * f16_slots_per_tile();
 }
 
 // phase 2 of the fp16 filter: as srml_split_top2_select with the extra radius terms (see kernel)

@@ -69,6 +69,7 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_qn_step_mb": (_P, _P, _P),
     "srml_qn_step_fused": (_P, _P, _P, _I, _L, _P),
     "srml_qn_step_mbf": (_P, _P, _P, _I, _L, _P),
+    "srml_kmeans_lloyd_small": (_P, _L, _I, _L, _P, _I, _P, _P, _P, _P, _P, _P, _P),
     "srml_qn_fused_scratch": (),
     "srml_qn_mb_scratch": (),
     "srml_kmeanspp_gram": (_P, _I, _L, _P, _I, _I, ctypes.c_ulonglong, _P, _P),

@@ -1,0 +1,30 @@
+"""Two ranks sharing the GPU (gloo process group over cuda:0 tensors, launched by torchrun as the
+north-star script is): the paths a one-rank-per-process job takes that the in-process tests do not —
+each rank's own page-locked shard streamed in (PendingBins streamed root level) under the
+node-partitioned histogram reduce-scatter (the padded node count of round 4's first 2-rank
+north-star failure)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scatter", ["1", "0"])
+def test_rf_data_parallel_two_ranks_streamed_root(tmp_path, scatter):
+    out = tmp_path / "ns.jsonl"
+    env = dict(os.environ, SRML_NS_BACKEND="gloo", SRML_RF_DP_SCATTER=scatter, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(29600 + int(scatter)),
+           os.path.join(ROOT, "tools", "northstar.py"), "--configs", "rf", "--scale", "0.002", "--out", str(out)]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    rec = json.loads(out.read_text().strip().splitlines()[-1])
+    assert "error" not in rec, rec
+    assert rec["n_gpus"] == 2 and rec["split_mode"] == "data_parallel"
+    assert rec["holdout_accuracy"] > 0.85, rec
+    assert all(rk["comm_calls"] > 0 for rk in rec["ranks"]), rec["ranks"]

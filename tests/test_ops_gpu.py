@@ -127,7 +127,8 @@ def test_logreg_binary_loss_grad(gpu_device, m, n):
         torch.testing.assert_close(again, out, rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("m,n,k", [(1000, 16, 20), (3000, 64, 5), (2000, 300, 130), (1024, 3000, 257), (777, 33, 1)])
+@pytest.mark.parametrize("m,n,k", [(1000, 16, 20), (3000, 64, 5), (2000, 300, 130), (1024, 3000, 257), (777, 33, 1),
+                                   (100003, 64, 20), (5001, 100, 33), (12345, 64, 64), (4096, 3, 2)])
 def test_nearest_centroid(gpu_device, m, n, k):
     g = torch.Generator().manual_seed(3)
     C = torch.randn(k, n, generator=g) * 3
@@ -164,7 +165,7 @@ def test_nearest_centroid_split(gpu_device, m, n, k):
 
 
 @pytest.mark.parametrize("m,n,k", [(5000, 16, 20), (20000, 3000, 50), (3000, 64, 200), (5000, 301, 300),
-                                   (70000, 1024, 1000)])
+                                   (70000, 1024, 1000), (100003, 64, 20), (9999, 130, 7), (37, 64, 20)])
 def test_cluster_sums(gpu_device, m, n, k):
     X = _rand(m, n, gpu_device, seed=15)
     labels = torch.randint(0, k, (m,), generator=torch.Generator().manual_seed(4)).int()
@@ -172,6 +173,32 @@ def test_cluster_sums(gpu_device, m, n, k):
     ref = torch.zeros(k, n, dtype=torch.float64).index_add_(0, labels.long(), X.double().cpu())
     torch.testing.assert_close(sums.cpu(), ref, rtol=1e-4, atol=1e-3)
     assert torch.equal(counts.cpu(), torch.bincount(labels.long(), minlength=k))
+
+
+@pytest.mark.parametrize("m,n,k", [(100003, 64, 20), (5000, 4, 1), (777, 16, 5), (20000, 32, 32), (33333, 60, 17),
+                                   (256, 64, 24), (70001, 48, 9)])
+def test_kmeans_lloyd_small_matches_reference(gpu_device, m, n, k):
+    """Fused small-k Lloyd step (one pass: VALU search + one-hot MFMA sums) against fp64: labels
+    are the arg-min up to fp32 near-ties, sums / counts / inertia are those of its own labels."""
+    g = torch.Generator().manual_seed(m + k)
+    C = torch.randn(k, n, generator=g) * 2
+    X = (C[torch.randint(0, k, (m,), generator=g)] + torch.randn(m, n, generator=g)).float()
+    Xd, Cd = X.to(gpu_device), C.float().to(gpu_device)
+    assert ops.lloyd_small_ok(Xd, k)
+    lab, dist, sums, counts, inertia = ops.kmeans_lloyd_small(Xd, Cd)
+    D = torch.cdist(X.double(), C.double()) ** 2
+    ref_d, _ = D.min(1)
+    lab_c = lab.long().cpu()
+    got = D[torch.arange(m), lab_c]
+    assert torch.all(got <= ref_d + 1e-4 * (1 + ref_d))
+    torch.testing.assert_close(dist.double().cpu(), got, rtol=1e-4, atol=1e-3)
+    ref_s = torch.zeros(k, n, dtype=torch.float64).index_add_(0, lab_c, X.double())
+    torch.testing.assert_close(sums.cpu(), ref_s, rtol=1e-5, atol=1e-3)
+    assert torch.equal(counts.cpu(), torch.bincount(lab_c, minlength=k))
+    assert abs(float(inertia.item()) - float(dist.double().sum())) <= 1e-6 * float(dist.double().sum()) + 1e-6
+    # search-only mode (nearest_centroid routes here) gives the same labels
+    l2, _ = ops.nearest_centroid(Xd, Cd)
+    assert torch.equal(l2.cpu(), lab.cpu())
 
 
 def _rf_setup(dev, m=5000, n=40, B=32, C=3, seed=0):
@@ -933,6 +960,29 @@ def test_kmeans_predict_certified_matches_exact(gpu_device, monkeypatch):
     assert got.dtype == torch.int32 and got.shape == (70000,)
     assert (got == ref).float().mean().item() > 0.9999
     assert (got == fp32).float().mean().item() > 0.9999
+
+
+def test_kmeans_predict_streamed_matches(gpu_device):
+    """Transform of a page-locked batch with the H2D streamed under the fp16 certified search
+    (several chunks, each its own plane scale, centred on the centres' mean): the same labels as
+    the one-shot device predict (both are the exact arg-min up to fp32 near-ties) and the fp64 one."""
+    from spark_rapids_ml_nai_amd.models.kmeans import kmeans_predict, kmeans_predict_streamed, predict_streams
+
+    g = np.random.default_rng(6)
+    m, n, k = 70000, 192, 400
+    host = torch.empty((m, n), dtype=torch.float32).pin_memory()
+    host.copy_(torch.from_numpy((g.standard_normal((m, n)) + 2.0).astype(np.float32)))
+    Xh = host.numpy()
+    C = torch.from_numpy(Xh[g.choice(m, k, replace=False)] + 0.1 * g.standard_normal((k, n)).astype(np.float32))
+    assert predict_streams(Xh, k)
+    got = kmeans_predict_streamed(Xh, C, gpu_device, chunk_bytes=9 << 20)  # ~12k-row chunks: 6 of them
+    X = torch.from_numpy(Xh).to(gpu_device)
+    one = kmeans_predict(X, C.to(gpu_device))
+    Xd, Cd = X.double(), C.double().to(gpu_device)
+    ref = ((Xd * Xd).sum(1, keepdim=True) - 2.0 * Xd @ Cd.T + (Cd * Cd).sum(1).view(1, -1)).argmin(1).int()
+    assert got.dtype == torch.int32 and got.shape == (m,)
+    assert (got == ref).float().mean().item() > 0.9999
+    assert (got == one).float().mean().item() > 0.9999
 
 
 @pytest.mark.parametrize("nseg,total", [(1, 5000), (37, 100000), (3000, 2_000_000)])

@@ -28,7 +28,9 @@ import torch.distributed as dist  # noqa: E402
 CONFIGS = {
     # name: (rows, cols, generator)
     "pca": (10_000, 128, "low_rank"),
-    "kmeans": (100_000_000, 64, "blobs"),
+    # uniform rows: 20 blobs would converge exactly (zero centre shift) after 2 iterations, and the
+    # tol-0 config exists to time all 20 Lloyd / centroid-all-reduce iterations
+    "kmeans": (100_000_000, 64, "uniform"),
     "logreg": (200_000_000, 256, "classification"),
     "rf": (50_000_000, 64, "classification"),
     "umap": (20_000_000, 128, "blobs"),
@@ -92,7 +94,16 @@ def _shard(gen: str, m: int, n: int, device, rank: int):
             del Xc, yc
         torch.cuda.empty_cache()
         return Xh.numpy(), (yh if gen == "classification" else None)
-    if gen == "low_rank":
+    if gen == "uniform" and m > step and device.type == "cuda":
+        Xh = torch.empty((m, n), dtype=torch.float32, pin_memory=True)
+        for c, r0 in enumerate(range(0, m, step)):
+            mc = min(step, m - r0)
+            Xh[r0: r0 + mc].copy_(datagen.uniform(mc, n, device, seed=seed * 1000 + c))
+        torch.cuda.empty_cache()
+        return Xh.numpy(), None
+    if gen == "uniform":
+        X = datagen.uniform(m, n, device, seed=seed)
+    elif gen == "low_rank":
         X = datagen.low_rank_matrix(m, n, device, seed=seed)
     elif gen == "blobs":
         X, _ = datagen.blobs(m, n, device, seed=seed, centers=20)
