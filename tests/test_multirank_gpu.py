@@ -28,3 +28,16 @@ def test_rf_data_parallel_two_ranks_streamed_root(tmp_path, scatter):
     assert rec["n_gpus"] == 2 and rec["split_mode"] == "data_parallel"
     assert rec["holdout_accuracy"] > 0.85, rec
     assert all(rk["comm_calls"] > 0 for rk in rec["ranks"]), rec["ranks"]
+
+
+@pytest.mark.gpu
+def test_rf_ensemble_fit_multiple_fewer_trees_than_ranks_streamed():
+    """ADVICE r3 (forest.py pending bins): a param map with numTrees < ranks leaves one rank with no
+    tree; its streamed chunks must still be binned before the next map reuses them."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29611", os.path.join(ROOT, "tools", "rf_pending_check.py")]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert rec["equal"] and rec["trees"] == [1, 4], rec
