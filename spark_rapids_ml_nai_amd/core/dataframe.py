@@ -161,7 +161,15 @@ def _list_offsets_values(arr: pa.Array) -> Tuple[np.ndarray, pa.Array]:
 
 
 def array_column_to_dense(col: Union[pa.ChunkedArray, pa.Array], dtype: Optional[np.dtype] = None) -> np.ndarray:
-    """list<float> column -> (rows, n) ndarray; zero-copy when rows are uniform and dtype matches."""
+    """list<float> column -> (rows, n) ndarray; zero-copy when rows are uniform and dtype matches.
+    A multi-chunk column is converted chunk by chunk and concatenated in numpy: Arrow's
+    ``combine_chunks`` overflows ``list<float>``'s int32 offsets past 2^31 values (a 1M x 3000
+    partition delivered as record batches)."""
+    if isinstance(col, pa.ChunkedArray) and col.num_chunks > 1:
+        parts = [array_column_to_dense(c, dtype) for c in col.chunks if len(c) > 0]
+        if not parts:
+            return np.zeros((0, 0), dtype=dtype or np.float32)
+        return np.concatenate(parts, 0)
     arr = _combine(col)
     m = len(arr)
     if m == 0:
@@ -200,6 +208,10 @@ class ChunkedRows:
 
     def to_numpy(self) -> np.ndarray:
         return np.concatenate(self.parts, 0) if len(self.parts) > 1 else self.parts[0]
+
+    def __array__(self, dtype: Any = None, copy: Any = None) -> np.ndarray:
+        a = self.to_numpy()
+        return a if dtype is None else a.astype(dtype, copy=False)
 
 
 def array_column_chunks(col: Union[pa.ChunkedArray, pa.Array], dtype: Optional[np.dtype] = None) -> ChunkedRows:

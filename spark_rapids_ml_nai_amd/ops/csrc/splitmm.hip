@@ -24,7 +24,6 @@
 //    distinct 4-bank groups), double-buffered with register prefetch so the next k step's
 //    global loads are in flight under the current 24 MFMAs per wave. Grid is 1-D, centroid tile
 //    fastest and XCD-remapped so the blocks sharing one X row tile run on one XCD's L2.
-#include <cstring>
 #include "common.h"
 
 #include "tile.h"
@@ -579,9 +578,8 @@ typedef __attribute__((address_space(1))) void* gbl_vptr;
 // tiled image.
 // PRIO: s_setprio(1) / (0) around every MFMA cluster: keeps hipcc from moving MFMAs across the
 // raw barriers into the load phase (cdna_hip_programming.md T5).
-template <bool TILED, int NP = 6, bool TOP2 = false, int WN_ = 4, bool PRIO = false, bool CAND = false, int RING = 0,
-          int TNW = 2>
-__global__ __launch_bounds__(WN_ * 128, (WN_ == 4 || TNW == 4) ? 1 : 2) void nearest_centroid_split_glds_kernel(
+template <bool TILED, int NP = 6, bool TOP2 = false, int WN_ = 4, bool PRIO = false, bool CAND = false, int RING = 0>
+__global__ __launch_bounds__(WN_ * 128, WN_ == 4 ? 1 : 2) void nearest_centroid_split_glds_kernel(
     const unsigned short* __restrict__ XP, long m, long xrows, int kp, const unsigned short* __restrict__ CP, int k,
     long crows, const float* __restrict__ cnorm, unsigned long long* __restrict__ best, int n_ctiles,
     float* __restrict__ lob = nullptr, const float* __restrict__ cg = nullptr, const float* __restrict__ xnorm = nullptr,
@@ -590,8 +588,10 @@ __global__ __launch_bounds__(WN_ * 128, (WN_ == 4 || TNW == 4) ? 1 : 2) void nea
   static_assert(!CAND || (NP == 1 && TOP2), "candidate lists come from the fp16 filter");
   static_assert(WN_ == 4 || (WN_ == 2 && NP != 6), "256 x 128 tiles are built for the filter passes");
   static_assert(NP == 6 || NP == 3 || (NP == 1 && TOP2), "NP = 1 is the fp16 certified filter");
-  static_assert(TNW == 2 || (TNW == 4 && WN_ == 2 && NP == 1), "128 x 128 wave tiles: the fp16 filter's 4-wave block");
-  constexpr int BM = 256, WM = 2, WN = WN_, BN = 32 * TNW * WN, TM = 4, TN = TNW;
+  // (128 x 128 wave tiles for the fp16 filter — 4 waves of 16 accumulator tiles, 8 fragment reads
+  // per 16 MFMAs — measured 7.8 vs 7.15 ms at 1M x 3000 x 1000: one wave per SIMD exposes every
+  // barrier and DMA wait; the 8-wave 128 x 64 layout stays)
+  constexpr int BM = 256, WM = 2, WN = WN_, BN = 64 * WN, TM = 4, TN = 2;
   // planes staged per operand: h, m, l for the 6-product set; the 3-product set (h.h, h.m, m.h)
   // never touches the l planes, so it stages 2 per operand (2/3 of the DMA and LDS traffic)
   constexpr int NPL = NP == 6 ? 3 : (NP == 3 ? 2 : 1);
@@ -606,8 +606,7 @@ __global__ __launch_bounds__(WN_ * 128, (WN_ == 4 || TNW == 4) ? 1 : 2) void nea
   // loads of group g + 2 are issued while group g computes (two groups of HBM-latency cover)
   // RING (fp16 filter probes, SRML_F16_RING): 10 * KPB + NG overrides the defaults below
   constexpr int KPB = RING ? RING / 10 : NP == 1 ? 3 : (NP == 3 && WN_ == 4 ? 2 : 1);  // k steps per barrier
-  // groups in the ring (2 x 72 KiB per CU for the two-block WN_ = 2 config; 3 x 48 KiB for one block per CU)
-  constexpr int NG = RING ? RING % 10 : NP == 1 && (WN_ == 4 || TNW == 4) ? 3 : 2;
+  constexpr int NG = RING ? RING % 10 : NP == 1 && WN_ == 4 ? 3 : 2;  // groups in the ring (2 x 72 KiB per CU at WN_ = 2)
   static_assert(!RING || (NP == 1 && KPB >= 1 && NG >= 2), "ring override is for the fp16 filter");
   constexpr int NS = (KPB > 1 || RING) ? NG * KPB : 3;
   constexpr int STAGE = NPL * (BM + BN) * 16;  // elements: X planes [NPL][BM][16], then C planes [NPL][BN][16]
@@ -1106,26 +1105,14 @@ SRML_API int srml_split_scatter_refined(const unsigned long long* best, const in
 }
 
 // ---- fp16 certified filter -----------------------------------------------------------------
-// Tile shape of the fp16 filter (SRML_F16_TILE):
-//   "wide" = 256 x 256 tile, 4 waves each 128 x 128 (16 accumulator tiles in the unified register
-//            file, one block per CU, 3-group ring): 8 fragment reads per 16 MFMAs;
-//   "8w"   = 256 x 256 tile, 8 waves each 128 x 64, one block per CU: 6 reads per 8 MFMAs;
-//   "128"  = 256 x 128 tiles, two 4-wave blocks per CU, 2-group rings (also SRML_F16_BN=128).
-enum { F16_8W = 0, F16_128 = 1, F16_WIDE = 2 };
-static int f16_mode() {
-  static const int mode = [] {
-    const char* t = getenv("SRML_F16_TILE");
-    if (t && !strcmp(t, "wide")) return (int)F16_WIDE;
-    if (t && !strcmp(t, "128")) return (int)F16_128;
-    if (t && !strcmp(t, "8w")) return (int)F16_8W;
-    if (getenv("SRML_F16_BN") && atoi(getenv("SRML_F16_BN")) == 128) return (int)F16_128;
-    return (int)F16_8W;
-  }();
-  return mode;
+// Centroid-tile width of the fp16 filter: 256 (256 x 256 tile, one 8-wave block per CU, 3-group
+// ring) or SRML_F16_BN=128 (256 x 128 tiles, two 4-wave blocks per CU, 2-group rings)
+static int f16_bn() {
+  static const int bn = getenv("SRML_F16_BN") && atoi(getenv("SRML_F16_BN")) == 128 ? 128 : 256;
+  return bn;
 }
-static int f16_bn() { return f16_mode() == F16_128 ? 128 : 256; }
-// result slots per centroid tile: one per wave column
-static int f16_slots_per_tile() { return f16_mode() == F16_8W ? 4 : 2; }
+// result slots per centroid tile: one per 64-wide wave column
+static int f16_slots_per_tile() { return f16_bn() / 64; }
 
 // One tiled fp16 plane of scale * (x - mu) (mu may be null), rows padded to rows_pad (% 256 == 0):
 // P = [rows_pad / 256][kp / 16][256][16]; *ovf |= 1 if an element of |scale v| >= 2^15 was clamped.
@@ -1168,11 +1155,7 @@ SRML_API int srml_nearest_centroid_f16_top2(const unsigned short* XP, long m, lo
   hipLaunchKernelGGL((nearest_centroid_split_glds_kernel<true, 1, true, 4, true, false, RG>), dim3((unsigned)nb),      \
                      dim3(512), 0, stream, XP, m, xrows, kp, CP, k, crows, cnorm, keys, (int)ct, lob, cg, xnorm,       \
                      dscale, xadd)
-  if (f16_mode() == F16_WIDE) {
-    hipLaunchKernelGGL((nearest_centroid_split_glds_kernel<true, 1, true, 2, true, false, 0, 4>), dim3((unsigned)nb),
-                       dim3(256), 0, stream, XP, m, xrows, kp, CP, k, crows, cnorm, keys, (int)ct, lob, cg, xnorm,
-                       dscale, xadd);
-  } else if (f16_bn() == 128) {
+  if (f16_bn() == 128) {
     if (prio) SRML_F16(2, true, 256);
     else SRML_F16(2, false, 256);
   } else if (ring == 23) {

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (round 4 measurement; the 128 x 128 variant was dropped after it: see profiles/pmc_kmeans_f16_filter_r4_8w_vs_wide.json)
 # fp16 certified KMeans filter, 128 x 128 wave tiles (SRML_F16_TILE=wide) vs the 8-wave 128 x 64
 # default: certified-search tests under each, kernel time of the filter at 1M x 3000 x 1000, one
 # MFMA-busy PMC pass each, then KMeans fit / transform at 1M rows.
