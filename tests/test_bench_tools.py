@@ -102,6 +102,14 @@ def test_chunked_rows_ingest_matches_contiguous():
     a = LinearRegression().fit(df)
     b = LinearRegression().fit(DataFrame.from_numpy(X, y))
     np.testing.assert_allclose(a.coefficients.toArray(), b.coefficients.toArray(), rtol=1e-6)
+    # transform of the multi-batch partition: per-batch views as well (Arrow's combine_chunks
+    # overflows list<float> offsets past 2^31 values), same predictions as the contiguous frame
+    pa_ = a.transform(df).to_numpy("prediction")
+    pb = a.transform(DataFrame.from_numpy(X, y)).to_numpy("prediction")
+    np.testing.assert_allclose(pa_, pb, rtol=1e-6, atol=1e-6)
+    from spark_rapids_ml_nai_amd.core.dataframe import array_column_to_dense
+
+    np.testing.assert_array_equal(array_column_to_dense(df.column("features"), np.float32), X)
 
 
 def test_sparse_regression_density_curves_and_redundant_columns():
