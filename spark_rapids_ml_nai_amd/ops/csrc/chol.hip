@@ -578,6 +578,9 @@ __global__ __launch_bounds__(1024) void cd_gram_pipe_kernel(const double* __rest
 
 SRML_API int srml_potrf_f64(double* A, int n, long lda, int* info, hipStream_t stream) {
   if (n <= 0) return 0;
+  // diagonal-block kernel: 1 = one wave, readlane broadcasts (64 us per 64 x 64 block); 0 = 256
+  // threads in LDS with two barriers per column. (One wave with the scaled pivot column shared
+  // through LDS broadcast reads measured 115 us: the chain is latency-bound, not readlane-bound.)
   static const int diag_reg = getenv("SRML_POTRF_REG") ? atoi(getenv("SRML_POTRF_REG")) : 1;
   hipError_t err = hipSuccess;
   SRML_TRY(err, hipMemsetAsync(info, 0, sizeof(int), stream));

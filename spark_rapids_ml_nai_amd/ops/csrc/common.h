@@ -14,6 +14,7 @@
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef double doublex2 __attribute__((ext_vector_type(2)));
 typedef double doublex4 __attribute__((ext_vector_type(4)));
 
 static constexpr int kWave = 64;
