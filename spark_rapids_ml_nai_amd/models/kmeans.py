@@ -276,10 +276,9 @@ def kmeans_fit(X: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext, k
             sums_l, counts_l = ops.cluster_sums(X, labels, k)
             last_anchor = n_delta
         elif moved.numel():
-            s_new, c_new = ops.cluster_sums_rows(X, moved, labels.index_select(0, moved), k)
-            s_old, c_old = ops.cluster_sums_rows(X, moved, prev.index_select(0, moved), k)
-            sums_l += s_new - s_old
-            counts_l = counts_l + (c_new - c_old)
+            ds, dc = ops.cluster_delta_sums(X, moved, labels.index_select(0, moved), prev.index_select(0, moved), k)
+            sums_l += ds
+            counts_l = counts_l + dc
             n_delta += 1
         prev = labels
         sums, counts = sums_l, counts_l

@@ -927,6 +927,29 @@ def cluster_sums_rows(X: torch.Tensor, rows: torch.Tensor, labels: torch.Tensor,
     return sums, off[1:] - off[:-1]
 
 
+def cluster_delta_sums(X: torch.Tensor, rows: torch.Tensor, new_lab: torch.Tensor, old_lab: torch.Tensor, k: int
+                       ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Change of the cluster sums / counts when ``rows`` move from ``old_lab`` to ``new_lab``:
+    (sums fp64 [k, n], counts int64 [k]) = those of X[rows] by new_lab minus by old_lab. Device:
+    ONE label sort of both lists (a leaving row enters as ~row and is subtracted by the sorted-sum
+    kernel) instead of two sorted sums and a difference."""
+    if not X.is_cuda or X.dtype != torch.float32 or deterministic():
+        s_new, c_new = cluster_sums_rows(X, rows, new_lab, k)
+        s_old, c_old = cluster_sums_rows(X, rows, old_lab, k)
+        return s_new - s_old, c_new - c_old
+    n = X.shape[1]
+    X = _c(X)
+    r32 = rows.to(torch.int32)
+    lab2 = torch.cat([new_lab.to(torch.int32), old_lab.to(torch.int32)])
+    rows2 = torch.cat([r32, torch.bitwise_not(r32)])
+    perm, off, slab = label_sort(lab2, k)
+    prow = _c(rows2.index_select(0, perm.long()))
+    sums = torch.zeros((k, n), dtype=torch.float64, device=X.device)
+    native.call("srml_kmeans_accumulate_sorted_f32", X.data_ptr(), int(prow.shape[0]), n, X.stride(0),
+                prow.data_ptr(), slab.data_ptr(), sums.data_ptr(), native.stream(X.device))
+    return sums, label_counts(new_lab, k) - label_counts(old_lab, k)
+
+
 # ------------------------------------------------------------------------------------------
 # Random forest primitives
 # ------------------------------------------------------------------------------------------

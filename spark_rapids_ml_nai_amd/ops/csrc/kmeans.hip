@@ -248,13 +248,17 @@ __global__ __launch_bounds__(256) void accumulate_sorted_kernel(const float* __r
     for (int u = 0; u < U; ++u) {
       const int i = i0 + u;
       if (i < cnt) {
-        const float* row = X + (long)s_row[i] * ld + c;
+        // a negative entry ~r SUBTRACTS row r (the Lloyd delta update: moved rows enter their new
+        // cluster and leave their old one in ONE label-sorted list)
+        const int rr = s_row[i];
+        const float sg = rr < 0 ? -1.f : 1.f;
+        const float* row = X + (long)(rr < 0 ? ~rr : rr) * ld + c;
         if constexpr (VW == 4) {
           const float4 q = *reinterpret_cast<const float4*>(row);
-          v[u][0] = q.x; v[u][1] = q.y; v[u][2] = q.z; v[u][3] = q.w;
+          v[u][0] = sg * q.x; v[u][1] = sg * q.y; v[u][2] = sg * q.z; v[u][3] = sg * q.w;
         } else {
 #pragma unroll
-          for (int j = 0; j < VW; ++j) v[u][j] = row[j];
+          for (int j = 0; j < VW; ++j) v[u][j] = sg * row[j];
         }
       }
     }

@@ -1137,6 +1137,21 @@ def test_rf_interleave_record_layout(gpu_device, m, n, rb):
         np.testing.assert_array_equal(got_g, rec[gi])
 
 
+def test_cluster_delta_sums_one_sort(gpu_device):
+    """cluster_delta_sums (one label sort, leaving rows as ~row subtracted) == sums by the new labels
+    minus sums by the old labels of the moved rows."""
+    X = _rand(20000, 301, gpu_device, seed=72)
+    g = torch.Generator().manual_seed(9)
+    rows = torch.randperm(20000, generator=g)[:1500].to(gpu_device)
+    old = torch.randint(0, 50, (1500,), generator=g).to(gpu_device)
+    new = (old + 1 + torch.randint(0, 49, (1500,), generator=g).to(gpu_device)) % 50
+    ds, dc = ops.cluster_delta_sums(X, rows, new, old, 50)
+    Xr = X.double().cpu()[rows.cpu()]
+    ref = torch.zeros(50, 301, dtype=torch.float64).index_add_(0, new.cpu(), Xr).index_add_(0, old.cpu(), -Xr)
+    torch.testing.assert_close(ds.cpu(), ref, rtol=1e-5, atol=1e-4)
+    assert torch.equal(dc.cpu(), torch.bincount(new.cpu(), minlength=50) - torch.bincount(old.cpu(), minlength=50))
+
+
 def test_kmeans_delta_sums_match_full_sums(gpu_device, monkeypatch):
     """Lloyd sums updated from the moved rows only (+x new cluster, -x old) give the same centres
     as recomputing every iteration's sums from all rows."""
