@@ -334,16 +334,18 @@ def kmeans_predict_streamed(host: np.ndarray, C: torch.Tensor, device: torch.dev
     """``kmeans_predict`` of a page-locked host matrix with its H2D streamed under the search
     (reference transform: ``clustering.py:493-499``, one cuML predict per batch): the rows cross
     PCIe in ~256 MB chunks on the copy stream (``ops.ingest.StreamedRows``) while the certified
-    fp16 filter labels the chunks already on the device, so the transform costs about its H2D.
+    fp16 filter labels the chunks already on the device, so the transform costs about its H2D
+    (``ops.ingest.RingRows``: three chunk buffers reused, not a device copy of the whole batch).
 
     Each chunk is centred on the centres' mean (the filter's operands are x - mu and c - mu; any
     mu keeps the labels exact, it only conditions the fp16 plane) with its own plane scale. Chunks
     the fp16 filter cannot take (no finite range) use ``kmeans_predict``."""
-    from ..ops.ingest import StreamedRows
+    from ..ops.ingest import RingRows
 
     if chunk_bytes <= 0:
         chunk_bytes = int(os.environ.get("SRML_PREDICT_CHUNK_MB", "256")) << 20
-    S = StreamedRows(host, device, torch.float32, chunk_bytes=chunk_bytes)
+    # a ring of three chunk buffers: ~0.75 GB of HBM whatever the batch size, no 12 GB allocation
+    S = RingRows(host, device, torch.float32, chunk_bytes=chunk_bytes, depth=3)
     Cf = C.float().to(device)
     mu = Cf.mean(0)
     labels = torch.empty(host.shape[0], dtype=torch.int32, device=device)

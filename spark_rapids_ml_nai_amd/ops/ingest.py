@@ -399,6 +399,70 @@ class StreamedRows:
         return _stall_seconds(self._stalls)
 
 
+class RingRows:
+    """Row chunks of a page-locked host matrix through a ring of ``depth`` device buffers (a
+    transform that consumes each chunk once: ~depth x chunk bytes of HBM instead of the whole
+    matrix, and no large allocation per call). The copy of chunk c + depth - 1 is queued on the
+    copy stream as soon as chunk c - 1 (the previous user of its buffer) is consumed, so up to
+    depth - 1 chunks cross PCIe while the current one is processed. Iterate ``chunks()``: each
+    yields (r0, r1, device view) valid until the next step of the iteration."""
+
+    def __init__(self, host: np.ndarray, device: torch.device, dtype: Optional[torch.dtype] = None,
+                 chunk_bytes: int = 256 << 20, depth: int = 3) -> None:
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore", UserWarning)
+            t = torch.from_numpy(np.ascontiguousarray(host))
+        if not t.is_pinned():
+            raise ValueError("RingRows needs a page-locked source")
+        if dtype is not None and t.dtype != dtype:
+            raise ValueError("RingRows copies without a cast: the source must already be %s" % dtype)
+        self.host, self.device = t, device
+        m = t.shape[0]
+        row_bytes = max(1, t[0].numel() * t.element_size()) if m else 1
+        self.chunk_rows = max(256, int(chunk_bytes // row_bytes))
+        self.bounds = [(r0, min(m, r0 + self.chunk_rows)) for r0 in range(0, m, self.chunk_rows)]
+        self.depth = max(2, int(depth))
+        nb = min(self.depth, len(self.bounds))
+        self.bufs = [torch.empty((self.chunk_rows,) + tuple(t.shape[1:]), dtype=t.dtype, device=device)
+                     for _ in range(nb)]
+        self._copy = copy_stream(device)
+        self._stalls: list = []
+
+    def chunks(self) -> Iterator[Any]:
+        cur = torch.cuda.current_stream(self.device)
+        ready: list = [None] * len(self.bounds)
+        done: list = [None] * len(self.bounds)
+        nb = len(self.bufs)
+
+        def issue(c: int) -> None:
+            r0, r1 = self.bounds[c]
+            if c >= nb:  # the buffer's previous chunk must be consumed first
+                self._copy.wait_event(done[c - nb])
+            else:
+                self._copy.wait_stream(cur)
+            with torch.cuda.stream(self._copy):
+                self.bufs[c % nb][: r1 - r0].copy_(self.host[r0:r1], non_blocking=True)
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record(self._copy)
+            ready[c] = ev
+
+        for c in range(nb):  # every buffer's first chunk
+            issue(c)
+        for c, (r0, r1) in enumerate(self.bounds):
+            if c >= 1 and c + nb - 1 < len(self.bounds):
+                issue(c + nb - 1)  # into chunk c - 1's buffer: chunk c - 1 was consumed below
+            _timed_wait(cur, ready[c], self._stalls)
+            buf = self.bufs[c % nb]
+            buf.record_stream(cur)
+            yield r0, r1, buf[: r1 - r0]
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            done[c] = ev
+
+    def exposed_seconds(self) -> float:
+        return _stall_seconds(self._stalls)
+
+
 def is_pinned(a: Any) -> bool:
     """Whether a numpy array's memory is page-locked (registered with the HIP runtime)."""
     if not isinstance(a, np.ndarray) or not torch.cuda.is_available():

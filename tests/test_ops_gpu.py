@@ -962,6 +962,23 @@ def test_kmeans_predict_certified_matches_exact(gpu_device, monkeypatch):
     assert (got == fp32).float().mean().item() > 0.9999
 
 
+def test_ring_rows_chunks_match_host(gpu_device):
+    """RingRows: every chunk seen through the 3-buffer ring equals its host rows, also when the
+    consumer enqueues work that reads the chunk after the next copies were queued."""
+    from spark_rapids_ml_nai_amd.ops.ingest import RingRows
+
+    host = torch.empty((10007, 96), dtype=torch.float32).pin_memory()
+    host.copy_(torch.randn(10007, 96))
+    R = RingRows(host.numpy(), gpu_device, torch.float32, chunk_bytes=96 * 4 * 700, depth=3)
+    assert len(R.bounds) == 15 and len(R.bufs) == 3
+    sums = []
+    for r0, r1, Xc in R.chunks():
+        sums.append((r0, r1, (Xc.double() * 1.5).sum(1)))  # queued on the compute stream
+    torch.cuda.synchronize()
+    for r0, r1, s in sums:
+        torch.testing.assert_close(s.cpu(), host[r0:r1].double().sum(1) * 1.5)
+
+
 def test_kmeans_predict_streamed_matches(gpu_device):
     """Transform of a page-locked batch with the H2D streamed under the fp16 certified search
     (several chunks, each its own plane scale, centred on the centres' mean): the same labels as
