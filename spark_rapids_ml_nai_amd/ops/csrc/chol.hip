@@ -187,13 +187,23 @@ __global__ __launch_bounds__(1024) void potrs_blocked_kernel(const double* __res
   // forward: L z = b (skipped when b already holds z: the augmented factorisation computed it)
   for (int j0 = 0; j0 < (backward_only ? 0 : n); j0 += TS_B) {
     const int nb = n - j0 < TS_B ? n - j0 : TS_B;
-    // x[j0 + r] -= L[j0 + r, 0:j0] . x[0:j0]: wave w takes rows r = w, w + 16, ...
+    // x[j0 + r] -= L[j0 + r, 0:j0] . x[0:j0]: wave w takes rows r = w, w + 16, ...; 8 loads in
+    // flight per lane (a dependent load per 64 columns left the sweep latency-bound)
     for (int r = wid; r < nb; r += 16) {
       const double* row = L + (long)(j0 + r) * lda;
-      double s = 0.0;
-      for (int c = lane; c < j0; c += 64) s = fma(row[c], x[c], s);
-      s = wave_sum(s);
-      if (lane == 0) x[j0 + r] -= s;
+      double s[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+      int c = lane;
+      for (; c + 7 * 64 < j0; c += 8 * 64) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = row[c + 64 * u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s[u] = fma(v[u], x[c + 64 * u], s[u]);
+      }
+      for (; c < j0; c += 64) s[0] = fma(row[c], x[c], s[0]);
+      double t8 = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+      t8 = wave_sum(t8);
+      if (lane == 0) x[j0 + r] -= t8;
     }
     for (int e = t; e < nb * nb; e += blockDim.x) {
       const int r = e / nb, c = e - r * nb;
@@ -217,10 +227,21 @@ __global__ __launch_bounds__(1024) void potrs_blocked_kernel(const double* __res
     const int nb = n - j0 < TS_B ? n - j0 : TS_B;
     // x[j0 + i] -= sum_{j >= j0 + nb} L[j][j0 + i] x[j]: lane = column i, waves split the rows j
     {
-      double s = 0.0;
-      if (lane < nb)
-        for (int j = j0 + nb + wid; j < n; j += 16) s = fma(L[(long)j * lda + j0 + lane], x[j], s);
-      part[wid][lane] = s;
+      // 8 rows in flight per lane: one dependent 512-B row load per iteration ran the backward
+      // sweep at ~23 GB/s (1.55 ms at n = 3000)
+      double s[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+      if (lane < nb) {
+        int j = j0 + nb + wid;
+        for (; j + 7 * 16 < n; j += 8 * 16) {
+          double v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = L[(long)(j + 16 * u) * lda + j0 + lane];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) s[u] = fma(v[u], x[j + 16 * u], s[u]);
+        }
+        for (; j < n; j += 16) s[0] = fma(L[(long)j * lda + j0 + lane], x[j], s[0]);
+      }
+      part[wid][lane] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
     }
     for (int e = t; e < nb * nb; e += blockDim.x) {
       const int r = e / nb, c = e - r * nb;
