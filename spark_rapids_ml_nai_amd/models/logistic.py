@@ -22,6 +22,8 @@ with q = sigma (standardization=True) or 1, intercepts unpenalised.
 """
 from __future__ import annotations
 
+import os
+
 from typing import Any, Dict, List, Optional, Tuple
 
 import numpy as np
@@ -126,12 +128,24 @@ def logistic_fit(X: Any, y: torch.Tensor, m_total: int, ctx: WorkerContext, reg:
         def evaluate_partials(w: torch.Tensor, b: torch.Tensor, flag: Optional[torch.Tensor]) -> None:
             ops.logistic_loss_grad(X, y32, w, b, K, _scratch, flag, ws=ws, leave_partials=True)
     # stream-ordered device evaluations (no host sync; allocations come from the graph's pool) may
-    # be replayed from a HIP graph
-    graph_safe = path in ("fused_binary_f32", "fused_multinomial_f32", "csr_binary", "two_pass_multinomial_f32",
-                          "two_pass_binary_f32") or path.startswith("lds_binary")
+    # be replayed from a HIP graph — when launches are what the batch costs: a graph is captured
+    # and instantiated per fit (5.4 ms at the 125k x 3000 shard), while an evaluation reading more
+    # than GRAPH_MAX_BYTES of X runs far longer than its five launches take to issue
+    graph_safe = (path in ("fused_binary_f32", "fused_multinomial_f32", "csr_binary", "two_pass_multinomial_f32",
+                           "two_pass_binary_f32") or path.startswith("lds_binary")) and _eval_bytes(X) <= GRAPH_MAX_BYTES
     res = minimize(P, theta0, evaluate, allreduce, y.device, batch=8 if not path.startswith("torch") else 2,
                    graph_safe=graph_safe, fold=fold, evaluate_partials=evaluate_partials)
     return _result(res, base, ctx, n, K, fit_intercept, inv_sigma, path)
+
+
+GRAPH_MAX_BYTES = int(os.environ.get("SRML_QN_GRAPH_MAX_MB", "64")) << 20
+
+
+def _eval_bytes(X: Any) -> int:
+    """Bytes of X one loss/gradient evaluation streams (dense values, or CSR values + indices)."""
+    if hasattr(X, "data") and hasattr(X, "indices") and not isinstance(X, torch.Tensor):
+        return int(X.data.numel() * X.data.element_size() + X.indices.numel() * X.indices.element_size())
+    return int(X.numel() * X.element_size())
 
 
 MAX_BATCH = 12  # models per fused multi-model pass (register-resident weights, like the multinomial pass)
