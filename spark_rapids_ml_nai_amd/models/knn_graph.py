@@ -113,8 +113,13 @@ def balanced_tile_range(tile_q0: torch.Tensor, tile_list: torch.Tensor, off: tor
 
 
 def knn_graph_ivf(X: torch.Tensor, k: int, nlist: Optional[int] = None, nprobe: Optional[int] = None,
-                  seed: int = 0, ctx: Any = None) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Approximate all-points graph: (euclidean distances [N, k], indices [N, k] int64)."""
+                  seed: int = 0, ctx: Any = None, list_order: bool = False) -> Any:
+    """Approximate all-points graph: (euclidean distances [N, k], indices [N, k] int64).
+
+    ``list_order=True`` returns ``(dist, idx, order)`` with the graph left in inverted-list order:
+    row i of the graph is original row ``order[i]`` and the indices are list-order positions.
+    Rows of one list are neighbours in space, so consumers that gather neighbour rows (the
+    spectral SpMM, the layout epochs) read mostly-local memory instead of random rows."""
     N = X.shape[0]
     nlist = int(nlist) if nlist else max(1, int(round(N / IVF_LIST_ROWS)))
     nlist = max(1, min(nlist, N))
@@ -144,6 +149,11 @@ def knn_graph_ivf(X: torch.Tensor, k: int, nlist: Optional[int] = None, nprobe: 
     del od, oi
     d2 = gather_rows(d2, ctx)
     pos = gather_rows(pos, ctx)
+    if list_order:
+        fin = torch.isfinite(d2)
+        rowmax = torch.where(fin, d2, torch.zeros_like(d2)).max(1, keepdim=True).values
+        d2 = torch.where(fin, d2, rowmax)
+        return torch.sqrt(d2.clamp_min(0)), torch.where(pos >= 0, pos, torch.full_like(pos, -1)), order
     # back to the original row order; missing neighbours (tiny lists) -> -1 at the row's max distance
     idx = torch.where(pos >= 0, order[pos.clamp_min(0)], torch.full_like(pos, -1))
     fin = torch.isfinite(d2)
@@ -157,13 +167,17 @@ def knn_graph_ivf(X: torch.Tensor, k: int, nlist: Optional[int] = None, nprobe: 
 
 
 def build_knn_graph(X: torch.Tensor, k: int, build_algo: str = "auto", build_kwds: Optional[dict] = None,
-                    seed: int = 0, ctx: Any = None) -> Tuple[torch.Tensor, torch.Tensor]:
+                    seed: int = 0, ctx: Any = None, list_order: bool = False) -> Any:
+    """(dist, idx); with ``list_order`` (dist, idx, order) where ``order`` is None unless the
+    builder left the graph in a locality order (see ``knn_graph_ivf``)."""
     algo = (build_algo or "auto").lower()
     if algo == "auto":
         algo = "brute_force_knn" if X.shape[0] <= BRUTE_MAX_ROWS else "ivf"
     kw = dict(build_kwds or {})
     if algo in ("brute_force_knn", "brute", "exact"):
-        return knn_graph_brute(X, k, ctx)
+        d, i = knn_graph_brute(X, k, ctx)
+        return (d, i, None) if list_order else (d, i)
     if algo in ("ivf", "ivfflat", "ivf_flat", "nn_descent"):
-        return knn_graph_ivf(X, k, nlist=kw.get("nlist"), nprobe=kw.get("nprobe"), seed=seed, ctx=ctx)
+        return knn_graph_ivf(X, k, nlist=kw.get("nlist"), nprobe=kw.get("nprobe"), seed=seed, ctx=ctx,
+                             list_order=list_order)
     raise ValueError("Unsupported build_algo %r (auto, brute_force_knn, ivf)" % build_algo)

@@ -22,6 +22,7 @@ Semantics follow umap-learn / cuML UMAP (what the reference calls on one GPU, ``
 from __future__ import annotations
 
 import math
+import os
 from typing import Any, Dict, Optional, Tuple
 
 import numpy as np
@@ -31,6 +32,9 @@ from .. import ops
 
 SMOOTH_K_TOLERANCE = 1e-5
 MIN_K_DIST_SCALE = 1e-3
+# IVF-built graphs stay in inverted-list order through the fuzzy set, spectral init and epochs
+# (neighbour gathers become mostly local); the embedding is scattered back to row order at the end
+LIST_ORDER = os.environ.get("SRML_UMAP_LIST_ORDER", "1") != "0"
 SPECTRAL_DENSE_N = 2048  # device Jacobi on the dense normalised adjacency up to this many vertices
 
 
@@ -373,13 +377,16 @@ def umap_fit(X: torch.Tensor, params: Dict[str, Any], y: Optional[torch.Tensor] 
     elif metric not in ("euclidean", "l2", "sqeuclidean"):
         raise ValueError("Unsupported UMAP metric %r" % metric)
     pre = params.get("precomputed_knn")
+    order = None  # graph row i is original row order[i] (IVF list order), None: original order
     if pre is not None:
         idx = torch.as_tensor(np.asarray(pre[0]), dtype=torch.int64, device=X.device)[:, :k]
         dist = torch.as_tensor(np.asarray(pre[1]), dtype=torch.float32, device=X.device)[:, :k]
     else:
         from .knn_graph import build_knn_graph
 
-        dist, idx = build_knn_graph(Xf, k, params.get("build_algo", "auto"), params.get("build_kwds"), seed, ctx)
+        g = build_knn_graph(Xf, k, params.get("build_algo", "auto"), params.get("build_kwds"), seed, ctx,
+                            list_order=LIST_ORDER)
+        dist, idx, order = g if LIST_ORDER else (g[0], g[1], None)
         if metric in ("cosine", "correlation"):
             dist = 0.5 * dist * dist  # 1 - cos for unit rows
         elif metric == "sqeuclidean":
@@ -398,6 +405,8 @@ def umap_fit(X: torch.Tensor, params: Dict[str, Any], y: Optional[torch.Tensor] 
         rows, cols, vals = fuzzy_union(rows, cols.clamp_min(0), w.reshape(-1), N, mix)
     if y is not None:
         yy = y.to(X.device).long().view(-1)
+        if order is not None:
+            yy = yy[order]
         rows, cols, vals = categorical_intersection(rows, cols, vals, yy, N)
     n_epochs = params.get("n_epochs")
     n_epochs = int(n_epochs) if n_epochs else _n_epochs_default(N)
@@ -417,6 +426,10 @@ def umap_fit(X: torch.Tensor, params: Dict[str, Any], y: Optional[torch.Tensor] 
     optimize_layout(emb, emb, rows, cols, vals, n_epochs, a, b, float(params.get("repulsion_strength", 1.0)),
                     float(params.get("learning_rate", 1.0)), float(params.get("negative_sample_rate", 5)), True, seed,
                     ctx=dist_ctx)
+    if order is not None:
+        out = torch.empty_like(emb)
+        out[order] = emb
+        emb = out
     return emb.cpu().numpy()
 
 

@@ -76,3 +76,24 @@ def test_umap_device_fit_trustworthiness(gpu_device, n):
         X, _ = make_blobs(n, 20, centers=10, cluster_std=3.0, random_state=4)
     emb = U.umap_fit(torch.from_numpy(X).float().to(gpu_device), {"n_neighbors": 15, "random_state": 1})
     assert trustworthiness(X, emb, n_neighbors=15) > 0.9
+
+
+@pytest.mark.parametrize("supervised", [False, True])
+def test_umap_ivf_list_order_matches_row_order(gpu_device, supervised, monkeypatch):
+    """IVF graphs run the fuzzy set / spectral init / epochs in inverted-list order and scatter
+    the embedding back: quality must match the row-order pipeline and rows must map back to
+    their own points (checked through trustworthiness against the ORIGINAL row order)."""
+    from sklearn.datasets import make_blobs
+    from sklearn.manifold import trustworthiness
+
+    X, y = make_blobs(12000, 16, centers=12, cluster_std=2.5, random_state=3)
+    Xt = torch.from_numpy(X).float().to(gpu_device)
+    params = {"n_neighbors": 15, "random_state": 2, "build_algo": "ivf", "n_epochs": 150,
+              "build_kwds": {"nlist": 24, "nprobe": 8}}
+    yt = torch.from_numpy(y).to(gpu_device) if supervised else None
+    tw = {}
+    for flag in (True, False):
+        monkeypatch.setattr(U, "LIST_ORDER", flag)
+        emb = U.umap_fit(Xt, params, y=yt)
+        tw[flag] = trustworthiness(X, emb, n_neighbors=15)
+    assert tw[True] > 0.9 and tw[True] > tw[False] - 0.01, tw
