@@ -35,6 +35,9 @@ MIN_K_DIST_SCALE = 1e-3
 # IVF-built graphs stay in inverted-list order through the fuzzy set, spectral init and epochs
 # (neighbour gathers become mostly local); the embedding is scattered back to row order at the end
 LIST_ORDER = os.environ.get("SRML_UMAP_LIST_ORDER", "1") != "0"
+# fit epochs on the symmetric fuzzy graph move heads only (ops.umap_epoch pull=True): each pair's
+# two directed edges apply its attraction to both ends, without scattered tail atomics
+PULL = os.environ.get("SRML_UMAP_PULL", "1") != "0"
 SPECTRAL_DENSE_N = 2048  # device Jacobi on the dense normalised adjacency up to this many vertices
 
 
@@ -307,7 +310,8 @@ def make_epochs_per_sample(w: torch.Tensor, n_epochs: int) -> torch.Tensor:
 
 def optimize_layout(emb_head: torch.Tensor, emb_tail: torch.Tensor, head: torch.Tensor, tail: torch.Tensor,
                     w: torch.Tensor, n_epochs: int, a: float, b: float, gamma: float, initial_alpha: float,
-                    negative_sample_rate: float, move_other: bool, seed: int, ctx: Any = None) -> torch.Tensor:
+                    negative_sample_rate: float, move_other: bool, seed: int, ctx: Any = None,
+                    pull: bool = False) -> torch.Tensor:
     """SGD epochs over the fuzzy-graph edges.
 
     Distributed (``ctx.world_size > 1``, identical graph and layout on every rank): rank r
@@ -334,7 +338,7 @@ def optimize_layout(emb_head: torch.Tensor, emb_tail: torch.Tensor, head: torch.
         alpha = initial_alpha * (1.0 - float(n) / float(n_epochs))
         before = (emb_head.clone(), None if same or not move_other else emb_tail.clone()) if world > 1 else None
         ops.umap_epoch(head, tail, eps, next_sample, next_neg, eps_neg, emb_head, emb_tail, a, b, gamma, alpha, n,
-                       move_other, seed)
+                       move_other, seed, pull=pull)
         if before is not None:
             for cur, old in ((emb_head, before[0]), (emb_tail, before[1])):
                 if old is None:
@@ -425,7 +429,7 @@ def umap_fit(X: torch.Tensor, params: Dict[str, Any], y: Optional[torch.Tensor] 
         emb = dist_ctx.comm.broadcast(emb, 0)
     optimize_layout(emb, emb, rows, cols, vals, n_epochs, a, b, float(params.get("repulsion_strength", 1.0)),
                     float(params.get("learning_rate", 1.0)), float(params.get("negative_sample_rate", 5)), True, seed,
-                    ctx=dist_ctx)
+                    ctx=dist_ctx, pull=PULL)
     if order is not None:
         out = torch.empty_like(emb)
         out[order] = emb

@@ -1935,15 +1935,20 @@ def umap_fuzzy_union_knn(idx: torch.Tensor, w: torch.Tensor, mix: float = 1.0
 
 def umap_epoch(head: torch.Tensor, tail: torch.Tensor, eps: torch.Tensor, next_sample: torch.Tensor,
                next_neg: torch.Tensor, eps_neg: torch.Tensor, emb_head: torch.Tensor, emb_tail: torch.Tensor,
-               a: float, b: float, gamma: float, alpha: float, epoch: int, move_other: bool, seed: int) -> None:
-    """In-place epoch ``epoch`` of umap-learn's optimize_layout_euclidean (edge-parallel)."""
+               a: float, b: float, gamma: float, alpha: float, epoch: int, move_other: bool, seed: int,
+               pull: bool = False) -> None:
+    """In-place epoch ``epoch`` of umap-learn's optimize_layout_euclidean (edge-parallel).
+
+    ``pull=True`` (symmetric edge lists only: every (j, k) has its (k, j) of equal weight) moves
+    heads only and applies each edge's attraction twice — the same expected update as moving
+    both ends, without scattered tail writes (see umap.hip)."""
     n_tail = emb_tail.shape[0]
     dim = emb_head.shape[1]
     if emb_head.is_cuda:
         native.call("srml_umap_epoch", head.data_ptr(), tail.data_ptr(), head.shape[0], eps.data_ptr(),
                     next_sample.data_ptr(), next_neg.data_ptr(), eps_neg.data_ptr(), emb_head.data_ptr(),
                     emb_tail.data_ptr(), n_tail, dim, float(a), float(b), float(gamma), float(alpha), float(epoch),
-                    int(bool(move_other)), int(seed) & 0xFFFFFFFF, native.stream(emb_head.device))
+                    int(bool(move_other)), int(bool(pull)), int(seed) & 0xFFFFFFFF, native.stream(emb_head.device))
         return
     # CPU reference: all due edges of the epoch update from one snapshot (synchronous Hogwild)
     ep = float(epoch)
@@ -1957,13 +1962,13 @@ def umap_epoch(head: torch.Tensor, tail: torch.Tensor, eps: torch.Tensor, next_s
     pb = d2.clamp_min(1e-30) ** b
     coef = torch.where(d2 > 0, (-2.0 * a * b * pb / d2.clamp_min(1e-30)) / (a * pb + 1.0), torch.zeros_like(d2))
     g = (coef * diff).clamp(-4, 4) * alpha
-    cur = cur + g
+    cur = cur + (2.0 * g if pull else g)
     next_sample[idx] += eps[idx]
     en = eps_neg[idx]
     n_neg = torch.where(en > 0, torch.floor((ep - next_neg[idx]) / en.clamp_min(1e-30)), torch.zeros_like(en))
     n_neg = n_neg.clamp_min(0).long()
     rep = torch.repeat_interleave(torch.arange(idx.numel()), n_neg)
-    delta = g
+    delta = 2.0 * g if pull else g
     if rep.numel():
         gen = torch.Generator().manual_seed((int(seed) * 1000003 + int(epoch)) & 0x7FFFFFFF)
         kk = torch.randint(0, n_tail, (rep.numel(),), generator=gen)
@@ -1976,7 +1981,7 @@ def umap_epoch(head: torch.Tensor, tail: torch.Tensor, eps: torch.Tensor, next_s
         gn = torch.where(skip, torch.zeros_like(gn), gn) * alpha
         delta = delta + torch.zeros_like(g).index_add_(0, rep, gn)
     next_neg[idx] += n_neg.float() * en
-    if move_other:
+    if move_other and not pull:
         emb_tail.index_add_(0, k, -g)
     emb_head.index_add_(0, j, delta)
 

@@ -5,9 +5,13 @@
 // embedding rows. A sampled edge pulls head and (when move_other) tail together; then it draws
 // its due number of negative samples from a counter-based hash RNG (seed, epoch, edge, draw) and
 // pushes the head away from them. The head row is kept in registers across the whole edge update
-// (attraction + all repulsions) and committed with one atomicAdd per coordinate, the tail
-// update is an atomicAdd too (Hogwild-style like the CPU/GPU references, but without lost
-// updates). Gradients are clipped to [-4, 4] as in umap-learn.
+// (attraction + all repulsions); the per-edge head deltas of one run of equal heads in a wave are
+// summed by a segmented shuffle scan and committed ONCE by the run's first lane. Float atomics
+// execute at the memory side (~17x slower for one-row-per-lane shapes, worse under contention),
+// so the "pull" form of a symmetric graph (fit: fuzzy union = A + A^T - A.A^T has both
+// directions of every pair) moves heads only, with the pair's two attraction halves applied by
+// its two directed edges: no tail atomics, and a run that starts and ends inside its wave is
+// committed with a plain store. Gradients are clipped to [-4, 4] as in umap-learn.
 //
 // Fuzzy simplicial set of a kNN graph (umap-learn smooth_knn_dist / compute_membership_strengths
 // / fuzzy union; cuML UMAP's fuzzy_simplicial_set):
@@ -41,73 +45,128 @@ __global__ __launch_bounds__(256) void umap_epoch_kernel(
     const int* __restrict__ head, const int* __restrict__ tail, long n_edges, const float* __restrict__ eps,
     float* __restrict__ next_sample, float* __restrict__ next_neg, const float* __restrict__ eps_neg,
     float* __restrict__ emb_head, float* __restrict__ emb_tail, int n_tail_vertices, int dim, float a, float b,
-    float gamma, float alpha, float epoch, int move_other, unsigned seed) {
+    float gamma, float alpha, float epoch, int move_other, int pull, unsigned seed) {
   constexpr int DM = D > 0 ? D : 32;
+  const int lane = threadIdx.x & 63;
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n_edges) return;
-  const float eps_e = eps[e];
-  if (eps_e <= 0.f || next_sample[e] > epoch) return;
+  const bool in = e < n_edges;
+  const float eps_e = in ? eps[e] : 0.f;
+  const bool act = eps_e > 0.f && next_sample[in ? e : 0] <= epoch;
+  if (__ballot(act) == 0ull) return;  // whole wave idle this epoch (uniform exit: no lane left behind)
   const int dd = D > 0 ? D : dim;
-  const int j = head[e], k = tail[e];
+  const int j = in ? head[e] : -1;
+  float* hj = emb_head + (long)(j < 0 ? 0 : j) * dd;
   float cur[DM], orig[DM];
-  float* hj = emb_head + (long)j * dd;
-  float* tk = emb_tail + (long)k * dd;
-  float dist2 = 0.f;
 #pragma unroll
-  for (int d = 0; d < DM; ++d) {
-    if (d < dd) {
-      cur[d] = hj[d];
-      orig[d] = cur[d];
-      const float diff = cur[d] - tk[d];
-      dist2 = fmaf(diff, diff, dist2);
-    }
-  }
-  float coef = 0.f;
-  if (dist2 > 0.f) {
-    const float pb = __powf(dist2, b);
-    coef = (-2.f * a * b * pb / dist2) / (a * pb + 1.f);
-  }
-#pragma unroll
-  for (int d = 0; d < DM; ++d) {
-    if (d < dd) {
-      const float g = clip4(coef * (cur[d] - tk[d]));
-      cur[d] += g * alpha;
-      if (move_other) atomicAdd(&tk[d], -g * alpha);
-    }
-  }
-  next_sample[e] += eps_e;
-  const float en = eps_neg[e];
-  const int n_neg = en > 0.f ? (int)((epoch - next_neg[e]) / en) : 0;
-  for (int p = 0; p < n_neg; ++p) {
-    const int kk = (int)(hash3(seed ^ (unsigned)e, (unsigned)epoch, (unsigned)p + 0x51ED27u * (unsigned)(e >> 32)) %
-                         (unsigned)n_tail_vertices);
-    const float* tn = emb_tail + (long)kk * dd;
-    float d2 = 0.f;
+  for (int d = 0; d < DM; ++d) cur[d] = orig[d] = 0.f;
+  if (act) {
+    const int k = tail[e];
+    float* tk = emb_tail + (long)k * dd;
+    float dist2 = 0.f;
 #pragma unroll
     for (int d = 0; d < DM; ++d) {
       if (d < dd) {
-        const float diff = cur[d] - tn[d];
-        d2 = fmaf(diff, diff, d2);
+        cur[d] = hj[d];
+        orig[d] = cur[d];
+        const float diff = cur[d] - tk[d];
+        dist2 = fmaf(diff, diff, dist2);
       }
     }
-    float c = 0.f;
-    if (d2 > 0.f) {
-      c = 2.f * gamma * b / ((0.001f + d2) * (a * __powf(d2, b) + 1.f));
-    } else if (j == kk) {
-      continue;
+    float coef = 0.f;
+    if (dist2 > 0.f) {
+      const float pb = __powf(dist2, b);
+      coef = (-2.f * a * b * pb / dist2) / (a * pb + 1.f);
     }
+    // pull: the graph holds both directions of every pair, so the reverse edge moves the tail
+    // and the head takes both halves of the pair's attraction here (no tail writes at all)
+    const float ascale = pull ? 2.f * alpha : alpha;
 #pragma unroll
     for (int d = 0; d < DM; ++d) {
       if (d < dd) {
-        const float g = c > 0.f ? clip4(c * (cur[d] - tn[d])) : 4.f;
-        cur[d] += g * alpha;
+        const float g = clip4(coef * (cur[d] - tk[d]));
+        cur[d] += g * ascale;
+        if (move_other && !pull) atomicAdd(&tk[d], -g * alpha);
+      }
+    }
+    next_sample[e] += eps_e;
+    const float en = eps_neg[e];
+    const int n_neg = en > 0.f ? (int)((epoch - next_neg[e]) / en) : 0;
+    for (int p = 0; p < n_neg; ++p) {
+      const int kk = (int)(hash3(seed ^ (unsigned)e, (unsigned)epoch, (unsigned)p + 0x51ED27u * (unsigned)(e >> 32)) %
+                           (unsigned)n_tail_vertices);
+      const float* tn = emb_tail + (long)kk * dd;
+      float d2 = 0.f;
+#pragma unroll
+      for (int d = 0; d < DM; ++d) {
+        if (d < dd) {
+          const float diff = cur[d] - tn[d];
+          d2 = fmaf(diff, diff, d2);
+        }
+      }
+      float c = 0.f;
+      if (d2 > 0.f) {
+        c = 2.f * gamma * b / ((0.001f + d2) * (a * __powf(d2, b) + 1.f));
+      } else if (j == kk) {
+        continue;
+      }
+#pragma unroll
+      for (int d = 0; d < DM; ++d) {
+        if (d < dd) {
+          const float g = c > 0.f ? clip4(c * (cur[d] - tn[d])) : 4.f;
+          cur[d] += g * alpha;
+        }
+      }
+    }
+    next_neg[e] += (float)n_neg * en;
+  }
+  // Edges are sorted by head: sum the head deltas of each run of equal heads inside the wave
+  // (segmented doubling scan; runs are contiguous, so an equal head o lanes on closes the gap)
+  float dl[DM];
+#pragma unroll
+  for (int d = 0; d < DM; ++d) dl[d] = cur[d] - orig[d];
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int jo = __shfl_down(j, o);
+    const bool take = lane + o < 64 && jo == j;
+#pragma unroll
+    for (int d = 0; d < DM; ++d) {
+      if (d < dd) {
+        const float v = __shfl_down(dl[d], o);
+        if (take) dl[d] += v;
       }
     }
   }
-  next_neg[e] += (float)n_neg * en;
+  const int jprev = __shfl_up(j, 1);
+  const bool leader = j >= 0 && (lane == 0 || jprev != j);
+  // does the run continue in the previous / next wave's edges?
+  int jp = -2, jn = -2;
+  if (lane == 0 && e > 0 && e - 1 < n_edges) jp = head[e - 1];
+  if (lane == 63 && e + 1 < n_edges) jn = head[e + 1];
+  jp = __shfl(jp, 0);
+  jn = __shfl(jn, 63);
+  const int j63 = __shfl(j, 63);
+  if (!leader) return;
+  bool nz = false;
 #pragma unroll
   for (int d = 0; d < DM; ++d)
-    if (d < dd) atomicAdd(&hj[d], cur[d] - orig[d]);
+    if (d < dd) nz |= dl[d] != 0.f;
+  if (!nz) return;
+  const bool crosses = (lane == 0 && jp == j) || (j63 == j && jn == j);
+  // a head is written only by its own run unless tails are moved: then one plain store per run
+  if ((pull || !move_other) && !crosses) {
+    if (!act) {
+#pragma unroll
+      for (int d = 0; d < DM; ++d)
+        if (d < dd) orig[d] = hj[d];
+    }
+#pragma unroll
+    for (int d = 0; d < DM; ++d)
+      if (d < dd) hj[d] = orig[d] + dl[d];
+  } else {
+#pragma unroll
+    for (int d = 0; d < DM; ++d)
+      if (d < dd) atomicAdd(&hj[d], dl[d]);
+  }
 }
 
 }  // namespace
@@ -115,14 +174,14 @@ __global__ __launch_bounds__(256) void umap_epoch_kernel(
 SRML_API int srml_umap_epoch(const int* head, const int* tail, long n_edges, const float* eps, float* next_sample,
                              float* next_neg, const float* eps_neg, float* emb_head, float* emb_tail,
                              int n_tail_vertices, int dim, float a, float b, float gamma, float alpha, float epoch,
-                             int move_other, unsigned seed, hipStream_t stream) {
+                             int move_other, int pull, unsigned seed, hipStream_t stream) {
   if (n_edges <= 0) return 0;
   if (dim < 1 || dim > 32 || n_tail_vertices < 1) return -8;
   const dim3 grid((unsigned)((n_edges + 255) / 256));
 #define SRML_UMAP_LAUNCH(DD)                                                                                         \
   hipLaunchKernelGGL(umap_epoch_kernel<DD>, grid, dim3(256), 0, stream, head, tail, n_edges, eps, next_sample,       \
                      next_neg, eps_neg, emb_head, emb_tail, n_tail_vertices, dim, a, b, gamma, alpha, epoch,         \
-                     move_other, seed)
+                     move_other, pull, seed)
   switch (dim) {
     case 2: SRML_UMAP_LAUNCH(2); break;
     case 3: SRML_UMAP_LAUNCH(3); break;

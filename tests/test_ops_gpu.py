@@ -1187,3 +1187,32 @@ def test_kmeans_delta_sums_match_full_sums(gpu_device, monkeypatch):
     # the sorted-segment kernel folds fp32 block partials into fp64 sums, so two groupings of the same
     # rows agree to fp32 rounding of the partials (~1e-7 of a coordinate), not bit for bit
     np.testing.assert_allclose(out[0.2]["cluster_centers_"], out[-1.0]["cluster_centers_"], rtol=1e-5, atol=2e-6)
+
+
+@pytest.mark.parametrize("pull", [False, True])
+@pytest.mark.parametrize("dim", [2, 5])
+def test_umap_epoch_head_runs(gpu_device, pull, dim):
+    # head-sorted edges with runs of 1..150 (inside a wave and across 64-lane / block boundaries),
+    # tails read from a separate table (no Hogwild read-after-write): the per-run head commit
+    # (plain store or boundary atomic) must equal the CPU reference
+    g = torch.Generator().manual_seed(11 + dim)
+    nh, nt = 400, 700
+    deg = torch.randint(1, 151, (nh,), generator=g)
+    deg[::7] = 1
+    head = torch.repeat_interleave(torch.arange(nh), deg).int()
+    tail = torch.randint(0, nt, (head.numel(),), generator=g).int()
+    E = head.numel()
+    eps = torch.where(torch.rand(E, generator=g) < 0.8, torch.ones(E), torch.full((E,), 3.0))
+    emb = torch.rand(nh, dim, generator=g) * 10
+    embt = torch.rand(nt, dim, generator=g) * 10
+    args = dict(a=1.577, b=0.895, gamma=1.0, alpha=0.7, epoch=1, move_other=False, seed=3, pull=pull)
+    e_cpu = emb.clone()
+    ops.umap_epoch(head, tail, eps, eps.clone(), torch.zeros(E), torch.zeros(E), e_cpu, embt.clone(), **args)
+    e_gpu = emb.clone().to(gpu_device)
+    ns = eps.clone().to(gpu_device)
+    ops.umap_epoch(head.to(gpu_device), tail.to(gpu_device), eps.to(gpu_device), ns,
+                   torch.zeros(E, device=gpu_device), torch.zeros(E, device=gpu_device), e_gpu,
+                   embt.to(gpu_device), **args)
+    torch.testing.assert_close(e_gpu.cpu(), e_cpu, rtol=1e-4, atol=1e-4)
+    # only the due edges advanced their schedule
+    torch.testing.assert_close(ns.cpu(), torch.where(eps <= 1, 2 * eps, eps))
