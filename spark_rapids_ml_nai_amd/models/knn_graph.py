@@ -142,10 +142,14 @@ def knn_graph_ivf(X: torch.Tensor, k: int, nlist: Optional[int] = None, nprobe: 
     tile_q0, tile_list = ivf_tiles(counts, off)
     T = int(tile_list.shape[0])
     lo, hi = balanced_tile_range(tile_q0, tile_list, off, counts, probes, ctx.rank if world > 1 else 0, world)
-    od, oi = ops.knn_lists(Xs, xn, off, probes.int(), tile_q0[lo:hi], tile_list[lo:hi], k)
+    # fp16 centred candidates (knn_lists_f16_ok): a few extra neighbours, re-ranked exactly below
+    kc = min(32, k + max(2, k // 4)) if ops.knn_lists_f16_ok(Xs, k, C) else k
+    od, oi = ops.knn_lists(Xs, xn, off, probes.int(), tile_q0[lo:hi], tile_list[lo:hi], kc, centroids=C)
     r0 = int(tile_q0[lo]) if lo < T else N
     r1 = int(tile_q0[hi]) if hi < T else N
     d2, pos = refine_sorted(Xs[r0:r1], Xs, oi[r0:r1].long())
+    if kc > k:
+        d2, pos = d2[:, :k].contiguous(), pos[:, :k].contiguous()
     del od, oi
     d2 = gather_rows(d2, ctx)
     pos = gather_rows(pos, ctx)

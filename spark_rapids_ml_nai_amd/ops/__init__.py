@@ -1449,6 +1449,8 @@ def rf_predict(X: torch.Tensor, roots: torch.Tensor, feature: torch.Tensor, thre
 # ------------------------------------------------------------------------------------------
 # Nearest-neighbour search
 # ------------------------------------------------------------------------------------------
+# all-points IVF kNN candidates on fp16 MFMAs with query-list centring (ops.knn_lists centroids=)
+KNN_LISTS_F16 = os.environ.get("SRML_KNN_LISTS_F16", "1") != "0"
 KNN_KMAX = 64          # register/LDS insertion-list kernel (srml_knn_f32)
 TOPK_KMAX = 16384      # distance-chunk + radix-select path (srml_knn_dist_f32 + srml_topk_rows_f32)
 _TOPK_SLICE = 65536    # columns per select block
@@ -1656,14 +1658,27 @@ def ivf_search(Q: torch.Tensor, probes: torch.Tensor, list_off: torch.Tensor, it
     return (od + qnorm.float().view(-1, 1)).clamp_min(0), oi
 
 
+def knn_lists_f16_ok(X: torch.Tensor, k: int, centroids: Optional[torch.Tensor]) -> bool:
+    """The centred fp16 candidate kernel applies (n <= 128, n % 4 == 0, k <= 32, fp32 rows)."""
+    return (KNN_LISTS_F16 and centroids is not None and X.is_cuda and X.dtype == torch.float32
+            and centroids.dtype == torch.float32 and X.dim() == 2 and 1 <= X.shape[1] <= 128
+            and X.shape[1] % 4 == 0 and 1 <= k <= 32 and X.stride(1) == 1 and X.stride(0) % 4 == 0
+            and X.data_ptr() % 16 == 0 and centroids.shape[0] >= 1)
+
+
 def knn_lists(X: torch.Tensor, xnorm: torch.Tensor, list_off: torch.Tensor, probes: torch.Tensor,
-              tile_q0: torch.Tensor, tile_list: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+              tile_q0: torch.Tensor, tile_list: torch.Tensor, k: int,
+              centroids: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """All-points kNN over IVF lists (rows of ``X`` sorted by list, ``list_off`` nlist+1 offsets).
 
     Every query tile (``tile_q0[i]``: first row of <= 128 rows of list ``tile_list[i]``) is
     compared with the items of the lists ``probes[tile_list[i]]``. Returns (N x k partial
     distances ||i||^2 - 2 q.i fp32, N x k item positions int32, ascending); rows outside the
     given tiles are +inf / -1.
+
+    With ``centroids`` (nlist x n, the lists' centres) and ``knn_lists_f16_ok``, the search runs
+    on fp16 MFMAs with rows centred on the query's list centre (knn_graph.hip): the returned
+    distances are then centred fp16 ranking keys, and the caller re-ranks the candidates exactly.
     """
     N, n = X.shape
     nprobe = int(probes.shape[1])
@@ -1708,6 +1723,14 @@ def knn_lists(X: torch.Tensor, xnorm: torch.Tensor, list_off: torch.Tensor, prob
         return od, oi
     if int(list_off[-1]) != N:
         raise ValueError("knn_lists: list offsets do not cover the %d rows" % N)
+    if knn_lists_f16_ok(X, k, centroids) and nprobe <= 128:
+        Cc = _c(centroids)
+        if Cc.shape != (probes.shape[0], n):
+            raise ValueError("knn_lists: centroids must be nlist x n")
+        native.call("srml_knn_lists_f16c", X.data_ptr(), n, X.stride(0), Cc.data_ptr(), _c(list_off.long()).data_ptr(),
+                    _c(probes.int()).data_ptr(), nprobe, _c(tile_q0.long()).data_ptr(), _c(tile_list.int()).data_ptr(),
+                    ntiles, int(k), od.data_ptr(), oi.data_ptr(), native.stream(X.device))
+        return od, oi
     X = _c(X)
     native.call("srml_knn_lists_f32", X.data_ptr(), n, X.stride(0), _c(xnorm.float()).data_ptr(),
                 _c(list_off.long()).data_ptr(), _c(probes.int()).data_ptr(), nprobe, _c(tile_q0.long()).data_ptr(),

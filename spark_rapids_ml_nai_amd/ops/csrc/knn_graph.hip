@@ -167,3 +167,322 @@ SRML_API int srml_knn_lists_f32(const float* X, int n, long ld, const float* xno
                        list_off, probes, nprobe, tile_q0, tile_list, ntiles, k, out_d, out_i);
   return srml_status();
 }
+
+// ------------------------------------------------------------------------------------------
+// fp16 candidate search, centred on the query list (n <= 128, k <= 32).
+//
+// Rows of one inverted list sit around its centroid, so a query tile of list c and the items of
+// c's probe lists are shifted by C_c while they are staged (fp32 load -> subtract -> fp16 LDS):
+// the dot products then see local magnitudes (~ the list radius, not ||x||) and fp16's 11-bit
+// mantissa ranks candidates almost like fp32; the caller asks for a few extra neighbours and
+// re-ranks them with exact fp32 distances (knn_refine_sort). Per 128 x 128 tile pair:
+//  * the query tile is staged ONCE per block (it was re-read for every item tile before), the
+//    next item tile is prefetched into registers while the MFMAs run on the current one
+//    (`v_mfma_f32_32x32x16_f16`: 16x the fp32 MFMA rate, 8 waves = 2 per SIMD);
+//  * item norms ||i - C_c||^2 of the rounded rows come from the staging pass (lane-contiguous
+//    coalesced loads: one row is 32 lanes x 16 B, reduced by 4 DPP adds per 16-lane group);
+//  * selection is a threshold filter in registers: a lane compares its 32 accumulator values
+//    (fmaf(-2, acc, ||i||^2)) with its rows' current k-th best and appends the rare survivors
+//    to per-row LDS candidate lists (LDS atomics), which one thread per row merges into its
+//    sorted top-k. A row that overflows its 32 slots keeps the values not yet taken (a per-lane
+//    mask) and the tile re-runs the append after the merge tightened the thresholds, so no
+//    candidate is lost and every value is appended at most once.
+namespace {
+typedef _Float16 kg_halfx8 __attribute__((ext_vector_type(8)));
+constexpr int F_BM = 128, F_BN = 128, F_KP = 128, F_RS = F_KP + 8;  // LDS row stride (halves)
+constexpr int F_CAP = 32, F_KQ = 32, F_PMAX = 128;
+
+__device__ __forceinline__ float kg_dpp(float v, int ctrl_sel) {
+  // ctrl_sel: 0 quad xor 1, 1 quad xor 2, 2 row_ror:4, 3 row_ror:8
+  const int x = __float_as_int(v);
+  int r;
+  switch (ctrl_sel) {
+    case 0: r = __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xf, 0xf, false); break;
+    case 1: r = __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xf, 0xf, false); break;
+    case 2: r = __builtin_amdgcn_update_dpp(0, x, 0x124, 0xf, 0xf, false); break;
+    default: r = __builtin_amdgcn_update_dpp(0, x, 0x128, 0xf, 0xf, false); break;
+  }
+  return __int_as_float(r);
+}
+
+// sum over the 16 lanes of a DPP row, in every lane of it
+__device__ __forceinline__ float kg_sum16(float v) {
+  v += kg_dpp(v, 0);
+  v += kg_dpp(v, 1);
+  v += kg_dpp(v, 2);
+  v += kg_dpp(v, 3);
+  return v;
+}
+
+// Wave w stages rows 16w .. 16w + 15 of a 128-row tile: load j covers rows 16w + 2j (lanes 0-31)
+// and 16w + 2j + 1 (lanes 32-63), columns 4 (lane & 31) .. + 3.
+struct KgPf {
+  floatx4 v[8];
+};
+
+__device__ __forceinline__ void kg_load(KgPf& pf, const float* __restrict__ X, long ld, long r0, long nvalid, int n,
+                                        int wid, int lane) {
+  const int col = 4 * (lane & 31);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int r = 16 * wid + 2 * j + (lane >> 5);
+    if (r < nvalid && col < n)
+      pf.v[j] = *reinterpret_cast<const floatx4*>(X + (r0 + r) * ld + col);  // plain: item tiles are re-read by the list's other query tiles through L2
+    else
+      pf.v[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
+template <bool NORMS>
+__device__ __forceinline__ void kg_store(const KgPf& pf, _Float16* __restrict__ dst, floatx4 cen,
+                                         float (*normp)[F_BN], int wid, int lane) {
+  const int col = 4 * (lane & 31);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int r = 16 * wid + 2 * j + (lane >> 5);
+    const floatx4 x = pf.v[j] - cen;
+    const _Float16 h0 = (_Float16)x[0], h1 = (_Float16)x[1], h2 = (_Float16)x[2], h3 = (_Float16)x[3];
+    typedef _Float16 halfx4 __attribute__((ext_vector_type(4)));
+    *reinterpret_cast<halfx4*>(dst + r * F_RS + col) = halfx4{h0, h1, h2, h3};
+    if constexpr (NORMS) {
+      const float f0 = (float)h0, f1 = (float)h1, f2 = (float)h2, f3 = (float)h3;
+      float s2 = fmaf(f0, f0, fmaf(f1, f1, fmaf(f2, f2, f3 * f3)));
+      s2 = kg_sum16(s2);
+      if ((lane & 15) == 0) normp[(lane >> 4) & 1][r] = s2;  // two 64-column halves per row
+    }
+  }
+}
+
+// Wave-wide bitonic sort of 64 (distance, index) pairs, ascending (index breaks ties).
+__device__ __forceinline__ void kg_bitonic64(float& d, int& id, int lane) {
+#pragma unroll
+  for (int size = 2; size <= 64; size <<= 1)
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const float od = __shfl_xor(d, stride, 64);
+      const int oi = __shfl_xor(id, stride, 64);
+      const bool up = (lane & size) == 0 || size == 64;
+      const bool lower = (lane & stride) == 0;
+      const bool other_less = od < d || (od == d && oi < id);
+      if ((lower == up) == other_less) {
+        d = od;
+        id = oi;
+      }
+    }
+}
+
+// Merge every row's candidate list into its sorted top list (32 slots, +inf padded): wave w
+// sorts rows 16w .. 16w + 15, one 64-lane bitonic sort of (top 32, candidates 32) per row.
+__device__ __forceinline__ void kg_merge(float (*topd)[F_KQ + 1], int (*topi)[F_KQ + 1], float (*cand_d)[F_CAP + 1],
+                                         int (*cand_i)[F_CAP + 1], int* cnt, float* thr_s, int k, int nq, int wid,
+                                         int lane) {
+  const float inf = __builtin_huge_valf();
+  for (int rr = 0; rr < F_BM / 8; ++rr) {
+    const int row = wid * (F_BM / 8) + rr;
+    const int m = min(cnt[row], F_CAP);
+    if (m == 0) continue;  // wave-uniform
+    float d;
+    int id;
+    if (lane < 32) {
+      d = topd[row][lane];
+      id = topi[row][lane];
+    } else {
+      const bool ok = lane - 32 < m;
+      d = ok ? cand_d[row][lane - 32] : inf;
+      id = ok ? cand_i[row][lane - 32] : -1;
+    }
+    kg_bitonic64(d, id, lane);
+    if (lane < 32) {
+      topd[row][lane] = d;
+      topi[row][lane] = id;
+    }
+    if (lane == k - 1 && row < nq) thr_s[row] = d;
+    if (lane == 0) cnt[row] = 0;
+  }
+}
+
+__global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
+    const float* __restrict__ X, int n, long ld, const float* __restrict__ C, const long long* __restrict__ list_off,
+    const int* __restrict__ probes, int nprobe, const long long* __restrict__ tile_q0,
+    const int* __restrict__ tile_list, int ntiles, int k, float* __restrict__ out_d, int* __restrict__ out_i) {
+  __shared__ __attribute__((aligned(16))) _Float16 Qs[F_BM * F_RS];
+  __shared__ __attribute__((aligned(16))) _Float16 Is[F_BN * F_RS];
+  __shared__ float normp[2][F_BN];
+  __shared__ float cand_d[F_BM][F_CAP + 1];
+  __shared__ int cand_i[F_BM][F_CAP + 1];
+  __shared__ int cnt[F_BM];
+  __shared__ float topd[F_BM][F_KQ + 1];
+  __shared__ int topi[F_BM][F_KQ + 1];
+  __shared__ __attribute__((aligned(16))) float thr_s[F_BM];
+  __shared__ int ovf[2];
+  __shared__ long long pl[F_PMAX][2];
+  const int b = xcd_remap(blockIdx.x, gridDim.x);
+  if (b >= ntiles) return;  // block-uniform
+  const int c = tile_list[b];
+  const long q0 = tile_q0[b];
+  const long q1 = min(q0 + (long)F_BM, (long)list_off[c + 1]);
+  const int nq = (int)(q1 - q0);
+  const int t = threadIdx.x;
+  const int lane = t & 63, wid = t >> 6;
+  const int wm = wid >> 2, wn = wid & 3;  // wave tile: rows 64 wm .. +64, columns 32 wn .. +32
+  const int li = lane & 31, lk = lane >> 5;
+  const float inf = __builtin_huge_valf();
+  for (int i = t; i < F_BM * (F_KQ + 1); i += 512) {
+    (&topd[0][0])[i] = inf;
+    (&topi[0][0])[i] = -1;
+  }
+  if (t < F_BM) {
+    cnt[t] = 0;
+    thr_s[t] = t < nq ? inf : -inf;  // rows past the tile never take candidates
+  }
+  if (t < 2) ovf[t] = 0;
+  floatx4 cen = floatx4{0.f, 0.f, 0.f, 0.f};
+  {
+    const int col = 4 * li;
+    if (col < n) cen = *reinterpret_cast<const floatx4*>(C + (long)c * n + col);
+  }
+  // probed lists' row ranges, read once into LDS (empty range for a missing probe)
+  if (t < nprobe) {
+    const int l = probes[(long)c * nprobe + t];
+    pl[t][0] = l >= 0 ? list_off[l] : 0;
+    pl[t][1] = l >= 0 ? list_off[l + 1] : 0;
+  }
+  __syncthreads();
+  // probe / item-tile iterator (block-uniform)
+  int p = -1;
+  long c0 = 0, e = 0;
+  auto next_tile = [&]() -> bool {
+    c0 += F_BN;
+    while (c0 >= e) {
+      if (++p >= nprobe) return false;
+      c0 = pl[p][0];
+      e = pl[p][1];
+    }
+    return true;
+  };
+  KgPf pf;
+  bool have = next_tile();
+  if (have) kg_load(pf, X, ld, c0, e - c0, n, wid, lane);
+  {
+    KgPf pq;
+    kg_load(pq, X, ld, q0, nq, n, wid, lane);
+    kg_store<false>(pq, Qs, cen, normp, wid, lane);
+  }
+  if (have) kg_store<true>(pf, Is, cen, normp, wid, lane);
+  __syncthreads();
+  const int nks = (n + 15) >> 4;
+  float thr[2][16];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) thr[mt][r] = thr_s[wm * 64 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk];
+  int par = 0;
+  while (have) {
+    const long tc0 = c0, te = e;
+    have = next_tile();
+    if (have) kg_load(pf, X, ld, c0, e - c0, n, wid, lane);  // next item tile, in flight during the MFMAs
+    floatx16 acc[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mt][r] = 0.f;
+    for (int ks = 0; ks < nks; ++ks) {
+      const kg_halfx8 bv = *reinterpret_cast<const kg_halfx8*>(Is + (wn * 32 + li) * F_RS + ks * 16 + lk * 8);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const kg_halfx8 av =
+            *reinterpret_cast<const kg_halfx8*>(Qs + (wm * 64 + mt * 32 + li) * F_RS + ks * 16 + lk * 8);
+        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bv, acc[mt], 0, 0, 0);
+      }
+    }
+    const int col = wn * 32 + li;
+    const long cg = tc0 + col;
+    const float inv = cg < te ? normp[0][col] + normp[1][col] : inf;
+    unsigned done = 0u;
+    bool first = true;
+    for (;;) {
+      // filter: one bit per accumulator value below its row's threshold, not yet taken
+      unsigned pass = 0u;
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          pass |= (unsigned)(fmaf(-2.f, acc[mt][r], inv) < thr[mt][r]) << (mt * 16 + r);
+      pass &= ~done;
+      if (pass) {
+        // per 16-value half: all slot atomics in flight together, then the writes
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          int slot[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (pass & (1u << (mt * 16 + r)))
+              slot[r] = atomicAdd(&cnt[wm * 64 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk], 1);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const unsigned bit = 1u << (mt * 16 + r);
+            if (pass & bit) {
+              const int row = wm * 64 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+              if (slot[r] < F_CAP) {
+                cand_d[row][slot[r]] = fmaf(-2.f, acc[mt][r], inv);
+                cand_i[row][slot[r]] = (int)cg;
+                done |= bit;
+              } else {
+                ovf[par] = 1;
+              }
+            }
+          }
+        }
+      }
+      __syncthreads();  // A: candidates visible; every wave is past its MFMAs on Is / normp
+      if (first && have) {
+        // pin the prefetched registers behind the barrier: otherwise the compiler hoists the
+        // centring/conversion above the append loop and waits for the loads right after the MFMAs
+#pragma unroll
+        for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(pf.v[j]));
+        kg_store<true>(pf, Is, cen, normp, wid, lane);
+      }
+      first = false;
+      const int full = ovf[par];  // block-uniform: some row ran out of candidate slots
+      if (t == 0) ovf[par ^ 1] = 0;
+      if (full) kg_merge(topd, topi, cand_d, cand_i, cnt, thr_s, k, nq, wid, lane);
+      __syncthreads();  // B: next item tile staged; merged lists and thresholds visible
+      par ^= 1;
+      if (!full) break;
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const floatx4 tv = *reinterpret_cast<const floatx4*>(&thr_s[wm * 64 + mt * 32 + 8 * g + 4 * lk]);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) thr[mt][4 * g + u] = tv[u];
+        }
+    }
+  }
+  kg_merge(topd, topi, cand_d, cand_i, cnt, thr_s, k, nq, wid, lane);  // the last candidates
+  __syncthreads();
+  if (t < nq) {
+    const long base = (q0 + t) * (long)k;
+    for (int j = 0; j < k; ++j) {
+      out_d[base + j] = topd[t][j];
+      out_i[base + j] = topi[t][j];
+    }
+  }
+}
+}  // namespace
+
+// fp16 centred variant of srml_knn_lists_f32 (see above): C is the nlist x n fp32 centroid table
+// (row-major, leading dimension n); out_d holds the centred fp16 partial distances
+// ||i - C_c||^2 - 2 (q - C_c).(i - C_c) — a ranking key, re-ranked exactly by the caller.
+// Requires n <= 128, n % 4 == 0, ld % 4 == 0, 16-byte aligned X and C, k <= 32.
+SRML_API int srml_knn_lists_f16c(const float* X, int n, long ld, const float* C, const long long* list_off,
+                                 const int* probes, int nprobe, const long long* tile_q0, const int* tile_list,
+                                 int ntiles, int k, float* out_d, int* out_i, hipStream_t stream) {
+  if (ntiles <= 0) return 0;
+  if (k < 1 || k > F_KQ || n < 1 || n > F_KP || (n & 3) || (ld & 3) || nprobe < 1 || nprobe > F_PMAX ||
+      (reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(C) & 15))
+    return -8;
+  hipLaunchKernelGGL(knn_lists_f16_kernel, dim3((unsigned)ntiles), dim3(512), 0, stream, X, n, ld, C, list_off, probes,
+                     nprobe, tile_q0, tile_list, ntiles, k, out_d, out_i);
+  return srml_status();
+}

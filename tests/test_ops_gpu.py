@@ -1216,3 +1216,67 @@ def test_umap_epoch_head_runs(gpu_device, pull, dim):
     torch.testing.assert_close(e_gpu.cpu(), e_cpu, rtol=1e-4, atol=1e-4)
     # only the due edges advanced their schedule
     torch.testing.assert_close(ns.cpu(), torch.where(eps <= 1, 2 * eps, eps))
+
+
+@pytest.mark.parametrize("N,n,nlist,nprobe,k", [(3000, 16, 12, 4, 15), (6000, 128, 20, 6, 19), (900, 4, 40, 3, 1),
+                                                (2500, 64, 7, 7, 32), (400, 128, 60, 2, 20)])
+def test_knn_lists_f16_centred(gpu_device, N, n, nlist, nprobe, k):
+    """fp16 centred IVF tile kernel: valid, duplicate-free candidates from the probed lists whose
+    sets match the fp32 brute force over the same lists (fp16 ranking may swap near-ties)."""
+    from spark_rapids_ml_nai_amd.models.knn_graph import ivf_tiles
+
+    X = _rand(N, n, gpu_device, seed=37) * 3.0 + 5.0  # offset: centring must take it out
+    g = torch.Generator().manual_seed(N + n)
+    lab = torch.randint(0, nlist, (N,), generator=g).to(gpu_device)
+    order = torch.argsort(lab, stable=True)
+    counts = torch.bincount(lab, minlength=nlist)
+    off = torch.zeros(nlist + 1, dtype=torch.int64, device=gpu_device)
+    off[1:] = torch.cumsum(counts, 0)
+    Xs = X[order].contiguous()
+    xn = ops.row_sqnorm(Xs)
+    C = torch.zeros(nlist, n, device=gpu_device).index_add_(0, lab[order], Xs) / counts.clamp_min(1).view(-1, 1)
+    rows = []
+    for c in range(nlist):
+        others = [j for j in torch.randperm(nlist, generator=g).tolist() if j != c][: nprobe - 1]
+        rows.append([c] + others)
+    probes = torch.tensor(rows, dtype=torch.int32, device=gpu_device)
+    tq, tl = ivf_tiles(counts, off)
+    assert ops.knn_lists_f16_ok(Xs, k, C)
+    d, i = ops.knn_lists(Xs, xn, off, probes, tq, tl, k, centroids=C)
+    dc, ic = ops.knn_lists(Xs.cpu(), xn.cpu(), off.cpu(), probes.cpu(), tq.cpu(), tl.cpu(), k)
+    i, d = i.cpu(), d.cpu()
+    # validity: members of the row's probed lists, no duplicates, -1 exactly where fp32 has none
+    offc, prc = off.cpu(), probes.cpu()
+    row_list = torch.repeat_interleave(torch.arange(nlist), counts.cpu())
+    lists_of = torch.bucketize(i.clamp_min(0), offc[1:], right=True)
+    allowed = (prc[row_list].unsqueeze(1) == lists_of.unsqueeze(2)).any(2)
+    assert bool((allowed | (i < 0)).all())
+    assert torch.equal(i < 0, ic < 0)
+    srt = torch.sort(i, 1).values
+    assert not bool(((srt[:, 1:] == srt[:, :-1]) & (srt[:, 1:] >= 0)).any())
+    # set recall against the fp32 selection
+    hit = (i.unsqueeze(2) == ic.unsqueeze(1)).any(2) & (i >= 0)
+    recall = hit.sum().item() / max(1, (ic >= 0).sum().item())
+    assert recall > 0.97, recall
+    # ascending ranking keys
+    fin = torch.isfinite(d)
+    dd = torch.where(fin, d, torch.full_like(d, 3e38))
+    assert bool((dd[:, 1:] >= dd[:, :-1]).all())
+
+
+def test_knn_graph_ivf_f16_recall(gpu_device, monkeypatch):
+    """End to end: the fp16-candidate IVF graph (extra candidates + exact re-rank) keeps the fp32
+    kernel's recall against the exact graph."""
+    from spark_rapids_ml_nai_amd.bench import datagen
+    from spark_rapids_ml_nai_amd.models import knn_graph as KG
+
+    X, _ = datagen.blobs(30000, 64, gpu_device, seed=5, centers=8)
+    _, ie = KG.knn_graph_brute(X, 15)
+    rec = {}
+    for flag in (True, False):
+        monkeypatch.setattr(ops, "KNN_LISTS_F16", flag)
+        dist, idx = KG.knn_graph_ivf(X, 15, nlist=30, nprobe=6, seed=1)
+        assert torch.isfinite(dist).all()
+        assert bool((dist[:, 1:] >= dist[:, :-1]).all())
+        rec[flag] = (idx.unsqueeze(2) == ie.unsqueeze(1)).any(2).float().mean().item()
+    assert rec[True] > rec[False] - 0.005 and rec[True] > 0.9, rec
