@@ -91,29 +91,47 @@ __global__ __launch_bounds__(256) void umap_epoch_kernel(
     next_sample[e] += eps_e;
     const float en = eps_neg[e];
     const int n_neg = en > 0.f ? (int)((epoch - next_neg[e]) / en) : 0;
-    for (int p = 0; p < n_neg; ++p) {
-      const int kk = (int)(hash3(seed ^ (unsigned)e, (unsigned)epoch, (unsigned)p + 0x51ED27u * (unsigned)(e >> 32)) %
-                           (unsigned)n_tail_vertices);
-      const float* tn = emb_tail + (long)kk * dd;
-      float d2 = 0.f;
+    // negative samples: their rows depend only on the hash, so for small layouts all draws of a
+    // group are loaded before any is used (one memory latency per group instead of one per draw)
+    constexpr int NPF = (D > 0 && D <= 4) ? 8 : 1;
+    for (int p0 = 0; p0 < n_neg; p0 += NPF) {
+      float tnv[NPF][DM];
+      int kkv[NPF];
 #pragma unroll
-      for (int d = 0; d < DM; ++d) {
-        if (d < dd) {
-          const float diff = cur[d] - tn[d];
-          d2 = fmaf(diff, diff, d2);
+      for (int q = 0; q < NPF; ++q) {
+        const int p = p0 + q;
+        kkv[q] = (int)(hash3(seed ^ (unsigned)e, (unsigned)epoch, (unsigned)p + 0x51ED27u * (unsigned)(e >> 32)) %
+                       (unsigned)n_tail_vertices);
+        if (p < n_neg) {
+          const float* tn = emb_tail + (long)kkv[q] * dd;
+#pragma unroll
+          for (int d = 0; d < DM; ++d)
+            if (d < dd) tnv[q][d] = tn[d];
         }
       }
-      float c = 0.f;
-      if (d2 > 0.f) {
-        c = 2.f * gamma * b / ((0.001f + d2) * (a * __powf(d2, b) + 1.f));
-      } else if (j == kk) {
-        continue;
-      }
 #pragma unroll
-      for (int d = 0; d < DM; ++d) {
-        if (d < dd) {
-          const float g = c > 0.f ? clip4(c * (cur[d] - tn[d])) : 4.f;
-          cur[d] += g * alpha;
+      for (int q = 0; q < NPF; ++q) {
+        if (p0 + q >= n_neg) break;
+        float d2 = 0.f;
+#pragma unroll
+        for (int d = 0; d < DM; ++d) {
+          if (d < dd) {
+            const float diff = cur[d] - tnv[q][d];
+            d2 = fmaf(diff, diff, d2);
+          }
+        }
+        float c = 0.f;
+        if (d2 > 0.f) {
+          c = 2.f * gamma * b / ((0.001f + d2) * (a * __powf(d2, b) + 1.f));
+        } else if (j == kkv[q]) {
+          continue;
+        }
+#pragma unroll
+        for (int d = 0; d < DM; ++d) {
+          if (d < dd) {
+            const float g = c > 0.f ? clip4(c * (cur[d] - tnv[q][d])) : 4.f;
+            cur[d] += g * alpha;
+          }
         }
       }
     }
