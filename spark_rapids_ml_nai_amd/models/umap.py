@@ -38,6 +38,9 @@ LIST_ORDER = os.environ.get("SRML_UMAP_LIST_ORDER", "1") != "0"
 # fit epochs on the symmetric fuzzy graph move heads only (ops.umap_epoch pull=True): each pair's
 # two directed edges apply its attraction to both ends, without scattered tail atomics
 PULL = os.environ.get("SRML_UMAP_PULL", "1") != "0"
+# pull epochs draw negatives from a per-epoch randomly ordered snapshot, 8 edges per 64 B line
+# (ops.umap_epoch neg_table): one memory request per 8 negative samples instead of 8
+NEG_LINES = os.environ.get("SRML_UMAP_NEG_LINES", "1") != "0"
 SPECTRAL_DENSE_N = 2048  # device Jacobi on the dense normalised adjacency up to this many vertices
 
 
@@ -334,11 +337,20 @@ def optimize_layout(emb_head: torch.Tensor, emb_tail: torch.Tensor, head: torch.
     next_sample = eps.clone()
     next_neg = eps_neg.clone()
     same = emb_head.data_ptr() == emb_tail.data_ptr()
+    neg = None
+    nt = emb_tail.shape[0]
+    if NEG_LINES and pull and same and emb_tail.is_cuda and nt >= 4096 and emb_tail.shape[1] <= 4:
+        # negatives from a per-epoch snapshot in a random vertex order, 8 edges per 64 B line
+        g = torch.Generator(device=emb_tail.device).manual_seed(int(seed) + 7)
+        ids = torch.randperm(nt, generator=g, device=emb_tail.device)[: (nt // 8) * 8].int().contiguous()
+        neg = (torch.empty((ids.shape[0], emb_tail.shape[1]), dtype=torch.float32, device=emb_tail.device), ids)
     for n in range(n_epochs):
         alpha = initial_alpha * (1.0 - float(n) / float(n_epochs))
         before = (emb_head.clone(), None if same or not move_other else emb_tail.clone()) if world > 1 else None
+        if neg is not None:
+            ops.umap_neg_table(emb_tail, neg[1], neg[0])
         ops.umap_epoch(head, tail, eps, next_sample, next_neg, eps_neg, emb_head, emb_tail, a, b, gamma, alpha, n,
-                       move_other, seed, pull=pull)
+                       move_other, seed, pull=pull, neg_table=neg)
         if before is not None:
             for cur, old in ((emb_head, before[0]), (emb_tail, before[1])):
                 if old is None:

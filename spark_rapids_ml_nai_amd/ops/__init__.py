@@ -1959,19 +1959,26 @@ def umap_fuzzy_union_knn(idx: torch.Tensor, w: torch.Tensor, mix: float = 1.0
 def umap_epoch(head: torch.Tensor, tail: torch.Tensor, eps: torch.Tensor, next_sample: torch.Tensor,
                next_neg: torch.Tensor, eps_neg: torch.Tensor, emb_head: torch.Tensor, emb_tail: torch.Tensor,
                a: float, b: float, gamma: float, alpha: float, epoch: int, move_other: bool, seed: int,
-               pull: bool = False) -> None:
+               pull: bool = False, neg_table: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> None:
     """In-place epoch ``epoch`` of umap-learn's optimize_layout_euclidean (edge-parallel).
 
     ``pull=True`` (symmetric edge lists only: every (j, k) has its (k, j) of equal weight) moves
     heads only and applies each edge's attraction twice — the same expected update as moving
-    both ends, without scattered tail writes (see umap.hip)."""
+    both ends, without scattered tail writes (see umap.hip).
+
+    ``neg_table=(tab, ids)`` (device only; ``umap_neg_table``): negative samples are drawn from
+    ``tab`` — a snapshot of ``emb_tail`` in the random vertex order ``ids`` (rows a multiple of 8)
+    — eight consecutive edges sharing one random 8-row line."""
     n_tail = emb_tail.shape[0]
     dim = emb_head.shape[1]
     if emb_head.is_cuda:
         native.call("srml_umap_epoch", head.data_ptr(), tail.data_ptr(), head.shape[0], eps.data_ptr(),
                     next_sample.data_ptr(), next_neg.data_ptr(), eps_neg.data_ptr(), emb_head.data_ptr(),
                     emb_tail.data_ptr(), n_tail, dim, float(a), float(b), float(gamma), float(alpha), float(epoch),
-                    int(bool(move_other)), int(bool(pull)), int(seed) & 0xFFFFFFFF, native.stream(emb_head.device))
+                    int(bool(move_other)), int(bool(pull)), int(seed) & 0xFFFFFFFF,
+                    neg_table[0].data_ptr() if neg_table is not None else None,
+                    neg_table[1].data_ptr() if neg_table is not None else None,
+                    int(neg_table[0].shape[0] // 8) if neg_table is not None else 0, native.stream(emb_head.device))
         return
     # CPU reference: all due edges of the epoch update from one snapshot (synchronous Hogwild)
     ep = float(epoch)
@@ -2007,6 +2014,17 @@ def umap_epoch(head: torch.Tensor, tail: torch.Tensor, eps: torch.Tensor, next_s
     if move_other and not pull:
         emb_tail.index_add_(0, k, -g)
     emb_head.index_add_(0, j, delta)
+
+
+def umap_neg_table(emb: torch.Tensor, ids: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """out[r] = emb[ids[r]] (device): the epoch's snapshot for line-shared negative draws."""
+    if ids.shape[0] != out.shape[0] or out.shape[1] != emb.shape[1]:
+        raise ValueError("umap_neg_table: shape mismatch")
+    if not emb.is_cuda:
+        return torch.index_select(emb, 0, ids.long(), out=out)
+    native.call("srml_umap_neg_table", _c(emb).data_ptr(), _c(ids).data_ptr(), ids.shape[0], emb.shape[1],
+                out.data_ptr(), native.stream(emb.device))
+    return out
 
 
 # ------------------------------------------------------------------------------------------

@@ -40,12 +40,19 @@ __device__ __forceinline__ unsigned hash3(unsigned a, unsigned b, unsigned c) {
 
 __device__ __forceinline__ float clip4(float v) { return fminf(fmaxf(v, -4.f), 4.f); }
 
+// x^b for x > 0 on the hardware log2 / exp2 (v_log_f32 / v_exp_f32): __powf lowers to the
+// full-precision OCML pow (~200 instructions), which made the epoch kernel VALU-bound
+__device__ __forceinline__ float fast_pow(float x, float b) {
+  return __builtin_amdgcn_exp2f(b * __builtin_amdgcn_logf(x));
+}
+
 template <int D>
 __global__ __launch_bounds__(256) void umap_epoch_kernel(
     const int* __restrict__ head, const int* __restrict__ tail, long n_edges, const float* __restrict__ eps,
     float* __restrict__ next_sample, float* __restrict__ next_neg, const float* __restrict__ eps_neg,
     float* __restrict__ emb_head, float* __restrict__ emb_tail, int n_tail_vertices, int dim, float a, float b,
-    float gamma, float alpha, float epoch, int move_other, int pull, unsigned seed) {
+    float gamma, float alpha, float epoch, int move_other, int pull, unsigned seed,
+    const float* __restrict__ neg_tab, const int* __restrict__ neg_ids, int neg_lines) {
   constexpr int DM = D > 0 ? D : 32;
   const int lane = threadIdx.x & 63;
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -74,8 +81,8 @@ __global__ __launch_bounds__(256) void umap_epoch_kernel(
     }
     float coef = 0.f;
     if (dist2 > 0.f) {
-      const float pb = __powf(dist2, b);
-      coef = (-2.f * a * b * pb / dist2) / (a * pb + 1.f);
+      const float pb = fast_pow(dist2, b);
+      coef = __fdividef(-2.f * a * b * pb, dist2 * (a * pb + 1.f));
     }
     // pull: the graph holds both directions of every pair, so the reverse edge moves the tail
     // and the head takes both halves of the pair's attraction here (no tail writes at all)
@@ -100,10 +107,24 @@ __global__ __launch_bounds__(256) void umap_epoch_kernel(
 #pragma unroll
       for (int q = 0; q < NPF; ++q) {
         const int p = p0 + q;
-        kkv[q] = (int)(hash3(seed ^ (unsigned)e, (unsigned)epoch, (unsigned)p + 0x51ED27u * (unsigned)(e >> 32)) %
-                       (unsigned)n_tail_vertices);
+        kkv[q] = -1;
         if (p < n_neg) {
-          const float* tn = emb_tail + (long)kkv[q] * dd;
+          const float* tn;
+          if (neg_tab != nullptr) {
+            // line-shared draw: the 8 edges e & ~7 .. e | 7 take the 8 consecutive rows of ONE
+            // random 8-row line of the randomly permuted negative table (one 64 B request for
+            // 8 lanes instead of 8); the rows of a line are unrelated vertices
+            const unsigned h = hash3(seed ^ (unsigned)(e >> 3), (unsigned)epoch, (unsigned)p + 0x2545F491u);
+            const long pos = (long)(((unsigned long long)h * (unsigned)neg_lines) >> 32) * 8 + (e & 7);
+            tn = neg_tab + pos * dd;
+            kkv[q] = (int)pos;  // a table position; resolved to a vertex id only on a zero distance
+          } else {
+            // uniform draw in [0, n): high half of hash * n (no integer division)
+            const unsigned h =
+                hash3(seed ^ (unsigned)e, (unsigned)epoch, (unsigned)p + 0x51ED27u * (unsigned)(e >> 32));
+            kkv[q] = (int)(((unsigned long long)h * (unsigned)n_tail_vertices) >> 32);
+            tn = emb_tail + (long)kkv[q] * dd;
+          }
 #pragma unroll
           for (int d = 0; d < DM; ++d)
             if (d < dd) tnv[q][d] = tn[d];
@@ -122,8 +143,8 @@ __global__ __launch_bounds__(256) void umap_epoch_kernel(
         }
         float c = 0.f;
         if (d2 > 0.f) {
-          c = 2.f * gamma * b / ((0.001f + d2) * (a * __powf(d2, b) + 1.f));
-        } else if (j == kkv[q]) {
+          c = __fdividef(2.f * gamma * b, (0.001f + d2) * (a * fast_pow(d2, b) + 1.f));
+        } else if (j == (neg_tab != nullptr ? neg_ids[kkv[q]] : kkv[q])) {
           continue;
         }
 #pragma unroll
@@ -189,17 +210,38 @@ __global__ __launch_bounds__(256) void umap_epoch_kernel(
 
 }  // namespace
 
+namespace {
+__global__ __launch_bounds__(256) void umap_neg_table_kernel(const float* __restrict__ emb, const int* __restrict__ ids,
+                                                             long rows, int dim, float* __restrict__ tab) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * dim) return;
+  const long r = i / dim;
+  tab[i] = emb[(long)ids[r] * dim + (i - r * dim)];
+}
+}  // namespace
+
+// tab[r] = emb[ids[r]] (rows x dim): the per-epoch snapshot of the layout in a random vertex order
+// that the line-shared negative draws read (srml_umap_epoch neg_tab).
+SRML_API int srml_umap_neg_table(const float* emb, const int* ids, long rows, int dim, float* tab, hipStream_t stream) {
+  if (rows <= 0) return 0;
+  const long tot = rows * (long)dim;
+  hipLaunchKernelGGL(umap_neg_table_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, emb, ids, rows,
+                     dim, tab);
+  return srml_status();
+}
+
 SRML_API int srml_umap_epoch(const int* head, const int* tail, long n_edges, const float* eps, float* next_sample,
                              float* next_neg, const float* eps_neg, float* emb_head, float* emb_tail,
                              int n_tail_vertices, int dim, float a, float b, float gamma, float alpha, float epoch,
-                             int move_other, int pull, unsigned seed, hipStream_t stream) {
+                             int move_other, int pull, unsigned seed, const float* neg_tab, const int* neg_ids,
+                             int neg_lines, hipStream_t stream) {
   if (n_edges <= 0) return 0;
   if (dim < 1 || dim > 32 || n_tail_vertices < 1) return -8;
   const dim3 grid((unsigned)((n_edges + 255) / 256));
 #define SRML_UMAP_LAUNCH(DD)                                                                                         \
   hipLaunchKernelGGL(umap_epoch_kernel<DD>, grid, dim3(256), 0, stream, head, tail, n_edges, eps, next_sample,       \
                      next_neg, eps_neg, emb_head, emb_tail, n_tail_vertices, dim, a, b, gamma, alpha, epoch,         \
-                     move_other, pull, seed)
+                     move_other, pull, seed, neg_tab, neg_ids, neg_lines)
   switch (dim) {
     case 2: SRML_UMAP_LAUNCH(2); break;
     case 3: SRML_UMAP_LAUNCH(3); break;

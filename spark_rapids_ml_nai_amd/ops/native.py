@@ -124,7 +124,9 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_oneshot_allreduce": (_P, _P, _L, _I, _P, _I, _I, ctypes.c_ulonglong, _L, ctypes.c_longlong, _P, _P),
     "srml_umap_smooth_knn": (_P, _P, _L, _I, _L, _D, _D, _I, _P, _I, _P, _P, _P, _P),
     "srml_umap_fuzzy_union_knn": (_P, _P, _L, _I, _L, ctypes.c_float, _P, _P, _P, _P),
-    "srml_umap_epoch": (_P, _P, _L, _P, _P, _P, _P, _P, _P, _I, _I, _F, _F, _F, _F, _F, _I, _I, ctypes.c_uint, _P),
+    "srml_umap_epoch": (_P, _P, _L, _P, _P, _P, _P, _P, _P, _I, _I, _F, _F, _F, _F, _F, _I, _I, ctypes.c_uint, _P, _P,
+                        _I, _P),
+    "srml_umap_neg_table": (_P, _P, _L, _I, _P, _P),
     "srml_syevj_f64": (_P, _I, _P, _P, _I, _D, _P),
     "srml_potrf_f64": (_P, _I, _L, _P, _P),
     "srml_potrs_f64": (_P, _I, _L, _P, _P),

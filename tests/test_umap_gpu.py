@@ -97,3 +97,25 @@ def test_umap_ivf_list_order_matches_row_order(gpu_device, supervised, monkeypat
         emb = U.umap_fit(Xt, params, y=yt)
         tw[flag] = trustworthiness(X, emb, n_neighbors=15)
     assert tw[True] > 0.9 and tw[True] > tw[False] - 0.01, tw
+
+
+def test_umap_neg_lines_matches_iid_negatives(gpu_device, monkeypatch):
+    """Line-shared negative draws from the per-epoch random-order snapshot keep the layout quality
+    of i.i.d. per-edge draws."""
+    from sklearn.datasets import make_blobs
+    from sklearn.manifold import trustworthiness
+
+    from spark_rapids_ml_nai_amd import ops
+
+    X, _ = make_blobs(10000, 16, centers=10, cluster_std=2.5, random_state=6)
+    Xt = torch.from_numpy(X).float().to(gpu_device)
+    emb = torch.randn(5003, 2, device=gpu_device)
+    ids = torch.randperm(5003, device=gpu_device)[:5000].int()
+    tab = ops.umap_neg_table(emb, ids, torch.empty(5000, 2, device=gpu_device))
+    assert torch.equal(tab, emb[ids.long()])
+    tw = {}
+    for flag in (True, False):
+        monkeypatch.setattr(U, "NEG_LINES", flag)
+        e = U.umap_fit(Xt, {"n_neighbors": 15, "random_state": 4, "n_epochs": 200})
+        tw[flag] = trustworthiness(X, e, n_neighbors=15)
+    assert tw[True] > 0.9 and tw[True] > tw[False] - 0.01, tw
