@@ -12,6 +12,8 @@ The reference fits UMAP on one GPU with cuML's own kNN (``umap.py:840-850,924-95
 """
 from __future__ import annotations
 
+import math
+
 from typing import Any, Optional, Tuple
 
 import numpy as np
@@ -125,6 +127,13 @@ def knn_graph_ivf(X: torch.Tensor, k: int, nlist: Optional[int] = None, nprobe: 
     nlist = max(1, min(nlist, N))
     nprobe = max(1, min(int(nprobe) if nprobe else IVF_NPROBE, nlist, ops.KNN_KMAX))
     C = train_quantizer(X, nlist, seed)
+    if nlist >= 64:
+        # spatial list order: lists grouped by a coarse k-means of their centroids, so the lists a
+        # list probes (and a row's neighbours) get nearby ids; everything indexed by list-order
+        # position downstream (UMAP's SpMM / epochs) then gathers from a compact window
+        kc = max(2, int(round(math.sqrt(nlist))))
+        cl = ops.nearest_list(C, train_quantizer(C, kc, seed + 1))
+        C = C.index_select(0, torch.argsort(cl.long() * nlist + torch.arange(nlist, device=C.device))).contiguous()
     world = ctx.world_size if ctx is not None else 1
     if world > 1:
         C = ctx.comm.broadcast(C, 0)

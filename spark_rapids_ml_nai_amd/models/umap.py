@@ -41,6 +41,11 @@ PULL = os.environ.get("SRML_UMAP_PULL", "1") != "0"
 # pull epochs draw negatives from a per-epoch randomly ordered snapshot, 8 edges per 64 B line
 # (ops.umap_epoch neg_table): one memory request per 8 negative samples instead of 8
 NEG_LINES = os.environ.get("SRML_UMAP_NEG_LINES", "1") != "0"
+# Chebyshev filter degree of the device spectral init's subspace iteration (1 = plain iteration,
+# the default). The filter resolves small eigen-gaps far faster, but on clustered data (20M blobs:
+# ~20 near-1 eigenvalues for a 16-vector block) the Ritz-change stop never fires and it ran to the
+# 300-product cap (20M fit 10.7 -> 22.2 s); the plain iteration settles into the cluster and stops.
+CHEB_DEGREE = int(os.environ.get("SRML_UMAP_CHEB_DEGREE", "1"))
 SPECTRAL_DENSE_N = 2048  # device Jacobi on the dense normalised adjacency up to this many vertices
 
 
@@ -220,13 +225,15 @@ def _cholqr2(Y: torch.Tensor) -> torch.Tensor:
 
 
 def _spectral_device(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n: int, dim: int, seed: int,
-                     iters: int = 300, tol: float = 1e-8, min_iters: int = 20) -> torch.Tensor:
+                     iters: int = 300, tol: float = 1e-6, min_iters: int = 20) -> torch.Tensor:
     """Top eigenvectors of D^-1/2 A D^-1/2 by subspace iteration: the SpMM is the in-tree CSR
     kernel (``ops.csr_spmm``, one row group per graph row), orthonormalisation is CholeskyQR2.
     The (row, col)-sorted union edges ARE the CSR (no sparse-tensor coalesce); the iteration
     stops once the Ritz values of the leading dim + 1 directions move by <= ``tol`` (checked at
     every re-orthonormalisation, from the product the next step needs anyway) — umap-learn's
-    eigsh runs at tol 1e-4 and the layout only needs a starting point."""
+    eigsh runs at tol 1e-4 and the layout only needs a starting point. The Ritz values come from
+    fp32 products, so a tolerance near fp32 resolution (1e-8 before) made the stop a coin toss:
+    164 products in one 20M fit and the 300 cap in the next."""
     from ..core.base import CSR
 
     dev = vals.device
@@ -247,15 +254,45 @@ def _spectral_device(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor,
     dinv = 1.0 / torch.sqrt(deg.clamp_min(1e-30))
     mv = (dinv[r64] * vals.double() * dinv[cols.long()]).float().contiguous()
     M = CSR(indptr=indptr, indices=ci, data=mv, shape=(n, n))
-    p = min(n, dim + 1 + 8)
+    # block size: dim + 1 wanted vectors + 8 guards, rounded up to the SpMM kernel's 16 columns
+    # (64 B W rows: one memory line per gathered neighbour, and a faster-converging subspace)
+    p = min(n, 16 if dim + 9 <= 16 else dim + 9)
     g = torch.Generator(device="cpu").manual_seed(int(seed))
     Y = torch.randn(n, p, generator=g).to(dev)
     Y[:, 0] = torch.sqrt(deg).float()
     Y = _cholqr2(Y)
+
+    def amul(V: torch.Tensor) -> torch.Tensor:
+        return 0.5 * (ops.csr_spmm(M, V) + V)  # (M + I) / 2: eigenvalues in [0, 1], order kept
+
     prev = None
     it = 0
-    while it < iters:
-        Z = 0.5 * (ops.csr_spmm(M, Y) + Y)  # (M + I) / 2: eigenvalues in [0, 1], order kept
+    if CHEB_DEGREE > 1:
+        # Chebyshev-filtered subspace iteration: each step applies T_d on [0, b] (b = the block's
+        # smallest Ritz value, an upper bound of the unwanted spectrum), which damps the unwanted
+        # directions like ~exp(-d sqrt(2 gap)) instead of (1 - gap)^d for d plain products
+        while it < iters:
+            Z = amul(Y)
+            it += 1
+            T = ops.dgemm(Y.double().contiguous(), Z.double().contiguous(), ta=True).cpu().numpy()
+            allr = np.sort(np.linalg.eigvalsh((T + T.T) * 0.5))[::-1]
+            ritz = allr[: dim + 1]
+            if prev is not None and it >= min_iters and \
+                    np.max(np.abs(ritz - prev)) <= tol * max(float(np.max(np.abs(ritz))), 1e-30):
+                break
+            prev = ritz
+            bcut = float(min(max(allr[-1], 0.0), allr[dim]))
+            if bcut >= 0.995 or it + CHEB_DEGREE > iters:
+                Y = _cholqr2(Z)  # spectrum too clustered for the filter: a plain step
+                continue
+            e, c = 0.5 * bcut, 0.5 * bcut
+            Y0, Y1 = Y, (Z - c * Y) / e
+            for _ in range(CHEB_DEGREE - 1):
+                Y0, Y1 = Y1, 2.0 * (amul(Y1) - c * Y1) / e - Y0
+                it += 1
+            Y = _cholqr2(Y1)
+    while CHEB_DEGREE <= 1 and it < iters:
+        Z = amul(Y)
         it += 1
         if it % 5 == 1:  # Y is orthonormal here: Ritz values of the current subspace
             T = ops.dgemm(Y.double().contiguous(), Z.double().contiguous(), ta=True).cpu().numpy()
@@ -269,7 +306,7 @@ def _spectral_device(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor,
         if it % 5 == 0:
             Y = _cholqr2(Y)
     Y = _cholqr2(Y)
-    Z = 0.5 * (ops.csr_spmm(M, Y) + Y)
+    Z = amul(Y)
     # Y^T Z: K = n rows in the millions -> the split-K fp64 MFMA GEMM (ordered fold)
     Yd = Y.double().contiguous()
     T = ops.dgemm(Yd, Z.double().contiguous(), ta=True)

@@ -127,9 +127,11 @@ __global__ __launch_bounds__(256) void csr_spmm_kernel(const long* __restrict__ 
 }
 
 // Column-per-lane variant for 4 < K <= 16: a group of G >= K lanes owns one row and lane k
-// accumulates output column k over the row's non-zeros (index / value loads are group-uniform
-// broadcasts, the W-row reads are one contiguous K-float segment): no cross-lane reduction,
-// where the nnz-split kernel spent 4 shuffles per column per row.
+// accumulates output column k over the row's non-zeros (no cross-lane reduction, where the
+// nnz-split kernel spent 4 shuffles per column per row). The row's (index, value) pairs are read
+// G at a time, one per lane (coalesced), and handed round the group by shuffles, so the G
+// W-row gathers of a chunk are independent loads in flight together instead of a chain of
+// index load -> W load pairs.
 template <typename T, int G>
 __global__ __launch_bounds__(256) void csr_spmm_cols_kernel(const long* __restrict__ indptr,
                                                             const int* __restrict__ indices,
@@ -142,20 +144,31 @@ __global__ __launch_bounds__(256) void csr_spmm_cols_kernel(const long* __restri
   const int l = threadIdx.x % G;
   const bool act = l < kk;
   const float b0 = (bias && act) ? bias[l] : 0.f;
-  for (long r = (long)blockIdx.x * GPB + g; r < m; r += (long)gridDim.x * GPB) {
-    const long p0 = indptr[r], p1 = indptr[r + 1];
+  // one row group per block, XCD-remapped: each XCD sweeps a contiguous row range, so the W rows
+  // of a list-ordered graph's neighbours stay in that XCD's L2 (round-robin blocks spread every
+  // XCD's gathers over the whole active window: 10 % L2 hits)
+  {
+    const long r = (long)xcd_remap(blockIdx.x, gridDim.x) * GPB + g;
+    const bool rv = r < m;
+    const long p0 = rv ? indptr[r] : 0, p1 = rv ? indptr[r + 1] : 0;
     float a0 = 0.f, a1 = 0.f;
-    long p = p0;
-    for (; p + 1 < p1; p += 2) {
-      const int c0 = indices[p], c1 = indices[p + 1];
-      const float v0 = (float)data[p], v1 = (float)data[p + 1];
-      if (act) {
-        a0 = fmaf(v0, W[(long)c0 * ldw + l], a0);
-        a1 = fmaf(v1, W[(long)c1 * ldw + l], a1);
+    for (long base = p0; __any(base < p1); base += G) {
+      const long p = base + l;
+      int c = 0;
+      float v = 0.f;
+      if (p < p1) {
+        c = indices[p];
+        v = (float)data[p];
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < G; s2 += 2) {
+        const int cs0 = __shfl(c, s2, G), cs1 = __shfl(c, s2 + 1, G);
+        const float vs0 = __shfl(v, s2, G), vs1 = __shfl(v, s2 + 1, G);
+        if (act && base + s2 < p1) a0 = fmaf(vs0, W[(long)cs0 * ldw + l], a0);
+        if (act && base + s2 + 1 < p1) a1 = fmaf(vs1, W[(long)cs1 * ldw + l], a1);
       }
     }
-    if (p < p1 && act) a0 = fmaf((float)data[p], W[(long)indices[p] * ldw + l], a0);
-    if (act) Z[r * ldz + l] = a0 + a1 + b0;
+    if (rv && act) Z[r * ldz + l] = a0 + a1 + b0;
   }
 }
 
@@ -267,9 +280,10 @@ static int csr_spmm_launch(const long* indptr, const int* indices, const T* data
                            int kk, const float* bias, float* Z, long ldw, long ldz, hipStream_t s) {
   if (m <= 0) return 0;
   if (kk < 1 || kk > 16 || ldw < kk || ldz < kk) return (int)hipErrorInvalidValue;
-  if (kk > 4) {  // column-per-lane groups
+  if (kk > 4) {  // column-per-lane groups, one block per 256 / Gc rows (no grid stride: see kernel)
     const int Gc = kk <= 8 ? 8 : 16;
-    const dim3 gridc(grid_for(m, Gc));
+    if ((m + 256 / Gc - 1) / (256 / Gc) > 0x7fffffffL) return (int)hipErrorInvalidValue;
+    const dim3 gridc((unsigned)((m + 256 / Gc - 1) / (256 / Gc)));
     if (Gc == 8)
       hipLaunchKernelGGL((csr_spmm_cols_kernel<T, 8>), gridc, dim3(256), 0, s, indptr, indices, data, m, W, kk, bias, Z,
                          ldw, ldz);

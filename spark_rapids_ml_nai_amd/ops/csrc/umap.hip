@@ -55,7 +55,9 @@ __global__ __launch_bounds__(256) void umap_epoch_kernel(
     const float* __restrict__ neg_tab, const int* __restrict__ neg_ids, int neg_lines) {
   constexpr int DM = D > 0 ? D : 32;
   const int lane = threadIdx.x & 63;
-  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  // XCD-remapped: each XCD sweeps a contiguous edge range, so the head / tail rows of a
+  // list-ordered graph stay in its L2
+  const long e = (long)xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   const bool in = e < n_edges;
   const float eps_e = in ? eps[e] : 0.f;
   const bool act = eps_e > 0.f && next_sample[in ? e : 0] <= epoch;
