@@ -41,3 +41,23 @@ def test_rf_ensemble_fit_multiple_fewer_trees_than_ranks_streamed():
     assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
     rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert rec["equal"] and rec["trees"] == [1, 4], rec
+
+
+@pytest.mark.gpu
+def test_umap_two_ranks_ivf_pull_neg_lines():
+    """UMAP on 2 ranks sharing the GPU: IVF graph built tile-range parallel in list order, pull-mode
+    epochs over strided edge shards with line-shared negatives from each rank's snapshot, one
+    all-reduce of the layout deltas per epoch; the scattered-back embedding must keep its quality."""
+    env = dict(os.environ, SRML_NS_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    out = os.path.join(ROOT, "gpurun_out", "ns_umap_2rank_test.jsonl")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29621",
+           os.path.join(ROOT, "tools", "northstar.py"), "--configs", "umap", "--scale", "0.006", "--out", out]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=115)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    with open(out) as f:
+        rec = json.loads(f.read().strip().splitlines()[-1])
+    assert "error" not in rec, rec
+    assert rec["n_gpus"] == 2 and rec["finite"], rec
+    assert rec["trustworthiness"] > 0.9 and rec["trust_gap"] < 0.15, rec
