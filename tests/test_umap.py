@@ -128,3 +128,21 @@ def test_umap_multi_column_input():
     model = UMAP(random_state=0).setFeaturesCols(["a", "b", "c"]).fit(df)
     out = model.transform(df)
     assert out.columns == ["features", "embedding"]
+
+
+def test_ivf_graph_list_order_maps_back():
+    """knn_graph_ivf(list_order=True) is the same graph relabelled: row i is original row order[i]
+    and its neighbours are list positions (CPU)."""
+    import numpy as np
+    import torch
+
+    from spark_rapids_ml_nai_amd.models.knn_graph import knn_graph_ivf
+
+    g = np.random.default_rng(3)
+    X = torch.from_numpy(np.concatenate([g.normal(c, 1.0, (300, 8)) for c in range(6)]).astype(np.float32))
+    d0, i0 = knn_graph_ivf(X, 7, nlist=12, nprobe=4, seed=2)
+    d1, i1, order = knn_graph_ivf(X, 7, nlist=12, nprobe=4, seed=2, list_order=True)
+    assert sorted(order.tolist()) == list(range(X.shape[0]))
+    back = torch.where(i1 >= 0, order[i1.clamp_min(0)], torch.full_like(i1, -1))
+    torch.testing.assert_close(d1, d0[order])
+    assert torch.equal(back, i0[order])
