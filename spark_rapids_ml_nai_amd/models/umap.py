@@ -257,8 +257,9 @@ def _spectral_device(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor,
     # block size: dim + 1 wanted vectors + 8 guards, rounded up to the SpMM kernel's 16 columns
     # (64 B W rows: one memory line per gathered neighbour, and a faster-converging subspace)
     p = min(n, 16 if dim + 9 <= 16 else dim + 9)
-    g = torch.Generator(device="cpu").manual_seed(int(seed))
-    Y = torch.randn(n, p, generator=g).to(dev)
+    # device RNG: a host randn of 20M x 16 plus its copy took 0.9 s of the 20M fit
+    g = torch.Generator(device=dev).manual_seed(int(seed))
+    Y = torch.randn((n, p), generator=g, device=dev)
     Y[:, 0] = torch.sqrt(deg).float()
     Y = _cholqr2(Y)
 
@@ -468,8 +469,8 @@ def umap_fit(X: torch.Tensor, params: Dict[str, Any], y: Optional[torch.Tensor] 
         if isinstance(init, str) and init == "spectral" and N > dim + 1:
             emb = spectral_init(rows, cols, vals, N, dim, seed)
         else:
-            g = torch.Generator(device="cpu").manual_seed(seed)
-            emb = (torch.rand(N, dim, generator=g) * 20.0 - 10.0).to(X.device)
+            g = torch.Generator(device=X.device).manual_seed(seed)
+            emb = torch.rand((N, dim), generator=g, device=X.device) * 20.0 - 10.0
         mn, mx = emb.min(0).values, emb.max(0).values
         emb = (10.0 * (emb - mn) / (mx - mn).clamp_min(1e-30)).float().contiguous()
     else:

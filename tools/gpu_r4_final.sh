@@ -9,3 +9,5 @@ timeout -k 10 150 python -c "import __graft_entry__ as g; g.smoke(); print('smok
 tail -1 gpurun_out/smoke_final.log
 timeout -k 10 400 python bench.py > gpurun_out/bench_final.json 2> gpurun_out/bench_final.err || { tail -20 gpurun_out/bench_final.err; exit 1; }
 tail -c 600 gpurun_out/bench_final.json
+timeout -k 10 200 python bench.py --rows 125000 > gpurun_out/bench_final_125k.json 2> gpurun_out/bench_final_125k.err || { tail -20 gpurun_out/bench_final_125k.err; exit 1; }
+tail -c 300 gpurun_out/bench_final_125k.json
