@@ -480,7 +480,9 @@ __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
       const int full = ovf[par];  // block-uniform: some row ran out of candidate slots
       first = false;
       if (t == 0) ovf[par ^ 1] = 0;
-      if (full) kg_merge(topd, topi, cand_d, cand_i, cnt, thr_s, k, nq, wid, lane, F_CAP / 2);
+      // every row with candidates is merged when one row overflows: fresher thresholds measured
+      // 2 % faster than merging only rows at least half full (4M rows: 0.1533 vs 0.1564 s)
+      if (full) kg_merge(topd, topi, cand_d, cand_i, cnt, thr_s, k, nq, wid, lane, 1);
       __syncthreads();  // B: next item tile staged; merged lists and thresholds visible
       par ^= 1;
       if (!full) break;
