@@ -130,7 +130,8 @@ def _umap_fit_worker(ctx: WorkerContext, payload: Tuple[Any, ...]) -> Tuple[np.n
     from .core.base import to_device
     from .models.umap import umap_fit
 
-    X, y, params = payload
+    X, y, params = payload[:3]
+    every_rank = len(payload) > 3 and bool(payload[3])
     Xd = to_device(np.ascontiguousarray(X, dtype=np.float32), ctx.device, torch.float32)
     yd = torch.as_tensor(np.asarray(y), device=ctx.device) if y is not None else None
     if ctx.world_size > 1:
@@ -138,12 +139,10 @@ def _umap_fit_worker(ctx: WorkerContext, payload: Tuple[Any, ...]) -> Tuple[np.n
         Xd = torch.cat([p.to(ctx.device) for p in ctx.comm.allgatherv(Xd)], 0)
         if yd is not None:
             yd = torch.cat([p.to(ctx.device) for p in ctx.comm.allgatherv(yd)], 0)
-    from .core.base import spmd_active
-
     emb = umap_fit(Xd, params, yd, ctx=ctx)
-    # in-process / Spark jobs build the model from rank 0's result only; under SPMD (torchrun)
-    # every rank returns its own model (the layouts are identical: one all-reduce per epoch)
-    if ctx.rank != 0 and not spmd_active():
+    # in-process / Spark jobs build the model from rank 0's result only; an SPMD (torchrun) fit
+    # asks every rank for its own model (the layouts are identical: one all-reduce per epoch)
+    if ctx.rank != 0 and not every_rank:
         return None, None
     return emb, Xd.cpu().numpy()
 
@@ -301,7 +300,7 @@ class UMAP(UMAPClass, _Estimator, _UMAPParams):
 
         nw = self.num_workers
         if spmd_active() or nw <= 1:
-            payloads = [(self._features(df), y, params)]
+            payloads = [(self._features(df), y, params, spmd_active())]
         else:
             if df.getNumPartitions() != nw:
                 df = df.repartition(nw)
