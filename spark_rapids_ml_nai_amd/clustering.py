@@ -295,6 +295,10 @@ def _dbscan_worker(ctx: WorkerContext, payload: Tuple[Any, ...]) -> Tuple[np.nda
     from .models.dbscan import dbscan_fit_predict
 
     X, eps, min_samples, metric = payload
+    if ctx.world_size > 1:  # an empty shard learns the feature count from the other ranks
+        nt = torch.tensor([float(X.shape[1] if X.ndim == 2 else 0)], dtype=torch.float64, device=ctx.device)
+        ctx.comm.allreduce(nt, op="max")
+        X = np.asarray(X, np.float32).reshape(-1, int(nt.item())) if X.size == 0 else X
     Xd = to_device(X, ctx.device, torch.float32)
     return dbscan_fit_predict(Xd, ctx, eps, min_samples, metric)
 
@@ -314,12 +318,8 @@ def _spark_dbscan_task(ctx: WorkerContext, table: Any, extra: Tuple[Any, ...]) -
         part = _DF([table])
         X = _dense_from_df(part, col, cols, np.float32)
         ids = np.asarray(part.to_numpy(id_col)).astype(np.int64)
-    else:
-        X, ids = None, np.zeros(0, np.int64)
-    nt = torch.tensor([float(X.shape[1] if X is not None else 0)], dtype=torch.float64, device=ctx.device)
-    ctx.comm.allreduce(nt, op="max")  # an empty rank still joins every collective
-    if X is None:
-        X = np.zeros((0, int(nt.item())), np.float32)
+    else:  # an empty rank still joins every collective (the worker agrees on n)
+        X, ids = np.zeros((0, 0), np.float32), np.zeros(0, np.int64)
     labels, _core = _dbscan_worker(ctx, (X, eps, min_samples, metric))
     yield pa.RecordBatch.from_arrays([pa.array(ids), pa.array(np.asarray(labels).astype(np.int32))],
                                      names=[id_col, pred_col])
@@ -410,11 +410,20 @@ class DBSCANModel(DBSCANClass, _ModelWithPredictionCol, _DBSCANParams):
 
     def _transform_df(self, df: DataFrame) -> DataFrame:
         from .core.base import run_worker_job
+        from .parallel.context import spmd_active
 
-        nw = max(1, self.num_workers)
-        parts = df.repartition(nw).partitions if df.getNumPartitions() != nw else df.partitions
-        payloads = [(self._features_all(DataFrame([p])), self.getEps(), self.getMinSamples(), self.getMetric())
-                    for p in parts]
+        if spmd_active():
+            # torchrun: the frame is this rank's whole shard; the rank labels its own rows (global
+            # cluster numbering, every rank's rows clustered together) and core_sample_indices_
+            # index into this rank's frame
+            parts = df.partitions
+            X = self._features_all(df) if df.count() else np.zeros((0, 0), np.float32)
+            payloads = [(X, self.getEps(), self.getMinSamples(), self.getMetric())]
+        else:
+            nw = max(1, self.num_workers)
+            parts = df.repartition(nw).partitions if df.getNumPartitions() != nw else df.partitions
+            payloads = [(self._features_all(DataFrame([p])), self.getEps(), self.getMinSamples(), self.getMetric())
+                        for p in parts]
         res = run_worker_job(_dbscan_worker, payloads)
         labels = np.concatenate([r[0] for r in res]).astype(np.int32)
         core = np.concatenate([r[1] for r in res])

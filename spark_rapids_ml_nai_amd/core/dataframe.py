@@ -587,9 +587,10 @@ class DataFrame:
     def limit(self, n: int) -> "DataFrame":
         return DataFrame([self._concat().slice(0, n)])
 
-    def with_row_id(self, name: str) -> "DataFrame":
-        """monotonically increasing int64 id (partition-major, like Spark's id generator)."""
-        parts, off = [], 0
+    def with_row_id(self, name: str, start: int = 0) -> "DataFrame":
+        """monotonically increasing int64 id (partition-major, like Spark's id generator) from
+        ``start`` (an SPMD rank's global row offset)."""
+        parts, off = [], int(start)
         for p in self._parts:
             ids = pa.array(np.arange(off, off + p.num_rows, dtype=np.int64))
             parts.append(p.append_column(pa.field(name, pa.int64()), ids))

@@ -168,7 +168,11 @@ class HasIDCol(Params):
         DataFrame gets ``monotonically_increasing_id()``, reference ``params.py:107-128``)."""
         def add(d: Any) -> Any:
             if hasattr(d, "with_row_id"):
-                return d.with_row_id(self.getIdCol())
+                # under torchrun the frame is this rank's shard: ids start at the rank's global
+                # row offset, so they are unique across ranks (collective, every rank calls it)
+                from ..parallel.context import spmd_row_offset
+
+                return d.with_row_id(self.getIdCol(), spmd_row_offset(d.count()))
             from pyspark.sql import functions as F  # type: ignore
 
             return d.withColumn(self.getIdCol(), F.monotonically_increasing_id())

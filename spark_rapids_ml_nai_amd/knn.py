@@ -43,7 +43,7 @@ from .core.params import (
     keyword_only,
 )
 from .core.persistence import MLReadable, MLWritable
-from .parallel.context import WorkerContext
+from .parallel.context import WorkerContext, spmd_active
 
 _DEFAULT_ID = "unique_id"
 
@@ -51,6 +51,19 @@ _DEFAULT_ID = "unique_id"
 # ------------------------------------------------------------------------------------------
 # worker closures (module level so cloudpickle ships them by reference)
 # ------------------------------------------------------------------------------------------
+def _agree_ncols(ctx: WorkerContext, items: np.ndarray, queries: np.ndarray) -> int:
+    """Feature count every rank agrees on: a rank holding no items and no queries (an empty
+    shard) learns it from the others, so it still joins every collective with the right shapes."""
+    import torch
+
+    n = items.shape[1] if items.ndim == 2 and items.shape[1] else (queries.shape[1] if queries.ndim == 2 else 0)
+    if ctx.world_size > 1:
+        nt = torch.tensor([float(n)], dtype=torch.float64, device=ctx.device)
+        ctx.comm.allreduce(nt, op="max")
+        n = int(nt.item())
+    return n
+
+
 def _exact_worker(ctx: WorkerContext, payload: Tuple[Any, ...]) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
     import torch
 
@@ -58,7 +71,7 @@ def _exact_worker(ctx: WorkerContext, payload: Tuple[Any, ...]) -> Tuple[np.ndar
     from .models.knn import exact_knn
 
     items, item_ids, queries, query_ids, k, metric = payload
-    n = items.shape[1] if items.ndim == 2 and items.shape[1] else queries.shape[1]
+    n = _agree_ncols(ctx, items, queries)
     X = to_device(items.reshape(-1, n), ctx.device, torch.float32)
     ids = torch.as_tensor(item_ids, dtype=torch.int64).to(ctx.device)
     Q = to_device(queries.reshape(-1, n), ctx.device, torch.float32)
@@ -73,7 +86,7 @@ def _ivf_worker(ctx: WorkerContext, payload: Tuple[Any, ...]) -> Tuple[np.ndarra
     from .models.knn import build_ivf, exact_knn, ivf_knn
 
     items, item_ids, queries, query_ids, k, metric, algorithm, nlist, nprobe, seed, cache = payload
-    n = items.shape[1] if items.ndim == 2 and items.shape[1] else queries.shape[1]
+    n = _agree_ncols(ctx, items, queries)
     Q = to_device(queries.reshape(-1, n), ctx.device, torch.float32)
     X = to_device(items.reshape(-1, n), ctx.device, torch.float32)
     ids = torch.as_tensor(item_ids, dtype=torch.int64).to(ctx.device)
@@ -102,8 +115,6 @@ def _spark_knn_task(ctx: WorkerContext, table: Any, extra: Tuple[Any, ...]) -> A
     ``knn.py:638-749``): split the partition by the query tag, search this rank's items for every
     rank's queries (device ring over RCCL), emit (query id, indices, distances) for this rank's
     queries. Item ids stay on the device: no id list travels through the driver."""
-    import torch
-
     col, cols, id_col, qname, k, metric, ivf = extra
     if table is not None and table.num_rows:
         part = DataFrame([table])
@@ -111,14 +122,8 @@ def _spark_knn_task(ctx: WorkerContext, table: Any, extra: Tuple[Any, ...]) -> A
         ids = np.asarray(part.to_numpy(id_col)).astype(np.int64)
         X = _dense_from_df(part, col, cols, np.float32)
         items, item_ids, queries, query_ids = X[~tag], ids[~tag], X[tag], ids[tag]
-        n_local = X.shape[1]
-    else:
-        n_local = 0
-    nt = torch.tensor([float(n_local)], dtype=torch.float64, device=ctx.device)
-    ctx.comm.allreduce(nt, op="max")  # an empty rank still takes part in every collective
-    n = int(nt.item())
-    if n_local == 0:
-        items, queries = np.zeros((0, n), np.float32), np.zeros((0, n), np.float32)
+    else:  # an empty rank still takes part in every collective (the workers agree on n)
+        items, queries = np.zeros((0, 0), np.float32), np.zeros((0, 0), np.float32)
         item_ids, query_ids = np.zeros(0, np.int64), np.zeros(0, np.int64)
     if ivf is None:
         qid, ind, dist = _exact_worker(ctx, (items, item_ids, queries, query_ids, k, metric))
@@ -309,9 +314,14 @@ class _NNModelBase(_NoPersistence, _NNParams):
         k = self.getK()
         if k < 1:
             raise ValueError("k must be >= 1")
-        nw = max(1, self.num_workers)
-        items = _split(self._item_df_withid, nw)
-        queries = _split(query_df_withid, nw)
+        if spmd_active():
+            # torchrun: this process is one rank and its frames are its whole shard (ids already
+            # global from _ensureIdCol); the rank returns the neighbours of its own queries
+            items, queries = [self._item_df_withid], [query_df_withid]
+        else:
+            nw = max(1, self.num_workers)
+            items = _split(self._item_df_withid, nw)
+            queries = _split(query_df_withid, nw)
         payloads = []
         for it, q in zip(items, queries):
             payloads.append((self._features(it), it.to_numpy(id_col).astype(np.int64), self._features(q),
@@ -537,7 +547,8 @@ class ApproximateNearestNeighborsModel(ApproximateNearestNeighborsClass, _NNMode
         nlist = ap.get("nlist", ap.get("n_lists"))
         nprobe = ap.get("nprobe", ap.get("n_probes"))
         # the built index is reusable across kneighbors calls only when the search runs in-process
-        cache = self._index_cache if max(1, self.num_workers) == 1 else None
+        # (one worker, or one SPMD rank over its own item shard)
+        cache = self._index_cache if (spmd_active() or max(1, self.num_workers) == 1) else None
         return (self.getAlgorithm(), nlist, nprobe, int(ap.get("seed", 1)), cache)
 
     def kneighbors(self, query_df: Any, sort_knn_df_by_query_id: bool = True) -> Tuple[DataFrame, DataFrame, DataFrame]:

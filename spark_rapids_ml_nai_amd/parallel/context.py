@@ -98,6 +98,19 @@ def spmd_active() -> bool:
     return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 
 
+def spmd_row_offset(n_local: int) -> int:
+    """This rank's first global row index in an SPMD job: the exclusive prefix sum of every rank's
+    local row count (ONE small all-gather; 0 outside SPMD). Collective: every rank must call it.
+    Gives a rank-local frame globally unique, rank-major row ids (the torchrun counterpart of
+    Spark's partition-major ``monotonically_increasing_id``)."""
+    if not spmd_active():
+        return 0
+    ctx = current_context() or spmd_context()
+    t = torch.tensor([int(n_local)], dtype=torch.int64, device=ctx.device)
+    sizes = ctx.comm.allgather(t).tolist()
+    return int(sum(sizes[: ctx.rank]))
+
+
 def infer_num_workers() -> int:
     if spmd_active():
         return dist.get_world_size()
