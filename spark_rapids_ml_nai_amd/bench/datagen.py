@@ -12,7 +12,7 @@ Spark executor's batches.
 """
 from __future__ import annotations
 
-from typing import Any, Optional, Tuple
+from typing import Any, Dict, List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -40,38 +40,118 @@ def low_rank_matrix(m: int, n: int, device: torch.device, seed: int = 0, effecti
 
 
 def regression(m: int, n: int, device: torch.device, seed: int = 0, n_informative: Optional[int] = None,
-               noise: float = 1.0, bias: float = 0.0) -> Tuple[torch.Tensor, torch.Tensor]:
+               noise: float = 1.0, bias: float = 0.0, n_targets: int = 1) -> Tuple[torch.Tensor, torch.Tensor]:
+    """N(0, 1) features, ground truth 100 U(0, 1) on ``n_informative`` random columns (shared by
+    every partition), ``y = X w + bias + N(0, noise^2)``; ``n_targets > 1`` gives an (m, T) target
+    (the multinomial-logistic ground truth of ``gen_data_distributed.py:445-455``)."""
     g = _gen(device, seed)
     X = torch.randn(m, n, device=device, generator=g, dtype=torch.float32)
     gw = _gen(device, 777)
     k = n_informative or max(1, n // 10)
-    w = torch.zeros(n, device=device)
+    w = torch.zeros(n, n_targets, device=device)
     idx = torch.randperm(n, device=device, generator=gw)[:k]
-    w[idx] = 100.0 * torch.rand(k, device=device, generator=gw)
-    y = X @ w + bias + noise * torch.randn(m, device=device, generator=g)
-    return X, y
+    w[idx] = 100.0 * torch.rand(k, n_targets, device=device, generator=gw)
+    y = X @ w + bias
+    if noise > 0.0:
+        y = y + noise * torch.randn(y.shape, device=device, generator=g)
+    return X, (y[:, 0] if n_targets == 1 else y)
+
+
+def logistic_labels(y: torch.Tensor, seed: int) -> torch.Tensor:
+    """The reference's ``--logistic_regression`` labels (``gen_data_distributed.py:513-537``):
+    binary ``Bernoulli(sigmoid(y))`` of the UNSCALED linear target, or for an (m, C) target a
+    class sampled from ``softmax(y)`` (uniform anchor against the cumulative probabilities)."""
+    g = _gen(y.device, seed + 7919)
+    if y.dim() == 1:
+        return torch.bernoulli(torch.sigmoid(y.double()), generator=g).float()
+    cdf = torch.softmax(y.double(), dim=1).cumsum(1)
+    anchor = torch.rand(y.shape[0], 1, device=y.device, generator=g, dtype=torch.float64)
+    return (anchor > cdf).sum(1).clamp_max(y.shape[1] - 1).float()
+
+
+_CLS_SHARED: Dict[Tuple[Any, ...], Tuple[np.ndarray, List[np.ndarray], Optional[np.ndarray], Optional[np.ndarray]]] = {}
+
+
+def classification_shared(n: int, n_informative: int, n_redundant: int, n_classes: int = 2,
+                          n_clusters_per_class: int = 2, class_sep: float = 1.0, random_state: int = 1,
+                          shuffle: bool = True
+                          ) -> Tuple[np.ndarray, List[np.ndarray], Optional[np.ndarray], Optional[np.ndarray]]:
+    """What every partition of the reference's distributed ``make_classification`` shares, drawn
+    from ONE ``RandomState(random_state)`` in the reference's order
+    (``gen_data_distributed.py:1047-1075``): hypercube-vertex centroids (scaled to +-class_sep),
+    one random covariance ``A_k = 2 U(n_inf, n_inf) - 1`` per cluster, the redundant mix
+    ``B = 2 U(n_inf, n_red) - 1`` (no rescaling) and the column shuffle. Shift 0 / scale 1 (the
+    reference's defaults) draw nothing. Cached: the bench draws its train and holdout shards from
+    the same parameters."""
+    key = (n, n_informative, n_redundant, n_classes, n_clusters_per_class, float(class_sep), int(random_state),
+           bool(shuffle))
+    hit = _CLS_SHARED.get(key)
+    if hit is not None:
+        return hit
+    from sklearn.datasets._samples_generator import _generate_hypercube
+
+    if n_informative + n_redundant > n:
+        raise ValueError("Number of informative and redundant features must sum to less than the number of features")
+    n_clusters = n_classes * n_clusters_per_class
+    if n_informative < np.log2(n_clusters):
+        raise ValueError("n_classes * n_clusters_per_class must be smaller or equal 2**n_informative")
+    gen = np.random.RandomState(int(random_state))
+    centroids = _generate_hypercube(n_clusters, n_informative, gen).astype(np.float64, copy=False)
+    centroids = centroids * (2 * class_sep) - class_sep
+    A = [2 * gen.uniform(size=(n_informative, n_informative)) - 1 for _ in range(n_clusters)]
+    B = 2 * gen.uniform(size=(n_informative, n_redundant)) - 1 if n_redundant > 0 else None
+    cols = None
+    if shuffle:
+        cols = np.arange(n)
+        gen.shuffle(cols)
+    _CLS_SHARED.clear()  # one parameter set at a time (4 x n_inf^2 doubles at the headline shape)
+    _CLS_SHARED[key] = (centroids, A, B, cols)
+    return _CLS_SHARED[key]
 
 
 def classification(m: int, n: int, device: torch.device, seed: int = 0, n_classes: int = 2,
                    n_informative: Optional[int] = None, n_redundant: Optional[int] = None,
-                   class_sep: float = 1.0, flip_y: float = 0.01) -> Tuple[torch.Tensor, torch.Tensor]:
+                   class_sep: float = 1.0, flip_y: float = 0.01, n_clusters_per_class: int = 2,
+                   random_state: int = 1, shuffle: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
+    """One partition (``m`` rows, partition seed ``seed``) of the reference's distributed
+    ``make_classification`` (``gen_data_distributed.py:1088-1151``), generated on the device:
+    balanced clusters (labels ``k % n_classes``), informative features ``z A_k + centroid_k`` with
+    ``z ~ N(0, I)``, redundant features ``X_inf B``, N(0, 1) useless features, ``flip_y`` label
+    noise, then the partition's rows and the shared columns shuffled. Defaults follow the
+    reference benchmark (``run_benchmark.sh``: n_informative = n_redundant = n / 3)."""
     g = _gen(device, seed)
     ni = n_informative if n_informative is not None else max(1, n // 3)
     nr = n_redundant if n_redundant is not None else max(0, n // 3)
     ni = min(ni, n)
     nr = min(nr, n - ni)
-    y = torch.randint(0, n_classes, (m,), device=device, generator=g)
-    gc = _gen(device, 999)
-    centroids = (torch.randint(0, 2, (n_classes, ni), device=device, generator=gc).float() * 2 - 1) * class_sep
+    centroids, A, B, cols = classification_shared(n, ni, nr, n_classes, n_clusters_per_class, class_sep,
+                                                  random_state, shuffle)
+    n_clusters = len(A)
+    per = [m // n_clusters] * n_clusters
+    for i in range(m - sum(per)):
+        per[i % n_clusters] += 1
     X = torch.empty(m, n, device=device, dtype=torch.float32)
-    X[:, :ni] = torch.randn(m, ni, device=device, generator=g) + centroids[y]
+    y = torch.empty(m, device=device, dtype=torch.int64)
+    Xi = torch.randn(m, ni, device=device, generator=g, dtype=torch.float32)
+    stop = 0
+    for k in range(n_clusters):
+        start, stop = stop, stop + per[k]
+        y[start:stop] = k % n_classes
+        Ak = torch.from_numpy(A[k]).to(device=device, dtype=torch.float32)
+        ck = torch.from_numpy(centroids[k]).to(device=device, dtype=torch.float32)
+        X[start:stop, :ni] = torch.addmm(ck, Xi[start:stop], Ak)
+    del Xi
     if nr > 0:
-        B = 2 * torch.rand(ni, nr, device=device, generator=gc) - 1
-        X[:, ni: ni + nr] = (X[:, :ni] @ B) / float(np.sqrt(ni))
+        X[:, ni: ni + nr] = X[:, :ni] @ torch.from_numpy(B).to(device=device, dtype=torch.float32)
     if ni + nr < n:
         X[:, ni + nr:] = torch.randn(m, n - ni - nr, device=device, generator=g)
-    flip = torch.rand(m, device=device, generator=g) < flip_y
-    y = torch.where(flip, torch.randint(0, n_classes, (m,), device=device, generator=g), y)
+    if flip_y >= 0.0:
+        flip = torch.rand(m, device=device, generator=g) < flip_y
+        y = torch.where(flip, torch.randint(0, n_classes, (m,), device=device, generator=g), y)
+    if shuffle:
+        perm = torch.randperm(m, device=device, generator=g)
+        X = X.index_select(0, perm).index_select(1, torch.from_numpy(cols).to(device))
+        y = y[perm]
     return X, y.float()
 
 

@@ -82,10 +82,11 @@ def gen_partition(args: argparse.Namespace, rows: int, seed: int, device: torch.
             num_partitions=args.output_num_files or 1)
         return X, y  # CSR (float64, as the reference's sparse VectorUDT) + labels
     elif args.type == "regression":
+        multi = args.logistic_regression and args.n_classes > 2
         X, y = datagen.regression(rows, n, device, seed, n_informative=args.n_informative, noise=args.noise,
-                                  bias=args.bias)
-        if args.logistic_regression:
-            y = (torch.sigmoid((y - y.mean()) / y.std().clamp_min(1e-12)) > 0.5).float()
+                                  bias=args.bias, n_targets=args.n_classes if multi else 1)
+        if args.logistic_regression:  # Bernoulli / softmax-sampled labels of the unscaled target
+            y = datagen.logistic_labels(y, seed)
     elif args.type == "classification":
         X, y = datagen.classification(rows, n, device, seed, n_classes=args.n_classes,
                                       n_informative=args.n_informative, n_redundant=args.n_redundant)

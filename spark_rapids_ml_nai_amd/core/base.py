@@ -833,8 +833,10 @@ def _eval_worker(ctx: WorkerContext, payload: Tuple[Any, ...]) -> List[List[Any]
                     continue
                 prob = res.get(m.getOrDefault("probabilityCol"))
                 width = int(prob.shape[1]) if isinstance(prob, torch.Tensor) and prob.dim() == 2 else 0
-                C = max(width, int(y.max()) + 1 if len(y) else 1, 1)
-                cm = ops.confusion_counts(yd, p, C)
+                finite = bool(np.isfinite(y).all()) if len(y) else True
+                C = max(width, int(y.max()) + 1 if len(y) and finite else 1, 1)
+                # the device C x C histogram takes C <= CONFUSION_MAX_CLASSES and finite labels
+                cm = ops.confusion_counts(yd, p, C) if finite and C <= ops.CONFUSION_MAX_CLASSES else None
                 if cm is None:  # a label / prediction outside [0, C): the host path handles any values
                     ph = p.double().cpu().numpy()
                     row.append(ClassificationSummary.from_arrays(

@@ -313,10 +313,12 @@ class DeviceQN:
         self._args = a
         self._keep = ptrs
         self._mb = None
-        self._fused = QN_MB and QN_STEP == "fused"
+        lib = native.lib()
+        # the one-launch step spins on software grid barriers: only when all its blocks are
+        # guaranteed co-resident (occupancy x CUs), else the multi-launch step
+        self._fused = QN_MB and QN_STEP == "fused" and bool(lib.srml_qn_fused_resident(N))
         self.fold: Optional[tuple] = None  # (partial-row workspace, rows, stride) the fused step folds
         if QN_MB and N <= 16384 and os.environ.get("SRML_QN_PROBE") != "1":
-            lib = native.lib()
             size = int(lib.srml_qn_fused_scratch() if self._fused else lib.srml_qn_mb_scratch())
             self._mb = torch.zeros(size, **f64)  # zeroed: the fused step's barrier words start at 0
         assert ctypes.sizeof(_QnArgs) == int(native.lib().srml_qn_args_size()), "QnArgs layout mismatch"
@@ -455,6 +457,11 @@ def minimize(P: QNProblem, theta0: np.ndarray, evaluate: Callable[[torch.Tensor,
     torch.cuda.synchronize(device)
     res = q.info()
     if res["status"] == "barrier timeout":
+        if q._mb is not None and q._fused:  # leave the barrier words at zero, as every launch must
+            from ..ops import native
+
+            off = int(native.lib().srml_qn_fused_barrier_offset())
+            q._mb[off: off + 1].zero_()
         raise RuntimeError("device L-BFGS step: a grid barrier timed out (blocks not co-resident)")
     res["theta"] = q.theta()
     if not res["done"]:

@@ -314,7 +314,9 @@ def logreg_workspace(X: Any) -> Optional[torch.Tensor]:
     if _is_csr(X) or not X.is_cuda or X.dtype != torch.float32:
         return None
     m, n = X.shape
-    nf = int(native.lib().srml_logreg_fold_ws(m, n))
+    # the layout the evaluation will see: X itself, or the (aligned, ld = n) copy _c makes
+    ptr, ld = (X.data_ptr(), X.stride(0)) if X.is_contiguous() else (0, n)
+    nf = int(native.lib().srml_logreg_fold_ws(m, n, ld, ptr))
     return torch.empty(nf, dtype=torch.float32, device=X.device) if nf > 0 else None
 
 
@@ -2531,10 +2533,16 @@ def _kind(t: torch.Tensor) -> Tuple[torch.Tensor, int]:
     return t, _KIND[t.dtype]
 
 
+CONFUSION_MAX_CLASSES = 4096  # srml_confusion_counts rejects larger C (status -2)
+
+
 def confusion_counts(y: torch.Tensor, pred: torch.Tensor, C: int) -> Optional[np.ndarray]:
     """(C, C) int64 counts of (label, prediction) pairs, or None when a label / prediction is not
-    an integer in [0, C) (the caller falls back to the host summary). Device: LDS-privatised
-    histogram (``srml_confusion_counts``); only the C x C counts come to the host."""
+    an integer in [0, C) or C > CONFUSION_MAX_CLASSES (the caller falls back to the host summary).
+    Device: LDS-privatised histogram (``srml_confusion_counts``); only the C x C counts come to
+    the host."""
+    if C > CONFUSION_MAX_CLASSES:
+        return None
     m = int(y.shape[0])
     if not y.is_cuda:
         yy, pp = y.double().cpu().numpy(), pred.double().cpu().numpy()

@@ -933,10 +933,25 @@ static long logreg_grid(long m) {
   return (m + rpb - 1) / rpb;
 }
 
-// Floats of the partial-row workspace srml_logreg_binary3_f32 needs for (m, n) (0: that shape
-// takes a kernel without partial rows, pass nullptr).
-SRML_API long srml_logreg_fold_ws(long m, int n) {
-  if (m <= 0 || n <= 1024 || n > 4096) return 0;
+// The prefetching column-split kernel (the only one with a partial-row epilogue) runs for this
+// shape / layout: 1024 < n <= 4096, 16-B aligned rows, n % 4 == 0, SRML_LOGREG_SPLIT == 2.
+static bool logreg_pf_eligible(int n, long ld, const void* X) {
+  static const int split = getenv("SRML_LOGREG_SPLIT") ? atoi(getenv("SRML_LOGREG_SPLIT")) : 2;
+  return split == 2 && n > 1024 && n <= 4096 && (n & 3) == 0 && (ld & 3) == 0 &&
+         (reinterpret_cast<uintptr_t>(X) & 15) == 0;
+}
+
+static bool logreg_fold_enabled() {
+  // SRML_LOGREG_FOLD=0: one fp64 atomic flush per block instead of partial rows + a fold
+  static const int fold = getenv("SRML_LOGREG_FOLD") ? atoi(getenv("SRML_LOGREG_FOLD")) : 1;
+  return fold != 0;
+}
+
+// Floats of the partial-row workspace srml_logreg_binary3_f32 needs for X (m x n, row stride ld)
+// — 0 unless the evaluation of exactly this operand writes partial rows (the consumer may then
+// fold them; any other kernel flushes into `out` and would leave a workspace unwritten).
+SRML_API long srml_logreg_fold_ws(long m, int n, long ld, const void* X) {
+  if (m <= 0 || !logreg_fold_enabled() || !logreg_pf_eligible(n, ld, X)) return 0;
   return logreg_grid(m) * (((n + 3) & ~3) + 4);
 }
 
@@ -997,17 +1012,14 @@ static int logreg_binary_launch(const float* X, long m, int n, long ld, const fl
   dim3 grid((unsigned)blocks), blk(256);
   static const int split = getenv("SRML_LOGREG_SPLIT") ? atoi(getenv("SRML_LOGREG_SPLIT")) : 2;
   // prefetching column-split kernel: needs 16-B aligned rows and n % 4 == 0 (no tail columns)
-  if (split == 2 && n > 1024 && n <= 4096 && (n & 3) == 0 && (ld & 3) == 0 &&
-      (reinterpret_cast<uintptr_t>(X) & 15) == 0) {
+  if (logreg_pf_eligible(n, ld, X)) {
     static const int rsel = getenv("SRML_LOGREG_R") ? atoi(getenv("SRML_LOGREG_R")) : 1;
     static const int dsel = getenv("SRML_LOGREG_D") ? atoi(getenv("SRML_LOGREG_D")) : 3;
     static const int nt = getenv("SRML_LOGREG_NT") ? atoi(getenv("SRML_LOGREG_NT")) : 1;  // nontemporal X stream: +2%
     const int VS = (n + 1023) / 1024;
-    // partial-row epilogue + fold kernel when the caller passed a workspace (SRML_LOGREG_FOLD=0:
-    // one fp64 atomic flush per block anyway)
-    static const int fold = getenv("SRML_LOGREG_FOLD") ? atoi(getenv("SRML_LOGREG_FOLD")) : 1;
+    // partial-row epilogue + fold kernel when the caller passed a workspace
     const long wst = ((n + 3) & ~3) + 4;
-    float* fws = fold ? fold_ws : nullptr;
+    float* fws = logreg_fold_enabled() ? fold_ws : nullptr;
 #define SRML_LR_PF(VV, RR, DD)                                                                              \
     hipLaunchKernelGGL((logreg_binary_pf_kernel<VV, RR, DD>), grid, blk, 0, stream, X, m, n, ld, y, w, b, bptr, \
                        flag, out, rpb, fws)

@@ -1696,6 +1696,25 @@ __global__ __launch_bounds__(MB_T) void qn_fused_kernel(QnArgs A, double* __rest
 
 SRML_API long srml_qn_fused_scratch() { return (long)F_END; }
 
+// Offset (in doubles) of the fused step's barrier words in its scratch: a caller that abandons a
+// step whose barrier timed out zeroes them before the scratch is used again.
+SRML_API long srml_qn_fused_barrier_offset() { return (long)F_BAR; }
+
+// 1 when the fused step's G = ceil(N / 32) blocks are guaranteed co-resident on the current
+// device (occupancy x CUs >= G), so its software grid barriers cannot wait on an unscheduled
+// block; 0 otherwise (the caller takes the multi-launch step instead).
+SRML_API int srml_qn_fused_resident(long N) {
+  const long G = (N + FU_E - 1) / FU_E;
+  if (N <= 0 || G > FU_GMAX) return 0;
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(qn_fused_kernel), MB_T,
+                                                   0) != hipSuccess)
+    return 0;
+  return (long)per_cu * cus >= G ? 1 : 0;
+}
+
 // One optimiser step as ONE launch (G = ceil(N / 32) <= 512 blocks; larger N: the single-block
 // step). fws (optional): the fused binary evaluation's partial rows (parts rows of wst floats,
 // srml_logreg_binary3_f32's workspace) folded in place of `out` — single-rank fits only (a

@@ -27,6 +27,7 @@ _F = ctypes.c_float
 
 # name -> argtypes (restype: int status, except the size queries in _LONG_RESULT)
 _LONG_RESULT = ("srml_rf_bootstrap_ws", "srml_logreg_fold_ws", "srml_qn_mb_scratch", "srml_qn_fused_scratch",
+                "srml_qn_fused_barrier_offset",
                 "srml_logreg_fold_parts", "srml_qn_args_size", "srml_logit_residual_ws", "srml_xtv_mfma_ws",
                 "srml_rf_partition_ws",
                 "srml_label_sort_ws", "srml_radix_sort_ws")
@@ -47,7 +48,7 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_logreg_binary2_f32": (_P, _L, _I, _L, _P, _P, _D, _P, _P, _P, _P),
     "srml_logreg_binary3_f32": (_P, _L, _I, _L, _P, _P, _D, _P, _P, _P, _P, _I, _P),
     "srml_logreg_fold_parts": (_L,),
-    "srml_logreg_fold_ws": (_L, _I),
+    "srml_logreg_fold_ws": (_L, _I, _L, _P),
     "srml_logreg_binary_lds_f32": (_P, _L, _I, _L, _P, _P, _D, _P, _P, _P, _P),
     "srml_logreg_binary_lds_f64": (_P, _L, _I, _L, _P, _P, _D, _P, _P, _P, _P),
     "srml_xtv2_f32": (_P, _L, _I, _L, _P, _I, _L, _P, _L, _L, _P, _P),
@@ -71,6 +72,8 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_qn_step_mbf": (_P, _P, _P, _I, _L, _P),
     "srml_kmeans_lloyd_small": (_P, _L, _I, _L, _P, _I, _P, _P, _P, _P, _P, _P, _P),
     "srml_qn_fused_scratch": (),
+    "srml_qn_fused_barrier_offset": (),
+    "srml_qn_fused_resident": (_L,),
     "srml_qn_mb_scratch": (),
     "srml_kmeanspp_gram": (_P, _I, _L, _P, _I, _I, ctypes.c_ulonglong, _P, _P),
     "srml_qn_max_history": (),

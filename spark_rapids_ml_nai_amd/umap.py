@@ -191,12 +191,15 @@ def _chunk_rows(arr: np.ndarray, limit: int) -> List[np.ndarray]:
 
 class _BroadcastChunks:
     """A driver array shipped to Spark tasks as a list of broadcasts (each <= BROADCAST_LIMIT);
-    ``value()`` reassembles it once per executor process (cached by ``key``)."""
+    ``value()`` reassembles it once per executor process. The cache holds every array of ONE model
+    (``group``: its embedding and its raw rows side by side); loading an array of another model
+    evicts the previous model's arrays only."""
 
-    _cache: Dict[str, np.ndarray] = {}
+    _cache: Dict[Tuple[str, str], np.ndarray] = {}
 
-    def __init__(self, spark: Any, arr: np.ndarray, limit: int, key: str) -> None:
-        self.key = key
+    def __init__(self, spark: Any, arr: np.ndarray, limit: int, group: str, name: str) -> None:
+        self.group = group
+        self.key = (group, name)
         self.shape = tuple(arr.shape)
         self.chunks = [spark.sparkContext.broadcast(c) for c in _chunk_rows(arr, limit)]
 
@@ -204,12 +207,14 @@ class _BroadcastChunks:
         return len(self.chunks)
 
     def value(self) -> np.ndarray:
-        v = _BroadcastChunks._cache.get(self.key)
+        cache = _BroadcastChunks._cache
+        v = cache.get(self.key)
         if v is None:
             parts = [np.asarray(b.value) for b in self.chunks]
             v = parts[0] if len(parts) == 1 else np.concatenate(parts, 0)
-            _BroadcastChunks._cache.clear()  # keep one model's training data per executor process
-            _BroadcastChunks._cache[self.key] = v
+            for k in [k for k in cache if k[0] != self.group]:
+                del cache[k]  # keep one model's training data per executor process
+            cache[self.key] = v
         return v
 
     def unpersist(self) -> None:
@@ -268,6 +273,8 @@ class UMAP(UMAPClass, _Estimator, _UMAPParams):
         from .parallel.spark import collect_arrow
 
         rows = int(sdf.sparkSession.conf.get("spark.sql.execution.arrow.maxRecordsPerBatch", "10000"))
+        if rows <= 0:  # Spark reads <= 0 as "no limit": one batch per 10k rows, not one per row
+            rows = 10000
         schema = StructType([StructField("embedding_", ArrayType(FloatType(), False), False),
                              StructField("raw_data_", ArrayType(FloatType(), False), False)])
         out = spark_barrier_job(sdf.select(*sel).repartition(max(1, self.num_workers)), _spark_umap_task,
@@ -353,8 +360,8 @@ class UMAPModel(UMAPClass, _Model, _UMAPParams):
         if bc is None or bc[0] != int(self.BROADCAST_LIMIT):
             key = uuid.uuid4().hex
             bc = (int(self.BROADCAST_LIMIT),
-                  _BroadcastChunks(spark, self.embedding_, self.BROADCAST_LIMIT, key + "e"),
-                  _BroadcastChunks(spark, self.raw_data_, self.BROADCAST_LIMIT, key + "r"))
+                  _BroadcastChunks(spark, self.embedding_, self.BROADCAST_LIMIT, key, "e"),
+                  _BroadcastChunks(spark, self.raw_data_, self.BROADCAST_LIMIT, key, "r"))
             self._broadcasts = bc
         light = copy.copy(self)
         light.embedding_ = np.zeros((0,) + self.embedding_.shape[1:], np.float32)

@@ -151,3 +151,65 @@ def test_gen_data_sparse_regression_cli(tmp_path):
               "--output_num_files", "2", "--output_dir", out, "--device", "cpu"])
     df = DataFrame.read_parquet(out)
     assert df.count() == 3000 and df.is_vector("feature_array")
+
+
+def _class_stats(X, y, c):
+    Xc = X[y == c].astype(np.float64)
+    ev = np.linalg.eigvalsh(np.cov(Xc, rowvar=False))[::-1]
+    return Xc.mean(0), ev
+
+
+def test_classification_generator_matches_make_classification():
+    """The device classification generator follows the reference's distributed make_classification
+    (2 clusters per class, per-cluster covariance A_k, unscaled redundant mix B, column shuffle,
+    flip_y): at 20k x 60 (20 informative, 20 redundant) its per-class statistics match sklearn's
+    make_classification drawn with the same random_state — the same centroids / A_k / B come out of
+    that RandomState, the rows differ only by sampling."""
+    import torch
+    from sklearn.datasets import make_classification
+
+    from spark_rapids_ml_nai_amd.bench import datagen
+
+    m, n, ni, nr = 20000, 60, 20, 20
+    X, y = datagen.classification(m, n, torch.device("cpu"), seed=11, n_informative=ni, n_redundant=nr,
+                                  random_state=1)
+    X, y = X.numpy(), y.numpy()
+    Xs, ys = make_classification(n_samples=m, n_features=n, n_informative=ni, n_redundant=nr, n_classes=2,
+                                 n_clusters_per_class=2, flip_y=0.01, random_state=1)
+    assert abs(y.mean() - 0.5) < 0.02 and abs(ys.mean() - 0.5) < 0.02
+    for c in (0, 1):
+        mu, ev = _class_stats(X, y, c)
+        mus, evs = _class_stats(Xs, ys, c)
+        # covariance rank: redundant columns are linear in the informative ones -> n - nr
+        tol = 1e-8 * ev[0]
+        assert (ev > tol).sum() == (evs > 1e-8 * evs[0]).sum() == n - nr
+        # spectrum shape: total variance and the leading eigenvalues within sampling / A_k noise
+        np.testing.assert_allclose(ev.sum(), evs.sum(), rtol=0.25)
+        np.testing.assert_allclose(ev[:5] / ev.sum(), evs[:5] / evs.sum(), atol=0.05)
+        # class means: same scale (the centroid geometry, mapped through B)
+        np.testing.assert_allclose(np.linalg.norm(mu), np.linalg.norm(mus), rtol=0.3)
+    # the classes are separated only jointly: a linear model is far from perfect and far from chance
+    from sklearn.linear_model import LogisticRegression as SkLR
+
+    acc = SkLR(max_iter=300).fit(X[:15000], y[:15000]).score(X[15000:], y[15000:])
+    acc_s = SkLR(max_iter=300).fit(Xs[:15000], ys[:15000]).score(Xs[15000:], ys[15000:])
+    assert 0.6 < acc < 0.99 and abs(acc - acc_s) < 0.1, (acc, acc_s)
+
+
+def test_logistic_labels_are_bernoulli_of_the_unscaled_target():
+    import torch
+
+    from spark_rapids_ml_nai_amd.bench import datagen
+
+    z = torch.linspace(-4, 4, 200001, dtype=torch.float64)
+    yb = datagen.logistic_labels(z, seed=3)
+    assert set(np.unique(yb.numpy()).tolist()) == {0.0, 1.0}
+    # P(y = 1 | z) = sigmoid(z): E[y] over the symmetric grid is 1/2, and near z = 0 it is mixed
+    assert abs(float(yb.mean()) - 0.5) < 0.01
+    mid = yb[(z.abs() < 0.2)].mean().item()
+    assert 0.4 < mid < 0.6
+    Y = torch.stack([z, -z, torch.zeros_like(z)], 1)
+    ym = datagen.logistic_labels(Y, seed=4).numpy()
+    assert set(np.unique(ym).tolist()) <= {0.0, 1.0, 2.0}
+    p = torch.softmax(Y, 1).mean(0).numpy()
+    np.testing.assert_allclose(np.bincount(ym.astype(int), minlength=3) / len(ym), p, atol=0.01)

@@ -335,6 +335,35 @@ def test_logistic_fit_fused_fold_matches_unfused(gpu_device, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n", [1501, 3001])
+def test_logistic_fit_unaligned_width_has_no_fold(gpu_device, monkeypatch, n):
+    """A width the prefetching kernel rejects (n % 4 != 0) gets no partial-row workspace, so the
+    default (mb) step cannot fold rows nobody wrote: the fit equals the unfolded single step."""
+    from spark_rapids_ml_nai_amd import ops
+    from spark_rapids_ml_nai_amd.models import qn as qnm
+    from spark_rapids_ml_nai_amd.models.logistic import logistic_fit
+    from spark_rapids_ml_nai_amd.parallel.context import WorkerContext
+
+    rng = np.random.default_rng(5)
+    m = 6000
+    X = rng.standard_normal((m, n)).astype(np.float32)
+    y = (X[:, :8].sum(1) + 0.5 * rng.standard_normal(m) > 0).astype(np.float32)
+    Xt, yt = torch.from_numpy(X).to(gpu_device), torch.from_numpy(y).to(gpu_device)
+    assert ops.logreg_workspace(Xt) is None
+    ctx = WorkerContext.single(gpu_device)
+    out = {}
+    for mode in ("single", "mb"):
+        monkeypatch.setattr(qnm, "QN_MB", mode != "single")
+        monkeypatch.setattr(qnm, "QN_STEP", mode)
+        out[mode] = logistic_fit(Xt, yt, m, ctx, reg=1e-2, l1_ratio=0.0, fit_intercept=True,
+                                 standardization=True, max_iter=40, tol=1e-10)
+    a, b = out["single"], out["mb"]
+    assert np.isfinite(np.asarray(b["coef_"])).all()
+    assert abs(a["objective"] - b["objective"]) <= 1e-6 * abs(a["objective"])
+    np.testing.assert_allclose(np.asarray(b["coef_"]), np.asarray(a["coef_"]), rtol=1e-3, atol=1e-5)
+
+
+@pytest.mark.gpu
 def test_logistic_fit_multi_batched_matches_single(gpu_device):
     """Hyper-parameter batching: a grid of binary fits sharing every pass over X (srml_mbin_f32 +
     srml_qn_step_batch) reproduces the one-at-a-time fits."""

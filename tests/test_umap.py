@@ -167,3 +167,36 @@ def test_umap_spmd_two_ranks_every_rank_gets_a_model(tmp_path):
     rec = json.loads(out.read_text().strip().splitlines()[-1])
     assert "error" not in rec and rec["n_gpus"] == 2 and rec["finite"], rec
     assert rec["trustworthiness"] > 0.9, rec
+
+
+def test_broadcast_chunks_cache_keeps_both_arrays_of_a_model():
+    """The executor-side cache holds a model's embedding AND raw rows together (the second array
+    must not evict the first), and only another model's arrays are evicted."""
+    import numpy as np
+
+    from spark_rapids_ml_nai_amd.umap import _BroadcastChunks
+
+    class _B:
+        def __init__(self, v):
+            self.value = v
+            self.reads = 0
+
+    class _SC:
+        def broadcast(self, v):
+            return _B(v)
+
+    class _Spark:
+        sparkContext = _SC()
+
+    _BroadcastChunks._cache.clear()
+    emb, raw = np.arange(12, dtype=np.float32).reshape(6, 2), np.ones((6, 4), np.float32)
+    e = _BroadcastChunks(_Spark(), emb, 16, "m1", "e")
+    r = _BroadcastChunks(_Spark(), raw, 16, "m1", "r")
+    assert len(e) == 3 and len(r) == 6
+    a0, b0 = e.value(), r.value()
+    assert e.value() is a0 and r.value() is b0  # cache hits for both arrays
+    np.testing.assert_array_equal(a0, emb)
+    other = _BroadcastChunks(_Spark(), emb, 1 << 20, "m2", "e")
+    other.value()
+    assert set(_BroadcastChunks._cache) == {("m2", "e")}
+    _BroadcastChunks._cache.clear()
