@@ -21,7 +21,7 @@ from __future__ import annotations
 import os
 import time
 
-from typing import Any, Dict, Optional, Tuple
+from typing import Any, Dict, List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -187,6 +187,52 @@ def _now(X: torch.Tensor) -> float:
     return time.perf_counter()
 
 
+LLOYD_BATCH = int(os.environ.get("SRML_LLOYD_BATCH", "4"))
+
+
+def _lloyd_small_loop(X: torch.Tensor, C: torch.Tensor, ctx: WorkerContext, k: int, max_iter: int,
+                      tol2: float) -> Tuple[torch.Tensor, int, float]:
+    """Device-resident small-k Lloyd loop (k <= 32, n <= 64): per iteration ONE fused step (labels,
+    sums, counts, inertia into the all-reduce buffer), the all-reduce, and the device centre update
+    (new centres, shift, convergence flag) — three launches, no host sync. The convergence flag is
+    copied back asynchronously once per LLOYD_BATCH iterations and read one batch late (the steps
+    launched after convergence return at once), like the device L-BFGS loop."""
+    n = X.shape[1]
+    dev = X.device
+    C64 = C.double().contiguous()
+    C32 = C64.float().contiguous()
+    cn = (C32 * C32).sum(1).contiguous()
+    buf = torch.zeros(k * n + k + 1, dtype=torch.float64, device=dev)
+    labels = torch.empty(X.shape[0], dtype=torch.int32, device=dev)
+    dist = torch.empty(X.shape[0], dtype=torch.float32, device=dev)
+    flags = torch.zeros(2, dtype=torch.int32, device=dev)  # [done, iterations]
+    stat = torch.zeros(2, dtype=torch.float64, device=dev)  # [inertia, max shift] of the last update
+    host = torch.zeros((2, 2), dtype=torch.int32, pin_memory=True)
+    stream = torch.cuda.current_stream(dev)
+    pending: List[Any] = []
+    it = j = 0
+    while it < max_iter:
+        for _ in range(min(max(1, LLOYD_BATCH), max_iter - it)):
+            buf.zero_()
+            ops.kmeans_lloyd_small(X, C32, cn, out=buf, done=flags, labels=labels, dist=dist)
+            ctx.comm.allreduce(buf)
+            ops.kmeans_small_update(buf, k, n, C64, C32, cn, tol2, flags, stat)
+            it += 1
+        slot = host[j % 2]
+        slot.copy_(flags, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        pending.append((ev, slot))
+        j += 1
+        if len(pending) >= 2:
+            ev0, s0 = pending.pop(0)
+            ev0.synchronize()
+            if int(s0[0]):
+                break
+    fl = flags.cpu()
+    return C64, int(fl[1]), float(stat[0].item())
+
+
 def kmeans_fit(X: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext, k: int, max_iter: int, tol: float,
                seed: int, init: str = "scalable-k-means++", oversampling: float = 2.0, init_steps: int = 2,
                timer: Any = None) -> Dict[str, Any]:
@@ -244,21 +290,10 @@ def kmeans_fit(X: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext, k
     # k <= 32, n <= 64 (the BASELINE k = 20 on 100M x 64): the fused one-pass step gives labels,
     # full cluster sums and the inertia together (no delta bookkeeping needed)
     fused_small = F16 is None and XP is None and ops.lloyd_small_ok(X, k) and not deterministic()
-    for it in range(max(0, max_iter)):
+    if fused_small:
+        C, n_iter, inertia = _lloyd_small_loop(X, C, ctx, k, max_iter, tol2)
+    for it in range(max(0, max_iter) if not fused_small else 0):
         n_iter = it + 1
-        if fused_small:
-            _, _, sums_l, counts_l, d2s = ops.kmeans_lloyd_small(X, C.float())
-            buf = torch.cat([sums_l.view(-1), counts_l.double(), d2s])
-            ctx.comm.allreduce(buf)
-            sums = buf[: k * n].view(k, n)
-            counts = buf[k * n: k * n + k]
-            inertia = float(buf[-1].item()) if it == max_iter - 1 else inertia
-            newC = torch.where(counts.view(-1, 1) > 0, sums / counts.clamp_min(1.0).view(-1, 1), C)
-            shift = float(((newC - C) ** 2).sum(1).max().item())
-            C = newC
-            if shift <= tol2:
-                break
-            continue
         if F16 is not None:
             labels, d2 = ops.nearest_centroid_f16(F16, C.float())
         elif XP is not None:

@@ -846,18 +846,38 @@ def lloyd_small_ok(X: torch.Tensor, k: int, search_only: bool = False) -> bool:
             and os.environ.get("SRML_KMEANS_SMALL", "1") != "0")
 
 
+def lloyd_kernel() -> str:
+    """Small-k Lloyd kernel: ``mfma`` (default: bf16 matrix cores over an exact 3-way split,
+    ``lloyd.hip``) or ``valu`` (``SRML_LLOYD_KERNEL=valu``: VALU distances + f32 one-hot MFMA)."""
+    return "valu" if os.environ.get("SRML_LLOYD_KERNEL", "mfma") == "valu" else "mfma"
+
+
 def kmeans_lloyd_small(X: torch.Tensor, C: torch.Tensor, cnorm: Optional[torch.Tensor] = None,
-                       with_sums: bool = True) -> Tuple[torch.Tensor, ...]:
-    """Fused small-k Lloyd step (``srml_kmeans_lloyd_small``, ONE pass over X): (labels int32,
-    squared distances fp32) and, with ``with_sums``, (cluster sums fp64 [k, n], counts int64 [k],
-    inertia fp64 [1]) by those labels."""
+                       with_sums: bool = True, out: Optional[torch.Tensor] = None,
+                       done: Optional[torch.Tensor] = None, labels: Optional[torch.Tensor] = None,
+                       dist: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, ...]:
+    """Fused small-k Lloyd step (ONE pass over X): (labels int32, squared distances fp32) and,
+    with ``with_sums``, (cluster sums fp64 [k, n], counts int64 [k], inertia fp64 [1]) by those
+    labels. ``out`` (fp64 [k n + k + 1], zeroed): the MFMA kernel accumulates [sums | counts |
+    inertia] there (the all-reduce buffer of the device Lloyd loop; the returned sums / counts /
+    inertia are views of it); ``done`` (int32 device flag): the step is a no-op once it is set;
+    ``labels`` / ``dist``: preallocated outputs (a loop reuses them)."""
     m, n = X.shape
     k = C.shape[0]
     dev = X.device
     C = _c(C.to(device=dev, dtype=torch.float32))
     cn = _c((C * C).sum(1) if cnorm is None else cnorm.to(device=dev, dtype=torch.float32))
-    labels = torch.empty(m, dtype=torch.int32, device=dev)
-    dist = torch.empty(m, dtype=torch.float32, device=dev)
+    labels = torch.empty(m, dtype=torch.int32, device=dev) if labels is None else labels
+    dist = torch.empty(m, dtype=torch.float32, device=dev) if dist is None else dist
+    if lloyd_kernel() == "mfma":
+        if with_sums and out is None:
+            out = torch.zeros(k * n + k + 1, dtype=torch.float64, device=dev)
+        native.call("srml_kmeans_lloyd_mfma", X.data_ptr(), m, n, X.stride(0), C.data_ptr(), k, cn.data_ptr(),
+                    labels.data_ptr(), dist.data_ptr(), out.data_ptr() if with_sums else None,
+                    done.data_ptr() if done is not None else None, native.stream(dev))
+        if not with_sums:
+            return labels, dist
+        return labels, dist, out[: k * n].view(k, n), out[k * n: k * n + k].long(), out[k * n + k:]
     sums = counts = inertia = None
     if with_sums:
         sums = torch.zeros((k, n), dtype=torch.float64, device=dev)
@@ -869,7 +889,20 @@ def kmeans_lloyd_small(X: torch.Tensor, C: torch.Tensor, cnorm: Optional[torch.T
                 native.stream(dev))
     if not with_sums:
         return labels, dist
+    if out is not None:
+        out[: k * n].copy_(sums.view(-1))
+        out[k * n: k * n + k].copy_(counts)
+        out[k * n + k:].copy_(inertia)
     return labels, dist, sums, counts.long(), inertia
+
+
+def kmeans_small_update(buf: torch.Tensor, k: int, n: int, C64: torch.Tensor, C32: torch.Tensor,
+                        cnorm: torch.Tensor, tol2: float, flags: torch.Tensor, stat: torch.Tensor) -> None:
+    """Device centre update of the small-k Lloyd loop (``srml_kmeans_small_update``): C = sums /
+    counts from the reduced ``buf`` (empty clusters keep theirs), fp32 copy + norms, the max
+    squared shift and the convergence flag (flags = [done, iterations]) — no host sync."""
+    native.call("srml_kmeans_small_update", buf.data_ptr(), k, n, C64.data_ptr(), C32.data_ptr(), cnorm.data_ptr(),
+                float(tol2), flags.data_ptr(), stat.data_ptr(), native.stream(buf.device))
 
 
 def cluster_sums(X: torch.Tensor, labels: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:

@@ -175,11 +175,14 @@ def test_cluster_sums(gpu_device, m, n, k):
     assert torch.equal(counts.cpu(), torch.bincount(labels.long(), minlength=k))
 
 
+@pytest.mark.parametrize("kernel", ["mfma", "valu"])
 @pytest.mark.parametrize("m,n,k", [(100003, 64, 20), (5000, 4, 1), (777, 16, 5), (20000, 32, 32), (33333, 60, 17),
                                    (256, 64, 24), (70001, 48, 9)])
-def test_kmeans_lloyd_small_matches_reference(gpu_device, m, n, k):
-    """Fused small-k Lloyd step (one pass: VALU search + one-hot MFMA sums) against fp64: labels
-    are the arg-min up to fp32 near-ties, sums / counts / inertia are those of its own labels."""
+def test_kmeans_lloyd_small_matches_reference(gpu_device, m, n, k, kernel, monkeypatch):
+    """Fused small-k Lloyd step (one pass: bf16 split-MFMA distances + exact one-hot sums, or the
+    VALU search + f32 one-hot MFMA) against fp64: labels are the arg-min up to fp32 near-ties,
+    sums / counts / inertia are those of its own labels."""
+    monkeypatch.setenv("SRML_LLOYD_KERNEL", kernel)
     g = torch.Generator().manual_seed(m + k)
     C = torch.randn(k, n, generator=g) * 2
     X = (C[torch.randint(0, k, (m,), generator=g)] + torch.randn(m, n, generator=g)).float()
@@ -1280,3 +1283,44 @@ def test_knn_graph_ivf_f16_recall(gpu_device, monkeypatch):
         assert bool((dist[:, 1:] >= dist[:, :-1]).all())
         rec[flag] = (idx.unsqueeze(2) == ie.unsqueeze(1)).any(2).float().mean().item()
     assert rec[True] > rec[False] - 0.005 and rec[True] > 0.9, rec
+
+
+@pytest.mark.parametrize("m,n,k", [(200003, 64, 20), (50000, 16, 7)])
+def test_kmeans_device_lloyd_loop_matches_host_loop(gpu_device, m, n, k):
+    """The device-resident small-k Lloyd loop (fused step + device centre update + convergence flag
+    read one batch late) reproduces a host Lloyd loop (the same device search for the labels, fp64
+    centre update and shift test on the host) on the same start: same centres, same iteration
+    count, same inertia. The search itself is checked against fp64 by the test above."""
+    from spark_rapids_ml_nai_amd.models.kmeans import _lloyd_small_loop
+    from spark_rapids_ml_nai_amd.parallel.context import WorkerContext
+
+    g = torch.Generator().manual_seed(m)
+    Ct = torch.randn(k, n, generator=g) * 3
+    X = (Ct[torch.randint(0, k, (m,), generator=g)] + torch.randn(m, n, generator=g)).float()
+    ctx = WorkerContext.single(gpu_device)
+    # a start from random rows (7 fixed iterations), and one near the true centres that converges
+    # within a few iterations (a random start can drift for hundreds of iterations on near-ties,
+    # where two fp32 searches may part ways)
+    starts = ((X[torch.randperm(m, generator=g)[:k]].double(), 7, 1e-30),
+              ((Ct + 0.3 * torch.randn(k, n, generator=g)).double(), 200, 1e-4))
+    for C0, max_iter, tol in starts:
+        C, it, inertia = _lloyd_small_loop(X.to(gpu_device), C0.to(gpu_device), ctx, k, max_iter, tol * tol)
+        Xd, Ch = X.double(), C0.clone()
+        ref_it = 0
+        for _ in range(max_iter):
+            ref_it += 1
+            lab = ops.kmeans_lloyd_small(X.to(gpu_device), Ch.float().to(gpu_device), with_sums=False)[0].long().cpu()
+            cnt = torch.bincount(lab, minlength=k).double()
+            S = torch.zeros(k, n, dtype=torch.float64).index_add_(0, lab, Xd)
+            newC = torch.where(cnt.view(-1, 1) > 0, S / cnt.clamp_min(1).view(-1, 1), Ch)
+            shift = float(((newC - Ch) ** 2).sum(1).max())
+            ref_inertia = float(((Xd - Ch[lab]) ** 2).sum())
+            Ch = newC
+            if shift <= tol * tol:
+                break
+        assert it == ref_it and (max_iter == 7 or it < max_iter), (it, ref_it)
+        # from a random start a near-tie row or two may take the other side in one of the two
+        # searches (their ||c||^2 round differently): a few rows' worth of centre movement
+        tol_c = 1e-4 if max_iter > 7 else 1e-2
+        torch.testing.assert_close(C.cpu(), Ch, rtol=1e-5, atol=tol_c)
+        assert abs(inertia - ref_inertia) <= (1e-5 if max_iter > 7 else 1e-3) * ref_inertia
