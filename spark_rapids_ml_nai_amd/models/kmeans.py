@@ -203,8 +203,12 @@ def _lloyd_small_loop(X: torch.Tensor, C: torch.Tensor, ctx: WorkerContext, k: i
     C32 = C64.float().contiguous()
     cn = (C32 * C32).sum(1).contiguous()
     buf = torch.zeros(k * n + k + 1, dtype=torch.float64, device=dev)
-    labels = torch.empty(X.shape[0], dtype=torch.int32, device=dev)
-    dist = torch.empty(X.shape[0], dtype=torch.float32, device=dev)
+    # MFMA kernel: no per-row outputs (0.8 GB of label / distance writes per 100M-row step saved)
+    rows_out = ops.lloyd_kernel() != "mfma"
+    labels = dist = None
+    if rows_out:
+        labels = torch.empty(X.shape[0], dtype=torch.int32, device=dev)
+        dist = torch.empty(X.shape[0], dtype=torch.float32, device=dev)
     flags = torch.zeros(2, dtype=torch.int32, device=dev)  # [done, iterations]
     stat = torch.zeros(2, dtype=torch.float64, device=dev)  # [inertia, max shift] of the last update
     host = torch.zeros((2, 2), dtype=torch.int32, pin_memory=True)
@@ -214,7 +218,7 @@ def _lloyd_small_loop(X: torch.Tensor, C: torch.Tensor, ctx: WorkerContext, k: i
     while it < max_iter:
         for _ in range(min(max(1, LLOYD_BATCH), max_iter - it)):
             buf.zero_()
-            ops.kmeans_lloyd_small(X, C32, cn, out=buf, done=flags, labels=labels, dist=dist)
+            ops.kmeans_lloyd_small(X, C32, cn, out=buf, done=flags, labels=labels, dist=dist, rows_out=rows_out)
             ctx.comm.allreduce(buf)
             ops.kmeans_small_update(buf, k, n, C64, C32, cn, tol2, flags, stat)
             it += 1

@@ -855,25 +855,34 @@ def lloyd_kernel() -> str:
 def kmeans_lloyd_small(X: torch.Tensor, C: torch.Tensor, cnorm: Optional[torch.Tensor] = None,
                        with_sums: bool = True, out: Optional[torch.Tensor] = None,
                        done: Optional[torch.Tensor] = None, labels: Optional[torch.Tensor] = None,
-                       dist: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, ...]:
+                       dist: Optional[torch.Tensor] = None, rows_out: bool = True) -> Tuple[torch.Tensor, ...]:
     """Fused small-k Lloyd step (ONE pass over X): (labels int32, squared distances fp32) and,
     with ``with_sums``, (cluster sums fp64 [k, n], counts int64 [k], inertia fp64 [1]) by those
     labels. ``out`` (fp64 [k n + k + 1], zeroed): the MFMA kernel accumulates [sums | counts |
     inertia] there (the all-reduce buffer of the device Lloyd loop; the returned sums / counts /
     inertia are views of it); ``done`` (int32 device flag): the step is a no-op once it is set;
-    ``labels`` / ``dist``: preallocated outputs (a loop reuses them)."""
+    ``labels`` / ``dist``: preallocated outputs (a loop reuses them). ``rows_out=False`` (MFMA
+    kernel, with ``out``): no per-row labels / distances are written (the Lloyd loop needs only
+    the sums, counts and inertia); (None, None, sums, counts, inertia) is returned."""
     m, n = X.shape
     k = C.shape[0]
     dev = X.device
     C = _c(C.to(device=dev, dtype=torch.float32))
     cn = _c((C * C).sum(1) if cnorm is None else cnorm.to(device=dev, dtype=torch.float32))
-    labels = torch.empty(m, dtype=torch.int32, device=dev) if labels is None else labels
-    dist = torch.empty(m, dtype=torch.float32, device=dev) if dist is None else dist
-    if lloyd_kernel() == "mfma":
+    mfma = lloyd_kernel() == "mfma"
+    if not rows_out and not (mfma and with_sums):
+        rows_out = True  # only the MFMA kernel's summing step runs without per-row outputs
+    if rows_out:
+        labels = torch.empty(m, dtype=torch.int32, device=dev) if labels is None else labels
+        dist = torch.empty(m, dtype=torch.float32, device=dev) if dist is None else dist
+    else:
+        labels = dist = None
+    if mfma:
         if with_sums and out is None:
             out = torch.zeros(k * n + k + 1, dtype=torch.float64, device=dev)
         native.call("srml_kmeans_lloyd_mfma", X.data_ptr(), m, n, X.stride(0), C.data_ptr(), k, cn.data_ptr(),
-                    labels.data_ptr(), dist.data_ptr(), out.data_ptr() if with_sums else None,
+                    labels.data_ptr() if rows_out else None, dist.data_ptr() if rows_out else None,
+                    out.data_ptr() if with_sums else None,
                     done.data_ptr() if done is not None else None, native.stream(dev))
         if not with_sums:
             return labels, dist

@@ -198,8 +198,8 @@ __global__ __launch_bounds__(LL_T, 2) void lloyd_mfma_kernel(const float* __rest
         if (live) {
           float dd = bv + xn;
           dd = dd > 0.f ? dd : 0.f;
-          labels[grow] = bi;
-          dist[grow] = dd;
+          if (labels) labels[grow] = bi;
+          if (dist) dist[grow] = dd;
           in_sum += (double)dd;
           if (acc_sums) atomicAdd(&sm.cnt[bi], 1.f);
         }
@@ -319,7 +319,8 @@ __global__ __launch_bounds__(256) void kmeans_small_update_kernel(const double* 
 
 // Small-k Lloyd step on the bf16 matrix cores (see above). out == nullptr: search only (labels /
 // squared distances). Otherwise out = [k x n sums | k counts | inertia] (fp64, zeroed by the
-// caller) accumulates this launch. done (nullable): a device flag; non-zero = return at once.
+// caller) accumulates this launch; labels / dist may then be nullptr (not written: the Lloyd loop
+// needs neither). done (nullable): a device flag; non-zero = return at once.
 // Needs k <= 32, n <= 64, n % 4 == 0, ld % 4 == 0, 16-B aligned X.
 SRML_API int srml_kmeans_lloyd_mfma(const float* X, long m, int n, long ld, const float* C, int k,
                                     const float* cnorm, int* labels, float* dist, double* out, const int* done,

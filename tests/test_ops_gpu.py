@@ -1324,3 +1324,20 @@ def test_kmeans_device_lloyd_loop_matches_host_loop(gpu_device, m, n, k):
         tol_c = 1e-4 if max_iter > 7 else 1e-2
         torch.testing.assert_close(C.cpu(), Ch, rtol=1e-5, atol=tol_c)
         assert abs(inertia - ref_inertia) <= (1e-5 if max_iter > 7 else 1e-3) * ref_inertia
+
+
+@pytest.mark.parametrize("m,n,k", [(300007, 64, 20), (40000, 12, 5)])
+def test_kmeans_lloyd_step_without_row_outputs(gpu_device, m, n, k):
+    """The Lloyd loop's step without per-row outputs accumulates the same sums / counts / inertia
+    as the step that writes labels and distances."""
+    g = torch.Generator().manual_seed(m + 7 * k)
+    C = torch.randn(k, n, generator=g) * 2 + 5
+    X = (C[torch.randint(0, k, (m,), generator=g)] + 1.5 * torch.randn(m, n, generator=g)).float().to(gpu_device)
+    Cd = C.float().to(gpu_device)
+    buf_e = torch.zeros(k * n + k + 1, dtype=torch.float64, device=gpu_device)
+    buf_c = torch.zeros_like(buf_e)
+    ops.kmeans_lloyd_small(X, Cd, out=buf_e)
+    lab, dist, _, _, _ = ops.kmeans_lloyd_small(X, Cd, out=buf_c, rows_out=False)
+    assert lab is None and dist is None
+    torch.testing.assert_close(buf_c[k * n: k * n + k], buf_e[k * n: k * n + k], rtol=0, atol=0)
+    torch.testing.assert_close(buf_c, buf_e, rtol=1e-9, atol=1e-6)

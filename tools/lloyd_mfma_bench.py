@@ -1,5 +1,6 @@
 """Small-k Lloyd step at the BASELINE KMeans shape (100M x 64 fp32, k = 20) on one MI355X: ms per
-fused step for the MFMA kernel (lloyd.hip) and the VALU kernel, the HBM rate (X read once per
+fused step for the MFMA kernel (lloyd.hip: with per-row labels / distances, and without them as the
+Lloyd loop runs it) and the VALU kernel, the HBM rate (X read once per
 step), and the device-resident 20-iteration loop (step + update, no host sync). One JSON line."""
 import json
 import os
@@ -45,6 +46,9 @@ for kern in ("mfma", "valu"):
     ms = timeit(lambda: ops.kmeans_lloyd_small(X, C, with_sums=False, labels=lab, dist=dist))
     out[kern + "_search_ms"] = round(ms, 3)
 os.environ["SRML_LLOYD_KERNEL"] = "mfma"
+ms = timeit(lambda: (buf.zero_(), ops.kmeans_lloyd_small(X, C, out=buf, rows_out=False)))
+out["norows_step_ms"] = round(ms, 3)
+out["norows_TBps"] = round(m * n * 4 / ms / 1e9, 2)
 from spark_rapids_ml_nai_amd.models.kmeans import _lloyd_small_loop  # noqa: E402
 from spark_rapids_ml_nai_amd.parallel.context import WorkerContext  # noqa: E402
 
