@@ -5,8 +5,9 @@
 * ``knn_graph_ivf`` — approximate (the north-star 20M x 128 graph, BASELINE.json config 5):
   k-means lists, every 128-row query tile of a list matched against the ``nprobe`` lists
   nearest to its list's centroid by the MFMA tile kernel ``ops.knn_lists``, candidates
-  re-scored exactly. Distributed, rank 0's quantiser is broadcast, every rank buckets the
-  replicated X identically and takes a contiguous, work-balanced range of query tiles.
+  re-scored exactly. Distributed, every phase shards: the quantiser's Lloyd iterations run on
+  1/W of the training sample per rank (cluster sums all-reduced), each rank buckets its 1/W of
+  the rows (labels all-gathered) and takes a contiguous, work-balanced range of query tiles.
 
 The reference fits UMAP on one GPU with cuML's own kNN (``umap.py:840-850,924-958``).
 """
@@ -69,20 +70,48 @@ def knn_graph_brute(X: torch.Tensor, k: int, ctx: Any = None) -> Tuple[torch.Ten
     return gather_rows(dist, ctx), gather_rows(idx, ctx)
 
 
+def record_phase(phases: Optional[dict], name: str, rows: int, t0: float, dev: torch.device) -> float:
+    """Per-rank phase log of a distributed graph / layout build: rows this rank processed and the
+    phase's wall time (the phase's device work drained first). Returns the new phase start."""
+    if phases is None:
+        return t0
+    import time
+
+    if dev.type == "cuda":
+        torch.cuda.current_stream(dev).synchronize()
+    t1 = time.perf_counter()
+    phases[name] = {"rows": int(rows), "s": round(t1 - t0, 4)}
+    return t1
+
+
 def train_quantizer(X: torch.Tensor, nlist: int, seed: int, iters: int = 10,
-                    train_rows_per_list: int = 64) -> torch.Tensor:
+                    train_rows_per_list: int = 64, ctx: Any = None) -> torch.Tensor:
     """IVF coarse quantiser: Lloyd iterations (fused MFMA nearest-centroid + cluster sums) on a
-    row subsample, as IVF trainers do."""
+    row subsample, as IVF trainers do. Distributed (``ctx``, X replicated): every rank draws the
+    same sample and seeds, labels its own 1/W of the sample and the cluster sums are all-reduced
+    (ONE k x (n + 1) fp64 buffer per iteration): every rank ends with the same centres."""
     m = X.shape[0]
     gen = torch.Generator(device=X.device).manual_seed(int(seed))  # device permutations: no host RNG
     ntrain = min(m, max(nlist * train_rows_per_list, 4 * nlist))
     T = X if ntrain == m else X.index_select(0, torch.randperm(m, generator=gen, device=X.device)[:ntrain])
     C = T.index_select(0, torch.randperm(T.shape[0], generator=gen, device=X.device)[:nlist]).float().clone()
-    FT = ops.quantizer_planes(T) if nlist > 256 else None  # bucketing only: the fp16 filter's arg-min
-    tn = ops.row_sqnorm(T) if FT is None else None
+    lo, hi = row_split(T.shape[0], ctx)
+    Tl = T[lo:hi].contiguous() if (lo, hi) != (0, T.shape[0]) else T
+    dist = ctx is not None and ctx.world_size > 1
+    FT = ops.quantizer_planes(Tl) if nlist > 256 and Tl.shape[0] else None  # bucketing only: the filter's arg-min
+    tn = ops.row_sqnorm(Tl) if FT is None and Tl.shape[0] else None
+    n = X.shape[1]
     for _ in range(max(1, iters)):
-        lab = ops.nearest_list(T, C, FT, tn)
-        sums, counts = ops.cluster_sums(T, lab, nlist)
+        if Tl.shape[0]:
+            lab = ops.nearest_list(Tl, C, FT, tn)
+            sums, counts = ops.cluster_sums(Tl, lab, nlist)
+        else:
+            sums = torch.zeros((nlist, n), dtype=torch.float64, device=X.device)
+            counts = torch.zeros(nlist, dtype=torch.int64, device=X.device)
+        if dist:
+            buf = torch.cat([sums.reshape(-1), counts.double()])
+            ctx.comm.allreduce(buf)
+            sums, counts = buf[: nlist * n].view(nlist, n), buf[nlist * n:]
         C = torch.where(counts.view(-1, 1) > 0, (sums / counts.clamp_min(1).double().view(-1, 1)).float(), C)
     return C.contiguous()
 
@@ -115,18 +144,23 @@ def balanced_tile_range(tile_q0: torch.Tensor, tile_list: torch.Tensor, off: tor
 
 
 def knn_graph_ivf(X: torch.Tensor, k: int, nlist: Optional[int] = None, nprobe: Optional[int] = None,
-                  seed: int = 0, ctx: Any = None, list_order: bool = False) -> Any:
+                  seed: int = 0, ctx: Any = None, list_order: bool = False, phases: Optional[dict] = None) -> Any:
     """Approximate all-points graph: (euclidean distances [N, k], indices [N, k] int64).
 
     ``list_order=True`` returns ``(dist, idx, order)`` with the graph left in inverted-list order:
     row i of the graph is original row ``order[i]`` and the indices are list-order positions.
     Rows of one list are neighbours in space, so consumers that gather neighbour rows (the
     spectral SpMM, the layout epochs) read mostly-local memory instead of random rows."""
+    import time
+
     N = X.shape[0]
     nlist = int(nlist) if nlist else max(1, int(round(N / IVF_LIST_ROWS)))
     nlist = max(1, min(nlist, N))
     nprobe = max(1, min(int(nprobe) if nprobe else IVF_NPROBE, nlist, ops.KNN_KMAX))
-    C = train_quantizer(X, nlist, seed)
+    t0 = time.perf_counter()
+    C = train_quantizer(X, nlist, seed, ctx=ctx)
+    ntrain = min(N, max(nlist * 64, 4 * nlist))
+    t0 = record_phase(phases, "quantizer", row_split(ntrain, ctx)[1] - row_split(ntrain, ctx)[0], t0, X.device)
     if nlist >= 64:
         # spatial list order: lists grouped by a coarse k-means of their centroids, so the lists a
         # list probes (and a row's neighbours) get nearby ids; everything indexed by list-order
@@ -135,9 +169,12 @@ def knn_graph_ivf(X: torch.Tensor, k: int, nlist: Optional[int] = None, nprobe: 
         cl = ops.nearest_list(C, train_quantizer(C, kc, seed + 1))
         C = C.index_select(0, torch.argsort(cl.long() * nlist + torch.arange(nlist, device=C.device))).contiguous()
     world = ctx.world_size if ctx is not None else 1
-    if world > 1:
-        C = ctx.comm.broadcast(C, 0)
-    lab = ops.nearest_list(X, C, ops.quantizer_planes(X) if nlist > 256 else None)
+    # bucketing: every rank labels its own row block, the labels are all-gathered (N x 4 B)
+    blo, bhi = row_split(N, ctx)
+    Xb = X[blo:bhi]
+    lab = ops.nearest_list(Xb, C, ops.quantizer_planes(Xb) if nlist > 256 and bhi > blo else None)
+    lab = gather_rows(lab.to(torch.int32), ctx)
+    t0 = record_phase(phases, "bucketing", bhi - blo, t0, X.device)
     order, off, _ = ops.label_sort(lab, nlist)  # stable counting sort by list
     order = order.long()
     counts = off[1:] - off[:-1]
@@ -162,6 +199,7 @@ def knn_graph_ivf(X: torch.Tensor, k: int, nlist: Optional[int] = None, nprobe: 
     del od, oi
     d2 = gather_rows(d2, ctx)
     pos = gather_rows(pos, ctx)
+    record_phase(phases, "knn_lists", r1 - r0, t0, X.device)
     if list_order:
         fin = torch.isfinite(d2)
         rowmax = torch.where(fin, d2, torch.zeros_like(d2)).max(1, keepdim=True).values
@@ -180,7 +218,7 @@ def knn_graph_ivf(X: torch.Tensor, k: int, nlist: Optional[int] = None, nprobe: 
 
 
 def build_knn_graph(X: torch.Tensor, k: int, build_algo: str = "auto", build_kwds: Optional[dict] = None,
-                    seed: int = 0, ctx: Any = None, list_order: bool = False) -> Any:
+                    seed: int = 0, ctx: Any = None, list_order: bool = False, phases: Optional[dict] = None) -> Any:
     """(dist, idx); with ``list_order`` (dist, idx, order) where ``order`` is None unless the
     builder left the graph in a locality order (see ``knn_graph_ivf``)."""
     algo = (build_algo or "auto").lower()
@@ -188,9 +226,14 @@ def build_knn_graph(X: torch.Tensor, k: int, build_algo: str = "auto", build_kwd
         algo = "brute_force_knn" if X.shape[0] <= BRUTE_MAX_ROWS else "ivf"
     kw = dict(build_kwds or {})
     if algo in ("brute_force_knn", "brute", "exact"):
+        import time
+
+        t0 = time.perf_counter()
         d, i = knn_graph_brute(X, k, ctx)
+        lo, hi = row_split(X.shape[0], ctx)
+        record_phase(phases, "knn_brute", hi - lo, t0, X.device)
         return (d, i, None) if list_order else (d, i)
     if algo in ("ivf", "ivfflat", "ivf_flat", "nn_descent"):
         return knn_graph_ivf(X, k, nlist=kw.get("nlist"), nprobe=kw.get("nprobe"), seed=seed, ctx=ctx,
-                             list_order=list_order)
+                             list_order=list_order, phases=phases)
     raise ValueError("Unsupported build_algo %r (auto, brute_force_knn, ivf)" % build_algo)

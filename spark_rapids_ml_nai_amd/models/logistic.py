@@ -115,7 +115,7 @@ def logistic_fit(X: Any, y: torch.Tensor, m_total: int, ctx: WorkerContext, reg:
     def evaluate(w: torch.Tensor, b: torch.Tensor, flag: Optional[torch.Tensor], out: torch.Tensor) -> None:
         ops.logistic_loss_grad(X, y32, w, b, K, out, flag, ws=ws)
 
-    allreduce = ctx.comm.allreduce if ctx.world_size > 1 else None
+    allreduce = ctx.comm.allreduce if ctx.distributed else None
     path = ops.logistic_path(X, K)
     fold = evaluate_partials = None
     if ws is not None and allreduce is None and path == "fused_binary_f32":
@@ -171,7 +171,7 @@ def logistic_fit_multi(X: Any, y: torch.Tensor, m_total: int, ctx: WorkerContext
     classes = stats["classes"]
     base = {"classes_": [float(c) for c in classes], "n_cols": int(n), "dtype": "float32"}
     y32 = (y if y.dtype == torch.float32 else y.to(torch.float32)).contiguous()
-    allreduce = ctx.comm.allreduce if ctx.world_size > 1 else None
+    allreduce = ctx.comm.allreduce if ctx.distributed else None
     out: List[Optional[Dict[str, Any]]] = [None] * len(settings)
     todo = []
     for i, s in enumerate(settings):

@@ -47,6 +47,8 @@ NEG_LINES = os.environ.get("SRML_UMAP_NEG_LINES", "1") != "0"
 # 300-product cap (20M fit 10.7 -> 22.2 s); the plain iteration settles into the cluster and stops.
 CHEB_DEGREE = int(os.environ.get("SRML_UMAP_CHEB_DEGREE", "1"))
 SPECTRAL_DENSE_N = 2048  # device Jacobi on the dense normalised adjacency up to this many vertices
+# per-phase {"rows": this rank's rows / edges, "s": seconds} of the last umap_fit in this process
+LAST_PHASES: Dict[str, Any] = {}
 
 
 def find_ab_params(spread: float, min_dist: float) -> Tuple[float, float]:
@@ -203,21 +205,37 @@ def _spectral_host(rows: np.ndarray, cols: np.ndarray, vals: np.ndarray, n: int,
     return v[:, order]
 
 
-def _cholqr2(Y: torch.Tensor) -> torch.Tensor:
+def _allreduce(t: torch.Tensor, ctx: Any) -> torch.Tensor:
+    if ctx is not None and ctx.world_size > 1:
+        ctx.comm.allreduce(t)
+    return t
+
+
+def _cholqr2(Y: torch.Tensor, ctx: Any = None) -> torch.Tensor:
     """Orthonormal basis of a tall-skinny device block: two CholeskyQR passes (fp64 Gram on the
-    device, p x p Cholesky on the host); Householder QR only if the Gram is numerically singular."""
+    device, p x p Cholesky on the host); Householder QR only if the Gram is numerically singular.
+    Distributed (``ctx``): Y is this rank's row block; the p x p Grams are all-reduced (every rank
+    applies the same R^-1 to its rows)."""
     W = Y
+    dist = ctx is not None and ctx.world_size > 1
     for _ in range(2):
         Wd = W.double()
         # Gram of a tall-skinny block: the streaming SYRK kernel (fp32 in, fp64 out); a library
         # fp64 GEMM with K = n rows picks a non-split-K tile and took 53 ms at 2M x 11
-        G = (ops.gram(W.float()) if W.is_cuda else Wd.T @ Wd).cpu().numpy()
+        Gt = ops.gram(W.float()) if (W.is_cuda and W.shape[0]) else Wd.T @ Wd
+        G = _allreduce(Gt.contiguous(), ctx).cpu().numpy()
         try:
             L = np.linalg.cholesky((G + G.T) * 0.5)
         except np.linalg.LinAlgError:
-            return torch.linalg.qr(Y)[0]
-        d = np.diag(L)
-        if d.min() <= 1e-6 * d.max():
+            L = None
+        d = np.diag(L) if L is not None else None
+        if L is None or d.min() <= 1e-6 * d.max():
+            if dist:  # a singular block shared by the ranks: orthonormalise the gathered block
+                from .knn_graph import gather_rows, row_split
+
+                full = torch.linalg.qr(gather_rows(Y.contiguous(), ctx))[0]
+                lo, hi = row_split(full.shape[0], ctx)
+                return full[lo:hi].contiguous()
             return torch.linalg.qr(Y)[0]
         Rinv = torch.from_numpy(np.linalg.solve(L, np.eye(L.shape[0])).T.copy()).to(Y.device)
         W = ops.dgemm(Wd, Rinv).to(Y.dtype)
@@ -225,7 +243,8 @@ def _cholqr2(Y: torch.Tensor) -> torch.Tensor:
 
 
 def _spectral_device(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n: int, dim: int, seed: int,
-                     iters: int = 300, tol: float = 1e-6, min_iters: int = 20) -> torch.Tensor:
+                     iters: int = 300, tol: float = 1e-6, min_iters: int = 20, ctx: Any = None,
+                     phases: Optional[dict] = None) -> torch.Tensor:
     """Top eigenvectors of D^-1/2 A D^-1/2 by subspace iteration: the SpMM is the in-tree CSR
     kernel (``ops.csr_spmm``, one row group per graph row), orthonormalisation is CholeskyQR2.
     The (row, col)-sorted union edges ARE the CSR (no sparse-tensor coalesce); the iteration
@@ -233,9 +252,19 @@ def _spectral_device(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor,
     every re-orthonormalisation, from the product the next step needs anyway) — umap-learn's
     eigsh runs at tol 1e-4 and the layout only needs a starting point. The Ritz values come from
     fp32 products, so a tolerance near fp32 resolution (1e-8 before) made the stop a coin toss:
-    164 products in one 20M fit and the 300 cap in the next."""
-    from ..core.base import CSR
+    164 products in one 20M fit and the 300 cap in the next.
 
+    Distributed (``ctx``, graph replicated): rank r owns a contiguous row block of the operator
+    and of the subspace block. Every product all-gathers the n x p block (the SpMM gathers
+    arbitrary neighbour rows), multiplies the rank's rows only, and the p x p Ritz / Gram
+    matrices are all-reduced: the SpMM, Gram and GEMM work divides by W, the subspace stays
+    bit-identical across ranks."""
+    from ..core.base import CSR
+    from .knn_graph import gather_rows, record_phase, row_split
+
+    import time
+
+    t0 = time.perf_counter()
     dev = vals.device
     r64 = rows.long()
     if r64.numel() > 1 and not bool((r64[1:] >= r64[:-1]).all()):
@@ -245,26 +274,35 @@ def _spectral_device(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor,
     # the degrees are the row sums of the same CSR (one pass of the SpMM kernel against a ones
     # column; an fp64 index_add over the ~15 n edges cost 0.3 s of atomics at n = 20M)
     indptr = torch.searchsorted(r64.contiguous(), torch.arange(n + 1, device=dev, dtype=torch.int64))
-    ci = cols.to(torch.int32).contiguous()
-    if dev.type == "cuda":
-        A = CSR(indptr=indptr, indices=ci, data=vals.float().contiguous(), shape=(n, n))
-        deg = ops.csr_row_sums(A)  # fp64 per-row accumulation (high-degree nodes keep their precision)
-    else:
-        deg = torch.zeros(n, dtype=torch.float64, device=dev).index_add_(0, r64, vals.double())
+    lo, hi = row_split(n, ctx)
+    e0, e1 = int(indptr[lo]), int(indptr[hi])
+    ip_l = (indptr[lo: hi + 1] - e0).contiguous()
+    ci = cols[e0:e1].to(torch.int32).contiguous()
+    vl = vals[e0:e1]
+    rl = r64[e0:e1]
+    A = CSR(indptr=ip_l, indices=ci, data=vl.float().contiguous(), shape=(hi - lo, n))
+    deg = gather_rows(ops.csr_row_sums(A), ctx)  # fp64 per-row accumulation, this rank's rows
     dinv = 1.0 / torch.sqrt(deg.clamp_min(1e-30))
-    mv = (dinv[r64] * vals.double() * dinv[cols.long()]).float().contiguous()
-    M = CSR(indptr=indptr, indices=ci, data=mv, shape=(n, n))
+    mv = (dinv[rl] * vl.double() * dinv[ci.long()]).float().contiguous()
+    M = CSR(indptr=ip_l, indices=ci, data=mv, shape=(hi - lo, n))
     # block size: dim + 1 wanted vectors + 8 guards, rounded up to the SpMM kernel's 16 columns
     # (64 B W rows: one memory line per gathered neighbour, and a faster-converging subspace)
     p = min(n, 16 if dim + 9 <= 16 else dim + 9)
-    # device RNG: a host randn of 20M x 16 plus its copy took 0.9 s of the 20M fit
+    # device RNG: a host randn of 20M x 16 plus its copy took 0.9 s of the 20M fit; every rank
+    # draws the whole block (same seed) and keeps its rows
     g = torch.Generator(device=dev).manual_seed(int(seed))
     Y = torch.randn((n, p), generator=g, device=dev)
     Y[:, 0] = torch.sqrt(deg).float()
-    Y = _cholqr2(Y)
+    Y = Y[lo:hi].contiguous()
+    Y = _cholqr2(Y, ctx)
 
     def amul(V: torch.Tensor) -> torch.Tensor:
-        return 0.5 * (ops.csr_spmm(M, V) + V)  # (M + I) / 2: eigenvalues in [0, 1], order kept
+        Vf = gather_rows(V.contiguous(), ctx)
+        return 0.5 * (ops.csr_spmm(M, Vf) + V)  # (M + I) / 2: eigenvalues in [0, 1], order kept
+
+    def ritz_matrix(Yb: torch.Tensor, Zb: torch.Tensor) -> np.ndarray:
+        T = ops.dgemm(Yb.double().contiguous(), Zb.double().contiguous(), ta=True)
+        return _allreduce(T.contiguous(), ctx).cpu().numpy()
 
     prev = None
     it = 0
@@ -275,7 +313,7 @@ def _spectral_device(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor,
         while it < iters:
             Z = amul(Y)
             it += 1
-            T = ops.dgemm(Y.double().contiguous(), Z.double().contiguous(), ta=True).cpu().numpy()
+            T = ritz_matrix(Y, Z)
             allr = np.sort(np.linalg.eigvalsh((T + T.T) * 0.5))[::-1]
             ritz = allr[: dim + 1]
             if prev is not None and it >= min_iters and \
@@ -284,19 +322,19 @@ def _spectral_device(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor,
             prev = ritz
             bcut = float(min(max(allr[-1], 0.0), allr[dim]))
             if bcut >= 0.995 or it + CHEB_DEGREE > iters:
-                Y = _cholqr2(Z)  # spectrum too clustered for the filter: a plain step
+                Y = _cholqr2(Z, ctx)  # spectrum too clustered for the filter: a plain step
                 continue
             e, c = 0.5 * bcut, 0.5 * bcut
             Y0, Y1 = Y, (Z - c * Y) / e
             for _ in range(CHEB_DEGREE - 1):
                 Y0, Y1 = Y1, 2.0 * (amul(Y1) - c * Y1) / e - Y0
                 it += 1
-            Y = _cholqr2(Y1)
+            Y = _cholqr2(Y1, ctx)
     while CHEB_DEGREE <= 1 and it < iters:
         Z = amul(Y)
         it += 1
         if it % 5 == 1:  # Y is orthonormal here: Ritz values of the current subspace
-            T = ops.dgemm(Y.double().contiguous(), Z.double().contiguous(), ta=True).cpu().numpy()
+            T = ritz_matrix(Y, Z)
             ritz = np.sort(np.linalg.eigvalsh((T + T.T) * 0.5))[::-1][: dim + 1]
             if prev is not None and it >= min_iters and \
                     np.max(np.abs(ritz - prev)) <= tol * max(float(np.max(np.abs(ritz))), 1e-30):
@@ -305,15 +343,19 @@ def _spectral_device(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor,
             prev = ritz
         Y = Z
         if it % 5 == 0:
-            Y = _cholqr2(Y)
-    Y = _cholqr2(Y)
+            Y = _cholqr2(Y, ctx)
+    Y = _cholqr2(Y, ctx)
     Z = amul(Y)
     # Y^T Z: K = n rows in the millions -> the split-K fp64 MFMA GEMM (ordered fold)
     Yd = Y.double().contiguous()
-    T = ops.dgemm(Yd, Z.double().contiguous(), ta=True)
-    w, V = np.linalg.eigh(T.cpu().numpy())
+    w, V = np.linalg.eigh(ritz_matrix(Y, Z))
     order = np.argsort(w)[::-1][1: dim + 1].copy()
-    return ops.dgemm(Yd, torch.from_numpy(np.ascontiguousarray(V[:, order])).to(dev)).float()
+    out = gather_rows(ops.dgemm(Yd, torch.from_numpy(np.ascontiguousarray(V[:, order])).to(dev)).float().contiguous(),
+                      ctx)
+    record_phase(phases, "spectral", hi - lo, t0, dev)
+    if phases is not None:
+        phases["spectral"]["products"] = it + 1
+    return out
 
 
 def _spectral_dense_device(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n: int, dim: int) -> torch.Tensor:
@@ -330,15 +372,19 @@ def _spectral_dense_device(rows: torch.Tensor, cols: torch.Tensor, vals: torch.T
     return V[:, 1: dim + 1].float().contiguous()
 
 
-def spectral_init(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n: int, dim: int, seed: int) -> torch.Tensor:
+def spectral_init(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n: int, dim: int, seed: int,
+                  ctx: Any = None, phases: Optional[dict] = None) -> torch.Tensor:
+    """Spectral layout (identical on every rank of a distributed fit: the large-graph subspace
+    iteration runs row-partitioned over the ranks, the small cases are computed redundantly)."""
     dev = vals.device
-    if dev.type != "cuda":
+    dist = ctx is not None and ctx.world_size > 1
+    if n > SPECTRAL_DENSE_N and (dev.type == "cuda" or dist):
+        coords = _spectral_device(rows, cols, vals, n, dim, seed, ctx=ctx, phases=phases)
+    elif dev.type != "cuda":
         coords = torch.from_numpy(_spectral_host(rows.cpu().numpy(), cols.cpu().numpy(), vals.cpu().numpy(), n, dim,
                                                  seed)).float().to(dev)
-    elif n <= SPECTRAL_DENSE_N:
-        coords = _spectral_dense_device(rows, cols, vals, n, dim)
     else:
-        coords = _spectral_device(rows, cols, vals, n, dim, seed)
+        coords = _spectral_dense_device(rows, cols, vals, n, dim)
     expansion = 10.0 / coords.abs().max().clamp_min(1e-30)
     g = torch.Generator(device=dev).manual_seed(int(seed) + 1)
     return coords * expansion + torch.randn(coords.shape, generator=g, device=dev) * 1e-4
@@ -352,7 +398,7 @@ def make_epochs_per_sample(w: torch.Tensor, n_epochs: int) -> torch.Tensor:
 def optimize_layout(emb_head: torch.Tensor, emb_tail: torch.Tensor, head: torch.Tensor, tail: torch.Tensor,
                     w: torch.Tensor, n_epochs: int, a: float, b: float, gamma: float, initial_alpha: float,
                     negative_sample_rate: float, move_other: bool, seed: int, ctx: Any = None,
-                    pull: bool = False) -> torch.Tensor:
+                    pull: bool = False, phases: Optional[dict] = None) -> torch.Tensor:
     """SGD epochs over the fuzzy-graph edges.
 
     Distributed (``ctx.world_size > 1``, identical graph and layout on every rank): rank r
@@ -371,6 +417,8 @@ def optimize_layout(emb_head: torch.Tensor, emb_tail: torch.Tensor, head: torch.
         head, tail, eps = head[shard], tail[shard], eps[shard]
         seed = (int(seed) + 0x9E3779B1 * ctx.rank) & 0x7FFFFFFF
     head, tail, eps = head.int().contiguous(), tail.int().contiguous(), eps.contiguous()
+    if phases is not None:
+        phases["epochs"] = {"rows": int(head.shape[0])}  # this rank's edges
     eps_neg = (eps / float(negative_sample_rate)).contiguous()
     next_sample = eps.clone()
     next_neg = eps_neg.clone()
@@ -406,11 +454,20 @@ def _n_epochs_default(n: int) -> int:
 def umap_fit(X: torch.Tensor, params: Dict[str, Any], y: Optional[torch.Tensor] = None, ctx: Any = None) -> np.ndarray:
     """Embedding (N x n_components, float32) of the rows of X.
 
-    ``ctx`` with ``world_size > 1`` (X replicated on every rank): the kNN graph is built
-    row-block / tile-range parallel and all-gathered, the fuzzy set is computed identically on
-    every rank, rank 0's initial layout is broadcast and the SGD epochs run edge-parallel
-    across ranks with one RCCL all-reduce of the layout deltas per epoch (``optimize_layout``).
+    ``ctx`` with ``world_size > 1`` (X replicated on every rank): every phase shards over the
+    ranks — the IVF quantiser's Lloyd iterations (1/W of the training sample each, sums
+    all-reduced), the bucketing (1/W of the rows each, labels all-gathered), the kNN lists (a
+    work-balanced range of query tiles, rows all-gathered), the spectral subspace iteration
+    (row-partitioned SpMM, all-gathered block per product, all-reduced p x p Grams) and the SGD
+    epochs (edge-parallel, one RCCL all-reduce of the layout deltas per epoch,
+    ``optimize_layout``); only the fuzzy union (kNN-structured, ~0.06 s at 20M) is computed on
+    every rank. ``LAST_PHASES`` holds this rank's per-phase rows and seconds of the last fit.
     """
+    import time
+
+    phases: Dict[str, Any] = {}
+    LAST_PHASES.clear()
+    t_ph = time.perf_counter()
     N = X.shape[0]
     k = int(min(params.get("n_neighbors", 15), N))
     dim = int(params.get("n_components", 2))
@@ -439,8 +496,9 @@ def umap_fit(X: torch.Tensor, params: Dict[str, Any], y: Optional[torch.Tensor] 
         from .knn_graph import build_knn_graph
 
         g = build_knn_graph(Xf, k, params.get("build_algo", "auto"), params.get("build_kwds"), seed, ctx,
-                            list_order=LIST_ORDER)
+                            list_order=LIST_ORDER, phases=phases)
         dist, idx, order = g if LIST_ORDER else (g[0], g[1], None)
+        t_ph = time.perf_counter()  # the graph's phases are logged inside (synchronised)
         if metric in ("cosine", "correlation"):
             dist = 0.5 * dist * dist  # 1 - cos for unit rows
         elif metric == "sqeuclidean":
@@ -465,21 +523,23 @@ def umap_fit(X: torch.Tensor, params: Dict[str, Any], y: Optional[torch.Tensor] 
     n_epochs = params.get("n_epochs")
     n_epochs = int(n_epochs) if n_epochs else _n_epochs_default(N)
     init = params.get("init", "spectral")
-    if dist_ctx is None or dist_ctx.rank == 0:
-        if isinstance(init, str) and init == "spectral" and N > dim + 1:
-            emb = spectral_init(rows, cols, vals, N, dim, seed)
-        else:
-            g = torch.Generator(device=X.device).manual_seed(seed)
-            emb = torch.rand((N, dim), generator=g, device=X.device) * 20.0 - 10.0
-        mn, mx = emb.min(0).values, emb.max(0).values
-        emb = (10.0 * (emb - mn) / (mx - mn).clamp_min(1e-30)).float().contiguous()
+    from .knn_graph import record_phase
+
+    record_phase(phases, "fuzzy_union", N, t_ph, X.device)
+    # every rank computes the same initial layout (the spectral iteration row-partitioned)
+    if isinstance(init, str) and init == "spectral" and N > dim + 1:
+        emb = spectral_init(rows, cols, vals, N, dim, seed, ctx=dist_ctx, phases=phases)
     else:
-        emb = torch.empty((N, dim), dtype=torch.float32, device=X.device)
-    if dist_ctx is not None:  # one initial layout for every rank
-        emb = dist_ctx.comm.broadcast(emb, 0)
+        g = torch.Generator(device=X.device).manual_seed(seed)
+        emb = torch.rand((N, dim), generator=g, device=X.device) * 20.0 - 10.0
+    mn, mx = emb.min(0).values, emb.max(0).values
+    emb = (10.0 * (emb - mn) / (mx - mn).clamp_min(1e-30)).float().contiguous()
+    t_ep = time.perf_counter()
     optimize_layout(emb, emb, rows, cols, vals, n_epochs, a, b, float(params.get("repulsion_strength", 1.0)),
                     float(params.get("learning_rate", 1.0)), float(params.get("negative_sample_rate", 5)), True, seed,
-                    ctx=dist_ctx, pull=PULL)
+                    ctx=dist_ctx, pull=PULL, phases=phases)
+    record_phase(phases, "epochs", phases.get("epochs", {}).get("rows", 0), t_ep, X.device)
+    LAST_PHASES.update(phases)
     if order is not None:
         out = torch.empty_like(emb)
         out[order] = emb

@@ -135,6 +135,13 @@ class WorkerContext:
     device_outputs: bool = False
 
     @property
+    def distributed(self) -> bool:
+        """The fit takes the multi-rank code path: world_size > 1, or a one-rank communicator over
+        a live process group (``SRML_COMM_FORCE_PG=1``: the per-rank proxy runs the collectives and
+        the multi-rank kernels of an N-GPU fit on one GPU)."""
+        return self.world_size > 1 or not getattr(self.comm, "_solo", True)
+
+    @property
     def is_gpu(self) -> bool:
         return self.device.type == "cuda"
 
