@@ -34,6 +34,9 @@ import numpy as np
 import torch
 
 QN_GRAPH = os.environ.get("SRML_QN_GRAPH", "1") != "0"
+# multi-rank fits: capture the batch INCLUDING its all-reduces (RCCL collectives recorded into the
+# HIP graph, replayed identically on every rank); SRML_QN_GRAPH_COMM=0 keeps them eager
+QN_GRAPH_COMM = os.environ.get("SRML_QN_GRAPH_COMM", "1") != "0"
 # the optimiser step for N <= 16384: "mb" (default) = four multi-block launches (srml_qn_step_mb;
 # a one-rank binary LogReg fit folds the evaluation's partial rows in the first: srml_qn_step_mbf);
 # "fused" = ONE launch with software grid barriers (srml_qn_step_fused, folds likewise);
@@ -358,6 +361,17 @@ class DeviceQN:
 
 
 # ------------------------------------------------------------------------------------------
+def _graph_capturable(allreduce: Callable) -> bool:
+    """Whether a bound ``Communicator.allreduce`` can be recorded into a HIP graph: RCCL
+    collectives can (one-shot and host-staged gloo ones cannot: a per-call epoch / a host copy)."""
+    comm = getattr(allreduce, "__self__", None)
+    if comm is None or getattr(comm, "backend", "none") != "nccl":
+        return False
+    from ..parallel import oneshot
+
+    return oneshot.comm_mode() == "rccl"
+
+
 def _comm_poll(allreduce: Optional[Callable]) -> Optional[Callable[[], None]]:
     """The non-blocking error poll of the communicator behind a bound ``allreduce`` (if any)."""
     return getattr(getattr(allreduce, "__self__", None), "poll", None)
@@ -417,7 +431,7 @@ def minimize(P: QNProblem, theta0: np.ndarray, evaluate: Callable[[torch.Tensor,
     # one-rank fits on a single-launch evaluation replay the batch as ONE HIP graph: 2 x batch
     # kernels with no per-launch host work (the first batch runs eagerly: one-time kernel set-up)
     graph = None
-    use_graph = graph_safe and allreduce is None and QN_GRAPH
+    use_graph = graph_safe and QN_GRAPH and (allreduce is None or (QN_GRAPH_COMM and _graph_capturable(allreduce)))
     while evals < cap:
         if graph is not None:
             graph.replay()
@@ -430,14 +444,22 @@ def minimize(P: QNProblem, theta0: np.ndarray, evaluate: Callable[[torch.Tensor,
                 graph = torch.cuda.CUDAGraph()
                 side = torch.cuda.Stream(device)
                 side.wait_stream(stream)
-                with torch.cuda.stream(side):
-                    graph.capture_begin()
-                    try:
-                        run_batch()
-                    finally:
-                        graph.capture_end()
+                try:
+                    with torch.cuda.stream(side):
+                        graph.capture_begin()
+                        try:
+                            run_batch()
+                        finally:
+                            graph.capture_end()
+                    GRAPH_STATS["captures"] += 1
+                except RuntimeError:
+                    if allreduce is None:
+                        raise
+                    # a backend that cannot record its collective: the remaining batches run
+                    # eagerly (the failed capture executed nothing)
+                    graph, use_graph = None, False
+                    GRAPH_STATS["comm_capture_failed"] = GRAPH_STATS.get("comm_capture_failed", 0) + 1
                 stream.wait_stream(side)
-                GRAPH_STATS["captures"] += 1
                 # capture records without running: the captured batch is still to be executed
                 # (replayed at the top of the next pass)
         evals += batch

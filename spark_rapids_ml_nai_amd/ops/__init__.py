@@ -1335,7 +1335,8 @@ def rf_route_segments(bins: torch.Tensor, idx: torch.Tensor, bounds: torch.Tenso
 
 def rf_sample_features(C: int, n: int, nf: int, seed: int, device: torch.device) -> torch.Tensor:
     """(C, nf) int32: per node a uniform random subset of nf of n features, ascending
-    (``srml_rf_sample_features``, selection sampling; CPU: the same draw order in numpy)."""
+    (``srml_rf_sample_features``: Floyd's algorithm for sparse subsets, nf <= n / 8, else
+    selection sampling; CPU: numpy's own uniform subsets)."""
     seed &= (1 << 64) - 1
     if device.type != "cuda":
         rng = np.random.default_rng(seed)

@@ -92,6 +92,7 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_split_bf16x3_tiled_centered_rows": (_P, _L, _P, _L, _I, _P, _I, _L, _P, _P),
     "srml_row_sqnorm_centered_f32": (_P, _L, _I, _L, _P, _P, _P),
     "srml_row_sqnorm_centered_amax_f32": (_P, _L, _I, _L, _P, _P, _P, _P),
+    "srml_rf_sample_features_floyd": (_I, _I),
     "srml_rf_bootstrap_ws": (_I, _L),
     "srml_rf_bootstrap": (_I, _L, _D, ctypes.c_ulonglong, _P, _P, _P, _P, _P),
     "srml_split_f16_tiled_centered": (_P, _L, _I, _L, _P, _I, _L, _F, _P, _P, _P),

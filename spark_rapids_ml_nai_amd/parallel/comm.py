@@ -419,6 +419,9 @@ class CommStats:
             self.calls += 1
             self.bytes += int(nbytes)
             self.wire_bytes += float(nbytes if wire_bytes is None else wire_bytes)
+        if device is not None and device.type == "cuda" and torch.cuda.is_current_stream_capturing():
+            yield  # recorded into a HIP graph (the QN batch): counted, not timed
+            return
         if device is not None and device.type == "cuda" and _rank_timers_enabled():
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()

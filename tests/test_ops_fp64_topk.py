@@ -5,6 +5,7 @@ import pytest
 import torch
 
 from spark_rapids_ml_nai_amd import ops
+from spark_rapids_ml_nai_amd.ops import native
 from spark_rapids_ml_nai_amd.utils import determinism
 
 
@@ -452,10 +453,53 @@ def _algorithm_s_np(C: int, n: int, nf: int, seed: int) -> np.ndarray:
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("C,n,nf", [(37, 3000, 1000), (9, 70, 9), (5, 64, 64), (6, 129, 1)])
+@pytest.mark.parametrize("C,n,nf", [(37, 3000, 1000), (9, 70, 9), (5, 64, 64), (6, 129, 17)])
 def test_rf_sample_features_matches_algorithm_s(gpu_device, C, n, nf):
     """The wave-parallel selection sampling (64 features per step, integer thresholds resolved by a
-    scalar pass) is bit-identical to the sequential Algorithm S on the same draws."""
+    scalar pass; dense subsets, nf > n / 8) is bit-identical to the sequential Algorithm S on the
+    same draws."""
+    assert int(native.lib().srml_rf_sample_features_floyd(n, nf)) == 0
     seed = 0x9E3779B97F4A7C15 ^ (C * n + nf)
     got = ops.rf_sample_features(C, n, nf, seed, gpu_device).cpu().numpy()
     np.testing.assert_array_equal(got, _algorithm_s_np(C, n, nf, seed))
+
+
+def _floyd_np(C: int, n: int, nf: int, seed: int) -> np.ndarray:
+    """Floyd's algorithm with the kernel's counter-based draws (u_i from splitmix64(base + i)),
+    one node at a time in numpy, ascending output."""
+    M = (1 << 64) - 1
+    out = np.zeros((C, nf), dtype=np.int32)
+    for c in range(C):
+        base = int(ops._mix64_np(np.array([(seed ^ int(ops._mix64_np(np.array([c + 1], dtype=np.uint64))[0])) & M],
+                                          dtype=np.uint64))[0])
+        u = (ops._mix64_np(np.uint64(base) + np.arange(nf, dtype=np.uint64)) >> np.uint64(11)).astype(np.float64)
+        u *= 2.0 ** -53
+        taken = set()
+        for i in range(nf):
+            j = n - nf + i
+            t = min(int(np.floor(u[i] * float(j + 1))), j)
+            taken.add(j if t in taken else t)
+        out[c] = np.sort(np.fromiter(taken, dtype=np.int64)).astype(np.int32)
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C,n,nf", [(41, 3000, 55), (7, 5000, 71), (5, 12000, 300), (9, 64, 8), (3, 16384, 2048),
+                                    (6, 129, 1)])
+def test_rf_sample_features_floyd_matches_oracle(gpu_device, C, n, nf):
+    """Sparse subsets take Floyd's algorithm (registers as the membership bitmap): bit-identical to
+    a sequential Floyd on the same draws, ascending and distinct."""
+    assert int(native.lib().srml_rf_sample_features_floyd(n, nf)) == 1
+    seed = 0x5DEECE66D ^ (C * n + nf)
+    got = ops.rf_sample_features(C, n, nf, seed, gpu_device).cpu().numpy()
+    np.testing.assert_array_equal(got, _floyd_np(C, n, nf, seed))
+
+
+@pytest.mark.gpu
+def test_rf_sample_features_floyd_uniform(gpu_device):
+    C, n, nf = 20000, 3000, 55
+    f = ops.rf_sample_features(C, n, nf, 777, gpu_device).cpu()
+    assert bool((f[:, 1:] > f[:, :-1]).all())
+    freq = torch.bincount(f.reshape(-1).long(), minlength=n).double() / C
+    p = nf / n  # each feature's inclusion probability; binomial sd sqrt(p (1 - p) / C) ~ 1e-3
+    assert (freq - p).abs().max().item() < 6 * (p * (1 - p) / C) ** 0.5

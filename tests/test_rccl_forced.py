@@ -57,6 +57,17 @@ with use_context(ctx):
         m = est.fit(df)
         fits[name] = m._rank_stats[0]
 out["fits"] = fits
+from spark_rapids_ml_nai_amd.models import qn as qnm
+out["qn_graph"] = dict(qnm.GRAPH_STATS)
+# the same LogReg on the one-rank path (no collectives): the captured-RCCL fit must equal it
+os.environ["SRML_COMM_FORCE_PG"] = "0"
+ctx1 = WorkerContext.single(dev)
+with use_context(ctx1):
+    m1 = LogisticRegression(maxIter=20).fit(df)
+os.environ["SRML_COMM_FORCE_PG"] = "1"
+with use_context(ctx):
+    m2 = LogisticRegression(maxIter=20).fit(df)
+out["lr_same"] = bool(np.allclose(np.asarray(m1.coef_), np.asarray(m2.coef_), rtol=1e-5, atol=1e-8))
 print("RESULT " + json.dumps(out))
 dist.destroy_process_group()
 """
@@ -78,8 +89,13 @@ def test_rccl_paths_on_one_gpu():
     for k in ("allreduce_ok", "allgatherv_ok", "bytes_ok", "bcast_ok", "sendrecv_ok", "single_node"):
         assert out[k], (k, out)
     assert out["stats_calls"] > 0 and out["stats_s"] > 0
+    # the LogReg batches (small shard: graph-safe) were captured WITH their RCCL all-reduces
+    assert out["qn_graph"]["captures"] >= 1 and out["qn_graph"].get("comm_capture_failed", 0) == 0, out["qn_graph"]
+    assert out["lr_same"]
     for name, st in out["fits"].items():
-        assert st["comm_calls"] > 0 and st["comm_s"] > 0, (name, st)
+        assert st["comm_calls"] > 0, (name, st)
+        if name != "logreg":  # captured collectives are counted, not timed
+            assert st["comm_s"] > 0, (name, st)
         parts = st["h2d_exposed_s"] + st["compute_s"] + st["comm_s"]
         assert abs(parts - st["wall_s"]) <= 0.05 * st["wall_s"] + 1e-6, (name, st)
 

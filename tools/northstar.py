@@ -34,6 +34,9 @@ CONFIGS = {
     "logreg": (200_000_000, 256, "classification"),
     "rf": (50_000_000, 64, "classification"),
     "umap": (20_000_000, 128, "blobs"),
+    # the same fit on non-blob rows: the reference-faithful classification generator (2 clusters
+    # per class with random covariances, redundant mixes, shuffled columns)
+    "umap_cls": (20_000_000, 128, "classification"),
 }
 
 
@@ -60,7 +63,7 @@ def _estimator(name: str, world: int):
         # all-reduced; SRML_NS_RF_MODE=ensemble gives the reference's tree-split ensemble instead
         return RandomForestClassifier(numTrees=100, maxDepth=16, maxBins=128, seed=1, featuresCol="features",
                                       labelCol="label", split_mode=os.environ.get("SRML_NS_RF_MODE", "data_parallel"))
-    if name == "umap":
+    if name.startswith("umap"):
         from spark_rapids_ml_nai_amd.umap import UMAP
 
         return UMAP(n_neighbors=15, n_components=2, random_state=1, featuresCol="features")
@@ -167,6 +170,21 @@ def _umap_quality(model, Xh, device, sample: int = 20_000, small_fit: bool = Tru
             "trustworthiness_small_fit": round(t_small, 5), "trust_gap": round(t_small - t_big, 5)}
 
 
+def _ivf_recall(Xh, device, sample: int = 100_000, k: int = 15) -> dict:
+    """Recall of the IVF all-points graph (the UMAP fit's builder, default list size / nprobe)
+    against the exact kNN on a row sample of the fitted data."""
+    from spark_rapids_ml_nai_amd.models.knn_graph import knn_graph, knn_graph_ivf
+
+    n = Xh.shape[0]
+    idx = np.sort(np.random.default_rng(1).choice(n, size=min(sample, n), replace=False))
+    Xs = torch.from_numpy(np.ascontiguousarray(Xh[idx])).to(device).float()
+    _, gi = knn_graph_ivf(Xs, k, seed=1)
+    _, ei = knn_graph(Xs, Xs, k)
+    gi, ei = gi.cpu().numpy(), ei.cpu().numpy()
+    hit = np.mean([len(set(a.tolist()) & set(b.tolist())) / float(k) for a, b in zip(gi, ei)])
+    return {"ivf_recall_sample": int(idx.size), "ivf_recall_at_15": round(float(hit), 5)}
+
+
 def main() -> None:
     if os.environ.get("SRML_NS_STACKDUMP"):  # periodic all-thread stacks (diagnosing a stuck rank)
         import faulthandler
@@ -248,11 +266,16 @@ def main() -> None:
                     pred = model.transform(DataFrame.from_numpy(Xq, yq)).to_numpy("prediction")
                     rec["holdout_accuracy"] = round(float((pred == yq).mean()), 5)
                     del Xq, yq
-            if name == "umap":
+            if name.startswith("umap"):
                 emb = np.asarray(model.embedding_)
                 rec["finite"] = bool(np.isfinite(emb).all())
+                from spark_rapids_ml_nai_amd.models import umap as _U
+
+                # this rank's per-phase rows / seconds of the timed fit (before the quality fit)
+                rec["umap_phases"] = json.loads(json.dumps(_U.LAST_PHASES))
                 if rank == 0:
                     rec.update(_umap_quality(model, Xh, device, small_fit=world == 1))
+                    rec.update(_ivf_recall(Xh, device))
             del model, df, Xh, yh
         except Exception as e:  # noqa: BLE001
             rec["error"] = repr(e)[:500]
