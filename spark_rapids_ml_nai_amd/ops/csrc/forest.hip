@@ -1004,11 +1004,15 @@ __global__ __launch_bounds__(256) void rf_sample_features_floyd_kernel(int C, in
     int t = (int)floor(u * (double)(j + 1));
     t = t > j ? j : t;
     // is t taken? word t >> 6 = register (t >> 12) of lane (t >> 6) & 63 (t is wave-uniform)
-    unsigned long long wt = 0ull;
+    // (readlane moves 32 bits: read the half of the word that holds bit t)
+    unsigned wt = 0u;
 #pragma unroll
     for (int q = 0; q < W; ++q)
-      if (q == (t >> 12)) wt = __builtin_amdgcn_readlane(w[q], (t >> 6) & 63);
-    const int pick = ((wt >> (t & 63)) & 1ull) ? j : t;
+      if (q == (t >> 12)) {
+        const unsigned half = (unsigned)(w[q] >> (t & 32));
+        wt = __builtin_amdgcn_readlane(half, (t >> 6) & 63);
+      }
+    const int pick = ((wt >> (t & 31)) & 1u) ? j : t;
 #pragma unroll
     for (int q = 0; q < W; ++q)
       if (q == (pick >> 12) && lane == ((pick >> 6) & 63)) w[q] |= 1ull << (pick & 63);
