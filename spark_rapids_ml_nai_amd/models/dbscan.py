@@ -57,14 +57,7 @@ def dbscan_fit_predict(X_local: torch.Tensor, ctx: WorkerContext, eps: float, mi
             if r != ctx.rank:
                 ops.uf_unite_pairs(parent, forests[r].to(X.device))
     ops.uf_compress(parent)
-    corb = core.bool()
-    root = parent.long()
-    has_core_nb = best != -1
-    nb = (best & 0xFFFFFFFF).clamp(0, max(N - 1, 0))
-    lab_root = torch.where(corb, root, torch.where(has_core_nb, root[nb], torch.full_like(root, -1)))
-    roots = torch.unique(root[corb])  # sorted ascending
-    labels = torch.full((N,), -1, dtype=torch.int64, device=X.device)
-    m = lab_root >= 0
-    labels[m] = torch.searchsorted(roots, lab_root[m])
+    # clusters numbered by ascending root (root-flag prefix scan on the device)
+    labels = ops.dbscan_labels(parent, core, best)
     sl = slice(start, start + X_local.shape[0])
     return labels[sl].cpu().numpy(), core[sl].bool().cpu().numpy()

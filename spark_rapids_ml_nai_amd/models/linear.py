@@ -67,8 +67,42 @@ def lsq_stats(X: torch.Tensor, y: torch.Tensor, m_total: int, ctx: WorkerContext
                     st.y_sumsq / mt)
 
 
+def _min_norm_prox(A: torch.Tensor, b: torch.Tensor, max_iter: int = 40, rtol: float = 1e-13) -> torch.Tensor:
+    """Minimum-norm solution of singular PSD normal equations by the proximal-point (iterated
+    Tikhonov) recursion x <- (A + d I)^-1 (b + d x) from x = 0: null-space components stay zero,
+    an eigen-direction with eigenvalue l converges at rate d / (l + d). One Cholesky of A + d I
+    (d = 1e-7 max diag A, well conditioned), then two triangular sweeps per step — the n > 4096
+    counterpart of the eigen path (cuML's eigDC fallback, regression.py:508-560). The rounding
+    component of b in the null space grows the iterate by ~eps |b| / d per step; the recursion
+    stops when the step size stops shrinking geometrically (that drift dominates), so the result
+    agrees with the eigen pseudo-inverse to ~1e-8 relative; eigenvalues below ~1e-5 max diag are
+    only partly resolved (directions that ill-posed have no stable min-norm answer in fp64)."""
+    n = A.shape[0]
+    d = max(float(A.diagonal().max()), 1e-300) * 1e-7
+    L, ok = ops.spd_factor(A + d * torch.eye(n, dtype=A.dtype, device=A.device))
+    if not ok:
+        return _min_norm_eig(A, b)
+    x = ops.spd_factor_solve(L, b)
+    prev = float("inf")
+    for _ in range(max_iter):
+        x1 = ops.spd_factor_solve(L, b + d * x)
+        step = float(torch.linalg.vector_norm(x1 - x))
+        x = x1
+        if step <= rtol * float(torch.linalg.vector_norm(x1)) or step > 0.5 * prev:
+            break
+        prev = step
+    return x
+
+
 def _min_norm_solve(A: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """Singular normal equations: minimum-norm least-squares solution (eigen-solver fallback)."""
+    """Singular normal equations: minimum-norm least-squares solution (device Jacobi eigensolver
+    up to n = 4096, the proximal-point Cholesky recursion beyond)."""
+    if A.is_cuda and A.shape[0] > 4096:
+        return _min_norm_prox(A, b)
+    return _min_norm_eig(A, b)
+
+
+def _min_norm_eig(A: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     w, V = ops.syevj(A) if A.is_cuda and A.shape[0] <= 4096 else torch.linalg.eigh(A)
     tol = max(float(w.max()), 0.0) * A.shape[0] * float(np.finfo(np.float64).eps)
     inv = torch.where(w > tol, 1.0 / torch.where(w > tol, w, torch.ones_like(w)), torch.zeros_like(w))

@@ -171,6 +171,13 @@ def fuzzy_union(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n: i
 def categorical_intersection(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, y: torch.Tensor,
                              n: int, unknown_dist: float = 1.0, far_dist: float = 5.0
                              ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    if vals.is_cuda:
+        # the device union is (row, col)-sorted with a symmetric pattern: native kernel, same edges
+        r64 = rows.long()
+        if r64.numel() < 2 or bool((r64[1:] >= r64[:-1]).all()):
+            out = ops.umap_categorical(r64, cols.long(), vals, y, n, unknown_dist, far_dist)
+            keep = out > 0
+            return r64[keep], cols.long()[keep], out[keep]
     yr, yc = y[rows], y[cols]
     unknown = (yr == -1) | (yc == -1)
     differ = (yr != yc) & ~unknown
@@ -268,8 +275,11 @@ def _spectral_device(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor,
     dev = vals.device
     r64 = rows.long()
     if r64.numel() > 1 and not bool((r64[1:] >= r64[:-1]).all()):
-        order = torch.argsort(r64 * n + cols.long())
-        r64, cols, vals = r64[order], cols[order], vals[order]
+        # (row, col) order: the in-tree LSD radix sort of the packed keys carries the values
+        keys = (r64 * n + cols.long()).contiguous()
+        vals = vals.float().contiguous().clone()
+        ops.radix_sort_pairs(keys, vals, max(1, int(n * n).bit_length()))
+        r64, cols = keys // n, keys % n
     # rows are sorted: the CSR row pointer is a binary search per row boundary (no atomics), and
     # the degrees are the row sums of the same CSR (one pass of the SpMM kernel against a ones
     # column; an fp64 index_add over the ~15 n edges cost 0.3 s of atomics at n = 20M)

@@ -1905,6 +1905,27 @@ def uf_unite_pairs(parent: torch.Tensor, other: torch.Tensor) -> None:
                 native.stream(parent.device))
 
 
+def dbscan_labels(parent: torch.Tensor, core: torch.Tensor, best: torch.Tensor) -> torch.Tensor:
+    """int64 cluster labels from the compressed forest (roots = each component's smallest core
+    index), the core flags (uint8) and ``best`` (nearest core neighbour in the low 32 bits, -1 =
+    none): clusters numbered by ascending root, border points take their core neighbour's cluster,
+    noise is -1. Device: ``srml_dbscan_labels`` (root-flag prefix scan; no unique / sort)."""
+    N = parent.shape[0]
+    if not parent.is_cuda:
+        corb = core.bool()
+        root = parent.long()
+        nb = (best & 0xFFFFFFFF).clamp(0, max(N - 1, 0))
+        lab_root = torch.where(corb, root, torch.where(best != -1, root[nb], torch.full_like(root, -1)))
+        is_root = corb & (root == torch.arange(N, device=parent.device))
+        cid = torch.cumsum(is_root.long(), 0) - is_root.long()
+        return torch.where(lab_root >= 0, cid[lab_root.clamp_min(0)], torch.full_like(lab_root, -1))
+    out = torch.empty(N, dtype=torch.int64, device=parent.device)
+    ws = torch.empty(int(native.lib().srml_dbscan_labels_ws(N)), dtype=torch.int32, device=parent.device)
+    native.call("srml_dbscan_labels", _c(parent.int()).data_ptr(), _c(core.to(torch.uint8)).data_ptr(),
+                _c(best.long()).data_ptr(), N, out.data_ptr(), ws.data_ptr(), native.stream(parent.device))
+    return out
+
+
 def uf_compress(parent: torch.Tensor) -> None:
     """Point every node directly at its root (the smallest index of its component)."""
     if not parent.is_cuda:
@@ -1940,13 +1961,14 @@ def knn_refine_sort(Q: torch.Tensor, X: torch.Tensor, pos: torch.Tensor, inner_p
     squared euclidean, or -2 q.x for ``inner_product`` — sorted ascending per row (ties keep the
     candidate order; missing candidates last at +inf): (d fp32, pos int64), both (mq, k).
     ``srml_knn_refine_sort_f32`` (one wave per query, no gathered copy of the rows) for fp32
-    device data with n <= 1024: k <= 64 in one launch; larger k in 64-candidate column panels,
+    device data (n <= 1024 from registers, wider rows stream the tail): k <= 64 in one launch;
+    larger k in 64-candidate column panels,
     each re-scored and sorted by the kernel, merged by the radix-select kernel (``topk_rows``,
     ties keep the candidate order). None otherwise (the caller keeps its torch path)."""
     mq, k = pos.shape
     n = Q.shape[1]
     if (not Q.is_cuda or Q.dtype != torch.float32 or X.dtype != torch.float32 or k < 1 or k > TOPK_KMAX
-            or n > 1024 or n < 1 or Q.stride(1) != 1 or X.stride(1) != 1):
+            or n < 1 or Q.stride(1) != 1 or X.stride(1) != 1):
         return None
     if k > 64:
         parts = [knn_refine_sort(Q, X, pos[:, c0: c0 + 64], inner_product) for c0 in range(0, k, 64)]
@@ -1999,6 +2021,21 @@ def umap_fuzzy_union_knn(idx: torch.Tensor, w: torch.Tensor, mix: float = 1.0
     nk = int(kept.item())
     keys = keys[:nk]
     return keys // m, keys % m, vals[:nk]
+
+
+def umap_categorical(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, y: torch.Tensor, n: int,
+                     unknown_dist: float = 1.0, far_dist: float = 5.0, mix: float = 1.0) -> torch.Tensor:
+    """New values of the (row, col)-sorted, pattern-symmetric fuzzy union after the categorical
+    intersection with labels ``y`` (-1 = unknown) and the re-normalised fuzzy union
+    (``srml_umap_categorical``: binary-searched transposes, no sort); same pattern and order."""
+    nnz = rows.shape[0]
+    dev = vals.device
+    out = torch.empty(nnz, dtype=torch.float32, device=dev)
+    ws = torch.empty(int(native.lib().srml_umap_categorical_ws(n, nnz)), dtype=torch.float64, device=dev)
+    native.call("srml_umap_categorical", _c(rows.long()).data_ptr(), _c(cols.long()).data_ptr(),
+                _c(vals.float()).data_ptr(), nnz, _c(y.long()).data_ptr(), n, float(unknown_dist), float(far_dist),
+                float(mix), out.data_ptr(), ws.data_ptr(), native.stream(dev))
+    return out
 
 
 def umap_epoch(head: torch.Tensor, tail: torch.Tensor, eps: torch.Tensor, next_sample: torch.Tensor,
@@ -2123,6 +2160,27 @@ def spd_solve(A: torch.Tensor, b: torch.Tensor) -> Tuple[torch.Tensor, bool]:
     x = b.double().contiguous().clone()
     native.call("srml_potrs_f64", L.data_ptr(), n, L.stride(0), x.data_ptr(), st)
     return x, int(info.item()) == 0
+
+
+def spd_factor(A: torch.Tensor) -> Tuple[torch.Tensor, bool]:
+    """Cholesky factor of a symmetric positive definite fp64 matrix (``srml_potrf_f64`` on the
+    device), for repeated ``spd_factor_solve`` calls; returns (L, ok)."""
+    if not A.is_cuda:
+        L, info = torch.linalg.cholesky_ex(A.double())
+        return L, int(info) == 0
+    L = A.double().contiguous().clone()
+    info = torch.zeros(1, dtype=torch.int32, device=A.device)
+    native.call("srml_potrf_f64", L.data_ptr(), L.shape[0], L.stride(0), info.data_ptr(), native.stream(A.device))
+    return L, int(info.item()) == 0
+
+
+def spd_factor_solve(L: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """x = (L L^T)^-1 b for a ``spd_factor`` factor (``srml_potrs_f64``: two triangular sweeps)."""
+    if not L.is_cuda:
+        return torch.cholesky_solve(b.double().view(-1, 1), L).view(-1)
+    x = b.double().contiguous().clone()
+    native.call("srml_potrs_f64", L.data_ptr(), L.shape[0], L.stride(0), x.data_ptr(), native.stream(L.device))
+    return x
 
 
 def cd_gram(A: torch.Tensor, b: torch.Tensor, l1: torch.Tensor, l2: torch.Tensor, max_iter: int, tol: float,
@@ -2312,8 +2370,8 @@ def _is_csr(X) -> bool:
 
 def logistic_path(X, K: int) -> str:
     """Which device pass ``logistic_loss_grad`` uses for X (reported by the fit / asserted in tests).
-    Every fp32 / CSR input runs on the srml kernels; only dense fp64 inputs wider than the LDS
-    kernels (``float32_inputs=False``) take the fp64 torch fallback."""
+    Every device input runs on the srml kernels (dense fp64 multinomial: margins and X^T R on the
+    fp64 MFMA GEMM around the fp64 softmax residual kernel)."""
     if _is_csr(X):
         if not X.data.is_cuda:
             return "torch-cpu"
@@ -2334,7 +2392,7 @@ def logistic_path(X, K: int) -> str:
         return "fused_multinomial_f32" if fused else "two_pass_multinomial_f32"
     if X.dtype == torch.float32:
         return "two_pass_wide_f32"
-    return "torch"
+    return "two_pass_multinomial_f64"
 
 
 def _glm_wide(X, y32: torch.Tensor, W: torch.Tensor, b: torch.Tensor, out: torch.Tensor,
@@ -2513,6 +2571,21 @@ def logistic_loss_grad(X, y32: torch.Tensor, w: torch.Tensor, b: torch.Tensor, K
         native.call("srml_logit_residual_f64", z.data_ptr(), m, 1, 1, _c(y32).data_ptr(), b.data_ptr(), 1, 1,
                     r.data_ptr(), 1, out[n:].data_ptr(), 1, out[n + 1:].data_ptr(), 1, fp, st)
         dgemm(X, r, ta=True, beta=1.0, out=out[:n].view(n, 1))
+    elif path == "two_pass_multinomial_f64":
+        # fp64 softmax: margins Z = X W^T and the gradient R^T X on the fp64 MFMA GEMM, the
+        # residual / bias gradient / loss in one fp64 pass (srml_logit_residual_f64, mode 0; K > 16:
+        # the wave-per-row srml_logit_residual_wide_f64 and the bias gradient as R's column sums)
+        Z = dgemm(X, w.view(K, n), tb=True)
+        R = torch.zeros((m, K), dtype=torch.float64, device=dev)  # stays 0 if the done flag skips it
+        if K <= 16:
+            native.call("srml_logit_residual_f64", Z.data_ptr(), m, K, K, _c(y32).data_ptr(), b.data_ptr(), 1, 0,
+                        R.data_ptr(), K, out[K * n:].data_ptr(), 1, out[K * n + K:].data_ptr(), 0, fp, st)
+        else:
+            native.call("srml_logit_residual_wide_f64", Z.data_ptr(), m, K, K, _c(y32).data_ptr(), b.data_ptr(), 1,
+                        R.data_ptr(), K, out[K * n + K:].data_ptr(), fp, st)
+            del Z
+            out[K * n: K * n + K] += col_moments(R, need_sq=False)[0]
+        dgemm(R, X, ta=True, beta=1.0, out=out[: K * n].view(K, n))
     elif path == "fused_binary_f32":
         # ws: the fit's partial-row workspace (ops.logreg_workspace), None = per-block atomic flush;
         # leave_partials: the rows stay unfolded for the fused optimiser step (srml_qn_step_fused)

@@ -65,6 +65,18 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// fast fp32 / full-precision fp64 exp and log for kernels templated on the value type
+__device__ __forceinline__ float fexp(float x) { return __expf(x); }
+__device__ __forceinline__ double fexp(double x) { return exp(x); }
+__device__ __forceinline__ float flog(float x) { return __logf(x); }
+__device__ __forceinline__ double flog(double x) { return log(x); }
+
 // Bijective XCD-aware remap of a 1-D block id (MI355X: 8 XCDs, blocks b and b+8 share one
 // XCD's L2). Consecutive *logical* ids land on the same XCD so neighbouring tiles that share
 // operand panels hit in that L2 (cdna_hip_programming.md §5.5 T1, bijective variant).

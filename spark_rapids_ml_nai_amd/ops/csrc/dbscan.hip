@@ -246,3 +246,106 @@ SRML_API int srml_uf_compress(int* parent, long N, hipStream_t stream) {
   hipLaunchKernelGGL(uf_compress_kernel, dim3(grid_for((N + 255) / 256)), dim3(256), 0, stream, parent, N);
   return srml_status();
 }
+
+// ------------------------------------------------------------------------------------------
+// Cluster labels from the compressed union-find forest (replaces a library unique + searchsorted):
+// the components' roots are the core points that are their own parent (the smallest core index
+// of each component), so cluster ids are the exclusive prefix count of those flags, read at each
+// point's root: ids follow the roots' order, i.e. sklearn's first-core-point numbering.
+//   K1: per 1024-element block the flags' exclusive prefix (wave scans) + the block total;
+//   K2: one block scans the block totals;
+//   K3: label = id of the root (core points), of the nearest core neighbour's root (border
+//       points with one), -1 otherwise (noise).
+// ------------------------------------------------------------------------------------------
+namespace {
+constexpr int DL_T = 1024;
+
+__global__ __launch_bounds__(DL_T) void dbscan_root_prefix_kernel(const int* __restrict__ parent,
+                                                                  const unsigned char* __restrict__ core, long N,
+                                                                  int* __restrict__ local, int* __restrict__ btot) {
+  __shared__ int ws[DL_T / 64];
+  const long i = (long)blockIdx.x * DL_T + threadIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int f = (i < N && core[i] && parent[i] == (int)i) ? 1 : 0;
+  int x = f;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) ws[wid] = x;
+  __syncthreads();
+  int base = 0;
+  for (int w = 0; w < wid; ++w) base += ws[w];
+  if (i < N) local[i] = base + x - f;
+  if (threadIdx.x == DL_T - 1) btot[blockIdx.x] = base + x;
+}
+
+__global__ __launch_bounds__(DL_T) void dbscan_block_scan_kernel(int* __restrict__ btot, long nb) {
+  __shared__ int carry;
+  __shared__ int ws[DL_T / 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (long c0 = 0; c0 < nb; c0 += DL_T) {
+    const long i = c0 + threadIdx.x;
+    const int v = i < nb ? btot[i] : 0;
+    int x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int y = __shfl_up(x, d, 64);
+      if (lane >= d) x += y;
+    }
+    if (lane == 63) ws[wid] = x;
+    __syncthreads();
+    int base = carry;
+    int tot = 0;
+    for (int w = 0; w < DL_T / 64; ++w) {
+      if (w < wid) base += ws[w];
+      tot += ws[w];
+    }
+    if (i < nb) btot[i] = base + x - v;  // exclusive
+    __syncthreads();
+    if (threadIdx.x == 0) carry += tot;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void dbscan_assign_labels_kernel(const int* __restrict__ parent,
+                                                                   const unsigned char* __restrict__ core,
+                                                                   const long long* __restrict__ best, long N,
+                                                                   const int* __restrict__ local,
+                                                                   const int* __restrict__ boff,
+                                                                   long long* __restrict__ labels) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < N; i += (long)gridDim.x * 256) {
+    long r = -1;
+    if (core[i]) {
+      r = parent[i];
+    } else if (best[i] != -1) {
+      const long nb = (long)(best[i] & 0xFFFFFFFFll);
+      r = parent[nb < N ? nb : N - 1];
+    }
+    labels[i] = r < 0 ? -1 : (long long)(local[r] + boff[r / DL_T]);
+  }
+}
+}  // namespace
+
+// labels (int64, N) of DBSCAN points from the compressed forest `parent` (int32, roots = smallest
+// core index), the core flags and `best` (nearest core neighbour in the low 32 bits, -1 = none).
+// ws: 2 N + N / 1024 + 1 int32 of workspace.
+SRML_API long srml_dbscan_labels_ws(long N) { return 2 * N + N / DL_T + 2; }
+
+SRML_API int srml_dbscan_labels(const int* parent, const unsigned char* core, const long long* best, long N,
+                                long long* labels, int* ws, hipStream_t stream) {
+  if (N <= 0) return 0;
+  const long nb = (N + DL_T - 1) / DL_T;
+  int* local = ws;
+  int* btot = ws + N;
+  hipLaunchKernelGGL(dbscan_root_prefix_kernel, dim3((unsigned)nb), dim3(DL_T), 0, stream, parent, core, N, local,
+                     btot);
+  hipLaunchKernelGGL(dbscan_block_scan_kernel, dim3(1), dim3(DL_T), 0, stream, btot, nb);
+  const long g = (N + 255) / 256;
+  hipLaunchKernelGGL(dbscan_assign_labels_kernel, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, stream, parent,
+                     core, best, N, local, btot, labels);
+  return srml_status();
+}

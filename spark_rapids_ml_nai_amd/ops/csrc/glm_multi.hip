@@ -420,27 +420,29 @@ SRML_API int srml_logit_residual_det_f32(const float* Z, long m, int K, long ldz
 // row by wave reductions); R = softmax(Z + b) - onehot(y) is written for the X^T R pass and the
 // per-row losses lse - z_y are block-reduced into ONE fp64 atomic per block. The bias gradient
 // (column sums of R) is formed by the caller's column-sum pass over R.
-__global__ __launch_bounds__(256) void logit_residual_wide_kernel(const float* __restrict__ Z, long m, int K, long ldz,
+// T = double (float32_inputs=False): the softmax runs in fp64 (exp/log), matching the K <= 16 path.
+template <typename T>
+__global__ __launch_bounds__(256) void logit_residual_wide_kernel(const T* __restrict__ Z, long m, int K, long ldz,
                                                                   const float* __restrict__ y,
                                                                   const double* __restrict__ b, long sb,
-                                                                  float* __restrict__ R, long ldr,
+                                                                  T* __restrict__ R, long ldr,
                                                                   double* __restrict__ loss, const int* __restrict__ flag) {
   if (flag && *flag) return;
   __shared__ double part[4];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   double lsum = 0.0;
   for (long r = (long)blockIdx.x * 4 + wid; r < m; r += (long)gridDim.x * 4) {
-    const float* z = Z + r * ldz;
-    float mx = -__builtin_huge_valf();
-    for (int c = lane; c < K; c += 64) mx = fmaxf(mx, z[c] + (float)b[(long)c * sb]);
+    const T* z = Z + r * ldz;
+    T mx = -(T)__builtin_huge_val();
+    for (int c = lane; c < K; c += 64) mx = fmax(mx, z[c] + (T)b[(long)c * sb]);
     mx = wave_max(mx);
-    float se = 0.f;
-    for (int c = lane; c < K; c += 64) se += __expf(z[c] + (float)b[(long)c * sb] - mx);
+    T se = 0;
+    for (int c = lane; c < K; c += 64) se += fexp(z[c] + (T)b[(long)c * sb] - mx);
     se = wave_sum(se);
-    const float lse = mx + __logf(se);
+    const T lse = mx + flog(se);
     const int yi = (int)y[r];
-    float* rr = R + r * ldr;
-    for (int c = lane; c < K; c += 64) rr[c] = __expf(z[c] + (float)b[(long)c * sb] - lse) - (c == yi ? 1.f : 0.f);
+    T* rr = R + r * ldr;
+    for (int c = lane; c < K; c += 64) rr[c] = fexp(z[c] + (T)b[(long)c * sb] - lse) - (c == yi ? (T)1 : (T)0);
     if (lane == 0) lsum += (double)lse - ((double)z[yi] + b[(long)yi * sb]);
   }
   if (lane == 0) part[wid] = lsum;
@@ -451,17 +453,29 @@ __global__ __launch_bounds__(256) void logit_residual_wide_kernel(const float* _
   }
 }
 
-// R (m x K, leading dim ldr) and loss += sum_r (lse_r - z_{r,y_r}) for K classes (any K >= 2).
-SRML_API int srml_logit_residual_wide_f32(const float* Z, long m, int K, long ldz, const float* y, const double* b,
-                                          long sb, float* R, long ldr, double* loss, const int* flag,
-                                          hipStream_t stream) {
+template <typename T>
+static int logit_residual_wide_launch(const T* Z, long m, int K, long ldz, const float* y, const double* b, long sb,
+                                      T* R, long ldr, double* loss, const int* flag, hipStream_t stream) {
   if (m <= 0) return 0;
   if (K < 2) return -2;
   long blocks = (m + 3) / 4;
   if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(logit_residual_wide_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, Z, m, K, ldz, y, b, sb,
-                     R, ldr, loss, flag);
+  hipLaunchKernelGGL(logit_residual_wide_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, stream, Z, m, K, ldz, y, b,
+                     sb, R, ldr, loss, flag);
   return srml_status();
+}
+
+// R (m x K, leading dim ldr) and loss += sum_r (lse_r - z_{r,y_r}) for K classes (any K >= 2).
+SRML_API int srml_logit_residual_wide_f32(const float* Z, long m, int K, long ldz, const float* y, const double* b,
+                                          long sb, float* R, long ldr, double* loss, const int* flag,
+                                          hipStream_t stream) {
+  return logit_residual_wide_launch(Z, m, K, ldz, y, b, sb, R, ldr, loss, flag, stream);
+}
+
+SRML_API int srml_logit_residual_wide_f64(const double* Z, long m, int K, long ldz, const float* y, const double* b,
+                                          long sb, double* R, long ldr, double* loss, const int* flag,
+                                          hipStream_t stream) {
+  return logit_residual_wide_launch(Z, m, K, ldz, y, b, sb, R, ldr, loss, flag, stream);
 }
 
 // ------------------------------------------------------------------------------------------

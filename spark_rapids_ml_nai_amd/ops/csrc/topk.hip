@@ -193,7 +193,9 @@ __global__ __launch_bounds__(TK_T) void topk_rows_kernel(const float* __restrict
 // the 64 lanes (ties keep the candidate order). Replaces index_select of the candidate rows +
 // elementwise + reduction + torch.sort (the gathered rows never touch HBM).
 // metric 0: squared euclidean; 1: -2 q.x (inner product, ascending = most similar first).
-template <int QT>
+// TAIL: dimensions past the 64*QT held in registers are streamed (the query row stays L2-hot
+// across the k candidates), so any n is served.
+template <int QT, bool TAIL>
 __global__ __launch_bounds__(256) void knn_refine_sort_kernel(const float* __restrict__ Q, long mq, int n, long ldq,
                                                               const float* __restrict__ X, long ldx,
                                                               const long long* __restrict__ pos, int k, long ldp,
@@ -225,6 +227,17 @@ __global__ __launch_bounds__(256) void knn_refine_sort_kernel(const float* __res
           acc = fmaf(df, df, acc);
         } else {
           acc = fmaf(qv[t], x, acc);
+        }
+      }
+    }
+    if (TAIL) {
+      for (int d = 64 * QT + lane; d < n; d += 64) {
+        const float qd = Q[q * ldq + d], x = xr[d];
+        if (metric == 0) {
+          const float df = qd - x;
+          acc = fmaf(df, df, acc);
+        } else {
+          acc = fmaf(qd, x, acc);
         }
       }
     }
@@ -438,15 +451,16 @@ SRML_API int srml_knn_refine_sort_f32(const float* Q, long mq, int n, long ldq, 
                                       const long long* pos, int k, long ldp, int metric, float* dout, long long* pout,
                                       hipStream_t stream) {
   if (mq <= 0) return 0;
-  if (k < 1 || k > 64 || n < 1 || n > 1024 || ldq < n || ldx < n || ldp < k || (metric != 0 && metric != 1)) return -2;
+  if (k < 1 || k > 64 || n < 1 || ldq < n || ldx < n || ldp < k || (metric != 0 && metric != 1)) return -2;
   const dim3 grid(ceil_div(mq, 4)), blk(256);
 #define SRML_KRS(QQ) \
-  hipLaunchKernelGGL(knn_refine_sort_kernel<QQ>, grid, blk, 0, stream, Q, mq, n, ldq, X, ldx, pos, k, ldp, metric, dout, pout)
-  if (n <= 64) SRML_KRS(1);
-  else if (n <= 128) SRML_KRS(2);
-  else if (n <= 256) SRML_KRS(4);
-  else if (n <= 512) SRML_KRS(8);
-  else SRML_KRS(16);
+  hipLaunchKernelGGL(QQ, grid, blk, 0, stream, Q, mq, n, ldq, X, ldx, pos, k, ldp, metric, dout, pout)
+  if (n <= 64) SRML_KRS((knn_refine_sort_kernel<1, false>));
+  else if (n <= 128) SRML_KRS((knn_refine_sort_kernel<2, false>));
+  else if (n <= 256) SRML_KRS((knn_refine_sort_kernel<4, false>));
+  else if (n <= 512) SRML_KRS((knn_refine_sort_kernel<8, false>));
+  else if (n <= 1024) SRML_KRS((knn_refine_sort_kernel<16, false>));
+  else SRML_KRS((knn_refine_sort_kernel<16, true>));
 #undef SRML_KRS
   return srml_status();
 }

@@ -409,3 +409,92 @@ SRML_API int srml_umap_fuzzy_union_knn(const long long* idx, const float* w, lon
                      ld, mix, keys, vals, kept);
   return srml_status();
 }
+
+// ------------------------------------------------------------------------------------------
+// Supervised UMAP: categorical simplicial-set intersection on the (row, col)-sorted fuzzy union
+// (umap-learn's categorical_simplicial_set_intersection + reset_local_connectivity + the second
+// fuzzy union), in place of a library unique / scatter-max / coalesce. The union's pattern is
+// symmetric, so every edge's transpose is found by a binary search in the other row's sorted
+// column run — no re-sort, the output keeps the input pattern and order:
+//   K1 row pointers (binary search per row), K2 scaled values v = w * exp(-unknown_dist) for an
+//   unknown label / * exp(-far_dist) for differing labels and the per-row max (one thread per
+//   row), K3 per edge a = v_ij / max_i, b = v_ji / max_j, out = mix (a + b - ab) + (1 - mix) ab.
+// ------------------------------------------------------------------------------------------
+namespace {
+__global__ __launch_bounds__(256) void ucat_indptr_kernel(const long long* __restrict__ rows, long nnz, long N,
+                                                          long long* __restrict__ indptr) {
+  for (long r = (long)blockIdx.x * 256 + threadIdx.x; r <= N; r += (long)gridDim.x * 256) {
+    long lo = 0, hi = nnz;
+    while (lo < hi) {
+      const long mid = (lo + hi) >> 1;
+      if (rows[mid] < r) lo = mid + 1;
+      else hi = mid;
+    }
+    indptr[r] = lo;
+  }
+}
+
+__global__ __launch_bounds__(256) void ucat_scale_kernel(const long long* __restrict__ indptr,
+                                                         const long long* __restrict__ cols,
+                                                         const float* __restrict__ vals, const long long* __restrict__ y,
+                                                         long N, double f_unknown, double f_far,
+                                                         double* __restrict__ v, double* __restrict__ rmax) {
+  for (long r = (long)blockIdx.x * 256 + threadIdx.x; r < N; r += (long)gridDim.x * 256) {
+    const long long yr = y[r];
+    double mx = 0.0;
+    for (long long e = indptr[r]; e < indptr[r + 1]; ++e) {
+      const long long yc = y[cols[e]];
+      double x = (double)vals[e];
+      if (yr == -1 || yc == -1) x *= f_unknown;
+      else if (yr != yc) x *= f_far;
+      v[e] = x;
+      mx = x > mx ? x : mx;
+    }
+    rmax[r] = mx;
+  }
+}
+
+__global__ __launch_bounds__(256) void ucat_union_kernel(const long long* __restrict__ rows,
+                                                         const long long* __restrict__ cols,
+                                                         const long long* __restrict__ indptr,
+                                                         const double* __restrict__ v, const double* __restrict__ rmax,
+                                                         long nnz, double mix, float* __restrict__ out) {
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < nnz; e += (long)gridDim.x * 256) {
+    const long long i = rows[e], j = cols[e];
+    const double a = v[e] / (rmax[i] > 1e-30 ? rmax[i] : 1e-30);
+    long long lo = indptr[j], hi = indptr[j + 1];
+    while (lo < hi) {
+      const long long mid = (lo + hi) >> 1;
+      if (cols[mid] < i) lo = mid + 1;
+      else hi = mid;
+    }
+    const double b = (lo < indptr[j + 1] && cols[lo] == i) ? v[lo] / (rmax[j] > 1e-30 ? rmax[j] : 1e-30) : 0.0;
+    const double ab = a * b;
+    out[e] = (float)(mix * (a + b - ab) + (1.0 - mix) * ab);
+  }
+}
+
+inline unsigned ucat_grid(long work) {
+  long b = (work + 255) / 256;
+  return (unsigned)(b < 1 ? 1 : (b > 8192 ? 8192 : b));
+}
+}  // namespace
+
+// rows / cols: int64 (row, col)-sorted union edges (symmetric pattern), vals fp32, y int64 labels
+// (-1 unknown). out: fp32 new values (same pattern). ws: (N + 1) int64 + nnz + N fp64 (= 8-byte words).
+SRML_API long srml_umap_categorical_ws(long N, long nnz) { return (N + 1) + nnz + N; }
+
+SRML_API int srml_umap_categorical(const long long* rows, const long long* cols, const float* vals, long nnz,
+                                   const long long* y, long N, double unknown_dist, double far_dist, double mix,
+                                   float* out, void* ws, hipStream_t stream) {
+  if (nnz <= 0 || N <= 0) return 0;
+  long long* indptr = reinterpret_cast<long long*>(ws);
+  double* v = reinterpret_cast<double*>(indptr + (N + 1));
+  double* rmax = v + nnz;
+  hipLaunchKernelGGL(ucat_indptr_kernel, dim3(ucat_grid(N + 1)), dim3(256), 0, stream, rows, nnz, N, indptr);
+  hipLaunchKernelGGL(ucat_scale_kernel, dim3(ucat_grid(N)), dim3(256), 0, stream, indptr, cols, vals, y, N,
+                     exp(-unknown_dist), exp(-far_dist), v, rmax);
+  hipLaunchKernelGGL(ucat_union_kernel, dim3(ucat_grid(nnz)), dim3(256), 0, stream, rows, cols, indptr, v, rmax, nnz,
+                     mix, out);
+  return srml_status();
+}

@@ -29,7 +29,7 @@ _F = ctypes.c_float
 _LONG_RESULT = ("srml_rf_bootstrap_ws", "srml_logreg_fold_ws", "srml_qn_mb_scratch", "srml_qn_fused_scratch",
                 "srml_qn_fused_barrier_offset",
                 "srml_logreg_fold_parts", "srml_qn_args_size", "srml_logit_residual_ws", "srml_xtv_mfma_ws",
-                "srml_rf_partition_ws",
+                "srml_rf_partition_ws", "srml_dbscan_labels_ws", "srml_umap_categorical_ws",
                 "srml_label_sort_ws", "srml_radix_sort_ws")
 SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_col_moments_f32": (_P, _L, _I, _L, _P, _P, _P),
@@ -123,6 +123,10 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_dbscan_link_f32": (_P, _L, _I, _L, _P, _F, _L, _L, _P, _P, _P, _P),
     "srml_uf_unite_pairs": (_P, _L, _P, _P),
     "srml_uf_compress": (_P, _L, _P),
+    "srml_dbscan_labels_ws": (_L,),
+    "srml_umap_categorical_ws": (_L, _L),
+    "srml_umap_categorical": (_P, _P, _P, _L, _P, _L, _D, _D, _D, _P, _P, _P),
+    "srml_dbscan_labels": (_P, _P, _P, _L, _P, _P, _P),
     "srml_oneshot_alloc": (_L, _P, _P),
     "srml_oneshot_open": (_P, _P),
     "srml_oneshot_close": (_P,),
@@ -191,6 +195,7 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_row_list": (_P, _I, _L, _P, _P),
     "srml_cd_sweep_global_f64": (_P, _I, _L, _P, _P, _P, _P, _P, _P, _P, _I, _P),
     "srml_logit_residual_wide_f32": (_P, _L, _I, _L, _P, _P, _L, _P, _L, _P, _P, _P),
+    "srml_logit_residual_wide_f64": (_P, _L, _I, _L, _P, _P, _L, _P, _L, _P, _P, _P),
 }
 
 _lock = threading.Lock()

@@ -1071,7 +1071,7 @@ def test_radix_sort_pairs_stable(gpu_device, n, bits):
 
 
 @pytest.mark.parametrize("mq,n,k,ip", [(1, 3, 1, False), (777, 128, 15, False), (300, 1000, 64, True),
-                                       (129, 65, 40, False)])
+                                       (129, 65, 40, False), (200, 3001, 33, False), (150, 2048, 64, True)])
 def test_knn_refine_sort_matches_torch(gpu_device, mq, n, k, ip):
     """Fused exact re-score + per-row sort of kNN candidates == fp64 torch oracle (-1 = missing)."""
     g = torch.Generator().manual_seed(mq + n + k)
@@ -1341,3 +1341,29 @@ def test_kmeans_lloyd_step_without_row_outputs(gpu_device, m, n, k):
     assert lab is None and dist is None
     torch.testing.assert_close(buf_c[k * n: k * n + k], buf_e[k * n: k * n + k], rtol=0, atol=0)
     torch.testing.assert_close(buf_c, buf_e, rtol=1e-9, atol=1e-6)
+
+
+def test_dbscan_labels_match_unique_oracle(gpu_device):
+    """Native label compaction (root-flag prefix scan) == the unique/searchsorted numbering."""
+    g = torch.Generator().manual_seed(9)
+    N = 300_001
+    core = (torch.rand(N, generator=g) < 0.6).to(torch.uint8)
+    # a compressed forest: every core point points at the smallest core index of its group
+    grp = torch.randint(0, 5000, (N,), generator=g)
+    idx = torch.arange(N)
+    big = N + 1
+    first = torch.full((5000,), big, dtype=torch.int64).scatter_reduce_(
+        0, grp[core.bool()], idx[core.bool()], "amin", include_self=True)
+    parent = torch.where(core.bool() & (first[grp] < big), first[grp], idx).int()
+    best = torch.where(torch.rand(N, generator=g) < 0.5, torch.randint(0, N, (N,), generator=g),
+                       torch.full((N,), -1, dtype=torch.int64))
+    best = torch.where(core.bool()[best.clamp_min(0)] & (best >= 0), best, torch.full_like(best, -1))
+    got = ops.dbscan_labels(parent.to(gpu_device), core.to(gpu_device), best.to(gpu_device)).cpu()
+    corb, root = core.bool(), parent.long()
+    nb = (best & 0xFFFFFFFF).clamp(0, N - 1)
+    lab_root = torch.where(corb, root, torch.where(best != -1, root[nb], torch.full_like(root, -1)))
+    roots = torch.unique(root[corb])
+    ref = torch.full((N,), -1, dtype=torch.int64)
+    m = lab_root >= 0
+    ref[m] = torch.searchsorted(roots, lab_root[m])
+    assert torch.equal(got, ref)

@@ -181,7 +181,8 @@ def _ref_loss_grad(X, y, W, b, K):
     (1500, 300, 20, torch.float32, "two_pass_wide_f32"),
     (1200, 257, 70, torch.float32, "two_pass_wide_f32"),
     (600, 20000, 1, torch.float32, "two_pass_binary_f32"),
-    (1500, 300, 20, torch.float64, "torch"),
+    (1500, 300, 20, torch.float64, "two_pass_multinomial_f64"),
+    (2000, 77, 3, torch.float64, "two_pass_multinomial_f64"),
     (5000, 3000, 1, torch.float32, "two_pass_deterministic_f32"),
     (3001, 130, 1, torch.float32, "two_pass_deterministic_f32"),
     (4000, 3000, 10, torch.float32, "two_pass_deterministic_f32"),

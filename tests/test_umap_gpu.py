@@ -119,3 +119,26 @@ def test_umap_neg_lines_matches_iid_negatives(gpu_device, monkeypatch):
         e = U.umap_fit(Xt, {"n_neighbors": 15, "random_state": 4, "n_epochs": 200})
         tw[flag] = trustworthiness(X, e, n_neighbors=15)
     assert tw[True] > 0.9 and tw[True] > tw[False] - 0.01, tw
+
+
+def test_categorical_intersection_native_matches_torch(gpu_device):
+    """Supervised UMAP: the native categorical intersection on the sorted, pattern-symmetric union
+    equals the torch reference (scale, per-row max reset, coalescing fuzzy union) in fp64."""
+    import torch
+
+    from spark_rapids_ml_nai_amd import ops
+    from spark_rapids_ml_nai_amd.models import umap as U
+
+    g = torch.Generator().manual_seed(3)
+    N, k = 4000, 12
+    idx = torch.rand(N, N, generator=g).argsort(1)[:, :k]  # distinct neighbours per row, like a kNN graph
+    w = torch.rand(N, k, generator=g) * 0.9 + 0.05
+    rows, cols, vals = ops.umap_fuzzy_union_knn(idx.to(gpu_device), w.to(gpu_device), 1.0)
+    y = torch.randint(-1, 5, (N,), generator=g)
+    r1, c1, v1 = U.categorical_intersection(rows, cols, vals, y.to(gpu_device), N)
+    r0, c0, v0 = U.categorical_intersection(rows.cpu(), cols.cpu(), vals.cpu(), y, N)
+    k1 = (r1.cpu() * N + c1.cpu())
+    k0 = (r0.long() * N + c0.long())
+    o1, o0 = torch.argsort(k1), torch.argsort(k0)
+    assert torch.equal(k1[o1], k0[o0])
+    torch.testing.assert_close(v1.cpu()[o1].double(), v0[o0].double(), rtol=1e-5, atol=1e-7)
