@@ -368,7 +368,7 @@ def kmeans_predict(X: torch.Tensor, C: torch.Tensor) -> torch.Tensor:
     return labels
 
 
-def kmeans_predict_streamed(host: np.ndarray, C: torch.Tensor, device: torch.device,
+def kmeans_predict_streamed(host: Any, C: torch.Tensor, device: torch.device,
                             chunk_bytes: int = 0) -> torch.Tensor:
     """``kmeans_predict`` of a page-locked host matrix with its H2D streamed under the search
     (reference transform: ``clustering.py:493-499``, one cuML predict per batch): the rows cross
@@ -378,7 +378,8 @@ def kmeans_predict_streamed(host: np.ndarray, C: torch.Tensor, device: torch.dev
 
     Each chunk is centred on the centres' mean (the filter's operands are x - mu and c - mu; any
     mu keeps the labels exact, it only conditions the fp16 plane) with its own plane scale. Chunks
-    the fp16 filter cannot take (no finite range) use ``kmeans_predict``."""
+    the fp16 filter cannot take (no finite range) use ``kmeans_predict``. ``host`` may be a
+    multi-batch ``ChunkedRows`` (the transform's Arrow batches, streamed batch by batch)."""
     from ..ops.ingest import RingRows
 
     if chunk_bytes <= 0:
@@ -402,8 +403,8 @@ def predict_streams(host: Any, k: int) -> bool:
     the fp16 certified filter (``SRML_KMEANS_PREDICT_STREAM=0`` disables)."""
     from ..ops.ingest import is_pinned
 
-    return (isinstance(host, np.ndarray) and host.ndim == 2 and host.shape[0] >= 65536 and k > 256
-            and host.dtype == np.float32 and torch.cuda.is_available()
+    return ((isinstance(host, np.ndarray) or hasattr(host, "parts")) and host.ndim == 2
+            and host.shape[0] >= 65536 and k > 256 and host.dtype == np.float32 and torch.cuda.is_available()
             and os.environ.get("SRML_KMEANS_PREDICT_STREAM", "1") == "1"
             and os.environ.get("SRML_KMEANS_PREDICT_SPLIT", "1") == "1"
             and ops.kmeans_filter_mode() == "f16" and is_pinned(host))

@@ -41,11 +41,13 @@ PULL = os.environ.get("SRML_UMAP_PULL", "1") != "0"
 # pull epochs draw negatives from a per-epoch randomly ordered snapshot, 8 edges per 64 B line
 # (ops.umap_epoch neg_table): one memory request per 8 negative samples instead of 8
 NEG_LINES = os.environ.get("SRML_UMAP_NEG_LINES", "1") != "0"
-# Chebyshev filter degree of the device spectral init's subspace iteration (1 = plain iteration,
-# the default). The filter resolves small eigen-gaps far faster, but on clustered data (20M blobs:
-# ~20 near-1 eigenvalues for a 16-vector block) the Ritz-change stop never fires and it ran to the
-# 300-product cap (20M fit 10.7 -> 22.2 s); the plain iteration settles into the cluster and stops.
-CHEB_DEGREE = int(os.environ.get("SRML_UMAP_CHEB_DEGREE", "1"))
+# Chebyshev filter degree of the device spectral init's subspace iteration (1 = plain iteration).
+# Degree 4 at the 1e-6 Ritz stop: 20M blobs 97 -> 29 products, 20M classification rows 232 -> 58
+# (fit 9.95 -> 6.32 s), trustworthiness unchanged (profiles/umap_spectral_cheb_r5.jsonl). Round 4's
+# degree 8 at a stop near fp32 resolution ran to the product cap on the clustered 20M graph; the
+# stop is now above fp32 noise and a stagnating Ritz change also ends the iteration.
+CHEB_DEGREE = int(os.environ.get("SRML_UMAP_CHEB_DEGREE", "4"))
+SPECTRAL_TOL = float(os.environ.get("SRML_UMAP_SPECTRAL_TOL", "1e-6"))  # Ritz-value stop (see _spectral_device)
 SPECTRAL_DENSE_N = 2048  # device Jacobi on the dense normalised adjacency up to this many vertices
 # per-phase {"rows": this rank's rows / edges, "s": seconds} of the last umap_fit in this process
 LAST_PHASES: Dict[str, Any] = {}
@@ -316,6 +318,8 @@ def _spectral_device(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor,
 
     prev = None
     it = 0
+    best = float("inf")
+    stall = 0
     if CHEB_DEGREE > 1:
         # Chebyshev-filtered subspace iteration: each step applies T_d on [0, b] (b = the block's
         # smallest Ritz value, an upper bound of the unwanted spectrum), which damps the unwanted
@@ -326,9 +330,13 @@ def _spectral_device(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor,
             T = ritz_matrix(Y, Z)
             allr = np.sort(np.linalg.eigvalsh((T + T.T) * 0.5))[::-1]
             ritz = allr[: dim + 1]
-            if prev is not None and it >= min_iters and \
-                    np.max(np.abs(ritz - prev)) <= tol * max(float(np.max(np.abs(ritz))), 1e-30):
-                break
+            if prev is not None:
+                rel = float(np.max(np.abs(ritz - prev))) / max(float(np.max(np.abs(ritz))), 1e-30)
+                # a change that stops shrinking for 4 checks near the tolerance is fp32 noise
+                stall = stall + 1 if rel >= 0.5 * best and rel <= 20.0 * tol else 0
+                best = min(best, rel)
+                if it >= min_iters and (rel <= tol or stall >= 4):
+                    break
             prev = ritz
             bcut = float(min(max(allr[-1], 0.0), allr[dim]))
             if bcut >= 0.995 or it + CHEB_DEGREE > iters:
@@ -389,7 +397,7 @@ def spectral_init(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n:
     dev = vals.device
     dist = ctx is not None and ctx.world_size > 1
     if n > SPECTRAL_DENSE_N and (dev.type == "cuda" or dist):
-        coords = _spectral_device(rows, cols, vals, n, dim, seed, ctx=ctx, phases=phases)
+        coords = _spectral_device(rows, cols, vals, n, dim, seed, tol=SPECTRAL_TOL, ctx=ctx, phases=phases)
     elif dev.type != "cuda":
         coords = torch.from_numpy(_spectral_host(rows.cpu().numpy(), cols.cpu().numpy(), vals.cpu().numpy(), n, dim,
                                                  seed)).float().to(dev)

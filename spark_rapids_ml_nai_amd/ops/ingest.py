@@ -407,20 +407,36 @@ class RingRows:
     depth - 1 chunks cross PCIe while the current one is processed. Iterate ``chunks()``: each
     yields (r0, r1, device view) valid until the next step of the iteration."""
 
-    def __init__(self, host: np.ndarray, device: torch.device, dtype: Optional[torch.dtype] = None,
+    def __init__(self, host: Any, device: torch.device, dtype: Optional[torch.dtype] = None,
                  chunk_bytes: int = 256 << 20, depth: int = 3) -> None:
-        with warnings.catch_warnings():
-            warnings.simplefilter("ignore", UserWarning)
-            t = torch.from_numpy(np.ascontiguousarray(host))
-        if not t.is_pinned():
-            raise ValueError("RingRows needs a page-locked source")
-        if dtype is not None and t.dtype != dtype:
-            raise ValueError("RingRows copies without a cast: the source must already be %s" % dtype)
-        self.host, self.device = t, device
-        m = t.shape[0]
-        row_bytes = max(1, t[0].numel() * t.element_size()) if m else 1
+        # host: one page-locked matrix, or a multi-batch ``ChunkedRows`` (its per-batch views are
+        # chunked separately: a chunk never spans two batches, so no host concatenation)
+        parts = list(host.parts) if hasattr(host, "parts") else [host]
+        ts = []
+        for a in parts:
+            with warnings.catch_warnings():
+                warnings.simplefilter("ignore", UserWarning)
+                t = torch.from_numpy(np.ascontiguousarray(a))
+            if not t.is_pinned():
+                raise ValueError("RingRows needs a page-locked source")
+            if dtype is not None and t.dtype != dtype:
+                raise ValueError("RingRows copies without a cast: the source must already be %s" % dtype)
+            ts.append(t)
+        t = ts[0]
+        self.device = device
+        row_bytes = max(1, t[0].numel() * t.element_size()) if t.shape[0] else 1
         self.chunk_rows = max(256, int(chunk_bytes // row_bytes))
-        self.bounds = [(r0, min(m, r0 + self.chunk_rows)) for r0 in range(0, m, self.chunk_rows)]
+        # bounds: global (r0, r1); _src: (host tensor, local row offset) of every chunk
+        self.bounds, self._src = [], []
+        g = 0
+        for tp in ts:
+            mp = int(tp.shape[0])
+            for l0 in range(0, mp, self.chunk_rows):
+                l1 = min(mp, l0 + self.chunk_rows)
+                self.bounds.append((g + l0, g + l1))
+                self._src.append((tp, l0))
+            g += mp
+        self.host = t if len(ts) == 1 else None
         self.depth = max(2, int(depth))
         nb = min(self.depth, len(self.bounds))
         self.bufs = [torch.empty((self.chunk_rows,) + tuple(t.shape[1:]), dtype=t.dtype, device=device)
@@ -440,8 +456,9 @@ class RingRows:
                 self._copy.wait_event(done[c - nb])
             else:
                 self._copy.wait_stream(cur)
+            src, l0 = self._src[c]
             with torch.cuda.stream(self._copy):
-                self.bufs[c % nb][: r1 - r0].copy_(self.host[r0:r1], non_blocking=True)
+                self.bufs[c % nb][: r1 - r0].copy_(src[l0: l0 + r1 - r0], non_blocking=True)
                 ev = torch.cuda.Event(enable_timing=True)
                 ev.record(self._copy)
             ready[c] = ev
@@ -464,7 +481,10 @@ class RingRows:
 
 
 def is_pinned(a: Any) -> bool:
-    """Whether a numpy array's memory is page-locked (registered with the HIP runtime)."""
+    """Whether a numpy array's memory (every batch of a ``ChunkedRows``) is page-locked
+    (registered with the HIP runtime)."""
+    if hasattr(a, "parts") and not isinstance(a, np.ndarray):
+        return bool(a.parts) and all(is_pinned(p) for p in a.parts)
     if not isinstance(a, np.ndarray) or not torch.cuda.is_available():
         return False
     with warnings.catch_warnings():

@@ -1003,6 +1003,13 @@ def test_kmeans_predict_streamed_matches(gpu_device):
     assert got.dtype == torch.int32 and got.shape == (m,)
     assert (got == ref).float().mean().item() > 0.9999
     assert (got == one).float().mean().item() > 0.9999
+    # a multi-batch transform input (Arrow batches as ChunkedRows views, chunks never span batches)
+    from spark_rapids_ml_nai_amd.core.dataframe import ChunkedRows
+
+    parts = ChunkedRows([Xh[:30001], Xh[30001:30001], Xh[30001:65000], Xh[65000:]])
+    assert predict_streams(parts, k)
+    got2 = kmeans_predict_streamed(parts, C, gpu_device, chunk_bytes=9 << 20)
+    assert got2.shape == (m,) and (got2 == got).float().mean().item() > 0.9999
 
 
 @pytest.mark.parametrize("nseg,total", [(1, 5000), (37, 100000), (3000, 2_000_000)])

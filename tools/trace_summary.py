@@ -23,6 +23,24 @@ def main(out_dir: str) -> None:
     print("dispatches %d, first-to-last span %.1f ms (warmup + timed)" % (len(rows), span))
     for k, (n, ms) in sorted(tot.items(), key=lambda kv: -kv[1][1])[:25]:
         print("%9.2f ms %6d  %s" % (ms, n, k[:110]))
+    # device-idle analysis: union of kernel intervals vs the span, and the largest gaps (the
+    # kernels on either side name where the host was working with nothing in flight)
+    busy, cur_s, cur_e, gaps = 0.0, None, None, []
+    prev_k = None
+    for s, e, k in rows:
+        if cur_e is None or s > cur_e:
+            if cur_e is not None:
+                busy += (cur_e - cur_s) / 1e6
+                gaps.append(((s - cur_e) / 1e6, prev_k, k))
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+        prev_k = k
+    if cur_e is not None:
+        busy += (cur_e - cur_s) / 1e6
+    print("device busy %.1f ms of %.1f ms span (idle %.1f ms)" % (busy, span, span - busy))
+    for g, a, b in sorted(gaps, reverse=True)[:int(os.environ.get("TRACE_GAPS", "15"))]:
+        print("  gap %8.2f ms after %s -> before %s" % (g, a[:60], b[:60]))
     for pat in ("rf_hist_kernel|rf_hist_wide_kernel", "nearest", "splitmm", "kmeanspp"):
         calls = [(e - s) / 1e6 for s, e, k in rows if any(p in k for p in pat.split("|"))]
         if calls:

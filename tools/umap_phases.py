@@ -19,6 +19,7 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=2_000_000)
     ap.add_argument("--cols", type=int, default=128)
+    ap.add_argument("--no-profile", action="store_true", help="skip cProfile (kernel-trace runs)")
     a = ap.parse_args()
     from spark_rapids_ml_nai_amd.bench import datagen
     from spark_rapids_ml_nai_amd.models import umap as U
@@ -31,12 +32,16 @@ def main() -> None:
     torch.cuda.synchronize()
     pr = cProfile.Profile()
     t0 = time.perf_counter()
-    pr.enable()
+    if not a.no_profile:
+        pr.enable()
     U.umap_fit(X, params)
     torch.cuda.synchronize()
-    pr.disable()
+    if not a.no_profile:
+        pr.disable()
     print("fit %.3f s" % (time.perf_counter() - t0), flush=True)
-    pstats.Stats(pr).sort_stats("cumulative").print_stats(35)
+    print("phases", U.LAST_PHASES, flush=True)
+    if not a.no_profile:
+        pstats.Stats(pr).sort_stats("cumulative").print_stats(35)
 
 
 if __name__ == "__main__":
