@@ -70,6 +70,28 @@ RF_DP_SCATTER = os.environ.get("SRML_RF_DP_SCATTER", "1") != "0"
 # node, so there the parent's histogram does not cover the children's features and every node is
 # built. SRML_RF_SIBLING_SUB=0 turns it off.
 RF_SIBLING_SUB = os.environ.get("SRML_RF_SIBLING_SUB", "1") != "0"
+# SRML_RF_LEVEL_LOG=1: per-level host timing of the last grow_forest call in LAST_LEVELS (segments,
+# candidates, seconds of host work vs waits on the device per section)
+LEVEL_LOG = os.environ.get("SRML_RF_LEVEL_LOG", "0") == "1"
+LAST_LEVELS: List[Dict[str, Any]] = []
+
+
+class _LevelClock:
+    """Accumulates wall time between marks into named sections (no-op unless LEVEL_LOG)."""
+
+    def __init__(self) -> None:
+        import time
+
+        self._now = time.perf_counter
+        self.t = self._now()
+        self.rec: Dict[str, Any] = {}
+
+    def mark(self, name: str) -> None:
+        if not LEVEL_LOG:
+            return
+        t = self._now()
+        self.rec[name] = round(self.rec.get(name, 0.0) + (t - self.t), 6)
+        self.t = t
 
 
 def _left_totals(hist: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
@@ -307,7 +329,7 @@ def _root_hist_streamed(pending: PendingBins, bins: torch.Tensor, idx: torch.Ten
         it[:, 3] = np.repeat(np.arange(nfc, dtype=np.int32), tot_ch)
         per_chunk.append(it)
     off = np.cumsum([0] + [a.shape[0] for a in per_chunk])
-    items_all = torch.from_numpy(np.concatenate(per_chunk, 0)).to(dev)
+    items_all = _h2d(np.concatenate(per_chunk, 0), dev)
     for ci, _rows in enumerate(pending.chunks()):
         if off[ci + 1] > off[ci]:
             ops.rf_hist(bins, idx, yv, None, items_all[off[ci]: off[ci + 1]], feats, Ch, B, SH, regression,
@@ -322,14 +344,23 @@ def _expand_siblings(built: torch.Tensor, derive: np.ndarray, sib_pos: np.ndarra
     dev = built.device
     C = derive.size
     full = torch.empty((C,) + tuple(built.shape[1:]), dtype=built.dtype, device=dev)
-    bpos = torch.from_numpy(np.nonzero(~derive)[0]).to(dev)
+    bpos = _h2d(np.nonzero(~derive)[0], dev)
     full.index_copy_(0, bpos, built)
     d = np.nonzero(derive)[0]
     if d.size:
-        dpos = torch.from_numpy(d).to(dev)
-        par = prev_hist.index_select(0, torch.from_numpy(parent_row[d]).to(dev))
-        full.index_copy_(0, dpos, par - full.index_select(0, torch.from_numpy(sib_pos[d]).to(dev)))
+        dpos = _h2d(d, dev)
+        par = prev_hist.index_select(0, _h2d(parent_row[d], dev))
+        full.index_copy_(0, dpos, par - full.index_select(0, _h2d(sib_pos[d], dev)))
     return full
+
+
+def _h2d(a: np.ndarray, dev: torch.device) -> torch.Tensor:
+    """Host array -> device without a blocking copy: staged through page-locked memory and queued
+    on the stream (the caching host allocator keeps the staging buffer until the copy ran)."""
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if dev.type != "cuda":
+        return t.to(dev)
+    return t.pin_memory().to(dev, non_blocking=True)
 
 
 def _pad_rows(t: torch.Tensor, rows: int) -> torch.Tensor:
@@ -410,9 +441,17 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
     prev_hist: Optional[torch.Tensor] = None  # last level's candidate histograms (cand order), summed
     prev_parent = None  # per segment: its parent's row of prev_hist
     depth = 0
+    # host copies per level: ONE at the end of a level (child bounds + child totals together) and
+    # ONE after the split search (split records with the winning feature ids gathered on the device)
+    tot_h = tot.cpu().numpy().astype(np.float64)
+    if LEVEL_LOG:
+        LAST_LEVELS.clear()
     while len(seg_tree):
         L = len(seg_tree)
-        tot_h = tot.cpu().numpy().astype(np.float64)
+        clk = _LevelClock()
+        if LEVEL_LOG:
+            LAST_LEVELS.append(clk.rec)
+            clk.rec.update(depth=depth, segments=int(L))
         wsum = tot_h[:, 0] if regression else tot_h.sum(1)
         imps = _impurities_np(tot_h, crit)
         rec.seg.append((seg_tree.copy(), seg_nid.copy(), _leaf_values_np(tot_h, regression), wsum.copy(), imps))
@@ -500,9 +539,10 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
                 it[:, 1] = np.repeat(rb, nfc_l)
                 it[:, 2] = np.repeat(re, nfc_l)
                 it[:, 3] = np.tile(np.arange(nfc_l), tot_ch) | np.repeat(single, nfc_l)
+            clk.mark("items_host")
             if not streamed_root:
-                items_t = torch.from_numpy(it).to(dev, non_blocking=False)
-                excl = ({"multi_nodes": torch.from_numpy(np.nonzero(nch != 1)[0]).to(dev)}
+                items_t = _h2d(it, dev)
+                excl = ({"multi_nodes": _h2d(np.nonzero(nch != 1)[0], dev)}
                         if dev.type == "cuda" else None)
                 hist = ops.rf_hist(bins, idx, yv, None, items_t, feats if Cp == C else _pad_rows(feats, Cp), Cp, B,
                                    SH, regression, pos_weight=wpos,
@@ -533,11 +573,15 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
                     res_left.append(_left_totals(hist, out))
                 prev_hist = hist if keep_hist else None
                 del hist
-            out_h = out.cpu().numpy()
+            # the winning feature ids gathered on the device: one copy of (records | feature id)
+            fsel = feats[:C].gather(1, out[:, 1].clamp_min(0).long().view(-1, 1)).to(out.dtype)
+            clk.mark("hist_split_launch")
+            rec_h = torch.cat([out, fsel], 1).cpu().numpy()
+            clk.mark("split_sync")
+            out_h = rec_h[:, :-1]
             res_out.append(out_h)
-            feats_h = feats.cpu().numpy()
             ok = out_h[:, 1] >= 0
-            res_feat.append(np.where(ok, feats_h[np.arange(C), np.where(ok, out_h[:, 1], 0).astype(np.int64)], -1))
+            res_feat.append(np.where(ok, rec_h[:, -1].astype(np.int64), -1))
         out_all = np.concatenate(res_out, 0)
         feat_all = np.concatenate(res_feat, 0)
         # ---- decide splits (honour max_leaves per tree) ----
@@ -578,22 +622,32 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
         if k == 0:
             break
         # ---- route + stable partition into child segments ----
-        meta = torch.from_numpy(np.stack([node_feature, node_bin, child_base])).to(dev)
+        clk.mark("decide_host")
+        if LEVEL_LOG:
+            clk.rec["candidates"] = int(cand.size)
+            clk.rec["splits"] = int(k)
+        meta = _h2d(np.stack([node_feature, node_bin, child_base]), dev)
         keys = ops.rf_route_segments(bins, idx, bounds, meta[0].contiguous(), meta[1].contiguous(),
                                      meta[2].contiguous())
-        idx, wpos, bounds = ops.rf_partition(keys, bounds, meta[0].contiguous(), meta[2].contiguous(), k, idx, wpos)
+        idx, wpos, bounds = ops.rf_partition(keys, bounds, meta[0].contiguous(), meta[2].contiguous(), k, idx, wpos,
+                                             kept=int(counts[j_sel].sum()))
         if regression:
             tot = _node_stats(yv, idx, wpos, bounds, S, regression)
         else:
             # children totals: each split node's left-child totals (prefix of its winning histogram up
             # to the split bin); node_feature >= 0 segments are in cand order == split order
-            left = torch.cat(res_left, 0)[torch.from_numpy(ci_sel).to(dev)]
-            split_seg = torch.from_numpy(np.nonzero(node_feature >= 0)[0]).to(dev)
+            left = torch.cat(res_left, 0)[_h2d(ci_sel, dev)]
+            split_seg = _h2d(np.nonzero(node_feature >= 0)[0], dev)
             right = tot[split_seg] - left
             tot = torch.stack([left, right], 1).reshape(2 * k, S)
         if data_parallel and regression:
             ctx.comm.allreduce(tot)
-        bounds_h = bounds.cpu().numpy().astype(np.int64)
+        # one copy: child bounds (exact in fp64 below 2^53 rows) and the children's totals
+        clk.mark("route_launch")
+        hb = torch.cat([bounds.double(), tot.reshape(-1).double()]).cpu().numpy()
+        clk.mark("end_sync")
+        bounds_h = hb[: 2 * k + 1].astype(np.int64)
+        tot_h = hb[2 * k + 1:].reshape(2 * k, -1)
         counts = np.diff(bounds_h)
         prev_parent = np.repeat(ci_sel, 2)  # new segments 2i, 2i + 1 come from candidate ci_sel[i]
         if not keep_hist:

@@ -1392,10 +1392,13 @@ def rf_bootstrap(T: int, m: int, rate: float, seed: int, device: torch.device
 
 
 def rf_partition(keys: torch.Tensor, bounds: torch.Tensor, node_feature: torch.Tensor, child_base: torch.Tensor,
-                 k: int, idx: torch.Tensor, wpos: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+                 k: int, idx: torch.Tensor, wpos: torch.Tensor, kept: Optional[int] = None
+                 ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """Stable re-partition of (idx, wpos) into the 2k child segments of the k split parents
     (child keys from ``rf_route_segments``; other positions leave the tree): (idx, wpos, bounds
-    of the 2k children). Device: prefix-count kernels + one scatter (``srml_rf_partition``)."""
+    of the 2k children). Device: prefix-count kernels + one scatter (``srml_rf_partition``).
+    ``kept``: the caller's count of positions in split parents (their rows all stay), which
+    spares reading it back from the device."""
     total = int(keys.shape[0])
     if not keys.is_cuda:
         keys_sorted, perm = torch.sort(keys, stable=True)
@@ -1413,7 +1416,8 @@ def rf_partition(keys: torch.Tensor, bounds: torch.Tensor, node_feature: torch.T
                 _c(node_feature.int()).data_ptr(), _c(child_base.int()).data_ptr(), int(k), _c(idx).data_ptr(),
                 _c(wpos.float()).data_ptr(), idx_out.data_ptr(), w_out.data_ptr(), nb.data_ptr(), ws.data_ptr(),
                 native.stream(dev))
-    kept = int(nb[-1].item())
+    if kept is None:
+        kept = int(nb[-1].item())
     return idx_out[:kept], w_out[:kept], nb
 
 
