@@ -1,7 +1,8 @@
-"""Poisson bagging (ops.rf_bootstrap) on the CPU path: distribution and layout."""
+"""Poisson bagging (ops.rf_bootstrap) on the CPU path: distribution and layout; per-segment stats."""
 import math
 
 import numpy as np
+import pytest
 import torch
 
 from spark_rapids_ml_nai_amd import ops
@@ -23,3 +24,20 @@ def test_rf_bootstrap_layout_and_distribution():
     assert torch.equal(idx, i2) and torch.equal(w, w2)  # reproducible
     i3, _, _ = ops.rf_bootstrap(T, m, rate, 100, torch.device("cpu"))
     assert not torch.equal(idx, i3)
+
+
+@pytest.mark.parametrize("regression,crit,S", [(True, 2, 3), (False, 0, 2), (False, 1, 5)])
+def test_seg_stats_match_numpy_formulas(regression, crit, S):
+    """Per-segment leaf values / weight sums / impurities formed on the device side (torch) equal
+    the numpy formulas, including empty segments."""
+    from spark_rapids_ml_nai_amd.models import forest
+
+    g = np.random.default_rng(S)
+    tot = g.random((500, S)) * 10
+    if regression:
+        tot[:, 2] = tot[:, 1] ** 2 / np.maximum(tot[:, 0], 1e-9) + g.random(500)
+    tot[::7] = 0.0
+    st = forest._seg_stats(torch.from_numpy(tot), regression, crit).numpy()
+    np.testing.assert_allclose(st[:, :-2], forest._leaf_values_np(tot, regression), rtol=1e-12, atol=1e-14)
+    np.testing.assert_allclose(st[:, -2], tot[:, 0] if regression else tot.sum(1), rtol=1e-12)
+    np.testing.assert_allclose(st[:, -1], forest._impurities_np(tot, crit), rtol=1e-12, atol=1e-14)
