@@ -147,7 +147,7 @@ def model_evidence(name: str, model: Any) -> Dict[str, Any]:
             ev["num_iters"] = int(model.num_iters)
             ev["objective"] = float(model.objective)
             info = getattr(model, "_solver_info", None) or {}
-            ev.update({k: info[k] for k in ("n_evals", "status", "path") if k in info})
+            ev.update({k: info[k] for k in ("n_evals", "n_margin_only", "status", "path") if k in info})
         elif name.startswith("random_forest"):
             ev["num_trees"] = int(model.getNumTrees)
             ev["total_nodes"] = int(model.totalNumNodes)

@@ -78,6 +78,8 @@ def _result(res: Dict[str, Any], base: Dict[str, Any], ctx: WorkerContext, n: in
     out.update(coef_=W.tolist(), intercept_=[float(v) for v in b], num_iters=int(res["iter"]),
                objective=float(res["f"]))
     out["_solver"] = {"n_evals": int(res["n_evals"]), "status": res["status"], "path": path}
+    if res.get("n_margin_only"):  # evaluations that read the cached margins instead of X
+        out["_solver"]["n_margin_only"] = int(res["n_margin_only"])
     return out
 
 
@@ -112,8 +114,9 @@ def logistic_fit(X: Any, y: torch.Tensor, m_total: int, ctx: WorkerContext, reg:
 
     ws = ops.logreg_workspace(X) if not sparse and K == 1 else None  # this fit's own partial rows
 
-    def evaluate(w: torch.Tensor, b: torch.Tensor, flag: Optional[torch.Tensor], out: torch.Tensor) -> None:
-        ops.logistic_loss_grad(X, y32, w, b, K, out, flag, ws=ws)
+    def evaluate(w: torch.Tensor, b: torch.Tensor, flag: Optional[torch.Tensor], out: torch.Tensor,
+                 zc: Optional[tuple] = None) -> None:
+        ops.logistic_loss_grad(X, y32, w, b, K, out, flag, ws=ws, zcache=zc)
 
     allreduce = ctx.comm.allreduce if ctx.distributed else None
     path = ops.logistic_path(X, K)
@@ -125,16 +128,20 @@ def logistic_fit(X: Any, y: torch.Tensor, m_total: int, ctx: WorkerContext, reg:
         fold = (ws, parts, wst)
         _scratch = torch.zeros(K * n + 2, dtype=torch.float64, device=X.device)
 
-        def evaluate_partials(w: torch.Tensor, b: torch.Tensor, flag: Optional[torch.Tensor]) -> None:
-            ops.logistic_loss_grad(X, y32, w, b, K, _scratch, flag, ws=ws, leave_partials=True)
+        def evaluate_partials(w: torch.Tensor, b: torch.Tensor, flag: Optional[torch.Tensor],
+                              zc: Optional[tuple] = None) -> None:
+            ops.logistic_loss_grad(X, y32, w, b, K, _scratch, flag, ws=ws, leave_partials=True, zcache=zc)
     # stream-ordered device evaluations (no host sync; allocations come from the graph's pool) may
     # be replayed from a HIP graph — when launches are what the batch costs: a graph is captured
     # and instantiated per fit (5.4 ms at the 125k x 3000 shard), while an evaluation reading more
     # than GRAPH_MAX_BYTES of X runs far longer than its five launches take to issue
     graph_safe = (path in ("fused_binary_f32", "fused_multinomial_f32", "csr_binary", "two_pass_multinomial_f32",
                            "two_pass_binary_f32") or path.startswith("lds_binary")) and _eval_bytes(X) <= GRAPH_MAX_BYTES
+    # line-search margin cache: binary fits on the prefetching kernel (ws exists exactly then)
+    zbuf = (torch.zeros(2 * X.shape[0], dtype=torch.float64, device=X.device)
+            if ws is not None and path == "fused_binary_f32" else None)
     res = minimize(P, theta0, evaluate, allreduce, y.device, batch=8 if not path.startswith("torch") else 2,
-                   graph_safe=graph_safe, fold=fold, evaluate_partials=evaluate_partials)
+                   graph_safe=graph_safe, fold=fold, evaluate_partials=evaluate_partials, zcache=zbuf)
     return _result(res, base, ctx, n, K, fit_intercept, inv_sigma, path)
 
 

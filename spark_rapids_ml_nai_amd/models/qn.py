@@ -46,8 +46,12 @@ QN_MB = QN_STEP in ("fused", "mb")
 GRAPH_STATS = {"captures": 0, "replays": 0}  # observability / tests
 STATUS = {0: "running", 1: "converged (gradient)", 2: "converged (objective change)", 3: "max iterations",
           4: "line search failed", 5: "barrier timeout"}
-F_DONE, F_STATUS, F_ITER, F_NEVAL, F_LS, F_COUNT, F_HEAD, F_STARTED, F_BRACKET = range(9)
-SC_F, SC_ALPHA, SC_DGINIT, SC_GAMMA, SC_GINF = range(5)
+F_DONE, F_STATUS, F_ITER, F_NEVAL, F_LS, F_COUNT, F_HEAD, F_STARTED, F_BRACKET, F_ZMODE, F_ZSEL, F_NCHEAP, F_ZC = \
+    range(13)
+SC_F, SC_ALPHA, SC_DGINIT, SC_GAMMA, SC_GINF, SC_ALPHA1, SC_BETA = range(7)
+# line-search margin cache (binary LogisticRegression on the multi-block step, Armijo, no L1): a
+# rejected trial's margins make the rest of its backtracking margins-only evaluations (qn.hip F_ZMODE)
+QN_ZCACHE = os.environ.get("SRML_QN_ZCACHE", "1") != "0"
 
 
 @dataclass
@@ -353,11 +357,22 @@ class DeviceQN:
     def theta(self) -> np.ndarray:
         return self.x.cpu().numpy().copy()
 
+    def zcache_supported(self) -> bool:
+        """The margin cache needs the multi-block step (the other steps ignore its flags), a
+        backtracking Armijo search and no L1 (the orthant projection is not linear in the step)."""
+        return self._mb is not None and not self._fused and not self.P.use_l1 and not self.P.wolfe
+
+    def enable_zcache(self, zbuf: torch.Tensor) -> tuple:
+        """Switch the margin cache on (``zbuf``: 2 m fp64): returns the evaluation's (flags, buffer,
+        scalars) triple for ``ops.logistic_loss_grad(zcache=...)``."""
+        self.flags[F_ZC] = 1
+        return (self.flags, zbuf, self._keep["sc"])
+
     def info(self) -> dict:
         fl = self.flags.cpu().numpy()
         sc = self._keep["sc"].cpu().numpy()
         return {"iter": int(fl[F_ITER]), "n_evals": int(fl[F_NEVAL]), "status": STATUS.get(int(fl[F_STATUS]), "?"),
-                "f": float(sc[SC_F]), "done": bool(fl[F_DONE])}
+                "f": float(sc[SC_F]), "done": bool(fl[F_DONE]), "n_margin_only": int(fl[F_NCHEAP])}
 
 
 # ------------------------------------------------------------------------------------------
@@ -381,7 +396,7 @@ def minimize(P: QNProblem, theta0: np.ndarray, evaluate: Callable[[torch.Tensor,
                                                                    torch.Tensor], None],
              allreduce: Optional[Callable[[torch.Tensor], None]], device: torch.device,
              batch: int = 8, graph_safe: bool = False, fold: Optional[tuple] = None,
-             evaluate_partials: Optional[Callable] = None) -> dict:
+             evaluate_partials: Optional[Callable] = None, zcache: Optional[torch.Tensor] = None) -> dict:
     """Run the QN iteration. ``evaluate(w, b, flag, out)`` must ADD the summed data-term
     [grad_w (K*n) | grad_b (K) | loss] of this rank's rows at (w, b) into ``out`` (device
     tensors; ``flag`` is the device done-flag it may use to early-exit, None on the host path).
@@ -392,6 +407,10 @@ def minimize(P: QNProblem, theta0: np.ndarray, evaluate: Callable[[torch.Tensor,
     ``fold`` = (workspace, rows, stride) with ``evaluate_partials(w, b, flag)``: a one-rank fit
     whose evaluation can leave per-block partial rows in the workspace instead of summing into
     ``out``; the fused device step then folds them itself (one launch less per evaluation).
+
+    ``zcache`` (2 m fp64, binary LogisticRegression on the prefetching kernel): the line-search
+    margin cache — ``evaluate`` / ``evaluate_partials`` then take a ``zc`` keyword (see
+    ``DeviceQN.enable_zcache``) and a rejected trial's backtracking costs margins-only passes.
 
     Returns {theta, f, iter, n_evals, status}.
     """
@@ -409,21 +428,26 @@ def minimize(P: QNProblem, theta0: np.ndarray, evaluate: Callable[[torch.Tensor,
         return {"theta": st.theta(), "f": st.f, "iter": st.iter, "n_evals": st.n_evals,
                 "status": STATUS[st.status if st.done else 3]}
     q = DeviceQN(P, theta0, device)
+    zc = None
+    if zcache is not None and QN_ZCACHE and q.zcache_supported():
+        zc = q.enable_zcache(zcache)
     if fold is not None and evaluate_partials is not None and allreduce is None and q._mb is not None:
         q.fold = fold
-        evaluate = lambda w, b, flag, out: evaluate_partials(w, b, flag)  # noqa: E731
+        evaluate = lambda w, b, flag, out, **kw: evaluate_partials(w, b, flag, **kw)  # noqa: E731
+    zkw = {"zc": zc} if zc is not None else {}
     poll = _comm_poll(allreduce)
     flag = q.flags[F_DONE: F_DONE + 1]
     host_flag = torch.zeros(2, dtype=torch.int32, pin_memory=True)
     events: list = []
-    cap = max(1, P.max_iter) * (P.max_ls + 1) + 2
+    # a margins-only trial accepted costs one more (full) evaluation of its iteration
+    cap = max(1, P.max_iter) * (P.max_ls + (2 if zc is not None else 1)) + 2
     evals = 0
     stream = torch.cuda.current_stream(device)
     j = 0
 
     def run_batch() -> None:
         for _ in range(batch):
-            evaluate(q.w_dev, q.b_dev, flag, q.out)
+            evaluate(q.w_dev, q.b_dev, flag, q.out, **zkw)
             if allreduce is not None:
                 allreduce(q.out)
             q.step()

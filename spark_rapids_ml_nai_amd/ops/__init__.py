@@ -2505,12 +2505,14 @@ def logistic_loss_grad_multi(X: torch.Tensor, y32: torch.Tensor, WB: torch.Tenso
 
 def logistic_loss_grad(X, y32: torch.Tensor, w: torch.Tensor, b: torch.Tensor, K: int, out: torch.Tensor,
                        flag: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None,
-                       leave_partials: bool = False) -> torch.Tensor:
+                       leave_partials: bool = False, zcache: Optional[tuple] = None) -> torch.Tensor:
     """ADD the summed logistic data term at (W, b) into ``out`` = [grad W (K*n, class-major) |
     grad b (K) | loss sum] (fp64). K == 1: binary (labels 0/1, sigmoid); K >= 2: softmax over K
     classes (labels 0..K-1). ``w`` (K*n) and ``b`` (K) are fp64 device tensors read by the kernel
     (no host round trip); ``flag`` (device int32, optional): the kernels skip once it is non-zero.
-    X: dense (m, n) or CSR."""
+    ``zcache`` = (QN flags, 2 m fp64 margin buffers, QN scalars): the line-search margin cache of
+    the binary prefetching kernel (``srml_logreg_binary4_f32``; the caller checked a fold
+    workspace exists for X, i.e. that kernel runs). X: dense (m, n) or CSR."""
     path = logistic_path(X, K)
     if _is_csr(X):
         m, n = X.shape
@@ -2593,9 +2595,16 @@ def logistic_loss_grad(X, y32: torch.Tensor, w: torch.Tensor, b: torch.Tensor, K
     elif path == "fused_binary_f32":
         # ws: the fit's partial-row workspace (ops.logreg_workspace), None = per-block atomic flush;
         # leave_partials: the rows stay unfolded for the fused optimiser step (srml_qn_step_fused)
-        native.call("srml_logreg_binary3_f32", X.data_ptr(), m, n, X.stride(0), y32.data_ptr(), w.data_ptr(), 0.0,
-                    b.data_ptr(), fp, out.data_ptr(), ws.data_ptr() if ws is not None else None,
-                    int(bool(leave_partials and ws is not None)), st)
+        if zcache is not None:
+            zfl, zb, zsc = zcache
+            native.call("srml_logreg_binary4_f32", X.data_ptr(), m, n, X.stride(0), y32.data_ptr(), w.data_ptr(),
+                        0.0, b.data_ptr(), fp, out.data_ptr(), ws.data_ptr() if ws is not None else None,
+                        int(bool(leave_partials and ws is not None)), zfl.data_ptr(), zb.data_ptr(), zsc.data_ptr(),
+                        st)
+        else:
+            native.call("srml_logreg_binary3_f32", X.data_ptr(), m, n, X.stride(0), y32.data_ptr(), w.data_ptr(),
+                        0.0, b.data_ptr(), fp, out.data_ptr(), ws.data_ptr() if ws is not None else None,
+                        int(bool(leave_partials and ws is not None)), st)
     elif path.startswith("lds_binary"):
         native.call("srml_logreg_binary_lds_" + path[-3:], X.data_ptr(), m, n, X.stride(0), y32.data_ptr(),
                     w.data_ptr(), 0.0, b.data_ptr(), fp, out.data_ptr(), st)

@@ -616,6 +616,15 @@ __global__ __launch_bounds__(256, 2) void logreg_binary_split_kernel(const float
 // loaded into a second register set while the current batch's margins are reduced / exchanged
 // through LDS and its gradient is accumulated, so each wave keeps 2 * R * V * 1 KiB of X in flight
 // across the per-batch barrier (the kernel is HBM-latency bound, not VALU bound).
+// Line-search margin cache (zfl != null; the optimiser's flag block, see qn.hip F_ZMODE): along a
+// search direction the margins are linear in the step, z(a) = z0 + (a / a1) (z(a1) - z0), so once
+// a full evaluation at a1 is rejected, the backtracking trials need only the loss from the two
+// stored margin vectors (16 B per row instead of the row's n floats):
+//   mode 0 / 2  full pass; the row margins (intercept included) go to zb[(1 - zsel) m + r];
+//   mode 1      loss / bias gradient from z0 = zb[zsel m ..], z1 = zb[(1 - zsel) m ..] and
+//               beta = zsc[SC_BETA]; the gradient columns of the partial row are zero.
+constexpr int LR_F_ZMODE = 9, LR_F_ZSEL = 10, LR_SC_BETA = 6;
+
 template <int V, int R, int D, bool NT = false>
 __global__ __launch_bounds__(256, 2) void logreg_binary_pf_kernel(const float* __restrict__ X, long m, int n, long ld,
                                                                   const float* __restrict__ y,
@@ -623,12 +632,58 @@ __global__ __launch_bounds__(256, 2) void logreg_binary_pf_kernel(const float* _
                                                                   const double* __restrict__ bptr,
                                                                   const int* __restrict__ flag,
                                                                   double* __restrict__ out, long rows_per_block,
-                                                                  float* __restrict__ ws) {
+                                                                  float* __restrict__ ws, const int* __restrict__ zfl,
+                                                                  double* __restrict__ zb,
+                                                                  const double* __restrict__ zsc) {
   if (flag && *flag) return;
   const double b = bptr ? *bptr : b_in;
   __shared__ double part[2][R][4];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
+  const int zmode = zfl ? zfl[LR_F_ZMODE] : 0;
+  const int zsel = zfl ? zfl[LR_F_ZSEL] : 0;
+  if (zmode == 1) {
+    const double beta = zsc[LR_SC_BETA];
+    const double* z0 = zb + (long)zsel * m;
+    const double* z1 = zb + (long)(1 - zsel) * m;
+    const long q0 = (long)blockIdx.x * rows_per_block;
+    const long q1 = min(m, q0 + rows_per_block);
+    double gbc = 0.0, lossc = 0.0;
+    for (long r = q0 + threadIdx.x; r < q1; r += 256) {
+      const double a = z0[r];
+      double res, lt;
+      logistic_terms(a + beta * (z1[r] - a), (double)y[r], res, lt);
+      gbc += res;
+      lossc += lt;
+    }
+    gbc = wave_sum(gbc);
+    lossc = wave_sum(lossc);
+    if (lane == 0) {
+      part[0][0][wid] = gbc;
+      part[1][0][wid] = lossc;
+    }
+    __syncthreads();
+    gbc = (part[0][0][0] + part[0][0][1]) + (part[0][0][2] + part[0][0][3]);
+    lossc = (part[1][0][0] + part[1][0][1]) + (part[1][0][2] + part[1][0][3]);
+    if (ws == nullptr) {
+      if (threadIdx.x == 0) {
+        atomicAdd(&out[n], gbc);
+        atomicAdd(&out[n + 1], lossc);
+      }
+      return;
+    }
+    const long wsc = (long)((n + 3) & ~3) + 4;
+    float* mine = ws + (long)blockIdx.x * wsc;
+    for (int c = 4 * threadIdx.x; c < n; c += 1024)
+      *reinterpret_cast<floatx4*>(mine + c) = floatx4{0.f, 0.f, 0.f, 0.f};
+    if (threadIdx.x == 0) {
+      double* md = reinterpret_cast<double*>(mine + wsc - 4);
+      md[0] = gbc;
+      md[1] = lossc;
+    }
+    return;
+  }
+  double* zw = zfl ? zb + (long)(1 - zsel) * m : nullptr;
   const int cbase = wid * 256 * V;
   double wreg[V][4];
   int coff[V];
@@ -682,6 +737,7 @@ __global__ __launch_bounds__(256, 2) void logreg_binary_pf_kernel(const float* _
         if (wid == 0 && lane == 0) {
           loss += lt;
           gb += res;
+          if (zw) zw[r] = z;
         }
         const float rf = (float)res;
 #pragma unroll
@@ -960,7 +1016,8 @@ SRML_API long srml_logreg_fold_parts(long m) { return m <= 0 ? 0 : logreg_grid(m
 
 static int logreg_binary_launch(const float* X, long m, int n, long ld, const float* y, const double* w, double b,
                                 const double* bptr, const int* flag, double* out, float* fold_ws, int leave,
-                                hipStream_t stream);
+                                hipStream_t stream, const int* zfl = nullptr, double* zb = nullptr,
+                                const double* zsc = nullptr);
 
 // b: intercept by value, or (bptr != null) read on the device; flag (optional): skip when *flag != 0
 SRML_API int srml_logreg_binary2_f32(const float* X, long m, int n, long ld, const float* y, const double* w, double b,
@@ -978,10 +1035,21 @@ SRML_API int srml_logreg_binary3_f32(const float* X, long m, int n, long ld, con
   return logreg_binary_launch(X, m, n, ld, y, w, b, bptr, flag, out, fold_ws, leave, stream);
 }
 
+// Same with the optimiser's line-search margin cache (see logreg_binary_pf_kernel): zfl = the QN
+// flag block, zb = 2 m doubles of margins, zsc = the QN scalars. Only the prefetching column-split
+// kernel implements it: -2 for any other shape (the caller checks srml_logreg_fold_ws > 0 first).
+SRML_API int srml_logreg_binary4_f32(const float* X, long m, int n, long ld, const float* y, const double* w, double b,
+                                     const double* bptr, const int* flag, double* out, float* fold_ws, int leave,
+                                     const int* zfl, double* zb, const double* zsc, hipStream_t stream) {
+  if (m > 0 && !logreg_pf_eligible(n, ld, X)) return -2;
+  return logreg_binary_launch(X, m, n, ld, y, w, b, bptr, flag, out, fold_ws, leave, stream, zfl, zb, zsc);
+}
+
 static int logreg_binary_launch(const float* X, long m, int n, long ld, const float* y, const double* w, double b,
                                 const double* bptr, const int* flag, double* out, float* fold_ws, int leave,
-                                hipStream_t stream) {
+                                hipStream_t stream, const int* zfl, double* zb, const double* zsc) {
   if (m <= 0) return 0;
+  if (zfl && !logreg_pf_eligible(n, ld, X)) return -2;
   static const int narrow = getenv("SRML_LOGREG_NARROW") ? atoi(getenv("SRML_LOGREG_NARROW")) : 1;
   if (narrow && n <= 512 && (n & 3) == 0 && (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0) {
     long nb = m / 256;  // ~256 rows (16 steps of 16) per block, 512 .. 4096 blocks
@@ -1022,7 +1090,7 @@ static int logreg_binary_launch(const float* X, long m, int n, long ld, const fl
     float* fws = logreg_fold_enabled() ? fold_ws : nullptr;
 #define SRML_LR_PF(VV, RR, DD)                                                                              \
     hipLaunchKernelGGL((logreg_binary_pf_kernel<VV, RR, DD>), grid, blk, 0, stream, X, m, n, ld, y, w, b, bptr, \
-                       flag, out, rpb, fws)
+                       flag, out, rpb, fws, zfl, zb, zsc)
 #define SRML_LR_PF_V(RR, DD) \
     do { if (VS == 2) SRML_LR_PF(2, RR, DD); else if (VS == 3) SRML_LR_PF(3, RR, DD); else SRML_LR_PF(4, RR, DD); } while (0)
     if (rsel == 2 && dsel == 1) SRML_LR_PF_V(2, 1);
@@ -1031,7 +1099,7 @@ static int logreg_binary_launch(const float* X, long m, int n, long ld, const fl
     else if (dsel == 3 && nt) {
 #define SRML_LR_PF_NT(VV)                                                                                        \
   hipLaunchKernelGGL((logreg_binary_pf_kernel<VV, 1, 3, true>), grid, blk, 0, stream, X, m, n, ld, y, w, b, bptr, \
-                     flag, out, rpb, fws)
+                     flag, out, rpb, fws, zfl, zb, zsc)
       if (VS == 2) SRML_LR_PF_NT(2);
       else if (VS == 3) SRML_LR_PF_NT(3);
       else SRML_LR_PF_NT(4);

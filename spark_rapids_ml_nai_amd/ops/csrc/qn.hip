@@ -32,9 +32,15 @@ constexpr int QN_NW = QN_T / 64;
 constexpr int QN_MMAX = 12;    // history capacity (runtime M <= 12; the reference uses 10)
 constexpr int QN_NV = 6 + 5 * QN_MMAX;
 
-enum { F_DONE = 0, F_STATUS, F_ITER, F_NEVAL, F_LS, F_COUNT, F_HEAD, F_STARTED, F_BRACKET };
+// F_ZC .. F_NCHEAP / SC_ALPHA1, SC_BETA: the line-search margin cache of the multi-block step
+// (binary LogisticRegression, Armijo, no L1; glm.hip logreg_binary_pf_kernel reads F_ZMODE /
+// F_ZSEL / SC_BETA): F_ZMODE is the mode of the NEXT evaluation — 0 full, 1 margins-only (a
+// backtracking trial: loss from z0 + beta (z1 - z0)), 2 full at a point a margins-only trial
+// already accepted; F_ZSEL selects which of the two margin buffers holds z0 (the accepted point).
+enum { F_DONE = 0, F_STATUS, F_ITER, F_NEVAL, F_LS, F_COUNT, F_HEAD, F_STARTED, F_BRACKET, F_ZMODE, F_ZSEL,
+       F_NCHEAP, F_ZC };
 enum { ST_RUNNING = 0, ST_CONV_GRAD = 1, ST_CONV_F = 2, ST_MAXITER = 3, ST_LS_FAIL = 4 };
-enum { SC_F = 0, SC_ALPHA, SC_DGINIT, SC_GAMMA, SC_GINF };
+enum { SC_F = 0, SC_ALPHA, SC_DGINIT, SC_GAMMA, SC_GINF, SC_ALPHA1, SC_BETA };
 
 }  // namespace
 
@@ -622,6 +628,7 @@ constexpr int MB_GAMAX = 512;  // K1 partial rows: the folding K1 runs ceil(N / 
 constexpr int MB_PW = 6 + 5 * QN_MMAX + 1;  // pass-1 partials: 6 dots, 5 history products per slot, max |pg|
 enum {
   S_STARTED = 0, S_ITER, S_COUNT, S_HEAD, S_LS, S_NEVAL, S_BRACKET, S_F, S_ALPHA, S_DGINIT, S_GAMMA, S_FHN, S_LOSS,
+  S_ZMODE, S_ZC, S_ALPHA1,
   S_PHASE = 16, S_STATUS, S_NEWP, S_CNT, S_HD, S_GAM, S_FT, S_GINF, S_ITERN, S_FN,
   S_CF = 32,                              // cf_a[QN_MMAX] | cf_t[QN_MMAX]
   S_SL = S_CF + 2 * QN_MMAX,              // chronological slots [QN_MMAX]
@@ -698,8 +705,8 @@ __device__ __forceinline__ void mb_grid_sum(const double* part, int G, int width
 // pre-step snapshot of the flags / scalars (block 0, thread 0 of K1): later kernels read these,
 // K2 / K4 rewrite the flags
 struct MbSnap {
-  int started, iter, count, head, ls, neval, bracket;
-  double f, alpha, dginit, gamma;
+  int started, iter, count, head, ls, neval, bracket, zmode, zc;
+  double f, alpha, dginit, gamma, alpha1;
 };
 
 __device__ __forceinline__ MbSnap mb_snap_load(const QnArgs& A) {
@@ -716,6 +723,9 @@ __device__ __forceinline__ MbSnap mb_snap_load(const QnArgs& A) {
   q.alpha = A.sc[SC_ALPHA];
   q.dginit = A.sc[SC_DGINIT];
   q.gamma = A.sc[SC_GAMMA];
+  q.zc = fl[F_ZC];
+  q.zmode = q.zc ? fl[F_ZMODE] : 0;
+  q.alpha1 = A.sc[SC_ALPHA1];
   return q;
 }
 
@@ -732,6 +742,9 @@ __device__ __forceinline__ void mb_snap_store(const QnArgs& A, const MbSnap& q, 
   scr[S_DGINIT] = q.dginit;
   scr[S_GAMMA] = q.gamma;
   scr[S_FHN] = (A.past > 0 && q.started) ? A.fh[(q.iter + 1) % A.past] : 0.0;
+  scr[S_ZMODE] = q.zmode;
+  scr[S_ZC] = q.zc;
+  scr[S_ALPHA1] = q.alpha1;
   scr[S_PHASE] = 0.0;
 }
 
@@ -819,6 +832,9 @@ __global__ __launch_bounds__(MB_T) void qn_mb2_kernel(QnArgs A, double* __restri
   const double f = scr[S_F], dginit = scr[S_DGINIT], alpha0 = scr[S_ALPHA], loss = scr[S_LOSS];
   const bool bracket = scr[S_BRACKET] != 0.0;
   const int pre_ls = (int)scr[S_LS], pre_neval = (int)scr[S_NEVAL];
+  const bool zc = scr[S_ZC] != 0.0;
+  const int zmode = (int)scr[S_ZMODE];
+  const double alpha1 = scr[S_ALPHA1];
   double xt = 0.0, gt = 0.0, xo = 0.0, go = 0.0, cv = 0.0, dv = 0.0, pv = 0.0, isg = 1.0;
   double Sv[QN_MMAX], Yv[QN_MMAX];
   if (own) {
@@ -842,10 +858,14 @@ __global__ __launch_bounds__(MB_T) void qn_mb2_kernel(QnArgs A, double* __restri
   const double ft = loss * A.inv_m + 0.5 * p0[0] + p0[1];
   if (first)  // the loss sum (read from the snapshot) and bias sums without a parameter (no intercept)
     for (long j = N; j < A.Kn + A.K + 1; ++j) A.out[j] = 0.0;
+  if (first && zc && zmode == 1) fl[F_NCHEAP] += 1;
   if (started) {
     bool accept = true;
     double width = 1.0;
-    if (!isfinite(ft)) {
+    if (zc && zmode == 2 && isfinite(ft)) {
+      // a margins-only trial passed the test at this point: this full evaluation supplies its
+      // gradient (and the exact loss), nothing is re-tested
+    } else if (!isfinite(ft)) {
       accept = false;
       width = 0.5;
     } else {
@@ -878,6 +898,23 @@ __global__ __launch_bounds__(MB_T) void qn_mb2_kernel(QnArgs A, double* __restri
         fl[F_NEVAL] = pre_neval + 1;
         if (width < 1.0) fl[F_BRACKET] = 1;
         A.sc[SC_ALPHA] = alpha;
+        if (zc && isfinite(ft)) {
+          // the rejected full evaluation's margins (at step alpha0) become z1; later trials of this
+          // search are margins-only evaluations at beta = alpha / alpha1
+          const double a1 = zmode == 0 ? alpha0 : alpha1;
+          A.sc[SC_ALPHA1] = a1;
+          A.sc[SC_BETA] = alpha / a1;
+          fl[F_ZMODE] = 1;
+        } else if (zc) {
+          fl[F_ZMODE] = 0;  // a non-finite loss: no trusted margins, the next trial runs in full
+        }
+      }
+      return;
+    }
+    if (zc && zmode == 1) {  // accepted on margins only: evaluate the same point in full next
+      if (first) {
+        fl[F_NEVAL] = pre_neval + 1;
+        fl[F_ZMODE] = 2;
       }
       return;
     }
@@ -885,6 +922,10 @@ __global__ __launch_bounds__(MB_T) void qn_mb2_kernel(QnArgs A, double* __restri
   if (first) {
     scr[S_PHASE] = 1.0;
     scr[S_FT] = ft;
+    if (zc) {  // this full evaluation's margins (the other buffer) are the new accepted point's
+      fl[F_ZSEL] ^= 1;
+      fl[F_ZMODE] = 0;
+    }
   }
   // accepted: pass 1 partials of this block's elements
   double v[MB_PW];

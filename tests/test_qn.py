@@ -336,6 +336,73 @@ def test_logistic_fit_fused_fold_matches_unfused(gpu_device, monkeypatch):
 
 
 @pytest.mark.gpu
+def test_logreg_margin_only_evaluation_matches_full(gpu_device):
+    """The line-search margin cache: full evaluations store the row margins; a margins-only
+    evaluation at beta between two stored points gives the loss / bias gradient of a full pass at
+    w0 + beta (w1 - w0) (margins are linear along a search direction) and no gradient columns."""
+    from spark_rapids_ml_nai_amd import ops
+
+    rng = np.random.default_rng(21)
+    m, n = 9000, 1100
+    X = torch.from_numpy(rng.standard_normal((m, n)).astype(np.float32)).to(gpu_device)
+    y = torch.from_numpy((rng.random(m) > 0.4).astype(np.float32)).to(gpu_device)
+    assert ops.logreg_workspace(X) is not None
+    w0 = torch.from_numpy(rng.standard_normal(n) * 0.05).to(gpu_device)
+    w1 = torch.from_numpy(rng.standard_normal(n) * 0.05).to(gpu_device)
+    b0 = torch.tensor([0.3], dtype=torch.float64, device=gpu_device)
+    b1 = torch.tensor([-0.2], dtype=torch.float64, device=gpu_device)
+    fl = torch.zeros(16, dtype=torch.int32, device=gpu_device)
+    zb = torch.zeros(2 * m, dtype=torch.float64, device=gpu_device)
+    sc = torch.zeros(8, dtype=torch.float64, device=gpu_device)
+    outs = []
+    for w, b, zsel in ((w0, b0, 1), (w1, b1, 0)):  # margins of w0 -> zb[0:m] (z0), w1 -> zb[m:] (z1)
+        fl[10] = zsel
+        o = torch.zeros(n + 2, dtype=torch.float64, device=gpu_device)
+        ops.logistic_loss_grad(X, y, w, b, 1, o, zcache=(fl, zb, sc))
+        outs.append(o)
+    fl[10] = 0
+    fl[9] = 1
+    beta = 0.37
+    sc[6] = beta
+    oc = torch.zeros(n + 2, dtype=torch.float64, device=gpu_device)
+    ops.logistic_loss_grad(X, y, w0, b0, 1, oc, zcache=(fl, zb, sc))
+    of = torch.zeros(n + 2, dtype=torch.float64, device=gpu_device)
+    ops.logistic_loss_grad(X, y, w0 + beta * (w1 - w0), b0 + beta * (b1 - b0), 1, of)
+    assert torch.count_nonzero(oc[:n]) == 0
+    torch.testing.assert_close(oc[n:], of[n:], rtol=1e-9, atol=1e-9)
+    # the stored margins themselves: z = X w + b in fp64 from fp32 rows
+    zref = X.double() @ w0 + b0
+    torch.testing.assert_close(zb[:m], zref, rtol=1e-9, atol=1e-7)
+
+
+@pytest.mark.gpu
+def test_logistic_fit_margin_cache_matches_full_evaluations(gpu_device, monkeypatch):
+    """A fit whose rejected line-search trials are margins-only evaluations reaches the optimum of
+    the all-full-evaluation fit, with fewer passes over X."""
+    from spark_rapids_ml_nai_amd.models import qn as qnm
+    from spark_rapids_ml_nai_amd.models.logistic import logistic_fit
+    from spark_rapids_ml_nai_amd.parallel.context import WorkerContext
+
+    rng = np.random.default_rng(12)
+    m, n = 30000, 1200
+    X = rng.standard_normal((m, n)).astype(np.float32)
+    y = (X[:, :10].sum(1) + 2.0 * rng.standard_normal(m) > 0).astype(np.float32)
+    Xt, yt = torch.from_numpy(X).to(gpu_device), torch.from_numpy(y).to(gpu_device)
+    ctx = WorkerContext.single(gpu_device)
+    out = {}
+    for zc in (False, True):
+        monkeypatch.setattr(qnm, "QN_ZCACHE", zc)
+        out[zc] = logistic_fit(Xt, yt, m, ctx, reg=1e-5, l1_ratio=0.0, fit_intercept=True,
+                               standardization=False, max_iter=200, tol=1e-30)
+    a, b = out[False], out[True]
+    assert abs(a["objective"] - b["objective"]) <= 1e-7 * abs(a["objective"]), (a["objective"], b["objective"])
+    np.testing.assert_allclose(np.asarray(b["coef_"]), np.asarray(a["coef_"]), rtol=2e-2, atol=2e-3)
+    sb = b["_solver"]
+    assert sb.get("n_margin_only", 0) > 0, sb
+    assert sb["n_evals"] - sb["n_margin_only"] < a["_solver"]["n_evals"], (a["_solver"], sb)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n", [1501, 3001])
 def test_logistic_fit_unaligned_width_has_no_fold(gpu_device, monkeypatch, n):
     """A width the prefetching kernel rejects (n % 4 != 0) gets no partial-row workspace, so the
