@@ -320,6 +320,17 @@ def logreg_workspace(X: Any) -> Optional[torch.Tensor]:
     return torch.empty(nf, dtype=torch.float32, device=X.device) if nf > 0 else None
 
 
+def logreg_zcache_ok(X: Any) -> bool:
+    """Whether the binary evaluation of this shard runs a kernel with the optimiser's line-search
+    margin cache (``srml_logreg_zcache_ok``: the narrow n <= 512 / prefetching 1024 < n <= 4096
+    kernels)."""
+    if _is_csr(X) or not X.is_cuda or X.dtype != torch.float32 or deterministic():
+        return False
+    m, n = X.shape
+    ptr, ld = (X.data_ptr(), X.stride(0)) if X.is_contiguous() else (0, n)
+    return bool(int(native.lib().srml_logreg_zcache_ok(m, n, ld, ptr)))
+
+
 def nearest_centroid(X: torch.Tensor, C: torch.Tensor, xnorm: Optional[torch.Tensor] = None,
                      cnorm: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """(labels int32 [m], squared distance fp32 [m]) of each row's nearest centroid (fused, no m x k matrix)."""

@@ -625,6 +625,52 @@ __global__ __launch_bounds__(256, 2) void logreg_binary_split_kernel(const float
 //               beta = zsc[SC_BETA]; the gradient columns of the partial row are zero.
 constexpr int LR_F_ZMODE = 9, LR_F_ZSEL = 10, LR_SC_BETA = 6;
 
+// margins-only evaluation of one block's rows (zmode 1, see logreg_binary_pf_kernel): loss and
+// bias gradient from z0 + beta (z1 - z0); the partial row's gradient columns (ws) are zero
+__device__ __forceinline__ void lr_margin_only(long m, int n, const float* __restrict__ y, double* __restrict__ out,
+                                               float* __restrict__ ws, const double* __restrict__ zb,
+                                               const double* __restrict__ zsc, int zsel, long q0, long rows) {
+  __shared__ double mred[2][4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const double beta = zsc[LR_SC_BETA];
+  const double* z0 = zb + (long)zsel * m;
+  const double* z1 = zb + (long)(1 - zsel) * m;
+  const long q1 = min(m, q0 + rows);
+  double gbc = 0.0, lossc = 0.0;
+  for (long r = q0 + threadIdx.x; r < q1; r += blockDim.x) {
+    const double a = z0[r];
+    double res, lt;
+    logistic_terms(a + beta * (z1[r] - a), (double)y[r], res, lt);
+    gbc += res;
+    lossc += lt;
+  }
+  gbc = wave_sum(gbc);
+  lossc = wave_sum(lossc);
+  if (lane == 0) {
+    mred[0][wid] = gbc;
+    mred[1][wid] = lossc;
+  }
+  __syncthreads();
+  gbc = (mred[0][0] + mred[0][1]) + (mred[0][2] + mred[0][3]);
+  lossc = (mred[1][0] + mred[1][1]) + (mred[1][2] + mred[1][3]);
+  if (ws == nullptr) {
+    if (threadIdx.x == 0) {
+      if (gbc != 0.0) atomicAdd(&out[n], gbc);
+      if (lossc != 0.0) atomicAdd(&out[n + 1], lossc);
+    }
+    return;
+  }
+  const long wsc = (long)((n + 3) & ~3) + 4;
+  float* mine = ws + (long)blockIdx.x * wsc;
+  for (int c = 4 * threadIdx.x; c < n; c += 4 * blockDim.x)
+    *reinterpret_cast<floatx4*>(mine + c) = floatx4{0.f, 0.f, 0.f, 0.f};
+  if (threadIdx.x == 0) {
+    double* md = reinterpret_cast<double*>(mine + wsc - 4);
+    md[0] = gbc;
+    md[1] = lossc;
+  }
+}
+
 template <int V, int R, int D, bool NT = false>
 __global__ __launch_bounds__(256, 2) void logreg_binary_pf_kernel(const float* __restrict__ X, long m, int n, long ld,
                                                                   const float* __restrict__ y,
@@ -643,44 +689,7 @@ __global__ __launch_bounds__(256, 2) void logreg_binary_pf_kernel(const float* _
   const int zmode = zfl ? zfl[LR_F_ZMODE] : 0;
   const int zsel = zfl ? zfl[LR_F_ZSEL] : 0;
   if (zmode == 1) {
-    const double beta = zsc[LR_SC_BETA];
-    const double* z0 = zb + (long)zsel * m;
-    const double* z1 = zb + (long)(1 - zsel) * m;
-    const long q0 = (long)blockIdx.x * rows_per_block;
-    const long q1 = min(m, q0 + rows_per_block);
-    double gbc = 0.0, lossc = 0.0;
-    for (long r = q0 + threadIdx.x; r < q1; r += 256) {
-      const double a = z0[r];
-      double res, lt;
-      logistic_terms(a + beta * (z1[r] - a), (double)y[r], res, lt);
-      gbc += res;
-      lossc += lt;
-    }
-    gbc = wave_sum(gbc);
-    lossc = wave_sum(lossc);
-    if (lane == 0) {
-      part[0][0][wid] = gbc;
-      part[1][0][wid] = lossc;
-    }
-    __syncthreads();
-    gbc = (part[0][0][0] + part[0][0][1]) + (part[0][0][2] + part[0][0][3]);
-    lossc = (part[1][0][0] + part[1][0][1]) + (part[1][0][2] + part[1][0][3]);
-    if (ws == nullptr) {
-      if (threadIdx.x == 0) {
-        atomicAdd(&out[n], gbc);
-        atomicAdd(&out[n + 1], lossc);
-      }
-      return;
-    }
-    const long wsc = (long)((n + 3) & ~3) + 4;
-    float* mine = ws + (long)blockIdx.x * wsc;
-    for (int c = 4 * threadIdx.x; c < n; c += 1024)
-      *reinterpret_cast<floatx4*>(mine + c) = floatx4{0.f, 0.f, 0.f, 0.f};
-    if (threadIdx.x == 0) {
-      double* md = reinterpret_cast<double*>(mine + wsc - 4);
-      md[0] = gbc;
-      md[1] = lossc;
-    }
+    lr_margin_only(m, n, y, out, ws, zb, zsc, zsel, (long)blockIdx.x * rows_per_block, rows_per_block);
     return;
   }
   double* zw = zfl ? zb + (long)(1 - zsel) * m : nullptr;
@@ -809,8 +818,18 @@ __global__ __launch_bounds__(256) void logreg_binary_narrow_kernel(const float* 
                                                                    const double* __restrict__ w, double b_in,
                                                                    const double* __restrict__ bptr,
                                                                    const int* __restrict__ flag,
-                                                                   double* __restrict__ out, long rows_per_block) {
+                                                                   double* __restrict__ out, long rows_per_block,
+                                                                   const int* __restrict__ zfl,
+                                                                   double* __restrict__ zb,
+                                                                   const double* __restrict__ zsc) {
   if (flag && *flag) return;
+  const int zmode = zfl ? zfl[LR_F_ZMODE] : 0;
+  const int zsel = zfl ? zfl[LR_F_ZSEL] : 0;
+  if (zmode == 1) {  // line-search margin cache: see logreg_binary_pf_kernel
+    lr_margin_only(m, n, y, out, nullptr, zb, zsc, zsel, (long)blockIdx.x * rows_per_block, rows_per_block);
+    return;
+  }
+  double* zw = zfl ? zb + (long)(1 - zsel) * m : nullptr;
   __shared__ float gsum[4][64 * G];
   __shared__ double red[2][4];
   const double b = bptr ? *bptr : b_in;
@@ -858,6 +877,7 @@ __global__ __launch_bounds__(256) void logreg_binary_narrow_kernel(const float* 
       if (sub == 0) {
         loss += lt;
         gb += res;
+        if (zw) zw[r] = dot + b;
       }
       const float rf = (float)res;
 #pragma unroll
@@ -1038,10 +1058,21 @@ SRML_API int srml_logreg_binary3_f32(const float* X, long m, int n, long ld, con
 // Same with the optimiser's line-search margin cache (see logreg_binary_pf_kernel): zfl = the QN
 // flag block, zb = 2 m doubles of margins, zsc = the QN scalars. Only the prefetching column-split
 // kernel implements it: -2 for any other shape (the caller checks srml_logreg_fold_ws > 0 first).
+static bool logreg_narrow_eligible(int n, long ld, const void* X) {
+  static const int narrow = getenv("SRML_LOGREG_NARROW") ? atoi(getenv("SRML_LOGREG_NARROW")) : 1;
+  return narrow && n <= 512 && (n & 3) == 0 && (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
+}
+
+// Whether the evaluation of X (m x n, row stride ld) runs a kernel with the line-search margin
+// cache (the narrow n <= 512 or the prefetching 1024 < n <= 4096 kernel).
+SRML_API int srml_logreg_zcache_ok(long m, int n, long ld, const void* X) {
+  return m > 0 && (logreg_narrow_eligible(n, ld, X) || logreg_pf_eligible(n, ld, X)) ? 1 : 0;
+}
+
 SRML_API int srml_logreg_binary4_f32(const float* X, long m, int n, long ld, const float* y, const double* w, double b,
                                      const double* bptr, const int* flag, double* out, float* fold_ws, int leave,
                                      const int* zfl, double* zb, const double* zsc, hipStream_t stream) {
-  if (m > 0 && !logreg_pf_eligible(n, ld, X)) return -2;
+  if (m > 0 && !srml_logreg_zcache_ok(m, n, ld, X)) return -2;
   return logreg_binary_launch(X, m, n, ld, y, w, b, bptr, flag, out, fold_ws, leave, stream, zfl, zb, zsc);
 }
 
@@ -1049,9 +1080,8 @@ static int logreg_binary_launch(const float* X, long m, int n, long ld, const fl
                                 const double* bptr, const int* flag, double* out, float* fold_ws, int leave,
                                 hipStream_t stream, const int* zfl, double* zb, const double* zsc) {
   if (m <= 0) return 0;
-  if (zfl && !logreg_pf_eligible(n, ld, X)) return -2;
-  static const int narrow = getenv("SRML_LOGREG_NARROW") ? atoi(getenv("SRML_LOGREG_NARROW")) : 1;
-  if (narrow && n <= 512 && (n & 3) == 0 && (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0) {
+  if (zfl && !logreg_pf_eligible(n, ld, X) && !logreg_narrow_eligible(n, ld, X)) return -2;
+  if (logreg_narrow_eligible(n, ld, X)) {
     long nb = m / 256;  // ~256 rows (16 steps of 16) per block, 512 .. 4096 blocks
     if (nb > 4096) nb = 4096;
     if (nb < 1) nb = 1;
@@ -1061,7 +1091,7 @@ static int logreg_binary_launch(const float* X, long m, int n, long ld, const fl
     const int G = (n + 63) / 64;
 #define SRML_LR_NARROW(GG, DD)                                                                                       \
   hipLaunchKernelGGL((logreg_binary_narrow_kernel<GG, DD>), dim3((unsigned)blocks), dim3(256), 0, stream, X, m, n, ld, \
-                     y, w, b, bptr, flag, out, rpb)
+                     y, w, b, bptr, flag, out, rpb, zfl, zb, zsc)
     if (G <= 1) SRML_LR_NARROW(1, 3);
     else if (G <= 2) SRML_LR_NARROW(2, 3);
     else if (G <= 4) SRML_LR_NARROW(4, 3);

@@ -50,6 +50,7 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_logreg_binary4_f32": (_P, _L, _I, _L, _P, _P, _D, _P, _P, _P, _P, _I, _P, _P, _P, _P),
     "srml_logreg_fold_parts": (_L,),
     "srml_logreg_fold_ws": (_L, _I, _L, _P),
+    "srml_logreg_zcache_ok": (_L, _I, _L, _P),
     "srml_logreg_binary_lds_f32": (_P, _L, _I, _L, _P, _P, _D, _P, _P, _P, _P),
     "srml_logreg_binary_lds_f64": (_P, _L, _I, _L, _P, _P, _D, _P, _P, _P, _P),
     "srml_xtv2_f32": (_P, _L, _I, _L, _P, _I, _L, _P, _L, _L, _P, _P),

@@ -336,17 +336,18 @@ def test_logistic_fit_fused_fold_matches_unfused(gpu_device, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_logreg_margin_only_evaluation_matches_full(gpu_device):
+@pytest.mark.parametrize("n", [1100, 256])  # prefetching column-split kernel / narrow kernel
+def test_logreg_margin_only_evaluation_matches_full(gpu_device, n):
     """The line-search margin cache: full evaluations store the row margins; a margins-only
     evaluation at beta between two stored points gives the loss / bias gradient of a full pass at
     w0 + beta (w1 - w0) (margins are linear along a search direction) and no gradient columns."""
     from spark_rapids_ml_nai_amd import ops
 
     rng = np.random.default_rng(21)
-    m, n = 9000, 1100
+    m = 9000
     X = torch.from_numpy(rng.standard_normal((m, n)).astype(np.float32)).to(gpu_device)
     y = torch.from_numpy((rng.random(m) > 0.4).astype(np.float32)).to(gpu_device)
-    assert ops.logreg_workspace(X) is not None
+    assert ops.logreg_zcache_ok(X)
     w0 = torch.from_numpy(rng.standard_normal(n) * 0.05).to(gpu_device)
     w1 = torch.from_numpy(rng.standard_normal(n) * 0.05).to(gpu_device)
     b0 = torch.tensor([0.3], dtype=torch.float64, device=gpu_device)
@@ -376,7 +377,8 @@ def test_logreg_margin_only_evaluation_matches_full(gpu_device):
 
 
 @pytest.mark.gpu
-def test_logistic_fit_margin_cache_matches_full_evaluations(gpu_device, monkeypatch):
+@pytest.mark.parametrize("n", [1200, 256])
+def test_logistic_fit_margin_cache_matches_full_evaluations(gpu_device, monkeypatch, n):
     """A fit whose rejected line-search trials are margins-only evaluations reaches the optimum of
     the all-full-evaluation fit, with fewer passes over X."""
     from spark_rapids_ml_nai_amd.models import qn as qnm
@@ -384,7 +386,7 @@ def test_logistic_fit_margin_cache_matches_full_evaluations(gpu_device, monkeypa
     from spark_rapids_ml_nai_amd.parallel.context import WorkerContext
 
     rng = np.random.default_rng(12)
-    m, n = 30000, 1200
+    m = 30000
     X = rng.standard_normal((m, n)).astype(np.float32)
     y = (X[:, :10].sum(1) + 2.0 * rng.standard_normal(m) > 0).astype(np.float32)
     Xt, yt = torch.from_numpy(X).to(gpu_device), torch.from_numpy(y).to(gpu_device)
