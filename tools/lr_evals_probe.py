@@ -23,5 +23,6 @@ for f32 in (True, False):
         mdl = est.fit(df)
         info = getattr(mdl, "_solver_info", {}) or {}
         print(json.dumps({"rows": m, "float32_inputs": f32, "maxIter": cap, "iters": int(mdl.num_iters),
-                          "objective": float(mdl.objective), **{k: info.get(k) for k in ("n_evals", "n_margin_only", "status", "path")}}),
+                          "objective": float(mdl.objective),
+                          **{k: info.get(k) for k in ("n_evals", "n_margin_only", "status", "path")}}),
               flush=True)
