@@ -18,10 +18,17 @@ from spark_rapids_ml_nai_amd.models import forest  # noqa: E402
 rows = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
 name = sys.argv[2] if len(sys.argv) > 2 else "random_forest_classifier"
 dev = torch.device("cuda", 0)
-wl = registry()[name]
-Xh, yh = make_shard(wl.data, rows, 3000, dev, 0, rows)
+if name == "northstar_rf":  # BASELINE.json config 4 shape: 64 features, 100 trees, depth 16
+    from spark_rapids_ml_nai_amd.classification import RandomForestClassifier
+
+    Xh, yh = make_shard("classification", rows, 64, dev, 0, rows)
+    est = RandomForestClassifier(numTrees=100, maxDepth=16, maxBins=128, seed=1, featuresCol="features",
+                                 labelCol="label", split_mode="data_parallel")
+else:
+    wl = registry()[name]
+    Xh, yh = make_shard(wl.data, rows, 3000, dev, 0, rows)
+    est = wl.make_estimator()
 df = DataFrame.from_numpy(Xh, yh)
-est = wl.make_estimator()
 est.fit(df)
 torch.cuda.synchronize()
 t0 = time.perf_counter()
