@@ -4,8 +4,8 @@
 set -o pipefail
 mkdir -p gpurun_out/umap_trace/raw
 export TMPDIR=/tmp
-timeout -k 10 300 python3 -u tools/umap_phases.py --rows 20000000 > gpurun_out/umap_phases_20M.txt 2>&1 || { tail -20 gpurun_out/umap_phases_20M.txt; exit 1; }
+
 timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/umap_trace/raw -o run -- python3 tools/umap_phases.py --rows 20000000 --no-profile > gpurun_out/umap_trace/log.txt 2>&1 || { tail -20 gpurun_out/umap_trace/log.txt; exit 1; }
-python3 tools/trace_summary.py gpurun_out/umap_trace > gpurun_out/umap_trace_summary.txt
+TRACE_AFTER_GAP_MS=1000 TRACE_GAPS=25 python3 tools/trace_summary.py gpurun_out/umap_trace > gpurun_out/umap_trace_summary.txt
 rm -rf gpurun_out/umap_trace/raw
-head -30 gpurun_out/umap_phases_20M.txt
+grep -v amdgpu gpurun_out/umap_trace/log.txt | head -5

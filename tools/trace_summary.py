@@ -15,6 +15,16 @@ def main(out_dir: str) -> None:
             for r in csv.DictReader(fh):
                 rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
+    # TRACE_AFTER_GAP_MS: keep only the dispatches after the LAST device-idle gap longer than this
+    # (a tool that sleeps between its warm-up and timed runs marks the timed region that way)
+    cut_ms = float(os.environ.get("TRACE_AFTER_GAP_MS", "0"))
+    if cut_ms > 0 and rows:
+        end, cut = rows[0][1], 0
+        for j in range(1, len(rows)):
+            if (rows[j][0] - end) / 1e6 > cut_ms:
+                cut = j
+            end = max(end, rows[j][1])
+        rows = rows[cut:]
     tot = defaultdict(lambda: [0, 0.0])
     for s, e, k in rows:
         tot[k][0] += 1

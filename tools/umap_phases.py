@@ -30,6 +30,7 @@ def main() -> None:
     params = {"n_neighbors": 15, "n_components": 2, "random_state": 1}
     U.umap_fit(X[:20000].contiguous(), params)  # warm up kernels / libraries
     torch.cuda.synchronize()
+    time.sleep(1.5)  # an idle marker before the timed fit (tools/trace_summary.py TRACE_AFTER_GAP_MS)
     pr = cProfile.Profile()
     t0 = time.perf_counter()
     if not a.no_profile:
