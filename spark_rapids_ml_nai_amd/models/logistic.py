@@ -139,12 +139,13 @@ def logistic_fit(X: Any, y: torch.Tensor, m_total: int, ctx: WorkerContext, reg:
                            "two_pass_binary_f32") or path.startswith("lds_binary")) and _eval_bytes(X) <= GRAPH_MAX_BYTES
     # line-search margin cache: binary fits on the narrow / prefetching kernels. Every rank's optimiser
     # must run the same state machine, so the ranks agree (a rank without rows has nothing to cache)
-    zok = path == "fused_binary_f32" and (X.shape[0] == 0 or ops.logreg_zcache_ok(X))
+    zok = ((path == "fused_binary_f32" and (X.shape[0] == 0 or ops.logreg_zcache_ok(X)))
+           or (path == "two_pass_multinomial_f32" and ops.XW_MFMA_MIN_K <= K <= 16))
     if allreduce is not None:
         flag_t = torch.tensor([1.0 if zok else 0.0], dtype=torch.float64, device=X.device)
         ctx.comm.allreduce(flag_t, op="min")
         zok = bool(flag_t.item() > 0)
-    zbuf = torch.zeros(2 * X.shape[0], dtype=torch.float64, device=X.device) if zok else None
+    zbuf = torch.zeros(2 * X.shape[0] * K, dtype=torch.float64, device=X.device) if zok else None
     res = minimize(P, theta0, evaluate, allreduce, y.device, batch=8 if not path.startswith("torch") else 2,
                    graph_safe=graph_safe, fold=fold, evaluate_partials=evaluate_partials, zcache=zbuf)
     return _result(res, base, ctx, n, K, fit_intercept, inv_sigma, path)

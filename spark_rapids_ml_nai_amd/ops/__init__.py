@@ -2453,7 +2453,7 @@ def mbin_supported(X, M: int) -> bool:
 
 def _glm_two_pass(X: torch.Tensor, y32: torch.Tensor, W: torch.Tensor, b: torch.Tensor, sb: int, mode: int,
                   grad: torch.Tensor, so_c: int, so_k: int, gb: torch.Tensor, sgb: int, loss: torch.Tensor, sl: int,
-                  flag: Optional[torch.Tensor]) -> None:
+                  flag: Optional[torch.Tensor], zc: Optional[tuple] = None) -> None:
     """Two passes over X for K margins: Z = X W^T (``srml_xw_f32``, one bandwidth-bound pass for
     K <= 32), the residual stage on the device (``srml_logit_residual_f32``: softmax (mode 0) or K
     independent sigmoids (mode 1), bias gradients and losses block-reduced into fp64), then
@@ -2461,11 +2461,29 @@ def _glm_two_pass(X: torch.Tensor, y32: torch.Tensor, W: torch.Tensor, b: torch.
     output locations given by base tensors + element strides."""
     m, n = X.shape
     K = W.shape[0]
-    Z = xw_t(X, W.to(torch.float32).contiguous()) if K >= XW_MFMA_MIN_K else xw(X, W.t().float().contiguous())
-    R = torch.empty((m, K), dtype=torch.float32, device=X.device)
     st = native.stream(X.device)
     fp = flag.data_ptr() if flag is not None else None
     yp = _c(y32).data_ptr()
+    if zc is not None:
+        # the optimiser's line-search margin cache (K in [XW_MFMA_MIN_K, 16], softmax): the margin
+        # and X^T R passes skip on the device while the step asks for a margins-only evaluation
+        zfl, zb, zsc = zc
+        skip = zfl[13:14]
+        Wt = W.to(torch.float32).contiguous()
+        Z = torch.empty((m, K), dtype=torch.float32, device=X.device)
+        X = _c(X)
+        native.call("srml_xw_t_f32_skip", X.data_ptr(), m, n, X.stride(0), Wt.data_ptr(), K, Wt.stride(0), None,
+                    Z.data_ptr(), Z.stride(0), skip.data_ptr(), st)
+        R = torch.empty((m, K), dtype=torch.float32, device=X.device)
+        native.call("srml_logit_residual_zc_f32", Z.data_ptr(), m, K, Z.stride(0), yp, b.data_ptr(), sb, mode,
+                    R.data_ptr(), K, gb.data_ptr(), sgb, loss.data_ptr(), sl, fp, zfl.data_ptr(), zb.data_ptr(),
+                    zsc.data_ptr(), st)
+        fn = "srml_xtv_mfma_f32" if K >= XTV_MFMA_MIN_K else "srml_xtv2_f32"
+        native.call(fn, X.data_ptr(), m, n, X.stride(0), R.data_ptr(), K, K, grad.data_ptr(), so_c, so_k,
+                    skip.data_ptr(), st)
+        return
+    Z = xw_t(X, W.to(torch.float32).contiguous()) if K >= XW_MFMA_MIN_K else xw(X, W.t().float().contiguous())
+    R = torch.empty((m, K), dtype=torch.float32, device=X.device)
     if deterministic():
         # no atomics: per-block partials into workspaces, folded in block order (bit-reproducible);
         # the margin pass has none to begin with
@@ -2521,9 +2539,10 @@ def logistic_loss_grad(X, y32: torch.Tensor, w: torch.Tensor, b: torch.Tensor, K
     grad b (K) | loss sum] (fp64). K == 1: binary (labels 0/1, sigmoid); K >= 2: softmax over K
     classes (labels 0..K-1). ``w`` (K*n) and ``b`` (K) are fp64 device tensors read by the kernel
     (no host round trip); ``flag`` (device int32, optional): the kernels skip once it is non-zero.
-    ``zcache`` = (QN flags, 2 m fp64 margin buffers, QN scalars): the line-search margin cache of
-    the binary prefetching kernel (``srml_logreg_binary4_f32``; the caller checked a fold
-    workspace exists for X, i.e. that kernel runs). X: dense (m, n) or CSR."""
+    ``zcache`` = (QN flags, 2 m K fp64 margin buffers, QN scalars): the optimiser's line-search
+    margin cache — binary: the narrow / prefetching kernels (``srml_logreg_binary4_f32``; the
+    caller checked ``logreg_zcache_ok``); multinomial (``two_pass_multinomial_f32``): the margin /
+    residual / X^T R passes. X: dense (m, n) or CSR."""
     path = logistic_path(X, K)
     if _is_csr(X):
         m, n = X.shape
@@ -2623,7 +2642,8 @@ def logistic_loss_grad(X, y32: torch.Tensor, w: torch.Tensor, b: torch.Tensor, K
         native.call("srml_mlogit_f32", X.data_ptr(), m, n, X.stride(0), y32.data_ptr(), w.data_ptr(), b.data_ptr(),
                     fp, K, out.data_ptr(), st)
     elif path == "two_pass_multinomial_f32" or (path == "two_pass_deterministic_f32" and K > 1):
-        _glm_two_pass(X, y32, w.view(K, n), b, 1, 0, out, 1, n, out[K * n:], 1, out[K * n + K:], 0, flag)
+        _glm_two_pass(X, y32, w.view(K, n), b, 1, 0, out, 1, n, out[K * n:], 1, out[K * n + K:], 0, flag,
+                      zc=zcache if path == "two_pass_multinomial_f32" else None)
     elif path == "two_pass_deterministic_f32":  # binary: one sigmoid model
         _glm_two_pass(X, y32, w.view(1, n), b, 1, 1, out, 1, n, out[n:], 1, out[n + 1:], 1, flag)
     else:  # pragma: no cover

@@ -269,6 +269,10 @@ SRML_API int srml_mbin_f32(const float* X, long m, int n, long ld, const float* 
 //   mode 1 (K independent binary models): R[r][k] = sigmoid(z_k) - y, loss_k += softplus(z_k) - y z_k.
 // Bias gradients (column sums of R) and the loss(es) are block-reduced and added into out:
 // gb_k at gb[k * sgb], loss at loss[0] (mode 0) or loss[k * sl] (mode 1).
+// zfl (optional): the optimiser's line-search margin cache (qn.hip F_ZMODE / F_ZSEL / SC_BETA), m x K
+// fp64 margins (bias included) per buffer in zb: a full evaluation stores its margins in buffer
+// 1 - zsel; a margins-only evaluation (F_ZMODE == 1) takes z = z0 + beta (z1 - z0) instead of Z + b
+// and writes no R (the X^T R pass is skipped then).
 template <typename TZ, int KB>
 __global__ __launch_bounds__(256) void logit_residual_kernel(const TZ* __restrict__ Z, long m, int K, long ldz,
                                                              const float* __restrict__ y,
@@ -276,8 +280,15 @@ __global__ __launch_bounds__(256) void logit_residual_kernel(const TZ* __restric
                                                              TZ* __restrict__ R, long ldr,
                                                              double* __restrict__ gb, long sgb,
                                                              double* __restrict__ loss, long sl,
-                                                             const int* __restrict__ flag, double* __restrict__ ws) {
+                                                             const int* __restrict__ flag, double* __restrict__ ws,
+                                                             const int* __restrict__ zfl = nullptr,
+                                                             double* __restrict__ zb = nullptr,
+                                                             const double* __restrict__ zsc = nullptr) {
   if (flag && *flag) return;
+  const int zmode = zfl ? zfl[9] : 0, zsel = zfl ? zfl[10] : 0;
+  const double beta = (zfl && zmode == 1) ? zsc[6] : 0.0;
+  const double* z0c = zfl ? zb + (long)zsel * m * K : nullptr;
+  double* z1c = zfl ? zb + (long)(1 - zsel) * m * K : nullptr;
   __shared__ double red[4][2 * KB + 1];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   double bk[KB], sg[KB], sls[KB];
@@ -291,8 +302,21 @@ __global__ __launch_bounds__(256) void logit_residual_kernel(const TZ* __restric
   for (long r = (long)blockIdx.x * 256 + threadIdx.x; r < m; r += (long)gridDim.x * 256) {
     double z[KB];
     const float yr = y[r];
+    if (zmode == 1) {
 #pragma unroll
-    for (int k = 0; k < KB; ++k) z[k] = k < K ? (double)Z[r * ldz + k] + bk[k] : 0.0;
+      for (int k = 0; k < KB; ++k) {
+        const double a = k < K ? z0c[r * K + k] : 0.0;
+        z[k] = k < K ? a + beta * (z1c[r * K + k] - a) : 0.0;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < KB; ++k) z[k] = k < K ? (double)Z[r * ldz + k] + bk[k] : 0.0;
+      if (zfl) {
+#pragma unroll
+        for (int k = 0; k < KB; ++k)
+          if (k < K) z1c[r * K + k] = z[k];
+      }
+    }
     if (mode == 0) {
       double zmax = -1e300;
 #pragma unroll
@@ -315,7 +339,7 @@ __global__ __launch_bounds__(256) void logit_residual_kernel(const TZ* __restric
         if (k < K) {
           const double res = e[k] * inv - (k == yi ? 1.0 : 0.0);
           if (k == yi) zy = z[k];
-          R[r * ldr + k] = (TZ)res;
+          if (zmode != 1) R[r * ldr + k] = (TZ)res;
           sg[k] += res;
         }
       }
@@ -326,7 +350,7 @@ __global__ __launch_bounds__(256) void logit_residual_kernel(const TZ* __restric
         if (k < K) {
           double res, l;
           logistic_terms(z[k], (double)yr, res, l);
-          R[r * ldr + k] = (TZ)res;
+          if (zmode != 1) R[r * ldr + k] = (TZ)res;
           sg[k] += res;
           sls[k] += l;
         }
@@ -373,13 +397,14 @@ SRML_API long srml_logit_residual_ws(long m, int K) { return m <= 0 ? 0 : logit_
 template <typename TZ>
 static int logit_residual_launch(const TZ* Z, long m, int K, long ldz, const float* y, const double* b, long sb,
                                  int mode, TZ* R, long ldr, double* gb, long sgb, double* loss, long sl,
-                                 const int* flag, double* ws, hipStream_t stream) {
+                                 const int* flag, double* ws, hipStream_t stream, const int* zfl = nullptr,
+                                 double* zb = nullptr, const double* zsc = nullptr) {
   if (m <= 0) return 0;
   if (K < 1 || K > 16) return -2;
   const long blocks = logit_residual_blocks(m);
 #define SRML_RES(KK)                                                                                             \
   hipLaunchKernelGGL((logit_residual_kernel<TZ, KK>), dim3((unsigned)blocks), dim3(256), 0, stream, Z, m, K, ldz, y, b, sb, \
-                     mode, R, ldr, gb, sgb, loss, sl, flag, ws)
+                     mode, R, ldr, gb, sgb, loss, sl, flag, ws, zfl, zb, zsc)
   if (K <= 4) SRML_RES(4);
   else if (K <= 8) SRML_RES(8);
   else SRML_RES(16);
@@ -397,6 +422,16 @@ SRML_API int srml_logit_residual_f32(const float* Z, long m, int K, long ldz, co
                                      int mode, float* R, long ldr, double* gb, long sgb, double* loss, long sl,
                                      const int* flag, hipStream_t stream) {
   return logit_residual_launch(Z, m, K, ldz, y, b, sb, mode, R, ldr, gb, sgb, loss, sl, flag, nullptr, stream);
+}
+
+// With the optimiser's line-search margin cache (see logit_residual_kernel): zfl = QN flags, zb =
+// 2 m K fp64 margins, zsc = QN scalars.
+SRML_API int srml_logit_residual_zc_f32(const float* Z, long m, int K, long ldz, const float* y, const double* b,
+                                        long sb, int mode, float* R, long ldr, double* gb, long sgb, double* loss,
+                                        long sl, const int* flag, const int* zfl, double* zb, const double* zsc,
+                                        hipStream_t stream) {
+  return logit_residual_launch(Z, m, K, ldz, y, b, sb, mode, R, ldr, gb, sgb, loss, sl, flag, nullptr, stream, zfl, zb,
+                               zsc);
 }
 
 // fp64 margins / residuals (float32_inputs=False two-pass GLM: margins and X^T R on the fp64 MFMA GEMM)

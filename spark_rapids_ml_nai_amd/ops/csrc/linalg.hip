@@ -194,7 +194,8 @@ template <int NT, int RT, bool PIPE>
 __global__ __launch_bounds__(256) void xw_mfma_kernel(const float* __restrict__ X, long m, int n, long ld,
                                                       const float* __restrict__ Wt, int K, long ldw,
                                                       const float* __restrict__ bias, float* __restrict__ out,
-                                                      long ldo, int vec) {
+                                                      long ldo, int vec, const int* __restrict__ skip) {
+  if (skip && *skip) return;  // the optimiser's margins-only evaluation: no pass over X
   const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
   const long row0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * (16 * RT);
   if (row0 >= m) return;
@@ -331,7 +332,7 @@ __global__ __launch_bounds__(256) void xw_mfma_kernel(const float* __restrict__ 
 }
 
 static int xw_t_launch(const float* X, long m, int n, long ld, const float* Wt, int K, long ldw, const float* bias,
-                       float* out, long ldo, int variant, hipStream_t stream) {
+                       float* out, long ldo, int variant, hipStream_t stream, const int* skip = nullptr) {
   if (m <= 0) return 0;
   if (n <= 0 || K < 1 || K > 32) return -2;
   const int vec = ((ld & 3) == 0) && ((ldw & 3) == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0) &&
@@ -342,7 +343,7 @@ static int xw_t_launch(const float* X, long m, int n, long ld, const float* Wt, 
   if (blocks > 0x7fffffffL) return -2;
 #define SRML_XWT(NT_, RT_, P_)                                                                                    \
   hipLaunchKernelGGL((xw_mfma_kernel<NT_, RT_, P_>), dim3((unsigned)blocks), dim3(256), 0, stream, X, m, n, ld, Wt, K, \
-                     ldw, bias, out, ldo, vec)
+                     ldw, bias, out, ldo, vec, skip)
   if (K <= 16) {
     if (rt == 4) { if (pipe) SRML_XWT(1, 4, true); else SRML_XWT(1, 4, false); }
     else { if (pipe) SRML_XWT(1, 2, true); else SRML_XWT(1, 2, false); }
@@ -359,6 +360,13 @@ SRML_API int srml_xw_t_f32(const float* X, long m, int n, long ld, const float* 
   // measured at 1M x 3000 (tools/skinny_bench.py --variants): double-buffered loads win everywhere;
   // 2 row tiles per wave (more waves in flight) up to K = 12, 4 (half the Wt re-reads) above
   return xw_t_launch(X, m, n, ld, Wt, K, ldw, bias, out, ldo, K <= 12 ? 3 : 2, stream);
+}
+
+// Same, skipped on the device when *skip != 0 (the QN step's F_SKIPX word: a margins-only
+// evaluation or a finished fit).
+SRML_API int srml_xw_t_f32_skip(const float* X, long m, int n, long ld, const float* Wt, int K, long ldw,
+                                const float* bias, float* out, long ldo, const int* skip, hipStream_t stream) {
+  return xw_t_launch(X, m, n, ld, Wt, K, ldw, bias, out, ldo, K <= 12 ? 3 : 2, stream, skip);
 }
 
 // Tuning entry (tools/skinny_bench.py): variant bit 0 = 2 row tiles per wave (else 4), bit 1 =

@@ -37,8 +37,10 @@ constexpr int QN_NV = 6 + 5 * QN_MMAX;
 // F_ZSEL / SC_BETA): F_ZMODE is the mode of the NEXT evaluation — 0 full, 1 margins-only (a
 // backtracking trial: loss from z0 + beta (z1 - z0)), 2 full at a point a margins-only trial
 // already accepted; F_ZSEL selects which of the two margin buffers holds z0 (the accepted point).
+// F_SKIPX: 1 while the next evaluation must not read X (margins-only, or the fit is done) — the
+// skip word of the multinomial margin pass / X^T R pass (two-pass GLM)
 enum { F_DONE = 0, F_STATUS, F_ITER, F_NEVAL, F_LS, F_COUNT, F_HEAD, F_STARTED, F_BRACKET, F_ZMODE, F_ZSEL,
-       F_NCHEAP, F_ZC };
+       F_NCHEAP, F_ZC, F_SKIPX };
 enum { ST_RUNNING = 0, ST_CONV_GRAD = 1, ST_CONV_F = 2, ST_MAXITER = 3, ST_LS_FAIL = 4 };
 enum { SC_F = 0, SC_ALPHA, SC_DGINIT, SC_GAMMA, SC_GINF, SC_ALPHA1, SC_BETA };
 
@@ -888,6 +890,7 @@ __global__ __launch_bounds__(MB_T) void qn_mb2_kernel(QnArgs A, double* __restri
           fl[F_NEVAL] = pre_neval + 1;
           fl[F_STATUS] = ST_LS_FAIL;
           fl[F_DONE] = 1;
+          fl[F_SKIPX] = 1;
         }
         return;
       }
@@ -905,8 +908,10 @@ __global__ __launch_bounds__(MB_T) void qn_mb2_kernel(QnArgs A, double* __restri
           A.sc[SC_ALPHA1] = a1;
           A.sc[SC_BETA] = alpha / a1;
           fl[F_ZMODE] = 1;
+          fl[F_SKIPX] = 1;
         } else if (zc) {
           fl[F_ZMODE] = 0;  // a non-finite loss: no trusted margins, the next trial runs in full
+          fl[F_SKIPX] = 0;
         }
       }
       return;
@@ -915,6 +920,7 @@ __global__ __launch_bounds__(MB_T) void qn_mb2_kernel(QnArgs A, double* __restri
       if (first) {
         fl[F_NEVAL] = pre_neval + 1;
         fl[F_ZMODE] = 2;
+        fl[F_SKIPX] = 0;
       }
       return;
     }
@@ -925,6 +931,7 @@ __global__ __launch_bounds__(MB_T) void qn_mb2_kernel(QnArgs A, double* __restri
     if (zc) {  // this full evaluation's margins (the other buffer) are the new accepted point's
       fl[F_ZSEL] ^= 1;
       fl[F_ZMODE] = 0;
+      fl[F_SKIPX] = 0;
     }
   }
   // accepted: pass 1 partials of this block's elements
@@ -1206,6 +1213,7 @@ __global__ __launch_bounds__(MB_T) void qn_mb4_kernel(QnArgs A, double* __restri
     if (first) {
       fl[F_STATUS] = status;
       fl[F_DONE] = 1;
+      fl[F_SKIPX] = 1;
     }
     return;
   }

@@ -58,8 +58,10 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_xtv_mfma_det_f32": (_P, _L, _I, _L, _P, _I, _L, _P, _L, _L, _P, _P, _P),
     "srml_fold_partials_f64": (_P, _L, _L, _L, _L, _P, _L, _L, _P, _P),
     "srml_xw_t_f32": (_P, _L, _I, _L, _P, _I, _L, _P, _P, _L, _P),
+    "srml_xw_t_f32_skip": (_P, _L, _I, _L, _P, _I, _L, _P, _P, _L, _P, _P),
     "srml_xw_t_f32_variant": (_P, _L, _I, _L, _P, _I, _L, _P, _P, _L, _I, _P),
     "srml_logit_residual_f32": (_P, _L, _I, _L, _P, _P, _L, _I, _P, _L, _P, _L, _P, _L, _P, _P),
+    "srml_logit_residual_zc_f32": (_P, _L, _I, _L, _P, _P, _L, _I, _P, _L, _P, _L, _P, _L, _P, _P, _P, _P, _P),
     "srml_logit_residual_f64": (_P, _L, _I, _L, _P, _P, _L, _I, _P, _L, _P, _L, _P, _L, _P, _P),
     "srml_logit_residual_det_f32": (_P, _L, _I, _L, _P, _P, _L, _I, _P, _L, _P, _L, _P, _L, _P, _P, _P),
     "srml_logit_residual_ws": (_L, _I),
