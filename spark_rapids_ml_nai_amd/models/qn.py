@@ -358,9 +358,10 @@ class DeviceQN:
         return self.x.cpu().numpy().copy()
 
     def zcache_supported(self) -> bool:
-        """The margin cache needs the multi-block step (the other steps ignore its flags), a
-        backtracking Armijo search and no L1 (the orthant projection is not linear in the step)."""
-        return self._mb is not None and not self._fused and not self.P.use_l1 and not self.P.wolfe
+        """The margin cache needs the multi-block or single-block step (the one-launch fused step
+        ignores its flags), a backtracking Armijo search and no L1 (the orthant projection is not
+        linear in the step)."""
+        return not (self._mb is not None and self._fused) and not self.P.use_l1 and not self.P.wolfe
 
     def enable_zcache(self, zbuf: torch.Tensor) -> tuple:
         """Switch the margin cache on (``zbuf``: 2 m fp64): returns the evaluation's (flags, buffer,

@@ -182,6 +182,10 @@ __device__ __forceinline__ void qn_step_body(const QnArgs& A) {
   const double dginit = A.sc[SC_DGINIT];
   const double pre_gamma = A.sc[SC_GAMMA];
   const double pre_fh_next = (A.past > 0 && started) ? A.fh[(pre_iter + 1) % A.past] : 0.0;
+  // line-search margin cache (see the multi-block step K2): the mode of the evaluation just summed
+  const bool zc = fl[F_ZC] != 0;
+  const int zmode = zc ? fl[F_ZMODE] : 0;
+  const double alpha1 = A.sc[SC_ALPHA1];
 
   // ---- pass 0: smooth gradient at xt (optimiser coordinates), penalties, directional terms
   double p0[4] = {0.0, 0.0, 0.0, 0.0};
@@ -219,10 +223,13 @@ __device__ __forceinline__ void qn_step_body(const QnArgs& A) {
   const double ft = lossv * A.inv_m + 0.5 * p0[0] + p0[1];
 
   // ---- line search decision (uniform: every thread sees the same reduced values)
+  if (tid == 0 && zc && zmode == 1) fl[F_NCHEAP] += 1;
   if (started) {
     bool accept = true;
     double width = 1.0;
-    if (!isfinite(ft)) {
+    if (zc && zmode == 2 && isfinite(ft)) {
+      // a margins-only trial passed at this point: this full evaluation supplies its gradient
+    } else if (!isfinite(ft)) {
       accept = false;
       width = 0.5;
     } else {
@@ -247,9 +254,11 @@ __device__ __forceinline__ void qn_step_body(const QnArgs& A) {
           fl[F_NEVAL] = pre_neval + 1;
           fl[F_STATUS] = ST_LS_FAIL;
           fl[F_DONE] = 1;
+          fl[F_SKIPX] = 1;
         }
         return;
       }
+      const double alpha_tried = alpha;
       alpha *= width;
       qn_set_trial(A, alpha);
       if (tid == 0) {
@@ -257,9 +266,32 @@ __device__ __forceinline__ void qn_step_body(const QnArgs& A) {
         fl[F_NEVAL] = pre_neval + 1;
         if (width < 1.0) fl[F_BRACKET] = 1;
         A.sc[SC_ALPHA] = alpha;
+        if (zc && isfinite(ft)) {
+          const double a1 = zmode == 0 ? alpha_tried : alpha1;
+          A.sc[SC_ALPHA1] = a1;
+          A.sc[SC_BETA] = alpha / a1;
+          fl[F_ZMODE] = 1;
+          fl[F_SKIPX] = 1;
+        } else if (zc) {
+          fl[F_ZMODE] = 0;
+          fl[F_SKIPX] = 0;
+        }
       }
       return;
     }
+    if (zc && zmode == 1) {  // accepted on margins only: evaluate the same point in full next
+      if (tid == 0) {
+        fl[F_NEVAL] = pre_neval + 1;
+        fl[F_ZMODE] = 2;
+        fl[F_SKIPX] = 0;
+      }
+      return;
+    }
+  }
+  if (tid == 0 && zc) {  // this full evaluation's margins are the accepted point's
+    fl[F_ZSEL] ^= 1;
+    fl[F_ZMODE] = 0;
+    fl[F_SKIPX] = 0;
   }
 
   // ---- accepted: pass 1 — pseudo-gradient at xt and every dot product of the compact form
@@ -552,6 +584,7 @@ __device__ __forceinline__ void qn_step_body(const QnArgs& A) {
     if (tid == 0) {
       fl[F_STATUS] = status;
       fl[F_DONE] = 1;
+      fl[F_SKIPX] = 1;
     }
     return;
   }

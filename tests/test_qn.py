@@ -377,7 +377,7 @@ def test_logreg_margin_only_evaluation_matches_full(gpu_device, n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,classes", [(1200, 2), (256, 2), (300, 4), (200, 11)])
+@pytest.mark.parametrize("n,classes", [(1200, 2), (256, 2), (300, 4), (200, 11), (2000, 9)])  # last: N > 16384
 def test_logistic_fit_margin_cache_matches_full_evaluations(gpu_device, monkeypatch, n, classes):
     """A fit whose rejected line-search trials are margins-only evaluations (binary: narrow /
     prefetching kernels; multinomial: the two-pass margin / residual / X^T R passes) reaches the
