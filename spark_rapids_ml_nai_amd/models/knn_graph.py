@@ -14,6 +14,7 @@ The reference fits UMAP on one GPU with cuML's own kNN (``umap.py:840-850,924-95
 from __future__ import annotations
 
 import math
+import os
 
 from typing import Any, Optional, Tuple
 
@@ -25,6 +26,9 @@ from .. import ops
 BRUTE_MAX_ROWS = 100_000  # build_algo="auto": exact graph up to this many rows, IVF lists beyond
 IVF_LIST_ROWS = 1024      # target rows per inverted list
 IVF_NPROBE = 16           # lists probed per query list
+# quantiser training: Lloyd iterations and sample rows per list (SRML_IVF_TRAIN_ITERS / _ROWS)
+IVF_TRAIN_ITERS = int(os.environ.get("SRML_IVF_TRAIN_ITERS", "10"))
+IVF_TRAIN_ROWS = int(os.environ.get("SRML_IVF_TRAIN_ROWS", "64"))
 
 
 def row_split(n: int, ctx: Any) -> Tuple[int, int]:
@@ -84,13 +88,15 @@ def record_phase(phases: Optional[dict], name: str, rows: int, t0: float, dev: t
     return t1
 
 
-def train_quantizer(X: torch.Tensor, nlist: int, seed: int, iters: int = 10,
-                    train_rows_per_list: int = 64, ctx: Any = None) -> torch.Tensor:
+def train_quantizer(X: torch.Tensor, nlist: int, seed: int, iters: Optional[int] = None,
+                    train_rows_per_list: Optional[int] = None, ctx: Any = None) -> torch.Tensor:
     """IVF coarse quantiser: Lloyd iterations (fused MFMA nearest-centroid + cluster sums) on a
     row subsample, as IVF trainers do. Distributed (``ctx``, X replicated): every rank draws the
     same sample and seeds, labels its own 1/W of the sample and the cluster sums are all-reduced
     (ONE k x (n + 1) fp64 buffer per iteration): every rank ends with the same centres."""
     m = X.shape[0]
+    iters = IVF_TRAIN_ITERS if iters is None else iters
+    train_rows_per_list = IVF_TRAIN_ROWS if train_rows_per_list is None else train_rows_per_list
     gen = torch.Generator(device=X.device).manual_seed(int(seed))  # device permutations: no host RNG
     ntrain = min(m, max(nlist * train_rows_per_list, 4 * nlist))
     T = X if ntrain == m else X.index_select(0, torch.randperm(m, generator=gen, device=X.device)[:ntrain])
@@ -159,7 +165,7 @@ def knn_graph_ivf(X: torch.Tensor, k: int, nlist: Optional[int] = None, nprobe: 
     nprobe = max(1, min(int(nprobe) if nprobe else IVF_NPROBE, nlist, ops.KNN_KMAX))
     t0 = time.perf_counter()
     C = train_quantizer(X, nlist, seed, ctx=ctx)
-    ntrain = min(N, max(nlist * 64, 4 * nlist))
+    ntrain = min(N, max(nlist * IVF_TRAIN_ROWS, 4 * nlist))
     t0 = record_phase(phases, "quantizer", row_split(ntrain, ctx)[1] - row_split(ntrain, ctx)[0], t0, X.device)
     if nlist >= 64:
         # spatial list order: lists grouped by a coarse k-means of their centroids, so the lists a
