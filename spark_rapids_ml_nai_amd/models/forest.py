@@ -73,6 +73,12 @@ RF_SIBLING_SUB = os.environ.get("SRML_RF_SIBLING_SUB", "1") != "0"
 # SRML_RF_LEVEL_LOG=1: per-level host timing of the last grow_forest call in LAST_LEVELS (segments,
 # candidates, seconds of host work vs waits on the device per section)
 LEVEL_LOG = os.environ.get("SRML_RF_LEVEL_LOG", "0") == "1"
+# one blocking device->host copy per level: the split decisions (which candidates split, their child
+# slots) are taken on the device, the route / partition / child totals run on the candidate count as
+# an upper bound, and ONE copy brings the split records, child bounds and child stats back
+# (SRML_RF_ONE_SYNC=0: the two-copy loop; max_leaves > 0 always takes it — its per-tree budget is
+# decided on the host)
+RF_ONE_SYNC = os.environ.get("SRML_RF_ONE_SYNC", "1") != "0"
 LAST_LEVELS: List[Dict[str, Any]] = []
 
 
@@ -393,6 +399,69 @@ def _pad_rows(t: torch.Tensor, rows: int) -> torch.Tensor:
     return torch.cat([t, torch.zeros((rows - t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)], 0)
 
 
+def _level_one_sync(bins: torch.Tensor, idx: torch.Tensor, wpos: torch.Tensor, bounds: torch.Tensor,
+                    tot: torch.Tensor, yv: torch.Tensor, cand: np.ndarray, L: int, res_out_d: List[torch.Tensor],
+                    res_fsel_d: List[torch.Tensor], res_left: List[torch.Tensor], S: int, regression: bool,
+                    crit: int, data_parallel: bool, ctx: WorkerContext, dev: torch.device, clk: "_LevelClock"
+                    ) -> Optional[tuple]:
+    """The split decisions, routing, re-partition and child totals of one level with ONE blocking
+    copy (RF_ONE_SYNC): candidate j splits iff its record has a feature (out[j, 1] >= 0); its children
+    take slots 2 r, 2 r + 1 with r its rank among the splitting candidates (an exclusive scan on the
+    device), so route / partition / node stats run with the candidate count C as the bound on the
+    splits (children past the real ones are empty segments). Returns None when nothing splits, else
+    (idx, wpos, bounds, tot, bounds_h, stats_h, out_all, feat_all, ci_sel) trimmed to the k splits."""
+    out_d = torch.cat(res_out_d, 0) if len(res_out_d) > 1 else res_out_d[0]
+    fsel_d = (torch.cat(res_fsel_d, 0) if len(res_fsel_d) > 1 else res_fsel_d[0]).view(-1)
+    C = int(cand.size)
+    ok_d = out_d[:, 1] >= 0
+    oki = ok_d.to(torch.int32)
+    pos_d = torch.cumsum(oki, 0, dtype=torch.int32) - oki
+    cand_d = _h2d(cand.astype(np.int64), dev)
+    node_feature = torch.full((L,), -1, dtype=torch.int32, device=dev)
+    node_bin = torch.zeros(L, dtype=torch.int32, device=dev)
+    child_base = torch.zeros(L, dtype=torch.int32, device=dev)
+    node_feature[cand_d] = torch.where(ok_d, fsel_d.to(torch.int32), torch.full_like(oki, -1))
+    node_bin[cand_d] = torch.where(ok_d, out_d[:, 2].to(torch.int32), torch.zeros_like(oki))
+    child_base[cand_d] = torch.where(ok_d, 2 * pos_d, torch.zeros_like(oki))
+    clk.mark("decide_host")
+    keys = ops.rf_route_segments(bins, idx, bounds, node_feature, node_bin, child_base)
+    idx_n, wpos_n, bounds_n = ops.rf_partition(keys, bounds, node_feature, child_base, C, idx, wpos, trim=False)
+    if regression:
+        tot_n = _node_stats(yv, idx_n, wpos_n, bounds_n, S, regression)
+    else:
+        # children totals: the winning histogram's prefix (left) and the parent's rest (right), moved to
+        # the split's child slots; candidates that do not split go to a discarded row
+        left = torch.cat(res_left, 0) if len(res_left) > 1 else res_left[0]
+        pair = torch.stack([left, tot.index_select(0, cand_d) - left], 1)
+        dest = torch.where(ok_d, pos_d.long(), torch.full_like(pos_d, C, dtype=torch.int64))
+        tot_n = torch.zeros((C + 1, 2, S), dtype=pair.dtype, device=dev)
+        tot_n.index_copy_(0, dest, pair)
+        tot_n = tot_n[:C].reshape(2 * C, S)
+    if data_parallel and regression:
+        ctx.comm.allreduce(tot_n)
+    clk.mark("route_launch")
+    stats = _seg_stats(tot_n, regression, crit)
+    V2 = int(stats.shape[1])
+    hb = torch.cat([bounds_n.double(), stats.reshape(-1), out_d.double().reshape(-1), fsel_d.double()]).cpu().numpy()
+    clk.mark("end_sync")
+    nb = 2 * C + 1
+    off = nb + 2 * C * V2
+    out_all = hb[off: off + 6 * C].reshape(C, 6)
+    feat_all = hb[off + 6 * C:]
+    ci_sel = np.nonzero(out_all[:, 1] >= 0)[0]
+    k = int(ci_sel.size)
+    if LEVEL_LOG:
+        clk.rec["candidates"] = C
+        clk.rec["splits"] = k
+    if k == 0:
+        return None
+    bounds_h = hb[: 2 * k + 1].astype(np.int64)
+    stats_h = hb[nb: nb + 2 * k * V2].reshape(2 * k, V2)
+    kept = int(bounds_h[-1])
+    return (idx_n[:kept], wpos_n[:kept], bounds_n[: 2 * k + 1], tot_n[: 2 * k], bounds_h, stats_h, out_all,
+            feat_all, ci_sel)
+
+
 def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: WorkerContext,
                 gen: torch.Generator, p: Dict[str, Any], S: int, regression: bool, data_parallel: bool,
                 gen_boot: Optional[torch.Generator], n_trees: int, pending: Optional[PendingBins] = None) -> List[Tree]:
@@ -491,6 +560,9 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
         # ---- histograms + split search, in groups of candidate segments bounded by memory ----
         res_out: List[np.ndarray] = []
         res_feat: List[np.ndarray] = []
+        one_sync = RF_ONE_SYNC and max_leaves <= 0
+        res_out_d: List[torch.Tensor] = []  # one_sync: the groups' split records / feature ids, on the device
+        res_fsel_d: List[torch.Tensor] = []
         res_left: List[torch.Tensor] = []  # classification: left-child totals of every candidate
         streamed_root = (pending is not None and depth == 0 and cand.size <= group and dev.type == "cuda"
                          and not deterministic())
@@ -602,12 +674,39 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
             # the winning feature ids gathered on the device: one copy of (records | feature id)
             fsel = feats[:C].gather(1, out[:, 1].clamp_min(0).long().view(-1, 1)).to(out.dtype)
             clk.mark("hist_split_launch")
+            if one_sync:
+                res_out_d.append(out[:C])
+                res_fsel_d.append(fsel)
+                continue
             rec_h = torch.cat([out, fsel], 1).cpu().numpy()
             clk.mark("split_sync")
             out_h = rec_h[:, :-1]
             res_out.append(out_h)
             ok = out_h[:, 1] >= 0
             res_feat.append(np.where(ok, rec_h[:, -1].astype(np.int64), -1))
+        if one_sync:
+            step = _level_one_sync(bins, idx, wpos, bounds, tot, yv, cand, L, res_out_d, res_fsel_d, res_left, S,
+                                   regression, crit, data_parallel, ctx, dev, clk)
+            if step is None:
+                break
+            idx, wpos, bounds, tot, bounds_h, stats_h, out_all, feat_all, ci_sel = step
+            counts = np.diff(bounds_h)
+            k = int(ci_sel.size)
+            j_sel = cand[ci_sel]
+            t_sel = seg_tree[j_sel]
+            b_sel = out_all[ci_sel, 2].astype(np.int64)
+            f_sel = feat_all[ci_sel].astype(np.int64)
+            lnode, rnode = rec.add_children(t_sel)
+            rec.split.append((t_sel, seg_nid[j_sel], f_sel, edges_h[f_sel, b_sel], out_all[ci_sel, 0].astype(np.float64),
+                              lnode, rnode))
+            np.add.at(n_leaves, t_sel, 1)
+            prev_parent = np.repeat(ci_sel, 2)
+            if not keep_hist:
+                prev_hist = None
+            seg_tree = np.repeat(t_sel, 2).astype(np.int64)
+            seg_nid = np.stack([lnode, rnode], 1).reshape(-1).astype(np.int64)
+            depth += 1
+            continue
         out_all = np.concatenate(res_out, 0)
         feat_all = np.concatenate(res_feat, 0)
         # ---- decide splits (honour max_leaves per tree) ----

@@ -1403,13 +1403,15 @@ def rf_bootstrap(T: int, m: int, rate: float, seed: int, device: torch.device
 
 
 def rf_partition(keys: torch.Tensor, bounds: torch.Tensor, node_feature: torch.Tensor, child_base: torch.Tensor,
-                 k: int, idx: torch.Tensor, wpos: torch.Tensor, kept: Optional[int] = None
+                 k: int, idx: torch.Tensor, wpos: torch.Tensor, kept: Optional[int] = None, trim: bool = True
                  ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """Stable re-partition of (idx, wpos) into the 2k child segments of the k split parents
     (child keys from ``rf_route_segments``; other positions leave the tree): (idx, wpos, bounds
     of the 2k children). Device: prefix-count kernels + one scatter (``srml_rf_partition``).
     ``kept``: the caller's count of positions in split parents (their rows all stay), which
-    spares reading it back from the device."""
+    spares reading it back from the device. ``trim=False`` (device): the position arrays keep their
+    full length (the kept prefix is ``bounds[-1]``; the caller slices after its own read of bounds).
+    ``k`` may be an upper bound on the splits: children past the real ones are empty segments."""
     total = int(keys.shape[0])
     if not keys.is_cuda:
         keys_sorted, perm = torch.sort(keys, stable=True)
@@ -1427,6 +1429,8 @@ def rf_partition(keys: torch.Tensor, bounds: torch.Tensor, node_feature: torch.T
                 _c(node_feature.int()).data_ptr(), _c(child_base.int()).data_ptr(), int(k), _c(idx).data_ptr(),
                 _c(wpos.float()).data_ptr(), idx_out.data_ptr(), w_out.data_ptr(), nb.data_ptr(), ws.data_ptr(),
                 native.stream(dev))
+    if not trim:
+        return idx_out, w_out, nb
     if kept is None:
         kept = int(nb[-1].item())
     return idx_out[:kept], w_out[:kept], nb
