@@ -79,6 +79,10 @@ LEVEL_LOG = os.environ.get("SRML_RF_LEVEL_LOG", "0") == "1"
 # (SRML_RF_ONE_SYNC=0: the two-copy loop; max_leaves > 0 always takes it — its per-tree budget is
 # decided on the host)
 RF_ONE_SYNC = os.environ.get("SRML_RF_ONE_SYNC", "1") != "0"
+# levels whose nodes average fewer in-bag positions than this gather from a row-major copy of the
+# bins (built once, at the first such level): a row's sampled features share cache lines there,
+# where the feature-major matrix costs one line per (row, feature) (0 = off)
+RM_ROWS = float(os.environ.get("SRML_RF_ROWMAJOR_ROWS", "10000"))
 LAST_LEVELS: List[Dict[str, Any]] = []
 
 
@@ -514,6 +518,7 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
     # the ranks of a data-parallel fit, whose generators share the seed)
     call_seed = int(torch.randint(0, 1 << 62, (1,), generator=gen, device=dev).item())
     bins_il = None
+    bins_rm: Optional[torch.Tensor] = None
     # packed cells need every item's weights <= 2^20: rows per item (<= WIDE_ROWS_MAX) x max weight
     pack_scale = None
     if (regression and RF_PACK and dev.type == "cuda" and IL_KERNEL == "wide" and not deterministic()
@@ -599,6 +604,7 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
                                            feats if Cp == C else _pad_rows(feats, Cp), C, B, SH, regression, fb, yscale)
                 pending = None
             il = None
+            rm = None
             fb_l, nfc_l, rpi_min, blocks = fb, nfc, ROWS_PER_ITEM, 8192
             if use_il and float(c_cnt.mean()) < IL_DENSITY * m:
                 if bins_il is None:
@@ -609,6 +615,11 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
                     # 1024-thread blocks over ~100-400 features: fewer, longer work items
                     fb_l, rpi_min, blocks = wide_fb, WIDE_ROWS_PER_ITEM, 2048
                     nfc_l = (nf + fb_l - 1) // fb_l
+            if il is None and RM_ROWS > 0 and dev.type == "cuda" and not deterministic() \
+                    and float(c_cnt.mean()) < RM_ROWS:
+                if bins_rm is None:
+                    bins_rm = bins.t().contiguous()  # (m, n) row-major, built once
+                rm = bins_rm
             # rows per work item: enough blocks to fill the chip, few per (node, feature chunk)
             rpi = int(min(WIDE_ROWS_MAX, max(rpi_min, (int(c_cnt.sum()) * nfc_l) // blocks)))
             rpi = (rpi + 511) // 512 * 512
@@ -646,6 +657,7 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
                                    SH, regression, pos_weight=wpos,
                                    fb=fb_l, yscale=yscale, exclusive=excl, bins_il=il,
                                    wide=il is not None and fb_l == wide_fb, rec_bytes=WIDE_REC_BYTES if wide_fb else 32,
+                                   bins_rm=rm,
                                    packed_scale=pack_scale if fb_l == wide_fb else None)
             if Cp > C:
                 hist[C:].zero_()  # padding nodes (no items; an `exclusive` histogram is not pre-zeroed)

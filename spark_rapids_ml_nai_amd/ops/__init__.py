@@ -1141,6 +1141,7 @@ def rf_hist(bins: torch.Tensor, idx: torch.Tensor, label: torch.Tensor, wcnt: Op
             regression: bool, pos_weight: Optional[torch.Tensor] = None, fb: Optional[int] = None,
             yscale: Optional[float] = None, exclusive: Optional[Dict[str, torch.Tensor]] = None,
             bins_il: Optional[torch.Tensor] = None, wide: bool = False, rec_bytes: int = 32,
+            bins_rm: Optional[torch.Tensor] = None,
             packed_scale: Optional[float] = None, out: Optional[torch.Tensor] = None,
             wy: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Per-(node, feature slot, bin) statistics: uint32 class counts or fp64 (count, sum[, sumsq]).
@@ -1234,11 +1235,12 @@ def rf_hist(bins: torch.Tensor, idx: torch.Tensor, label: torch.Tensor, wcnt: Op
                     int(bins_il is not None), st)
         native.call("srml_rf_hist_fixed_finish", hist.data_ptr(), hist.numel(), float(yscale), st)
         return hist
-    src = bins_il if bins_il is not None else bins
-    native.call("srml_rf_hist", src.data_ptr(), m, idx.data_ptr(), wy.data_ptr(), _c(items).data_ptr(),
-                int(items.shape[0]), _c(node_feats).data_ptr(), nf, B, S, int(regression), float(yscale), fb,
-                hist.data_ptr() if not regression else None, hist.data_ptr() if regression else None,
-                int(bins_il is not None), st)
+    src = bins_il if bins_il is not None else (bins_rm if bins_rm is not None else bins)
+    mode = 1 if bins_il is not None else (2 if bins_rm is not None else 0)
+    native.call("srml_rf_hist", src.data_ptr(), m if mode != 2 else int(bins_rm.shape[1]), idx.data_ptr(),
+                wy.data_ptr(), _c(items).data_ptr(), int(items.shape[0]), _c(node_feats).data_ptr(), nf, B, S,
+                int(regression), float(yscale), fb, hist.data_ptr() if not regression else None,
+                hist.data_ptr() if regression else None, mode, st)
     return hist
 
 

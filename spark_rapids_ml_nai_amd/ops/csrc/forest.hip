@@ -203,7 +203,10 @@ __device__ __forceinline__ unsigned rec_word(const uint4& lo, const uint4& hi, i
   }
 }
 
-template <bool REG, bool FIXED = false, bool IL = false>
+// RM: `bins` is row-major (m x n bytes; the kernel's `m` argument carries the row stride n): a row's
+// sampled features sit within its n bytes, so the deep levels' per-row gathers share cache lines
+// instead of touching one line per (row, feature) of the feature-major matrix.
+template <bool REG, bool FIXED = false, bool IL = false, bool RM = false>
 __global__ __launch_bounds__(256) void rf_hist_kernel(const unsigned char* __restrict__ bins, long m,
                                                       const int* __restrict__ idx, const float2* __restrict__ wy,
                                                       const int4* __restrict__ items, const int* __restrict__ node_feats,
@@ -230,7 +233,7 @@ __global__ __launch_bounds__(256) void rf_hist_kernel(const unsigned char* __res
 #pragma unroll
   for (int j = 0; j < FB; ++j) {
     const int f = (j < nfb) ? node_feats[(long)node * nf + f_begin + j] : 0;
-    col[j] = bins + (long)f * m;
+    col[j] = RM ? bins + f : bins + (long)f * m;
     grp[j] = f >> 5;
     byo[j] = f & 31;
   }
@@ -266,8 +269,8 @@ __global__ __launch_bounds__(256) void rf_hist_kernel(const unsigned char* __res
     } else {
 #pragma unroll
       for (int j = 0; j < FB; ++j) {
-        b1[j] = col[j][r1];
-        b2[j] = col[j][r2];
+        b1[j] = RM ? col[j][(long)r1 * m] : col[j][r1];
+        b2[j] = RM ? col[j][(long)r2 * m] : col[j][r2];
       }
     }
     const unsigned w1 = (unsigned)a1.x, w2 = (unsigned)a2.x;
@@ -341,7 +344,7 @@ SRML_API int srml_rf_hist(const unsigned char* bins, long m, const int* idx, con
   if (n_items <= 0) return 0;
   if (regression && S != 2) return -6;
   if (fb < 1 || fb > FB) return -7;
-  if (il && (reinterpret_cast<uintptr_t>(bins) & 15)) return -8;
+  if (il == 1 && (reinterpret_cast<uintptr_t>(bins) & 15)) return -8;
   const size_t lds = ((size_t)fb * B * (regression ? 3 : S) + 1) * sizeof(unsigned);
   if (lds > 160 * 1024) return -5;
   const float2* w2 = reinterpret_cast<const float2*>(wy);
@@ -354,7 +357,21 @@ SRML_API int srml_rf_hist(const unsigned char* bins, long m, const int* idx, con
     hipLaunchKernelGGL((rf_hist_kernel<RG, false, ILV>), dim3(n_items), dim3(256), lds, stream, bins, m, idx, w2,  \
                        it, node_feats, nf, B, S, fb, YS, hist_u, hist_d);                                          \
   } while (0)
-  if (regression) {
+  if (il == 2) {  // row-major bins (m carries the row stride)
+    if (lds > 64 * 1024)
+      (void)hipFuncSetAttribute((const void*)rf_hist_kernel<false, false, false, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (regression) {
+      if (lds > 64 * 1024)
+        (void)hipFuncSetAttribute((const void*)rf_hist_kernel<true, false, false, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL((rf_hist_kernel<true, false, false, true>), dim3(n_items), dim3(256), lds, stream, bins, m,
+                         idx, w2, it, node_feats, nf, B, S, fb, yscale, hist_u, hist_d);
+    } else {
+      hipLaunchKernelGGL((rf_hist_kernel<false, false, false, true>), dim3(n_items), dim3(256), lds, stream, bins, m,
+                         idx, w2, it, node_feats, nf, B, S, fb, 1.0, hist_u, hist_d);
+    }
+  } else if (regression) {
     if (il) SRML_RF_HIST(true, true, yscale);
     else SRML_RF_HIST(true, false, yscale);
   } else {
@@ -671,7 +688,7 @@ SRML_API int srml_rf_hist_fixed(const unsigned char* bins, long m, const int* id
                                 double* hist_d, int il, hipStream_t stream) {
   if (n_items <= 0) return 0;
   if (fb < 1 || fb > FB) return -7;
-  if (il && (reinterpret_cast<uintptr_t>(bins) & 15)) return -8;
+  if (il == 1 && (reinterpret_cast<uintptr_t>(bins) & 15)) return -8;
   const size_t lds = ((size_t)fb * B * 3 + 1) * sizeof(unsigned);
   if (lds > 160 * 1024) return -5;
   const float2* w2 = reinterpret_cast<const float2*>(wy);

@@ -46,3 +46,19 @@ def test_one_sync_levels_match_two_sync_gpu(monkeypatch, regression, gpu_device)
     Xq = np.random.default_rng(9).standard_normal((500, 24)).astype(np.float32)
     np.testing.assert_array_equal(a.transform(DataFrame.from_numpy(Xq)).to_numpy("prediction"),
                                   b.transform(DataFrame.from_numpy(Xq)).to_numpy("prediction"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("regression", [False, True])
+def test_row_major_bins_match_feature_major_gpu(monkeypatch, regression, gpu_device):
+    """Histograms gathered from the row-major copy of the bins grow the same trees."""
+    from spark_rapids_ml_nai_amd.models import forest
+
+    monkeypatch.setattr(forest, "RM_ROWS", 0.0)
+    a = _fit(monkeypatch, True, regression, "cuda")
+    monkeypatch.setattr(forest, "RM_ROWS", 1e12)
+    b = _fit(monkeypatch, True, regression, "cuda")
+    assert a.totalNumNodes == b.totalNumNodes
+    Xq = np.random.default_rng(9).standard_normal((500, 24)).astype(np.float32)
+    np.testing.assert_array_equal(a.transform(DataFrame.from_numpy(Xq)).to_numpy("prediction"),
+                                  b.transform(DataFrame.from_numpy(Xq)).to_numpy("prediction"))
