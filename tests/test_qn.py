@@ -411,6 +411,33 @@ def test_logistic_fit_margin_cache_matches_full_evaluations(gpu_device, monkeypa
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("fit_intercept,standardization", [(False, False), (True, True), (False, True)])
+def test_logistic_fit_margin_cache_intercept_and_scaling(gpu_device, monkeypatch, fit_intercept, standardization):
+    """The margins stay linear in the step with or without an intercept and with the
+    standardisation folded into the coefficients: same optimum as the all-full-evaluation fit."""
+    from spark_rapids_ml_nai_amd.models import qn as qnm
+    from spark_rapids_ml_nai_amd.models.logistic import logistic_fit
+    from spark_rapids_ml_nai_amd.parallel.context import WorkerContext
+
+    rng = np.random.default_rng(31)
+    m, n = 20000, 1100
+    X = (rng.standard_normal((m, n)) * rng.uniform(0.2, 5.0, n) + rng.uniform(-1, 1, n)).astype(np.float32)
+    y = (X[:, :6].sum(1) + rng.standard_normal(m) > 0).astype(np.float32)
+    Xt, yt = torch.from_numpy(X).to(gpu_device), torch.from_numpy(y).to(gpu_device)
+    ctx = WorkerContext.single(gpu_device)
+    out = {}
+    for zc in (False, True):
+        monkeypatch.setattr(qnm, "QN_ZCACHE", zc)
+        out[zc] = logistic_fit(Xt, yt, m, ctx, reg=1e-4, l1_ratio=0.0, fit_intercept=fit_intercept,
+                               standardization=standardization, max_iter=100, tol=1e-30)
+    a, b = out[False], out[True]
+    assert abs(a["objective"] - b["objective"]) <= 1e-7 * abs(a["objective"]), (a["objective"], b["objective"])
+    assert b["_solver"].get("n_margin_only", 0) > 0, b["_solver"]
+    np.testing.assert_allclose(np.asarray(b["coef_"]), np.asarray(a["coef_"]), rtol=2e-2, atol=2e-3)
+    np.testing.assert_allclose(np.asarray(b["intercept_"]), np.asarray(a["intercept_"]), rtol=2e-3, atol=2e-3)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n", [1501, 3001])
 def test_logistic_fit_unaligned_width_has_no_fold(gpu_device, monkeypatch, n):
     """A width the prefetching kernel rejects (n % 4 != 0) gets no partial-row workspace, so the
