@@ -83,6 +83,11 @@ RF_ONE_SYNC = os.environ.get("SRML_RF_ONE_SYNC", "1") != "0"
 # bins (built once, at the first such level): a row's sampled features share cache lines there,
 # where the feature-major matrix costs one line per (row, feature) (0 = off)
 RM_ROWS = float(os.environ.get("SRML_RF_ROWMAJOR_ROWS", "10000"))
+# classification levels on the row-major copy whose nodes average fewer positions than this build
+# each node's histogram and split search in one block (ops.rf_node_split: the histograms stay in
+# LDS) instead of rf_hist + rf_best_split (0 = off); nodes above FUSED_MAX_ROWS keep the unfused path
+FUSED_ROWS = float(os.environ.get("SRML_RF_FUSED_ROWS", "10000"))
+FUSED_MAX_ROWS = 1 << 20
 LAST_LEVELS: List[Dict[str, Any]] = []
 
 
@@ -566,6 +571,7 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
         res_out: List[np.ndarray] = []
         res_feat: List[np.ndarray] = []
         one_sync = RF_ONE_SYNC and max_leaves <= 0
+        wy_lvl: Optional[torch.Tensor] = None  # (weight, class) pairs of this level's positions (fused split)
         res_out_d: List[torch.Tensor] = []  # one_sync: the groups' split records / feature ids, on the device
         res_fsel_d: List[torch.Tensor] = []
         res_left: List[torch.Tensor] = []  # classification: left-child totals of every candidate
@@ -618,71 +624,84 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
             if il is None and RM_ROWS > 0 and dev.type == "cuda" and not deterministic() \
                     and float(c_cnt.mean()) < RM_ROWS:
                 if bins_rm is None:
-                    bins_rm = bins.t().contiguous()  # (m, n) row-major, built once
+                    bins_rm = ops.rf_row_major(bins)  # (m, n) row-major, built once
                 rm = bins_rm
-            # rows per work item: enough blocks to fill the chip, few per (node, feature chunk)
-            rpi = int(min(WIDE_ROWS_MAX, max(rpi_min, (int(c_cnt.sum()) * nfc_l) // blocks)))
-            rpi = (rpi + 511) // 512 * 512
-            nch = (c_cnt + rpi - 1) // rpi
-            tot_ch = int(nch.sum())
-            node_rep = np.repeat(np.arange(C), nch)
-            first = np.repeat(np.cumsum(nch) - nch, nch)
-            chunk = np.arange(tot_ch) - first
-            rb = c_start[node_rep] + chunk * rpi
-            re = np.minimum(rb + rpi, c_start[node_rep] + c_cnt[node_rep])
-            it = np.empty((tot_ch * nfc_l, 4), dtype=np.int32)
-            # single-chunk nodes own their histogram cells: plain stores, no zeroing, no atomics
-            single = np.where(nch[node_rep] == 1, 1 << 30, 0).astype(np.int32)
-            if CHUNK_MAJOR_ITEMS:
-                # feature-chunk-major launch order: the blocks in flight at any time all read
-                # feature chunk c of their nodes — a few dozen adjacent bin columns, so every column
-                # comes from HBM about once per level and the other nodes' gathers hit L2 / MALL
-                # (node-major order streamed each node's own sample: deep levels re-read the whole
-                # matrix once per node)
-                it[:, 0] = np.tile(node_rep, nfc_l)
-                it[:, 1] = np.tile(rb, nfc_l)
-                it[:, 2] = np.tile(re, nfc_l)
-                it[:, 3] = np.repeat(np.arange(nfc_l, dtype=np.int32), tot_ch) | np.tile(single, nfc_l)
+            fused = (rm is not None and not regression and not data_parallel and derive is None
+                     and not streamed_root and FUSED_ROWS > 0 and float(c_cnt.mean()) < FUSED_ROWS
+                     and int(c_cnt.max()) <= FUSED_MAX_ROWS and ops.rf_node_split_ok(nf, B, SH))
+            if fused:
+                # small nodes: histogram + split search per node in one block, nothing to HBM between
+                if wy_lvl is None:
+                    wy_lvl = ops.rf_hist_wy(idx, yv, None, wpos)
+                se = _h2d(np.stack([c_start, c_start + c_cnt], 1).astype(np.int32), dev)
+                clk.mark("items_host")
+                out, left_c = ops.rf_node_split(rm, idx, wy_lvl, se, feats, B, SH, crit, min_leaf, min_gain)
+                res_left.append(left_c)
+                prev_hist = None
             else:
-                it[:, 0] = np.repeat(node_rep, nfc_l)
-                it[:, 1] = np.repeat(rb, nfc_l)
-                it[:, 2] = np.repeat(re, nfc_l)
-                it[:, 3] = np.tile(np.arange(nfc_l), tot_ch) | np.repeat(single, nfc_l)
-            clk.mark("items_host")
-            if not streamed_root:
-                items_t = _h2d(it, dev)
-                excl = ({"multi_nodes": _h2d(np.nonzero(nch != 1)[0], dev)}
-                        if dev.type == "cuda" else None)
-                hist = ops.rf_hist(bins, idx, yv, None, items_t, feats if Cp == C else _pad_rows(feats, Cp), Cp, B,
-                                   SH, regression, pos_weight=wpos,
-                                   fb=fb_l, yscale=yscale, exclusive=excl, bins_il=il,
-                                   wide=il is not None and fb_l == wide_fb, rec_bytes=WIDE_REC_BYTES if wide_fb else 32,
-                                   bins_rm=rm,
-                                   packed_scale=pack_scale if fb_l == wide_fb else None)
-            if Cp > C:
-                hist[C:].zero_()  # padding nodes (no items; an `exclusive` histogram is not pre-zeroed)
-            if scatter:
-                own = ctx.comm.reduce_scatter(hist)  # summed histograms of this rank's Cp / W nodes
-                del hist
-                out_o, _ = ops.rf_best_split(own, B, SH, regression, crit, min_leaf, min_gain)
-                recs = [out_o] if regression else [out_o, _left_totals(own, out_o)]
-                del own
-                # every rank's split records (+ left totals): a few doubles per node
-                allr = ctx.comm.allgather(torch.cat(recs, 1).contiguous())[:C]
-                out = allr[:, :6]
-                if not regression:
-                    res_left.append(allr[:, 6:])
-            else:
-                if data_parallel:
-                    ctx.comm.allreduce(hist)  # (sibling subtraction: the built half only)
-                if derive is not None:
-                    hist, C = _expand_siblings(hist, derive, sib_pos, prev_hist, prev_parent[cand]), int(cand.size)
-                    feats = torch.arange(n, device=dev, dtype=torch.int32).repeat(C, 1)
-                out, _ = ops.rf_best_split(hist, B, SH, regression, crit, min_leaf, min_gain)
-                if not regression:
-                    res_left.append(_left_totals(hist, out))
-                prev_hist = hist if keep_hist else None
-                del hist
+                # rows per work item: enough blocks to fill the chip, few per (node, feature chunk)
+                rpi = int(min(WIDE_ROWS_MAX, max(rpi_min, (int(c_cnt.sum()) * nfc_l) // blocks)))
+                rpi = (rpi + 511) // 512 * 512
+                nch = (c_cnt + rpi - 1) // rpi
+                tot_ch = int(nch.sum())
+                node_rep = np.repeat(np.arange(C), nch)
+                first = np.repeat(np.cumsum(nch) - nch, nch)
+                chunk = np.arange(tot_ch) - first
+                rb = c_start[node_rep] + chunk * rpi
+                re = np.minimum(rb + rpi, c_start[node_rep] + c_cnt[node_rep])
+                it = np.empty((tot_ch * nfc_l, 4), dtype=np.int32)
+                # single-chunk nodes own their histogram cells: plain stores, no zeroing, no atomics
+                single = np.where(nch[node_rep] == 1, 1 << 30, 0).astype(np.int32)
+                if CHUNK_MAJOR_ITEMS:
+                    # feature-chunk-major launch order: the blocks in flight at any time all read
+                    # feature chunk c of their nodes — a few dozen adjacent bin columns, so every column
+                    # comes from HBM about once per level and the other nodes' gathers hit L2 / MALL
+                    # (node-major order streamed each node's own sample: deep levels re-read the whole
+                    # matrix once per node)
+                    it[:, 0] = np.tile(node_rep, nfc_l)
+                    it[:, 1] = np.tile(rb, nfc_l)
+                    it[:, 2] = np.tile(re, nfc_l)
+                    it[:, 3] = np.repeat(np.arange(nfc_l, dtype=np.int32), tot_ch) | np.tile(single, nfc_l)
+                else:
+                    it[:, 0] = np.repeat(node_rep, nfc_l)
+                    it[:, 1] = np.repeat(rb, nfc_l)
+                    it[:, 2] = np.repeat(re, nfc_l)
+                    it[:, 3] = np.tile(np.arange(nfc_l), tot_ch) | np.repeat(single, nfc_l)
+                clk.mark("items_host")
+                if not streamed_root:
+                    items_t = _h2d(it, dev)
+                    excl = ({"multi_nodes": _h2d(np.nonzero(nch != 1)[0], dev)}
+                            if dev.type == "cuda" else None)
+                    hist = ops.rf_hist(bins, idx, yv, None, items_t, feats if Cp == C else _pad_rows(feats, Cp),
+                                       Cp, B, SH, regression, pos_weight=wpos, fb=fb_l, yscale=yscale,
+                                       exclusive=excl, bins_il=il, wide=il is not None and fb_l == wide_fb,
+                                       rec_bytes=WIDE_REC_BYTES if wide_fb else 32, bins_rm=rm,
+                                       packed_scale=pack_scale if fb_l == wide_fb else None)
+                if Cp > C:
+                    hist[C:].zero_()  # padding nodes (no items; an `exclusive` histogram is not pre-zeroed)
+                if scatter:
+                    own = ctx.comm.reduce_scatter(hist)  # summed histograms of this rank's Cp / W nodes
+                    del hist
+                    out_o, _ = ops.rf_best_split(own, B, SH, regression, crit, min_leaf, min_gain)
+                    recs = [out_o] if regression else [out_o, _left_totals(own, out_o)]
+                    del own
+                    # every rank's split records (+ left totals): a few doubles per node
+                    allr = ctx.comm.allgather(torch.cat(recs, 1).contiguous())[:C]
+                    out = allr[:, :6]
+                    if not regression:
+                        res_left.append(allr[:, 6:])
+                else:
+                    if data_parallel:
+                        ctx.comm.allreduce(hist)  # (sibling subtraction: the built half only)
+                    if derive is not None:
+                        hist = _expand_siblings(hist, derive, sib_pos, prev_hist, prev_parent[cand])
+                        C = int(cand.size)
+                        feats = torch.arange(n, device=dev, dtype=torch.int32).repeat(C, 1)
+                    out, _ = ops.rf_best_split(hist, B, SH, regression, crit, min_leaf, min_gain)
+                    if not regression:
+                        res_left.append(_left_totals(hist, out))
+                    prev_hist = hist if keep_hist else None
+                    del hist
             # the winning feature ids gathered on the device: one copy of (records | feature id)
             fsel = feats[:C].gather(1, out[:, 1].clamp_min(0).long().view(-1, 1)).to(out.dtype)
             clk.mark("hist_split_launch")

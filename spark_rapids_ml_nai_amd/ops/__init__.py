@@ -1109,6 +1109,17 @@ def rf_interleave(bins: torch.Tensor, rec_bytes: int = 32) -> torch.Tensor:
     return out
 
 
+def rf_row_major(bins: torch.Tensor) -> torch.Tensor:
+    """Row-major (m, n) copy of a feature-major (n, m) uint8 bin matrix (``srml_rf_transpose_u8``
+    on the device: LDS-tiled, one pass each way)."""
+    n, m = bins.shape
+    if not bins.is_cuda:
+        return bins.t().contiguous()
+    out = torch.empty((m, n), dtype=torch.uint8, device=bins.device)
+    native.call("srml_rf_transpose_u8", _c(bins).data_ptr(), m, n, out.data_ptr(), native.stream(bins.device))
+    return out
+
+
 def rf_il_useful(n: int, nf: int, fb: int) -> bool:
     """Whether a node's chunk of ``fb`` ascending sampled features (nf of n) spans few enough
     32-feature records that the record layout halves the bin loads per row (at least)."""
@@ -1257,6 +1268,40 @@ def rf_best_split(hist: torch.Tensor, B: int, S: int, regression: bool, crit: in
                 hist.data_ptr() if regression else None, nodes, nf, B, S, int(regression), int(crit),
                 float(min_leaf), float(min_gain), out.data_ptr(), tot.data_ptr(), native.stream(dev))
     return out, tot
+
+
+def rf_node_split_ok(nf: int, B: int, S: int) -> bool:
+    """Whether the fused small-node classification split (``rf_node_split``) takes nf sampled
+    features x B bins x S classes (the whole node histogram within 150 KiB of LDS)."""
+    return bool(int(native.lib().srml_rf_node_split_ok(int(nf), int(B), int(S))))
+
+
+def rf_node_split(bins_rm: torch.Tensor, idx: torch.Tensor, wy: torch.Tensor, se: torch.Tensor,
+                  node_feats: torch.Tensor, B: int, S: int, crit: int, min_leaf: float,
+                  min_gain: float) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Classification histogram + split search of small nodes in one kernel (``srml_rf_node_split``,
+    the node's histogram never leaves LDS). ``bins_rm``: row-major (m, n) uint8 bins; ``idx`` /
+    ``wy``: the level's row ids and (weight, class) pairs (``rf_hist_wy``); ``se``: (nodes, 2)
+    int32 [begin, end) positions; ``node_feats``: (nodes, nf) ascending sampled feature ids.
+    Returns the ``rf_best_split`` record (nodes, 6) and the winner's left-child class totals
+    (nodes, S) (zeros without a split) — equal to ``rf_hist`` + ``rf_best_split`` + the
+    left-prefix of the winning histogram."""
+    nodes, nf = int(node_feats.shape[0]), int(node_feats.shape[1])
+    dev = bins_rm.device
+    if se.shape != (nodes, 2) or idx.dtype != torch.int32 or wy.dtype != torch.float32 or wy.shape[-1] != 2:
+        raise ValueError("rf_node_split: se (nodes, 2) int32, idx int32, wy (P, 2) float32")
+    if wy.shape[0] != idx.shape[0]:
+        raise ValueError("rf_node_split: wy holds %d positions, idx %d" % (wy.shape[0], idx.shape[0]))
+    if not rf_node_split_ok(nf, B, S):
+        raise ValueError("rf_node_split: nf=%d B=%d S=%d exceeds the LDS histogram" % (nf, B, S))
+    out = torch.empty((nodes, 6), dtype=torch.float64, device=dev)
+    left = torch.empty((nodes, S), dtype=torch.float64, device=dev)
+    rm = _c(bins_rm)
+    native.call("srml_rf_node_split", rm.data_ptr(), int(rm.shape[1]), _c(idx).data_ptr(), _c(wy).data_ptr(),
+                _c(se.to(torch.int32)).data_ptr(), nodes, _c(node_feats.to(torch.int32)).data_ptr(), nf, int(B),
+                int(S), int(crit), float(min_leaf), float(min_gain), out.data_ptr(), left.data_ptr(),
+                native.stream(dev))
+    return out, left
 
 
 def _impurity_ref(s: torch.Tensor, crit: int) -> torch.Tensor:

@@ -657,6 +657,67 @@ __global__ __launch_bounds__(256) void rf_interleave4_kernel(const unsigned char
   }
 }
 
+// Row-major copy of the feature-major (n x m) bin matrix: out[r * n + f] = bins[f * m + r] (the
+// deep levels' gathers, rf_hist RM / rf_node_split). 64-row x 64-feature byte tiles through LDS:
+// 16-B loads along each feature's rows, 8-B stores along each row's features (byte accesses at
+// the edges / unaligned shapes): one pass over the matrix each way (torch's strided uint8 copy of
+// the transpose took ~16 ms at 1M x 3000).
+__global__ __launch_bounds__(256) void rf_transpose_u8_kernel(const unsigned char* __restrict__ in, long m, int n,
+                                                              unsigned char* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) unsigned char tile[64][68];
+  const long r0 = (long)blockIdx.x * 64;
+  const int f0 = blockIdx.y * 64;
+  const int t = threadIdx.x;
+  {
+    const int fl = t >> 2, rc = (t & 3) * 16;
+    const int f = f0 + fl;
+    const long r = r0 + rc;
+    unsigned w[4] = {0u, 0u, 0u, 0u};
+    if (f < n) {
+      const unsigned char* src = in + (long)f * m + r;
+      if (r + 16 <= m && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+        const uint4 v = *reinterpret_cast<const uint4*>(src);
+        w[0] = v.x;
+        w[1] = v.y;
+        w[2] = v.z;
+        w[3] = v.w;
+      } else {
+        for (int k = 0; k < 16; ++k)
+          if (r + k < m) w[k >> 2] |= (unsigned)src[k] << (8 * (k & 3));
+      }
+    }
+    unsigned* d = reinterpret_cast<unsigned*>(&tile[fl][rc]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) d[q] = w[q];
+  }
+  __syncthreads();
+  const int rl = t >> 2, fc = (t & 3) * 16;
+  const long r = r0 + rl;
+  if (r >= m) return;
+  unsigned w[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    w[q] = (unsigned)tile[fc + 4 * q][rl] | ((unsigned)tile[fc + 4 * q + 1][rl] << 8) |
+           ((unsigned)tile[fc + 4 * q + 2][rl] << 16) | ((unsigned)tile[fc + 4 * q + 3][rl] << 24);
+  unsigned char* dst = out + r * n + f0 + fc;
+  if (f0 + fc + 16 <= n && (reinterpret_cast<uintptr_t>(dst) & 7) == 0) {
+    reinterpret_cast<uint2*>(dst)[0] = make_uint2(w[0], w[1]);
+    reinterpret_cast<uint2*>(dst)[1] = make_uint2(w[2], w[3]);
+  } else {
+    for (int k = 0; k < 16; ++k)
+      if (f0 + fc + k < n) dst[k] = (unsigned char)(w[k >> 2] >> (8 * (k & 3)));
+  }
+}
+
+SRML_API int srml_rf_transpose_u8(const unsigned char* bins, long m, int n, unsigned char* out, hipStream_t stream) {
+  if (m <= 0 || n <= 0) return 0;
+  const long gy = (n + 63) / 64;
+  if (gy > 65535) return -2;
+  hipLaunchKernelGGL(rf_transpose_u8_kernel, dim3((unsigned)((m + 63) / 64), (unsigned)gy), dim3(256), 0, stream, bins,
+                     m, n, out);
+  return srml_status();
+}
+
 // rb = record bytes (features per record): 32 (the 8-feature item kernel's layout) or 64
 SRML_API int srml_rf_interleave_u8(const unsigned char* bins, long m, int n, int rb, unsigned char* out,
                                    hipStream_t stream) {
@@ -753,6 +814,16 @@ __device__ __forceinline__ double impurity(const double* s, int S, int crit, dou
   return acc;
 }
 
+// classification gain of one threshold (shared by the split kernels, so they agree bit for bit)
+template <int SMAX>
+__device__ __forceinline__ double class_split_gain(const double* left, const double* tot, int S, int crit, double nl,
+                                                   double nr, double ntot, double pimp) {
+  double right[SMAX];
+#pragma unroll
+  for (int c = 0; c < SMAX; ++c) right[c] = tot[c] - left[c];
+  return pimp - (nl / ntot) * impurity<SMAX>(left, S, crit, nl) - (nr / ntot) * impurity<SMAX>(right, S, crit, nr);
+}
+
 template <int SMAX, bool REG>
 __global__ __launch_bounds__(256) void rf_best_split_kernel(const unsigned* __restrict__ hist_u,
                                                             const double* __restrict__ hist_d, int nf, int B, int S,
@@ -814,10 +885,7 @@ __global__ __launch_bounds__(256) void rf_best_split_kernel(const unsigned* __re
         const double sl = left[1], sr = tot[1] - left[1];
         gain = (sl * sl / nl + sr * sr / nr - tot[1] * tot[1] / ntot) / ntot;
       } else {
-        double right[SMAX];
-#pragma unroll
-        for (int c = 0; c < SMAX; ++c) right[c] = tot[c] - left[c];
-        gain = pimp - (nl / ntot) * impurity<SMAX>(left, S, crit, nl) - (nr / ntot) * impurity<SMAX>(right, S, crit, nr);
+        gain = class_split_gain<SMAX>(left, tot, S, crit, nl, nr, ntot, pimp);
       }
       const int key = f * 1024 + b;
       if (gain > best || (gain == best && key < bkey)) { best = gain; bkey = key; }
@@ -884,6 +952,232 @@ SRML_API int srml_rf_best_split(const unsigned* hist_u, const double* hist_d, in
   else if (S <= 16) SRML_RF_SPLIT(16);
   else if (S <= 32) SRML_RF_SPLIT(32);
   else return -6;
+  return srml_status();
+}
+
+// ------------------------------------------------------------------------------------------
+// Fused histogram + split search for small classification nodes (the deep levels). One 512-thread
+// block per node keeps the node's whole histogram ([feature slot][class][bin] u32 weighted counts
+// of every sampled feature) in LDS, so nothing goes to HBM between the two phases: the unfused
+// level writes nf * B * S cells per node, re-reads them in rf_best_split_kernel and once more
+// (cumsum + gather) for the left-child totals, and at the deep levels it launches one 256-thread
+// block per 8-feature chunk of a ~200-row node. Rows are gathered from the ROW-MAJOR bin copy: a
+// wave takes NS_U rows at a time (wave-uniform row id, weight and class) and its lanes fetch the
+// row's sampled features — ascending ids, so one row's gathers share cache lines — and add the
+// weight into their own feature's cells (distinct features per lane: no same-address LDS
+// atomics). The split search gives each feature to a wave with the bins spread over the lanes
+// (a run of consecutive bins per lane, exclusive wave scan of the class counts) instead of one
+// thread per feature. Counts are integers below 2^32 per node, so every left / right total is
+// exact and the gains (class_split_gain), the winner (highest gain, then lowest feature slot, then
+// lowest bin) and the record equal rf_best_split_kernel's on the same histogram. Outputs per node:
+// the rf_best_split record {gain, slot, bin, n_left, n_right, impurity} and the winner's
+// left-child class totals (zeros without a split). Reference: tree.py:309-414 (cuML's level-wise
+// split search).
+// ------------------------------------------------------------------------------------------
+constexpr int NS_T = 512;
+constexpr int NS_W = NS_T / 64;
+constexpr int NS_FL = 4;  // sampled features per lane: nf <= 256
+constexpr int NS_U = 4;   // rows in flight per wave
+
+__device__ __forceinline__ unsigned wave_excl_scan_u32(unsigned v, int lane) {
+  unsigned x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  return x - v;
+}
+
+__device__ __forceinline__ unsigned wave_sum_u32(unsigned v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ bool split_better(double g, int k, double bg, int bk) {
+  return g > bg || (g == bg && k < bk);
+}
+
+template <int SMAX>
+__global__ __launch_bounds__(NS_T) void rf_node_split_kernel(const unsigned char* __restrict__ bins_rm, long ldr,
+                                                             const int* __restrict__ idx,
+                                                             const float2* __restrict__ wy,
+                                                             const int* __restrict__ se,
+                                                             const int* __restrict__ node_feats, int nf, int B, int S,
+                                                             int crit, double min_leaf, double min_gain,
+                                                             double* __restrict__ out, double* __restrict__ left_out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned lh[];  // [nf][S][B]
+  __shared__ double s_gain[NS_W];
+  __shared__ int s_key[NS_W];
+  __shared__ double s_tot[SMAX];
+  const int node = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int cells = nf * S * B;
+  for (int i = threadIdx.x; i < cells; i += NS_T) lh[i] = 0u;
+  long foff[NS_FL];
+#pragma unroll
+  for (int q = 0; q < NS_FL; ++q) {
+    const int j = lane + 64 * q;
+    foff[q] = j < nf ? (long)node_feats[(long)node * nf + j] : 0;
+  }
+  __syncthreads();
+  const int rb = se[2 * node], re = se[2 * node + 1];
+  for (int i0 = rb + wave * NS_U; i0 < re; i0 += NS_W * NS_U) {
+    int r[NS_U], c[NS_U];
+    unsigned w[NS_U];
+#pragma unroll
+    for (int u = 0; u < NS_U; ++u) {
+      const int i = i0 + u;
+      const bool v = i < re;
+      r[u] = v ? idx[i] : 0;
+      const float2 a = v ? wy[i] : make_float2(0.f, 0.f);
+      w[u] = (unsigned)a.x;
+      c[u] = (int)a.y;
+    }
+    int bv[NS_U][NS_FL];
+#pragma unroll
+    for (int u = 0; u < NS_U; ++u)
+#pragma unroll
+      for (int q = 0; q < NS_FL; ++q)
+        bv[u][q] = (lane + 64 * q < nf && w[u]) ? (int)bins_rm[(long)r[u] * ldr + foff[q]] : 0;
+#pragma unroll
+    for (int u = 0; u < NS_U; ++u)
+#pragma unroll
+      for (int q = 0; q < NS_FL; ++q) {
+        const int j = lane + 64 * q;
+        if (j < nf && w[u]) atomicAdd(&lh[(j * S + c[u]) * B + bv[u][q]], w[u]);
+      }
+  }
+  __syncthreads();
+  // node totals from feature slot 0 (every slot's histogram sums to them)
+  if (wave == 0) {
+    for (int cc = 0; cc < S; ++cc) {
+      unsigned v = 0;
+      for (int b = lane; b < B; b += 64) v += lh[cc * B + b];
+      v = wave_sum_u32(v);
+      if (lane == 0) s_tot[cc] = (double)v;
+    }
+  }
+  __syncthreads();
+  double tot[SMAX];
+#pragma unroll
+  for (int cc = 0; cc < SMAX; ++cc) tot[cc] = cc < S ? s_tot[cc] : 0.0;
+  double ntot = 0.0;
+#pragma unroll
+  for (int cc = 0; cc < SMAX; ++cc) ntot += tot[cc];
+  const double pimp = impurity<SMAX>(tot, S, crit, ntot);
+  double best = -1.0;
+  int bkey = 0x7fffffff;
+  const int bpl = (B + 63) >> 6;
+  const int b0 = lane * bpl;
+  for (int f = wave; f < nf; f += NS_W) {
+    const unsigned* hf = lh + f * S * B;
+    unsigned pre[SMAX];
+#pragma unroll
+    for (int cc = 0; cc < SMAX; ++cc) {
+      pre[cc] = 0u;
+      if (cc < S) {  // wave-uniform
+        unsigned own = 0;
+        for (int k = 0; k < bpl; ++k)
+          if (b0 + k < B) own += hf[cc * B + b0 + k];
+        pre[cc] = wave_excl_scan_u32(own, lane);
+      }
+    }
+    for (int k = 0; k < bpl; ++k) {
+      const int b = b0 + k;
+      if (b >= B - 1) break;
+      double left[SMAX];
+      double nl = 0.0;
+#pragma unroll
+      for (int cc = 0; cc < SMAX; ++cc) {
+        if (cc < S) pre[cc] += hf[cc * B + b];
+        left[cc] = cc < S ? (double)pre[cc] : 0.0;
+      }
+#pragma unroll
+      for (int cc = 0; cc < SMAX; ++cc) nl += left[cc];
+      const double nr = ntot - nl;
+      if (nl < min_leaf || nr < min_leaf || nl <= 0.0 || nr <= 0.0) continue;
+      const double gain = class_split_gain<SMAX>(left, tot, S, crit, nl, nr, ntot, pimp);
+      const int key = f * 1024 + b;
+      if (split_better(gain, key, best, bkey)) {
+        best = gain;
+        bkey = key;
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double og = __shfl_xor(best, o, 64);
+    const int ok = __shfl_xor(bkey, o, 64);
+    if (split_better(og, ok, best, bkey)) {
+      best = og;
+      bkey = ok;
+    }
+  }
+  if (lane == 0) {
+    s_gain[wave] = best;
+    s_key[wave] = bkey;
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  double g = s_gain[0];
+  int key = s_key[0];
+  for (int k = 1; k < NS_W; ++k)
+    if (split_better(s_gain[k], s_key[k], g, key)) {
+      g = s_gain[k];
+      key = s_key[k];
+    }
+  const bool ok = (g > min_gain || (g >= 0.0 && min_gain < 0.0)) && key != 0x7fffffff && g > 1e-15;
+  const int f = ok ? key / 1024 : 0, bb = ok ? key % 1024 : -1;
+  double nl = 0.0;
+  for (int cc = 0; cc < S; ++cc) {
+    unsigned v = 0;
+    for (int b = lane; b <= bb; b += 64) v += lh[(f * S + cc) * B + b];
+    v = wave_sum_u32(v);
+    if (lane == 0) left_out[(long)node * S + cc] = (double)v;
+    nl += (double)v;
+  }
+  if (lane == 0) {
+    double* o = out + (long)node * 6;
+    o[0] = ok ? g : -1.0;
+    o[1] = ok ? (double)f : -1.0;
+    o[2] = ok ? (double)bb : -1.0;
+    o[3] = nl;
+    o[4] = ok ? ntot - nl : 0.0;
+    o[5] = pimp;
+  }
+}
+
+// whether srml_rf_node_split takes (nf sampled features, B bins, S classes)
+SRML_API int srml_rf_node_split_ok(int nf, int B, int S) {
+  return nf >= 1 && nf <= 64 * NS_FL && S >= 1 && S <= 8 && B >= 2 && B <= 1024 &&
+         (long)nf * S * B * (long)sizeof(unsigned) <= 150 * 1024;
+}
+
+// bins_rm: row-major uint8 bins (row r at bins_rm + r * ldr); idx / wy: the level's positions
+// (row id, (weight, class)); se: (nodes, 2) int32 [begin, end) positions of each node; node_feats:
+// (nodes, nf) ascending sampled feature ids. out: (nodes, 6) fp64, left: (nodes, S) fp64.
+SRML_API int srml_rf_node_split(const unsigned char* bins_rm, long ldr, const int* idx, const float* wy, const int* se,
+                                int nodes, const int* node_feats, int nf, int B, int S, int crit, double min_leaf,
+                                double min_gain, double* out, double* left, hipStream_t stream) {
+  if (nodes <= 0) return 0;
+  if (!srml_rf_node_split_ok(nf, B, S)) return -6;
+  const size_t lds = (size_t)nf * S * B * sizeof(unsigned);
+  const float2* w2 = reinterpret_cast<const float2*>(wy);
+#define SRML_RF_NODE_SPLIT(SM)                                                                                     \
+  do {                                                                                                             \
+    if (lds > 64 * 1024)                                                                                           \
+      (void)hipFuncSetAttribute((const void*)rf_node_split_kernel<SM>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                (int)lds);                                                                         \
+    hipLaunchKernelGGL((rf_node_split_kernel<SM>), dim3(nodes), dim3(NS_T), lds, stream, bins_rm, ldr, idx, w2, se,  \
+                       node_feats, nf, B, S, crit, min_leaf, min_gain, out, left);                                 \
+  } while (0)
+  if (S <= 2) SRML_RF_NODE_SPLIT(2);
+  else if (S <= 4) SRML_RF_NODE_SPLIT(4);
+  else SRML_RF_NODE_SPLIT(8);
+#undef SRML_RF_NODE_SPLIT
   return srml_status();
 }
 

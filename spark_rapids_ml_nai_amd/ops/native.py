@@ -155,6 +155,9 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_rf_hist_fb": (_I, _I, _I),
     "srml_rf_hist_fb_max": (),
     "srml_rf_best_split": (_P, _P, _I, _I, _I, _I, _I, _I, _D, _D, _P, _P, _P),
+    "srml_rf_node_split_ok": (_I, _I, _I),
+    "srml_rf_transpose_u8": (_P, _L, _I, _P, _P),
+    "srml_rf_node_split": (_P, _L, _P, _P, _P, _I, _P, _I, _I, _I, _I, _D, _D, _P, _P, _P),
     "srml_rf_route": (_P, _L, _P, _P, _L, _P, _P, _P, _P, _P),
     "srml_rf_route_segments": (_P, _L, _P, _L, _P, _I, _P, _P, _P, _P, _P),
     "srml_rf_node_stats": (_P, _P, _P, _L, _P, _I, _I, _I, _P, _P),

@@ -62,3 +62,85 @@ def test_row_major_bins_match_feature_major_gpu(monkeypatch, regression, gpu_dev
     Xq = np.random.default_rng(9).standard_normal((500, 24)).astype(np.float32)
     np.testing.assert_array_equal(a.transform(DataFrame.from_numpy(Xq)).to_numpy("prediction"),
                                   b.transform(DataFrame.from_numpy(Xq)).to_numpy("prediction"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("S,B,nf,crit,min_leaf", [(2, 128, 55, 0, 1.0), (3, 32, 200, 1, 4.0), (5, 64, 17, 0, 1.0),
+                                                  (2, 256, 40, 1, 1.0)])
+def test_rf_node_split_matches_hist_and_best_split(S, B, nf, crit, min_leaf, gpu_device):
+    """The fused small-node split (histogram in LDS + wave-parallel scan) returns exactly the records
+    of rf_hist + rf_best_split and the left-child totals of the winning histogram prefix."""
+    import torch
+
+    from spark_rapids_ml_nai_amd import ops
+    from spark_rapids_ml_nai_amd.models import forest
+
+    g = torch.Generator().manual_seed(S * 1000 + nf)
+    m, n, C = 60000, 300, 97
+    rm = torch.randint(0, B, (m, n), generator=g, dtype=torch.uint8)
+    cnt = torch.randint(0, 600, (C,), generator=g)
+    cnt[3] = 1  # single-row node: no split
+    cnt[5] = 2000
+    starts = torch.cat([torch.zeros(1, dtype=torch.long), cnt.cumsum(0)[:-1]])
+    P = int(cnt.sum())
+    assert P <= m  # positions are distinct rows
+    idx = torch.randperm(m, generator=g)[:P].to(torch.int32)
+    w = torch.randint(1, 4, (P,), generator=g).float()
+    label = torch.randint(0, S, (m,), generator=g).float()
+    feats = torch.stack([torch.randperm(n, generator=g)[:nf].sort().values for _ in range(C)]).to(torch.int32)
+    dev = torch.device(gpu_device)
+    rm_d, idx_d, w_d, lab_d, f_d = (t.to(dev) for t in (rm, idx, w, label, feats))
+    wy = ops.rf_hist_wy(idx_d, lab_d, None, w_d)
+    se = torch.stack([starts, starts + cnt], 1).to(torch.int32).to(dev)
+    out_f, left_f = ops.rf_node_split(rm_d, idx_d, wy, se, f_d, B, S, crit, min_leaf, 0.0)
+    fb = ops.rf_hist_fb(B, S, False)
+    nfc = (nf + fb - 1) // fb
+    items = torch.tensor([[c, int(starts[c]), int(starts[c] + cnt[c]), k] for c in range(C) for k in range(nfc)
+                          if cnt[c] > 0], dtype=torch.int32).to(dev)
+    hist = ops.rf_hist(rm_d.t().contiguous(), idx_d, lab_d, None, items, f_d, C, B, S, False, pos_weight=w_d, fb=fb)
+    out_r, _ = ops.rf_best_split(hist, B, S, False, crit, min_leaf, 0.0)
+    left_r = forest._left_totals(hist, out_r)
+    assert torch.equal(out_f.cpu(), out_r.cpu())
+    assert torch.equal(left_f.cpu(), left_r.cpu())
+    assert int((out_f[:, 1] >= 0).sum()) > C // 2
+
+
+def _fit_multi(monkeypatch, fused: bool, classes: int, crit: str):
+    from spark_rapids_ml_nai_amd.classification import RandomForestClassifier
+    from spark_rapids_ml_nai_amd.models import forest
+
+    monkeypatch.setattr(forest, "RM_ROWS", 1e12)
+    monkeypatch.setattr(forest, "FUSED_ROWS", 1e12 if fused else 0.0)
+    g = np.random.default_rng(6)
+    X = g.standard_normal((8000, 40)).astype(np.float32)
+    y = (np.digitize(X[:, 0] + 0.5 * X[:, 3] * X[:, 5] + 0.3 * g.standard_normal(8000),
+                     np.linspace(-1.5, 1.5, classes - 1))).astype(np.float64)
+    est = RandomForestClassifier(numTrees=5, maxDepth=8, maxBins=48, seed=11, impurity=crit,
+                                 minInstancesPerNode=2)
+    return est.fit(DataFrame.from_numpy(X, y))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("classes,crit", [(2, "gini"), (4, "entropy")])
+def test_fused_node_split_grows_same_forest_gpu(monkeypatch, classes, crit, gpu_device):
+    a = _fit_multi(monkeypatch, False, classes, crit)
+    b = _fit_multi(monkeypatch, True, classes, crit)
+    assert a.totalNumNodes == b.totalNumNodes
+    Xq = np.random.default_rng(9).standard_normal((700, 40)).astype(np.float32)
+    pa = a.transform(DataFrame.from_numpy(Xq))
+    pb = b.transform(DataFrame.from_numpy(Xq))
+    np.testing.assert_array_equal(pa.to_numpy("prediction"), pb.to_numpy("prediction"))
+    np.testing.assert_array_equal(pa.to_numpy("probability"), pb.to_numpy("probability"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,m", [(37, 1007), (3000, 4101), (64, 4096), (130, 65)])
+def test_rf_row_major_transpose_gpu(n, m, gpu_device):
+    import torch
+
+    from spark_rapids_ml_nai_amd import ops
+
+    g = torch.Generator().manual_seed(n + m)
+    bins = torch.randint(0, 256, (n, m), generator=g, dtype=torch.uint8)
+    got = ops.rf_row_major(bins.to(gpu_device))
+    assert torch.equal(got.cpu(), bins.t().contiguous())
