@@ -88,6 +88,11 @@ RM_ROWS = float(os.environ.get("SRML_RF_ROWMAJOR_ROWS", "10000"))
 # LDS) instead of rf_hist + rf_best_split (0 = off); nodes above FUSED_MAX_ROWS keep the unfused path
 FUSED_ROWS = float(os.environ.get("SRML_RF_FUSED_ROWS", "10000"))
 FUSED_MAX_ROWS = 1 << 20
+FUSED_MIN_NODES = 256  # one block per node: fewer nodes leave most CUs idle
+# narrow feature samples (several rows per wave instruction) measured slower than the unfused
+# record-layout kernels: north-star 50M x 64 (8 sampled features) levels 12-15 51 / 47 / 47 / 55 ms
+# fused vs 32 / 36 / 42 / 57 ms (profiles/rf_levels_northstar_50M_r5_fused_narrow.txt)
+FUSED_MIN_NF = 33
 LAST_LEVELS: List[Dict[str, Any]] = []
 
 
@@ -612,7 +617,18 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
             il = None
             rm = None
             fb_l, nfc_l, rpi_min, blocks = fb, nfc, ROWS_PER_ITEM, 8192
-            if use_il and float(c_cnt.mean()) < IL_DENSITY * m:
+            # (a data-parallel level sums its histograms over the ranks: fused only on one rank)
+            fused = (not regression and (not data_parallel or W == 1) and derive is None and not streamed_root
+                     and dev.type == "cuda" and not deterministic() and FUSED_ROWS > 0
+                     and float(c_cnt.mean()) < FUSED_ROWS and C >= FUSED_MIN_NODES and nf >= FUSED_MIN_NF
+                     and ops.rf_node_split_ok(nf, B, SH))
+            # nodes above FUSED_MAX_ROWS (one block each would straggle) take the unfused kernels;
+            # their records are merged back by node below
+            big = np.nonzero(c_cnt > FUSED_MAX_ROWS)[0] if fused else np.zeros(0, dtype=np.int64)
+            if LEVEL_LOG:
+                clk.rec["fused"] = bool(fused)
+                clk.rec["fused_big_nodes"] = int(big.size)
+            if use_il and not fused and float(c_cnt.mean()) < IL_DENSITY * m:
                 if bins_il is None:
                     # built once, at the first sparse level
                     bins_il = ops.rf_interleave(bins, WIDE_REC_BYTES if wide_fb else 32)
@@ -621,24 +637,31 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
                     # 1024-thread blocks over ~100-400 features: fewer, longer work items
                     fb_l, rpi_min, blocks = wide_fb, WIDE_ROWS_PER_ITEM, 2048
                     nfc_l = (nf + fb_l - 1) // fb_l
-            if il is None and RM_ROWS > 0 and dev.type == "cuda" and not deterministic() \
-                    and float(c_cnt.mean()) < RM_ROWS:
+            if fused or (il is None and RM_ROWS > 0 and dev.type == "cuda" and not deterministic()
+                         and float(c_cnt.mean()) < RM_ROWS):
                 if bins_rm is None:
                     bins_rm = ops.rf_row_major(bins)  # (m, n) row-major, built once
                 rm = bins_rm
-            fused = (rm is not None and not regression and not data_parallel and derive is None
-                     and not streamed_root and FUSED_ROWS > 0 and float(c_cnt.mean()) < FUSED_ROWS
-                     and int(c_cnt.max()) <= FUSED_MAX_ROWS and ops.rf_node_split_ok(nf, B, SH))
+            merge = None
             if fused:
                 # small nodes: histogram + split search per node in one block, nothing to HBM between
                 if wy_lvl is None:
                     wy_lvl = ops.rf_hist_wy(idx, yv, None, wpos)
-                se = _h2d(np.stack([c_start, c_start + c_cnt], 1).astype(np.int32), dev)
+                se_h = np.stack([c_start, c_start + c_cnt], 1).astype(np.int32)
+                se_h[big] = 0  # big nodes: empty here (records replaced below)
+                se = _h2d(se_h, dev)
                 clk.mark("items_host")
                 out, left_c = ops.rf_node_split(rm, idx, wy_lvl, se, feats, B, SH, crit, min_leaf, min_gain)
-                res_left.append(left_c)
                 prev_hist = None
-            else:
+                if big.size:
+                    # the big nodes run the unfused path below on their own (node slots 0 .. len(big))
+                    big_t = _h2d(big, dev)
+                    merge = (out, left_c, big_t, C, feats)
+                    c_start, c_cnt, feats = c_start[big], c_cnt[big], feats.index_select(0, big_t)
+                    C = Cp = int(big.size)
+                else:
+                    res_left.append(left_c)
+            if not fused or merge is not None:
                 # rows per work item: enough blocks to fill the chip, few per (node, feature chunk)
                 rpi = int(min(WIDE_ROWS_MAX, max(rpi_min, (int(c_cnt.sum()) * nfc_l) // blocks)))
                 rpi = (rpi + 511) // 512 * 512
@@ -702,6 +725,12 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
                         res_left.append(_left_totals(hist, out))
                     prev_hist = hist if keep_hist else None
                     del hist
+            if merge is not None:
+                out_f, left_f, big_t, C, feats = merge
+                out_f[big_t] = out
+                left_f[big_t] = res_left.pop()
+                out = out_f
+                res_left.append(left_f)
             # the winning feature ids gathered on the device: one copy of (records | feature id)
             fsel = feats[:C].gather(1, out[:, 1].clamp_min(0).long().view(-1, 1)).to(out.dtype)
             clk.mark("hist_split_launch")

@@ -962,10 +962,10 @@ SRML_API int srml_rf_best_split(const unsigned* hist_u, const double* hist_d, in
 // level writes nf * B * S cells per node, re-reads them in rf_best_split_kernel and once more
 // (cumsum + gather) for the left-child totals, and at the deep levels it launches one 256-thread
 // block per 8-feature chunk of a ~200-row node. Rows are gathered from the ROW-MAJOR bin copy: a
-// wave takes NS_U rows at a time (wave-uniform row id, weight and class) and its lanes fetch the
-// row's sampled features — ascending ids, so one row's gathers share cache lines — and add the
-// weight into their own feature's cells (distinct features per lane: no same-address LDS
-// atomics). The split search gives each feature to a wave with the bins spread over the lanes
+// row gets the next power of two >= nf lanes (64 / that rows per wave instruction, NS_U
+// instructions in flight) and its lanes fetch the row's sampled features — ascending ids, so one
+// row's gathers share cache lines (a 64-feature row is one line) — and add the row's weight into
+// their own feature's cells. The split search gives each feature to a wave with the bins spread over the lanes
 // (a run of consecutive bins per lane, exclusive wave scan of the class counts) instead of one
 // thread per feature. Counts are integers below 2^32 per node, so every left / right total is
 // exact and the gains (class_split_gain), the winner (highest gain, then lowest feature slot, then
@@ -999,14 +999,15 @@ __device__ __forceinline__ bool split_better(double g, int k, double bg, int bk)
   return g > bg || (g == bg && k < bk);
 }
 
-template <int SMAX>
+template <int SMAX, bool MULTI>
 __global__ __launch_bounds__(NS_T) void rf_node_split_kernel(const unsigned char* __restrict__ bins_rm, long ldr,
                                                              const int* __restrict__ idx,
                                                              const float2* __restrict__ wy,
                                                              const int* __restrict__ se,
                                                              const int* __restrict__ node_feats, int nf, int B, int S,
                                                              int crit, double min_leaf, double min_gain,
-                                                             double* __restrict__ out, double* __restrict__ left_out) {
+                                                             double* __restrict__ out, double* __restrict__ left_out,
+                                                             int lpr_log2) {
   extern __shared__ __attribute__((aligned(16))) unsigned lh[];  // [nf][S][B]
   __shared__ double s_gain[NS_W];
   __shared__ int s_key[NS_W];
@@ -1016,20 +1017,26 @@ __global__ __launch_bounds__(NS_T) void rf_node_split_kernel(const unsigned char
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int cells = nf * S * B;
   for (int i = threadIdx.x; i < cells; i += NS_T) lh[i] = 0u;
+  // lanes per row: the next power of two >= nf (<= 64); a wave instruction covers 64 / LPR rows,
+  // lane (sub, fl) = row sub, features fl, fl + LPR, ... (several per lane only when nf > 64)
+  // (!MULTI: one row per wave instruction, the row id / weight / class stay wave-uniform)
+  const int lg = MULTI ? lpr_log2 : 6;
+  const int LPR = 1 << lg, RPW = 64 >> lg;
+  const int sub = MULTI ? lane >> lg : 0, fl = MULTI ? (lane & (LPR - 1)) : lane;
   long foff[NS_FL];
 #pragma unroll
   for (int q = 0; q < NS_FL; ++q) {
-    const int j = lane + 64 * q;
+    const int j = fl + LPR * q;
     foff[q] = j < nf ? (long)node_feats[(long)node * nf + j] : 0;
   }
   __syncthreads();
   const int rb = se[2 * node], re = se[2 * node + 1];
-  for (int i0 = rb + wave * NS_U; i0 < re; i0 += NS_W * NS_U) {
+  for (int i0 = rb + wave * NS_U * RPW; i0 < re; i0 += NS_W * NS_U * RPW) {
     int r[NS_U], c[NS_U];
     unsigned w[NS_U];
 #pragma unroll
     for (int u = 0; u < NS_U; ++u) {
-      const int i = i0 + u;
+      const int i = i0 + u * RPW + sub;
       const bool v = i < re;
       r[u] = v ? idx[i] : 0;
       const float2 a = v ? wy[i] : make_float2(0.f, 0.f);
@@ -1041,12 +1048,12 @@ __global__ __launch_bounds__(NS_T) void rf_node_split_kernel(const unsigned char
     for (int u = 0; u < NS_U; ++u)
 #pragma unroll
       for (int q = 0; q < NS_FL; ++q)
-        bv[u][q] = (lane + 64 * q < nf && w[u]) ? (int)bins_rm[(long)r[u] * ldr + foff[q]] : 0;
+        bv[u][q] = (fl + LPR * q < nf && w[u]) ? (int)bins_rm[(long)r[u] * ldr + foff[q]] : 0;
 #pragma unroll
     for (int u = 0; u < NS_U; ++u)
 #pragma unroll
       for (int q = 0; q < NS_FL; ++q) {
-        const int j = lane + 64 * q;
+        const int j = fl + LPR * q;
         if (j < nf && w[u]) atomicAdd(&lh[(j * S + c[u]) * B + bv[u][q]], w[u]);
       }
   }
@@ -1166,17 +1173,25 @@ SRML_API int srml_rf_node_split(const unsigned char* bins_rm, long ldr, const in
   if (!srml_rf_node_split_ok(nf, B, S)) return -6;
   const size_t lds = (size_t)nf * S * B * sizeof(unsigned);
   const float2* w2 = reinterpret_cast<const float2*>(wy);
-#define SRML_RF_NODE_SPLIT(SM)                                                                                     \
+  int lpr = 0;
+  while ((1 << lpr) < nf && lpr < 6) ++lpr;
+#define SRML_RF_NODE_SPLIT_L(SM, MU)                                                                               \
   do {                                                                                                             \
     if (lds > 64 * 1024)                                                                                           \
-      (void)hipFuncSetAttribute((const void*)rf_node_split_kernel<SM>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                                (int)lds);                                                                         \
-    hipLaunchKernelGGL((rf_node_split_kernel<SM>), dim3(nodes), dim3(NS_T), lds, stream, bins_rm, ldr, idx, w2, se,  \
-                       node_feats, nf, B, S, crit, min_leaf, min_gain, out, left);                                 \
+      (void)hipFuncSetAttribute((const void*)rf_node_split_kernel<SM, MU>,                                         \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                             \
+    hipLaunchKernelGGL((rf_node_split_kernel<SM, MU>), dim3(nodes), dim3(NS_T), lds, stream, bins_rm, ldr, idx, w2, \
+                       se, node_feats, nf, B, S, crit, min_leaf, min_gain, out, left, lpr);                        \
+  } while (0)
+#define SRML_RF_NODE_SPLIT(SM)                      \
+  do {                                              \
+    if (lpr < 6) SRML_RF_NODE_SPLIT_L(SM, true);    \
+    else SRML_RF_NODE_SPLIT_L(SM, false);           \
   } while (0)
   if (S <= 2) SRML_RF_NODE_SPLIT(2);
   else if (S <= 4) SRML_RF_NODE_SPLIT(4);
   else SRML_RF_NODE_SPLIT(8);
+#undef SRML_RF_NODE_SPLIT_L
 #undef SRML_RF_NODE_SPLIT
   return srml_status();
 }

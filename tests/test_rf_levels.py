@@ -66,7 +66,8 @@ def test_row_major_bins_match_feature_major_gpu(monkeypatch, regression, gpu_dev
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("S,B,nf,crit,min_leaf", [(2, 128, 55, 0, 1.0), (3, 32, 200, 1, 4.0), (5, 64, 17, 0, 1.0),
-                                                  (2, 256, 40, 1, 1.0)])
+                                                  (2, 256, 40, 1, 1.0), (2, 128, 8, 0, 1.0), (3, 16, 1, 1, 2.0),
+                                                  (2, 64, 96, 0, 1.0)])
 def test_rf_node_split_matches_hist_and_best_split(S, B, nf, crit, min_leaf, gpu_device):
     """The fused small-node split (histogram in LDS + wave-parallel scan) returns exactly the records
     of rf_hist + rf_best_split and the left-child totals of the winning histogram prefix."""
@@ -111,6 +112,8 @@ def _fit_multi(monkeypatch, fused: bool, classes: int, crit: str):
 
     monkeypatch.setattr(forest, "RM_ROWS", 1e12)
     monkeypatch.setattr(forest, "FUSED_ROWS", 1e12 if fused else 0.0)
+    monkeypatch.setattr(forest, "FUSED_MIN_NODES", 1)
+    monkeypatch.setattr(forest, "FUSED_MIN_NF", 1)
     g = np.random.default_rng(6)
     X = g.standard_normal((8000, 40)).astype(np.float32)
     y = (np.digitize(X[:, 0] + 0.5 * X[:, 3] * X[:, 5] + 0.3 * g.standard_normal(8000),
@@ -121,8 +124,12 @@ def _fit_multi(monkeypatch, fused: bool, classes: int, crit: str):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("classes,crit", [(2, "gini"), (4, "entropy")])
-def test_fused_node_split_grows_same_forest_gpu(monkeypatch, classes, crit, gpu_device):
+@pytest.mark.parametrize("classes,crit,max_rows", [(2, "gini", 1 << 20), (4, "entropy", 1 << 20), (3, "gini", 700)])
+def test_fused_node_split_grows_same_forest_gpu(monkeypatch, classes, crit, max_rows, gpu_device):
+    """max_rows 700: nodes above it take the unfused kernels within the same level (merged by node)."""
+    from spark_rapids_ml_nai_amd.models import forest
+
+    monkeypatch.setattr(forest, "FUSED_MAX_ROWS", max_rows)
     a = _fit_multi(monkeypatch, False, classes, crit)
     b = _fit_multi(monkeypatch, True, classes, crit)
     assert a.totalNumNodes == b.totalNumNodes
