@@ -78,7 +78,7 @@ def main() -> None:
     ap.add_argument("--no-quality", action="store_true",
                     help="skip the held-out quality metrics (scored after the timed fits)")
     ap.add_argument("--dump-models", type=str, default=None,
-                    help="rank 0 saves each workload's last fitted model under this directory")
+                    help="saves each workload's last fitted model under this directory (rank 0 writes)")
     args = ap.parse_args()
 
     if args.gpus < 1:
@@ -107,6 +107,11 @@ def main() -> None:
 
         bind_numa_local(device)  # pinned staging buffers on the GPU's own socket
     force_pg = os.environ.get("SRML_COMM_FORCE_PG", "0") == "1"
+    if world > 1:
+        # bound every multi-rank fit: a stuck collective aborts the communicator after this many
+        # seconds and the fit raises CommTimeout (the bench then exits non-zero) instead of holding
+        # the node until the launcher's lease runs out
+        os.environ.setdefault("SRML_COMM_TIMEOUT", "300")
     if world > 1 or force_pg:
         from datetime import timedelta
 
@@ -118,7 +123,11 @@ def main() -> None:
         # SRML_DIST_BACKEND=gloo: multi-rank rehearsal with several ranks sharing one GPU
         # (RCCL refuses two ranks on one device); the default on GPUs is RCCL ("nccl")
         backend = os.environ.get("SRML_DIST_BACKEND", "nccl" if use_gpu else "gloo")
-        dist.init_process_group(backend, timeout=timedelta(minutes=30),
+        from spark_rapids_ml_nai_amd.parallel.comm import comm_timeout
+
+        # per-operation timeout = the fit watchdog's bound: RCCL's own watchdog then tears a stuck
+        # collective down, and gloo (whose abort cannot interrupt a blocked collective) times out
+        dist.init_process_group(backend, timeout=timedelta(seconds=comm_timeout(600) if world > 1 else 600),
                                 **({"device_id": device} if use_gpu and backend == "nccl" else {}))
 
     from spark_rapids_ml_nai_amd import DataFrame
@@ -223,13 +232,20 @@ def main() -> None:
                 Xq, yq = make_shard(wl.data, H, args.cols, device, rank, m_total, seed=HOLDOUT_SEED)
                 results[name]["quality"] = model_quality(name, model, Xq, yq if wl.label else None)
                 del Xq, yq
-            if args.dump_models and rank == 0:
+            if args.dump_models:  # every rank calls save; under SPMD rank 0 alone writes
                 model.write().overwrite().save(os.path.join(args.dump_models, name))
             del df, Xh, yh, model
         except Exception as e:  # noqa: BLE001
             errors[name] = repr(e)[:400]
             if rank == 0:
                 traceback.print_exc(file=sys.stderr)
+            from spark_rapids_ml_nai_amd.parallel.comm import CommError
+
+            if isinstance(e, CommError) or (world > 1 and not dist.is_initialized()):
+                # the communicator was aborted (watchdog / dead peer): no later workload can run
+                print("bench.py: rank %d: communicator failed during %s: %r" % (rank, name, e), file=sys.stderr,
+                      flush=True)
+                sys.exit(3)
         if use_gpu:
             torch.cuda.empty_cache()
 

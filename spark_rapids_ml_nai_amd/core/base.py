@@ -384,7 +384,17 @@ def _fit_worker(ctx: WorkerContext, payload: Tuple[HostPartition, Callable, Dict
     tag = "rank %d/%d" % (ctx.rank, ctx.world_size)
     _worker_log.info("%s: Loading data (%d rows x %d cols) onto %s", tag, hp.rows, hp.n_cols, ctx.device)
     _maybe_inject_fault(ctx, "ingest")
-    if hp.rows == 0:
+    desc = None
+    if ctx.world_size > 1:
+        # the partition descriptor's one all-gather of row counts, BEFORE any numeric collective:
+        # every rank learns which ranks are empty and raises the same error together, instead of
+        # the empty rank raising alone while its peers block in their first all-reduce
+        desc = PartitionDescriptor.build(ctx, hp.rows, hp.n_cols)
+        empty = [r for r, n in desc.parts_rank_size if n == 0]
+        if empty:
+            raise RuntimeError("A worker received no data. Please increase amount of data or use fewer workers. "
+                               "(ranks with no rows: %s of %d)" % (empty, ctx.world_size))
+    elif hp.rows == 0:
         raise RuntimeError("A worker received no data. Please increase amount of data or use fewer workers.")
     dtype = torch.float32 if float32 else torch.float64
     streamed = None
@@ -413,7 +423,8 @@ def _fit_worker(ctx: WorkerContext, payload: Tuple[HostPartition, Callable, Dict
     y = to_device(hp.y, ctx.device) if hp.y is not None else None
     _worker_log.info("%s: Initializing context (partition descriptor, %s communicator)", tag,
                      ctx.comm.backend if hasattr(ctx.comm, "backend") else "local")
-    desc = PartitionDescriptor.build(ctx, hp.rows, hp.n_cols)
+    if desc is None:
+        desc = PartitionDescriptor.build(ctx, hp.rows, hp.n_cols)
     inp = FitInput(X=X, y=y, cols=hp.cols, desc=desc, host=hp, stream=streamed)
     _maybe_inject_fault(ctx, "fit")
     _worker_log.info("%s: Invoking fit (%d global rows)", tag, desc.m)

@@ -14,12 +14,14 @@ import importlib
 import json
 import os
 import shutil
+import threading
 import time
 from typing import Any, Dict, Optional, Type
 
 import numpy as np
 
 SPARK_VERSION_TAG = "3.5.0"  # metadata compatibility tag (no Spark needed)
+_save_state = threading.local()
 
 
 def _jsonable(v: Any) -> Any:
@@ -69,11 +71,52 @@ class MLWriter:
         return self
 
     def save(self, path: str) -> None:
-        if os.path.exists(path):
-            if not self.shouldOverwrite:
-                raise IOError("Path %s already exists. Use write().overwrite().save(path)." % path)
-            shutil.rmtree(path)
-        self.saveImpl(path)
+        """Write the instance to ``path``.
+
+        In an SPMD job (torchrun: every rank holds the same fitted model) only rank 0 writes, the
+        way the reference's Spark driver is the only writer (``core.py:249-336``); the other ranks
+        wait for rank 0's outcome (one object broadcast) and raise the same error if it failed, so
+        a ``load`` on any rank after ``save`` returns sees the complete directory. The directory is
+        written under a temporary sibling name and renamed into place, so a reader never sees a
+        half-written model."""
+        from ..parallel.context import current_context, spmd_active, spmd_context
+
+        if not spmd_active() or getattr(_save_state, "nested", False):
+            # single process, or a sub-model written from inside rank 0's save (CrossValidatorModel's
+            # bestModel): plain local write, no collective
+            self._save_local(path)
+            return
+        ctx = current_context() or spmd_context()
+        err = None
+        if ctx.rank == 0:
+            _save_state.nested = True
+            try:
+                self._save_local(path)
+            except Exception as e:  # noqa: BLE001 - re-raised below, on every rank
+                err = (type(e).__name__, str(e))
+            finally:
+                _save_state.nested = False
+        err = ctx.comm.broadcast_object(err, src=0)
+        if err is not None:
+            kind, msg = err
+            raise (IOError if kind in ("OSError", "IOError", "FileExistsError", "PermissionError")
+                   else RuntimeError)("model save on rank 0 failed: %s: %s" % (kind, msg))
+
+    def _save_local(self, path: str) -> None:
+        path = os.path.abspath(path)
+        if os.path.exists(path) and not self.shouldOverwrite:
+            raise IOError("Path %s already exists. Use write().overwrite().save(path)." % path)
+        parent = os.path.dirname(path)
+        os.makedirs(parent, exist_ok=True)
+        tmp = os.path.join(parent, ".%s.tmp-%d-%d" % (os.path.basename(path), os.getpid(), time.monotonic_ns()))
+        try:
+            self.saveImpl(tmp)
+            if os.path.exists(path):
+                shutil.rmtree(path)
+            os.rename(tmp, path)
+        finally:
+            if os.path.exists(tmp):
+                shutil.rmtree(tmp, ignore_errors=True)
 
     def _metadata(self, extra: Optional[Dict[str, Any]] = None) -> Dict[str, Any]:
         inst = self.instance

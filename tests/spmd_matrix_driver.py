@@ -34,7 +34,9 @@ def global_data() -> dict:
     yr = (Xr @ rng.uniform(-3, 3, D) + 0.5 + 0.1 * rng.standard_normal(N)).astype(np.float64)
     yc = (Xr[:, 0] - 2 * Xr[:, 1] + 0.5 * rng.standard_normal(N) > 0).astype(np.float64)
     ym = np.argmax(Xr[:, :3] + 0.3 * rng.standard_normal((N, 3)), 1).astype(np.float64)
-    return dict(Xb=Xb, Q=Q, Xr=Xr, yr=yr, yc=yc, ym=ym)
+    # sparse copy of Xr: ~70 % of the entries zeroed, so LogisticRegression takes the CSR path
+    Xs = np.where(rng.random((N, D)) < 0.7, 0.0, Xr).astype(np.float32)
+    return dict(Xb=Xb, Q=Q, Xr=Xr, yr=yr, yc=yc, ym=ym, lab=lab.astype(np.float64), Xs=Xs)
 
 
 def main() -> None:
@@ -136,6 +138,49 @@ def main() -> None:
                          seed=5).fit(frame(g["Xr"], g["yr"]))
     out["cv_avg"] = np.asarray(cvm.avgMetrics, np.float64)
     out["cv_best_coef"] = np.asarray(cvm.bestModel.coef_, np.float64).ravel()
+
+    # ---- sparse (CSR) LogisticRegression on VectorUDT rows
+    import scipy.sparse as sps
+
+    sdf = DataFrame.from_numpy(sps.csr_matrix(g["Xs"][lo:hi]), g["yc"][lo:hi], num_partitions=2)
+    ls = LogisticRegression(regParam=0.01, maxIter=50, **nw).fit(sdf)
+    out["logreg_sparse_objective"] = np.array([ls.objective])
+    out["logreg_sparse_coef"] = np.asarray(ls.coef_, np.float64)
+    out["logreg_sparse_pred"] = ls.transform(sdf).to_numpy("prediction")
+    # ---- data-parallel random forest: every rank grows the SAME trees from globally reduced
+    # histograms, so every rank's model predicts the whole dataset identically
+    rdp = RandomForestClassifier(numTrees=6, maxDepth=6, seed=1, split_mode="data_parallel", **nw).fit(
+        frame(g["Xr"], g["yc"]))
+    out["rfdp_pred_all"] = rdp.transform(DataFrame.from_numpy(g["Xr"])).to_numpy("prediction")
+    # ---- supervised UMAP (categorical target intersection)
+    us = UMAP(n_neighbors=10, n_epochs=80, random_state=0, labelCol="label", **nw).setFeaturesCol("features").fit(
+        frame(g["Xb"], g["lab"]))
+    out["umap_sup_transform"] = us.transform(frame(g["Xb"])).to_numpy("embedding")
+    # ---- fp64 inputs (float32_inputs=False): PCA and OLS on the fp64 data
+    Xr64 = g["Xr"].astype(np.float64)
+    p64 = PCA(k=3, inputCol="features", float32_inputs=False, **nw).fit(frame(Xr64))
+    out["pca64_components"] = np.asarray(p64.components_)
+    l64 = LinearRegression(float32_inputs=False, **nw).fit(frame(Xr64, g["yr"]))
+    out["ols64_coef"] = np.asarray(l64.coef_, np.float64).ravel()
+    # ---- save -> load round trips from every rank to ONE shared path per model (rank-0 writes)
+    from spark_rapids_ml_nai_amd.classification import LogisticRegressionModel
+    from spark_rapids_ml_nai_amd.clustering import KMeansModel
+    from spark_rapids_ml_nai_amd.feature import PCAModel
+    from spark_rapids_ml_nai_amd.regression import RandomForestRegressionModel
+
+    mdir = os.path.join(args.out, "models")
+    rt = []
+    for tag, mdl, cls, X, colname in (("pca", pm, PCAModel, g["Xr"], "pca"), ("kmeans", km, KMeansModel, g["Xb"],
+                                                                                "prediction"),
+                                      ("logreg", lg, LogisticRegressionModel, g["Xr"], "prediction"),
+                                      ("rfr", rfr, RandomForestRegressionModel, g["Xr"], "prediction")):
+        p = os.path.join(mdir, tag)
+        mdl.write().overwrite().save(p)
+        back = cls.load(p)
+        a = mdl.transform(frame(X)).to_numpy(colname)
+        b = back.transform(frame(X)).to_numpy(colname)
+        rt.append(float(np.max(np.abs(np.asarray(a, np.float64) - np.asarray(b, np.float64)))))
+    out["roundtrip_maxdiff"] = np.array(rt)
 
     os.makedirs(args.out, exist_ok=True)
     np.savez(os.path.join(args.out, "rank%d.npz" % rank), **out)

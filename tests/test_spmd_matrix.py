@@ -18,6 +18,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DRIVER = os.path.join(ROOT, "tests", "spmd_matrix_driver.py")
 pytestmark = [pytest.mark.dist]
+WORLDS = [2, 4, 8]
 
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 from spmd_matrix_driver import global_data  # noqa: E402
@@ -48,7 +49,7 @@ def runs(tmp_path_factory):
                        text=True, timeout=600, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-4000:]
     res[1] = _load(d, 1)
-    for w in (2, 4):
+    for w in WORLDS:
         d = str(tmp_path_factory.mktemp("w%d" % w))
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % w,
                "--master-addr", "127.0.0.1", "--master-port", str(_port()), DRIVER, "--out", d]
@@ -62,7 +63,6 @@ def _cat(ranks: list, key: str) -> np.ndarray:
     return np.concatenate([r[key] for r in ranks])
 
 
-WORLDS = [2, 4]
 
 
 @pytest.mark.parametrize("w", WORLDS)
@@ -143,7 +143,9 @@ def test_forests_cv_and_umap(runs, w):
     acc = lambda p: (p == g["yc"]).mean()  # noqa: E731
     assert abs(acc(_cat(ranks, "rfc_pred")) - acc(single["rfc_pred"])) < 0.07
     r2 = lambda p: 1 - np.mean((p - g["yr"]) ** 2) / np.var(g["yr"])  # noqa: E731
-    assert abs(r2(_cat(ranks, "rfr_pred")) - r2(single["rfr_pred"])) < 0.09
+    # ensemble mode (reference semantics) grows each rank's trees on its local rows only: at 8 ranks
+    # a tree sees ~150 of the 1200 rows, so the R^2 gap widens beyond the reference's 2-worker gate
+    assert abs(r2(_cat(ranks, "rfr_pred")) - r2(single["rfr_pred"])) < (0.09 if w <= 4 else 0.2)
     # CrossValidator: every rank sees the same metrics and best model; close to the 1-rank run
     for r in ranks:
         np.testing.assert_allclose(r["cv_avg"], ranks[0]["cv_avg"], rtol=1e-9)
@@ -159,3 +161,47 @@ def test_forests_cv_and_umap(runs, w):
     t_w = trustworthiness(g["Xb"], emb, n_neighbors=10)
     t_1 = trustworthiness(g["Xb"], single["umap_transform"], n_neighbors=10)
     assert t_w > t_1 - 0.02, (t_w, t_1)
+
+
+@pytest.mark.parametrize("w", WORLDS)
+def test_sparse_logreg_matches_single(runs, w):
+    single, ranks = runs[1][0], runs[w]
+    o1 = float(single["logreg_sparse_objective"][0])
+    for r in ranks:
+        assert abs(float(r["logreg_sparse_objective"][0]) - o1) <= 1e-5 * abs(o1) + 1e-8
+        np.testing.assert_allclose(r["logreg_sparse_coef"], single["logreg_sparse_coef"], rtol=1e-3, atol=1e-3)
+    assert (_cat(ranks, "logreg_sparse_pred") == single["logreg_sparse_pred"]).mean() > 0.995
+
+
+@pytest.mark.parametrize("w", WORLDS)
+def test_data_parallel_forest_is_one_model(runs, w):
+    g = global_data()
+    single, ranks = runs[1][0], runs[w]
+    for r in ranks[1:]:  # the same trees on every rank
+        np.testing.assert_array_equal(r["rfdp_pred_all"], ranks[0]["rfdp_pred_all"])
+    acc = lambda p: (p == g["yc"]).mean()  # noqa: E731
+    assert abs(acc(ranks[0]["rfdp_pred_all"]) - acc(single["rfdp_pred_all"])) < 0.07
+
+
+@pytest.mark.parametrize("w", WORLDS)
+def test_supervised_umap_and_fp64(runs, w):
+    from sklearn.manifold import trustworthiness
+
+    g = global_data()
+    single, ranks = runs[1][0], runs[w]
+    emb = _cat(ranks, "umap_sup_transform")
+    assert emb.shape == (g["Xb"].shape[0], 2) and np.isfinite(emb).all()
+    t_w = trustworthiness(g["Xb"], emb, n_neighbors=10)
+    t_1 = trustworthiness(g["Xb"], single["umap_sup_transform"], n_neighbors=10)
+    assert t_w > t_1 - 0.03, (t_w, t_1)
+    for r in ranks:
+        np.testing.assert_allclose(np.abs(r["pca64_components"]), np.abs(single["pca64_components"]), atol=1e-6)
+        c1 = single["ols64_coef"]
+        np.testing.assert_allclose(r["ols64_coef"], c1, rtol=1e-7, atol=1e-8 * np.abs(c1).max())
+
+
+@pytest.mark.parametrize("w", WORLDS)
+def test_save_load_round_trip_on_every_rank(runs, w):
+    for r in runs[w]:
+        assert r["roundtrip_maxdiff"].shape == (4,)
+        assert float(r["roundtrip_maxdiff"].max()) <= 1e-6, r["roundtrip_maxdiff"]
