@@ -39,15 +39,20 @@ def low_rank_matrix(m: int, n: int, device: torch.device, seed: int = 0, effecti
     return (U * s) @ V.T
 
 
-def regression(m: int, n: int, device: torch.device, seed: int = 0, n_informative: Optional[int] = None,
-               noise: float = 1.0, bias: float = 0.0, n_targets: int = 1) -> Tuple[torch.Tensor, torch.Tensor]:
-    """N(0, 1) features, ground truth 100 U(0, 1) on ``n_informative`` random columns (shared by
-    every partition), ``y = X w + bias + N(0, noise^2)``; ``n_targets > 1`` gives an (m, T) target
-    (the multinomial-logistic ground truth of ``gen_data_distributed.py:445-455``)."""
+def regression(m: int, n: int, device: torch.device, seed: int = 0, n_informative: int = 10,
+               noise: float = 0.0, bias: float = 0.0, n_targets: int = 1) -> Tuple[torch.Tensor, torch.Tensor]:
+    """sklearn ``make_regression`` semantics with its defaults, as the reference's generators use
+    them (``gen_data.py:339-392`` passes no ``n_informative`` -> 10; ``gen_data_distributed.py:364``
+    defaults it to 10; noise 0 and bias 0 unless the workload's script sets them, e.g. ``--noise 10``
+    for the linear-regression data, ``run_benchmark.sh:251-260``): N(0, 1) features, ground truth
+    100 U(0, 1) on ``n_informative`` random columns (shared by every partition; the random column
+    choice is sklearn's column shuffle), ``y = X w + bias + N(0, noise^2)``. Rows are i.i.d., so
+    sklearn's row shuffle changes nothing. ``n_targets > 1`` gives an (m, T) target (the
+    multinomial-logistic ground truth of ``gen_data_distributed.py:445-455``)."""
     g = _gen(device, seed)
     X = torch.randn(m, n, device=device, generator=g, dtype=torch.float32)
     gw = _gen(device, 777)
-    k = n_informative or max(1, n // 10)
+    k = max(1, min(int(n_informative), n))
     w = torch.zeros(n, n_targets, device=device)
     idx = torch.randperm(n, device=device, generator=gw)[:k]
     w[idx] = 100.0 * torch.rand(k, n_targets, device=device, generator=gw)

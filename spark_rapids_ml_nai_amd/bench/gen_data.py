@@ -48,7 +48,7 @@ def _parser() -> argparse.ArgumentParser:
     p.add_argument("--n_informative", type=int, default=None)
     p.add_argument("--n_redundant", type=int, default=None)
     p.add_argument("--n_classes", type=int, default=2)
-    p.add_argument("--noise", type=float, default=1.0)
+    p.add_argument("--noise", type=float, default=0.0)  # make_regression's default
     p.add_argument("--bias", type=float, default=0.0)
     p.add_argument("--logistic_regression", action="store_true", help="regression: emit 0/1 labels")
     p.add_argument("--effective_rank", type=int, default=10)
@@ -83,7 +83,7 @@ def gen_partition(args: argparse.Namespace, rows: int, seed: int, device: torch.
         return X, y  # CSR (float64, as the reference's sparse VectorUDT) + labels
     elif args.type == "regression":
         multi = args.logistic_regression and args.n_classes > 2
-        X, y = datagen.regression(rows, n, device, seed, n_informative=args.n_informative, noise=args.noise,
+        X, y = datagen.regression(rows, n, device, seed, n_informative=args.n_informative or 10, noise=args.noise,
                                   bias=args.bias, n_targets=args.n_classes if multi else 1)
         if args.logistic_regression:  # Bernoulli / softmax-sampled labels of the unscaled target
             y = datagen.logistic_labels(y, seed)

@@ -83,15 +83,15 @@ def _registry() -> Dict[str, Workload]:
         from ..regression import LinearRegression
 
         reg["linear_regression"] = Workload(
-            "linear_regression", "regression",
+            "linear_regression", "regression_noise10",
             lambda: LinearRegression(regParam=0.0, elasticNetParam=0.0, standardization=False,
                                      featuresCol="features", labelCol="label"), label=True)
         reg["linear_regression_elasticnet"] = Workload(
-            "linear_regression_elasticnet", "regression",
+            "linear_regression_elasticnet", "regression_noise10",
             lambda: LinearRegression(regParam=1e-5, elasticNetParam=0.5, tol=1e-30, maxIter=10, standardization=False,
                                      featuresCol="features", labelCol="label"), label=True)
         reg["linear_regression_ridge"] = Workload(
-            "linear_regression_ridge", "regression",
+            "linear_regression_ridge", "regression_noise10",
             lambda: LinearRegression(regParam=1e-5, elasticNetParam=0.0, tol=1e-30, maxIter=10, standardization=False,
                                      featuresCol="features", labelCol="label"), label=True)
     except ImportError:
@@ -208,8 +208,10 @@ def make_shard(family: str, m_local: int, n: int, device: torch.device, rank: in
     elif family == "uniform":
         X = datagen.uniform(m_local, n, device, seed=seed)
         y = None
-    elif family == "regression":
+    elif family == "regression":  # random forest regressor data: make_regression defaults (noise 0)
         X, y = datagen.regression(m_local, n, device, seed=seed)
+    elif family == "regression_noise10":  # linear-regression data: --noise 10 (run_benchmark.sh:251-260)
+        X, y = datagen.regression(m_local, n, device, seed=seed, noise=10.0)
     elif family == "classification":
         X, y = datagen.classification(m_local, n, device, seed=seed, n_informative=n // 3, n_redundant=n // 3)
     else:

@@ -723,7 +723,10 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
                     out, _ = ops.rf_best_split(hist, B, SH, regression, crit, min_leaf, min_gain)
                     if not regression:
                         res_left.append(_left_totals(hist, out))
-                    prev_hist = hist if keep_hist else None
+                    # (a fused level's big nodes: this histogram covers only them, not the level's
+                    # candidate list that the next level's parent rows index, so nothing is kept and
+                    # the next level histograms every node)
+                    prev_hist = hist if keep_hist and merge is None else None
                     del hist
             if merge is not None:
                 out_f, left_f, big_t, C, feats = merge

@@ -213,3 +213,38 @@ def test_logistic_labels_are_bernoulli_of_the_unscaled_target():
     assert set(np.unique(ym).tolist()) <= {0.0, 1.0, 2.0}
     p = torch.softmax(Y, 1).mean(0).numpy()
     np.testing.assert_allclose(np.bincount(ym.astype(int), minlength=3) / len(ym), p, atol=0.01)
+
+
+def test_regression_family_matches_sklearn_make_regression():
+    """The bench's regression family has sklearn make_regression's semantics at the reference's
+    settings (n_informative 10; noise 10 for the linear-regression data, 0 for the forest data;
+    bias 0): the same coefficient support size and range, the same residual noise variance."""
+    import torch
+    from sklearn.datasets import make_regression
+
+    from spark_rapids_ml_nai_amd.bench import datagen
+    from spark_rapids_ml_nai_amd.bench.suite import make_shard
+
+    m, n = 20000, 300
+    for noise, family in ((10.0, "regression_noise10"), (0.0, "regression")):
+        X, y = make_shard(family, m, n, torch.device("cpu"), 0, m)
+        Xs, ys, cs = make_regression(n_samples=m, n_features=n, noise=noise, coef=True, random_state=0)
+        X64 = X.astype(np.float64)
+        w, *_ = np.linalg.lstsq(X64, y.astype(np.float64), rcond=None)
+        ws, *_ = np.linalg.lstsq(Xs, ys, rcond=None)
+        # support: exactly 10 informative columns, coefficients in (0, 100) like sklearn's 100 U(0, 1)
+        assert int((np.abs(w) > 1.0).sum()) == int((np.abs(ws) > 1.0).sum()) == int(np.count_nonzero(cs)) == 10
+        big = w[np.abs(w) > 1.0]
+        assert big.min() > 0 and big.max() < 100
+        # noise: residual standard deviation equals the requested noise (0 -> fp32 rounding only)
+        res, res_s = np.std(y - X64 @ w), np.std(ys - Xs @ ws)
+        if noise > 0:
+            assert abs(res / noise - 1) < 0.03 and abs(res_s / noise - 1) < 0.03
+        else:
+            assert res < 1e-3 * np.std(y) and res_s < 1e-9
+        assert abs(float(np.mean(y))) < 0.1 * np.std(y)  # bias 0
+    # the generator's defaults are make_regression's
+    _, y0 = datagen.regression(2000, 50, torch.device("cpu"), seed=3)
+    Xd, _ = datagen.regression(2000, 50, torch.device("cpu"), seed=3)
+    w, *_ = np.linalg.lstsq(Xd.double().numpy(), y0.double().numpy(), rcond=None)
+    assert int((np.abs(w) > 1.0).sum()) == 10

@@ -106,7 +106,66 @@ def test_rf_node_split_matches_hist_and_best_split(S, B, nf, crit, min_leaf, gpu
     assert int((out_f[:, 1] >= 0).sum()) > C // 2
 
 
-def _fit_multi(monkeypatch, fused: bool, classes: int, crit: str):
+@pytest.mark.gpu
+@pytest.mark.parametrize("S,B,nf,crit,min_leaf", [(2, 128, 55, 0, 1.0), (3, 32, 200, 1, 4.0), (5, 64, 17, 0, 1.0),
+                                                  (2, 16, 3, 1, 2.0)])
+def test_rf_node_split_matches_cpu_oracle(S, B, nf, crit, min_leaf, gpu_device):
+    """The fused split against a CPU oracle: numpy per-node histograms of the weighted class counts
+    and the torch-CPU gini / entropy scan (``_rf_best_split_ref``). Exact ties may pick another
+    (feature, bin) on the device, so the check is: same validity, the same best gain, the chosen
+    split's gain equal to the maximum, and its left totals equal to the oracle histogram's prefix."""
+    import torch
+
+    from spark_rapids_ml_nai_amd import ops
+
+    rng = np.random.default_rng(S * 31 + nf)
+    m, n, C = 20000, 240, 61
+    rm = rng.integers(0, B, (m, n), dtype=np.uint8)
+    cnt = rng.integers(0, 400, C)
+    cnt[2], cnt[7] = 1, 0
+    starts = np.concatenate([[0], np.cumsum(cnt)[:-1]])
+    P = int(cnt.sum())
+    idx = rng.permutation(m)[:P].astype(np.int32)
+    w = rng.integers(1, 4, P).astype(np.float32)
+    label = rng.integers(0, S, m).astype(np.float32)
+    # informative labels on a few columns so most nodes have a real best split
+    label = np.where(rm[:, 5] < B // 2, label, (label + 1) % S).astype(np.float32)
+    feats = np.stack([np.sort(rng.permutation(n)[:nf]) for _ in range(C)]).astype(np.int32)
+    dev = torch.device(gpu_device)
+    idx_d = torch.from_numpy(idx).to(dev)
+    wy = ops.rf_hist_wy(idx_d, torch.from_numpy(label).to(dev), None, torch.from_numpy(w).to(dev))
+    se = torch.from_numpy(np.stack([starts, starts + cnt], 1).astype(np.int32)).to(dev)
+    out, left = ops.rf_node_split(torch.from_numpy(rm).to(dev), idx_d, wy, se, torch.from_numpy(feats).to(dev),
+                                  B, S, crit, min_leaf, 0.0)
+    out, left = out.cpu().numpy(), left.cpu().numpy()
+    hist = np.zeros((C, nf, B, S), np.float64)
+    for c in range(C):
+        rows = idx[starts[c]: starts[c] + cnt[c]]
+        ww, yy = w[starts[c]: starts[c] + cnt[c]].astype(np.float64), label[rows].astype(np.int64)
+        for j in range(nf):
+            np.add.at(hist[c, j], (rm[rows, feats[c, j]].astype(np.int64), yy), ww)
+    ref, _ = ops._rf_best_split_ref(torch.from_numpy(hist), S, False, crit, min_leaf, 0.0)
+    ref = ref.numpy()
+    np.testing.assert_array_equal(out[:, 1] >= 0, ref[:, 1] >= 0)
+    ok = ref[:, 1] >= 0
+    assert ok.sum() > C // 2
+    np.testing.assert_allclose(out[ok, 0], ref[ok, 0], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(out[:, 5], ref[:, 5], rtol=1e-9, atol=1e-12)  # parent impurity
+    for c in np.nonzero(ok)[0]:
+        f, b = int(out[c, 1]), int(out[c, 2])
+        lt = hist[c, f, : b + 1].sum(0)
+        # the device's choice is a maximiser of the oracle's gain surface: its gain, scored by the
+        # oracle on the 2-bin histogram (left | right) of exactly that split, is the best gain
+        two = np.stack([lt, hist[c, f].sum(0) - lt])[None, None]
+        one, _ = ops._rf_best_split_ref(torch.from_numpy(two), S, False, crit, min_leaf, 0.0)
+        # its record / left totals are the oracle histogram's prefix at that bin
+        np.testing.assert_array_equal(left[c], lt)
+        assert out[c, 3] == lt.sum() and out[c, 4] == hist[c, 0].sum() - lt.sum()
+        np.testing.assert_allclose(one[0, 0], ref[c, 0], rtol=1e-9, atol=1e-12)
+    assert np.all(left[~ok] == 0)
+
+
+def _fit_multi(monkeypatch, fused: bool, classes: int, crit: str, subset: str = "auto"):
     from spark_rapids_ml_nai_amd.classification import RandomForestClassifier
     from spark_rapids_ml_nai_amd.models import forest
 
@@ -119,19 +178,23 @@ def _fit_multi(monkeypatch, fused: bool, classes: int, crit: str):
     y = (np.digitize(X[:, 0] + 0.5 * X[:, 3] * X[:, 5] + 0.3 * g.standard_normal(8000),
                      np.linspace(-1.5, 1.5, classes - 1))).astype(np.float64)
     est = RandomForestClassifier(numTrees=5, maxDepth=8, maxBins=48, seed=11, impurity=crit,
-                                 minInstancesPerNode=2)
+                                 minInstancesPerNode=2, featureSubsetStrategy=subset)
     return est.fit(DataFrame.from_numpy(X, y))
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("classes,crit,max_rows", [(2, "gini", 1 << 20), (4, "entropy", 1 << 20), (3, "gini", 700)])
-def test_fused_node_split_grows_same_forest_gpu(monkeypatch, classes, crit, max_rows, gpu_device):
-    """max_rows 700: nodes above it take the unfused kernels within the same level (merged by node)."""
+@pytest.mark.parametrize("classes,crit,max_rows,subset", [(2, "gini", 1 << 20, "auto"), (4, "entropy", 1 << 20, "auto"),
+                                                           (3, "gini", 700, "auto"), (3, "gini", 700, "all"),
+                                                           (2, "entropy", 300, "all")])
+def test_fused_node_split_grows_same_forest_gpu(monkeypatch, classes, crit, max_rows, subset, gpu_device):
+    """max_rows 700: nodes above it take the unfused kernels within the same level (merged by node).
+    subset "all" (40 features): sibling subtraction is on, so a level that mixes fused and big
+    nodes must not hand its big-node-only histogram to the next level's sibling derivation."""
     from spark_rapids_ml_nai_amd.models import forest
 
     monkeypatch.setattr(forest, "FUSED_MAX_ROWS", max_rows)
-    a = _fit_multi(monkeypatch, False, classes, crit)
-    b = _fit_multi(monkeypatch, True, classes, crit)
+    a = _fit_multi(monkeypatch, False, classes, crit, subset)
+    b = _fit_multi(monkeypatch, True, classes, crit, subset)
     assert a.totalNumNodes == b.totalNumNodes
     Xq = np.random.default_rng(9).standard_normal((700, 40)).astype(np.float32)
     pa = a.transform(DataFrame.from_numpy(Xq))
