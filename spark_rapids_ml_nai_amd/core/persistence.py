@@ -76,9 +76,10 @@ class MLWriter:
         In an SPMD job (torchrun: every rank holds the same fitted model) only rank 0 writes, the
         way the reference's Spark driver is the only writer (``core.py:249-336``); the other ranks
         wait for rank 0's outcome (one object broadcast) and raise the same error if it failed, so
-        a ``load`` on any rank after ``save`` returns sees the complete directory. The directory is
-        written under a temporary sibling name and renamed into place, so a reader never sees a
-        half-written model."""
+        a ``load`` on any rank after ``save`` returns sees the complete directory. A barrier opens
+        the save, so no rank is still reading an earlier model at the path when rank 0 replaces it.
+        The directory is written under a temporary sibling name and renamed into place, so a
+        reader never sees a half-written model."""
         from ..parallel.context import current_context, spmd_active, spmd_context
 
         if not spmd_active() or getattr(_save_state, "nested", False):
@@ -87,6 +88,9 @@ class MLWriter:
             self._save_local(path)
             return
         ctx = current_context() or spmd_context()
+        # the save is a collective: every rank has arrived (so no rank is still reading an earlier
+        # model at this path) before rank 0 replaces the directory
+        ctx.comm.barrier()
         err = None
         if ctx.rank == 0:
             _save_state.nested = True

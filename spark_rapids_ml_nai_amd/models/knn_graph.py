@@ -25,7 +25,17 @@ from .. import ops
 
 BRUTE_MAX_ROWS = 100_000  # build_algo="auto": exact graph up to this many rows, IVF lists beyond
 IVF_LIST_ROWS = 1024      # target rows per inverted list
-IVF_NPROBE = 16           # lists probed per query list
+IVF_NPROBE = 16           # lists probed per query list (probe="list")
+IVF_NPROBE_MAX = 128      # list-probing kernel's probe table (knn_graph.hip F_PMAX)
+# per-query probing (probe="query", the default): every row scans the SRML_IVF_QPROBES lists whose
+# centres are nearest to IT (not to its list's centre), chosen among the SRML_IVF_POOL x probes
+# lists nearest to its list's centre; the device pair kernel keeps <= 32 per row
+IVF_PROBE = os.environ.get("SRML_IVF_PROBE", "query")
+IVF_QPROBES = int(os.environ.get("SRML_IVF_QPROBES", "32"))
+IVF_POOL_MULT = int(os.environ.get("SRML_IVF_POOL", "8"))
+IVF_QPROBES_DEV_MAX = 32
+IVF_SEED_PROBES = int(os.environ.get("SRML_IVF_SEED_PROBES", "8"))  # list probes of the per-query seed pass
+IVF_PAIR_BYTES = int(os.environ.get("SRML_IVF_PAIR_MB", "4096")) << 20  # per-chunk partial-list budget
 # quantiser training: Lloyd iterations and sample rows per list (SRML_IVF_TRAIN_ITERS / _ROWS)
 IVF_TRAIN_ITERS = int(os.environ.get("SRML_IVF_TRAIN_ITERS", "10"))
 IVF_TRAIN_ROWS = int(os.environ.get("SRML_IVF_TRAIN_ROWS", "64"))
@@ -149,8 +159,108 @@ def balanced_tile_range(tile_q0: torch.Tensor, tile_list: torch.Tensor, off: tor
     return lo, int(max(lo, min(cuts[rank + 1], T)))
 
 
+def row_tile_range(tile_q0: torch.Tensor, N: int, rank: int, world: int) -> Tuple[int, int]:
+    """Contiguous tile range of ``rank`` holding ~N / world rows (cuts on tile boundaries): the
+    per-query probing work is about the same per row."""
+    T = int(tile_q0.shape[0])
+    if world <= 1 or T == 0:
+        return 0, T
+    targets = torch.tensor([N * r // world for r in range(world + 1)], dtype=tile_q0.dtype, device=tile_q0.device)
+    cuts = torch.searchsorted(tile_q0, targets).cpu().tolist()
+    cuts[0], cuts[-1] = 0, T
+    return int(cuts[rank]), int(max(cuts[rank], cuts[rank + 1]))
+
+
+def query_probe_search(Xs: torch.Tensor, xn: torch.Tensor, C: torch.Tensor, counts: torch.Tensor,
+                       off: torch.Tensor, tile_q0: torch.Tensor, tile_list: torch.Tensor, tlo: int, thi: int, k: int,
+                       kc: int, p: int, seed_probes: int = IVF_SEED_PROBES, pool_mult: int = IVF_POOL_MULT,
+                       phases: Optional[dict] = None) -> Tuple[torch.Tensor, torch.Tensor, int, int]:
+    """Per-query IVF probing over the query tiles ``tlo .. thi`` (rows r0 .. r1 of the list-sorted
+    ``Xs``): (exact squared distances (r1 - r0, k), sorted positions int64, r0, r1).
+
+    1. seed: list probing with ``seed_probes`` lists (every row of list c scans the lists nearest
+       to c's centre; the dense tile kernel), re-ranked exactly: each row's k-th distance so far;
+    2. pool: each list's ``pool_mult * p`` nearest lists by centre (one small C x C kNN); probes:
+       each row's ``p`` nearest pool centres (``ops.knn_pool_probes``, fp16 MFMA tiles), minus the
+       lists the seed already scanned;
+    3. inverted search: the (row, list) pairs are grouped by list with the counting sort, every
+       128-pair tile of list l is matched against l's items (``ops.knn_pairs``) keeping only items
+       below the row's seeded threshold, then the seed's and the pairs' candidates are merged by
+       the radix select and the ``kc`` best re-ranked exactly.
+    Rows are processed in chunks that bound the partial lists to ``IVF_PAIR_BYTES``."""
+    import time
+
+    N = Xs.shape[0]
+    nlist = C.shape[0]
+    dev = Xs.device
+    T = int(tile_q0.shape[0])
+    r0 = int(tile_q0[tlo]) if tlo < T else N
+    r1 = int(tile_q0[thi]) if thi < T else N
+    if r1 <= r0:
+        e = torch.empty((0, k), device=dev)
+        return e, e.long(), r0, r1
+    t0 = time.perf_counter()
+    nonempty = int((counts > 0).sum())
+    cn = torch.where(counts > 0, ops.row_sqnorm(C), torch.full((nlist,), float("inf"), device=dev))
+    zero = torch.zeros(nlist, device=dev)
+    # 1. seed: list probing, exact re-rank
+    s1 = max(1, min(int(seed_probes), nonempty, IVF_NPROBE_MAX))
+    _, probes1 = ops.knn(C, C, s1, inorm=cn, qnorm=zero)
+    probes1 = torch.where(torch.isfinite(cn[probes1.clamp_min(0)]) & (probes1 >= 0), probes1,
+                          torch.full_like(probes1, -1)).int()
+    od, oi = ops.knn_lists(Xs, xn, off, probes1, tile_q0[tlo:thi], tile_list[tlo:thi], kc, centroids=C)
+    d2s, poss = refine_sorted(Xs[r0:r1], Xs, oi[r0:r1].long())
+    del od, oi
+    # the fp16 keys of the pair search carry ~1e-3 relative rounding: a 1 % slack keeps every item
+    # that can still enter the row's exact top k
+    thr = torch.full((N,), float("inf"), dtype=torch.float32, device=dev)
+    thr[r0:r1] = d2s[:, min(k, d2s.shape[1]) - 1] * 1.01 + 1e-30
+    t0 = record_phase(phases, "query_seed", r1 - r0, t0, dev)
+    # 2. probes
+    cap = IVF_QPROBES_DEV_MAX if ops.knn_lists_f16_ok(Xs, kc, C) else nonempty
+    p = max(1, min(int(p), nonempty, cap))
+    P = max(p, min(nonempty, int(pool_mult) * p))
+    _, pool = ops.knn(C, C, P, inorm=cn, qnorm=zero)
+    probes = ops.knn_pool_probes(Xs, off, C, pool.int(), tile_q0[tlo:thi], tile_list[tlo:thi], p, r0, r1)
+    t0 = record_phase(phases, "query_probes", r1 - r0, t0, dev)
+    # 3. pairs, in row chunks
+    rows_per_chunk = max(128, IVF_PAIR_BYTES // (p * kc * 8))
+    d_parts, p_parts = [], []
+    ta = tlo
+    while ta < thi:
+        ca = int(tile_q0[ta])
+        tb = min(thi, int(torch.searchsorted(tile_q0, torch.tensor([ca + rows_per_chunk], device=dev,
+                                                                       dtype=tile_q0.dtype)).item()))
+        tb = max(tb, ta + 1)
+        cb = int(tile_q0[tb]) if tb < T else N
+        pr = probes[ca - r0: cb - r0].long()
+        rlist = torch.bucketize(torch.arange(ca, cb, device=dev), off[1:], right=True)
+        seen = (probes1[rlist].long().unsqueeze(1) == pr.unsqueeze(2)).any(2)  # scanned by the seed
+        flat = torch.where(seen | (pr < 0), torch.full_like(pr, -1), pr).reshape(-1)
+        del seen, rlist, pr
+        perm, poff, _ = ops.label_sort(flat, nlist)  # pairs grouped by probed list; dropped pairs trail
+        perm = perm[: int(poff[-1])].long()
+        qrows = (ca + perm // p).int()
+        pt_q0, pt_list = ivf_tiles(poff[1:] - poff[:-1], poff)
+        odp, oip = ops.knn_pairs(Xs, off, C, poff, qrows, perm.int(), pt_q0, pt_list, kc, (cb - ca) * p,
+                                 thr_row=thr)
+        del qrows, perm, flat
+        vals = torch.cat([d2s[ca - r0: cb - r0], odp.view(cb - ca, p * kc)], 1)
+        ids = torch.cat([poss[ca - r0: cb - r0], oip.view(cb - ca, p * kc).long()], 1)
+        del odp, oip
+        _, cand = ops.topk_rows(vals, kc, ids=ids)
+        del vals, ids
+        d2, pos = refine_sorted(Xs[ca:cb], Xs, cand)
+        d_parts.append(d2[:, :k])
+        p_parts.append(pos[:, :k])
+        ta = tb
+    record_phase(phases, "query_pairs", r1 - r0, t0, dev)
+    return torch.cat(d_parts), torch.cat(p_parts), r0, r1
+
+
 def knn_graph_ivf(X: torch.Tensor, k: int, nlist: Optional[int] = None, nprobe: Optional[int] = None,
-                  seed: int = 0, ctx: Any = None, list_order: bool = False, phases: Optional[dict] = None) -> Any:
+                  seed: int = 0, ctx: Any = None, list_order: bool = False, phases: Optional[dict] = None,
+                  probe: Optional[str] = None) -> Any:
     """Approximate all-points graph: (euclidean distances [N, k], indices [N, k] int64).
 
     ``list_order=True`` returns ``(dist, idx, order)`` with the graph left in inverted-list order:
@@ -162,7 +272,12 @@ def knn_graph_ivf(X: torch.Tensor, k: int, nlist: Optional[int] = None, nprobe: 
     N = X.shape[0]
     nlist = int(nlist) if nlist else max(1, int(round(N / IVF_LIST_ROWS)))
     nlist = max(1, min(nlist, N))
-    nprobe = max(1, min(int(nprobe) if nprobe else IVF_NPROBE, nlist, ops.KNN_KMAX))
+    probe = (probe or IVF_PROBE).lower()
+    if probe not in ("query", "list"):
+        raise ValueError("probe must be 'query' or 'list', got %r" % probe)
+    if probe == "query":
+        qprobes = int(nprobe) if nprobe else IVF_QPROBES
+    nprobe = max(1, min(int(nprobe) if nprobe else IVF_NPROBE, nlist, IVF_NPROBE_MAX))
     t0 = time.perf_counter()
     C = train_quantizer(X, nlist, seed, ctx=ctx)
     ntrain = min(N, max(nlist * IVF_TRAIN_ROWS, 4 * nlist))
@@ -186,23 +301,30 @@ def knn_graph_ivf(X: torch.Tensor, k: int, nlist: Optional[int] = None, nprobe: 
     counts = off[1:] - off[:-1]
     Xs = X.index_select(0, order).contiguous()
     xn = ops.row_sqnorm(Xs)
-    # probe lists: nearest non-empty lists to each list's centroid (itself first)
-    cn = torch.where(counts > 0, ops.row_sqnorm(C), torch.full((nlist,), float("inf"), device=X.device))
-    _, probes = ops.knn(C, C, nprobe, inorm=cn, qnorm=torch.zeros(nlist, device=X.device))
-    ok = (probes >= 0) & torch.isfinite(cn[probes.clamp_min(0)])
-    probes = torch.where(ok, probes, torch.full_like(probes, -1))
     tile_q0, tile_list = ivf_tiles(counts, off)
     T = int(tile_list.shape[0])
-    lo, hi = balanced_tile_range(tile_q0, tile_list, off, counts, probes, ctx.rank if world > 1 else 0, world)
     # fp16 centred candidates (knn_lists_f16_ok): a few extra neighbours, re-ranked exactly below
     kc = min(32, k + max(2, k // 4)) if ops.knn_lists_f16_ok(Xs, k, C) else k
-    od, oi = ops.knn_lists(Xs, xn, off, probes.int(), tile_q0[lo:hi], tile_list[lo:hi], kc, centroids=C)
-    r0 = int(tile_q0[lo]) if lo < T else N
-    r1 = int(tile_q0[hi]) if hi < T else N
-    d2, pos = refine_sorted(Xs[r0:r1], Xs, oi[r0:r1].long())
-    if kc > k:
-        d2, pos = d2[:, :k].contiguous(), pos[:, :k].contiguous()
-    del od, oi
+    if probe == "query" and X.is_cuda and not ops.knn_lists_f16_ok(Xs, kc, C):
+        probe = "list"  # no device pair kernel for these rows (n > 128 or k > 32): the list kernels
+    if probe == "query":
+        lo, hi = row_tile_range(tile_q0, N, ctx.rank if world > 1 else 0, world)
+        d2, pos, r0, r1 = query_probe_search(Xs, xn, C, counts, off, tile_q0, tile_list, lo, hi, k, kc, qprobes,
+                                             phases=phases)
+    else:
+        # probe lists: nearest non-empty lists to each list's centroid (itself first)
+        cn = torch.where(counts > 0, ops.row_sqnorm(C), torch.full((nlist,), float("inf"), device=X.device))
+        _, probes = ops.knn(C, C, nprobe, inorm=cn, qnorm=torch.zeros(nlist, device=X.device))
+        ok = (probes >= 0) & torch.isfinite(cn[probes.clamp_min(0)])
+        probes = torch.where(ok, probes, torch.full_like(probes, -1))
+        lo, hi = balanced_tile_range(tile_q0, tile_list, off, counts, probes, ctx.rank if world > 1 else 0, world)
+        od, oi = ops.knn_lists(Xs, xn, off, probes.int(), tile_q0[lo:hi], tile_list[lo:hi], kc, centroids=C)
+        r0 = int(tile_q0[lo]) if lo < T else N
+        r1 = int(tile_q0[hi]) if hi < T else N
+        d2, pos = refine_sorted(Xs[r0:r1], Xs, oi[r0:r1].long())
+        if kc > k:
+            d2, pos = d2[:, :k].contiguous(), pos[:, :k].contiguous()
+        del od, oi
     d2 = gather_rows(d2, ctx)
     pos = gather_rows(pos, ctx)
     record_phase(phases, "knn_lists", r1 - r0, t0, X.device)
@@ -241,5 +363,5 @@ def build_knn_graph(X: torch.Tensor, k: int, build_algo: str = "auto", build_kwd
         return (d, i, None) if list_order else (d, i)
     if algo in ("ivf", "ivfflat", "ivf_flat", "nn_descent"):
         return knn_graph_ivf(X, k, nlist=kw.get("nlist"), nprobe=kw.get("nprobe"), seed=seed, ctx=ctx,
-                             list_order=list_order, phases=phases)
+                             list_order=list_order, phases=phases, probe=kw.get("probe"))
     raise ValueError("Unsupported build_algo %r (auto, brute_force_knn, ivf)" % build_algo)

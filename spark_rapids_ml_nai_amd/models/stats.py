@@ -42,12 +42,9 @@ def scatter_stats(X: torch.Tensor, ctx: WorkerContext, m_total: int, stream: Any
     mu0 = None
     m_r = 0
     for r0, r1, Xc in chunks:
-        cs, cq = ops.col_moments(Xc, need_sq=need_sq)
+        ops.col_moments(Xc, need_sq=need_sq, out=(s, q))  # accumulated in place: no per-chunk fill / add
         if mu0 is None:
-            mu0 = cs / max(r1 - r0, 1)
-        s += cs
-        if need_sq:
-            q += cq
+            mu0 = s / max(r1 - r0, 1)  # the first chunk's means
         ops.gram(Xc, mu0, out=G, finalize=False)
         if y is not None:
             ops.xtv(Xc, y[r0:r1].view(-1, 1), out=xty)

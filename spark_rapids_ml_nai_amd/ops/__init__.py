@@ -28,15 +28,30 @@ def _c(t: torch.Tensor) -> torch.Tensor:
 
 
 # ------------------------------------------------------------------------------------------
-def col_moments(X: torch.Tensor, need_sq: bool = True) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
-    """Per-column fp64 (sum, sum of squares) of a row-major (m, n) matrix."""
+def col_moments(X: torch.Tensor, need_sq: bool = True,
+                out: Optional[Tuple[torch.Tensor, Optional[torch.Tensor]]] = None
+                ) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """Per-column fp64 (sum, sum of squares) of a row-major (m, n) matrix. ``out`` = (sum, sumsq)
+    fp64 accumulators to ADD into (the kernel folds with atomics: a streamed pass over row chunks
+    needs no per-chunk zero fill or add)."""
     m, n = X.shape
     if not X.is_cuda:
         Xd = X.double()
+        if out is not None:
+            out[0].add_(Xd.sum(0))
+            if need_sq:
+                out[1].add_((Xd * Xd).sum(0))
+            return out
         return Xd.sum(0), (Xd * Xd).sum(0) if need_sq else None
     X = _c(X)
-    s = torch.zeros(n, dtype=torch.float64, device=X.device)
-    q = torch.zeros(n, dtype=torch.float64, device=X.device) if need_sq else None
+    if out is not None:
+        s, q = out[0], (out[1] if need_sq else None)
+        if s.dtype != torch.float64 or not s.is_contiguous() or (q is not None and (q.dtype != torch.float64
+                                                                                    or not q.is_contiguous())):
+            raise ValueError("col_moments(out=): contiguous fp64 accumulators")
+    else:
+        s = torch.zeros(n, dtype=torch.float64, device=X.device)
+        q = torch.zeros(n, dtype=torch.float64, device=X.device) if need_sq else None
     name = "srml_col_moments_f32" if X.dtype == torch.float32 else "srml_col_moments_f64"
     if X.dtype not in (torch.float32, torch.float64):
         raise TypeError("col_moments supports fp32/fp64")
@@ -242,6 +257,13 @@ def xtv(X: torch.Tensor, V: torch.Tensor, out: Optional[torch.Tensor] = None) ->
             oc = out[:, c0: c0 + kk]
             native.call("srml_xtv_mfma_f32", X.data_ptr(), m, n, X.stride(0), Vc.data_ptr(), kk, Vc.stride(0),
                         oc.data_ptr(), oc.stride(0), oc.stride(1), None, native.stream(X.device))
+        return out
+    if k <= 4 and out.is_contiguous() and out.dtype == torch.float64:
+        # the kernel folds into out with fp64 atomics: accumulate in place (a streamed X^T y over
+        # row chunks then needs no per-chunk temporary, zero fill or add)
+        Vc = _c(V2.to(torch.float32))
+        native.call("srml_xtv_f32", X.data_ptr(), m, n, X.stride(0), Vc.data_ptr(), k, Vc.stride(0), out.data_ptr(),
+                    native.stream(X.device))
         return out
     for c0 in range(0, k, 4):
         kk = min(4, k - c0)
@@ -866,7 +888,8 @@ def lloyd_kernel() -> str:
 def kmeans_lloyd_small(X: torch.Tensor, C: torch.Tensor, cnorm: Optional[torch.Tensor] = None,
                        with_sums: bool = True, out: Optional[torch.Tensor] = None,
                        done: Optional[torch.Tensor] = None, labels: Optional[torch.Tensor] = None,
-                       dist: Optional[torch.Tensor] = None, rows_out: bool = True) -> Tuple[torch.Tensor, ...]:
+                       dist: Optional[torch.Tensor] = None, rows_out: bool = True,
+                       mu: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, ...]:
     """Fused small-k Lloyd step (ONE pass over X): (labels int32, squared distances fp32) and,
     with ``with_sums``, (cluster sums fp64 [k, n], counts int64 [k], inertia fp64 [1]) by those
     labels. ``out`` (fp64 [k n + k + 1], zeroed): the MFMA kernel accumulates [sums | counts |
@@ -874,7 +897,9 @@ def kmeans_lloyd_small(X: torch.Tensor, C: torch.Tensor, cnorm: Optional[torch.T
     inertia are views of it); ``done`` (int32 device flag): the step is a no-op once it is set;
     ``labels`` / ``dist``: preallocated outputs (a loop reuses them). ``rows_out=False`` (MFMA
     kernel, with ``out``): no per-row labels / distances are written (the Lloyd loop needs only
-    the sums, counts and inertia); (None, None, sums, counts, inertia) is returned."""
+    the sums, counts and inertia); (None, None, sums, counts, inertia) is returned. ``mu`` (MFMA
+    kernel): the rows are searched and summed as x - mu against ``C`` / ``cnorm`` given CENTRED
+    (C - mu): the returned sums are of x - mu (labels and distances are unchanged)."""
     m, n = X.shape
     k = C.shape[0]
     dev = X.device
@@ -888,13 +913,17 @@ def kmeans_lloyd_small(X: torch.Tensor, C: torch.Tensor, cnorm: Optional[torch.T
         dist = torch.empty(m, dtype=torch.float32, device=dev) if dist is None else dist
     else:
         labels = dist = None
+    if mu is not None and not mfma:
+        raise ValueError("kmeans_lloyd_small: mu needs the MFMA kernel")
     if mfma:
         if with_sums and out is None:
             out = torch.zeros(k * n + k + 1, dtype=torch.float64, device=dev)
+        muc = _c(mu.to(device=dev, dtype=torch.float32).view(-1)) if mu is not None else None
         native.call("srml_kmeans_lloyd_mfma", X.data_ptr(), m, n, X.stride(0), C.data_ptr(), k, cn.data_ptr(),
                     labels.data_ptr() if rows_out else None, dist.data_ptr() if rows_out else None,
                     out.data_ptr() if with_sums else None,
-                    done.data_ptr() if done is not None else None, native.stream(dev))
+                    done.data_ptr() if done is not None else None, muc.data_ptr() if muc is not None else None,
+                    native.stream(dev))
         if not with_sums:
             return labels, dist
         return labels, dist, out[: k * n].view(k, n), out[k * n: k * n + k].long(), out[k * n + k:]
@@ -1846,6 +1875,99 @@ def knn_lists(X: torch.Tensor, xnorm: torch.Tensor, list_off: torch.Tensor, prob
     native.call("srml_knn_lists_f32", X.data_ptr(), n, X.stride(0), _c(xnorm.float()).data_ptr(),
                 _c(list_off.long()).data_ptr(), _c(probes.int()).data_ptr(), nprobe, _c(tile_q0.long()).data_ptr(),
                 _c(tile_list.int()).data_ptr(), ntiles, int(k), od.data_ptr(), oi.data_ptr(), native.stream(X.device))
+    return od, oi
+
+
+def knn_pool_probes(X: torch.Tensor, list_off: torch.Tensor, C: torch.Tensor, pool: torch.Tensor,
+                    tile_q0: torch.Tensor, tile_list: torch.Tensor, p: int, r0: int, r1: int,
+                    pool_rows: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Per-query IVF probes: the ``p`` lists whose centres are nearest to each row of the given
+    query tiles (rows ``r0 .. r1`` of ``X``, sorted by list), chosen among the ``P`` lists of the
+    row's own list's pool (``pool``: nlist x P list ids nearest to each list's centre, all valid).
+    Returns (r1 - r0, p) int32 list ids, nearest first.
+
+    Device (``knn_lists_f16_ok``): the pool centres are laid out as P-row virtual lists after X's
+    rows (``pool_rows``: a (N + nlist P, n) buffer whose first N rows are X, or None to build one)
+    and the fp16 centred list kernel ranks them, so the rows need no gathered copy. Host: exact
+    fp32 distances."""
+    N, n = X.shape
+    nlist, P = int(pool.shape[0]), int(pool.shape[1])
+    p = min(int(p), P)
+    out = torch.full((r1 - r0, p), -1, dtype=torch.int32, device=X.device)
+    if r1 <= r0 or tile_q0.shape[0] == 0:
+        return out
+    if not knn_lists_f16_ok(X, p, C):
+        lo = list_off.cpu().numpy()
+        for q0, c in zip(tile_q0.cpu().tolist(), tile_list.cpu().tolist()):
+            q1 = min(q0 + 128, int(lo[c + 1]))
+            cand = pool[c].long()
+            d = torch.cdist(X[q0:q1].float(), C[cand].float())
+            j = torch.topk(d, p, dim=1, largest=False).indices
+            out[q0 - r0: q1 - r0] = cand[j].int()
+        return out
+    if pool_rows is None or pool_rows.shape[0] < N + nlist * P:
+        pool_rows = torch.empty((N + nlist * P, n), dtype=torch.float32, device=X.device)
+        pool_rows[:N] = X
+    torch.index_select(C, 0, pool.reshape(-1).long(), out=pool_rows[N: N + nlist * P])
+    off_e = torch.cat([list_off.long(), N + P * torch.arange(1, nlist + 1, device=X.device, dtype=torch.int64)])
+    probes_e = torch.cat([torch.arange(nlist, 2 * nlist, device=X.device, dtype=torch.int32),
+                          torch.full((nlist,), -1, device=X.device, dtype=torch.int32)]).view(-1, 1)
+    # the kernel writes row q of the tiles at q * p: the outputs hold rows r0 .. r1 only, so their
+    # base pointers are shifted back by r0 rows (no row outside r0 .. r1 is written)
+    od = torch.empty((r1 - r0, p), dtype=torch.float32, device=X.device)
+    oi = torch.empty((r1 - r0, p), dtype=torch.int32, device=X.device)
+    native.call("srml_knn_lists_f16c", pool_rows.data_ptr(), n, pool_rows.stride(0), _c(C).data_ptr(),
+                _c(off_e).data_ptr(), _c(probes_e).data_ptr(), 1, _c(tile_q0.long()).data_ptr(),
+                _c(tile_list.int()).data_ptr(), int(tile_q0.shape[0]), p, od.data_ptr() - 4 * r0 * p,
+                oi.data_ptr() - 4 * r0 * p, native.stream(X.device))
+    flat = pool.reshape(-1)
+    pos = oi.long() - N
+    return torch.where(pos >= 0, flat[pos.clamp_min(0)], torch.full_like(pos, -1)).int()
+
+
+def knn_pairs(X: torch.Tensor, list_off: torch.Tensor, C: torch.Tensor, pair_off: torch.Tensor,
+              qrows: torch.Tensor, qslot: torch.Tensor, tile_q0: torch.Tensor, tile_list: torch.Tensor, k: int,
+              nslots: int, thr_row: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Per-query probing, inverted: the (row, probed list) pairs sorted by list (``pair_off``:
+    nlist + 1 offsets; ``qrows``: the X row of each sorted pair; ``qslot``: its output slot);
+    every pair's k nearest items of its list. Returns slot-major (nslots, k) squared distances
+    (device: fp16-rounded ranking keys, comparable across one row's lists; re-rank exactly) and
+    item rows int32, ascending (+inf / -1 padding). ``thr_row`` (N floats, indexed by X row): keep
+    only items whose squared distance is below the row's threshold (its k-th best so far)."""
+    N, n = X.shape
+    nlist = int(list_off.shape[0]) - 1
+    od = torch.full((nslots, k), float("inf"), dtype=torch.float32, device=X.device)
+    oi = torch.full((nslots, k), -1, dtype=torch.int32, device=X.device)
+    ntiles = int(tile_q0.shape[0])
+    if ntiles == 0:
+        return od, oi
+    if not knn_lists_f16_ok(X, k, C):
+        lo = list_off.cpu().numpy()
+        po = pair_off.cpu().numpy()
+        for q0, c in zip(tile_q0.cpu().tolist(), tile_list.cpu().tolist()):
+            q1 = min(q0 + 128, int(po[c + 1]))
+            rows = qrows[q0:q1].long()
+            items = torch.arange(int(lo[c]), int(lo[c + 1]), device=X.device)
+            if items.numel() == 0:
+                continue
+            d = torch.cdist(X[rows].float(), X[items].float()) ** 2
+            if thr_row is not None:
+                d = torch.where(d < thr_row[rows].view(-1, 1), d, torch.full_like(d, float("inf")))
+            kk = min(k, items.numel())
+            v, j = torch.topk(d, kk, dim=1, largest=False)
+            j = torch.where(torch.isfinite(v), j, torch.full_like(j, -1))
+            sl = qslot[q0:q1].long()
+            od[sl, :kk] = v
+            oi[sl, :kk] = torch.where(j >= 0, items[j.clamp_min(0)], torch.full_like(j, -1)).int()
+        return od, oi
+    if C.shape != (nlist, n):
+        raise ValueError("knn_pairs: centroids must be nlist x n")
+    self_probe = torch.arange(nlist, device=X.device, dtype=torch.int32)
+    native.call("srml_knn_pairs_f16c", X.data_ptr(), n, X.stride(0), _c(C).data_ptr(), _c(list_off.long()).data_ptr(),
+                _c(pair_off.long()).data_ptr(), _c(qrows.int()).data_ptr(), _c(qslot.int()).data_ptr(),
+                _c(tile_q0.long()).data_ptr(), _c(tile_list.int()).data_ptr(), ntiles, int(k), od.data_ptr(),
+                oi.data_ptr(), self_probe.data_ptr(), _c(thr_row.float()).data_ptr() if thr_row is not None else None,
+                native.stream(X.device))
     return od, oi
 
 

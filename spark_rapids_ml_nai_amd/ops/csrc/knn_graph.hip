@@ -315,16 +315,42 @@ __device__ __forceinline__ void kg_merge(float (*topd)[F_KQ + 1], int (*topi)[F_
         topd[row0 + q][lane] = d[q];
         topi[row0 + q][lane] = id[q];
       }
-      if (lane == k - 1 && row0 + q < nq) thr_s[row0 + q] = d[q];
+      // (the k-th best only falls; min() also keeps a seeded threshold while fewer than k
+      // candidates have been found)
+      if (lane == k - 1 && row0 + q < nq) thr_s[row0 + q] = fminf(thr_s[row0 + q], d[q]);
       if (lane == 0) cnt[row0 + q] = 0;
     }
   }
 }
 
+// Wave w loads query rows 16w .. 16w + 15 of a tile given by row ids (the PAIRS mode's queries
+// are gathered: rows that probe the tile's list come from anywhere in X)
+__device__ __forceinline__ void kg_load_rows(KgPf& pf, const float* __restrict__ X, long ld,
+                                             const int* __restrict__ rows, long nvalid, int n, int wid, int lane) {
+  const int col = min(4 * (lane & 31), n - 4);
+  const long rmax = nvalid > 0 ? nvalid - 1 : 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const long r = min((long)(16 * wid + 2 * j + (lane >> 5)), rmax);
+    pf.v[j] = *reinterpret_cast<const floatx4*>(X + (long)rows[r] * ld + col);
+  }
+}
+
+// PAIRS = false: a tile is <= 128 consecutive rows of list c = tile_list[b] (its rows X[q0 ..)),
+// scanning the lists probes[c][0 .. nprobe); output row = the query's sorted row.
+// PAIRS = true (per-query probing, inverted): the (row, probed list) pairs are sorted by list; a
+// tile is <= 128 consecutive pairs of list c = tile_list[b] (pair positions q0 .. bounded by
+// pair_off[c + 1]), its queries are the rows qrows[q0 ..], gathered, and it scans list c's own
+// items (probes[c][0] = c, nprobe = 1). Both operands are centred on C_c, and ||q - C_c||^2 of the
+// rounded query is added to the keys, so keys of one row from different lists compare (they are
+// the fp16-rounded ||q - i||^2); output row = qslot[pair position] (the caller's per-pair slot).
+template <bool PAIRS>
 __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
     const float* __restrict__ X, int n, long ld, const float* __restrict__ C, const long long* __restrict__ list_off,
     const int* __restrict__ probes, int nprobe, const long long* __restrict__ tile_q0,
-    const int* __restrict__ tile_list, int ntiles, int k, float* __restrict__ out_d, int* __restrict__ out_i) {
+    const int* __restrict__ tile_list, int ntiles, int k, float* __restrict__ out_d, int* __restrict__ out_i,
+    const int* __restrict__ qrows = nullptr, const int* __restrict__ qslot = nullptr,
+    const long long* __restrict__ pair_off = nullptr, const float* __restrict__ thr_row = nullptr) {
   __shared__ __attribute__((aligned(16))) _Float16 Qs[F_BM * F_RS];
   __shared__ __attribute__((aligned(16))) _Float16 Is[F_BN * F_RS];
   __shared__ float cand_d[F_BM][F_CAP + 1];
@@ -339,11 +365,12 @@ __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
   if (b >= ntiles) return;  // block-uniform
   const int c = tile_list[b];
   const long q0 = tile_q0[b];
-  const long q1 = min(q0 + (long)F_BM, (long)list_off[c + 1]);
+  const long q1 = min(q0 + (long)F_BM, (long)(PAIRS ? pair_off : list_off)[c + 1]);
   const int nq = (int)(q1 - q0);
   const int t = threadIdx.x;
   const int lane = t & 63, wid = t >> 6;
   const int wm = wid >> 2, wn = wid & 3;  // wave tile: rows 64 wm .. +64, columns 32 wn .. +32
+  __shared__ float qn_s[F_BM];  // PAIRS: ||q - C_c||^2 of the rounded queries
   const int li = lane & 31, lk = lane >> 5;
   const float inf = __builtin_huge_valf();
   for (int i = t; i < F_BM * (F_KQ + 1); i += 512) {
@@ -388,7 +415,8 @@ __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
   if (have) kg_load(pfa, X, ld, c0, e - c0, n, wid, lane);
   {
     KgPf pq;
-    kg_load(pq, X, ld, q0, nq, n, wid, lane);
+    if (PAIRS) kg_load_rows(pq, X, ld, qrows + q0, nq, n, wid, lane);
+    else kg_load(pq, X, ld, q0, nq, n, wid, lane);
     kg_store(pq, Qs, cen, wid, lane, nq, n);
   }
   if (have) kg_store(pfa, Is, cen, wid, lane, te - tc0, n);
@@ -396,6 +424,22 @@ __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
   long h1c0 = c0, h1e = e;
   if (have1) kg_load(pfa, X, ld, c0, e - c0, n, wid, lane);
   __syncthreads();
+  if (PAIRS) {
+    // ||q - C_c||^2 of the staged (rounded, centred) queries; padding columns are zero. A seeded
+    // row threshold (thr_row: its k-th best squared distance so far, from lists it already
+    // scanned) becomes the key threshold thr - ||q - C_c||^2: only items that can enter the row's
+    // top k are appended, so the candidate lists rarely fill and the merges all but vanish
+    if (t < nq) {
+      float a = 0.f;
+      for (int j = 0; j < F_KP; j += 2) {
+        const kg_half2 h = *reinterpret_cast<const kg_half2*>(Qs + t * F_RS + j);
+        a = __builtin_amdgcn_fdot2(h, h, a, false);
+      }
+      qn_s[t] = a;
+      if (thr_row) thr_s[t] = thr_row[qrows[q0 + t]] - a;
+    }
+    __syncthreads();
+  }
   const int nks = (n + 15) >> 4;
   int par = 0;
   while (have) {
@@ -497,9 +541,10 @@ __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
   kg_merge(topd, topi, cand_d, cand_i, cnt, thr_s, k, nq, wid, lane, 1);  // the last candidates
   __syncthreads();
   if (t < nq) {
-    const long base = (q0 + t) * (long)k;
+    const long base = (PAIRS ? (long)qslot[q0 + t] : q0 + t) * (long)k;
+    const float add = PAIRS ? qn_s[t] : 0.f;
     for (int j = 0; j < k; ++j) {
-      out_d[base + j] = topd[t][j];
+      out_d[base + j] = topd[t][j] + add;
       out_i[base + j] = topi[t][j];
     }
   }
@@ -517,8 +562,29 @@ SRML_API int srml_knn_lists_f16c(const float* X, int n, long ld, const float* C,
   if (k < 1 || k > F_KQ || n < 1 || n > F_KP || (n & 3) || (ld & 3) || nprobe < 1 || nprobe > F_PMAX ||
       (reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(C) & 15))
     return -8;
-  hipLaunchKernelGGL(knn_lists_f16_kernel, dim3((unsigned)ntiles), dim3(512), 0, stream, X, n, ld, C, list_off, probes,
-                     nprobe, tile_q0, tile_list, ntiles, k, out_d, out_i);
+  hipLaunchKernelGGL(knn_lists_f16_kernel<false>, dim3((unsigned)ntiles), dim3(512), 0, stream, X, n, ld, C, list_off,
+                     probes, nprobe, tile_q0, tile_list, ntiles, k, out_d, out_i, nullptr, nullptr, nullptr);
+  return srml_status();
+}
+
+// Per-query probing (PAIRS mode of the kernel above): (row, probed list) pairs sorted by list,
+// qrows[i] = the sorted X row of pair position i, qslot[i] = its output slot, pair_off = nlist + 1
+// pair offsets per list; tiles (tile_q0 = first pair position, tile_list = list) of <= 128 pairs.
+// out_d / out_i: slot-major (nslots x k): the fp16-rounded ||q - i||^2 (centred on the probed
+// list's centre, comparable across one row's lists) and the sorted item positions, ascending.
+// thr_row (nullable, indexed by X row): only items with a key below the row's threshold are kept
+// (a slot may then hold fewer than k: +inf / -1 padding).
+SRML_API int srml_knn_pairs_f16c(const float* X, int n, long ld, const float* C, const long long* list_off,
+                                 const long long* pair_off, const int* qrows, const int* qslot,
+                                 const long long* tile_q0, const int* tile_list, int ntiles, int k, float* out_d,
+                                 int* out_i, const int* self_probe, const float* thr_row, hipStream_t stream) {
+  if (ntiles <= 0) return 0;
+  if (k < 1 || k > F_KQ || n < 1 || n > F_KP || (n & 3) || (ld & 3) || !qrows || !qslot || !pair_off ||
+      !self_probe || (reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(C) & 15))
+    return -8;
+  // self_probe: nlist ints, self_probe[c] = c (list c scans its own items)
+  hipLaunchKernelGGL(knn_lists_f16_kernel<true>, dim3((unsigned)ntiles), dim3(512), 0, stream, X, n, ld, C, list_off,
+                     self_probe, 1, tile_q0, tile_list, ntiles, k, out_d, out_i, qrows, qslot, pair_off, thr_row);
   return srml_status();
 }
 

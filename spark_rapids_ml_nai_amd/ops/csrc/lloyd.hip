@@ -89,7 +89,8 @@ __global__ __launch_bounds__(LL_T, 2) void lloyd_mfma_kernel(const float* __rest
                                                              const float* __restrict__ C, int k,
                                                              const float* __restrict__ cnorm,
                                                              int* __restrict__ labels, float* __restrict__ dist,
-                                                             double* __restrict__ out, const int* __restrict__ done) {
+                                                             double* __restrict__ out, const int* __restrict__ done,
+                                                             const float* __restrict__ mu) {
   using S = LloydSmem<NV>;
   constexpr int KS = S::KS, NQ = S::NQ;
   __shared__ S sm;
@@ -127,6 +128,12 @@ __global__ __launch_bounds__(LL_T, 2) void lloyd_mfma_kernel(const float* __rest
   floatx4* tw = sm.tile[wid];
   int* slab = sm.lab[wid];
   floatx4 pre[NV];
+  // mu (nullable): every staged row is x - mu (C and cnorm are then the centred centres): the
+  // sums accumulate in fp32 per wave over ~50k rows, so data far from the origin would lose
+  // centre precision to the fp32 accumulator; centred rows keep the sums at the data's spread.
+  // A lane always stages the same 4 columns (f % NV = lane % NV: NV divides 64).
+  floatx4 mu4 = floatx4{0.f, 0.f, 0.f, 0.f};
+  if (mu && 4 * (lane % NV) < n) mu4 = *reinterpret_cast<const floatx4*>(mu + 4 * (lane % NV));
   auto fetch = [&](long g) {
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
@@ -143,7 +150,7 @@ __global__ __launch_bounds__(LL_T, 2) void lloyd_mfma_kernel(const float* __rest
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int f = lane + 64 * i, rr = f / NV, comp = f % NV;
-      tw[slot<NV>(rr, comp)] = pre[i];
+      tw[slot<NV>(rr, comp)] = pre[i] - mu4;  // (padding rows: -mu, never labelled or summed)
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -317,16 +324,19 @@ __global__ __launch_bounds__(256) void kmeans_small_update_kernel(const double* 
 
 }  // namespace
 
-// Small-k Lloyd step on the bf16 matrix cores (see above). out == nullptr: search only (labels /
-// squared distances). Otherwise out = [k x n sums | k counts | inertia] (fp64, zeroed by the
-// caller) accumulates this launch; labels / dist may then be nullptr (not written: the Lloyd loop
-// needs neither). done (nullable): a device flag; non-zero = return at once.
+// Small-k Lloyd step on the bf16 matrix cores (see above). mu (nullable, n floats, 16-B aligned):
+// search / sum the rows x - mu against centres C given already centred (C - mu, their norms); the
+// sums are then of x - mu. out == nullptr: search only (labels / squared distances). Otherwise
+// out = [k x n sums | k counts | inertia] (fp64, zeroed by the caller) accumulates this launch;
+// labels / dist may then be nullptr (not written: the Lloyd loop needs neither). done (nullable):
+// a device flag; non-zero = return at once.
 // Needs k <= 32, n <= 64, n % 4 == 0, ld % 4 == 0, 16-B aligned X.
 SRML_API int srml_kmeans_lloyd_mfma(const float* X, long m, int n, long ld, const float* C, int k,
                                     const float* cnorm, int* labels, float* dist, double* out, const int* done,
-                                    hipStream_t stream) {
+                                    const float* mu, hipStream_t stream) {
   if (m <= 0) return 0;
-  if (k < 1 || k > LL_KP || n < 1 || n > 64 || (n & 3) || (ld & 3) || (reinterpret_cast<uintptr_t>(X) & 15))
+  if (k < 1 || k > LL_KP || n < 1 || n > 64 || (n & 3) || (ld & 3) || (reinterpret_cast<uintptr_t>(X) & 15) ||
+      (reinterpret_cast<uintptr_t>(mu) & 15))
     return (int)hipErrorInvalidValue;
   static int cus = 0;
   if (!cus) {
@@ -340,7 +350,7 @@ SRML_API int srml_kmeans_lloyd_mfma(const float* X, long m, int n, long ld, cons
   const unsigned grid = (unsigned)(want < 2L * cus ? want : 2L * cus);
 #define SRML_LL(NV)                                                                                                   \
   hipLaunchKernelGGL((lloyd_mfma_kernel<NV>), dim3(grid), dim3(LL_T), 0, stream, X, m, n, ld, C, k, cnorm, labels, \
-                     dist, out, done)
+                     dist, out, done, mu)
   if (n <= 16) SRML_LL(4);
   else if (n <= 32) SRML_LL(8);
   else SRML_LL(16);

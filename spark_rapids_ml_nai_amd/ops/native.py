@@ -75,7 +75,7 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_qn_step_fused": (_P, _P, _P, _I, _L, _P),
     "srml_qn_step_mbf": (_P, _P, _P, _I, _L, _P),
     "srml_kmeans_lloyd_small": (_P, _L, _I, _L, _P, _I, _P, _P, _P, _P, _P, _P, _P),
-    "srml_kmeans_lloyd_mfma": (_P, _L, _I, _L, _P, _I, _P, _P, _P, _P, _P, _P),
+    "srml_kmeans_lloyd_mfma": (_P, _L, _I, _L, _P, _I, _P, _P, _P, _P, _P, _P, _P),
     "srml_kmeans_small_update": (_P, _I, _I, _P, _P, _P, _D, _P, _P, _P),
     "srml_qn_fused_scratch": (),
     "srml_qn_fused_barrier_offset": (),
@@ -123,6 +123,7 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_ivf_search_f32": (_P, _L, _I, _L, _P, _I, _P, _P, _L, _P, _P, _I, _P, _P, _P),
     "srml_knn_lists_f32": (_P, _I, _L, _P, _P, _P, _I, _P, _P, _I, _I, _P, _P, _P),
     "srml_knn_lists_f16c": (_P, _I, _L, _P, _P, _P, _I, _P, _P, _I, _I, _P, _P, _P),
+    "srml_knn_pairs_f16c": (_P, _I, _L, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P),
     "srml_dbscan_degree_f32": (_P, _L, _I, _L, _P, _F, _L, _L, _P, _P),
     "srml_dbscan_link_f32": (_P, _L, _I, _L, _P, _F, _L, _L, _P, _P, _P, _P),
     "srml_uf_unite_pairs": (_P, _L, _P, _P),

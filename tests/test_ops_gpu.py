@@ -1350,6 +1350,31 @@ def test_kmeans_lloyd_step_without_row_outputs(gpu_device, m, n, k):
     torch.testing.assert_close(buf_c, buf_e, rtol=1e-9, atol=1e-6)
 
 
+def test_kmeans_lloyd_loop_far_from_origin(gpu_device):
+    """Data offset 1e3 from the origin (spread ~1): one device Lloyd step's centres equal the fp64
+    cluster means of the same labels to the data's spread precision. The MFMA kernel stages x - mu
+    (mu = the start centres' mean), so its per-wave fp32 sums never carry the 1e3 offset."""
+    from spark_rapids_ml_nai_amd.models.kmeans import _lloyd_small_loop
+    from spark_rapids_ml_nai_amd.parallel.context import WorkerContext
+
+    m, n, k = 400000, 64, 20
+    g = torch.Generator().manual_seed(11)
+    base = torch.randn(k, n, generator=g, dtype=torch.float64) * 3
+    X = (1e3 + base[torch.randint(0, k, (m,), generator=g)] + torch.randn(m, n, generator=g, dtype=torch.float64))
+    Xf = X.float()
+    C0 = Xf[torch.randperm(m, generator=g)[:k]].double()
+    ctx = WorkerContext.single(torch.device(gpu_device))
+    C, it, _ = _lloyd_small_loop(Xf.to(gpu_device), C0.to(gpu_device), ctx, k, 1, 0.0)
+    lab = ops.kmeans_lloyd_small(Xf.to(gpu_device), C0.float().to(gpu_device), with_sums=False)[0].long().cpu()
+    Xd = Xf.double()
+    cnt = torch.bincount(lab, minlength=k).double()
+    S = torch.zeros(k, n, dtype=torch.float64).index_add_(0, lab, Xd)
+    ref = torch.where(cnt.view(-1, 1) > 0, S / cnt.clamp_min(1).view(-1, 1), C0)
+    assert it == 1
+    # fp32 sums of the raw rows would be off by ~1e3 * 2^-24 * sqrt(rows per wave) ~ 1e-2
+    assert float((C.cpu() - ref).abs().max()) < 2e-4
+
+
 def test_dbscan_labels_match_unique_oracle(gpu_device):
     """Native label compaction (root-flag prefix scan) == the unique/searchsorted numbering."""
     g = torch.Generator().manual_seed(9)
@@ -1374,3 +1399,104 @@ def test_dbscan_labels_match_unique_oracle(gpu_device):
     m = lab_root >= 0
     ref[m] = torch.searchsorted(roots, lab_root[m])
     assert torch.equal(got, ref)
+
+
+def _ivf_fixture(gpu_device, N, n, nlist, seed):
+    X = _rand(N, n, gpu_device, seed=seed) * 3.0 + 5.0
+    g = torch.Generator().manual_seed(N + n + seed)
+    lab = torch.randint(0, nlist, (N,), generator=g).to(gpu_device)
+    order = torch.argsort(lab, stable=True)
+    counts = torch.bincount(lab, minlength=nlist)
+    off = torch.zeros(nlist + 1, dtype=torch.int64, device=gpu_device)
+    off[1:] = torch.cumsum(counts, 0)
+    Xs = X[order].contiguous()
+    C = torch.zeros(nlist, n, device=gpu_device).index_add_(0, lab[order], Xs) / counts.clamp_min(1).view(-1, 1)
+    return Xs, C, counts, off, g
+
+
+@pytest.mark.parametrize("N,n,nlist,p,k,seeded", [(3000, 16, 12, 4, 15, False), (6000, 128, 20, 6, 19, False),
+                                                  (2500, 64, 7, 7, 32, False), (900, 4, 40, 3, 1, False),
+                                                  (6000, 128, 20, 6, 19, True), (3000, 16, 12, 4, 15, True)])
+def test_knn_pairs_per_query_probing(gpu_device, N, n, nlist, p, k, seeded):
+    """Per-query probing, inverted (the PAIRS mode of the fp16 list kernel): every (row, list) pair
+    gets the k nearest items of that list — the same sets as the fp32 torch path up to fp16
+    near-ties, keys within fp16 rounding of the true squared distances, written at the pair's
+    slot — with the queries gathered from anywhere in X."""
+    from spark_rapids_ml_nai_amd.models.knn_graph import ivf_tiles
+
+    Xs, C, counts, off, g = _ivf_fixture(gpu_device, N, n, nlist, 41)
+    probes = torch.stack([torch.randperm(nlist, generator=g)[:p] for _ in range(N)]).int().to(gpu_device)
+    flat = probes.reshape(-1)
+    perm, poff, _ = ops.label_sort(flat, nlist)
+    perm = perm.long()
+    qrows = (perm // p).int()
+    tq, tl = ivf_tiles(poff[1:] - poff[:-1], poff)
+    assert ops.knn_lists_f16_ok(Xs, k, C)
+    thr = None
+    if seeded:  # a per-row threshold: a low quantile of the squared distances to a row sample
+        smp = Xs[torch.randperm(N, generator=g)[:256].to(gpu_device)]
+        thr = torch.quantile(torch.cdist(Xs, smp).pow(2), 0.02, dim=1).contiguous()
+    d, i = ops.knn_pairs(Xs, off, C, poff, qrows, perm.int(), tq, tl, k, N * p, thr_row=thr)
+    dc, ic = ops.knn_pairs(Xs.cpu(), off.cpu(), C.cpu(), poff.cpu(), qrows.cpu(), perm.int().cpu(), tq.cpu(), tl.cpu(),
+                           k, N * p, thr_row=thr.cpu() if seeded else None)
+    d, i = d.cpu(), i.cpu()
+    # slot s = row * p + j holds items of list probes[row, j] only
+    offc = off.cpu()
+    lists_of = torch.bucketize(i.clamp_min(0).long(), offc[1:], right=True)
+    want = probes.cpu().reshape(-1).long().view(-1, 1)
+    assert bool(((lists_of == want) | (i < 0)).all())
+    if seeded:  # fp16 keys near the threshold may land on either side of it
+        assert abs(int((i >= 0).sum()) - int((ic >= 0).sum())) <= 0.01 * int((ic >= 0).sum()) + 10
+        assert int((ic >= 0).sum()) < 0.9 * ic.numel()  # the threshold did cut
+    else:
+        assert torch.equal(i < 0, ic < 0)
+    hit = (i.unsqueeze(2) == ic.unsqueeze(1)).any(2) & (i >= 0)
+    assert hit.sum().item() / max(1, (ic >= 0).sum().item()) > 0.97
+    # keys = fp16-rounded ||q - i||^2 of the slot's row and item
+    row = torch.arange(N).repeat_interleave(p)
+    ok = i >= 0
+    true = ((Xs.cpu()[row].unsqueeze(1) - Xs.cpu()[i.clamp_min(0).long()]) ** 2).sum(-1)
+    scale = true.max()
+    err = torch.where(ok, (d - true).abs(), torch.zeros_like(d))
+    assert float(err.max()) <= 2e-3 * float(scale) + 1e-3
+
+
+@pytest.mark.parametrize("N,n,nlist,p,P", [(5000, 32, 40, 8, 24), (3000, 128, 25, 4, 25), (1200, 8, 64, 16, 32)])
+def test_knn_pool_probes_match_cpu(gpu_device, N, n, nlist, p, P):
+    """Each row's p nearest list centres among its list's pool (fp16 centred MFMA ranking of the
+    pool laid out as virtual lists) equal the exact fp32 choice up to near-ties."""
+    from spark_rapids_ml_nai_amd.models.knn_graph import ivf_tiles
+
+    Xs, C, counts, off, g = _ivf_fixture(gpu_device, N, n, nlist, 43)
+    cn = ops.row_sqnorm(C)
+    _, pool = ops.knn(C, C, P, inorm=cn, qnorm=torch.zeros(nlist, device=gpu_device))
+    tq, tl = ivf_tiles(counts, off)
+    got = ops.knn_pool_probes(Xs, off, C, pool.int(), tq, tl, p, 0, N).cpu()
+    ref = ops.knn_pool_probes(Xs.cpu(), off.cpu(), C.cpu(), pool.int().cpu(), tq.cpu(), tl.cpu(), p, 0, N)
+    assert got.shape == ref.shape == (N, p) and bool((got >= 0).all())
+    # members of the row's own list's pool, distinct
+    row_list = torch.repeat_interleave(torch.arange(nlist), counts.cpu())
+    assert bool((got.unsqueeze(2) == pool.cpu()[row_list].unsqueeze(1)).any(2).all())
+    srt = torch.sort(got, 1).values
+    assert not bool((srt[:, 1:] == srt[:, :-1]).any())
+    overlap = (got.unsqueeze(2) == ref.unsqueeze(1)).any(2).float().mean().item()
+    assert overlap > 0.97, overlap
+    assert (got[:, 0] == ref[:, 0]).float().mean().item() > 0.97  # nearest centre first
+
+
+def test_knn_graph_query_probing_recall(gpu_device):
+    """End to end at a scale where list probing falls short: per-query probing (the default) beats
+    probing by the list's centre at the same probe count, and reaches >= 0.95 recall."""
+    from spark_rapids_ml_nai_amd.bench import datagen
+    from spark_rapids_ml_nai_amd.models import knn_graph as KG
+
+    X, _ = datagen.classification(120000, 64, gpu_device, seed=5, n_informative=21, n_redundant=21)
+    X = X.contiguous()
+    q = torch.randperm(X.shape[0], generator=torch.Generator().manual_seed(0))[:3000].to(gpu_device)
+    de, ie = KG.knn_graph(X[q], X, 15)
+    rec = {}
+    for probe in ("list", "query"):
+        dist, idx = KG.knn_graph_ivf(X, 15, nprobe=16, seed=1, probe=probe)
+        assert torch.isfinite(dist).all() and bool((dist[:, 1:] >= dist[:, :-1]).all())
+        rec[probe] = (idx[q].unsqueeze(2) == ie.unsqueeze(1)).any(2).float().mean().item()
+    assert rec["query"] > rec["list"] + 0.05 and rec["query"] >= 0.95, rec

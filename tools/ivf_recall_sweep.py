@@ -22,6 +22,8 @@ def main() -> None:
     ap.add_argument("--queries", type=int, default=2000)
     ap.add_argument("--k", type=int, default=15)
     ap.add_argument("--cols", type=int, default=128)
+    ap.add_argument("--probe", default="list,query", help="list: probe the list centre's nearest lists; "
+                    "query: each row's own nearest lists (per-query probing)")
     a = ap.parse_args()
     from spark_rapids_ml_nai_amd.bench import datagen
     from spark_rapids_ml_nai_amd.models.knn_graph import knn_graph, knn_graph_ivf
@@ -41,10 +43,11 @@ def main() -> None:
             q = torch.randperm(N, device=dev, generator=g)[: a.queries]
             _, ei = knn_graph(X.index_select(0, q), X, a.k + 1)
             ei = ei.cpu()
-            for npb in [int(x) for x in a.nprobe.split(",")]:
+            for probe, npb in [(pm, int(x)) for pm in a.probe.split(",") for x in a.nprobe.split(",")]:
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
-                _, gi = knn_graph_ivf(X, a.k, nprobe=npb, seed=1)
+                phases = {}
+                _, gi = knn_graph_ivf(X, a.k, nprobe=npb, seed=1, probe=probe, phases=phases)
                 torch.cuda.synchronize()
                 dt = time.perf_counter() - t0
                 gq = gi.index_select(0, q).cpu()
@@ -53,8 +56,11 @@ def main() -> None:
                     # the exact list includes the row itself (distance 0): compare the k nearest,
                     # self included, as the IVF graph also returns the row itself first
                     hit += len(set(gq[r].tolist()) & set(ei[r, : a.k].tolist())) / float(a.k)
-                print(json.dumps({"family": fam, "rows": N, "cols": n, "nprobe": npb, "k": a.k,
-                                  "recall": round(hit / q.shape[0], 4), "graph_s": round(dt, 3)}), flush=True)
+                print(json.dumps({"family": fam, "rows": N, "cols": n, "probe": probe, "nprobe": npb, "k": a.k,
+                                  "recall": round(hit / q.shape[0], 4), "graph_s": round(dt, 3),
+                                  "phases": {k: v["s"] for k, v in phases.items()}}), flush=True)
+                del gi
+                torch.cuda.empty_cache()
             del X
             torch.cuda.empty_cache()
 

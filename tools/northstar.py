@@ -170,19 +170,23 @@ def _umap_quality(model, Xh, device, sample: int = 20_000, small_fit: bool = Tru
             "trustworthiness_small_fit": round(t_small, 5), "trust_gap": round(t_small - t_big, 5)}
 
 
-def _ivf_recall(Xh, device, sample: int = 100_000, k: int = 15) -> dict:
-    """Recall of the IVF all-points graph (the UMAP fit's builder, default list size / nprobe)
-    against the exact kNN on a row sample of the fitted data."""
-    from spark_rapids_ml_nai_amd.models.knn_graph import knn_graph, knn_graph_ivf
+def _ivf_recall(Xh, device, sample: int = 2000, k: int = 15) -> dict:
+    """Recall@15 of the all-points IVF graph the UMAP fit builds (same builder and defaults), over
+    ALL fitted rows: a query sample's graph rows against their exact neighbours among all N rows."""
+    from spark_rapids_ml_nai_amd.models.knn_graph import IVF_PROBE, IVF_QPROBES, knn_graph, knn_graph_ivf
 
-    n = Xh.shape[0]
-    idx = np.sort(np.random.default_rng(1).choice(n, size=min(sample, n), replace=False))
-    Xs = torch.from_numpy(np.ascontiguousarray(Xh[idx])).to(device).float()
-    _, gi = knn_graph_ivf(Xs, k, seed=1)
-    _, ei = knn_graph(Xs, Xs, k)
-    gi, ei = gi.cpu().numpy(), ei.cpu().numpy()
+    X = torch.from_numpy(Xh).to(device).float()
+    n = X.shape[0]
+    q = torch.from_numpy(np.sort(np.random.default_rng(1).choice(n, size=min(sample, n), replace=False))).to(device)
+    _, gi = knn_graph_ivf(X, k, seed=1)
+    gi = gi.index_select(0, q).cpu().numpy()
+    _, ei = knn_graph(X.index_select(0, q), X, k)
+    ei = ei.cpu().numpy()
+    del X
+    torch.cuda.empty_cache()
     hit = np.mean([len(set(a.tolist()) & set(b.tolist())) / float(k) for a, b in zip(gi, ei)])
-    return {"ivf_recall_sample": int(idx.size), "ivf_recall_at_15": round(float(hit), 5)}
+    return {"ivf_recall_queries": int(q.numel()), "ivf_recall_at_15": round(float(hit), 5),
+            "ivf_probe": IVF_PROBE, "ivf_qprobes": IVF_QPROBES}
 
 
 def main() -> None:

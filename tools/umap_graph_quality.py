@@ -20,7 +20,8 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--families", default="classification,low_rank")
-    ap.add_argument("--graphs", default="brute,ivf16,ivf32,ivf64")
+    ap.add_argument("--graphs", default="brute,list16,query16,query32",
+                    help="brute | list<N> (probe by the list centre) | query<N> (per-query probes) | ivf<N>")
     ap.add_argument("--sample", type=int, default=20_000)
     a = ap.parse_args()
     from northstar import trustworthiness
@@ -48,6 +49,9 @@ def main() -> None:
         for gname in a.graphs.split(","):
             if gname == "brute":
                 kw = dict(build_algo="brute_force_knn")
+            elif gname.startswith("list") or gname.startswith("query"):  # probe mode + count
+                mode = "list" if gname.startswith("list") else "query"
+                kw = dict(build_algo="ivf", build_kwds={"nprobe": int(gname[len(mode):]), "probe": mode})
             else:
                 kw = dict(build_algo="ivf", build_kwds={"nprobe": int(gname[3:])})
             est = UMAP(n_neighbors=15, n_components=2, random_state=1, featuresCol="features", **kw)
