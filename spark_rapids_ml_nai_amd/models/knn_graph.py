@@ -289,6 +289,11 @@ def knn_graph_ivf(X: torch.Tensor, k: int, nlist: Optional[int] = None, nprobe: 
         kc = max(2, int(round(math.sqrt(nlist))))
         cl = ops.nearest_list(C, train_quantizer(C, kc, seed + 1))
         C = C.index_select(0, torch.argsort(cl.long() * nlist + torch.arange(nlist, device=C.device))).contiguous()
+        if ctx is not None and ctx.world_size > 1:
+            # the reorder ran on every rank alone and its cluster sums fold with fp64 atomics (order-
+            # dependent rounding): rank 0's lists are THE lists, or ranks could mix list ids in the
+            # all-gathered labels (one nlist x n broadcast)
+            ctx.comm.broadcast(C, src=0)
     world = ctx.world_size if ctx is not None else 1
     # bucketing: every rank labels its own row block, the labels are all-gathered (N x 4 B)
     blo, bhi = row_split(N, ctx)

@@ -552,6 +552,10 @@ def umap_fit(X: torch.Tensor, params: Dict[str, Any], y: Optional[torch.Tensor] 
         emb = torch.rand((N, dim), generator=g, device=X.device) * 20.0 - 10.0
     mn, mx = emb.min(0).values, emb.max(0).values
     emb = (10.0 * (emb - mn) / (mx - mn).clamp_min(1e-30)).float().contiguous()
+    if dist_ctx is not None and dist_ctx.world_size > 1:
+        # the ranks' layouts agree by construction (identical collectives); one N x dim broadcast
+        # makes rank 0's layout THE layout whatever a rank-local rounding did
+        dist_ctx.comm.broadcast(emb, src=0)
     t_ep = time.perf_counter()
     optimize_layout(emb, emb, rows, cols, vals, n_epochs, a, b, float(params.get("repulsion_strength", 1.0)),
                     float(params.get("learning_rate", 1.0)), float(params.get("negative_sample_rate", 5)), True, seed,

@@ -1365,14 +1365,16 @@ def test_kmeans_lloyd_loop_far_from_origin(gpu_device):
     C0 = Xf[torch.randperm(m, generator=g)[:k]].double()
     ctx = WorkerContext.single(torch.device(gpu_device))
     C, it, _ = _lloyd_small_loop(Xf.to(gpu_device), C0.to(gpu_device), ctx, k, 1, 0.0)
-    lab = ops.kmeans_lloyd_small(Xf.to(gpu_device), C0.float().to(gpu_device), with_sums=False)[0].long().cpu()
     Xd = Xf.double()
+    # fp64 labels (a raw-coordinate fp32 search at this offset is itself wrong: ||c||^2 ~ 6e7 rounds
+    # by ~4, more than the distance gaps; the centred kernel sees the spread only)
+    lab = torch.cdist(Xd, C0).argmin(1)
     cnt = torch.bincount(lab, minlength=k).double()
     S = torch.zeros(k, n, dtype=torch.float64).index_add_(0, lab, Xd)
     ref = torch.where(cnt.view(-1, 1) > 0, S / cnt.clamp_min(1).view(-1, 1), C0)
     assert it == 1
-    # fp32 sums of the raw rows would be off by ~1e3 * 2^-24 * sqrt(rows per wave) ~ 1e-2
-    assert float((C.cpu() - ref).abs().max()) < 2e-4
+    # (a near-tie row taking the other side moves a centre by ~spread / count ~ 2e-4)
+    assert float((C.cpu() - ref).abs().max()) < 1e-3
 
 
 def test_dbscan_labels_match_unique_oracle(gpu_device):
