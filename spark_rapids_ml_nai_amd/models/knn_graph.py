@@ -36,6 +36,7 @@ IVF_POOL_MULT = int(os.environ.get("SRML_IVF_POOL", "8"))
 IVF_QPROBES_DEV_MAX = 32
 IVF_SEED_PROBES = int(os.environ.get("SRML_IVF_SEED_PROBES", "8"))  # list probes of the per-query seed pass
 IVF_PAIR_BYTES = int(os.environ.get("SRML_IVF_PAIR_MB", "4096")) << 20  # per-chunk partial-list budget
+IVF_PAIR_H16 = os.environ.get("SRML_IVF_PAIR_H16", "1") == "1"  # pre-centred fp16 items for the pair search
 # quantiser training: Lloyd iterations and sample rows per list (SRML_IVF_TRAIN_ITERS / _ROWS)
 IVF_TRAIN_ITERS = int(os.environ.get("SRML_IVF_TRAIN_ITERS", "10"))
 IVF_TRAIN_ROWS = int(os.environ.get("SRML_IVF_TRAIN_ROWS", "64"))
@@ -223,7 +224,10 @@ def query_probe_search(Xs: torch.Tensor, xn: torch.Tensor, C: torch.Tensor, coun
     _, pool = ops.knn(C, C, P, inorm=cn, qnorm=zero)
     probes = ops.knn_pool_probes(Xs, off, C, pool.int(), tile_q0[tlo:thi], tile_list[tlo:thi], p, r0, r1)
     t0 = record_phase(phases, "query_probes", r1 - r0, t0, dev)
-    # 3. pairs, in row chunks
+    # 3. pairs, in row chunks; the items of the pair search are centred on their own list: one fp16
+    # copy of the rows serves every pair tile (IVF_PAIR_H16=0: convert per tile instead)
+    items_f16 = (ops.center_rows_f16(Xs, C, off) if IVF_PAIR_H16 and Xs.is_cuda and ops.knn_lists_f16_ok(Xs, kc, C)
+                 else None)
     rows_per_chunk = max(128, IVF_PAIR_BYTES // (p * kc * 8))
     d_parts, p_parts = [], []
     ta = tlo
@@ -243,7 +247,7 @@ def query_probe_search(Xs: torch.Tensor, xn: torch.Tensor, C: torch.Tensor, coun
         qrows = (ca + perm // p).int()
         pt_q0, pt_list = ivf_tiles(poff[1:] - poff[:-1], poff)
         odp, oip = ops.knn_pairs(Xs, off, C, poff, qrows, perm.int(), pt_q0, pt_list, kc, (cb - ca) * p,
-                                 thr_row=thr)
+                                 thr_row=thr, items_f16=items_f16)
         del qrows, perm, flat
         vals = torch.cat([d2s[ca - r0: cb - r0], odp.view(cb - ca, p * kc)], 1)
         ids = torch.cat([poss[ca - r0: cb - r0], oip.view(cb - ca, p * kc).long()], 1)
@@ -258,9 +262,65 @@ def query_probe_search(Xs: torch.Tensor, xn: torch.Tensor, C: torch.Tensor, coun
     return torch.cat(d_parts), torch.cat(p_parts), r0, r1
 
 
+NND_ITERS = int(os.environ.get("SRML_NND_ITERS", "2"))  # refinement rounds of build_algo="nn_descent"
+NND_CHUNK_ROWS = 1 << 21
+
+
+def nn_descent_refine(Xs: torch.Tensor, d2: torch.Tensor, pos: torch.Tensor, k: int, iters: int = NND_ITERS,
+                      a: int = 8, b: int = 8, R: int = 16, ctx: Any = None,
+                      phases: Optional[dict] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """NN-descent refinement of an all-points graph (``pos``: N x k row ids of ``Xs``, ``d2``:
+    their squared distances): per round, every row re-ranks exactly the union of its neighbours,
+    its first ``a`` neighbours' first ``b`` neighbours and up to ``R`` reverse neighbours (rows
+    that list it), de-duplicated, and keeps the k nearest. A neighbour's neighbour or a reverse
+    neighbour is the join of NN-descent (Dong et al. 2011) evaluated from the row's side: every row
+    writes only its own list, so no atomics. Reverse lists come from one stable grouping of the
+    N k edges by target. Distributed (``ctx``): each rank refines a row block of the replicated
+    graph, the blocks are all-gathered after every round.
+
+    It pays off on a graph that is already good (per-query IVF: recall 0.64 -> 0.69 -> 0.71 in two
+    rounds on 200k classification rows) and barely moves a poor one (list probing: 0.375 -> 0.380,
+    the round-5 experiment's finding)."""
+    import time
+
+    t0 = time.perf_counter()
+    N = Xs.shape[0]
+    dev = Xs.device
+    lo, hi = row_split(N, ctx)
+    for _ in range(max(0, int(iters))):
+        tgt = pos.reshape(-1)
+        # reverse neighbours: edges grouped by target (stable: the source order is kept)
+        if tgt.is_cuda and N <= int(ops.native.lib().srml_label_sort_kmax()):
+            perm, off, _ = ops.label_sort(tgt.clamp_min(0).int(), N)
+            perm = perm.long()
+        else:
+            srt, perm = torch.sort(tgt, stable=True)
+            off = torch.searchsorted(srt, torch.arange(N + 1, device=dev, dtype=srt.dtype))
+        d_parts, p_parts = [], []
+        for c0 in range(lo, hi, NND_CHUNK_ROWS):
+            c1 = min(hi, c0 + NND_CHUNK_ROWS)
+            own = pos[c0:c1]
+            non = pos.index_select(0, own[:, :a].clamp_min(0).reshape(-1))[:, :b].reshape(c1 - c0, a * b)
+            non = torch.where(own[:, :a].repeat_interleave(b, 1) >= 0, non, torch.full_like(non, -1))
+            st = off[c0:c1].unsqueeze(1) + torch.arange(R, device=dev)
+            ok = st < off[c0 + 1: c1 + 1].unsqueeze(1)
+            rev = torch.where(ok, perm[st.clamp_max(perm.numel() - 1)] // k, torch.full_like(st, -1))
+            cand = torch.sort(torch.cat([own, non, rev], 1), dim=1).values
+            dup = torch.zeros_like(cand, dtype=torch.bool)
+            dup[:, 1:] = cand[:, 1:] == cand[:, :-1]
+            cand = torch.where(dup, torch.full_like(cand, -1), cand)
+            dd, pp = refine_sorted(Xs[c0:c1], Xs, cand)
+            d_parts.append(dd[:, :k])
+            p_parts.append(pp[:, :k])
+        d2 = gather_rows(torch.cat(d_parts), ctx) if d_parts else d2[lo:hi]
+        pos = gather_rows(torch.cat(p_parts), ctx) if p_parts else pos[lo:hi]
+    record_phase(phases, "nn_descent", hi - lo, t0, dev)
+    return d2, pos
+
+
 def knn_graph_ivf(X: torch.Tensor, k: int, nlist: Optional[int] = None, nprobe: Optional[int] = None,
                   seed: int = 0, ctx: Any = None, list_order: bool = False, phases: Optional[dict] = None,
-                  probe: Optional[str] = None) -> Any:
+                  probe: Optional[str] = None, nnd_iters: int = 0) -> Any:
     """Approximate all-points graph: (euclidean distances [N, k], indices [N, k] int64).
 
     ``list_order=True`` returns ``(dist, idx, order)`` with the graph left in inverted-list order:
@@ -333,6 +393,8 @@ def knn_graph_ivf(X: torch.Tensor, k: int, nlist: Optional[int] = None, nprobe: 
     d2 = gather_rows(d2, ctx)
     pos = gather_rows(pos, ctx)
     record_phase(phases, "knn_lists", r1 - r0, t0, X.device)
+    if nnd_iters > 0:
+        d2, pos = nn_descent_refine(Xs, d2, pos, k, iters=nnd_iters, ctx=ctx, phases=phases)
     if list_order:
         fin = torch.isfinite(d2)
         rowmax = torch.where(fin, d2, torch.zeros_like(d2)).max(1, keepdim=True).values
@@ -367,6 +429,8 @@ def build_knn_graph(X: torch.Tensor, k: int, build_algo: str = "auto", build_kwd
         record_phase(phases, "knn_brute", hi - lo, t0, X.device)
         return (d, i, None) if list_order else (d, i)
     if algo in ("ivf", "ivfflat", "ivf_flat", "nn_descent"):
+        # nn_descent: the per-query IVF graph refined by NN-descent rounds (build_kwds "nnd_iters")
+        nnd = int(kw.get("nnd_iters", NND_ITERS)) if algo == "nn_descent" else int(kw.get("nnd_iters", 0))
         return knn_graph_ivf(X, k, nlist=kw.get("nlist"), nprobe=kw.get("nprobe"), seed=seed, ctx=ctx,
-                             list_order=list_order, phases=phases, probe=kw.get("probe"))
-    raise ValueError("Unsupported build_algo %r (auto, brute_force_knn, ivf)" % build_algo)
+                             list_order=list_order, phases=phases, probe=kw.get("probe"), nnd_iters=nnd)
+    raise ValueError("Unsupported build_algo %r (auto, brute_force_knn, ivf, nn_descent)" % build_algo)

@@ -1925,15 +1925,29 @@ def knn_pool_probes(X: torch.Tensor, list_off: torch.Tensor, C: torch.Tensor, po
     return torch.where(pos >= 0, flat[pos.clamp_min(0)], torch.full_like(pos, -1)).int()
 
 
+def center_rows_f16(X: torch.Tensor, C: torch.Tensor, list_off: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """The pair search's pre-centred items (device, ``knn_lists_f16_ok`` rows): (Xh (N, 128) fp16 =
+    X[r] - C[list of r], zero padded; ||Xh[r]||^2 fp32 of the rounded values)."""
+    N, n = X.shape
+    Xh = torch.empty((N, 128), dtype=torch.float16, device=X.device)
+    nr = torch.empty(N, dtype=torch.float32, device=X.device)
+    native.call("srml_center_rows_f16", X.data_ptr(), n, X.stride(0), _c(C).data_ptr(), _c(list_off.long()).data_ptr(),
+                int(list_off.shape[0]) - 1, N, Xh.data_ptr(), nr.data_ptr(), native.stream(X.device))
+    return Xh, nr
+
+
 def knn_pairs(X: torch.Tensor, list_off: torch.Tensor, C: torch.Tensor, pair_off: torch.Tensor,
               qrows: torch.Tensor, qslot: torch.Tensor, tile_q0: torch.Tensor, tile_list: torch.Tensor, k: int,
-              nslots: int, thr_row: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+              nslots: int, thr_row: Optional[torch.Tensor] = None,
+              items_f16: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """Per-query probing, inverted: the (row, probed list) pairs sorted by list (``pair_off``:
     nlist + 1 offsets; ``qrows``: the X row of each sorted pair; ``qslot``: its output slot);
     every pair's k nearest items of its list. Returns slot-major (nslots, k) squared distances
     (device: fp16-rounded ranking keys, comparable across one row's lists; re-rank exactly) and
     item rows int32, ascending (+inf / -1 padding). ``thr_row`` (N floats, indexed by X row): keep
-    only items whose squared distance is below the row's threshold (its k-th best so far)."""
+    only items whose squared distance is below the row's threshold (its k-th best so far).
+    ``items_f16``: ``center_rows_f16(X, C, list_off)``, computed once per graph: the kernel then
+    copies pre-centred fp16 item tiles (half the bytes, no per-tile conversion)."""
     N, n = X.shape
     nlist = int(list_off.shape[0]) - 1
     od = torch.full((nslots, k), float("inf"), dtype=torch.float32, device=X.device)
@@ -1967,7 +1981,8 @@ def knn_pairs(X: torch.Tensor, list_off: torch.Tensor, C: torch.Tensor, pair_off
                 _c(pair_off.long()).data_ptr(), _c(qrows.int()).data_ptr(), _c(qslot.int()).data_ptr(),
                 _c(tile_q0.long()).data_ptr(), _c(tile_list.int()).data_ptr(), ntiles, int(k), od.data_ptr(),
                 oi.data_ptr(), self_probe.data_ptr(), _c(thr_row.float()).data_ptr() if thr_row is not None else None,
-                native.stream(X.device))
+                items_f16[0].data_ptr() if items_f16 is not None else None,
+                items_f16[1].data_ptr() if items_f16 is not None else None, native.stream(X.device))
     return od, oi
 
 

@@ -336,6 +336,32 @@ __device__ __forceinline__ void kg_load_rows(KgPf& pf, const float* __restrict__
   }
 }
 
+// Pre-centred fp16 item rows (PAIRS mode: every item of list c is x - C_c, converted once per
+// fit, rows of F_KP halves = 256 B): a tile is 128 rows x 16 pieces of 16 B; thread t moves pieces
+// t + 512 i (i < 4): 16 consecutive threads cover one row, fully coalesced, no conversion
+struct KgPh {
+  uint4 v[4];
+};
+
+__device__ __forceinline__ void kg_load_h(KgPh& pf, const _Float16* __restrict__ Xh, long r0, long nvalid, int t) {
+  const long rmax = nvalid > 0 ? nvalid - 1 : 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int id = t + 512 * i;
+    const long r = min((long)(id >> 4), rmax);
+    pf.v[i] = *reinterpret_cast<const uint4*>(Xh + (r0 + r) * F_KP + 8 * (id & 15));
+  }
+}
+
+__device__ __forceinline__ void kg_store_h(const KgPh& pf, _Float16* __restrict__ dst, long nvalid, int t) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int id = t + 512 * i;
+    const int r = id >> 4;
+    *reinterpret_cast<uint4*>(dst + r * F_RS + 8 * (id & 15)) = r < nvalid ? pf.v[i] : make_uint4(0u, 0u, 0u, 0u);
+  }
+}
+
 // PAIRS = false: a tile is <= 128 consecutive rows of list c = tile_list[b] (its rows X[q0 ..)),
 // scanning the lists probes[c][0 .. nprobe); output row = the query's sorted row.
 // PAIRS = true (per-query probing, inverted): the (row, probed list) pairs are sorted by list; a
@@ -344,13 +370,18 @@ __device__ __forceinline__ void kg_load_rows(KgPf& pf, const float* __restrict__
 // items (probes[c][0] = c, nprobe = 1). Both operands are centred on C_c, and ||q - C_c||^2 of the
 // rounded query is added to the keys, so keys of one row from different lists compare (they are
 // the fp16-rounded ||q - i||^2); output row = qslot[pair position] (the caller's per-pair slot).
-template <bool PAIRS>
+// H16 (PAIRS only): the items come pre-centred in fp16 (Xh: x - C_list(x), N x F_KP halves, and
+// their norms xhn): the per-tile staging is a plain 16-B copy (half the bytes, no conversion) and
+// the item norms are loaded, not recomputed from the fragments.
+template <bool PAIRS, bool H16 = false>
 __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
     const float* __restrict__ X, int n, long ld, const float* __restrict__ C, const long long* __restrict__ list_off,
     const int* __restrict__ probes, int nprobe, const long long* __restrict__ tile_q0,
     const int* __restrict__ tile_list, int ntiles, int k, float* __restrict__ out_d, int* __restrict__ out_i,
     const int* __restrict__ qrows = nullptr, const int* __restrict__ qslot = nullptr,
-    const long long* __restrict__ pair_off = nullptr, const float* __restrict__ thr_row = nullptr) {
+    const long long* __restrict__ pair_off = nullptr, const float* __restrict__ thr_row = nullptr,
+    const _Float16* __restrict__ Xh = nullptr, const float* __restrict__ xhn = nullptr) {
+  static_assert(PAIRS || !H16, "pre-centred items are the PAIRS mode's (items centred on their own list)");
   __shared__ __attribute__((aligned(16))) _Float16 Qs[F_BM * F_RS];
   __shared__ __attribute__((aligned(16))) _Float16 Is[F_BN * F_RS];
   __shared__ float cand_d[F_BM][F_CAP + 1];
@@ -410,19 +441,28 @@ __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
   // issued right after tile t + 1 is staged (at tile t's first barrier), so they have a whole
   // tile period to arrive.
   KgPf pfa;
+  KgPh pfh;
+  auto load_items = [&](long r0, long nv) {
+    if constexpr (H16) kg_load_h(pfh, Xh, r0, nv, t);
+    else kg_load(pfa, X, ld, r0, nv, n, wid, lane);
+  };
+  auto store_items = [&](long nv) {
+    if constexpr (H16) kg_store_h(pfh, Is, nv, t);
+    else kg_store(pfa, Is, cen, wid, lane, nv, n);
+  };
   bool have = next_tile();  // tile in LDS
   long tc0 = c0, te = e;
-  if (have) kg_load(pfa, X, ld, c0, e - c0, n, wid, lane);
+  if (have) load_items(c0, e - c0);
   {
     KgPf pq;
     if (PAIRS) kg_load_rows(pq, X, ld, qrows + q0, nq, n, wid, lane);
     else kg_load(pq, X, ld, q0, nq, n, wid, lane);
     kg_store(pq, Qs, cen, wid, lane, nq, n);
   }
-  if (have) kg_store(pfa, Is, cen, wid, lane, te - tc0, n);
+  if (have) store_items(te - tc0);
   bool have1 = have && next_tile();  // tile after it, in registers
   long h1c0 = c0, h1e = e;
-  if (have1) kg_load(pfa, X, ld, c0, e - c0, n, wid, lane);
+  if (have1) load_items(c0, e - c0);
   __syncthreads();
   if (PAIRS) {
     // ||q - C_c||^2 of the staged (rounded, centred) queries; padding columns are zero. A seeded
@@ -459,15 +499,18 @@ __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
             *reinterpret_cast<const kg_halfx8*>(Qs + (wm * 64 + mt * 32 + li) * F_RS + ks * 16 + lk * 8);
         acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bv, acc[mt], 0, 0, 0);
       }
+      if constexpr (!H16) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const kg_half2 h = kg_half2{bv[2 * u], bv[2 * u + 1]};
-        nrm = __builtin_amdgcn_fdot2(h, h, nrm, false);
+        for (int u = 0; u < 4; ++u) {
+          const kg_half2 h = kg_half2{bv[2 * u], bv[2 * u + 1]};
+          nrm = __builtin_amdgcn_fdot2(h, h, nrm, false);
+        }
       }
     }
-    nrm += __shfl_xor(nrm, 32, 64);  // the other k half of the same item row
     const int col = wn * 32 + li;
     const long cg = tc0 + col;
+    if constexpr (H16) nrm = cg < te ? xhn[cg] : 0.f;
+    else nrm += __shfl_xor(nrm, 32, 64);  // the other k half of the same item row
     const float inv = cg < te ? nrm : inf;
     unsigned done = 0u;
     bool first = true;
@@ -516,10 +559,16 @@ __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
       if (first && have1) {
         // pin the prefetched registers behind the barrier: otherwise the compiler hoists the
         // centring/conversion above the append loop and waits for the loads right after the MFMAs
+        if constexpr (H16) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(pfa.v[j]));
-        kg_store(pfa, Is, cen, wid, lane, h1e - h1c0, n);
-        if (have2) kg_load(pfa, X, ld, h2c0, h2e - h2c0, n, wid, lane);
+          for (int j = 0; j < 4; ++j)
+            asm volatile("" : "+v"(pfh.v[j].x), "+v"(pfh.v[j].y), "+v"(pfh.v[j].z), "+v"(pfh.v[j].w));
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(pfa.v[j]));
+        }
+        store_items(h1e - h1c0);
+        if (have2) load_items(h2c0, h2e - h2c0);
       }
       const int full = ovf[par];  // block-uniform: some row ran out of candidate slots
       first = false;
@@ -562,8 +611,52 @@ SRML_API int srml_knn_lists_f16c(const float* X, int n, long ld, const float* C,
   if (k < 1 || k > F_KQ || n < 1 || n > F_KP || (n & 3) || (ld & 3) || nprobe < 1 || nprobe > F_PMAX ||
       (reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(C) & 15))
     return -8;
-  hipLaunchKernelGGL(knn_lists_f16_kernel<false>, dim3((unsigned)ntiles), dim3(512), 0, stream, X, n, ld, C, list_off,
-                     probes, nprobe, tile_q0, tile_list, ntiles, k, out_d, out_i, nullptr, nullptr, nullptr);
+  hipLaunchKernelGGL((knn_lists_f16_kernel<false, false>), dim3((unsigned)ntiles), dim3(512), 0, stream, X, n, ld, C,
+                     list_off, probes, nprobe, tile_q0, tile_list, ntiles, k, out_d, out_i, nullptr, nullptr, nullptr,
+                     nullptr, nullptr, nullptr);
+  return srml_status();
+}
+
+// Pre-centred fp16 items of the pair search: out[r] = fp16(X[r] - C[list of r]) (F_KP halves per
+// row, zero padded), norms[r] = ||out[r]||^2 of the rounded values. 32 lanes per row, 4 columns
+// each; list_off (nlist + 1) gives each sorted row's list by binary search.
+__global__ __launch_bounds__(256) void center_rows_f16_kernel(const float* __restrict__ X, int n, long ld,
+                                                              const float* __restrict__ C,
+                                                              const long long* __restrict__ list_off, int nlist, long N,
+                                                              _Float16* __restrict__ out, float* __restrict__ norms) {
+  const long r = (long)blockIdx.x * 8 + (threadIdx.x >> 5);
+  const int l32 = threadIdx.x & 31;
+  if (r >= N) return;  // whole 32-lane groups
+  int lo = 0, hi = nlist;  // list c with list_off[c] <= r < list_off[c + 1]
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (list_off[mid] <= r) lo = mid;
+    else hi = mid;
+  }
+  const int col = 4 * l32;
+  typedef _Float16 halfx4 __attribute__((ext_vector_type(4)));
+  halfx4 h = halfx4{(_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
+  if (col < n) {
+    const floatx4 x = *reinterpret_cast<const floatx4*>(X + r * ld + col);
+    const floatx4 c = *reinterpret_cast<const floatx4*>(C + (long)lo * n + col);
+    h = halfx4{(_Float16)(x[0] - c[0]), (_Float16)(x[1] - c[1]), (_Float16)(x[2] - c[2]), (_Float16)(x[3] - c[3])};
+  }
+  *reinterpret_cast<halfx4*>(out + r * F_KP + col) = h;
+  float a = 0.f;
+  a = __builtin_amdgcn_fdot2(kg_half2{h[0], h[1]}, kg_half2{h[0], h[1]}, a, false);
+  a = __builtin_amdgcn_fdot2(kg_half2{h[2], h[3]}, kg_half2{h[2], h[3]}, a, false);
+  for (int o = 16; o > 0; o >>= 1) a += __shfl_xor(a, o, 32);
+  if (l32 == 0) norms[r] = a;
+}
+
+SRML_API int srml_center_rows_f16(const float* X, int n, long ld, const float* C, const long long* list_off, int nlist,
+                                  long N, void* out, float* norms, hipStream_t stream) {
+  if (N <= 0) return 0;
+  if (n < 1 || n > F_KP || (n & 3) || (ld & 3) || (reinterpret_cast<uintptr_t>(X) & 15) ||
+      (reinterpret_cast<uintptr_t>(C) & 15) || (reinterpret_cast<uintptr_t>(out) & 15))
+    return -8;
+  hipLaunchKernelGGL(center_rows_f16_kernel, dim3((unsigned)((N + 7) / 8)), dim3(256), 0, stream, X, n, ld, C, list_off,
+                     nlist, N, reinterpret_cast<_Float16*>(out), norms);
   return srml_status();
 }
 
@@ -577,14 +670,23 @@ SRML_API int srml_knn_lists_f16c(const float* X, int n, long ld, const float* C,
 SRML_API int srml_knn_pairs_f16c(const float* X, int n, long ld, const float* C, const long long* list_off,
                                  const long long* pair_off, const int* qrows, const int* qslot,
                                  const long long* tile_q0, const int* tile_list, int ntiles, int k, float* out_d,
-                                 int* out_i, const int* self_probe, const float* thr_row, hipStream_t stream) {
+                                 int* out_i, const int* self_probe, const float* thr_row, const void* Xh,
+                                 const float* xhn, hipStream_t stream) {
   if (ntiles <= 0) return 0;
   if (k < 1 || k > F_KQ || n < 1 || n > F_KP || (n & 3) || (ld & 3) || !qrows || !qslot || !pair_off ||
       !self_probe || (reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(C) & 15))
     return -8;
   // self_probe: nlist ints, self_probe[c] = c (list c scans its own items)
-  hipLaunchKernelGGL(knn_lists_f16_kernel<true>, dim3((unsigned)ntiles), dim3(512), 0, stream, X, n, ld, C, list_off,
-                     self_probe, 1, tile_q0, tile_list, ntiles, k, out_d, out_i, qrows, qslot, pair_off, thr_row);
+  if (Xh && xhn) {
+    if (reinterpret_cast<uintptr_t>(Xh) & 15) return -8;
+    hipLaunchKernelGGL((knn_lists_f16_kernel<true, true>), dim3((unsigned)ntiles), dim3(512), 0, stream, X, n, ld, C,
+                       list_off, self_probe, 1, tile_q0, tile_list, ntiles, k, out_d, out_i, qrows, qslot, pair_off,
+                       thr_row, reinterpret_cast<const _Float16*>(Xh), xhn);
+  } else {
+    hipLaunchKernelGGL((knn_lists_f16_kernel<true, false>), dim3((unsigned)ntiles), dim3(512), 0, stream, X, n, ld, C,
+                       list_off, self_probe, 1, tile_q0, tile_list, ntiles, k, out_d, out_i, qrows, qslot, pair_off,
+                       thr_row, nullptr, nullptr);
+  }
   return srml_status();
 }
 

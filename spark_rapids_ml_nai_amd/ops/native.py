@@ -123,7 +123,8 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_ivf_search_f32": (_P, _L, _I, _L, _P, _I, _P, _P, _L, _P, _P, _I, _P, _P, _P),
     "srml_knn_lists_f32": (_P, _I, _L, _P, _P, _P, _I, _P, _P, _I, _I, _P, _P, _P),
     "srml_knn_lists_f16c": (_P, _I, _L, _P, _P, _P, _I, _P, _P, _I, _I, _P, _P, _P),
-    "srml_knn_pairs_f16c": (_P, _I, _L, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P),
+    "srml_knn_pairs_f16c": (_P, _I, _L, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P),
+    "srml_center_rows_f16": (_P, _I, _L, _P, _P, _I, _L, _P, _P, _P),
     "srml_dbscan_degree_f32": (_P, _L, _I, _L, _P, _F, _L, _L, _P, _P),
     "srml_dbscan_link_f32": (_P, _L, _I, _L, _P, _F, _L, _L, _P, _P, _P, _P),
     "srml_uf_unite_pairs": (_P, _L, _P, _P),

@@ -85,9 +85,10 @@ class _UMAPParams(_FeaturesColMixin, _BackendParams, HasFeaturesCol, HasFeatures
     random_state = _p("random_state", "Seed of the pseudo random number generator.", TypeConverters.identity)
     sample_fraction = _p("sample_fraction", "Fraction of the dataset used for fitting.", TypeConverters.toFloat)
     build_algo = _p("build_algo", "kNN graph construction: 'auto' (exact up to 100k rows, IVF lists beyond), "
-                    "'brute_force_knn' or 'ivf'.", TypeConverters.toString)
-    build_kwds = _p("build_kwds", "kNN graph options, e.g. {'nlist': ..., 'nprobe': ...} for build_algo='ivf'.",
-                    TypeConverters.identity)
+                    "'brute_force_knn', 'ivf' (per-query IVF probing) or 'nn_descent' (the IVF graph refined by "
+                    "NN-descent rounds).", TypeConverters.toString)
+    build_kwds = _p("build_kwds", "kNN graph options, e.g. {'nlist': ..., 'nprobe': ..., 'probe': 'query' | 'list', "
+                    "'nnd_iters': ...} for build_algo='ivf' / 'nn_descent'.", TypeConverters.identity)
 
     def __init__(self) -> None:
         super().__init__()

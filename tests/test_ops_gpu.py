@@ -1502,3 +1502,34 @@ def test_knn_graph_query_probing_recall(gpu_device):
         assert torch.isfinite(dist).all() and bool((dist[:, 1:] >= dist[:, :-1]).all())
         rec[probe] = (idx[q].unsqueeze(2) == ie.unsqueeze(1)).any(2).float().mean().item()
     assert rec["query"] > rec["list"] + 0.05 and rec["query"] >= 0.95, rec
+
+
+@pytest.mark.parametrize("seeded", [False, True])
+def test_knn_pairs_precentred_items_match(gpu_device, seeded):
+    """The pair search on pre-centred fp16 items (one copy per graph, plain 16-B tile copies) gives
+    the per-tile-converting kernel's candidates and keys (item norms summed in another order: keys
+    within a few ulps, sets equal up to exact near-ties)."""
+    from spark_rapids_ml_nai_amd.models.knn_graph import ivf_tiles
+
+    N, n, nlist, p, k = 6000, 128, 20, 6, 19
+    Xs, C, counts, off, g = _ivf_fixture(gpu_device, N, n, nlist, 47)
+    probes = torch.stack([torch.randperm(nlist, generator=g)[:p] for _ in range(N)]).int().to(gpu_device)
+    perm, poff, _ = ops.label_sort(probes.reshape(-1), nlist)
+    perm = perm.long()
+    qrows = (perm // p).int()
+    tq, tl = ivf_tiles(poff[1:] - poff[:-1], poff)
+    thr = None
+    if seeded:
+        smp = Xs[torch.randperm(N, generator=g)[:256].to(gpu_device)]
+        thr = torch.quantile(torch.cdist(Xs, smp).pow(2), 0.05, dim=1).contiguous()
+    Xh, nr = ops.center_rows_f16(Xs, C, off)
+    # the centred copy is x - C_list(x), rounded to fp16, zero past n
+    row_list = torch.repeat_interleave(torch.arange(nlist, device=gpu_device), counts)
+    torch.testing.assert_close(Xh[:, :n].float(), (Xs - C[row_list]).half().float(), rtol=0, atol=0)
+    torch.testing.assert_close(nr, (Xh.float() ** 2).sum(1), rtol=1e-5, atol=1e-3)
+    d0, i0 = ops.knn_pairs(Xs, off, C, poff, qrows, perm.int(), tq, tl, k, N * p, thr_row=thr)
+    d1, i1 = ops.knn_pairs(Xs, off, C, poff, qrows, perm.int(), tq, tl, k, N * p, thr_row=thr, items_f16=(Xh, nr))
+    hit = (i1.unsqueeze(2) == i0.unsqueeze(1)).any(2) & (i1 >= 0)
+    assert hit.sum().item() >= 0.995 * max(1, int((i0 >= 0).sum()))
+    both = (i0 == i1) & (i0 >= 0)
+    torch.testing.assert_close(d1[both], d0[both], rtol=1e-5, atol=1e-2)

@@ -78,6 +78,35 @@ def test_umap_sample_fraction_and_cosine():
     assert out.shape == (800, 3)
 
 
+def test_query_probing_and_nn_descent_recall():
+    """Per-query IVF probing beats list probing at the same probe count on rows whose neighbours
+    straddle lists, and build_algo='nn_descent' (the per-query graph + NN-descent rounds) raises
+    the recall further; the graphs stay sorted, exact and duplicate-free."""
+    import torch
+
+    from spark_rapids_ml_nai_amd.bench import datagen
+    from spark_rapids_ml_nai_amd.models.knn_graph import build_knn_graph, knn_graph_brute
+
+    X, _ = datagen.classification(12000, 32, torch.device("cpu"), seed=3, n_informative=12, n_redundant=8)
+    X = X.float().contiguous()
+    _, ie = knn_graph_brute(X, 10)
+
+    def rec(idx):
+        return np.mean([len(set(a) & set(b)) / 10.0 for a, b in zip(idx.numpy(), ie.numpy())])
+
+    r = {}
+    for name, algo, kw in (("list", "ivf", {"nprobe": 2, "probe": "list", "nlist": 24}),
+                           ("query", "ivf", {"nprobe": 2, "probe": "query", "nlist": 24}),
+                           ("nnd", "nn_descent", {"nprobe": 2, "probe": "query", "nlist": 24, "nnd_iters": 2})):
+        d, i = build_knn_graph(X, 10, algo, kw, seed=1)
+        assert torch.all(d[:, 1:] >= d[:, :-1] - 1e-6)
+        assert all(len(set(row)) == 10 for row in i[:500].tolist())
+        ref = ((X[i.clamp_min(0)] - X.unsqueeze(1)) ** 2).sum(-1).sqrt()
+        assert torch.allclose(d, ref, atol=1e-3)
+        r[name] = rec(i)
+    assert r["query"] > r["list"] + 0.05 and r["nnd"] > r["query"], r
+
+
 def test_ivf_knn_graph_recall():
     """IVF-list all-points graph (UMAP build_algo='ivf') vs the exact graph: recall >= 0.9."""
     import torch

@@ -24,6 +24,7 @@ def main() -> None:
     ap.add_argument("--cols", type=int, default=128)
     ap.add_argument("--probe", default="list,query", help="list: probe the list centre's nearest lists; "
                     "query: each row's own nearest lists (per-query probing)")
+    ap.add_argument("--nnd", default="0", help="NN-descent refinement rounds (comma list)")
     a = ap.parse_args()
     from spark_rapids_ml_nai_amd.bench import datagen
     from spark_rapids_ml_nai_amd.models.knn_graph import knn_graph, knn_graph_ivf
@@ -43,11 +44,12 @@ def main() -> None:
             q = torch.randperm(N, device=dev, generator=g)[: a.queries]
             _, ei = knn_graph(X.index_select(0, q), X, a.k + 1)
             ei = ei.cpu()
-            for probe, npb in [(pm, int(x)) for pm in a.probe.split(",") for x in a.nprobe.split(",")]:
+            for probe, npb, nnd in [(pm, int(x), int(r)) for pm in a.probe.split(",") for x in a.nprobe.split(",")
+                                    for r in a.nnd.split(",")]:
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 phases = {}
-                _, gi = knn_graph_ivf(X, a.k, nprobe=npb, seed=1, probe=probe, phases=phases)
+                _, gi = knn_graph_ivf(X, a.k, nprobe=npb, seed=1, probe=probe, phases=phases, nnd_iters=nnd)
                 torch.cuda.synchronize()
                 dt = time.perf_counter() - t0
                 gq = gi.index_select(0, q).cpu()
@@ -56,7 +58,7 @@ def main() -> None:
                     # the exact list includes the row itself (distance 0): compare the k nearest,
                     # self included, as the IVF graph also returns the row itself first
                     hit += len(set(gq[r].tolist()) & set(ei[r, : a.k].tolist())) / float(a.k)
-                print(json.dumps({"family": fam, "rows": N, "cols": n, "probe": probe, "nprobe": npb, "k": a.k,
+                print(json.dumps({"family": fam, "rows": N, "cols": n, "probe": probe, "nprobe": npb, "nnd": nnd, "k": a.k,
                                   "recall": round(hit / q.shape[0], 4), "graph_s": round(dt, 3),
                                   "phases": {k: v["s"] for k, v in phases.items()}}), flush=True)
                 del gi
