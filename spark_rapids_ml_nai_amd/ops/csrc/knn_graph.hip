@@ -440,8 +440,11 @@ __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
   // item tiles flow: registers -> centred fp16 LDS tile -> MFMA. The loads of tile t + 2 are
   // issued right after tile t + 1 is staged (at tile t's first barrier), so they have a whole
   // tile period to arrive.
+  // H16: two register buffers (16 VGPRs each) keep tiles t + 1 AND t + 2 in flight while tile t
+  // computes: a pair tile scans only ~8 item tiles, so one tile of lead exposed the load latency
+  // at every step; buffer (t + 1) & 1 is staged at tile t's first barrier, then reloaded with t + 3
   KgPf pfa;
-  KgPh pfh;
+  KgPh pfh, pfh2;
   auto load_items = [&](long r0, long nv) {
     if constexpr (H16) kg_load_h(pfh, Xh, r0, nv, t);
     else kg_load(pfa, X, ld, r0, nv, n, wid, lane);
@@ -463,6 +466,15 @@ __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
   bool have1 = have && next_tile();  // tile after it, in registers
   long h1c0 = c0, h1e = e;
   if (have1) load_items(c0, e - c0);
+  bool have2 = false;  // H16: the tile after that, in the second buffer
+  long h2c0 = 0, h2e = 0;
+  if constexpr (H16) {
+    have2 = have1 && next_tile();
+    h2c0 = c0;
+    h2e = e;
+    if (have2) kg_load_h(pfh2, Xh, c0, e - c0, t);
+  }
+  int par2 = 0;  // H16: which buffer holds tile t + 1
   __syncthreads();
   if (PAIRS) {
     // ||q - C_c||^2 of the staged (rounded, centred) queries; padding columns are zero. A seeded
@@ -483,8 +495,16 @@ __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
   const int nks = (n + 15) >> 4;
   int par = 0;
   while (have) {
-    const bool have2 = have1 && next_tile();
-    const long h2c0 = c0, h2e = e;
+    // the next tile to fetch: t + 2 (one buffer) or t + 3 (H16's two)
+    bool haveN;
+    long hNc0, hNe;
+    if constexpr (H16) {
+      haveN = have2 && next_tile();
+    } else {
+      haveN = have1 && next_tile();
+    }
+    hNc0 = c0;
+    hNe = e;
     floatx16 acc[2];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
@@ -560,15 +580,18 @@ __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
         // pin the prefetched registers behind the barrier: otherwise the compiler hoists the
         // centring/conversion above the append loop and waits for the loads right after the MFMAs
         if constexpr (H16) {
+          KgPh& cur = par2 ? pfh2 : pfh;
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            asm volatile("" : "+v"(pfh.v[j].x), "+v"(pfh.v[j].y), "+v"(pfh.v[j].z), "+v"(pfh.v[j].w));
+            asm volatile("" : "+v"(cur.v[j].x), "+v"(cur.v[j].y), "+v"(cur.v[j].z), "+v"(cur.v[j].w));
+          kg_store_h(cur, Is, h1e - h1c0, t);
+          if (haveN) kg_load_h(cur, Xh, hNc0, hNe - hNc0, t);
         } else {
 #pragma unroll
           for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(pfa.v[j]));
+          store_items(h1e - h1c0);
+          if (haveN) load_items(hNc0, hNe - hNc0);
         }
-        store_items(h1e - h1c0);
-        if (have2) load_items(h2c0, h2e - h2c0);
       }
       const int full = ovf[par];  // block-uniform: some row ran out of candidate slots
       first = false;
@@ -583,9 +606,19 @@ __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
     tc0 = h1c0;
     te = h1e;
     have = have1;
-    h1c0 = h2c0;
-    h1e = h2e;
-    have1 = have2;
+    if constexpr (H16) {  // shift the two in-flight tiles; the fetched one is t + 3
+      h1c0 = h2c0;
+      h1e = h2e;
+      have1 = have2;
+      h2c0 = hNc0;
+      h2e = hNe;
+      have2 = haveN;
+      par2 ^= 1;
+    } else {
+      h1c0 = hNc0;
+      h1e = hNe;
+      have1 = haveN;
+    }
   }
   kg_merge(topd, topi, cand_d, cand_i, cnt, thr_s, k, nq, wid, lane, 1);  // the last candidates
   __syncthreads();

@@ -63,6 +63,10 @@ def test_every_phase_shards(fits, w):
         assert 0.5 * N / w <= ph["knn_lists"]["rows"] <= 1.5 * N / w  # work-balanced tile ranges
         assert abs(ph["epochs"]["rows"] - one["epochs"]["rows"] / w) <= 1  # edges e % W == r
         assert ph["fuzzy_union"]["rows"] == N  # the only replicated phase
+        # per-query probing (seed / probes / pairs) and the NN-descent round shard by rows too
+        for name in ("query_seed", "query_probes", "query_pairs"):
+            assert 0.5 * N / w <= ph[name]["rows"] <= 1.5 * N / w, (name, ph[name])
+        assert abs(ph["nn_descent"]["rows"] - N / w) <= 1
 
 
 @pytest.mark.parametrize("w", [2, 4])

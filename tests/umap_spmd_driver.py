@@ -42,8 +42,8 @@ def main() -> None:
     from spark_rapids_ml_nai_amd.models import umap as U
 
     X = torch.from_numpy(data())
-    params = {"n_neighbors": 12, "n_components": 2, "random_state": 5, "n_epochs": 120, "build_algo": "ivf",
-              "build_kwds": {"nlist": 24, "nprobe": 8}}
+    params = {"n_neighbors": 12, "n_components": 2, "random_state": 5, "n_epochs": 120, "build_algo": "nn_descent",
+              "build_kwds": {"nlist": 24, "nprobe": 8, "nnd_iters": 1}}
     emb = U.umap_fit(X, params, ctx=ctx)
     os.makedirs(a.out, exist_ok=True)
     np.savez(os.path.join(a.out, "rank%d.npz" % rank), emb=emb, phases=json.dumps(U.LAST_PHASES))
