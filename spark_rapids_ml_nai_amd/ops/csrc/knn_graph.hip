@@ -341,10 +341,13 @@ __device__ __forceinline__ void kg_load_rows(KgPf& pf, const float* __restrict__
 // t + 512 i (i < 4): 16 consecutive threads cover one row, fully coalesced, no conversion
 struct KgPh {
   uint4 v[4];
+  float nrm;  // ||item||^2 of this lane's MFMA column (row `col` of the tile), loaded with the tile
 };
 
-__device__ __forceinline__ void kg_load_h(KgPh& pf, const _Float16* __restrict__ Xh, long r0, long nvalid, int t) {
+__device__ __forceinline__ void kg_load_h(KgPh& pf, const _Float16* __restrict__ Xh, const float* __restrict__ xhn,
+                                          long r0, long nvalid, int t, int col) {
   const long rmax = nvalid > 0 ? nvalid - 1 : 0;
+  pf.nrm = xhn[r0 + min((long)col, rmax)];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int id = t + 512 * i;
@@ -445,13 +448,19 @@ __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
   // at every step; buffer (t + 1) & 1 is staged at tile t's first barrier, then reloaded with t + 3
   KgPf pfa;
   KgPh pfh, pfh2;
+  const int my_col = wn * 32 + li;  // this lane's item column in every MFMA tile
+  float is_nrm = 0.f;              // H16: its item norm for the tile now in Is
   auto load_items = [&](long r0, long nv) {
-    if constexpr (H16) kg_load_h(pfh, Xh, r0, nv, t);
+    if constexpr (H16) kg_load_h(pfh, Xh, xhn, r0, nv, t, my_col);
     else kg_load(pfa, X, ld, r0, nv, n, wid, lane);
   };
   auto store_items = [&](long nv) {
-    if constexpr (H16) kg_store_h(pfh, Is, nv, t);
-    else kg_store(pfa, Is, cen, wid, lane, nv, n);
+    if constexpr (H16) {
+      kg_store_h(pfh, Is, nv, t);
+      is_nrm = pfh.nrm;
+    } else {
+      kg_store(pfa, Is, cen, wid, lane, nv, n);
+    }
   };
   bool have = next_tile();  // tile in LDS
   long tc0 = c0, te = e;
@@ -472,7 +481,7 @@ __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
     have2 = have1 && next_tile();
     h2c0 = c0;
     h2e = e;
-    if (have2) kg_load_h(pfh2, Xh, c0, e - c0, t);
+    if (have2) kg_load_h(pfh2, Xh, xhn, c0, e - c0, t, my_col);
   }
   int par2 = 0;  // H16: which buffer holds tile t + 1
   __syncthreads();
@@ -529,7 +538,7 @@ __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
     }
     const int col = wn * 32 + li;
     const long cg = tc0 + col;
-    if constexpr (H16) nrm = cg < te ? xhn[cg] : 0.f;
+    if constexpr (H16) nrm = is_nrm;  // came with the tile (no load on the MFMA -> filter path)
     else nrm += __shfl_xor(nrm, 32, 64);  // the other k half of the same item row
     const float inv = cg < te ? nrm : inf;
     unsigned done = 0u;
@@ -580,12 +589,18 @@ __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
         // pin the prefetched registers behind the barrier: otherwise the compiler hoists the
         // centring/conversion above the append loop and waits for the loads right after the MFMAs
         if constexpr (H16) {
-          KgPh& cur = par2 ? pfh2 : pfh;
+          // (two static branches, not a runtime-selected reference: a dynamically chosen register
+          // array would be demoted to scratch memory)
+          auto rotate = [&](KgPh& cur) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
-            asm volatile("" : "+v"(cur.v[j].x), "+v"(cur.v[j].y), "+v"(cur.v[j].z), "+v"(cur.v[j].w));
-          kg_store_h(cur, Is, h1e - h1c0, t);
-          if (haveN) kg_load_h(cur, Xh, hNc0, hNe - hNc0, t);
+            for (int j = 0; j < 4; ++j)
+              asm volatile("" : "+v"(cur.v[j].x), "+v"(cur.v[j].y), "+v"(cur.v[j].z), "+v"(cur.v[j].w));
+            kg_store_h(cur, Is, h1e - h1c0, t);
+            is_nrm = cur.nrm;
+            if (haveN) kg_load_h(cur, Xh, xhn, hNc0, hNe - hNc0, t, my_col);
+          };
+          if (par2) rotate(pfh2);
+          else rotate(pfh);
         } else {
 #pragma unroll
           for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(pfa.v[j]));
