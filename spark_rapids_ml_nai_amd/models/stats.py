@@ -45,7 +45,8 @@ def scatter_stats(X: torch.Tensor, ctx: WorkerContext, m_total: int, stream: Any
         ops.col_moments(Xc, need_sq=need_sq, out=(s, q))  # accumulated in place: no per-chunk fill / add
         if mu0 is None:
             mu0 = s / max(r1 - r0, 1)  # the first chunk's means
-        ops.gram(Xc, mu0, out=G, finalize=False)
+            mu0f = mu0.float() if Xc.dtype == torch.float32 else mu0  # the Gram's shift, converted once
+        ops.gram(Xc, mu0f, out=G, finalize=False)
         if y is not None:
             ops.xtv(Xc, y[r0:r1].view(-1, 1), out=xty)
         m_r += r1 - r0

@@ -599,14 +599,21 @@ def nearest_centroid_f16(F: F16Planes, C: torch.Tensor, approx: bool = False) ->
     filter's arg-min and only exact ties of the filtered distances are re-searched."""
     m, k, dev = F.m, C.shape[0], F.X.device
     st = native.stream(dev)
-    W = _c(C.float().to(dev) - F.mu.view(1, -1))  # centred centres: the operands of every search
-    cn = (W.double() * W.double()).sum(1).float()  # fp64 norms, one fp32 rounding (in the radius)
+    # centred centres W = C - mu (the operands of every search), their fp64 norms with one fp32
+    # rounding (in the radius), the radius terms cg, and the overflow / flagged counters zeroed:
+    # one launch (X's own plane never overflows, s comes from its maximum; only the centres can)
+    Cd = _c(C.to(dev)) if C.dtype in (torch.float32, torch.float64) else _c(C.to(dev, torch.float32))
+    W = torch.empty((k, F.n), dtype=torch.float32, device=dev)
+    cn = torch.empty(k, dtype=torch.float32, device=dev)
+    cg = torch.empty(k, dtype=torch.float32, device=dev)
+    zero2 = torch.empty(2, dtype=torch.int32, device=dev)  # [ovf, flagged count]
+    native.call("srml_f16_centre_prep", Cd.data_ptr(), int(Cd.dtype == torch.float64), k, F.n, F.mu.data_ptr(),
+                float(2.0 * F.tau), int(bool(approx)), W.data_ptr(), cn.data_ptr(), cg.data_ptr(), zero2.data_ptr(), st)
+    ovf = zero2[0:1]
     crows = max(256, (k + 255) // 256 * 256)
     CP = torch.empty((crows // 256, F.kp // 16, 256, 16), dtype=torch.float16, device=dev)
-    F.ovf.zero_()  # X's own plane never overflows (s comes from its maximum); only the centres can
     native.call("srml_split_f16_tiled_centered", W.data_ptr(), k, F.n, W.stride(0), None, F.kp, crows, F.scale,
-                CP.data_ptr(), F.ovf.data_ptr(), st)
-    cg = torch.zeros_like(cn) if approx else (2.0 * F.tau) * cn.clamp_min(0).sqrt()
+                CP.data_ptr(), ovf.data_ptr(), st)
     xadd, z, z2 = (0.0, 0.0, 0.0) if approx else (F.xadd, F.z, F.z2)
     dscale = -2.0 / (F.scale * F.scale)
     nslot = int(native.lib().srml_nearest_centroid_f16_top2_nslot(k))
@@ -614,7 +621,7 @@ def nearest_centroid_f16(F: F16Planes, C: torch.Tensor, approx: bool = False) ->
     dist = torch.empty(m, dtype=torch.float32, device=dev)
     flagged = torch.empty(m, dtype=torch.int32, device=dev)
     thr = torch.empty(m, dtype=torch.float32, device=dev)
-    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    cnt = zero2[1:2]  # zeroed by the centre prep
     # row chunks of whole 256-row tiles within the 2^32 work-item grid (512-thread blocks x
     # centre tiles); the select appends each chunk's uncertified rows (chunk-relative) to flagged
     step = split_rows_per_launch(k)
@@ -629,7 +636,7 @@ def nearest_centroid_f16(F: F16Planes, C: torch.Tensor, approx: bool = False) ->
                     st)
         c0 = int(cnt.item()) if r0 else 0
         native.call("srml_split_top2_select_f16_thr", keys.data_ptr(), lob.data_ptr(), mc, nslot, xn.data_ptr(),
-                    cg.data_ptr(), xadd, z, z2, F.ovf.data_ptr(), labels[r0:].data_ptr(), dist[r0:].data_ptr(),
+                    cg.data_ptr(), xadd, z, z2, ovf.data_ptr(), labels[r0:].data_ptr(), dist[r0:].data_ptr(),
                     flagged.data_ptr(), cnt.data_ptr(), thr.data_ptr(), st)
         if r0:
             nc = int(cnt.item())

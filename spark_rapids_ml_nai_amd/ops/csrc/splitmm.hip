@@ -1114,6 +1114,46 @@ static int f16_bn() {
 // result slots per centroid tile: one per 64-wide wave column
 static int f16_slots_per_tile() { return f16_bn() / 64; }
 
+// Centre operands of one fp16 filter search, in one launch (was ~10 torch launches per Lloyd
+// iteration): W = fp32(C - mu) (C fp64 or fp32 rows, k x n), cn = fp32 of the fp64 norm of W's
+// rows, cg = 2 tau sqrt(cn) (0 when approx), and the overflow / flagged counters zeroed. One
+// 64-lane wave per centre.
+template <typename T>
+__global__ __launch_bounds__(256) void f16_centre_prep_kernel(const T* __restrict__ C, int k, int n,
+                                                              const float* __restrict__ mu, float tau2, int approx,
+                                                              float* __restrict__ W, float* __restrict__ cn,
+                                                              float* __restrict__ cg, int* __restrict__ zero2) {
+  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (blockIdx.x == 0 && threadIdx.x < 2) zero2[threadIdx.x] = 0;
+  if (j >= k) return;  // whole waves
+  double a = 0.0;
+  for (int d = lane; d < n; d += 64) {
+    const float w = (float)((double)C[(long)j * n + d] - (double)mu[d]);
+    W[(long)j * n + d] = w;
+    a += (double)w * (double)w;
+  }
+  for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+  if (lane == 0) {
+    const float c = (float)a;
+    cn[j] = c;
+    cg[j] = approx ? 0.f : tau2 * sqrtf(c > 0.f ? c : 0.f);
+  }
+}
+
+SRML_API int srml_f16_centre_prep(const void* C, int c_f64, int k, int n, const float* mu, float tau2, int approx,
+                                  float* W, float* cn, float* cg, int* zero2, hipStream_t stream) {
+  if (k <= 0) return 0;
+  const dim3 grid((unsigned)((k + 3) / 4));
+  if (c_f64)
+    hipLaunchKernelGGL(f16_centre_prep_kernel<double>, grid, dim3(256), 0, stream,
+                       reinterpret_cast<const double*>(C), k, n, mu, tau2, approx, W, cn, cg, zero2);
+  else
+    hipLaunchKernelGGL(f16_centre_prep_kernel<float>, grid, dim3(256), 0, stream, reinterpret_cast<const float*>(C),
+                       k, n, mu, tau2, approx, W, cn, cg, zero2);
+  return srml_status();
+}
+
 // One tiled fp16 plane of scale * (x - mu) (mu may be null), rows padded to rows_pad (% 256 == 0):
 // P = [rows_pad / 256][kp / 16][256][16]; *ovf |= 1 if an element of |scale v| >= 2^15 was clamped.
 SRML_API int srml_split_f16_tiled_centered(const float* X, long m, int n, long ld, const float* mu, int kp,

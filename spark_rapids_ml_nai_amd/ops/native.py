@@ -122,6 +122,7 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_knn_f32": (_P, _L, _I, _L, _P, _L, _L, _P, _I, _I, _P, _P, ctypes.c_longlong, _P),
     "srml_ivf_search_f32": (_P, _L, _I, _L, _P, _I, _P, _P, _L, _P, _P, _I, _P, _P, _P),
     "srml_knn_lists_f32": (_P, _I, _L, _P, _P, _P, _I, _P, _P, _I, _I, _P, _P, _P),
+    "srml_f16_centre_prep": (_P, _I, _I, _I, _P, _F, _I, _P, _P, _P, _P, _P),
     "srml_knn_lists_f16c": (_P, _I, _L, _P, _P, _P, _I, _P, _P, _I, _I, _P, _P, _P),
     "srml_knn_pairs_f16c": (_P, _I, _L, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P),
     "srml_center_rows_f16": (_P, _I, _L, _P, _P, _I, _L, _P, _P, _P),
