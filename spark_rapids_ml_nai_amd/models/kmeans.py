@@ -321,7 +321,7 @@ def kmeans_fit(X: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext, k
     for it in range(max(0, max_iter) if not fused_small else 0):
         n_iter = it + 1
         if F16 is not None:
-            labels, d2 = ops.nearest_centroid_f16(F16, C.float())
+            labels, d2 = ops.nearest_centroid_f16(F16, C)  # fp64 centres: centred + rounded in its prep kernel
         elif XP is not None:
             labels, d2 = ops.nearest_centroid_split(XP, X.shape[0], C.float(), xnorm_s, X=X if certified else None,
                                                     mu=mu)
