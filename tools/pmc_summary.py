@@ -27,6 +27,10 @@ def main():
         out["l2_hit_rate"] = round(tot["TCC_HIT_sum"] / max(1.0, tot["TCC_HIT_sum"] + tot["TCC_MISS_sum"]), 4)
     if tot.get("SQ_LDS_IDX_ACTIVE"):
         out["lds_bank_conflict_frac"] = round(tot.get("SQ_LDS_BANK_CONFLICT", 0.0) / tot["SQ_LDS_IDX_ACTIVE"], 4)
+    if tot.get("SQ_WAVES"):
+        for key in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU"):
+            if key in tot:
+                out[key.lower()[3:] + "_per_wave"] = round(tot[key] / tot["SQ_WAVES"], 1)
     if tot.get("SQ_WAVE_CYCLES"):
         out["wait_inst_lds_frac"] = round(tot.get("SQ_WAIT_INST_LDS", 0.0) / tot["SQ_WAVE_CYCLES"], 4)
     print(json.dumps(out, indent=1))
