@@ -392,7 +392,7 @@ __device__ __forceinline__ void kg_store_h(const KgPh& pf, _Float16* __restrict_
 // H16 (PAIRS only): the items come pre-centred in fp16 (Xh: x - C_list(x), N x F_KP halves, and
 // their norms xhn): the per-tile staging is a plain 16-B copy (half the bytes, no conversion) and
 // the item norms are loaded, not recomputed from the fragments.
-template <bool PAIRS, bool H16 = false>
+template <bool PAIRS, bool H16 = false, bool H2 = H16>
 __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
     const float* __restrict__ X, int n, long ld, const float* __restrict__ C, const long long* __restrict__ list_off,
     const int* __restrict__ probes, int nprobe, const long long* __restrict__ tile_q0,
@@ -401,6 +401,7 @@ __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
     const long long* __restrict__ pair_off = nullptr, const float* __restrict__ thr_row = nullptr,
     const _Float16* __restrict__ Xh = nullptr, const float* __restrict__ xhn = nullptr) {
   static_assert(PAIRS || !H16, "pre-centred items are the PAIRS mode's (items centred on their own list)");
+  static_assert(H16 || !H2, "the two-buffer prefetch is the fp16 items'");
   __shared__ __attribute__((aligned(16))) _Float16 Qs[F_BM * F_RS];
   __shared__ __attribute__((aligned(16))) _Float16 Is[F_BN * F_RS];
   __shared__ float cand_d[F_BM][F_CAP + 1];
@@ -459,9 +460,11 @@ __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
   // item tiles flow: registers -> centred fp16 LDS tile -> MFMA. The loads of tile t + 2 are
   // issued right after tile t + 1 is staged (at tile t's first barrier), so they have a whole
   // tile period to arrive.
-  // H16: two register buffers (16 VGPRs each) keep tiles t + 1 AND t + 2 in flight while tile t
-  // computes: a pair tile scans only ~8 item tiles, so one tile of lead exposed the load latency
-  // at every step; buffer (t + 1) & 1 is staged at tile t's first barrier, then reloaded with t + 3
+  // H2 (fp16 items, SRML_KG_H2=1): two register buffers (16 VGPRs each) keep tiles t + 1 AND t + 2
+  // in flight while tile t computes; buffer (t + 1) & 1 is staged at tile t's first barrier, then
+  // reloaded with t + 3. Since the query fragments live in registers (64 VGPRs) it spills one
+  // fragment and measured 5 % slower than one buffer (20M rows: 1.205 vs 1.140 s), so one buffer
+  // is the default
   KgPf pfa;
   KgPh pfh, pfh2;
   const int my_col = wn * 32 + li;  // this lane's item column in every MFMA tile
@@ -493,7 +496,7 @@ __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
   if (have1) load_items(c0, e - c0);
   bool have2 = false;  // H16: the tile after that, in the second buffer
   long h2c0 = 0, h2e = 0;
-  if constexpr (H16) {
+  if constexpr (H2) {
     have2 = have1 && next_tile();
     h2c0 = c0;
     h2e = e;
@@ -518,12 +521,20 @@ __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
     __syncthreads();
   }
   const int nks = (n + 15) >> 4;
+  // this wave's query fragments stay in registers for the whole scan: re-reading them from LDS
+  // for every item tile made the MFMA operand traffic (24 KB per wave and tile) LDS-bound
+  kg_halfx8 areg[2][F_KP / 16];
+#pragma unroll
+  for (int ks = 0; ks < F_KP / 16; ++ks)
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+      areg[mt][ks] = *reinterpret_cast<const kg_halfx8*>(Qs + (wm * 64 + mt * 32 + li) * F_RS + ks * 16 + lk * 8);
   int par = 0;
   while (have) {
     // the next tile to fetch: t + 2 (one buffer) or t + 3 (H16's two)
     bool haveN;
     long hNc0, hNe;
-    if constexpr (H16) {
+    if constexpr (H2) {
       haveN = have2 && next_tile();
     } else {
       haveN = have1 && next_tile();
@@ -536,14 +547,12 @@ __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[mt][r] = 0.f;
     float nrm = 0.f;  // ||i - C_c||^2 of the rounded item row, from the B fragments themselves
-    for (int ks = 0; ks < nks; ++ks) {
+#pragma unroll
+    for (int ks = 0; ks < F_KP / 16; ++ks) {
+      if (ks >= nks) break;  // block-uniform (zero padding columns past n)
       const kg_halfx8 bv = *reinterpret_cast<const kg_halfx8*>(Is + (wn * 32 + li) * F_RS + ks * 16 + lk * 8);
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
-        const kg_halfx8 av =
-            *reinterpret_cast<const kg_halfx8*>(Qs + (wm * 64 + mt * 32 + li) * F_RS + ks * 16 + lk * 8);
-        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bv, acc[mt], 0, 0, 0);
-      }
+      for (int mt = 0; mt < 2; ++mt) acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(areg[mt][ks], bv, acc[mt], 0, 0, 0);
       if constexpr (!H16) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -604,7 +613,7 @@ __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
       if (first && have1) {
         // pin the prefetched registers behind the barrier: otherwise the compiler hoists the
         // centring/conversion above the append loop and waits for the loads right after the MFMAs
-        if constexpr (H16) {
+        if constexpr (H2) {
           // (two static branches, not a runtime-selected reference: a dynamically chosen register
           // array would be demoted to scratch memory)
           auto rotate = [&](KgPh& cur) {
@@ -618,8 +627,14 @@ __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
           if (par2) rotate(pfh2);
           else rotate(pfh);
         } else {
+          if constexpr (H16) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(pfa.v[j]));
+            for (int j = 0; j < 4; ++j)
+              asm volatile("" : "+v"(pfh.v[j].x), "+v"(pfh.v[j].y), "+v"(pfh.v[j].z), "+v"(pfh.v[j].w));
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(pfa.v[j]));
+          }
           store_items(h1e - h1c0);
           if (haveN) load_items(hNc0, hNe - hNc0);
         }
@@ -637,7 +652,7 @@ __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
     tc0 = h1c0;
     te = h1e;
     have = have1;
-    if constexpr (H16) {  // shift the two in-flight tiles; the fetched one is t + 3
+    if constexpr (H2) {  // shift the two in-flight tiles; the fetched one is t + 3
       h1c0 = h2c0;
       h1e = h2e;
       have1 = have2;
@@ -743,9 +758,18 @@ SRML_API int srml_knn_pairs_f16c(const float* X, int n, long ld, const float* C,
   // self_probe: nlist ints, self_probe[c] = c (list c scans its own items)
   if (Xh && xhn) {
     if (reinterpret_cast<uintptr_t>(Xh) & 15) return -8;
-    hipLaunchKernelGGL((knn_lists_f16_kernel<true, true>), dim3((unsigned)ntiles), dim3(512), 0, stream, X, n, ld, C,
-                       list_off, self_probe, 1, tile_q0, tile_list, ntiles, k, out_d, out_i, qrows, qslot, pair_off,
-                       thr_row, reinterpret_cast<const _Float16*>(Xh), xhn);
+    static const int two = [] {
+      const char* e = getenv("SRML_KG_H2");
+      return e ? atoi(e) : 0;
+    }();
+    if (two)
+      hipLaunchKernelGGL((knn_lists_f16_kernel<true, true, true>), dim3((unsigned)ntiles), dim3(512), 0, stream, X, n,
+                         ld, C, list_off, self_probe, 1, tile_q0, tile_list, ntiles, k, out_d, out_i, qrows, qslot,
+                         pair_off, thr_row, reinterpret_cast<const _Float16*>(Xh), xhn);
+    else
+      hipLaunchKernelGGL((knn_lists_f16_kernel<true, true, false>), dim3((unsigned)ntiles), dim3(512), 0, stream, X, n,
+                         ld, C, list_off, self_probe, 1, tile_q0, tile_list, ntiles, k, out_d, out_i, qrows, qslot,
+                         pair_off, thr_row, reinterpret_cast<const _Float16*>(Xh), xhn);
   } else {
     hipLaunchKernelGGL((knn_lists_f16_kernel<true, false>), dim3((unsigned)ntiles), dim3(512), 0, stream, X, n, ld, C,
                        list_off, self_probe, 1, tile_q0, tile_list, ntiles, k, out_d, out_i, qrows, qslot, pair_off,
