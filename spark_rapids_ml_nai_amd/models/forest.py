@@ -79,6 +79,8 @@ LEVEL_LOG = os.environ.get("SRML_RF_LEVEL_LOG", "0") == "1"
 # (SRML_RF_ONE_SYNC=0: the two-copy loop; max_leaves > 0 always takes it — its per-tree budget is
 # decided on the host)
 RF_ONE_SYNC = os.environ.get("SRML_RF_ONE_SYNC", "1") != "0"
+# the one-sync level bookkeeping in native kernels (ops.rf_decide / rf_level_pack); 0: torch ops
+RF_LEVEL_NATIVE = os.environ.get("SRML_RF_LEVEL_NATIVE", "1") != "0"
 # levels whose nodes average fewer in-bag positions than this gather from a row-major copy of the
 # bins (built once, at the first such level): a row's sampled features share cache lines there,
 # where the feature-major matrix costs one line per (row, feature) (0 = off)
@@ -117,13 +119,7 @@ class _LevelClock:
 def _left_totals(hist: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
     """(C, S) fp64 class totals of each node's left child under its best split (zeros for nodes
     without one): the winning feature's histogram summed up to the split bin."""
-    C = hist.shape[0]
-    ok = out[:, 1] >= 0
-    slot = torch.where(ok, out[:, 1], torch.zeros_like(out[:, 1])).long()
-    b = torch.where(ok, out[:, 2], torch.zeros_like(out[:, 2])).long()
-    ar = torch.arange(C, device=hist.device)
-    left = hist[ar, slot].double().cumsum(1)[ar, b]  # (C, S)
-    return torch.where(ok.view(-1, 1), left, torch.zeros_like(left))
+    return ops.rf_left_totals(hist, out)
 
 
 def feature_subset_size(strategy: Any, n: int, n_trees: int, classification: bool) -> int:
@@ -349,7 +345,7 @@ def _root_hist_streamed(pending: PendingBins, bins: torch.Tensor, idx: torch.Ten
     nfc = (nf + fb - 1) // fb
     Ch = feats.shape[0]  # histogram rows: C, or C padded for the node-partitioned reduce-scatter
     assert C == len(c_start) and Ch >= C
-    hist = torch.zeros((Ch, nf, B, SH), dtype=torch.float64 if regression else torch.int32, device=dev)
+    hist = ops.zeros((Ch, nf, B, SH), dtype=torch.float64 if regression else torch.int32, device=dev)
     wy = ops.rf_hist_wy(idx, yv, None, wpos)
     rows_at = torch.tensor([r0 for r0, _ in pending.bounds] + [m], dtype=idx.dtype, device=dev)
     # P[j, c]: first position of segment j whose row is >= the start of chunk c
@@ -410,7 +406,51 @@ def _h2d(a: np.ndarray, dev: torch.device) -> torch.Tensor:
 
 def _pad_rows(t: torch.Tensor, rows: int) -> torch.Tensor:
     """``t`` with zero rows appended up to ``rows``."""
-    return torch.cat([t, torch.zeros((rows - t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)], 0)
+    return torch.cat([t, ops.zeros((rows - t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)], 0)
+
+
+def _level_one_sync_device(bins: torch.Tensor, idx: torch.Tensor, wpos: torch.Tensor, bounds: torch.Tensor,
+                           tot: torch.Tensor, yv: torch.Tensor, cand: np.ndarray, L: int, out_d: torch.Tensor,
+                           fsel_d: torch.Tensor, res_left: List[torch.Tensor], S: int, regression: bool, crit: int,
+                           data_parallel: bool, ctx: WorkerContext, dev: torch.device, clk: "_LevelClock"
+                           ) -> Optional[tuple]:
+    """``_level_one_sync`` with its bookkeeping in native kernels (ops.rf_decide / rf_level_pack:
+    split ranks, routing arrays, children totals, segment stats and the read-back buffer) — the
+    torch version launched ~55 library kernels per level. Same results and return value."""
+    C = int(cand.size)
+    cand_d = _h2d(cand.astype(np.int64), dev)
+    left = None
+    if not regression:
+        left = torch.cat(res_left, 0) if len(res_left) > 1 else res_left[0]
+    node_feature, node_bin, child_base, tot_n = ops.rf_decide(out_d, fsel_d, cand_d, L, left,
+                                                              None if regression else tot)
+    clk.mark("decide_host")
+    keys = ops.rf_route_segments(bins, idx, bounds, node_feature, node_bin, child_base)
+    idx_n, wpos_n, bounds_n = ops.rf_partition(keys, bounds, node_feature, child_base, C, idx, wpos, trim=False)
+    if regression:
+        tot_n = _node_stats(yv, idx_n, wpos_n, bounds_n, S, regression)
+        if data_parallel:
+            ctx.comm.allreduce(tot_n)
+    clk.mark("route_launch")
+    V2 = 3 if regression else int(tot_n.shape[1]) + 2
+    hb = ops.rf_level_pack(bounds_n, tot_n, regression, crit, out_d, fsel_d).cpu().numpy()
+    clk.mark("end_sync")
+    nb = 2 * C + 1
+    off = nb + 2 * C * V2
+    out_all = hb[off: off + 6 * C].reshape(C, 6)
+    feat_all = hb[off + 6 * C:]
+    ci_sel = np.nonzero(out_all[:, 1] >= 0)[0]
+    k = int(ci_sel.size)
+    if LEVEL_LOG:
+        clk.rec["candidates"] = C
+        clk.rec["splits"] = k
+    if k == 0:
+        return None
+    bounds_h = hb[: 2 * k + 1].astype(np.int64)
+    stats_h = hb[nb: nb + 2 * k * V2].reshape(2 * k, V2)
+    kept = int(bounds_h[-1])
+    return (idx_n[:kept], wpos_n[:kept], bounds_n[: 2 * k + 1], tot_n[: 2 * k], bounds_h, stats_h, out_all,
+            feat_all, ci_sel)
 
 
 def _level_one_sync(bins: torch.Tensor, idx: torch.Tensor, wpos: torch.Tensor, bounds: torch.Tensor,
@@ -427,13 +467,16 @@ def _level_one_sync(bins: torch.Tensor, idx: torch.Tensor, wpos: torch.Tensor, b
     out_d = torch.cat(res_out_d, 0) if len(res_out_d) > 1 else res_out_d[0]
     fsel_d = (torch.cat(res_fsel_d, 0) if len(res_fsel_d) > 1 else res_fsel_d[0]).view(-1)
     C = int(cand.size)
+    if RF_LEVEL_NATIVE and dev.type == "cuda" and out_d.dtype == torch.float64 and fsel_d.dtype == torch.float64:
+        return _level_one_sync_device(bins, idx, wpos, bounds, tot, yv, cand, L, out_d, fsel_d, res_left, S,
+                                      regression, crit, data_parallel, ctx, dev, clk)
     ok_d = out_d[:, 1] >= 0
     oki = ok_d.to(torch.int32)
     pos_d = torch.cumsum(oki, 0, dtype=torch.int32) - oki
     cand_d = _h2d(cand.astype(np.int64), dev)
     node_feature = torch.full((L,), -1, dtype=torch.int32, device=dev)
-    node_bin = torch.zeros(L, dtype=torch.int32, device=dev)
-    child_base = torch.zeros(L, dtype=torch.int32, device=dev)
+    node_bin = ops.zeros(L, dtype=torch.int32, device=dev)
+    child_base = ops.zeros(L, dtype=torch.int32, device=dev)
     node_feature[cand_d] = torch.where(ok_d, fsel_d.to(torch.int32), torch.full_like(oki, -1))
     node_bin[cand_d] = torch.where(ok_d, out_d[:, 2].to(torch.int32), torch.zeros_like(oki))
     child_base[cand_d] = torch.where(ok_d, 2 * pos_d, torch.zeros_like(oki))
@@ -448,7 +491,7 @@ def _level_one_sync(bins: torch.Tensor, idx: torch.Tensor, wpos: torch.Tensor, b
         left = torch.cat(res_left, 0) if len(res_left) > 1 else res_left[0]
         pair = torch.stack([left, tot.index_select(0, cand_d) - left], 1)
         dest = torch.where(ok_d, pos_d.long(), torch.full_like(pos_d, C, dtype=torch.int64))
-        tot_n = torch.zeros((C + 1, 2, S), dtype=pair.dtype, device=dev)
+        tot_n = ops.zeros((C + 1, 2, S), dtype=pair.dtype, device=dev)
         tot_n.index_copy_(0, dest, pair)
         tot_n = tot_n[:C].reshape(2 * C, S)
     if data_parallel and regression:
@@ -735,7 +778,7 @@ def grow_forest(bins: torch.Tensor, edges_h: np.ndarray, y: torch.Tensor, ctx: W
                 out = out_f
                 res_left.append(left_f)
             # the winning feature ids gathered on the device: one copy of (records | feature id)
-            fsel = feats[:C].gather(1, out[:, 1].clamp_min(0).long().view(-1, 1)).to(out.dtype)
+            fsel = ops.rf_gather_feature(feats[:C], out)
             clk.mark("hist_split_launch")
             if one_sync:
                 res_out_d.append(out[:C])

@@ -36,7 +36,7 @@ def _global_rows(X: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext,
     n = X.shape[1]
     start = sum(s for r, s in desc.parts_rank_size if r < desc.rank)
     stop = start + X.shape[0]
-    out = torch.zeros((len(idx), n), dtype=torch.float64, device=X.device)
+    out = ops.zeros((len(idx), n), dtype=torch.float64, device=X.device)
     mine = np.nonzero((idx >= start) & (idx < stop))[0]
     if len(mine):
         rows = torch.from_numpy(idx[mine] - start).to(X.device)
@@ -86,7 +86,7 @@ def _weighted_lloyd(P: torch.Tensor, w: torch.Tensor, C: torch.Tensor, iters: in
             break
         prev = lab
         sums, _ = ops.cluster_sums(Pw, lab, k)
-        cnt = torch.zeros(k, dtype=torch.float64, device=P.device).index_add_(0, lab.long(), wd)
+        cnt = ops.zeros(k, dtype=torch.float64, device=P.device).index_add_(0, lab.long(), wd)
         C = torch.where(cnt.view(-1, 1) > 0, sums / cnt.clamp_min(1e-300).view(-1, 1), C)
     return C
 
@@ -222,15 +222,15 @@ def _lloyd_small_loop(X: torch.Tensor, C: torch.Tensor, ctx: WorkerContext, k: i
     C64 = (C.double() - mu).contiguous() if mu is not None else C.double().contiguous()
     C32 = C64.float().contiguous()
     cn = (C32 * C32).sum(1).contiguous()
-    buf = torch.zeros(k * n + k + 1, dtype=torch.float64, device=dev)
+    buf = ops.zeros(k * n + k + 1, dtype=torch.float64, device=dev)
     mu32 = mu.float().contiguous() if mu is not None else None
     labels = dist = None
     if rows_out:
         labels = torch.empty(X.shape[0], dtype=torch.int32, device=dev)
         dist = torch.empty(X.shape[0], dtype=torch.float32, device=dev)
-    flags = torch.zeros(2, dtype=torch.int32, device=dev)  # [done, iterations]
-    stat = torch.zeros(2, dtype=torch.float64, device=dev)  # [inertia, max shift] of the last update
-    host = torch.zeros((2, 2), dtype=torch.int32, pin_memory=True)
+    flags = ops.zeros(2, dtype=torch.int32, device=dev)  # [done, iterations]
+    stat = ops.zeros(2, dtype=torch.float64, device=dev)  # [inertia, max shift] of the last update
+    host = ops.zeros((2, 2), dtype=torch.int32, pin_memory=True)
     stream = torch.cuda.current_stream(dev)
     pending: List[Any] = []
     it = j = 0
@@ -257,6 +257,42 @@ def _lloyd_small_loop(X: torch.Tensor, C: torch.Tensor, ctx: WorkerContext, k: i
     if mu is not None:
         C64 = C64 + mu
     return C64, int(fl[1]), float(stat[0].item())
+
+
+def _lloyd_f16_loop(X: torch.Tensor, F16: Any, C: torch.Tensor, ctx: WorkerContext, k: int, max_iter: int,
+                    tol2: float) -> Tuple[torch.Tensor, int, float, int]:
+    """Lloyd iterations on the fp16 certified filter with device bookkeeping: per iteration the
+    search (``ops.nearest_centroid_f16``), the moved-row count, a delta or full cluster-sum update
+    of the local [sums | counts | inertia] buffer, ONE all-reduce of it, and the in-place centre
+    update whose (max shift, inertia) read-back is the iteration's convergence test. Returns
+    (centres fp64, iterations, inertia of the last search, delta iterations)."""
+    m, n = X.shape
+    kn = k * n
+    L = torch.empty(kn + k + 1, dtype=torch.float64, device=X.device)
+    G = torch.empty_like(L)
+    book = ops.LloydBook(X, k)
+    C = C.to(device=X.device, dtype=torch.float64).contiguous()
+    prev = None
+    n_iter = n_delta = last_anchor = 0
+    inertia = 0.0
+    for it in range(max(0, max_iter)):
+        n_iter = it + 1
+        labels, d2 = ops.nearest_centroid_f16(F16, C)
+        nm = book.moved(labels, prev) if prev is not None else -1
+        if nm < 0 or nm > DELTA_FRAC * m or (n_delta and n_delta % REANCHOR == 0 and n_delta != last_anchor):
+            book.full_into(X, labels, L)
+            last_anchor = n_delta
+        elif nm:
+            book.delta_into(X, labels, prev, nm, L)
+            n_delta += 1
+        book.inertia_into(d2, L)
+        G.copy_(L)
+        ctx.comm.allreduce(G)
+        shift, inertia = book.update(G, C)
+        prev = labels
+        if shift <= tol2:
+            break
+    return C, n_iter, inertia, n_delta
 
 
 def kmeans_fit(X: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext, k: int, max_iter: int, tol: float,
@@ -316,9 +352,14 @@ def kmeans_fit(X: torch.Tensor, desc: PartitionDescriptor, ctx: WorkerContext, k
     # k <= 32, n <= 64 (the BASELINE k = 20 on 100M x 64): the fused one-pass step gives labels,
     # full cluster sums and the inertia together (no delta bookkeeping needed)
     fused_small = F16 is None and XP is None and ops.lloyd_small_ok(X, k) and not deterministic()
+    # the fp16 certified filter on the device: the whole iteration's bookkeeping runs in native
+    # kernels (ops.LloydBook), same delta / re-anchor schedule as the loop below
+    booked = F16 is not None and X.is_cuda and not deterministic() and os.environ.get("SRML_LLOYD_BOOK", "1") == "1"
     if fused_small:
         C, n_iter, inertia = _lloyd_small_loop(X, C, ctx, k, max_iter, tol2)
-    for it in range(max(0, max_iter) if not fused_small else 0):
+    elif booked:
+        C, n_iter, inertia, n_delta = _lloyd_f16_loop(X, F16, C, ctx, k, max_iter, tol2)
+    for it in range(max(0, max_iter) if not (fused_small or booked) else 0):
         n_iter = it + 1
         if F16 is not None:
             labels, d2 = ops.nearest_centroid_f16(F16, C)  # fp64 centres: centred + rounded in its prep kernel

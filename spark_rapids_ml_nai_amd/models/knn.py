@@ -151,8 +151,8 @@ def exact_knn(items: torch.Tensor, item_ids: torch.Tensor, queries: torch.Tensor
             return (torch.full((Q.shape[0], k), float("inf"), device=Q.device),
                     torch.full((Q.shape[0], k), -1, dtype=torch.int64, device=Q.device))
         if metric == "inner_product":
-            z_i = torch.zeros(items.shape[0], device=items.device)
-            z_q = torch.zeros(Q.shape[0], device=items.device)
+            z_i = ops.zeros(items.shape[0], device=items.device)
+            z_q = ops.zeros(Q.shape[0], device=items.device)
             d, li = ops.knn(Q, items, k, inorm=z_i, qnorm=z_q)  # d = -2 q.i
         else:
             d, li = ops.knn(Q, items, k)

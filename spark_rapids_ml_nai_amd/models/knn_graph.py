@@ -123,8 +123,8 @@ def train_quantizer(X: torch.Tensor, nlist: int, seed: int, iters: Optional[int]
             lab = ops.nearest_list(Tl, C, FT, tn)
             sums, counts = ops.cluster_sums(Tl, lab, nlist)
         else:
-            sums = torch.zeros((nlist, n), dtype=torch.float64, device=X.device)
-            counts = torch.zeros(nlist, dtype=torch.int64, device=X.device)
+            sums = ops.zeros((nlist, n), dtype=torch.float64, device=X.device)
+            counts = ops.zeros(nlist, dtype=torch.int64, device=X.device)
         if dist:
             buf = torch.cat([sums.reshape(-1), counts.double()])
             ctx.comm.allreduce(buf)
@@ -203,7 +203,7 @@ def query_probe_search(Xs: torch.Tensor, xn: torch.Tensor, C: torch.Tensor, coun
     t0 = time.perf_counter()
     nonempty = int((counts > 0).sum())
     cn = torch.where(counts > 0, ops.row_sqnorm(C), torch.full((nlist,), float("inf"), device=dev))
-    zero = torch.zeros(nlist, device=dev)
+    zero = ops.zeros(nlist, device=dev)
     # 1. seed: list probing, exact re-rank
     s1 = max(1, min(int(seed_probes), nonempty, IVF_NPROBE_MAX))
     _, probes1 = ops.knn(C, C, s1, inorm=cn, qnorm=zero)
@@ -379,7 +379,7 @@ def knn_graph_ivf(X: torch.Tensor, k: int, nlist: Optional[int] = None, nprobe: 
     else:
         # probe lists: nearest non-empty lists to each list's centroid (itself first)
         cn = torch.where(counts > 0, ops.row_sqnorm(C), torch.full((nlist,), float("inf"), device=X.device))
-        _, probes = ops.knn(C, C, nprobe, inorm=cn, qnorm=torch.zeros(nlist, device=X.device))
+        _, probes = ops.knn(C, C, nprobe, inorm=cn, qnorm=ops.zeros(nlist, device=X.device))
         ok = (probes >= 0) & torch.isfinite(cn[probes.clamp_min(0)])
         probes = torch.where(ok, probes, torch.full_like(probes, -1))
         lo, hi = balanced_tile_range(tile_q0, tile_list, off, counts, probes, ctx.rank if world > 1 else 0, world)

@@ -126,7 +126,7 @@ def logistic_fit(X: Any, y: torch.Tensor, m_total: int, ctx: WorkerContext, reg:
         # folds them (one launch per evaluation instead of three)
         parts, wst = ops.logreg_fold_layout(X)
         fold = (ws, parts, wst)
-        _scratch = torch.zeros(K * n + 2, dtype=torch.float64, device=X.device)
+        _scratch = ops.zeros(K * n + 2, dtype=torch.float64, device=X.device)
 
         def evaluate_partials(w: torch.Tensor, b: torch.Tensor, flag: Optional[torch.Tensor],
                               zc: Optional[tuple] = None) -> None:
@@ -145,7 +145,7 @@ def logistic_fit(X: Any, y: torch.Tensor, m_total: int, ctx: WorkerContext, reg:
         flag_t = torch.tensor([1.0 if zok else 0.0], dtype=torch.float64, device=X.device)
         ctx.comm.allreduce(flag_t, op="min")
         zok = bool(flag_t.item() > 0)
-    zbuf = torch.zeros(2 * X.shape[0] * K, dtype=torch.float64, device=X.device) if zok else None
+    zbuf = ops.zeros(2 * X.shape[0] * K, dtype=torch.float64, device=X.device) if zok else None
     res = minimize(P, theta0, evaluate, allreduce, y.device, batch=8 if not path.startswith("torch") else 2,
                    graph_safe=graph_safe, fold=fold, evaluate_partials=evaluate_partials, zcache=zbuf)
     return _result(res, base, ctx, n, K, fit_intercept, inv_sigma, path)

@@ -33,6 +33,8 @@ from typing import Callable, List, Optional
 import numpy as np
 import torch
 
+from .. import ops
+
 QN_GRAPH = os.environ.get("SRML_QN_GRAPH", "1") != "0"
 # multi-rank fits: capture the batch INCLUDING its all-reduces (RCCL collectives recorded into the
 # HIP graph, replayed identically on every rank); SRML_QN_GRAPH_COMM=0 keeps them eager
@@ -284,16 +286,16 @@ class DeviceQN:
         if M > int(native.lib().srml_qn_max_history()):
             raise ValueError("L-BFGS memory %d exceeds the kernel's capacity" % M)
         f64 = dict(dtype=torch.float64, device=device)
-        self.vec = torch.zeros((6 + 2 * M) * N, **f64)  # x g pg d xt gt S Y
+        self.vec = ops.zeros((6 + 2 * M) * N, **f64)  # x g pg d xt gt S Y
         v = self.vec
         self.x, self.g, self.pg, self.d, self.xt, self.gt = (v[i * N:(i + 1) * N] for i in range(6))
         self.S = v[6 * N: (6 + M) * N]
         self.Y = v[(6 + M) * N:]
-        self.small = torch.zeros(2 * M * M + max(P.past, 1) + 8, **f64)  # SY YY fh sc
+        self.small = ops.zeros(2 * M * M + max(P.past, 1) + 8, **f64)  # SY YY fh sc
         self.coef = torch.from_numpy(np.concatenate([P.l2, P.l1, P.inv_sigma]).astype(np.float64)).to(device)
-        self.flags = flags if flags is not None else torch.zeros(16, dtype=torch.int32, device=device)
-        self.wb = wb if wb is not None else torch.zeros(P.Kn + P.K, **f64)
-        self.out = out if out is not None else torch.zeros(P.out_len, **f64)
+        self.flags = flags if flags is not None else ops.zeros(16, dtype=torch.int32, device=device)
+        self.wb = wb if wb is not None else ops.zeros(P.Kn + P.K, **f64)
+        self.out = out if out is not None else ops.zeros(P.out_len, **f64)
         assert self.wb.numel() == P.Kn + P.K and self.out.numel() == P.out_len and self.flags.numel() == 16
         th = torch.from_numpy(np.asarray(theta0, dtype=np.float64)).to(device)
         self.xt.copy_(th)
@@ -315,7 +317,7 @@ class DeviceQN:
             setattr(a, k, t.data_ptr())
 
         if os.environ.get("SRML_QN_PROBE") == "1":  # per-section wall-clock stamps of the step kernel
-            self.probe = torch.zeros(16, dtype=torch.int64, device=device)
+            self.probe = ops.zeros(16, dtype=torch.int64, device=device)
             a.probe = self.probe.data_ptr()
         self._args = a
         self._keep = ptrs
@@ -327,7 +329,7 @@ class DeviceQN:
         self.fold: Optional[tuple] = None  # (partial-row workspace, rows, stride) the fused step folds
         if QN_MB and N <= 16384 and os.environ.get("SRML_QN_PROBE") != "1":
             size = int(lib.srml_qn_fused_scratch() if self._fused else lib.srml_qn_mb_scratch())
-            self._mb = torch.zeros(size, **f64)  # zeroed: the fused step's barrier words start at 0
+            self._mb = ops.zeros(size, **f64)  # zeroed: the fused step's barrier words start at 0
         assert ctypes.sizeof(_QnArgs) == int(native.lib().srml_qn_args_size()), "QnArgs layout mismatch"
 
     @property
@@ -417,7 +419,7 @@ def minimize(P: QNProblem, theta0: np.ndarray, evaluate: Callable[[torch.Tensor,
     """
     if device.type != "cuda":
         st = HostQN(P, theta0)
-        out = torch.zeros(P.out_len, dtype=torch.float64, device=device)
+        out = ops.zeros(P.out_len, dtype=torch.float64, device=device)
         cap = max(1, P.max_iter) * (P.max_ls + 1) + 2
         while not st.done and st.n_evals < cap:
             wb = torch.from_numpy(st.wb()).to(device)
@@ -438,7 +440,7 @@ def minimize(P: QNProblem, theta0: np.ndarray, evaluate: Callable[[torch.Tensor,
     zkw = {"zc": zc} if zc is not None else {}
     poll = _comm_poll(allreduce)
     flag = q.flags[F_DONE: F_DONE + 1]
-    host_flag = torch.zeros(2, dtype=torch.int32, pin_memory=True)
+    host_flag = ops.zeros(2, dtype=torch.int32, pin_memory=True)
     events: list = []
     # a margins-only trial accepted costs one more (full) evaluation of its iteration
     cap = max(1, P.max_iter) * (P.max_ls + (2 if zc is not None else 1)) + 2
@@ -531,14 +533,14 @@ def minimize_batch(Ps: List[QNProblem], theta0s: List[np.ndarray],
     n = Ps[0].n
     assert all(P.K == 1 and P.n == n for P in Ps), "batched QN needs binary problems of one width"
     f64 = dict(dtype=torch.float64, device=device)
-    WB = torch.zeros((B, n + 1), **f64)
-    OUT = torch.zeros((B, n + 2), **f64)
-    FL = torch.zeros((B, 16), dtype=torch.int32, device=device)
+    WB = ops.zeros((B, n + 1), **f64)
+    OUT = ops.zeros((B, n + 2), **f64)
+    FL = ops.zeros((B, 16), dtype=torch.int32, device=device)
     qs = [DeviceQN(P, th, device, wb=WB[j], out=OUT[j], flags=FL[j]) for j, (P, th) in enumerate(zip(Ps, theta0s))]
     raw = b"".join(bytes(q._args) for q in qs)
     args_dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
     st = native.stream(device)
-    host = torch.zeros(2, dtype=torch.int32, pin_memory=True)
+    host = ops.zeros(2, dtype=torch.int32, pin_memory=True)
     cap = max(max(1, P.max_iter) * (P.max_ls + 1) + 2 for P in Ps)
     evals, j = 0, 0
     events: list = []

@@ -35,10 +35,10 @@ def scatter_stats(X: torch.Tensor, ctx: WorkerContext, m_total: int, stream: Any
     n = X.shape[1]
     dev = X.device
     chunks = stream.chunks() if stream is not None else [(0, X.shape[0], X)]
-    s = torch.zeros(n, dtype=torch.float64, device=dev)
-    q = torch.zeros(n, dtype=torch.float64, device=dev) if need_sq else None
-    G = torch.zeros((n, n), dtype=torch.float64, device=dev)
-    xty = torch.zeros((n, 1), dtype=torch.float64, device=dev) if y is not None else None
+    s = ops.zeros(n, dtype=torch.float64, device=dev)
+    q = ops.zeros(n, dtype=torch.float64, device=dev) if need_sq else None
+    G = ops.zeros((n, n), dtype=torch.float64, device=dev)
+    xty = ops.zeros((n, 1), dtype=torch.float64, device=dev) if y is not None else None
     mu0 = None
     m_r = 0
     for r0, r1, Xc in chunks:
@@ -52,11 +52,11 @@ def scatter_stats(X: torch.Tensor, ctx: WorkerContext, m_total: int, stream: Any
         m_r += r1 - r0
     ops.gram_mirror(G)
     if mu0 is None:
-        mu0 = torch.zeros(n, dtype=torch.float64, device=dev)
+        mu0 = ops.zeros(n, dtype=torch.float64, device=dev)
     mean_r = s / max(m_r, 1)
     d = mean_r - mu0
     G -= float(m_r) * torch.outer(d, d)  # local scatter about the local mean
-    ys = torch.zeros(2, dtype=torch.float64, device=dev)
+    ys = ops.zeros(2, dtype=torch.float64, device=dev)
     if y is not None:
         yd = y.double()
         ys = torch.stack([yd.sum(), (yd * yd).sum()])

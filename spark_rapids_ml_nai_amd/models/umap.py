@@ -97,7 +97,7 @@ def smooth_knn_dist(dist: torch.Tensor, k: float, n_iter: int = 64, local_connec
     n_nz = (d > 0).sum(1)
     index = int(math.floor(local_connectivity))
     interp = local_connectivity - index
-    rho = torch.zeros(m, dtype=torch.float64, device=d.device)
+    rho = ops.zeros(m, dtype=torch.float64, device=d.device)
     ok = n_nz >= local_connectivity
     if index > 0:
         base = nz_sorted[:, index - 1]
@@ -110,10 +110,10 @@ def smooth_knn_dist(dist: torch.Tensor, k: float, n_iter: int = 64, local_connec
     anyz = n_nz > 0
     rho = torch.where(~ok & anyz, nz_sorted.masked_fill(~torch.isfinite(nz_sorted), -1).max(1).values, rho)
     rho = torch.where(torch.isfinite(rho), rho, torch.zeros_like(rho))
-    lo = torch.zeros(m, dtype=torch.float64, device=d.device)
+    lo = ops.zeros(m, dtype=torch.float64, device=d.device)
     hi = torch.full((m,), float("inf"), dtype=torch.float64, device=d.device)
     mid = torch.ones(m, dtype=torch.float64, device=d.device)
-    done = torch.zeros(m, dtype=torch.bool, device=d.device)
+    done = ops.zeros(m, dtype=torch.bool, device=d.device)
     dd = d[:, 1:] - rho.view(-1, 1)
     for _ in range(n_iter):
         psum = torch.where(dd > 0, torch.exp(-dd / mid.view(-1, 1)), torch.ones_like(dd)).sum(1)
@@ -161,9 +161,9 @@ def fuzzy_union(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n: i
     c2 = torch.cat([cols, rows])
     v2 = torch.cat([vals, vals]).double()
     ur, uc, inv, nu = _coalesce(r2, c2, v2, n)
-    s = torch.zeros(nu, dtype=torch.float64, device=vals.device).index_add_(0, inv, v2)
-    cnt = torch.zeros(nu, dtype=torch.int64, device=vals.device).index_add_(0, inv, torch.ones_like(inv))
-    lp = torch.zeros(nu, dtype=torch.float64, device=vals.device).index_add_(0, inv, torch.log(v2))
+    s = ops.zeros(nu, dtype=torch.float64, device=vals.device).index_add_(0, inv, v2)
+    cnt = ops.zeros(nu, dtype=torch.int64, device=vals.device).index_add_(0, inv, torch.ones_like(inv))
+    lp = ops.zeros(nu, dtype=torch.float64, device=vals.device).index_add_(0, inv, torch.log(v2))
     prod = torch.where(cnt >= 2, torch.exp(lp), torch.zeros_like(lp))
     out = set_op_mix_ratio * (s - prod) + (1.0 - set_op_mix_ratio) * prod
     keep = out > 0
@@ -187,7 +187,7 @@ def categorical_intersection(rows: torch.Tensor, cols: torch.Tensor, vals: torch
     v = torch.where(unknown, v * math.exp(-unknown_dist), v)
     v = torch.where(differ, v * math.exp(-far_dist), v)
     # reset_local_connectivity: normalise rows by their max, then fuzzy union again
-    rmax = torch.zeros(n, dtype=torch.float64, device=v.device).scatter_reduce_(0, rows.long(), v, "amax",
+    rmax = ops.zeros(n, dtype=torch.float64, device=v.device).scatter_reduce_(0, rows.long(), v, "amax",
                                                                                include_self=True)
     v = v / rmax[rows.long()].clamp_min(1e-30)
     return fuzzy_union(rows, cols, v.float(), n)
@@ -381,9 +381,9 @@ def _spectral_dense_device(rows: torch.Tensor, cols: torch.Tensor, vals: torch.T
     Jacobi kernel (``ops.syevj``); the top non-trivial eigenvectors of M are the smallest
     non-trivial ones of the normalised Laplacian (umap-learn's spectral_layout)."""
     dev = vals.device
-    deg = torch.zeros(n, dtype=torch.float64, device=dev).index_add_(0, rows.long(), vals.double())
+    deg = ops.zeros(n, dtype=torch.float64, device=dev).index_add_(0, rows.long(), vals.double())
     dinv = 1.0 / torch.sqrt(deg.clamp_min(1e-30))
-    M = torch.zeros((n, n), dtype=torch.float64, device=dev)
+    M = ops.zeros((n, n), dtype=torch.float64, device=dev)
     M.index_put_((rows.long(), cols.long()), dinv[rows.long()] * vals.double() * dinv[cols.long()], accumulate=True)
     M = 0.5 * (M + M.T)
     w, V = ops.syevj(M)  # descending

@@ -50,8 +50,8 @@ def col_moments(X: torch.Tensor, need_sq: bool = True,
                                                                                     or not q.is_contiguous())):
             raise ValueError("col_moments(out=): contiguous fp64 accumulators")
     else:
-        s = torch.zeros(n, dtype=torch.float64, device=X.device)
-        q = torch.zeros(n, dtype=torch.float64, device=X.device) if need_sq else None
+        s = zeros(n, dtype=torch.float64, device=X.device)
+        q = zeros(n, dtype=torch.float64, device=X.device) if need_sq else None
     name = "srml_col_moments_f32" if X.dtype == torch.float32 else "srml_col_moments_f64"
     if X.dtype not in (torch.float32, torch.float64):
         raise TypeError("col_moments supports fp32/fp64")
@@ -68,7 +68,7 @@ def gram(X: torch.Tensor, mean: Optional[torch.Tensor] = None, out: Optional[tor
     is accumulated, in place; call ``gram_mirror(out)`` once after the last chunk."""
     m, n = X.shape
     if out is None:
-        out = torch.zeros((n, n), dtype=torch.float64, device=X.device)
+        out = zeros((n, n), dtype=torch.float64, device=X.device)
     if not X.is_cuda or X.dtype != torch.float32:
         Xc = X - mean.to(X.dtype) if mean is not None else X
         if X.is_cuda:
@@ -135,11 +135,11 @@ def xw(X: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor] = None) ->
     if k >= XW_MFMA_MIN_K:
         return xw_t(X, W.t().to(torch.float32).contiguous(), bias)
     kk = next(w for w in _XW_WIDTHS if w >= k)
-    Wp = torch.zeros((n, kk), dtype=torch.float32, device=X.device)
+    Wp = zeros((n, kk), dtype=torch.float32, device=X.device)
     Wp[:, :k] = W.to(torch.float32)
     bp = None
     if bias is not None:
-        bp = torch.zeros(kk, dtype=torch.float32, device=X.device)
+        bp = zeros(kk, dtype=torch.float32, device=X.device)
         bp[:k] = bias.to(torch.float32)
     out = torch.empty((m, kk), dtype=torch.float32, device=X.device)
     native.call("srml_xw_f32", X.data_ptr(), m, n, X.stride(0), Wp.data_ptr(), kk,
@@ -180,7 +180,7 @@ def dgemm(A: torch.Tensor, B: torch.Tensor, ta: bool = False, tb: bool = False, 
     K = A.shape[0] if ta else A.shape[1]
     N = B.shape[0] if tb else B.shape[1]
     if out is None:
-        out = torch.zeros((M, N), dtype=torch.float64, device=A.device)
+        out = zeros((M, N), dtype=torch.float64, device=A.device)
         beta = 0.0
     if not A.is_cuda:
         a = A.double().T if ta else A.double()
@@ -240,7 +240,7 @@ def xtv(X: torch.Tensor, V: torch.Tensor, out: Optional[torch.Tensor] = None) ->
     V2 = V.reshape(m, -1)
     k = V2.shape[1]
     if out is None:
-        out = torch.zeros((n, k), dtype=torch.float64, device=X.device)
+        out = zeros((n, k), dtype=torch.float64, device=X.device)
     if not X.is_cuda:
         out += X.double().T @ V2.double()
         return out
@@ -268,7 +268,7 @@ def xtv(X: torch.Tensor, V: torch.Tensor, out: Optional[torch.Tensor] = None) ->
     for c0 in range(0, k, 4):
         kk = min(4, k - c0)
         Vc = _c(V2[:, c0: c0 + kk].to(torch.float32))
-        tmp = torch.zeros((n, kk), dtype=torch.float64, device=X.device)
+        tmp = zeros((n, kk), dtype=torch.float64, device=X.device)
         native.call("srml_xtv_f32", X.data_ptr(), m, n, X.stride(0), Vc.data_ptr(), kk, Vc.stride(0), tmp.data_ptr(),
                     native.stream(X.device))
         out[:, c0: c0 + kk] += tmp
@@ -315,7 +315,7 @@ def logreg_binary_loss_grad(X: torch.Tensor, y: torch.Tensor, w: torch.Tensor, b
         loss = torch.nn.functional.softplus(z).sum() - (yd * z).sum()
         return torch.cat([Xd.T @ r, r.sum().view(1), loss.view(1)])
     X = _c(X)
-    out = torch.zeros(n + 2, dtype=torch.float64, device=X.device) if out is None else zero_(out)
+    out = zeros(n + 2, dtype=torch.float64, device=X.device) if out is None else zero_(out)
     wf = _c(w.to(device=X.device, dtype=torch.float64))
     yf = _c(y.to(torch.float32))
     ws = logreg_workspace(X)
@@ -427,7 +427,7 @@ def split_bf16x3(X: torch.Tensor, row_multiple: int = 128, tiled: bool = False,
         X = X.float() - mu.float().view(1, -1)
     rows_pad = max(row_multiple, (m + row_multiple - 1) // row_multiple * row_multiple)
     if not X.is_cuda or X.dtype != torch.float32:
-        P = torch.zeros((3, rows_pad, kp), dtype=torch.bfloat16, device=X.device)
+        P = zeros((3, rows_pad, kp), dtype=torch.bfloat16, device=X.device)
         r = X.float()
         for p in range(3):
             P[p, :m, :n] = r.to(torch.bfloat16)
@@ -490,7 +490,7 @@ def _nearest_centroid_certified(XP: torch.Tensor, X: torch.Tensor, m: int, k: in
     labels = torch.empty(m, dtype=torch.int32, device=dev)
     dist = torch.empty(m, dtype=torch.float32, device=dev)
     flagged = torch.empty(m, dtype=torch.int32, device=dev)
-    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    cnt = zeros(1, dtype=torch.int32, device=dev)
     native.call("srml_split_top2_select", keys.data_ptr(), lob.data_ptr(), m, nslot, xn.data_ptr(), cg.data_ptr(),
                 labels.data_ptr(), dist.data_ptr(), flagged.data_ptr(), cnt.data_ptr(), st)
     del keys, lob
@@ -557,7 +557,7 @@ class F16Planes:
         dev = X.device
         st = native.stream(dev)
         self.xnorm = torch.empty(m, dtype=torch.float32, device=dev)
-        amax = torch.zeros(1, dtype=torch.int32, device=dev)
+        amax = zeros(1, dtype=torch.int32, device=dev)
         native.call("srml_row_sqnorm_centered_amax_f32", X.data_ptr(), m, n, X.stride(0), self.mu.data_ptr(),
                     self.xnorm.data_ptr(), amax.data_ptr(), st)
         a = float(amax.view(torch.float32).item())
@@ -574,7 +574,7 @@ class F16Planes:
         self.kp = (n + 15) // 16 * 16
         self.rows_pad = max(256, (m + 255) // 256 * 256)
         self.P = torch.empty((self.rows_pad // 256, self.kp // 16, 256, 16), dtype=torch.float16, device=dev)
-        self.ovf = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.ovf = zeros(1, dtype=torch.int32, device=dev)
         native.call("srml_split_f16_tiled_centered", X.data_ptr(), m, n, X.stride(0), self.mu.data_ptr(), self.kp,
                     self.rows_pad, self.scale, self.P.data_ptr(), self.ovf.data_ptr(), st)
         self.tau = certify_tau16(n)
@@ -650,23 +650,27 @@ def nearest_centroid_f16(F: F16Planes, C: torch.Tensor, approx: bool = False) ->
         X = F.X
         assert X.stride(1) == 1
         cap = F16_CAND_CAP
-        ccount = torch.zeros(nf, dtype=torch.int32, device=dev)
         cand = torch.empty(nf * cap, dtype=torch.int32, device=dev)
-        scratch = torch.zeros(1, dtype=torch.int32, device=dev)
         stepr = split_rows_per_launch(k)
+        plane = F.P is not None and os.environ.get("SRML_F16_GATHER", "plane") == "plane"
+        # plane gather: the same launch gathers the rows' norms and zeroes their candidate counters
+        ccount = torch.empty(nf, dtype=torch.int32, device=dev) if plane else zeros(nf, dtype=torch.int32,
+                                                                                          device=dev)
+        scratch = None if plane else zeros(1, dtype=torch.int32, device=dev)
         for q0 in range(0, nf, stepr):
             nq = min(stepr, nf - q0)
             rq = rows[q0: q0 + nq]
             rp = max(256, (nq + 255) // 256 * 256)
             Pr = torch.empty((rp // 256, F.kp // 16, 256, 16), dtype=torch.float16, device=dev)
-            if F.P is not None and os.environ.get("SRML_F16_GATHER", "plane") == "plane":
+            if plane:
                 # the flagged rows' slots of the filter's own plane (32 B per k step, no re-conversion)
-                native.call("srml_f16_plane_gather_rows", F.P.data_ptr(), F.rows_pad, F.kp, rq.data_ptr(), nq, rp,
-                            Pr.data_ptr(), st)
+                xr = torch.empty(nq, dtype=torch.float32, device=dev)
+                native.call("srml_f16_plane_gather_rows_ex", F.P.data_ptr(), F.rows_pad, F.kp, rq.data_ptr(), nq, rp,
+                            Pr.data_ptr(), F.xnorm.data_ptr(), xr.data_ptr(), ccount[q0:].data_ptr(), st)
             else:
                 native.call("srml_split_f16_tiled_centered_rows", X.data_ptr(), X.stride(0), rq.data_ptr(), nq, F.n,
                             F.mu.data_ptr(), F.kp, rp, F.scale, Pr.data_ptr(), scratch.data_ptr(), st)
-            xr = F.xnorm.index_select(0, rq.long())
+                xr = F.xnorm.index_select(0, rq.long())
             native.call("srml_nearest_centroid_f16_cand", Pr.data_ptr(), nq, rp, F.kp, CP.data_ptr(), k, crows,
                         cn.data_ptr(), cg.data_ptr(), xr.data_ptr(), dscale, xadd, thr[q0:].data_ptr(),
                         ccount[q0:].data_ptr(), cand[q0 * cap:].data_ptr(), cap, st)
@@ -800,7 +804,7 @@ def kmeanspp_gram(G: torch.Tensor, w: torch.Tensor, k: int, seed: int, trials: O
         ldg = nc
         if nc % 4 and nc <= 4096 and L <= 8:  # the register kernel reads 4-candidate groups from 32-B aligned rows
             ldg = nc + (-nc) % 4
-            Gp = torch.zeros((nc, ldg), dtype=torch.float64, device=G.device)
+            Gp = zeros((nc, ldg), dtype=torch.float64, device=G.device)
             Gp[:, :nc] = Gd
             Gd = Gp
         native.call("srml_kmeanspp_gram", Gd.data_ptr(), nc, ldg, _c(w.double()).data_ptr(), int(k), L, seed,
@@ -862,7 +866,7 @@ def label_counts(labels: torch.Tensor, k: int) -> torch.Tensor:
     if not lab.is_cuda or k > int(native.lib().srml_label_sort_kmax()) + 1:
         ok = lab[(lab >= 0) & (lab < k)].long()
         return torch.bincount(ok, minlength=k)[:k]
-    counts = torch.zeros(k, dtype=torch.int64, device=lab.device)
+    counts = zeros(k, dtype=torch.int64, device=lab.device)
     native.call("srml_label_counts", lab.data_ptr(), lab.shape[0], int(k), counts.data_ptr(), native.stream(lab.device))
     return counts
 
@@ -924,7 +928,7 @@ def kmeans_lloyd_small(X: torch.Tensor, C: torch.Tensor, cnorm: Optional[torch.T
         raise ValueError("kmeans_lloyd_small: mu needs the MFMA kernel")
     if mfma:
         if with_sums and out is None:
-            out = torch.zeros(k * n + k + 1, dtype=torch.float64, device=dev)
+            out = zeros(k * n + k + 1, dtype=torch.float64, device=dev)
         muc = _c(mu.to(device=dev, dtype=torch.float32).view(-1)) if mu is not None else None
         native.call("srml_kmeans_lloyd_mfma", X.data_ptr(), m, n, X.stride(0), C.data_ptr(), k, cn.data_ptr(),
                     labels.data_ptr() if rows_out else None, dist.data_ptr() if rows_out else None,
@@ -936,9 +940,9 @@ def kmeans_lloyd_small(X: torch.Tensor, C: torch.Tensor, cnorm: Optional[torch.T
         return labels, dist, out[: k * n].view(k, n), out[k * n: k * n + k].long(), out[k * n + k:]
     sums = counts = inertia = None
     if with_sums:
-        sums = torch.zeros((k, n), dtype=torch.float64, device=dev)
-        counts = torch.zeros(k, dtype=torch.int32, device=dev)
-        inertia = torch.zeros(1, dtype=torch.float64, device=dev)
+        sums = zeros((k, n), dtype=torch.float64, device=dev)
+        counts = zeros(k, dtype=torch.int32, device=dev)
+        inertia = zeros(1, dtype=torch.float64, device=dev)
     native.call("srml_kmeans_lloyd_small", X.data_ptr(), m, n, X.stride(0), C.data_ptr(), k, cn.data_ptr(),
                 labels.data_ptr(), dist.data_ptr(), sums.data_ptr() if with_sums else None,
                 counts.data_ptr() if with_sums else None, inertia.data_ptr() if with_sums else None,
@@ -950,6 +954,82 @@ def kmeans_lloyd_small(X: torch.Tensor, C: torch.Tensor, cnorm: Optional[torch.T
         out[k * n: k * n + k].copy_(counts)
         out[k * n + k:].copy_(inertia)
     return labels, dist, sums, counts.long(), inertia
+
+
+class LloydBook:
+    """Device bookkeeping of the large-k Lloyd loop (``lloyd_book.hip``), the loop's local buffer
+    ``L`` = [sums (k n) | counts (k) | inertia] in fp64 being updated in place:
+
+    * ``moved(labels, prev)``: number of rows whose label changed (one read-back);
+    * ``delta_into(X, labels, prev, nm, L)``: L's sums / counts += the moved rows' change (rows
+      entering their new cluster, ``~row`` leaving the old one, ONE label sort of both lists, the
+      sorted-sum kernel reading X through the row list);
+    * ``full_into(X, labels, L)``: L's sums / counts of all rows (label sort + sorted sums);
+    * ``inertia_into(d2, L)``: L's inertia = sum of the squared distances (fp64, fixed order);
+    * ``update(G, C)``: C (fp64, in place) = sums / counts of the all-reduced buffer G (empty
+      clusters keep theirs) -> (max squared centre shift, inertia), one read-back.
+
+    No torch library kernels run in an iteration (the torch bookkeeping was ~37 launches each)."""
+
+    def __init__(self, X: torch.Tensor, k: int) -> None:
+        self.m, self.n = X.shape
+        self.k = k
+        dev = X.device
+        self.dev = dev
+        lib = native.lib()
+        self.blk = torch.empty(max(1, int(lib.srml_lloyd_moved_ws(max(1, self.m)))), dtype=torch.int64, device=dev)
+        self.dtot = torch.empty(1, dtype=torch.int64, device=dev)
+        self.sum_ws = torch.empty(int(lib.srml_sum_f32_ws()), dtype=torch.float64, device=dev)
+        self.part = torch.empty(max(1, k), dtype=torch.float64, device=dev)
+        self.out = torch.empty(2, dtype=torch.float64, device=dev)
+        self.h_out = torch.empty(2, dtype=torch.float64, pin_memory=True)
+        self.h_tot = torch.empty(1, dtype=torch.int64, pin_memory=True)
+        self.sorted_ok = X.dtype == torch.float32 and k <= int(lib.srml_label_sort_kmax())
+
+    def _read(self, host: torch.Tensor, dev_t: torch.Tensor) -> torch.Tensor:
+        host.copy_(dev_t, non_blocking=True)
+        torch.cuda.current_stream(self.dev).synchronize()
+        return host
+
+    def moved(self, labels: torch.Tensor, prev: torch.Tensor) -> int:
+        native.call("srml_lloyd_moved_count", labels.data_ptr(), prev.data_ptr(), self.m, self.blk.data_ptr(),
+                    self.dtot.data_ptr(), native.stream(self.dev))
+        return int(self._read(self.h_tot, self.dtot)[0])
+
+    def delta_into(self, X: torch.Tensor, labels: torch.Tensor, prev: torch.Tensor, nm: int,
+                   L: torch.Tensor) -> None:
+        k, n, st = self.k, self.n, native.stream(self.dev)
+        rows2 = torch.empty(2 * nm, dtype=torch.int32, device=self.dev)
+        lab2 = torch.empty(2 * nm, dtype=torch.int32, device=self.dev)
+        native.call("srml_lloyd_moved_compact", labels.data_ptr(), prev.data_ptr(), self.m, self.blk.data_ptr(), nm,
+                    rows2.data_ptr(), lab2.data_ptr(), L[k * n:].data_ptr(), st)
+        perm, _, slab = label_sort(lab2, k)
+        native.call("srml_kmeans_accumulate_sorted_rows_f32", X.data_ptr(), 2 * nm, n, X.stride(0), perm.data_ptr(),
+                    rows2.data_ptr(), slab.data_ptr(), L.data_ptr(), st)
+
+    def full_into(self, X: torch.Tensor, labels: torch.Tensor, L: torch.Tensor) -> None:
+        k, n = self.k, self.n
+        if not self.sorted_ok:
+            sums, counts = cluster_sums(X, labels, k)
+            L[: k * n].copy_(sums.view(-1))
+            L[k * n: k * n + k].copy_(counts)
+            return
+        st = native.stream(self.dev)
+        perm, off, slab = label_sort(labels, k)
+        native.call("srml_memset_async", L.data_ptr(), 0, k * n * 8, st)
+        native.call("srml_kmeans_accumulate_sorted_rows_f32", X.data_ptr(), self.m, n, X.stride(0), perm.data_ptr(),
+                    None, slab.data_ptr(), L.data_ptr(), st)
+        native.call("srml_counts_from_offsets", off.data_ptr(), k, L[k * n:].data_ptr(), st)
+
+    def inertia_into(self, d2: torch.Tensor, L: torch.Tensor) -> None:
+        native.call("srml_sum_f32_f64", d2.data_ptr(), d2.shape[0], self.sum_ws.data_ptr(), L[-1:].data_ptr(),
+                    native.stream(self.dev))
+
+    def update(self, G: torch.Tensor, C: torch.Tensor) -> Tuple[float, float]:
+        native.call("srml_lloyd_centre_update", G.data_ptr(), self.k, self.n, C.data_ptr(), self.part.data_ptr(),
+                    self.out.data_ptr(), native.stream(self.dev))
+        h = self._read(self.h_out, self.out)
+        return float(h[0]), float(h[1])
 
 
 def kmeans_small_update(buf: torch.Tensor, k: int, n: int, C64: torch.Tensor, C32: torch.Tensor,
@@ -965,7 +1045,7 @@ def cluster_sums(X: torch.Tensor, labels: torch.Tensor, k: int) -> Tuple[torch.T
     """(sums fp64 [k, n], counts int64 [k]) of rows grouped by label."""
     m, n = X.shape
     if not X.is_cuda or X.dtype not in (torch.float32, torch.float64):
-        sums = torch.zeros((k, n), dtype=torch.float64, device=X.device)
+        sums = zeros((k, n), dtype=torch.float64, device=X.device)
         sums.index_add_(0, labels.long(), X.double())
         counts = torch.bincount(labels.long(), minlength=k)
         return sums, counts
@@ -985,16 +1065,16 @@ def cluster_sums(X: torch.Tensor, labels: torch.Tensor, k: int) -> Tuple[torch.T
         native.call(name, X.data_ptr(), m, n, X.stride(0), perm.data_ptr(), off.data_ptr(), k,
                     sums.data_ptr(), splits, ws.data_ptr() if ws is not None else None, native.stream(X.device))
         return sums, counts
-    counts = torch.zeros(k, dtype=torch.int32, device=X.device)
+    counts = zeros(k, dtype=torch.int32, device=X.device)
     st = native.stream(X.device)
     if k * n * 4 + k * 4 <= 64 * 1024:
-        sums = torch.zeros((k, n), dtype=torch.float64, device=X.device)
+        sums = zeros((k, n), dtype=torch.float64, device=X.device)
         native.call("srml_kmeans_accumulate_f32", X.data_ptr(), m, n, X.stride(0), lab.data_ptr(), k, sums.data_ptr(),
                     None, counts.data_ptr(), st)
         return sums, counts.long()
     # large k*n: visit rows in label-sorted order (segment sums, ~(m/256 + k) * n fp64 atomics)
     perm, off, slab = label_sort(lab, k)
-    sums = torch.zeros((k, n), dtype=torch.float64, device=X.device)
+    sums = zeros((k, n), dtype=torch.float64, device=X.device)
     native.call("srml_kmeans_accumulate_sorted_f32", X.data_ptr(), m, n, X.stride(0), perm.data_ptr(),
                 slab.data_ptr(), sums.data_ptr(), st)
     return sums, off[1:] - off[:-1]
@@ -1012,7 +1092,7 @@ def cluster_sums_rows(X: torch.Tensor, rows: torch.Tensor, labels: torch.Tensor,
     lab = _c(labels.to(torch.int32))
     perm, off, slab = label_sort(lab, k)
     prow = _c(rows.to(torch.int32).index_select(0, perm.long()))
-    sums = torch.zeros((k, n), dtype=torch.float64, device=X.device)
+    sums = zeros((k, n), dtype=torch.float64, device=X.device)
     native.call("srml_kmeans_accumulate_sorted_f32", X.data_ptr(), int(rows.shape[0]), n, X.stride(0),
                 prow.data_ptr(), slab.data_ptr(), sums.data_ptr(), native.stream(X.device))
     return sums, off[1:] - off[:-1]
@@ -1035,7 +1115,7 @@ def cluster_delta_sums(X: torch.Tensor, rows: torch.Tensor, new_lab: torch.Tenso
     rows2 = torch.cat([r32, torch.bitwise_not(r32)])
     perm, off, slab = label_sort(lab2, k)
     prow = _c(rows2.index_select(0, perm.long()))
-    sums = torch.zeros((k, n), dtype=torch.float64, device=X.device)
+    sums = zeros((k, n), dtype=torch.float64, device=X.device)
     native.call("srml_kmeans_accumulate_sorted_f32", X.data_ptr(), int(prow.shape[0]), n, X.stride(0),
                 prow.data_ptr(), slab.data_ptr(), sums.data_ptr(), native.stream(X.device))
     return sums, label_counts(new_lab, k) - label_counts(old_lab, k)
@@ -1218,7 +1298,7 @@ def rf_hist(bins: torch.Tensor, idx: torch.Tensor, label: torch.Tensor, wcnt: Op
         if items.shape[0] == 0:
             return hist
     elif not bins.is_cuda or items.shape[0] == 0:
-        hist = torch.zeros((nodes, nf, B, S), dtype=hdt, device=dev)
+        hist = zeros((nodes, nf, B, S), dtype=hdt, device=dev)
         if items.shape[0] == 0:
             return hist
     elif exclusive is not None:
@@ -1228,7 +1308,7 @@ def rf_hist(bins: torch.Tensor, idx: torch.Tensor, label: torch.Tensor, wcnt: Op
         if exclusive["multi_nodes"].numel():
             hist.index_fill_(0, exclusive["multi_nodes"], 0)
     else:
-        hist = torch.zeros((nodes, nf, B, S), dtype=hdt, device=dev)
+        hist = zeros((nodes, nf, B, S), dtype=hdt, device=dev)
     if not bins.is_cuda:
         it = items.cpu().numpy()
         for node, rb, re, fc in it:
@@ -1427,6 +1507,75 @@ def rf_route_segments(bins: torch.Tensor, idx: torch.Tensor, bounds: torch.Tenso
     return keys
 
 
+def rf_left_totals(hist: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """(C, S) fp64 class totals of every node's left child under its best split (zeros without
+    one): the winning feature's histogram (C, nslot, B, S) summed up to the split bin
+    (``srml_rf_left_totals``; torch on the host)."""
+    C, nslot, B, S = hist.shape
+    if hist.is_cuda and hist.dtype in (torch.int32, torch.float64) and hist.is_contiguous():
+        left = torch.empty((C, S), dtype=torch.float64, device=hist.device)
+        native.call("srml_rf_left_totals", hist.data_ptr(), int(hist.dtype == torch.float64), C, nslot, B, S,
+                    _c(out.double()).data_ptr(), left.data_ptr(), native.stream(hist.device))
+        return left
+    ok = out[:, 1] >= 0
+    slot = torch.where(ok, out[:, 1], torch.zeros_like(out[:, 1])).long()
+    b = torch.where(ok, out[:, 2], torch.zeros_like(out[:, 2])).long()
+    ar = torch.arange(C, device=hist.device)
+    left = hist[ar, slot].double().cumsum(1)[ar, b]
+    return torch.where(ok.view(-1, 1), left, torch.zeros_like(left))
+
+
+def rf_gather_feature(feats: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """(C, 1) winning feature ids (``feats[c, out[c, 1]]``, slot clamped at 0) in out's dtype."""
+    C = out.shape[0]
+    if feats.is_cuda and feats.dtype == torch.int32 and out.dtype == torch.float64 and feats.stride(1) == 1:
+        fsel = torch.empty((C, 1), dtype=torch.float64, device=out.device)
+        native.call("srml_rf_gather_feature", feats.data_ptr(), feats.stride(0), _c(out).data_ptr(), C,
+                    fsel.data_ptr(), native.stream(out.device))
+        return fsel
+    return feats[:C].gather(1, out[:, 1].clamp_min(0).long().view(-1, 1)).to(out.dtype)
+
+
+def rf_decide(out: torch.Tensor, fsel: torch.Tensor, cand: torch.Tensor, L: int, left: Optional[torch.Tensor],
+              tot: Optional[torch.Tensor]) -> Tuple[torch.Tensor, ...]:
+    """One level's split decisions on the device (``srml_rf_decide``): candidate j (segment
+    cand[j]) splits iff out[j, 1] >= 0, its children are segments 2 r, 2 r + 1 with r its rank among
+    the splitting candidates. Returns (node_feature, node_bin, child_base) (L int32 each: -1 / 0 / 0
+    off the splits) and, with ``left`` / ``tot`` (classification), the children's totals (2C, S)
+    (left = prefix, right = parent - left; rows past the real children zero)."""
+    dev = out.device
+    C = out.shape[0]
+    st = native.stream(dev)
+    node = torch.empty((3, L), dtype=torch.int32, device=dev)
+    native.call("srml_memset_async", node[0].data_ptr(), 0xFF, L * 4, st)
+    native.call("srml_memset_async", node[1].data_ptr(), 0, 2 * L * 4, st)
+    pos = torch.empty(max(C, 1), dtype=torch.int32, device=dev)
+    k_d = torch.empty(1, dtype=torch.int64, device=dev)
+    tot_n = None
+    if left is not None:
+        S = int(left.shape[1])
+        tot_n = torch.empty((2 * C, S), dtype=torch.float64, device=dev)
+    native.call("srml_rf_decide", _c(out).data_ptr(), _c(fsel).data_ptr(), _c(cand).data_ptr(), C, pos.data_ptr(),
+                k_d.data_ptr(), node[0].data_ptr(), node[1].data_ptr(), node[2].data_ptr(),
+                _c(left).data_ptr() if left is not None else None,
+                _c(tot.double()).data_ptr() if left is not None else None,
+                int(left.shape[1]) if left is not None else 0, tot_n.data_ptr() if tot_n is not None else None, st)
+    return node[0], node[1], node[2], tot_n
+
+
+def rf_level_pack(bounds: torch.Tensor, tot_n: torch.Tensor, regression: bool, crit: int, out: torch.Tensor,
+                  fsel: torch.Tensor) -> torch.Tensor:
+    """The level's read-back buffer (``srml_rf_level_pack``, fp64, on the device): [child bounds
+    (2C + 1) | per child [leaf value(s) | weight | impurity] (forest._seg_stats) | out (6C) | fsel]."""
+    C = out.shape[0]
+    S = int(tot_n.shape[1])
+    V2 = 3 if regression else S + 2
+    hb = torch.empty(2 * C + 1 + 2 * C * V2 + 7 * C, dtype=torch.float64, device=out.device)
+    native.call("srml_rf_level_pack", _c(bounds).data_ptr(), C, _c(tot_n).data_ptr(), S, int(bool(regression)),
+                int(crit), _c(out).data_ptr(), _c(fsel).data_ptr(), hb.data_ptr(), native.stream(out.device))
+    return hb
+
+
 def rf_sample_features(C: int, n: int, nf: int, seed: int, device: torch.device) -> torch.Tensor:
     """(C, nf) int32: per node a uniform random subset of nf of n features, ascending
     (``srml_rf_sample_features``: Floyd's algorithm for sparse subsets, nf <= n / 8, else
@@ -1435,7 +1584,7 @@ def rf_sample_features(C: int, n: int, nf: int, seed: int, device: torch.device)
     if device.type != "cuda":
         rng = np.random.default_rng(seed)
         return torch.from_numpy(np.sort(np.stack([rng.choice(n, nf, replace=False) for _ in range(C)]), 1)
-                                .astype(np.int32)) if C else torch.zeros((0, nf), dtype=torch.int32)
+                                .astype(np.int32)) if C else zeros((0, nf), dtype=torch.int32)
     out = torch.empty((C, nf), dtype=torch.int32, device=device)
     native.call("srml_rf_sample_features", C, n, nf, seed, out.data_ptr(), native.stream(device))
     return out
@@ -1533,7 +1682,7 @@ def rf_node_stats(idx: torch.Tensor, wpos: torch.Tensor, label: torch.Tensor, bo
             vals = torch.stack([wr, wr * yr, wr * yr * yr], 0)
         else:
             vals = torch.stack([wr * (yr.long() == c) for c in range(S)], 0)
-        cs = torch.cat([torch.zeros((K, 1), dtype=torch.float64), vals.cumsum(1)], 1)
+        cs = torch.cat([zeros((K, 1), dtype=torch.float64), vals.cumsum(1)], 1)
         b = bounds.long()
         return (cs[:, b[1:]] - cs[:, b[:-1]]).T.contiguous()
     if deterministic():  # one block per segment, fixed-order reduction, no atomics
@@ -1542,7 +1691,7 @@ def rf_node_stats(idx: torch.Tensor, wpos: torch.Tensor, label: torch.Tensor, bo
                     _c(label.float()).data_ptr(), _c(bounds.long()).data_ptr(), nseg, int(S), int(regression),
                     out.data_ptr(), native.stream(dev))
         return out
-    out = torch.zeros((nseg, K), dtype=torch.float64, device=dev)
+    out = zeros((nseg, K), dtype=torch.float64, device=dev)
     native.call("srml_rf_node_stats", idx.data_ptr(), _c(wpos.float()).data_ptr(), _c(label.float()).data_ptr(),
                 int(idx.shape[0]), _c(bounds.long()).data_ptr(), nseg, int(S), int(regression), out.data_ptr(),
                 native.stream(dev))
@@ -1559,7 +1708,7 @@ def rf_predict(X: torch.Tensor, roots: torch.Tensor, feature: torch.Tensor, thre
     T = roots.shape[0]
     if not X.is_cuda or X.dtype != torch.float32 or S > 32:
         Xf = X.float()
-        out = torch.zeros((m, S), dtype=torch.float32, device=X.device)
+        out = zeros((m, S), dtype=torch.float32, device=X.device)
         leaves = torch.empty((m, T), dtype=torch.int32, device=X.device) if want_leaves else None
         rows = torch.arange(m, device=X.device)
         for t in range(T):
@@ -1741,7 +1890,7 @@ def _ivf_large_k(Q: torch.Tensor, nq: int, probes: torch.Tensor, list_off: torch
     lo = _c(list_off.long())
     ql = _c(qlist.int()) if qlist is not None else None
     nprobe = int(pr.shape[1])
-    cmax = torch.zeros(1, dtype=torch.int64, device=dev)
+    cmax = zeros(1, dtype=torch.int64, device=dev)
     native.call("srml_ivf_candidate_max", pr.data_ptr(), nprobe, ql.data_ptr() if ql is not None else None, nq,
                 lo.data_ptr(), cmax.data_ptr(), st)
     L = int(cmax.item())
@@ -2030,7 +2179,7 @@ def dbscan_degree(X: torch.Tensor, xnorm: torch.Tensor, eps2: float, t0: int, t1
     """eps-neighbourhood sizes (self included) accumulated over tile pairs [t0, t1) into int32 counts."""
     N = X.shape[0]
     if counts is None:
-        counts = torch.zeros(N, dtype=torch.int32, device=X.device)
+        counts = zeros(N, dtype=torch.int32, device=X.device)
     if not X.is_cuda or X.dtype != torch.float32:
         for diag, r0, c0, d in _db_tiles(X, xnorm, eps2, t0, t1):
             adj = torch.isfinite(d)
@@ -2223,7 +2372,7 @@ def umap_fuzzy_union_knn(idx: torch.Tensor, w: torch.Tensor, mix: float = 1.0
     dev = ix.device
     keys = torch.empty(2 * m * kk, dtype=torch.int64, device=dev)
     vals = torch.empty(2 * m * kk, dtype=torch.float32, device=dev)
-    kept = torch.zeros(1, dtype=torch.int64, device=dev)
+    kept = zeros(1, dtype=torch.int64, device=dev)
     native.call("srml_umap_fuzzy_union_knn", ix.data_ptr(), wv.data_ptr(), m, kk, kk, float(mix), keys.data_ptr(),
                 vals.data_ptr(), kept.data_ptr(), native.stream(dev))
     # absent entries carry key m*m: after the (row, col) sort they trail the kept ones
@@ -2348,10 +2497,10 @@ def spd_solve(A: torch.Tensor, b: torch.Tensor) -> Tuple[torch.Tensor, bool]:
     if not A.is_cuda:
         L, info = torch.linalg.cholesky_ex(A.double())
         if int(info) != 0:
-            return torch.zeros(n, dtype=torch.float64), False
+            return zeros(n, dtype=torch.float64), False
         return torch.cholesky_solve(b.double().view(-1, 1), L).view(-1), True
     st = native.stream(A.device)
-    info = torch.zeros(1, dtype=torch.int32, device=A.device)
+    info = zeros(1, dtype=torch.int32, device=A.device)
     if n * 8 <= 110 * 1024:
         # augmented factorisation of [A b; b^T 1]: the trailing updates carry b along, so the last
         # row of the factor is z^T = (L^-1 b)^T and only the backward sweep L^T x = z remains. A
@@ -2379,7 +2528,7 @@ def spd_factor(A: torch.Tensor) -> Tuple[torch.Tensor, bool]:
         L, info = torch.linalg.cholesky_ex(A.double())
         return L, int(info) == 0
     L = A.double().contiguous().clone()
-    info = torch.zeros(1, dtype=torch.int32, device=A.device)
+    info = zeros(1, dtype=torch.int32, device=A.device)
     native.call("srml_potrf_f64", L.data_ptr(), L.shape[0], L.stride(0), info.data_ptr(), native.stream(A.device))
     return L, int(info.item()) == 0
 
@@ -2397,14 +2546,14 @@ def cd_gram(A: torch.Tensor, b: torch.Tensor, l1: torch.Tensor, l2: torch.Tensor
             w0: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, int]:
     """Cyclic coordinate descent: argmin 1/2 w'Aw - b'w + sum l1|w| + 1/2 sum l2 w^2 (fp64)."""
     n = A.shape[0]
-    w = (torch.zeros(n, dtype=torch.float64, device=A.device) if w0 is None else w0.double().clone()).contiguous()
+    w = (zeros(n, dtype=torch.float64, device=A.device) if w0 is None else w0.double().clone()).contiguous()
     if A.is_cuda and 2 * n * 8 > 150 * 1024:
         # wider than the LDS-resident kernels: global-memory block-cyclic sweeps, one launch
         # sequence per sweep, the convergence word read once per sweep
         A = A.double().contiguous()
-        g = torch.zeros(n, dtype=torch.float64, device=A.device)
-        dv = torch.zeros(64, dtype=torch.float64, device=A.device)
-        stats = torch.zeros(2, dtype=torch.float64, device=A.device)
+        g = zeros(n, dtype=torch.float64, device=A.device)
+        dv = zeros(64, dtype=torch.float64, device=A.device)
+        stats = zeros(2, dtype=torch.float64, device=A.device)
         bb, l1c, l2c = _c(b.double()), _c(l1.double()), _c(l2.double())
         st = native.stream(A.device)
         it = 0
@@ -2440,7 +2589,7 @@ def cd_gram(A: torch.Tensor, b: torch.Tensor, l1: torch.Tensor, l2: torch.Tensor
                 break
         return torch.from_numpy(wh).to(A.device), it
     A = A.double().contiguous()
-    iters = torch.zeros(1, dtype=torch.int32, device=A.device)
+    iters = zeros(1, dtype=torch.int32, device=A.device)
     native.call("srml_cd_gram_f64", A.data_ptr(), n, A.stride(0), _c(b.double()).data_ptr(), _c(l1.double()).data_ptr(),
                 _c(l2.double()).data_ptr(), w.data_ptr(), int(max_iter), float(tol), iters.data_ptr(),
                 native.stream(A.device))
@@ -2494,7 +2643,7 @@ def csr_logreg_binary_loss_grad(A, y: torch.Tensor, w: torch.Tensor, b: float,
         g = (Xs.t() @ r.view(-1, 1)).view(-1)
         return torch.cat([g, r.sum().view(1), loss.view(1)])
     _csr_check(A)
-    out = torch.zeros(n + 2, dtype=torch.float64, device=A.data.device) if out is None else zero_(out)
+    out = zeros(n + 2, dtype=torch.float64, device=A.data.device) if out is None else zero_(out)
     wf = _c(w.to(device=A.data.device, dtype=torch.float64))
     yf = _c(y.to(torch.float32))
     native.call("srml_csr_logreg_binary_" + _sfx(A), A.indptr.data_ptr(), A.indices.data_ptr(), A.data.data_ptr(),
@@ -2533,7 +2682,7 @@ def csr_spmtm(A, R: torch.Tensor) -> torch.Tensor:
         return (_csr_torch(A).t() @ R.to(A.data.dtype)).double()
     _csr_check(A)
     Rf = _c(R.to(torch.float32))
-    out = torch.zeros(n, K, dtype=torch.float64, device=A.data.device)
+    out = zeros(n, K, dtype=torch.float64, device=A.data.device)
     st = native.stream(A.data.device)
     for c0 in range(0, K, 16):
         kk = min(16, K - c0)
@@ -2547,7 +2696,7 @@ def csr_row_sums(A) -> torch.Tensor:
     m = A.shape[0]
     if not A.data.is_cuda:
         rows = torch.repeat_interleave(torch.arange(m), (A.indptr[1:] - A.indptr[:-1]).cpu())
-        return torch.zeros(m, dtype=torch.float64).index_add_(0, rows, A.data.double().cpu())
+        return zeros(m, dtype=torch.float64).index_add_(0, rows, A.data.double().cpu())
     out = torch.empty(m, dtype=torch.float64, device=A.data.device)
     native.call("srml_csr_row_sums_f32", A.indptr.data_ptr(), _c(A.data.float()).data_ptr(), m, out.data_ptr(),
                 native.stream(A.data.device))
@@ -2561,12 +2710,12 @@ def csr_col_moments(A) -> Tuple[torch.Tensor, torch.Tensor]:
     if not A.data.is_cuda:
         d = A.data.double()
         cols = A.indices.long()
-        s = torch.zeros(n, dtype=torch.float64).index_add_(0, cols, d)
-        q = torch.zeros(n, dtype=torch.float64).index_add_(0, cols, d * d)
+        s = zeros(n, dtype=torch.float64).index_add_(0, cols, d)
+        q = zeros(n, dtype=torch.float64).index_add_(0, cols, d * d)
         return s, q
     _csr_check(A)
-    s = torch.zeros(n, dtype=torch.float64, device=dev)
-    q = torch.zeros(n, dtype=torch.float64, device=dev)
+    s = zeros(n, dtype=torch.float64, device=dev)
+    q = zeros(n, dtype=torch.float64, device=dev)
     native.call("srml_csr_col_moments_" + _sfx(A), A.indices.data_ptr(), A.data.data_ptr(), A.data.numel(),
                 s.data_ptr(), q.data_ptr(), native.stream(dev))
     return s, q
@@ -2624,7 +2773,7 @@ def _glm_wide(X, y32: torch.Tensor, W: torch.Tensor, b: torch.Tensor, out: torch
         Z = torch.empty((m, K), dtype=torch.float32, device=dev)
         for c0 in range(0, K, 32):
             xw_t(X, _c(Wf[c0: c0 + 32]), out=Z[:, c0: c0 + 32])
-    R = torch.zeros((m, K), dtype=torch.float32, device=dev)  # stays 0 if the done flag skips the residual
+    R = zeros((m, K), dtype=torch.float32, device=dev)  # stays 0 if the done flag skips the residual
     Kn = K * n
     native.call("srml_logit_residual_wide_f32", Z.data_ptr(), m, K, K, _c(y32).data_ptr(), _c(b).data_ptr(), 1,
                 R.data_ptr(), K, out[Kn + K:].data_ptr(), fp, st)
@@ -2786,7 +2935,7 @@ def logistic_loss_grad(X, y32: torch.Tensor, w: torch.Tensor, b: torch.Tensor, K
         # margins (one SpMM pass, all classes) -> the softmax residual kernel (R, bias gradient,
         # loss) -> the X^T R SpMTM pass
         Z = csr_spmm(X, w.view(K, n).t())
-        R = torch.zeros((m, K), dtype=torch.float32, device=dev)  # stays 0 if the done flag skips the residual
+        R = zeros((m, K), dtype=torch.float32, device=dev)  # stays 0 if the done flag skips the residual
         native.call("srml_logit_residual_f32", Z.data_ptr(), m, K, K, _c(y32).data_ptr(), b.data_ptr(), 1, 0,
                     R.data_ptr(), K, out[K * n:].data_ptr(), 1, out[K * n + K:].data_ptr(), 0, fp, st)
         out[: K * n] += csr_spmtm(X, R).t().reshape(-1)
@@ -2798,7 +2947,7 @@ def logistic_loss_grad(X, y32: torch.Tensor, w: torch.Tensor, b: torch.Tensor, K
         # fp64 inputs wider than the LDS kernels: margins and X^T r on the fp64 MFMA GEMM (split-K
         # over rows), the residual / loss / bias gradient in one fp64 pass (srml_logit_residual_f64)
         z = dgemm(X, w.view(n, 1))
-        r = torch.zeros((m, 1), dtype=torch.float64, device=dev)  # stays 0 if the done flag skips it
+        r = zeros((m, 1), dtype=torch.float64, device=dev)  # stays 0 if the done flag skips it
         native.call("srml_logit_residual_f64", z.data_ptr(), m, 1, 1, _c(y32).data_ptr(), b.data_ptr(), 1, 1,
                     r.data_ptr(), 1, out[n:].data_ptr(), 1, out[n + 1:].data_ptr(), 1, fp, st)
         dgemm(X, r, ta=True, beta=1.0, out=out[:n].view(n, 1))
@@ -2807,7 +2956,7 @@ def logistic_loss_grad(X, y32: torch.Tensor, w: torch.Tensor, b: torch.Tensor, K
         # residual / bias gradient / loss in one fp64 pass (srml_logit_residual_f64, mode 0; K > 16:
         # the wave-per-row srml_logit_residual_wide_f64 and the bias gradient as R's column sums)
         Z = dgemm(X, w.view(K, n), tb=True)
-        R = torch.zeros((m, K), dtype=torch.float64, device=dev)  # stays 0 if the done flag skips it
+        R = zeros((m, K), dtype=torch.float64, device=dev)  # stays 0 if the done flag skips it
         if K <= 16:
             native.call("srml_logit_residual_f64", Z.data_ptr(), m, K, K, _c(y32).data_ptr(), b.data_ptr(), 1, 0,
                         R.data_ptr(), K, out[K * n:].data_ptr(), 1, out[K * n + K:].data_ptr(), 0, fp, st)
@@ -2872,8 +3021,16 @@ def zero_(t: torch.Tensor) -> torch.Tensor:
     if not t.is_cuda:
         return t.zero_()
     assert t.is_contiguous()
-    native.call("srml_memset_async", t.data_ptr(), 0, t.nbytes, native.stream(t.device))
+    if t.numel():
+        native.call("srml_memset_async", t.data_ptr(), 0, t.nbytes, native.stream(t.device))
     return t
+
+
+def zeros(*size: Any, **kw: Any) -> torch.Tensor:
+    """``torch.zeros`` whose device fill is a stream-ordered DMA memset (``srml_memset_async``)
+    instead of a dispatcher fill kernel: the fits allocate zeroed accumulators in their level /
+    iteration loops, and each torch fill was one more library launch of serial host work."""
+    return zero_(torch.empty(*size, **kw))
 
 
 # ------------------------------------------------------------------------------------------

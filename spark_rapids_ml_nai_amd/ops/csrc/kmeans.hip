@@ -219,13 +219,14 @@ template <int VW>
 __global__ __launch_bounds__(256) void accumulate_sorted_kernel(const float* __restrict__ X, long m, int n, long ld,
                                                                 const int* __restrict__ perm,
                                                                 const int* __restrict__ slab,
-                                                                double* __restrict__ sums, int rpb) {
+                                                                double* __restrict__ sums, int rpb,
+                                                                const int* __restrict__ rows = nullptr) {
   __shared__ int s_row[256];
   __shared__ int s_lab[256];
   const long r0 = (long)blockIdx.x * rpb;
   const int cnt = (int)min((long)rpb, m - r0);
   for (int i = threadIdx.x; i < cnt; i += 256) {
-    s_row[i] = perm[r0 + i];
+    s_row[i] = rows ? rows[perm[r0 + i]] : perm[r0 + i];  // rows: perm indexes a row list
     s_lab[i] = slab[r0 + i];
   }
   __syncthreads();
@@ -617,9 +618,12 @@ SRML_API int srml_kmeans_accumulate_f32(const float* X, long m, int n, long ld, 
   return srml_status();
 }
 
-// sums (k*n fp64, zeroed) += rows of X grouped by label, rows visited in label-sorted order.
-SRML_API int srml_kmeans_accumulate_sorted_f32(const float* X, long m, int n, long ld, const int* perm,
-                                               const int* sorted_labels, double* sums, hipStream_t stream) {
+// sums (k*n fp64) += rows of X grouped by label, rows visited in label-sorted order. rows
+// (nullable): perm indexes this list of (possibly ~negated) row ids instead of X directly (the
+// Lloyd delta update's moved-row list, sorted by label without a gathered copy).
+SRML_API int srml_kmeans_accumulate_sorted_rows_f32(const float* X, long m, int n, long ld, const int* perm,
+                                                    const int* rows, const int* sorted_labels, double* sums,
+                                                    hipStream_t stream) {
   if (m <= 0) return 0;
   const bool vec = ((ld & 3) == 0) && ((n & 3) == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
   // rows per block: 256, or fewer so a short list (the Lloyd delta update: ~1 % of the rows move)
@@ -633,13 +637,18 @@ SRML_API int srml_kmeans_accumulate_sorted_f32(const float* X, long m, int n, lo
   if (vec) {
     dim3 grid((unsigned)gx, (unsigned)((n / 4 + 255) / 256));
     hipLaunchKernelGGL(accumulate_sorted_kernel<4>, grid, dim3(256), 0, stream, X, m, n, ld, perm, sorted_labels,
-                       sums, rpb);
+                       sums, rpb, rows);
   } else {
     dim3 grid((unsigned)gx, (unsigned)((n + 255) / 256));
     hipLaunchKernelGGL(accumulate_sorted_kernel<1>, grid, dim3(256), 0, stream, X, m, n, ld, perm, sorted_labels,
-                       sums, rpb);
+                       sums, rpb, rows);
   }
   return srml_status();
+}
+
+SRML_API int srml_kmeans_accumulate_sorted_f32(const float* X, long m, int n, long ld, const int* perm,
+                                               const int* sorted_labels, double* sums, hipStream_t stream) {
+  return srml_kmeans_accumulate_sorted_rows_f32(X, m, n, ld, perm, nullptr, sorted_labels, sums, stream);
 }
 
 // Deterministic / fp64 cluster sums: rows visited in label-sorted order (perm), cluster l owns

@@ -392,7 +392,7 @@ __device__ __forceinline__ void kg_store_h(const KgPh& pf, _Float16* __restrict_
 // H16 (PAIRS only): the items come pre-centred in fp16 (Xh: x - C_list(x), N x F_KP halves, and
 // their norms xhn): the per-tile staging is a plain 16-B copy (half the bytes, no conversion) and
 // the item norms are loaded, not recomputed from the fragments.
-template <bool PAIRS, bool H16 = false, bool H2 = H16>
+template <bool PAIRS, bool H16 = false>
 __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
     const float* __restrict__ X, int n, long ld, const float* __restrict__ C, const long long* __restrict__ list_off,
     const int* __restrict__ probes, int nprobe, const long long* __restrict__ tile_q0,
@@ -401,7 +401,6 @@ __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
     const long long* __restrict__ pair_off = nullptr, const float* __restrict__ thr_row = nullptr,
     const _Float16* __restrict__ Xh = nullptr, const float* __restrict__ xhn = nullptr) {
   static_assert(PAIRS || !H16, "pre-centred items are the PAIRS mode's (items centred on their own list)");
-  static_assert(H16 || !H2, "the two-buffer prefetch is the fp16 items'");
   __shared__ __attribute__((aligned(16))) _Float16 Qs[F_BM * F_RS];
   __shared__ __attribute__((aligned(16))) _Float16 Is[F_BN * F_RS];
   __shared__ float cand_d[F_BM][F_CAP + 1];
@@ -460,13 +459,10 @@ __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
   // item tiles flow: registers -> centred fp16 LDS tile -> MFMA. The loads of tile t + 2 are
   // issued right after tile t + 1 is staged (at tile t's first barrier), so they have a whole
   // tile period to arrive.
-  // H2 (fp16 items, SRML_KG_H2=1): two register buffers (16 VGPRs each) keep tiles t + 1 AND t + 2
-  // in flight while tile t computes; buffer (t + 1) & 1 is staged at tile t's first barrier, then
-  // reloaded with t + 3. Since the query fragments live in registers (64 VGPRs) it spills one
-  // fragment and measured 5 % slower than one buffer (20M rows: 1.205 vs 1.140 s), so one buffer
-  // is the default
+  // (a second fp16 register buffer keeping tiles t + 1 AND t + 2 in flight measured 5 % slower
+  // once the query fragments moved to registers: it spilled, 20M rows 1.205 vs 1.140 s)
   KgPf pfa;
-  KgPh pfh, pfh2;
+  KgPh pfh;
   const int my_col = wn * 32 + li;  // this lane's item column in every MFMA tile
   float is_nrm = 0.f;              // H16: its item norm for the tile now in Is
   auto load_items = [&](long r0, long nv) {
@@ -494,15 +490,6 @@ __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
   bool have1 = have && next_tile();  // tile after it, in registers
   long h1c0 = c0, h1e = e;
   if (have1) load_items(c0, e - c0);
-  bool have2 = false;  // H16: the tile after that, in the second buffer
-  long h2c0 = 0, h2e = 0;
-  if constexpr (H2) {
-    have2 = have1 && next_tile();
-    h2c0 = c0;
-    h2e = e;
-    if (have2) kg_load_h(pfh2, Xh, xhn, c0, e - c0, t, my_col);
-  }
-  int par2 = 0;  // H16: which buffer holds tile t + 1
   __syncthreads();
   if (PAIRS) {
     // ||q - C_c||^2 of the staged (rounded, centred) queries; padding columns are zero. A seeded
@@ -531,16 +518,9 @@ __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
       areg[mt][ks] = *reinterpret_cast<const kg_halfx8*>(Qs + (wm * 64 + mt * 32 + li) * F_RS + ks * 16 + lk * 8);
   int par = 0;
   while (have) {
-    // the next tile to fetch: t + 2 (one buffer) or t + 3 (H16's two)
-    bool haveN;
-    long hNc0, hNe;
-    if constexpr (H2) {
-      haveN = have2 && next_tile();
-    } else {
-      haveN = have1 && next_tile();
-    }
-    hNc0 = c0;
-    hNe = e;
+    // the next tile to fetch: t + 2
+    const bool haveN = have1 && next_tile();
+    const long hNc0 = c0, hNe = e;
     floatx16 acc[2];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
@@ -613,31 +593,16 @@ __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
       if (first && have1) {
         // pin the prefetched registers behind the barrier: otherwise the compiler hoists the
         // centring/conversion above the append loop and waits for the loads right after the MFMAs
-        if constexpr (H2) {
-          // (two static branches, not a runtime-selected reference: a dynamically chosen register
-          // array would be demoted to scratch memory)
-          auto rotate = [&](KgPh& cur) {
+        if constexpr (H16) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-              asm volatile("" : "+v"(cur.v[j].x), "+v"(cur.v[j].y), "+v"(cur.v[j].z), "+v"(cur.v[j].w));
-            kg_store_h(cur, Is, h1e - h1c0, t);
-            is_nrm = cur.nrm;
-            if (haveN) kg_load_h(cur, Xh, xhn, hNc0, hNe - hNc0, t, my_col);
-          };
-          if (par2) rotate(pfh2);
-          else rotate(pfh);
+          for (int j = 0; j < 4; ++j)
+            asm volatile("" : "+v"(pfh.v[j].x), "+v"(pfh.v[j].y), "+v"(pfh.v[j].z), "+v"(pfh.v[j].w));
         } else {
-          if constexpr (H16) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-              asm volatile("" : "+v"(pfh.v[j].x), "+v"(pfh.v[j].y), "+v"(pfh.v[j].z), "+v"(pfh.v[j].w));
-          } else {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(pfa.v[j]));
-          }
-          store_items(h1e - h1c0);
-          if (haveN) load_items(hNc0, hNe - hNc0);
+          for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(pfa.v[j]));
         }
+        store_items(h1e - h1c0);
+        if (haveN) load_items(hNc0, hNe - hNc0);
       }
       const int full = ovf[par];  // block-uniform: some row ran out of candidate slots
       first = false;
@@ -652,19 +617,9 @@ __global__ __launch_bounds__(512, 1) void knn_lists_f16_kernel(
     tc0 = h1c0;
     te = h1e;
     have = have1;
-    if constexpr (H2) {  // shift the two in-flight tiles; the fetched one is t + 3
-      h1c0 = h2c0;
-      h1e = h2e;
-      have1 = have2;
-      h2c0 = hNc0;
-      h2e = hNe;
-      have2 = haveN;
-      par2 ^= 1;
-    } else {
-      h1c0 = hNc0;
-      h1e = hNe;
-      have1 = haveN;
-    }
+    h1c0 = hNc0;
+    h1e = hNe;
+    have1 = haveN;
   }
   kg_merge(topd, topi, cand_d, cand_i, cnt, thr_s, k, nq, wid, lane, 1);  // the last candidates
   __syncthreads();
@@ -758,18 +713,9 @@ SRML_API int srml_knn_pairs_f16c(const float* X, int n, long ld, const float* C,
   // self_probe: nlist ints, self_probe[c] = c (list c scans its own items)
   if (Xh && xhn) {
     if (reinterpret_cast<uintptr_t>(Xh) & 15) return -8;
-    static const int two = [] {
-      const char* e = getenv("SRML_KG_H2");
-      return e ? atoi(e) : 0;
-    }();
-    if (two)
-      hipLaunchKernelGGL((knn_lists_f16_kernel<true, true, true>), dim3((unsigned)ntiles), dim3(512), 0, stream, X, n,
-                         ld, C, list_off, self_probe, 1, tile_q0, tile_list, ntiles, k, out_d, out_i, qrows, qslot,
-                         pair_off, thr_row, reinterpret_cast<const _Float16*>(Xh), xhn);
-    else
-      hipLaunchKernelGGL((knn_lists_f16_kernel<true, true, false>), dim3((unsigned)ntiles), dim3(512), 0, stream, X, n,
-                         ld, C, list_off, self_probe, 1, tile_q0, tile_list, ntiles, k, out_d, out_i, qrows, qslot,
-                         pair_off, thr_row, reinterpret_cast<const _Float16*>(Xh), xhn);
+    hipLaunchKernelGGL((knn_lists_f16_kernel<true, true>), dim3((unsigned)ntiles), dim3(512), 0, stream, X, n, ld, C,
+                       list_off, self_probe, 1, tile_q0, tile_list, ntiles, k, out_d, out_i, qrows, qslot, pair_off,
+                       thr_row, reinterpret_cast<const _Float16*>(Xh), xhn);
   } else {
     hipLaunchKernelGGL((knn_lists_f16_kernel<true, false>), dim3((unsigned)ntiles), dim3(512), 0, stream, X, n, ld, C,
                        list_off, self_probe, 1, tile_q0, tile_list, ntiles, k, out_d, out_i, qrows, qslot, pair_off,

@@ -1254,9 +1254,18 @@ SRML_API int srml_split_f16_tiled_centered_rows(const float* X, long ld, const i
 // r of the output = row ridx[r] of the source, bit-identical to converting X[ridx[r]] again but
 // reading 32 B of fp16 per (row, k step) instead of 64 B of fp32; one thread per (row, k step),
 // each 32-B slot moved as two 16-B halves with the source / destination swizzles undone / applied.
+// xn / xn_out (nullable): also gather the rows' norms; zero_out (nullable): m ints zeroed (the
+// candidate search's per-row counters), so the re-search needs no separate fill / gather launches.
 __global__ __launch_bounds__(256) void f16_plane_gather_kernel(const uintx4* __restrict__ src, int ks_n,
                                                                const int* __restrict__ ridx, long m, long rows_pad,
-                                                               uintx4* __restrict__ dst) {
+                                                               uintx4* __restrict__ dst,
+                                                               const float* __restrict__ xn = nullptr,
+                                                               float* __restrict__ xn_out = nullptr,
+                                                               int* __restrict__ zero_out = nullptr) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < m; i += (long)gridDim.x * 256) {
+    if (xn_out) xn_out[i] = xn[ridx[i]];
+    if (zero_out) zero_out[i] = 0;
+  }
   const long total = rows_pad * ks_n;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
     const long img = i >> 8;
@@ -1279,17 +1288,25 @@ __global__ __launch_bounds__(256) void f16_plane_gather_kernel(const uintx4* __r
   }
 }
 
-SRML_API int srml_f16_plane_gather_rows(const unsigned short* P, long src_rows_pad, int kp, const int* ridx, long m,
-                                        long rows_pad, unsigned short* out, hipStream_t stream) {
+SRML_API int srml_f16_plane_gather_rows_ex(const unsigned short* P, long src_rows_pad, int kp, const int* ridx, long m,
+                                           long rows_pad, unsigned short* out, const float* xn, float* xn_out,
+                                           int* zero_out, hipStream_t stream) {
   if (rows_pad <= 0) return 0;
   if ((kp & 15) || rows_pad < m || (rows_pad & 255) || (src_rows_pad & 255) || !ridx) return -2;
   if ((reinterpret_cast<uintptr_t>(P) & 15) || (reinterpret_cast<uintptr_t>(out) & 15)) return -5;
+  if (xn_out && !xn) return -2;
   const long total = rows_pad * (long)(kp / 16);
   long blocks = (total + 255) / 256;
   if (blocks > 65536) blocks = 65536;
   hipLaunchKernelGGL(f16_plane_gather_kernel, dim3((unsigned)blocks), dim3(256), 0, stream,
-                     reinterpret_cast<const uintx4*>(P), kp / 16, ridx, m, rows_pad, reinterpret_cast<uintx4*>(out));
+                     reinterpret_cast<const uintx4*>(P), kp / 16, ridx, m, rows_pad, reinterpret_cast<uintx4*>(out), xn,
+                     xn_out, zero_out);
   return srml_status();
+}
+
+SRML_API int srml_f16_plane_gather_rows(const unsigned short* P, long src_rows_pad, int kp, const int* ridx, long m,
+                                        long rows_pad, unsigned short* out, hipStream_t stream) {
+  return srml_f16_plane_gather_rows_ex(P, src_rows_pad, kp, ridx, m, rows_pad, out, nullptr, nullptr, nullptr, stream);
 }
 
 // select of the filter pass with the flagged rows' thresholds (thr_out[p] for flagged[p])

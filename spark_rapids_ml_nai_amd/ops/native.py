@@ -30,7 +30,7 @@ _LONG_RESULT = ("srml_rf_bootstrap_ws", "srml_logreg_fold_ws", "srml_qn_mb_scrat
                 "srml_qn_fused_barrier_offset",
                 "srml_logreg_fold_parts", "srml_qn_args_size", "srml_logit_residual_ws", "srml_xtv_mfma_ws",
                 "srml_rf_partition_ws", "srml_dbscan_labels_ws", "srml_umap_categorical_ws",
-                "srml_label_sort_ws", "srml_radix_sort_ws")
+                "srml_label_sort_ws", "srml_radix_sort_ws", "srml_lloyd_moved_ws", "srml_sum_f32_ws")
 SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_col_moments_f32": (_P, _L, _I, _L, _P, _P, _P),
     "srml_col_moments_f64": (_P, _L, _I, _L, _P, _P, _P),
@@ -105,6 +105,7 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_split_top2_select_f16": (_P, _P, _L, _I, _P, _P, _F, _F, _F, _P, _P, _P, _P, _P, _P),
     "srml_split_f16_tiled_centered_rows": (_P, _L, _P, _L, _I, _P, _I, _L, _F, _P, _P, _P),
     "srml_f16_plane_gather_rows": (_P, _L, _I, _P, _L, _L, _P, _P),
+    "srml_f16_plane_gather_rows_ex": (_P, _L, _I, _P, _L, _L, _P, _P, _P, _P, _P),
     "srml_split_top2_select_f16_thr": (_P, _P, _L, _I, _P, _P, _F, _F, _F, _P, _P, _P, _P, _P, _P, _P),
     "srml_nearest_centroid_f16_cand": (_P, _L, _L, _I, _P, _I, _L, _P, _P, _P, _F, _F, _P, _P, _P, _I, _P),
     "srml_kmeans_cand_exact": (_P, _L, _P, _P, _L, _I, _I, _P, _I, _P, _P, _I, _P, _P, _P),
@@ -113,6 +114,14 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_split_scatter_refined": (_P, _P, _I, _P, _P, _P, _P),
     "srml_kmeans_accumulate_f32": (_P, _L, _I, _L, _P, _I, _P, _P, _P, _P),
     "srml_kmeans_accumulate_sorted_f32": (_P, _L, _I, _L, _P, _P, _P, _P),
+    "srml_kmeans_accumulate_sorted_rows_f32": (_P, _L, _I, _L, _P, _P, _P, _P, _P),
+    "srml_lloyd_moved_ws": (_L,),
+    "srml_lloyd_moved_count": (_P, _P, _L, _P, _P, _P),
+    "srml_lloyd_moved_compact": (_P, _P, _L, _P, _L, _P, _P, _P, _P),
+    "srml_counts_from_offsets": (_P, _I, _P, _P),
+    "srml_sum_f32_ws": (),
+    "srml_sum_f32_f64": (_P, _L, _P, _P, _P),
+    "srml_lloyd_centre_update": (_P, _I, _I, _P, _P, _P, _P),
     "srml_kmeans_segment_sums_f32": (_P, _L, _I, _L, _P, _P, _I, _P, _I, _P, _P),
     "srml_kmeans_segment_sums_f64": (_P, _L, _I, _L, _P, _P, _I, _P, _I, _P, _P),
     "srml_nearest_centroid_f64": (_P, _L, _I, _L, _P, _I, _L, _P, _P, _P, _P, _P, _P),
@@ -197,6 +206,10 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_memset_async": (_P, _I, _L, _P),
     "srml_rf_predict_nodes2": (_P, _L, _L, _I, _P, _P, _I, _P, _I, _P, _P, _P),
     "srml_rf_predict": (_P, _L, _L, _P, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P),
+    "srml_rf_left_totals": (_P, _I, _L, _I, _I, _I, _P, _P, _P),
+    "srml_rf_gather_feature": (_P, _L, _P, _L, _P, _P),
+    "srml_rf_decide": (_P, _P, _P, _L, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P),
+    "srml_rf_level_pack": (_P, _L, _P, _I, _I, _I, _P, _P, _P, _P),
     "srml_rf_sample_features": (_I, _I, _I, ctypes.c_ulonglong, _P, _P),
     "srml_rf_partition": (_P, _L, _P, _I, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P),
     "srml_rf_partition_ws": (_L, _I),

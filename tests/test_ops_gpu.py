@@ -1199,6 +1199,64 @@ def test_kmeans_delta_sums_match_full_sums(gpu_device, monkeypatch):
     np.testing.assert_allclose(out[0.2]["cluster_centers_"], out[-1.0]["cluster_centers_"], rtol=1e-5, atol=2e-6)
 
 
+@pytest.mark.parametrize("tol", [0.0, 1e-3])
+def test_kmeans_device_bookkeeping_matches_torch_loop(gpu_device, monkeypatch, tol):
+    """The fp16-filter Lloyd loop with native bookkeeping (moved-row count / compaction, in-place
+    delta and full sums, fp64 inertia, device centre update + shift) gives the torch loop's centres,
+    iteration count and delta schedule; the moved-row kernels match a torch oracle."""
+    from spark_rapids_ml_nai_amd import ops
+    from spark_rapids_ml_nai_amd.models import kmeans as km
+    from spark_rapids_ml_nai_amd.parallel.context import PartitionDescriptor, WorkerContext
+
+    X = _rand(30000, 300, gpu_device, seed=73)
+    ctx = WorkerContext.single(gpu_device)
+    desc = PartitionDescriptor.build(ctx, X.shape[0], X.shape[1])
+    monkeypatch.setenv("SRML_KMEANS_SPLIT", "1")
+    out = {}
+    for book in ("1", "0"):
+        monkeypatch.setenv("SRML_LLOYD_BOOK", book)
+        out[book] = km.kmeans_fit(X, desc, ctx, k=300, max_iter=15, tol=tol, seed=5, init="random")
+    assert out["1"]["n_iter"] == out["0"]["n_iter"]
+    assert out["1"]["delta_iters"] == out["0"]["delta_iters"]
+    np.testing.assert_allclose(out["1"]["cluster_centers_"], out["0"]["cluster_centers_"], rtol=1e-5, atol=2e-6)
+
+    # the moved-row pass against torch: count, ascending compaction, +-1 count updates, sorted sums
+    g = torch.Generator().manual_seed(3)
+    m, k = 5000, 40
+    lab = torch.randint(0, k, (m,), generator=g, dtype=torch.int32)
+    prev = lab.clone()
+    flip = torch.randperm(m, generator=g)[:700]
+    prev[flip] = torch.randint(0, k, (700,), generator=g, dtype=torch.int32)
+    Xs = torch.randn(m, 12, generator=g)
+    book = ops.LloydBook(Xs.to(gpu_device), k)
+    nm = book.moved(lab.to(gpu_device), prev.to(gpu_device))
+    moved = torch.nonzero(lab != prev).view(-1)
+    assert nm == moved.numel()
+    L = torch.zeros(k * 12 + k + 1, dtype=torch.float64, device=gpu_device)
+    book.delta_into(Xs.to(gpu_device), lab.to(gpu_device), prev.to(gpu_device), nm, L)
+    ref_s = torch.zeros(k, 12, dtype=torch.float64)
+    ref_s.index_add_(0, lab[moved].long(), Xs[moved].double())
+    ref_s.index_add_(0, prev[moved].long(), -Xs[moved].double())
+    ref_c = (torch.bincount(lab[moved].long(), minlength=k) - torch.bincount(prev[moved].long(), minlength=k)).double()
+    torch.testing.assert_close(L[: k * 12].view(k, 12).cpu(), ref_s, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(L[k * 12: k * 12 + k].cpu(), ref_c, rtol=0, atol=0)
+    # full pass + inertia + update
+    book.full_into(Xs.to(gpu_device), lab.to(gpu_device), L)
+    d2 = torch.rand(m, generator=g)
+    book.inertia_into(d2.to(gpu_device), L)
+    ref_full = torch.zeros(k, 12, dtype=torch.float64).index_add_(0, lab.long(), Xs.double())
+    torch.testing.assert_close(L[: k * 12].view(k, 12).cpu(), ref_full, rtol=1e-5, atol=1e-5)
+    assert float(L[-1]) == pytest.approx(float(d2.double().sum()), rel=1e-12)
+    C = torch.randn(k, 12, dtype=torch.float64, generator=g)
+    Cd = C.to(gpu_device)
+    shift, inertia = book.update(L, Cd)
+    cnt = torch.bincount(lab.long(), minlength=k).double()
+    newC = torch.where(cnt.view(-1, 1) > 0, ref_full / cnt.clamp_min(1).view(-1, 1), C)
+    torch.testing.assert_close(Cd.cpu(), newC, rtol=1e-6, atol=1e-6)
+    assert shift == pytest.approx(float(((newC - C) ** 2).sum(1).max()), rel=1e-6)
+    assert inertia == float(L[-1])
+
+
 @pytest.mark.parametrize("pull", [False, True])
 @pytest.mark.parametrize("dim", [2, 5])
 def test_umap_epoch_head_runs(gpu_device, pull, dim):

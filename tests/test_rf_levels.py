@@ -214,3 +214,36 @@ def test_rf_row_major_transpose_gpu(n, m, gpu_device):
     bins = torch.randint(0, 256, (n, m), generator=g, dtype=torch.uint8)
     got = ops.rf_row_major(bins.to(gpu_device))
     assert torch.equal(got.cpu(), bins.t().contiguous())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("regression,impurity", [(False, "gini"), (False, "entropy"), (True, "variance")])
+def test_native_level_bookkeeping_matches_torch_gpu(monkeypatch, regression, impurity, gpu_device):
+    """The level bookkeeping in native kernels (split ranks, routing arrays, children totals,
+    segment stats, packed read-back) grows the trees of the torch-op version: same structure and
+    predictions, leaf values / impurities / importances to fp64 rounding."""
+    from spark_rapids_ml_nai_amd.models import forest
+
+    g = np.random.default_rng(5)
+    X = g.standard_normal((5000, 20)).astype(np.float32)
+    if regression:
+        from spark_rapids_ml_nai_amd.regression import RandomForestRegressor as E
+
+        y = (X[:, 0] * 2 + np.sin(X[:, 1] * 3) + 0.1 * g.standard_normal(5000)).astype(np.float64)
+    else:
+        from spark_rapids_ml_nai_amd.classification import RandomForestClassifier as E
+
+        y = ((X[:, 0] + X[:, 2] * X[:, 3]) > 0.2).astype(np.float64) + (X[:, 1] > 1.0)
+    models = {}
+    for native_lvl in (True, False):
+        monkeypatch.setattr(forest, "RF_LEVEL_NATIVE", native_lvl)
+        models[native_lvl] = E(numTrees=5, maxDepth=8, maxBins=32, seed=11, impurity=impurity).fit(
+            DataFrame.from_numpy(X, y))
+    a, b = models[True], models[False]
+    assert a.totalNumNodes == b.totalNumNodes
+    Xq = g.standard_normal((400, 20)).astype(np.float32)
+    pa = a.transform(DataFrame.from_numpy(Xq))
+    pb = b.transform(DataFrame.from_numpy(Xq))
+    np.testing.assert_allclose(pa.to_numpy("prediction"), pb.to_numpy("prediction"), rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(np.asarray(a.featureImportances.toArray()), np.asarray(b.featureImportances.toArray()),
+                               rtol=1e-9, atol=1e-12)
