@@ -349,8 +349,7 @@ def _root_hist_streamed(pending: PendingBins, bins: torch.Tensor, idx: torch.Ten
     wy = ops.rf_hist_wy(idx, yv, None, wpos)
     rows_at = torch.tensor([r0 for r0, _ in pending.bounds] + [m], dtype=idx.dtype, device=dev)
     # P[j, c]: first position of segment j whose row is >= the start of chunk c
-    P = torch.stack([torch.searchsorted(idx[int(s0): int(s0) + int(cn)], rows_at)
-                     for s0, cn in zip(c_start, c_cnt)]).cpu().numpy().astype(np.int64) + c_start[:, None]
+    P = ops.seg_lower_bound(idx, c_start, c_cnt, rows_at)
     per_chunk = []
     for ci in range(len(pending.bounds)):
         lo, hi = P[:, ci], P[:, ci + 1]

@@ -37,13 +37,31 @@ class LSQStats:
 
     m: int
     xbar: torch.Tensor
-    xstd: torch.Tensor
+    sumsq: torch.Tensor  # global column sums of squares
+    scatter: torch.Tensor  # global centred scatter (n x n, NOT divided by m)
+    xty: torch.Tensor  # global raw X^T y
     ybar: float
     ystd: float
-    cov: torch.Tensor  # centred scatter / m  (n x n)
-    xy_c: torch.Tensor  # centred cross moment / m
-    xy_raw: torch.Tensor  # uncentred cross moment / m
     yy_raw: float
+
+    @property
+    def xstd(self) -> torch.Tensor:
+        return (self.sumsq / float(self.m) - self.xbar * self.xbar).clamp_min(0.0).sqrt()
+
+    @property
+    def cov(self) -> torch.Tensor:
+        """centred scatter / m"""
+        return self.scatter / float(self.m)
+
+    @property
+    def xy_raw(self) -> torch.Tensor:
+        """uncentred cross moment / m"""
+        return self.xty.view(-1) / float(self.m)
+
+    @property
+    def xy_c(self) -> torch.Tensor:
+        """centred cross moment / m"""
+        return self.xy_raw - self.xbar * self.ybar
 
     @property
     def raw2(self) -> torch.Tensor:
@@ -57,13 +75,9 @@ def lsq_stats(X: torch.Tensor, y: torch.Tensor, m_total: int, ctx: WorkerContext
 
     st = scatter_stats(X, ctx, m_total, stream=stream, y=y, need_sq=True)
     mt = float(m_total)
-    mean = st.mean
-    cov = st.scatter / mt
-    xy_raw = st.xty / mt
-    var = (st.sumsq / mt - mean * mean).clamp_min(0.0)
     ybar = st.y_sum / mt
     yvar = max(st.y_sumsq / mt - ybar * ybar, 0.0)
-    return LSQStats(m_total, mean, torch.sqrt(var), ybar, float(np.sqrt(yvar)), cov, xy_raw - mean * ybar, xy_raw,
+    return LSQStats(m_total, st.mean, st.sumsq, st.scatter, st.xty.view(-1), ybar, float(np.sqrt(yvar)),
                     st.y_sumsq / mt)
 
 
@@ -114,39 +128,54 @@ def lsq_solve(st: LSQStats, reg: float, l1_ratio: float, fit_intercept: bool, st
               max_iter: int, tol: float) -> Dict[str, Any]:
     n = st.xbar.shape[0]
     dev = st.xbar.device
-    xstd = st.xstd
-    nz = xstd > 0
-    safe = torch.where(nz, xstd, torch.ones_like(xstd))
     if st.ystd == 0.0 and fit_intercept:
         # constant label: Spark returns zero coefficients and intercept = label mean
         return {"coef_": [0.0] * n, "intercept_": st.ybar}
     ystd = st.ystd if st.ystd > 0 else 1.0
-    denom = torch.outer(safe, safe)
-    if fit_intercept:
-        A = st.cov / denom
-        b = st.xy_c / (safe * ystd)
-    else:
-        A = st.raw2 / denom
-        b = st.xy_raw / (safe * ystd)
-    keep = nz.double()
-    A = A * torch.outer(keep, keep)
-    b = b * keep
     # Penalties of the reference's solvers (regression.py:508-560: cuML RidgeMG with alpha * m, CD
     # with alpha / l1_ratio; i.e. sklearn Ridge / Lasso / ElasticNet): in raw units
     #   1/(2m) ||y - Xw - b||^2 + reg * (l1_ratio ||s w||_1 + (1 - l1_ratio)/2 ||s w||^2),
     # s = feature std (standardization) or 1. Solved here in standardised units (w_t = w s_x / ystd,
     # objective scaled by 1/ystd^2), which moves one 1/ystd onto the L1 weight and none onto L2.
-    lam = reg / ystd
-    ones = torch.ones(n, dtype=torch.float64, device=dev)
-    l1 = lam * l1_ratio * (ones if standardization else 1.0 / safe)
-    l2 = reg * (1.0 - l1_ratio) * (ones if standardization else 1.0 / (safe * safe))
-    if reg == 0.0 or l1_ratio == 0.0:
-        Areg = A + torch.diag(l2 + (1.0 - keep))  # constant columns: identity rows, zero rhs
+    direct = reg == 0.0 or l1_ratio == 0.0
+    if dev.type == "cuda":
+        # one kernel forms the scaled system (+ diag(l2 + 1 - keep) for the direct solvers: constant
+        # columns get identity rows and a zero rhs) and the per-feature vectors [safe|keep|b|l1|l2]
+        A = torch.empty((n, n), dtype=torch.float64, device=dev)
+        vec = torch.empty(5 * n, dtype=torch.float64, device=dev)
+        ops.native.call("srml_lsq_prepare", st.scatter.data_ptr(), n, st.xbar.data_ptr(), st.sumsq.data_ptr(),
+                        st.xty.data_ptr(), float(st.m), float(st.ybar), float(ystd), float(reg), float(l1_ratio),
+                        int(fit_intercept), int(standardization), int(direct), A.data_ptr(), vec.data_ptr(),
+                        ops.native.stream(dev))
+        safe, keep, b, l1, l2 = vec.view(5, n)
+        Areg = A
+    else:
+        xstd = st.xstd
+        nz = xstd > 0
+        safe = torch.where(nz, xstd, torch.ones_like(xstd))
+        denom = torch.outer(safe, safe)
+        A = (st.cov if fit_intercept else st.raw2) / denom
+        b = (st.xy_c if fit_intercept else st.xy_raw) / (safe * ystd)
+        keep = nz.double()
+        A = A * torch.outer(keep, keep)
+        b = b * keep
+        lam = reg / ystd
+        ones = torch.ones(n, dtype=torch.float64, device=dev)
+        l1 = lam * l1_ratio * (ones if standardization else 1.0 / safe)
+        l2 = reg * (1.0 - l1_ratio) * (ones if standardization else 1.0 / (safe * safe))
+        Areg = A + torch.diag(l2 + (1.0 - keep)) if direct else A
+    if direct:
         wt, ok = ops.spd_solve(Areg, b)
         if not ok:
             wt = _min_norm_solve(Areg, b)
     else:
         wt, _ = ops.cd_gram(A, b, l1, l2, max_iter, tol)
+    if dev.type == "cuda":
+        out = torch.empty(n + 1, dtype=torch.float64, device=dev)
+        ops.native.call("srml_lsq_finish", ops._c(wt.double()).data_ptr(), n, vec.data_ptr(), st.xbar.data_ptr(),
+                        float(ystd), float(st.ybar), int(fit_intercept), out.data_ptr(), ops.native.stream(dev))
+        h = out.cpu().tolist()
+        return {"coef_": h[:n], "intercept_": float(h[n])}
     wt = wt * keep
     w = wt * ystd / safe
     intercept = float(st.ybar - float((st.xbar * w).sum())) if fit_intercept else 0.0

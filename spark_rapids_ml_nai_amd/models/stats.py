@@ -35,10 +35,15 @@ def scatter_stats(X: torch.Tensor, ctx: WorkerContext, m_total: int, stream: Any
     n = X.shape[1]
     dev = X.device
     chunks = stream.chunks() if stream is not None else [(0, X.shape[0], X)]
-    s = ops.zeros(n, dtype=torch.float64, device=dev)
-    q = ops.zeros(n, dtype=torch.float64, device=dev) if need_sq else None
-    G = ops.zeros((n, n), dtype=torch.float64, device=dev)
-    xty = ops.zeros((n, 1), dtype=torch.float64, device=dev) if y is not None else None
+    # the two all-reduce buffers are allocated whole and the accumulators are views of them: small =
+    # [column sums | sums of squares | y sum, y sum of squares], big = [scatter | X^T y]
+    ns = n + (n if need_sq else 0)
+    small = ops.zeros(ns + 2, dtype=torch.float64, device=dev)
+    big = ops.zeros(n * n + (n if y is not None else 0), dtype=torch.float64, device=dev)
+    s = small[:n]
+    q = small[n: 2 * n] if need_sq else None
+    G = big[: n * n].view(n, n)
+    xty = big[n * n:].view(n, 1) if y is not None else None
     mu0 = None
     m_r = 0
     for r0, r1, Xc in chunks:
@@ -53,24 +58,29 @@ def scatter_stats(X: torch.Tensor, ctx: WorkerContext, m_total: int, stream: Any
     ops.gram_mirror(G)
     if mu0 is None:
         mu0 = ops.zeros(n, dtype=torch.float64, device=dev)
-    mean_r = s / max(m_r, 1)
-    d = mean_r - mu0
-    G -= float(m_r) * torch.outer(d, d)  # local scatter about the local mean
-    ys = ops.zeros(2, dtype=torch.float64, device=dev)
+    mean_r = s / max(m_r, 1)  # (before the all-reduce sums s over the ranks)
     if y is not None:
-        yd = y.double()
-        ys = torch.stack([yd.sum(), (yd * yd).sum()])
-    small = torch.cat([s] + ([q] if need_sq else []) + [ys])
+        if dev.type == "cuda" and y.dtype in (torch.float32, torch.float64) and y.is_contiguous():
+            ws = torch.empty(int(ops.native.lib().srml_sum_sq_ws()), dtype=torch.float64, device=dev)
+            ops.native.call("srml_sum_sq", y.data_ptr(), int(y.dtype == torch.float64), y.shape[0], ws.data_ptr(),
+                            small[ns:].data_ptr(), ops.native.stream(dev))
+        else:
+            yd = y.double()
+            small[ns:] = torch.stack([yd.sum(), (yd * yd).sum()])
     ctx.comm.allreduce(small)
     s_g = small[:n]
     q_g = small[n: 2 * n] if need_sq else None
-    ys = small[-2:]
     mean = s_g / float(m_total)
-    e = mean_r - mean
-    G += float(m_r) * torch.outer(e, e)
-    big = torch.cat([G.view(-1)] + ([xty.view(-1)] if y is not None else []))
+    # local scatter about mu0 -> about the local mean -> about the global mean, in one pass
+    if dev.type == "cuda":
+        ops.native.call("srml_scatter_shift", G.data_ptr(), n, mean_r.data_ptr(), mu0.data_ptr(), mean.data_ptr(),
+                        float(m_r), ops.native.stream(dev))
+    else:
+        d = mean_r - mu0
+        e = mean_r - mean
+        G += float(m_r) * (torch.outer(e, e) - torch.outer(d, d))
     ctx.comm.allreduce(big)
-    scatter = big[: n * n].view(n, n)
-    xty_g = big[n * n:] if y is not None else None
-    ysh = ys.cpu().tolist()
+    scatter = G
+    xty_g = xty.view(-1) if y is not None else None
+    ysh = small[ns:].cpu().tolist()
     return ScatterStats(m_total, mean, q_g, scatter, xty_g, ysh[0], ysh[1])

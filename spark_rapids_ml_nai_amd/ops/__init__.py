@@ -1576,6 +1576,22 @@ def rf_level_pack(bounds: torch.Tensor, tot_n: torch.Tensor, regression: bool, c
     return hb
 
 
+def seg_lower_bound(idx: torch.Tensor, start: np.ndarray, count: np.ndarray, vals: torch.Tensor) -> np.ndarray:
+    """(nseg, nv) int64 host array: for every segment idx[start[j] : start[j] + count[j]] (ascending)
+    the global position of the first entry >= vals[c] (one device launch for all segments)."""
+    nseg, nv = len(start), int(vals.numel())
+    if not idx.is_cuda or idx.dtype != torch.int32:
+        return np.stack([torch.searchsorted(idx[int(s0): int(s0) + int(cn)], vals.to(idx.device)).cpu().numpy()
+                         + int(s0) for s0, cn in zip(start, count)]).astype(np.int64)
+    dev = idx.device
+    se = torch.from_numpy(np.stack([np.asarray(start, np.int64), np.asarray(count, np.int64)])).pin_memory().to(
+        dev, non_blocking=True)
+    out = torch.empty((nseg, nv), dtype=torch.int64, device=dev)
+    native.call("srml_seg_lower_bound", idx.data_ptr(), se[0].data_ptr(), se[1].data_ptr(), nseg,
+                _c(vals.to(device=dev, dtype=torch.int32)).data_ptr(), nv, out.data_ptr(), native.stream(dev))
+    return out.cpu().numpy()
+
+
 def rf_sample_features(C: int, n: int, nf: int, seed: int, device: torch.device) -> torch.Tensor:
     """(C, nf) int32: per node a uniform random subset of nf of n features, ascending
     (``srml_rf_sample_features``: Floyd's algorithm for sparse subsets, nf <= n / 8, else

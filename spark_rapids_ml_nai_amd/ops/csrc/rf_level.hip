@@ -217,3 +217,35 @@ SRML_API int srml_rf_level_pack(const long long* bounds, long C, const double* t
                      regression, crit, out, fsel, hb);
   return srml_status();
 }
+
+namespace {
+// out[j, c] = start[j] + lower_bound(idx[start[j] .. start[j] + count[j]), vals[c])
+__global__ __launch_bounds__(RL_THREADS) void seg_lower_bound_kernel(const int* __restrict__ idx,
+                                                                     const long long* __restrict__ start,
+                                                                     const long long* __restrict__ count, long nseg,
+                                                                     const int* __restrict__ vals, int nv,
+                                                                     long long* __restrict__ out) {
+  const long i = (long)blockIdx.x * RL_THREADS + threadIdx.x;
+  if (i >= nseg * nv) return;
+  const long j = i / nv;
+  const int c = (int)(i - j * nv);
+  const int v = vals[c];
+  long lo = start[j], hi = start[j] + count[j];
+  while (lo < hi) {
+    const long mid = (lo + hi) >> 1;
+    if (idx[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  out[i] = lo;
+}
+}  // namespace
+
+// Per-segment lower bounds of nv values in ascending segments of idx (the streamed root level's
+// chunk boundaries inside every tree's bootstrap rows): out (nseg x nv, int64) = global positions.
+SRML_API int srml_seg_lower_bound(const int* idx, const long long* start, const long long* count, long nseg,
+                                  const int* vals, int nv, long long* out, hipStream_t stream) {
+  if (nseg <= 0 || nv <= 0) return 0;
+  hipLaunchKernelGGL(seg_lower_bound_kernel, dim3(ceil_div(nseg * nv, RL_THREADS)), dim3(RL_THREADS), 0, stream, idx,
+                     start, count, nseg, vals, nv, out);
+  return srml_status();
+}

@@ -30,7 +30,7 @@ _LONG_RESULT = ("srml_rf_bootstrap_ws", "srml_logreg_fold_ws", "srml_qn_mb_scrat
                 "srml_qn_fused_barrier_offset",
                 "srml_logreg_fold_parts", "srml_qn_args_size", "srml_logit_residual_ws", "srml_xtv_mfma_ws",
                 "srml_rf_partition_ws", "srml_dbscan_labels_ws", "srml_umap_categorical_ws",
-                "srml_label_sort_ws", "srml_radix_sort_ws", "srml_lloyd_moved_ws", "srml_sum_f32_ws")
+                "srml_label_sort_ws", "srml_radix_sort_ws", "srml_lloyd_moved_ws", "srml_sum_f32_ws", "srml_sum_sq_ws")
 SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_col_moments_f32": (_P, _L, _I, _L, _P, _P, _P),
     "srml_col_moments_f64": (_P, _L, _I, _L, _P, _P, _P),
@@ -210,6 +210,12 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_rf_gather_feature": (_P, _L, _P, _L, _P, _P),
     "srml_rf_decide": (_P, _P, _P, _L, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P),
     "srml_rf_level_pack": (_P, _L, _P, _I, _I, _I, _P, _P, _P, _P),
+    "srml_seg_lower_bound": (_P, _P, _P, _L, _P, _I, _P, _P),
+    "srml_scatter_shift": (_P, _I, _P, _P, _P, _D, _P),
+    "srml_sum_sq_ws": (),
+    "srml_sum_sq": (_P, _I, _L, _P, _P, _P),
+    "srml_lsq_prepare": (_P, _I, _P, _P, _P, _D, _D, _D, _D, _D, _I, _I, _I, _P, _P, _P),
+    "srml_lsq_finish": (_P, _I, _P, _P, _D, _D, _I, _P, _P),
     "srml_rf_sample_features": (_I, _I, _I, ctypes.c_ulonglong, _P, _P),
     "srml_rf_partition": (_P, _L, _P, _I, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P),
     "srml_rf_partition_ws": (_L, _I),
