@@ -584,6 +584,47 @@ class F16Planes:
 F16_CAND_CAP = 64  # candidate-list capacity per re-searched row (more: that row scans every centre)
 
 
+def _f16_centre_planes(F: F16Planes, C: torch.Tensor, approx: bool) -> Tuple[torch.Tensor, ...]:
+    """The centre side of an fp16 search on F's scaled plane: centred centres W = C - mu, their
+    norms cn (fp64 sum, one fp32 rounding; allocated for the padded tile rows, entries past k
+    unset), the radius terms cg, the [ovf, flagged count] counters zeroed — one launch — and the
+    tiled fp16 plane CP of scale * W (X's own plane never overflows; only the centres can)."""
+    k, dev = C.shape[0], F.X.device
+    st = native.stream(dev)
+    Cd = _c(C.to(dev)) if C.dtype in (torch.float32, torch.float64) else _c(C.to(dev, torch.float32))
+    crows = max(256, (k + 255) // 256 * 256)
+    W = torch.empty((k, F.n), dtype=torch.float32, device=dev)
+    cn = torch.empty(crows, dtype=torch.float32, device=dev)
+    cg = torch.empty(k, dtype=torch.float32, device=dev)
+    zero2 = torch.empty(2, dtype=torch.int32, device=dev)  # [ovf, flagged count]
+    native.call("srml_f16_centre_prep", Cd.data_ptr(), int(Cd.dtype == torch.float64), k, F.n, F.mu.data_ptr(),
+                float(2.0 * F.tau), int(bool(approx)), W.data_ptr(), cn.data_ptr(), cg.data_ptr(), zero2.data_ptr(), st)
+    CP = torch.empty((crows // 256, F.kp // 16, 256, 16), dtype=torch.float16, device=dev)
+    native.call("srml_split_f16_tiled_centered", W.data_ptr(), k, F.n, W.stride(0), None, F.kp, crows, F.scale,
+                CP.data_ptr(), zero2[0:1].data_ptr(), st)
+    return W, cn, cg, zero2, CP, crows
+
+
+def nearest_f16_labels(F: F16Planes, C: torch.Tensor) -> Optional[torch.Tensor]:
+    """int32 arg-min labels of F's rows over the centres C on the fp16 planes (approximate: the
+    filter's arg-min, lowest index on ties) in ONE pass per 256-row tile over all centres
+    (``srml_nearest_f16_rowloop``: no per-(row, centre tile) slots), or None when the planes are not
+    128 halves wide (the caller takes ``nearest_centroid_f16(approx=True)``)."""
+    if F.kp != 128 or os.environ.get("SRML_F16_ROWLOOP", "1") == "0":
+        return None
+    dev = F.X.device
+    _, cn, _, _, CP, crows = _f16_centre_planes(F, C, True)
+    labels = torch.empty(F.m, dtype=torch.int32, device=dev)
+    rc = native.lib().srml_nearest_f16_rowloop(F.P.data_ptr(), F.m, F.rows_pad, F.kp, CP.data_ptr(), C.shape[0],
+                                                crows, cn.data_ptr(), float(-2.0 / (F.scale * F.scale)),
+                                                labels.data_ptr(), native.stream(dev))
+    if rc == -2:
+        return None
+    if rc != 0:
+        raise RuntimeError("srml_nearest_f16_rowloop failed (%d)" % rc)
+    return labels
+
+
 def nearest_centroid_f16(F: F16Planes, C: torch.Tensor, approx: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
     """(labels, squared distances) of F.X's rows under centres C by the fp16 certified filter:
     one fp16 MFMA product per (row, centre) on the scaled planes (a third of the 3-product bf16
@@ -599,21 +640,8 @@ def nearest_centroid_f16(F: F16Planes, C: torch.Tensor, approx: bool = False) ->
     filter's arg-min and only exact ties of the filtered distances are re-searched."""
     m, k, dev = F.m, C.shape[0], F.X.device
     st = native.stream(dev)
-    # centred centres W = C - mu (the operands of every search), their fp64 norms with one fp32
-    # rounding (in the radius), the radius terms cg, and the overflow / flagged counters zeroed:
-    # one launch (X's own plane never overflows, s comes from its maximum; only the centres can)
-    Cd = _c(C.to(dev)) if C.dtype in (torch.float32, torch.float64) else _c(C.to(dev, torch.float32))
-    W = torch.empty((k, F.n), dtype=torch.float32, device=dev)
-    cn = torch.empty(k, dtype=torch.float32, device=dev)
-    cg = torch.empty(k, dtype=torch.float32, device=dev)
-    zero2 = torch.empty(2, dtype=torch.int32, device=dev)  # [ovf, flagged count]
-    native.call("srml_f16_centre_prep", Cd.data_ptr(), int(Cd.dtype == torch.float64), k, F.n, F.mu.data_ptr(),
-                float(2.0 * F.tau), int(bool(approx)), W.data_ptr(), cn.data_ptr(), cg.data_ptr(), zero2.data_ptr(), st)
+    W, cn, cg, zero2, CP, crows = _f16_centre_planes(F, C, approx)
     ovf = zero2[0:1]
-    crows = max(256, (k + 255) // 256 * 256)
-    CP = torch.empty((crows // 256, F.kp // 16, 256, 16), dtype=torch.float16, device=dev)
-    native.call("srml_split_f16_tiled_centered", W.data_ptr(), k, F.n, W.stride(0), None, F.kp, crows, F.scale,
-                CP.data_ptr(), ovf.data_ptr(), st)
     xadd, z, z2 = (0.0, 0.0, 0.0) if approx else (F.xadd, F.z, F.z2)
     dscale = -2.0 / (F.scale * F.scale)
     nslot = int(native.lib().srml_nearest_centroid_f16_top2_nslot(k))
@@ -697,7 +725,8 @@ def nearest_list(X: torch.Tensor, C: torch.Tensor, F: Optional[F16Planes] = None
     MFMA product per pair, ``nearest_centroid_f16(approx=True)``) when ``F`` (planes of X) is given
     and C has > 256 rows; else the fp32 MFMA search."""
     if F is not None and C.shape[0] > 256:
-        return nearest_centroid_f16(F, C, approx=True)[0]
+        lab = nearest_f16_labels(F, C)
+        return lab if lab is not None else nearest_centroid_f16(F, C, approx=True)[0]
     return nearest_centroid(X, C, xnorm)[0]
 
 

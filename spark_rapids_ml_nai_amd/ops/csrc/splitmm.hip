@@ -1362,3 +1362,122 @@ SRML_API int srml_kmeans_cand_exact(const float* X, long ld, const float* mu, co
 #undef SRML_CE
   return srml_status();
 }
+
+// ------------------------------------------------------------------------------------------
+// Arg-min over ALL centres per row in one block per 256-row tile: the IVF bucketing / quantiser
+// labels (approximate: the fp16 planes' arg-min, lowest index on ties) for short rows (kp = 128:
+// 8 k steps) and many centres. The top-2 filter above writes one (key, bound) slot per (row,
+// 64-centre tile) — at 20M rows x 19.5k lists that is 73 GB of slots written and re-read by the
+// select, while the products themselves are ~100 TFLOP: the rows' fragments here stay in
+// registers for the whole scan, the centre tiles (64 KB of fp16 images + their norms) stream
+// through a 2-buffer LDS ring by LDS-DMA, and each lane keeps its row's running minimum (the
+// transposed 32 x 32 tiles of split_epilogue_top2_t: 16 centres per lane and tile), so a row costs
+// 4 bytes of output.
+namespace {
+template <int KS>
+__global__ __launch_bounds__(512, 1) void nearest_f16_rowloop_kernel(const unsigned short* __restrict__ XP, long m,
+                                                                     const unsigned short* __restrict__ CP, int k,
+                                                                     int n_ctiles, const float* __restrict__ cnorm,
+                                                                     float dscale, int* __restrict__ labels) {
+  constexpr int CT = 256;             // centres per staged tile
+  constexpr int IMG = CT * 16;        // halves per (tile, k step) image (8 KB)
+  constexpr int CHUNKS = KS * 8;      // 1 KB DMA chunks per centre tile
+  constexpr int CPW = CHUNKS / 8;     // ... per wave
+  __shared__ __attribute__((aligned(1024))) unsigned short lds[2][KS * IMG];
+  __shared__ __attribute__((aligned(1024))) float cn_s[2][CT];
+  const long tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6, li = lane & 31, lk = lane >> 5;
+  const int rr = 32 * wid + li;  // this lane's row in the tile (B operand column)
+  halfx8 xb[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+    xb[ks] = *reinterpret_cast<const halfx8*>(XP + ((tile * KS + ks) << 12) + rr * 16 + 8 * (lk ^ ((rr >> 3) & 1)));
+  auto issue = [&](int c, int buf) {
+    const unsigned short* src = CP + ((long)c * KS << 12);
+#pragma unroll
+    for (int i = 0; i < CPW; ++i) {
+      const int ch = wid * CPW + i;
+      __builtin_amdgcn_global_load_lds((gbl_vptr)(src + ch * 512 + lane * 8), (lds_vptr)(&lds[buf][ch * 512]), 16, 0,
+                                       0);
+    }
+    if (wid == 0) {
+#pragma unroll
+      for (int i = 0; i < CT / 64; ++i)
+        __builtin_amdgcn_global_load_lds((gbl_vptr)(cnorm + (long)c * CT + i * 64 + lane), (lds_vptr)(&cn_s[buf][i * 64]),
+                                         4, 0, 0);
+    }
+  };
+  float best = __builtin_huge_valf();
+  int bi = 0x7fffffff;
+  issue(0, 0);
+  if (n_ctiles > 1) issue(1, 1);
+  for (int c = 0; c < n_ctiles; ++c) {
+    const int buf = c & 1;
+    // tile c landed for every wave (tile c + 1 may stay in flight), every wave is past tile c - 1
+    if (c + 1 < n_ctiles) {
+      if (wid == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(CPW + CT / 64) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"i"(CPW) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    const bool last = c == n_ctiles - 1;
+    const int cbase = c * CT;
+#pragma unroll 2
+    for (int nt = 0; nt < CT / 32; ++nt) {
+      floatx16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+      const int cl = nt * 32 + li;  // this lane's centre row of the A fragment
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const halfx8 a = *reinterpret_cast<const halfx8*>(&lds[buf][ks * IMG + cl * 16 + 8 * (lk ^ ((cl >> 3) & 1))]);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, xb[ks], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const floatx4 cn = *reinterpret_cast<const floatx4*>(&cn_s[buf][nt * 32 + 8 * q + 4 * lk]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int j = cbase + nt * 32 + 8 * q + 4 * lk + u;
+          float d = fmaf(dscale, acc[4 * q + u], cn[u]);
+          if (last && j >= k) d = __builtin_huge_valf();
+          if (d < best) {
+            best = d;
+            bi = j;
+          }
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave is done with buffer `buf`
+    if (c + 2 < n_ctiles) issue(c + 2, buf);
+  }
+  const float ov = __shfl_xor(best, 32, 64);
+  const int oi = __shfl_xor(bi, 32, 64);
+  if (ov < best || (ov == best && oi < bi)) {
+    best = ov;
+    bi = oi;
+  }
+  const long row = tile * 256 + rr;
+  if (lk == 0 && row < m) labels[row] = bi == 0x7fffffff ? 0 : bi;
+}
+}  // namespace
+
+// labels[r] = arg-min_j (cnorm[j] + dscale <P_r, CP_j>) over j < k (lowest index on ties): XP / CP
+// tiled fp16 planes with kp = 128 (rows padded to 256), cnorm readable for crows = n_ctiles * 256
+// entries (entries past k are ignored). Returns -2 for other widths (the caller takes the top-2 path).
+SRML_API int srml_nearest_f16_rowloop(const unsigned short* XP, long m, long xrows, int kp, const unsigned short* CP,
+                                      int k, long crows, const float* cnorm, float dscale, int* labels,
+                                      hipStream_t stream) {
+  if (m <= 0 || k <= 0) return 0;
+  if (kp != 128 || xrows < m || (xrows & 255) || crows < k || (crows & 255)) return -2;
+  if ((reinterpret_cast<uintptr_t>(XP) & 15) || (reinterpret_cast<uintptr_t>(CP) & 15) ||
+      (reinterpret_cast<uintptr_t>(cnorm) & 3))
+    return -5;
+  const long nb = (m + 255) / 256;
+  if (nb > srml_max_blocks(512)) return -3;
+  hipLaunchKernelGGL(nearest_f16_rowloop_kernel<8>, dim3((unsigned)nb), dim3(512), 0, stream, XP, m, CP, k,
+                     (int)(crows / 256), cnorm, dscale, labels);
+  return srml_status();
+}

@@ -105,6 +105,7 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_split_top2_select_f16": (_P, _P, _L, _I, _P, _P, _F, _F, _F, _P, _P, _P, _P, _P, _P),
     "srml_split_f16_tiled_centered_rows": (_P, _L, _P, _L, _I, _P, _I, _L, _F, _P, _P, _P),
     "srml_f16_plane_gather_rows": (_P, _L, _I, _P, _L, _L, _P, _P),
+    "srml_nearest_f16_rowloop": (_P, _L, _L, _I, _P, _I, _L, _P, _F, _P, _P),
     "srml_f16_plane_gather_rows_ex": (_P, _L, _I, _P, _L, _L, _P, _P, _P, _P, _P),
     "srml_split_top2_select_f16_thr": (_P, _P, _L, _I, _P, _P, _F, _F, _F, _P, _P, _P, _P, _P, _P, _P),
     "srml_nearest_centroid_f16_cand": (_P, _L, _L, _I, _P, _I, _L, _P, _P, _P, _F, _F, _P, _P, _P, _I, _P),

@@ -1591,3 +1591,31 @@ def test_knn_pairs_precentred_items_match(gpu_device, seeded):
     assert hit.sum().item() >= 0.995 * max(1, int((i0 >= 0).sum()))
     both = (i0 == i1) & (i0 >= 0)
     torch.testing.assert_close(d1[both], d0[both], rtol=1e-5, atol=1e-2)
+
+
+@pytest.mark.parametrize("m,k", [(5000, 700), (3000, 257), (777, 1800)])
+def test_nearest_f16_rowloop_matches_filter_argmin(gpu_device, m, k):
+    """The one-pass-per-row-tile fp16 arg-min (IVF bucketing labels) equals the top-2 filter's
+    approximate arg-min, and every label is within fp16 rounding of the exact fp64 nearest centre
+    (partial last centre tile, padded row tile)."""
+    from spark_rapids_ml_nai_amd import ops
+
+    X = _rand(m, 128, gpu_device, seed=m + k)
+    C = X[torch.randperm(m, generator=torch.Generator().manual_seed(k))[: min(k, m)].to(gpu_device)]
+    if C.shape[0] < k:
+        C = torch.cat([C, C[: k - C.shape[0]] + 0.01], 0)
+    F = ops.quantizer_planes(X)
+    assert F is not None
+    lab = ops.nearest_f16_labels(F, C)
+    assert lab is not None and lab.dtype == torch.int32 and lab.shape == (m,)
+    ref = ops.nearest_centroid_f16(F, C, approx=True)[0]
+    assert (lab == ref).float().mean().item() > 0.999
+    d = torch.cdist(X.double(), C.double()) ** 2
+    exact = d.min(1).values
+    got = d.gather(1, lab.long().view(-1, 1)).view(-1)
+    assert bool((lab >= 0).all()) and bool((lab < k).all())
+    # fp16 near-ties only: the label's distance exceeds the nearest by a small fraction of the row's scale
+    assert float(((got - exact) / d.mean(1)).max()) < 5e-3
+    # other widths fall back (None)
+    F2 = ops.quantizer_planes(X[:, :100].contiguous())
+    assert ops.nearest_f16_labels(F2, C[:, :100].contiguous()) is None
