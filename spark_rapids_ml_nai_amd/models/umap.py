@@ -47,7 +47,10 @@ NEG_LINES = os.environ.get("SRML_UMAP_NEG_LINES", "1") != "0"
 # degree 8 at a stop near fp32 resolution ran to the product cap on the clustered 20M graph; the
 # stop is now above fp32 noise and a stagnating Ritz change also ends the iteration.
 CHEB_DEGREE = int(os.environ.get("SRML_UMAP_CHEB_DEGREE", "4"))
-SPECTRAL_TOL = float(os.environ.get("SRML_UMAP_SPECTRAL_TOL", "1e-6"))  # Ritz-value stop (see _spectral_device)
+# Ritz-value stop of the spectral init (see _spectral_device): umap-learn's eigsh tolerance. At 20M
+# rows 1e-4 / 1e-5 / 1e-6 take 34 / 42 / 46 products (1.00 / 1.21 / 1.32 s) for trustworthiness
+# 0.7095 / 0.7092 / 0.7102 (profiles/northstar_r6_umap_spectral_tol*.jsonl)
+SPECTRAL_TOL = float(os.environ.get("SRML_UMAP_SPECTRAL_TOL", "1e-4"))
 SPECTRAL_DENSE_N = 2048  # device Jacobi on the dense normalised adjacency up to this many vertices
 # per-phase {"rows": this rank's rows / edges, "s": seconds} of the last umap_fit in this process
 LAST_PHASES: Dict[str, Any] = {}
