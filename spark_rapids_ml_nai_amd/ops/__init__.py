@@ -613,6 +613,8 @@ def nearest_f16_labels(F: F16Planes, C: torch.Tensor) -> Optional[torch.Tensor]:
     if F.kp != 128 or os.environ.get("SRML_F16_ROWLOOP", "1") == "0":
         return None
     dev = F.X.device
+    # (the centre plane's overflow flag is not read: the callers' centres are Lloyd means of rows
+    # of X — convex combinations inside the range the plane's scale was chosen for)
     _, cn, _, _, CP, crows = _f16_centre_planes(F, C, True)
     labels = torch.empty(F.m, dtype=torch.int32, device=dev)
     rc = native.lib().srml_nearest_f16_rowloop(F.P.data_ptr(), F.m, F.rows_pad, F.kp, CP.data_ptr(), C.shape[0],
