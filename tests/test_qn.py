@@ -406,8 +406,13 @@ def test_logistic_fit_margin_cache_matches_full_evaluations(gpu_device, monkeypa
     np.testing.assert_allclose(np.asarray(b["coef_"]), np.asarray(a["coef_"]), rtol=2e-2, atol=2e-3)
     sb = b["_solver"]
     assert sb.get("n_margin_only", 0) > 0, sb
-    if classes == 2:  # (the pass count is trajectory-dependent once the search runs on fp noise)
-        assert sb["n_evals"] - sb["n_margin_only"] < a["_solver"]["n_evals"], (a["_solver"], sb)
+    if classes == 2:
+        # full passes per L-BFGS iteration: the cache serves the rejected trials. (Total pass counts
+        # are not compared: at tol 1e-30 both fits end when the search runs on fp noise, and the
+        # atomics' summation order makes that tail's length differ run to run.)
+        full_b = (sb["n_evals"] - sb["n_margin_only"]) / max(1, b["num_iters"])
+        full_a = a["_solver"]["n_evals"] / max(1, a["num_iters"])
+        assert full_b <= full_a, (a["_solver"], a["num_iters"], sb, b["num_iters"])
 
 
 @pytest.mark.gpu
