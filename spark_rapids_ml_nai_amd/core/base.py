@@ -398,6 +398,9 @@ def _fit_worker(ctx: WorkerContext, payload: Tuple[HostPartition, Callable, Dict
         raise RuntimeError("A worker received no data. Please increase amount of data or use fewer workers.")
     dtype = torch.float32 if float32 else torch.float64
     streamed = None
+    # the copy alone: the descriptor's all-gather above is already in comm_s (counting it here too
+    # double-counts the wait for a slower peer)
+    t_h2d = time.perf_counter()
     from ..ops.ingest import StreamedParts, StreamedRows, is_pinned, uvm_enabled
 
     stream_ok = (ctx.is_gpu and getattr(fit_fn, "streaming_ingest", False) and not uvm_enabled()
@@ -419,7 +422,7 @@ def _fit_worker(ctx: WorkerContext, payload: Tuple[HostPartition, Callable, Dict
         X = to_device(hp.X, ctx.device, dtype) if hp.X is not None else None
         if h2d_ev:
             h2d_ev[1].record()  # pinned sources are queued asynchronously: time them on the stream
-    h2d_host_s = time.perf_counter() - t_start
+    h2d_host_s = time.perf_counter() - t_h2d
     y = to_device(hp.y, ctx.device) if hp.y is not None else None
     _worker_log.info("%s: Initializing context (partition descriptor, %s communicator)", tag,
                      ctx.comm.backend if hasattr(ctx.comm, "backend") else "local")
