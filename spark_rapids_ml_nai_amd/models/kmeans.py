@@ -203,6 +203,9 @@ def _now(X: torch.Tensor) -> float:
 
 
 LLOYD_BATCH = int(os.environ.get("SRML_LLOYD_BATCH", "4"))
+# small-k MFMA loop: keep every row's label and, once under 1/4 of the rows move per step, sum only
+# the moved rows' change: the one-hot GEMM runs on the tiles holding a moved row (=0: off)
+LLOYD_SMALL_DELTA = os.environ.get("SRML_LLOYD_SMALL_DELTA", "1") == "1"
 
 
 def _lloyd_small_loop(X: torch.Tensor, C: torch.Tensor, ctx: WorkerContext, k: int, max_iter: int,
@@ -211,7 +214,11 @@ def _lloyd_small_loop(X: torch.Tensor, C: torch.Tensor, ctx: WorkerContext, k: i
     sums, counts, inertia into the all-reduce buffer), the all-reduce, and the device centre update
     (new centres, shift, convergence flag) — three launches, no host sync. The convergence flag is
     copied back asynchronously once per LLOYD_BATCH iterations and read one batch late (the steps
-    launched after convergence return at once), like the device L-BFGS loop."""
+    launched after convergence return at once), like the device L-BFGS loop. With the label book
+    (MFMA kernel, LLOYD_SMALL_DELTA) a step after one with few moved rows is a DELTA step: its
+    one-hot GEMM sums only the moved rows' change (onehot(new) - onehot(old)) and is skipped on
+    tiles without one, and the update adds the change to the running sums (the reduced buffer
+    then carries changes on every rank alike: the mode follows the reduced moved count)."""
     n = X.shape[1]
     dev = X.device
     # MFMA kernel: no per-row outputs (0.8 GB of label / distance writes per 100M-row step saved),
@@ -222,15 +229,21 @@ def _lloyd_small_loop(X: torch.Tensor, C: torch.Tensor, ctx: WorkerContext, k: i
     C64 = (C.double() - mu).contiguous() if mu is not None else C.double().contiguous()
     C32 = C64.float().contiguous()
     cn = (C32 * C32).sum(1).contiguous()
-    buf = ops.zeros(k * n + k + 1, dtype=torch.float64, device=dev)
+    use_book = not rows_out and LLOYD_SMALL_DELTA
+    buf = ops.zeros(k * n + k + 2, dtype=torch.float64, device=dev)
     mu32 = mu.float().contiguous() if mu is not None else None
     labels = dist = None
     if rows_out:
         labels = torch.empty(X.shape[0], dtype=torch.int32, device=dev)
         dist = torch.empty(X.shape[0], dtype=torch.float32, device=dev)
-    flags = ops.zeros(2, dtype=torch.int32, device=dev)  # [done, iterations]
+    flags = ops.zeros(3, dtype=torch.int32, device=dev)  # [done, iterations, delta mode]
+    book = G = None
+    if use_book:
+        m = X.shape[0]
+        book = (torch.empty(m, dtype=torch.int32, device=dev), flags[2:3])
+        G = torch.empty(k * n + k, dtype=torch.float64, device=dev)
     stat = ops.zeros(2, dtype=torch.float64, device=dev)  # [inertia, max shift] of the last update
-    host = ops.zeros((2, 2), dtype=torch.int32, pin_memory=True)
+    host = ops.zeros((2, 3), dtype=torch.int32, pin_memory=True)
     stream = torch.cuda.current_stream(dev)
     pending: List[Any] = []
     it = j = 0
@@ -238,9 +251,9 @@ def _lloyd_small_loop(X: torch.Tensor, C: torch.Tensor, ctx: WorkerContext, k: i
         for _ in range(min(max(1, LLOYD_BATCH), max_iter - it)):
             buf.zero_()
             ops.kmeans_lloyd_small(X, C32, cn, out=buf, done=flags, labels=labels, dist=dist, rows_out=rows_out,
-                                   mu=mu32)
+                                   mu=mu32, book=book)
             ctx.comm.allreduce(buf)
-            ops.kmeans_small_update(buf, k, n, C64, C32, cn, tol2, flags, stat)
+            ops.kmeans_small_update(buf, k, n, C64, C32, cn, tol2, flags, stat, G=G)
             it += 1
         slot = host[j % 2]
         slot.copy_(flags, non_blocking=True)

@@ -931,7 +931,8 @@ def kmeans_lloyd_small(X: torch.Tensor, C: torch.Tensor, cnorm: Optional[torch.T
                        with_sums: bool = True, out: Optional[torch.Tensor] = None,
                        done: Optional[torch.Tensor] = None, labels: Optional[torch.Tensor] = None,
                        dist: Optional[torch.Tensor] = None, rows_out: bool = True,
-                       mu: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, ...]:
+                       mu: Optional[torch.Tensor] = None,
+                       book: Optional[Tuple[torch.Tensor, ...]] = None) -> Tuple[torch.Tensor, ...]:
     """Fused small-k Lloyd step (ONE pass over X): (labels int32, squared distances fp32) and,
     with ``with_sums``, (cluster sums fp64 [k, n], counts int64 [k], inertia fp64 [1]) by those
     labels. ``out`` (fp64 [k n + k + 1], zeroed): the MFMA kernel accumulates [sums | counts |
@@ -941,7 +942,11 @@ def kmeans_lloyd_small(X: torch.Tensor, C: torch.Tensor, cnorm: Optional[torch.T
     kernel, with ``out``): no per-row labels / distances are written (the Lloyd loop needs only
     the sums, counts and inertia); (None, None, sums, counts, inertia) is returned. ``mu`` (MFMA
     kernel): the rows are searched and summed as x - mu against ``C`` / ``cnorm`` given CENTRED
-    (C - mu): the returned sums are of x - mu (labels and distances are unchanged)."""
+    (C - mu): the returned sums are of x - mu (labels and distances are unchanged). ``book`` (MFMA
+    kernel, with ``out`` of k n + k + 2 doubles): the device Lloyd loop's label book (labels int32
+    [m], mode int32 [1]): every row's label is kept and out[k n + k + 1] counts the rows whose
+    label changed; when mode is set the step is a DELTA step — out gets the sums' and counts'
+    change only, from the tiles holding a moved row (see ``lloyd.hip``)."""
     m, n = X.shape
     k = C.shape[0]
     dev = X.device
@@ -961,11 +966,14 @@ def kmeans_lloyd_small(X: torch.Tensor, C: torch.Tensor, cnorm: Optional[torch.T
         if with_sums and out is None:
             out = zeros(k * n + k + 1, dtype=torch.float64, device=dev)
         muc = _c(mu.to(device=dev, dtype=torch.float32).view(-1)) if mu is not None else None
+        bk = [t.data_ptr() for t in book] if book is not None else [None] * 2
+        if book is not None and (out is None or out.numel() < k * n + k + 2 or book[0].numel() < m):
+            raise ValueError("kmeans_lloyd_small: a label book needs out of k n + k + 2 and m labels")
         native.call("srml_kmeans_lloyd_mfma", X.data_ptr(), m, n, X.stride(0), C.data_ptr(), k, cn.data_ptr(),
                     labels.data_ptr() if rows_out else None, dist.data_ptr() if rows_out else None,
                     out.data_ptr() if with_sums else None,
                     done.data_ptr() if done is not None else None, muc.data_ptr() if muc is not None else None,
-                    native.stream(dev))
+                    *bk, native.stream(dev))
         if not with_sums:
             return labels, dist
         return labels, dist, out[: k * n].view(k, n), out[k * n: k * n + k].long(), out[k * n + k:]
@@ -1064,12 +1072,17 @@ class LloydBook:
 
 
 def kmeans_small_update(buf: torch.Tensor, k: int, n: int, C64: torch.Tensor, C32: torch.Tensor,
-                        cnorm: torch.Tensor, tol2: float, flags: torch.Tensor, stat: torch.Tensor) -> None:
+                        cnorm: torch.Tensor, tol2: float, flags: torch.Tensor, stat: torch.Tensor,
+                        G: Optional[torch.Tensor] = None) -> None:
     """Device centre update of the small-k Lloyd loop (``srml_kmeans_small_update``): C = sums /
     counts from the reduced ``buf`` (empty clusters keep theirs), fp32 copy + norms, the max
-    squared shift and the convergence flag (flags = [done, iterations]) — no host sync."""
+    squared shift and the convergence flag (flags = [done, iterations, delta mode]) — no host
+    sync. With a label book: ``G`` (k n + k fp64) keeps the running sums / counts (a full step
+    sets them, a delta step adds its change) and the next step is a delta step when under 1/4 of
+    the rows (all ranks) moved."""
     native.call("srml_kmeans_small_update", buf.data_ptr(), k, n, C64.data_ptr(), C32.data_ptr(), cnorm.data_ptr(),
-                float(tol2), flags.data_ptr(), stat.data_ptr(), native.stream(buf.device))
+                float(tol2), flags.data_ptr(), stat.data_ptr(), G.data_ptr() if G is not None else None,
+                native.stream(buf.device))
 
 
 def cluster_sums(X: torch.Tensor, labels: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:

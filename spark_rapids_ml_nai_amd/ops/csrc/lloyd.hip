@@ -75,8 +75,10 @@ struct LloydSmem {
   ll_bf16x8 cpl[3][KS][64];                      // centre planes, lane-linear A fragments
   float cn[LL_KP];                               // ||c||^2 (+inf for padding centres)
   int lab[4][64];                                // per wave: the tile's labels (-1: no row)
+  int lob[4][64];                                // per wave, delta step: a moved row's old label (-1: none)
   float cnt[LL_KP];                              // block counts (exact in fp32 below 2^24 rows/block)
   double in[4];
+  unsigned moved;  // rows whose label changed (label book)
 };
 
 template <int NV>
@@ -90,11 +92,19 @@ __global__ __launch_bounds__(LL_T, 2) void lloyd_mfma_kernel(const float* __rest
                                                              const float* __restrict__ cnorm,
                                                              int* __restrict__ labels, float* __restrict__ dist,
                                                              double* __restrict__ out, const int* __restrict__ done,
-                                                             const float* __restrict__ mu) {
+                                                             const float* __restrict__ mu, int* __restrict__ book,
+                                                             const int* __restrict__ mode) {
   using S = LloydSmem<NV>;
   constexpr int KS = S::KS, NQ = S::NQ;
   __shared__ S sm;
   if (done && *done) return;  // converged: the remaining launches of a batch are no-ops
+  // label book: book receives every row's label. *mode != 0, a delta step: book holds the
+  // previous step's labels; a row whose label changed moves its count, and the one-hot of the sums
+  // GEMM becomes onehot(new) - onehot(old) on the moved rows only (0 elsewhere; +-1 exact in
+  // bf16): the GEMM computes the sums' CHANGE, and runs only for the tiles that hold a moved row.
+  // (The old label is loaded after the search: prefetching it with the tile's rows measured
+  // slower, 6.3 vs 6.2 ms per 100M x 64 delta step, and cost two more registers.)
+  const bool dmode = book != nullptr && mode != nullptr && *mode != 0;
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int r32 = lane & 31, hh = lane >> 5;
   // ---- centre planes (A fragments: row = centre r32, k = 16 s + 8 hh + j) and norms
@@ -112,6 +122,7 @@ __global__ __launch_bounds__(LL_T, 2) void lloyd_mfma_kernel(const float* __rest
     sm.cn[t] = t < k ? cnorm[t] : __builtin_huge_valf();
     sm.cnt[t] = 0.f;
   }
+  if (t == 0) sm.moved = 0u;
   __syncthreads();
   float cnr[16];  // this lane half's 16 centre norms, in accumulator-register order
 #pragma unroll
@@ -127,6 +138,7 @@ __global__ __launch_bounds__(LL_T, 2) void lloyd_mfma_kernel(const float* __rest
   const long W = (long)gridDim.x * 4;
   floatx4* tw = sm.tile[wid];
   int* slab = sm.lab[wid];
+  int* slob = sm.lob[wid];
   floatx4 pre[NV];
   // mu (nullable): every staged row is x - mu (C and cnorm are then the centred centres): the
   // sums accumulate in fp32 per wave over ~50k rows, so data far from the origin would lose
@@ -155,6 +167,7 @@ __global__ __launch_bounds__(LL_T, 2) void lloyd_mfma_kernel(const float* __rest
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     fetch(g + W);  // next tile's rows: in flight under this tile's MFMAs
+    bool tile_moved = false;
     // ---- distances: two 32-row N tiles (rolled: the register budget holds one tile's operands)
 #pragma unroll 1
     for (int nt = 0; nt < 2; ++nt) {
@@ -200,19 +213,42 @@ __global__ __launch_bounds__(LL_T, 2) void lloyd_mfma_kernel(const float* __rest
       xn += __shfl_xor(xn, 32, 64);
       const long grow = g * 64 + row;
       const bool live = grow < m;
+      bool mv = false;
+      int old = -1;
       if (hh == 0) {
         slab[row] = live ? bi : -1;
+        slob[row] = -1;
         if (live) {
           float dd = bv + xn;
           dd = dd > 0.f ? dd : 0.f;
           if (labels) labels[grow] = bi;
           if (dist) dist[grow] = dd;
           in_sum += (double)dd;
-          if (acc_sums) atomicAdd(&sm.cnt[bi], 1.f);
+          if (book) {
+            if (dmode) old = book[grow];
+            book[grow] = bi;
+          }
+          mv = dmode && old != bi;
+          if (acc_sums && !dmode) {
+            atomicAdd(&sm.cnt[bi], 1.f);
+          } else if (mv) {
+            atomicAdd(&sm.cnt[bi], 1.f);
+            atomicAdd(&sm.cnt[old], -1.f);
+            slob[row] = old;
+          } else if (dmode) {
+            slab[row] = -1;  // unmoved: no change to sum
+          }
+        }
+      }
+      if (dmode) {
+        const unsigned long long bal = __ballot(mv);
+        if (bal) {
+          tile_moved = true;
+          if (lane == 0) atomicAdd(&sm.moved, (unsigned)__popcll(bal));
         }
       }
     }
-    if (!acc_sums) continue;
+    if (!acc_sums || (dmode && !tile_moved)) continue;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     // ---- cluster sums: K = the tile's 64 rows in 4 steps of 16
@@ -228,6 +264,14 @@ __global__ __launch_bounds__(LL_T, 2) void lloyd_mfma_kernel(const float* __rest
 #pragma unroll
       for (int p = 0; p < 4; ++p)
         oh[p] = (lv[2 * p] == r32 ? 0x3f80u : 0u) | (lv[2 * p + 1] == r32 ? 0x3f800000u : 0u);
+      if (dmode) {  // - onehot(old) of the moved rows (bf16 -1.0 = 0xbf80)
+        const i4 oa = *reinterpret_cast<const i4*>(&slob[r0]);
+        const i4 ob = *reinterpret_cast<const i4*>(&slob[r0 + 4]);
+        const int ov[8] = {oa[0], oa[1], oa[2], oa[3], ob[0], ob[1], ob[2], ob[3]};
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+          oh[p] |= (ov[2 * p] == r32 ? 0xbf80u : 0u) | (ov[2 * p + 1] == r32 ? 0xbf800000u : 0u);
+      }
       const ll_bf16x8 a = __builtin_bit_cast(ll_bf16x8, oh);
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
@@ -257,6 +301,7 @@ __global__ __launch_bounds__(LL_T, 2) void lloyd_mfma_kernel(const float* __rest
   if (!acc_sums) return;
   const long kn = (long)k * n;
   if (t == 0) atomicAdd(&out[kn + k], (sm.in[0] + sm.in[1]) + (sm.in[2] + sm.in[3]));
+  if (t == 0 && book && sm.moved) atomicAdd(&out[kn + k + 1], (double)sm.moved);
   if (t < k && sm.cnt[t] != 0.f) atomicAdd(&out[kn + t], (double)sm.cnt[t]);
   // accs[q][r] = sums[cluster (r & 3) + 8 (r >> 2) + 4 hh][column 32 q + r32]; the tile images are
   // free now: [4 waves][32 clusters][NQ * 32 columns] floats (<= 8 KB per wave)
@@ -281,21 +326,33 @@ __global__ __launch_bounds__(LL_T, 2) void lloyd_mfma_kernel(const float* __rest
 // Centre update of the device Lloyd loop (one block): new centre = sums / counts (empty clusters
 // keep theirs), the largest squared shift, convergence flag; fp32 copy + norms for the next
 // search. Skips once flags[0] (done) is set. stat: [inertia of the last step, last max shift].
+// With a label book (G non-null): buf = [sums | counts | inertia | moved] of this step, a full
+// step's (flags[2] == 0) or a delta step's (1) change; G (k n + k) = the running sums / counts
+// (G = buf or G += buf); the next step is a delta step when fewer than 1/4 of all ranks' rows
+// moved in this one (a full step counts none). A full step cannot count moved rows without
+// reading the book, which costs more (+0.6 ms per 100M rows) than a delta step saves early on.
 __global__ __launch_bounds__(256) void kmeans_small_update_kernel(const double* __restrict__ buf, int k, int n,
                                                                    double* __restrict__ C64, float* __restrict__ C32,
                                                                    float* __restrict__ cnorm, double tol2,
-                                                                   int* __restrict__ flags, double* __restrict__ stat) {
+                                                                   int* __restrict__ flags, double* __restrict__ stat,
+                                                                   double* __restrict__ G) {
   if (flags[0]) return;
   __shared__ double shift[LL_KP];
   const int t = threadIdx.x;
   const long kn = (long)k * n;
+  if (G) {
+    const bool delta = flags[2] == 1;
+    for (long i = t; i < kn + k; i += 256) G[i] = delta ? G[i] + buf[i] : buf[i];
+    __syncthreads();
+  }
+  const double* sums = G ? G : buf;
   for (int j = t >> 3; j < k; j += 32) {  // 8 threads per centre
-    const double cnt = buf[kn + j];
+    const double cnt = sums[kn + j];
     double sh = 0.0;
     float nn = 0.f;
     for (int d = t & 7; d < n; d += 8) {
       const double old = C64[(long)j * n + d];
-      const double nw = cnt > 0.0 ? buf[(long)j * n + d] / cnt : old;
+      const double nw = cnt > 0.0 ? sums[(long)j * n + d] / cnt : old;
       sh += (nw - old) * (nw - old);
       C64[(long)j * n + d] = nw;
       const float f = (float)nw;
@@ -319,6 +376,11 @@ __global__ __launch_bounds__(256) void kmeans_small_update_kernel(const double* 
     stat[1] = mx;
     flags[1] += 1;
     if (mx <= tol2) flags[0] = 1;
+    if (G) {
+      double m_total = 0.0;  // every rank's rows: the reduced running counts
+      for (int j = 0; j < k; ++j) m_total += G[kn + j];
+      flags[2] = buf[kn + k + 1] * 4.0 < m_total ? 1 : 0;
+    }
   }
 }
 
@@ -330,13 +392,17 @@ __global__ __launch_bounds__(256) void kmeans_small_update_kernel(const double* 
 // out = [k x n sums | k counts | inertia] (fp64, zeroed by the caller) accumulates this launch;
 // labels / dist may then be nullptr (not written: the Lloyd loop needs neither). done (nullable):
 // a device flag; non-zero = return at once.
+// Label book (book non-null, out needs k n + k + 2 doubles): book (m int32) receives every row's
+// label, out[k n + k + 1] the rows whose label changed; when *mode != 0 the step is a delta step:
+// out gets the sums' and counts' CHANGE (the rows whose label differs from book's).
 // Needs k <= 32, n <= 64, n % 4 == 0, ld % 4 == 0, 16-B aligned X.
 SRML_API int srml_kmeans_lloyd_mfma(const float* X, long m, int n, long ld, const float* C, int k,
                                     const float* cnorm, int* labels, float* dist, double* out, const int* done,
-                                    const float* mu, hipStream_t stream) {
+                                    const float* mu, int* book, const int* mode, hipStream_t stream) {
   if (m <= 0) return 0;
   if (k < 1 || k > LL_KP || n < 1 || n > 64 || (n & 3) || (ld & 3) || (reinterpret_cast<uintptr_t>(X) & 15) ||
-      (reinterpret_cast<uintptr_t>(mu) & 15))
+      (reinterpret_cast<uintptr_t>(mu) & 15) || m > 0xffffffffL ||
+      (book && (!out || !mode)))
     return (int)hipErrorInvalidValue;
   static int cus = 0;
   if (!cus) {
@@ -350,7 +416,7 @@ SRML_API int srml_kmeans_lloyd_mfma(const float* X, long m, int n, long ld, cons
   const unsigned grid = (unsigned)(want < 2L * cus ? want : 2L * cus);
 #define SRML_LL(NV)                                                                                                   \
   hipLaunchKernelGGL((lloyd_mfma_kernel<NV>), dim3(grid), dim3(LL_T), 0, stream, X, m, n, ld, C, k, cnorm, labels, \
-                     dist, out, done, mu)
+                     dist, out, done, mu, book, mode)
   if (n <= 16) SRML_LL(4);
   else if (n <= 32) SRML_LL(8);
   else SRML_LL(16);
@@ -359,11 +425,12 @@ SRML_API int srml_kmeans_lloyd_mfma(const float* X, long m, int n, long ld, cons
 }
 
 // One centre update of the device Lloyd loop (see kmeans_small_update_kernel). flags = [done,
-// iterations]; stat = [inertia, max shift] of the last update that ran.
+// iterations, delta mode]; stat = [inertia, max shift] of the last update that ran. G (nullable):
+// the label book's running sums / counts.
 SRML_API int srml_kmeans_small_update(const double* buf, int k, int n, double* C64, float* C32, float* cnorm,
-                                      double tol2, int* flags, double* stat, hipStream_t stream) {
+                                      double tol2, int* flags, double* stat, double* G, hipStream_t stream) {
   if (k < 1 || k > LL_KP || n < 1) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(kmeans_small_update_kernel, dim3(1), dim3(256), 0, stream, buf, k, n, C64, C32, cnorm, tol2, flags,
-                     stat);
+                     stat, G);
   return srml_status();
 }

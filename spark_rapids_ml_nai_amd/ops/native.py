@@ -75,8 +75,8 @@ SIGNATURES: Dict[str, Tuple[Any, ...]] = {
     "srml_qn_step_fused": (_P, _P, _P, _I, _L, _P),
     "srml_qn_step_mbf": (_P, _P, _P, _I, _L, _P),
     "srml_kmeans_lloyd_small": (_P, _L, _I, _L, _P, _I, _P, _P, _P, _P, _P, _P, _P),
-    "srml_kmeans_lloyd_mfma": (_P, _L, _I, _L, _P, _I, _P, _P, _P, _P, _P, _P, _P),
-    "srml_kmeans_small_update": (_P, _I, _I, _P, _P, _P, _D, _P, _P, _P),
+    "srml_kmeans_lloyd_mfma": (_P, _L, _I, _L, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P),
+    "srml_kmeans_small_update": (_P, _I, _I, _P, _P, _P, _D, _P, _P, _P, _P),
     "srml_qn_fused_scratch": (),
     "srml_qn_fused_barrier_offset": (),
     "srml_qn_fused_resident": (_L,),

@@ -1416,6 +1416,50 @@ def test_kmeans_lloyd_step_without_row_outputs(gpu_device, m, n, k):
     torch.testing.assert_close(buf_c, buf_e, rtol=1e-9, atol=1e-6)
 
 
+@pytest.mark.parametrize("m,n,k", [(300007, 64, 20), (40000, 12, 5)])
+def test_kmeans_lloyd_delta_step_matches_full_step(gpu_device, m, n, k):
+    """Label book of the small-k loop: a full step, then forced delta steps on the next centres
+    (the sums GEMM on onehot(new) - onehot(old) of the moved rows, skipped on tiles without one).
+    The running sums / counts after each equal a full step's on those centres, and the moved count
+    equals the rows whose label changed."""
+    g = torch.Generator().manual_seed(m + k)
+    Ct = torch.randn(k, n, generator=g) * 2
+    X = (Ct[torch.randint(0, k, (m,), generator=g)] + 1.5 * torch.randn(m, n, generator=g)).float().to(gpu_device)
+    kn = k * n
+    C64 = X[torch.randperm(m, generator=g)[:k].to(gpu_device)].double().contiguous()
+    C32 = C64.float().contiguous()
+    cn = (C32 * C32).sum(1).contiguous()
+    flags = torch.zeros(3, dtype=torch.int32, device=gpu_device)
+    book = (torch.empty(m, dtype=torch.int32, device=gpu_device), flags[2:3])
+    G = torch.empty(kn + k, dtype=torch.float64, device=gpu_device)
+    buf = torch.zeros(kn + k + 2, dtype=torch.float64, device=gpu_device)
+    stat = torch.zeros(2, dtype=torch.float64, device=gpu_device)
+    lab0 = ops.kmeans_lloyd_small(X, C32, with_sums=False)[0].clone()
+    ops.kmeans_lloyd_small(X, C32, cn, out=buf, done=flags, rows_out=False, book=book)
+    full0 = buf.clone()
+    assert float(full0[kn + k + 1]) == 0.0  # a full step counts no moved rows
+    ops.kmeans_small_update(buf, k, n, C64, C32, cn, 0.0, flags, stat, G=G)
+    assert torch.equal(book[0], lab0) and int(flags[2].item()) == 1  # next: a delta step
+    torch.testing.assert_close(G, full0[: kn + k], rtol=0, atol=0)
+    for rnd, md in enumerate((1, 1)):  # two delta steps
+        C1 = C32.clone()
+        lab1 = ops.kmeans_lloyd_small(X, C1, with_sums=False)[0].clone()
+        ref = torch.zeros(kn + k + 2, dtype=torch.float64, device=gpu_device)
+        ops.kmeans_lloyd_small(X, C1, out=ref, rows_out=False)
+        flags[2] = md  # whatever the moved count
+        buf.zero_()
+        ops.kmeans_lloyd_small(X, C32, cn, out=buf, done=flags, rows_out=False, book=book)
+        nm = int((lab1 != lab0).sum())
+        assert int(buf[kn + k + 1].item()) == nm and (rnd > 0 or nm > 0)
+        ops.kmeans_small_update(buf, k, n, C64, C32, cn, 0.0, flags, stat, G=G)
+        assert torch.equal(book[0], lab1)
+        torch.testing.assert_close(G[kn:], ref[kn: kn + k], rtol=0, atol=0)
+        torch.testing.assert_close(G[:kn], ref[:kn], rtol=1e-9, atol=1e-6 * float(ref[:kn].abs().max()))
+        torch.testing.assert_close(buf[kn + k], ref[kn + k])  # the inertia is a full one
+        assert int(flags[2].item()) == (1 if nm * 4 < m else 0)
+        lab0 = lab1
+
+
 def test_kmeans_lloyd_loop_far_from_origin(gpu_device):
     """Data offset 1e3 from the origin (spread ~1): one device Lloyd step's centres equal the fp64
     cluster means of the same labels to the data's spread precision. The MFMA kernel stages x - mu
