@@ -102,8 +102,8 @@ __global__ __launch_bounds__(LL_T, 2) void lloyd_mfma_kernel(const float* __rest
   // previous step's labels; a row whose label changed moves its count, and the one-hot of the sums
   // GEMM becomes onehot(new) - onehot(old) on the moved rows only (0 elsewhere; +-1 exact in
   // bf16): the GEMM computes the sums' CHANGE, and runs only for the tiles that hold a moved row.
-  // (The old label is loaded after the search: prefetching it with the tile's rows measured
-  // slower, 6.3 vs 6.2 ms per 100M x 64 delta step, and cost two more registers.)
+  // (The old label is loaded per 32-row half before its MFMAs: prefetching it with the tile's rows
+  // measured slower, 6.3 vs 6.2 ms per 100M x 64 delta step, and cost two more registers.)
   const bool dmode = book != nullptr && mode != nullptr && *mode != 0;
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int r32 = lane & 31, hh = lane >> 5;
@@ -172,6 +172,8 @@ __global__ __launch_bounds__(LL_T, 2) void lloyd_mfma_kernel(const float* __rest
 #pragma unroll 1
     for (int nt = 0; nt < 2; ++nt) {
       const int row = 32 * nt + r32;
+      // the book's label of this lane's row, loaded before the MFMAs so they cover its latency
+      const int oldv = (dmode && hh == 0 && g * 64 + row < m) ? book[g * 64 + row] : -1;
       floatx16 acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -225,7 +227,7 @@ __global__ __launch_bounds__(LL_T, 2) void lloyd_mfma_kernel(const float* __rest
           if (dist) dist[grow] = dd;
           in_sum += (double)dd;
           if (book) {
-            if (dmode) old = book[grow];
+            old = oldv;
             book[grow] = bi;
           }
           mv = dmode && old != bi;
