@@ -61,3 +61,29 @@ def test_umap_two_ranks_ivf_pull_neg_lines():
     assert "error" not in rec, rec
     assert rec["n_gpus"] == 2 and rec["finite"], rec
     assert rec["trustworthiness"] > 0.9, rec
+
+
+@pytest.mark.gpu
+def test_kmeans_small_k_two_ranks_delta_steps_match_full_steps():
+    """The small-k Lloyd loop on 2 ranks sharing the GPU (gloo all-reduce of the step buffer), on
+    blobs from random start rows: with delta steps (label book; the mode follows the REDUCED moved count,
+    so both ranks switch together) the fit reaches the same centres in the same iterations as with
+    every step summing all rows."""
+    import numpy as np
+
+    recs = {}
+    for delta in ("1", "0"):
+        env = dict(os.environ, SRML_LLOYD_SMALL_DELTA=delta, MASTER_ADDR="127.0.0.1")
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+               "--master-addr", "127.0.0.1", "--master-port", str(29631 + int(delta)),
+               os.path.join(ROOT, "tools", "kmeans_spmd_check.py")]
+        r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=55)
+        assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+        recs[delta] = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    a, b = np.asarray(recs["1"]["centres"]), np.asarray(recs["0"]["centres"])
+    assert a.shape == (20, 64) and recs["1"]["world"] == 2
+    assert min(recs["1"]["iters"], recs["0"]["iters"]) >= 3, (recs["1"]["iters"], recs["0"]["iters"])
+    # the two runs' sums round differently (measured: 20 / 20 iterations, centres 3e-8 apart); a
+    # near-tie row taking the other side would move its centres by ~4e-4, wrong delta sums by O(1)
+    assert abs(recs["1"]["iters"] - recs["0"]["iters"]) <= 2, (recs["1"]["iters"], recs["0"]["iters"])
+    assert float(np.abs(a - b).max()) < 1e-3, float(np.abs(a - b).max())
