@@ -32,7 +32,8 @@ def main() -> None:
     model = est.fit(DataFrame.from_numpy(X[b[rank]:b[rank + 1]]))
     if rank == 0:
         ma = getattr(model, "_model_attributes", {}) or {}
-        print(json.dumps({"iters": int(ma.get("n_iter", -1)), "world": world, "delta": os.environ.get("SRML_LLOYD_SMALL_DELTA"),
+        print(json.dumps({"iters": int(ma.get("n_iter", -1)), "world": world,
+                          "delta": os.environ.get("SRML_LLOYD_SMALL_DELTA"),
                           "centres": np.asarray(model.cluster_centers_, dtype=np.float64).tolist()}), flush=True)
     if world > 1:
         dist.barrier()
