@@ -1,6 +1,6 @@
 // Dense SPD solves and Gram-matrix coordinate descent for the linear models, on device.
 //
-//  * srml_potrf_f64: blocked right-looking Cholesky (lower, row-major), 64-wide panels:
+//  * srml_potrf_f64: blocked right-looking Cholesky (lower, row-major), 32-wide panels (64: env):
 //      diag block factored in LDS by one workgroup -> panel TRSM (thread per row, L11 in LDS)
 //      -> trailing update A22 -= A21 A21^T on the f64 MFMA GEMM (srml_dgemm).
 //    A non-positive pivot sets *info = column + 1 (the caller falls back to an eigen solve).
@@ -19,8 +19,12 @@ extern "C" int srml_dgemm(int ta, int tb, int M, int N, int K, double alpha, con
                           const double* B, long ldb, double beta, double* C, long ldc, hipStream_t stream);
 
 namespace {
-constexpr int NB = 64;
+// panel width: 64 (SRML_POTRF_NB=64) or 32 (default): the panel chain (diagonal factor -> TRSM ->
+// next panel) is latency-bound, and a 32-wide panel shortens both kernels' dependent chains ~4x
+// for twice the panels
+constexpr int NB_MAX = 64;
 
+template <int NB>
 __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A, long lda, int k0, int nb,
                                                          int* __restrict__ info) {
   __shared__ double S[NB][NB + 1];
@@ -69,6 +73,7 @@ __device__ __forceinline__ double bcast_f64(double v, int src) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
+template <int NB>
 __global__ __launch_bounds__(64) void potrf_diag_reg_kernel(double* __restrict__ A, long lda, int k0, int nb,
                                                             int* __restrict__ info) {
   const int i = threadIdx.x;
@@ -103,6 +108,7 @@ __global__ __launch_bounds__(64) void potrf_diag_reg_kernel(double* __restrict__
 
 // rows r >= k1: x (1 x NB) solves x L11^T = A[r, k0:k0+NB] (only full panels reach the TRSM: the
 // last, possibly narrower, diagonal block has no rows below it)
+template <int NB>
 __global__ __launch_bounds__(256) void potrf_trsm_kernel(double* __restrict__ A, long lda, int k0, int k1, int n) {
   __shared__ double L[NB][NB + 1];
   const int t = threadIdx.x;
@@ -603,18 +609,29 @@ SRML_API int srml_potrf_f64(double* A, int n, long lda, int* info, hipStream_t s
   // threads in LDS with two barriers per column. (One wave with the scaled pivot column shared
   // through LDS broadcast reads measured 115 us: the chain is latency-bound, not readlane-bound.)
   static const int diag_reg = getenv("SRML_POTRF_REG") ? atoi(getenv("SRML_POTRF_REG")) : 1;
+  static const int nbw = (getenv("SRML_POTRF_NB") && atoi(getenv("SRML_POTRF_NB")) == NB_MAX) ? NB_MAX : 32;
   hipError_t err = hipSuccess;
   SRML_TRY(err, hipMemsetAsync(info, 0, sizeof(int), stream));
-  for (int k0 = 0; k0 < n; k0 += NB) {
-    const int nb = n - k0 < NB ? n - k0 : NB;
+  for (int k0 = 0; k0 < n; k0 += nbw) {
+    const int nb = n - k0 < nbw ? n - k0 : nbw;
     const int k1 = k0 + nb;
-    if (diag_reg)
-      hipLaunchKernelGGL(potrf_diag_reg_kernel, dim3(1), dim3(64), 0, stream, A, lda, k0, nb, info);
-    else
-      hipLaunchKernelGGL(potrf_diag_kernel, dim3(1), dim3(256), 0, stream, A, lda, k0, nb, info);
+    if (nbw == NB_MAX) {
+      if (diag_reg)
+        hipLaunchKernelGGL(potrf_diag_reg_kernel<NB_MAX>, dim3(1), dim3(64), 0, stream, A, lda, k0, nb, info);
+      else
+        hipLaunchKernelGGL(potrf_diag_kernel<NB_MAX>, dim3(1), dim3(256), 0, stream, A, lda, k0, nb, info);
+    } else {
+      if (diag_reg)
+        hipLaunchKernelGGL(potrf_diag_reg_kernel<32>, dim3(1), dim3(64), 0, stream, A, lda, k0, nb, info);
+      else
+        hipLaunchKernelGGL(potrf_diag_kernel<32>, dim3(1), dim3(256), 0, stream, A, lda, k0, nb, info);
+    }
     if (k1 < n) {
       const int m2 = n - k1;
-      hipLaunchKernelGGL(potrf_trsm_kernel, dim3((m2 + 255) / 256), dim3(256), 0, stream, A, lda, k0, k1, n);
+      if (nbw == NB_MAX)
+        hipLaunchKernelGGL(potrf_trsm_kernel<NB_MAX>, dim3((m2 + 255) / 256), dim3(256), 0, stream, A, lda, k0, k1, n);
+      else
+        hipLaunchKernelGGL(potrf_trsm_kernel<32>, dim3((m2 + 255) / 256), dim3(256), 0, stream, A, lda, k0, k1, n);
       const int rc = srml_dgemm(0, 1, m2, m2, nb, -1.0, A + (long)k1 * lda + k0, lda, A + (long)k1 * lda + k0, lda,
                                 1.0, A + (long)k1 * lda + k1, lda, stream);
       if (rc) return rc;
