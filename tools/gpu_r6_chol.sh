@@ -4,7 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out/chol6
 export TMPDIR=/tmp
-for V in 32 64 32 64; do
+for V in ${POTRF_NBS:-32 64 32 64}; do
   SRML_POTRF_NB=$V timeout -k 10 200 python -u -m pytest tests/test_ops_gpu.py -x -q --timeout 120 --timeout-method thread -k "spd or linear or ridge" > gpurun_out/chol6/pytest_$V.log 2>&1 || { tail -30 gpurun_out/chol6/pytest_$V.log; exit 1; }
   echo "V=$V $(tail -1 gpurun_out/chol6/pytest_$V.log)"
   rm -rf gpurun_out/chol6/p_$V
