@@ -17,6 +17,8 @@
 
 extern "C" int srml_dgemm(int ta, int tb, int M, int N, int K, double alpha, const double* A, long lda,
                           const double* B, long ldb, double beta, double* C, long ldc, hipStream_t stream);
+extern "C" int srml_dgemm_syrk_lower(int M, int K, double alpha, const double* A, long lda, double beta, double* C,
+                                     long ldc, hipStream_t stream);
 
 namespace {
 // panel width: 64 (SRML_POTRF_NB=64) or 32 (default): the panel chain (diagonal factor -> TRSM ->
@@ -632,8 +634,12 @@ SRML_API int srml_potrf_f64(double* A, int n, long lda, int* info, hipStream_t s
         hipLaunchKernelGGL(potrf_trsm_kernel<NB_MAX>, dim3((m2 + 255) / 256), dim3(256), 0, stream, A, lda, k0, k1, n);
       else
         hipLaunchKernelGGL(potrf_trsm_kernel<32>, dim3((m2 + 255) / 256), dim3(256), 0, stream, A, lda, k0, k1, n);
-      const int rc = srml_dgemm(0, 1, m2, m2, nb, -1.0, A + (long)k1 * lda + k0, lda, A + (long)k1 * lda + k0, lda,
-                                1.0, A + (long)k1 * lda + k1, lda, stream);
+      // trailing update A22 -= A21 A21^T on the lower-triangle tiles only (SRML_POTRF_SYRK=0: full)
+      static const int syrk = getenv("SRML_POTRF_SYRK") ? atoi(getenv("SRML_POTRF_SYRK")) : 1;
+      const int rc = syrk ? srml_dgemm_syrk_lower(m2, nb, -1.0, A + (long)k1 * lda + k0, lda, 1.0,
+                                                  A + (long)k1 * lda + k1, lda, stream)
+                          : srml_dgemm(0, 1, m2, m2, nb, -1.0, A + (long)k1 * lda + k0, lda, A + (long)k1 * lda + k0,
+                                       lda, 1.0, A + (long)k1 * lda + k1, lda, stream);
       if (rc) return rc;
     }
   }

@@ -388,10 +388,11 @@ constexpr int DK = 16;
 __global__ __launch_bounds__(256) void dgemm_kernel(int M, int N, int K, double alpha, const double* __restrict__ A,
                                                     long lda, int ta, const double* __restrict__ B, long ldb, int tb,
                                                     double beta, double* __restrict__ C, long ldc, int kchunk,
-                                                    double* __restrict__ ws) {
+                                                    double* __restrict__ ws, int lower) {
   __shared__ double As[DK][DT + 1];  // As[k][i]
   __shared__ double Bs[DK][DT + 1];  // Bs[k][j]
   const int i0 = blockIdx.y * DT, j0 = blockIdx.x * DT;
+  if (lower && j0 >= i0 + DT) return;  // lower: tiles wholly above the diagonal are not computed
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int wi = wid >> 1, wj = wid & 1;
   doublex4 acc[2][2];
@@ -485,7 +486,19 @@ SRML_API int srml_dgemm(int ta, int tb, int M, int N, int K, double alpha, const
   if (M <= 0 || N <= 0) return 0;
   dim3 grid(ceil_div(N, DT), ceil_div(M, DT), 1);
   hipLaunchKernelGGL(dgemm_kernel, grid, dim3(256), 0, stream, M, N, K, alpha, A, lda, ta, B, ldb, tb, beta, C, ldc,
-                     K > 0 ? K : 1, (double*)nullptr);
+                     K > 0 ? K : 1, (double*)nullptr, 0);
+  return srml_status();
+}
+
+// C = alpha A A^T + beta C (A: M x K row-major) on the 64 x 64 tiles that touch the lower
+// triangle only (the entries above the diagonal of diagonal tiles are computed too): the
+// Cholesky trailing update, whose upper triangle is never read.
+SRML_API int srml_dgemm_syrk_lower(int M, int K, double alpha, const double* A, long lda, double beta, double* C,
+                                   long ldc, hipStream_t stream) {
+  if (M <= 0) return 0;
+  dim3 grid(ceil_div(M, DT), ceil_div(M, DT), 1);
+  hipLaunchKernelGGL(dgemm_kernel, grid, dim3(256), 0, stream, M, M, K, alpha, A, lda, 0, A, lda, 1, beta, C, ldc,
+                     K > 0 ? K : 1, (double*)nullptr, 1);
   return srml_status();
 }
 
@@ -501,7 +514,7 @@ SRML_API int srml_dgemm_splitk(int ta, int tb, int M, int N, int K, double alpha
   splits = (K + kchunk - 1) / kchunk;
   dim3 grid(ceil_div(N, DT), ceil_div(M, DT), (unsigned)splits);
   hipLaunchKernelGGL(dgemm_kernel, grid, dim3(256), 0, stream, M, N, K, alpha, A, lda, ta, B, ldb, tb, beta, C, ldc,
-                     kchunk, ws);
+                     kchunk, ws, 0);
   int st = srml_status();
   if (st) return st;
   const long MN = (long)M * N;
