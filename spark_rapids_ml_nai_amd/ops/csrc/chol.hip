@@ -113,11 +113,14 @@ __global__ __launch_bounds__(64) void potrf_diag_reg_kernel(double* __restrict__
 template <int NB>
 __global__ __launch_bounds__(256) void potrf_trsm_kernel(double* __restrict__ A, long lda, int k0, int k1, int n) {
   __shared__ double L[NB][NB + 1];
+  __shared__ double rd[NB];  // 1 / L[j][j]: a multiply, not a division, on each row's chain
   const int t = threadIdx.x;
   for (int idx = t; idx < NB * NB; idx += 256) {
     const int i = idx / NB, j = idx % NB;
     L[i][j] = A[(long)(k0 + i) * lda + k0 + j];
   }
+  __syncthreads();
+  if (t < NB) rd[t] = 1.0 / L[t][t];
   __syncthreads();
   const int r = k1 + blockIdx.x * 256 + t;
   if (r >= n) return;
@@ -130,7 +133,7 @@ __global__ __launch_bounds__(256) void potrf_trsm_kernel(double* __restrict__ A,
     double s = x[j];
 #pragma unroll
     for (int l = 0; l < j; ++l) s -= x[l] * L[j][l];
-    x[j] = s / L[j][j];
+    x[j] = s * rd[j];
   }
 #pragma unroll
   for (int j = 0; j < NB; ++j) row[j] = x[j];

@@ -4,7 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out/chol7
 export TMPDIR=/tmp
-for V in 1 0 1 0; do
+for V in ${POTRF_SYRKS:-1 0 1 0}; do
   SRML_POTRF_SYRK=$V timeout -k 10 200 python -u -m pytest tests/test_ops_gpu.py tests/test_linear_solvers.py -x -q --timeout 120 --timeout-method thread -k "spd or linear or ridge" > gpurun_out/chol7/pytest_$V.log 2>&1 || { tail -30 gpurun_out/chol7/pytest_$V.log; exit 1; }
   echo "V=$V $(tail -1 gpurun_out/chol7/pytest_$V.log)"
   rm -rf gpurun_out/chol7/p_$V
